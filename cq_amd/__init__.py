@@ -1,0 +1,148 @@
+"""cq_amd -- MI355X executor for cq's SELECT path (CSV scan, WHERE, GROUP BY, JOIN).
+
+The product is the native library ``cq_amd/lib/libcqgpu.so`` (HIP for gfx950 +
+C++ host), whose C ABI is declared in ``include/cqgpu.h``.  This module is a thin
+ctypes binding used by bench.py, __graft_entry__.py and the tests; it never
+computes results itself and raises if the native library is missing.
+"""
+from __future__ import annotations
+
+import ctypes as C
+import os
+
+from . import abi
+
+HERE = os.path.dirname(os.path.abspath(__file__))
+LIB_PATH = os.path.join(HERE, "lib", "libcqgpu.so")
+
+_lib = None
+
+
+class Stats(C.Structure):
+    _fields_ = [("scan_ms", C.c_double), ("total_ms", C.c_double), ("scan_bytes", C.c_uint64),
+                ("records", C.c_uint64), ("groups", C.c_uint64), ("lds_spills", C.c_uint64),
+                ("grid", C.c_int), ("path", C.c_int), ("retries", C.c_int)]
+
+
+def lib():
+    """Load libcqgpu.so (fails loudly: there is no CPU fallback)."""
+    global _lib
+    if _lib is None:
+        if not os.path.exists(LIB_PATH):
+            raise RuntimeError(f"cq_amd native library missing: {LIB_PATH} (run __graft_entry__.build())")
+        L = C.CDLL(LIB_PATH, mode=C.RTLD_GLOBAL)
+        TP = C.POINTER(abi.Table)
+        L.evaluate_query.restype = TP
+        L.evaluate_query.argtypes = [C.POINTER(abi.Node)]
+        L.cqgpu_table_open.restype = C.c_void_p
+        L.cqgpu_table_open.argtypes = [C.c_char_p, abi.CsvConfig]
+        L.cqgpu_table_from_bytes.restype = C.c_void_p
+        L.cqgpu_table_from_bytes.argtypes = [C.c_void_p, C.c_size_t, abi.CsvConfig, C.c_uint64,
+                                             C.c_char_p, C.c_size_t]
+        L.cqgpu_table_free.argtypes = [C.c_void_p]
+        L.cqgpu_table_bytes.restype = C.c_size_t
+        L.cqgpu_table_bytes.argtypes = [C.c_void_p]
+        L.cqgpu_query.restype = TP
+        L.cqgpu_query.argtypes = [C.POINTER(abi.Node), C.POINTER(C.c_void_p), C.c_int]
+        L.cqgpu_result_free.argtypes = [TP]
+        L.cqgpu_query_partial.restype = C.c_size_t
+        L.cqgpu_query_partial.argtypes = [C.POINTER(abi.Node), C.POINTER(C.c_void_p), C.c_int,
+                                          C.POINTER(C.c_void_p)]
+        L.cqgpu_merge_partials.restype = TP
+        L.cqgpu_merge_partials.argtypes = [C.POINTER(abi.Node), C.POINTER(C.c_void_p),
+                                           C.POINTER(C.c_size_t), C.c_int]
+        L.cqgpu_last_stats.argtypes = [C.POINTER(Stats)]
+        L.cqgpu_last_error.restype = C.c_char_p
+        L.cqgpu_last_ineligible.restype = C.c_char_p
+        _lib = L
+    return _lib
+
+
+def global_csv_config() -> abi.CsvConfig:
+    return abi.CsvConfig.in_dll(lib(), "global_csv_config")
+
+
+class Table:
+    """A CSV table resident in HBM on the current HIP device."""
+
+    def __init__(self, handle):
+        if not handle:
+            raise RuntimeError("cq_amd: " + (lib().cqgpu_last_error() or b"").decode())
+        self.handle = C.c_void_p(handle)
+
+    @classmethod
+    def open(cls, path: str, cfg: abi.CsvConfig | None = None) -> "Table":
+        return cls(lib().cqgpu_table_open(path.encode(), cfg or abi.csv_config()))
+
+    @classmethod
+    def from_bytes(cls, data: bytes, cfg: abi.CsvConfig | None = None, base_offset: int = 0,
+                   header: bytes | None = None) -> "Table":
+        buf = C.create_string_buffer(data, len(data)) if not isinstance(data, C.Array) else data
+        h = lib().cqgpu_table_from_bytes(C.cast(buf, C.c_void_p), len(data), cfg or abi.csv_config(),
+                                         base_offset, header, len(header) if header else 0)
+        return cls(h)
+
+    @property
+    def nbytes(self) -> int:
+        return lib().cqgpu_table_bytes(self.handle)
+
+    def close(self):
+        if self.handle:
+            lib().cqgpu_table_free(self.handle)
+            self.handle = None
+
+    def __del__(self):
+        try:
+            self.close()
+        except Exception:
+            pass
+
+
+def _tables_arg(tables):
+    arr = (C.c_void_p * len(tables))(*[t.handle.value for t in tables])
+    return arr, len(tables)
+
+
+def query(ast, tables) -> dict | None:
+    """Run a plan (pointer to a reference-layout node) over resident tables."""
+    arr, n = _tables_arg(tables)
+    tp = lib().cqgpu_query(ast, arr, n)
+    if not tp:
+        return None
+    res = abi.table_to_py(tp)
+    lib().cqgpu_result_free(tp)
+    return res
+
+
+def query_raw(ast, tables):
+    """Like query() but returns the result pointer (caller frees with result_free)."""
+    arr, n = _tables_arg(tables)
+    return lib().cqgpu_query(ast, arr, n)
+
+
+def result_free(tp):
+    lib().cqgpu_result_free(tp)
+
+
+def evaluate(ast) -> dict | None:
+    """The drop-in entry point: evaluate_query(ASTNode*) on files named in the plan."""
+    tp = lib().evaluate_query(ast)
+    if not tp:
+        return None
+    res = abi.table_to_py(tp)
+    lib().cqgpu_result_free(tp)
+    return res
+
+
+def stats() -> dict:
+    s = Stats()
+    lib().cqgpu_last_stats(C.byref(s))
+    return {f: getattr(s, f) for f, _ in Stats._fields_}
+
+
+def last_error() -> str:
+    return (lib().cqgpu_last_error() or b"").decode("latin-1")
+
+
+def last_ineligible() -> str:
+    return (lib().cqgpu_last_ineligible() or b"").decode("latin-1")

@@ -1,0 +1,107 @@
+// plan.h -- compiled SELECT plan shared by the host executor and the kernels.
+#pragma once
+#include <stdint.h>
+#include "cell.h"
+
+namespace cq {
+
+constexpr int MAX_NEED = 8;     // distinct CSV columns one scan parses
+constexpr int MAX_PROG = 128;   // predicate instructions
+constexpr int MAX_CONST = 48;   // literal cells
+constexpr int MAX_ACC = 8;      // accumulators (one per aggregate SELECT item)
+constexpr int VM_STACK = 8;
+
+// predicate bytecode (WHERE tree of evaluator_conditions.c:62-164 and
+// evaluator_expressions.c:23-263, flattened in post-order)
+enum : uint8_t {
+    OP_COL = 0,    // push cells[a]
+    OP_CONST,      // push consts[b]
+    OP_NULLV,      // push NULL (unresolvable identifier, unsupported expression value)
+    OP_ARITH,      // a = AR_*; pop r, l; push arith(l, r)
+    OP_NEG,        // unary minus
+    OP_CMP,        // a = CMP_*; pop r, l; push bool
+    OP_IN,         // b = item count, a = negate; pops items then left
+    OP_LIKE,       // a = case-sensitive
+    OP_NOT,
+    OP_AND,
+    OP_OR,
+    OP_BOOL,       // push bool a
+};
+enum : uint8_t { CMP_EQ = 0, CMP_NE, CMP_LT, CMP_GT, CMP_LE, CMP_GE };
+
+struct Insn {
+    uint8_t op;
+    uint8_t a;
+    uint16_t b;
+};
+
+// accumulator kinds
+enum : uint8_t { ACC_SUM = 0, ACC_MIN = 1, ACC_MAX = 2 };
+
+struct AccSpec {
+    uint8_t kind;   // ACC_*
+    uint8_t slot;   // need slot of the argument column
+    uint8_t pad[2];
+};
+
+struct ScanPlan {
+    uint64_t n;            // bytes in the table
+    uint64_t data_begin;   // first byte a data record may start at
+    uint64_t range_begin;  // records are owned by [range_begin, range_end)
+    uint64_t range_end;
+    uint32_t delim;
+    uint32_t quote;
+    int32_t nneed;
+    int32_t max_col;
+    int16_t need_col[MAX_NEED];
+    int32_t nprog;         // 0: no WHERE
+    Insn prog[MAX_PROG];
+    int32_t nconst;
+    Cell consts[MAX_CONST];
+    int32_t group_slot;    // -1: one group (aggregate query without GROUP BY)
+    int32_t nacc;
+    AccSpec acc[MAX_ACC];
+    int32_t want_rows;     // 1: also emit matching record offsets (row-returning)
+};
+
+// scan statistics written by the kernel (one per launch)
+struct ScanStats {
+    unsigned long long records;     // data records seen
+    unsigned long long passed;      // records passing WHERE
+    unsigned long long short_rows;  // records too short for a needed column
+    unsigned long long lds_spills;  // records aggregated straight into the global table
+    unsigned long long overflow;    // global table full: host must retry larger
+    unsigned long long rows_emitted;
+    unsigned int acc_classes[MAX_ACC];  // OR of value classes seen per accumulator (1 num, 2 str, 4 date)
+};
+
+// global (HBM) group table, structure of arrays, capacity `cap` (power of two)
+struct GroupTable {
+    uint32_t cap;
+    uint32_t* tag;                 // 0 empty, 1 being written, else hash tag
+    uint32_t* kcls;
+    uint32_t* klen;
+    uint64_t* kv;
+    unsigned long long* cnt;
+    unsigned long long* first;     // min record byte offset
+    double* sum[MAX_ACC];          // ACC_SUM: sum of numeric cells
+    unsigned long long* num[MAX_ACC];  // ACC_SUM: numeric cell count
+    Cell* ext[MAX_ACC];            // ACC_MIN/MAX: extreme cell
+    unsigned long long* extpos[MAX_ACC];
+    uint32_t* lock[MAX_ACC];
+    uint32_t* used;                // number of occupied slots
+};
+
+// dense group record handed back to the host
+struct GroupOut {
+    uint32_t kcls, klen;
+    uint64_t kv;
+    unsigned long long cnt;
+    unsigned long long first;
+    double sum[MAX_ACC];
+    unsigned long long num[MAX_ACC];
+    Cell ext[MAX_ACC];
+    unsigned long long extpos[MAX_ACC];
+};
+
+}  // namespace cq

@@ -1,0 +1,112 @@
+/*
+ * cqgpu.h -- C ABI of libcqgpu, the MI355X executor for cq's SELECT path.
+ *
+ * Drop-in boundary: the unchanged cq CLI and parser call
+ *     ResultSet* evaluate_query(ASTNode* query_ast);     reference include/evaluator.h:32
+ * and read/write the global CSV configuration
+ *     extern CsvConfig global_csv_config;                reference include/evaluator.h:29,
+ *                                                        defined evaluator.c:23
+ * libcqgpu exports both symbols with the reference's exact binary layout
+ * (include/cq_abi.h), so `main.c` plus the reference front-end objects link
+ * against libcqgpu.so instead of the reference evaluator.
+ *
+ * Below the drop-in entry point the library exposes the pieces the benchmark
+ * and the multi-GPU driver use: tables resident in HBM (the second boundary,
+ * replacing csv_load, reference csv_reader.h:76, on the GPU path only) and
+ * queries over resident tables.
+ *
+ * Error convention (reference evaluator.c:28, evaluator_joins.c:221): NULL
+ * result plus a message on stderr; cqgpu_last_error() returns the message.
+ * Calls are synchronous and not reentrant, like the reference's.
+ */
+#ifndef CQGPU_H
+#define CQGPU_H
+
+#include <stddef.h>
+#include <stdint.h>
+#include "cq_abi.h"
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+/* ---- drop-in (reference evaluator.h) ------------------------------------- */
+/* replaces evaluate_query (reference evaluator.c:290-348); returns a heap
+ * result table the caller frees with the reference's csv_free (csv_reader.c:467)
+ * or cqgpu_result_free. */
+cq_table* evaluate_query(cq_node* query_ast);
+/* replaces the reference global (evaluator.c:23), written by main.c:99-101 */
+extern cq_csv_config global_csv_config;
+
+/* ---- resident tables (replace csv_load on the GPU path) ------------------- */
+typedef struct cqgpu_table cqgpu_table;
+/* mmap + upload to the current HIP device (reference mmap.c:78-108 + csv_load) */
+cqgpu_table* cqgpu_table_open(const char* path, cq_csv_config cfg);
+/* upload a caller buffer; `base_offset` is the position of data[0] in the whole
+ * file (0 unless this is a shard) and `header` the file's header record bytes
+ * when the shard does not start at the file start (NULL otherwise). */
+cqgpu_table* cqgpu_table_from_bytes(const void* data, size_t n, cq_csv_config cfg,
+                                    uint64_t base_offset, const char* header, size_t header_len);
+void cqgpu_table_free(cqgpu_table* t);
+size_t cqgpu_table_bytes(const cqgpu_table* t);
+int cqgpu_table_ncols(const cqgpu_table* t);
+
+/* ---- queries over resident tables ---------------------------------------- */
+/* FROM binds tables[0]; the j-th JOIN binds tables[1 + j]; paths in the plan
+ * are ignored.  Same result contract as evaluate_query. */
+cq_table* cqgpu_query(cq_node* query_ast, cqgpu_table* const* tables, int ntables);
+void cqgpu_result_free(cq_table* r);
+
+/* ---- partial aggregation for range-partitioned multi-GPU queries --------- */
+/* Run the aggregate part of `query_ast` on this rank's shard and serialize the
+ * per-group partial state (canonical keys, counts, sums, extremes, first-row
+ * positions in whole-file byte offsets, representative cells) into a malloc'd
+ * blob.  Returns blob size (0 on error); *blob_out is freed with free(). */
+size_t cqgpu_query_partial(cq_node* query_ast, cqgpu_table* const* tables, int ntables,
+                           void** blob_out);
+/* Merge the partial blobs of all ranks (any order) into the final result, with
+ * HAVING / ORDER BY / DISTINCT / LIMIT applied as evaluate_query would. */
+cq_table* cqgpu_merge_partials(cq_node* query_ast, const void* const* blobs, const size_t* sizes,
+                               int nblobs);
+
+/* ---- introspection -------------------------------------------------------- */
+typedef struct {
+    double scan_ms;              /* device time of the last fused scan kernel (HIP events) */
+    double total_ms;             /* wall time of the last query inside the library */
+    uint64_t scan_bytes;         /* table bytes the scan covered */
+    uint64_t records;            /* data records scanned */
+    uint64_t groups;             /* result groups before HAVING/LIMIT */
+    uint64_t lds_spills;         /* records aggregated directly in HBM (LDS table full) */
+    int grid;                    /* scan blocks launched */
+    int path;                    /* 1 = GPU executor, 2 = fallback evaluator */
+    int retries;                 /* global group table regrowths */
+} cqgpu_stats;
+int cqgpu_last_stats(cqgpu_stats* out);
+const char* cqgpu_last_error(void);
+/* why the last plan was not GPU-eligible ("" when it was) */
+const char* cqgpu_last_ineligible(void);
+
+/* Tokenizer / typing checks: record start offsets of all data records (file
+ * order; returns the total count, writes at most `cap`), and the typed cells
+ * of columns `cols` at given records (a result table, freed like any other). */
+size_t cqgpu_debug_records(cqgpu_table* t, unsigned long long* out, size_t cap);
+cq_table* cqgpu_debug_cells(cqgpu_table* t, const int* cols, int ncols,
+                            const unsigned long long* recs, size_t nrec);
+/* the fused scan kernel's own parse of ascending columns `cols` for every
+ * record (rows in arbitrary order, their record offsets in recs_out) */
+cq_table* cqgpu_debug_scan_cells(cqgpu_table* t, const int* cols, int ncols,
+                                 unsigned long long* recs_out, size_t cap);
+/* Planner check without a device: compile `query_ast` against a header line and
+ * describe the plan (or why it is not GPU-eligible) into `out`. */
+int cqgpu_explain(cq_node* query_ast, const char* header, cq_csv_config cfg, char* out, size_t cap);
+
+/* Optional fallback for plans outside the GPU subset: the reference evaluator
+ * compiled with evaluate_query renamed.  Without one, such
+ * plans return NULL with a message. */
+typedef cq_table* (*cqgpu_fallback_fn)(cq_node*);
+void cqgpu_set_fallback(cqgpu_fallback_fn fn);
+
+#ifdef __cplusplus
+}
+#endif
+#endif /* CQGPU_H */

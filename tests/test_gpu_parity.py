@@ -1,0 +1,178 @@
+"""HIP executor parity: GPU results vs the reference's golden vectors and the oracle.
+
+Runs on an MI355X (pytest -m gpu).  Every query goes through the C ABI
+(evaluate_query / cqgpu_query in cq_amd/lib/libcqgpu.so).  Counts, group sets,
+group order, MIN/MAX and representative cells must be bit-exact; SUM/AVG are
+compared with the north_star tolerance of 1e-6 relative (the GPU adds in a
+different order than the reference's sequential double sum).
+"""
+import ctypes as C
+import os
+
+import pytest
+
+import cqtest
+import cq_amd
+from cq_amd import abi, datagen
+
+pytestmark = pytest.mark.gpu
+
+SUMAVG_REL = 1e-6
+QUERIES = cqtest.golden("queries.json")
+
+# golden queries outside the GPU subset of this round (they take the
+# fallback path or return an error): joins, STDDEV/MEDIAN, composite keys,
+# row-returning projections and LIKE-free function calls
+EXPECTED_INELIGIBLE_MARKERS = ("JOIN", "STDDEV", "MEDIAN", "GROUP BY role, active",
+                               "GROUP BY w1, w2, w3",
+                               # MIN/MAX over a column mixing numbers and strings
+                               "MIN(a), MAX(a), MIN(b), MAX(b), MIN(d) FROM '{D}/edge_numbers.csv'")
+
+
+def _row_returning(sql):
+    up = sql.upper()
+    return not any(f in up for f in ("COUNT(", "SUM(", "AVG(", "MIN(", "MAX(", "STDDEV(", "MEDIAN("))
+
+
+def expected_ineligible(sql):
+    return any(m in sql for m in EXPECTED_INELIGIBLE_MARKERS) or _row_returning(sql)
+
+
+def tolerant_columns(ast):
+    """indices of SELECT items computing SUM or AVG (1e-6 relative allowed)."""
+    sel = ast.contents.u.q.select.contents
+    out = set()
+    for i in range(sel.u.sel.count):
+        t = sel.u.sel.texts[i].decode("latin-1").upper()
+        if t.startswith("SUM(") or t.startswith("AVG("):
+            out.add(i)
+    return out
+
+
+def compare(got, want, tol_cols, ctx):
+    assert (got is None) == (want is None), f"{ctx}: got={got} want={want}"
+    if want is None:
+        return
+    assert got["columns"] == want["columns"], ctx
+    assert len(got["rows"]) == len(want["rows"]), f"{ctx}: {len(got['rows'])} vs {len(want['rows'])}"
+    for i, (gr, wr) in enumerate(zip(got["rows"], want["rows"])):
+        for j, (g, w) in enumerate(zip(gr, wr)):
+            rel = SUMAVG_REL if j in tol_cols else 0.0
+            assert cqtest.cell_equal(g, w, rel), f"{ctx}: row {i} col {j}: got {g} want {w}"
+
+
+@pytest.mark.skipif(not cqtest.front_available(), reason="reference front end not built")
+@pytest.mark.parametrize("idx", range(len(QUERIES)))
+def test_golden_query(idx):
+    q = QUERIES[idx]
+    sql = cqtest.sql_for(q["sql"])
+    with cqtest.Parsed(sql) as ast:
+        got = cq_amd.evaluate(ast)
+        inel = cq_amd.last_ineligible()
+        tol = tolerant_columns(ast)
+    if inel:
+        assert expected_ineligible(q["sql"]), f"unexpectedly ineligible ({inel}): {q['sql']}"
+        pytest.skip(f"outside this round's GPU subset: {inel}")
+    assert cq_amd.stats()["path"] == 1
+    want = cqtest.table_from_json(q["result"])
+    compare(got, want, tol, q["sql"])
+
+
+# ---------------------------------------------------------------- typing parity via GROUP BY
+EDGE_FILES = ["edge_numbers.csv", "edge_dates.csv", "edge_quotes.csv", "edge_ws.csv", "edge_lines.csv",
+              "test_data.csv", "users.csv", "orders.csv", "products.csv", "events.csv",
+              "coordinates.csv", "emails.csv", "cities.csv", "test_numeric.csv"]
+
+
+def _header(path):
+    with open(path, "rb") as fh:
+        data = fh.read()
+    lib = cqtest.oracle()
+    tp = lib.orc_load(data, len(data), abi.csv_config())
+    names = [tp.contents.columns[i].name.decode("latin-1") for i in range(tp.contents.ncols)]
+    lib.orc_free(tp)
+    return names
+
+
+@pytest.mark.skipif(not cqtest.front_available(), reason="reference front end not built")
+@pytest.mark.parametrize("fname", EDGE_FILES)
+def test_typed_cells_by_group(fname):
+    """GROUP BY every column: group keys, first-row cells and counts pin the typing."""
+    path = os.path.join(cqtest.GOLDEN_DATA, fname)
+    for col in _header(path):
+        if not col or any(ch in col for ch in " ,.'\"()") or col.upper() in ("SELECT", "FROM", "GROUP", "ORDER", "BY"):
+            continue
+        sql = f"SELECT {col}, COUNT(*) FROM '{path}' GROUP BY {col}"
+        want, unsup = cqtest.oracle_query(sql)
+        assert not unsup
+        with cqtest.Parsed(sql) as ast:
+            got = cq_amd.evaluate(ast)
+        assert not cq_amd.last_ineligible(), sql
+        compare(got, want, set(), sql)
+
+
+# ---------------------------------------------------------------- synthetic, larger
+@pytest.fixture(scope="module")
+def synth_role(tmp_path_factory):
+    p = tmp_path_factory.mktemp("synth") / "role.csv"
+    datagen.write_shape_a(str(p), 200_000, seed=3, with_role=True)
+    return str(p)
+
+
+SYNTH_QUERIES = [
+    "SELECT role, COUNT(*), SUM(height), AVG(height) FROM '{P}' WHERE age > 30 GROUP BY role",
+    "SELECT COUNT(*) FROM '{P}' WHERE age > 30",
+    "SELECT COUNT(*), SUM(height), AVG(height), MIN(height), MAX(age) FROM '{P}' WHERE gender = 'f'",
+    "SELECT name, COUNT(*), MIN(role), MAX(role) FROM '{P}' WHERE age BETWEEN 20 AND 40 GROUP BY name",
+    "SELECT age, COUNT(*), AVG(height) FROM '{P}' WHERE role IN ('role_001', 'role_500', 'role_999') GROUP BY age",
+    "SELECT gender, COUNT(*), SUM(age) FROM '{P}' WHERE NOT (age % 3 = 0 OR height < 1.5) GROUP BY gender",
+    "SELECT height, COUNT(*), MIN(age) FROM '{P}' GROUP BY height ORDER BY height DESC LIMIT 20",
+    "SELECT role, COUNT(*) FROM '{P}' GROUP BY role HAVING COUNT(*) > 205 ORDER BY COUNT(*) DESC",
+    "SELECT surname, COUNT(*) FROM '{P}' WHERE name LIKE 'A%' OR surname ILIKE 'b%' GROUP BY surname",
+]
+
+
+@pytest.mark.parametrize("tmpl", SYNTH_QUERIES)
+def test_synthetic_vs_oracle(synth_role, tmpl):
+    sql = tmpl.replace("{P}", synth_role)
+    want, unsup = cqtest.oracle_query(sql)
+    assert not unsup
+    with cqtest.Parsed(sql) as ast:
+        got = cq_amd.evaluate(ast)
+        tol = tolerant_columns(ast)
+    assert not cq_amd.last_ineligible(), (sql, cq_amd.last_ineligible())
+    compare(got, want, tol, sql)
+
+
+def test_resident_table_reuse(synth_role):
+    """cqgpu_query on a resident table gives the same answer every time."""
+    sql = SYNTH_QUERIES[0].replace("{P}", synth_role)
+    t = cq_amd.Table.open(synth_role)
+    with cqtest.Parsed(sql) as ast:
+        first = cq_amd.query(ast, [t])
+        for _ in range(3):
+            again = cq_amd.query(ast, [t])
+            compare(again, first, {2, 3}, sql)
+    t.close()
+
+
+def test_many_groups_spill(tmp_path):
+    """more distinct keys than one LDS table holds: the HBM table takes the rest."""
+    lines = [b"k,v\n"] + [b"key%06d,%d\n" % (i % 50000, i) for i in range(150_000)]
+    p = tmp_path / "many.csv"
+    p.write_bytes(b"".join(lines))
+    sql = f"SELECT k, COUNT(*), SUM(v), MIN(v) FROM '{p}' GROUP BY k"
+    want, _ = cqtest.oracle_query(sql)
+    with cqtest.Parsed(sql) as ast:
+        got = cq_amd.evaluate(ast)
+    compare(got, want, {2}, sql)
+
+
+def test_empty_and_header_only(tmp_path):
+    p = tmp_path / "h.csv"
+    p.write_bytes(b"a,b\n")
+    for sql in (f"SELECT COUNT(*), SUM(a) FROM '{p}'", f"SELECT a, COUNT(*) FROM '{p}' GROUP BY a"):
+        want, _ = cqtest.oracle_query(sql)
+        with cqtest.Parsed(sql) as ast:
+            got = cq_amd.evaluate(ast)
+        compare(got, want, set(), sql)
