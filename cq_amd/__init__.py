@@ -77,8 +77,9 @@ class Table:
     @classmethod
     def from_bytes(cls, data: bytes, cfg: abi.CsvConfig | None = None, base_offset: int = 0,
                    header: bytes | None = None) -> "Table":
-        buf = C.create_string_buffer(data, len(data)) if not isinstance(data, C.Array) else data
-        h = lib().cqgpu_table_from_bytes(C.cast(buf, C.c_void_p), len(data), cfg or abi.csv_config(),
+        # bytes: pass the object's own buffer (no copy); the library copies it to HBM
+        ptr = C.cast(C.c_char_p(data), C.c_void_p) if isinstance(data, bytes) else C.cast(data, C.c_void_p)
+        h = lib().cqgpu_table_from_bytes(ptr, len(data), cfg or abi.csv_config(),
                                          base_offset, header, len(header) if header else 0)
         return cls(h)
 
