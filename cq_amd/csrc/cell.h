@@ -519,13 +519,21 @@ CQ_HD bool like(const uint8_t* s, uint32_t sl, const uint8_t* p, uint32_t pl, bo
 // INT the value, DBL sign + round-half-even(|x|*1e6) below 2^43 where the text
 // is exact, and the value itself above (GK_BIG), where distinct doubles never
 // share a text.
-enum : uint32_t { GK_STR = 0, GK_INT = 1, GK_DBL = 2, GK_BIG = 3, GK_DATE = 4 };
+enum : uint32_t { GK_STR = 0, GK_INT = 1, GK_DBL = 2, GK_BIG = 3, GK_LONG = 5, GK_ALL = 7 };
 
+// A group key in 16 bytes + class/length.  Text keys of at most 16 bytes (all
+// NULL and DATE keys, most strings) are stored inline, little-endian, zero
+// padded, so equality is two 64-bit compares.  Longer text keys (GK_LONG) keep
+// the address of their bytes in w0 and a 64-bit content hash in w1.  INT / DBL
+// / BIG keep their canonical payload in w0.
 struct GKey {
     uint32_t cls;
     uint32_t len;       // text classes: bytes (<= 255)
-    uint64_t v;         // GK_STR: address (0 = "NULL"); GK_DATE: date bits; else payload
+    uint64_t w0;
+    uint64_t w1;
 };
+
+CQ_HD uint32_t gk_clslen(const GKey& k) { return (k.cls << 16) | k.len; }
 
 // round-half-even(|x| * 1e6) for |x| < 2^43 (exact in 128-bit): glibc printf
 // formats the exact binary value and breaks exact ties to even.
@@ -555,48 +563,6 @@ CQ_HD uint64_t micro_units(double ax) {
     return q;
 }
 
-CQ_HD GKey group_key(const Cell& c) {
-    GKey k;
-    k.len = 0;
-    switch (c.kind) {
-        case K_NULL: k.cls = GK_STR; k.len = 4; k.v = 0; break;   // "NULL"
-        case K_INT: k.cls = GK_INT; k.v = c.bits; break;
-        case K_DATE: k.cls = GK_DATE; k.len = 10; k.v = c.bits; break;
-        case K_DBL: {
-            double x = as_dbl(c.bits);
-            double ax = x < 0 ? -x : x;
-            bool neg = (c.bits >> 63) != 0;
-            if (ax < 8796093022208.0) { k.cls = GK_DBL; k.v = micro_units(ax) | ((uint64_t)neg << 63); }
-            else { k.cls = GK_BIG; k.v = c.bits; }
-            break;
-        }
-        default: k.cls = GK_STR; k.len = c.len > 255 ? 255 : c.len; k.v = c.bits; break;
-    }
-    return k;
-}
-
-CQ_HD bool gk_text(const GKey& k) { return k.cls == GK_STR || k.cls == GK_DATE; }
-
-// i-th byte of a text key
-CQ_HD uint8_t gk_byte(const GKey& k, uint32_t i) {
-    if (k.cls == GK_DATE) {
-        uint32_t y = (uint32_t)(k.v >> 32), m = (uint32_t)((k.v >> 16) & 0xffff), d = (uint32_t)(k.v & 0xffff);
-        switch (i) {
-            case 0: return (uint8_t)('0' + (y / 1000) % 10);
-            case 1: return (uint8_t)('0' + (y / 100) % 10);
-            case 2: return (uint8_t)('0' + (y / 10) % 10);
-            case 3: return (uint8_t)('0' + y % 10);
-            case 4: case 7: return '-';
-            case 5: return (uint8_t)('0' + (m / 10) % 10);
-            case 6: return (uint8_t)('0' + m % 10);
-            case 8: return (uint8_t)('0' + (d / 10) % 10);
-            default: return (uint8_t)('0' + d % 10);
-        }
-    }
-    if (k.v == 0) return (uint8_t)("NULL"[i]);
-    return ((const uint8_t*)(uintptr_t)k.v)[i];
-}
-
 CQ_HD uint64_t mix64(uint64_t h) {
     h ^= h >> 33; h *= 0xff51afd7ed558ccdULL;
     h ^= h >> 33; h *= 0xc4ceb9fe1a85ec53ULL;
@@ -604,21 +570,79 @@ CQ_HD uint64_t mix64(uint64_t h) {
     return h;
 }
 
-CQ_HD uint64_t gk_hash(const GKey& k) {
-    if (!gk_text(k)) return mix64(k.v * 0x9E3779B97F4A7C15ULL + k.cls);
+CQ_HD uint64_t fnv_bytes(const uint8_t* p, uint32_t n) {
     uint64_t h = 1469598103934665603ULL;
-    for (uint32_t i = 0; i < k.len; i++) { h ^= gk_byte(k, i); h *= 1099511628211ULL; }
-    return mix64(h ^ k.len);
+    for (uint32_t i = 0; i < n; i++) { h ^= p[i]; h *= 1099511628211ULL; }
+    return h;
+}
+
+// text key from bytes (trimmed STRING cell, the literal "NULL", a rendered DATE)
+CQ_HD GKey text_key(const uint8_t* p, uint32_t len) {
+    GKey k;
+    if (len > 255) len = 255;
+    k.len = len;
+    if (len <= 16) {
+        k.cls = GK_STR;
+        uint64_t w0 = 0, w1 = 0;
+        for (uint32_t i = 0; i < len; i++) {
+            uint64_t b = p[i];
+            if (i < 8) w0 |= b << (8 * i);
+            else w1 |= b << (8 * (i - 8));
+        }
+        k.w0 = w0;
+        k.w1 = w1;
+    } else {
+        k.cls = GK_LONG;
+        k.w0 = (uint64_t)(uintptr_t)p;
+        k.w1 = fnv_bytes(p, len);
+    }
+    return k;
+}
+
+CQ_HD GKey date_key(uint64_t bits) {   // "%04d-%02d-%02d" packed inline
+    uint32_t y = (uint32_t)(bits >> 32), m = (uint32_t)((bits >> 16) & 0xffff), d = (uint32_t)(bits & 0xffff);
+    uint8_t t[10];
+    t[0] = (uint8_t)('0' + (y / 1000) % 10); t[1] = (uint8_t)('0' + (y / 100) % 10);
+    t[2] = (uint8_t)('0' + (y / 10) % 10);   t[3] = (uint8_t)('0' + y % 10);
+    t[4] = '-'; t[5] = (uint8_t)('0' + (m / 10) % 10); t[6] = (uint8_t)('0' + m % 10);
+    t[7] = '-'; t[8] = (uint8_t)('0' + (d / 10) % 10); t[9] = (uint8_t)('0' + d % 10);
+    return text_key(t, 10);
+}
+
+CQ_HD GKey group_key(const Cell& c) {
+    GKey k;
+    k.len = 0;
+    k.w1 = 0;
+    switch (c.kind) {
+        case K_NULL: { const uint8_t t[4] = {'N', 'U', 'L', 'L'}; k = text_key(t, 4); break; }
+        case K_INT: k.cls = GK_INT; k.w0 = c.bits; break;
+        case K_DATE: k = date_key(c.bits); break;
+        case K_DBL: {
+            double x = as_dbl(c.bits);
+            double ax = x < 0 ? -x : x;
+            bool neg = (c.bits >> 63) != 0;
+            if (ax < 8796093022208.0) { k.cls = GK_DBL; k.w0 = micro_units(ax) | ((uint64_t)neg << 63); }
+            else { k.cls = GK_BIG; k.w0 = c.bits; }
+            break;
+        }
+        default: k = text_key((const uint8_t*)(uintptr_t)c.bits, c.len); break;
+    }
+    return k;
+}
+
+CQ_HD uint64_t gk_hash(const GKey& k) {
+    uint64_t a = k.cls == GK_LONG ? 0 : k.w0;      // GK_LONG: w0 is an address, w1 the content hash
+    return mix64(a * 0x9E3779B97F4A7C15ULL ^ mix64(k.w1 + gk_clslen(k)));
 }
 
 CQ_HD bool gk_equal(const GKey& a, const GKey& b) {
-    bool at = gk_text(a), bt = gk_text(b);
-    if (at != bt) return false;
-    if (!at) return a.cls == b.cls && a.v == b.v;
-    if (a.len != b.len) return false;
-    if (a.cls == b.cls && a.v == b.v) return true;
+    if (a.cls != b.cls || a.len != b.len || a.w1 != b.w1) return false;
+    if (a.w0 == b.w0) return true;
+    if (a.cls != GK_LONG) return false;
+    const uint8_t* p = (const uint8_t*)(uintptr_t)a.w0;
+    const uint8_t* q = (const uint8_t*)(uintptr_t)b.w0;
     for (uint32_t i = 0; i < a.len; i++)
-        if (gk_byte(a, i) != gk_byte(b, i)) return false;
+        if (p[i] != q[i]) return false;
     return true;
 }
 

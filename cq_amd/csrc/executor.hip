@@ -709,9 +709,9 @@ void compile_aggregate(const cqgpu_table* t, cq_node* q, Compiled& C) {
 
 // ------------------------------------------------------------------ host groups
 struct HGroup {
-    uint32_t kcls = 0, klen = 0;
-    uint64_t kv = 0;
-    std::string kbytes;                 // GK_STR key bytes
+    uint32_t kcls = 0, klen = 0;        // cell.h GKey class and text length
+    uint64_t kw0 = 0, kw1 = 0;          // key words (GK_LONG: w1 = content hash)
+    std::string kbytes;                 // text-class key bytes
     unsigned long long cnt = 0, first = NOPOS;   // first: whole-file byte offset
     double sum[MAX_ACC] = {};
     unsigned long long num[MAX_ACC] = {};
@@ -770,9 +770,9 @@ TableArena make_arena(DevCtx& c, const ScanPlan& P, uint32_t cap, size_t out_cap
     struct Part { void** p; size_t bytes; int fill; };
     std::vector<Part> parts;
     parts.push_back({(void**)&A.gt.tag, cap * 4ull, 0});
-    parts.push_back({(void**)&A.gt.kcls, cap * 4ull, 0});
-    parts.push_back({(void**)&A.gt.klen, cap * 4ull, 0});
-    parts.push_back({(void**)&A.gt.kv, cap * 8ull, 0});
+    parts.push_back({(void**)&A.gt.clslen, cap * 4ull, 0});
+    parts.push_back({(void**)&A.gt.w0, cap * 8ull, 0});
+    parts.push_back({(void**)&A.gt.w1, cap * 8ull, 0});
     parts.push_back({(void**)&A.gt.cnt, cap * 8ull, 0});
     parts.push_back({(void**)&A.gt.first, cap * 8ull, 0xff});
     for (int a = 0; a < P.nacc; a++) {
@@ -908,12 +908,12 @@ std::vector<HGroup> run_aggregate(DevCtx& c, const cqgpu_table* t, Compiled& C, 
     batch.insert(batch.end(), repcells.begin(), repcells.end());
     for (auto& o : outs)
         for (int a = 0; a < C.P.nacc; a++) batch.push_back(o.ext[a]);
-    // group key strings (needed to merge partials across ranks)
+    // long text keys live in the table bytes (needed to merge partials across ranks)
     for (auto& o : outs) {
         Cell k;
-        k.kind = (o.kcls == GK_STR && o.kv != 0) ? K_STR : K_NULL;
-        k.len = o.klen;
-        k.bits = o.kv;
+        k.kind = (o.clslen >> 16) == GK_LONG ? K_STR : K_NULL;
+        k.len = o.clslen & 0xffff;
+        k.bits = o.w0;
         batch.push_back(k);
     }
     std::vector<HCell> hb = fetch_cells(c, batch);
@@ -923,10 +923,16 @@ std::vector<HGroup> run_aggregate(DevCtx& c, const cqgpu_table* t, Compiled& C, 
     for (size_t g = 0; g < outs.size(); g++) {
         const GroupOut& o = outs[g];
         HGroup h;
-        h.kcls = o.kcls;
-        h.klen = o.klen;
-        h.kv = o.kv;
-        if (o.kcls == GK_STR) h.kbytes = o.kv ? hb[base_key + g].s : std::string("NULL");
+        h.kcls = o.clslen >> 16;
+        h.klen = o.clslen & 0xffff;
+        h.kw0 = o.w0;
+        h.kw1 = o.w1;
+        if (h.kcls == GK_LONG) {
+            h.kbytes = hb[base_key + g].s;
+        } else if (h.kcls == GK_STR) {
+            for (uint32_t i = 0; i < h.klen; i++)
+                h.kbytes.push_back((char)((i < 8 ? o.w0 >> (8 * i) : o.w1 >> (8 * (i - 8))) & 0xff));
+        }
         h.cnt = o.cnt;
         h.first = o.first == NOPOS ? NOPOS : o.first + t->base_offset;
         for (int a = 0; a < MAX_ACC; a++) {

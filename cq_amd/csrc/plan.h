@@ -73,15 +73,16 @@ struct ScanStats {
     unsigned long long overflow;    // global table full: host must retry larger
     unsigned long long rows_emitted;
     unsigned int acc_classes[MAX_ACC];  // OR of value classes seen per accumulator (1 num, 2 str, 4 date)
+    unsigned long long slow_records;    // records the fast field walk handed to the general parser
 };
 
 // global (HBM) group table, structure of arrays, capacity `cap` (power of two)
 struct GroupTable {
     uint32_t cap;
     uint32_t* tag;                 // 0 empty, 1 being written, else hash tag
-    uint32_t* kcls;
-    uint32_t* klen;
-    uint64_t* kv;
+    uint32_t* clslen;              // key class << 16 | text length
+    uint64_t* w0;                  // key words (cell.h GKey)
+    uint64_t* w1;
     unsigned long long* cnt;
     unsigned long long* first;     // min record byte offset
     double* sum[MAX_ACC];          // ACC_SUM: sum of numeric cells
@@ -94,8 +95,8 @@ struct GroupTable {
 
 // dense group record handed back to the host
 struct GroupOut {
-    uint32_t kcls, klen;
-    uint64_t kv;
+    uint32_t clslen, pad;
+    uint64_t w0, w1;
     unsigned long long cnt;
     unsigned long long first;
     double sum[MAX_ACC];
