@@ -630,9 +630,15 @@ CQ_HD GKey group_key(const Cell& c) {
     return k;
 }
 
+// Two multiplies.  Multiplicative hashing mixes every input bit only into the
+// TOP bits of the product, so the result is rotated: its low bits (the table
+// index) are the product's top 24 bits; the high 32 bits (the slot tag) are
+// only a filter before the full key compare.
 CQ_HD uint64_t gk_hash(const GKey& k) {
-    uint64_t a = k.cls == GK_LONG ? 0 : k.w0;      // GK_LONG: w0 is an address, w1 the content hash
-    return mix64(a * 0x9E3779B97F4A7C15ULL ^ mix64(k.w1 + gk_clslen(k)));
+    const uint64_t a = k.cls == GK_LONG ? 0 : k.w0;      // GK_LONG: w0 is an address, w1 the content hash
+    const uint64_t x = a ^ (a >> 29) ^ (k.w1 * 0x9E3779B97F4A7C15ULL) ^ ((uint64_t)gk_clslen(k) << 7);
+    const uint64_t h = x * 0xD6E8FEB86659FD93ULL;
+    return (h >> 40) | (h << 24);
 }
 
 CQ_HD bool gk_equal(const GKey& a, const GKey& b) {

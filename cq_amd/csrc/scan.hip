@@ -7,22 +7,28 @@
 //
 //   stage     the window (+16 B before, +2 KiB after) is copied from registers
 //             into LDS; the next window's 16 B/lane loads are already in flight
-//   classify  each lane turns 64 window bytes into three 64-bit masks in LDS:
-//             record terminators ('\n' '\r'), separators (terminators + the
-//             delimiter) and "bad" bytes (every other byte below '-': quotes,
-//             whitespace, NUL, '+', ...), with exact SWAR byte tests
+//   classify  each lane turns 64 window bytes into two 64-bit masks in LDS --
+//             record terminators ('\n' '\r') and separators (terminators and
+//             the delimiter) -- plus a "has a quote byte" flag, branch-free SWAR
 //   split     record starts come from the terminator mask; a block-wide scan
 //             gives every record an LDS slot
-//   parse     one lane per record walks its fields with find-first-set on the
-//             separator mask and types the needed cells with specialised int /
-//             decimal / string parsers reading LDS; any field the fast parsers
-//             cannot prove identical to infer_type/parse_value (quotes,
-//             whitespace, date-shaped numbers, >15 significant digits ...) goes
-//             through the general parser in cell.h -- same semantics, slower
+//   parse     one lane per record takes a 128-bit view of both masks at its
+//             start and pops separators up to the last needed column (the
+//             column walk is uniform across the wave); needed fields are typed
+//             by specialised int / decimal / string parsers reading LDS.  A
+//             field the fast parsers cannot prove identical to infer_type /
+//             parse_value (date-shaped, long numerals) goes through the general
+//             cell parser; a record with quotes, control or blank bytes in a
+//             needed field, or longer than the view, goes through the general
+//             parse_line cursor (csv_reader.c:278-338) -- same semantics, slower
 //   filter    WHERE bytecode (plan.h OP_*), or a direct compare for col-op-const
 //   group     LDS open-addressing table, 16-byte inline keys, COUNT / SUM / AVG /
 //             MIN / MAX accumulators; flushed once per block into the HBM table
 //             (per-thread registers when the query has no GROUP BY)
+//
+// Every per-record array (cells, accumulator pointers) is indexed with
+// compile-time indices only, so it lives in registers: a run-time index would
+// move it to scratch memory, which costs more than the whole parse.
 //
 // Records are owned by the window holding their first byte, so every byte range
 // [range_begin, range_end) can be scanned independently: that is also how the
@@ -37,16 +43,18 @@ constexpr int WIN = 32768;                   // window bytes (64 per lane)
 constexpr int PRE = 16;                      // bytes staged before the window
 constexpr int MARGIN = 2048;                 // bytes staged after the window
 constexpr int TILE = PRE + WIN + MARGIN;     // 34832
-constexpr int TILE16 = TILE / 16;            // 2177 uint4 per tile
+constexpr int TILE16 = TILE / 16;            // 2177 16-byte loads per tile
 constexpr int NMW = (WIN + MARGIN) / 64;     // mask words covering [ws, ws + WIN + MARGIN)
 constexpr int RSMAX = 2048;                  // record slots per pass
 constexpr int LDS_BUDGET = 160 * 1024;       // LDS bytes per CU
 constexpr int PF = (TILE16 + SCAN_T - 1) / SCAN_T;   // prefetch registers per lane (5)
 constexpr uint64_t NOPOS = ~0ULL;
+constexpr uint32_t NONE = 255;               // "no separator in the 128-bit view"
 typedef uint32_t v4u __attribute__((ext_vector_type(4)));   // one 16-byte load
 
 // ------------------------------------------------------------------ helpers
 __device__ __forceinline__ bool is_nl(uint32_t c) { return c == '\n' || c == '\r'; }
+__device__ __forceinline__ bool is_blank(uint32_t c) { return c == ' ' || c == '\t' || c == 0x0b || c == 0x0c; }
 
 // LDS-only barrier: waits for this wave's LDS traffic, not for in-flight global
 // loads (the next window's prefetch must stay in flight across it)
@@ -54,18 +62,14 @@ __device__ __forceinline__ void lds_barrier() {
     asm volatile("s_waitcnt lgkmcnt(0)\n\ts_barrier" ::: "memory");
 }
 
-// exact per-byte tests on a dword: 0x80 in every byte that matches
-__device__ __forceinline__ uint32_t zero_bytes(uint32_t v) {
-    return ~(((v & 0x7F7F7F7Fu) + 0x7F7F7F7Fu) | v | 0x7F7F7F7Fu);
+// exact per-byte tests on a dword.  nonzero_bytes: 0x80 in every nonzero byte.
+__device__ __forceinline__ uint32_t nonzero_bytes(uint32_t t) {
+    return (((t & 0x7F7F7F7Fu) + 0x7F7F7F7Fu) | t) & 0x80808080u;
 }
-__device__ __forceinline__ uint32_t eq_bytes(uint32_t x, uint32_t rep) { return zero_bytes(x ^ rep); }
 // 0x80 in every byte < n, for 0 < n <= 0x80 (rep_n = n * 0x01010101): no borrows
 // cross bytes because every byte of (x | 0x80..) is >= 0x80 >= n
 __device__ __forceinline__ uint32_t lt_bytes(uint32_t x, uint32_t rep_n) {
     return ~((x | 0x80808080u) - rep_n) & ~x & 0x80808080u;
-}
-__device__ __forceinline__ uint32_t pack4(uint32_t m) {   // 0x80 flags -> 4 bits
-    return ((m >> 7) & 1u) | ((m >> 14) & 2u) | ((m >> 21) & 4u) | ((m >> 28) & 8u);
 }
 
 // block-wide exclusive scan of one value per thread (SCAN_T threads)
@@ -91,84 +95,143 @@ __device__ uint32_t block_excl_scan(uint32_t v, uint32_t* wsum, uint32_t* total)
     return base + x - v;
 }
 
+// ------------------------------------------------------------------ per-record cells
+// cells of one record in registers: callers index them with unrolled loops only
+struct Cells {
+    Cell c[MAX_NEED];
+};
+
+// cells.c[a] for a uniform run-time slot `a`, without a run-time index
+// (field-wise selects: a branch per slot would let the optimiser merge the
+// copies into one load through a computed address, i.e. back into memory)
+__device__ __forceinline__ Cell sel_cell(bool t, const Cell& x, const Cell& y) {
+    Cell r;
+    r.kind = t ? x.kind : y.kind;
+    r.len = t ? x.len : y.len;
+    r.bits = t ? x.bits : y.bits;
+    return r;
+}
+__device__ __forceinline__ Cell get_cell(const Cells& cs, int a) {
+    Cell r = cs.c[0];
+#pragma unroll
+    for (int k = 1; k < MAX_NEED; k++) r = sel_cell(k == a, cs.c[k], r);
+    return r;
+}
+
+// the general cell parser (cell.h parse_cell) kept out of line: it carries the
+// date test and the big-number strtod fallback, which the fast paths rarely need
+__device__ __noinline__ Cell parse_cell_slow(const uint8_t* f, uint32_t len) { return parse_cell(f, len); }
+__device__ __noinline__ GKey group_key_slow(const Cell c) { return group_key(c); }
+
 // ------------------------------------------------------------------ general record parse
-// parse_line (csv_reader.c:278-338) restricted to the needed columns, reading
-// global memory: the exact path for records the fast walk declines, and for the
-// representative-row gather.  Fills cells[0..nneed) (NULL for columns the
-// record is too short to have); false when the record is short.
-__device__ bool parse_record_global(const uint8_t* rec, const ScanPlan& P, Cell* cells) {
-    if (P.nneed == 0) return true;
-    const uint32_t delim = P.delim, quote = P.quote;
-    uint32_t i = 0;
-    int col = 0, k = 0;
-    int want = P.need_col[0];
-    while (true) {
-        uint32_t c = rec[i];
-        while (c == ' ' || c == '\t' || c == 0x0b || c == 0x0c) { i = i + 1; c = rec[i]; }
-        if (is_nl(c)) break;                       // trailing empty field dropped
-        uint32_t fs, flen;
-        if (c == quote) {                          // quoted field (:294-317)
-            i = i + 1;
-            fs = i;
-            uint32_t acc = 0;
-            bool closed = false;
-            flen = 0;
-            while (true) {
-                c = rec[i];
-                if (is_nl(c)) break;
-                if (c == quote) {
-                    if (rec[i + 1] == quote) { i = i + 2; acc += 2; }
-                    else { flen = i - fs; i = i + 1; closed = true; break; }
-                } else {
-                    i = i + 1;
-                }
-            }
-            if (!closed) flen = acc;
-            c = rec[i];
-            while (c != delim && !is_nl(c)) { i = i + 1; c = rec[i]; }
-        } else {                                   // unquoted field (:318-324)
-            fs = i;
-            while (c != delim && !is_nl(c)) { i = i + 1; c = rec[i]; }
-            flen = i - fs;
-        }
-        if (col == want) {
-            cells[k] = parse_cell(rec + fs, flen);
-            if (++k == P.nneed) return true;
-            want = P.need_col[k];
-        }
-        col++;
-        if (c != delim) break;
+// One field of parse_line (csv_reader.c:278-338) at rec[i]: leading blanks are
+// skipped; returns false if the record ends there (a trailing field of blanks
+// is dropped).  On return [fs, fs + flen) is the field's value (a quoted field
+// without its quotes, `""` kept as two bytes; an unclosed quoted field has the
+// length of its `""` pairs) and i is at the terminator (delimiter or newline).
+__device__ __forceinline__ bool g_field(const uint8_t* rec, uint32_t& i, uint32_t delim, uint32_t quote,
+                                        uint32_t& fs, uint32_t& flen) {
+    uint32_t c = rec[i];
+    while (is_blank(c)) { i = i + 1; c = rec[i]; }
+    if (is_nl(c)) return false;
+    if (c == quote) {                          // quoted field (:294-317)
         i = i + 1;
+        fs = i;
+        uint32_t acc = 0;
+        bool closed = false;
+        flen = 0;
+        while (true) {
+            c = rec[i];
+            if (is_nl(c)) break;
+            if (c == quote) {
+                if (rec[i + 1] == quote) { i = i + 2; acc += 2; }
+                else { flen = i - fs; i = i + 1; closed = true; break; }
+            } else {
+                i = i + 1;
+            }
+        }
+        if (!closed) flen = acc;
+        c = rec[i];
+        while (c != delim && !is_nl(c)) { i = i + 1; c = rec[i]; }
+    } else {                                   // unquoted field (:318-324)
+        fs = i;
+        while (c != delim && !is_nl(c)) { i = i + 1; c = rec[i]; }
+        flen = i - fs;
     }
-    for (; k < P.nneed; k++) cells[k] = cell_null();
-    return false;
+    return true;
+}
+
+// parse_line restricted to the needed columns, into registers (unrolled over
+// the need slots).  Returns true when the record is too short for a needed column.
+__device__ __forceinline__ bool parse_record_regs(const uint8_t* rec, const ScanPlan& P, Cells& cs) {
+    const uint32_t delim = P.delim, quote = P.quote;
+    uint32_t i = 0, fs = 0, flen = 0;
+    int col = 0;
+    bool ended = false;
+#pragma unroll
+    for (int k = 0; k < MAX_NEED; k++) {
+        if (k >= P.nneed) break;
+        const int want = P.need_col[k];
+        Cell c = cell_null();
+        while (!ended && col < want) {
+            if (!g_field(rec, i, delim, quote, fs, flen) || rec[i] != delim) ended = true;
+            else { i = i + 1; col++; }
+        }
+        if (!ended) {
+            if (!g_field(rec, i, delim, quote, fs, flen)) {
+                ended = true;
+            } else {
+                c = parse_cell_slow(rec + fs, flen);
+                if (rec[i] == delim) { i = i + 1; col++; }
+                else ended = true;                  // later columns do not exist
+            }
+        }
+        cs.c[k] = c;
+    }
+    return ended;
+}
+
+// the same into a global array (representative-row gather)
+__device__ void parse_record_out(const uint8_t* rec, const ScanPlan& P, Cell* out) {
+    const uint32_t delim = P.delim, quote = P.quote;
+    uint32_t i = 0, fs = 0, flen = 0;
+    int col = 0;
+    bool ended = false;
+    for (int k = 0; k < P.nneed; k++) {
+        const int want = P.need_col[k];
+        Cell c = cell_null();
+        while (!ended && col < want) {
+            if (!g_field(rec, i, delim, quote, fs, flen) || rec[i] != delim) ended = true;
+            else { i = i + 1; col++; }
+        }
+        if (!ended) {
+            if (!g_field(rec, i, delim, quote, fs, flen)) {
+                ended = true;
+            } else {
+                c = parse_cell(rec + fs, flen);
+                if (rec[i] == delim) { i = i + 1; col++; }
+                else ended = true;
+            }
+        }
+        out[k] = c;
+    }
 }
 
 // ------------------------------------------------------------------ predicate VM
+// value stack in registers: select-based access (no run-time array index)
 struct Stack {
-    Cell s0, s1, s2, s3, s4, s5, s6, s7;
+    Cell s[8];
     __device__ __forceinline__ Cell get(int i) const {
-        switch (i) {
-            case 0: return s0; case 1: return s1; case 2: return s2; case 3: return s3;
-            case 4: return s4; case 5: return s5; case 6: return s6; default: return s7;
-        }
+        Cell r = s[0];
+#pragma unroll
+        for (int j = 1; j < 8; j++) r = sel_cell(j == i, s[j], r);
+        return r;
     }
     __device__ __forceinline__ void set(int i, const Cell& v) {
-        switch (i) {
-            case 0: s0 = v; break; case 1: s1 = v; break; case 2: s2 = v; break;
-            case 3: s3 = v; break; case 4: s4 = v; break; case 5: s5 = v; break;
-            case 6: s6 = v; break; default: s7 = v; break;
-        }
+#pragma unroll
+        for (int j = 0; j < 8; j++) s[j] = sel_cell(j == i, v, s[j]);
     }
 };
-
-__device__ __forceinline__ Cell cell_at(const Cell* cells, int k) {
-    switch (k) {
-        case 0: return cells[0]; case 1: return cells[1]; case 2: return cells[2];
-        case 3: return cells[3]; case 4: return cells[4]; case 5: return cells[5];
-        case 6: return cells[6]; default: return cells[7];
-    }
-}
 
 __device__ __forceinline__ bool cmp_result(uint32_t op, int c) {
     switch (op) {
@@ -182,16 +245,16 @@ __device__ __forceinline__ bool cmp_result(uint32_t op, int c) {
 }
 
 // evaluate_condition (evaluator_conditions.c:62-164) over the flattened WHERE tree
-__device__ bool eval_where(const ScanPlan& P, const Cell* cells) {
-    if (P.nprog == 3 && P.prog[0].op == OP_COL && P.prog[1].op == OP_CONST && P.prog[2].op == OP_CMP)
-        return cmp_result(P.prog[2].a, compare(cell_at(cells, P.prog[0].a), P.consts[P.prog[1].b]));
+__device__ __forceinline__ bool eval_where_vm(const ScanPlan& P, const Cells& cs) {
     Stack st;
+#pragma unroll
+    for (int j = 0; j < 8; j++) st.s[j] = cell_null();
     int sp = 0;
     uint32_t bs = 0;   // bool stack, top = bit 0
     for (int pc = 0; pc < P.nprog; pc++) {
         const Insn in = P.prog[pc];
         switch (in.op) {
-            case OP_COL: st.set(sp++, cell_at(cells, in.a)); break;
+            case OP_COL: st.set(sp++, get_cell(cs, in.a)); break;
             case OP_CONST: st.set(sp++, P.consts[in.b]); break;
             case OP_NULLV: st.set(sp++, cell_null()); break;
             case OP_ARITH: {
@@ -253,7 +316,7 @@ __device__ __forceinline__ uint32_t tag_of(uint64_t h) {
     return t < 2 ? t + 2 : t;
 }
 
-__device__ int g_insert(const GroupTable& gt, const GKey& k, uint64_t h, ScanStats* st) {
+__device__ int g_insert(const GroupTable& gt, const GKey k, uint64_t h, ScanStats* st) {
     const uint32_t tg = tag_of(h);
     const uint32_t mask = gt.cap - 1;
     const uint32_t cl = gk_clslen(k);
@@ -298,7 +361,7 @@ __device__ int g_insert(const GroupTable& gt, const GKey& k, uint64_t h, ScanSta
 // lock releases it in the same trip.  Callers must reach these with the whole
 // wave (uniform control flow), passing `need` = false for idle lanes.
 __device__ void g_ext_update(bool need, const GroupTable& gt, int a, uint8_t kind, uint32_t i,
-                             const Cell& c, uint64_t pos, ScanStats* st) {
+                             const Cell c, uint64_t pos, ScanStats* st) {
     if (pos == NOPOS) need = false;
     uint32_t trips = 0;
     while (__any(need)) {
@@ -352,7 +415,7 @@ struct ExtLds {            // ACC_MIN / ACC_MAX
     uint32_t* lock;
 };
 
-__device__ int l_insert(const LdsTable& t, const GKey& k, uint64_t h) {
+__device__ __forceinline__ int l_insert(const LdsTable& t, const GKey k, uint64_t h) {
     const uint32_t tg = tag_of(h);
     const uint32_t cl = gk_clslen(k);
     for (uint32_t probe = 0; probe < 64; probe++) {
@@ -387,8 +450,8 @@ __device__ int l_insert(const LdsTable& t, const GKey& k, uint64_t h) {
 }
 
 // wave-uniform LDS MIN/MAX update (see g_ext_update)
-__device__ void lds_ext_update(bool need, const ExtLds& e, uint32_t s, uint8_t kind, const Cell& c,
-                               uint64_t pos) {
+__device__ __forceinline__ void lds_ext_update(bool need, const ExtLds& e, uint32_t s, uint8_t kind,
+                                               const Cell c, uint64_t pos) {
     while (__any(need)) {
         if (need) {
             if (atomicCAS(&e.lock[s], 0u, 1u) == 0u) {
@@ -404,22 +467,42 @@ __device__ void lds_ext_update(bool need, const ExtLds& e, uint32_t s, uint8_t k
     }
 }
 
-// ------------------------------------------------------------------ fast field parsers
-// 16 bytes of the tile starting at byte offset `o` (any alignment), little-endian
-__device__ __forceinline__ void load16(const uint8_t* tile, uint32_t o, uint64_t& w0, uint64_t& w1) {
-    const uint32_t* t32 = (const uint32_t*)tile;
-    const uint32_t a = o >> 2, sh = (o & 3) * 8;
-    const uint32_t d0 = t32[a], d1 = t32[a + 1], d2 = t32[a + 2], d3 = t32[a + 3], d4 = t32[a + 4];
-    const uint32_t e0 = (uint32_t)((((uint64_t)d1 << 32) | d0) >> sh);
-    const uint32_t e1 = (uint32_t)((((uint64_t)d2 << 32) | d1) >> sh);
-    const uint32_t e2 = (uint32_t)((((uint64_t)d3 << 32) | d2) >> sh);
-    const uint32_t e3 = (uint32_t)((((uint64_t)d4 << 32) | d3) >> sh);
-    w0 = (uint64_t)e0 | ((uint64_t)e1 << 32);
-    w1 = (uint64_t)e2 | ((uint64_t)e3 << 32);
+// ------------------------------------------------------------------ fast field path
+// 128-bit view of a per-64-byte mask starting at window offset 64*wi + o
+struct View {
+    uint64_t lo, hi;
+};
+__device__ __forceinline__ View view128(const uint64_t* m, uint32_t wi, uint32_t o) {
+    const uint64_t a0 = m[wi], a1 = m[wi + 1];
+    View v;
+    v.lo = o ? (a0 >> o) | (a1 << (64 - o)) : a0;
+    v.hi = a1 >> o;
+    return v;
+}
+__device__ __forceinline__ uint32_t first128(const View& v) {
+    return v.lo ? (uint32_t)__builtin_ctzll(v.lo) : (v.hi ? 64u + (uint32_t)__builtin_ctzll(v.hi) : NONE);
+}
+__device__ __forceinline__ void pop128(View& v) {
+    if (v.lo) v.lo &= v.lo - 1;
+    else v.hi &= v.hi - 1;
 }
 
-__device__ __forceinline__ uint32_t byte_of(uint64_t w0, uint64_t w1, uint32_t i) {
-    return (uint32_t)((i < 8 ? w0 >> (8 * i) : w1 >> (8 * (i - 8))) & 0xff);
+// 16 bytes of the tile at byte offset `o` (any alignment), as four dwords
+__device__ __forceinline__ void load16(const uint8_t* tile, uint32_t o, uint32_t& e0, uint32_t& e1,
+                                       uint32_t& e2, uint32_t& e3) {
+    const uint32_t* t32 = (const uint32_t*)tile;
+    const uint32_t a = o >> 2, sh = o & 3;
+    const uint32_t d0 = t32[a], d1 = t32[a + 1], d2 = t32[a + 2], d3 = t32[a + 3], d4 = t32[a + 4];
+    e0 = __builtin_amdgcn_alignbyte(d1, d0, sh);
+    e1 = __builtin_amdgcn_alignbyte(d2, d1, sh);
+    e2 = __builtin_amdgcn_alignbyte(d3, d2, sh);
+    e3 = __builtin_amdgcn_alignbyte(d4, d3, sh);
+}
+
+// bytes [0, len) of a dword holding bytes [4j, 4j + 4) of a field
+__device__ __forceinline__ uint32_t len_mask(uint32_t len, uint32_t j) {
+    const uint32_t n = len > 4 * j ? len - 4 * j : 0;
+    return n >= 4 ? 0xFFFFFFFFu : ((1u << (8 * n)) - 1);
 }
 
 __device__ __forceinline__ double pow10_exact(uint32_t e) {   // 10^e, e <= 22, exact in double
@@ -428,38 +511,45 @@ __device__ __forceinline__ double pow10_exact(uint32_t e) {   // 10^e, e <= 22, 
     return r;
 }
 
-// Type one field of `len` bytes at tile offset `o` that holds no bad byte (no
-// whitespace, quote, NUL, '+').  Returns false when the exact general parser
-// must decide: date-shaped fields (parse_date may accept them), numerals past
-// the exact fast cases, fields over 16 bytes, or a delimiter strtod/strtoll
-// could read across (`num_ok` false).  `want_key`: also produce the group key.
-__device__ __forceinline__ bool fast_cell(const uint8_t* tile, uint32_t o, uint32_t len,
-                                          const uint8_t* gfield, bool num_ok, Cell& out,
-                                          bool want_key, GKey& key) {
+enum : int { FF_OK = 0, FF_CELL = 1, FF_REC = 2 };
+
+// Type a field of `len` bytes at tile offset `to` whose bytes hold no record
+// terminator, delimiter or quote.  FF_OK: `out` (and `key` when want_key) are
+// final.  FF_CELL: the field is clean but needs the general cell parser (date
+// shaped, long numerals, long fields, a delimiter strtod could read across).
+// FF_REC: a byte <= ' ' (blank, control, NUL) -- leading blanks move the field
+// start and blank-only last fields are dropped, so the record path decides.
+__device__ __forceinline__ int fast_field(const uint8_t* tile, uint32_t to, uint32_t len, bool num_ok,
+                                          bool want_key, Cell& out, GKey& key) {
     if (len == 0) {
         out = cell_null();
         if (want_key) key = group_key(out);
-        return true;
+        return FF_OK;
     }
-    if (len > 16) return false;
-    uint64_t w0, w1;
-    load16(tile, o, w0, w1);
-    if (len <= 8) {
-        if (len < 8) w0 &= (1ULL << (8 * len)) - 1;
-        w1 = 0;
-    } else if (len < 16) {
-        w1 &= (1ULL << (8 * (len - 8))) - 1;
+    if (len > 16) {
+        for (uint32_t i = 0; i < len; i++)
+            if (tile[to + i] <= 0x20) return FF_REC;
+        return FF_CELL;
     }
-    const uint32_t c0 = (uint32_t)(w0 & 0xff);
+    uint32_t d0, d1, d2, d3;
+    load16(tile, to, d0, d1, d2, d3);
+    const uint32_t m0 = len_mask(len, 0), m1 = len_mask(len, 1), m2 = len_mask(len, 2), m3 = len_mask(len, 3);
+    const uint32_t low = lt_bytes(d0 | ~m0, 0x21212121u) | lt_bytes(d1 | ~m1, 0x21212121u) |
+                         lt_bytes(d2 | ~m2, 0x21212121u) | lt_bytes(d3 | ~m3, 0x21212121u);
+    if (low) return FF_REC;
+    const uint64_t w0 = (uint64_t)(d0 & m0) | ((uint64_t)(d1 & m1) << 32);
+    const uint64_t w1 = (uint64_t)(d2 & m2) | ((uint64_t)(d3 & m3) << 32);
+    const uint32_t c0 = d0 & 0xff;
+    if (c0 == '+') return FF_CELL;
     const bool lead_num = is_digit(c0) || c0 == '-' || c0 == '.';
-    if (len >= 8 && len <= 10 && lead_num) return false;     // parse_date may accept it
-    // infer_type's numeric shape ([+-] digits with at most one '.', at least one digit)
+    if (len >= 8 && len <= 10 && c0 != '.' && lead_num) return FF_CELL;   // parse_date may accept it
+    // infer_type's numeric shape: [-] digits with at most one '.', at least one digit
     bool numeric = lead_num, dot = false, dig = false;
     uint64_t w = 0;
     uint32_t nsig = 0, frac = 0;
     if (numeric) {
         for (uint32_t i = (c0 == '-') ? 1u : 0u; i < len; i++) {
-            const uint32_t b = byte_of(w0, w1, i);
+            const uint32_t b = (uint32_t)((i < 8 ? w0 >> (8 * i) : w1 >> (8 * (i - 8))) & 0xff);
             if (is_digit(b)) {
                 dig = true;
                 if (nsig || b != '0') { w = w * 10 + (b - '0'); nsig++; }
@@ -474,103 +564,35 @@ __device__ __forceinline__ bool fast_cell(const uint8_t* tile, uint32_t o, uint3
         numeric = numeric && dig;
     }
     if (numeric) {
-        if (!num_ok) return false;
+        if (!num_ok) return FF_CELL;
         const bool neg = c0 == '-';
         if (!dot) {
-            if (nsig > 18) return false;                       // strtoll range: general path
+            if (nsig > 18) return FF_CELL;                     // strtoll range: general path
             out = cell_int(neg ? -(int64_t)w : (int64_t)w);
         } else {
-            if (nsig > 15 || frac > 22) return false;          // Clinger's exact case only
+            if (nsig > 15 || frac > 22) return FF_CELL;        // Clinger's exact case only
             double v = (double)w;                              // exact: w < 10^15
             if (frac) v = v / pow10_exact(frac);               // one correctly rounded division
             out = cell_dbl(neg ? -v : v);
         }
         if (want_key) key = group_key(out);
-        return true;
+        return FF_OK;
     }
-    // STRING without whitespace or NUL: already what trim_whitespace returns
+    // STRING with no blank or NUL: exactly what cq_strndup + trim_whitespace give
     out.kind = K_STR;
     out.len = len;
-    out.bits = (uint64_t)(uintptr_t)gfield;
+    out.bits = 0;                                              // caller sets the address
     if (want_key) {
         key.cls = GK_STR;
         key.len = len;
         key.w0 = w0;
         key.w1 = w1;
     }
-    return true;
-}
-
-// any set bit of the per-64-byte masks `m` in [a, b)
-__device__ __forceinline__ bool any_bits(const uint64_t* m, uint32_t a, uint32_t b) {
-    if (a >= b) return false;
-    const uint32_t wa = a >> 6, wb = (b - 1) >> 6;
-    const uint64_t lo = ~0ULL << (a & 63);
-    const uint64_t hi = ((b & 63) == 0) ? ~0ULL : ((1ULL << (b & 63)) - 1);
-    if (wa == wb) return (m[wa] & lo & hi) != 0;
-    if (m[wa] & lo) return true;
-    for (uint32_t w = wa + 1; w < wb; w++)
-        if (m[w]) return true;
-    return (m[wb] & hi) != 0;
-}
-
-// Walk the record at window offset r with the separator mask.  Returns false if
-// the record must take the general path: a field starting with a bad byte
-// (quote, leading whitespace), or a record running past the staged bytes.
-// Fills cells (NULL where the record is short) and the group key.
-__device__ __forceinline__ bool fast_record(const uint8_t* tile, const uint64_t* sepw, const uint64_t* nlw,
-                                            const uint64_t* badw, uint32_t r, const uint8_t* grec,
-                                            const ScanPlan& P, bool num_ok, Cell* cells, GKey& key,
-                                            bool& short_row) {
-    short_row = false;
-    if (P.nneed == 0) return true;
-    uint32_t pos = r;
-    int col = 0, k = 0;
-    int want = P.need_col[0];
-    while (true) {
-        const uint32_t wi = pos >> 6;
-        if (wi >= (uint32_t)NMW) return false;
-        if ((badw[wi] >> (pos & 63)) & 1ULL) return false;
-        const uint64_t m = sepw[wi] >> (pos & 63);
-        uint32_t e;
-        if (m) {
-            e = pos + (uint32_t)__ffsll((long long)m) - 1;
-        } else {
-            uint32_t w = wi + 1;
-            while (w < (uint32_t)NMW && sepw[w] == 0) w++;
-            if (w >= (uint32_t)NMW) return false;
-            e = w * 64 + (uint32_t)__ffsll((long long)sepw[w]) - 1;
-        }
-        const bool at_nl = (nlw[e >> 6] >> (e & 63)) & 1ULL;
-        if (e == pos && at_nl) break;                  // empty trailing field: dropped
-        if (col == want) {
-            const uint32_t len = e - pos;
-            const bool gkey = k == P.group_slot;
-            Cell c;
-            const bool ok = !any_bits(badw, pos, e) &&
-                            fast_cell(tile, PRE + pos, len, grec + (pos - r), num_ok, c, gkey, key);
-            if (!ok) {
-                c = parse_cell(grec + (pos - r), len);
-                if (gkey) key = group_key(c);
-            }
-            cells[k] = c;
-            if (++k == P.nneed) return true;
-            want = P.need_col[k];
-        }
-        col++;
-        if (at_nl) break;
-        pos = e + 1;
-    }
-    for (; k < P.nneed; k++) {
-        cells[k] = cell_null();
-        if (k == P.group_slot) key = group_key(cells[k]);
-    }
-    short_row = true;
-    return true;
+    return FF_OK;
 }
 
 // ------------------------------------------------------------------ the scan kernel
-// dynamic LDS: [tile][nl/sep/bad masks][rs][scan scratch][group table][accumulators]
+// dynamic LDS: [tile][nl/sep masks][quote flags][rs][scan scratch][group table][accumulators]
 __device__ __forceinline__ uint8_t* carve(uint8_t*& q, size_t bytes) {
     uint8_t* r = q;
     q += (bytes + 15) & ~(size_t)15;
@@ -584,6 +606,39 @@ __device__ __forceinline__ void prefetch(const uint8_t* g, uint64_t ws, v4u* pf)
         const int i = threadIdx.x + j * SCAN_T;
         if (i < TILE16) pf[j] = __builtin_nontemporal_load(src + i);
     }
+}
+
+// classify 64 staged bytes: terminator and separator masks, quote presence
+__device__ __forceinline__ void classify64(const uint8_t* p, uint32_t rep_d, uint32_t rep_q, uint64_t& nlm,
+                                           uint64_t& sepm, bool& has_q) {
+    const v4u* src = (const v4u*)p;
+    uint32_t nl_lo = 0, nl_hi = 0, sp_lo = 0, sp_hi = 0, qacc = 0x80808080u;
+#pragma unroll
+    for (int v = 0; v < 4; v++) {
+        const v4u x4 = src[v];
+#pragma unroll
+        for (int j = 0; j < 4; j++) {
+            const uint32_t x = x4[j];
+            const uint32_t nl_inv = nonzero_bytes(x ^ 0x0A0A0A0Au) & nonzero_bytes(x ^ 0x0D0D0D0Du);
+            const uint32_t sp_inv = nl_inv & nonzero_bytes(x ^ rep_d);
+            qacc &= nonzero_bytes(x ^ rep_q);
+            // 0x80 flags -> nibbles: separators in bits 0-3, terminators in bits 4-7
+            const uint32_t c = ((~sp_inv & 0x80808080u) >> 7) | ((~nl_inv & 0x80808080u) >> 3);
+            uint32_t t = c | (c >> 7);
+            t = t | (t >> 14);
+            const int d = v * 4 + j, sh = (d & 7) * 4;
+            if (d < 8) {
+                sp_lo |= (t & 0xFu) << sh;
+                nl_lo |= ((t >> 4) & 0xFu) << sh;
+            } else {
+                sp_hi |= (t & 0xFu) << sh;
+                nl_hi |= ((t >> 4) & 0xFu) << sh;
+            }
+        }
+    }
+    nlm = (uint64_t)nl_lo | ((uint64_t)nl_hi << 32);
+    sepm = (uint64_t)sp_lo | ((uint64_t)sp_hi << 32);
+    has_q = qacc != 0x80808080u;
 }
 
 // The plan and the table descriptor live in constant memory (written on the
@@ -605,8 +660,8 @@ __global__ __launch_bounds__(SCAN_T) void scan_kernel(const uint8_t* __restrict_
     uint8_t* tile = carve(q, TILE);
     uint64_t* nlw = (uint64_t*)carve(q, NMW * 8);
     uint64_t* sepw = (uint64_t*)carve(q, NMW * 8);
-    uint64_t* badw = (uint64_t*)carve(q, NMW * 8);
-    uint32_t* rs = (uint32_t*)carve(q, RSMAX * 4);
+    uint8_t* qfl = carve(q, NMW);
+    uint16_t* rs = (uint16_t*)carve(q, RSMAX * 2);
     uint32_t* wsum = (uint32_t*)carve(q, 64);
     LdsTable lt;
     LdsAcc la[MAX_ACC];
@@ -661,6 +716,15 @@ __global__ __launch_bounds__(SCAN_T) void scan_kernel(const uint8_t* __restrict_
         my_sum[a] = 0.0; my_num[a] = 0; my_ext[a] = cell_null(); my_pos[a] = NOPOS; my_cls[a] = 0;
     }
 
+    // uniform plan facts
+    const int nneed = P.nneed;
+    const int gslot = GROUPED ? P.group_slot : -1;
+    const bool simple = P.nprog == 3 && P.prog[0].op == OP_COL && P.prog[1].op == OP_CONST && P.prog[2].op == OP_CMP;
+    const int wslot = simple ? P.prog[0].a : 0;
+    const uint32_t wop = simple ? P.prog[2].a : 0;
+    const Cell wconst = simple ? P.consts[P.prog[1].b] : cell_null();
+    const GKey null_key = group_key(cell_null());
+
     const uint64_t lo_ok = P.data_begin > P.range_begin ? P.data_begin : P.range_begin;
     const uint64_t hi_ok = P.range_end < P.n ? P.range_end : P.n;
     const uint64_t first_win = P.range_begin / WIN;
@@ -668,7 +732,7 @@ __global__ __launch_bounds__(SCAN_T) void scan_kernel(const uint8_t* __restrict_
     const uint32_t delim = P.delim, quote = P.quote;
     const uint32_t rep_d = delim * 0x01010101u, rep_q = quote * 0x01010101u;
     // strtoll/strtod read past the field end: a delimiter they could consume
-    // (digit, '.', letter) disables the fast numeric parsers
+    // (digit, '.', letter) sends numerals to the general cell parser
     const bool num_ok = !(is_digit(delim) || delim == '.' || ((delim | 32) >= 'a' && (delim | 32) <= 'z'));
 
     v4u pf[PF];
@@ -687,41 +751,28 @@ __global__ __launch_bounds__(SCAN_T) void scan_kernel(const uint8_t* __restrict_
         if (w + gridDim.x < last_win) prefetch(g, (w + gridDim.x) * WIN, pf);   // in flight meanwhile
 
         // ---- classify: lane t -> mask word t (lanes 0..31 also the margin words)
-        for (int wi = tid; wi < NMW; wi += SCAN_T) {
-            const v4u* src = (const v4u*)(tile + PRE + wi * 64);
-            uint64_t nlm = 0, sepm = 0, badm = 0;
-#pragma unroll
-            for (int v = 0; v < 4; v++) {
-                const v4u x4 = src[v];
-                const uint32_t xs[4] = {x4.x, x4.y, x4.z, x4.w};
-#pragma unroll
-                for (int j = 0; j < 4; j++) {
-                    const uint32_t x = xs[j];
-                    uint32_t special = lt_bytes(x, 0x2D2D2D2Du);
-                    if (delim >= 0x2D) special |= eq_bytes(x, rep_d);
-                    if (quote >= 0x2D) special |= eq_bytes(x, rep_q);
-                    if (special) {
-                        const uint32_t nl = eq_bytes(x, 0x0A0A0A0Au) | eq_bytes(x, 0x0D0D0D0Du);
-                        const uint32_t dl = eq_bytes(x, rep_d) & ~nl;
-                        const uint32_t bd = special & ~nl & ~dl;
-                        const int sh = v * 16 + j * 4;
-                        nlm |= (uint64_t)pack4(nl) << sh;
-                        sepm |= (uint64_t)pack4(nl | dl) << sh;
-                        badm |= (uint64_t)pack4(bd) << sh;
-                    }
-                }
+        uint64_t my_nl;
+        {
+            uint64_t sepm;
+            bool hq;
+            classify64(tile + PRE + tid * 64, rep_d, rep_q, my_nl, sepm, hq);
+            nlw[tid] = my_nl;
+            sepw[tid] = sepm;
+            qfl[tid] = hq;
+            if (tid < NMW - SCAN_T) {
+                uint64_t n2;
+                classify64(tile + PRE + (SCAN_T + tid) * 64, rep_d, rep_q, n2, sepm, hq);
+                nlw[SCAN_T + tid] = n2;
+                sepw[SCAN_T + tid] = sepm;
+                qfl[SCAN_T + tid] = hq;
             }
-            nlw[wi] = nlm;
-            sepw[wi] = sepm;
-            badw[wi] = badm;
         }
         lds_barrier();
         // ---- record starts in this lane's 64 window bytes
         uint64_t starts;
         {
-            const uint64_t nlm = nlw[tid];
             const uint64_t prev_nl = (tid == 0) ? (is_nl(tile[PRE - 1]) ? 1ULL : 0ULL) : (nlw[tid - 1] >> 63);
-            starts = ~nlm & ((nlm << 1) | prev_nl);
+            starts = ~my_nl & ((my_nl << 1) | prev_nl);
             const uint64_t base = ws + (uint64_t)tid * 64;
             if (base + 64 <= lo_ok || base >= hi_ok) {
                 starts = 0;
@@ -740,7 +791,7 @@ __global__ __launch_bounds__(SCAN_T) void scan_kernel(const uint8_t* __restrict_
                 while (m) {
                     const int b = __ffsll((long long)m) - 1;
                     m &= m - 1;
-                    if (ri >= chunk && ri < chunk + RSMAX) rs[ri - chunk] = tid * 64 + b;
+                    if (ri >= chunk && ri < chunk + RSMAX) rs[ri - chunk] = (uint16_t)(tid * 64 + b);
                     ri++;
                 }
             }
@@ -752,36 +803,79 @@ __global__ __launch_bounds__(SCAN_T) void scan_kernel(const uint8_t* __restrict_
                 const bool valid = ri < nrec;
                 const uint32_t r = valid ? rs[ri] : 0;
                 const uint64_t rec = ws + r;
-                Cell cells[MAX_NEED];
+                Cells cs;
 #pragma unroll
-                for (int k = 0; k < MAX_NEED; k++) cells[k] = cell_null();
-                GKey key;
-                key.cls = 0; key.len = 0; key.w0 = 0; key.w1 = 0;
+                for (int k = 0; k < MAX_NEED; k++) cs.c[k] = cell_null();
+                GKey key = null_key;
                 bool pass = false;
                 if (valid) {
-                    bool short_row = false;
-                    if (!fast_record(tile, sepw, nlw, badw, r, g + rec, P, num_ok, cells, key, short_row)) {
+                    // -- fast walk over the 128-bit mask views at the record start
+                    const uint32_t wi = r >> 6, o = r & 63;
+                    View S = view128(sepw, wi, o);
+                    const uint32_t rend = first128(view128(nlw, wi, o));
+                    bool fail = (qfl[wi] | qfl[wi + 1]) != 0;
+                    bool ended = false;
+                    uint32_t fs = 0;
+                    int col = 0;
+#pragma unroll
+                    for (int k = 0; k < MAX_NEED; k++) {
+                        if (k >= nneed) break;
+                        const int want = P.need_col[k];
+                        for (; col < want; col++) {            // uniform trip count
+                            const uint32_t e = first128(S);
+                            if (e == NONE) fail = true;
+                            else if (e == rend) ended = true;
+                            fs = e + 1;
+                            pop128(S);
+                        }
+                        Cell c = cell_null();
+                        if (!ended && !fail) {
+                            const uint32_t e = first128(S);
+                            if (e == NONE) {
+                                fail = true;
+                            } else {
+                                const uint32_t len = e - fs;
+                                const int st = fast_field(tile, PRE + r + fs, len, num_ok, k == gslot, c, key);
+                                if (st == FF_CELL) {
+                                    c = parse_cell_slow(g + rec + fs, len);
+                                    if (k == gslot) key = group_key_slow(c);
+                                } else if (st == FF_REC) {
+                                    fail = true;
+                                }
+                                if (c.kind == K_STR && st == FF_OK) c.bits = (uint64_t)(uintptr_t)(g + rec + fs);
+                            }
+                        }
+                        cs.c[k] = c;
+                    }
+                    bool short_row = ended;
+                    if (fail) {
+                        // -- the general parse_line cursor over global memory
                         my_slow++;
-                        short_row = !parse_record_global(g + rec, P, cells);
-                        if (GROUPED) key = group_key(cell_at(cells, P.group_slot));
+                        short_row = parse_record_regs(g + rec, P, cs);
+                        if (GROUPED) key = group_key_slow(get_cell(cs, gslot));
                     }
                     my_records++;
                     if (short_row) my_short++;
-                    pass = P.nprog == 0 || eval_where(P, cells);
+                    if (P.nprog == 0) pass = true;
+                    else if (simple) pass = cmp_result(wop, compare(get_cell(cs, wslot), wconst));
+                    else pass = eval_where_vm(P, cs);
                     if (pass) my_pass++;
                 }
                 if (pass && row_out) {
                     const unsigned long long slot = atomicAdd(&stats->rows_emitted, 1ULL);
                     if (slot < row_cap) {
                         row_out[slot] = rec;
-                        if (cells_out)   // debug: the cells this kernel parsed
-                            for (int k = 0; k < P.nneed; k++) cells_out[slot * P.nneed + k] = cell_at(cells, k);
+                        if (cells_out) {   // debug: the cells this kernel parsed
+#pragma unroll
+                            for (int k = 0; k < MAX_NEED; k++)
+                                if (k < nneed) cells_out[slot * nneed + k] = cs.c[k];
+                        }
                     }
                 }
                 if (pass) {
 #pragma unroll
                     for (int a = 0; a < MAX_ACC; a++)
-                        if (a < P.nacc) my_cls[a] |= class_bit(cell_at(cells, P.acc[a].slot));
+                        if (a < P.nacc) my_cls[a] |= class_bit(get_cell(cs, P.acc[a].slot));
                 }
                 if (!GROUPED) {
                     if (pass) {
@@ -789,8 +883,8 @@ __global__ __launch_bounds__(SCAN_T) void scan_kernel(const uint8_t* __restrict_
                         if (rec < my_first) my_first = rec;
 #pragma unroll
                         for (int a = 0; a < MAX_ACC; a++) {
-                            if (a >= P.nacc) continue;
-                            const Cell c = cell_at(cells, P.acc[a].slot);
+                            if (a >= P.nacc) break;
+                            const Cell c = get_cell(cs, P.acc[a].slot);
                             if (P.acc[a].kind == ACC_SUM) {
                                 if (is_num(c)) { my_sum[a] += num_of(c); my_num[a]++; }
                             } else if (c.kind != K_NULL && ext_better(P.acc[a].kind, c, rec, my_ext[a], my_pos[a])) {
@@ -813,8 +907,9 @@ __global__ __launch_bounds__(SCAN_T) void scan_kernel(const uint8_t* __restrict_
                         if (rec < lt.first[s]) atomicMin(&lt.first[s], (unsigned long long)rec);
 #pragma unroll
                         for (int a = 0; a < MAX_ACC; a++) {
-                            if (a >= P.nacc || !la[a].sum) continue;
-                            const Cell c = cell_at(cells, P.acc[a].slot);
+                            if (a >= P.nacc) break;
+                            if (!la[a].sum) continue;
+                            const Cell c = get_cell(cs, P.acc[a].slot);
                             if (is_num(c)) {
                                 atomicAdd(&la[a].sum[s], num_of(c));
                                 atomicAdd(&la[a].num[s], 1u);
@@ -823,8 +918,9 @@ __global__ __launch_bounds__(SCAN_T) void scan_kernel(const uint8_t* __restrict_
                     }
 #pragma unroll
                     for (int a = 0; a < MAX_ACC; a++) {
-                        if (a >= P.nacc || !le[a].c) continue;   // uniform
-                        const Cell c = cell_at(cells, P.acc[a].slot);
+                        if (a >= P.nacc) break;
+                        if (!le[a].c) continue;                  // uniform
+                        const Cell c = get_cell(cs, P.acc[a].slot);
                         lds_ext_update(in_lds && c.kind != K_NULL, le[a], in_lds ? (uint32_t)s : 0u,
                                        P.acc[a].kind, c, rec);
                     }
@@ -837,8 +933,10 @@ __global__ __launch_bounds__(SCAN_T) void scan_kernel(const uint8_t* __restrict_
                             if (gi >= 0) {
                                 atomicAdd(&gt.cnt[gi], 1ULL);
                                 atomicMin(&gt.first[gi], (unsigned long long)rec);
-                                for (int a = 0; a < P.nacc; a++) {
-                                    const Cell c = cell_at(cells, P.acc[a].slot);
+#pragma unroll
+                                for (int a = 0; a < MAX_ACC; a++) {
+                                    if (a >= P.nacc) break;
+                                    const Cell c = get_cell(cs, P.acc[a].slot);
                                     if (P.acc[a].kind == ACC_SUM && is_num(c)) {
                                         atomicAdd(&gt.sum[a][gi], num_of(c));
                                         atomicAdd(&gt.num[a][gi], 1ULL);
@@ -846,9 +944,11 @@ __global__ __launch_bounds__(SCAN_T) void scan_kernel(const uint8_t* __restrict_
                                 }
                             }
                         }
-                        for (int a = 0; a < P.nacc; a++) {
+#pragma unroll
+                        for (int a = 0; a < MAX_ACC; a++) {
+                            if (a >= P.nacc) break;
                             if (P.acc[a].kind == ACC_SUM) continue;   // uniform
-                            const Cell c = cell_at(cells, P.acc[a].slot);
+                            const Cell c = get_cell(cs, P.acc[a].slot);
                             g_ext_update(spill && gi >= 0 && c.kind != K_NULL, gt, a, P.acc[a].kind,
                                          gi >= 0 ? (uint32_t)gi : 0u, c, rec, stats);
                         }
@@ -878,7 +978,9 @@ __global__ __launch_bounds__(SCAN_T) void scan_kernel(const uint8_t* __restrict_
             if (ps) atomicAdd(&stats->passed, ps);
         }
     }
-    for (int a = 0; a < P.nacc; a++) {
+#pragma unroll
+    for (int a = 0; a < MAX_ACC; a++) {
+        if (a >= P.nacc) break;
         uint32_t m = my_cls[a];
         for (int o = 32; o > 0; o >>= 1) m |= __shfl_down(m, o, 64);
         if ((tid & 63) == 0 && m) atomicOr(&stats->acc_classes[a], m);
@@ -911,15 +1013,18 @@ __global__ __launch_bounds__(SCAN_T) void scan_kernel(const uint8_t* __restrict_
             if (gi >= 0) {
                 if (c) atomicAdd(&gt.cnt[gi], c);
                 if (f != NOPOS) atomicMin(&gt.first[gi], f);
-                for (int a = 0; a < P.nacc; a++)
-                    if (P.acc[a].kind == ACC_SUM && nm[a]) {
+#pragma unroll
+                for (int a = 0; a < MAX_ACC; a++)
+                    if (a < P.nacc && P.acc[a].kind == ACC_SUM && nm[a]) {
                         atomicAdd(&gt.sum[a][gi], sm[a]);
                         atomicAdd(&gt.num[a][gi], nm[a]);
                     }
             }
         }
         gi = __shfl(gi, 0, 64);
-        for (int a = 0; a < P.nacc; a++) {
+#pragma unroll
+        for (int a = 0; a < MAX_ACC; a++) {
+            if (a >= P.nacc) break;
             if (P.acc[a].kind == ACC_SUM) continue;
             g_ext_update(gi >= 0 && my_pos[a] != NOPOS, gt, a, P.acc[a].kind, gi >= 0 ? (uint32_t)gi : 0u,
                          my_ext[a], my_pos[a], stats);
@@ -942,7 +1047,9 @@ __global__ __launch_bounds__(SCAN_T) void scan_kernel(const uint8_t* __restrict_
             if (gi >= 0) {
                 atomicAdd(&gt.cnt[gi], (unsigned long long)lt.cnt[i]);
                 atomicMin(&gt.first[gi], lt.first[i]);
-                for (int a = 0; a < P.nacc; a++) {
+#pragma unroll
+                for (int a = 0; a < MAX_ACC; a++) {
+                    if (a >= P.nacc) break;
                     if (la[a].sum && la[a].num[i]) {
                         atomicAdd(&gt.sum[a][gi], la[a].sum[i]);
                         atomicAdd(&gt.num[a][gi], (unsigned long long)la[a].num[i]);
@@ -950,7 +1057,9 @@ __global__ __launch_bounds__(SCAN_T) void scan_kernel(const uint8_t* __restrict_
                 }
             }
         }
-        for (int a = 0; a < P.nacc; a++) {
+#pragma unroll
+        for (int a = 0; a < MAX_ACC; a++) {
+            if (a >= P.nacc) break;
             if (!le[a].c) continue;                     // uniform
             const bool ok = act && gi >= 0;
             const Cell c = ok ? le[a].c[i] : cell_null();
@@ -994,9 +1103,7 @@ __global__ void gather_kernel(const uint8_t* __restrict__ g,
     const ScanPlan& P = c_plan;
     const uint32_t i = blockIdx.x * blockDim.x + threadIdx.x;
     if (i >= nrec) return;
-    Cell cells[MAX_NEED];
-    parse_record_global(g + recs[i], P, cells);
-    for (int k = 0; k < P.nneed; k++) out[(uint64_t)i * P.nneed + k] = cells[k];
+    parse_record_out(g + recs[i], P, out + (uint64_t)i * P.nneed);
 }
 
 // string bytes of cells -> packed host-visible buffer
@@ -1032,7 +1139,7 @@ static size_t lds_slot_bytes(const cq::ScanPlan* P) {
 }
 static size_t lds_fixed_bytes() {
     auto r16 = [](size_t x) { return (x + 15) & ~(size_t)15; };
-    return r16(cq::TILE) + 3 * r16(cq::NMW * 8) + r16(cq::RSMAX * 4) + r16(64);
+    return r16(cq::TILE) + 2 * r16(cq::NMW * 8) + r16(cq::NMW) + r16(cq::RSMAX * 2) + r16(64);
 }
 
 // group-table capacity: the largest power of two <= 2048 that fits the budget
