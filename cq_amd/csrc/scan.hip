@@ -111,10 +111,13 @@ __device__ __forceinline__ Cell sel_cell(bool t, const Cell& x, const Cell& y) {
     r.bits = t ? x.bits : y.bits;
     return r;
 }
-__device__ __forceinline__ Cell get_cell(const Cells& cs, int a) {
+__device__ __forceinline__ Cell get_cell(const Cells& cs, int a, int n = MAX_NEED) {
     Cell r = cs.c[0];
 #pragma unroll
-    for (int k = 1; k < MAX_NEED; k++) r = sel_cell(k == a, cs.c[k], r);
+    for (int k = 1; k < MAX_NEED; k++) {
+        if (k >= n) break;                        // n is uniform: a scalar branch
+        r = sel_cell(k == a, cs.c[k], r);
+    }
     return r;
 }
 
@@ -483,8 +486,10 @@ __device__ __forceinline__ uint32_t first128(const View& v) {
     return v.lo ? (uint32_t)__builtin_ctzll(v.lo) : (v.hi ? 64u + (uint32_t)__builtin_ctzll(v.hi) : NONE);
 }
 __device__ __forceinline__ void pop128(View& v) {
-    if (v.lo) v.lo &= v.lo - 1;
-    else v.hi &= v.hi - 1;
+    const bool l = v.lo != 0;
+    const uint64_t hi2 = v.hi & (v.hi - 1);
+    v.lo = v.lo & (v.lo - 1);
+    v.hi = l ? v.hi : hi2;
 }
 
 // 16 bytes of the tile at byte offset `o` (any alignment), as four dwords
@@ -505,74 +510,104 @@ __device__ __forceinline__ uint32_t len_mask(uint32_t len, uint32_t j) {
     return n >= 4 ? 0xFFFFFFFFu : ((1u << (8 * n)) - 1);
 }
 
-__device__ __forceinline__ double pow10_exact(uint32_t e) {   // 10^e, e <= 22, exact in double
+// 10^e for e <= 15, exact in double (every partial product is exact), branch-free
+__device__ __forceinline__ double pow10_exact(uint32_t e) {
     double r = 1.0, b = 10.0;
-    while (e) { if (e & 1) r *= b; b *= b; e >>= 1; }   // every partial product is exact
+#pragma unroll
+    for (int i = 0; i < 4; i++) {
+        r = ((e >> i) & 1) ? r * b : r;
+        b = b * b;
+    }
     return r;
 }
 
-enum : int { FF_OK = 0, FF_CELL = 1, FF_REC = 2 };
+// four decimal digit values in bytes 0..3 (byte 0 most significant) -> 0..9999
+__device__ __forceinline__ uint32_t dig4(uint32_t h) {
+    const uint32_t t = (h << 3) + (h << 1) + (h >> 8);   // bytes 0, 2: 10*b0+b1, 10*b2+b3
+    return (t & 0xffu) * 100u + ((t >> 16) & 0xffu);
+}
+__device__ __forceinline__ uint32_t dig8(uint64_t v) {
+    return dig4((uint32_t)v) * 10000u + dig4((uint32_t)(v >> 32));
+}
+
+// 0x80 in every byte that is a decimal digit
+__device__ __forceinline__ uint32_t digit_bytes(uint32_t x) { return lt_bytes(x ^ 0x30303030u, 0x0A0A0A0Au); }
+// 0x80 flags -> 0xFF bytes
+__device__ __forceinline__ uint32_t spread(uint32_t f) { return f | (f - (f >> 7)); }
+
+enum : int { FF_OK = 0, FF_SLOW = 1 };
 
 // Type a field of `len` bytes at tile offset `to` whose bytes hold no record
-// terminator, delimiter or quote.  FF_OK: `out` (and `key` when want_key) are
-// final.  FF_CELL: the field is clean but needs the general cell parser (date
-// shaped, long numerals, long fields, a delimiter strtod could read across).
-// FF_REC: a byte <= ' ' (blank, control, NUL) -- leading blanks move the field
-// start and blank-only last fields are dropped, so the record path decides.
+// terminator, delimiter or quote (infer_type + parse_value, csv_reader.c:
+// 136-240).  FF_OK: `out` (and `key` when want_key) are final; FF_SLOW: the
+// general record path decides -- a byte <= ' ' (blank, control, NUL: leading
+// blanks move the field start and a blank-only last field is dropped), a date
+// shaped field, a leading '+', a numeral past the exact fast cases, a field over
+// 16 bytes, or a delimiter strtod/strtoll could read across (num_ok false).
+// Control flow depends only on the field's shape, which is normally the same
+// for every record of a column, so the wave rarely diverges here.
 __device__ __forceinline__ int fast_field(const uint8_t* tile, uint32_t to, uint32_t len, bool num_ok,
                                           bool want_key, Cell& out, GKey& key) {
+    out = cell_null();
     if (len == 0) {
-        out = cell_null();
         if (want_key) key = group_key(out);
         return FF_OK;
     }
-    if (len > 16) {
-        for (uint32_t i = 0; i < len; i++)
-            if (tile[to + i] <= 0x20) return FF_REC;
-        return FF_CELL;
-    }
+    if (len > 16) return FF_SLOW;
     uint32_t d0, d1, d2, d3;
     load16(tile, to, d0, d1, d2, d3);
     const uint32_t m0 = len_mask(len, 0), m1 = len_mask(len, 1), m2 = len_mask(len, 2), m3 = len_mask(len, 3);
     const uint32_t low = lt_bytes(d0 | ~m0, 0x21212121u) | lt_bytes(d1 | ~m1, 0x21212121u) |
                          lt_bytes(d2 | ~m2, 0x21212121u) | lt_bytes(d3 | ~m3, 0x21212121u);
-    if (low) return FF_REC;
-    const uint64_t w0 = (uint64_t)(d0 & m0) | ((uint64_t)(d1 & m1) << 32);
-    const uint64_t w1 = (uint64_t)(d2 & m2) | ((uint64_t)(d3 & m3) << 32);
-    const uint32_t c0 = d0 & 0xff;
-    if (c0 == '+') return FF_CELL;
-    const bool lead_num = is_digit(c0) || c0 == '-' || c0 == '.';
-    if (len >= 8 && len <= 10 && c0 != '.' && lead_num) return FF_CELL;   // parse_date may accept it
+    const uint32_t c0 = d0 & 0xffu;
+    if (low || c0 == '+') return FF_SLOW;
+    d0 &= m0; d1 &= m1; d2 &= m2; d3 &= m3;
+    const bool neg = c0 == '-';
     // infer_type's numeric shape: [-] digits with at most one '.', at least one digit
-    bool numeric = lead_num, dot = false, dig = false;
-    uint64_t w = 0;
-    uint32_t nsig = 0, frac = 0;
-    if (numeric) {
-        for (uint32_t i = (c0 == '-') ? 1u : 0u; i < len; i++) {
-            const uint32_t b = (uint32_t)((i < 8 ? w0 >> (8 * i) : w1 >> (8 * (i - 8))) & 0xff);
-            if (is_digit(b)) {
-                dig = true;
-                if (nsig || b != '0') { w = w * 10 + (b - '0'); nsig++; }
-                if (dot) frac++;
-            } else if (b == '.' && !dot) {
-                dot = true;
-            } else {
-                numeric = false;
-                break;
-            }
+    const uint32_t f0 = m0 & 0x80808080u, f1 = m1 & 0x80808080u, f2 = m2 & 0x80808080u, f3 = m3 & 0x80808080u;
+    const uint32_t g0 = digit_bytes(d0) & f0, g1 = digit_bytes(d1) & f1, g2 = digit_bytes(d2) & f2,
+                   g3 = digit_bytes(d3) & f3;
+    const uint32_t p0 = ~nonzero_bytes(d0 ^ 0x2E2E2E2Eu) & f0, p1 = ~nonzero_bytes(d1 ^ 0x2E2E2E2Eu) & f1,
+                   p2 = ~nonzero_bytes(d2 ^ 0x2E2E2E2Eu) & f2, p3 = ~nonzero_bytes(d3 ^ 0x2E2E2E2Eu) & f3;
+    const uint32_t other = ((f0 & ~g0 & ~p0) & ~(neg ? 0x80u : 0u)) | (f1 & ~g1 & ~p1) | (f2 & ~g2 & ~p2) |
+                           (f3 & ~g3 & ~p3);
+    const uint32_t ndig = __popc(g0) + __popc(g1) + __popc(g2) + __popc(g3);
+    const uint32_t ndot = __popc(p0) + __popc(p1) + __popc(p2) + __popc(p3);
+    const uint64_t w0 = (uint64_t)d0 | ((uint64_t)d1 << 32), w1 = (uint64_t)d2 | ((uint64_t)d3 << 32);
+    if (len >= 8 && len <= 10 && (is_digit(c0) || c0 == '-')) return FF_SLOW;   // parse_date may accept it
+    if (other == 0 && ndig != 0 && ndot <= 1) {
+        if (!num_ok) return FF_SLOW;
+        // digit values (sign and dot bytes -> 0), dot removed, right-aligned in 16 bytes
+        uint64_t v0 = (w0 ^ 0x3030303030303030ULL) &
+                      ((uint64_t)spread(g0) | ((uint64_t)spread(g1) << 32));
+        uint64_t v1 = (w1 ^ 0x3030303030303030ULL) &
+                      ((uint64_t)spread(g2) | ((uint64_t)spread(g3) << 32));
+        const uint64_t dotm0 = (uint64_t)p0 | ((uint64_t)p1 << 32), dotm1 = (uint64_t)p2 | ((uint64_t)p3 << 32);
+        const uint32_t pb = dotm0 ? (uint32_t)__builtin_ctzll(dotm0) : (dotm1 ? 64u + (uint32_t)__builtin_ctzll(dotm1) : 128u);
+        const uint32_t p = pb >> 3;                                // dot byte index (16: none)
+        if (ndot) {
+            const uint64_t k0 = p >= 8 ? ~0ULL : ((1ULL << (8 * p)) - 1);
+            const uint64_t k1 = p >= 8 ? ((1ULL << (8 * (p - 8))) - 1) : 0ULL;
+            const uint64_t s0 = (v0 >> 8) | (v1 << 56), s1 = v1 >> 8;
+            v0 = (v0 & k0) | (s0 & ~k0);
+            v1 = (v1 & k1) | (s1 & ~k1);
         }
-        numeric = numeric && dig;
-    }
-    if (numeric) {
-        if (!num_ok) return FF_CELL;
-        const bool neg = c0 == '-';
-        if (!dot) {
-            if (nsig > 18) return FF_CELL;                     // strtoll range: general path
-            out = cell_int(neg ? -(int64_t)w : (int64_t)w);
+        const uint32_t lc = len - ndot;                            // digit positions (sign counted as 0)
+        const uint32_t sh = 8 * (16 - lc);                         // 0..120
+        uint64_t a0, a1;
+        if (sh >= 64) {
+            a1 = v0 << (sh - 64);
+            a0 = 0;
         } else {
-            if (nsig > 15 || frac > 22) return FF_CELL;        // Clinger's exact case only
-            double v = (double)w;                              // exact: w < 10^15
-            if (frac) v = v / pow10_exact(frac);               // one correctly rounded division
+            a1 = sh ? (v1 << sh) | (v0 >> (64 - sh)) : v1;
+            a0 = v0 << sh;
+        }
+        const uint64_t W = (uint64_t)dig8(a0) * 100000000ULL + dig8(a1);
+        if (!ndot) {
+            out = cell_int(neg ? -(int64_t)W : (int64_t)W);
+        } else {
+            if (W > (1ULL << 53)) return FF_SLOW;                  // Clinger's exact case only
+            const double v = (double)W / pow10_exact(len - 1 - p);   // one correctly rounded division
             out = cell_dbl(neg ? -v : v);
         }
         if (want_key) key = group_key(out);
@@ -821,29 +856,19 @@ __global__ __launch_bounds__(SCAN_T) void scan_kernel(const uint8_t* __restrict_
                     for (int k = 0; k < MAX_NEED; k++) {
                         if (k >= nneed) break;
                         const int want = P.need_col[k];
-                        for (; col < want; col++) {            // uniform trip count
+                        for (; col < want; col++) {            // uniform trip count, no branches
                             const uint32_t e = first128(S);
-                            if (e == NONE) fail = true;
-                            else if (e == rend) ended = true;
+                            fail = fail || (e == NONE && !ended);
+                            ended = ended || e == rend;
                             fs = e + 1;
                             pop128(S);
                         }
+                        const uint32_t e = first128(S);
+                        fail = fail || (e == NONE && !ended);
                         Cell c = cell_null();
-                        if (!ended && !fail) {
-                            const uint32_t e = first128(S);
-                            if (e == NONE) {
-                                fail = true;
-                            } else {
-                                const uint32_t len = e - fs;
-                                const int st = fast_field(tile, PRE + r + fs, len, num_ok, k == gslot, c, key);
-                                if (st == FF_CELL) {
-                                    c = parse_cell_slow(g + rec + fs, len);
-                                    if (k == gslot) key = group_key_slow(c);
-                                } else if (st == FF_REC) {
-                                    fail = true;
-                                }
-                                if (c.kind == K_STR && st == FF_OK) c.bits = (uint64_t)(uintptr_t)(g + rec + fs);
-                            }
+                        if (!ended && !fail) {                 // uniform unless the record is short
+                            fail = fast_field(tile, PRE + r + fs, e - fs, num_ok, k == gslot, c, key) != FF_OK;
+                            if (c.kind == K_STR) c.bits = (uint64_t)(uintptr_t)(g + rec + fs);
                         }
                         cs.c[k] = c;
                     }
@@ -852,12 +877,12 @@ __global__ __launch_bounds__(SCAN_T) void scan_kernel(const uint8_t* __restrict_
                         // -- the general parse_line cursor over global memory
                         my_slow++;
                         short_row = parse_record_regs(g + rec, P, cs);
-                        if (GROUPED) key = group_key_slow(get_cell(cs, gslot));
+                        if (GROUPED) key = group_key_slow(get_cell(cs, gslot, nneed));
                     }
                     my_records++;
                     if (short_row) my_short++;
                     if (P.nprog == 0) pass = true;
-                    else if (simple) pass = cmp_result(wop, compare(get_cell(cs, wslot), wconst));
+                    else if (simple) pass = cmp_result(wop, compare(get_cell(cs, wslot, nneed), wconst));
                     else pass = eval_where_vm(P, cs);
                     if (pass) my_pass++;
                 }
@@ -875,7 +900,8 @@ __global__ __launch_bounds__(SCAN_T) void scan_kernel(const uint8_t* __restrict_
                 if (pass) {
 #pragma unroll
                     for (int a = 0; a < MAX_ACC; a++)
-                        if (a < P.nacc) my_cls[a] |= class_bit(get_cell(cs, P.acc[a].slot));
+                        if (a < P.nacc && P.acc[a].kind != ACC_SUM)
+                            my_cls[a] |= class_bit(get_cell(cs, P.acc[a].slot, nneed));
                 }
                 if (!GROUPED) {
                     if (pass) {
@@ -884,7 +910,7 @@ __global__ __launch_bounds__(SCAN_T) void scan_kernel(const uint8_t* __restrict_
 #pragma unroll
                         for (int a = 0; a < MAX_ACC; a++) {
                             if (a >= P.nacc) break;
-                            const Cell c = get_cell(cs, P.acc[a].slot);
+                            const Cell c = get_cell(cs, P.acc[a].slot, nneed);
                             if (P.acc[a].kind == ACC_SUM) {
                                 if (is_num(c)) { my_sum[a] += num_of(c); my_num[a]++; }
                             } else if (c.kind != K_NULL && ext_better(P.acc[a].kind, c, rec, my_ext[a], my_pos[a])) {
@@ -909,7 +935,7 @@ __global__ __launch_bounds__(SCAN_T) void scan_kernel(const uint8_t* __restrict_
                         for (int a = 0; a < MAX_ACC; a++) {
                             if (a >= P.nacc) break;
                             if (!la[a].sum) continue;
-                            const Cell c = get_cell(cs, P.acc[a].slot);
+                            const Cell c = get_cell(cs, P.acc[a].slot, nneed);
                             if (is_num(c)) {
                                 atomicAdd(&la[a].sum[s], num_of(c));
                                 atomicAdd(&la[a].num[s], 1u);
@@ -920,7 +946,7 @@ __global__ __launch_bounds__(SCAN_T) void scan_kernel(const uint8_t* __restrict_
                     for (int a = 0; a < MAX_ACC; a++) {
                         if (a >= P.nacc) break;
                         if (!le[a].c) continue;                  // uniform
-                        const Cell c = get_cell(cs, P.acc[a].slot);
+                        const Cell c = get_cell(cs, P.acc[a].slot, nneed);
                         lds_ext_update(in_lds && c.kind != K_NULL, le[a], in_lds ? (uint32_t)s : 0u,
                                        P.acc[a].kind, c, rec);
                     }
@@ -936,7 +962,7 @@ __global__ __launch_bounds__(SCAN_T) void scan_kernel(const uint8_t* __restrict_
 #pragma unroll
                                 for (int a = 0; a < MAX_ACC; a++) {
                                     if (a >= P.nacc) break;
-                                    const Cell c = get_cell(cs, P.acc[a].slot);
+                                    const Cell c = get_cell(cs, P.acc[a].slot, nneed);
                                     if (P.acc[a].kind == ACC_SUM && is_num(c)) {
                                         atomicAdd(&gt.sum[a][gi], num_of(c));
                                         atomicAdd(&gt.num[a][gi], 1ULL);
@@ -948,7 +974,7 @@ __global__ __launch_bounds__(SCAN_T) void scan_kernel(const uint8_t* __restrict_
                         for (int a = 0; a < MAX_ACC; a++) {
                             if (a >= P.nacc) break;
                             if (P.acc[a].kind == ACC_SUM) continue;   // uniform
-                            const Cell c = get_cell(cs, P.acc[a].slot);
+                            const Cell c = get_cell(cs, P.acc[a].slot, nneed);
                             g_ext_update(spill && gi >= 0 && c.kind != K_NULL, gt, a, P.acc[a].kind,
                                          gi >= 0 ? (uint32_t)gi : 0u, c, rec, stats);
                         }

@@ -176,3 +176,64 @@ def test_empty_and_header_only(tmp_path):
         with cqtest.Parsed(sql) as ast:
             got = cq_amd.evaluate(ast)
         compare(got, want, set(), sql)
+
+
+# ---------------------------------------------------------------- field-shape fuzz
+def _fuzz_field(rng):
+    """one CSV field drawn from the shapes the fast and general parsers split on"""
+    k = rng.integers(0, 16)
+    digits = lambda n: "".join(str(d) for d in rng.integers(0, 10, n))
+    if k == 0:
+        return digits(rng.integers(1, 19))                       # ints up to 18 digits
+    if k == 1:
+        return "-" + digits(rng.integers(1, 17))
+    if k == 2:
+        return digits(rng.integers(0, 9)) + "." + digits(rng.integers(0, 9))
+    if k == 3:
+        return "-" + digits(rng.integers(0, 7)) + "." + digits(rng.integers(1, 10))
+    if k == 4:
+        return "%04d-%02d-%02d" % (rng.integers(900, 3000), rng.integers(0, 14), rng.integers(0, 33))
+    if k == 5:
+        return "%02d/%02d/%04d" % (rng.integers(0, 14), rng.integers(0, 33), rng.integers(900, 3000))
+    if k == 6:
+        return digits(8)                                         # compact-date shaped
+    if k == 7:
+        return " " + digits(rng.integers(1, 5)) + " "
+    if k == 8:
+        return '"' + digits(rng.integers(1, 4)) + ',' + digits(2) + '"'
+    if k == 9:
+        return ""
+    if k == 10:
+        return "+" + digits(rng.integers(1, 5))
+    if k == 11:
+        return "".join(rng.choice(list("abcXYZ_.-0123456789"), rng.integers(1, 24)))
+    if k == 12:
+        return "1e5" if rng.integers(0, 2) else "0x1F"
+    if k == 13:
+        return digits(rng.integers(1, 4)) + "." + digits(rng.integers(10, 20))    # long fractions
+    if k == 14:
+        return "00" + digits(rng.integers(1, 6))
+    return "-"
+
+
+def test_field_shape_fuzz(tmp_path):
+    import numpy as np
+    rng = np.random.default_rng(7)
+    lines = ["a,b,c"]
+    for _ in range(20000):
+        lines.append(",".join(_fuzz_field(rng) for _ in range(3)))
+    p = tmp_path / "fuzz.csv"
+    p.write_text("\n".join(lines) + "\n")
+    for sql in (f"SELECT a, COUNT(*) FROM '{p}' GROUP BY a",
+                f"SELECT b, COUNT(*), SUM(c), MIN(a), MAX(a) FROM '{p}' GROUP BY b",
+                f"SELECT c, COUNT(*), SUM(a) FROM '{p}' WHERE b > 0 GROUP BY c"):
+        want, unsup = cqtest.oracle_query(sql)
+        assert not unsup
+        with cqtest.Parsed(sql) as ast:
+            got = cq_amd.evaluate(ast)
+            tol = tolerant_columns(ast)
+        inel = cq_amd.last_ineligible()
+        if inel:
+            assert "MIN/MAX" in inel, inel
+            continue
+        compare(got, want, tol, sql)
