@@ -139,7 +139,10 @@ def main():
                 raise RuntimeError(cq_amd.last_error())
             ng = tp.contents.nrows
             cq_amd.result_free(tp)
-            return ng, cq_amd.stats()["scan_ms"]
+            st = cq_amd.stats()
+        if os.environ.get("CQ_BENCH_DEBUG"):
+            print("stats", st, file=sys.stderr)
+        return ng, st["scan_ms"]
         blob = C.c_void_p()
         n = L.cqgpu_query_partial(ast, (C.c_void_p * 1)(table.handle.value), 1, C.byref(blob))
         if n == 0:
@@ -167,9 +170,10 @@ def main():
             cq_amd.result_free(tp)
         return ng, scan_ms
 
+    ng = None
     for _ in range(args.warmup):
         ng, _ = step()
-    if rank == 0 and ng != 1000:
+    if rank == 0 and ng is not None and ng != 1000:
         print(f"warning: {ng} groups (expected 1000)", file=sys.stderr)
 
     def barrier():

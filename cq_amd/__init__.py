@@ -13,7 +13,8 @@ import os
 from . import abi
 
 HERE = os.path.dirname(os.path.abspath(__file__))
-LIB_PATH = os.path.join(HERE, "lib", "libcqgpu.so")
+# CQ_AMD_LIB: profiling builds of the same library (scripts/prof_stages.sh)
+LIB_PATH = os.environ.get("CQ_AMD_LIB") or os.path.join(HERE, "lib", "libcqgpu.so")
 
 _lib = None
 
@@ -21,7 +22,8 @@ _lib = None
 class Stats(C.Structure):
     _fields_ = [("scan_ms", C.c_double), ("total_ms", C.c_double), ("scan_bytes", C.c_uint64),
                 ("records", C.c_uint64), ("groups", C.c_uint64), ("lds_spills", C.c_uint64),
-                ("grid", C.c_int), ("path", C.c_int), ("retries", C.c_int)]
+                ("grid", C.c_int), ("path", C.c_int), ("retries", C.c_int),
+                ("slow_records", C.c_uint64), ("passed", C.c_uint64)]
 
 
 def lib():

@@ -31,12 +31,14 @@
 using namespace cq;
 
 extern "C" {
+uint32_t cq_scan_cand_stride(const ScanPlan* P, int grouped);
 size_t cq_scan_lds_bytes(const ScanPlan* P, int grouped);
 int cq_scan_occupancy(const ScanPlan* P, int grouped);
 hipError_t cq_launch_scan(const uint8_t* g, const ScanPlan* P, const GroupTable* gt, ScanStats* stats,
                           unsigned long long* row_out, unsigned long long row_cap, int grouped, int grid,
-                          hipStream_t s, Cell* cells_out = nullptr);
-hipError_t cq_launch_compact(const GroupTable* gt, int nacc, GroupOut* out, unsigned int* count,
+                          hipStream_t s, Cell* cells_out, unsigned long long* slow_list,
+                          unsigned long long slow_cap);
+hipError_t cq_launch_compact(const GroupTable* gt, const ScanPlan* P, GroupOut* out, unsigned int* count,
                              unsigned int cap_out, hipStream_t s);
 hipError_t cq_launch_gather(const uint8_t* g, const ScanPlan* P, const unsigned long long* recs,
                             uint32_t nrec, Cell* out, hipStream_t s);
@@ -759,14 +761,19 @@ struct TableArena {
     ScanStats* stats;
     GroupOut* out;
     unsigned int* out_count;
+    unsigned long long* slow_list;     // records the fast scan declines (scan.hip slow_kernel)
+    unsigned long long slow_cap;
 };
 
 size_t align256(size_t x) { return (x + 255) & ~(size_t)255; }
 
-TableArena make_arena(DevCtx& c, const ScanPlan& P, uint32_t cap, size_t out_cap) {
+TableArena make_arena(DevCtx& c, const ScanPlan& P, uint32_t cap, size_t out_cap, size_t cand_blocks = 0,
+                      uint32_t cand_stride = 16, unsigned long long slow_cap = 1ull << 20) {
     TableArena A;
     memset(&A.gt, 0, sizeof A.gt);
+    A.slow_cap = slow_cap;
     A.gt.cap = cap;
+    A.gt.cand_stride = cand_stride;
     struct Part { void** p; size_t bytes; int fill; };
     std::vector<Part> parts;
     parts.push_back({(void**)&A.gt.tag, cap * 4ull, 0});
@@ -783,12 +790,15 @@ TableArena make_arena(DevCtx& c, const ScanPlan& P, uint32_t cap, size_t out_cap
             parts.push_back({(void**)&A.gt.ext[a], cap * (size_t)sizeof(Cell), 0});
             parts.push_back({(void**)&A.gt.extpos[a], cap * 8ull, 0xff});
             parts.push_back({(void**)&A.gt.lock[a], cap * 4ull, 0});
+            parts.push_back({(void**)&A.gt.extref[a], cap * 8ull, 0xff});
+            parts.push_back({(void**)&A.gt.cand[a], std::max<size_t>(cand_blocks, 1) * cand_stride * sizeof(ExtCand), 0});
         }
     }
     parts.push_back({(void**)&A.gt.used, 256, 0});
     parts.push_back({(void**)&A.stats, 256, 0});
     parts.push_back({(void**)&A.out_count, 256, 0});
     parts.push_back({(void**)&A.out, out_cap * sizeof(GroupOut), 0});
+    parts.push_back({(void**)&A.slow_list, slow_cap * 8ull, 0});
     size_t total = 0;
     for (auto& p : parts) total += align256(p.bytes);
     uint8_t* base = (uint8_t*)workspace(c, total);
@@ -817,29 +827,61 @@ std::vector<HGroup> run_aggregate(DevCtx& c, const cqgpu_table* t, Compiled& C, 
     const int grouped = C.grouped ? 1 : 0;
     uint32_t cap = grouped ? 8192 : 64;
     int retries = 0;
-    const uint64_t windows = (t->n + 32767) / 32768;
+    const uint64_t windows = (t->n + 31679) / 31680;   // scan.hip WSTRIDE
     int per_cu = cq_scan_occupancy(&C.P, grouped);
     int grid = (int)std::min<uint64_t>(std::max<uint64_t>(windows, 1), (uint64_t)c.ncu * per_cu);
     ScanStats st;
     std::vector<GroupOut> outs;
+    uint64_t chunk = 0;          // 0: the whole table in one launch
     while (true) {
-        TableArena A = make_arena(c, C.P, cap, cap / 2 + 1);
-        HIPCHECK(hipEventRecord(c.ev0, c.stream));
-        HIPCHECK(cq_launch_scan(t->g, &C.P, &A.gt, A.stats, nullptr, 0, grouped, grid, c.stream));
-        HIPCHECK(hipEventRecord(c.ev1, c.stream));
-        HIPCHECK(hipMemcpyAsync(&st, A.stats, sizeof st, hipMemcpyDeviceToHost, c.stream));
-        HIPCHECK(hipStreamSynchronize(c.stream));
-        float ms = 0;
-        HIPCHECK(hipEventElapsedTime(&ms, c.ev0, c.ev1));
-        g_stats.scan_ms = ms;
+        TableArena A = make_arena(c, C.P, cap, cap / 2 + 1, (size_t)grid, cq_scan_cand_stride(&C.P, grouped));
+        memset(&st, 0, sizeof st);
+        float ms_total = 0;
+        bool slow_over = false;
+        const uint64_t step = chunk ? chunk : std::max<uint64_t>(t->n, 1);
+        for (uint64_t b = 0; b < std::max<uint64_t>(t->n, 1); b += step) {
+            ScanPlan P = C.P;
+            P.range_begin = b;
+            P.range_end = std::min<uint64_t>(b + step, t->n);
+            const uint64_t wins = (P.range_end - P.range_begin + 31679) / 31680 + 1;
+            const int g2 = chunk ? (int)std::min<uint64_t>(grid, wins) : grid;
+            HIPCHECK(hipEventRecord(c.ev0, c.stream));
+            HIPCHECK(cq_launch_scan(t->g, &P, &A.gt, A.stats, nullptr, 0, grouped, g2, c.stream, nullptr,
+                                    A.slow_list, A.slow_cap));
+            HIPCHECK(hipEventRecord(c.ev1, c.stream));
+            ScanStats s1;
+            HIPCHECK(hipMemcpyAsync(&s1, A.stats, sizeof s1, hipMemcpyDeviceToHost, c.stream));
+            HIPCHECK(hipStreamSynchronize(c.stream));
+            float ms = 0;
+            HIPCHECK(hipEventElapsedTime(&ms, c.ev0, c.ev1));
+            ms_total += ms;
+            st.records += s1.records;
+            st.passed += s1.passed;
+            st.short_rows += s1.short_rows;
+            st.lds_spills += s1.lds_spills;
+            st.rows_emitted += s1.rows_emitted;
+            st.slow_records += s1.slow_records;
+            st.overflow = std::max(st.overflow, s1.overflow);
+            for (int a = 0; a < MAX_ACC; a++) st.acc_classes[a] |= s1.acc_classes[a];
+            if (s1.slow_records > A.slow_cap) { slow_over = true; break; }
+            if (chunk) HIPCHECK(hipMemsetAsync(A.stats, 0, sizeof(ScanStats), c.stream));
+        }
+        g_stats.scan_ms = ms_total;
         g_stats.grid = grid;
+        if (st.overflow >= 2)   // a bounded spin gave up: a kernel bug, never a data property
+            throw HipError{st.overflow == 2 ? "scan kernel: MIN/MAX lock timeout" : "scan kernel: group insert timeout"};
+        if (slow_over) {        // too many records for the general kernel's list: rescan in chunks
+            if (chunk) throw HipError{"scan: slow-record list overflow"};
+            chunk = A.slow_cap;
+            continue;
+        }
         if (st.overflow) {
             if (cap >= (1u << 30)) throw HipError{"group table overflow"};
             cap *= 8;
             retries++;
             continue;
         }
-        HIPCHECK(cq_launch_compact(&A.gt, C.P.nacc, A.out, A.out_count, cap / 2 + 1, c.stream));
+        HIPCHECK(cq_launch_compact(&A.gt, &C.P, A.out, A.out_count, cap / 2 + 1, c.stream));
         unsigned int ng = 0;
         HIPCHECK(hipMemcpyAsync(&ng, A.out_count, 4, hipMemcpyDeviceToHost, c.stream));
         HIPCHECK(hipStreamSynchronize(c.stream));
@@ -851,6 +893,8 @@ std::vector<HGroup> run_aggregate(DevCtx& c, const cqgpu_table* t, Compiled& C, 
     g_stats.retries = retries;
     g_stats.records = st.records;
     g_stats.lds_spills = st.lds_spills;
+    g_stats.slow_records = st.slow_records;
+    g_stats.passed = st.passed;
     g_stats.scan_bytes = t->n;
     if (stats_out) *stats_out = st;
     // MIN/MAX over a column mixing value classes depends on row order in the
@@ -868,6 +912,9 @@ std::vector<HGroup> run_aggregate(DevCtx& c, const cqgpu_table* t, Compiled& C, 
         for (int a = 0; a < MAX_ACC; a++) z.extpos[a] = NOPOS;
         outs.push_back(z);
     }
+    // never let a kernel bug turn into an out-of-bounds gather below
+    for (auto& o : outs)
+        if (o.first != NOPOS && o.first >= t->n) throw HipError{"scan kernel: group first-row offset out of range"};
     // first-appearance order (create_groups appends groups in row order)
     std::sort(outs.begin(), outs.end(), [](const GroupOut& a, const GroupOut& b) { return a.first < b.first; });
     // representative cells of each group's first row, and string extremes
@@ -1434,12 +1481,13 @@ size_t cqgpu_debug_records(cqgpu_table* t, unsigned long long* out, size_t cap) 
         P.data_begin = t->data_begin;
         P.range_end = t->n;
         P.group_slot = -1;
-        TableArena A = make_arena(c, P, 64, 2);
+        TableArena A = make_arena(c, P, 64, 2, 0, 16, t->n + 1);
         unsigned long long* d;
         HIPCHECK(hipMalloc(&d, std::max<size_t>(cap, 1) * 8));
-        uint64_t windows = (t->n + 32767) / 32768;
+        uint64_t windows = (t->n + 31679) / 31680;
         int grid = (int)std::min<uint64_t>(std::max<uint64_t>(windows, 1), (uint64_t)c.ncu * cq_scan_occupancy(&P, 0));
-        HIPCHECK(cq_launch_scan(t->g, &P, &A.gt, A.stats, d, cap, 0, grid, c.stream));
+        HIPCHECK(cq_launch_scan(t->g, &P, &A.gt, A.stats, d, cap, 0, grid, c.stream, nullptr, A.slow_list,
+                                A.slow_cap));
         ScanStats st;
         HIPCHECK(hipMemcpyAsync(&st, A.stats, sizeof st, hipMemcpyDeviceToHost, c.stream));
         HIPCHECK(hipStreamSynchronize(c.stream));
@@ -1471,14 +1519,15 @@ cq_table* cqgpu_debug_scan_cells(cqgpu_table* t, const int* cols, int ncols, uns
         if (ncols > MAX_NEED || ncols < 1) throw HipError{"bad column count"};
         P.nneed = ncols;
         for (int i = 0; i < ncols; i++) P.need_col[i] = (int16_t)cols[i];   // ascending expected
-        TableArena A = make_arena(c, P, 64, 2);
+        TableArena A = make_arena(c, P, 64, 2, 0, 16, t->n + 1);
         unsigned long long* d;
         Cell* dc;
         HIPCHECK(hipMalloc(&d, std::max<size_t>(cap, 1) * 8));
         HIPCHECK(hipMalloc(&dc, std::max<size_t>(cap, 1) * ncols * sizeof(Cell)));
-        uint64_t windows = (t->n + 32767) / 32768;
+        uint64_t windows = (t->n + 31679) / 31680;
         int grid = (int)std::min<uint64_t>(std::max<uint64_t>(windows, 1), (uint64_t)c.ncu * cq_scan_occupancy(&P, 0));
-        HIPCHECK(cq_launch_scan(t->g, &P, &A.gt, A.stats, d, cap, 0, grid, c.stream, dc));
+        HIPCHECK(cq_launch_scan(t->g, &P, &A.gt, A.stats, d, cap, 0, grid, c.stream, dc, A.slow_list,
+                                A.slow_cap));
         ScanStats st;
         HIPCHECK(hipMemcpyAsync(&st, A.stats, sizeof st, hipMemcpyDeviceToHost, c.stream));
         HIPCHECK(hipStreamSynchronize(c.stream));

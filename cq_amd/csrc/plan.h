@@ -76,6 +76,13 @@ struct ScanStats {
     unsigned long long slow_records;    // records the fast field walk handed to the general parser
 };
 
+// a MIN/MAX candidate published by one block (or wave) for one group
+struct ExtCand {
+    Cell c;
+    unsigned long long pos;
+    unsigned long long pad;
+};
+
 // global (HBM) group table, structure of arrays, capacity `cap` (power of two)
 struct GroupTable {
     uint32_t cap;
@@ -90,6 +97,11 @@ struct GroupTable {
     Cell* ext[MAX_ACC];            // ACC_MIN/MAX: extreme cell
     unsigned long long* extpos[MAX_ACC];
     uint32_t* lock[MAX_ACC];
+    // lock-free MIN/MAX merge across blocks: extref holds the index of the best
+    // published candidate (~0: none); candidate slot = block * cand_stride + LDS slot
+    unsigned long long* extref[MAX_ACC];
+    ExtCand* cand[MAX_ACC];
+    uint32_t cand_stride;
     uint32_t* used;                // number of occupied slots
 };
 

@@ -3,27 +3,30 @@
 // One pass over the CSV bytes resident in HBM does what the reference spreads
 // over csv_load (csv_reader.c:375-465), filter_rows (evaluator_utils.c:986),
 // create_groups (evaluator_aggregates.c:108) and evaluate_aggregate (:263).
-// Per 32 KiB window, one 512-thread block:
+// One 512-thread block per window; consecutive windows start WSTRIDE bytes apart
+// and each stages 32 KiB -- 64 bytes before its start and 1 KiB of overlap with
+// the next window after its end -- so every lane owns one 64-byte mask word:
 //
-//   stage     the window (+16 B before, +2 KiB after) is copied from registers
-//             into LDS; the next window's 16 B/lane loads are already in flight
-//   classify  each lane turns 64 window bytes into two 64-bit masks in LDS --
-//             record terminators ('\n' '\r') and separators (terminators and
-//             the delimiter) -- plus a "has a quote byte" flag, branch-free SWAR
-//   split     record starts come from the terminator mask; a block-wide scan
-//             gives every record an LDS slot
-//   parse     one lane per record takes a 128-bit view of both masks at its
-//             start and pops separators up to the last needed column (the
-//             column walk is uniform across the wave); needed fields are typed
-//             by specialised int / decimal / string parsers reading LDS.  A
-//             field the fast parsers cannot prove identical to infer_type /
-//             parse_value (date-shaped, long numerals) goes through the general
-//             cell parser; a record with quotes, control or blank bytes in a
-//             needed field, or longer than the view, goes through the general
-//             parse_line cursor (csv_reader.c:278-338) -- same semantics, slower
+//   stage     the tile is copied from registers into LDS; the next window's
+//             16 B/lane loads are already in flight
+//   classify  each lane turns its 64 bytes into two 64-bit masks -- record
+//             terminators ('\n' '\r') and separators (terminators and the
+//             delimiter) -- and a quote-presence flag, branch-free SWAR
+//   index     one block-wide scan numbers the separators, terminators and record
+//             starts; every lane writes the tile positions of its separators
+//             (the separator list), the separator index of its terminators, and
+//             one slot per record start: so field c of a record is simply the
+//             bytes between separators j0+c-1 and j0+c
+//   parse     one lane per record types its needed fields with specialised int /
+//             decimal / string parsers reading LDS.  A record with a quote in
+//             front of its last needed field, a blank or control byte or a date
+//             or long numeral in a needed field, or running past the tile, goes
+//             through the general parse_line cursor (csv_reader.c:278-338) and
+//             cell parser -- same semantics, slower; both read the LDS copy
 //   filter    WHERE bytecode (plan.h OP_*), or a direct compare for col-op-const
-//   group     LDS open-addressing table, 16-byte inline keys, COUNT / SUM / AVG /
-//             MIN / MAX accumulators; flushed once per block into the HBM table
+//   group     LDS open-addressing table with 16-byte inline keys and fire-and-
+//             forget LDS atomics for COUNT / SUM / AVG / first-row order, lock-
+//             protected MIN / MAX; flushed once per block into the HBM table
 //             (per-thread registers when the query has no GROUP BY)
 //
 // Every per-record array (cells, accumulator pointers) is indexed with
@@ -38,19 +41,31 @@
 
 namespace cq {
 
-constexpr int SCAN_T = 512;                  // threads per block (8 waves)
-constexpr int WIN = 32768;                   // window bytes (64 per lane)
-constexpr int PRE = 16;                      // bytes staged before the window
-constexpr int MARGIN = 2048;                 // bytes staged after the window
-constexpr int TILE = PRE + WIN + MARGIN;     // 34832
-constexpr int TILE16 = TILE / 16;            // 2177 16-byte loads per tile
-constexpr int NMW = (WIN + MARGIN) / 64;     // mask words covering [ws, ws + WIN + MARGIN)
+constexpr int SCAN_T = 1024;                 // threads per block (16 waves, 4 per SIMD)
+constexpr int TILE = 32768;                  // bytes staged per window (64 per lane)
+constexpr int PREB = 64;                     // staged bytes before the window start
+constexpr int WSTRIDE = 31680;               // window stride: 1 KiB of the tile overlaps the next window
+constexpr int TILE_PAD = 32;                 // LDS slack after the tile for 16-byte field loads
+constexpr int LB = TILE / SCAN_T;            // bytes classified per lane (32)
+constexpr int NW = TILE / LB;                // mask words per tile (one per lane)
+constexpr int TILE16 = TILE / 16;            // 16-byte loads per tile
+constexpr int PF = TILE16 / SCAN_T;          // prefetch registers per lane (2)
+constexpr int ECAP = 8192;                   // separator positions kept per tile
+constexpr int NLCAP = 4096;                  // terminator indices kept per tile
 constexpr int RSMAX = 2048;                  // record slots per pass
+constexpr int KSTR = 1024;                   // LDS bytes for string literals
 constexpr int LDS_BUDGET = 160 * 1024;       // LDS bytes per CU
-constexpr int PF = (TILE16 + SCAN_T - 1) / SCAN_T;   // prefetch registers per lane (5)
 constexpr uint64_t NOPOS = ~0ULL;
-constexpr uint32_t NONE = 255;               // "no separator in the 128-bit view"
 typedef uint32_t v4u __attribute__((ext_vector_type(4)));   // one 16-byte load
+static_assert(TILE16 % SCAN_T == 0, "tile loads split evenly over the block");
+static_assert(NW == SCAN_T, "one mask word per lane");
+
+// The plan and the table descriptor live in constant memory (written on the
+// launch stream before each launch): passed by value they would be copied to
+// per-lane scratch, because the kernel indexes their arrays at run time.
+__constant__ ScanPlan c_plan;
+__constant__ GroupTable c_gt;
+__device__ __forceinline__ const ScanPlan& c_plan_ref() { return c_plan; }
 
 // ------------------------------------------------------------------ helpers
 __device__ __forceinline__ bool is_nl(uint32_t c) { return c == '\n' || c == '\r'; }
@@ -72,33 +87,37 @@ __device__ __forceinline__ uint32_t lt_bytes(uint32_t x, uint32_t rep_n) {
     return ~((x | 0x80808080u) - rep_n) & ~x & 0x80808080u;
 }
 
-// block-wide exclusive scan of one value per thread (SCAN_T threads)
-__device__ uint32_t block_excl_scan(uint32_t v, uint32_t* wsum, uint32_t* total) {
+// block-wide exclusive scan of two values per thread (SCAN_T threads)
+__device__ __forceinline__ void block_excl_scan2(uint32_t a, uint32_t b, uint32_t* wsum, uint32_t& ea,
+                                                 uint32_t& eb, uint32_t& ta, uint32_t& tb) {
     const int lane = threadIdx.x & 63, wid = threadIdx.x >> 6;
-    uint32_t x = v;
+    uint32_t x = a, y = b;
 #pragma unroll
     for (int o = 1; o < 64; o <<= 1) {
-        uint32_t y = __shfl_up(x, o, 64);
-        if (lane >= o) x += y;
+        const uint32_t u = __shfl_up(x, o, 64), v = __shfl_up(y, o, 64);
+        if (lane >= o) { x += u; y += v; }
     }
-    if (lane == 63) wsum[wid] = x;
+    if (lane == 63) { wsum[wid] = x; wsum[16 + wid] = y; }
     lds_barrier();
-    uint32_t base = 0, tot = 0;
+    uint32_t ba = 0, bb = 0, sa = 0, sb = 0;
 #pragma unroll
     for (int w = 0; w < SCAN_T / 64; w++) {
-        uint32_t s = wsum[w];
-        if (w < wid) base += s;
-        tot += s;
+        const uint32_t p = wsum[w], q = wsum[16 + w];
+        if (w < wid) { ba += p; bb += q; }
+        sa += p;
+        sb += q;
     }
-    *total = tot;
-    lds_barrier();
-    return base + x - v;
+    ea = ba + x - a;
+    eb = bb + y - b;
+    ta = sa;
+    tb = sb;
 }
 
 // ------------------------------------------------------------------ per-record cells
 // cells of one record in registers: callers index them with unrolled loops only
-struct Cells {
-    Cell c[MAX_NEED];
+template <int N>
+struct CellsT {
+    Cell c[N];
 };
 
 // cells.c[a] for a uniform run-time slot `a`, without a run-time index
@@ -111,10 +130,11 @@ __device__ __forceinline__ Cell sel_cell(bool t, const Cell& x, const Cell& y) {
     r.bits = t ? x.bits : y.bits;
     return r;
 }
-__device__ __forceinline__ Cell get_cell(const Cells& cs, int a, int n = MAX_NEED) {
+template <int N>
+__device__ __forceinline__ Cell get_cell(const CellsT<N>& cs, int a, int n = N) {
     Cell r = cs.c[0];
 #pragma unroll
-    for (int k = 1; k < MAX_NEED; k++) {
+    for (int k = 1; k < N; k++) {
         if (k >= n) break;                        // n is uniform: a scalar branch
         r = sel_cell(k == a, cs.c[k], r);
     }
@@ -127,15 +147,29 @@ __device__ __noinline__ Cell parse_cell_slow(const uint8_t* f, uint32_t len) { r
 __device__ __noinline__ GKey group_key_slow(const Cell c) { return group_key(c); }
 
 // ------------------------------------------------------------------ general record parse
-// One field of parse_line (csv_reader.c:278-338) at rec[i]: leading blanks are
+// Byte source of the general parser: the staged tile while the record lasts in
+// it, HBM after.  Cells point at the tile copy when the field (plus the bytes
+// strtod/strtoll may read past it) is staged, at HBM otherwise.
+struct Src {
+    const uint8_t* t;   // record start in the tile (LDS); unused when lim == 0
+    const uint8_t* g;   // record start in HBM
+    uint32_t lim;       // bytes of the record inside the tile
+    bool lds_cells;     // cells may point into the tile (false: the delimiter could extend a numeral)
+    __device__ __forceinline__ uint32_t at(uint32_t i) const { return i < lim ? (uint32_t)t[i] : (uint32_t)g[i]; }
+    __device__ __forceinline__ const uint8_t* ptr(uint32_t i, uint32_t n) const {
+        return (lds_cells && i + n + 48 <= lim) ? t + i : g + i;
+    }
+};
+
+// One field of parse_line (csv_reader.c:278-338) at byte i: leading blanks are
 // skipped; returns false if the record ends there (a trailing field of blanks
 // is dropped).  On return [fs, fs + flen) is the field's value (a quoted field
 // without its quotes, `""` kept as two bytes; an unclosed quoted field has the
 // length of its `""` pairs) and i is at the terminator (delimiter or newline).
-__device__ __forceinline__ bool g_field(const uint8_t* rec, uint32_t& i, uint32_t delim, uint32_t quote,
+__device__ __forceinline__ bool g_field(const Src& S, uint32_t& i, uint32_t delim, uint32_t quote,
                                         uint32_t& fs, uint32_t& flen) {
-    uint32_t c = rec[i];
-    while (is_blank(c)) { i = i + 1; c = rec[i]; }
+    uint32_t c = S.at(i);
+    while (is_blank(c)) { i = i + 1; c = S.at(i); }
     if (is_nl(c)) return false;
     if (c == quote) {                          // quoted field (:294-317)
         i = i + 1;
@@ -144,21 +178,21 @@ __device__ __forceinline__ bool g_field(const uint8_t* rec, uint32_t& i, uint32_
         bool closed = false;
         flen = 0;
         while (true) {
-            c = rec[i];
+            c = S.at(i);
             if (is_nl(c)) break;
             if (c == quote) {
-                if (rec[i + 1] == quote) { i = i + 2; acc += 2; }
+                if (S.at(i + 1) == quote) { i = i + 2; acc += 2; }
                 else { flen = i - fs; i = i + 1; closed = true; break; }
             } else {
                 i = i + 1;
             }
         }
         if (!closed) flen = acc;
-        c = rec[i];
-        while (c != delim && !is_nl(c)) { i = i + 1; c = rec[i]; }
+        c = S.at(i);
+        while (c != delim && !is_nl(c)) { i = i + 1; c = S.at(i); }
     } else {                                   // unquoted field (:318-324)
         fs = i;
-        while (c != delim && !is_nl(c)) { i = i + 1; c = rec[i]; }
+        while (c != delim && !is_nl(c)) { i = i + 1; c = S.at(i); }
         flen = i - fs;
     }
     return true;
@@ -166,26 +200,27 @@ __device__ __forceinline__ bool g_field(const uint8_t* rec, uint32_t& i, uint32_
 
 // parse_line restricted to the needed columns, into registers (unrolled over
 // the need slots).  Returns true when the record is too short for a needed column.
-__device__ __forceinline__ bool parse_record_regs(const uint8_t* rec, const ScanPlan& P, Cells& cs) {
+template <int N>
+__device__ __forceinline__ bool parse_record_regs(const Src& S, const ScanPlan& P, CellsT<N>& cs) {
     const uint32_t delim = P.delim, quote = P.quote;
     uint32_t i = 0, fs = 0, flen = 0;
     int col = 0;
     bool ended = false;
 #pragma unroll
-    for (int k = 0; k < MAX_NEED; k++) {
+    for (int k = 0; k < N; k++) {
         if (k >= P.nneed) break;
         const int want = P.need_col[k];
         Cell c = cell_null();
         while (!ended && col < want) {
-            if (!g_field(rec, i, delim, quote, fs, flen) || rec[i] != delim) ended = true;
+            if (!g_field(S, i, delim, quote, fs, flen) || S.at(i) != delim) ended = true;
             else { i = i + 1; col++; }
         }
         if (!ended) {
-            if (!g_field(rec, i, delim, quote, fs, flen)) {
+            if (!g_field(S, i, delim, quote, fs, flen)) {
                 ended = true;
             } else {
-                c = parse_cell_slow(rec + fs, flen);
-                if (rec[i] == delim) { i = i + 1; col++; }
+                c = parse_cell_slow(S.ptr(fs, flen), flen);
+                if (S.at(i) == delim) { i = i + 1; col++; }
                 else ended = true;                  // later columns do not exist
             }
         }
@@ -194,8 +229,9 @@ __device__ __forceinline__ bool parse_record_regs(const uint8_t* rec, const Scan
     return ended;
 }
 
-// the same into a global array (representative-row gather)
+// the same from HBM into a global array (representative-row gather)
 __device__ void parse_record_out(const uint8_t* rec, const ScanPlan& P, Cell* out) {
+    const Src S{rec, rec, 0, false};
     const uint32_t delim = P.delim, quote = P.quote;
     uint32_t i = 0, fs = 0, flen = 0;
     int col = 0;
@@ -204,15 +240,15 @@ __device__ void parse_record_out(const uint8_t* rec, const ScanPlan& P, Cell* ou
         const int want = P.need_col[k];
         Cell c = cell_null();
         while (!ended && col < want) {
-            if (!g_field(rec, i, delim, quote, fs, flen) || rec[i] != delim) ended = true;
+            if (!g_field(S, i, delim, quote, fs, flen) || S.at(i) != delim) ended = true;
             else { i = i + 1; col++; }
         }
         if (!ended) {
-            if (!g_field(rec, i, delim, quote, fs, flen)) {
+            if (!g_field(S, i, delim, quote, fs, flen)) {
                 ended = true;
             } else {
                 c = parse_cell(rec + fs, flen);
-                if (rec[i] == delim) { i = i + 1; col++; }
+                if (S.at(i) == delim) { i = i + 1; col++; }
                 else ended = true;
             }
         }
@@ -247,8 +283,10 @@ __device__ __forceinline__ bool cmp_result(uint32_t op, int c) {
     }
 }
 
-// evaluate_condition (evaluator_conditions.c:62-164) over the flattened WHERE tree
-__device__ __forceinline__ bool eval_where_vm(const ScanPlan& P, const Cells& cs) {
+// evaluate_condition (evaluator_conditions.c:62-164) over the flattened WHERE tree;
+// kc: the literal cells (LDS copy, string bytes staged in LDS)
+template <int N>
+__device__ __forceinline__ bool eval_where_vm(const ScanPlan& P, const Cell* kc, const CellsT<N>& cs) {
     Stack st;
 #pragma unroll
     for (int j = 0; j < 8; j++) st.s[j] = cell_null();
@@ -258,7 +296,7 @@ __device__ __forceinline__ bool eval_where_vm(const ScanPlan& P, const Cells& cs
         const Insn in = P.prog[pc];
         switch (in.op) {
             case OP_COL: st.set(sp++, get_cell(cs, in.a)); break;
-            case OP_CONST: st.set(sp++, P.consts[in.b]); break;
+            case OP_CONST: st.set(sp++, kc[in.b]); break;
             case OP_NULLV: st.set(sp++, cell_null()); break;
             case OP_ARITH: {
                 Cell r = st.get(--sp), l = st.get(--sp);
@@ -299,6 +337,9 @@ __device__ __forceinline__ bool eval_where_vm(const ScanPlan& P, const Cells& cs
     return (bs & 1u) != 0;
 }
 
+// Out-of-line entry points for the rare paths, so the hot loop stays small in
+// the instruction cache.  Cells travel by value (a by-reference argument would
+// force the caller's register-resident cells into scratch memory).
 // ------------------------------------------------------------------ MIN/MAX order
 // reference keeps the first cell that compares strictly better (evaluator_aggregates.c:311-326);
 // within one value class that is the lexicographic (value, position) extreme
@@ -340,7 +381,7 @@ __device__ int g_insert(const GroupTable& gt, const GKey k, uint64_t h, ScanStat
             t = old;
         }
         for (uint32_t spin = 0; t == 1; spin++) {
-            if (spin > (1u << 24)) { atomicExch(&st->overflow, 2ULL); return -1; }   // never hang
+            if (spin > (1u << 20)) { atomicExch(&st->overflow, 3ULL); return -1; }   // never hang
             t = __hip_atomic_load(&gt.tag[i], __ATOMIC_ACQUIRE, __HIP_MEMORY_SCOPE_AGENT);
         }
         if (t == tg) {
@@ -389,64 +430,94 @@ __device__ void g_ext_update(bool need, const GroupTable& gt, int a, uint8_t kin
                 need = false;
             }
         }
-        if (++trips > (1u << 24)) {                    // never hang: report and give up
+        if (++trips > (1u << 20)) {                    // never hang: report and give up
             if (need) atomicExch(&st->overflow, 2ULL);
             break;
         }
     }
 }
 
+// Publish candidate `idx` (already written to gt.cand[a][idx]) as the group's
+// extreme if it is better than the current one: a lock-free pointer swing.  Most
+// candidates lose the first comparison and never write, so even a group every
+// block touches sees few atomics; no lane ever waits on another.
+__device__ void g_ext_swing(const GroupTable& gt, int a, uint8_t kind, uint32_t gi, uint64_t idx) {
+    unsigned long long* slot = &gt.extref[a][gi];
+    const ExtCand mine = gt.cand[a][idx];
+    unsigned long long cur = __hip_atomic_load(slot, __ATOMIC_ACQUIRE, __HIP_MEMORY_SCOPE_AGENT);
+    while (true) {
+        if (cur != NOPOS) {
+            const ExtCand o = gt.cand[a][cur];
+            if (!ext_better(kind, mine.c, mine.pos, o.c, o.pos)) return;
+        }
+        const unsigned long long prev = atomicCAS(slot, cur, (unsigned long long)idx);
+        if (prev == cur) return;
+        cur = prev;
+        __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");
+    }
+}
+
 // ------------------------------------------------------------------ LDS table
-// structure of arrays carved from dynamic LDS; capacity H (power of two) is
-// chosen by the host so that the window tile and every accumulator fit
+// Structure of arrays carved from dynamic LDS; capacity H (power of two) is
+// chosen by the host so that the tile, the indexes and every accumulator fit.
 struct LdsTable {
     uint32_t H;
-    uint32_t* tag;
-    uint32_t* clslen;
-    uint64_t* w0;
-    uint64_t* w1;
-    uint32_t* cnt;
-    unsigned long long* first;
+    uint32_t* hdr;      // 0 empty, 1 being written, else 0x80000000 | hash tag << 19 | key class/length
+    v4u* key;           // key words w0, w1
+    uint32_t* cnt;      // COUNT(*) of the block's records in the group
+    uint32_t* first;    // min over them of (window iteration << 15 | tile position)
 };
-struct LdsAcc {            // ACC_SUM
-    double* sum;
-    uint32_t* num;
+struct LdsAcc {         // ACC_SUM
+    double* sum;        // sum of numeric cells
+    uint32_t* miss;     // cells that were not numeric (numeric count = cnt - miss)
 };
-struct ExtLds {            // ACC_MIN / ACC_MAX
+struct ExtLds {         // ACC_MIN / ACC_MAX
     Cell* c;
     unsigned long long* pos;
     uint32_t* lock;
 };
 
-__device__ __forceinline__ int l_insert(const LdsTable& t, const GKey k, uint64_t h) {
-    const uint32_t tg = tag_of(h);
-    const uint32_t cl = gk_clslen(k);
-    for (uint32_t probe = 0; probe < 64; probe++) {
-        uint32_t i = (uint32_t)(h + probe) & (t.H - 1);
-        uint32_t cur = __hip_atomic_load(&t.tag[i], __ATOMIC_ACQUIRE, __HIP_MEMORY_SCOPE_WORKGROUP);
+__device__ __forceinline__ uint32_t lds_hdr(const GKey& k, uint64_t h) {
+    return 0x80000000u | (((uint32_t)(h >> 40) & 0xFFFu) << 19) | gk_clslen(k);
+}
+__device__ __forceinline__ v4u key_words(const GKey& k) {
+    v4u r;
+    r.x = (uint32_t)k.w0; r.y = (uint32_t)(k.w0 >> 32); r.z = (uint32_t)k.w1; r.w = (uint32_t)(k.w1 >> 32);
+    return r;
+}
+__device__ __forceinline__ bool key_match(const GKey& k, const v4u& mine, const v4u& slot) {
+    if (mine.z != slot.z || mine.w != slot.w) return false;
+    if (mine.x == slot.x && mine.y == slot.y) return true;
+    if (k.cls != GK_LONG) return false;
+    GKey o = k;                                     // long keys: same hash and length, compare bytes
+    o.w0 = (uint64_t)slot.x | ((uint64_t)slot.y << 32);
+    return gk_equal(o, k);
+}
+
+// find or insert the slot of key k (hash h); -1 if the probe window is full
+__device__ __forceinline__ int l_insert(const LdsTable& t, const GKey& k, uint64_t h) {
+    const uint32_t hd = lds_hdr(k, h);
+    const v4u kk = key_words(k);
+    for (uint32_t probe = 0; probe < 32; probe++) {
+        const uint32_t i = (uint32_t)(h + probe) & (t.H - 1);
+        uint32_t cur = __hip_atomic_load(&t.hdr[i], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
+        if (cur == hd && key_match(k, kk, t.key[i])) return (int)i;   // the common case: one round trip
         if (cur == 0) {
-            uint32_t old = atomicCAS(&t.tag[i], 0u, 1u);
+            const uint32_t old = atomicCAS(&t.hdr[i], 0u, 1u);
             if (old == 0) {
-                t.clslen[i] = cl;
-                t.w0[i] = k.w0;
-                t.w1[i] = k.w1;
-                __hip_atomic_store(&t.tag[i], tg, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_WORKGROUP);
+                t.key[i] = kk;
+                __hip_atomic_store(&t.hdr[i], hd, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_WORKGROUP);
                 return (int)i;
             }
             cur = old;
         }
         for (uint32_t spin = 0; cur == 1; spin++) {
-            if (spin > (1u << 24)) return -1;          // the HBM table takes the record
-            cur = __hip_atomic_load(&t.tag[i], __ATOMIC_ACQUIRE, __HIP_MEMORY_SCOPE_WORKGROUP);
+            if (spin > (1u << 20)) return -1;           // the HBM table takes the record
+            cur = __hip_atomic_load(&t.hdr[i], __ATOMIC_ACQUIRE, __HIP_MEMORY_SCOPE_WORKGROUP);
         }
-        if (cur == tg && t.clslen[i] == cl && t.w1[i] == k.w1) {
-            const uint64_t ow0 = t.w0[i];
-            if (ow0 == k.w0) return (int)i;
-            if (k.cls == GK_LONG) {
-                GKey o;
-                o.cls = GK_LONG; o.len = k.len; o.w0 = ow0; o.w1 = k.w1;
-                if (gk_equal(o, k)) return (int)i;
-            }
+        if (cur == hd) {                                // published meanwhile: re-read the key
+            __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "workgroup");
+            if (key_match(k, kk, t.key[i])) return (int)i;
         }
     }
     return -1;
@@ -471,27 +542,6 @@ __device__ __forceinline__ void lds_ext_update(bool need, const ExtLds& e, uint3
 }
 
 // ------------------------------------------------------------------ fast field path
-// 128-bit view of a per-64-byte mask starting at window offset 64*wi + o
-struct View {
-    uint64_t lo, hi;
-};
-__device__ __forceinline__ View view128(const uint64_t* m, uint32_t wi, uint32_t o) {
-    const uint64_t a0 = m[wi], a1 = m[wi + 1];
-    View v;
-    v.lo = o ? (a0 >> o) | (a1 << (64 - o)) : a0;
-    v.hi = a1 >> o;
-    return v;
-}
-__device__ __forceinline__ uint32_t first128(const View& v) {
-    return v.lo ? (uint32_t)__builtin_ctzll(v.lo) : (v.hi ? 64u + (uint32_t)__builtin_ctzll(v.hi) : NONE);
-}
-__device__ __forceinline__ void pop128(View& v) {
-    const bool l = v.lo != 0;
-    const uint64_t hi2 = v.hi & (v.hi - 1);
-    v.lo = v.lo & (v.lo - 1);
-    v.hi = l ? v.hi : hi2;
-}
-
 // 16 bytes of the tile at byte offset `o` (any alignment), as four dwords
 __device__ __forceinline__ void load16(const uint8_t* tile, uint32_t o, uint32_t& e0, uint32_t& e1,
                                        uint32_t& e2, uint32_t& e3) {
@@ -537,15 +587,37 @@ __device__ __forceinline__ uint32_t spread(uint32_t f) { return f | (f - (f >> 7
 
 enum : int { FF_OK = 0, FF_SLOW = 1 };
 
+// 8 bytes of the tile at byte offset `o` (any alignment), as two dwords
+__device__ __forceinline__ void load8(const uint8_t* tile, uint32_t o, uint32_t& e0, uint32_t& e1) {
+    const uint32_t* t32 = (const uint32_t*)tile;
+    const uint32_t a = o >> 2, sh = o & 3;
+    const uint32_t d0 = t32[a], d1 = t32[a + 1], d2 = t32[a + 2];
+    e0 = __builtin_amdgcn_alignbyte(d1, d0, sh);
+    e1 = __builtin_amdgcn_alignbyte(d2, d1, sh);
+}
+
+// Shape flags of a numeral candidate over one dword of field bytes (f: 0x80 in
+// the bytes inside the field): digits, dots, and bytes that are neither.
+struct NumFlags {
+    uint32_t dig, dot, other;
+};
+__device__ __forceinline__ NumFlags num_flags(uint32_t d, uint32_t f) {
+    NumFlags r;
+    r.dig = digit_bytes(d) & f;
+    r.dot = ~nonzero_bytes(d ^ 0x2E2E2E2Eu) & f;
+    r.other = f & ~r.dig & ~r.dot;
+    return r;
+}
+
 // Type a field of `len` bytes at tile offset `to` whose bytes hold no record
-// terminator, delimiter or quote (infer_type + parse_value, csv_reader.c:
-// 136-240).  FF_OK: `out` (and `key` when want_key) are final; FF_SLOW: the
-// general record path decides -- a byte <= ' ' (blank, control, NUL: leading
-// blanks move the field start and a blank-only last field is dropped), a date
-// shaped field, a leading '+', a numeral past the exact fast cases, a field over
-// 16 bytes, or a delimiter strtod/strtoll could read across (num_ok false).
-// Control flow depends only on the field's shape, which is normally the same
-// for every record of a column, so the wave rarely diverges here.
+// terminator or delimiter (infer_type + parse_value, csv_reader.c:136-240).
+// FF_OK: `out` (and `key` when want_key) are final; FF_SLOW: the general record
+// path decides -- a byte <= ' ' (blank, control, NUL: leading blanks move the
+// field start and a blank-only last field is dropped), a date-shaped field, a
+// leading '+', a numeral past the exact fast cases, a field over 16 bytes, or a
+// delimiter strtod/strtoll could read across (num_ok false).  Branches follow
+// the field's shape, which is normally the same for every record of a column,
+// so the wave rarely diverges here; fields of <= 8 bytes take the 64-bit path.
 __device__ __forceinline__ int fast_field(const uint8_t* tile, uint32_t to, uint32_t len, bool num_ok,
                                           bool want_key, Cell& out, GKey& key) {
     out = cell_null();
@@ -554,64 +626,79 @@ __device__ __forceinline__ int fast_field(const uint8_t* tile, uint32_t to, uint
         return FF_OK;
     }
     if (len > 16) return FF_SLOW;
-    uint32_t d0, d1, d2, d3;
-    load16(tile, to, d0, d1, d2, d3);
-    const uint32_t m0 = len_mask(len, 0), m1 = len_mask(len, 1), m2 = len_mask(len, 2), m3 = len_mask(len, 3);
-    const uint32_t low = lt_bytes(d0 | ~m0, 0x21212121u) | lt_bytes(d1 | ~m1, 0x21212121u) |
-                         lt_bytes(d2 | ~m2, 0x21212121u) | lt_bytes(d3 | ~m3, 0x21212121u);
+    const bool wide = len > 8;
+    uint32_t d0, d1, d2 = 0, d3 = 0;
+    if (!wide) load8(tile, to, d0, d1);
+    else load16(tile, to, d0, d1, d2, d3);
+    const uint32_t m0 = len_mask(len, 0), m1 = len_mask(len, 1);
+    const uint32_t m2 = wide ? len_mask(len, 2) : 0u, m3 = wide ? len_mask(len, 3) : 0u;
+    uint32_t low = lt_bytes(d0 | ~m0, 0x21212121u) | lt_bytes(d1 | ~m1, 0x21212121u);
+    if (wide) low |= lt_bytes(d2 | ~m2, 0x21212121u) | lt_bytes(d3 | ~m3, 0x21212121u);
+    d0 &= m0; d1 &= m1; d2 &= m2; d3 &= m3;
     const uint32_t c0 = d0 & 0xffu;
     if (low || c0 == '+') return FF_SLOW;
-    d0 &= m0; d1 &= m1; d2 &= m2; d3 &= m3;
-    const bool neg = c0 == '-';
-    // infer_type's numeric shape: [-] digits with at most one '.', at least one digit
-    const uint32_t f0 = m0 & 0x80808080u, f1 = m1 & 0x80808080u, f2 = m2 & 0x80808080u, f3 = m3 & 0x80808080u;
-    const uint32_t g0 = digit_bytes(d0) & f0, g1 = digit_bytes(d1) & f1, g2 = digit_bytes(d2) & f2,
-                   g3 = digit_bytes(d3) & f3;
-    const uint32_t p0 = ~nonzero_bytes(d0 ^ 0x2E2E2E2Eu) & f0, p1 = ~nonzero_bytes(d1 ^ 0x2E2E2E2Eu) & f1,
-                   p2 = ~nonzero_bytes(d2 ^ 0x2E2E2E2Eu) & f2, p3 = ~nonzero_bytes(d3 ^ 0x2E2E2E2Eu) & f3;
-    const uint32_t other = ((f0 & ~g0 & ~p0) & ~(neg ? 0x80u : 0u)) | (f1 & ~g1 & ~p1) | (f2 & ~g2 & ~p2) |
-                           (f3 & ~g3 & ~p3);
-    const uint32_t ndig = __popc(g0) + __popc(g1) + __popc(g2) + __popc(g3);
-    const uint32_t ndot = __popc(p0) + __popc(p1) + __popc(p2) + __popc(p3);
     const uint64_t w0 = (uint64_t)d0 | ((uint64_t)d1 << 32), w1 = (uint64_t)d2 | ((uint64_t)d3 << 32);
-    if (len >= 8 && len <= 10 && (is_digit(c0) || c0 == '-')) return FF_SLOW;   // parse_date may accept it
-    if (other == 0 && ndig != 0 && ndot <= 1) {
-        if (!num_ok) return FF_SLOW;
-        // digit values (sign and dot bytes -> 0), dot removed, right-aligned in 16 bytes
-        uint64_t v0 = (w0 ^ 0x3030303030303030ULL) &
-                      ((uint64_t)spread(g0) | ((uint64_t)spread(g1) << 32));
-        uint64_t v1 = (w1 ^ 0x3030303030303030ULL) &
-                      ((uint64_t)spread(g2) | ((uint64_t)spread(g3) << 32));
-        const uint64_t dotm0 = (uint64_t)p0 | ((uint64_t)p1 << 32), dotm1 = (uint64_t)p2 | ((uint64_t)p3 << 32);
-        const uint32_t pb = dotm0 ? (uint32_t)__builtin_ctzll(dotm0) : (dotm1 ? 64u + (uint32_t)__builtin_ctzll(dotm1) : 128u);
-        const uint32_t p = pb >> 3;                                // dot byte index (16: none)
-        if (ndot) {
-            const uint64_t k0 = p >= 8 ? ~0ULL : ((1ULL << (8 * p)) - 1);
-            const uint64_t k1 = p >= 8 ? ((1ULL << (8 * (p - 8))) - 1) : 0ULL;
-            const uint64_t s0 = (v0 >> 8) | (v1 << 56), s1 = v1 >> 8;
-            v0 = (v0 & k0) | (s0 & ~k0);
-            v1 = (v1 & k1) | (s1 & ~k1);
+    const bool lead = is_digit(c0) || c0 == '-' || c0 == '.';
+    if (lead) {
+        if (c0 != '.' && len >= 8 && len <= 10) return FF_SLOW;   // parse_date may accept it
+        const bool neg = c0 == '-';
+        // infer_type's numeric shape: [-] digits with at most one '.', at least one digit
+        const NumFlags n0 = num_flags(d0, m0 & 0x80808080u), n1 = num_flags(d1, m1 & 0x80808080u);
+        NumFlags n2 = {0, 0, 0}, n3 = {0, 0, 0};
+        if (wide) { n2 = num_flags(d2, m2 & 0x80808080u); n3 = num_flags(d3, m3 & 0x80808080u); }
+        const uint32_t other = (n0.other & ~(neg ? 0x80u : 0u)) | n1.other | n2.other | n3.other;
+        const uint32_t ndig = __popc(n0.dig) + __popc(n1.dig) + __popc(n2.dig) + __popc(n3.dig);
+        const uint32_t ndot = __popc(n0.dot) + __popc(n1.dot) + __popc(n2.dot) + __popc(n3.dot);
+        if (other == 0 && ndig != 0 && ndot <= 1) {
+            if (!num_ok) return FF_SLOW;
+            // digit values (sign and dot bytes -> 0), dot removed, right-aligned
+            const uint64_t dm0 = (uint64_t)n0.dot | ((uint64_t)n1.dot << 32);
+            const uint64_t dm1 = (uint64_t)n2.dot | ((uint64_t)n3.dot << 32);
+            const uint32_t pa = (uint32_t)__builtin_ctzg(dm0, 64), pz = (uint32_t)__builtin_ctzg(dm1, 64);
+            const uint32_t p = (pa < 64 ? pa : 64 + pz) >> 3;       // dot byte index (16: none)
+            const uint32_t lc = len - ndot;                         // digit positions (sign counted as 0)
+            uint64_t W;
+            if (!wide) {
+                uint64_t v = (w0 ^ 0x3030303030303030ULL) & ((uint64_t)spread(n0.dig) | ((uint64_t)spread(n1.dig) << 32));
+                if (ndot) {
+                    const uint64_t k = (1ULL << (8 * p)) - 1;       // p <= 7
+                    v = (v & k) | ((v >> 8) & ~k);
+                }
+                v <<= 8 * (8 - lc);
+                W = dig8(v);
+            } else {
+                uint64_t v0 = (w0 ^ 0x3030303030303030ULL) &
+                              ((uint64_t)spread(n0.dig) | ((uint64_t)spread(n1.dig) << 32));
+                uint64_t v1 = (w1 ^ 0x3030303030303030ULL) &
+                              ((uint64_t)spread(n2.dig) | ((uint64_t)spread(n3.dig) << 32));
+                if (ndot) {
+                    const uint64_t k0 = p >= 8 ? ~0ULL : ((1ULL << (8 * p)) - 1);
+                    const uint64_t k1 = p >= 8 ? ((1ULL << (8 * (p - 8))) - 1) : 0ULL;
+                    const uint64_t s0 = (v0 >> 8) | (v1 << 56), s1 = v1 >> 8;
+                    v0 = (v0 & k0) | (s0 & ~k0);
+                    v1 = (v1 & k1) | (s1 & ~k1);
+                }
+                const uint32_t sh = 8 * (16 - lc);                  // 0..120
+                uint64_t a0, a1;
+                if (sh >= 64) {
+                    a1 = v0 << (sh - 64);
+                    a0 = 0;
+                } else {
+                    a1 = sh ? (v1 << sh) | (v0 >> (64 - sh)) : v1;
+                    a0 = v0 << sh;
+                }
+                W = (uint64_t)dig8(a0) * 100000000ULL + dig8(a1);
+            }
+            if (!ndot) {
+                out = cell_int(neg ? -(int64_t)W : (int64_t)W);
+            } else {
+                if (W > (1ULL << 53)) return FF_SLOW;               // Clinger's exact case only
+                const double v = (double)W / pow10_exact(len - 1 - p);   // one correctly rounded division
+                out = cell_dbl(neg ? -v : v);
+            }
+            if (want_key) key = group_key(out);
+            return FF_OK;
         }
-        const uint32_t lc = len - ndot;                            // digit positions (sign counted as 0)
-        const uint32_t sh = 8 * (16 - lc);                         // 0..120
-        uint64_t a0, a1;
-        if (sh >= 64) {
-            a1 = v0 << (sh - 64);
-            a0 = 0;
-        } else {
-            a1 = sh ? (v1 << sh) | (v0 >> (64 - sh)) : v1;
-            a0 = v0 << sh;
-        }
-        const uint64_t W = (uint64_t)dig8(a0) * 100000000ULL + dig8(a1);
-        if (!ndot) {
-            out = cell_int(neg ? -(int64_t)W : (int64_t)W);
-        } else {
-            if (W > (1ULL << 53)) return FF_SLOW;                  // Clinger's exact case only
-            const double v = (double)W / pow10_exact(len - 1 - p);   // one correctly rounded division
-            out = cell_dbl(neg ? -v : v);
-        }
-        if (want_key) key = group_key(out);
-        return FF_OK;
     }
     // STRING with no blank or NUL: exactly what cq_strndup + trim_whitespace give
     out.kind = K_STR;
@@ -627,29 +714,32 @@ __device__ __forceinline__ int fast_field(const uint8_t* tile, uint32_t to, uint
 }
 
 // ------------------------------------------------------------------ the scan kernel
-// dynamic LDS: [tile][nl/sep masks][quote flags][rs][scan scratch][group table][accumulators]
 __device__ __forceinline__ uint8_t* carve(uint8_t*& q, size_t bytes) {
     uint8_t* r = q;
     q += (bytes + 15) & ~(size_t)15;
     return r;
 }
 
+// the tile of the window starting at ws: bytes [ws - PREB, ws - PREB + TILE)
 __device__ __forceinline__ void prefetch(const uint8_t* g, uint64_t ws, v4u* pf) {
-    const v4u* src = (const v4u*)(g + ws - PRE);
+    const v4u* src = (const v4u*)(g + ws - PREB);
 #pragma unroll
     for (int j = 0; j < PF; j++) {
-        const int i = threadIdx.x + j * SCAN_T;
-        if (i < TILE16) pf[j] = __builtin_nontemporal_load(src + i);
+#ifdef CQ_PLAIN_LOADS
+        pf[j] = src[threadIdx.x + j * SCAN_T];
+#else
+        pf[j] = __builtin_nontemporal_load(src + threadIdx.x + j * SCAN_T);
+#endif
     }
 }
 
-// classify 64 staged bytes: terminator and separator masks, quote presence
-__device__ __forceinline__ void classify64(const uint8_t* p, uint32_t rep_d, uint32_t rep_q, uint64_t& nlm,
-                                           uint64_t& sepm, bool& has_q) {
+// classify LB = 32 staged bytes: terminator and separator masks, quote presence
+__device__ __forceinline__ void classify32(const uint8_t* p, uint32_t rep_d, uint32_t rep_q, uint32_t& nlm,
+                                           uint32_t& sepm, bool& has_q) {
     const v4u* src = (const v4u*)p;
-    uint32_t nl_lo = 0, nl_hi = 0, sp_lo = 0, sp_hi = 0, qacc = 0x80808080u;
+    uint32_t nl = 0, sp = 0, qacc = 0x80808080u;
 #pragma unroll
-    for (int v = 0; v < 4; v++) {
+    for (int v = 0; v < 2; v++) {
         const v4u x4 = src[v];
 #pragma unroll
         for (int j = 0; j < 4; j++) {
@@ -661,65 +751,71 @@ __device__ __forceinline__ void classify64(const uint8_t* p, uint32_t rep_d, uin
             const uint32_t c = ((~sp_inv & 0x80808080u) >> 7) | ((~nl_inv & 0x80808080u) >> 3);
             uint32_t t = c | (c >> 7);
             t = t | (t >> 14);
-            const int d = v * 4 + j, sh = (d & 7) * 4;
-            if (d < 8) {
-                sp_lo |= (t & 0xFu) << sh;
-                nl_lo |= ((t >> 4) & 0xFu) << sh;
-            } else {
-                sp_hi |= (t & 0xFu) << sh;
-                nl_hi |= ((t >> 4) & 0xFu) << sh;
-            }
+            const int sh = (v * 4 + j) * 4;
+            sp |= (t & 0xFu) << sh;
+            nl |= ((t >> 4) & 0xFu) << sh;
         }
     }
-    nlm = (uint64_t)nl_lo | ((uint64_t)nl_hi << 32);
-    sepm = (uint64_t)sp_lo | ((uint64_t)sp_hi << 32);
+    nlm = nl;
+    sepm = sp;
     has_q = qacc != 0x80808080u;
 }
 
-// The plan and the table descriptor live in constant memory (written on the
-// launch stream before each launch): passed by value they would be copied to
-// per-lane scratch, because the kernel indexes their arrays at run time.
-__constant__ ScanPlan c_plan;
-__constant__ GroupTable c_gt;
+// bits of m below bit b
+__device__ __forceinline__ uint32_t popc_below(uint32_t m, uint32_t b) {
+    return (uint32_t)__popc(m & ((1u << b) - 1));
+}
 
-template <bool GROUPED>
+
+// WHERE shapes the fast kernel is specialised for
+enum : int { W_NONE = 0, W_SIMPLE = 1, W_VM = 2 };
+
+// Fast scan kernel, specialised on the plan's shape: GROUPED (GROUP BY key or
+// one group), KN need slots and KA accumulators at most, the WHERE shape WM and
+// whether any MIN/MAX accumulator exists (EXT).  It has no general-parser code:
+// a record the fast field path cannot type exactly is appended to `slow_list`
+// and handled completely (filter, rows, aggregation) by slow_kernel.
+template <bool GROUPED, int KN, int KA, int WM, bool EXT>
 __global__ __launch_bounds__(SCAN_T) void scan_kernel(const uint8_t* __restrict__ g,
                                                       ScanStats* __restrict__ stats,
                                                       unsigned long long* __restrict__ row_out,
                                                       unsigned long long row_cap, uint32_t lds_h,
-                                                      Cell* __restrict__ cells_out) {
+                                                      Cell* __restrict__ cells_out,
+                                                      unsigned long long* __restrict__ slow_list,
+                                                      unsigned long long slow_cap) {
     const ScanPlan& P = c_plan;
     const GroupTable& gt = c_gt;
     extern __shared__ __align__(16) uint8_t smem[];
     uint8_t* q = smem;
-    uint8_t* tile = carve(q, TILE);
-    uint64_t* nlw = (uint64_t*)carve(q, NMW * 8);
-    uint64_t* sepw = (uint64_t*)carve(q, NMW * 8);
-    uint8_t* qfl = carve(q, NMW);
-    uint16_t* rs = (uint16_t*)carve(q, RSMAX * 2);
-    uint32_t* wsum = (uint32_t*)carve(q, 64);
+    uint8_t* tile = carve(q, TILE + TILE_PAD);
+    uint16_t* E = (uint16_t*)carve(q, ECAP * 2);         // tile positions of separators
+    uint16_t* NLI = (uint16_t*)carve(q, NLCAP * 2);      // separator index of each terminator
+    uint16_t* QP = (uint16_t*)carve(q, (NW + 1) * 2);    // quote words before each mask word
+    uint32_t* rs = (uint32_t*)carve(q, RSMAX * 4);       // record: tile position | first separator << 16
+    uint16_t* rq = (uint16_t*)carve(q, RSMAX * 2);       // record: terminators before it
+    uint32_t* wsum = (uint32_t*)carve(q, 32 * 4);
+    Cell* kc = (Cell*)carve(q, MAX_CONST * sizeof(Cell)); // literal cells, strings staged in LDS
+    uint8_t* kstr = carve(q, KSTR);
     LdsTable lt;
-    LdsAcc la[MAX_ACC];
-    ExtLds le[MAX_ACC];
+    LdsAcc la[KA];
+    ExtLds le[KA];
     const uint32_t H = lds_h;
     lt.H = H;
-    lt.tag = nullptr; lt.clslen = nullptr; lt.w0 = nullptr; lt.w1 = nullptr; lt.cnt = nullptr; lt.first = nullptr;
+    lt.hdr = nullptr; lt.key = nullptr; lt.cnt = nullptr; lt.first = nullptr;
     if (GROUPED) {
-        lt.tag = (uint32_t*)carve(q, H * 4);
-        lt.clslen = (uint32_t*)carve(q, H * 4);
-        lt.w0 = (uint64_t*)carve(q, H * 8);
-        lt.w1 = (uint64_t*)carve(q, H * 8);
+        lt.key = (v4u*)carve(q, H * 16);
+        lt.hdr = (uint32_t*)carve(q, H * 4);
         lt.cnt = (uint32_t*)carve(q, H * 4);
-        lt.first = (unsigned long long*)carve(q, H * 8);
+        lt.first = (uint32_t*)carve(q, H * 4);
     }
 #pragma unroll
-    for (int a = 0; a < MAX_ACC; a++) {
-        la[a].sum = nullptr; la[a].num = nullptr;
+    for (int a = 0; a < KA; a++) {
+        la[a].sum = nullptr; la[a].miss = nullptr;
         le[a].c = nullptr; le[a].pos = nullptr; le[a].lock = nullptr;
         if (!GROUPED || a >= P.nacc) continue;
         if (P.acc[a].kind == ACC_SUM) {
             la[a].sum = (double*)carve(q, H * 8);
-            la[a].num = (uint32_t*)carve(q, H * 4);
+            la[a].miss = (uint32_t*)carve(q, H * 4);
         } else {
             le[a].c = (Cell*)carve(q, H * sizeof(Cell));
             le[a].pos = (unsigned long long*)carve(q, H * 8);
@@ -730,160 +826,207 @@ __global__ __launch_bounds__(SCAN_T) void scan_kernel(const uint8_t* __restrict_
 
     if (GROUPED) {
         for (uint32_t i = tid; i < H; i += SCAN_T) {
-            lt.tag[i] = 0; lt.cnt[i] = 0; lt.first[i] = NOPOS;
+            lt.hdr[i] = 0; lt.cnt[i] = 0; lt.first[i] = 0xFFFFFFFFu;
 #pragma unroll
-            for (int a = 0; a < MAX_ACC; a++) {
-                if (la[a].sum) { la[a].sum[i] = 0.0; la[a].num[i] = 0; }
-                if (le[a].c) { le[a].pos[i] = NOPOS; le[a].lock[i] = 0; le[a].c[i] = cell_null(); }
+            for (int a = 0; a < KA; a++) {
+                if (a >= P.nacc) break;
+                if (la[a].sum) { la[a].sum[i] = 0.0; la[a].miss[i] = 0; }
+                if (EXT && le[a].c) { le[a].pos[i] = NOPOS; le[a].lock[i] = 0; le[a].c[i] = cell_null(); }
             }
         }
     }
+    if (tid == 0) {                                      // literals: string bytes into LDS
+        uint32_t used = 0;
+        for (int i = 0; i < P.nconst; i++) {
+            Cell c = P.consts[i];
+            if (c.kind == K_STR && c.len <= KSTR - used) {
+                const uint8_t* s = str_ptr(c);
+                for (uint32_t j = 0; j < c.len; j++) kstr[used + j] = s[j];
+                c.bits = (uint64_t)(uintptr_t)(kstr + used);
+                used += c.len;
+            }
+            kc[i] = c;
+        }
+    }
+    __syncthreads();
+
     // per-thread partials (single-group mode) and statistics
-    unsigned long long my_cnt = 0, my_first = NOPOS, my_records = 0, my_short = 0, my_spill = 0,
-                       my_slow = 0, my_pass = 0;
-    double my_sum[MAX_ACC];
-    unsigned long long my_num[MAX_ACC];
-    Cell my_ext[MAX_ACC];
-    unsigned long long my_pos[MAX_ACC];
-    uint32_t my_cls[MAX_ACC];
+    unsigned long long my_cnt = 0, my_first = NOPOS, my_records = 0, my_short = 0, my_spill = 0, my_pass = 0;
+    double my_sum[KA];
+    unsigned long long my_num[KA];
+    Cell my_ext[KA];
+    unsigned long long my_pos[KA];
+    uint32_t my_cls[KA];
 #pragma unroll
-    for (int a = 0; a < MAX_ACC; a++) {
+    for (int a = 0; a < KA; a++) {
         my_sum[a] = 0.0; my_num[a] = 0; my_ext[a] = cell_null(); my_pos[a] = NOPOS; my_cls[a] = 0;
     }
 
     // uniform plan facts
     const int nneed = P.nneed;
+    const int nacc = P.nacc;
     const int gslot = GROUPED ? P.group_slot : -1;
-    const bool simple = P.nprog == 3 && P.prog[0].op == OP_COL && P.prog[1].op == OP_CONST && P.prog[2].op == OP_CMP;
-    const int wslot = simple ? P.prog[0].a : 0;
-    const uint32_t wop = simple ? P.prog[2].a : 0;
-    const Cell wconst = simple ? P.consts[P.prog[1].b] : cell_null();
+    const int wslot = WM == W_SIMPLE ? P.prog[0].a : -1;
+    const uint32_t wop = WM == W_SIMPLE ? P.prog[2].a : 0;
+    const Cell wconst = WM == W_SIMPLE ? kc[P.prog[1].b] : cell_null();
     const GKey null_key = group_key(cell_null());
+    const int clast = nneed > 0 ? P.need_col[nneed - 1] : 0;
 
     const uint64_t lo_ok = P.data_begin > P.range_begin ? P.data_begin : P.range_begin;
     const uint64_t hi_ok = P.range_end < P.n ? P.range_end : P.n;
-    const uint64_t first_win = P.range_begin / WIN;
-    const uint64_t last_win = (hi_ok + WIN - 1) / WIN;
+    const uint64_t first_win = P.range_begin / WSTRIDE;
+    const uint64_t last_win = (hi_ok + WSTRIDE - 1) / WSTRIDE;
     const uint32_t delim = P.delim, quote = P.quote;
     const uint32_t rep_d = delim * 0x01010101u, rep_q = quote * 0x01010101u;
     // strtoll/strtod read past the field end: a delimiter they could consume
     // (digit, '.', letter) sends numerals to the general cell parser
     const bool num_ok = !(is_digit(delim) || delim == '.' || ((delim | 32) >= 'a' && (delim | 32) <= 'z'));
+    const uint64_t tile_g = (uint64_t)(uintptr_t)tile;
 
     v4u pf[PF];
     uint64_t w = first_win + blockIdx.x;
-    if (w < last_win) prefetch(g, w * WIN, pf);
+    if (w < last_win) prefetch(g, w * WSTRIDE, pf);
 
-    for (; w < last_win; w += gridDim.x) {
-        const uint64_t ws = w * WIN;
+    for (uint32_t iter = 0; w < last_win; w += gridDim.x, iter++) {
+        const uint64_t ws = w * WSTRIDE;
+        const uint64_t gt0 = (uint64_t)(uintptr_t)(g + ws - PREB);   // HBM address of tile byte 0
         lds_barrier();                                   // previous window fully consumed
 #pragma unroll
-        for (int j = 0; j < PF; j++) {
-            const int i = tid + j * SCAN_T;
-            if (i < TILE16) ((v4u*)tile)[i] = pf[j];
-        }
+        for (int j = 0; j < PF; j++) ((v4u*)tile)[tid + j * SCAN_T] = pf[j];
         lds_barrier();
-        if (w + gridDim.x < last_win) prefetch(g, (w + gridDim.x) * WIN, pf);   // in flight meanwhile
+        if (w + gridDim.x < last_win) prefetch(g, (w + gridDim.x) * WSTRIDE, pf);   // in flight meanwhile
 
-        // ---- classify: lane t -> mask word t (lanes 0..31 also the margin words)
-        uint64_t my_nl;
-        {
-            uint64_t sepm;
-            bool hq;
-            classify64(tile + PRE + tid * 64, rep_d, rep_q, my_nl, sepm, hq);
-            nlw[tid] = my_nl;
-            sepw[tid] = sepm;
-            qfl[tid] = hq;
-            if (tid < NMW - SCAN_T) {
-                uint64_t n2;
-                classify64(tile + PRE + (SCAN_T + tid) * 64, rep_d, rep_q, n2, sepm, hq);
-                nlw[SCAN_T + tid] = n2;
-                sepw[SCAN_T + tid] = sepm;
-                qfl[SCAN_T + tid] = hq;
-            }
-        }
-        lds_barrier();
-        // ---- record starts in this lane's 64 window bytes
-        uint64_t starts;
-        {
-            const uint64_t prev_nl = (tid == 0) ? (is_nl(tile[PRE - 1]) ? 1ULL : 0ULL) : (nlw[tid - 1] >> 63);
-            starts = ~my_nl & ((my_nl << 1) | prev_nl);
-            const uint64_t base = ws + (uint64_t)tid * 64;
-            if (base + 64 <= lo_ok || base >= hi_ok) {
+#if defined(CQ_PROF_STAGE) && CQ_PROF_STAGE == 0   // profiling build: staging only
+        if (tid == 0) my_records += ((const uint32_t*)tile)[w & 1023];
+        continue;
+#endif
+        // ---- classify this lane's LB bytes
+        uint32_t nlm, sepm;
+        bool hq;
+        classify32(tile + tid * LB, rep_d, rep_q, nlm, sepm, hq);
+        // ---- record starts owned by this window: [ws, ws + WSTRIDE) within [lo_ok, hi_ok)
+        uint32_t starts = 0;
+        if (tid > 0) {
+            const uint32_t prev_nl = is_nl(tile[tid * LB - 1]) ? 1u : 0u;
+            starts = ~nlm & ((nlm << 1) | prev_nl);
+            const uint64_t base = ws - PREB + (uint64_t)tid * LB;       // file offset of bit 0
+            const uint64_t lo = lo_ok > ws ? lo_ok : ws;
+            const uint64_t hi = hi_ok < ws + WSTRIDE ? hi_ok : ws + WSTRIDE;
+            if (base + LB <= lo || base >= hi) {
                 starts = 0;
             } else {
-                if (base < lo_ok) starts &= ~0ULL << (lo_ok - base);
-                if (base + 64 > hi_ok) starts &= (1ULL << (hi_ok - base)) - 1;
+                if (base < lo) starts &= ~0u << (lo - base);
+                if (base + LB > hi) starts &= (1u << (hi - base)) - 1;
             }
         }
-        const uint32_t cnt = (uint32_t)__popcll(starts);
-        uint32_t total;
-        const uint32_t idx = block_excl_scan(cnt, wsum, &total);
+        // ---- number separators, terminators, records and quote words
+        const uint32_t nsep = (uint32_t)__popc(sepm), nnl = (uint32_t)__popc(nlm);
+        const uint32_t nrs = (uint32_t)__popc(starts);
+        uint32_t e_sn, e_rq, t_sn, t_rq;
+        block_excl_scan2(nsep | (nnl << 16), nrs | ((hq ? 1u : 0u) << 16), wsum, e_sn, e_rq, t_sn, t_rq);
+        const uint32_t sep_base = e_sn & 0xFFFF, nl_base = e_sn >> 16, rec_base = e_rq & 0xFFFF;
+        const uint32_t nsep_tot = min(t_sn & 0xFFFF, (uint32_t)ECAP), nnl_tot = min(t_sn >> 16, (uint32_t)NLCAP);
+        const uint32_t total = t_rq & 0xFFFF;
+        QP[tid] = (uint16_t)(e_rq >> 16);
+        if (tid == SCAN_T - 1) QP[NW] = (uint16_t)(t_rq >> 16);
+#ifndef CQ_NO_INDEX
+        {
+            uint32_t m = sepm;
+            uint32_t j = sep_base;
+            while (m) {
+                const uint32_t b = (uint32_t)__builtin_ctzg(m, 32);
+                m &= m - 1;
+                if (j < ECAP) E[j] = (uint16_t)(tid * LB + b);
+                j++;
+            }
+            m = nlm;
+            j = nl_base;
+            while (m) {
+                const uint32_t b = (uint32_t)__builtin_ctzg(m, 32);
+                m &= m - 1;
+                if (j < NLCAP) NLI[j] = (uint16_t)(sep_base + popc_below(sepm, b));
+                j++;
+            }
+        }
+#endif
         for (uint32_t chunk = 0; chunk < total; chunk += RSMAX) {
             {
-                uint64_t m = starts;
-                uint32_t ri = idx;
+                uint32_t m = starts;
+                uint32_t ri = rec_base;
                 while (m) {
-                    const int b = __ffsll((long long)m) - 1;
+                    const uint32_t b = (uint32_t)__builtin_ctzg(m, 32);
                     m &= m - 1;
-                    if (ri >= chunk && ri < chunk + RSMAX) rs[ri - chunk] = (uint16_t)(tid * 64 + b);
+                    if (ri >= chunk && ri < chunk + RSMAX) {
+                        rs[ri - chunk] = (tid * LB + b) | ((sep_base + popc_below(sepm, b)) << 16);
+                        rq[ri - chunk] = (uint16_t)(nl_base + popc_below(nlm, b));
+                    }
                     ri++;
                 }
             }
             lds_barrier();
+#if defined(CQ_PROF_STAGE) && CQ_PROF_STAGE == 1   // profiling build: split + classify only
+            const uint32_t nrec = 0;
+            if (tid == 0) my_records += min((uint32_t)RSMAX, total - chunk);
+#else
             const uint32_t nrec = min((uint32_t)RSMAX, total - chunk);
+#endif
             for (uint32_t base0 = 0; base0 < nrec; base0 += SCAN_T) {
                 // trip count is block-uniform: every lane of a wave runs every trip
                 const uint32_t ri = base0 + tid;
                 const bool valid = ri < nrec;
-                const uint32_t r = valid ? rs[ri] : 0;
-                const uint64_t rec = ws + r;
-                Cells cs;
-#pragma unroll
-                for (int k = 0; k < MAX_NEED; k++) cs.c[k] = cell_null();
+                const uint32_t ent = valid ? rs[ri] : 0;
+                const uint32_t pos = ent & 0xFFFF, j0 = ent >> 16;
+                const uint32_t qi = valid ? rq[ri] : 0;
+                const uint64_t rec = ws - PREB + pos;
+                CellsT<KN> cs;
+                Cell wc = cell_null();
+                Cell av[KA];
                 GKey key = null_key;
-                bool pass = false;
-                if (valid) {
-                    // -- fast walk over the 128-bit mask views at the record start
-                    const uint32_t wi = r >> 6, o = r & 63;
-                    View S = view128(sepw, wi, o);
-                    const uint32_t rend = first128(view128(nlw, wi, o));
-                    bool fail = (qfl[wi] | qfl[wi + 1]) != 0;
-                    bool ended = false;
-                    uint32_t fs = 0;
-                    int col = 0;
+                // -- fields from the separator list: field c = (E[j0+c-1], E[j0+c])
+                bool fail = !valid || qi >= nnl_tot;
+                const uint32_t jn = fail ? 0u : NLI[qi];            // the record's terminator
+                fail = fail || jn >= nsep_tot;
+                uint32_t fend = pos;                                // end of the last field typed
 #pragma unroll
-                    for (int k = 0; k < MAX_NEED; k++) {
-                        if (k >= nneed) break;
-                        const int want = P.need_col[k];
-                        for (; col < want; col++) {            // uniform trip count, no branches
-                            const uint32_t e = first128(S);
-                            fail = fail || (e == NONE && !ended);
-                            ended = ended || e == rend;
-                            fs = e + 1;
-                            pop128(S);
-                        }
-                        const uint32_t e = first128(S);
-                        fail = fail || (e == NONE && !ended);
-                        Cell c = cell_null();
-                        if (!ended && !fail) {                 // uniform unless the record is short
-                            fail = fast_field(tile, PRE + r + fs, e - fs, num_ok, k == gslot, c, key) != FF_OK;
-                            if (c.kind == K_STR) c.bits = (uint64_t)(uintptr_t)(g + rec + fs);
-                        }
-                        cs.c[k] = c;
+                for (int k = 0; k < KN; k++) {
+                    if (k >= nneed) break;
+                    const uint32_t c = (uint32_t)P.need_col[k];
+                    Cell cell = cell_null();
+                    if (!fail && j0 + c <= jn) {                   // the record has column c
+                        const uint32_t fs = c ? (uint32_t)E[j0 + c - 1] + 1 : pos;
+                        const uint32_t fe = E[j0 + c];
+                        fail = fast_field(tile, fs, fe - fs, num_ok, k == gslot, cell, key) != FF_OK;
+                        if (cell.kind == K_STR) cell.bits = tile_g + fs;
+                        fend = fe;
                     }
-                    bool short_row = ended;
-                    if (fail) {
-                        // -- the general parse_line cursor over global memory
-                        my_slow++;
-                        short_row = parse_record_regs(g + rec, P, cs);
-                        if (GROUPED) key = group_key_slow(get_cell(cs, gslot, nneed));
+                    cs.c[k] = cell;
+                    if (WM == W_SIMPLE && k == wslot) wc = cell;
+#pragma unroll
+                    for (int a = 0; a < KA; a++)
+                        if (a < nacc && P.acc[a].slot == k) av[a] = cell;
+                }
+                // a quote before the end of the last typed field may hide separators
+                fail = fail || QP[fend / LB + 1] != QP[pos / LB];
+                // -- records the fast path declines go to slow_kernel, whole
+                const bool slow = valid && fail;
+                const uint64_t sb = __ballot(slow);
+                if (sb) {
+                    unsigned long long base = 0;
+                    if ((tid & 63) == 0) base = atomicAdd(&stats->slow_records, (unsigned long long)__popcll(sb));
+                    base = __shfl(base, 0, 64);
+                    if (slow) {
+                        const unsigned long long i = base + __popcll(sb & ((1ULL << (tid & 63)) - 1));
+                        if (i < slow_cap) slow_list[i] = rec;
                     }
+                }
+                bool pass = false;
+                if (valid && !fail) {
+                    if (key.cls == GK_LONG) key.w0 = key.w0 - tile_g + gt0;
                     my_records++;
-                    if (short_row) my_short++;
-                    if (P.nprog == 0) pass = true;
-                    else if (simple) pass = cmp_result(wop, compare(get_cell(cs, wslot, nneed), wconst));
-                    else pass = eval_where_vm(P, cs);
+                    if (j0 + (uint32_t)clast > jn) my_short++;
+                    if (WM == W_NONE) pass = true;
+                    else if (WM == W_SIMPLE) pass = cmp_result(wop, compare(wc, wconst));
+                    else pass = P.nprog == 0 || eval_where_vm(P, kc, cs);
                     if (pass) my_pass++;
                 }
                 if (pass && row_out) {
@@ -892,28 +1035,32 @@ __global__ __launch_bounds__(SCAN_T) void scan_kernel(const uint8_t* __restrict_
                         row_out[slot] = rec;
                         if (cells_out) {   // debug: the cells this kernel parsed
 #pragma unroll
-                            for (int k = 0; k < MAX_NEED; k++)
-                                if (k < nneed) cells_out[slot * nneed + k] = cs.c[k];
+                            for (int k = 0; k < KN; k++) {
+                                if (k >= nneed) break;
+                                Cell c = cs.c[k];
+                                if (c.kind == K_STR) c.bits = c.bits - tile_g + gt0;
+                                cells_out[slot * nneed + k] = c;
+                            }
                         }
                     }
                 }
-                if (pass) {
+                if (EXT && pass) {
 #pragma unroll
-                    for (int a = 0; a < MAX_ACC; a++)
-                        if (a < P.nacc && P.acc[a].kind != ACC_SUM)
-                            my_cls[a] |= class_bit(get_cell(cs, P.acc[a].slot, nneed));
+                    for (int a = 0; a < KA; a++)
+                        if (a < nacc && P.acc[a].kind != ACC_SUM) my_cls[a] |= class_bit(av[a]);
                 }
                 if (!GROUPED) {
                     if (pass) {
                         my_cnt++;
                         if (rec < my_first) my_first = rec;
 #pragma unroll
-                        for (int a = 0; a < MAX_ACC; a++) {
-                            if (a >= P.nacc) break;
-                            const Cell c = get_cell(cs, P.acc[a].slot, nneed);
+                        for (int a = 0; a < KA; a++) {
+                            if (a >= nacc) break;
+                            Cell c = av[a];
                             if (P.acc[a].kind == ACC_SUM) {
                                 if (is_num(c)) { my_sum[a] += num_of(c); my_num[a]++; }
-                            } else if (c.kind != K_NULL && ext_better(P.acc[a].kind, c, rec, my_ext[a], my_pos[a])) {
+                            } else if (EXT && c.kind != K_NULL && ext_better(P.acc[a].kind, c, rec, my_ext[a], my_pos[a])) {
+                                if (c.kind == K_STR) c.bits = c.bits - tile_g + gt0;
                                 my_ext[a] = c;
                                 my_pos[a] = rec;
                             }
@@ -924,31 +1071,36 @@ __global__ __launch_bounds__(SCAN_T) void scan_kernel(const uint8_t* __restrict_
                     int s = -1;
                     if (pass) {
                         h = gk_hash(key);
+#ifdef CQ_NO_INSERT   // profiling build: direct-mapped slot, results wrong
+                        s = (int)(h & (H - 1));
+#else
                         s = l_insert(lt, key, h);
+#endif
                     }
                     const bool in_lds = pass && s >= 0;
                     const bool spill = pass && s < 0;
                     if (in_lds) {
                         atomicAdd(&lt.cnt[s], 1u);
-                        if (rec < lt.first[s]) atomicMin(&lt.first[s], (unsigned long long)rec);
+                        atomicMin(&lt.first[s], (iter << 15) | pos);
 #pragma unroll
-                        for (int a = 0; a < MAX_ACC; a++) {
-                            if (a >= P.nacc) break;
+                        for (int a = 0; a < KA; a++) {
+                            if (a >= nacc) break;
                             if (!la[a].sum) continue;
-                            const Cell c = get_cell(cs, P.acc[a].slot, nneed);
-                            if (is_num(c)) {
-                                atomicAdd(&la[a].sum[s], num_of(c));
-                                atomicAdd(&la[a].num[s], 1u);
-                            }
+                            const Cell c = av[a];
+                            if (is_num(c)) atomicAdd(&la[a].sum[s], num_of(c));
+                            else atomicAdd(&la[a].miss[s], 1u);
                         }
                     }
+                    if (EXT) {
 #pragma unroll
-                    for (int a = 0; a < MAX_ACC; a++) {
-                        if (a >= P.nacc) break;
-                        if (!le[a].c) continue;                  // uniform
-                        const Cell c = get_cell(cs, P.acc[a].slot, nneed);
-                        lds_ext_update(in_lds && c.kind != K_NULL, le[a], in_lds ? (uint32_t)s : 0u,
-                                       P.acc[a].kind, c, rec);
+                        for (int a = 0; a < KA; a++) {
+                            if (a >= nacc) break;
+                            if (!le[a].c) continue;              // uniform
+                            Cell c = av[a];
+                            if (c.kind == K_STR) c.bits = c.bits - tile_g + gt0;
+                            lds_ext_update(in_lds && c.kind != K_NULL, le[a], in_lds ? (uint32_t)s : 0u,
+                                           P.acc[a].kind, c, rec);
+                        }
                     }
                     if (__any(spill)) {
                         // LDS table full: this record goes straight to the HBM table
@@ -960,9 +1112,9 @@ __global__ __launch_bounds__(SCAN_T) void scan_kernel(const uint8_t* __restrict_
                                 atomicAdd(&gt.cnt[gi], 1ULL);
                                 atomicMin(&gt.first[gi], (unsigned long long)rec);
 #pragma unroll
-                                for (int a = 0; a < MAX_ACC; a++) {
-                                    if (a >= P.nacc) break;
-                                    const Cell c = get_cell(cs, P.acc[a].slot, nneed);
+                                for (int a = 0; a < KA; a++) {
+                                    if (a >= nacc) break;
+                                    const Cell c = av[a];
                                     if (P.acc[a].kind == ACC_SUM && is_num(c)) {
                                         atomicAdd(&gt.sum[a][gi], num_of(c));
                                         atomicAdd(&gt.num[a][gi], 1ULL);
@@ -970,13 +1122,16 @@ __global__ __launch_bounds__(SCAN_T) void scan_kernel(const uint8_t* __restrict_
                                 }
                             }
                         }
+                        if (EXT) {
 #pragma unroll
-                        for (int a = 0; a < MAX_ACC; a++) {
-                            if (a >= P.nacc) break;
-                            if (P.acc[a].kind == ACC_SUM) continue;   // uniform
-                            const Cell c = get_cell(cs, P.acc[a].slot, nneed);
-                            g_ext_update(spill && gi >= 0 && c.kind != K_NULL, gt, a, P.acc[a].kind,
-                                         gi >= 0 ? (uint32_t)gi : 0u, c, rec, stats);
+                            for (int a = 0; a < KA; a++) {
+                                if (a >= nacc) break;
+                                if (P.acc[a].kind == ACC_SUM) continue;   // uniform
+                                Cell c = av[a];
+                                if (c.kind == K_STR) c.bits = c.bits - tile_g + gt0;
+                                g_ext_update(spill && gi >= 0 && c.kind != K_NULL, gt, a, P.acc[a].kind,
+                                             gi >= 0 ? (uint32_t)gi : 0u, c, rec, stats);
+                            }
                         }
                     }
                 }
@@ -988,28 +1143,28 @@ __global__ __launch_bounds__(SCAN_T) void scan_kernel(const uint8_t* __restrict_
 
     // ---- statistics and value-class masks
     {
-        unsigned long long r = my_records, s = my_short, sp = my_spill, sl = my_slow, ps = my_pass;
+        unsigned long long r = my_records, s = my_short, sp = my_spill, ps = my_pass;
         for (int o = 32; o > 0; o >>= 1) {
             r += __shfl_down(r, o, 64);
             s += __shfl_down(s, o, 64);
             sp += __shfl_down(sp, o, 64);
-            sl += __shfl_down(sl, o, 64);
             ps += __shfl_down(ps, o, 64);
         }
         if ((tid & 63) == 0) {
             if (r) atomicAdd(&stats->records, r);
             if (s) atomicAdd(&stats->short_rows, s);
             if (sp) atomicAdd(&stats->lds_spills, sp);
-            if (sl) atomicAdd(&stats->slow_records, sl);
             if (ps) atomicAdd(&stats->passed, ps);
         }
     }
+    if (EXT) {
 #pragma unroll
-    for (int a = 0; a < MAX_ACC; a++) {
-        if (a >= P.nacc) break;
-        uint32_t m = my_cls[a];
-        for (int o = 32; o > 0; o >>= 1) m |= __shfl_down(m, o, 64);
-        if ((tid & 63) == 0 && m) atomicOr(&stats->acc_classes[a], m);
+        for (int a = 0; a < KA; a++) {
+            if (a >= nacc) break;
+            uint32_t m = my_cls[a];
+            for (int o = 32; o > 0; o >>= 1) m |= __shfl_down(m, o, 64);
+            if ((tid & 63) == 0 && m) atomicOr(&stats->acc_classes[a], m);
+        }
     }
 
     if (!GROUPED) {
@@ -1020,10 +1175,10 @@ __global__ __launch_bounds__(SCAN_T) void scan_kernel(const uint8_t* __restrict_
             const unsigned long long ff = __shfl_down(f, o, 64);
             f = ff < f ? ff : f;
         }
-        double sm[MAX_ACC];
-        unsigned long long nm[MAX_ACC];
+        double sm[KA];
+        unsigned long long nm[KA];
 #pragma unroll
-        for (int a = 0; a < MAX_ACC; a++) {
+        for (int a = 0; a < KA; a++) {
             sm[a] = my_sum[a];
             nm[a] = my_num[a];
             for (int o = 32; o > 0; o >>= 1) {
@@ -1040,65 +1195,190 @@ __global__ __launch_bounds__(SCAN_T) void scan_kernel(const uint8_t* __restrict_
                 if (c) atomicAdd(&gt.cnt[gi], c);
                 if (f != NOPOS) atomicMin(&gt.first[gi], f);
 #pragma unroll
-                for (int a = 0; a < MAX_ACC; a++)
-                    if (a < P.nacc && P.acc[a].kind == ACC_SUM && nm[a]) {
+                for (int a = 0; a < KA; a++)
+                    if (a < nacc && P.acc[a].kind == ACC_SUM && nm[a]) {
                         atomicAdd(&gt.sum[a][gi], sm[a]);
                         atomicAdd(&gt.num[a][gi], nm[a]);
                     }
             }
         }
         gi = __shfl(gi, 0, 64);
+        if (EXT) {
 #pragma unroll
-        for (int a = 0; a < MAX_ACC; a++) {
-            if (a >= P.nacc) break;
-            if (P.acc[a].kind == ACC_SUM) continue;
-            g_ext_update(gi >= 0 && my_pos[a] != NOPOS, gt, a, P.acc[a].kind, gi >= 0 ? (uint32_t)gi : 0u,
-                         my_ext[a], my_pos[a], stats);
+            for (int a = 0; a < KA; a++) {
+                if (a >= nacc) break;
+                if (P.acc[a].kind == ACC_SUM) continue;
+                // wave-reduce the extreme first: one published candidate per wave
+                Cell e = my_ext[a];
+                unsigned long long ep = my_pos[a];
+                for (int o = 32; o > 0; o >>= 1) {
+                    Cell x;
+                    x.kind = __shfl_down(e.kind, o, 64);
+                    x.len = __shfl_down(e.len, o, 64);
+                    x.bits = __shfl_down(e.bits, o, 64);
+                    const unsigned long long xp = __shfl_down(ep, o, 64);
+                    if (xp != NOPOS && ext_better(P.acc[a].kind, x, xp, e, ep)) { e = x; ep = xp; }
+                }
+                if ((tid & 63) == 0 && gi >= 0 && ep != NOPOS) {
+                    const uint64_t idx = (uint64_t)blockIdx.x * gt.cand_stride + (tid >> 6);
+                    ExtCand ec;
+                    ec.c = e; ec.pos = ep; ec.pad = 0;
+                    gt.cand[a][idx] = ec;
+                    __threadfence();
+                    g_ext_swing(gt, a, P.acc[a].kind, (uint32_t)gi, idx);
+                }
+            }
         }
         return;
     }
 
-    // ---- flush the LDS table into the global table (wave-uniform trips)
+    // ---- flush the LDS table into the global table
     for (uint32_t b0 = 0; b0 < H; b0 += SCAN_T) {
         const uint32_t i = b0 + tid;
-        const bool act = i < H && lt.tag[i] >= 2;
+        const bool act = i < H && lt.hdr[i] >= 2;
         int gi = -1;
         if (act) {
+            const uint32_t hd = lt.hdr[i];
+            const v4u kw = lt.key[i];
             GKey k;
-            k.cls = lt.clslen[i] >> 16;
-            k.len = lt.clslen[i] & 0xffff;
-            k.w0 = lt.w0[i];
-            k.w1 = lt.w1[i];
+            k.cls = (hd >> 16) & 7;
+            k.len = hd & 0xFFFF;
+            k.w0 = (uint64_t)kw.x | ((uint64_t)kw.y << 32);
+            k.w1 = (uint64_t)kw.z | ((uint64_t)kw.w << 32);
             gi = g_insert(gt, k, gk_hash(k), stats);
             if (gi >= 0) {
-                atomicAdd(&gt.cnt[gi], (unsigned long long)lt.cnt[i]);
-                atomicMin(&gt.first[gi], lt.first[i]);
+                const uint32_t n = lt.cnt[i];
+                const uint32_t f = lt.first[i];
+                const uint64_t fw = first_win + blockIdx.x + (uint64_t)(f >> 15) * gridDim.x;
+                atomicAdd(&gt.cnt[gi], (unsigned long long)n);
+                atomicMin(&gt.first[gi], (unsigned long long)(fw * WSTRIDE - PREB + (f & 0x7FFF)));
 #pragma unroll
-                for (int a = 0; a < MAX_ACC; a++) {
-                    if (a >= P.nacc) break;
-                    if (la[a].sum && la[a].num[i]) {
+                for (int a = 0; a < KA; a++) {
+                    if (a >= nacc) break;
+                    if (!la[a].sum) continue;
+                    const uint32_t num = n - la[a].miss[i];
+                    if (num) {
                         atomicAdd(&gt.sum[a][gi], la[a].sum[i]);
-                        atomicAdd(&gt.num[a][gi], (unsigned long long)la[a].num[i]);
+                        atomicAdd(&gt.num[a][gi], (unsigned long long)num);
+                    }
+                }
+            }
+        }
+        if (EXT && act && gi >= 0) {
+#pragma unroll
+            for (int a = 0; a < KA; a++) {
+                if (a >= nacc) break;
+                if (!le[a].c || le[a].pos[i] == NOPOS) continue;
+                const uint64_t idx = (uint64_t)blockIdx.x * gt.cand_stride + i;
+                ExtCand ec;
+                ec.c = le[a].c[i]; ec.pos = le[a].pos[i]; ec.pad = 0;
+                gt.cand[a][idx] = ec;
+                __threadfence();
+                g_ext_swing(gt, a, P.acc[a].kind, (uint32_t)gi, idx);
+            }
+        }
+    }
+}
+
+// The records scan_kernel declined (quotes before a needed field, blanks or
+// control bytes in one, date-shaped or long fields, records past the tile):
+// general parse_line + parse_value from HBM, WHERE bytecode, aggregation straight
+// into the HBM table.  Grid-stride with block-uniform trips (the MIN/MAX lock
+// loops need whole waves).
+template <bool GROUPED>
+__global__ __launch_bounds__(256) void slow_kernel(const uint8_t* __restrict__ g, ScanStats* __restrict__ stats,
+                                                   unsigned long long* __restrict__ row_out,
+                                                   unsigned long long row_cap, Cell* __restrict__ cells_out,
+                                                   const unsigned long long* __restrict__ slow_list,
+                                                   unsigned long long slow_cap) {
+    const ScanPlan& P = c_plan;
+    const GroupTable& gt = c_gt;
+    const unsigned long long listed = __hip_atomic_load(&stats->slow_records, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    const unsigned long long n = listed < slow_cap ? listed : slow_cap;
+    const int nneed = P.nneed, nacc = P.nacc;
+    unsigned long long my_records = 0, my_short = 0, my_pass = 0;
+    for (unsigned long long b0 = (unsigned long long)blockIdx.x * blockDim.x; b0 < n;
+         b0 += (unsigned long long)gridDim.x * blockDim.x) {
+        const unsigned long long i = b0 + threadIdx.x;
+        const bool valid = i < n;
+        const uint64_t rec = valid ? slow_list[i] : 0;
+        CellsT<MAX_NEED> cs;
+#pragma unroll
+        for (int k = 0; k < MAX_NEED; k++) cs.c[k] = cell_null();
+        bool pass = false;
+        if (valid) {
+            const Src S{g + rec, g + rec, 0, false};
+            const bool short_row = parse_record_regs(S, P, cs);
+            my_records++;
+            if (short_row) my_short++;
+            pass = P.nprog == 0 || eval_where_vm(P, P.consts, cs);
+            if (pass) my_pass++;
+        }
+        if (pass && row_out) {
+            const unsigned long long slot = atomicAdd(&stats->rows_emitted, 1ULL);
+            if (slot < row_cap) {
+                row_out[slot] = rec;
+                if (cells_out)
+                    for (int k = 0; k < nneed; k++) cells_out[slot * nneed + k] = get_cell(cs, k, nneed);
+            }
+        }
+        if (pass) {
+            for (int a = 0; a < nacc; a++)
+                if (P.acc[a].kind != ACC_SUM) {
+                    const uint32_t m = class_bit(get_cell(cs, P.acc[a].slot, nneed));
+                    if (m) atomicOr(&stats->acc_classes[a], m);
+                }
+        }
+        GKey key;
+        key.cls = GK_ALL; key.len = 0; key.w0 = 0; key.w1 = 0;
+        uint64_t h = 0x12345678ULL;
+        if (GROUPED && pass) {
+            key = group_key(get_cell(cs, P.group_slot, nneed));
+            h = gk_hash(key);
+        }
+        int gi = -1;
+        if (pass) {
+            gi = g_insert(gt, key, h, stats);
+            if (gi >= 0) {
+                atomicAdd(&gt.cnt[gi], 1ULL);
+                atomicMin(&gt.first[gi], (unsigned long long)rec);
+                for (int a = 0; a < nacc; a++) {
+                    const Cell c = get_cell(cs, P.acc[a].slot, nneed);
+                    if (P.acc[a].kind == ACC_SUM && is_num(c)) {
+                        atomicAdd(&gt.sum[a][gi], num_of(c));
+                        atomicAdd(&gt.num[a][gi], 1ULL);
                     }
                 }
             }
         }
 #pragma unroll
         for (int a = 0; a < MAX_ACC; a++) {
-            if (a >= P.nacc) break;
-            if (!le[a].c) continue;                     // uniform
-            const bool ok = act && gi >= 0;
-            const Cell c = ok ? le[a].c[i] : cell_null();
-            const uint64_t pos = ok ? le[a].pos[i] : NOPOS;
-            g_ext_update(ok, gt, a, P.acc[a].kind, ok ? (uint32_t)gi : 0u, c, pos, stats);
+            if (a >= nacc) break;
+            if (P.acc[a].kind == ACC_SUM) continue;      // uniform
+            const Cell c = get_cell(cs, P.acc[a].slot, nneed);
+            g_ext_update(pass && gi >= 0 && c.kind != K_NULL, gt, a, P.acc[a].kind, gi >= 0 ? (uint32_t)gi : 0u,
+                         c, rec, stats);
         }
+    }
+    for (int o = 32; o > 0; o >>= 1) {
+        my_records += __shfl_down(my_records, o, 64);
+        my_short += __shfl_down(my_short, o, 64);
+        my_pass += __shfl_down(my_pass, o, 64);
+    }
+    if ((threadIdx.x & 63) == 0) {
+        if (my_records) atomicAdd(&stats->records, my_records);
+        if (my_short) atomicAdd(&stats->short_rows, my_short);
+        if (my_pass) atomicAdd(&stats->passed, my_pass);
     }
 }
 
 // ------------------------------------------------------------------ compaction
-__global__ void compact_kernel(int nacc, GroupOut* out, unsigned int* count,
+__global__ void compact_kernel(int nacc, uint32_t kinds, GroupOut* out, unsigned int* count,
                                unsigned int cap_out) {
     const GroupTable& gt = c_gt;
+    uint8_t kind_of[MAX_ACC];
+#pragma unroll
+    for (int a = 0; a < MAX_ACC; a++) kind_of[a] = (uint8_t)((kinds >> (2 * a)) & 3);
     const uint32_t i = blockIdx.x * blockDim.x + threadIdx.x;
     if (i >= gt.cap) return;
     if (gt.tag[i] < 2) return;
@@ -1116,6 +1396,10 @@ __global__ void compact_kernel(int nacc, GroupOut* out, unsigned int* count,
         r.num[a] = (a < nacc && gt.num[a]) ? gt.num[a][i] : 0ULL;
         r.ext[a] = (a < nacc && gt.ext[a]) ? gt.ext[a][i] : cell_null();
         r.extpos[a] = (a < nacc && gt.extpos[a]) ? gt.extpos[a][i] : NOPOS;
+        if (a < nacc && gt.extref[a] && gt.extref[a][i] != NOPOS) {   // the swung candidate
+            const ExtCand o = gt.cand[a][gt.extref[a][i]];
+            if (ext_better(kind_of[a], o.c, o.pos, r.ext[a], r.extpos[a])) { r.ext[a] = o.c; r.extpos[a] = o.pos; }
+        }
     }
     out[o] = r;
 }
@@ -1159,13 +1443,15 @@ __global__ void parse_literals_kernel(const uint8_t* __restrict__ text,
 // ------------------------------------------------------------------ host wrappers
 extern "C" {
 static size_t lds_slot_bytes(const cq::ScanPlan* P) {
-    size_t b = 4 + 4 + 8 + 8 + 4 + 8;   // tag, clslen, w0, w1, cnt, first
+    size_t b = 16 + 4 + 4 + 4;   // key, hdr, cnt, first
     for (int a = 0; a < P->nacc; a++) b += P->acc[a].kind == cq::ACC_SUM ? 12 : sizeof(cq::Cell) + 12;
     return b;
 }
 static size_t lds_fixed_bytes() {
     auto r16 = [](size_t x) { return (x + 15) & ~(size_t)15; };
-    return r16(cq::TILE) + 2 * r16(cq::NMW * 8) + r16(cq::NMW) + r16(cq::RSMAX * 2) + r16(64);
+    return r16(cq::TILE + cq::TILE_PAD) + r16(cq::ECAP * 2) + r16(cq::NLCAP * 2) + r16((cq::NW + 1) * 2) +
+           r16(cq::RSMAX * 4) + r16(cq::RSMAX * 2) + r16(32 * 4) + r16(cq::MAX_CONST * sizeof(cq::Cell)) +
+           r16(cq::KSTR);
 }
 
 // group-table capacity: the largest power of two <= 2048 that fits the budget
@@ -1178,49 +1464,95 @@ uint32_t cq_scan_lds_slots(const cq::ScanPlan* P, int grouped) {
     return h;
 }
 
+// MIN/MAX candidate slots per block (GroupTable.cand_stride): an LDS slot, or a wave
+uint32_t cq_scan_cand_stride(const cq::ScanPlan* P, int grouped) {
+    const uint32_t h = cq_scan_lds_slots(P, grouped);
+    const uint32_t waves = cq::SCAN_T / 64;
+    return h > waves ? h : waves;
+}
+
 size_t cq_scan_lds_bytes(const cq::ScanPlan* P, int grouped) {
     size_t b = lds_fixed_bytes();
     if (grouped) b += (size_t)cq_scan_lds_slots(P, grouped) * lds_slot_bytes(P) + 512;
     return b;
 }
 
+}  // extern "C"
+
+// plan shape -> kernel instance
+static int where_mode(const cq::ScanPlan* P) {
+    if (P->nprog == 0) return cq::W_NONE;
+    if (P->nprog == 3 && P->prog[0].op == cq::OP_COL && P->prog[1].op == cq::OP_CONST && P->prog[2].op == cq::OP_CMP)
+        return cq::W_SIMPLE;
+    return cq::W_VM;
+}
+static bool has_ext(const cq::ScanPlan* P) {
+    for (int a = 0; a < P->nacc; a++)
+        if (P->acc[a].kind != cq::ACC_SUM) return true;
+    return false;
+}
+static bool small_plan(const cq::ScanPlan* P) { return P->nneed <= 4 && P->nacc <= 2; }
+
+typedef void (*scan_fn_t)(const uint8_t*, cq::ScanStats*, unsigned long long*, unsigned long long, uint32_t,
+                          cq::Cell*, unsigned long long*, unsigned long long);
+template <bool G>
+static scan_fn_t pick_scan(const cq::ScanPlan* P) {
+    using namespace cq;
+    if (!small_plan(P)) return scan_kernel<G, 8, 8, W_VM, true>;
+    const int wm = where_mode(P);
+    const bool ext = has_ext(P);
+    if (wm == W_NONE) return ext ? scan_kernel<G, 4, 2, W_NONE, true> : scan_kernel<G, 4, 2, W_NONE, false>;
+    if (wm == W_SIMPLE) return ext ? scan_kernel<G, 4, 2, W_SIMPLE, true> : scan_kernel<G, 4, 2, W_SIMPLE, false>;
+    return ext ? scan_kernel<G, 4, 2, W_VM, true> : scan_kernel<G, 4, 2, W_VM, false>;
+}
+static scan_fn_t scan_fn(const cq::ScanPlan* P, int grouped) {
+    return grouped ? pick_scan<true>(P) : pick_scan<false>(P);
+}
+
+extern "C" {
+// the fast scan, then the general kernel over the records it declined
 hipError_t cq_launch_scan(const uint8_t* g, const cq::ScanPlan* P, const cq::GroupTable* gt,
                           cq::ScanStats* stats, unsigned long long* row_out,
                           unsigned long long row_cap, int grouped, int grid, hipStream_t s,
-                          cq::Cell* cells_out) {
+                          cq::Cell* cells_out, unsigned long long* slow_list, unsigned long long slow_cap) {
     const size_t lds = cq_scan_lds_bytes(P, grouped);
     hipError_t e = hipMemcpyToSymbolAsync(HIP_SYMBOL(cq::c_plan), P, sizeof *P, 0, hipMemcpyHostToDevice, s);
     if (e == hipSuccess) e = hipMemcpyToSymbolAsync(HIP_SYMBOL(cq::c_gt), gt, sizeof *gt, 0, hipMemcpyHostToDevice, s);
     if (e != hipSuccess) return e;
-    if (grouped) {
-        (void)hipFuncSetAttribute((const void*)cq::scan_kernel<true>,
-                                  hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds);
-        hipLaunchKernelGGL(cq::scan_kernel<true>, dim3(grid), dim3(cq::SCAN_T), lds, s, g,
-                           stats, row_out, row_cap, cq_scan_lds_slots(P, grouped), cells_out);
-    } else {
-        (void)hipFuncSetAttribute((const void*)cq::scan_kernel<false>,
-                                  hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds);
-        hipLaunchKernelGGL(cq::scan_kernel<false>, dim3(grid), dim3(cq::SCAN_T), lds, s, g,
-                           stats, row_out, row_cap, 0u, cells_out);
-    }
+    const uint32_t h = cq_scan_lds_slots(P, grouped);
+    const scan_fn_t fn = scan_fn(P, grouped);
+    (void)hipFuncSetAttribute((const void*)fn, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds);
+    hipLaunchKernelGGL(fn, dim3(grid), dim3(cq::SCAN_T), lds, s, g, stats, row_out, row_cap, h, cells_out,
+                       slow_list, slow_cap);
+    e = hipGetLastError();
+    if (e != hipSuccess) return e;
+    if (grouped)
+        hipLaunchKernelGGL(cq::slow_kernel<true>, dim3(256), dim3(256), 0, s, g, stats, row_out, row_cap, cells_out,
+                           slow_list, slow_cap);
+    else
+        hipLaunchKernelGGL(cq::slow_kernel<false>, dim3(256), dim3(256), 0, s, g, stats, row_out, row_cap, cells_out,
+                           slow_list, slow_cap);
     return hipGetLastError();
 }
 
 int cq_scan_occupancy(const cq::ScanPlan* P, int grouped) {
     const size_t lds = cq_scan_lds_bytes(P, grouped);
     int blocks = 0;
-    const void* fn = grouped ? (const void*)cq::scan_kernel<true> : (const void*)cq::scan_kernel<false>;
+    const void* fn = (const void*)scan_fn(P, grouped);
     (void)hipFuncSetAttribute(fn, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds);
     if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&blocks, fn, cq::SCAN_T, lds) != hipSuccess) return 1;
     return blocks > 0 ? blocks : 1;
 }
 
-hipError_t cq_launch_compact(const cq::GroupTable* gt, int nacc, cq::GroupOut* out,
+hipError_t cq_launch_compact(const cq::GroupTable* gt, const cq::ScanPlan* P, cq::GroupOut* out,
                              unsigned int* count, unsigned int cap_out, hipStream_t s) {
+    const int nacc = P->nacc;
+    uint32_t kinds = 0;
+    for (int a = 0; a < nacc; a++) kinds |= (uint32_t)P->acc[a].kind << (2 * a);
     const dim3 grid((gt->cap + 255) / 256);
     hipError_t e = hipMemcpyToSymbolAsync(HIP_SYMBOL(cq::c_gt), gt, sizeof *gt, 0, hipMemcpyHostToDevice, s);
     if (e != hipSuccess) return e;
-    hipLaunchKernelGGL(cq::compact_kernel, grid, dim3(256), 0, s, nacc, out, count, cap_out);
+    hipLaunchKernelGGL(cq::compact_kernel, grid, dim3(256), 0, s, nacc, kinds, out, count, cap_out);
     return hipGetLastError();
 }
 

@@ -80,6 +80,8 @@ typedef struct {
     int grid;                    /* scan blocks launched */
     int path;                    /* 1 = GPU executor, 2 = fallback evaluator */
     int retries;                 /* global group table regrowths */
+    uint64_t slow_records;       /* records the fast field path handed to the general parser */
+    uint64_t passed;             /* records that passed WHERE */
 } cqgpu_stats;
 int cqgpu_last_stats(cqgpu_stats* out);
 const char* cqgpu_last_error(void);
