@@ -46,7 +46,7 @@ def parse_args():
     ap.add_argument("--warmup", type=int, default=3)
     ap.add_argument("--rows", type=int, default=100_000_000, help="data rows per GPU")
     ap.add_argument("--seed", type=int, default=42)
-    ap.add_argument("--cpu-rows", type=int, default=2_000_000,
+    ap.add_argument("--cpu-rows", type=int, default=8_000_000,
                     help="rows of the CPU-baseline sample (reference evaluator)")
     ap.add_argument("--no-cpu", action="store_true")
     ap.add_argument("--traffic", default=os.path.join(ROOT, "profiles", "hbm_traffic.json"))
@@ -100,6 +100,7 @@ def main():
 
     import cq_amd
     from cq_amd import abi, datagen
+    from cq_amd.dist import gather_blobs
     cq_amd.lib()
 
     # ---- synthetic shard of this rank (one N x rows file, row-range partitioned)
@@ -148,22 +149,12 @@ def main():
         if n == 0:
             raise RuntimeError(cq_amd.last_error())
         scan_ms = cq_amd.stats()["scan_ms"]
-        mine = torch.frombuffer(bytearray(C.string_at(blob, n)), dtype=torch.uint8).cuda()
+        mine = C.string_at(blob, n)
         C.CDLL(None).free(blob)
-        lens = [torch.zeros(1, dtype=torch.int64, device="cuda") for _ in range(world)]
-        dist.all_gather(lens, torch.tensor([n], dtype=torch.int64, device="cuda"))
-        mx = int(max(x.item() for x in lens))
-        pad = torch.zeros(mx, dtype=torch.uint8, device="cuda")
-        pad[:n] = mine
-        outs = [torch.empty(mx, dtype=torch.uint8, device="cuda") for _ in range(world)]
-        dist.all_gather(outs, pad)
+        blobs = gather_blobs(mine, device=torch.device("cuda", local))
         ng = 0
         if rank == 0:
-            host = [bytes(o[: int(lens[i].item())].cpu().numpy()) for i, o in enumerate(outs)]
-            bufs = [C.create_string_buffer(h, len(h)) for h in host]
-            ptrs = (C.c_void_p * world)(*[C.cast(b, C.c_void_p).value for b in bufs])
-            szs = (C.c_size_t * world)(*[len(h) for h in host])
-            tp = L.cqgpu_merge_partials(ast, ptrs, szs, world)
+            tp = cq_amd.merge_partials(ast, blobs)
             if not tp:
                 raise RuntimeError(cq_amd.last_error())
             ng = tp.contents.nrows

@@ -137,6 +137,27 @@ def evaluate(ast) -> dict | None:
     return res
 
 
+def query_partial(ast, tables) -> bytes:
+    """Partial group state of this shard (cqgpu_query_partial), as bytes."""
+    arr, n = _tables_arg(tables)
+    blob = C.c_void_p()
+    size = lib().cqgpu_query_partial(ast, arr, n, C.byref(blob))
+    if size == 0:
+        raise RuntimeError(last_error() or "cqgpu_query_partial failed")
+    try:
+        return C.string_at(blob, size)
+    finally:
+        C.CDLL(None).free(blob)
+
+
+def merge_partials(ast, blobs):
+    """cqgpu_merge_partials over byte blobs; returns the result pointer (free with result_free)."""
+    bufs = [C.create_string_buffer(b, len(b)) for b in blobs]
+    ptrs = (C.c_void_p * len(bufs))(*[C.cast(b, C.c_void_p).value for b in bufs])
+    sizes = (C.c_size_t * len(bufs))(*[len(b) for b in blobs])
+    return lib().cqgpu_merge_partials(ast, ptrs, sizes, len(bufs))
+
+
 def stats() -> dict:
     s = Stats()
     lib().cqgpu_last_stats(C.byref(s))

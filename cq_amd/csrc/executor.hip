@@ -722,6 +722,37 @@ struct HGroup {
     std::vector<HCell> reps;            // representative cells (first row)
 };
 
+// little-endian byte writer / reader of the partial-aggregation blobs
+struct Blob {
+    std::vector<uint8_t> d;
+    void raw(const void* p, size_t n) { const uint8_t* b = (const uint8_t*)p; d.insert(d.end(), b, b + n); }
+    void u32(uint32_t v) { raw(&v, 4); }
+    void u64(uint64_t v) { raw(&v, 8); }
+    void f64(double v) { raw(&v, 8); }
+    void str(const std::string& s) { u32((uint32_t)s.size()); raw(s.data(), s.size()); }
+    void cell(const HCell& h) { u32(h.kind); u64(h.bits); str(h.s); }
+};
+struct Reader {
+    const uint8_t* p;
+    size_t n, o;
+    void raw(void* dst, size_t k) {
+        if (o + k > n) throw HipError{"truncated partial blob"};
+        memcpy(dst, p + o, k);
+        o += k;
+    }
+    uint32_t u32() { uint32_t v; raw(&v, 4); return v; }
+    uint64_t u64() { uint64_t v; raw(&v, 8); return v; }
+    double f64() { double v; raw(&v, 8); return v; }
+    std::string str() {
+        const uint32_t k = u32();
+        if (o + k > n) throw HipError{"truncated partial blob"};
+        std::string s((const char*)p + o, k);
+        o += k;
+        return s;
+    }
+    HCell cell() { HCell h; h.kind = u32(); h.bits = u64(); h.s = str(); return h; }
+};
+
 // literal cells parsed on the device with the same parser as the data
 struct Literals {
     uint8_t* dev = nullptr;
@@ -1601,14 +1632,160 @@ cq_table* cqgpu_debug_cells(cqgpu_table* t, const int* cols, int ncols, const un
     }
 }
 
-size_t cqgpu_query_partial(cq_node*, cqgpu_table* const*, int, void** blob_out) {
+// ---- partial aggregation across ranks (range-partitioned tables)
+// Blob: "CQP1", column names, per-accumulator value classes, then per group its
+// key, COUNT, first-row offset (whole-file), SUM/AVG state, MIN/MAX extreme with
+// its offset, and representative cells.  Merging is order-free: counts and sums
+// add, first offsets and extremes take the (value, offset) minimum, and the
+// representative row is the one of the smallest first offset -- what
+// create_groups / evaluate_aggregate give on the whole file.
+size_t cqgpu_query_partial(cq_node* q, cqgpu_table* const* tables, int ntables, void** blob_out) {
     if (blob_out) *blob_out = nullptr;
-    set_err("cq_amd: partial aggregation not built yet");
-    return 0;
+    g_inel.clear();
+    g_err.clear();
+    try {
+        DevCtx& c = ctx();
+        if (ntables < 1 || !tables[0]) throw HipError{"no table"};
+        const cqgpu_table* t = tables[0];
+        check_plan_shape(q, t);
+        Compiled C;
+        compile_aggregate(t, q, C);
+        Literals L;
+        ScanStats st;
+        memset(&st, 0, sizeof st);
+        std::vector<HGroup> groups = run_aggregate(c, t, C, L, &st);
+        Blob b;
+        b.u32(0x31505143u);                          // "CQP1"
+        b.u32((uint32_t)t->names.size());
+        for (auto& nm : t->names) b.str(nm);
+        b.u32((uint32_t)C.P.nacc);
+        for (int a = 0; a < C.P.nacc; a++) b.u32(st.acc_classes[a]);
+        const uint32_t nrep = (uint32_t)C.rep_cols.size();
+        b.u32(nrep);
+        b.u64(groups.size());
+        for (const HGroup& h : groups) {
+            b.u32(h.kcls); b.u32(h.klen); b.u64(h.kw0); b.u64(h.kw1); b.str(h.kbytes);
+            b.u64(h.cnt); b.u64(h.first);
+            for (int a = 0; a < C.P.nacc; a++) {
+                b.f64(h.sum[a]); b.u64(h.num[a]); b.u64(h.extpos[a]); b.cell(h.ext[a]);
+            }
+            for (uint32_t r = 0; r < nrep; r++) b.cell(r < h.reps.size() ? h.reps[r] : HCell());
+        }
+        void* out = malloc(std::max<size_t>(b.d.size(), 1));
+        if (!out) throw HipError{"out of host memory"};
+        memcpy(out, b.d.data(), b.d.size());
+        *blob_out = out;
+        return b.d.size();
+    } catch (Ineligible& e) {
+        g_inel = e.why;
+        set_err("cq_amd: query outside the GPU executor's subset: %s", e.why.c_str());
+        return 0;
+    } catch (HipError& e) {
+        set_err("cq_amd: %s", e.msg.c_str());
+        return 0;
+    }
 }
-cq_table* cqgpu_merge_partials(cq_node*, const void* const*, const size_t*, int) {
-    set_err("cq_amd: partial aggregation not built yet");
-    return nullptr;
+
+cq_table* cqgpu_merge_partials(cq_node* q, const void* const* blobs, const size_t* sizes, int nblobs) {
+    g_inel.clear();
+    g_err.clear();
+    try {
+        DevCtx& c = ctx();
+        if (nblobs < 1) throw HipError{"no partials"};
+        struct Part {
+            std::vector<std::string> names;
+            std::vector<uint32_t> classes;
+            std::vector<HGroup> groups;
+        };
+        std::vector<Part> parts(nblobs);
+        uint32_t nacc = 0, nrep = 0;
+        for (int bi = 0; bi < nblobs; bi++) {
+            Reader r{(const uint8_t*)blobs[bi], sizes[bi], 0};
+            if (r.u32() != 0x31505143u) throw HipError{"bad partial blob"};
+            Part& pt = parts[bi];
+            pt.names.resize(r.u32());
+            for (auto& nm : pt.names) nm = r.str();
+            const uint32_t na = r.u32();
+            for (uint32_t a = 0; a < na; a++) pt.classes.push_back(r.u32());
+            const uint32_t nr = r.u32();
+            if (bi == 0) { nacc = na; nrep = nr; }
+            else if (pt.names != parts[0].names || na != nacc || nr != nrep)
+                throw HipError{"partials from different plans"};
+            const uint64_t ng = r.u64();
+            for (uint64_t gi = 0; gi < ng; gi++) {
+                HGroup h;
+                h.kcls = r.u32(); h.klen = r.u32(); h.kw0 = r.u64(); h.kw1 = r.u64(); h.kbytes = r.str();
+                h.cnt = r.u64(); h.first = r.u64();
+                for (uint32_t a = 0; a < nacc; a++) {
+                    h.sum[a] = r.f64(); h.num[a] = r.u64(); h.extpos[a] = r.u64(); h.ext[a] = r.cell();
+                }
+                for (uint32_t k = 0; k < nrep; k++) h.reps.push_back(r.cell());
+                pt.groups.push_back(std::move(h));
+            }
+        }
+        // the plan binds columns by name: compile it against the shards' header
+        cqgpu_table meta;
+        meta.names = parts[0].names;
+        check_plan_shape(q, &meta);
+        Compiled C;
+        compile_aggregate(&meta, q, C);
+        if ((uint32_t)C.P.nacc != nacc || (uint32_t)C.rep_cols.size() != nrep)
+            throw HipError{"partials do not match the plan"};
+        for (uint32_t a = 0; a < nacc; a++) {
+            if (C.P.acc[a].kind == ACC_SUM) continue;
+            uint32_t m = 0;
+            for (auto& pt : parts) m |= pt.classes[a];
+            if (m & (m - 1)) throw Ineligible{"MIN/MAX over a column mixing numbers, strings and dates"};
+        }
+        std::vector<HGroup> merged;
+        std::unordered_map<std::string, size_t> where;
+        for (auto& pt : parts) {
+            for (HGroup& h : pt.groups) {
+                // group identity: class + text for text keys, class + payload otherwise
+                std::string id = std::to_string(h.kcls) + ":";
+                if (h.kcls == GK_STR || h.kcls == GK_LONG) id += h.kbytes;
+                else id += std::to_string(h.kw0);
+                auto it = where.find(id);
+                if (it == where.end()) {
+                    where.emplace(id, merged.size());
+                    merged.push_back(std::move(h));
+                    continue;
+                }
+                HGroup& m = merged[it->second];
+                m.cnt += h.cnt;
+                if (h.first < m.first) { m.first = h.first; m.reps = h.reps; }
+                for (uint32_t a = 0; a < nacc; a++) {
+                    m.sum[a] += h.sum[a];
+                    m.num[a] += h.num[a];
+                    if (C.P.acc[a].kind == ACC_SUM || h.extpos[a] == NOPOS) continue;
+                    bool better = m.extpos[a] == NOPOS;
+                    if (!better) {   // first strictly better wins (evaluator_aggregates.c:311-326)
+                        const int cv = hcompare(h.ext[a], m.ext[a]);
+                        better = (C.P.acc[a].kind == ACC_MIN ? cv < 0 : cv > 0) || (cv == 0 && h.extpos[a] < m.extpos[a]);
+                    }
+                    if (better) { m.ext[a] = h.ext[a]; m.extpos[a] = h.extpos[a]; }
+                }
+            }
+        }
+        // one group without GROUP BY, present even with no rows
+        if (!C.grouped && merged.size() > 1) throw HipError{"partials disagree on the single group"};
+        std::stable_sort(merged.begin(), merged.end(),
+                         [](const HGroup& x, const HGroup& y) { return x.first < y.first; });
+        Literals L;
+        parse_literals(c, C.lits, L);
+        g_stats.groups = merged.size();
+        cq_table* res = build_groups(C, merged, L, c);
+        post_ops(c, res, q);
+        g_stats.path = 1;
+        return res;
+    } catch (Ineligible& e) {
+        g_inel = e.why;
+        set_err("cq_amd: query outside the GPU executor's subset: %s", e.why.c_str());
+        return nullptr;
+    } catch (HipError& e) {
+        set_err("cq_amd: %s", e.msg.c_str());
+        return nullptr;
+    }
 }
 
 }  // extern "C"
