@@ -59,6 +59,7 @@ constexpr uint64_t NOPOS = ~0ULL;
 
 std::string g_err, g_inel;
 cqgpu_stats g_stats;
+unsigned long long g_clk[8];     // profiling builds: ScanStats.clk of the last scan
 cqgpu_fallback_fn g_fallback = nullptr;
 
 void set_err(const char* fmt, ...) {
@@ -899,6 +900,12 @@ std::vector<HGroup> run_aggregate(DevCtx& c, const cqgpu_table* t, Compiled& C, 
         }
         g_stats.scan_ms = ms_total;
         g_stats.grid = grid;
+        for (int i = 0; i < 8; i++) g_clk[i] = 0;
+        {
+            ScanStats s2;
+            HIPCHECK(hipMemcpy(&s2, A.stats, sizeof s2, hipMemcpyDeviceToHost));
+            for (int i = 0; i < 8; i++) g_clk[i] = s2.clk[i];
+        }
         if (st.overflow >= 2)   // a bounded spin gave up: a kernel bug, never a data property
             throw HipError{st.overflow == 2 ? "scan kernel: MIN/MAX lock timeout" : "scan kernel: group insert timeout"};
         if (slow_over) {        // too many records for the general kernel's list: rescan in chunks
@@ -1450,6 +1457,12 @@ cq_table* evaluate_query(cq_node* q) {
     cq_table* r = cqgpu_query(q, tables.data(), (int)tables.size());
     for (auto* t : tables) cqgpu_table_free(t);
     return r;
+}
+
+// profiling builds (-DCQ_CLOCKS): per-phase shader cycles of the last scan
+int cqgpu_debug_clocks(unsigned long long* out8) {
+    for (int i = 0; i < 8; i++) out8[i] = g_clk[i];
+    return 0;
 }
 
 int cqgpu_last_stats(cqgpu_stats* out) {

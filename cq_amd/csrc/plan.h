@@ -74,6 +74,7 @@ struct ScanStats {
     unsigned long long rows_emitted;
     unsigned int acc_classes[MAX_ACC];  // OR of value classes seen per accumulator (1 num, 2 str, 4 date)
     unsigned long long slow_records;    // records the fast field walk handed to the general parser
+    unsigned long long clk[8];          // profiling builds (CQ_CLOCKS): shader cycles per phase, summed over waves
 };
 
 // a MIN/MAX candidate published by one block (or wave) for one group

@@ -58,6 +58,7 @@ constexpr int LDS_BUDGET = 160 * 1024;       // LDS bytes per CU
 constexpr uint64_t NOPOS = ~0ULL;
 typedef uint32_t v4u __attribute__((ext_vector_type(4)));   // one 16-byte load
 static_assert(TILE16 % SCAN_T == 0, "tile loads split evenly over the block");
+static_assert(PF == 2, "a lane stages exactly the 32 bytes it classifies");
 static_assert(NW == SCAN_T, "one mask word per lane");
 
 // The plan and the table descriptor live in constant memory (written on the
@@ -87,16 +88,23 @@ __device__ __forceinline__ uint32_t lt_bytes(uint32_t x, uint32_t rep_n) {
     return ~((x | 0x80808080u) - rep_n) & ~x & 0x80808080u;
 }
 
+// inclusive prefix sum over a wave with DPP row shifts and row broadcasts
+// (no LDS round trips, unlike shuffles)
+__device__ __forceinline__ uint32_t wave_incl_scan(uint32_t x) {
+    x += (uint32_t)__builtin_amdgcn_update_dpp(0, (int)x, 0x111, 0xf, 0xf, true);   // row_shr:1
+    x += (uint32_t)__builtin_amdgcn_update_dpp(0, (int)x, 0x112, 0xf, 0xf, true);   // row_shr:2
+    x += (uint32_t)__builtin_amdgcn_update_dpp(0, (int)x, 0x114, 0xf, 0xf, true);   // row_shr:4
+    x += (uint32_t)__builtin_amdgcn_update_dpp(0, (int)x, 0x118, 0xf, 0xf, true);   // row_shr:8
+    x += (uint32_t)__builtin_amdgcn_update_dpp(0, (int)x, 0x142, 0xa, 0xf, false);  // row_bcast:15
+    x += (uint32_t)__builtin_amdgcn_update_dpp(0, (int)x, 0x143, 0xc, 0xf, false);  // row_bcast:31
+    return x;
+}
+
 // block-wide exclusive scan of two values per thread (SCAN_T threads)
 __device__ __forceinline__ void block_excl_scan2(uint32_t a, uint32_t b, uint32_t* wsum, uint32_t& ea,
                                                  uint32_t& eb, uint32_t& ta, uint32_t& tb) {
     const int lane = threadIdx.x & 63, wid = threadIdx.x >> 6;
-    uint32_t x = a, y = b;
-#pragma unroll
-    for (int o = 1; o < 64; o <<= 1) {
-        const uint32_t u = __shfl_up(x, o, 64), v = __shfl_up(y, o, 64);
-        if (lane >= o) { x += u; y += v; }
-    }
+    const uint32_t x = wave_incl_scan(a), y = wave_incl_scan(b);
     if (lane == 63) { wsum[wid] = x; wsum[16 + wid] = y; }
     lds_barrier();
     uint32_t ba = 0, bb = 0, sa = 0, sb = 0;
@@ -713,6 +721,53 @@ __device__ __forceinline__ int fast_field(const uint8_t* tile, uint32_t to, uint
     return FF_OK;
 }
 
+// 64-bit SWAR byte tests (0x80 in the matching bytes; no carries or borrows
+// cross bytes, so 64-bit adds/subs are exact)
+constexpr uint64_t H80 = 0x8080808080808080ULL, L7F = 0x7F7F7F7F7F7F7F7FULL, B01 = 0x0101010101010101ULL;
+__device__ __forceinline__ uint64_t nz64(uint64_t t) { return (((t & L7F) + L7F) | t) & H80; }
+__device__ __forceinline__ uint64_t lt64(uint64_t x, uint64_t rep) { return ~((x | H80) - rep) & ~x & H80; }
+__device__ __forceinline__ uint64_t spread64(uint64_t f) { return f | (f - (f >> 7)); }
+
+// The common short fields in one straight pass: 1-8 bytes, no byte <= ' ', not
+// signed, and -- when digit-led -- at most 7 bytes (so never date-shaped).
+// Returns false when the field is not of that kind (fast_field decides then).
+// On true, `out` is the cell and `w` the field bytes zero-padded (the inline
+// group key of a STRING).
+__device__ __forceinline__ bool lean_field(const uint8_t* tile, uint32_t to, uint32_t len, bool num_ok, Cell& out,
+                                           uint64_t& w) {
+    if (len == 0 || len > 8) return false;
+    uint32_t d0, d1;
+    load8(tile, to, d0, d1);
+    const uint64_t k = len == 8 ? ~0ULL : ((1ULL << (8 * len)) - 1);
+    w = ((uint64_t)d0 | ((uint64_t)d1 << 32)) & k;
+    const uint64_t f = k & H80;
+    const uint32_t c0 = d0 & 0xffu;
+    const bool numlead = is_digit(c0) || c0 == '.';
+    if ((lt64(w | ~k, 0x21 * B01) != 0) | (c0 == '-') | (c0 == '+') | (numlead && (len == 8 || !num_ok))) return false;
+    if (numlead) {
+        const uint64_t dig = lt64(w ^ (0x30 * B01), 0x0A * B01) & f;
+        const uint64_t dot = ~nz64(w ^ (0x2E * B01)) & f;
+        const uint32_t ndot = (uint32_t)__popcll(dot);
+        if ((f & ~dig & ~dot) == 0 && dig != 0 && ndot <= 1) {
+            uint64_t v = (w ^ (0x30 * B01)) & spread64(dig);
+            const uint32_t p = (uint32_t)__builtin_ctzg(dot, 64) >> 3;   // dot byte (8: none)
+            if (ndot) {
+                const uint64_t m = (1ULL << (8 * p)) - 1;                 // p <= 6
+                v = (v & m) | ((v >> 8) & ~m);
+            }
+            v <<= 8 * (8 - (len - ndot));
+            const uint64_t W = dig8(v);
+            if (!ndot) out = cell_int((int64_t)W);
+            else out = cell_dbl((double)W / pow10_exact(len - 1 - p));  // exact operands: correctly rounded
+            return true;
+        }
+    }
+    out.kind = K_STR;                 // STRING: no blank or NUL, so already what trim_whitespace gives
+    out.len = len;
+    out.bits = 0;                     // caller sets the address
+    return true;
+}
+
 // ------------------------------------------------------------------ the scan kernel
 __device__ __forceinline__ uint8_t* carve(uint8_t*& q, size_t bytes) {
     uint8_t* r = q;
@@ -724,23 +779,22 @@ __device__ __forceinline__ uint8_t* carve(uint8_t*& q, size_t bytes) {
 __device__ __forceinline__ void prefetch(const uint8_t* g, uint64_t ws, v4u* pf) {
     const v4u* src = (const v4u*)(g + ws - PREB);
 #pragma unroll
-    for (int j = 0; j < PF; j++) {
+    for (int j = 0; j < PF; j++) {   // lane t: the 32 bytes it classifies, [32t, 32t + 32)
 #ifdef CQ_PLAIN_LOADS
-        pf[j] = src[threadIdx.x + j * SCAN_T];
+        pf[j] = src[PF * threadIdx.x + j];
 #else
-        pf[j] = __builtin_nontemporal_load(src + threadIdx.x + j * SCAN_T);
+        pf[j] = __builtin_nontemporal_load(src + PF * threadIdx.x + j);
 #endif
     }
 }
 
 // classify LB = 32 staged bytes: terminator and separator masks, quote presence
-__device__ __forceinline__ void classify32(const uint8_t* p, uint32_t rep_d, uint32_t rep_q, uint32_t& nlm,
+__device__ __forceinline__ void classify32(const v4u a, const v4u b, uint32_t rep_d, uint32_t rep_q, uint32_t& nlm,
                                            uint32_t& sepm, bool& has_q) {
-    const v4u* src = (const v4u*)p;
     uint32_t nl = 0, sp = 0, qacc = 0x80808080u;
 #pragma unroll
     for (int v = 0; v < 2; v++) {
-        const v4u x4 = src[v];
+        const v4u x4 = v ? b : a;
 #pragma unroll
         for (int j = 0; j < 4; j++) {
             const uint32_t x = x4[j];
@@ -766,6 +820,17 @@ __device__ __forceinline__ uint32_t popc_below(uint32_t m, uint32_t b) {
     return (uint32_t)__popc(m & ((1u << b) - 1));
 }
 
+
+// Profiling builds (-DCQ_CLOCKS): per-phase shader cycles, summed over waves
+#ifdef CQ_CLOCKS
+#define CLK_DECL uint64_t clk_acc[8] = {0, 0, 0, 0, 0, 0, 0, 0}; uint64_t clk_t = clock64();
+#define CLK(i) { const uint64_t n_ = clock64(); clk_acc[i] += n_ - clk_t; clk_t = n_; }
+#define CLK_FLUSH(st) if ((threadIdx.x & 63) == 0) { for (int i_ = 0; i_ < 8; i_++) atomicAdd(&(st)->clk[i_], clk_acc[i_]); }
+#else
+#define CLK_DECL
+#define CLK(i)
+#define CLK_FLUSH(st)
+#endif
 
 // WHERE shapes the fast kernel is specialised for
 enum : int { W_NONE = 0, W_SIMPLE = 1, W_VM = 2 };
@@ -886,15 +951,19 @@ __global__ __launch_bounds__(SCAN_T) void scan_kernel(const uint8_t* __restrict_
     v4u pf[PF];
     uint64_t w = first_win + blockIdx.x;
     if (w < last_win) prefetch(g, w * WSTRIDE, pf);
+    CLK_DECL
 
     for (uint32_t iter = 0; w < last_win; w += gridDim.x, iter++) {
         const uint64_t ws = w * WSTRIDE;
         const uint64_t gt0 = (uint64_t)(uintptr_t)(g + ws - PREB);   // HBM address of tile byte 0
         lds_barrier();                                   // previous window fully consumed
+        CLK(0)
 #pragma unroll
-        for (int j = 0; j < PF; j++) ((v4u*)tile)[tid + j * SCAN_T] = pf[j];
+        for (int j = 0; j < PF; j++) ((v4u*)tile)[PF * tid + j] = pf[j];
+        const v4u own0 = pf[0], own1 = pf[1];            // this lane's 32 bytes, still in registers
         lds_barrier();
         if (w + gridDim.x < last_win) prefetch(g, (w + gridDim.x) * WSTRIDE, pf);   // in flight meanwhile
+        CLK(1)
 
 #if defined(CQ_PROF_STAGE) && CQ_PROF_STAGE == 0   // profiling build: staging only
         if (tid == 0) my_records += ((const uint32_t*)tile)[w & 1023];
@@ -903,7 +972,7 @@ __global__ __launch_bounds__(SCAN_T) void scan_kernel(const uint8_t* __restrict_
         // ---- classify this lane's LB bytes
         uint32_t nlm, sepm;
         bool hq;
-        classify32(tile + tid * LB, rep_d, rep_q, nlm, sepm, hq);
+        classify32(own0, own1, rep_d, rep_q, nlm, sepm, hq);
         // ---- record starts owned by this window: [ws, ws + WSTRIDE) within [lo_ok, hi_ok)
         uint32_t starts = 0;
         if (tid > 0) {
@@ -919,6 +988,7 @@ __global__ __launch_bounds__(SCAN_T) void scan_kernel(const uint8_t* __restrict_
                 if (base + LB > hi) starts &= (1u << (hi - base)) - 1;
             }
         }
+        CLK(2)
         // ---- number separators, terminators, records and quote words
         const uint32_t nsep = (uint32_t)__popc(sepm), nnl = (uint32_t)__popc(nlm);
         const uint32_t nrs = (uint32_t)__popc(starts);
@@ -949,6 +1019,7 @@ __global__ __launch_bounds__(SCAN_T) void scan_kernel(const uint8_t* __restrict_
             }
         }
 #endif
+        CLK(3)
         for (uint32_t chunk = 0; chunk < total; chunk += RSMAX) {
             {
                 uint32_t m = starts;
@@ -995,7 +1066,15 @@ __global__ __launch_bounds__(SCAN_T) void scan_kernel(const uint8_t* __restrict_
                     if (!fail && j0 + c <= jn) {                   // the record has column c
                         const uint32_t fs = c ? (uint32_t)E[j0 + c - 1] + 1 : pos;
                         const uint32_t fe = E[j0 + c];
-                        fail = fast_field(tile, fs, fe - fs, num_ok, k == gslot, cell, key) != FF_OK;
+                        uint64_t kw;
+                        if (lean_field(tile, fs, fe - fs, num_ok, cell, kw)) {
+                            if (k == gslot) {
+                                if (cell.kind == K_STR) { key.cls = GK_STR; key.len = cell.len; key.w0 = kw; key.w1 = 0; }
+                                else key = group_key(cell);
+                            }
+                        } else {
+                            fail = fast_field(tile, fs, fe - fs, num_ok, k == gslot, cell, key) != FF_OK;
+                        }
                         if (cell.kind == K_STR) cell.bits = tile_g + fs;
                         fend = fe;
                     }
@@ -1007,6 +1086,7 @@ __global__ __launch_bounds__(SCAN_T) void scan_kernel(const uint8_t* __restrict_
                 }
                 // a quote before the end of the last typed field may hide separators
                 fail = fail || QP[fend / LB + 1] != QP[pos / LB];
+                CLK(4)
                 // -- records the fast path declines go to slow_kernel, whole
                 const bool slow = valid && fail;
                 const uint64_t sb = __ballot(slow);
@@ -1135,11 +1215,14 @@ __global__ __launch_bounds__(SCAN_T) void scan_kernel(const uint8_t* __restrict_
                         }
                     }
                 }
+                CLK(5)
             }
             lds_barrier();
+            CLK(6)
         }
     }
     __syncthreads();
+    CLK_FLUSH(stats)
 
     // ---- statistics and value-class masks
     {

@@ -101,6 +101,9 @@ cq_table* cqgpu_debug_scan_cells(cqgpu_table* t, const int* cols, int ncols,
 /* Planner check without a device: compile `query_ast` against a header line and
  * describe the plan (or why it is not GPU-eligible) into `out`. */
 int cqgpu_explain(cq_node* query_ast, const char* header, cq_csv_config cfg, char* out, size_t cap);
+/* profiling builds (-DCQ_CLOCKS): shader cycles per scan phase of the last scan,
+ * summed over waves (all zero in the normal build) */
+int cqgpu_debug_clocks(unsigned long long* out8);
 
 /* Optional fallback for plans outside the GPU subset: the reference evaluator
  * compiled with evaluate_query renamed.  Without one, such
