@@ -856,8 +856,8 @@ __global__ __launch_bounds__(SCAN_T) void scan_kernel(const uint8_t* __restrict_
     uint16_t* E = (uint16_t*)carve(q, ECAP * 2);         // tile positions of separators
     uint16_t* NLI = (uint16_t*)carve(q, NLCAP * 2);      // separator index of each terminator
     uint16_t* QP = (uint16_t*)carve(q, (NW + 1) * 2);    // quote words before each mask word
-    uint32_t* rs = (uint32_t*)carve(q, RSMAX * 4);       // record: tile position | first separator << 16
-    uint16_t* rq = (uint16_t*)carve(q, RSMAX * 2);       // record: terminators before it
+    uint64_t* rs = (uint64_t*)carve(q, RSMAX * 8);       // record: tile position | first separator << 16
+                                                         //         | terminators before it << 32
     uint32_t* wsum = (uint32_t*)carve(q, 32 * 4);
     Cell* kc = (Cell*)carve(q, MAX_CONST * sizeof(Cell)); // literal cells, strings staged in LDS
     uint8_t* kstr = carve(q, KSTR);
@@ -956,13 +956,18 @@ __global__ __launch_bounds__(SCAN_T) void scan_kernel(const uint8_t* __restrict_
     for (uint32_t iter = 0; w < last_win; w += gridDim.x, iter++) {
         const uint64_t ws = w * WSTRIDE;
         const uint64_t gt0 = (uint64_t)(uintptr_t)(g + ws - PREB);   // HBM address of tile byte 0
-        lds_barrier();                                   // previous window fully consumed
+        // (no barrier here: the previous window's last reads of the tile and its
+        //  indexes are behind its end-of-chunk barrier or its scan barrier)
         CLK(0)
 #pragma unroll
         for (int j = 0; j < PF; j++) ((v4u*)tile)[PF * tid + j] = pf[j];
         const v4u own0 = pf[0], own1 = pf[1];            // this lane's 32 bytes, still in registers
         lds_barrier();
+#ifdef CQ_NO_MEM   // profiling build: re-read the block's first tile (L2-resident), results wrong
+        if (w + gridDim.x < last_win) prefetch(g, (first_win + blockIdx.x) * WSTRIDE, pf);
+#else
         if (w + gridDim.x < last_win) prefetch(g, (w + gridDim.x) * WSTRIDE, pf);   // in flight meanwhile
+#endif
         CLK(1)
 
 #if defined(CQ_PROF_STAGE) && CQ_PROF_STAGE == 0   // profiling build: staging only
@@ -1028,8 +1033,8 @@ __global__ __launch_bounds__(SCAN_T) void scan_kernel(const uint8_t* __restrict_
                     const uint32_t b = (uint32_t)__builtin_ctzg(m, 32);
                     m &= m - 1;
                     if (ri >= chunk && ri < chunk + RSMAX) {
-                        rs[ri - chunk] = (tid * LB + b) | ((sep_base + popc_below(sepm, b)) << 16);
-                        rq[ri - chunk] = (uint16_t)(nl_base + popc_below(nlm, b));
+                        rs[ri - chunk] = (uint64_t)((tid * LB + b) | ((sep_base + popc_below(sepm, b)) << 16)) |
+                                         ((uint64_t)(nl_base + popc_below(nlm, b)) << 32);
                     }
                     ri++;
                 }
@@ -1045,9 +1050,9 @@ __global__ __launch_bounds__(SCAN_T) void scan_kernel(const uint8_t* __restrict_
                 // trip count is block-uniform: every lane of a wave runs every trip
                 const uint32_t ri = base0 + tid;
                 const bool valid = ri < nrec;
-                const uint32_t ent = valid ? rs[ri] : 0;
-                const uint32_t pos = ent & 0xFFFF, j0 = ent >> 16;
-                const uint32_t qi = valid ? rq[ri] : 0;
+                const uint64_t ent = valid ? rs[ri] : 0;
+                const uint32_t pos = (uint32_t)ent & 0xFFFF, j0 = ((uint32_t)ent) >> 16;
+                const uint32_t qi = (uint32_t)(ent >> 32);
                 const uint64_t rec = ws - PREB + pos;
                 CellsT<KN> cs;
                 Cell wc = cell_null();
@@ -1533,7 +1538,7 @@ static size_t lds_slot_bytes(const cq::ScanPlan* P) {
 static size_t lds_fixed_bytes() {
     auto r16 = [](size_t x) { return (x + 15) & ~(size_t)15; };
     return r16(cq::TILE + cq::TILE_PAD) + r16(cq::ECAP * 2) + r16(cq::NLCAP * 2) + r16((cq::NW + 1) * 2) +
-           r16(cq::RSMAX * 4) + r16(cq::RSMAX * 2) + r16(32 * 4) + r16(cq::MAX_CONST * sizeof(cq::Cell)) +
+           r16(cq::RSMAX * 8) + r16(32 * 4) + r16(cq::MAX_CONST * sizeof(cq::Cell)) +
            r16(cq::KSTR);
 }
 
