@@ -46,6 +46,10 @@ hipError_t cq_launch_copy_strings(const Cell* cells, uint32_t n, const unsigned 
                                   uint8_t* out, hipStream_t s);
 hipError_t cq_launch_parse_literals(const uint8_t* text, const unsigned int* offs,
                                     const unsigned int* lens, uint32_t n, Cell* out, hipStream_t s);
+hipError_t cq_launch_project(const uint8_t* g, const unsigned long long* recs, uint32_t nrec,
+                             const ProjDesc* D, Cell* scratch, Cell* out, hipStream_t s);
+hipError_t cq_sort_offsets(void* temp, size_t* temp_bytes, const unsigned long long* in,
+                           unsigned long long* out, size_t n, int bits, hipStream_t s);
 }
 
 // reference evaluator.c:23
@@ -125,6 +129,17 @@ void* workspace(DevCtx& c, size_t bytes) {
     }
     return c.ws;
 }
+
+// owned device allocation
+struct DevBuf {
+    void* p = nullptr;
+    DevBuf() = default;
+    explicit DevBuf(size_t bytes) { HIPCHECK(hipMalloc(&p, std::max<size_t>(bytes, 256))); }
+    DevBuf(const DevBuf&) = delete;
+    DevBuf& operator=(const DevBuf&) = delete;
+    ~DevBuf() { if (p) (void)hipFree(p); }
+    template <class T> T* as() const { return (T*)p; }
+};
 
 void* pinned(DevCtx& c, size_t bytes) {
     if (bytes > c.pinned_size) {
@@ -380,17 +395,19 @@ struct Compiler {
     Compiled& C;
     std::vector<Insn> code;
     int depth = 0, bdepth = 0;
+    int need_cap = MAX_NEED;         // distinct columns one plan may reference
+    int lit_cap = MAX_CONST;
 
     int need(int col) {
         auto it = std::find(C.need_cols.begin(), C.need_cols.end(), col);
         if (it != C.need_cols.end()) return (int)(it - C.need_cols.begin());
-        if ((int)C.need_cols.size() >= MAX_NEED) throw Ineligible{"more than 8 referenced columns"};
+        if ((int)C.need_cols.size() >= need_cap) throw Ineligible{"more than 8 referenced columns"};
         C.need_cols.push_back(col);
         return (int)C.need_cols.size() - 1;
     }
     int lit(const char* text) {
         C.lits.push_back(text ? text : "");
-        if ((int)C.lits.size() > MAX_CONST) throw Ineligible{"too many literals"};
+        if ((int)C.lits.size() > lit_cap) throw Ineligible{"too many literals"};
         return (int)C.lits.size() - 1;
     }
     void emit(uint8_t op, int a = 0, int b = 0) {
@@ -482,7 +499,7 @@ struct Compiler {
             }
             default:
                 throw Ineligible{"expression kind " + std::to_string(e->kind) +
-                                 " (function/CASE/subquery) in WHERE"};
+                                 " (function/CASE/subquery)"};
         }
     }
 
@@ -595,6 +612,39 @@ std::string agg_display_name(const char* cs) {
     return std::string(dot ? dot + 1 : cs);
 }
 
+// order the need slots by column so one left-to-right pass parses them all,
+// and fill the table-dependent plan fields
+void finish_plan(const cqgpu_table* t, Compiled& C, Compiler& cc) {
+    std::vector<int> order(C.need_cols.size());
+    for (size_t i = 0; i < order.size(); i++) order[i] = (int)i;
+    std::sort(order.begin(), order.end(), [&](int a, int b) { return C.need_cols[a] < C.need_cols[b]; });
+    std::vector<int> remap(order.size());
+    for (size_t i = 0; i < order.size(); i++) remap[order[i]] = (int)i;
+    std::vector<int> sorted(order.size());
+    for (size_t i = 0; i < order.size(); i++) sorted[remap[i]] = C.need_cols[i];
+    C.P.nneed = (int)sorted.size();
+    for (int i = 0; i < C.P.nneed; i++) C.P.need_col[i] = (int16_t)sorted[i];
+    C.P.max_col = C.P.nneed ? sorted.back() : -1;
+    for (auto& in : cc.code) {
+        if (in.op == OP_COL) {
+            auto it = std::find(C.need_cols.begin(), C.need_cols.end(), (int)in.b);
+            in.a = (uint8_t)remap[it - C.need_cols.begin()];
+        }
+    }
+    for (int a = 0; a < C.P.nacc; a++) C.P.acc[a].slot = (uint8_t)remap[C.P.acc[a].slot];
+    if (C.P.group_slot >= 0) C.P.group_slot = remap[C.P.group_slot];
+    C.need_cols = sorted;
+    C.P.nprog = (int)cc.code.size();
+    std::copy(cc.code.begin(), cc.code.end(), C.P.prog);
+    C.P.nconst = (int)C.lits.size();
+    C.P.delim = (uint8_t)t->cfg.delimiter;
+    C.P.quote = (uint8_t)t->cfg.quote;
+    C.P.n = t->n;
+    C.P.data_begin = t->data_begin;
+    C.P.range_begin = 0;
+    C.P.range_end = t->n;
+}
+
 // compile the aggregate SELECT (evaluator.c:69-258 + build_aggregated_result)
 void compile_aggregate(const cqgpu_table* t, cq_node* q, Compiled& C) {
     memset(&C.P, 0, sizeof C.P);
@@ -679,35 +729,7 @@ void compile_aggregate(const cqgpu_table* t, cq_node* q, Compiled& C) {
         else oc.rep = (int)(it - C.rep_cols.begin());
         C.outs.push_back(oc);
     }
-    // order the need slots by column so one left-to-right pass parses them all
-    std::vector<int> order(C.need_cols.size());
-    for (size_t i = 0; i < order.size(); i++) order[i] = (int)i;
-    std::sort(order.begin(), order.end(), [&](int a, int b) { return C.need_cols[a] < C.need_cols[b]; });
-    std::vector<int> remap(order.size());
-    for (size_t i = 0; i < order.size(); i++) remap[order[i]] = (int)i;
-    std::vector<int> sorted(order.size());
-    for (size_t i = 0; i < order.size(); i++) sorted[remap[i]] = C.need_cols[i];
-    C.P.nneed = (int)sorted.size();
-    for (int i = 0; i < C.P.nneed; i++) C.P.need_col[i] = (int16_t)sorted[i];
-    C.P.max_col = C.P.nneed ? sorted.back() : -1;
-    for (auto& in : cc.code) {
-        if (in.op == OP_COL) {
-            auto it = std::find(C.need_cols.begin(), C.need_cols.end(), (int)in.b);
-            in.a = (uint8_t)remap[it - C.need_cols.begin()];
-        }
-    }
-    for (int a = 0; a < C.P.nacc; a++) C.P.acc[a].slot = (uint8_t)remap[C.P.acc[a].slot];
-    if (C.P.group_slot >= 0) C.P.group_slot = remap[C.P.group_slot];
-    C.need_cols = sorted;
-    C.P.nprog = (int)cc.code.size();
-    std::copy(cc.code.begin(), cc.code.end(), C.P.prog);
-    C.P.nconst = (int)C.lits.size();
-    C.P.delim = (uint8_t)t->cfg.delimiter;
-    C.P.quote = (uint8_t)t->cfg.quote;
-    C.P.n = t->n;
-    C.P.data_begin = t->data_begin;
-    C.P.range_begin = 0;
-    C.P.range_end = t->n;
+    finish_plan(t, C, cc);
 }
 
 // ------------------------------------------------------------------ host groups
@@ -757,12 +779,17 @@ struct Reader {
 // literal cells parsed on the device with the same parser as the data
 struct Literals {
     uint8_t* dev = nullptr;
+    Cell* dcells = nullptr;           // device copy of `cells`
     std::vector<Cell> cells;
     ~Literals() { if (dev) (void)hipFree(dev); }
 };
 
 void parse_literals(DevCtx& c, const std::vector<std::string>& texts, Literals& L) {
     size_t n = texts.size();
+    if (L.dev) HIPCHECK(hipFree(L.dev));
+    L.dev = nullptr;
+    L.dcells = nullptr;
+    L.cells.clear();
     if (!n) return;
     std::vector<unsigned int> offs(n), lens(n);
     std::string blob;
@@ -782,6 +809,7 @@ void parse_literals(DevCtx& c, const std::vector<std::string>& texts, Literals& 
     HIPCHECK(hipMemcpyAsync(doffs, offs.data(), n * 4, hipMemcpyHostToDevice, c.stream));
     HIPCHECK(hipMemcpyAsync(dlens, lens.data(), n * 4, hipMemcpyHostToDevice, c.stream));
     HIPCHECK(cq_launch_parse_literals(dtext, doffs, dlens, (uint32_t)n, dcells, c.stream));
+    L.dcells = dcells;
     L.cells.resize(n);
     HIPCHECK(hipMemcpyAsync(L.cells.data(), dcells, n * sizeof(Cell), hipMemcpyDeviceToHost, c.stream));
     HIPCHECK(hipStreamSynchronize(c.stream));
@@ -850,8 +878,11 @@ double now_ms() {
 }
 
 // run the fused scan (with regrowth on overflow) and return the groups
+// row_out (optional): offsets of the records passing WHERE, unordered; entries
+// past row_cap are counted in ScanStats.rows_emitted but not written
 std::vector<HGroup> run_aggregate(DevCtx& c, const cqgpu_table* t, Compiled& C, Literals& L,
-                                  ScanStats* stats_out) {
+                                  ScanStats* stats_out, unsigned long long* row_out = nullptr,
+                                  unsigned long long row_cap = 0) {
     parse_literals(c, C.lits, L);
     for (size_t i = 0; i < L.cells.size(); i++) C.P.consts[i] = L.cells[i];
     std::vector<HGroup> groups;
@@ -878,7 +909,9 @@ std::vector<HGroup> run_aggregate(DevCtx& c, const cqgpu_table* t, Compiled& C, 
             const uint64_t wins = (P.range_end - P.range_begin + 31679) / 31680 + 1;
             const int g2 = chunk ? (int)std::min<uint64_t>(grid, wins) : grid;
             HIPCHECK(hipEventRecord(c.ev0, c.stream));
-            HIPCHECK(cq_launch_scan(t->g, &P, &A.gt, A.stats, nullptr, 0, grouped, g2, c.stream, nullptr,
+            const unsigned long long done = st.rows_emitted;
+            HIPCHECK(cq_launch_scan(t->g, &P, &A.gt, A.stats, row_out ? row_out + std::min(done, row_cap) : nullptr,
+                                    row_cap > done ? row_cap - done : 0, grouped, g2, c.stream, nullptr,
                                     A.slow_list, A.slow_cap));
             HIPCHECK(hipEventRecord(c.ev1, c.stream));
             ScanStats s1;
@@ -1294,13 +1327,199 @@ void apply_limit(cq_table* r, int limit, int offset) {    // apply_limit_offset 
     r->nrows = cnt;
 }
 
-void post_ops(DevCtx& c, cq_table* res, cq_node* q) {
+void post_ops(DevCtx& c, cq_table* res, cq_node* q, bool rows = false, bool limited = false) {
     cq_node* sel = q->u.q.select;
-    if (q->u.q.having) apply_having(c, res, q->u.q.having, sel);
+    if (q->u.q.having && !rows) apply_having(c, res, q->u.q.having, sel);   // grouped paths only
     cq_node* ob = q->u.q.order_by;
     if (ob && ob->kind == CQ_N_ORDER_BY && ob->u.ord.key) sort_result(res, sel, ob->u.ord.key, ob->u.ord.desc);
     if (sel && sel->u.sel.distinct) apply_distinct(res);
-    apply_limit(res, q->u.q.limit, q->u.q.offset);
+    if (!limited) apply_limit(res, q->u.q.limit, q->u.q.offset);
+}
+
+// ------------------------------------------------------------------ row-returning SELECT
+// projection of build_result (evaluator_utils.c:249-549): one program per output
+// column; `*` expands to every table column (:263-295), other items evaluate their
+// AST node with evaluate_expression (:345-371, :502-506)
+struct RowPlan {
+    std::vector<std::string> names;
+    std::vector<int> cols;            // CSV columns parsed per record, ascending
+    std::vector<Insn> code;           // OP_COL b = index into cols
+    std::vector<uint32_t> off;        // program k = code[off[k], off[k+1])
+    std::vector<std::string> lits;
+};
+
+std::string row_display_name(const char* cs) {
+    const char* as = ci_find(cs, " AS ");
+    if (as) return std::string(as + 4);                       // extract_column_alias (:57-63)
+    if (strchr(cs, '(')) return std::string(cs);
+    const char* dot = strchr(cs, '.');
+    return std::string(dot ? dot + 1 : cs);
+}
+
+void compile_rows(const cqgpu_table* t, cq_node* q, Compiled& C, RowPlan& R) {
+    memset(&C.P, 0, sizeof C.P);
+    const char* alias = (q->u.q.from && q->u.q.from->u.from.alias) ? q->u.q.from->u.from.alias : "main";
+    Compiler cc{t, q, alias, C};
+    if (q->u.q.where) cc.cond(q->u.q.where);
+    C.P.group_slot = -1;
+    finish_plan(t, C, cc);
+    cq_node* sel = q->u.q.select;
+    R.off.push_back(0);
+    if (!sel || sel->kind != CQ_N_SELECT) return;         // build_result: no SELECT -> no columns
+    Compiled PC;
+    Compiler pc{t, q, alias, PC};
+    pc.need_cap = 32767;
+    pc.lit_cap = 1 << 20;
+    bool star = false;
+    for (int i = 0; i < sel->u.sel.count; i++)
+        if (sel->u.sel.texts[i] && !strcmp(sel->u.sel.texts[i], "*")) star = true;
+    auto close = [&]() {
+        R.code.insert(R.code.end(), pc.code.begin(), pc.code.end());
+        R.off.push_back((uint32_t)R.code.size());
+        pc.code.clear();
+        pc.depth = 0;
+    };
+    for (int i = 0; i < sel->u.sel.count; i++) {
+        const char* cs = sel->u.sel.texts[i] ? sel->u.sel.texts[i] : "";
+        if (star && !strcmp(cs, "*")) {
+            for (int j = 0; j < (int)t->names.size(); j++) {
+                R.names.push_back(t->names[j]);
+                pc.need(j);
+                pc.emit(OP_COL, 0, j);
+                close();
+            }
+            continue;
+        }
+        R.names.push_back(row_display_name(cs));
+        cq_node* node = sel->u.sel.exprs ? sel->u.sel.exprs[i] : nullptr;
+        if (node) {
+            pc.expr(node);                                     // throws on subquery/window/function
+        } else {
+            // evaluate_column_expression (:194-246) on the spec text
+            std::string cn = cs;
+            const char* as = ci_find(cs, " AS ");
+            if (as) cn.assign(cs, (size_t)(as - cs));
+            if (cn.find('(') != std::string::npos) throw Ineligible{"scalar function in SELECT"};
+            int col = col_index_fallback(t, cn.c_str());
+            if (col >= 0) { pc.need(col); pc.emit(OP_COL, 0, col); }
+            else pc.emit(OP_NULLV);
+        }
+        close();
+    }
+    // parse the referenced columns in one ascending pass; OP_COL b -> position
+    R.cols = PC.need_cols;
+    std::sort(R.cols.begin(), R.cols.end());
+    for (auto& in : R.code)
+        if (in.op == OP_COL)
+            in.b = (uint16_t)(std::lower_bound(R.cols.begin(), R.cols.end(), (int)in.b) - R.cols.begin());
+    R.lits = PC.lits;
+}
+
+// convert projected device cells of `n` rows into result rows [at, at + n)
+void append_rows(DevCtx& c, cq_table* r, int at, const std::vector<Cell>& cells, int nout, int n) {
+    std::vector<HCell> h = fetch_cells(c, cells);
+    for (int i = 0; i < n; i++) {
+        cq_row& row = r->rows[at + i];
+        row.ncols = nout;
+        row.values = (cq_value*)calloc(std::max(nout, 1), sizeof(cq_value));
+        for (int k = 0; k < nout; k++) row.values[k] = to_value(h[(size_t)i * nout + k]);
+    }
+}
+
+cq_table* run_rows(DevCtx& c, const cqgpu_table* t, Compiled& C, RowPlan& R, cq_node* q, bool* limited) {
+    const int nout = (int)R.names.size();
+    *limited = false;
+    // 1. scan: WHERE over every record, matching record offsets out (unordered)
+    Literals L;
+    ScanStats st;
+    // test knobs: CQGPU_ROW_CAP0 (first-pass offset capacity), CQGPU_ROW_BATCH (projection batch)
+    const char* cap_env = getenv("CQGPU_ROW_CAP0");
+    unsigned long long cap = std::min<unsigned long long>(t->n / 2 + 2, 1ull << 24);
+    if (cap_env && atoll(cap_env) > 0) cap = std::min<unsigned long long>(cap, (unsigned long long)atoll(cap_env));
+    DevBuf rows(cap * 8);
+    (void)run_aggregate(c, t, C, L, &st, rows.as<unsigned long long>(), cap);
+    if (st.rows_emitted > cap) {          // exact count known now: rescan into a buffer that fits
+        cap = st.rows_emitted;
+        DevBuf bigger(cap * 8);
+        std::swap(rows.p, bigger.p);
+        (void)run_aggregate(c, t, C, L, &st, rows.as<unsigned long long>(), cap);
+        if (st.rows_emitted != cap) throw HipError{"row scan: matching-row count changed between passes"};
+    }
+    const unsigned long long n = st.rows_emitted;
+    if (n > (unsigned long long)INT32_MAX) throw Ineligible{"more than 2^31-1 result rows"};
+    g_stats.groups = n;
+    // 2. file order: radix sort of the byte offsets
+    DevBuf sorted(n * 8);
+    if (n > 1) {
+        int bits = 1;
+        while (bits < 64 && (1ull << bits) <= t->n) bits++;
+        size_t tb = 0;
+        HIPCHECK(cq_sort_offsets(nullptr, &tb, rows.as<unsigned long long>(), sorted.as<unsigned long long>(), n,
+                                 bits, c.stream));
+        DevBuf temp(tb);
+        HIPCHECK(cq_sort_offsets(temp.p, &tb, rows.as<unsigned long long>(), sorted.as<unsigned long long>(), n,
+                                 bits, c.stream));
+    } else if (n == 1) {
+        HIPCHECK(hipMemcpyAsync(sorted.p, rows.p, 8, hipMemcpyDeviceToDevice, c.stream));
+    }
+    // LIMIT/OFFSET without ORDER BY or DISTINCT keeps a contiguous run of rows:
+    // project only that run (apply_limit_offset, evaluator_utils.c:703-733)
+    unsigned long long lo = 0, hi = n;
+    cq_node* sel = q->u.q.select;
+    cq_node* ob = q->u.q.order_by;
+    const bool ordered = ob && ob->kind == CQ_N_ORDER_BY && ob->u.ord.key;
+    const bool distinct = sel && sel->u.sel.distinct;
+    if (!ordered && !distinct && (q->u.q.limit >= 0 || q->u.q.offset >= 0)) {
+        const unsigned long long off = q->u.q.offset >= 0 ? (unsigned long long)q->u.q.offset : 0;
+        const unsigned long long lim = q->u.q.limit >= 0 ? (unsigned long long)q->u.q.limit : n;
+        lo = std::min(off, n);
+        hi = std::min(n, lo + lim);
+        *limited = true;
+    }
+    cq_table* r = new_result(R.names);
+    const int nr = (int)(hi - lo);
+    r->nrows = r->row_capacity = nr;
+    r->rows = (cq_row*)calloc(std::max(nr, 1), sizeof(cq_row));
+    if (!nr || !nout) {
+        for (int i = 0; i < nr; i++) { r->rows[i].ncols = nout; r->rows[i].values = (cq_value*)calloc(1, sizeof(cq_value)); }
+        return r;
+    }
+    // 3. projection on the device, in batches
+    Literals LP;
+    parse_literals(c, R.lits, LP);
+    const int ncols = (int)R.cols.size();
+    std::vector<int16_t> cols16(R.cols.begin(), R.cols.end());
+    DevBuf dcols(cols16.size() * 2), dcode(R.code.size() * sizeof(Insn)), doff(R.off.size() * 4);
+    if (!cols16.empty())
+        HIPCHECK(hipMemcpyAsync(dcols.p, cols16.data(), cols16.size() * 2, hipMemcpyHostToDevice, c.stream));
+    if (!R.code.empty())
+        HIPCHECK(hipMemcpyAsync(dcode.p, R.code.data(), R.code.size() * sizeof(Insn), hipMemcpyHostToDevice, c.stream));
+    HIPCHECK(hipMemcpyAsync(doff.p, R.off.data(), R.off.size() * 4, hipMemcpyHostToDevice, c.stream));
+    ProjDesc D;
+    D.cols = dcols.as<int16_t>();
+    D.code = dcode.as<Insn>();
+    D.off = doff.as<uint32_t>();
+    D.consts = LP.dcells;
+    D.ncols = ncols;
+    D.nout = nout;
+    D.delim = (uint8_t)t->cfg.delimiter;
+    D.quote = (uint8_t)t->cfg.quote;
+    const size_t per = (size_t)(ncols + nout) * sizeof(Cell);
+    int batch = (int)std::max<size_t>(1024, std::min<size_t>(1u << 20, (512u << 20) / per));
+    const char* batch_env = getenv("CQGPU_ROW_BATCH");
+    if (batch_env && atoi(batch_env) > 0) batch = std::min(batch, atoi(batch_env));
+    DevBuf scratch((size_t)batch * std::max(ncols, 1) * sizeof(Cell)), dout((size_t)batch * nout * sizeof(Cell));
+    std::vector<Cell> hcells;
+    for (int b = 0; b < nr; b += batch) {
+        const int m = std::min(batch, nr - b);
+        HIPCHECK(cq_launch_project(t->g, sorted.as<unsigned long long>() + lo + b, (uint32_t)m, &D,
+                                   scratch.as<Cell>(), dout.as<Cell>(), c.stream));
+        hcells.resize((size_t)m * nout);
+        HIPCHECK(hipMemcpyAsync(hcells.data(), dout.p, hcells.size() * sizeof(Cell), hipMemcpyDeviceToHost, c.stream));
+        HIPCHECK(hipStreamSynchronize(c.stream));
+        append_rows(c, r, b, hcells, nout, m);
+    }
+    return r;
 }
 
 // ------------------------------------------------------------------ query dispatch
@@ -1313,9 +1532,12 @@ void check_plan_shape(cq_node* q, const cqgpu_table* t) {
     char d = t->cfg.delimiter;
     if (d == '\n' || d == '\r' || is_space((unsigned char)d) || d == t->cfg.quote || d == 0)
         throw Ineligible{"whitespace/quote delimiter"};
+}
+
+bool is_row_query(cq_node* q) {      // evaluator.c:259-262: neither GROUP BY nor aggregates
     cq_node* gb = q->u.q.group_by;
     bool grouped = gb && gb->kind == CQ_N_GROUP_BY && gb->u.grp.keys && gb->u.grp.nkeys > 0;
-    if (!grouped && !has_aggregates(q->u.q.select)) throw Ineligible{"row-returning SELECT"};
+    return !grouped && !has_aggregates(q->u.q.select);
 }
 
 cq_table* query_impl(cq_node* q, cqgpu_table* const* tables, int ntables) {
@@ -1323,6 +1545,15 @@ cq_table* query_impl(cq_node* q, cqgpu_table* const* tables, int ntables) {
     if (ntables < 1 || !tables[0]) throw HipError{"no table"};
     const cqgpu_table* t = tables[0];
     check_plan_shape(q, t);
+    if (is_row_query(q)) {
+        Compiled C;
+        RowPlan R;
+        compile_rows(t, q, C, R);
+        bool limited = false;
+        cq_table* res = run_rows(c, t, C, R, q, &limited);
+        post_ops(c, res, q, true, limited);
+        return res;
+    }
     Compiled C;
     compile_aggregate(t, q, C);
     Literals L;
@@ -1483,8 +1714,30 @@ int cqgpu_explain(cq_node* q, const char* header, cq_csv_config cfg, char* out, 
         t.names = split_header(header, header + hl, cfg.delimiter, cfg.quote, cfg.has_header);
         check_plan_shape(q, &t);
         Compiled C;
+        std::string s;
+        if (is_row_query(q)) {
+            RowPlan R;
+            compile_rows(&t, q, C, R);
+            s = "rows\nneed:";
+            for (int i = 0; i < C.P.nneed; i++) s += " " + std::to_string(C.P.need_col[i]);
+            s += "\ncols:";
+            for (int cidx : R.cols) s += " " + std::to_string(cidx);
+            s += "\nnames:";
+            for (auto& n : R.names) s += " [" + n + "]";
+            s += "\nprogs:";
+            for (size_t k = 0; k + 1 < R.off.size(); k++) {
+                s += " [";
+                for (uint32_t i = R.off[k]; i < R.off[k + 1]; i++)
+                    s += (i > R.off[k] ? " " : "") + std::to_string(R.code[i].op) + "/" +
+                         std::to_string(R.code[i].a) + "/" + std::to_string(R.code[i].b);
+                s += "]";
+            }
+            s += "\n";
+            snprintf(out, cap, "%s", s.c_str());
+            return 0;
+        }
         compile_aggregate(&t, q, C);
-        std::string s = "need:";
+        s = "need:";
         for (int i = 0; i < C.P.nneed; i++) s += " " + std::to_string(C.P.need_col[i]);
         s += "\nprog:";
         for (int i = 0; i < C.P.nprog; i++)
@@ -1661,6 +1914,7 @@ size_t cqgpu_query_partial(cq_node* q, cqgpu_table* const* tables, int ntables, 
         if (ntables < 1 || !tables[0]) throw HipError{"no table"};
         const cqgpu_table* t = tables[0];
         check_plan_shape(q, t);
+        if (is_row_query(q)) throw Ineligible{"row-returning SELECT across partials"};
         Compiled C;
         compile_aggregate(t, q, C);
         Literals L;
@@ -1740,6 +1994,7 @@ cq_table* cqgpu_merge_partials(cq_node* q, const void* const* blobs, const size_
         cqgpu_table meta;
         meta.names = parts[0].names;
         check_plan_shape(q, &meta);
+        if (is_row_query(q)) throw Ineligible{"row-returning SELECT across partials"};
         Compiled C;
         compile_aggregate(&meta, q, C);
         if ((uint32_t)C.P.nacc != nacc || (uint32_t)C.rep_cols.size() != nrep)

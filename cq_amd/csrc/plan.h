@@ -64,6 +64,19 @@ struct ScanPlan {
     int32_t want_rows;     // 1: also emit matching record offsets (row-returning)
 };
 
+// projection of a row-returning SELECT (device pointers): ncols CSV columns
+// parsed per record (ascending), nout programs code[off[k], off[k+1])
+struct ProjDesc {
+    const int16_t* cols;
+    const Insn* code;
+    const uint32_t* off;
+    const Cell* consts;
+    int32_t ncols;
+    int32_t nout;
+    uint32_t delim;
+    uint32_t quote;
+};
+
 // scan statistics written by the kernel (one per launch)
 struct ScanStats {
     unsigned long long records;     // data records seen

@@ -237,21 +237,22 @@ __device__ __forceinline__ bool parse_record_regs(const Src& S, const ScanPlan& 
     return ended;
 }
 
-// the same from HBM into a global array (representative-row gather)
-__device__ void parse_record_out(const uint8_t* rec, const ScanPlan& P, Cell* out) {
+// parse_line restricted to an ascending column list, from HBM into a global
+// array (representative-row gather, projection); out[k * stride] = column cols[k]
+__device__ void parse_cols_out(const uint8_t* rec, const int16_t* cols, int ncols, uint32_t delim,
+                               uint32_t quote, Cell* out, uint64_t stride) {
     const Src S{rec, rec, 0, false};
-    const uint32_t delim = P.delim, quote = P.quote;
     uint32_t i = 0, fs = 0, flen = 0;
     int col = 0;
     bool ended = false;
-    for (int k = 0; k < P.nneed; k++) {
-        const int want = P.need_col[k];
+    for (int k = 0; k < ncols; k++) {
+        const int want = cols[k];
         Cell c = cell_null();
         while (!ended && col < want) {
             if (!g_field(S, i, delim, quote, fs, flen) || S.at(i) != delim) ended = true;
             else { i = i + 1; col++; }
         }
-        if (!ended) {
+        if (!ended && col == want) {
             if (!g_field(S, i, delim, quote, fs, flen)) {
                 ended = true;
             } else {
@@ -260,8 +261,12 @@ __device__ void parse_record_out(const uint8_t* rec, const ScanPlan& P, Cell* ou
                 else ended = true;
             }
         }
-        out[k] = c;
+        out[k * stride] = c;
     }
+}
+
+__device__ void parse_record_out(const uint8_t* rec, const ScanPlan& P, Cell* out) {
+    parse_cols_out(rec, P.need_col, P.nneed, P.delim, P.quote, out, 1);
 }
 
 // ------------------------------------------------------------------ predicate VM
@@ -816,6 +821,17 @@ __device__ __forceinline__ void classify32(const v4u a, const v4u b, uint32_t re
 }
 
 // bits of m below bit b
+// one counter atomic per wave: this lane's slot among the wave's lanes with `on`
+__device__ __forceinline__ unsigned long long wave_slot(bool on, unsigned long long* ctr) {
+    const uint64_t m = __ballot(on);
+    if (!m) return 0;
+    const uint32_t lane = threadIdx.x & 63, lead = (uint32_t)__builtin_ctzll(m);
+    unsigned long long base = 0;
+    if (lane == lead) base = atomicAdd(ctr, (unsigned long long)__popcll(m));
+    base = __shfl(base, (int)lead, 64);
+    return base + (unsigned long long)__popcll(m & ((1ull << lane) - 1));
+}
+
 __device__ __forceinline__ uint32_t popc_below(uint32_t m, uint32_t b) {
     return (uint32_t)__popc(m & ((1u << b) - 1));
 }
@@ -1114,9 +1130,9 @@ __global__ __launch_bounds__(SCAN_T) void scan_kernel(const uint8_t* __restrict_
                     else pass = P.nprog == 0 || eval_where_vm(P, kc, cs);
                     if (pass) my_pass++;
                 }
-                if (pass && row_out) {
-                    const unsigned long long slot = atomicAdd(&stats->rows_emitted, 1ULL);
-                    if (slot < row_cap) {
+                if (row_out) {
+                    const unsigned long long slot = wave_slot(pass, &stats->rows_emitted);
+                    if (pass && slot < row_cap) {
                         row_out[slot] = rec;
                         if (cells_out) {   // debug: the cells this kernel parsed
 #pragma unroll
@@ -1402,9 +1418,9 @@ __global__ __launch_bounds__(256) void slow_kernel(const uint8_t* __restrict__ g
             pass = P.nprog == 0 || eval_where_vm(P, P.consts, cs);
             if (pass) my_pass++;
         }
-        if (pass && row_out) {
-            const unsigned long long slot = atomicAdd(&stats->rows_emitted, 1ULL);
-            if (slot < row_cap) {
+        if (row_out) {
+            const unsigned long long slot = wave_slot(pass, &stats->rows_emitted);
+            if (pass && slot < row_cap) {
                 row_out[slot] = rec;
                 if (cells_out)
                     for (int k = 0; k < nneed; k++) cells_out[slot * nneed + k] = get_cell(cs, k, nneed);
@@ -1502,6 +1518,55 @@ __global__ void gather_kernel(const uint8_t* __restrict__ g,
     const uint32_t i = blockIdx.x * blockDim.x + threadIdx.x;
     if (i >= nrec) return;
     parse_record_out(g + recs[i], P, out + (uint64_t)i * P.nneed);
+}
+
+// ------------------------------------------------------------------ projection
+// evaluate_expression (evaluator_expressions.c:23-263) for one SELECT item of a
+// row-returning query (build_result, evaluator_utils.c:249-549): the program's
+// OP_COL operand b indexes the parsed columns of this record (cells[b * cstride])
+__device__ Cell eval_value(const Insn* code, uint32_t b, uint32_t e, const Cell* cells, uint64_t cstride,
+                           const Cell* consts) {
+    Stack st;
+#pragma unroll
+    for (int j = 0; j < 8; j++) st.s[j] = cell_null();
+    int sp = 0;
+    for (uint32_t pc = b; pc < e; pc++) {
+        const Insn in = code[pc];
+        switch (in.op) {
+            case OP_COL: st.set(sp++, cells[(uint64_t)in.b * cstride]); break;
+            case OP_CONST: st.set(sp++, consts[in.b]); break;
+            case OP_ARITH: {
+                Cell r = st.get(--sp), l = st.get(--sp);
+                st.set(sp++, arith(in.a, l, r));
+                break;
+            }
+            case OP_NEG: { Cell x = st.get(--sp); st.set(sp++, negate(x)); break; }
+            default: st.set(sp++, cell_null()); break;
+        }
+    }
+    return sp > 0 ? st.get(sp - 1) : cell_null();
+}
+
+// one thread per matching record: parse the referenced columns (column-major
+// scratch), then evaluate every output program into out[row * nout + o]
+__global__ __launch_bounds__(256) void project_kernel(const uint8_t* __restrict__ g,
+                                                      const unsigned long long* __restrict__ recs, uint32_t nrec,
+                                                      ProjDesc D, Cell* __restrict__ scratch,
+                                                      Cell* __restrict__ out) {
+    const uint32_t i = blockIdx.x * blockDim.x + threadIdx.x;
+    if (i >= nrec) return;
+    Cell* mine = scratch + i;
+    if (D.ncols) parse_cols_out(g + recs[i], D.cols, D.ncols, D.delim, D.quote, mine, nrec);
+    Cell* o = out + (uint64_t)i * D.nout;
+    for (int k = 0; k < D.nout; k++) {
+        const uint32_t b = D.off[k], e = D.off[k + 1];
+        const Insn first = D.code[b];
+        Cell v;
+        if (e == b + 1 && first.op == OP_COL) v = mine[(uint64_t)first.b * nrec];
+        else if (e == b + 1 && first.op == OP_CONST) v = D.consts[first.b];
+        else v = eval_value(D.code, b, e, mine, nrec, D.consts);
+        o[k] = v;
+    }
 }
 
 // string bytes of cells -> packed host-visible buffer
@@ -1650,6 +1715,14 @@ hipError_t cq_launch_gather(const uint8_t* g, const cq::ScanPlan* P, const unsig
     hipError_t e = hipMemcpyToSymbolAsync(HIP_SYMBOL(cq::c_plan), P, sizeof *P, 0, hipMemcpyHostToDevice, s);
     if (e != hipSuccess) return e;
     hipLaunchKernelGGL(cq::gather_kernel, dim3((nrec + 127) / 128), dim3(128), 0, s, g, recs, nrec, out);
+    return hipGetLastError();
+}
+
+hipError_t cq_launch_project(const uint8_t* g, const unsigned long long* recs, uint32_t nrec,
+                             const cq::ProjDesc* D, cq::Cell* scratch, cq::Cell* out, hipStream_t s) {
+    if (!nrec) return hipSuccess;
+    hipLaunchKernelGGL(cq::project_kernel, dim3((nrec + 255) / 256), dim3(256), 0, s, g, recs, nrec, *D, scratch,
+                       out);
     return hipGetLastError();
 }
 
