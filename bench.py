@@ -141,9 +141,9 @@ def main():
             ng = tp.contents.nrows
             cq_amd.result_free(tp)
             st = cq_amd.stats()
-        if os.environ.get("CQ_BENCH_DEBUG"):
-            print("stats", st, file=sys.stderr)
-        return ng, st["scan_ms"]
+            if os.environ.get("CQ_BENCH_DEBUG"):
+                print("stats", st, file=sys.stderr)
+            return ng, st["scan_ms"]
         blob = C.c_void_p()
         n = L.cqgpu_query_partial(ast, (C.c_void_p * 1)(table.handle.value), 1, C.byref(blob))
         if n == 0:

@@ -23,7 +23,7 @@ class Stats(C.Structure):
     _fields_ = [("scan_ms", C.c_double), ("total_ms", C.c_double), ("scan_bytes", C.c_uint64),
                 ("records", C.c_uint64), ("groups", C.c_uint64), ("lds_spills", C.c_uint64),
                 ("grid", C.c_int), ("path", C.c_int), ("retries", C.c_int),
-                ("slow_records", C.c_uint64), ("passed", C.c_uint64)]
+                ("slow_records", C.c_uint64), ("passed", C.c_uint64), ("scan_kernel", C.c_int)]
 
 
 def lib():
@@ -56,6 +56,8 @@ def lib():
         L.cqgpu_last_stats.argtypes = [C.POINTER(Stats)]
         L.cqgpu_last_error.restype = C.c_char_p
         L.cqgpu_last_ineligible.restype = C.c_char_p
+        L.cqgpu_set_scan_kernel.restype = C.c_int
+        L.cqgpu_set_scan_kernel.argtypes = [C.c_int]
         _lib = L
     return _lib
 
@@ -162,6 +164,11 @@ def stats() -> dict:
     s = Stats()
     lib().cqgpu_last_stats(C.byref(s))
     return {f: getattr(s, f) for f, _ in Stats._fields_}
+
+
+def set_scan_kernel(mode: int) -> int:
+    """0: automatic (lean_kernel where it applies), 1: always the general scan_kernel."""
+    return lib().cqgpu_set_scan_kernel(mode)
 
 
 def last_error() -> str:

@@ -48,6 +48,8 @@ hipError_t cq_launch_parse_literals(const uint8_t* text, const unsigned int* off
                                     const unsigned int* lens, uint32_t n, Cell* out, hipStream_t s);
 hipError_t cq_launch_project(const uint8_t* g, const unsigned long long* recs, uint32_t nrec,
                              const ProjDesc* D, Cell* scratch, Cell* out, hipStream_t s);
+int cq_set_scan_mode(int mode);
+int cq_scan_uses_lean(const cq::ScanPlan* P, int with_cells);
 hipError_t cq_sort_offsets(void* temp, size_t* temp_bytes, const unsigned long long* in,
                            unsigned long long* out, size_t n, int bits, hipStream_t s);
 }
@@ -933,6 +935,7 @@ std::vector<HGroup> run_aggregate(DevCtx& c, const cqgpu_table* t, Compiled& C, 
         }
         g_stats.scan_ms = ms_total;
         g_stats.grid = grid;
+        g_stats.scan_kernel = cq_scan_uses_lean(&C.P, 0);
         for (int i = 0; i < 8; i++) g_clk[i] = 0;
         {
             ScanStats s2;
@@ -1704,6 +1707,7 @@ int cqgpu_last_stats(cqgpu_stats* out) {
 const char* cqgpu_last_error(void) { return g_err.c_str(); }
 const char* cqgpu_last_ineligible(void) { return g_inel.c_str(); }
 void cqgpu_set_fallback(cqgpu_fallback_fn fn) { g_fallback = fn; }
+int cqgpu_set_scan_kernel(int mode) { return cq_set_scan_mode(mode); }
 
 // plan explanation for a header line, no device needed (planner unit tests)
 int cqgpu_explain(cq_node* q, const char* header, cq_csv_config cfg, char* out, size_t cap) {

@@ -82,6 +82,7 @@ typedef struct {
     int retries;                 /* global group table regrowths */
     uint64_t slow_records;       /* records the fast field path handed to the general parser */
     uint64_t passed;             /* records that passed WHERE */
+    int scan_kernel;             /* 1 = lean_kernel (wave-autonomous), 0 = general scan_kernel */
 } cqgpu_stats;
 int cqgpu_last_stats(cqgpu_stats* out);
 const char* cqgpu_last_error(void);
@@ -104,6 +105,12 @@ int cqgpu_explain(cq_node* query_ast, const char* header, cq_csv_config cfg, cha
 /* profiling builds (-DCQ_CLOCKS): shader cycles per scan phase of the last scan,
  * summed over waves (all zero in the normal build) */
 int cqgpu_debug_clocks(unsigned long long* out8);
+
+/* Scan kernel choice: 0 = automatic (lean_kernel for the plan shapes it covers,
+ * the general scan_kernel otherwise), 1 = always scan_kernel.  Returns the
+ * previous mode.  Both produce identical results; the knob exists for A/B
+ * measurements and for parity tests of both kernels. */
+int cqgpu_set_scan_kernel(int mode);
 
 /* Optional fallback for plans outside the GPU subset: the reference evaluator
  * compiled with evaluate_query renamed.  Without one, such
