@@ -34,9 +34,9 @@ extern "C" {
 uint32_t cq_scan_cand_stride(const ScanPlan* P, int grouped);
 size_t cq_scan_lds_bytes(const ScanPlan* P, int grouped);
 int cq_scan_occupancy(const ScanPlan* P, int grouped);
-hipError_t cq_launch_scan(const uint8_t* g, const ScanPlan* P, const GroupTable* gt, ScanStats* stats,
-                          unsigned long long* row_out, unsigned long long row_cap, int grouped, int grid,
-                          hipStream_t s, Cell* cells_out, unsigned long long* slow_list,
+hipError_t cq_launch_scan(const uint8_t* g, const ScanPlan* P, const GroupTable* gt, const GroupTable* rt,
+                          ScanStats* stats, unsigned long long* row_out, unsigned long long row_cap, int grouped,
+                          int grid, hipStream_t s, Cell* cells_out, unsigned long long* slow_list,
                           unsigned long long slow_cap);
 hipError_t cq_launch_compact(const GroupTable* gt, const ScanPlan* P, GroupOut* out, unsigned int* count,
                              unsigned int cap_out, hipStream_t s);
@@ -820,6 +820,7 @@ void parse_literals(DevCtx& c, const std::vector<std::string>& texts, Literals& 
 // group table arena in the device workspace
 struct TableArena {
     GroupTable gt;
+    GroupTable rt;                     // raw-byte keys of lean_kernel (lean.hip), merged into gt
     ScanStats* stats;
     GroupOut* out;
     unsigned int* out_count;
@@ -833,7 +834,10 @@ TableArena make_arena(DevCtx& c, const ScanPlan& P, uint32_t cap, size_t out_cap
                       uint32_t cand_stride = 16, unsigned long long slow_cap = 1ull << 20) {
     TableArena A;
     memset(&A.gt, 0, sizeof A.gt);
+    memset(&A.rt, 0, sizeof A.rt);
     A.slow_cap = slow_cap;
+    A.rt.cap = cap;
+    A.rt.cand_stride = cand_stride;
     A.gt.cap = cap;
     A.gt.cand_stride = cand_stride;
     struct Part { void** p; size_t bytes; int fill; };
@@ -857,6 +861,21 @@ TableArena make_arena(DevCtx& c, const ScanPlan& P, uint32_t cap, size_t out_cap
         }
     }
     parts.push_back({(void**)&A.gt.used, 256, 0});
+    bool sums_only = true;
+    for (int a = 0; a < P.nacc; a++) sums_only = sums_only && P.acc[a].kind == ACC_SUM;
+    if (sums_only) {   // lean_kernel plans: the raw-key table
+        parts.push_back({(void**)&A.rt.tag, cap * 4ull, 0});
+        parts.push_back({(void**)&A.rt.clslen, cap * 4ull, 0});
+        parts.push_back({(void**)&A.rt.w0, cap * 8ull, 0});
+        parts.push_back({(void**)&A.rt.w1, cap * 8ull, 0});
+        parts.push_back({(void**)&A.rt.cnt, cap * 8ull, 0});
+        parts.push_back({(void**)&A.rt.first, cap * 8ull, 0xff});
+        for (int a = 0; a < P.nacc; a++) {
+            parts.push_back({(void**)&A.rt.sum[a], cap * 8ull, 0});
+            parts.push_back({(void**)&A.rt.num[a], cap * 8ull, 0});
+        }
+        parts.push_back({(void**)&A.rt.used, 256, 0});
+    }
     parts.push_back({(void**)&A.stats, 256, 0});
     parts.push_back({(void**)&A.out_count, 256, 0});
     parts.push_back({(void**)&A.out, out_cap * sizeof(GroupOut), 0});
@@ -912,7 +931,7 @@ std::vector<HGroup> run_aggregate(DevCtx& c, const cqgpu_table* t, Compiled& C, 
             const int g2 = chunk ? (int)std::min<uint64_t>(grid, wins) : grid;
             HIPCHECK(hipEventRecord(c.ev0, c.stream));
             const unsigned long long done = st.rows_emitted;
-            HIPCHECK(cq_launch_scan(t->g, &P, &A.gt, A.stats, row_out ? row_out + std::min(done, row_cap) : nullptr,
+            HIPCHECK(cq_launch_scan(t->g, &P, &A.gt, A.rt.tag ? &A.rt : nullptr, A.stats, row_out ? row_out + std::min(done, row_cap) : nullptr,
                                     row_cap > done ? row_cap - done : 0, grouped, g2, c.stream, nullptr,
                                     A.slow_list, A.slow_cap));
             HIPCHECK(hipEventRecord(c.ev1, c.stream));
@@ -1787,7 +1806,7 @@ size_t cqgpu_debug_records(cqgpu_table* t, unsigned long long* out, size_t cap) 
         HIPCHECK(hipMalloc(&d, std::max<size_t>(cap, 1) * 8));
         uint64_t windows = (t->n + 31679) / 31680;
         int grid = (int)std::min<uint64_t>(std::max<uint64_t>(windows, 1), (uint64_t)c.ncu * cq_scan_occupancy(&P, 0));
-        HIPCHECK(cq_launch_scan(t->g, &P, &A.gt, A.stats, d, cap, 0, grid, c.stream, nullptr, A.slow_list,
+        HIPCHECK(cq_launch_scan(t->g, &P, &A.gt, A.rt.tag ? &A.rt : nullptr, A.stats, d, cap, 0, grid, c.stream, nullptr, A.slow_list,
                                 A.slow_cap));
         ScanStats st;
         HIPCHECK(hipMemcpyAsync(&st, A.stats, sizeof st, hipMemcpyDeviceToHost, c.stream));
@@ -1827,7 +1846,7 @@ cq_table* cqgpu_debug_scan_cells(cqgpu_table* t, const int* cols, int ncols, uns
         HIPCHECK(hipMalloc(&dc, std::max<size_t>(cap, 1) * ncols * sizeof(Cell)));
         uint64_t windows = (t->n + 31679) / 31680;
         int grid = (int)std::min<uint64_t>(std::max<uint64_t>(windows, 1), (uint64_t)c.ncu * cq_scan_occupancy(&P, 0));
-        HIPCHECK(cq_launch_scan(t->g, &P, &A.gt, A.stats, d, cap, 0, grid, c.stream, dc, A.slow_list,
+        HIPCHECK(cq_launch_scan(t->g, &P, &A.gt, A.rt.tag ? &A.rt : nullptr, A.stats, d, cap, 0, grid, c.stream, dc, A.slow_list,
                                 A.slow_cap));
         ScanStats st;
         HIPCHECK(hipMemcpyAsync(&st, A.stats, sizeof st, hipMemcpyDeviceToHost, c.stream));

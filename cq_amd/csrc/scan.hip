@@ -1334,11 +1334,13 @@ static scan_fn_t scan_fn(const cq::ScanPlan* P, int grouped) {
 extern "C" {
 // the fast scan, then the general kernel over the records it declined
 int cq_lean_eligible(const cq::ScanPlan* P);
-uint64_t cq_lean_windows(uint64_t bytes);
+uint64_t cq_lean_windows(uint64_t begin, uint64_t end);
 int cq_lean_waves_per_block();
-hipError_t cq_launch_lean(const uint8_t* g, const cq::ScanPlan* P, const cq::GroupTable* gt, cq::ScanStats* stats,
-                          unsigned long long* row_out, unsigned long long row_cap, int grouped, int grid,
-                          hipStream_t s, unsigned long long* slow_list, unsigned long long slow_cap);
+hipError_t cq_launch_lean(const uint8_t* g, const cq::ScanPlan* P, const cq::GroupTable* gt,
+                          const cq::GroupTable* rt, cq::ScanStats* stats, unsigned long long* row_out,
+                          unsigned long long row_cap, int grouped, int grid, hipStream_t s,
+                          unsigned long long* slow_list, unsigned long long slow_cap);
+hipError_t cq_launch_raw_merge(const cq::GroupTable* rt, cq::ScanStats* stats, hipStream_t s);
 
 // cqgpu_set_scan_kernel(1) or CQ_SCAN_KERNEL=general: scan_kernel for every plan
 // (A/B runs, parity tests of both kernels)
@@ -1375,24 +1377,25 @@ static int device_cus() {
 }
 
 hipError_t cq_launch_scan(const uint8_t* g, const cq::ScanPlan* P, const cq::GroupTable* gt,
-                          cq::ScanStats* stats, unsigned long long* row_out,
+                          const cq::GroupTable* rt, cq::ScanStats* stats, unsigned long long* row_out,
                           unsigned long long row_cap, int grouped, int grid, hipStream_t s,
                           cq::Cell* cells_out, unsigned long long* slow_list, unsigned long long slow_cap) {
-    if (cq_scan_uses_lean(P, cells_out != nullptr)) {
+    if (cq_scan_uses_lean(P, cells_out != nullptr) && (!grouped || rt)) {
         // slow_kernel reads this file's plan and table symbols
         hipError_t e0 = hipMemcpyToSymbolAsync(HIP_SYMBOL(cq::c_plan), P, sizeof *P, 0, hipMemcpyHostToDevice, s);
         if (e0 == hipSuccess)
             e0 = hipMemcpyToSymbolAsync(HIP_SYMBOL(cq::c_gt), gt, sizeof *gt, 0, hipMemcpyHostToDevice, s);
         if (e0 != hipSuccess) return e0;
-        // one 16-wave block per CU, each wave streaming its own 2 KiB windows
+        // one 16-wave block per CU, each wave streaming its own windows
         const uint64_t hi = P->range_end < P->n ? P->range_end : P->n;
-        const uint64_t wins = cq_lean_windows(hi) - P->range_begin / 2048 + 1;
+        const uint64_t wins = cq_lean_windows(P->range_begin, hi) + 1;
         const uint64_t per = (uint64_t)cq_lean_waves_per_block();
         uint64_t lg = (wins + per - 1) / per;
         if (lg > (uint64_t)device_cus()) lg = (uint64_t)device_cus();
         if (lg < 1) lg = 1;
         if ((wins + lg * per - 1) / (lg * per) < (1u << 17)) {   // first-row codes hold 17 bits of round
-            hipError_t e = cq_launch_lean(g, P, gt, stats, row_out, row_cap, grouped, (int)lg, s, slow_list, slow_cap);
+            hipError_t e = cq_launch_lean(g, P, gt, rt, stats, row_out, row_cap, grouped, (int)lg, s, slow_list,
+                                          slow_cap);
             if (e != hipSuccess) return e;
             if (grouped)
                 hipLaunchKernelGGL(cq::slow_kernel<true>, dim3(256), dim3(256), 0, s, g, stats, row_out, row_cap,
@@ -1400,7 +1403,9 @@ hipError_t cq_launch_scan(const uint8_t* g, const cq::ScanPlan* P, const cq::Gro
             else
                 hipLaunchKernelGGL(cq::slow_kernel<false>, dim3(256), dim3(256), 0, s, g, stats, row_out, row_cap,
                                    cells_out, slow_list, slow_cap);
-            return hipGetLastError();
+            e = hipGetLastError();
+            if (e == hipSuccess && grouped) e = cq_launch_raw_merge(rt, stats, s);
+            return e;
         }
     }
     const size_t lds = cq_scan_lds_bytes(P, grouped);
