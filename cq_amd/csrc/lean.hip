@@ -7,12 +7,15 @@
 // COUNT / SUM / AVG (at most 4 parsed columns, 2 distinct SUM arguments).
 //
 // Every wave works on its own windows with no block barrier in the loop, so one
-// wave's byte classification overlaps another's record work on the same SIMD:
+// wave's byte classification overlaps another's record work on the same SIMD.
+// The record work is arranged as a few batched LDS round trips (record start ->
+// bitmap view -> field bytes -> hash slot) with the arithmetic between them:
 //
-//   load      a window is 2 KiB, lane l holds bytes [32l, 32l + 32) in registers
-//             (two 16-byte non-temporal loads, issued one window ahead); windows
-//             start WS = 1920 bytes apart and own the records starting in their
-//             first WS bytes, so the last 128 bytes only serve the record views
+//   load      a window stages 2 KiB, lane l bytes [32l, 32l + 32) (two 16-byte
+//             non-temporal loads, issued one window ahead): the 16 bytes before
+//             the window's own range (record-start context), its WS = 1952 owned
+//             bytes, and 80 bytes after them for the record views.  Windows start
+//             WS bytes apart and own the records that start in their range
 //   classify  per lane two 32-bit masks -- separators (delimiter and record
 //             terminators '\n' '\r') and terminators -- plus a quote mask when
 //             the window holds a quote; stored as the window's LDS bitmaps
@@ -23,12 +26,14 @@
 //             set separator bit.  A record whose needed fields are not all inside
 //             those 64 bytes, or that has a quote in front of its last needed
 //             field, goes whole to the slow list and slow_kernel (scan.hip)
-//   values    parse_value (csv_reader.c:195-240) is a pure function of the field
-//             bytes, so its result is memoised: per WHERE / SUM column a 512-entry
-//             LDS table maps the raw bytes of a field (<= 8 bytes) to the WHERE
-//             outcome or the SUM addend; only a miss runs the exact field typers
-//             (scanlib.h) and fills the entry.  A wave stops consulting a column's
-//             table once most lookups miss (high-cardinality column)
+//   values    WHERE / SUM fields of 1-7 bytes shaped `digits[.digits]` are typed
+//             in registers: M = the digits, k = digits after the dot, exactly
+//             parse_value's INTEGER M or DOUBLE strtod = RN(M / 10^k).  A WHERE
+//             against a numeric literal L compares INTEGER fields with integer
+//             thresholds ceil(L) / floor(L) and DOUBLE fields as RN(M / 10^k)
+//             against L (value_compare, csv_reader.c:98-130); a short STRING
+//             literal compares big-endian byte words (strcmp).  Any other field
+//             shape runs the exact field typers (scanlib.h) or goes slow
 //   group     the block's LDS open-addressing table is keyed by the RAW bytes of
 //             the GROUP BY field (<= 16 bytes): a raw key partitions the rows at
 //             least as finely as the reference's printf-canonical key.  Blocks
@@ -37,7 +42,12 @@
 //             general parser (parse_cell + group_key) and merges it into the
 //             canonical HBM table -- so "1.5" and "1.50" still meet there
 //   aggregate COUNT and SUM are fire-and-forget LDS atomics; the block flushes once
+//
+// SUM addends of DOUBLE fields are M * RN(10^-k) (within 2 ulp of the reference's
+// RN(M / 10^k); SUM / AVG parity is 1e-6 relative, north_star), INTEGER addends
+// are exact.
 #include <hip/hip_runtime.h>
+#include <cmath>
 #include <cstring>
 #include "plan.h"
 #include "scanlib.h"
@@ -49,19 +59,31 @@ constexpr int LT = 1024;                  // threads per block
 constexpr int NWV = LT / 64;              // waves per block
 constexpr int LB = 32;                    // staged bytes per lane
 constexpr int WB = 64 * LB;               // staged window bytes (2 KiB)
-constexpr int WS = WB - 128;              // window stride: records starting in [ws, ws + WS) are owned
+constexpr int HEAD = 16;                  // staged bytes before the owned range
+constexpr int WS = 1952;                  // window stride = owned bytes
 constexpr int NMW = WB / 32;              // 32-bit bitmap words per window
 constexpr int WBYTES = WB + 32;           // staged bytes + slack for 16-byte field loads
 constexpr int RSN = 64;                   // record slots per pass
 constexpr int MAXS = 2;                   // distinct SUM arguments
-constexpr int PROBES = 32;                // LDS probe window before spilling to HBM
-constexpr int MEMO_N = 512;               // memo entries per WHERE / SUM column
+constexpr int KN = 4;                     // need slots
 constexpr uint32_t NOFIRST = 0xFFFFFFFFu;
-static_assert(WS + 64 + 16 <= WB, "a record view (64 bytes) plus a 16-byte field load stays in the window");
+static_assert(HEAD + WS + 64 + 16 <= WB, "a record view (64 bytes) plus a field load stays in the window");
+static_assert(WS % 16 == 0, "16-byte aligned window loads");
 
-// memo values (SUM: IEEE bits of the addend; NaN payloads never come out of a parse)
-constexpr uint64_t MV_NOTNUM = 0x7FF80000000000A1ULL;   // not INTEGER / DOUBLE: SUM skips it
-constexpr uint64_t MV_SLOW = 0x7FF80000000000A2ULL;     // only the general parser can type it
+// profiling build LEAN_CLK: shader cycles per phase, summed over waves into ScanStats.clk
+#ifdef LEAN_CLK
+#define LCLK(i)                                                   \
+    do {                                                          \
+        const uint64_t t_ = __builtin_amdgcn_s_memtime();          \
+        clk_[i] += t_ - clk_last_;                                \
+        clk_last_ = t_;                                           \
+    } while (0)
+#else
+#define LCLK(i) do {} while (0)
+#endif
+
+// WHERE shapes of this kernel
+enum : int { LW_NONE = 0, LW_NUM = 1, LW_STR = 2, LW_GEN = 3 };
 
 // per-wave LDS area
 struct WaveLds {
@@ -72,17 +94,28 @@ struct WaveLds {
 };
 static_assert(sizeof(WaveLds) % 16 == 0, "16-byte aligned wave areas");
 
-// what the lean kernel needs beyond the ScanPlan
+// everything the kernel reads from constant memory
 struct LeanPlan {
+    uint64_t lo_ok, hi_ok;       // records starting in [lo_ok, hi_ok) are owned by this launch
+    uint64_t first_win, last_win;
+    uint32_t wcol;               // WHERE: CSV column compared
+    uint32_t wop;                // CMP_*
+    uint32_t wtt;                // its truth table (tt_result)
+    int32_t wlo, whi;            // LW_NUM: INTEGER M < L <=> M < wlo; M > L <=> M > whi
+    double wl;                   // LW_NUM: the literal as a double
+    uint64_t wstr;               // LW_STR: literal bytes, big-endian word (zero padded)
+    uint32_t pass_null;          // WHERE outcome of a NULL / missing field
+    Cell wconst;                 // LW_GEN: the literal cell
     int32_t ns;                  // distinct SUM argument slots
     int32_t sum_slot[MAXS];      // need slot of each
+    uint32_t scol[MAXS];         // CSV column of each
+    int32_t nacc;
     int32_t acc_sidx[MAX_ACC];   // accumulator -> SUM index
-    int32_t wslot;               // W_SIMPLE: need slot compared
-    uint32_t wop;                // CMP_*
-    int32_t wconst;              // consts index of the literal
+    uint32_t gcol;               // GROUP BY CSV column
+    uint32_t delim, quote;
 };
 
-__constant__ ScanPlan c_plan;
+__constant__ ScanPlan c_plan;        // raw_merge_kernel
 __constant__ GroupTable c_gt;        // canonical keys (shared with slow_kernel)
 __constant__ GroupTable c_rt;        // raw-byte keys (GK_RAW): block flushes and LDS spills
 __constant__ LeanPlan c_lp;
@@ -95,22 +128,28 @@ __device__ __forceinline__ GKey raw_key(uint32_t len, uint64_t w0, uint64_t w1) 
 }
 
 struct Win {            // one window in flight
-    v4u a, b;           // bytes [32l, 32l + 32)
-    uint32_t prev;      // byte before the window (lane 0)
+    v4u a, b;           // staged bytes [32l, 32l + 32)
 };
 
 __device__ __forceinline__ void load_win(const uint8_t* g, uint64_t w, Win& x) {
-    const uint64_t ws = w * WS;
-    const v4u* src = (const v4u*)(g + ws);
+    const v4u* src = (const v4u*)(g + w * WS - HEAD);   // g has 64 padding bytes before byte 0
     const int lane = threadIdx.x & 63;
     x.a = __builtin_nontemporal_load(src + 2 * lane);
     x.b = __builtin_nontemporal_load(src + 2 * lane + 1);
-    x.prev = lane == 0 ? (uint32_t)g[ws - 1] : 0u;   // g has 64 padding bytes before byte 0
 }
 
-// separator / terminator bits of 32 bytes (bit i = byte i)
-__device__ __forceinline__ void classify(const v4u a, const v4u b, uint32_t rep_d, uint32_t& sep, uint32_t& nl) {
-    uint32_t s = 0, n = 0;
+// 0x80 flags -> a nibble (bit i = byte i)
+__device__ __forceinline__ uint32_t nib(uint32_t f) {
+    uint32_t t = f >> 7;
+    t |= t >> 7;
+    t |= t >> 14;
+    return t & 0xFu;
+}
+
+// separator / terminator / quote bits of 32 bytes (bit i = byte i)
+__device__ __forceinline__ void classify(const v4u a, const v4u b, uint32_t rep_d, uint32_t rep_q, uint32_t& sep,
+                                         uint32_t& nl, uint32_t& qf) {
+    uint32_t s = 0, n = 0, q = 0;
 #pragma unroll
     for (int v = 0; v < 2; v++) {
 #pragma unroll
@@ -125,47 +164,33 @@ __device__ __forceinline__ void classify(const v4u a, const v4u b, uint32_t rep_
             const int sh = (v * 4 + j) * 4;
             s |= (t & 0xFu) << sh;
             n |= ((t >> 4) & 0xFu) << sh;
+            q |= ~nonzero_bytes(x ^ rep_q) & 0x80808080u;
         }
     }
     sep = s;
     nl = n;
-}
-__device__ __forceinline__ bool any_byte(const v4u a, const v4u b, uint32_t rep) {
-    uint32_t acc = 0x80808080u;
-#pragma unroll
-    for (int j = 0; j < 4; j++) acc &= nonzero_bytes(a[j] ^ rep) & nonzero_bytes(b[j] ^ rep);
-    return acc != 0x80808080u;
+    qf = q;
 }
 __device__ __forceinline__ uint32_t byte_bits(const v4u a, const v4u b, uint32_t rep) {
     uint32_t m = 0;
 #pragma unroll
     for (int v = 0; v < 2; v++) {
 #pragma unroll
-        for (int j = 0; j < 4; j++) {
-            const uint32_t x = v ? b[j] : a[j];
-            const uint32_t f = ~nonzero_bytes(x ^ rep) & 0x80808080u;
-            uint32_t t = (f >> 7);
-            t = t | (t >> 7);
-            t = t | (t >> 14);
-            m |= (t & 0xFu) << ((v * 4 + j) * 4);
-        }
+        for (int j = 0; j < 4; j++) m |= nib(~nonzero_bytes((v ? b[j] : a[j]) ^ rep) & 0x80808080u) << ((v * 4 + j) * 4);
     }
     return m;
 }
 
-// same-wave LDS hand-off: DS operations of one wave complete in order, so only
-// the compiler must not move accesses across this point
-__device__ __forceinline__ void wave_sync() {
-    asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+// same-wave LDS hand-off: DS operations of one wave execute in issue order, so only
+// the compiler must not move LDS accesses across this point
+__device__ __forceinline__ void wave_order() {
+    asm volatile("" ::: "memory");
     __builtin_amdgcn_wave_barrier();
+    asm volatile("" ::: "memory");
 }
 
 __device__ __forceinline__ uint32_t ctz64(uint64_t x) { return (uint32_t)__builtin_ctzg(x, 64); }
-__device__ __forceinline__ uint32_t rotl(uint32_t x, int r) { return (x << r) | (x >> (32 - r)); }
-__device__ __forceinline__ uint32_t fmix(uint32_t x) {      // murmur3 finaliser
-    x ^= x >> 16; x *= 0x85EBCA6Bu; x ^= x >> 13; x *= 0xC2B2AE35u; x ^= x >> 16;
-    return x;
-}
+__device__ __forceinline__ uint32_t rotl(uint32_t x, int r) { return __builtin_amdgcn_alignbit(x, x, 32 - r); }
 
 // 64 bitmap bits starting at window offset p
 __device__ __forceinline__ void views(const WaveLds& W, uint32_t p, uint64_t& sv, uint64_t& nv) {
@@ -182,85 +207,181 @@ __device__ __forceinline__ uint64_t qview(const WaveLds& W, uint32_t p) {
     return (uint64_t)__builtin_amdgcn_alignbit(q1, q0, sh) | ((uint64_t)__builtin_amdgcn_alignbit(q2, q1, sh) << 32);
 }
 
-// raw bytes of a field of `len` <= 8 at window offset o, zero padded; false when
-// a byte <= ' ' (blank, control, NUL) is inside: those need the general parser
-__device__ __forceinline__ bool raw8(const uint8_t* bytes, uint32_t o, uint32_t len, uint64_t& w) {
-    uint32_t d0, d1;
-    load8(bytes, o, d0, d1);
-    const uint64_t k = len >= 8 ? ~0ULL : ((1ULL << (8 * len)) - 1);
-    w = ((uint64_t)d0 | ((uint64_t)d1 << 32)) & k;
-    return lt64(w | ~k, 0x21 * B01) == 0;
+// bytes [0, len) of two dwords (len <= 8)
+__device__ __forceinline__ void mask8(uint32_t len, uint32_t& d0, uint32_t& d1) {
+    const uint32_t n1 = len > 4 ? len - 4 : 0;
+    d0 &= len >= 4 ? 0xFFFFFFFFu : ((1u << (8 * len)) - 1);
+    d1 &= n1 >= 4 ? 0xFFFFFFFFu : ((1u << (8 * n1)) - 1);
+}
+
+// 0x80 in every byte < 0x21 (blank, control, NUL) among the bytes of f-flags
+__device__ __forceinline__ uint32_t low_bytes(uint32_t d, uint32_t f) { return lt_bytes(d, 0x21212121u) & f; }
+
+// A field of 1..7 bytes shaped [digits][.][digits] with at least one digit (no sign,
+// so never date-shaped: parse_date needs 8-10 bytes): infer_type gives INTEGER
+// (no dot) or DOUBLE, parse_value M or strtod = RN(M / 10^k).  d0/d1: the field's
+// first 8 bytes, unmasked.  Branch-free; M, k and dot are meaningful when ok.
+struct Num {
+    uint32_t M, k;
+    bool ok, dot;
+};
+__device__ __forceinline__ Num num7(uint32_t d0, uint32_t d1, uint32_t len) {
+    Num r;
+    const uint32_t f0 = len_mask(len, 0) & 0x80808080u, f1 = len_mask(len, 1) & 0x80808080u;
+    const uint32_t x0 = d0 ^ 0x30303030u, x1 = d1 ^ 0x30303030u;
+    const uint32_t g0 = lt_bytes(x0, 0x0A0A0A0Au) & f0, g1 = lt_bytes(x1, 0x0A0A0A0Au) & f1;   // digits
+    const uint32_t t0 = ~nonzero_bytes(d0 ^ 0x2E2E2E2Eu) & f0, t1 = ~nonzero_bytes(d1 ^ 0x2E2E2E2Eu) & f1;  // dots
+    const uint32_t ndot = (uint32_t)__popc(t0) + (uint32_t)__popc(t1);
+    r.ok = (len - 1 <= 6u) & ((g0 | t0) == f0) & ((g1 | t1) == f1) & (ndot <= 1) & ((g0 | g1) != 0);
+    uint64_t v = ((uint64_t)(x0 & spread(g0)) | ((uint64_t)(x1 & spread(g1)) << 32));   // digit values, dot -> 0
+    const uint64_t tm = (uint64_t)t0 | ((uint64_t)t1 << 32);
+    uint32_t pd = ctz64(tm) >> 3;                                       // dot byte (8: none)
+    pd = pd > 7 ? 7u : pd;
+    r.dot = ndot != 0;
+    const uint64_t lo = (1ULL << (8 * pd)) - 1;
+    v = r.dot ? ((v & lo) | ((v >> 8) & ~lo)) : v;
+    r.k = r.dot ? len - 1 - pd : 0u;
+    r.k = r.k > 7 ? 7u : r.k;
+    uint32_t nd2 = len - ndot;                                            // digits
+    nd2 = nd2 - 1 > 7u ? 1u : nd2;
+    v <<= 8 * (8 - nd2);                                                 // right-align the digits
+    r.M = dig8(v);
+    return r;
+}
+
+// Field `c` of the record at window offset p from its 64-bit separator view sv
+// (delimiters and terminators, bit i = byte p + i) and its end e (the first
+// terminator; 64: beyond the view).  Clearing the c lowest separator bits leaves
+// the field's end as the lowest bit; the cleared bits' highest is its start - 1.
+// A column past the record's end is missing (length 0: NULL); a field the view
+// cannot bound fails the fast path.  c is uniform: a scalar loop.
+__device__ __forceinline__ void field_of(uint64_t sv, uint32_t e, uint32_t c, uint32_t p, uint32_t& fp,
+                                         uint32_t& fl, bool& fail, uint32_t& last) {
+    uint64_t s = sv;
+    for (uint32_t i = 0; i < c; i++) s &= s - 1;
+    const uint64_t cl = sv ^ s;
+    const uint32_t start = cl ? 64u - (uint32_t)__builtin_clzll(cl) : 0u;
+    const uint32_t end = ctz64(s);
+    const bool gone = start > e;
+    fail |= gone ? (e == 64) : (end == 64);
+    fp = p + start;
+    fl = gone ? 0u : end - start;
+    const uint32_t l = gone ? e : end;
+    last = l > last ? l : last;
+}
+
+// value_compare outcome through a truth table: bit 0 for <, bit 1 for ==, bit 2 for >
+__device__ __forceinline__ bool tt_result(uint32_t tt, int c) { return (tt >> (c < 0 ? 0 : (c == 0 ? 1 : 2))) & 1; }
+
+// 10^k (exact) and ~10^-k (three rounded products, SUM addends only), k = 0..7
+__device__ __forceinline__ double p10(uint32_t k) {
+    return ((k & 1) ? 10.0 : 1.0) * ((k & 2) ? 100.0 : 1.0) * ((k & 4) ? 1e4 : 1.0);
+}
+__device__ __forceinline__ double inv10(uint32_t k) {
+    return ((k & 1) ? 0.1 : 1.0) * ((k & 2) ? 0.01 : 1.0) * ((k & 4) ? 1e-4 : 1.0);
 }
 
 // exact typing of a field (infer_type + parse_value); false: only the general
 // parser can tell (dates, signs, long numerals, blanks ...)
-__device__ __forceinline__ bool type_field(const uint8_t* bytes, uint32_t o, uint32_t len, bool num_ok, Cell& c) {
+__device__ __forceinline__ bool type_field(const uint8_t* bytes, uint32_t o, uint32_t len, Cell& c) {
     if (len == 0) { c = cell_null(); return true; }
     uint64_t kw;
-    if (lean_field(bytes, o, len, num_ok, c, kw)) return true;
+    if (lean_field(bytes, o, len, true, c, kw)) return true;
     GKey unused;
-    return fast_field(bytes, o, len, num_ok, false, c, unused) == FF_OK;
+    return fast_field(bytes, o, len, true, false, c, unused) == FF_OK;
 }
 
-// LDS group table (structure of arrays carved from dynamic LDS), raw-byte keys
+__device__ __forceinline__ uint64_t bswap64(uint32_t d0, uint32_t d1) {
+    return ((uint64_t)__builtin_bswap32(d0) << 32) | __builtin_bswap32(d1);
+}
+
+// LDS group table (structure of arrays carved from dynamic LDS), raw-byte keys.
+// Slots are grouped in buckets of BS = 16; a key's home bucket is its hash's top
+// bits, and a bucket's 16 u16 fingerprints (0: free, FP_BUSY: being written) are
+// read with two 16-byte loads.  A lookup is two batched round trips:
+// fingerprints, then the first matching slot's key.  Keys missing from their
+// home bucket's first match (new keys, bucket overflow, fingerprint collisions)
+// take lt_slow: lock-free linear probing over the slots from the home bucket.
+constexpr uint32_t BS = 16;
+constexpr uint32_t FP_BUSY = 0xFFFEu;   // fingerprints are odd
 struct LTab {
-    uint32_t H;
-    v4u* A;               // {header, first-row code, key bytes 0-3, key bytes 4-7}
+    uint32_t H;           // slots (multiple of BS)
+    uint32_t NB;          // buckets
+    v4u* F;               // fingerprints: bucket b = F[2b], F[2b + 1]
+    v4u* A;               // {0x80000000 | len, first-row code, key bytes 0-3, key bytes 4-7}
     uint2* B;             // key bytes 8-15
     uint32_t* cnt;
     double* sum[MAXS];
     uint32_t* miss[MAXS]; // SUM arguments that were not numeric
 };
 
-// find or insert raw key (len, w0, w1) with hash h; -1 when the probe window is
-// full.  `a` returns the slot's first 16 bytes as read (first-row code in a.y).
-__device__ __forceinline__ int lt_find(const LTab& t, uint32_t len, uint64_t w0, uint64_t w1, uint32_t h, v4u& a) {
-    const uint32_t hd = 0x80000000u | (h & 0x7FF80000u) | len;
-    const uint32_t k0 = (uint32_t)w0, k1 = (uint32_t)(w0 >> 32);
-    const bool wide = len > 8;
-    for (uint32_t probe = 0; probe < PROBES; probe++) {
-        const uint32_t i = (h + probe) & (t.H - 1);
-        uint32_t* ap = (uint32_t*)(t.A + i);
-        a = t.A[i];
-        if (a.x == hd && a.z == k0 && a.w == k1) {
-            if (!wide) return (int)i;
-            const uint2 b = t.B[i];
-            if (b.x == (uint32_t)w1 && b.y == (uint32_t)(w1 >> 32)) return (int)i;
-        }
-        uint32_t cur = a.x;
-        if (cur == 0) {
-            const uint32_t old = atomicCAS(ap, 0u, 1u);
-            if (old == 0) {
-                ap[2] = k0;
-                ap[3] = k1;
-                t.B[i] = make_uint2((uint32_t)w1, (uint32_t)(w1 >> 32));
-                __hip_atomic_store(ap, hd, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_WORKGROUP);
-                a.x = hd;
-                a.y = NOFIRST;
-                return (int)i;
-            }
-            cur = old;
-        }
-        for (uint32_t spin = 0; cur == 1; spin++) {
-            if (spin > (1u << 20)) return -1;             // the HBM table takes the record
-            cur = __hip_atomic_load(ap, __ATOMIC_ACQUIRE, __HIP_MEMORY_SCOPE_WORKGROUP);
-        }
-        if (cur == hd) {                                   // published meanwhile: re-read the key
-            __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "workgroup");
-            a = t.A[i];
-            if (a.z == k0 && a.w == k1) {
-                if (!wide) return (int)i;
-                const uint2 b = t.B[i];
-                if (b.x == (uint32_t)w1 && b.y == (uint32_t)(w1 >> 32)) return (int)i;
-            }
-        }
+__device__ __forceinline__ uint32_t key_hash(uint32_t len, uint32_t k0, uint32_t k1, uint32_t k2, uint32_t k3) {
+    uint32_t x = k0 ^ rotl(k1, 7) ^ rotl(k2, 13) ^ rotl(k3, 21) ^ (len << 27);
+    x *= 0x9E3779B1u;
+    x ^= x >> 15;
+    x *= 0x85EBCA6Bu;
+    return x ^ (x >> 13);
+}
+__device__ __forceinline__ uint32_t fp_of(uint32_t h) { return (h & 0xFFFFu) | 1u; }
+__device__ __forceinline__ uint32_t bucket_of(uint32_t h, uint32_t nb) { return __umulhi(h, nb); }
+
+// index of the first of the 16 u16 fingerprints equal to fp (16: none); the lowest
+// flag of the SWAR zero-half test is exact
+__device__ __forceinline__ uint32_t fp_first(const v4u q0, const v4u q1, uint32_t fp) {
+    const uint32_t rep = fp * 0x00010001u;
+    uint32_t m = 0;
+#pragma unroll
+    for (int j = 0; j < 8; j++) {
+        const uint32_t x = (j < 4 ? q0[j & 3] : q1[j & 3]) ^ rep;
+        const uint32_t f = (x - 0x00010001u) & ~x & 0x80008000u;
+        m |= ((f >> 15) & 1u) << (2 * j);
+        m |= (f >> 31) << (2 * j + 1);
     }
-    return -1;
+    return (uint32_t)__builtin_ctz(m | 0x10000u);
 }
 
-__device__ __forceinline__ uint32_t key_hash(uint32_t len, uint64_t w0, uint64_t w1) {
-    return fmix((uint32_t)w0 ^ rotl((uint32_t)(w0 >> 32), 11) ^ rotl((uint32_t)w1, 19) ^
-                rotl((uint32_t)(w1 >> 32), 27) ^ (len << 26));
+// Find the key or insert it: linear probing over slots from the home bucket.  A
+// free fingerprint is claimed FP_BUSY by CAS on its dword, the key written, then
+// the fingerprint published; every inserter of a key probes the same sequence,
+// so two of them meet at the same first free slot and the loser finds the
+// winner's key.  -1: the table is full or a claim never resolved (the HBM raw
+// table takes the record).
+__device__ __forceinline__ int lt_slow(const LTab& t, uint32_t len, uint32_t k0, uint32_t k1, uint32_t k2,
+                                       uint32_t k3, uint32_t h, uint32_t& first) {
+    const uint32_t hd = 0x80000000u | len, fp = fp_of(h);
+    uint32_t slot = bucket_of(h, t.NB) * BS;
+    uint32_t* f32 = (uint32_t*)t.F;
+    uint32_t n = 0;
+    for (uint32_t it = 0; it < 4 * t.H + 4096; it++) {
+        const uint32_t sh = 16 * (slot & 1);
+        const uint32_t d = __hip_atomic_load(f32 + (slot >> 1), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
+        const uint32_t x = (d >> sh) & 0xFFFFu;
+        if (x == 0) {
+            const uint32_t old = atomicCAS(f32 + (slot >> 1), d, d | (FP_BUSY << sh));
+            if (old == d) {                                 // claimed: write the key, publish
+                t.A[slot] = v4u{hd, NOFIRST, k0, k1};
+                t.B[slot] = make_uint2(k2, k3);
+                __builtin_amdgcn_fence(__ATOMIC_RELEASE, "workgroup");
+                atomicXor(f32 + (slot >> 1), (FP_BUSY ^ fp) << sh);
+                first = NOFIRST;
+                return (int)slot;
+            }
+            continue;                                       // the dword changed: look again
+        }
+        if (x == FP_BUSY) continue;                         // being written: look again
+        if (x == fp) {
+            __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "workgroup");
+            const v4u a = t.A[slot];
+            const uint2 b = t.B[slot];
+            if (a.x == hd && a.z == k0 && a.w == k1 && b.x == k2 && b.y == k3) {
+                first = a.y;
+                return (int)slot;
+            }
+        }
+        if (++n == t.H) return -1;
+        slot = slot + 1 == t.H ? 0 : slot + 1;
+    }
+    return -1;
 }
 
 // the canonical group key of a raw key: bytes staged in LDS (zero padded, so
@@ -279,31 +400,31 @@ __device__ __forceinline__ uint8_t* carve(uint8_t*& q, size_t bytes) {
     return r;
 }
 
-// GROUPED: GROUP BY (else one group); WM: W_NONE / W_SIMPLE; NS: distinct SUM arguments
+// GROUPED: GROUP BY (else one group); WM: LW_*; NS: distinct SUM arguments (0-2)
 template <bool GROUPED, int WM, int NS>
 __global__ __launch_bounds__(LT) void lean_kernel(const uint8_t* __restrict__ g, ScanStats* __restrict__ stats,
                                                   unsigned long long* __restrict__ row_out,
                                                   unsigned long long row_cap, uint32_t lds_h,
                                                   unsigned long long* __restrict__ slow_list,
                                                   unsigned long long slow_cap) {
-    constexpr int KN = 4;
-    constexpr int NR = 1 + NS;                         // memo roles: 0 WHERE, 1 + j SUM j
-    const ScanPlan& P = c_plan;
+    const LeanPlan& LP = c_lp;
     const GroupTable& gt = c_gt;
     const GroupTable& rt = c_rt;
-    const LeanPlan& LP = c_lp;
     extern __shared__ __align__(16) uint8_t smem[];
     uint8_t* q = smem;
     WaveLds* waves = (WaveLds*)carve(q, sizeof(WaveLds) * NWV);
-    v4u* memo = (v4u*)carve(q, sizeof(v4u) * MEMO_N * NR);
-    const int tid = threadIdx.x, lane = tid & 63, wv = tid >> 6;
+    const int tid = threadIdx.x, lane = tid & 63;
+    const int wv = __builtin_amdgcn_readfirstlane(tid >> 6);   // wave-uniform: the window loop is scalar
     WaveLds& W = waves[wv];
     LTab lt;
     lt.H = lds_h;
+    lt.NB = 0; lt.F = nullptr;
     lt.A = nullptr; lt.B = nullptr; lt.cnt = nullptr;
 #pragma unroll
     for (int s = 0; s < MAXS; s++) { lt.sum[s] = nullptr; lt.miss[s] = nullptr; }
     if (GROUPED) {
+        lt.NB = lds_h / BS;
+        lt.F = (v4u*)carve(q, (size_t)lds_h * 2);
         lt.A = (v4u*)carve(q, (size_t)lds_h * 16);
         lt.B = (uint2*)carve(q, (size_t)lds_h * 8);
         lt.cnt = (uint32_t*)carve(q, (size_t)lds_h * 4);
@@ -319,27 +440,20 @@ __global__ __launch_bounds__(LT) void lean_kernel(const uint8_t* __restrict__ g,
 #pragma unroll
             for (int s = 0; s < NS; s++) { lt.sum[s][i] = 0.0; lt.miss[s][i] = 0; }
         }
+        for (uint32_t i = tid; i < lt.NB * 2; i += LT) lt.F[i] = v4u{0u, 0u, 0u, 0u};
+        __syncthreads();
     }
-    for (uint32_t i = tid; i < (uint32_t)(MEMO_N * NR); i += LT) memo[i] = v4u{0u, 0u, 0u, 0u};   // raw 0: empty
-    __syncthreads();
 
     // uniform plan facts
-    const int nneed = P.nneed;
-    const int gslot = GROUPED ? P.group_slot : -1;
-    const Cell wconst = WM == W_SIMPLE ? P.consts[LP.wconst] : cell_null();
-    const uint32_t wop = WM == W_SIMPLE ? LP.wop : 0u;
-    const bool pass_null = WM == W_SIMPLE ? cmp_result(wop, compare(cell_null(), wconst)) : true;
-    int rslot[NR];                                     // need slot of each memo role (-1: none)
-    rslot[0] = WM == W_SIMPLE ? LP.wslot : -1;
+    const uint32_t wcol = WM != LW_NONE ? LP.wcol : 0u;
+    const uint32_t gcol = GROUPED ? LP.gcol : 0u;
+    uint32_t scol[MAXS];
 #pragma unroll
-    for (int j = 0; j < NS; j++) rslot[1 + j] = j < LP.ns ? LP.sum_slot[j] : -1;
-    const uint32_t rep_d = P.delim * 0x01010101u, rep_q = P.quote * 0x01010101u;
-    const bool num_ok = true;                          // the host admits plans whose delimiter no numeral parse consumes
-    const uint64_t lo_ok = P.data_begin > P.range_begin ? P.data_begin : P.range_begin;
-    const uint64_t hi_ok = P.range_end < P.n ? P.range_end : P.n;
-    const uint64_t first_win = P.range_begin / WS;
-    const uint64_t last_win = (hi_ok + WS - 1) / WS;
+    for (int j = 0; j < MAXS; j++) scol[j] = j < NS ? LP.scol[j] : 0u;
+    const uint32_t rep_d = LP.delim * 0x01010101u, rep_q = LP.quote * 0x01010101u;
+    const uint64_t lo_ok = LP.lo_ok, hi_ok = LP.hi_ok, last_win = LP.last_win;
     const uint64_t tile_g = (uint64_t)(uintptr_t)W.bytes;
+    const uint64_t wstep = (uint64_t)gridDim.x * NWV;
 
     // per-lane single-group partials and per-wave statistics
     uint32_t my_cnt = 0;
@@ -347,18 +461,24 @@ __global__ __launch_bounds__(LT) void lean_kernel(const uint8_t* __restrict__ g,
     double my_sum[MAXS] = {0.0, 0.0};
     uint32_t my_num[MAXS] = {0u, 0u};
     unsigned long long n_rec = 0, n_pass = 0, n_spill = 0;
-    uint32_t m_look[NR], m_miss[NR];                   // memo statistics (wave-uniform)
-    bool m_on[NR];
-#pragma unroll
-    for (int r = 0; r < NR; r++) { m_look[r] = 0; m_miss[r] = 0; m_on[r] = true; }
 
+#ifdef LEAN_CLK
+    uint64_t clk_[8] = {0, 0, 0, 0, 0, 0, 0, 0};
+    uint64_t clk_last_ = __builtin_amdgcn_s_memtime();
+#endif
     Win nx;
-    uint64_t w = first_win + (uint64_t)blockIdx.x * NWV + wv;
+    uint64_t w = LP.first_win + (uint64_t)blockIdx.x * NWV + wv;
     if (w < last_win) load_win(g, w, nx);
-    for (uint32_t round = 0; w < last_win; round++, w += (uint64_t)gridDim.x * NWV) {
+    for (uint32_t round = 0; w < last_win; round++, w += wstep) {
         const uint64_t ws = w * WS;
+#ifdef LEAN_CLK
+        asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+#endif
         const Win cur = nx;
-        if (w + (uint64_t)gridDim.x * NWV < last_win) load_win(g, w + (uint64_t)gridDim.x * NWV, nx);
+        LCLK(0);
+#ifndef LEAN_NOMEM   // profiling build LEAN_NOMEM: every window re-processes the first one (no HBM reads)
+        if (w + wstep < last_win) load_win(g, w + wstep, nx);
+#endif
 
         // ---- stage and classify
         ((v4u*)W.bytes)[2 * lane] = cur.a;
@@ -367,25 +487,26 @@ __global__ __launch_bounds__(LT) void lean_kernel(const uint8_t* __restrict__ g,
         if (lane == 0) n_rec += W.bytes[w & 2047];
         continue;
 #endif
-        uint32_t sep, nl;
-        classify(cur.a, cur.b, rep_d, sep, nl);
+        uint32_t sep, nl, qf;
+        classify(cur.a, cur.b, rep_d, rep_q, sep, nl, qf);
         W.bm[lane] = make_uint2(sep, nl);
-        const bool wq = __ballot(any_byte(cur.a, cur.b, rep_q)) != 0;   // window holds a quote (uniform)
+        const bool wq = __ballot(qf != 0) != 0;           // window holds a quote (uniform)
         if (wq) W.qt[lane] = byte_bits(cur.a, cur.b, rep_q);
 
-        // ---- record starts owned by this window: [ws, ws + WS) within [lo_ok, hi_ok)
-        const uint32_t prevnl = (uint32_t)__builtin_amdgcn_update_dpp((int)(cur.prev == '\n' || cur.prev == '\r'),
-                                                                      (int)(nl >> 31), 0x138, 0xf, 0xf, false);
+        // ---- record starts owned by this window: file [ws, ws + WS) within [lo_ok, hi_ok)
+        const uint32_t prevnl = (uint32_t)__builtin_amdgcn_update_dpp(0, (int)(nl >> 31), 0x138, 0xf, 0xf, true);
         uint32_t starts = ~nl & ((nl << 1) | prevnl);
         {
-            const uint64_t base = ws + (uint64_t)lane * LB;
-            const uint64_t lo = lo_ok > ws ? lo_ok : ws;
-            const uint64_t hi = hi_ok < ws + WS ? hi_ok : ws + WS;
-            if (base + LB <= lo || base >= hi) {
+            const uint64_t lo64 = (lo_ok > ws ? lo_ok : ws) - ws;
+            const uint64_t hi64 = hi_ok < ws + WS ? hi_ok : ws + WS;
+            const uint32_t lo_s = HEAD + (uint32_t)(lo64 < (uint64_t)WS ? lo64 : (uint64_t)WS);   // staged offsets
+            const uint32_t hi_s = hi64 > ws ? HEAD + (uint32_t)(hi64 - ws) : (uint32_t)HEAD;
+            const uint32_t b0 = (uint32_t)lane * LB;
+            if (b0 + LB <= lo_s || b0 >= hi_s) {
                 starts = 0;
             } else {
-                if (base < lo) starts &= ~0u << (lo - base);
-                if (base + LB > hi) starts &= (1u << (hi - base)) - 1;
+                if (lo_s > b0) starts &= ~0u << (lo_s - b0);
+                if (hi_s < b0 + LB) starts &= (1u << (hi_s - b0)) - 1;
             }
         }
         const uint32_t nst = (uint32_t)__popc(starts);
@@ -393,6 +514,7 @@ __global__ __launch_bounds__(LT) void lean_kernel(const uint8_t* __restrict__ g,
         const uint32_t rbase = incl - nst;
         const uint32_t R = (uint32_t)__builtin_amdgcn_readlane((int)incl, 63);
 
+        LCLK(1);
 #if defined(LEAN_PROF) && LEAN_PROF == 1   // profiling build: + classify, bitmaps, record numbering
         n_rec += R;
         continue;
@@ -400,162 +522,130 @@ __global__ __launch_bounds__(LT) void lean_kernel(const uint8_t* __restrict__ g,
         for (uint32_t pass = 0; pass < R; pass += RSN) {
             // this pass's record starts -> W.rs
             {
-                uint32_t m = starts, r = rbase;
+                uint32_t m = starts, r = rbase - pass;
                 while (m) {
                     const uint32_t b = (uint32_t)__builtin_ctz(m);
                     m &= m - 1;
-                    if (r >= pass && r < pass + RSN) W.rs[r - pass] = (uint16_t)(lane * LB + b);
+                    if (r < (uint32_t)RSN) W.rs[r] = (uint16_t)(lane * LB + b);
                     r++;
                 }
             }
-            wave_sync();
+            wave_order();
             const bool valid = pass + lane < R;
-            const uint32_t p = valid ? W.rs[lane] : 0u;
+            const uint32_t p = valid ? W.rs[lane] : (uint32_t)HEAD;
 
-            // ---- field bounds of the need slots (separator bits only, unrolled)
+            // ---- role fields (WHERE, SUM 0/1, GROUP BY): position and length (0: NULL / missing)
             uint64_t sv, nv;
             views(W, p, sv, nv);
             const uint32_t e = ctz64(nv);                  // record end (64: beyond the view)
-            uint64_t s = sv;
-            uint32_t col = 0, fstart = 0, lastpos = 0;
-            bool fail = !valid, gone = false;
-            uint32_t fpos[KN], flen[KN];
-            bool fex[KN];
+            bool fail = !valid;
+            uint32_t lastpos = 0;
+            uint32_t wfp = p, wfl = 0, gfp = p, klen = 0;
+            uint32_t sfp[MAXS], sfl[MAXS];
 #pragma unroll
-            for (int k = 0; k < KN; k++) {
-                fpos[k] = 0; flen[k] = 0; fex[k] = false;
-                if (k >= nneed) break;
-                const uint32_t c = (uint32_t)P.need_col[k];
-                for (; col < c; col++) {                   // skip to column c (uniform trip count)
-                    fstart = ctz64(s) + 1;
-                    s &= s - 1;
-                }
-                if (!gone && fstart > e) {                 // the record ended before column c
-                    gone = true;
-                    if (e == 64) fail = true;              // ... or we cannot see where: general path
-                    lastpos = e;
-                }
-                if (!gone) {
-                    const uint32_t fe = ctz64(s);
-                    if (fe == 64) fail = true;             // field runs past the view
-                    fpos[k] = p + fstart;
-                    flen[k] = fe - fstart;
-                    fex[k] = true;
-                    lastpos = fe;
-                    s &= s - 1;
-                    col = c + 1;
-                    fstart = fe + 1;
-                }
-            }
+            for (int j = 0; j < MAXS; j++) { sfp[j] = p; sfl[j] = 0; }
+            if (WM != LW_NONE) field_of(sv, e, wcol, p, wfp, wfl, fail, lastpos);
+#pragma unroll
+            for (int j = 0; j < NS; j++) field_of(sv, e, scol[j], p, sfp[j], sfl[j], fail, lastpos);
+            if (GROUPED) field_of(sv, e, gcol, p, gfp, klen, fail, lastpos);
             // a quote at or before the last byte examined may hide separators
-            if (wq && valid && (qview(W, p) & ((2ULL << (lastpos < 63 ? lastpos : 63)) - 1))) fail = true;
+            if (wq) fail |= (qview(W, p) & ((2ULL << (lastpos < 63 ? lastpos : 63)) - 1)) != 0;
 
-#if defined(LEAN_PROF) && LEAN_PROF == 2   // profiling build: + record list and field walk
-            n_rec += __popcll(__ballot(fail || ((fpos[0] + flen[KN - 1]) & 1)));
-            wave_sync();
+            // ---- field bytes of the roles (one batch of LDS reads)
+            uint32_t wd0 = 0, wd1 = 0;
+            if (WM != LW_NONE) load8(W.bytes, wfp, wd0, wd1);
+            uint32_t sd0[MAXS], sd1[MAXS];
+#pragma unroll
+            for (int j = 0; j < MAXS; j++) {
+                sd0[j] = sd1[j] = 0;
+                if (j < NS) load8(W.bytes, sfp[j], sd0[j], sd1[j]);
+            }
+            uint32_t k0 = 0, k1 = 0, k2 = 0, k3 = 0;
+            if (GROUPED) load16(W.bytes, gfp, k0, k1, k2, k3);
+
+            LCLK(2);
+#if defined(LEAN_PROF) && LEAN_PROF == 2   // profiling build: + record list, field walk, field loads
+            n_rec += __popcll(__ballot(fail || ((wd0 ^ sd0[0] ^ k0 ^ lastpos) & 1)));
+            wave_order();
             continue;
 #endif
-            // ---- WHERE outcome and SUM addends: memo lookups (unrolled over roles)
-            uint64_t val[NR], raw[NR];
-            uint32_t midx[NR];
-            uint32_t todo = 0;                             // roles this lane must type (bit r), memo fill (bit 8 + r)
-#pragma unroll
-            for (int r = 0; r < NR; r++) {
-                val[r] = r == 0 ? (uint64_t)pass_null : MV_NOTNUM;   // missing column / empty field: NULL
-                raw[r] = 0;
-                midx[r] = 0;
-                const int slot = rslot[r];
-                if (slot < 0) continue;                    // uniform
-                uint32_t fp = fpos[0], fl = flen[0];
-                bool ex = fex[0];
-#pragma unroll
-                for (int k = 1; k < KN; k++)
-                    if (k == slot) { fp = fpos[k]; fl = flen[k]; ex = fex[k]; }
-                if (fail || !ex || fl == 0) continue;
-                bool memo_ok = false;
-                if (fl <= 8 && m_on[r]) {
-                    uint64_t x;
-                    if (raw8(W.bytes, fp, fl, x)) {
-                        const uint32_t mi = fmix((uint32_t)x ^ rotl((uint32_t)(x >> 32), 16)) & (MEMO_N - 1);
-                        const v4u m = memo[r * MEMO_N + mi];
-                        raw[r] = x;
-                        midx[r] = mi;
-                        memo_ok = true;
-                        if (m.x == (uint32_t)x && m.y == (uint32_t)(x >> 32)) {
-                            val[r] = (uint64_t)m.z | ((uint64_t)m.w << 32);
-                            continue;
-                        }
+            // ---- WHERE outcome: numerals and short strings in registers, else the exact typers
+            bool pass_ = true;
+            if (WM != LW_NONE) {
+                bool outcome = LP.pass_null != 0;          // missing column / empty field: NULL
+                bool typed = wfl == 0;
+                if (WM == LW_NUM) {
+                    const Num n = num7(wd0, wd1, wfl);
+                    int c = (int)n.M < LP.wlo ? -1 : ((int)n.M > LP.whi ? 1 : 0);
+                    if (__any(n.ok & n.dot)) {             // DOUBLE fields: strtod = RN(M / 10^k)
+                        const double d = (double)n.M / p10(n.k);
+                        if (n.dot) c = d < LP.wl ? -1 : (d > LP.wl ? 1 : 0);
                     }
+                    if (n.ok) outcome = tt_result(LP.wtt, c);
+                    typed |= n.ok;
+                } else if (WM == LW_STR) {
+                    // a STRING field of <= 8 bytes: no leading digit / sign / dot (never a
+                    // numeral or date), no byte <= ' ' (trim_whitespace is a no-op)
+                    uint32_t a0 = wd0, a1 = wd1;
+                    const uint32_t c0 = a0 & 0xFFu;
+                    mask8(wfl, a0, a1);
+                    const uint32_t f0 = len_mask(wfl, 0) & 0x80808080u, f1 = len_mask(wfl, 1) & 0x80808080u;
+                    const bool ok = (wfl - 1 < 8u) & !(is_digit(c0) | (c0 == '-') | (c0 == '+') | (c0 == '.')) &
+                                    ((low_bytes(a0, f0) | low_bytes(a1, f1)) == 0);
+                    const uint64_t x = bswap64(a0, a1);
+                    if (ok) outcome = tt_result(LP.wtt, x < LP.wstr ? -1 : (x > LP.wstr ? 1 : 0));
+                    typed |= ok;
                 }
-                todo |= (1u << r) | (memo_ok ? (0x100u << r) : 0u);
-            }
-#pragma unroll
-            for (int r = 0; r < NR; r++) {                 // memo hit statistics, per wave
-                if (rslot[r] < 0 || !m_on[r]) continue;
-                const uint32_t looked = (uint32_t)__popcll(__ballot(raw[r] != 0));
-                const uint32_t missed = (uint32_t)__popcll(__ballot(((todo >> (8 + r)) & 1) != 0));
-                m_look[r] += looked;
-                m_miss[r] += missed;
-            }
-            if (__any(todo & 0xFF)) {                      // misses: the exact typers, one site
-#pragma unroll 1
-                for (int r = 0; r < NR; r++) {
-                    if (!__any((todo >> r) & 1)) continue;
-                    const int slot = rslot[r];
-                    uint32_t fp = fpos[0], fl = flen[0];
-#pragma unroll
-                    for (int k = 1; k < KN; k++)
-                        if (k == slot) { fp = fpos[k]; fl = flen[k]; }
-                    if ((todo >> r) & 1) {
+                const bool gen = !typed & !fail;
+                if (__any(gen)) {                          // the exact typers (rare shapes)
+                    if (gen) {
                         Cell c;
-                        uint64_t v;
-                        if (!type_field(W.bytes, fp, fl, num_ok, c)) {
-                            v = MV_SLOW;
+                        if (!type_field(W.bytes, wfp, wfl, c)) {
+                            fail = true;
                         } else {
-                            if (c.kind == K_STR) c.bits = tile_g + fp;
-                            if (r == 0) v = cmp_result(wop, compare(c, wconst)) ? 1u : 0u;
-                            else v = is_num(c) ? dbl_bits(num_of(c)) : MV_NOTNUM;
+                            if (c.kind == K_STR) c.bits = tile_g + wfp;
+                            outcome = tt_result(LP.wtt, compare(c, LP.wconst));
                         }
-                        uint64_t x = raw[0];
-                        uint32_t mi = midx[0];
+                    }
+                }
+                pass_ = outcome;
+            }
+
+            // ---- SUM addends (numeric: true and the value)
+            double sval[MAXS];
+            bool snum[MAXS];
 #pragma unroll
-                        for (int j = 1; j < NR; j++)
-                            if (j == r) { x = raw[j]; mi = midx[j]; }
-                        if ((todo >> (8 + r)) & 1)
-                            memo[r * MEMO_N + mi] = v4u{(uint32_t)x, (uint32_t)(x >> 32), (uint32_t)v, (uint32_t)(v >> 32)};
-#pragma unroll
-                        for (int j = 0; j < NR; j++)
-                            if (j == r) val[j] = v;
+            for (int j = 0; j < MAXS; j++) {
+                sval[j] = 0.0;
+                snum[j] = false;
+                if (j >= NS) continue;
+                const Num n = num7(sd0[j], sd1[j], sfl[j]);
+                sval[j] = (double)n.M * inv10(n.k);
+                snum[j] = n.ok;
+                const bool gen = !n.ok & (sfl[j] != 0) & !fail;
+                if (__any(gen)) {
+                    if (gen) {
+                        Cell c;
+                        if (!type_field(W.bytes, sfp[j], sfl[j], c)) fail = true;
+                        else if (is_num(c)) { sval[j] = num_of(c); snum[j] = true; }
                     }
                 }
             }
-#pragma unroll
-            for (int r = 0; r < NR; r++)
-                if (val[r] == MV_SLOW) fail = true;
 
             // ---- GROUP BY key: the raw field bytes (<= 16, no byte <= ' ')
-            uint32_t klen = 0;
-            uint64_t kw0 = 0, kw1 = 0;
-            if (GROUPED && !fail) {
-                uint32_t fp = fpos[0], fl = flen[0];
-                bool ex = fex[0];
-#pragma unroll
-                for (int k = 1; k < KN; k++)
-                    if (k == gslot) { fp = fpos[k]; fl = flen[k]; ex = fex[k]; }
-                if (ex && fl > 0) {
-                    klen = fl;
-                    if (fl <= 8) {
-                        if (!raw8(W.bytes, fp, fl, kw0)) fail = true;
-                    } else if (fl <= 16) {
-                        if (!raw8(W.bytes, fp, 8, kw0) || !raw8(W.bytes, fp + 8, fl - 8, kw1)) fail = true;
-                    } else {
-                        fail = true;
-                    }
-                }
+            uint32_t h = 0;
+            if (GROUPED) {
+                const uint32_t m0 = len_mask(klen, 0), m1 = len_mask(klen, 1), m2 = len_mask(klen, 2), m3 = len_mask(klen, 3);
+                k0 &= m0; k1 &= m1; k2 &= m2; k3 &= m3;
+                const uint32_t lowb = low_bytes(k0, m0 & 0x80808080u) | low_bytes(k1, m1 & 0x80808080u) |
+                                      low_bytes(k2, m2 & 0x80808080u) | low_bytes(k3, m3 & 0x80808080u);
+                fail |= (lowb != 0) | (klen > 16);
+                h = key_hash(klen, k0, k1, k2, k3);
             }
 
+            LCLK(3);
             // ---- declined records go whole to slow_kernel
-            const uint64_t rec = ws + p;
+            const uint64_t rec = ws - HEAD + p;
             const bool slow = valid && fail;
             const uint64_t sb = __ballot(slow);
             if (sb) {
@@ -567,8 +657,8 @@ __global__ __launch_bounds__(LT) void lean_kernel(const uint8_t* __restrict__ g,
                     if (i < slow_cap) slow_list[i] = rec;
                 }
             }
-            const bool ok = valid && !fail;
-            const bool pass_ = ok && (WM == W_NONE || val[0] == 1);
+            const bool ok = valid & !fail;
+            pass_ = pass_ & ok;
             n_rec += (unsigned long long)__popcll(__ballot(ok));
             n_pass += (unsigned long long)__popcll(__ballot(pass_));
             if (row_out) {
@@ -576,50 +666,67 @@ __global__ __launch_bounds__(LT) void lean_kernel(const uint8_t* __restrict__ g,
                 if (pass_ && slot < row_cap) row_out[slot] = rec;
             }
 #if defined(LEAN_PROF) && LEAN_PROF == 3   // profiling build: + values, filter, keys
-            n_rec += __popcll(__ballot((kw0 ^ val[NR - 1]) & 1));
-            wave_sync();
+            n_rec += __popcll(__ballot((h ^ (uint32_t)sval[0]) & 1));
+            wave_order();
             continue;
 #endif
 
+            LCLK(4);
             // ---- aggregate
             if (!GROUPED) {
-                if (pass_) {
-                    my_cnt++;
-                    if (rec < my_first) my_first = rec;
+                my_cnt += pass_ ? 1u : 0u;
+                my_first = pass_ && rec < my_first ? rec : my_first;
 #pragma unroll
-                    for (int j = 0; j < NS; j++)
-                        if (val[1 + j] != MV_NOTNUM) { my_sum[j] += as_dbl(val[1 + j]); my_num[j]++; }
+                for (int j = 0; j < NS; j++) {
+                    my_sum[j] += pass_ && snum[j] ? sval[j] : 0.0;
+                    my_num[j] += pass_ && snum[j] ? 1u : 0u;
                 }
             } else {
-                int slot = -1;
-                const uint32_t h = key_hash(klen, kw0, kw1);
-                if (pass_) {
-                    v4u a;
-                    slot = lt_find(lt, klen, kw0, kw1, h, a);
-                    if (slot >= 0) {
-                        const uint32_t fc = (round << 15) | ((uint32_t)wv << 11) | p;
-                        atomicAdd(&lt.cnt[slot], 1u);
-                        if (fc < a.y) atomicMin((uint32_t*)(lt.A + slot) + 1, fc);
+                // home bucket for every lane: fingerprints, then the matching slot's key
+                const uint32_t bk = bucket_of(h, lt.NB);
+                const v4u q0 = lt.F[2 * bk], q1 = lt.F[2 * bk + 1];
+                const uint32_t j = fp_first(q0, q1, fp_of(h));
+                const uint32_t s0 = bk * BS + (j < BS ? j : BS - 1);
+                const v4u a = lt.A[s0];
+                const uint2 b = lt.B[s0];
+                const bool hit = (j < BS) & (a.x == (0x80000000u | klen)) & (a.z == k0) & (a.w == k1) & (b.x == k2) &
+                                 (b.y == k3);
+                int slot = hit ? (int)s0 : -1;
+                uint32_t first = a.y;
+                const bool miss = pass_ & !hit;
+                if (__any(miss)) {                         // new keys (rare after the first windows)
+                    if (miss) slot = lt_slow(lt, klen, k0, k1, k2, k3, h, first);
+                }
+                const bool add = pass_ & (slot >= 0);
+                if (add) {
+                    const uint32_t fc = (round << 15) | ((uint32_t)wv << 11) | p;
+                    atomicAdd(&lt.cnt[slot], 1u);
+                    if (fc < first) atomicMin((uint32_t*)(lt.A + slot) + 1, fc);
 #pragma unroll
-                        for (int j = 0; j < NS; j++) {
-                            if (val[1 + j] != MV_NOTNUM) atomicAdd(&lt.sum[j][slot], as_dbl(val[1 + j]));
-                            else atomicAdd(&lt.miss[j][slot], 1u);
-                        }
+                    for (int j = 0; j < NS; j++) atomicAdd(&lt.sum[j][slot], snum[j] ? sval[j] : 0.0);
+                }
+#pragma unroll
+                for (int j = 0; j < NS; j++) {
+                    const bool nn = add & !snum[j];
+                    if (__any(nn)) {
+                        if (nn) atomicAdd(&lt.miss[j][slot], 1u);
                     }
                 }
                 const bool spill = pass_ && slot < 0;
                 if (__any(spill)) {                        // LDS table full: straight to the HBM raw table
                     n_spill += (unsigned long long)__popcll(__ballot(spill));
                     if (spill) {
-                        const GKey k = raw_key(klen, kw0, kw1);
-                        const int gi = g_insert(rt, k, gk_hash(k), stats);
+                        const GKey kk = raw_key(klen, (uint64_t)k0 | ((uint64_t)k1 << 32), (uint64_t)k2 | ((uint64_t)k3 << 32));
+                        const int gi = g_insert(rt, kk, gk_hash(kk), stats);
                         if (gi >= 0) {
                             atomicAdd(&rt.cnt[gi], 1ULL);
                             atomicMin(&rt.first[gi], (unsigned long long)rec);
-                            for (int a = 0; a < P.nacc; a++) {
-                                const uint64_t v = LP.acc_sidx[a] == 0 ? val[1] : val[NR - 1];
-                                if (v != MV_NOTNUM) {
-                                    atomicAdd(&rt.sum[a][gi], as_dbl(v));
+                            for (int a = 0; a < LP.nacc; a++) {
+                                const int j = LP.acc_sidx[a];
+                                const bool nm = j == 0 ? snum[0] : snum[MAXS - 1];
+                                const double v = j == 0 ? sval[0] : sval[MAXS - 1];
+                                if (nm) {
+                                    atomicAdd(&rt.sum[a][gi], v);
                                     atomicAdd(&rt.num[a][gi], 1ULL);
                                 }
                             }
@@ -627,13 +734,15 @@ __global__ __launch_bounds__(LT) void lean_kernel(const uint8_t* __restrict__ g,
                     }
                 }
             }
-            wave_sync();                                   // W.rs is rewritten by the next pass
+            wave_order();                                  // W.rs is rewritten by the next pass
+            LCLK(5);
         }
-        // a column whose memo misses more than half the time stops consulting it
-#pragma unroll
-        for (int r = 0; r < NR; r++)
-            if (m_on[r] && m_look[r] >= 512 && 2 * m_miss[r] > m_look[r]) m_on[r] = false;
+        LCLK(6);
     }
+#ifdef LEAN_CLK
+    if (lane == 0)
+        for (int i = 0; i < 8; i++) atomicAdd(&stats->clk[i], (unsigned long long)clk_[i]);
+#endif
 
     // ---- statistics
     if (lane == 0) {
@@ -665,7 +774,7 @@ __global__ __launch_bounds__(LT) void lean_kernel(const uint8_t* __restrict__ g,
             if (gi >= 0) {
                 if (c) atomicAdd(&gt.cnt[gi], c);
                 if (f != ~0ULL) atomicMin(&gt.first[gi], f);
-                for (int a = 0; a < P.nacc; a++) {
+                for (int a = 0; a < LP.nacc; a++) {
                     const int j = LP.acc_sidx[a];
                     const double sa = j == 0 ? sm[0] : sm[MAXS - 1];
                     const unsigned long long na = j == 0 ? nm[0] : nm[MAXS - 1];
@@ -692,10 +801,10 @@ __global__ __launch_bounds__(LT) void lean_kernel(const uint8_t* __restrict__ g,
         const uint32_t n = lt.cnt[i];
         if (n) atomicAdd(&rt.cnt[gi], (unsigned long long)n);
         if (a.y != NOFIRST) {
-            const uint64_t fw = first_win + ((uint64_t)(a.y >> 15) * gridDim.x + blockIdx.x) * NWV + ((a.y >> 11) & 15);
-            atomicMin(&rt.first[gi], (unsigned long long)(fw * WS + (a.y & 2047)));
+            const uint64_t fw = LP.first_win + ((uint64_t)(a.y >> 15) * gridDim.x + blockIdx.x) * NWV + ((a.y >> 11) & 15);
+            atomicMin(&rt.first[gi], (unsigned long long)(fw * WS - HEAD + (a.y & 2047)));
         }
-        for (int acc = 0; acc < P.nacc; acc++) {
+        for (int acc = 0; acc < LP.nacc; acc++) {
             const int j = LP.acc_sidx[acc];
             const double sa = j == 0 ? lt.sum[0][i] : lt.sum[MAXS - 1][i];
             const uint32_t ms = j == 0 ? lt.miss[0][i] : lt.miss[MAXS - 1][i];
@@ -741,14 +850,36 @@ namespace {
 using namespace cq;
 using lean::LeanPlan;
 
+bool hcmp_result(uint32_t op, int c) {
+    switch (op) {
+        case CMP_EQ: return c == 0;
+        case CMP_NE: return c != 0;
+        case CMP_LT: return c < 0;
+        case CMP_GT: return c > 0;
+        case CMP_LE: return c <= 0;
+        default: return c >= 0;
+    }
+}
+
+// numeric literal thresholds for INTEGER fields M in [0, 10^7]: M < L <=> M < ceil(L),
+// M > L <=> M > floor(L) (L finite; clamped to int32)
+void int_thresholds(double L, int32_t* lo, int32_t* hi) {
+    const double c = std::ceil(L), f = std::floor(L);
+    *lo = c >= 2147483647.0 ? 2147483647 : (c <= -2147483648.0 ? (-2147483647 - 1) : (int32_t)c);
+    *hi = f >= 2147483647.0 ? 2147483647 : (f <= -2147483648.0 ? (-2147483647 - 1) : (int32_t)f);
+}
+
 bool lean_shape(const ScanPlan* P, LeanPlan* lp, int* wm) {
-    if (P->nneed > 4 || P->nacc > MAX_ACC) return false;
+    if (P->nneed > lean::KN || P->nacc > MAX_ACC) return false;
     // numeral parses (strtod / strtoll) must stop at the delimiter
     const uint32_t d = P->delim;
     if ((d - '0') < 10u || d == '.' || ((d | 32) >= 'a' && (d | 32) <= 'z') || d == '+' || d == '-') return false;
     if (d == '\n' || d == '\r' || d <= ' ') return false;
     *lp = LeanPlan{};
-    lp->wslot = -1;
+    lp->delim = P->delim;
+    lp->quote = P->quote;
+    if (P->group_slot >= 0) lp->gcol = (uint32_t)P->need_col[P->group_slot];
+    lp->nacc = P->nacc;
     for (int a = 0; a < P->nacc; a++) {
         if (P->acc[a].kind != ACC_SUM) return false;
         const int slot = P->acc[a].slot;
@@ -756,46 +887,66 @@ bool lean_shape(const ScanPlan* P, LeanPlan* lp, int* wm) {
         while (j < lp->ns && lp->sum_slot[j] != slot) j++;
         if (j == lp->ns) {
             if (lp->ns == lean::MAXS) return false;
+            lp->scol[lp->ns] = (uint32_t)P->need_col[slot];
             lp->sum_slot[lp->ns++] = slot;
         }
         lp->acc_sidx[a] = j;
     }
     if (P->nprog == 0) {
-        *wm = W_NONE;
+        *wm = lean::LW_NONE;
     } else if (P->nprog == 3 && P->prog[0].op == OP_COL && P->prog[1].op == OP_CONST && P->prog[2].op == OP_CMP) {
-        *wm = W_SIMPLE;
-        lp->wslot = P->prog[0].a;
-        lp->wconst = P->prog[1].b;
+        lp->wcol = (uint32_t)P->need_col[P->prog[0].a];
         lp->wop = P->prog[2].a;
+        lp->wtt = (hcmp_result(lp->wop, -1) ? 1u : 0u) | (hcmp_result(lp->wop, 0) ? 2u : 0u) | (hcmp_result(lp->wop, 1) ? 4u : 0u);
+        const Cell& L = P->consts[P->prog[1].b];
+        lp->wconst = L;
+        lp->pass_null = hcmp_result(lp->wop, L.kind == K_NULL ? 0 : -1) ? 1u : 0u;   // NULL < any non-NULL
+        if (L.kind == K_INT || L.kind == K_DBL) {
+            *wm = lean::LW_NUM;
+            if (L.kind == K_INT) lp->wl = (double)(int64_t)L.bits;
+            else memcpy(&lp->wl, &L.bits, 8);
+            int_thresholds(lp->wl, &lp->wlo, &lp->whi);
+        } else if (L.kind == K_STR && L.len <= 8) {
+            *wm = lean::LW_STR;                    // the bytes are filled in by the caller (device address)
+        } else {
+            *wm = lean::LW_GEN;
+        }
     } else {
         return false;
     }
     return true;
 }
 
-int ns_of(const LeanPlan& lp) { return lp.ns > 1 ? 2 : 1; }
-size_t lean_slot_bytes(int ns) { return 16 + 8 + 4 + (size_t)ns * 12; }
-size_t lean_fixed_bytes(int ns) {
-    return sizeof(lean::WaveLds) * lean::NWV + sizeof(v4u) * lean::MEMO_N * (1 + ns);
-}
+int ns_of(const LeanPlan& lp) { return lp.ns; }
+size_t lean_slot_bytes(int ns) { return 2 + 16 + 8 + 4 + (size_t)ns * 12; }
+size_t lean_fixed_bytes() { return sizeof(lean::WaveLds) * lean::NWV; }
 
 uint32_t lean_slots(int ns, int grouped) {
     if (!grouped) return 0;
     uint32_t h = 2048;
-    while (h > 64 && lean_fixed_bytes(ns) + (size_t)h * lean_slot_bytes(ns) + 256 > (size_t)(160 * 1024)) h >>= 1;
+    while (h > 64 && lean_fixed_bytes() + (size_t)h * lean_slot_bytes(ns) + 512 > (size_t)(160 * 1024)) h >>= 1;
     return h;
 }
 size_t lean_lds(int ns, int grouped) {
-    return lean_fixed_bytes(ns) + (size_t)lean_slots(ns, grouped) * lean_slot_bytes(ns) + 256;
+    return lean_fixed_bytes() + (size_t)lean_slots(ns, grouped) * lean_slot_bytes(ns) + 512;
 }
 
 typedef void (*lean_fn_t)(const uint8_t*, ScanStats*, unsigned long long*, unsigned long long, uint32_t,
                           unsigned long long*, unsigned long long);
 
+template <bool G, int WM>
+lean_fn_t pick_ns(int ns) {
+    if (ns == 0) return lean::lean_kernel<G, WM, 0>;
+    return ns == 1 ? lean::lean_kernel<G, WM, 1> : lean::lean_kernel<G, WM, 2>;
+}
 template <bool G>
-lean_fn_t pick(int wm, int ns) {
-    if (wm == W_NONE) return ns <= 1 ? lean::lean_kernel<G, W_NONE, 1> : lean::lean_kernel<G, W_NONE, 2>;
-    return ns <= 1 ? lean::lean_kernel<G, W_SIMPLE, 1> : lean::lean_kernel<G, W_SIMPLE, 2>;
+lean_fn_t pick_fn(int wm, int ns) {
+    switch (wm) {
+        case lean::LW_NONE: return pick_ns<G, lean::LW_NONE>(ns);
+        case lean::LW_NUM: return pick_ns<G, lean::LW_NUM>(ns);
+        case lean::LW_STR: return pick_ns<G, lean::LW_STR>(ns);
+        default: return pick_ns<G, lean::LW_GEN>(ns);
+    }
 }
 
 }  // namespace
@@ -830,16 +981,38 @@ hipError_t cq_launch_lean(const uint8_t* g, const cq::ScanPlan* P, const cq::Gro
     LeanPlan lp;
     int wm = 0;
     if (!lean_shape(P, &lp, &wm)) return hipErrorInvalidValue;
+    if (wm == lean::LW_STR) {   // the literal's bytes (a STRING cell points at device memory)
+        const Cell& L = P->consts[P->prog[1].b];
+        uint8_t b[8] = {0, 0, 0, 0, 0, 0, 0, 0};
+        if (L.len) {
+            hipError_t e = hipMemcpyAsync(b, (const void*)(uintptr_t)L.bits, L.len, hipMemcpyDeviceToHost, s);
+            if (e == hipSuccess) e = hipStreamSynchronize(s);
+            if (e != hipSuccess) return e;
+        }
+        uint64_t x = 0;
+        for (int i = 0; i < 8; i++) x = (x << 8) | b[i];
+        lp.wstr = x;
+        bool nul = false;
+        for (uint32_t i = 0; i < L.len; i++) nul = nul || b[i] == 0;
+        if (nul) wm = lean::LW_GEN;          // strcmp stops at a NUL: the general compare decides
+    }
+    const uint64_t hi = P->range_end < P->n ? P->range_end : P->n;
+    lp.lo_ok = P->data_begin > P->range_begin ? P->data_begin : P->range_begin;
+    lp.hi_ok = hi;
+    lp.first_win = P->range_begin / lean::WS;
+    lp.last_win = (hi + lean::WS - 1) / lean::WS;
     const int ns = ns_of(lp);
     const uint32_t h = lean_slots(ns, grouped);
     const size_t lds = lean_lds(ns, grouped);
-    hipError_t e = hipMemcpyToSymbolAsync(HIP_SYMBOL(lean::c_plan), P, sizeof *P, 0, hipMemcpyHostToDevice, s);
-    if (e == hipSuccess) e = hipMemcpyToSymbolAsync(HIP_SYMBOL(lean::c_gt), gt, sizeof *gt, 0, hipMemcpyHostToDevice, s);
+    hipError_t e = hipMemcpyToSymbolAsync(HIP_SYMBOL(lean::c_gt), gt, sizeof *gt, 0, hipMemcpyHostToDevice, s);
     if (e == hipSuccess) e = hipMemcpyToSymbolAsync(HIP_SYMBOL(lean::c_lp), &lp, sizeof lp, 0, hipMemcpyHostToDevice, s);
-    if (e == hipSuccess && rt)
+    if (e == hipSuccess && rt) {
         e = hipMemcpyToSymbolAsync(HIP_SYMBOL(lean::c_rt), rt, sizeof *rt, 0, hipMemcpyHostToDevice, s);
+        if (e == hipSuccess)
+            e = hipMemcpyToSymbolAsync(HIP_SYMBOL(lean::c_plan), P, sizeof *P, 0, hipMemcpyHostToDevice, s);
+    }
     if (e != hipSuccess) return e;
-    const lean_fn_t fn = grouped ? pick<true>(wm, ns) : pick<false>(wm, ns);
+    const lean_fn_t fn = grouped ? pick_fn<true>(wm, ns) : pick_fn<false>(wm, ns);
     (void)hipFuncSetAttribute((const void*)fn, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds);
     hipLaunchKernelGGL(fn, dim3(grid), dim3(lean::LT), lds, s, g, stats, row_out, row_cap, h, slow_list, slow_cap);
     return hipGetLastError();
