@@ -133,6 +133,8 @@ def main():
     ast = C.pointer(q)
     L = cq_amd.lib()
 
+    kernel_used = [1]
+
     def step():
         if dist is None:
             tp = L.cqgpu_query(ast, (C.c_void_p * 1)(table.handle.value), 1)
@@ -143,6 +145,7 @@ def main():
             st = cq_amd.stats()
             if os.environ.get("CQ_BENCH_DEBUG"):
                 print("stats", st, file=sys.stderr)
+            kernel_used[0] = st.get("scan_kernel", 0)
             return ng, st["scan_ms"]
         blob = C.c_void_p()
         n = L.cqgpu_query_partial(ast, (C.c_void_p * 1)(table.handle.value), 1, C.byref(blob))
@@ -234,7 +237,8 @@ def main():
                 "unit": "GB/s",
                 "frac": achieved / HBM_PEAK_GBS,
                 "traffic": traffic,
-                "kernel": "cq::scan_kernel<true>",
+                "kernel": ("cq::lean::lean_kernel<true, LW_NUM, 1> (+ slow_kernel, raw_merge_kernel)"
+                           if kernel_used[0] else "cq::scan_kernel<true>"),
                 "kernel_ms": avg_scan_ms,
                 "bytes_per_launch": nbytes,
             },

@@ -44,6 +44,10 @@ hipError_t cq_launch_gather(const uint8_t* g, const ScanPlan* P, const unsigned 
                             uint32_t nrec, Cell* out, hipStream_t s);
 hipError_t cq_launch_copy_strings(const Cell* cells, uint32_t n, const unsigned long long* offs,
                                   uint8_t* out, hipStream_t s);
+cq::Cell cq_host_parse_cell(const uint8_t* text, uint32_t len);
+hipError_t cq_launch_finish(const uint8_t* g, uint64_t n, const cq::GroupOut* out, const unsigned int* count,
+                            unsigned int cap_out, const cq::FinishDesc* D, cq::Cell* cells, uint8_t* bytes,
+                            hipStream_t s);
 hipError_t cq_launch_parse_literals(const uint8_t* text, const unsigned int* offs,
                                     const unsigned int* lens, uint32_t n, Cell* out, hipStream_t s);
 hipError_t cq_launch_project(const uint8_t* g, const unsigned long long* recs, uint32_t nrec,
@@ -103,6 +107,10 @@ struct DevCtx {
     size_t ws_size = 0;
     void* pinned = nullptr;
     size_t pinned_size = 0;
+    // per-query scratch (literals, gathers, string fetches): a bump region reset at
+    // the start of every query, so the query path makes no hipMalloc / hipFree
+    uint8_t* bump = nullptr;
+    size_t bump_size = 0, bump_used = 0;
 };
 DevCtx g_ctx[64];
 
@@ -131,6 +139,42 @@ void* workspace(DevCtx& c, size_t bytes) {
     }
     return c.ws;
 }
+
+// per-query device scratch: from the context's bump region when it fits, else an
+// owned allocation freed with the object
+constexpr size_t BUMP_BYTES = 8u << 20;
+void bump_reset(DevCtx& c) { c.bump_used = 0; }
+struct Scratch {
+    uint8_t* p = nullptr;
+    bool owned = false;
+    Scratch() = default;
+    Scratch(DevCtx& c, size_t bytes) { get(c, bytes); }
+    void get(DevCtx& c, size_t bytes) {
+        release();
+        bytes = (std::max<size_t>(bytes, 16) + 255) & ~(size_t)255;
+        if (!c.bump) {
+            HIPCHECK(hipMalloc(&c.bump, BUMP_BYTES));
+            c.bump_size = BUMP_BYTES;
+            c.bump_used = 0;
+        }
+        if (c.bump_used + bytes <= c.bump_size) {
+            p = c.bump + c.bump_used;
+            c.bump_used += bytes;
+            owned = false;
+        } else {
+            HIPCHECK(hipMalloc(&p, bytes));
+            owned = true;
+        }
+    }
+    void release() {
+        if (p && owned) (void)hipFree(p);
+        p = nullptr;
+        owned = false;
+    }
+    Scratch(const Scratch&) = delete;
+    Scratch& operator=(const Scratch&) = delete;
+    ~Scratch() { release(); }
+};
 
 // owned device allocation
 struct DevBuf {
@@ -352,8 +396,8 @@ std::vector<HCell> fetch_cells(DevCtx& c, const std::vector<Cell>& cells) {
         return out;
     size_t n = cells.size();
     size_t need = n * sizeof(Cell) + n * 8 + total + 16;
-    uint8_t* d;
-    HIPCHECK(hipMalloc(&d, need));
+    Scratch sc(c, need);
+    uint8_t* d = sc.p;
     Cell* dc = (Cell*)d;
     unsigned long long* doffs = (unsigned long long*)(d + n * sizeof(Cell));
     uint8_t* dout = d + n * sizeof(Cell) + n * 8;
@@ -363,7 +407,6 @@ std::vector<HCell> fetch_cells(DevCtx& c, const std::vector<Cell>& cells) {
     std::vector<char> hb(total + 1, 0);
     if (total) HIPCHECK(hipMemcpyAsync(hb.data(), dout, total, hipMemcpyDeviceToHost, c.stream));
     HIPCHECK(hipStreamSynchronize(c.stream));
-    HIPCHECK(hipFree(d));
     for (size_t i = 0; i < n; i++)
         if (cells[i].kind == K_STR) out[i].s.assign(hb.data() + offs[i], cells[i].len);
     return out;
@@ -780,41 +823,55 @@ struct Reader {
 
 // literal cells parsed on the device with the same parser as the data
 struct Literals {
-    uint8_t* dev = nullptr;
+    Scratch dev;
     Cell* dcells = nullptr;           // device copy of `cells`
-    std::vector<Cell> cells;
-    ~Literals() { if (dev) (void)hipFree(dev); }
+    std::vector<Cell> cells;          // STRING bits: device addresses
+    std::vector<HCell> host;          // the same cells with host strings
 };
 
+// typed on the host by cell.h's parser (hostcell.cpp, the kernels' own typing
+// code); STRING literals get a device copy of their bytes for the kernels
 void parse_literals(DevCtx& c, const std::vector<std::string>& texts, Literals& L) {
     size_t n = texts.size();
-    if (L.dev) HIPCHECK(hipFree(L.dev));
-    L.dev = nullptr;
+    L.dev.release();
     L.dcells = nullptr;
     L.cells.clear();
+    L.host.clear();
     if (!n) return;
-    std::vector<unsigned int> offs(n), lens(n);
+    std::vector<size_t> offs(n);
     std::string blob;
     for (size_t i = 0; i < n; i++) {
-        offs[i] = (unsigned int)blob.size();
-        lens[i] = (unsigned int)texts[i].size();
+        offs[i] = blob.size();
         blob += texts[i];
         blob.append(16, '\0');            // strtoll/strtod stop at the C string's NUL
     }
-    size_t need = blob.size() + n * 8 + n * sizeof(Cell) + 64;
-    HIPCHECK(hipMalloc(&L.dev, need));
-    uint8_t* dtext = L.dev;
-    unsigned int* doffs = (unsigned int*)(L.dev + ((blob.size() + 15) & ~15ull));
-    unsigned int* dlens = doffs + n;
-    Cell* dcells = (Cell*)(((uintptr_t)(dlens + n) + 15) & ~(uintptr_t)15);
-    HIPCHECK(hipMemcpyAsync(dtext, blob.data(), blob.size(), hipMemcpyHostToDevice, c.stream));
-    HIPCHECK(hipMemcpyAsync(doffs, offs.data(), n * 4, hipMemcpyHostToDevice, c.stream));
-    HIPCHECK(hipMemcpyAsync(dlens, lens.data(), n * 4, hipMemcpyHostToDevice, c.stream));
-    HIPCHECK(cq_launch_parse_literals(dtext, doffs, dlens, (uint32_t)n, dcells, c.stream));
-    L.dcells = dcells;
     L.cells.resize(n);
-    HIPCHECK(hipMemcpyAsync(L.cells.data(), dcells, n * sizeof(Cell), hipMemcpyDeviceToHost, c.stream));
-    HIPCHECK(hipStreamSynchronize(c.stream));
+    L.host.resize(n);
+    bool any_str = false;
+    for (size_t i = 0; i < n; i++) {
+        const uint8_t* t = (const uint8_t*)blob.data() + offs[i];
+        Cell x = cq_host_parse_cell(t, (uint32_t)texts[i].size());
+        L.host[i].kind = x.kind;
+        L.host[i].bits = x.bits;
+        if (x.kind == K_STR) {
+            const size_t off = (size_t)((const uint8_t*)(uintptr_t)x.bits - (const uint8_t*)blob.data());
+            L.host[i].s.assign(blob.data() + off, x.len);
+            x.bits = off;                  // relocated to the device copy below
+            any_str = true;
+        }
+        L.cells[i] = x;
+    }
+    const size_t cell_off = (blob.size() + 15) & ~(size_t)15;
+    L.dev.get(c, cell_off + n * sizeof(Cell));
+    for (size_t i = 0; i < n; i++)
+        if (L.cells[i].kind == K_STR) L.cells[i].bits += (uint64_t)(uintptr_t)L.dev.p;
+    std::vector<uint8_t> up(cell_off + n * sizeof(Cell), 0);
+    memcpy(up.data(), blob.data(), blob.size());
+    memcpy(up.data() + cell_off, L.cells.data(), n * sizeof(Cell));
+    (void)any_str;
+    HIPCHECK(hipMemcpyAsync(L.dev.p, up.data(), up.size(), hipMemcpyHostToDevice, c.stream));
+    L.dcells = (Cell*)(L.dev.p + cell_off);
+    HIPCHECK(hipStreamSynchronize(c.stream));   // the staging vector goes out of scope
 }
 
 // group table arena in the device workspace
@@ -916,12 +973,36 @@ std::vector<HGroup> run_aggregate(DevCtx& c, const cqgpu_table* t, Compiled& C, 
     int grid = (int)std::min<uint64_t>(std::max<uint64_t>(windows, 1), (uint64_t)c.ncu * per_cu);
     ScanStats st;
     std::vector<GroupOut> outs;
+    // what finish_kernel gathers per group: representative cells (ascending columns),
+    // MIN/MAX cells, the long-key text; STRING bytes inline up to SB
+    constexpr uint32_t SB = 48;
+    FinishDesc FD;
+    memset(&FD, 0, sizeof FD);
+    std::vector<int> rep_ord(C.rep_cols.size());
+    for (size_t i = 0; i < rep_ord.size(); i++) rep_ord[i] = (int)i;
+    std::sort(rep_ord.begin(), rep_ord.end(), [&](int a, int b) { return C.rep_cols[a] < C.rep_cols[b]; });
+    if (rep_ord.size() > (size_t)MAX_NEED) throw Ineligible{"too many representative columns"};
+    FD.ncols = (int32_t)rep_ord.size();
+    for (size_t i = 0; i < rep_ord.size(); i++) FD.cols[i] = (int16_t)C.rep_cols[rep_ord[i]];
+    FD.delim = C.P.delim;
+    FD.quote = C.P.quote;
+    FD.nacc = C.P.nacc;
+    FD.sb = SB;
+    const uint32_t ncell = (uint32_t)FD.ncols + (uint32_t)FD.nacc + 1;
+    std::vector<Cell> fcells;
+    std::vector<uint8_t> fbytes;
     uint64_t chunk = 0;          // 0: the whole table in one launch
     while (true) {
         TableArena A = make_arena(c, C.P, cap, cap / 2 + 1, (size_t)grid, cq_scan_cand_stride(&C.P, grouped));
+        const unsigned int cap_out = cap / 2 + 1;
+        Scratch fin(c, (size_t)cap_out * ncell * (sizeof(Cell) + SB) + 64);
+        Cell* dcells = (Cell*)fin.p;
+        uint8_t* dbytes = fin.p + (size_t)cap_out * ncell * sizeof(Cell);
         memset(&st, 0, sizeof st);
+        unsigned long long last_clk[8] = {0, 0, 0, 0, 0, 0, 0, 0};
         float ms_total = 0;
-        bool slow_over = false;
+        bool slow_over = false, finished = false;
+        unsigned int ng = 0;
         const uint64_t step = chunk ? chunk : std::max<uint64_t>(t->n, 1);
         for (uint64_t b = 0; b < std::max<uint64_t>(t->n, 1); b += step) {
             ScanPlan P = C.P;
@@ -935,12 +1016,19 @@ std::vector<HGroup> run_aggregate(DevCtx& c, const cqgpu_table* t, Compiled& C, 
                                     row_cap > done ? row_cap - done : 0, grouped, g2, c.stream, nullptr,
                                     A.slow_list, A.slow_cap));
             HIPCHECK(hipEventRecord(c.ev1, c.stream));
+            if (!chunk) {      // one launch: compact and finish speculatively, one sync for all
+                HIPCHECK(cq_launch_compact(&A.gt, &C.P, A.out, A.out_count, cap_out, c.stream));
+                HIPCHECK(cq_launch_finish(t->g, t->n, A.out, A.out_count, cap_out, &FD, dcells, dbytes, c.stream));
+                HIPCHECK(hipMemcpyAsync(&ng, A.out_count, 4, hipMemcpyDeviceToHost, c.stream));
+                finished = true;
+            }
             ScanStats s1;
             HIPCHECK(hipMemcpyAsync(&s1, A.stats, sizeof s1, hipMemcpyDeviceToHost, c.stream));
             HIPCHECK(hipStreamSynchronize(c.stream));
             float ms = 0;
             HIPCHECK(hipEventElapsedTime(&ms, c.ev0, c.ev1));
             ms_total += ms;
+            for (int i = 0; i < 8; i++) last_clk[i] = s1.clk[i];
             st.records += s1.records;
             st.passed += s1.passed;
             st.short_rows += s1.short_rows;
@@ -955,12 +1043,7 @@ std::vector<HGroup> run_aggregate(DevCtx& c, const cqgpu_table* t, Compiled& C, 
         g_stats.scan_ms = ms_total;
         g_stats.grid = grid;
         g_stats.scan_kernel = cq_scan_uses_lean(&C.P, 0);
-        for (int i = 0; i < 8; i++) g_clk[i] = 0;
-        {
-            ScanStats s2;
-            HIPCHECK(hipMemcpy(&s2, A.stats, sizeof s2, hipMemcpyDeviceToHost));
-            for (int i = 0; i < 8; i++) g_clk[i] = s2.clk[i];
-        }
+        for (int i = 0; i < 8; i++) g_clk[i] = last_clk[i];
         if (st.overflow >= 2)   // a bounded spin gave up: a kernel bug, never a data property
             throw HipError{st.overflow == 2 ? "scan kernel: MIN/MAX lock timeout" : "scan kernel: group insert timeout"};
         if (slow_over) {        // too many records for the general kernel's list: rescan in chunks
@@ -974,12 +1057,21 @@ std::vector<HGroup> run_aggregate(DevCtx& c, const cqgpu_table* t, Compiled& C, 
             retries++;
             continue;
         }
-        HIPCHECK(cq_launch_compact(&A.gt, &C.P, A.out, A.out_count, cap / 2 + 1, c.stream));
-        unsigned int ng = 0;
-        HIPCHECK(hipMemcpyAsync(&ng, A.out_count, 4, hipMemcpyDeviceToHost, c.stream));
-        HIPCHECK(hipStreamSynchronize(c.stream));
+        if (!finished) {
+            HIPCHECK(cq_launch_compact(&A.gt, &C.P, A.out, A.out_count, cap_out, c.stream));
+            HIPCHECK(cq_launch_finish(t->g, t->n, A.out, A.out_count, cap_out, &FD, dcells, dbytes, c.stream));
+            HIPCHECK(hipMemcpyAsync(&ng, A.out_count, 4, hipMemcpyDeviceToHost, c.stream));
+            HIPCHECK(hipStreamSynchronize(c.stream));
+        }
+        ng = std::min(ng, cap_out);
         outs.resize(ng);
-        if (ng) HIPCHECK(hipMemcpyAsync(outs.data(), A.out, ng * sizeof(GroupOut), hipMemcpyDeviceToHost, c.stream));
+        fcells.resize((size_t)ng * ncell);
+        fbytes.resize((size_t)ng * ncell * SB);
+        if (ng) {
+            HIPCHECK(hipMemcpyAsync(outs.data(), A.out, ng * sizeof(GroupOut), hipMemcpyDeviceToHost, c.stream));
+            HIPCHECK(hipMemcpyAsync(fcells.data(), dcells, fcells.size() * sizeof(Cell), hipMemcpyDeviceToHost, c.stream));
+            HIPCHECK(hipMemcpyAsync(fbytes.data(), dbytes, fbytes.size(), hipMemcpyDeviceToHost, c.stream));
+        }
         HIPCHECK(hipStreamSynchronize(c.stream));
         break;
     }
@@ -1004,71 +1096,46 @@ std::vector<HGroup> run_aggregate(DevCtx& c, const cqgpu_table* t, Compiled& C, 
         z.first = NOPOS;
         for (int a = 0; a < MAX_ACC; a++) z.extpos[a] = NOPOS;
         outs.push_back(z);
+        fcells.assign(ncell, Cell{K_NULL, 0, 0});
+        fbytes.assign((size_t)ncell * SB, 0);
     }
     // never let a kernel bug turn into an out-of-bounds gather below
     for (auto& o : outs)
         if (o.first != NOPOS && o.first >= t->n) throw HipError{"scan kernel: group first-row offset out of range"};
+    // host cells of the finish output; STRINGs longer than SB fetched in one batch
+    std::vector<HCell> hcells(fcells.size());
+    std::vector<Cell> longs;
+    std::vector<size_t> long_at;
+    for (size_t k = 0; k < fcells.size(); k++) {
+        hcells[k].kind = fcells[k].kind;
+        hcells[k].bits = fcells[k].bits;
+        if (fcells[k].kind != K_STR) continue;
+        if (fcells[k].len <= SB) {
+            hcells[k].s.assign((const char*)fbytes.data() + k * SB, fcells[k].len);
+        } else {
+            longs.push_back(fcells[k]);
+            long_at.push_back(k);
+        }
+    }
+    if (!longs.empty()) {
+        std::vector<HCell> hl = fetch_cells(c, longs);
+        for (size_t i = 0; i < longs.size(); i++) hcells[long_at[i]] = hl[i];
+    }
     // first-appearance order (create_groups appends groups in row order)
-    std::sort(outs.begin(), outs.end(), [](const GroupOut& a, const GroupOut& b) { return a.first < b.first; });
-    // representative cells of each group's first row, and string extremes
-    std::vector<Cell> want;
-    std::vector<unsigned long long> recs;
-    for (auto& o : outs) recs.push_back(o.first);
-    std::vector<Cell> repcells;
-    if (!C.rep_cols.empty() && !recs.empty() && recs[0] != NOPOS) {
-        ScanPlan RP;
-        memset(&RP, 0, sizeof RP);
-        RP.delim = C.P.delim;
-        RP.quote = C.P.quote;
-        RP.n = C.P.n;
-        std::vector<int> cols = C.rep_cols;
-        std::vector<int> ord(cols.size());
-        for (size_t i = 0; i < ord.size(); i++) ord[i] = (int)i;
-        std::sort(ord.begin(), ord.end(), [&](int a, int b) { return cols[a] < cols[b]; });
-        RP.nneed = (int)cols.size();
-        for (int i = 0; i < RP.nneed; i++) RP.need_col[i] = (int16_t)cols[ord[i]];
-        size_t nr = recs.size();
-        uint8_t* d;
-        HIPCHECK(hipMalloc(&d, nr * 8 + nr * RP.nneed * sizeof(Cell) + 64));
-        unsigned long long* drecs = (unsigned long long*)d;
-        Cell* dcells = (Cell*)(d + ((nr * 8 + 15) & ~15ull));
-        HIPCHECK(hipMemcpyAsync(drecs, recs.data(), nr * 8, hipMemcpyHostToDevice, c.stream));
-        HIPCHECK(cq_launch_gather(t->g, &RP, drecs, (uint32_t)nr, dcells, c.stream));
-        std::vector<Cell> got(nr * RP.nneed);
-        HIPCHECK(hipMemcpyAsync(got.data(), dcells, got.size() * sizeof(Cell), hipMemcpyDeviceToHost, c.stream));
-        HIPCHECK(hipStreamSynchronize(c.stream));
-        HIPCHECK(hipFree(d));
-        repcells.resize(nr * cols.size());
-        for (size_t g = 0; g < nr; g++)
-            for (int i = 0; i < RP.nneed; i++) repcells[g * cols.size() + ord[i]] = got[g * RP.nneed + i];
-    }
-    // one batched string fetch: group keys are not needed on the single-GPU path,
-    // representative and extreme cells are
-    std::vector<Cell> batch;
-    batch.insert(batch.end(), repcells.begin(), repcells.end());
-    for (auto& o : outs)
-        for (int a = 0; a < C.P.nacc; a++) batch.push_back(o.ext[a]);
-    // long text keys live in the table bytes (needed to merge partials across ranks)
-    for (auto& o : outs) {
-        Cell k;
-        k.kind = (o.clslen >> 16) == GK_LONG ? K_STR : K_NULL;
-        k.len = o.clslen & 0xffff;
-        k.bits = o.w0;
-        batch.push_back(k);
-    }
-    std::vector<HCell> hb = fetch_cells(c, batch);
-    size_t nrep = C.rep_cols.size();
-    size_t base_ext = repcells.size();
-    size_t base_key = base_ext + outs.size() * C.P.nacc;
-    for (size_t g = 0; g < outs.size(); g++) {
-        const GroupOut& o = outs[g];
+    std::vector<uint32_t> order(outs.size());
+    for (size_t i = 0; i < order.size(); i++) order[i] = (uint32_t)i;
+    std::sort(order.begin(), order.end(), [&](uint32_t a, uint32_t b) { return outs[a].first < outs[b].first; });
+    const size_t nrep = C.rep_cols.size();
+    for (uint32_t gi : order) {
+        const GroupOut& o = outs[gi];
+        const HCell* cs = hcells.data() + (size_t)gi * ncell;
         HGroup h;
         h.kcls = o.clslen >> 16;
         h.klen = o.clslen & 0xffff;
         h.kw0 = o.w0;
         h.kw1 = o.w1;
         if (h.kcls == GK_LONG) {
-            h.kbytes = hb[base_key + g].s;
+            h.kbytes = cs[FD.ncols + FD.nacc].s;
         } else if (h.kcls == GK_STR) {
             for (uint32_t i = 0; i < h.klen; i++)
                 h.kbytes.push_back((char)((i < 8 ? o.w0 >> (8 * i) : o.w1 >> (8 * (i - 8))) & 0xff));
@@ -1079,14 +1146,12 @@ std::vector<HGroup> run_aggregate(DevCtx& c, const cqgpu_table* t, Compiled& C, 
             h.sum[a] = o.sum[a];
             h.num[a] = o.num[a];
             if (a < C.P.nacc) {
-                h.ext[a] = hb[base_ext + g * C.P.nacc + a];
+                h.ext[a] = cs[FD.ncols + a];
                 h.extpos[a] = o.extpos[a] == NOPOS ? NOPOS : o.extpos[a] + t->base_offset;
             }
         }
-        if (!repcells.empty())
-            for (size_t r = 0; r < nrep; r++) h.reps.push_back(hb[g * nrep + r]);
-        else
-            h.reps.resize(nrep);
+        h.reps.resize(nrep);
+        for (size_t i = 0; i < rep_ord.size(); i++) h.reps[rep_ord[i]] = cs[i];
         groups.push_back(std::move(h));
     }
     return groups;
@@ -1123,7 +1188,7 @@ cq_table* build_groups(const Compiled& C, const std::vector<HGroup>& groups, con
     r->nrows = r->row_capacity = (int)groups.size();
     r->rows = (cq_row*)malloc(sizeof(cq_row) * std::max<size_t>(groups.size(), 1));
     std::vector<HCell> litcells;
-    if (!L.cells.empty()) litcells = fetch_cells(c, L.cells);
+    if (!L.cells.empty()) litcells = L.host;
     for (size_t g = 0; g < groups.size(); g++) {
         const HGroup& h = groups[g];
         cq_row& row = r->rows[g];
@@ -1255,7 +1320,7 @@ void apply_having(DevCtx& c, cq_table* r, cq_node* having, cq_node* sel) {
         for (auto* n : lits) texts.push_back(n->u.text ? n->u.text : "");
         Literals L;
         parse_literals(c, texts, L);
-        std::vector<HCell> hc = fetch_cells(c, L.cells);
+        std::vector<HCell> hc = L.host;
         for (size_t i = 0; i < lits.size(); i++) H.lit.emplace_back(lits[i], hc[i]);
     }
     int w = 0;
@@ -1563,6 +1628,7 @@ bool is_row_query(cq_node* q) {      // evaluator.c:259-262: neither GROUP BY no
 }
 
 cq_table* query_impl(cq_node* q, cqgpu_table* const* tables, int ntables) {
+    bump_reset(ctx());
     DevCtx& c = ctx();
     if (ntables < 1 || !tables[0]) throw HipError{"no table"};
     const cqgpu_table* t = tables[0];
@@ -1934,6 +2000,7 @@ size_t cqgpu_query_partial(cq_node* q, cqgpu_table* const* tables, int ntables, 
     g_err.clear();
     try {
         DevCtx& c = ctx();
+        bump_reset(c);
         if (ntables < 1 || !tables[0]) throw HipError{"no table"};
         const cqgpu_table* t = tables[0];
         check_plan_shape(q, t);

@@ -115,10 +115,12 @@ struct LeanPlan {
     uint32_t delim, quote;
 };
 
-__constant__ ScanPlan c_plan;        // raw_merge_kernel
-__constant__ GroupTable c_gt;        // canonical keys (shared with slow_kernel)
-__constant__ GroupTable c_rt;        // raw-byte keys (GK_RAW): block flushes and LDS spills
-__constant__ LeanPlan c_lp;
+// kernel arguments (kernarg segment: no per-launch symbol copies)
+struct LeanArgs {
+    LeanPlan lp;
+    GroupTable gt;       // canonical keys (shared with slow_kernel)
+    GroupTable rt;       // raw-byte keys (GK_RAW): block flushes and LDS spills
+};
 
 constexpr uint32_t GK_RAW = 6;       // raw field bytes as key (cell.h GK_* never produce 6)
 __device__ __forceinline__ GKey raw_key(uint32_t len, uint64_t w0, uint64_t w1) {
@@ -406,10 +408,10 @@ __global__ __launch_bounds__(LT) void lean_kernel(const uint8_t* __restrict__ g,
                                                   unsigned long long* __restrict__ row_out,
                                                   unsigned long long row_cap, uint32_t lds_h,
                                                   unsigned long long* __restrict__ slow_list,
-                                                  unsigned long long slow_cap) {
-    const LeanPlan& LP = c_lp;
-    const GroupTable& gt = c_gt;
-    const GroupTable& rt = c_rt;
+                                                  unsigned long long slow_cap, const LeanArgs args) {
+    const LeanPlan& LP = args.lp;
+    const GroupTable& gt = args.gt;
+    const GroupTable& rt = args.rt;
     extern __shared__ __align__(16) uint8_t smem[];
     uint8_t* q = smem;
     WaveLds* waves = (WaveLds*)carve(q, sizeof(WaveLds) * NWV);
@@ -820,10 +822,8 @@ __global__ __launch_bounds__(LT) void lean_kernel(const uint8_t* __restrict__ g,
 // Raw keys -> canonical keys: every distinct raw GROUP BY field is typed once by
 // the general parser (infer_type + parse_value, then create_groups' key text,
 // evaluator_aggregates.c:122-141) and its partial state merged into c_gt.
-__global__ __launch_bounds__(256) void raw_merge_kernel(ScanStats* __restrict__ stats) {
-    const GroupTable& gt = c_gt;
-    const GroupTable& rt = c_rt;
-    const ScanPlan& P = c_plan;
+__global__ __launch_bounds__(256) void raw_merge_kernel(ScanStats* __restrict__ stats, const GroupTable gt,
+                                                        const GroupTable rt, int nacc) {
     __shared__ __align__(16) uint8_t buf[256 * 32];
     const uint32_t i = blockIdx.x * 256 + threadIdx.x;
     if (i >= rt.cap || rt.tag[i] < 2) return;
@@ -832,7 +832,7 @@ __global__ __launch_bounds__(256) void raw_merge_kernel(ScanStats* __restrict__ 
     if (gi < 0) return;
     atomicAdd(&gt.cnt[gi], rt.cnt[i]);
     atomicMin(&gt.first[gi], rt.first[i]);
-    for (int a = 0; a < P.nacc; a++) {
+    for (int a = 0; a < nacc; a++) {
         const unsigned long long n = rt.num[a][i];
         if (n) {
             atomicAdd(&gt.sum[a][gi], rt.sum[a][i]);
@@ -932,7 +932,7 @@ size_t lean_lds(int ns, int grouped) {
 }
 
 typedef void (*lean_fn_t)(const uint8_t*, ScanStats*, unsigned long long*, unsigned long long, uint32_t,
-                          unsigned long long*, unsigned long long);
+                          unsigned long long*, unsigned long long, const lean::LeanArgs);
 
 template <bool G, int WM>
 lean_fn_t pick_ns(int ns) {
@@ -1004,23 +1004,22 @@ hipError_t cq_launch_lean(const uint8_t* g, const cq::ScanPlan* P, const cq::Gro
     const int ns = ns_of(lp);
     const uint32_t h = lean_slots(ns, grouped);
     const size_t lds = lean_lds(ns, grouped);
-    hipError_t e = hipMemcpyToSymbolAsync(HIP_SYMBOL(lean::c_gt), gt, sizeof *gt, 0, hipMemcpyHostToDevice, s);
-    if (e == hipSuccess) e = hipMemcpyToSymbolAsync(HIP_SYMBOL(lean::c_lp), &lp, sizeof lp, 0, hipMemcpyHostToDevice, s);
-    if (e == hipSuccess && rt) {
-        e = hipMemcpyToSymbolAsync(HIP_SYMBOL(lean::c_rt), rt, sizeof *rt, 0, hipMemcpyHostToDevice, s);
-        if (e == hipSuccess)
-            e = hipMemcpyToSymbolAsync(HIP_SYMBOL(lean::c_plan), P, sizeof *P, 0, hipMemcpyHostToDevice, s);
-    }
-    if (e != hipSuccess) return e;
+    lean::LeanArgs args;
+    memset(&args, 0, sizeof args);
+    args.lp = lp;
+    args.gt = *gt;
+    if (rt) args.rt = *rt;
     const lean_fn_t fn = grouped ? pick_fn<true>(wm, ns) : pick_fn<false>(wm, ns);
     (void)hipFuncSetAttribute((const void*)fn, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds);
-    hipLaunchKernelGGL(fn, dim3(grid), dim3(lean::LT), lds, s, g, stats, row_out, row_cap, h, slow_list, slow_cap);
+    hipLaunchKernelGGL(fn, dim3(grid), dim3(lean::LT), lds, s, g, stats, row_out, row_cap, h, slow_list, slow_cap,
+                       args);
     return hipGetLastError();
 }
 
 // raw-key table -> canonical table (after cq_launch_lean of a grouped plan)
-hipError_t cq_launch_raw_merge(const cq::GroupTable* rt, cq::ScanStats* stats, hipStream_t s) {
-    hipLaunchKernelGGL(lean::raw_merge_kernel, dim3((rt->cap + 255) / 256), dim3(256), 0, s, stats);
+hipError_t cq_launch_raw_merge(const cq::GroupTable* gt, const cq::GroupTable* rt, int nacc, cq::ScanStats* stats,
+                               hipStream_t s) {
+    hipLaunchKernelGGL(lean::raw_merge_kernel, dim3((rt->cap + 255) / 256), dim3(256), 0, s, stats, *gt, *rt, nacc);
     return hipGetLastError();
 }
 

@@ -77,6 +77,16 @@ struct ProjDesc {
     uint32_t quote;
 };
 
+// finish_kernel (scan.hip): what to gather for every compacted group
+struct FinishDesc {
+    int16_t cols[MAX_NEED];   // representative columns, ascending
+    int32_t ncols;
+    uint32_t delim;
+    uint32_t quote;
+    int32_t nacc;
+    uint32_t sb;              // inline STRING bytes per cell
+};
+
 // scan statistics written by the kernel (one per launch)
 struct ScanStats {
     unsigned long long records;     // data records seen

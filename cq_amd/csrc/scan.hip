@@ -1239,6 +1239,41 @@ __global__ __launch_bounds__(256) void project_kernel(const uint8_t* __restrict_
 }
 
 // string bytes of cells -> packed host-visible buffer
+// After compaction, per group: the representative cells of its first row
+// (build_aggregated_result's non-aggregate columns, evaluator_aggregates.c:679-689),
+// its MIN/MAX cells and its long-key text, with the first `sb` bytes of every
+// STRING inline -- so the host fetches a whole aggregate result in one copy.
+__global__ void finish_kernel(const uint8_t* __restrict__ g, uint64_t n, const GroupOut* __restrict__ out,
+                              const unsigned int* __restrict__ count, unsigned int cap_out, FinishDesc D,
+                              Cell* __restrict__ cells, uint8_t* __restrict__ bytes) {
+    const uint32_t ncell = (uint32_t)(D.ncols + D.nacc + 1);
+    const uint32_t i = blockIdx.x * blockDim.x + threadIdx.x;
+    const uint32_t ng = *count < cap_out ? *count : cap_out;
+    if (i >= ng) return;
+    Cell* cs = cells + (size_t)i * ncell;
+    const unsigned long long first = out[i].first;
+    if (D.ncols) {
+        if (first != NOPOS && first < n) {
+            parse_cols_out(g + first, D.cols, D.ncols, D.delim, D.quote, cs, 1);
+        } else {
+            for (int k = 0; k < D.ncols; k++) cs[k] = cell_null();
+        }
+    }
+    for (int a = 0; a < D.nacc; a++) cs[D.ncols + a] = out[i].ext[a];
+    Cell kc = cell_null();
+    const uint32_t cl = out[i].clslen;
+    if ((cl >> 16) == GK_LONG) { kc.kind = K_STR; kc.len = cl & 0xffff; kc.bits = out[i].w0; }
+    cs[D.ncols + D.nacc] = kc;
+    for (uint32_t k = 0; k < ncell; k++) {
+        const Cell c = cs[k];
+        if (c.kind != K_STR) continue;
+        const uint8_t* src = (const uint8_t*)(uintptr_t)c.bits;
+        uint8_t* dst = bytes + ((size_t)i * ncell + k) * D.sb;
+        const uint32_t m = c.len < D.sb ? c.len : D.sb;
+        for (uint32_t j = 0; j < m; j++) dst[j] = src[j];
+    }
+}
+
 __global__ void copy_strings_kernel(const Cell* __restrict__ cells, uint32_t n,
                                     const unsigned long long* __restrict__ offs,
                                     uint8_t* __restrict__ out) {
@@ -1340,7 +1375,8 @@ hipError_t cq_launch_lean(const uint8_t* g, const cq::ScanPlan* P, const cq::Gro
                           const cq::GroupTable* rt, cq::ScanStats* stats, unsigned long long* row_out,
                           unsigned long long row_cap, int grouped, int grid, hipStream_t s,
                           unsigned long long* slow_list, unsigned long long slow_cap);
-hipError_t cq_launch_raw_merge(const cq::GroupTable* rt, cq::ScanStats* stats, hipStream_t s);
+hipError_t cq_launch_raw_merge(const cq::GroupTable* gt, const cq::GroupTable* rt, int nacc, cq::ScanStats* stats,
+                               hipStream_t s);
 
 // cqgpu_set_scan_kernel(1) or CQ_SCAN_KERNEL=general: scan_kernel for every plan
 // (A/B runs, parity tests of both kernels)
@@ -1404,7 +1440,7 @@ hipError_t cq_launch_scan(const uint8_t* g, const cq::ScanPlan* P, const cq::Gro
                 hipLaunchKernelGGL(cq::slow_kernel<false>, dim3(256), dim3(256), 0, s, g, stats, row_out, row_cap,
                                    cells_out, slow_list, slow_cap);
             e = hipGetLastError();
-            if (e == hipSuccess && grouped) e = cq_launch_raw_merge(rt, stats, s);
+            if (e == hipSuccess && grouped) e = cq_launch_raw_merge(gt, rt, P->nacc, stats, s);
             return e;
         }
     }
@@ -1463,6 +1499,14 @@ hipError_t cq_launch_project(const uint8_t* g, const unsigned long long* recs, u
     if (!nrec) return hipSuccess;
     hipLaunchKernelGGL(cq::project_kernel, dim3((nrec + 255) / 256), dim3(256), 0, s, g, recs, nrec, *D, scratch,
                        out);
+    return hipGetLastError();
+}
+
+hipError_t cq_launch_finish(const uint8_t* g, uint64_t n, const cq::GroupOut* out, const unsigned int* count,
+                            unsigned int cap_out, const cq::FinishDesc* D, cq::Cell* cells, uint8_t* bytes,
+                            hipStream_t s) {
+    hipLaunchKernelGGL(cq::finish_kernel, dim3((cap_out + 127) / 128), dim3(128), 0, s, g, n, out, count, cap_out, *D,
+                       cells, bytes);
     return hipGetLastError();
 }
 
