@@ -45,6 +45,41 @@ hipError_t cq_launch_gather(const uint8_t* g, const ScanPlan* P, const unsigned 
 hipError_t cq_launch_copy_strings(const Cell* cells, uint32_t n, const unsigned long long* offs,
                                   uint8_t* out, hipStream_t s);
 cq::Cell cq_host_parse_cell(const uint8_t* text, uint32_t len);
+hipError_t cq_launch_cells(const uint8_t* g, const unsigned long long* recs, uint32_t n, const cq::ColsDesc* D,
+                           cq::Cell* out, hipStream_t s);
+hipError_t cq_launch_join_code(const cq::Cell* cells, uint32_t stride, uint32_t kcol, uint32_t n,
+                               unsigned long long* codes, uint32_t* cls, uint32_t* idx, unsigned int* per_class,
+                               hipStream_t s);
+hipError_t cq_launch_gather_codes(const unsigned long long* codes, const uint32_t* idx, uint32_t n,
+                                  unsigned long long* out, hipStream_t s);
+hipError_t cq_launch_join_count(const cq::Cell* L, uint32_t ls, uint32_t lk, uint32_t nL, const cq::JoinRight* J,
+                                uint32_t* lo, unsigned long long* cnt, hipStream_t s);
+hipError_t cq_launch_join_emit(const cq::Cell* L, uint32_t ls, uint32_t lk, uint32_t nL, const cq::JoinRight* J,
+                               const uint32_t* lo, const unsigned long long* cnt, const unsigned long long* offs,
+                               uint2* pairs, hipStream_t s);
+hipError_t cq_sort_classes(void* temp, size_t* temp_bytes, const unsigned int* kin, unsigned int* kout,
+                           const unsigned int* vin, unsigned int* vout, size_t n, hipStream_t s);
+hipError_t cq_sort_codes_seg(void* temp, size_t* temp_bytes, const unsigned long long* kin, unsigned long long* kout,
+                             const unsigned int* vin, unsigned int* vout, size_t n, const int* seg_begin,
+                             const int* seg_end, int nseg, hipStream_t s);
+hipError_t cq_launch_join_agg(const uint2* pairs, unsigned long long np, const cq::JoinMap* M, const cq::Cell* L,
+                              const cq::Cell* R, const cq::ScanPlan* P, const cq::GroupTable* gt,
+                              cq::ScanStats* stats, int grouped, hipStream_t s);
+hipError_t cq_launch_join_filter(const uint2* pairs, unsigned long long np, const cq::JoinMap* M, const cq::Cell* L,
+                                 const cq::Cell* R, const cq::ScanPlan* P, unsigned int* flags, hipStream_t s);
+hipError_t cq_launch_join_project(const uint2* pairs, unsigned long long np, const unsigned int* flags,
+                                  const unsigned int* pos, unsigned long long lo, uint32_t m, const cq::JoinMap* M,
+                                  const cq::Cell* L, const cq::Cell* R, const cq::Insn* code, const uint32_t* off,
+                                  int nout, const cq::Cell* consts, cq::Cell* scratch, cq::Cell* out, hipStream_t s);
+hipError_t cq_launch_join_finish(const cq::GroupOut* out, const unsigned int* count, unsigned int cap_out,
+                                 const uint2* pairs, const cq::JoinMap* M, const cq::Cell* L, const cq::Cell* R,
+                                 int nacc, uint32_t sb, cq::Cell* cells, uint8_t* bytes, hipStream_t s);
+hipError_t cq_sort_codes(void* temp, size_t* temp_bytes, const unsigned long long* kin, unsigned long long* kout,
+                         const unsigned int* vin, unsigned int* vout, size_t n, hipStream_t s);
+hipError_t cq_excl_sum_u64(void* temp, size_t* temp_bytes, const unsigned long long* in, unsigned long long* out,
+                           size_t n, hipStream_t s);
+hipError_t cq_excl_sum_u32(void* temp, size_t* temp_bytes, const unsigned int* in, unsigned int* out, size_t n,
+                           hipStream_t s);
 hipError_t cq_launch_finish(const uint8_t* g, uint64_t n, const cq::GroupOut* out, const unsigned int* count,
                             unsigned int cap_out, const cq::FinishDesc* D, cq::Cell* cells, uint8_t* bytes,
                             hipStream_t s);
@@ -955,6 +990,81 @@ double now_ms() {
     return std::chrono::duration<double, std::milli>(std::chrono::steady_clock::now().time_since_epoch()).count();
 }
 
+// compacted groups + finish output -> host groups in first-appearance order
+// (create_groups appends groups in row order); `limit`: first positions are below it
+std::vector<HGroup> make_groups(DevCtx& c, const Compiled& C, uint64_t limit, uint64_t base_offset,
+                                std::vector<GroupOut>& outs, std::vector<Cell>& fcells, std::vector<uint8_t>& fbytes,
+                                int nrep_sorted, const std::vector<int>& rep_ord, uint32_t SB) {
+    std::vector<HGroup> groups;
+    const uint32_t ncell = (uint32_t)nrep_sorted + (uint32_t)C.P.nacc + 1;
+    // single group: always present (evaluator.c:232-247), even with no rows
+    if (!C.grouped && outs.empty()) {
+        GroupOut z;
+        memset(&z, 0, sizeof z);
+        z.first = NOPOS;
+        for (int a = 0; a < MAX_ACC; a++) z.extpos[a] = NOPOS;
+        outs.push_back(z);
+        fcells.assign(ncell, Cell{K_NULL, 0, 0});
+        fbytes.assign((size_t)ncell * SB, 0);
+    }
+    // never let a kernel bug turn into an out-of-bounds gather below
+    for (auto& o : outs)
+        if (o.first != NOPOS && o.first >= limit) throw HipError{"scan kernel: group first-row offset out of range"};
+    // host cells of the finish output; STRINGs longer than SB fetched in one batch
+    std::vector<HCell> hcells(fcells.size());
+    std::vector<Cell> longs;
+    std::vector<size_t> long_at;
+    for (size_t k = 0; k < fcells.size(); k++) {
+        hcells[k].kind = fcells[k].kind;
+        hcells[k].bits = fcells[k].bits;
+        if (fcells[k].kind != K_STR) continue;
+        if (fcells[k].len <= SB) {
+            hcells[k].s.assign((const char*)fbytes.data() + k * SB, fcells[k].len);
+        } else {
+            longs.push_back(fcells[k]);
+            long_at.push_back(k);
+        }
+    }
+    if (!longs.empty()) {
+        std::vector<HCell> hl = fetch_cells(c, longs);
+        for (size_t i = 0; i < longs.size(); i++) hcells[long_at[i]] = hl[i];
+    }
+    // first-appearance order (create_groups appends groups in row order)
+    std::vector<uint32_t> order(outs.size());
+    for (size_t i = 0; i < order.size(); i++) order[i] = (uint32_t)i;
+    std::sort(order.begin(), order.end(), [&](uint32_t a, uint32_t b) { return outs[a].first < outs[b].first; });
+    const size_t nrep = C.rep_cols.size();
+    for (uint32_t gi : order) {
+        const GroupOut& o = outs[gi];
+        const HCell* cs = hcells.data() + (size_t)gi * ncell;
+        HGroup h;
+        h.kcls = o.clslen >> 16;
+        h.klen = o.clslen & 0xffff;
+        h.kw0 = o.w0;
+        h.kw1 = o.w1;
+        if (h.kcls == GK_LONG) {
+            h.kbytes = cs[nrep_sorted + C.P.nacc].s;
+        } else if (h.kcls == GK_STR) {
+            for (uint32_t i = 0; i < h.klen; i++)
+                h.kbytes.push_back((char)((i < 8 ? o.w0 >> (8 * i) : o.w1 >> (8 * (i - 8))) & 0xff));
+        }
+        h.cnt = o.cnt;
+        h.first = o.first == NOPOS ? NOPOS : o.first + base_offset;
+        for (int a = 0; a < MAX_ACC; a++) {
+            h.sum[a] = o.sum[a];
+            h.num[a] = o.num[a];
+            if (a < C.P.nacc) {
+                h.ext[a] = cs[nrep_sorted + a];
+                h.extpos[a] = o.extpos[a] == NOPOS ? NOPOS : o.extpos[a] + base_offset;
+            }
+        }
+        h.reps.resize(nrep);
+        for (size_t i = 0; i < rep_ord.size(); i++) h.reps[rep_ord[i]] = cs[i];
+        groups.push_back(std::move(h));
+    }
+    return groups;
+}
+
 // run the fused scan (with regrowth on overflow) and return the groups
 // row_out (optional): offsets of the records passing WHERE, unordered; entries
 // past row_cap are counted in ScanStats.rows_emitted but not written
@@ -1089,72 +1199,7 @@ std::vector<HGroup> run_aggregate(DevCtx& c, const cqgpu_table* t, Compiled& C, 
         unsigned m = st.acc_classes[a];
         if (m & (m - 1)) throw Ineligible{"MIN/MAX over a column mixing numbers, strings and dates"};
     }
-    // single group: always present (evaluator.c:232-247), even with no rows
-    if (!C.grouped && outs.empty()) {
-        GroupOut z;
-        memset(&z, 0, sizeof z);
-        z.first = NOPOS;
-        for (int a = 0; a < MAX_ACC; a++) z.extpos[a] = NOPOS;
-        outs.push_back(z);
-        fcells.assign(ncell, Cell{K_NULL, 0, 0});
-        fbytes.assign((size_t)ncell * SB, 0);
-    }
-    // never let a kernel bug turn into an out-of-bounds gather below
-    for (auto& o : outs)
-        if (o.first != NOPOS && o.first >= t->n) throw HipError{"scan kernel: group first-row offset out of range"};
-    // host cells of the finish output; STRINGs longer than SB fetched in one batch
-    std::vector<HCell> hcells(fcells.size());
-    std::vector<Cell> longs;
-    std::vector<size_t> long_at;
-    for (size_t k = 0; k < fcells.size(); k++) {
-        hcells[k].kind = fcells[k].kind;
-        hcells[k].bits = fcells[k].bits;
-        if (fcells[k].kind != K_STR) continue;
-        if (fcells[k].len <= SB) {
-            hcells[k].s.assign((const char*)fbytes.data() + k * SB, fcells[k].len);
-        } else {
-            longs.push_back(fcells[k]);
-            long_at.push_back(k);
-        }
-    }
-    if (!longs.empty()) {
-        std::vector<HCell> hl = fetch_cells(c, longs);
-        for (size_t i = 0; i < longs.size(); i++) hcells[long_at[i]] = hl[i];
-    }
-    // first-appearance order (create_groups appends groups in row order)
-    std::vector<uint32_t> order(outs.size());
-    for (size_t i = 0; i < order.size(); i++) order[i] = (uint32_t)i;
-    std::sort(order.begin(), order.end(), [&](uint32_t a, uint32_t b) { return outs[a].first < outs[b].first; });
-    const size_t nrep = C.rep_cols.size();
-    for (uint32_t gi : order) {
-        const GroupOut& o = outs[gi];
-        const HCell* cs = hcells.data() + (size_t)gi * ncell;
-        HGroup h;
-        h.kcls = o.clslen >> 16;
-        h.klen = o.clslen & 0xffff;
-        h.kw0 = o.w0;
-        h.kw1 = o.w1;
-        if (h.kcls == GK_LONG) {
-            h.kbytes = cs[FD.ncols + FD.nacc].s;
-        } else if (h.kcls == GK_STR) {
-            for (uint32_t i = 0; i < h.klen; i++)
-                h.kbytes.push_back((char)((i < 8 ? o.w0 >> (8 * i) : o.w1 >> (8 * (i - 8))) & 0xff));
-        }
-        h.cnt = o.cnt;
-        h.first = o.first == NOPOS ? NOPOS : o.first + t->base_offset;
-        for (int a = 0; a < MAX_ACC; a++) {
-            h.sum[a] = o.sum[a];
-            h.num[a] = o.num[a];
-            if (a < C.P.nacc) {
-                h.ext[a] = cs[FD.ncols + a];
-                h.extpos[a] = o.extpos[a] == NOPOS ? NOPOS : o.extpos[a] + t->base_offset;
-            }
-        }
-        h.reps.resize(nrep);
-        for (size_t i = 0; i < rep_ord.size(); i++) h.reps[rep_ord[i]] = cs[i];
-        groups.push_back(std::move(h));
-    }
-    return groups;
+    return make_groups(c, C, t->n, t->base_offset, outs, fcells, fbytes, FD.ncols, rep_ord, SB);
 }
 
 // ------------------------------------------------------------------ result tables
@@ -1609,13 +1654,357 @@ cq_table* run_rows(DevCtx& c, const cqgpu_table* t, Compiled& C, RowPlan& R, cq_
     return r;
 }
 
+void check_plan_shape(cq_node* q, const cqgpu_table* t, bool join_ok);
+bool is_row_query(cq_node* q);
+
+// ------------------------------------------------------------------ INNER JOIN
+// process_joins + perform_join (reference evaluator_joins.c:237-274, :63-181) for
+// one INNER JOIN with an `ident = ident` ON: both sides' needed columns parsed on
+// the device, the right side sorted by key code, (l, r) pairs in nested-loop
+// order, then WHERE / GROUP BY / aggregates or the projection over the pairs.
+
+// every data record of t, file order (csv_load's rows)
+uint32_t all_records(DevCtx& c, const cqgpu_table* t, DevBuf& out) {
+    Compiled C;
+    memset(&C.P, 0, sizeof C.P);
+    C.P.group_slot = -1;
+    C.P.delim = (uint8_t)t->cfg.delimiter;
+    C.P.quote = (uint8_t)t->cfg.quote;
+    C.P.n = t->n;
+    C.P.data_begin = t->data_begin;
+    C.P.range_end = t->n;
+    Literals L;
+    ScanStats st;
+    unsigned long long cap = std::max<unsigned long long>(t->n / 2 + 2, 16);
+    DevBuf rows(cap * 8);
+    (void)run_aggregate(c, t, C, L, &st, rows.as<unsigned long long>(), cap);
+    const unsigned long long n = st.rows_emitted;
+    if (n > cap) throw HipError{"join: record count exceeds the offset buffer"};
+    if (n >= (1ull << 32)) throw Ineligible{"join side over 2^32 rows"};
+    DevBuf sorted(n * 8);
+    if (n > 1) {
+        int bits = 1;
+        while (bits < 64 && (1ull << bits) <= t->n) bits++;
+        size_t tb = 0;
+        HIPCHECK(cq_sort_offsets(nullptr, &tb, rows.as<unsigned long long>(), sorted.as<unsigned long long>(), n, bits,
+                                 c.stream));
+        DevBuf temp(tb);
+        HIPCHECK(cq_sort_offsets(temp.p, &tb, rows.as<unsigned long long>(), sorted.as<unsigned long long>(), n, bits,
+                                 c.stream));
+    } else if (n == 1) {
+        HIPCHECK(hipMemcpyAsync(sorted.p, rows.p, 8, hipMemcpyDeviceToDevice, c.stream));
+    }
+    std::swap(out.p, sorted.p);
+    return (uint32_t)n;
+}
+
+// join_match's column lookup (evaluator_joins.c:40-60 via resolve_column): the
+// name is looked up in its own side's table, else by alias in either table --
+// and the value is then read from its own side's row at that index
+int join_on_index(const char* name, const cqgpu_table* own, const cqgpu_table* L, const char* la,
+                  const cqgpu_table* R, const char* ra) {
+    if (!name) return -1;
+    int idx = col_index(own, name);
+    if (idx >= 0) return idx;
+    const char* dot = strchr(name, '.');
+    if (!dot) return -1;
+    std::string al(name, (size_t)(dot - name));
+    if (!strcasecmp(la, al.c_str())) return col_index(L, dot + 1);
+    if (!strcasecmp(ra, al.c_str())) return col_index(R, dot + 1);
+    return -1;
+}
+
+struct JoinSide {
+    DevBuf recs, cells;
+    uint32_t n = 0;
+    std::vector<int> cols;            // CSV columns parsed, ascending
+    int slot(int col) const { return (int)(std::find(cols.begin(), cols.end(), col) - cols.begin()); }
+};
+
+void load_side(DevCtx& c, const cqgpu_table* t, JoinSide& S) {
+    std::sort(S.cols.begin(), S.cols.end());
+    S.cols.erase(std::unique(S.cols.begin(), S.cols.end()), S.cols.end());
+    if ((int)S.cols.size() > MAX_NEED) throw Ineligible{"join: more than 8 columns of one side"};
+    S.n = all_records(c, t, S.recs);
+    ColsDesc D;
+    memset(&D, 0, sizeof D);
+    D.ncols = (int)S.cols.size();
+    for (int k = 0; k < D.ncols; k++) D.cols[k] = (int16_t)S.cols[k];
+    D.delim = (uint8_t)t->cfg.delimiter;
+    D.quote = (uint8_t)t->cfg.quote;
+    DevBuf cells((size_t)std::max<uint32_t>(S.n, 1) * std::max(D.ncols, 1) * sizeof(Cell));
+    std::swap(S.cells.p, cells.p);
+    HIPCHECK(cq_launch_cells(t->g, S.recs.as<unsigned long long>(), S.n, &D, S.cells.as<Cell>(), c.stream));
+}
+
+// joined column -> (side, cell index)
+JoinMap join_map(const std::vector<int>& jcols, int nl, const JoinSide& A, const JoinSide& B) {
+    JoinMap M;
+    memset(&M, 0, sizeof M);
+    if ((int)jcols.size() > MAX_NEED) throw Ineligible{"join: too many columns"};
+    M.n = (int)jcols.size();
+    for (int k = 0; k < M.n; k++) {
+        const int j = jcols[k];
+        M.side[k] = j < nl ? 0 : 1;
+        M.col[k] = (int8_t)(j < nl ? A.slot(j) : B.slot(j - nl));
+    }
+    M.lstride = (uint32_t)std::max<size_t>(A.cols.size(), 1);
+    M.rstride = (uint32_t)std::max<size_t>(B.cols.size(), 1);
+    return M;
+}
+
+cq_table* run_join(DevCtx& c, cq_node* q, const cqgpu_table* L, const cqgpu_table* R) {
+    cq_node* jn = q->u.q.joins[0];
+    if (q->u.q.join_count != 1 || !jn || jn->kind != CQ_N_JOIN) throw Ineligible{"more than one JOIN"};
+    if (jn->u.join.kind != CQ_JOIN_INNER) throw Ineligible{"LEFT/RIGHT/FULL JOIN"};
+    if (!R) throw Ineligible{"join table failed to load"};
+    cq_node* on = jn->u.join.on;
+    if (!on) throw Ineligible{"JOIN without ON (cross product)"};
+    const char* la = (q->u.q.from && q->u.q.from->u.from.alias) ? q->u.q.from->u.from.alias : "main";
+    const char* ra = jn->u.join.alias ? jn->u.join.alias : "right";
+    const int nl = (int)L->names.size();
+    // ON operands (anything but `ident = ident` matches no pair)
+    int kl = -1, kr = -1;
+    if (on->kind == CQ_N_CONDITION && on->u.bin.op && !strcmp(on->u.bin.op, "=") && on->u.bin.lhs && on->u.bin.rhs &&
+        on->u.bin.lhs->kind == CQ_N_IDENTIFIER && on->u.bin.rhs->kind == CQ_N_IDENTIFIER) {
+        kl = join_on_index(on->u.bin.lhs->u.text, L, L, la, R, ra);
+        kr = join_on_index(on->u.bin.rhs->u.text, R, L, la, R, ra);
+    }
+    const bool keyed = kl >= 0 && kr >= 0;
+    // the joined table's schema: alias.col names (evaluator_joins.c:30-37)
+    cqgpu_table J;
+    J.cfg = L->cfg;
+    for (auto& nm : L->names) J.names.push_back(std::string(la) + "." + nm);
+    for (auto& nm : R->names) J.names.push_back(std::string(ra) + "." + nm);
+    const bool rows = is_row_query(q);
+    Compiled C;
+    RowPlan RP;
+    if (rows) compile_rows(&J, q, C, RP);
+    else compile_aggregate(&J, q, C);
+    // the columns each side parses
+    JoinSide A, B;
+    if (keyed) { A.cols.push_back(kl); B.cols.push_back(kr); }
+    auto want = [&](int j) { if (j < nl) A.cols.push_back(j); else B.cols.push_back(j - nl); };
+    for (int j : C.need_cols) want(j);
+    for (int j : C.rep_cols) want(j);
+    for (int j : RP.cols) want(j);
+    if (A.cols.empty()) A.cols.push_back(0);
+    if (B.cols.empty()) B.cols.push_back(0);
+    load_side(c, L, A);
+    load_side(c, R, B);
+    // pairs in (l, r) order
+    unsigned long long np = 0;
+    DevBuf pairs(8);
+    if (keyed && A.n && B.n) {
+        const uint32_t ls = (uint32_t)A.cols.size(), rs = (uint32_t)B.cols.size();
+        const uint32_t lk = (uint32_t)A.slot(kl), rk = (uint32_t)B.slot(kr);
+        // right side: codes and classes, rows grouped by class, then sorted by code per class
+        DevBuf rcodes((size_t)B.n * 8), rcls((size_t)B.n * 4), ridx((size_t)B.n * 4), ccls((size_t)B.n * 4),
+            ridx_c((size_t)B.n * 4), codes_c((size_t)B.n * 8), scodes((size_t)B.n * 8), sidx((size_t)B.n * 4),
+            pc(64);
+        HIPCHECK(hipMemsetAsync(pc.p, 0, 64, c.stream));
+        HIPCHECK(cq_launch_join_code(B.cells.as<Cell>(), rs, rk, B.n, rcodes.as<unsigned long long>(),
+                                     rcls.as<uint32_t>(), ridx.as<uint32_t>(), pc.as<unsigned int>(), c.stream));
+        size_t tb = 0;
+        HIPCHECK(cq_sort_classes(nullptr, &tb, rcls.as<unsigned int>(), ccls.as<unsigned int>(), ridx.as<unsigned int>(),
+                                 ridx_c.as<unsigned int>(), B.n, c.stream));
+        DevBuf temp(tb);
+        HIPCHECK(cq_sort_classes(temp.p, &tb, rcls.as<unsigned int>(), ccls.as<unsigned int>(), ridx.as<unsigned int>(),
+                                 ridx_c.as<unsigned int>(), B.n, c.stream));
+        unsigned int per[4] = {0, 0, 0, 0};
+        HIPCHECK(hipMemcpyAsync(per, pc.p, 16, hipMemcpyDeviceToHost, c.stream));
+        HIPCHECK(hipStreamSynchronize(c.stream));
+        JoinRight JR;
+        memset(&JR, 0, sizeof JR);
+        JR.seg[0] = 0;
+        for (int k = 0; k < 4; k++) JR.seg[k + 1] = JR.seg[k] + per[k];
+        int segs[8];
+        for (int k = 0; k < 4; k++) { segs[k] = (int)JR.seg[k]; segs[4 + k] = (int)JR.seg[k + 1]; }
+        int* dsegs = (int*)((uint8_t*)pc.p + 32);
+        HIPCHECK(hipMemcpyAsync(dsegs, segs, 32, hipMemcpyHostToDevice, c.stream));
+        HIPCHECK(cq_launch_gather_codes(rcodes.as<unsigned long long>(), ridx_c.as<uint32_t>(), B.n,
+                                        codes_c.as<unsigned long long>(), c.stream));
+        size_t tb1 = 0;
+        HIPCHECK(cq_sort_codes_seg(nullptr, &tb1, codes_c.as<unsigned long long>(), scodes.as<unsigned long long>(),
+                                   ridx_c.as<unsigned int>(), sidx.as<unsigned int>(), B.n, dsegs, dsegs + 4, 4,
+                                   c.stream));
+        DevBuf temp1(tb1);
+        HIPCHECK(cq_sort_codes_seg(temp1.p, &tb1, codes_c.as<unsigned long long>(), scodes.as<unsigned long long>(),
+                                   ridx_c.as<unsigned int>(), sidx.as<unsigned int>(), B.n, dsegs, dsegs + 4, 4,
+                                   c.stream));
+        HIPCHECK(hipStreamSynchronize(c.stream));        // segs (host) and the sort's inputs stay alive until here
+        JR.scodes = scodes.as<unsigned long long>();
+        JR.sidx = sidx.as<uint32_t>();
+        JR.ridx_c = ridx_c.as<uint32_t>();
+        JR.cells = B.cells.as<Cell>();
+        JR.stride = rs;
+        JR.kcol = rk;
+        DevBuf lo((size_t)A.n * 4), cnt((size_t)A.n * 8), offs((size_t)A.n * 8);
+        HIPCHECK(cq_launch_join_count(A.cells.as<Cell>(), ls, lk, A.n, &JR, lo.as<uint32_t>(),
+                                      cnt.as<unsigned long long>(), c.stream));
+        size_t tb2 = 0;
+        HIPCHECK(cq_excl_sum_u64(nullptr, &tb2, cnt.as<unsigned long long>(), offs.as<unsigned long long>(), A.n,
+                                 c.stream));
+        DevBuf temp2(tb2);
+        HIPCHECK(cq_excl_sum_u64(temp2.p, &tb2, cnt.as<unsigned long long>(), offs.as<unsigned long long>(), A.n,
+                                 c.stream));
+        unsigned long long last[2] = {0, 0};
+        HIPCHECK(hipMemcpyAsync(&last[0], offs.as<unsigned long long>() + A.n - 1, 8, hipMemcpyDeviceToHost, c.stream));
+        HIPCHECK(hipMemcpyAsync(&last[1], cnt.as<unsigned long long>() + A.n - 1, 8, hipMemcpyDeviceToHost, c.stream));
+        HIPCHECK(hipStreamSynchronize(c.stream));
+        np = last[0] + last[1];
+        DevBuf pb(np * 8);
+        std::swap(pairs.p, pb.p);
+        HIPCHECK(cq_launch_join_emit(A.cells.as<Cell>(), ls, lk, A.n, &JR, lo.as<uint32_t>(),
+                                     cnt.as<unsigned long long>(), offs.as<unsigned long long>(), pairs.as<uint2>(),
+                                     c.stream));
+        HIPCHECK(hipStreamSynchronize(c.stream));        // before the scratch buffers of this block are freed
+    }
+    g_stats.records = np;
+    Literals Lit;
+    parse_literals(c, C.lits, Lit);
+    for (size_t i = 0; i < Lit.cells.size(); i++) C.P.consts[i] = Lit.cells[i];
+    if (rows) {
+        // WHERE flags -> output positions -> projection of the window LIMIT keeps
+        const JoinMap MW = join_map(C.need_cols, nl, A, B);
+        const JoinMap MP = join_map(RP.cols, nl, A, B);
+        DevBuf flags(std::max<unsigned long long>(np, 1) * 4), pos(std::max<unsigned long long>(np, 1) * 4);
+        unsigned long long npass = 0;
+        if (np) {
+            HIPCHECK(cq_launch_join_filter(pairs.as<uint2>(), np, &MW, A.cells.as<Cell>(), B.cells.as<Cell>(), &C.P,
+                                           flags.as<unsigned int>(), c.stream));
+            size_t tb = 0;
+            HIPCHECK(cq_excl_sum_u32(nullptr, &tb, flags.as<unsigned int>(), pos.as<unsigned int>(), np, c.stream));
+            DevBuf temp(tb);
+            HIPCHECK(cq_excl_sum_u32(temp.p, &tb, flags.as<unsigned int>(), pos.as<unsigned int>(), np, c.stream));
+            unsigned int last[2] = {0, 0};
+            HIPCHECK(hipMemcpyAsync(&last[0], pos.as<unsigned int>() + np - 1, 4, hipMemcpyDeviceToHost, c.stream));
+            HIPCHECK(hipMemcpyAsync(&last[1], flags.as<unsigned int>() + np - 1, 4, hipMemcpyDeviceToHost, c.stream));
+            HIPCHECK(hipStreamSynchronize(c.stream));
+            npass = (unsigned long long)last[0] + last[1];
+        }
+        if (npass > (unsigned long long)INT32_MAX) throw Ineligible{"more than 2^31-1 result rows"};
+        g_stats.groups = npass;
+        unsigned long long lo = 0, hi = npass;
+        cq_node* sel = q->u.q.select;
+        cq_node* ob = q->u.q.order_by;
+        const bool ordered = ob && ob->kind == CQ_N_ORDER_BY && ob->u.ord.key;
+        const bool distinct = sel && sel->u.sel.distinct;
+        bool limited = false;
+        if (!ordered && !distinct && (q->u.q.limit >= 0 || q->u.q.offset >= 0)) {
+            const unsigned long long off = q->u.q.offset >= 0 ? (unsigned long long)q->u.q.offset : 0;
+            const unsigned long long lim = q->u.q.limit >= 0 ? (unsigned long long)q->u.q.limit : npass;
+            lo = std::min(off, npass);
+            hi = std::min(npass, lo + lim);
+            limited = true;
+        }
+        const int nout = (int)RP.names.size();
+        cq_table* res = new_result(RP.names);
+        const int nr = (int)(hi - lo);
+        res->nrows = res->row_capacity = nr;
+        res->rows = (cq_row*)calloc(std::max(nr, 1), sizeof(cq_row));
+        if (!nr || !nout) {
+            for (int i = 0; i < nr; i++) { res->rows[i].ncols = nout; res->rows[i].values = (cq_value*)calloc(1, sizeof(cq_value)); }
+        } else {
+            Literals LP;
+            parse_literals(c, RP.lits, LP);
+            DevBuf dcode(std::max<size_t>(RP.code.size(), 1) * sizeof(Insn)), doff(RP.off.size() * 4);
+            if (!RP.code.empty())
+                HIPCHECK(hipMemcpyAsync(dcode.p, RP.code.data(), RP.code.size() * sizeof(Insn), hipMemcpyHostToDevice, c.stream));
+            HIPCHECK(hipMemcpyAsync(doff.p, RP.off.data(), RP.off.size() * 4, hipMemcpyHostToDevice, c.stream));
+            const int batch = 1 << 20;
+            DevBuf scratch((size_t)std::min(nr, batch) * std::max(MP.n, 1) * sizeof(Cell));
+            DevBuf dout((size_t)std::min(nr, batch) * nout * sizeof(Cell));
+            std::vector<Cell> hcells;
+            for (int b = 0; b < nr; b += batch) {
+                const int m = std::min(batch, nr - b);
+                HIPCHECK(cq_launch_join_project(pairs.as<uint2>(), np, flags.as<unsigned int>(), pos.as<unsigned int>(),
+                                                lo + b, (uint32_t)m, &MP, A.cells.as<Cell>(), B.cells.as<Cell>(),
+                                                dcode.as<Insn>(), doff.as<uint32_t>(), nout, LP.dcells,
+                                                scratch.as<Cell>(), dout.as<Cell>(), c.stream));
+                hcells.resize((size_t)m * nout);
+                HIPCHECK(hipMemcpyAsync(hcells.data(), dout.p, hcells.size() * sizeof(Cell), hipMemcpyDeviceToHost, c.stream));
+                HIPCHECK(hipStreamSynchronize(c.stream));
+                append_rows(c, res, b, hcells, nout, m);
+            }
+        }
+        post_ops(c, res, q, true, limited);
+        return res;
+    }
+    // aggregates over the pairs
+    std::vector<HGroup> groups;
+    if (!C.group_missing) {
+        const int grouped = C.grouped ? 1 : 0;
+        const JoinMap MA = join_map(C.need_cols, nl, A, B);
+        const JoinMap MR = join_map(C.rep_cols, nl, A, B);
+        constexpr uint32_t SB = 48;
+        const uint32_t ncell = (uint32_t)MR.n + (uint32_t)C.P.nacc + 1;
+        uint32_t cap = grouped ? 8192 : 64;
+        std::vector<GroupOut> outs;
+        std::vector<Cell> fcells;
+        std::vector<uint8_t> fbytes;
+        ScanStats st;
+        while (true) {
+            TableArena Ar = make_arena(c, C.P, cap, cap / 2 + 1, 1, cq_scan_cand_stride(&C.P, grouped));
+            const unsigned int cap_out = cap / 2 + 1;
+            Scratch fin(c, (size_t)cap_out * ncell * (sizeof(Cell) + SB) + 64);
+            Cell* dcells = (Cell*)fin.p;
+            uint8_t* dbytes = fin.p + (size_t)cap_out * ncell * sizeof(Cell);
+            HIPCHECK(hipEventRecord(c.ev0, c.stream));
+            HIPCHECK(cq_launch_join_agg(pairs.as<uint2>(), np, &MA, A.cells.as<Cell>(), B.cells.as<Cell>(), &C.P, &Ar.gt,
+                                        Ar.stats, grouped, c.stream));
+            HIPCHECK(hipEventRecord(c.ev1, c.stream));
+            HIPCHECK(cq_launch_compact(&Ar.gt, &C.P, Ar.out, Ar.out_count, cap_out, c.stream));
+            HIPCHECK(cq_launch_join_finish(Ar.out, Ar.out_count, cap_out, pairs.as<uint2>(), &MR, A.cells.as<Cell>(),
+                                           B.cells.as<Cell>(), C.P.nacc, SB, dcells, dbytes, c.stream));
+            unsigned int ng = 0;
+            HIPCHECK(hipMemcpyAsync(&ng, Ar.out_count, 4, hipMemcpyDeviceToHost, c.stream));
+            HIPCHECK(hipMemcpyAsync(&st, Ar.stats, sizeof st, hipMemcpyDeviceToHost, c.stream));
+            HIPCHECK(hipStreamSynchronize(c.stream));
+            float ms = 0;
+            HIPCHECK(hipEventElapsedTime(&ms, c.ev0, c.ev1));
+            g_stats.scan_ms = ms;
+            if (st.overflow >= 2) throw HipError{"join aggregate: lock / insert timeout"};
+            if (st.overflow) {
+                if (cap >= (1u << 30)) throw HipError{"group table overflow"};
+                cap *= 8;
+                continue;
+            }
+            ng = std::min(ng, cap_out);
+            outs.resize(ng);
+            fcells.resize((size_t)ng * ncell);
+            fbytes.resize((size_t)ng * ncell * SB);
+            if (ng) {
+                HIPCHECK(hipMemcpyAsync(outs.data(), Ar.out, ng * sizeof(GroupOut), hipMemcpyDeviceToHost, c.stream));
+                HIPCHECK(hipMemcpyAsync(fcells.data(), dcells, fcells.size() * sizeof(Cell), hipMemcpyDeviceToHost, c.stream));
+                HIPCHECK(hipMemcpyAsync(fbytes.data(), dbytes, fbytes.size(), hipMemcpyDeviceToHost, c.stream));
+            }
+            HIPCHECK(hipStreamSynchronize(c.stream));
+            break;
+        }
+        g_stats.passed = st.passed;
+        for (int a = 0; a < C.P.nacc; a++) {
+            if (C.P.acc[a].kind == ACC_SUM) continue;
+            unsigned m = st.acc_classes[a];
+            if (m & (m - 1)) throw Ineligible{"MIN/MAX over a column mixing numbers, strings and dates"};
+        }
+        std::vector<int> rep_ord(C.rep_cols.size());
+        for (size_t i = 0; i < rep_ord.size(); i++) rep_ord[i] = (int)i;
+        groups = make_groups(c, C, std::max<unsigned long long>(np, 1), 0, outs, fcells, fbytes, MR.n, rep_ord, SB);
+    }
+    g_stats.groups = groups.size();
+    cq_table* res = build_groups(C, groups, Lit, c);
+    post_ops(c, res, q);
+    return res;
+}
+
 // ------------------------------------------------------------------ query dispatch
-void check_plan_shape(cq_node* q, const cqgpu_table* t) {
+void check_plan_shape(cq_node* q, const cqgpu_table* t, bool join_ok = false) {
     if (!q || q->kind != CQ_N_QUERY) throw Ineligible{"not a SELECT query"};
     cq_node* f = q->u.q.from;
     if (!f || f->kind != CQ_N_FROM) throw Ineligible{"no FROM clause"};
     if (f->u.from.subquery) throw Ineligible{"FROM subquery"};
-    if (q->u.q.join_count > 0) throw Ineligible{"JOIN"};
+    if (q->u.q.join_count > 0 && !join_ok) throw Ineligible{"JOIN"};
     char d = t->cfg.delimiter;
     if (d == '\n' || d == '\r' || is_space((unsigned char)d) || d == t->cfg.quote || d == 0)
         throw Ineligible{"whitespace/quote delimiter"};
@@ -1632,6 +2021,12 @@ cq_table* query_impl(cq_node* q, cqgpu_table* const* tables, int ntables) {
     DevCtx& c = ctx();
     if (ntables < 1 || !tables[0]) throw HipError{"no table"};
     const cqgpu_table* t = tables[0];
+    if (q && q->kind == CQ_N_QUERY && q->u.q.join_count > 0) {
+        check_plan_shape(q, t, true);
+        if (ntables < 2) throw Ineligible{"join table not given"};
+        if (tables[1]) check_plan_shape(q, tables[1], true);
+        return run_join(c, q, t, tables[1]);
+    }
     check_plan_shape(q, t);
     if (is_row_query(q)) {
         Compiled C;

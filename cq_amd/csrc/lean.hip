@@ -78,6 +78,8 @@ static_assert(WS % 16 == 0, "16-byte aligned window loads");
         clk_[i] += t_ - clk_last_;                                \
         clk_last_ = t_;                                           \
     } while (0)
+#elif defined(LEAN_MARK)   // asm listing markers (section sizes of the hot path)
+#define LCLK(i) asm volatile(";@@LCLK " #i ::: "memory")
 #else
 #define LCLK(i) do {} while (0)
 #endif
@@ -247,7 +249,12 @@ __device__ __forceinline__ Num num7(uint32_t d0, uint32_t d1, uint32_t len) {
     uint32_t nd2 = len - ndot;                                            // digits
     nd2 = nd2 - 1 > 7u ? 1u : nd2;
     v <<= 8 * (8 - nd2);                                                 // right-align the digits
-    r.M = dig8(v);
+    // digits -> value: three byte dot products (v_dot4_u32_u8) over 3 + 3 + 2 digits
+    const uint32_t vl = (uint32_t)v, vh = (uint32_t)(v >> 32);
+    const uint32_t e1 = __builtin_amdgcn_udot4(vl, 0x00010A64u, 0u, false);
+    const uint32_t e2 = __builtin_amdgcn_udot4(__builtin_amdgcn_alignbyte(vh, vl, 3), 0x00010A64u, 0u, false);
+    const uint32_t e3 = __builtin_amdgcn_udot4(vh, 0x010A0000u, 0u, false);
+    r.M = __umul24(__umul24(e1, 1000u) + e2, 100u) + e3;
     return r;
 }
 
@@ -454,6 +461,12 @@ __global__ __launch_bounds__(LT) void lean_kernel(const uint8_t* __restrict__ g,
     for (int j = 0; j < MAXS; j++) scol[j] = j < NS ? LP.scol[j] : 0u;
     const uint32_t rep_d = LP.delim * 0x01010101u, rep_q = LP.quote * 0x01010101u;
     const uint64_t lo_ok = LP.lo_ok, hi_ok = LP.hi_ok, last_win = LP.last_win;
+    // WHERE facts in scalar registers (no constant reloads inside the loop)
+    const bool pass_null = __builtin_amdgcn_readfirstlane(LP.pass_null) != 0;
+    const int wlo = __builtin_amdgcn_readfirstlane(LP.wlo), whi = __builtin_amdgcn_readfirstlane(LP.whi);
+    const uint32_t wtt = __builtin_amdgcn_readfirstlane(LP.wtt);
+    const double wl = WM == LW_NUM ? LP.wl : 0.0;
+    const uint64_t wstr = WM == LW_STR ? LP.wstr : 0ull;
     const uint64_t tile_g = (uint64_t)(uintptr_t)W.bytes;
     const uint64_t wstep = (uint64_t)gridDim.x * NWV;
 
@@ -574,16 +587,16 @@ __global__ __launch_bounds__(LT) void lean_kernel(const uint8_t* __restrict__ g,
             // ---- WHERE outcome: numerals and short strings in registers, else the exact typers
             bool pass_ = true;
             if (WM != LW_NONE) {
-                bool outcome = LP.pass_null != 0;          // missing column / empty field: NULL
+                bool outcome = pass_null;                  // missing column / empty field: NULL
                 bool typed = wfl == 0;
                 if (WM == LW_NUM) {
                     const Num n = num7(wd0, wd1, wfl);
-                    int c = (int)n.M < LP.wlo ? -1 : ((int)n.M > LP.whi ? 1 : 0);
+                    int c = (int)n.M < wlo ? -1 : ((int)n.M > whi ? 1 : 0);
                     if (__any(n.ok & n.dot)) {             // DOUBLE fields: strtod = RN(M / 10^k)
                         const double d = (double)n.M / p10(n.k);
-                        if (n.dot) c = d < LP.wl ? -1 : (d > LP.wl ? 1 : 0);
+                        if (n.dot) c = d < wl ? -1 : (d > wl ? 1 : 0);
                     }
-                    if (n.ok) outcome = tt_result(LP.wtt, c);
+                    if (n.ok) outcome = tt_result(wtt, c);
                     typed |= n.ok;
                 } else if (WM == LW_STR) {
                     // a STRING field of <= 8 bytes: no leading digit / sign / dot (never a
@@ -595,7 +608,7 @@ __global__ __launch_bounds__(LT) void lean_kernel(const uint8_t* __restrict__ g,
                     const bool ok = (wfl - 1 < 8u) & !(is_digit(c0) | (c0 == '-') | (c0 == '+') | (c0 == '.')) &
                                     ((low_bytes(a0, f0) | low_bytes(a1, f1)) == 0);
                     const uint64_t x = bswap64(a0, a1);
-                    if (ok) outcome = tt_result(LP.wtt, x < LP.wstr ? -1 : (x > LP.wstr ? 1 : 0));
+                    if (ok) outcome = tt_result(wtt, x < wstr ? -1 : (x > wstr ? 1 : 0));
                     typed |= ok;
                 }
                 const bool gen = !typed & !fail;
@@ -606,7 +619,7 @@ __global__ __launch_bounds__(LT) void lean_kernel(const uint8_t* __restrict__ g,
                             fail = true;
                         } else {
                             if (c.kind == K_STR) c.bits = tile_g + wfp;
-                            outcome = tt_result(LP.wtt, compare(c, LP.wconst));
+                            outcome = tt_result(wtt, compare(c, LP.wconst));
                         }
                     }
                 }

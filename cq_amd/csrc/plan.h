@@ -87,6 +87,34 @@ struct FinishDesc {
     uint32_t sb;              // inline STRING bytes per cell
 };
 
+// INNER JOIN (evaluator_joins.c:63-181) on the device: columns of one side parsed
+// per record into a row-major cell array (ncols cells per row)
+struct ColsDesc {
+    int16_t cols[MAX_NEED];   // CSV columns, ascending
+    int32_t ncols;
+    uint32_t delim;
+    uint32_t quote;
+};
+// where each need slot of a plan over the joined row lives: side 0 = left cells,
+// 1 = right cells, col = index within that side's row of cells
+struct JoinMap {
+    int8_t side[MAX_NEED];
+    int8_t col[MAX_NEED];
+    int32_t n;
+    uint32_t lstride, rstride;
+};
+
+// the right side of a join, sorted by key class then by key code (scan.hip
+// join_count_kernel / join_emit_kernel)
+struct JoinRight {
+    const unsigned long long* scodes;   // codes, sorted within each class segment
+    const uint32_t* sidx;               // row of each sorted code
+    const uint32_t* ridx_c;             // rows grouped by class, row order within a class
+    const Cell* cells;
+    uint32_t stride, kcol;
+    uint32_t seg[5];                    // class segment bounds (0 NULL, 1 number, 2 string, 3 date)
+};
+
 // scan statistics written by the kernel (one per launch)
 struct ScanStats {
     unsigned long long records;     // data records seen

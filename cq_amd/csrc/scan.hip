@@ -37,6 +37,7 @@
 // [range_begin, range_end) can be scanned independently: that is also how the
 // multi-GPU path shards a file.
 #include <hip/hip_runtime.h>
+#include <algorithm>
 #include <cstdlib>
 #include <cstring>
 #include "plan.h"
@@ -1295,6 +1296,285 @@ __global__ void parse_literals_kernel(const uint8_t* __restrict__ text,
     out[i] = parse_cell(text + offs[i], lens[i]);
 }
 
+// ------------------------------------------------------------------ INNER JOIN
+// perform_join (evaluator_joins.c:63-181) as a hash-free sort join on the device:
+// the right side's key codes are radix-sorted (stable, so equal keys keep row
+// order), every left row binary-searches its run, and the (l, r) pairs come out
+// in the reference's nested-loop order (left rows ascending, then right rows).
+// value_compare (csv_reader.c:98-130) equality is what "matches" means:
+// numbers compare as doubles, strings by strcmp, dates by (y, m, d), NULL = NULL;
+// the host refuses key columns that mix value classes (cross-class pairs
+// compare "equal" in the reference).
+
+// the columns of one side, parsed per record (parse_line + parse_value)
+__global__ void cells_kernel(const uint8_t* __restrict__ g, const unsigned long long* __restrict__ recs, uint32_t n,
+                             ColsDesc D, Cell* __restrict__ out) {
+    const uint32_t i = blockIdx.x * blockDim.x + threadIdx.x;
+    if (i >= n) return;
+    parse_cols_out(g + recs[i], D.cols, D.ncols, D.delim, D.quote, out + (uint64_t)i * D.ncols, 1);
+}
+
+// value class of a key under value_compare: 0 NULL, 1 number, 2 string, 3 date.
+// Keys of different non-NULL classes compare "equal" (csv_reader.c:128): a left
+// key matches the equal keys of its own class plus EVERY non-NULL right key of
+// another class; NULL matches only NULL.
+__device__ __forceinline__ uint32_t key_class(const Cell& c) {
+    return c.kind == K_NULL ? 0u : (c.kind == K_STR ? 2u : (c.kind == K_DATE ? 3u : 1u));
+}
+__device__ __forceinline__ uint64_t join_code(const Cell& c) {
+    if (c.kind == K_NULL) return 0;
+    if (c.kind == K_STR) return fnv_bytes(str_ptr(c), c.len);
+    if (c.kind == K_DATE) return c.bits;
+    double d = num_of(c);
+    if (d == 0.0) d = 0.0;                                    // -0 == +0 under value_compare
+    return dbl_bits(d);
+}
+
+// key code, class and row index of every row; rows per class
+__global__ void join_code_kernel(const Cell* __restrict__ cells, uint32_t stride, uint32_t kcol, uint32_t n,
+                                 unsigned long long* __restrict__ codes, uint32_t* __restrict__ cls,
+                                 uint32_t* __restrict__ idx, unsigned int* __restrict__ per_class) {
+    const uint32_t i = blockIdx.x * blockDim.x + threadIdx.x;
+    if (i >= n) return;
+    const Cell c = cells[(uint64_t)i * stride + kcol];
+    codes[i] = join_code(c);
+    const uint32_t k = key_class(c);
+    cls[i] = k;
+    if (idx) idx[i] = i;
+    if (per_class) atomicAdd(&per_class[k], 1u);
+}
+
+__global__ void gather_codes_kernel(const unsigned long long* __restrict__ codes, const uint32_t* __restrict__ idx,
+                                    uint32_t n, unsigned long long* __restrict__ out) {
+    const uint32_t i = blockIdx.x * blockDim.x + threadIdx.x;
+    if (i < n) out[i] = codes[idx[i]];
+}
+
+// The right side after two stable sorts: by class (ridx_c: per-class row lists
+// in row order, segments seg[0..4]) and then by code within each class (scodes /
+// sidx).  A left row's matches: its class's equal-code run (STRING codes are
+// hashes: verified byte for byte) merged by row number with the whole lists of the
+// other non-NULL classes.
+
+
+__device__ __forceinline__ void eq_run(const JoinRight& J, uint32_t k, unsigned long long code, uint32_t& lo,
+                                       uint32_t& hi) {
+    uint32_t a = J.seg[k], b = J.seg[k + 1];
+    while (a < b) {
+        const uint32_t mid = (a + b) >> 1;
+        if (J.scodes[mid] < code) a = mid + 1; else b = mid;
+    }
+    lo = a;
+    hi = a;
+    while (hi < J.seg[k + 1] && J.scodes[hi] == code) hi++;
+}
+
+__global__ void join_count_kernel(const Cell* __restrict__ L, uint32_t ls, uint32_t lk, uint32_t nL, JoinRight J,
+                                  uint32_t* __restrict__ lo_out, unsigned long long* __restrict__ cnt) {
+    const uint32_t l = blockIdx.x * blockDim.x + threadIdx.x;
+    if (l >= nL) return;
+    const Cell kc = L[(uint64_t)l * ls + lk];
+    const uint32_t k = key_class(kc);
+    uint32_t lo, hi;
+    eq_run(J, k, join_code(kc), lo, hi);
+    unsigned long long n = hi - lo;
+    if (k == 2) {
+        n = 0;
+        for (uint32_t j = lo; j < hi; j++) n += compare(kc, J.cells[(uint64_t)J.sidx[j] * J.stride + J.kcol]) == 0;
+    }
+    if (k != 0)
+        for (uint32_t y = 1; y < 4; y++)
+            if (y != k) n += J.seg[y + 1] - J.seg[y];
+    lo_out[l] = lo;
+    cnt[l] = n;
+}
+
+__global__ void join_emit_kernel(const Cell* __restrict__ L, uint32_t ls, uint32_t lk, uint32_t nL, JoinRight J,
+                                 const uint32_t* __restrict__ lo_in, const unsigned long long* __restrict__ cnt,
+                                 const unsigned long long* __restrict__ offs, uint2* __restrict__ pairs) {
+    const uint32_t l = blockIdx.x * blockDim.x + threadIdx.x;
+    if (l >= nL) return;
+    const unsigned long long want = cnt[l];
+    if (!want) return;
+    const Cell kc = L[(uint64_t)l * ls + lk];
+    const uint32_t k = key_class(kc);
+    const unsigned long long code = join_code(kc);
+    // three row-ordered streams: the equal run, and the other two non-NULL classes
+    uint32_t e = lo_in[l];
+    const uint32_t ee = J.seg[k + 1];
+    uint32_t ya = 0, yb = 0, za = 0, zb = 0;
+    if (k != 0) {
+        const uint32_t y = k == 1 ? 2 : 1, z = k == 3 ? 2 : 3;
+        ya = J.seg[y]; yb = J.seg[y + 1];
+        za = J.seg[z]; zb = J.seg[z + 1];
+    }
+    const unsigned long long o = offs[l];
+    for (unsigned long long m = 0; m < want; m++) {
+        // next verified row of the equal run (~0: exhausted)
+        uint32_t re = 0xFFFFFFFFu;
+        while (e < ee && J.scodes[e] == code) {
+            const uint32_t r = J.sidx[e];
+            if (k != 2 || compare(kc, J.cells[(uint64_t)r * J.stride + J.kcol]) == 0) { re = r; break; }
+            e++;
+        }
+        const uint32_t ry = ya < yb ? J.ridx_c[ya] : 0xFFFFFFFFu;
+        const uint32_t rz = za < zb ? J.ridx_c[za] : 0xFFFFFFFFu;
+        uint32_t r = re;
+        int src = 0;
+        if (ry < r) { r = ry; src = 1; }
+        if (rz < r) { r = rz; src = 2; }
+        if (r == 0xFFFFFFFFu) break;                          // never: counts and streams agree
+        pairs[o + m] = make_uint2(l, r);
+        if (src == 0) e++;
+        else if (src == 1) ya++;
+        else za++;
+    }
+}
+
+// the plan's need slots of one joined row
+__device__ __forceinline__ void join_cells(const JoinMap& M, const Cell* L, const Cell* R, uint2 pr,
+                                           CellsT<MAX_NEED>& cs) {
+#pragma unroll
+    for (int k = 0; k < MAX_NEED; k++) {
+        cs.c[k] = cell_null();
+        if (k < M.n)
+            cs.c[k] = M.side[k] ? R[(uint64_t)pr.y * M.rstride + M.col[k]] : L[(uint64_t)pr.x * M.lstride + M.col[k]];
+    }
+}
+
+// WHERE + GROUP BY + aggregates over the joined rows (filter_rows, create_groups,
+// evaluate_aggregate over perform_join's table); a group's `first` is its first
+// pair's index, i.e. its first row of the joined table
+__global__ __launch_bounds__(256) void join_agg_kernel(const uint2* __restrict__ pairs, unsigned long long np,
+                                                       JoinMap M, const Cell* __restrict__ L,
+                                                       const Cell* __restrict__ R, ScanStats* __restrict__ stats,
+                                                       int grouped) {
+    const ScanPlan& P = c_plan;
+    const GroupTable& gt = c_gt;
+    const int nneed = P.nneed, nacc = P.nacc;
+    unsigned long long my_pass = 0;
+    for (unsigned long long b0 = (unsigned long long)blockIdx.x * blockDim.x; b0 < np;
+         b0 += (unsigned long long)gridDim.x * blockDim.x) {
+        const unsigned long long i = b0 + threadIdx.x;
+        const bool valid = i < np;
+        CellsT<MAX_NEED> cs;
+        bool pass = false;
+        if (valid) {
+            join_cells(M, L, R, pairs[i], cs);
+            pass = P.nprog == 0 || eval_where_vm(P, P.consts, cs);
+        } else {
+#pragma unroll
+            for (int k = 0; k < MAX_NEED; k++) cs.c[k] = cell_null();
+        }
+        if (pass) {
+            my_pass++;
+            for (int a = 0; a < nacc; a++)
+                if (P.acc[a].kind != ACC_SUM) {
+                    const uint32_t m = class_bit(get_cell(cs, P.acc[a].slot, nneed));
+                    if (m) atomicOr(&stats->acc_classes[a], m);
+                }
+        }
+        GKey key;
+        key.cls = GK_ALL; key.len = 0; key.w0 = 0; key.w1 = 0;
+        uint64_t h = 0x12345678ULL;
+        if (grouped && pass) {
+            key = group_key(get_cell(cs, P.group_slot, nneed));
+            h = gk_hash(key);
+        }
+        int gi = -1;
+        if (pass) {
+            gi = g_insert(gt, key, h, stats);
+            if (gi >= 0) {
+                atomicAdd(&gt.cnt[gi], 1ULL);
+                atomicMin(&gt.first[gi], i);
+                for (int a = 0; a < nacc; a++) {
+                    const Cell c = get_cell(cs, P.acc[a].slot, nneed);
+                    if (P.acc[a].kind == ACC_SUM && is_num(c)) {
+                        atomicAdd(&gt.sum[a][gi], num_of(c));
+                        atomicAdd(&gt.num[a][gi], 1ULL);
+                    }
+                }
+            }
+        }
+#pragma unroll
+        for (int a = 0; a < MAX_ACC; a++) {
+            if (a >= nacc) break;
+            if (P.acc[a].kind == ACC_SUM) continue;      // uniform
+            const Cell c = get_cell(cs, P.acc[a].slot, nneed);
+            g_ext_update(pass && gi >= 0 && c.kind != K_NULL, gt, a, P.acc[a].kind, gi >= 0 ? (uint32_t)gi : 0u,
+                         c, i, stats);
+        }
+    }
+    for (int o = 32; o > 0; o >>= 1) my_pass += __shfl_down(my_pass, o, 64);
+    if ((threadIdx.x & 63) == 0 && my_pass) atomicAdd(&stats->passed, my_pass);
+}
+
+// WHERE over the joined rows of a row-returning query: 1 / 0 per pair
+__global__ void join_filter_kernel(const uint2* __restrict__ pairs, unsigned long long np, JoinMap M,
+                                   const Cell* __restrict__ L, const Cell* __restrict__ R,
+                                   unsigned int* __restrict__ flags) {
+    const ScanPlan& P = c_plan;
+    const unsigned long long i = (unsigned long long)blockIdx.x * blockDim.x + threadIdx.x;
+    if (i >= np) return;
+    CellsT<MAX_NEED> cs;
+    join_cells(M, L, R, pairs[i], cs);
+    flags[i] = (P.nprog == 0 || eval_where_vm(P, P.consts, cs)) ? 1u : 0u;
+}
+
+// build_result's projection (evaluator_utils.c:249-549) of the passing joined rows
+// whose output index falls in [lo, lo + m): M maps the projection's columns
+__global__ void join_project_kernel(const uint2* __restrict__ pairs, unsigned long long np,
+                                    const unsigned int* __restrict__ flags, const unsigned int* __restrict__ pos,
+                                    unsigned long long lo, uint32_t m, JoinMap M, const Cell* __restrict__ L,
+                                    const Cell* __restrict__ R, const Insn* __restrict__ code,
+                                    const uint32_t* __restrict__ off, int nout, const Cell* __restrict__ consts,
+                                    Cell* __restrict__ scratch, Cell* __restrict__ out) {
+    const unsigned long long i = (unsigned long long)blockIdx.x * blockDim.x + threadIdx.x;
+    if (i >= np || !flags[i]) return;
+    const unsigned long long o = pos[i];
+    if (o < lo || o >= lo + m) return;
+    const uint64_t row = o - lo;
+    const uint2 pr = pairs[i];
+    Cell* cs = scratch + row * (uint64_t)(M.n ? M.n : 1);
+    for (int k = 0; k < M.n; k++)
+        cs[k] = M.side[k] ? R[(uint64_t)pr.y * M.rstride + M.col[k]] : L[(uint64_t)pr.x * M.lstride + M.col[k]];
+    for (int k = 0; k < nout; k++) out[row * nout + k] = eval_value(code, off[k], off[k + 1], cs, 1, consts);
+}
+
+// finish_kernel for joined groups: representative cells from the group's first pair
+__global__ void join_finish_kernel(const GroupOut* __restrict__ out, const unsigned int* __restrict__ count,
+                                   unsigned int cap_out, const uint2* __restrict__ pairs, JoinMap M,
+                                   const Cell* __restrict__ L, const Cell* __restrict__ R, int nacc, uint32_t sb,
+                                   Cell* __restrict__ cells, uint8_t* __restrict__ bytes) {
+    const uint32_t ncell = (uint32_t)(M.n + nacc + 1);
+    const uint32_t i = blockIdx.x * blockDim.x + threadIdx.x;
+    const uint32_t ng = *count < cap_out ? *count : cap_out;
+    if (i >= ng) return;
+    Cell* cs = cells + (size_t)i * ncell;
+    const unsigned long long first = out[i].first;
+    for (int k = 0; k < M.n; k++) {
+        Cell c = cell_null();
+        if (first != NOPOS) {
+            const uint2 pr = pairs[first];
+            c = M.side[k] ? R[(uint64_t)pr.y * M.rstride + M.col[k]] : L[(uint64_t)pr.x * M.lstride + M.col[k]];
+        }
+        cs[k] = c;
+    }
+    for (int a = 0; a < nacc; a++) cs[M.n + a] = out[i].ext[a];
+    Cell kc = cell_null();
+    const uint32_t cl = out[i].clslen;
+    if ((cl >> 16) == GK_LONG) { kc.kind = K_STR; kc.len = cl & 0xffff; kc.bits = out[i].w0; }
+    cs[M.n + nacc] = kc;
+    for (uint32_t k = 0; k < ncell; k++) {
+        const Cell c = cs[k];
+        if (c.kind != K_STR) continue;
+        const uint8_t* src = (const uint8_t*)(uintptr_t)c.bits;
+        uint8_t* dst = bytes + ((size_t)i * ncell + k) * sb;
+        const uint32_t mm = c.len < sb ? c.len : sb;
+        for (uint32_t j = 0; j < mm; j++) dst[j] = src[j];
+    }
+}
+
 }  // namespace cq
 
 // ------------------------------------------------------------------ host wrappers
@@ -1507,6 +1787,77 @@ hipError_t cq_launch_finish(const uint8_t* g, uint64_t n, const cq::GroupOut* ou
                             hipStream_t s) {
     hipLaunchKernelGGL(cq::finish_kernel, dim3((cap_out + 127) / 128), dim3(128), 0, s, g, n, out, count, cap_out, *D,
                        cells, bytes);
+    return hipGetLastError();
+}
+
+// ---- INNER JOIN kernels (executor.hip run_join)
+static unsigned grid_of(uint64_t n, unsigned b) { return (unsigned)std::max<uint64_t>(1, (n + b - 1) / b); }
+
+hipError_t cq_launch_cells(const uint8_t* g, const unsigned long long* recs, uint32_t n, const cq::ColsDesc* D,
+                           cq::Cell* out, hipStream_t s) {
+    if (!n) return hipSuccess;
+    hipLaunchKernelGGL(cq::cells_kernel, dim3(grid_of(n, 128)), dim3(128), 0, s, g, recs, n, *D, out);
+    return hipGetLastError();
+}
+hipError_t cq_launch_join_code(const cq::Cell* cells, uint32_t stride, uint32_t kcol, uint32_t n,
+                               unsigned long long* codes, uint32_t* cls, uint32_t* idx, unsigned int* per_class,
+                               hipStream_t s) {
+    if (!n) return hipSuccess;
+    hipLaunchKernelGGL(cq::join_code_kernel, dim3(grid_of(n, 256)), dim3(256), 0, s, cells, stride, kcol, n, codes,
+                       cls, idx, per_class);
+    return hipGetLastError();
+}
+hipError_t cq_launch_gather_codes(const unsigned long long* codes, const uint32_t* idx, uint32_t n,
+                                  unsigned long long* out, hipStream_t s) {
+    if (!n) return hipSuccess;
+    hipLaunchKernelGGL(cq::gather_codes_kernel, dim3(grid_of(n, 256)), dim3(256), 0, s, codes, idx, n, out);
+    return hipGetLastError();
+}
+hipError_t cq_launch_join_count(const cq::Cell* L, uint32_t ls, uint32_t lk, uint32_t nL, const cq::JoinRight* J,
+                                uint32_t* lo, unsigned long long* cnt, hipStream_t s) {
+    if (!nL) return hipSuccess;
+    hipLaunchKernelGGL(cq::join_count_kernel, dim3(grid_of(nL, 256)), dim3(256), 0, s, L, ls, lk, nL, *J, lo, cnt);
+    return hipGetLastError();
+}
+hipError_t cq_launch_join_emit(const cq::Cell* L, uint32_t ls, uint32_t lk, uint32_t nL, const cq::JoinRight* J,
+                               const uint32_t* lo, const unsigned long long* cnt, const unsigned long long* offs,
+                               uint2* pairs, hipStream_t s) {
+    if (!nL) return hipSuccess;
+    hipLaunchKernelGGL(cq::join_emit_kernel, dim3(grid_of(nL, 256)), dim3(256), 0, s, L, ls, lk, nL, *J, lo, cnt, offs,
+                       pairs);
+    return hipGetLastError();
+}
+hipError_t cq_launch_join_agg(const uint2* pairs, unsigned long long np, const cq::JoinMap* M, const cq::Cell* L,
+                              const cq::Cell* R, const cq::ScanPlan* P, const cq::GroupTable* gt,
+                              cq::ScanStats* stats, int grouped, hipStream_t s) {
+    hipError_t e = hipMemcpyToSymbolAsync(HIP_SYMBOL(cq::c_plan), P, sizeof *P, 0, hipMemcpyHostToDevice, s);
+    if (e == hipSuccess) e = hipMemcpyToSymbolAsync(HIP_SYMBOL(cq::c_gt), gt, sizeof *gt, 0, hipMemcpyHostToDevice, s);
+    if (e != hipSuccess || !np) return e;
+    const unsigned grid = (unsigned)std::min<uint64_t>(grid_of(np, 256), 4096);
+    hipLaunchKernelGGL(cq::join_agg_kernel, dim3(grid), dim3(256), 0, s, pairs, np, *M, L, R, stats, grouped);
+    return hipGetLastError();
+}
+hipError_t cq_launch_join_filter(const uint2* pairs, unsigned long long np, const cq::JoinMap* M, const cq::Cell* L,
+                                 const cq::Cell* R, const cq::ScanPlan* P, unsigned int* flags, hipStream_t s) {
+    hipError_t e = hipMemcpyToSymbolAsync(HIP_SYMBOL(cq::c_plan), P, sizeof *P, 0, hipMemcpyHostToDevice, s);
+    if (e != hipSuccess || !np) return e;
+    hipLaunchKernelGGL(cq::join_filter_kernel, dim3(grid_of(np, 256)), dim3(256), 0, s, pairs, np, *M, L, R, flags);
+    return hipGetLastError();
+}
+hipError_t cq_launch_join_project(const uint2* pairs, unsigned long long np, const unsigned int* flags,
+                                  const unsigned int* pos, unsigned long long lo, uint32_t m, const cq::JoinMap* M,
+                                  const cq::Cell* L, const cq::Cell* R, const cq::Insn* code, const uint32_t* off,
+                                  int nout, const cq::Cell* consts, cq::Cell* scratch, cq::Cell* out, hipStream_t s) {
+    if (!np || !m) return hipSuccess;
+    hipLaunchKernelGGL(cq::join_project_kernel, dim3(grid_of(np, 256)), dim3(256), 0, s, pairs, np, flags, pos, lo, m,
+                       *M, L, R, code, off, nout, consts, scratch, out);
+    return hipGetLastError();
+}
+hipError_t cq_launch_join_finish(const cq::GroupOut* out, const unsigned int* count, unsigned int cap_out,
+                                 const uint2* pairs, const cq::JoinMap* M, const cq::Cell* L, const cq::Cell* R,
+                                 int nacc, uint32_t sb, cq::Cell* cells, uint8_t* bytes, hipStream_t s) {
+    hipLaunchKernelGGL(cq::join_finish_kernel, dim3(grid_of(cap_out, 128)), dim3(128), 0, s, out, count, cap_out,
+                       pairs, *M, L, R, nacc, sb, cells, bytes);
     return hipGetLastError();
 }
 

@@ -5,7 +5,7 @@ export TMPDIR=/tmp
 OUT=gpurun_out/${PROF_TAG:-pmclean}
 mkdir -p $OUT
 B="python bench.py --rows 10000000 --steps 2 --warmup 1 --no-cpu"
-for st in ${STAGES:-l0 l1 l2 l3 nomem base}; do
+for st in ${STAGES:-l0 l1 l2 l3 base}; do
   L=$PWD/cq_amd/lib/libcqgpu_$st.so
   [ $st = base ] && L=$PWD/cq_amd/lib/libcqgpu.so
   CQ_AMD_LIB=$L timeout -k 10 300 rocprofv3 --pmc SQ_INSTS_VALU SQ_INSTS_SALU SQ_INSTS_LDS SQ_WAIT_INST_LDS SQ_INSTS_BRANCH SQ_WAVE_CYCLES SQ_WAIT_ANY SQ_ACTIVE_INST_VALU --output-format csv -d $OUT/$st -o run -- $B > $OUT/$st.log 2>&1 || exit 1

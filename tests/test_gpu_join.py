@@ -1,0 +1,130 @@
+"""INNER JOIN on the GPU (executor.hip run_join, scan.hip join kernels) against the
+oracle's nested-loop perform_join (reference evaluator_joins.c:63-181).
+
+Cases: many-to-many keys (pairs in (l, r) order), string / double / NULL keys, keys mixing value classes
+(NULL = NULL matches under value_compare), short rows, WHERE over both sides,
+GROUP BY either side with COUNT/SUM/AVG/MIN/MAX, row-returning SELECT with
+ORDER BY / LIMIT / OFFSET, the ON operand quirk (each name is resolved to a
+column index and read from its own side's row) and an unresolvable ON column (no
+pairs).
+
+Counts, group sets / order, row sets and order bit-exact; SUM/AVG 1e-6 relative.
+"""
+import numpy as np
+import pytest
+
+import cqtest
+import cq_amd
+
+pytestmark = pytest.mark.gpu
+REL = 1e-6
+
+
+@pytest.fixture(scope="module")
+def files(tmp_path_factory):
+    d = tmp_path_factory.mktemp("join")
+    rng = np.random.default_rng(17)
+    f = {}
+    # users: id (with duplicates and gaps), name, age, role
+    lines = ["id,name,age,role"]
+    for i in range(3000):
+        uid = int(rng.integers(0, 2500))
+        role = "role_%02d" % rng.integers(0, 37)
+        age = "" if rng.integers(0, 50) == 0 else str(int(rng.integers(18, 90)))
+        lines.append(f"{uid},n{i % 97},{age},{role}")
+    lines.append("")                                    # empty line: skipped
+    lines.append("2600,short")                          # short row
+    f["users"] = d / "users.csv"
+    f["users"].write_text("\n".join(lines) + "\n")
+    # orders: id, price, quantity, customer_id (some NULL keys, some doubles)
+    lines = ["id,price,quantity,customer_id"]
+    for i in range(5000):
+        cid = int(rng.integers(0, 2700))
+        k = rng.integers(0, 60)
+        cs = "" if k == 0 else (f"{cid}.0" if k == 1 else str(cid))
+        lines.append(f"{i},{rng.integers(100, 99999) / 100:.2f},{rng.integers(1, 9)},{cs}")
+    f["orders"] = d / "orders.csv"
+    f["orders"].write_text("\n".join(lines) + "\n")
+    # string keys, with NULLs on both sides
+    a = ["k,v"] + [f"{'' if i % 41 == 0 else 'key%03d' % (i % 150)},{i}" for i in range(900)]
+    b = ["k,w"] + [f"{'' if i % 53 == 0 else 'key%03d' % (i % 170)},{i * 3}" for i in range(700)]
+    f["sa"] = d / "sa.csv"
+    f["sa"].write_text("\n".join(a) + "\n")
+    f["sb"] = d / "sb.csv"
+    f["sb"].write_text("\n".join(b) + "\n")
+    # keys mixing numbers and strings
+    f["mixed"] = d / "mixed.csv"
+    f["mixed"].write_text("k,z\n1,a\nx,b\n2,c\n,d\n2020-01-02,e\nx,f\n1.0,g\n")
+    return f
+
+
+def _tol(sql):
+    sel = sql.split(" FROM ")[0]
+    items = [s.strip() for s in sel[len("SELECT "):].split(",")]
+    return {i for i, s in enumerate(items) if s.upper().startswith(("SUM(", "AVG("))}
+
+
+def _check(sql, expect_rows=None):
+    want, unsup = cqtest.oracle_query(sql)
+    assert not unsup, sql
+    with cqtest.Parsed(sql) as ast:
+        got = cq_amd.evaluate(ast)
+        inel = cq_amd.last_ineligible()
+    assert not inel, (sql, inel)
+    assert cq_amd.stats()["path"] == 1, sql
+    assert (got is None) == (want is None), sql
+    if want is None:
+        return
+    tol = _tol(sql)
+    assert got["columns"] == want["columns"], sql
+    assert len(got["rows"]) == len(want["rows"]), (sql, len(got["rows"]), len(want["rows"]))
+    if expect_rows is not None:
+        assert len(want["rows"]) >= expect_rows, sql
+    for i, (g, w) in enumerate(zip(got["rows"], want["rows"])):
+        for j, (x, y) in enumerate(zip(g, w)):
+            assert cqtest.cell_equal(x, y, REL if j in tol else 0.0), f"{sql}: row {i} col {j}: {x} vs {y}"
+
+
+NUM = [
+    "SELECT COUNT(*) FROM '{U}' AS u JOIN '{O}' AS o ON u.id = o.customer_id",
+    "SELECT COUNT(*) FROM '{U}' AS u JOIN '{O}' AS o ON o.customer_id = u.id",
+    "SELECT COUNT(*), SUM(o.price), AVG(o.quantity) FROM '{U}' AS u JOIN '{O}' AS o ON u.id = o.customer_id WHERE u.age > 40",
+    "SELECT u.role, COUNT(*), SUM(o.price), AVG(o.price) FROM '{U}' AS u JOIN '{O}' AS o ON u.id = o.customer_id GROUP BY u.role",
+    "SELECT o.quantity, COUNT(*), MIN(u.age), MAX(u.name) FROM '{U}' AS u JOIN '{O}' AS o ON u.id = o.customer_id GROUP BY o.quantity",
+    "SELECT u.role, COUNT(*) FROM '{U}' AS u JOIN '{O}' AS o ON u.id = o.customer_id WHERE o.price > 500 AND u.age < 60 GROUP BY u.role HAVING COUNT(*) > 20 ORDER BY u.role",
+    "SELECT u.name, o.price, o.id FROM '{U}' AS u JOIN '{O}' AS o ON u.id = o.customer_id WHERE o.quantity = 3",
+    "SELECT u.id, u.name, o.price FROM '{U}' AS u JOIN '{O}' AS o ON u.id = o.customer_id LIMIT 50 OFFSET 10",
+    "SELECT u.name, o.price FROM '{U}' AS u JOIN '{O}' AS o ON u.id = o.customer_id ORDER BY o.price DESC LIMIT 25",
+    "SELECT COUNT(*) FROM '{U}' AS u JOIN '{O}' AS o ON u.nosuch = o.customer_id",
+    "SELECT COUNT(*) FROM '{U}' AS u JOIN '{O}' AS o ON u.age = o.quantity",
+    "SELECT u.age, COUNT(*), SUM(o.price) FROM '{U}' AS u JOIN '{O}' AS o ON u.age = o.customer_id GROUP BY u.age",
+]
+STR = [
+    "SELECT COUNT(*) FROM '{A}' AS a JOIN '{B}' AS b ON a.k = b.k",
+    "SELECT a.k, COUNT(*), SUM(b.w), MIN(a.v) FROM '{A}' AS a JOIN '{B}' AS b ON a.k = b.k GROUP BY a.k",
+    "SELECT a.v, b.w FROM '{A}' AS a JOIN '{B}' AS b ON a.k = b.k WHERE b.w < 300",
+]
+
+
+@pytest.mark.parametrize("tmpl", NUM)
+def test_join_numeric(files, tmpl):
+    _check(tmpl.replace("{U}", str(files["users"])).replace("{O}", str(files["orders"])))
+
+
+@pytest.mark.parametrize("tmpl", STR)
+def test_join_strings(files, tmpl):
+    _check(tmpl.replace("{A}", str(files["sa"])).replace("{B}", str(files["sb"])))
+
+
+MIXED = [
+    "SELECT COUNT(*) FROM '{M}' AS a JOIN '{M}' AS b ON a.k = b.k",
+    "SELECT a.k, a.z, b.z FROM '{M}' AS a JOIN '{M}' AS b ON a.k = b.k",
+    "SELECT a.z, COUNT(*) FROM '{M}' AS a JOIN '{A}' AS b ON a.k = b.k GROUP BY a.z",
+]
+
+
+@pytest.mark.parametrize("tmpl", MIXED)
+def test_join_mixed_classes(files, tmpl):
+    """keys of different value classes compare "equal" (csv_reader.c:128): every
+    left key meets every right key of another non-NULL class, in row order"""
+    _check(tmpl.replace("{M}", str(files["mixed"])).replace("{A}", str(files["sa"])))
