@@ -16,7 +16,7 @@ import os
 import shutil
 
 
-def pmc(d, kernel="scan_kernel"):
+def pmc(d, kernel="lean_kernel"):
     out = collections.defaultdict(list)
     for f in glob.glob(os.path.join(d, "**", "*counter_collection.csv"), recursive=True):
         per = collections.defaultdict(lambda: collections.defaultdict(float))
