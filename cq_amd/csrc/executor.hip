@@ -53,10 +53,12 @@ hipError_t cq_launch_join_code(const cq::Cell* cells, uint32_t stride, uint32_t 
 hipError_t cq_launch_gather_codes(const unsigned long long* codes, const uint32_t* idx, uint32_t n,
                                   unsigned long long* out, hipStream_t s);
 hipError_t cq_launch_join_count(const cq::Cell* L, uint32_t ls, uint32_t lk, uint32_t nL, const cq::JoinRight* J,
-                                uint32_t* lo, unsigned long long* cnt, hipStream_t s);
+                                int outer_left, uint32_t* lo, unsigned long long* cnt, hipStream_t s);
 hipError_t cq_launch_join_emit(const cq::Cell* L, uint32_t ls, uint32_t lk, uint32_t nL, const cq::JoinRight* J,
                                const uint32_t* lo, const unsigned long long* cnt, const unsigned long long* offs,
-                               uint2* pairs, hipStream_t s);
+                               uint2* pairs, unsigned int* rmatched, hipStream_t s);
+hipError_t cq_launch_join_fill(const unsigned int* flags, const unsigned int* pos, uint32_t n, unsigned long long base,
+                               int right_side, uint2* pairs, hipStream_t s);
 hipError_t cq_sort_classes(void* temp, size_t* temp_bytes, const unsigned int* kin, unsigned int* kout,
                            const unsigned int* vin, unsigned int* vout, size_t n, hipStream_t s);
 hipError_t cq_sort_codes_seg(void* temp, size_t* temp_bytes, const unsigned long long* kin, unsigned long long* kout,
@@ -1756,7 +1758,9 @@ JoinMap join_map(const std::vector<int>& jcols, int nl, const JoinSide& A, const
 cq_table* run_join(DevCtx& c, cq_node* q, const cqgpu_table* L, const cqgpu_table* R) {
     cq_node* jn = q->u.q.joins[0];
     if (q->u.q.join_count != 1 || !jn || jn->kind != CQ_N_JOIN) throw Ineligible{"more than one JOIN"};
-    if (jn->u.join.kind != CQ_JOIN_INNER) throw Ineligible{"LEFT/RIGHT/FULL JOIN"};
+    const int kind = jn->u.join.kind;
+    const bool outer_left = kind == CQ_JOIN_LEFT || kind == CQ_JOIN_FULL;
+    const bool outer_right = kind == CQ_JOIN_RIGHT || kind == CQ_JOIN_FULL;
     if (!R) throw Ineligible{"join table failed to load"};
     cq_node* on = jn->u.join.on;
     if (!on) throw Ineligible{"JOIN without ON (cross product)"};
@@ -1840,7 +1844,7 @@ cq_table* run_join(DevCtx& c, cq_node* q, const cqgpu_table* L, const cqgpu_tabl
         JR.stride = rs;
         JR.kcol = rk;
         DevBuf lo((size_t)A.n * 4), cnt((size_t)A.n * 8), offs((size_t)A.n * 8);
-        HIPCHECK(cq_launch_join_count(A.cells.as<Cell>(), ls, lk, A.n, &JR, lo.as<uint32_t>(),
+        HIPCHECK(cq_launch_join_count(A.cells.as<Cell>(), ls, lk, A.n, &JR, outer_left ? 1 : 0, lo.as<uint32_t>(),
                                       cnt.as<unsigned long long>(), c.stream));
         size_t tb2 = 0;
         HIPCHECK(cq_excl_sum_u64(nullptr, &tb2, cnt.as<unsigned long long>(), offs.as<unsigned long long>(), A.n,
@@ -1852,13 +1856,39 @@ cq_table* run_join(DevCtx& c, cq_node* q, const cqgpu_table* L, const cqgpu_tabl
         HIPCHECK(hipMemcpyAsync(&last[0], offs.as<unsigned long long>() + A.n - 1, 8, hipMemcpyDeviceToHost, c.stream));
         HIPCHECK(hipMemcpyAsync(&last[1], cnt.as<unsigned long long>() + A.n - 1, 8, hipMemcpyDeviceToHost, c.stream));
         HIPCHECK(hipStreamSynchronize(c.stream));
-        np = last[0] + last[1];
-        DevBuf pb(np * 8);
+        const unsigned long long nleft = last[0] + last[1];
+        // RIGHT / FULL: right rows no left row matched, appended in row order
+        DevBuf unm(outer_right ? (size_t)B.n * 4 : 4), upos(outer_right ? (size_t)B.n * 4 : 4);
+        if (outer_right) HIPCHECK(hipMemsetD32Async((hipDeviceptr_t)unm.p, 1u, B.n, c.stream));
+        DevBuf pb((nleft + (outer_right ? B.n : 0)) * 8);
         std::swap(pairs.p, pb.p);
         HIPCHECK(cq_launch_join_emit(A.cells.as<Cell>(), ls, lk, A.n, &JR, lo.as<uint32_t>(),
                                      cnt.as<unsigned long long>(), offs.as<unsigned long long>(), pairs.as<uint2>(),
-                                     c.stream));
+                                     outer_right ? unm.as<unsigned int>() : nullptr, c.stream));
+        np = nleft;
+        if (outer_right) {
+            size_t tb3 = 0;
+            HIPCHECK(cq_excl_sum_u32(nullptr, &tb3, unm.as<unsigned int>(), upos.as<unsigned int>(), B.n, c.stream));
+            DevBuf temp3(tb3);
+            HIPCHECK(cq_excl_sum_u32(temp3.p, &tb3, unm.as<unsigned int>(), upos.as<unsigned int>(), B.n, c.stream));
+            unsigned int ul[2] = {0, 0};
+            HIPCHECK(hipMemcpyAsync(&ul[0], upos.as<unsigned int>() + B.n - 1, 4, hipMemcpyDeviceToHost, c.stream));
+            HIPCHECK(hipMemcpyAsync(&ul[1], unm.as<unsigned int>() + B.n - 1, 4, hipMemcpyDeviceToHost, c.stream));
+            HIPCHECK(cq_launch_join_fill(unm.as<unsigned int>(), upos.as<unsigned int>(), B.n, nleft, 1,
+                                         pairs.as<uint2>(), c.stream));
+            HIPCHECK(hipStreamSynchronize(c.stream));
+            np += (unsigned long long)ul[0] + ul[1];
+        }
         HIPCHECK(hipStreamSynchronize(c.stream));        // before the scratch buffers of this block are freed
+    }
+    else if (outer_left || outer_right) {
+        // nothing matches: every row of the outer side(s), NULL-padded
+        const unsigned long long nl2 = outer_left ? A.n : 0, nr2 = outer_right ? B.n : 0;
+        DevBuf pb(std::max<unsigned long long>(nl2 + nr2, 1) * 8);
+        std::swap(pairs.p, pb.p);
+        if (nl2) HIPCHECK(cq_launch_join_fill(nullptr, nullptr, (uint32_t)nl2, 0, 0, pairs.as<uint2>(), c.stream));
+        if (nr2) HIPCHECK(cq_launch_join_fill(nullptr, nullptr, (uint32_t)nr2, nl2, 1, pairs.as<uint2>(), c.stream));
+        np = nl2 + nr2;
     }
     g_stats.records = np;
     Literals Lit;

@@ -1370,7 +1370,7 @@ __device__ __forceinline__ void eq_run(const JoinRight& J, uint32_t k, unsigned 
 }
 
 __global__ void join_count_kernel(const Cell* __restrict__ L, uint32_t ls, uint32_t lk, uint32_t nL, JoinRight J,
-                                  uint32_t* __restrict__ lo_out, unsigned long long* __restrict__ cnt) {
+                                  int outer_left, uint32_t* __restrict__ lo_out, unsigned long long* __restrict__ cnt) {
     const uint32_t l = blockIdx.x * blockDim.x + threadIdx.x;
     if (l >= nL) return;
     const Cell kc = L[(uint64_t)l * ls + lk];
@@ -1386,12 +1386,15 @@ __global__ void join_count_kernel(const Cell* __restrict__ L, uint32_t ls, uint3
         for (uint32_t y = 1; y < 4; y++)
             if (y != k) n += J.seg[y + 1] - J.seg[y];
     lo_out[l] = lo;
-    cnt[l] = n;
+    cnt[l] = (outer_left && n == 0) ? 1 : n;             // LEFT / FULL: the unmatched row, NULL-padded
 }
+
+constexpr uint32_t JOIN_NONE = 0xFFFFFFFFu;      // pair side absent (outer joins): NULL cells
 
 __global__ void join_emit_kernel(const Cell* __restrict__ L, uint32_t ls, uint32_t lk, uint32_t nL, JoinRight J,
                                  const uint32_t* __restrict__ lo_in, const unsigned long long* __restrict__ cnt,
-                                 const unsigned long long* __restrict__ offs, uint2* __restrict__ pairs) {
+                                 const unsigned long long* __restrict__ offs, uint2* __restrict__ pairs,
+                                 unsigned int* __restrict__ rmatched) {
     const uint32_t l = blockIdx.x * blockDim.x + threadIdx.x;
     if (l >= nL) return;
     const unsigned long long want = cnt[l];
@@ -1423,12 +1426,28 @@ __global__ void join_emit_kernel(const Cell* __restrict__ L, uint32_t ls, uint32
         int src = 0;
         if (ry < r) { r = ry; src = 1; }
         if (rz < r) { r = rz; src = 2; }
-        if (r == 0xFFFFFFFFu) break;                          // never: counts and streams agree
+        if (r == 0xFFFFFFFFu) {                               // only an outer join's unmatched left row
+            if (m == 0) pairs[o] = make_uint2(l, JOIN_NONE);
+            break;
+        }
         pairs[o + m] = make_uint2(l, r);
+        if (rmatched) rmatched[r] = 0u;                       // rmatched starts 1: "unmatched"
         if (src == 0) e++;
         else if (src == 1) ya++;
         else za++;
     }
+}
+
+// outer joins: pairs for the unmatched right rows (flags: 1 = unmatched; RIGHT / FULL, appended after
+// the left-major part in row order), or every row of one side (ON that matches
+// nothing: `ident = ident` not resolvable, or another condition shape)
+__global__ void join_fill_kernel(const unsigned int* __restrict__ flags, const unsigned int* __restrict__ pos,
+                                 uint32_t n, unsigned long long base, int right_side, uint2* __restrict__ pairs) {
+    const uint32_t i = blockIdx.x * blockDim.x + threadIdx.x;
+    if (i >= n) return;
+    if (flags && !flags[i]) return;                           // matched: not appended
+    const unsigned long long at = base + (pos ? pos[i] : i);
+    pairs[at] = right_side ? make_uint2(JOIN_NONE, i) : make_uint2(i, JOIN_NONE);
 }
 
 // the plan's need slots of one joined row
@@ -1437,8 +1456,11 @@ __device__ __forceinline__ void join_cells(const JoinMap& M, const Cell* L, cons
 #pragma unroll
     for (int k = 0; k < MAX_NEED; k++) {
         cs.c[k] = cell_null();
-        if (k < M.n)
-            cs.c[k] = M.side[k] ? R[(uint64_t)pr.y * M.rstride + M.col[k]] : L[(uint64_t)pr.x * M.lstride + M.col[k]];
+        if (k < M.n) {
+            const uint32_t row = M.side[k] ? pr.y : pr.x;
+            if (row != JOIN_NONE)
+                cs.c[k] = M.side[k] ? R[(uint64_t)row * M.rstride + M.col[k]] : L[(uint64_t)row * M.lstride + M.col[k]];
+        }
     }
 }
 
@@ -1536,8 +1558,11 @@ __global__ void join_project_kernel(const uint2* __restrict__ pairs, unsigned lo
     const uint64_t row = o - lo;
     const uint2 pr = pairs[i];
     Cell* cs = scratch + row * (uint64_t)(M.n ? M.n : 1);
-    for (int k = 0; k < M.n; k++)
-        cs[k] = M.side[k] ? R[(uint64_t)pr.y * M.rstride + M.col[k]] : L[(uint64_t)pr.x * M.lstride + M.col[k]];
+    for (int k = 0; k < M.n; k++) {
+        const uint32_t rw = M.side[k] ? pr.y : pr.x;
+        cs[k] = rw == JOIN_NONE ? cell_null()
+                                : (M.side[k] ? R[(uint64_t)rw * M.rstride + M.col[k]] : L[(uint64_t)rw * M.lstride + M.col[k]]);
+    }
     for (int k = 0; k < nout; k++) out[row * nout + k] = eval_value(code, off[k], off[k + 1], cs, 1, consts);
 }
 
@@ -1556,7 +1581,9 @@ __global__ void join_finish_kernel(const GroupOut* __restrict__ out, const unsig
         Cell c = cell_null();
         if (first != NOPOS) {
             const uint2 pr = pairs[first];
-            c = M.side[k] ? R[(uint64_t)pr.y * M.rstride + M.col[k]] : L[(uint64_t)pr.x * M.lstride + M.col[k]];
+            const uint32_t rw = M.side[k] ? pr.y : pr.x;
+            if (rw != JOIN_NONE)
+                c = M.side[k] ? R[(uint64_t)rw * M.rstride + M.col[k]] : L[(uint64_t)rw * M.lstride + M.col[k]];
         }
         cs[k] = c;
     }
@@ -1814,16 +1841,24 @@ hipError_t cq_launch_gather_codes(const unsigned long long* codes, const uint32_
     return hipGetLastError();
 }
 hipError_t cq_launch_join_count(const cq::Cell* L, uint32_t ls, uint32_t lk, uint32_t nL, const cq::JoinRight* J,
-                                uint32_t* lo, unsigned long long* cnt, hipStream_t s) {
+                                int outer_left, uint32_t* lo, unsigned long long* cnt, hipStream_t s) {
     if (!nL) return hipSuccess;
-    hipLaunchKernelGGL(cq::join_count_kernel, dim3(grid_of(nL, 256)), dim3(256), 0, s, L, ls, lk, nL, *J, lo, cnt);
+    hipLaunchKernelGGL(cq::join_count_kernel, dim3(grid_of(nL, 256)), dim3(256), 0, s, L, ls, lk, nL, *J, outer_left,
+                       lo, cnt);
     return hipGetLastError();
 }
 hipError_t cq_launch_join_emit(const cq::Cell* L, uint32_t ls, uint32_t lk, uint32_t nL, const cq::JoinRight* J,
                                const uint32_t* lo, const unsigned long long* cnt, const unsigned long long* offs,
-                               uint2* pairs, hipStream_t s) {
+                               uint2* pairs, unsigned int* rmatched, hipStream_t s) {
     if (!nL) return hipSuccess;
     hipLaunchKernelGGL(cq::join_emit_kernel, dim3(grid_of(nL, 256)), dim3(256), 0, s, L, ls, lk, nL, *J, lo, cnt, offs,
+                       pairs, rmatched);
+    return hipGetLastError();
+}
+hipError_t cq_launch_join_fill(const unsigned int* flags, const unsigned int* pos, uint32_t n, unsigned long long base,
+                               int right_side, uint2* pairs, hipStream_t s) {
+    if (!n) return hipSuccess;
+    hipLaunchKernelGGL(cq::join_fill_kernel, dim3(grid_of(n, 256)), dim3(256), 0, s, flags, pos, n, base, right_side,
                        pairs);
     return hipGetLastError();
 }

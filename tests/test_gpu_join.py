@@ -123,6 +123,27 @@ MIXED = [
 ]
 
 
+OUTER = [
+    "SELECT COUNT(*) FROM '{U}' AS u LEFT JOIN '{O}' AS o ON u.id = o.customer_id",
+    "SELECT COUNT(*) FROM '{U}' AS u RIGHT JOIN '{O}' AS o ON u.id = o.customer_id",
+    "SELECT COUNT(*) FROM '{U}' AS u FULL JOIN '{O}' AS o ON u.id = o.customer_id",
+    "SELECT u.role, COUNT(*), SUM(o.price), MAX(o.id) FROM '{U}' AS u LEFT JOIN '{O}' AS o ON u.id = o.customer_id GROUP BY u.role",
+    "SELECT o.quantity, COUNT(*), MIN(u.name) FROM '{U}' AS u RIGHT JOIN '{O}' AS o ON u.id = o.customer_id GROUP BY o.quantity",
+    "SELECT u.id, u.name, o.id, o.price FROM '{U}' AS u FULL JOIN '{O}' AS o ON u.id = o.customer_id WHERE o.quantity = 2 OR u.age > 80",
+    "SELECT u.id, o.id FROM '{U}' AS u LEFT JOIN '{O}' AS o ON u.id = o.customer_id LIMIT 40 OFFSET 2990",
+    "SELECT u.id, o.id FROM '{U}' AS u RIGHT JOIN '{O}' AS o ON u.id = o.customer_id ORDER BY o.id DESC LIMIT 30",
+    "SELECT COUNT(*), SUM(o.price) FROM '{U}' AS u LEFT JOIN '{O}' AS o ON u.nosuch = o.customer_id",
+    "SELECT COUNT(*) FROM '{U}' AS u FULL JOIN '{O}' AS o ON u.id > o.customer_id",
+]
+
+
+@pytest.mark.parametrize("tmpl", OUTER)
+def test_join_outer(files, tmpl):
+    """LEFT / RIGHT / FULL (evaluator_joins.c:128-171): unmatched left rows NULL-padded
+    in place, unmatched right rows appended after, in row order"""
+    _check(tmpl.replace("{U}", str(files["users"])).replace("{O}", str(files["orders"])))
+
+
 @pytest.mark.parametrize("tmpl", MIXED)
 def test_join_mixed_classes(files, tmpl):
     """keys of different value classes compare "equal" (csv_reader.c:128): every
