@@ -16,6 +16,8 @@
 #include <cstdlib>
 #include <cstring>
 #include <string>
+#include <map>
+#include <tuple>
 #include <unordered_map>
 #include <vector>
 
@@ -76,6 +78,22 @@ hipError_t cq_launch_join_project(const uint2* pairs, unsigned long long np, con
 hipError_t cq_launch_join_finish(const cq::GroupOut* out, const unsigned int* count, unsigned int cap_out,
                                  const uint2* pairs, const cq::JoinMap* M, const cq::Cell* L, const cq::Cell* R,
                                  int nacc, uint32_t sb, cq::Cell* cells, uint8_t* bytes, hipStream_t s);
+hipError_t cq_launch_vla_prep(const cq::Cell* cells, uint32_t n, uint32_t nc, int gslot, uint32_t vslot,
+                              unsigned long long* kw0, unsigned long long* kw1, unsigned long long* kcl,
+                              unsigned long long* vkey, unsigned int* flag, hipStream_t s);
+hipError_t cq_launch_vla_compact(const unsigned int* flag, const unsigned int* pos, uint32_t n, unsigned int* perm,
+                                 hipStream_t s);
+hipError_t cq_launch_vla_gather(const unsigned long long* a, const unsigned int* perm, uint32_t m,
+                                unsigned long long* out, hipStream_t s);
+hipError_t cq_launch_vla_heads(const unsigned long long* kw0, const unsigned long long* kw1,
+                               const unsigned long long* kcl, const unsigned int* perm, uint32_t m, unsigned int* head,
+                               hipStream_t s);
+hipError_t cq_launch_vla_starts(const unsigned int* head, const unsigned int* sid, uint32_t m, unsigned int* start,
+                                hipStream_t s);
+hipError_t cq_launch_vla_reduce(const unsigned long long* vkey, const unsigned long long* kw0,
+                                const unsigned long long* kw1, const unsigned long long* kcl, const unsigned int* perm,
+                                const unsigned int* start, uint32_t nseg, uint32_t m, int kind, unsigned long long* out,
+                                hipStream_t s);
 hipError_t cq_sort_codes(void* temp, size_t* temp_bytes, const unsigned long long* kin, unsigned long long* kout,
                          const unsigned int* vin, unsigned int* vout, size_t n, hipStream_t s);
 hipError_t cq_excl_sum_u64(void* temp, size_t* temp_bytes, const unsigned long long* in, unsigned long long* out,
@@ -450,7 +468,7 @@ std::vector<HCell> fetch_cells(DevCtx& c, const std::vector<Cell>& cells) {
 }
 
 // ------------------------------------------------------------------ compiled plan
-enum OutKind { OUT_COUNT, OUT_SUM, OUT_AVG, OUT_EXT, OUT_REP, OUT_CONST, OUT_NULL };
+enum OutKind { OUT_COUNT, OUT_SUM, OUT_AVG, OUT_EXT, OUT_REP, OUT_CONST, OUT_NULL, OUT_VLA };
 struct OutCol {
     OutKind kind = OUT_NULL;
     int acc = -1;          // accumulator index for SUM/AVG/EXT
@@ -468,6 +486,8 @@ struct Compiled {
     std::vector<std::string> names;
     std::vector<int> rep_cols;       // csv column per rep slot
     int max_depth = 0;
+    int group_col = -1;              // csv column of the GROUP BY key
+    std::vector<std::pair<int, int>> vla;   // STDDEV (0) / MEDIAN (1) and their csv column
 };
 
 struct Compiler {
@@ -754,6 +774,7 @@ void compile_aggregate(const cqgpu_table* t, cq_node* q, Compiled& C) {
             }
         }
         int gc = col_index_fallback(t, key);
+        C.group_col = gc;
         if (gc < 0) C.group_missing = true;
         else C.P.group_slot = cc.need(gc);
     }
@@ -775,11 +796,22 @@ void compile_aggregate(const cqgpu_table* t, cq_node* q, Compiled& C) {
             size_t pc = cn.find(')', par + 1);
             std::string arg = pc != std::string::npos ? cn.substr(par + 1, pc - par - 1) : cn;
             const char* f = fn.c_str();
-            if (!strcasecmp(f, "STDDEV") || !strcasecmp(f, "STDDEV_POP") || !strcasecmp(f, "MEDIAN"))
-                throw Ineligible{"STDDEV/MEDIAN"};
+            const bool is_vla = !strcasecmp(f, "STDDEV") || !strcasecmp(f, "STDDEV_POP") || !strcasecmp(f, "MEDIAN");
             if (!strcasecmp(f, "COUNT") && arg == "*") { oc.kind = OUT_COUNT; C.outs.push_back(oc); continue; }
             int col = col_index_fallback(t, arg.c_str());
             if (col < 0) { oc.kind = OUT_NULL; C.outs.push_back(oc); continue; }
+            if (is_vla) {          // value-list aggregates: compute_vla after the scan
+                const std::pair<int, int> v{!strcasecmp(f, "MEDIAN") ? 1 : 0, col};
+                auto it = std::find(C.vla.begin(), C.vla.end(), v);
+                oc.acc = (int)(it - C.vla.begin());
+                if (it == C.vla.end()) {
+                    if (C.vla.size() >= (size_t)MAX_ACC) throw Ineligible{"too many STDDEV/MEDIAN"};
+                    C.vla.push_back(v);
+                }
+                oc.kind = OUT_VLA;
+                C.outs.push_back(oc);
+                continue;
+            }
             if (!strcasecmp(f, "COUNT")) { oc.kind = OUT_COUNT; C.outs.push_back(oc); continue; }
             uint8_t kind = (!strcasecmp(f, "SUM") || !strcasecmp(f, "AVG")) ? ACC_SUM
                          : (!strcasecmp(f, "MIN") ? ACC_MIN : ACC_MAX);
@@ -825,6 +857,8 @@ struct HGroup {
     HCell ext[MAX_ACC];
     unsigned long long extpos[MAX_ACC] = {NOPOS, NOPOS, NOPOS, NOPOS, NOPOS, NOPOS, NOPOS, NOPOS};
     std::vector<HCell> reps;            // representative cells (first row)
+    double vla[MAX_ACC] = {};           // STDDEV / MEDIAN results
+    bool vla_ok[MAX_ACC] = {};          // false: no numeric value (NULL)
 };
 
 // little-endian byte writer / reader of the partial-aggregation blobs
@@ -1252,6 +1286,9 @@ cq_table* build_groups(const Compiled& C, const std::vector<HGroup>& groups, con
                     v.bits = dbl_bits(h.num[o.acc] ? h.sum[o.acc] / (double)h.num[o.acc] : 0.0);
                     break;
                 case OUT_EXT: if (h.extpos[o.acc] != NOPOS) v = h.ext[o.acc]; break;
+                case OUT_VLA:
+                    if (h.vla_ok[o.acc]) { v.kind = K_DBL; v.bits = dbl_bits(h.vla[o.acc]); }
+                    break;
                 case OUT_REP: if (h.cnt > 0 && o.rep < (int)h.reps.size()) v = h.reps[o.rep]; break;
                 case OUT_CONST: if (h.cnt > 0) v = litcells[o.lit]; break;
                 default: break;
@@ -1656,6 +1693,122 @@ cq_table* run_rows(DevCtx& c, const cqgpu_table* t, Compiled& C, RowPlan& R, cq_
     return r;
 }
 
+// STDDEV / MEDIAN (evaluate_aggregate, evaluator_aggregates.c:328-411): the
+// WHERE-passing records' group key and value cells, sorted on the device by
+// (key, value), reduced per group (scan.hip vla_* kernels), matched back to the
+// scan's groups by key
+void compute_vla(DevCtx& c, const cqgpu_table* t, const Compiled& C, std::vector<HGroup>& groups) {
+    if (C.vla.empty() || groups.empty()) return;
+    const cqgpu_stats saved = g_stats;
+    Compiled W = C;                          // the WHERE alone, matching records out
+    W.grouped = false;
+    W.P.group_slot = -1;
+    W.P.nacc = 0;
+    W.rep_cols.clear();
+    W.vla.clear();
+    Literals L;
+    ScanStats st;
+    const unsigned long long cap = t->n / 2 + 2;
+    DevBuf rows(cap * 8);
+    (void)run_aggregate(c, t, W, L, &st, rows.as<unsigned long long>(), cap);
+    const unsigned long long n64 = st.rows_emitted;
+    g_stats = saved;
+    if (n64 > cap) throw HipError{"STDDEV/MEDIAN: record count exceeds the offset buffer"};
+    if (n64 >= (1ull << 31)) throw Ineligible{"STDDEV/MEDIAN over more than 2^31 rows"};
+    const uint32_t n = (uint32_t)n64;
+    std::vector<int> cols;
+    if (C.grouped) cols.push_back(C.group_col);
+    for (auto& v : C.vla) cols.push_back(v.second);
+    std::sort(cols.begin(), cols.end());
+    cols.erase(std::unique(cols.begin(), cols.end()), cols.end());
+    ColsDesc D;
+    memset(&D, 0, sizeof D);
+    D.ncols = (int)cols.size();
+    for (int k = 0; k < D.ncols; k++) D.cols[k] = (int16_t)cols[k];
+    D.delim = (uint8_t)t->cfg.delimiter;
+    D.quote = (uint8_t)t->cfg.quote;
+    auto slot = [&](int col) { return (int)(std::find(cols.begin(), cols.end(), col) - cols.begin()); };
+    DevBuf cells((size_t)std::max<uint32_t>(n, 1) * D.ncols * sizeof(Cell));
+    HIPCHECK(cq_launch_cells(t->g, rows.as<unsigned long long>(), n, &D, cells.as<Cell>(), c.stream));
+    // host map: group key -> group (GK_LONG keys by content hash, as the kernel keys them)
+    std::map<std::tuple<uint64_t, uint64_t, uint64_t>, size_t> at;
+    for (size_t g = 0; g < groups.size(); g++) {
+        const HGroup& h = groups[g];
+        const uint64_t cl = C.grouped ? ((uint64_t)h.kcls << 16 | h.klen) : ((uint64_t)GK_ALL << 16);
+        const uint64_t w0 = !C.grouped || h.kcls == GK_LONG ? 0 : h.kw0;
+        const uint64_t w1 = C.grouped ? h.kw1 : 0;
+        at[std::make_tuple(cl, w0, w1)] = g;
+    }
+    const size_t N = std::max<uint32_t>(n, 1);
+    DevBuf kw0(N * 8), kw1(N * 8), kcl(N * 8), vkey(N * 8), flag(N * 4), pos(N * 4), perm(N * 4), perm2(N * 4),
+        keys(N * 8), keys2(N * 8), head(N * 4), sid(N * 4), start(N * 4), out(N * 32);
+    for (size_t vi = 0; vi < C.vla.size(); vi++) {
+        const int kind = C.vla[vi].first;
+        HIPCHECK(cq_launch_vla_prep(cells.as<Cell>(), n, (uint32_t)D.ncols, C.grouped ? slot(C.group_col) : -1,
+                                    (uint32_t)slot(C.vla[vi].second), kw0.as<unsigned long long>(),
+                                    kw1.as<unsigned long long>(), kcl.as<unsigned long long>(),
+                                    vkey.as<unsigned long long>(), flag.as<unsigned int>(), c.stream));
+        uint32_t m = 0;
+        if (n) {
+            size_t tb = 0;
+            HIPCHECK(cq_excl_sum_u32(nullptr, &tb, flag.as<unsigned int>(), pos.as<unsigned int>(), n, c.stream));
+            DevBuf temp(tb);
+            HIPCHECK(cq_excl_sum_u32(temp.p, &tb, flag.as<unsigned int>(), pos.as<unsigned int>(), n, c.stream));
+            unsigned int last[2] = {0, 0};
+            HIPCHECK(hipMemcpyAsync(&last[0], pos.as<unsigned int>() + n - 1, 4, hipMemcpyDeviceToHost, c.stream));
+            HIPCHECK(hipMemcpyAsync(&last[1], flag.as<unsigned int>() + n - 1, 4, hipMemcpyDeviceToHost, c.stream));
+            HIPCHECK(hipStreamSynchronize(c.stream));
+            m = last[0] + last[1];
+        }
+        if (!m) continue;                   // no numeric value anywhere: every group NULL
+        HIPCHECK(cq_launch_vla_compact(flag.as<unsigned int>(), pos.as<unsigned int>(), n, perm.as<unsigned int>(),
+                                       c.stream));
+        // LSD: value, then the key words (stable sorts keep the value order inside a key)
+        const unsigned long long* passes[4] = {vkey.as<unsigned long long>(), kcl.as<unsigned long long>(),
+                                               kw1.as<unsigned long long>(), kw0.as<unsigned long long>()};
+        for (int ps = 0; ps < 4; ps++) {
+            if (ps > 0 && !C.grouped) break;
+            HIPCHECK(cq_launch_vla_gather(passes[ps], perm.as<unsigned int>(), m, keys.as<unsigned long long>(),
+                                          c.stream));
+            size_t tb = 0;
+            HIPCHECK(cq_sort_codes(nullptr, &tb, keys.as<unsigned long long>(), keys2.as<unsigned long long>(),
+                                   perm.as<unsigned int>(), perm2.as<unsigned int>(), m, c.stream));
+            DevBuf temp(tb);
+            HIPCHECK(cq_sort_codes(temp.p, &tb, keys.as<unsigned long long>(), keys2.as<unsigned long long>(),
+                                   perm.as<unsigned int>(), perm2.as<unsigned int>(), m, c.stream));
+            HIPCHECK(hipStreamSynchronize(c.stream));
+            std::swap(perm.p, perm2.p);
+        }
+        HIPCHECK(cq_launch_vla_heads(kw0.as<unsigned long long>(), kw1.as<unsigned long long>(),
+                                     kcl.as<unsigned long long>(), perm.as<unsigned int>(), m, head.as<unsigned int>(),
+                                     c.stream));
+        size_t tb = 0;
+        HIPCHECK(cq_excl_sum_u32(nullptr, &tb, head.as<unsigned int>(), sid.as<unsigned int>(), m, c.stream));
+        DevBuf temp(tb);
+        HIPCHECK(cq_excl_sum_u32(temp.p, &tb, head.as<unsigned int>(), sid.as<unsigned int>(), m, c.stream));
+        unsigned int last[2] = {0, 0};
+        HIPCHECK(hipMemcpyAsync(&last[0], sid.as<unsigned int>() + m - 1, 4, hipMemcpyDeviceToHost, c.stream));
+        HIPCHECK(hipMemcpyAsync(&last[1], head.as<unsigned int>() + m - 1, 4, hipMemcpyDeviceToHost, c.stream));
+        HIPCHECK(hipStreamSynchronize(c.stream));
+        const uint32_t nseg = last[0] + last[1];
+        HIPCHECK(cq_launch_vla_starts(head.as<unsigned int>(), sid.as<unsigned int>(), m, start.as<unsigned int>(),
+                                      c.stream));
+        HIPCHECK(cq_launch_vla_reduce(vkey.as<unsigned long long>(), kw0.as<unsigned long long>(),
+                                      kw1.as<unsigned long long>(), kcl.as<unsigned long long>(), perm.as<unsigned int>(),
+                                      start.as<unsigned int>(), nseg, m, kind, out.as<unsigned long long>(), c.stream));
+        std::vector<unsigned long long> h((size_t)nseg * 4);
+        HIPCHECK(hipMemcpyAsync(h.data(), out.p, h.size() * 8, hipMemcpyDeviceToHost, c.stream));
+        HIPCHECK(hipStreamSynchronize(c.stream));
+        for (uint32_t sg = 0; sg < nseg; sg++) {
+            auto it = at.find(std::make_tuple((uint64_t)h[4 * sg], (uint64_t)h[4 * sg + 1], (uint64_t)h[4 * sg + 2]));
+            if (it == at.end()) continue;
+            HGroup& g = groups[it->second];
+            g.vla[vi] = as_dbl(h[4 * sg + 3]);
+            g.vla_ok[vi] = true;
+        }
+    }
+}
+
 void check_plan_shape(cq_node* q, const cqgpu_table* t, bool join_ok);
 bool is_row_query(cq_node* q);
 
@@ -1785,6 +1938,7 @@ cq_table* run_join(DevCtx& c, cq_node* q, const cqgpu_table* L, const cqgpu_tabl
     RowPlan RP;
     if (rows) compile_rows(&J, q, C, RP);
     else compile_aggregate(&J, q, C);
+    if (!C.vla.empty()) throw Ineligible{"STDDEV/MEDIAN over a join"};
     // the columns each side parses
     JoinSide A, B;
     if (keyed) { A.cols.push_back(kl); B.cols.push_back(kr); }
@@ -2071,6 +2225,7 @@ cq_table* query_impl(cq_node* q, cqgpu_table* const* tables, int ntables) {
     compile_aggregate(t, q, C);
     Literals L;
     std::vector<HGroup> groups = run_aggregate(c, t, C, L, nullptr);
+    compute_vla(c, t, C, groups);
     g_stats.groups = groups.size();
     cq_table* res = build_groups(C, groups, L, c);
     post_ops(c, res, q);
@@ -2432,6 +2587,7 @@ size_t cqgpu_query_partial(cq_node* q, cqgpu_table* const* tables, int ntables, 
         if (is_row_query(q)) throw Ineligible{"row-returning SELECT across partials"};
         Compiled C;
         compile_aggregate(t, q, C);
+        if (!C.vla.empty()) throw Ineligible{"STDDEV/MEDIAN across partials (needs every value)"};
         Literals L;
         ScanStats st;
         memset(&st, 0, sizeof st);

@@ -1602,6 +1602,101 @@ __global__ void join_finish_kernel(const GroupOut* __restrict__ out, const unsig
     }
 }
 
+// ------------------------------------------------------------------ STDDEV / MEDIAN
+// evaluate_aggregate's value-list aggregates (evaluator_aggregates.c:328-411): the
+// numeric values of a column per group, sorted by (group key, value) on the
+// device, then one pass per group: population STDDEV (mean first, then the
+// squared deviations) and MEDIAN (middle value, or the mean of the middle two).
+
+// per passing record: group key words (GK_LONG keys by content hash) and the
+// column's numeric value as an order-preserving 64-bit key; flag 1 when numeric
+__global__ void vla_prep_kernel(const Cell* __restrict__ cells, uint32_t n, uint32_t nc, int gslot, uint32_t vslot,
+                                unsigned long long* __restrict__ kw0, unsigned long long* __restrict__ kw1,
+                                unsigned long long* __restrict__ kcl, unsigned long long* __restrict__ vkey,
+                                unsigned int* __restrict__ flag) {
+    const uint32_t i = blockIdx.x * blockDim.x + threadIdx.x;
+    if (i >= n) return;
+    GKey k;
+    k.cls = GK_ALL; k.len = 0; k.w0 = 0; k.w1 = 0;
+    if (gslot >= 0) k = group_key(cells[(uint64_t)i * nc + gslot]);
+    kw0[i] = k.cls == GK_LONG ? 0ull : k.w0;
+    kw1[i] = k.w1;
+    kcl[i] = gk_clslen(k);
+    const Cell v = cells[(uint64_t)i * nc + vslot];
+    const uint64_t b = dbl_bits(num_of(v));
+    vkey[i] = (b >> 63) ? ~b : (b | 0x8000000000000000ULL);
+    flag[i] = is_num(v) ? 1u : 0u;
+}
+
+__global__ void vla_compact_kernel(const unsigned int* __restrict__ flag, const unsigned int* __restrict__ pos,
+                                   uint32_t n, unsigned int* __restrict__ perm) {
+    const uint32_t i = blockIdx.x * blockDim.x + threadIdx.x;
+    if (i < n && flag[i]) perm[pos[i]] = i;
+}
+
+__global__ void vla_gather_kernel(const unsigned long long* __restrict__ a, const unsigned int* __restrict__ perm,
+                                  uint32_t m, unsigned long long* __restrict__ out) {
+    const uint32_t i = blockIdx.x * blockDim.x + threadIdx.x;
+    if (i < m) out[i] = a[perm[i]];
+}
+
+// 1 where a new group starts in the sorted order
+__global__ void vla_heads_kernel(const unsigned long long* __restrict__ kw0, const unsigned long long* __restrict__ kw1,
+                                 const unsigned long long* __restrict__ kcl, const unsigned int* __restrict__ perm,
+                                 uint32_t m, unsigned int* __restrict__ head) {
+    const uint32_t i = blockIdx.x * blockDim.x + threadIdx.x;
+    if (i >= m) return;
+    const uint32_t p = perm[i];
+    bool h = i == 0;
+    if (!h) {
+        const uint32_t q = perm[i - 1];
+        h = kw0[p] != kw0[q] || kw1[p] != kw1[q] || kcl[p] != kcl[q];
+    }
+    head[i] = h ? 1u : 0u;
+}
+
+__global__ void vla_starts_kernel(const unsigned int* __restrict__ head, const unsigned int* __restrict__ sid,
+                                  uint32_t m, unsigned int* __restrict__ start) {
+    const uint32_t i = blockIdx.x * blockDim.x + threadIdx.x;
+    if (i < m && head[i]) start[sid[i]] = i;
+}
+
+__device__ __forceinline__ double vla_value(unsigned long long k) {
+    const uint64_t b = (k >> 63) ? (k & 0x7FFFFFFFFFFFFFFFULL) : ~k;
+    return as_dbl(b);
+}
+
+// one thread per group: kind 0 STDDEV (population), 1 MEDIAN
+__global__ void vla_reduce_kernel(const unsigned long long* __restrict__ vkey, const unsigned long long* __restrict__ kw0,
+                                  const unsigned long long* __restrict__ kw1, const unsigned long long* __restrict__ kcl,
+                                  const unsigned int* __restrict__ perm, const unsigned int* __restrict__ start,
+                                  uint32_t nseg, uint32_t m, int kind, unsigned long long* __restrict__ out) {
+    const uint32_t s = blockIdx.x * blockDim.x + threadIdx.x;
+    if (s >= nseg) return;
+    const uint32_t a = start[s], b = s + 1 < nseg ? start[s + 1] : m;
+    const uint32_t n = b - a;
+    double r;
+    if (kind == 0) {
+        double sum = 0;
+        for (uint32_t i = a; i < b; i++) sum += vla_value(vkey[perm[i]]);
+        const double mean = sum / n;
+        double vs = 0;
+        for (uint32_t i = a; i < b; i++) {
+            const double d = vla_value(vkey[perm[i]]) - mean;
+            vs += d * d;
+        }
+        r = sqrt(vs / n);
+    } else {
+        r = (n & 1) ? vla_value(vkey[perm[a + n / 2]])
+                    : (vla_value(vkey[perm[a + n / 2 - 1]]) + vla_value(vkey[perm[a + n / 2]])) / 2.0;
+    }
+    const uint32_t p = perm[a];
+    out[4 * (uint64_t)s + 0] = kcl[p];
+    out[4 * (uint64_t)s + 1] = kw0[p];
+    out[4 * (uint64_t)s + 2] = kw1[p];
+    out[4 * (uint64_t)s + 3] = dbl_bits(r);
+}
+
 }  // namespace cq
 
 // ------------------------------------------------------------------ host wrappers
@@ -1893,6 +1988,50 @@ hipError_t cq_launch_join_finish(const cq::GroupOut* out, const unsigned int* co
                                  int nacc, uint32_t sb, cq::Cell* cells, uint8_t* bytes, hipStream_t s) {
     hipLaunchKernelGGL(cq::join_finish_kernel, dim3(grid_of(cap_out, 128)), dim3(128), 0, s, out, count, cap_out,
                        pairs, *M, L, R, nacc, sb, cells, bytes);
+    return hipGetLastError();
+}
+
+// ---- STDDEV / MEDIAN kernels (executor.hip compute_vla)
+hipError_t cq_launch_vla_prep(const cq::Cell* cells, uint32_t n, uint32_t nc, int gslot, uint32_t vslot,
+                              unsigned long long* kw0, unsigned long long* kw1, unsigned long long* kcl,
+                              unsigned long long* vkey, unsigned int* flag, hipStream_t s) {
+    if (!n) return hipSuccess;
+    hipLaunchKernelGGL(cq::vla_prep_kernel, dim3(grid_of(n, 256)), dim3(256), 0, s, cells, n, nc, gslot, vslot, kw0,
+                       kw1, kcl, vkey, flag);
+    return hipGetLastError();
+}
+hipError_t cq_launch_vla_compact(const unsigned int* flag, const unsigned int* pos, uint32_t n, unsigned int* perm,
+                                 hipStream_t s) {
+    if (!n) return hipSuccess;
+    hipLaunchKernelGGL(cq::vla_compact_kernel, dim3(grid_of(n, 256)), dim3(256), 0, s, flag, pos, n, perm);
+    return hipGetLastError();
+}
+hipError_t cq_launch_vla_gather(const unsigned long long* a, const unsigned int* perm, uint32_t m,
+                                unsigned long long* out, hipStream_t s) {
+    if (!m) return hipSuccess;
+    hipLaunchKernelGGL(cq::vla_gather_kernel, dim3(grid_of(m, 256)), dim3(256), 0, s, a, perm, m, out);
+    return hipGetLastError();
+}
+hipError_t cq_launch_vla_heads(const unsigned long long* kw0, const unsigned long long* kw1,
+                               const unsigned long long* kcl, const unsigned int* perm, uint32_t m, unsigned int* head,
+                               hipStream_t s) {
+    if (!m) return hipSuccess;
+    hipLaunchKernelGGL(cq::vla_heads_kernel, dim3(grid_of(m, 256)), dim3(256), 0, s, kw0, kw1, kcl, perm, m, head);
+    return hipGetLastError();
+}
+hipError_t cq_launch_vla_starts(const unsigned int* head, const unsigned int* sid, uint32_t m, unsigned int* start,
+                                hipStream_t s) {
+    if (!m) return hipSuccess;
+    hipLaunchKernelGGL(cq::vla_starts_kernel, dim3(grid_of(m, 256)), dim3(256), 0, s, head, sid, m, start);
+    return hipGetLastError();
+}
+hipError_t cq_launch_vla_reduce(const unsigned long long* vkey, const unsigned long long* kw0,
+                                const unsigned long long* kw1, const unsigned long long* kcl, const unsigned int* perm,
+                                const unsigned int* start, uint32_t nseg, uint32_t m, int kind, unsigned long long* out,
+                                hipStream_t s) {
+    if (!nseg) return hipSuccess;
+    hipLaunchKernelGGL(cq::vla_reduce_kernel, dim3(grid_of(nseg, 64)), dim3(64), 0, s, vkey, kw0, kw1, kcl, perm, start,
+                       nseg, m, kind, out);
     return hipGetLastError();
 }
 

@@ -1,0 +1,70 @@
+"""STDDEV / MEDIAN on the GPU (executor.hip compute_vla, scan.hip vla_* kernels)
+against the oracle's evaluate_aggregate (reference evaluator_aggregates.c:328-411).
+
+Population STDDEV (two passes: mean, squared deviations) within 1e-6 relative;
+MEDIAN bit-exact (middle value, or the mean of the two middle values); groups
+without a numeric value give NULL; strings, dates and NULLs are skipped; WHERE
+filters first.
+"""
+import numpy as np
+import pytest
+
+import cqtest
+import cq_amd
+from cq_amd import datagen
+
+pytestmark = pytest.mark.gpu
+REL = 1e-6
+
+
+@pytest.fixture(scope="module")
+def files(tmp_path_factory):
+    d = tmp_path_factory.mktemp("stats")
+    rng = np.random.default_rng(23)
+    lines = ["g,x,y,s"]
+    for i in range(40_000):
+        g = "g%02d" % rng.integers(0, 60)
+        k = rng.integers(0, 30)
+        x = "" if k == 0 else ("abc" if k == 1 else ("%d" % rng.integers(-500, 500) if k < 15
+                                                    else "%.3f" % rng.normal(10.0, 3.0)))
+        y = "%d" % rng.integers(0, 7)
+        lines.append(f"{g},{x},{y},{'t' if i % 3 else 'f'}")
+    lines.append("gnull,abc,1,t")                  # a group with no numeric x
+    f = {"mix": d / "mix.csv"}
+    f["mix"].write_text("\n".join(lines) + "\n")
+    f["role"] = d / "role.csv"
+    datagen.write_shape_a(str(f["role"]), 200_000, seed=5, with_role=True)
+    return f
+
+
+def _check(sql):
+    want, unsup = cqtest.oracle_query(sql)
+    assert not unsup, sql
+    with cqtest.Parsed(sql) as ast:
+        got = cq_amd.evaluate(ast)
+        inel = cq_amd.last_ineligible()
+    assert not inel, (sql, inel)
+    assert cq_amd.stats()["path"] == 1
+    sel = sql.split(" FROM ")[0][len("SELECT "):]
+    tol = {i for i, t in enumerate(s.strip().upper() for s in sel.split(",")) if t.startswith(("STDDEV", "SUM", "AVG"))}
+    assert got["columns"] == want["columns"], sql
+    assert len(got["rows"]) == len(want["rows"]), sql
+    for i, (g, w) in enumerate(zip(got["rows"], want["rows"])):
+        for j, (x, y) in enumerate(zip(g, w)):
+            assert cqtest.cell_equal(x, y, REL if j in tol else 0.0), f"{sql}: row {i} col {j}: {x} vs {y}"
+
+
+QUERIES = [
+    "SELECT STDDEV(x), MEDIAN(x), COUNT(*) FROM '{M}'",
+    "SELECT g, STDDEV(x), MEDIAN(x), AVG(x) FROM '{M}' GROUP BY g",
+    "SELECT g, MEDIAN(y), STDDEV_POP(y) FROM '{M}' WHERE s = 't' GROUP BY g",
+    "SELECT y, MEDIAN(x), COUNT(*) FROM '{M}' WHERE x > 0 GROUP BY y ORDER BY y",
+    "SELECT s, STDDEV(x) FROM '{M}' WHERE g = 'gnull' GROUP BY s",
+    "SELECT role, STDDEV(height), MEDIAN(age) FROM '{R}' WHERE age > 30 GROUP BY role",
+    "SELECT MEDIAN(height), STDDEV(age) FROM '{R}'",
+]
+
+
+@pytest.mark.parametrize("tmpl", QUERIES)
+def test_stddev_median(files, tmpl):
+    _check(tmpl.replace("{M}", str(files["mix"])).replace("{R}", str(files["role"])))
