@@ -115,14 +115,21 @@ struct LeanPlan {
     int32_t acc_sidx[MAX_ACC];   // accumulator -> SUM index
     uint32_t gcol;               // GROUP BY CSV column
     uint32_t delim, quote;
+    uint32_t rcol[KN];           // the roles' CSV columns, ascending
+    uint32_t rrole[KN];          // their roles: R_WHERE, R_SUM0, R_SUM1, R_GROUP
 };
+enum : uint32_t { R_WHERE = 0, R_SUM0 = 1, R_SUM1 = 2, R_GROUP = 3 };
 
-// kernel arguments (kernarg segment: no per-launch symbol copies)
+// kernel arguments (kernarg segment).  The two HBM group tables (canonical keys,
+// shared with slow_kernel, and raw-byte keys for block flushes and LDS spills) are
+// read through a pointer to a device copy instead: only the rare spill path and
+// the final flush touch them, and their ~1 KB of pointers held in scalar
+// registers across the window loop spilled SGPRs into VGPR lanes.
 struct LeanArgs {
     LeanPlan lp;
-    GroupTable gt;       // canonical keys (shared with slow_kernel)
-    GroupTable rt;       // raw-byte keys (GK_RAW): block flushes and LDS spills
 };
+enum : int { TAB_GT = 0, TAB_RT = 1 };
+__device__ GroupTable g_lean_tabs[2];
 
 constexpr uint32_t GK_RAW = 6;       // raw field bytes as key (cell.h GK_* never produce 6)
 __device__ __forceinline__ GKey raw_key(uint32_t len, uint64_t w0, uint64_t w1) {
@@ -150,30 +157,45 @@ __device__ __forceinline__ uint32_t nib(uint32_t f) {
     return t & 0xFu;
 }
 
-// separator / terminator / quote bits of 32 bytes (bit i = byte i)
+// separator / terminator / quote bits of 32 bytes (bit i = byte i).
+//
+// Byte classes by v_perm_b32 lookups: a selector byte 0-7 picks a table byte,
+// 8-11 the sign of table byte 1/3/5/7, 12 gives 0x00 and 13-255 give 0xFF.  With
+// z = x ^ 0x08 the terminators land on selectors 2 ('\n') and 5 ('\r'), with
+// z = x ^ delim the delimiter on 0; those table bytes are 0x40, all others 0, so
+// a byte's lookup is 0x40 exactly when it is in the class, else 0x00 or 0xFF
+// (bit 6 and not bit 7 is the flag).  Needs delim >= 0x10, so that '\n' / '\r'
+// xor delim and delim xor 0x08 are never selectors 0-12 (lean_shape: delim > ' ').
+// The 0x40 flags of two dwords become a byte of bits with one v_dot4_u32_u8
+// each (weights 1..128), four such bytes the 32-bit mask.  Quote presence is
+// the borrow-based zero-byte test (exact for "any").
+__device__ __forceinline__ uint32_t flags40(uint32_t r) {
+    return r & ~(r >> 1) & 0x40404040u;
+}
 __device__ __forceinline__ void classify(const v4u a, const v4u b, uint32_t rep_d, uint32_t rep_q, uint32_t& sep,
                                          uint32_t& nl, uint32_t& qf) {
-    uint32_t s = 0, n = 0, q = 0;
+    uint32_t us[4], un[4], q = 0;
 #pragma unroll
-    for (int v = 0; v < 2; v++) {
-#pragma unroll
-        for (int j = 0; j < 4; j++) {
-            const uint32_t x = v ? b[j] : a[j];
-            const uint32_t nl_inv = nonzero_bytes(x ^ 0x0A0A0A0Au) & nonzero_bytes(x ^ 0x0D0D0D0Du);
-            const uint32_t sp_inv = nl_inv & nonzero_bytes(x ^ rep_d);
-            // 0x80 flags -> nibbles: separators in bits 0-3, terminators in bits 4-7
-            const uint32_t c = ((~sp_inv & 0x80808080u) >> 7) | ((~nl_inv & 0x80808080u) >> 3);
-            uint32_t t = c | (c >> 7);
-            t = t | (t >> 14);
-            const int sh = (v * 4 + j) * 4;
-            s |= (t & 0xFu) << sh;
-            n |= ((t >> 4) & 0xFu) << sh;
-            q |= ~nonzero_bytes(x ^ rep_q) & 0x80808080u;
+    for (int j = 0; j < 8; j++) {
+        const uint32_t x = j < 4 ? a[j & 3] : b[j & 3];
+        const uint32_t rn = __builtin_amdgcn_perm(0x00004000u, 0x00400000u, x ^ 0x08080808u);
+        const uint32_t rd = __builtin_amdgcn_perm(0u, 0x00000040u, x ^ rep_d);
+        const uint32_t fs = flags40(rn & rd), fn = flags40(rn);
+        const uint32_t w = (j & 1) ? 0x80402010u : 0x08040201u;
+        if (j & 1) {
+            us[j >> 1] = __builtin_amdgcn_udot4(fs, w, us[j >> 1], false);
+            un[j >> 1] = __builtin_amdgcn_udot4(fn, w, un[j >> 1], false);
+        } else {
+            us[j >> 1] = __builtin_amdgcn_udot4(fs, w, 0u, false);
+            un[j >> 1] = __builtin_amdgcn_udot4(fn, w, 0u, false);
         }
+        const uint32_t t = x ^ rep_q;
+        q |= (t - 0x01010101u) & ~t;
     }
-    sep = s;
-    nl = n;
-    qf = q;
+    // us[p] = 0x40 * (bits of bytes 8p .. 8p + 7)
+    sep = (us[0] >> 6) | (us[1] << 2) | (us[2] << 10) | (us[3] << 18);
+    nl = (un[0] >> 6) | (un[1] << 2) | (un[2] << 10) | (un[3] << 18);
+    qf = q & 0x80808080u;
 }
 __device__ __forceinline__ uint32_t byte_bits(const v4u a, const v4u b, uint32_t rep) {
     uint32_t m = 0;
@@ -209,6 +231,13 @@ __device__ __forceinline__ uint64_t qview(const WaveLds& W, uint32_t p) {
     const uint32_t wi = p >> 5, sh = p & 31;
     const uint32_t q0 = W.qt[wi], q1 = W.qt[wi + 1], q2 = W.qt[wi + 2];
     return (uint64_t)__builtin_amdgcn_alignbit(q1, q0, sh) | ((uint64_t)__builtin_amdgcn_alignbit(q2, q1, sh) << 32);
+}
+
+// 4 bytes of the tile at byte offset o (any alignment)
+__device__ __forceinline__ void load4(const uint8_t* tile, uint32_t o, uint32_t& e0) {
+    const uint32_t* t32 = (const uint32_t*)tile;
+    const uint32_t a = o >> 2, sh = o & 3;
+    e0 = __builtin_amdgcn_alignbyte(t32[a + 1], t32[a], sh);
 }
 
 // bytes [0, len) of two dwords (len <= 8)
@@ -258,16 +287,43 @@ __device__ __forceinline__ Num num7(uint32_t d0, uint32_t d1, uint32_t len) {
     return r;
 }
 
+// num7 for fields of 1..4 bytes (one dword): the same M, k, dot and ok for every
+// field num7 accepts with len <= 4; ok is false for longer fields.  The kernel
+// takes it when every lane's field of the role fits (a wave-uniform choice).
+__device__ __forceinline__ Num num4(uint32_t d0, uint32_t len) {
+    Num r;
+    const uint32_t f = len_mask(len, 0) & 0x80808080u;
+    const uint32_t x = d0 ^ 0x30303030u;
+    const uint32_t g = lt_bytes(x, 0x0A0A0A0Au) & f;                   // digits
+    const uint32_t t = ~nonzero_bytes(d0 ^ 0x2E2E2E2Eu) & f;            // dots
+    const uint32_t ndot = (uint32_t)__popc(t);
+    r.ok = (len - 1 <= 3u) & ((g | t) == f) & (ndot <= 1) & (g != 0);
+    uint32_t v = x & spread(g);                                         // digit values, dot -> 0
+    uint32_t pd = (uint32_t)__builtin_ctz(t | 0x80000000u) >> 3;        // dot byte (3 when none or last)
+    r.dot = ndot != 0;
+    const uint32_t lo = (1u << (8 * pd)) - 1;
+    v = r.dot ? ((v & lo) | ((v >> 8) & ~lo)) : v;
+    r.k = r.dot ? len - 1 - pd : 0u;
+    r.k = r.k > 3 ? 3u : r.k;
+    uint32_t nd = len - ndot;                                           // digits
+    nd = nd - 1 > 3u ? 1u : nd;
+    v <<= 8 * (4 - nd);                                                 // right-align the digits
+    r.M = __builtin_amdgcn_udot4(v, 0x010A6400u, __umul24(v & 0xFFu, 1000u), false);
+    return r;
+}
+
 // Field `c` of the record at window offset p from its 64-bit separator view sv
 // (delimiters and terminators, bit i = byte p + i) and its end e (the first
 // terminator; 64: beyond the view).  Clearing the c lowest separator bits leaves
 // the field's end as the lowest bit; the cleared bits' highest is its start - 1.
 // A column past the record's end is missing (length 0: NULL); a field the view
-// cannot bound fails the fast path.  c is uniform: a scalar loop.
-__device__ __forceinline__ void field_of(uint64_t sv, uint32_t e, uint32_t c, uint32_t p, uint32_t& fp,
-                                         uint32_t& fl, bool& fail, uint32_t& last) {
-    uint64_t s = sv;
-    for (uint32_t i = 0; i < c; i++) s &= s - 1;
+// cannot bound fails the fast path.  The roles' columns come in ascending order,
+// so s and `done` carry the cleared bits from one role to the next (the clears
+// of a record total its largest column, not the sum of the columns).  c is
+// uniform: a scalar loop.
+__device__ __forceinline__ void field_next(uint64_t sv, uint64_t& s, uint32_t& done, uint32_t e, uint32_t c,
+                                           uint32_t p, uint32_t& fp, uint32_t& fl, bool& fail, uint32_t& last) {
+    for (; done < c; done++) s &= s - 1;
     const uint64_t cl = sv ^ s;
     const uint32_t start = cl ? 64u - (uint32_t)__builtin_clzll(cl) : 0u;
     const uint32_t end = ctz64(s);
@@ -313,6 +369,18 @@ __device__ __forceinline__ uint64_t bswap64(uint32_t d0, uint32_t d1) {
 // take lt_slow: lock-free linear probing over the slots from the home bucket.
 constexpr uint32_t BS = 16;
 constexpr uint32_t FP_BUSY = 0xFFFEu;   // fingerprints are odd
+
+// LDS bytes per table slot (fingerprint, key, count, SUM/miss per argument) and
+// the slots of a plan shape: a compile-time constant of each kernel instance, so
+// every table array sits at an immediate LDS offset
+constexpr uint32_t slot_bytes(int ns) { return 2 + 16 + 8 + 4 + (uint32_t)ns * 12; }
+constexpr uint32_t fixed_bytes() { return (uint32_t)(sizeof(WaveLds) * NWV); }
+constexpr uint32_t slots_for(int ns, bool grouped) {
+    if (!grouped) return 0;
+    uint32_t h = 2048;
+    while (h > 64 && fixed_bytes() + h * slot_bytes(ns) + 512 > 160u * 1024u) h >>= 1;
+    return h;
+}
 struct LTab {
     uint32_t H;           // slots (multiple of BS)
     uint32_t NB;          // buckets
@@ -413,18 +481,18 @@ __device__ __forceinline__ uint8_t* carve(uint8_t*& q, size_t bytes) {
 template <bool GROUPED, int WM, int NS>
 __global__ __launch_bounds__(LT) void lean_kernel(const uint8_t* __restrict__ g, ScanStats* __restrict__ stats,
                                                   unsigned long long* __restrict__ row_out,
-                                                  unsigned long long row_cap, uint32_t lds_h,
+                                                  unsigned long long row_cap, uint32_t lds_h_unused,
                                                   unsigned long long* __restrict__ slow_list,
-                                                  unsigned long long slow_cap, const LeanArgs args) {
+                                                  unsigned long long slow_cap, const LeanArgs args,
+                                                  const GroupTable* __restrict__ tabs) {
     const LeanPlan& LP = args.lp;
-    const GroupTable& gt = args.gt;
-    const GroupTable& rt = args.rt;
     extern __shared__ __align__(16) uint8_t smem[];
     uint8_t* q = smem;
     WaveLds* waves = (WaveLds*)carve(q, sizeof(WaveLds) * NWV);
     const int tid = threadIdx.x, lane = tid & 63;
     const int wv = __builtin_amdgcn_readfirstlane(tid >> 6);   // wave-uniform: the window loop is scalar
     WaveLds& W = waves[wv];
+    constexpr uint32_t lds_h = slots_for(NS, GROUPED);
     LTab lt;
     lt.H = lds_h;
     lt.NB = 0; lt.F = nullptr;
@@ -454,11 +522,13 @@ __global__ __launch_bounds__(LT) void lean_kernel(const uint8_t* __restrict__ g,
     }
 
     // uniform plan facts
-    const uint32_t wcol = WM != LW_NONE ? LP.wcol : 0u;
-    const uint32_t gcol = GROUPED ? LP.gcol : 0u;
-    uint32_t scol[MAXS];
+    constexpr int NR = (WM != LW_NONE ? 1 : 0) + NS + (GROUPED ? 1 : 0);   // roles
+    uint32_t rcol[KN], rrole[KN];
 #pragma unroll
-    for (int j = 0; j < MAXS; j++) scol[j] = j < NS ? LP.scol[j] : 0u;
+    for (int k = 0; k < KN; k++) {
+        rcol[k] = __builtin_amdgcn_readfirstlane(LP.rcol[k]);
+        rrole[k] = __builtin_amdgcn_readfirstlane(LP.rrole[k]);
+    }
     const uint32_t rep_d = LP.delim * 0x01010101u, rep_q = LP.quote * 0x01010101u;
     const uint64_t lo_ok = LP.lo_ok, hi_ok = LP.hi_ok, last_win = LP.last_win;
     // WHERE facts in scalar registers (no constant reloads inside the loop)
@@ -559,24 +629,51 @@ __global__ __launch_bounds__(LT) void lean_kernel(const uint8_t* __restrict__ g,
             uint32_t sfp[MAXS], sfl[MAXS];
 #pragma unroll
             for (int j = 0; j < MAXS; j++) { sfp[j] = p; sfl[j] = 0; }
-            if (WM != LW_NONE) field_of(sv, e, wcol, p, wfp, wfl, fail, lastpos);
+            {
+                uint64_t s = sv;
+                uint32_t done = 0;
 #pragma unroll
-            for (int j = 0; j < NS; j++) field_of(sv, e, scol[j], p, sfp[j], sfl[j], fail, lastpos);
-            if (GROUPED) field_of(sv, e, gcol, p, gfp, klen, fail, lastpos);
+                for (int k = 0; k < NR; k++) {
+                    uint32_t fp_, fl_;
+                    field_next(sv, s, done, e, rcol[k], p, fp_, fl_, fail, lastpos);
+                    const uint32_t role = rrole[k];
+                    if (WM != LW_NONE && role == R_WHERE) { wfp = fp_; wfl = fl_; }
+                    if (NS > 0 && role == R_SUM0) { sfp[0] = fp_; sfl[0] = fl_; }
+                    if (NS > 1 && role == R_SUM1) { sfp[MAXS - 1] = fp_; sfl[MAXS - 1] = fl_; }
+                    if (GROUPED && role == R_GROUP) { gfp = fp_; klen = fl_; }
+                }
+            }
             // a quote at or before the last byte examined may hide separators
             if (wq) fail |= (qview(W, p) & ((2ULL << (lastpos < 63 ? lastpos : 63)) - 1)) != 0;
 
+            // ---- wave-uniform field-size classes: every lane's numeric WHERE / SUM field
+            //      fits a dword (num4), every GROUP BY key fits 8 bytes (two-word keys)
+            const bool w4 = WM == LW_NUM && __all(!valid | (wfl <= 4u));
+            bool s4 = NS > 0;
+#pragma unroll
+            for (int j = 0; j < NS; j++) s4 = s4 && __all(!valid | (sfl[j] <= 4u));
+            const bool g8 = GROUPED && __all(!valid | (klen <= 8u));
+
             // ---- field bytes of the roles (one batch of LDS reads)
             uint32_t wd0 = 0, wd1 = 0;
-            if (WM != LW_NONE) load8(W.bytes, wfp, wd0, wd1);
+            if (WM != LW_NONE) {
+                if (w4) load4(W.bytes, wfp, wd0);
+                else load8(W.bytes, wfp, wd0, wd1);
+            }
             uint32_t sd0[MAXS], sd1[MAXS];
 #pragma unroll
             for (int j = 0; j < MAXS; j++) {
                 sd0[j] = sd1[j] = 0;
-                if (j < NS) load8(W.bytes, sfp[j], sd0[j], sd1[j]);
+                if (j < NS) {
+                    if (s4) load4(W.bytes, sfp[j], sd0[j]);
+                    else load8(W.bytes, sfp[j], sd0[j], sd1[j]);
+                }
             }
             uint32_t k0 = 0, k1 = 0, k2 = 0, k3 = 0;
-            if (GROUPED) load16(W.bytes, gfp, k0, k1, k2, k3);
+            if (GROUPED) {
+                if (g8) load8(W.bytes, gfp, k0, k1);
+                else load16(W.bytes, gfp, k0, k1, k2, k3);
+            }
 
             LCLK(2);
 #if defined(LEAN_PROF) && LEAN_PROF == 2   // profiling build: + record list, field walk, field loads
@@ -590,7 +687,7 @@ __global__ __launch_bounds__(LT) void lean_kernel(const uint8_t* __restrict__ g,
                 bool outcome = pass_null;                  // missing column / empty field: NULL
                 bool typed = wfl == 0;
                 if (WM == LW_NUM) {
-                    const Num n = num7(wd0, wd1, wfl);
+                    const Num n = w4 ? num4(wd0, wfl) : num7(wd0, wd1, wfl);
                     int c = (int)n.M < wlo ? -1 : ((int)n.M > whi ? 1 : 0);
                     if (__any(n.ok & n.dot)) {             // DOUBLE fields: strtod = RN(M / 10^k)
                         const double d = (double)n.M / p10(n.k);
@@ -634,8 +731,14 @@ __global__ __launch_bounds__(LT) void lean_kernel(const uint8_t* __restrict__ g,
                 sval[j] = 0.0;
                 snum[j] = false;
                 if (j >= NS) continue;
-                const Num n = num7(sd0[j], sd1[j], sfl[j]);
-                sval[j] = (double)n.M * inv10(n.k);
+                Num n;
+                if (s4) {
+                    n = num4(sd0[j], sfl[j]);
+                    sval[j] = (double)n.M * (((n.k & 1) ? 0.1 : 1.0) * ((n.k & 2) ? 0.01 : 1.0));   // = inv10(k), k <= 3
+                } else {
+                    n = num7(sd0[j], sd1[j], sfl[j]);
+                    sval[j] = (double)n.M * inv10(n.k);
+                }
                 snum[j] = n.ok;
                 const bool gen = !n.ok & (sfl[j] != 0) & !fail;
                 if (__any(gen)) {
@@ -650,12 +753,21 @@ __global__ __launch_bounds__(LT) void lean_kernel(const uint8_t* __restrict__ g,
             // ---- GROUP BY key: the raw field bytes (<= 16, no byte <= ' ')
             uint32_t h = 0;
             if (GROUPED) {
-                const uint32_t m0 = len_mask(klen, 0), m1 = len_mask(klen, 1), m2 = len_mask(klen, 2), m3 = len_mask(klen, 3);
-                k0 &= m0; k1 &= m1; k2 &= m2; k3 &= m3;
-                const uint32_t lowb = low_bytes(k0, m0 & 0x80808080u) | low_bytes(k1, m1 & 0x80808080u) |
-                                      low_bytes(k2, m2 & 0x80808080u) | low_bytes(k3, m3 & 0x80808080u);
-                fail |= (lowb != 0) | (klen > 16);
-                h = key_hash(klen, k0, k1, k2, k3);
+                if (g8) {
+                    const uint32_t m0 = len_mask(klen, 0), m1 = len_mask(klen, 1);
+                    k0 &= m0; k1 &= m1;
+                    const uint32_t lowb = low_bytes(k0, m0 & 0x80808080u) | low_bytes(k1, m1 & 0x80808080u);
+                    fail |= lowb != 0;
+                    h = key_hash(klen, k0, k1, 0u, 0u);
+                } else {
+                    const uint32_t m0 = len_mask(klen, 0), m1 = len_mask(klen, 1), m2 = len_mask(klen, 2),
+                                   m3 = len_mask(klen, 3);
+                    k0 &= m0; k1 &= m1; k2 &= m2; k3 &= m3;
+                    const uint32_t lowb = low_bytes(k0, m0 & 0x80808080u) | low_bytes(k1, m1 & 0x80808080u) |
+                                          low_bytes(k2, m2 & 0x80808080u) | low_bytes(k3, m3 & 0x80808080u);
+                    fail |= (lowb != 0) | (klen > 16);
+                    h = key_hash(klen, k0, k1, k2, k3);
+                }
             }
 
             LCLK(3);
@@ -703,9 +815,11 @@ __global__ __launch_bounds__(LT) void lean_kernel(const uint8_t* __restrict__ g,
                 const uint32_t j = fp_first(q0, q1, fp_of(h));
                 const uint32_t s0 = bk * BS + (j < BS ? j : BS - 1);
                 const v4u a = lt.A[s0];
-                const uint2 b = lt.B[s0];
-                const bool hit = (j < BS) & (a.x == (0x80000000u | klen)) & (a.z == k0) & (a.w == k1) & (b.x == k2) &
-                                 (b.y == k3);
+                bool hit = (j < BS) & (a.x == (0x80000000u | klen)) & (a.z == k0) & (a.w == k1);
+                if (!g8) {           // a stored key of the same length <= 8 has zero words 2-3
+                    const uint2 b = lt.B[s0];
+                    hit = hit & (b.x == k2) & (b.y == k3);
+                }
                 int slot = hit ? (int)s0 : -1;
                 uint32_t first = a.y;
                 const bool miss = pass_ & !hit;
@@ -731,6 +845,7 @@ __global__ __launch_bounds__(LT) void lean_kernel(const uint8_t* __restrict__ g,
                 if (__any(spill)) {                        // LDS table full: straight to the HBM raw table
                     n_spill += (unsigned long long)__popcll(__ballot(spill));
                     if (spill) {
+                        const GroupTable& rt = tabs[TAB_RT];
                         const GKey kk = raw_key(klen, (uint64_t)k0 | ((uint64_t)k1 << 32), (uint64_t)k2 | ((uint64_t)k3 << 32));
                         const int gi = g_insert(rt, kk, gk_hash(kk), stats);
                         if (gi >= 0) {
@@ -783,6 +898,7 @@ __global__ __launch_bounds__(LT) void lean_kernel(const uint8_t* __restrict__ g,
             }
         }
         if (lane == 0) {
+            const GroupTable& gt = tabs[TAB_GT];
             GKey k;
             k.cls = GK_ALL; k.len = 0; k.w0 = 0; k.w1 = 0;
             const int gi = g_insert(gt, k, 0x12345678ULL, stats);
@@ -806,6 +922,7 @@ __global__ __launch_bounds__(LT) void lean_kernel(const uint8_t* __restrict__ g,
     // ---- flush the block's raw keys into the HBM raw table (raw_merge_kernel
     //      types each distinct raw key once and merges it into the canonical table)
     __syncthreads();
+    const GroupTable& rt = tabs[TAB_RT];
     for (uint32_t i = tid; i < lds_h; i += LT) {
         const v4u a = lt.A[i];
         if (a.x < 2) continue;
@@ -931,21 +1048,16 @@ bool lean_shape(const ScanPlan* P, LeanPlan* lp, int* wm) {
 }
 
 int ns_of(const LeanPlan& lp) { return lp.ns; }
-size_t lean_slot_bytes(int ns) { return 2 + 16 + 8 + 4 + (size_t)ns * 12; }
-size_t lean_fixed_bytes() { return sizeof(lean::WaveLds) * lean::NWV; }
+size_t lean_slot_bytes(int ns) { return lean::slot_bytes(ns); }
+size_t lean_fixed_bytes() { return lean::fixed_bytes(); }
 
-uint32_t lean_slots(int ns, int grouped) {
-    if (!grouped) return 0;
-    uint32_t h = 2048;
-    while (h > 64 && lean_fixed_bytes() + (size_t)h * lean_slot_bytes(ns) + 512 > (size_t)(160 * 1024)) h >>= 1;
-    return h;
-}
+uint32_t lean_slots(int ns, int grouped) { return lean::slots_for(ns, grouped != 0); }
 size_t lean_lds(int ns, int grouped) {
     return lean_fixed_bytes() + (size_t)lean_slots(ns, grouped) * lean_slot_bytes(ns) + 512;
 }
 
 typedef void (*lean_fn_t)(const uint8_t*, ScanStats*, unsigned long long*, unsigned long long, uint32_t,
-                          unsigned long long*, unsigned long long, const lean::LeanArgs);
+                          unsigned long long*, unsigned long long, const lean::LeanArgs, const GroupTable*);
 
 template <bool G, int WM>
 lean_fn_t pick_ns(int ns) {
@@ -1015,17 +1127,44 @@ hipError_t cq_launch_lean(const uint8_t* g, const cq::ScanPlan* P, const cq::Gro
     lp.first_win = P->range_begin / lean::WS;
     lp.last_win = (hi + lean::WS - 1) / lean::WS;
     const int ns = ns_of(lp);
+    {   // the roles in ascending column order (lean_kernel's field walk)
+        uint32_t nr = 0;
+        auto add = [&](uint32_t col, uint32_t role) {
+            uint32_t i = nr++;
+            while (i > 0 && lp.rcol[i - 1] > col) {
+                lp.rcol[i] = lp.rcol[i - 1];
+                lp.rrole[i] = lp.rrole[i - 1];
+                i--;
+            }
+            lp.rcol[i] = col;
+            lp.rrole[i] = role;
+        };
+        if (wm != lean::LW_NONE) add(lp.wcol, lean::R_WHERE);
+        for (int j = 0; j < ns; j++) add(lp.scol[j], j == 0 ? lean::R_SUM0 : lean::R_SUM1);
+        if (grouped) add(lp.gcol, lean::R_GROUP);
+    }
     const uint32_t h = lean_slots(ns, grouped);
     const size_t lds = lean_lds(ns, grouped);
     lean::LeanArgs args;
     memset(&args, 0, sizeof args);
     args.lp = lp;
-    args.gt = *gt;
-    if (rt) args.rt = *rt;
+    static GroupTable* tabs_dev = nullptr;
+    if (!tabs_dev) {
+        hipError_t e = hipGetSymbolAddress((void**)&tabs_dev, HIP_SYMBOL(lean::g_lean_tabs));
+        if (e != hipSuccess) return e;
+    }
+    static GroupTable tabs[2];
+    tabs[0] = *gt;
+    if (rt) tabs[1] = *rt;
+    else memset(&tabs[1], 0, sizeof tabs[1]);
+    {
+        hipError_t e = hipMemcpyAsync(tabs_dev, tabs, sizeof tabs, hipMemcpyHostToDevice, s);
+        if (e != hipSuccess) return e;
+    }
     const lean_fn_t fn = grouped ? pick_fn<true>(wm, ns) : pick_fn<false>(wm, ns);
     (void)hipFuncSetAttribute((const void*)fn, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds);
     hipLaunchKernelGGL(fn, dim3(grid), dim3(lean::LT), lds, s, g, stats, row_out, row_cap, h, slow_list, slow_cap,
-                       args);
+                       args, (const GroupTable*)tabs_dev);
     return hipGetLastError();
 }
 
