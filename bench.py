@@ -36,6 +36,9 @@ sys.path.insert(0, ROOT)
 METRIC = "rows/sec scanned (filter+GROUP BY) at 1/2/4/8 GPUs; % of HBM read peak"
 QUERY = ("SELECT role, COUNT(*), SUM(height), AVG(height) FROM '{path}' "
          "WHERE age > 30 GROUP BY role")
+# --config 2 (not the bench line; a measurement of BASELINE configs[1]):
+# Shape A without role, filter + COUNT
+QUERY2 = "SELECT COUNT(*) FROM '{path}' WHERE age > 30"
 HBM_PEAK_GBS = 8000.0   # MI355X HBM3E spec (MI355X_MICROARCH.md, chip-level parameters)
 
 
@@ -50,19 +53,24 @@ def parse_args():
                     help="rows of the CPU-baseline sample (reference evaluator)")
     ap.add_argument("--no-cpu", action="store_true")
     ap.add_argument("--traffic", default=os.path.join(ROOT, "profiles", "hbm_traffic.json"))
+    ap.add_argument("--config", type=int, default=3, choices=(2, 3),
+                    help="3: the bench line (filter + GROUP BY); 2: Shape A filter + COUNT")
     return ap.parse_args()
 
 
-def build_plan(path):
+def build_plan(path, config=3):
     from cq_amd import abi
     P = abi.Plan()
+    if config == 2:
+        q = P.query([P.func("COUNT", P.lit("*"))], path, where=P.cond(">", P.ident("age"), P.lit("30")))
+        return P, q
     q = P.query([P.ident("role"), P.func("COUNT", P.lit("*")), P.func("SUM", P.ident("height")),
                  P.func("AVG", P.ident("height"))], path,
                 where=P.cond(">", P.ident("age"), P.lit("30")), group_by=["role"])
     return P, q
 
 
-def cpu_baseline(rows, seed):
+def cpu_baseline(rows, seed, config=3):
     """Reference evaluator (single-threaded C, -O2) on a bounded sample, 1 core."""
     from cq_amd import datagen
     probe = os.path.join(ROOT, "oracle", "_ref", "ref_probe")
@@ -71,11 +79,11 @@ def cpu_baseline(rows, seed):
         return None
     with tempfile.TemporaryDirectory() as d:
         path = os.path.join(d, "sample.csv")
-        datagen.write_shape_a(path, rows, seed=seed, with_role=True)
-        out = subprocess.run(["taskset", "-c", "0", probe, "time", QUERY.format(path=path)],
-                             capture_output=True, timeout=600)
+        datagen.write_shape_a(path, rows, seed=seed, with_role=config == 3)
+        query = (QUERY if config == 3 else QUERY2).format(path=path)
+        out = subprocess.run(["taskset", "-c", "0", probe, "time", query], capture_output=True, timeout=600)
         if out.returncode != 0:
-            out = subprocess.run([probe, "time", QUERY.format(path=path)], capture_output=True, timeout=600)
+            out = subprocess.run([probe, "time", query], capture_output=True, timeout=600)
         res = json.loads(out.stdout.decode())
     secs = res["seconds"]
     return {"value": rows / secs, "unit": "rows/s", "cores": 1, "kind": kind,
@@ -105,14 +113,15 @@ def main():
 
     # ---- synthetic shard of this rank (one N x rows file, row-range partitioned)
     t0 = time.time()
-    header = b"name,surname,age,gender,height,role\n"
+    role = args.config == 3
+    header = b"name,surname,age,gender,height,role\n" if role else b"name,surname,age,gender,height\n"
     import numpy as np
     rng = np.random.default_rng([args.seed, rank])
     chunks = []
     left = args.rows
     while left > 0:
         n = min(1 << 22, left)
-        chunks.append(datagen.shape_a_chunk(rng, n, True))
+        chunks.append(datagen.shape_a_chunk(rng, n, role))
         left -= n
     body = b"".join(chunks)
     del chunks
@@ -129,7 +138,7 @@ def main():
     del body, shard
     gen_s = time.time() - t0
 
-    P, q = build_plan("big.csv")
+    P, q = build_plan("big.csv", args.config)
     ast = C.pointer(q)
     L = cq_amd.lib()
 
@@ -167,8 +176,9 @@ def main():
     ng = None
     for _ in range(args.warmup):
         ng, _ = step()
-    if rank == 0 and ng is not None and ng != 1000:
-        print(f"warning: {ng} groups (expected 1000)", file=sys.stderr)
+    want_groups = 1000 if role else 1
+    if rank == 0 and ng is not None and ng != want_groups:
+        print(f"warning: {ng} groups (expected {want_groups})", file=sys.stderr)
 
     def barrier():
         if dist is not None:
@@ -205,7 +215,7 @@ def main():
         cpu = None
         if world == 1 and not args.no_cpu:
             try:
-                cpu = cpu_baseline(args.cpu_rows, args.seed)
+                cpu = cpu_baseline(args.cpu_rows, args.seed, args.config)
             except Exception as e:  # reported, never fatal
                 print(f"cpu baseline failed: {e}", file=sys.stderr)
         line = {
@@ -220,14 +230,16 @@ def main():
             "scaling": "weak",
             "vs_baseline": None,
             "dtype": "u8",
-            "data": "synthetic: Shape A+role CSV (generate_big_dataset.py columns + role_%03d, "
-                    f"seed {args.seed}), resident in HBM before timing",
+            "data": ("synthetic: Shape A+role CSV (generate_big_dataset.py columns + role_%03d, "
+                     if role else "synthetic: Shape A CSV (generate_big_dataset.py columns, ")
+                    + f"seed {args.seed}), resident in HBM before timing",
             "config": {
-                "workload": "config3 per GPU: SELECT role, COUNT(*), SUM(height), AVG(height) "
-                            "FROM 'big.csv' WHERE age > 30 GROUP BY role",
+                "workload": ("config3 per GPU: SELECT role, COUNT(*), SUM(height), AVG(height) "
+                             "FROM 'big.csv' WHERE age > 30 GROUP BY role" if role else
+                             "config2 per GPU: SELECT COUNT(*) FROM 'big.csv' WHERE age > 30"),
                 "rows_per_gpu": args.rows,
                 "bytes_per_gpu": nbytes,
-                "groups": 1000,
+                "groups": want_groups,
                 "parallelism": f"dp{world} (newline-snapped row ranges, RCCL all_gather of partials)",
             },
             "roofline": {
@@ -237,8 +249,9 @@ def main():
                 "unit": "GB/s",
                 "frac": achieved / HBM_PEAK_GBS,
                 "traffic": traffic,
-                "kernel": ("cq::lean::lean_kernel<true, LW_NUM, 1> (+ slow_kernel, raw_merge_kernel)"
-                           if kernel_used[0] else "cq::scan_kernel<true>"),
+                "kernel": (("cq::lean::lean_kernel<true, LW_NUM, 1> (+ slow_kernel, raw_merge_kernel)" if role
+                            else "cq::lean::lean_kernel<false, LW_NUM, 0> (+ slow_kernel)")
+                           if kernel_used[0] else "cq::scan_kernel"),
                 "kernel_ms": avg_scan_ms,
                 "bytes_per_launch": nbytes,
             },

@@ -33,6 +33,7 @@
 using namespace cq;
 
 extern "C" {
+uint32_t cq_lean_pick_ws(const uint8_t* data, uint64_t n);
 uint32_t cq_scan_cand_stride(const ScanPlan* P, int grouped);
 size_t cq_scan_lds_bytes(const ScanPlan* P, int grouped);
 int cq_scan_occupancy(const ScanPlan* P, int grouped);
@@ -280,6 +281,7 @@ struct cqgpu_table {
     std::vector<std::string> names;
     uint64_t data_begin = 0;
     int device = 0;
+    uint32_t lean_ws = 0;            // lean_kernel window stride for this file's record lengths
 };
 
 namespace {
@@ -356,6 +358,7 @@ cqgpu_table* upload(const uint8_t* host, size_t n, cq_csv_config cfg, uint64_t b
         if (p > ls) t->names = split_header(ls, p, cfg.delimiter, cfg.quote, cfg.has_header);
         t->data_begin = cfg.has_header ? (uint64_t)(p - d) : 0;
     }
+    t->lean_ws = cq_lean_pick_ws(host + t->data_begin, n - std::min<uint64_t>(n, t->data_begin));
     size_t total = PAD_BEFORE + n + PAD_AFTER;
     HIPCHECK(hipMalloc(&t->dbuf, total));
     HIPCHECK(hipMemsetAsync(t->dbuf, '\n', PAD_BEFORE, c.stream));
@@ -745,6 +748,7 @@ void finish_plan(const cqgpu_table* t, Compiled& C, Compiler& cc) {
     C.P.data_begin = t->data_begin;
     C.P.range_begin = 0;
     C.P.range_end = t->n;
+    C.P.lean_ws = t->lean_ws;
 }
 
 // compile the aggregate SELECT (evaluator.c:69-258 + build_aggregated_result)

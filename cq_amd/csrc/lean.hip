@@ -60,7 +60,7 @@ constexpr int NWV = LT / 64;              // waves per block
 constexpr int LB = 32;                    // staged bytes per lane
 constexpr int WB = 64 * LB;               // staged window bytes (2 KiB)
 constexpr int HEAD = 16;                  // staged bytes before the owned range
-constexpr int WS = 1952;                  // window stride = owned bytes
+constexpr int WS = 1952;                  // largest window stride = owned bytes (LeanPlan.ws: the file's)
 constexpr int NMW = WB / 32;              // 32-bit bitmap words per window
 constexpr int WBYTES = WB + 32;           // staged bytes + slack for 16-byte field loads
 constexpr int RSN = 64;                   // record slots per pass
@@ -115,6 +115,7 @@ struct LeanPlan {
     int32_t acc_sidx[MAX_ACC];   // accumulator -> SUM index
     uint32_t gcol;               // GROUP BY CSV column
     uint32_t delim, quote;
+    uint32_t ws;                 // window stride: multiple of 16, <= WS
     uint32_t rcol[KN];           // the roles' CSV columns, ascending
     uint32_t rrole[KN];          // their roles: R_WHERE, R_SUM0, R_SUM1, R_GROUP
 };
@@ -142,8 +143,8 @@ struct Win {            // one window in flight
     v4u a, b;           // staged bytes [32l, 32l + 32)
 };
 
-__device__ __forceinline__ void load_win(const uint8_t* g, uint64_t w, Win& x) {
-    const v4u* src = (const v4u*)(g + w * WS - HEAD);   // g has 64 padding bytes before byte 0
+__device__ __forceinline__ void load_win(const uint8_t* g, uint64_t w, uint32_t ws, Win& x) {
+    const v4u* src = (const v4u*)(g + w * ws - HEAD);   // g has 64 padding bytes before byte 0
     const int lane = threadIdx.x & 63;
     x.a = __builtin_nontemporal_load(src + 2 * lane);
     x.b = __builtin_nontemporal_load(src + 2 * lane + 1);
@@ -402,19 +403,23 @@ __device__ __forceinline__ uint32_t key_hash(uint32_t len, uint32_t k0, uint32_t
 __device__ __forceinline__ uint32_t fp_of(uint32_t h) { return (h & 0xFFFFu) | 1u; }
 __device__ __forceinline__ uint32_t bucket_of(uint32_t h, uint32_t nb) { return __umulhi(h, nb); }
 
-// index of the first of the 16 u16 fingerprints equal to fp (16: none); the lowest
-// flag of the SWAR zero-half test is exact
+// index of the first of the 16 u16 fingerprints equal to fp (16: none).  Per
+// dword the borrow-based zero-half test (its lowest flag is exact) leaves flags at
+// bits 15 and 31; one v_dot4_u32_u8 per dword weighs them 4^j * {1, 2} into a
+// chained 8-bit mask (times 0x80) per four dwords.
 __device__ __forceinline__ uint32_t fp_first(const v4u q0, const v4u q1, uint32_t fp) {
     const uint32_t rep = fp * 0x00010001u;
-    uint32_t m = 0;
+    uint32_t m0 = 0, m1 = 0;
 #pragma unroll
-    for (int j = 0; j < 8; j++) {
-        const uint32_t x = (j < 4 ? q0[j & 3] : q1[j & 3]) ^ rep;
-        const uint32_t f = (x - 0x00010001u) & ~x & 0x80008000u;
-        m |= ((f >> 15) & 1u) << (2 * j);
-        m |= (f >> 31) << (2 * j + 1);
+    for (int j = 0; j < 4; j++) {
+        const uint32_t x0 = q0[j] ^ rep, x1 = q1[j] ^ rep;
+        const uint32_t f0 = (x0 - 0x00010001u) & ~x0 & 0x80008000u;
+        const uint32_t f1 = (x1 - 0x00010001u) & ~x1 & 0x80008000u;
+        const uint32_t w = (1u << (2 * j + 8)) | (2u << (2 * j + 24));     // bytes 1 and 3
+        m0 = __builtin_amdgcn_udot4(f0, w, m0, false);
+        m1 = __builtin_amdgcn_udot4(f1, w, m1, false);
     }
-    return (uint32_t)__builtin_ctz(m | 0x10000u);
+    return (uint32_t)__builtin_ctz((m0 >> 7) | (m1 << 1) | 0x10000u);
 }
 
 // Find the key or insert it: linear probing over slots from the home bucket.  A
@@ -531,6 +536,7 @@ __global__ __launch_bounds__(LT) void lean_kernel(const uint8_t* __restrict__ g,
     }
     const uint32_t rep_d = LP.delim * 0x01010101u, rep_q = LP.quote * 0x01010101u;
     const uint64_t lo_ok = LP.lo_ok, hi_ok = LP.hi_ok, last_win = LP.last_win;
+    const uint32_t wstr_b = __builtin_amdgcn_readfirstlane(LP.ws);   // window stride
     // WHERE facts in scalar registers (no constant reloads inside the loop)
     const bool pass_null = __builtin_amdgcn_readfirstlane(LP.pass_null) != 0;
     const int wlo = __builtin_amdgcn_readfirstlane(LP.wlo), whi = __builtin_amdgcn_readfirstlane(LP.whi);
@@ -553,16 +559,16 @@ __global__ __launch_bounds__(LT) void lean_kernel(const uint8_t* __restrict__ g,
 #endif
     Win nx;
     uint64_t w = LP.first_win + (uint64_t)blockIdx.x * NWV + wv;
-    if (w < last_win) load_win(g, w, nx);
+    if (w < last_win) load_win(g, w, wstr_b, nx);
     for (uint32_t round = 0; w < last_win; round++, w += wstep) {
-        const uint64_t ws = w * WS;
+        const uint64_t ws = w * wstr_b;
 #ifdef LEAN_CLK
         asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
 #endif
         const Win cur = nx;
         LCLK(0);
 #ifndef LEAN_NOMEM   // profiling build LEAN_NOMEM: every window re-processes the first one (no HBM reads)
-        if (w + wstep < last_win) load_win(g, w + wstep, nx);
+        if (w + wstep < last_win) load_win(g, w + wstep, wstr_b, nx);
 #endif
 
         // ---- stage and classify
@@ -583,8 +589,8 @@ __global__ __launch_bounds__(LT) void lean_kernel(const uint8_t* __restrict__ g,
         uint32_t starts = ~nl & ((nl << 1) | prevnl);
         {
             const uint64_t lo64 = (lo_ok > ws ? lo_ok : ws) - ws;
-            const uint64_t hi64 = hi_ok < ws + WS ? hi_ok : ws + WS;
-            const uint32_t lo_s = HEAD + (uint32_t)(lo64 < (uint64_t)WS ? lo64 : (uint64_t)WS);   // staged offsets
+            const uint64_t hi64 = hi_ok < ws + wstr_b ? hi_ok : ws + wstr_b;
+            const uint32_t lo_s = HEAD + (uint32_t)(lo64 < (uint64_t)wstr_b ? lo64 : (uint64_t)wstr_b);   // staged offsets
             const uint32_t hi_s = hi64 > ws ? HEAD + (uint32_t)(hi64 - ws) : (uint32_t)HEAD;
             const uint32_t b0 = (uint32_t)lane * LB;
             if (b0 + LB <= lo_s || b0 >= hi_s) {
@@ -934,7 +940,7 @@ __global__ __launch_bounds__(LT) void lean_kernel(const uint8_t* __restrict__ g,
         if (n) atomicAdd(&rt.cnt[gi], (unsigned long long)n);
         if (a.y != NOFIRST) {
             const uint64_t fw = LP.first_win + ((uint64_t)(a.y >> 15) * gridDim.x + blockIdx.x) * NWV + ((a.y >> 11) & 15);
-            atomicMin(&rt.first[gi], (unsigned long long)(fw * WS - HEAD + (a.y & 2047)));
+            atomicMin(&rt.first[gi], (unsigned long long)(fw * LP.ws - HEAD + (a.y & 2047)));
         }
         for (int acc = 0; acc < LP.nacc; acc++) {
             const int j = LP.acc_sidx[acc];
@@ -1086,8 +1092,31 @@ int cq_lean_eligible(const cq::ScanPlan* P) {
 }
 
 // windows covering the records that start in [begin, end)
-uint64_t cq_lean_windows(uint64_t begin, uint64_t end) {
-    return (end + lean::WS - 1) / lean::WS - begin / lean::WS;
+uint64_t cq_lean_windows(uint64_t begin, uint64_t end, uint32_t ws) {
+    if (!ws) ws = lean::WS;
+    return (end + ws - 1) / ws - begin / ws;
+}
+
+// The window stride for a file: a window's records are handled one per lane, so
+// a stride holding ~58 records of the file's average length fills a wave in one
+// pass instead of spilling a few records into a second, nearly empty pass (and
+// never more than the staged bytes allow).  The average comes from up to 256 KiB
+// of the data bytes (records split on '\n' / '\r' runs, as csv_load does).
+uint32_t cq_lean_pick_ws(const uint8_t* data, uint64_t n) {
+    const uint64_t m = n < (256u << 10) ? n : (256u << 10);
+    uint64_t recs = 0;
+    bool in_rec = false;
+    for (uint64_t i = 0; i < m; i++) {
+        const bool term = data[i] == '\n' || data[i] == '\r';
+        if (!term && !in_rec) recs++;
+        in_rec = !term;
+    }
+    if (recs < 16) return lean::WS;
+    const double avg = (double)m / (double)recs;
+    uint64_t ws = (uint64_t)(58.0 * avg) & ~(uint64_t)15;
+    if (ws > (uint64_t)lean::WS) ws = lean::WS;
+    if (ws < 256) ws = 256;
+    return (uint32_t)ws;
 }
 int cq_lean_waves_per_block() { return lean::NWV; }
 
@@ -1124,8 +1153,10 @@ hipError_t cq_launch_lean(const uint8_t* g, const cq::ScanPlan* P, const cq::Gro
     const uint64_t hi = P->range_end < P->n ? P->range_end : P->n;
     lp.lo_ok = P->data_begin > P->range_begin ? P->data_begin : P->range_begin;
     lp.hi_ok = hi;
-    lp.first_win = P->range_begin / lean::WS;
-    lp.last_win = (hi + lean::WS - 1) / lean::WS;
+    lp.ws = P->lean_ws ? P->lean_ws : (uint32_t)lean::WS;
+    if (lp.ws > (uint32_t)lean::WS || lp.ws % 16) return hipErrorInvalidValue;
+    lp.first_win = P->range_begin / lp.ws;
+    lp.last_win = (hi + lp.ws - 1) / lp.ws;
     const int ns = ns_of(lp);
     {   // the roles in ascending column order (lean_kernel's field walk)
         uint32_t nr = 0;

@@ -62,6 +62,7 @@ struct ScanPlan {
     int32_t nacc;
     AccSpec acc[MAX_ACC];
     int32_t want_rows;     // 1: also emit matching record offsets (row-returning)
+    uint32_t lean_ws;      // lean_kernel window stride (0: the largest, lean::WS)
 };
 
 // projection of a row-returning SELECT (device pointers): ncols CSV columns

@@ -1771,7 +1771,7 @@ static scan_fn_t scan_fn(const cq::ScanPlan* P, int grouped) {
 extern "C" {
 // the fast scan, then the general kernel over the records it declined
 int cq_lean_eligible(const cq::ScanPlan* P);
-uint64_t cq_lean_windows(uint64_t begin, uint64_t end);
+uint64_t cq_lean_windows(uint64_t begin, uint64_t end, uint32_t ws);
 int cq_lean_waves_per_block();
 hipError_t cq_launch_lean(const uint8_t* g, const cq::ScanPlan* P, const cq::GroupTable* gt,
                           const cq::GroupTable* rt, cq::ScanStats* stats, unsigned long long* row_out,
@@ -1826,7 +1826,7 @@ hipError_t cq_launch_scan(const uint8_t* g, const cq::ScanPlan* P, const cq::Gro
         if (e0 != hipSuccess) return e0;
         // one 16-wave block per CU, each wave streaming its own windows
         const uint64_t hi = P->range_end < P->n ? P->range_end : P->n;
-        const uint64_t wins = cq_lean_windows(P->range_begin, hi) + 1;
+        const uint64_t wins = cq_lean_windows(P->range_begin, hi, P->lean_ws) + 1;
         const uint64_t per = (uint64_t)cq_lean_waves_per_block();
         uint64_t lg = (wins + per - 1) / per;
         if (lg > (uint64_t)device_cus()) lg = (uint64_t)device_cus();
