@@ -49,7 +49,10 @@ def main():
                    "write_bytes": write, "source": a.prefix + "_pmc.json",
                    "correction": "FETCH_SIZE(KiB)*1024*2 + WRITE_SIZE(KiB)*1024 (MI355X_MICROARCH.md HBM)"}
         json.dump(traffic, open(os.path.join(os.path.dirname(a.prefix), "hbm_traffic.json"), "w"), indent=1)
-    for f in ("bench.json", "pytest_gpu.log"):
+    stats2 = glob.glob(os.path.join(a.src, "kt2", "**", "*kernel_stats.csv"), recursive=True)
+    if stats2:
+        shutil.copy(stats2[0], a.prefix + "_config2_kernel_stats.csv")
+    for f in ("bench.json", "bench2.json", "pytest_gpu.log"):
         p = os.path.join(a.src, f)
         if os.path.exists(p):
             shutil.copy(p, a.prefix + "_" + f)
