@@ -53,6 +53,14 @@ def lib():
         L.cqgpu_merge_partials.restype = TP
         L.cqgpu_merge_partials.argtypes = [C.POINTER(abi.Node), C.POINTER(C.c_void_p),
                                            C.POINTER(C.c_size_t), C.c_int]
+        L.cqgpu_route_plan.restype = C.c_int
+        L.cqgpu_route_plan.argtypes = [C.POINTER(abi.Node), C.POINTER(C.c_void_p), C.c_int, C.c_int, C.c_int,
+                                       C.POINTER(C.c_uint64), C.POINTER(C.c_uint64)]
+        L.cqgpu_route_fill.restype = C.c_int
+        L.cqgpu_route_fill.argtypes = [C.c_void_p, C.c_uint64, C.c_void_p, C.c_void_p]
+        L.cqgpu_table_from_routed.restype = C.c_void_p
+        L.cqgpu_table_from_routed.argtypes = [C.c_void_p, C.c_size_t, C.c_void_p, C.c_size_t, abi.CsvConfig,
+                                              C.c_char_p, C.c_size_t]
         L.cqgpu_last_stats.argtypes = [C.POINTER(Stats)]
         L.cqgpu_last_error.restype = C.c_char_p
         L.cqgpu_last_ineligible.restype = C.c_char_p
@@ -150,6 +158,30 @@ def query_partial(ast, tables) -> bytes:
         return C.string_at(blob, size)
     finally:
         C.CDLL(None).free(blob)
+
+
+def route_plan(ast, tables, side: int, nranks: int) -> tuple[list[int], list[int]]:
+    """Join-key routing of tables[side] (tables = [FROM shard, JOIN shard]):
+    per destination rank the send-buffer byte count and record count."""
+    arr, n = _tables_arg(tables)
+    nb = (C.c_uint64 * nranks)()
+    nr = (C.c_uint64 * nranks)()
+    if lib().cqgpu_route_plan(ast, arr, n, side, nranks, nb, nr) != 0:
+        raise RuntimeError(last_error() or "cqgpu_route_plan failed")
+    return list(nb), list(nr)
+
+
+def route_fill(table: "Table", gid_base: int, dev_bytes_ptr: int, dev_gids_ptr: int) -> None:
+    """Write the planned send buffer (device pointers, e.g. torch tensors' data_ptr())."""
+    if lib().cqgpu_route_fill(table.handle, gid_base, dev_bytes_ptr, dev_gids_ptr) != 0:
+        raise RuntimeError(last_error() or "cqgpu_route_fill failed")
+
+
+def table_from_routed(dev_bytes_ptr: int, nbytes: int, dev_gids_ptr: int, nrec: int, header: bytes,
+                      cfg: abi.CsvConfig | None = None) -> "Table":
+    """A join side rebuilt from received records (device memory) and their global ids."""
+    return Table(lib().cqgpu_table_from_routed(dev_bytes_ptr, nbytes, dev_gids_ptr, nrec,
+                                               cfg or abi.csv_config(), header, len(header)))
 
 
 def merge_partials(ast, blobs):

@@ -17,6 +17,7 @@
 #include <cstring>
 #include <string>
 #include <map>
+#include <memory>
 #include <tuple>
 #include <unordered_map>
 #include <vector>
@@ -112,6 +113,19 @@ int cq_set_scan_mode(int mode);
 int cq_scan_uses_lean(const cq::ScanPlan* P, int with_cells);
 hipError_t cq_sort_offsets(void* temp, size_t* temp_bytes, const unsigned long long* in,
                            unsigned long long* out, size_t n, int bits, hipStream_t s);
+hipError_t cq_launch_route_len(const uint8_t* g, const unsigned long long* recs, uint32_t n,
+                               const unsigned long long* codes, const uint32_t* cls, uint32_t nranks, uint32_t* len,
+                               uint32_t* dest, unsigned long long* per_rank, hipStream_t s);
+hipError_t cq_sort_dest(void* temp, size_t* temp_bytes, const unsigned int* kin, unsigned int* kout,
+                        const unsigned int* vin, unsigned int* vout, size_t n, int bits, hipStream_t s);
+hipError_t cq_launch_gather_len(const uint32_t* len, const uint32_t* order, uint32_t n, unsigned long long* out,
+                                hipStream_t s);
+hipError_t cq_launch_route_copy(const uint8_t* g, const unsigned long long* recs, const uint32_t* order,
+                                const uint32_t* len, const unsigned long long* off, uint32_t n, uint64_t gid_base,
+                                uint8_t* out, unsigned long long* gids, hipStream_t s);
+hipError_t cq_launch_pair_gid(const uint2* pairs, const unsigned long long* pidx, uint32_t n,
+                              const unsigned long long* lg, const unsigned long long* rg, unsigned long long* out,
+                              hipStream_t s);
 }
 
 // reference evaluator.c:23
@@ -272,6 +286,13 @@ std::string rtrim(std::string s) {
 }  // namespace
 
 // ------------------------------------------------------------------ resident table
+// join-key repartition state of a shard between cqgpu_route_plan and cqgpu_route_fill
+struct RouteState {
+    DevBuf recs, order, len, off;
+    uint32_t n = 0;
+    uint64_t bytes = 0;
+};
+
 struct cqgpu_table {
     uint8_t* dbuf = nullptr;
     const uint8_t* g = nullptr;      // device byte 0
@@ -282,6 +303,9 @@ struct cqgpu_table {
     uint64_t data_begin = 0;
     int device = 0;
     uint32_t lean_ws = 0;            // lean_kernel window stride for this file's record lengths
+    unsigned long long* gids = nullptr;   // routed tables: global record id of each record (device)
+    uint64_t ngids = 0;
+    std::unique_ptr<RouteState> route;    // pending repartition (cqgpu_route_plan)
 };
 
 namespace {
@@ -1912,7 +1936,31 @@ JoinMap join_map(const std::vector<int>& jcols, int nl, const JoinSide& A, const
     return M;
 }
 
-cq_table* run_join(DevCtx& c, cq_node* q, const cqgpu_table* L, const cqgpu_table* R) {
+// per-rank state of a repartitioned join (cqgpu_query_partial over routed tables)
+struct JoinPartial {
+    std::vector<std::string> names;   // joined schema (alias.col)
+    std::vector<HGroup> groups;       // first / extpos: (global left id << 32) | global right id
+    uint32_t acc_classes[MAX_ACC] = {};
+    uint32_t lmask = 0, rmask = 0;    // bit k: a key of value class k (1 number, 2 string, 3 date)
+};
+
+// global record ids of a join side: the routed ids, or the local row index
+void side_gids(DevCtx& c, const cqgpu_table* t, uint32_t n, DevBuf& own, const unsigned long long** out) {
+    if (t->gids) {
+        if (t->ngids != n) throw HipError{"routed table: record count differs from its ids"};
+        *out = t->gids;
+        return;
+    }
+    std::vector<unsigned long long> h(std::max<uint32_t>(n, 1));
+    for (uint32_t i = 0; i < n; i++) h[i] = i;
+    DevBuf b(h.size() * 8);
+    std::swap(own.p, b.p);
+    HIPCHECK(hipMemcpyAsync(own.p, h.data(), h.size() * 8, hipMemcpyHostToDevice, c.stream));
+    HIPCHECK(hipStreamSynchronize(c.stream));
+    *out = own.as<unsigned long long>();
+}
+
+cq_table* run_join(DevCtx& c, cq_node* q, const cqgpu_table* L, const cqgpu_table* R, JoinPartial* part = nullptr) {
     cq_node* jn = q->u.q.joins[0];
     if (q->u.q.join_count != 1 || !jn || jn->kind != CQ_N_JOIN) throw Ineligible{"more than one JOIN"};
     const int kind = jn->u.join.kind;
@@ -1932,12 +1980,17 @@ cq_table* run_join(DevCtx& c, cq_node* q, const cqgpu_table* L, const cqgpu_tabl
         kr = join_on_index(on->u.bin.rhs->u.text, R, L, la, R, ra);
     }
     const bool keyed = kl >= 0 && kr >= 0;
+    if (part) {
+        if (kind != CQ_JOIN_INNER) throw Ineligible{"outer JOIN across partials"};
+        if (!keyed) throw Ineligible{"JOIN without an `ident = ident` ON across partials"};
+    }
     // the joined table's schema: alias.col names (evaluator_joins.c:30-37)
     cqgpu_table J;
     J.cfg = L->cfg;
     for (auto& nm : L->names) J.names.push_back(std::string(la) + "." + nm);
     for (auto& nm : R->names) J.names.push_back(std::string(ra) + "." + nm);
     const bool rows = is_row_query(q);
+    if (part && rows) throw Ineligible{"row-returning SELECT across partials"};
     Compiled C;
     RowPlan RP;
     if (rows) compile_rows(&J, q, C, RP);
@@ -1980,6 +2033,20 @@ cq_table* run_join(DevCtx& c, cq_node* q, const cqgpu_table* L, const cqgpu_tabl
         memset(&JR, 0, sizeof JR);
         JR.seg[0] = 0;
         for (int k = 0; k < 4; k++) JR.seg[k + 1] = JR.seg[k] + per[k];
+        if (part) {
+            // key value classes present on each side (cross-class pairs are not routable)
+            DevBuf lc((size_t)A.n * 8), lk2((size_t)A.n * 4), lpc(64);
+            HIPCHECK(hipMemsetAsync(lpc.p, 0, 64, c.stream));
+            HIPCHECK(cq_launch_join_code(A.cells.as<Cell>(), ls, lk, A.n, lc.as<unsigned long long>(),
+                                         lk2.as<uint32_t>(), nullptr, lpc.as<unsigned int>(), c.stream));
+            unsigned int lper[4] = {0, 0, 0, 0};
+            HIPCHECK(hipMemcpyAsync(lper, lpc.p, 16, hipMemcpyDeviceToHost, c.stream));
+            HIPCHECK(hipStreamSynchronize(c.stream));
+            for (int k = 1; k < 4; k++) {
+                if (lper[k]) part->lmask |= 1u << k;
+                if (per[k]) part->rmask |= 1u << k;
+            }
+        }
         int segs[8];
         for (int k = 0; k < 4; k++) { segs[k] = (int)JR.seg[k]; segs[4 + k] = (int)JR.seg[k + 1]; }
         int* dsegs = (int*)((uint8_t*)pc.p + 32);
@@ -2179,6 +2246,43 @@ cq_table* run_join(DevCtx& c, cq_node* q, const cqgpu_table* L, const cqgpu_tabl
         std::vector<int> rep_ord(C.rep_cols.size());
         for (size_t i = 0; i < rep_ord.size(); i++) rep_ord[i] = (int)i;
         groups = make_groups(c, C, std::max<unsigned long long>(np, 1), 0, outs, fcells, fbytes, MR.n, rep_ord, SB);
+        if (part) {
+            for (int a = 0; a < C.P.nacc; a++) part->acc_classes[a] = st.acc_classes[a];
+            // pair positions -> global (left id, right id) order keys
+            std::vector<unsigned long long> pidx;
+            for (const HGroup& h : groups) {
+                if (h.first != NOPOS) pidx.push_back(h.first);
+                for (int a = 0; a < C.P.nacc; a++)
+                    if (h.extpos[a] != NOPOS) pidx.push_back(h.extpos[a]);
+            }
+            for (unsigned long long p : pidx)
+                if (p >= np) throw HipError{"join partial: pair position out of range"};
+            if (!pidx.empty()) {
+                DevBuf lown, rown;
+                const unsigned long long *lg = nullptr, *rg = nullptr;
+                side_gids(c, L, A.n, lown, &lg);
+                side_gids(c, R, B.n, rown, &rg);
+                DevBuf dp(pidx.size() * 8), dk(pidx.size() * 8);
+                HIPCHECK(hipMemcpyAsync(dp.p, pidx.data(), pidx.size() * 8, hipMemcpyHostToDevice, c.stream));
+                HIPCHECK(cq_launch_pair_gid(pairs.as<uint2>(), dp.as<unsigned long long>(), (uint32_t)pidx.size(), lg,
+                                            rg, dk.as<unsigned long long>(), c.stream));
+                std::vector<unsigned long long> keys(pidx.size());
+                HIPCHECK(hipMemcpyAsync(keys.data(), dk.p, keys.size() * 8, hipMemcpyDeviceToHost, c.stream));
+                HIPCHECK(hipStreamSynchronize(c.stream));
+                size_t k = 0;
+                for (HGroup& h : groups) {
+                    if (h.first != NOPOS) h.first = keys[k++];
+                    for (int a = 0; a < C.P.nacc; a++)
+                        if (h.extpos[a] != NOPOS) h.extpos[a] = keys[k++];
+                }
+            }
+        }
+    }
+    if (part) {
+        // a rank that saw no groups still reports the plan's single group (COUNT = 0 ...)
+        part->names = J.names;
+        part->groups = std::move(groups);
+        return nullptr;
     }
     g_stats.groups = groups.size();
     cq_table* res = build_groups(C, groups, Lit, c);
@@ -2283,9 +2387,148 @@ cqgpu_table* cqgpu_table_from_bytes(const void* data, size_t n, cq_csv_config cf
     }
 }
 
+// ---- join-key repartition (multi-GPU JOIN) -----------------------------------
+int cqgpu_route_plan(cq_node* q, cqgpu_table* const* tables, int ntables, int side, int nranks,
+                     uint64_t* bytes_per_rank, uint64_t* recs_per_rank) {
+    g_inel.clear();
+    g_err.clear();
+    try {
+        DevCtx& c = ctx();
+        bump_reset(c);
+        if (ntables < 2 || !tables[0] || !tables[1] || (side != 0 && side != 1)) throw HipError{"route: bad tables"};
+        if (nranks < 1 || nranks > 4096) throw HipError{"route: bad rank count"};
+        if (!q || q->kind != CQ_N_QUERY || q->u.q.join_count != 1 || !q->u.q.joins[0]) throw Ineligible{"not one JOIN"};
+        check_plan_shape(q, tables[0], true);
+        cq_node* jn = q->u.q.joins[0];
+        if (jn->u.join.kind != CQ_JOIN_INNER) throw Ineligible{"outer JOIN across partials"};
+        cq_node* on = jn->u.join.on;
+        const cqgpu_table* L = tables[0];
+        const cqgpu_table* R = tables[1];
+        const char* la = (q->u.q.from && q->u.q.from->u.from.alias) ? q->u.q.from->u.from.alias : "main";
+        const char* ra = jn->u.join.alias ? jn->u.join.alias : "right";
+        int k = -1;
+        if (on && on->kind == CQ_N_CONDITION && on->u.bin.op && !strcmp(on->u.bin.op, "=") && on->u.bin.lhs &&
+            on->u.bin.rhs && on->u.bin.lhs->kind == CQ_N_IDENTIFIER && on->u.bin.rhs->kind == CQ_N_IDENTIFIER) {
+            // same operand binding as run_join (evaluator_joins.c:49-52)
+            k = side == 0 ? join_on_index(on->u.bin.lhs->u.text, L, L, la, R, ra)
+                          : join_on_index(on->u.bin.rhs->u.text, R, L, la, R, ra);
+        }
+        if (k < 0) throw Ineligible{"JOIN without an `ident = ident` ON across partials"};
+        cqgpu_table* t = tables[side];
+        auto st = std::make_unique<RouteState>();
+        JoinSide S;
+        S.cols.push_back(k);
+        load_side(c, t, S);
+        std::swap(st->recs.p, S.recs.p);
+        const uint32_t n = S.n;
+        st->n = n;
+        std::vector<unsigned long long> per(2 * (size_t)nranks, 0);
+        if (n) {
+            DevBuf codes((size_t)n * 8), cls((size_t)n * 4), dest((size_t)n * 4), dsorted((size_t)n * 4),
+                idx((size_t)n * 4), len((size_t)n * 4), order((size_t)n * 4), lens((size_t)n * 8),
+                off((size_t)n * 8), dper(per.size() * 8);
+            HIPCHECK(hipMemsetAsync(dper.p, 0, per.size() * 8, c.stream));
+            HIPCHECK(cq_launch_join_code(S.cells.as<Cell>(), 1, 0, n, codes.as<unsigned long long>(), cls.as<uint32_t>(),
+                                         idx.as<uint32_t>(), nullptr, c.stream));
+            HIPCHECK(cq_launch_route_len(t->g, st->recs.as<unsigned long long>(), n, codes.as<unsigned long long>(),
+                                         cls.as<uint32_t>(), (uint32_t)nranks, len.as<uint32_t>(), dest.as<uint32_t>(),
+                                         dper.as<unsigned long long>(), c.stream));
+            int bits = 1;
+            while ((1 << bits) < nranks) bits++;
+            size_t tb = 0;
+            HIPCHECK(cq_sort_dest(nullptr, &tb, dest.as<unsigned int>(), dsorted.as<unsigned int>(), idx.as<unsigned int>(),
+                                  order.as<unsigned int>(), n, bits, c.stream));
+            DevBuf temp(tb);
+            HIPCHECK(cq_sort_dest(temp.p, &tb, dest.as<unsigned int>(), dsorted.as<unsigned int>(), idx.as<unsigned int>(),
+                                  order.as<unsigned int>(), n, bits, c.stream));
+            HIPCHECK(cq_launch_gather_len(len.as<uint32_t>(), order.as<uint32_t>(), n, lens.as<unsigned long long>(),
+                                          c.stream));
+            size_t tb2 = 0;
+            HIPCHECK(cq_excl_sum_u64(nullptr, &tb2, lens.as<unsigned long long>(), off.as<unsigned long long>(), n,
+                                     c.stream));
+            DevBuf temp2(tb2);
+            HIPCHECK(cq_excl_sum_u64(temp2.p, &tb2, lens.as<unsigned long long>(), off.as<unsigned long long>(), n,
+                                     c.stream));
+            HIPCHECK(hipMemcpyAsync(per.data(), dper.p, per.size() * 8, hipMemcpyDeviceToHost, c.stream));
+            HIPCHECK(hipStreamSynchronize(c.stream));
+            std::swap(st->order.p, order.p);
+            std::swap(st->len.p, len.p);
+            std::swap(st->off.p, off.p);
+        }
+        st->bytes = 0;
+        for (int r = 0; r < nranks; r++) {
+            st->bytes += per[r];
+            if (bytes_per_rank) bytes_per_rank[r] = per[r];
+            if (recs_per_rank) recs_per_rank[r] = per[nranks + r];
+        }
+        t->route = std::move(st);
+        return 0;
+    } catch (Ineligible& e) {
+        g_inel = e.why;
+        set_err("cq_amd: query outside the GPU executor's subset: %s", e.why.c_str());
+        return -1;
+    } catch (HipError& e) {
+        set_err("cq_amd: %s", e.msg.c_str());
+        return -1;
+    }
+}
+
+int cqgpu_route_fill(cqgpu_table* t, uint64_t gid_base, void* dev_bytes, uint64_t* dev_gids) {
+    g_err.clear();
+    try {
+        DevCtx& c = ctx();
+        if (!t || !t->route) throw HipError{"route_fill without route_plan"};
+        RouteState& st = *t->route;
+        if (gid_base + st.n > (1ull << 32)) throw HipError{"route: more than 2^32 records on a join side"};
+        if (st.n) {
+            if (!dev_bytes || !dev_gids) throw HipError{"route_fill: null output buffer"};
+            HIPCHECK(cq_launch_route_copy(t->g, st.recs.as<unsigned long long>(), st.order.as<uint32_t>(),
+                                          st.len.as<uint32_t>(), st.off.as<unsigned long long>(), st.n, gid_base,
+                                          (uint8_t*)dev_bytes, (unsigned long long*)dev_gids, c.stream));
+            HIPCHECK(hipStreamSynchronize(c.stream));
+        }
+        t->route.reset();
+        return 0;
+    } catch (HipError& e) {
+        set_err("cq_amd: %s", e.msg.c_str());
+        return -1;
+    }
+}
+
+cqgpu_table* cqgpu_table_from_routed(const void* dev_bytes, size_t n, const uint64_t* dev_gids, size_t nrec,
+                                     cq_csv_config cfg, const char* header, size_t header_len) {
+    g_err.clear();
+    cqgpu_table* t = nullptr;
+    try {
+        DevCtx& c = ctx();
+        if (!header) throw HipError{"routed table needs the header record"};
+        if ((n && !dev_bytes) || (nrec && !dev_gids)) throw HipError{"routed table: null buffer"};
+        t = upload(nullptr, 0, cfg, 0, header, header_len);
+        // replace the empty upload with the received bytes (records already '\n'-terminated)
+        (void)hipFree(t->dbuf);
+        t->dbuf = nullptr;
+        HIPCHECK(hipMalloc(&t->dbuf, PAD_BEFORE + n + PAD_AFTER));
+        HIPCHECK(hipMemsetAsync(t->dbuf, '\n', PAD_BEFORE, c.stream));
+        HIPCHECK(hipMemsetAsync(t->dbuf + PAD_BEFORE + n, '\n', PAD_AFTER, c.stream));
+        if (n) HIPCHECK(hipMemcpyAsync(t->dbuf + PAD_BEFORE, dev_bytes, n, hipMemcpyDeviceToDevice, c.stream));
+        t->g = t->dbuf + PAD_BEFORE;
+        t->n = n;
+        HIPCHECK(hipMalloc((void**)&t->gids, std::max<size_t>(nrec, 1) * 8));
+        if (nrec) HIPCHECK(hipMemcpyAsync(t->gids, dev_gids, nrec * 8, hipMemcpyDeviceToDevice, c.stream));
+        t->ngids = nrec;
+        HIPCHECK(hipStreamSynchronize(c.stream));
+        return t;
+    } catch (HipError& e) {
+        set_err("cq_amd: %s", e.msg.c_str());
+        cqgpu_table_free(t);
+        return nullptr;
+    }
+}
+
 void cqgpu_table_free(cqgpu_table* t) {
     if (!t) return;
     if (t->dbuf) (void)hipFree(t->dbuf);
+    if (t->gids) (void)hipFree(t->gids);
     delete t;
 }
 
@@ -2587,6 +2830,41 @@ size_t cqgpu_query_partial(cq_node* q, cqgpu_table* const* tables, int ntables, 
         bump_reset(c);
         if (ntables < 1 || !tables[0]) throw HipError{"no table"};
         const cqgpu_table* t = tables[0];
+        if (q && q->kind == CQ_N_QUERY && q->u.q.join_count > 0) {
+            // repartitioned INNER JOIN: this rank's routed sides (cqgpu_route_* + cqgpu_table_from_routed)
+            check_plan_shape(q, t, true);
+            if (ntables < 2 || !tables[1]) throw Ineligible{"join table not given"};
+            JoinPartial jp;
+            (void)run_join(c, q, t, tables[1], &jp);
+            Compiled C;
+            cqgpu_table J;
+            J.names = jp.names;
+            compile_aggregate(&J, q, C);
+            Blob b;
+            b.u32(0x314a5143u);                      // "CQJ1"
+            b.u32((uint32_t)jp.names.size());
+            for (auto& nm : jp.names) b.str(nm);
+            b.u32((uint32_t)C.P.nacc);
+            for (int a = 0; a < C.P.nacc; a++) b.u32(jp.acc_classes[a]);
+            const uint32_t nrep = (uint32_t)C.rep_cols.size();
+            b.u32(nrep);
+            b.u32(jp.lmask);
+            b.u32(jp.rmask);
+            b.u64(jp.groups.size());
+            for (const HGroup& h : jp.groups) {
+                b.u32(h.kcls); b.u32(h.klen); b.u64(h.kw0); b.u64(h.kw1); b.str(h.kbytes);
+                b.u64(h.cnt); b.u64(h.first);
+                for (int a = 0; a < C.P.nacc; a++) {
+                    b.f64(h.sum[a]); b.u64(h.num[a]); b.u64(h.extpos[a]); b.cell(h.ext[a]);
+                }
+                for (uint32_t r = 0; r < nrep; r++) b.cell(r < h.reps.size() ? h.reps[r] : HCell());
+            }
+            void* out = malloc(std::max<size_t>(b.d.size(), 1));
+            if (!out) throw HipError{"out of host memory"};
+            memcpy(out, b.d.data(), b.d.size());
+            *blob_out = out;
+            return b.d.size();
+        }
         check_plan_shape(q, t);
         if (is_row_query(q)) throw Ineligible{"row-returning SELECT across partials"};
         Compiled C;
@@ -2640,16 +2918,20 @@ cq_table* cqgpu_merge_partials(cq_node* q, const void* const* blobs, const size_
             std::vector<HGroup> groups;
         };
         std::vector<Part> parts(nblobs);
-        uint32_t nacc = 0, nrep = 0;
+        uint32_t nacc = 0, nrep = 0, magic0 = 0, lmask = 0, rmask = 0;
         for (int bi = 0; bi < nblobs; bi++) {
             Reader r{(const uint8_t*)blobs[bi], sizes[bi], 0};
-            if (r.u32() != 0x31505143u) throw HipError{"bad partial blob"};
+            const uint32_t magic = r.u32();
+            if (magic != 0x31505143u && magic != 0x314a5143u) throw HipError{"bad partial blob"};
+            if (bi == 0) magic0 = magic;
+            else if (magic != magic0) throw HipError{"partials from different plans"};
             Part& pt = parts[bi];
             pt.names.resize(r.u32());
             for (auto& nm : pt.names) nm = r.str();
             const uint32_t na = r.u32();
             for (uint32_t a = 0; a < na; a++) pt.classes.push_back(r.u32());
             const uint32_t nr = r.u32();
+            if (magic == 0x314a5143u) { lmask |= r.u32(); rmask |= r.u32(); }
             if (bi == 0) { nacc = na; nrep = nr; }
             else if (pt.names != parts[0].names || na != nacc || nr != nrep)
                 throw HipError{"partials from different plans"};
@@ -2666,9 +2948,18 @@ cq_table* cqgpu_merge_partials(cq_node* q, const void* const* blobs, const size_
             }
         }
         // the plan binds columns by name: compile it against the shards' header
+        const bool joined = magic0 == 0x314a5143u;
+        if (joined) {
+            // value_compare calls keys of different non-NULL classes equal (csv_reader.c:128):
+            // such pairs span ranks after a hash repartition, so the plan is refused
+            for (int x = 1; x < 4; x++)
+                for (int y = 1; y < 4; y++)
+                    if (x != y && (lmask >> x & 1) && (rmask >> y & 1))
+                        throw Ineligible{"join keys of different value classes across partials"};
+        }
         cqgpu_table meta;
         meta.names = parts[0].names;
-        check_plan_shape(q, &meta);
+        check_plan_shape(q, &meta, joined);
         if (is_row_query(q)) throw Ineligible{"row-returning SELECT across partials"};
         Compiled C;
         compile_aggregate(&meta, q, C);

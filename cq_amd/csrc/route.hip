@@ -1,0 +1,124 @@
+// route.hip -- join-key repartition for the multi-GPU JOIN.
+//
+// Each rank holds a contiguous byte range of both join inputs.  Every record is
+// sent to rank hash(key class, key code) mod N, so all records whose keys can be
+// equal under value_compare (reference csv_reader.c:98-130, evaluator_joins.c:40-60)
+// meet on one rank: the code is join_code (scan.hip) -- the double bits for
+// INTEGER/DOUBLE (they compare as doubles), the (y, m, d) word for DATE, the FNV
+// hash of the bytes for STRING, 0 for NULL.  Cross-class "equal" pairs cannot be
+// routed this way; the executor refuses such inputs after the exchange.
+//
+// The send buffer is the records themselves (bytes up to the terminator, one
+// '\n' appended), grouped by destination and in file order within a destination,
+// plus one u64 global record id per record.  Concatenated in source-rank order the
+// received records are a file-ordered subsequence of the whole input, so the local
+// join's (l, r) nested-loop order is the global one restricted to this rank.
+// Work is byte copying: HBM-bound, no LDS, no MFMA.
+#include <hip/hip_runtime.h>
+#include <hipcub/hipcub.hpp>
+#include <stdint.h>
+
+namespace {
+
+__device__ __forceinline__ uint64_t mix64(uint64_t x) {      // splitmix64 finalizer
+    x ^= x >> 30; x *= 0xbf58476d1ce4e5b9ull;
+    x ^= x >> 27; x *= 0x94d049bb133111ebull;
+    return x ^ (x >> 31);
+}
+
+// record length (through the terminator, which becomes '\n') and destination rank
+__global__ void route_len_kernel(const uint8_t* __restrict__ g, const unsigned long long* __restrict__ recs,
+                                 uint32_t n, const unsigned long long* __restrict__ codes,
+                                 const uint32_t* __restrict__ cls, uint32_t nranks, uint32_t* __restrict__ len,
+                                 uint32_t* __restrict__ dest, unsigned long long* __restrict__ per_rank) {
+    const uint32_t i = blockIdx.x * blockDim.x + threadIdx.x;
+    if (i >= n) return;
+    const uint8_t* p = g + recs[i];
+    uint32_t k = 0;
+    while (p[k] != '\n' && p[k] != '\r') k++;       // the table is padded with '\n' after its end
+    len[i] = k + 1;
+    const uint32_t d = (uint32_t)(mix64(codes[i] ^ ((uint64_t)cls[i] << 62)) % nranks);
+    dest[i] = d;
+    atomicAdd(&per_rank[d], (unsigned long long)(k + 1));
+    atomicAdd(&per_rank[nranks + d], 1ull);
+}
+
+__global__ void gather_len_kernel(const uint32_t* __restrict__ len, const uint32_t* __restrict__ order, uint32_t n,
+                                  unsigned long long* __restrict__ out) {
+    const uint32_t j = blockIdx.x * blockDim.x + threadIdx.x;
+    if (j < n) out[j] = len[order[j]];
+}
+
+// one wave per record: lanes copy the record's bytes, lane 0 writes the '\n'
+__global__ void route_copy_kernel(const uint8_t* __restrict__ g, const unsigned long long* __restrict__ recs,
+                                  const uint32_t* __restrict__ order, const uint32_t* __restrict__ len,
+                                  const unsigned long long* __restrict__ off, uint32_t n, uint64_t gid_base,
+                                  uint8_t* __restrict__ out, unsigned long long* __restrict__ gids) {
+    const uint32_t j = (blockIdx.x * blockDim.x + threadIdx.x) / 64;
+    const uint32_t lane = threadIdx.x & 63;
+    if (j >= n) return;
+    const uint32_t i = order[j];
+    const uint8_t* src = g + recs[i];
+    uint8_t* dst = out + off[j];
+    const uint32_t m = len[i] - 1;
+    for (uint32_t k = lane; k < m; k += 64) dst[k] = src[k];
+    if (lane == 0) {
+        dst[m] = '\n';
+        gids[j] = gid_base + i;
+    }
+}
+
+// (l, r) pair -> (global left id << 32 | global right id); ids < 2^32 (checked on the host)
+__global__ void pair_gid_kernel(const uint2* __restrict__ pairs, const unsigned long long* __restrict__ pidx,
+                                uint32_t n, const unsigned long long* __restrict__ lg,
+                                const unsigned long long* __restrict__ rg, unsigned long long* __restrict__ out) {
+    const uint32_t i = blockIdx.x * blockDim.x + threadIdx.x;
+    if (i >= n) return;
+    const uint2 pr = pairs[pidx[i]];
+    out[i] = (lg[pr.x] << 32) | rg[pr.y];
+}
+
+inline uint32_t blocks(uint64_t n, uint32_t b) { return (uint32_t)((n + b - 1) / b); }
+
+}  // namespace
+
+extern "C" {
+
+hipError_t cq_launch_route_len(const uint8_t* g, const unsigned long long* recs, uint32_t n,
+                               const unsigned long long* codes, const uint32_t* cls, uint32_t nranks, uint32_t* len,
+                               uint32_t* dest, unsigned long long* per_rank, hipStream_t s) {
+    if (!n) return hipSuccess;
+    route_len_kernel<<<blocks(n, 256), 256, 0, s>>>(g, recs, n, codes, cls, nranks, len, dest, per_rank);
+    return hipGetLastError();
+}
+
+// stable sort of record indices by destination rank
+hipError_t cq_sort_dest(void* temp, size_t* temp_bytes, const unsigned int* kin, unsigned int* kout,
+                        const unsigned int* vin, unsigned int* vout, size_t n, int bits, hipStream_t s) {
+    return hipcub::DeviceRadixSort::SortPairs(temp, *temp_bytes, kin, kout, vin, vout, (int)n, 0, bits, s);
+}
+
+hipError_t cq_launch_gather_len(const uint32_t* len, const uint32_t* order, uint32_t n, unsigned long long* out,
+                                hipStream_t s) {
+    if (!n) return hipSuccess;
+    gather_len_kernel<<<blocks(n, 256), 256, 0, s>>>(len, order, n, out);
+    return hipGetLastError();
+}
+
+hipError_t cq_launch_route_copy(const uint8_t* g, const unsigned long long* recs, const uint32_t* order,
+                                const uint32_t* len, const unsigned long long* off, uint32_t n, uint64_t gid_base,
+                                uint8_t* out, unsigned long long* gids, hipStream_t s) {
+    if (!n) return hipSuccess;
+    route_copy_kernel<<<blocks((uint64_t)n * 64, 256), 256, 0, s>>>(g, recs, order, len, off, n, gid_base, out, gids);
+    return hipGetLastError();
+}
+
+hipError_t cq_launch_pair_gid(const uint2* pairs, const unsigned long long* pidx, uint32_t n,
+                              const unsigned long long* lg, const unsigned long long* rg, unsigned long long* out,
+                              hipStream_t s) {
+    if (!n) return hipSuccess;
+    pair_gid_kernel<<<blocks(n, 256), 256, 0, s>>>(pairs, pidx, n, lg, rg, out);
+    return hipGetLastError();
+}
+
+}  // extern "C"

@@ -69,6 +69,34 @@ size_t cqgpu_query_partial(cq_node* query_ast, cqgpu_table* const* tables, int n
 cq_table* cqgpu_merge_partials(cq_node* query_ast, const void* const* blobs, const size_t* sizes,
                                int nblobs);
 
+/* ---- join-key repartition for the multi-GPU JOIN ---
+ * One INNER JOIN with an `ident = ident` ON (reference evaluator_joins.c:40-60,
+ * :63-181) over range-partitioned inputs: every rank routes each record of its
+ * shard of side `side` (0 = FROM table, 1 = JOIN table) to rank
+ * hash(key value class, key code) mod nranks, exchanges the records with an
+ * all-to-all (RCCL over xGMI), rebuilds each side from what it received
+ * (concatenated in source-rank order) and runs cqgpu_query_partial on the pair;
+ * cqgpu_merge_partials gives the whole-input result -- groups in first-appearance
+ * order of the (l, r) nested loop, as perform_join + create_groups would.
+ * Inputs whose keys mix value classes (which value_compare calls "equal") are
+ * refused by the merge.
+ *
+ * route_plan: computes the routing of tables[side] (tables = {FROM shard, JOIN
+ * shard}, needed to bind the ON operands) and writes per destination rank the
+ * byte count and record count of the send buffer.  Returns 0, or -1 with
+ * cqgpu_last_error() / cqgpu_last_ineligible() set. */
+int cqgpu_route_plan(cq_node* query_ast, cqgpu_table* const* tables, int ntables, int side, int nranks,
+                     uint64_t* bytes_per_rank, uint64_t* recs_per_rank);
+/* route_fill: writes the planned send buffer into device memory: records grouped
+ * by destination rank (file order within a rank, each '\n'-terminated) into
+ * dev_bytes, and their global record ids (gid_base + local record index) into
+ * dev_gids.  gid_base = records of this side on lower ranks. */
+int cqgpu_route_fill(cqgpu_table* t, uint64_t gid_base, void* dev_bytes, uint64_t* dev_gids);
+/* table over received records (device memory, copied) with their global ids and
+ * the side's header record */
+cqgpu_table* cqgpu_table_from_routed(const void* dev_bytes, size_t n, const uint64_t* dev_gids, size_t nrec,
+                                     cq_csv_config cfg, const char* header, size_t header_len);
+
 /* ---- introspection -------------------------------------------------------- */
 typedef struct {
     double scan_ms;              /* device time of the last fused scan kernel (HIP events) */
