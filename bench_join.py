@@ -1,0 +1,218 @@
+#!/usr/bin/env python3
+"""Join benchmark: BASELINE.json configs[4] shape (users x orders hash join), weak-scaled.
+
+Per GPU: `--users` users rows and `--orders` orders rows (synthetic, seed 42;
+users id = 10^10 + i, orders customer_id = 10^10 + U[0, N x users), i.e. SURVEY.md
+section 8d's config 5 at a per-GPU size that fits one step in seconds), resident in
+HBM as CSV bytes.  One step = the whole repartitioned join of
+    SELECT u.role, COUNT(*), SUM(o.price) FROM 'users.csv' AS u
+    JOIN 'orders.csv' AS o ON u.id = o.customer_id GROUP BY u.role
+on every rank: device key routing of both shards (route.hip), the record
+all-to-all over RCCL (cq_amd.dist.exchange; skipped at N = 1), rebuilding both
+sides from the received records, the device join + group aggregate (run_join),
+the partial-blob all_gather and the merge on rank 0.
+
+    python bench_join.py [--gpus N] [--steps K] [--warmup W] [--users U] [--orders O]
+
+Prints one JSON line (rank 0): rows/s = (users + orders rows, all ranks) / step
+time, plus the joined pair count (= all orders rows: every customer_id exists).
+Not the driver's bench line (bench.py is); a measurement of the join path.
+"""
+import argparse
+import json
+import os
+import sys
+import time
+
+import numpy as np
+import torch
+
+ROOT = os.path.dirname(os.path.abspath(__file__))
+sys.path.insert(0, ROOT)
+
+
+def _digits(v: np.ndarray, w: int) -> np.ndarray:
+    out = np.empty((v.size, w), dtype=np.uint8)
+    x = v.astype(np.int64).copy()
+    for k in range(w - 1, -1, -1):
+        out[:, k] = 48 + x % 10
+        x //= 10
+    return out
+
+
+def users_shard(n: int, first_id: int, rng) -> bytes:
+    """`id,name,age,role` rows, fixed width: 10^10+i, 6 letters, 10-80, role_000-999"""
+    m = np.empty((n, 31), dtype=np.uint8)
+    m[:, 0:11] = _digits(np.arange(n, dtype=np.int64) + 10**10 + first_id, 11)
+    m[:, 11] = 44
+    m[:, 12:18] = rng.integers(65, 81, n).astype(np.uint8)[:, None]
+    m[:, 18] = 44
+    m[:, 19:21] = _digits(rng.integers(10, 81, n), 2)
+    m[:, 21] = 44
+    m[:, 22:27] = np.frombuffer(b"role_", dtype=np.uint8)
+    m[:, 27:30] = _digits(rng.integers(0, 1000, n), 3)
+    m[:, 30] = 10
+    return m.tobytes()
+
+
+def orders_shard(n: int, first_id: int, n_users_total: int, rng) -> bytes:
+    """`id,price,quantity,customer_id` rows: 10^10+i, ddd.dd, 1-9, 10^10+U[0, users)"""
+    m = np.empty((n, 33), dtype=np.uint8)
+    m[:, 0:11] = _digits(np.arange(n, dtype=np.int64) + 10**10 + first_id, 11)
+    m[:, 11] = 44
+    price = rng.integers(100, 100000, n)
+    m[:, 12:15] = _digits(price // 100, 3)
+    m[:, 15] = 46
+    m[:, 16:18] = _digits(price % 100, 2)
+    m[:, 18] = 44
+    m[:, 19] = 48 + rng.integers(1, 10, n).astype(np.uint8)
+    m[:, 20] = 44
+    m[:, 21:32] = _digits(rng.integers(0, n_users_total, n) + 10**10, 11)
+    m[:, 32] = 10
+    return m.tobytes()
+
+
+def main():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--gpus", type=int, default=1)
+    ap.add_argument("--steps", type=int, default=5)
+    ap.add_argument("--warmup", type=int, default=1)
+    ap.add_argument("--users", type=int, default=20_000_000, help="users rows per GPU")
+    ap.add_argument("--orders", type=int, default=20_000_000, help="orders rows per GPU")
+    ap.add_argument("--seed", type=int, default=42)
+    args = ap.parse_args()
+    rank = int(os.environ.get("RANK", "0"))
+    world = int(os.environ.get("WORLD_SIZE", "1"))
+    local = int(os.environ.get("LOCAL_RANK", "0"))
+    torch.cuda.set_device(local)
+    dev = torch.device("cuda", local)
+    torch.zeros(1, device=dev)
+    dist = None
+    if world > 1:
+        import torch.distributed as dist
+        dist.init_process_group("nccl", device_id=dev)
+
+    import ctypes as C
+    import cq_amd
+    from cq_amd import abi
+    from cq_amd.dist import exchange, exclusive_base, gather_blobs
+    cq_amd.lib()
+
+    t0 = time.time()
+    rng = np.random.default_rng([args.seed, rank])
+    uh, oh = b"id,name,age,role\n", b"id,price,quantity,customer_id\n"
+    ub = users_shard(args.users, rank * args.users, rng)
+    ob = orders_shard(args.orders, rank * args.orders, world * args.users, rng)
+    ut = cq_amd.Table.from_bytes(uh + ub if rank == 0 else ub, header=None if rank == 0 else uh)
+    ot = cq_amd.Table.from_bytes(oh + ob if rank == 0 else ob, header=None if rank == 0 else oh)
+    in_bytes = len(ub) + len(ob)
+    del ub, ob
+    gen_s = time.time() - t0
+
+    P = abi.Plan()
+    q = P.query([P.ident("u.role"), P.func("COUNT", P.lit("*")), P.func("SUM", P.ident("o.price"))],
+                "users.csv", alias="u", group_by=["u.role"],
+                joins=[("orders.csv", "o", P.cond("=", P.ident("u.id"), P.ident("o.customer_id")),
+                        abi.JOIN_INNER)])
+    ast = C.pointer(q)
+    phase = {}
+
+    def step():
+        ts = time.perf_counter()
+        routed = []
+        for side, (tab, hdr) in enumerate(((ut, uh), (ot, oh))):
+            nb, nr = cq_amd.route_plan(ast, [ut, ot], side, world)
+            base = exclusive_base(sum(nr), dev) if dist is not None else 0
+            sb = torch.empty(max(sum(nb), 1), dtype=torch.uint8, device=dev)
+            sg = torch.empty(max(sum(nr), 1), dtype=torch.int64, device=dev)
+            cq_amd.route_fill(tab, base, sb.data_ptr(), sg.data_ptr())
+            if dist is not None:
+                rb, _ = exchange(sb[: sum(nb)], nb)
+                rg, _ = exchange(sg[: sum(nr)], nr)
+                torch.cuda.synchronize(dev)
+            else:
+                rb, rg = sb[: sum(nb)], sg[: sum(nr)]
+            routed.append(cq_amd.table_from_routed(rb.data_ptr(), rb.numel(), rg.data_ptr(), rg.numel(), hdr))
+            del sb, sg, rb, rg
+        tr = time.perf_counter()
+        blob = cq_amd.query_partial(ast, routed)
+        st = cq_amd.stats()
+        tj = time.perf_counter()
+        blobs = gather_blobs(blob, dev) if dist is not None else [blob]
+        pairs = 0
+        if rank == 0:
+            tp = cq_amd.merge_partials(ast, blobs)
+            if not tp:
+                raise RuntimeError(cq_amd.last_error())
+            res = abi.table_to_py(tp)
+            cq_amd.result_free(tp)
+            pairs = int(sum(r[1][1] for r in res["rows"]))   # COUNT(*) cells: ("I", n)
+        for t in routed:
+            t.close()
+        te = time.perf_counter()
+        phase.setdefault("route_exchange_ms", []).append((tr - ts) * 1e3)
+        phase.setdefault("join_agg_ms", []).append((tj - tr) * 1e3)
+        phase.setdefault("merge_ms", []).append((te - tj) * 1e3)
+        phase.setdefault("pair_agg_kernel_ms", []).append(st["scan_ms"])
+        return pairs
+
+    pairs = 0
+    for _ in range(args.warmup):
+        pairs = step()
+    for k in phase:
+        phase[k].clear()
+
+    def barrier():
+        if dist is not None:
+            dist.barrier()
+        torch.cuda.synchronize(dev)
+
+    barrier()
+    t1 = time.perf_counter()
+    for _ in range(args.steps):
+        pairs = step()
+    barrier()
+    elapsed = time.perf_counter() - t1
+    if dist is not None:
+        t = torch.tensor([elapsed], dtype=torch.float64, device=dev)
+        dist.all_reduce(t, op=dist.ReduceOp.MAX)
+        elapsed = float(t.item())
+    rows_total = (args.users + args.orders) * world
+    if rank == 0:
+        if pairs != args.orders * world:
+            print(f"warning: {pairs} joined pairs, expected {args.orders * world}", file=sys.stderr)
+        line = {
+            "metric": "join rows/s (users + orders rows, key-repartitioned hash join + GROUP BY)",
+            "value": rows_total / (elapsed / args.steps),
+            "unit": "rows/s",
+            "n_gpus": world,
+            "steps": args.steps,
+            "warmup": args.warmup,
+            "ms_per_step": elapsed * 1e3 / args.steps,
+            "higher_is_better": True,
+            "scaling": "weak",
+            "vs_baseline": None,
+            "dtype": "u8",
+            "data": f"synthetic users/orders CSV (SURVEY.md 8d config 5 shape, seed {args.seed}), resident in HBM",
+            "config": {
+                "workload": "config5 per GPU: SELECT u.role, COUNT(*), SUM(o.price) FROM users u "
+                            "JOIN orders o ON u.id = o.customer_id GROUP BY u.role",
+                "users_per_gpu": args.users,
+                "orders_per_gpu": args.orders,
+                "bytes_per_gpu": in_bytes,
+                "joined_pairs": pairs,
+                "parallelism": f"dp{world} (hash repartition all_to_all over RCCL)",
+            },
+            "phases_ms": {k: sum(v) / len(v) for k, v in phase.items()},
+            "setup_s": gen_s,
+        }
+        print(json.dumps(line), flush=True)
+    ut.close()
+    ot.close()
+    if dist is not None:
+        dist.barrier()
+        dist.destroy_process_group()
+
+
+if __name__ == "__main__":
+    main()
