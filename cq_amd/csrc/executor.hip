@@ -115,7 +115,12 @@ hipError_t cq_sort_offsets(void* temp, size_t* temp_bytes, const unsigned long l
                            unsigned long long* out, size_t n, int bits, hipStream_t s);
 hipError_t cq_launch_route_len(const uint8_t* g, const unsigned long long* recs, uint32_t n,
                                const unsigned long long* codes, const uint32_t* cls, uint32_t nranks, uint32_t* len,
-                               uint32_t* dest, unsigned long long* per_rank, hipStream_t s);
+                               uint32_t* dest, hipStream_t s);
+hipError_t cq_launch_route_bounds(const uint32_t* dsorted, const unsigned long long* off,
+                                  const unsigned long long* lens, uint32_t n, uint32_t nranks,
+                                  unsigned long long* starts, hipStream_t s);
+hipError_t cq_sort_codes(void* temp, size_t* temp_bytes, const unsigned long long* kin, unsigned long long* kout,
+                         const unsigned int* vin, unsigned int* vout, size_t n, hipStream_t s);
 hipError_t cq_sort_dest(void* temp, size_t* temp_bytes, const unsigned int* kin, unsigned int* kout,
                         const unsigned int* vin, unsigned int* vout, size_t n, int bits, hipStream_t s);
 hipError_t cq_launch_gather_len(const uint32_t* len, const uint32_t* order, uint32_t n, unsigned long long* out,
@@ -2053,14 +2058,26 @@ cq_table* run_join(DevCtx& c, cq_node* q, const cqgpu_table* L, const cqgpu_tabl
         HIPCHECK(hipMemcpyAsync(dsegs, segs, 32, hipMemcpyHostToDevice, c.stream));
         HIPCHECK(cq_launch_gather_codes(rcodes.as<unsigned long long>(), ridx_c.as<uint32_t>(), B.n,
                                         codes_c.as<unsigned long long>(), c.stream));
+        // within each class segment by code (stable); one full-width radix sort per
+        // non-empty segment (a segmented sort runs each segment in one workgroup)
         size_t tb1 = 0;
-        HIPCHECK(cq_sort_codes_seg(nullptr, &tb1, codes_c.as<unsigned long long>(), scodes.as<unsigned long long>(),
-                                   ridx_c.as<unsigned int>(), sidx.as<unsigned int>(), B.n, dsegs, dsegs + 4, 4,
-                                   c.stream));
+        for (int k = 0; k < 4; k++) {
+            if (!per[k]) continue;
+            size_t tk = 0;
+            HIPCHECK(cq_sort_codes(nullptr, &tk, codes_c.as<unsigned long long>(), scodes.as<unsigned long long>(),
+                                   ridx_c.as<unsigned int>(), sidx.as<unsigned int>(), per[k], c.stream));
+            tb1 = std::max(tb1, tk);
+        }
         DevBuf temp1(tb1);
-        HIPCHECK(cq_sort_codes_seg(temp1.p, &tb1, codes_c.as<unsigned long long>(), scodes.as<unsigned long long>(),
-                                   ridx_c.as<unsigned int>(), sidx.as<unsigned int>(), B.n, dsegs, dsegs + 4, 4,
-                                   c.stream));
+        for (int k = 0; k < 4; k++) {
+            if (!per[k]) continue;
+            const size_t o = JR.seg[k];
+            size_t tk = tb1;
+            HIPCHECK(cq_sort_codes(temp1.p, &tk, codes_c.as<unsigned long long>() + o,
+                                   scodes.as<unsigned long long>() + o, ridx_c.as<unsigned int>() + o,
+                                   sidx.as<unsigned int>() + o, per[k], c.stream));
+        }
+        (void)dsegs;
         HIPCHECK(hipStreamSynchronize(c.stream));        // segs (host) and the sort's inputs stay alive until here
         JR.scodes = scodes.as<unsigned long long>();
         JR.sidx = sidx.as<uint32_t>();
@@ -2426,13 +2443,12 @@ int cqgpu_route_plan(cq_node* q, cqgpu_table* const* tables, int ntables, int si
         if (n) {
             DevBuf codes((size_t)n * 8), cls((size_t)n * 4), dest((size_t)n * 4), dsorted((size_t)n * 4),
                 idx((size_t)n * 4), len((size_t)n * 4), order((size_t)n * 4), lens((size_t)n * 8),
-                off((size_t)n * 8), dper(per.size() * 8);
-            HIPCHECK(hipMemsetAsync(dper.p, 0, per.size() * 8, c.stream));
+                off((size_t)n * 8), dst((2 * (size_t)nranks + 2) * 8);
             HIPCHECK(cq_launch_join_code(S.cells.as<Cell>(), 1, 0, n, codes.as<unsigned long long>(), cls.as<uint32_t>(),
                                          idx.as<uint32_t>(), nullptr, c.stream));
             HIPCHECK(cq_launch_route_len(t->g, st->recs.as<unsigned long long>(), n, codes.as<unsigned long long>(),
                                          cls.as<uint32_t>(), (uint32_t)nranks, len.as<uint32_t>(), dest.as<uint32_t>(),
-                                         dper.as<unsigned long long>(), c.stream));
+                                         c.stream));
             int bits = 1;
             while ((1 << bits) < nranks) bits++;
             size_t tb = 0;
@@ -2449,8 +2465,16 @@ int cqgpu_route_plan(cq_node* q, cqgpu_table* const* tables, int ntables, int si
             DevBuf temp2(tb2);
             HIPCHECK(cq_excl_sum_u64(temp2.p, &tb2, lens.as<unsigned long long>(), off.as<unsigned long long>(), n,
                                      c.stream));
-            HIPCHECK(hipMemcpyAsync(per.data(), dper.p, per.size() * 8, hipMemcpyDeviceToHost, c.stream));
+            HIPCHECK(cq_launch_route_bounds(dsorted.as<uint32_t>(), off.as<unsigned long long>(),
+                                            lens.as<unsigned long long>(), n, (uint32_t)nranks,
+                                            dst.as<unsigned long long>(), c.stream));
+            std::vector<unsigned long long> starts(2 * (size_t)nranks + 2);
+            HIPCHECK(hipMemcpyAsync(starts.data(), dst.p, starts.size() * 8, hipMemcpyDeviceToHost, c.stream));
             HIPCHECK(hipStreamSynchronize(c.stream));
+            for (int r = 0; r < nranks; r++) {
+                per[nranks + r] = starts[r + 1] - starts[r];
+                per[r] = starts[nranks + 2 + r] - starts[nranks + 1 + r];
+            }
             std::swap(st->order.p, order.p);
             std::swap(st->len.p, len.p);
             std::swap(st->off.p, off.p);

@@ -30,17 +30,34 @@ __device__ __forceinline__ uint64_t mix64(uint64_t x) {      // splitmix64 final
 __global__ void route_len_kernel(const uint8_t* __restrict__ g, const unsigned long long* __restrict__ recs,
                                  uint32_t n, const unsigned long long* __restrict__ codes,
                                  const uint32_t* __restrict__ cls, uint32_t nranks, uint32_t* __restrict__ len,
-                                 uint32_t* __restrict__ dest, unsigned long long* __restrict__ per_rank) {
+                                 uint32_t* __restrict__ dest) {
     const uint32_t i = blockIdx.x * blockDim.x + threadIdx.x;
     if (i >= n) return;
     const uint8_t* p = g + recs[i];
     uint32_t k = 0;
     while (p[k] != '\n' && p[k] != '\r') k++;       // the table is padded with '\n' after its end
     len[i] = k + 1;
-    const uint32_t d = (uint32_t)(mix64(codes[i] ^ ((uint64_t)cls[i] << 62)) % nranks);
-    dest[i] = d;
-    atomicAdd(&per_rank[d], (unsigned long long)(k + 1));
-    atomicAdd(&per_rank[nranks + d], 1ull);
+    dest[i] = (uint32_t)(mix64(codes[i] ^ ((uint64_t)cls[i] << 62)) % nranks);
+}
+
+// per-destination record and byte starts from the destination-sorted layout
+// (thread j in [0, n]: destinations in (dsorted[j-1], dsorted[j]] start at j)
+__global__ void route_bounds_kernel(const uint32_t* __restrict__ dsorted, const unsigned long long* __restrict__ off,
+                                    const unsigned long long* __restrict__ lens, uint32_t n, uint32_t nranks,
+                                    unsigned long long* __restrict__ starts) {
+    const uint32_t j = blockIdx.x * blockDim.x + threadIdx.x;
+    if (j > n) return;
+    const int64_t lo = j == 0 ? -1 : (int64_t)dsorted[j - 1];
+    const int64_t hi = j == n ? (int64_t)nranks - 1 : (int64_t)dsorted[j];
+    const unsigned long long b = j < n ? off[j] : off[n - 1] + lens[n - 1];
+    for (int64_t d = lo + 1; d <= hi; d++) {
+        starts[d] = j;
+        starts[nranks + 1 + d] = b;
+    }
+    if (j == n) {
+        starts[nranks] = n;
+        starts[2 * nranks + 1] = b;
+    }
 }
 
 __global__ void gather_len_kernel(const uint32_t* __restrict__ len, const uint32_t* __restrict__ order, uint32_t n,
@@ -86,9 +103,19 @@ extern "C" {
 
 hipError_t cq_launch_route_len(const uint8_t* g, const unsigned long long* recs, uint32_t n,
                                const unsigned long long* codes, const uint32_t* cls, uint32_t nranks, uint32_t* len,
-                               uint32_t* dest, unsigned long long* per_rank, hipStream_t s) {
+                               uint32_t* dest, hipStream_t s) {
     if (!n) return hipSuccess;
-    route_len_kernel<<<blocks(n, 256), 256, 0, s>>>(g, recs, n, codes, cls, nranks, len, dest, per_rank);
+    route_len_kernel<<<blocks(n, 256), 256, 0, s>>>(g, recs, n, codes, cls, nranks, len, dest);
+    return hipGetLastError();
+}
+
+// starts[0..nranks]: record index where each destination begins (starts[nranks] = n);
+// starts[nranks+1 .. 2*nranks+1]: the same in send-buffer bytes
+hipError_t cq_launch_route_bounds(const uint32_t* dsorted, const unsigned long long* off,
+                                  const unsigned long long* lens, uint32_t n, uint32_t nranks,
+                                  unsigned long long* starts, hipStream_t s) {
+    if (!n) return hipSuccess;
+    route_bounds_kernel<<<blocks((uint64_t)n + 1, 256), 256, 0, s>>>(dsorted, off, lens, n, nranks, starts);
     return hipGetLastError();
 }
 

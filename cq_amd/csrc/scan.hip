@@ -1334,14 +1334,22 @@ __device__ __forceinline__ uint64_t join_code(const Cell& c) {
 __global__ void join_code_kernel(const Cell* __restrict__ cells, uint32_t stride, uint32_t kcol, uint32_t n,
                                  unsigned long long* __restrict__ codes, uint32_t* __restrict__ cls,
                                  uint32_t* __restrict__ idx, unsigned int* __restrict__ per_class) {
+    // per-class counts: block-local LDS counters, one global atomic per class per block
+    // (a global atomic per row serialises 10^7 rows on four addresses)
+    __shared__ unsigned int cnt[4];
+    if (threadIdx.x < 4) cnt[threadIdx.x] = 0;
+    __syncthreads();
     const uint32_t i = blockIdx.x * blockDim.x + threadIdx.x;
-    if (i >= n) return;
-    const Cell c = cells[(uint64_t)i * stride + kcol];
-    codes[i] = join_code(c);
-    const uint32_t k = key_class(c);
-    cls[i] = k;
-    if (idx) idx[i] = i;
-    if (per_class) atomicAdd(&per_class[k], 1u);
+    if (i < n) {
+        const Cell c = cells[(uint64_t)i * stride + kcol];
+        codes[i] = join_code(c);
+        const uint32_t k = key_class(c);
+        cls[i] = k;
+        if (idx) idx[i] = i;
+        if (per_class) atomicAdd(&cnt[k], 1u);
+    }
+    __syncthreads();
+    if (per_class && threadIdx.x < 4 && cnt[threadIdx.x]) atomicAdd(&per_class[threadIdx.x], cnt[threadIdx.x]);
 }
 
 __global__ void gather_codes_kernel(const unsigned long long* __restrict__ codes, const uint32_t* __restrict__ idx,
