@@ -66,22 +66,31 @@ __global__ void gather_len_kernel(const uint32_t* __restrict__ len, const uint32
     if (j < n) out[j] = len[order[j]];
 }
 
-// one wave per record: lanes copy the record's bytes, lane 0 writes the '\n'
+// one wave per 64 consecutive output records: each lane loads one record's
+// (source, destination, length) coalesced, then the wave copies the records one
+// after another with lane k moving byte k (records are ~30-40 B: one pass each)
 __global__ void route_copy_kernel(const uint8_t* __restrict__ g, const unsigned long long* __restrict__ recs,
                                   const uint32_t* __restrict__ order, const uint32_t* __restrict__ len,
                                   const unsigned long long* __restrict__ off, uint32_t n, uint64_t gid_base,
                                   uint8_t* __restrict__ out, unsigned long long* __restrict__ gids) {
-    const uint32_t j = (blockIdx.x * blockDim.x + threadIdx.x) / 64;
+    const uint64_t j0 = ((uint64_t)blockIdx.x * blockDim.x + threadIdx.x) & ~(uint64_t)63;
     const uint32_t lane = threadIdx.x & 63;
-    if (j >= n) return;
-    const uint32_t i = order[j];
-    const uint8_t* src = g + recs[i];
-    uint8_t* dst = out + off[j];
-    const uint32_t m = len[i] - 1;
-    for (uint32_t k = lane; k < m; k += 64) dst[k] = src[k];
-    if (lane == 0) {
-        dst[m] = '\n';
+    const uint64_t j = j0 + lane;
+    unsigned long long src = 0, dst = 0;
+    uint32_t m = 0;
+    if (j < n) {
+        const uint32_t i = order[j];
+        src = recs[i];
+        dst = off[j];
+        m = len[i];
         gids[j] = gid_base + i;
+    }
+    const uint32_t cnt = (uint32_t)((uint64_t)n - j0 < 64 ? (uint64_t)n - j0 : 64);
+    for (uint32_t r = 0; r < cnt; r++) {
+        const unsigned long long s = __shfl(src, (int)r);
+        const unsigned long long d = __shfl(dst, (int)r);
+        const uint32_t mm = (uint32_t)__shfl((int)m, (int)r);
+        for (uint32_t k = lane; k < mm; k += 64) out[d + k] = k + 1 == mm ? (uint8_t)'\n' : g[s + k];
     }
 }
 
@@ -136,7 +145,7 @@ hipError_t cq_launch_route_copy(const uint8_t* g, const unsigned long long* recs
                                 const uint32_t* len, const unsigned long long* off, uint32_t n, uint64_t gid_base,
                                 uint8_t* out, unsigned long long* gids, hipStream_t s) {
     if (!n) return hipSuccess;
-    route_copy_kernel<<<blocks((uint64_t)n * 64, 256), 256, 0, s>>>(g, recs, order, len, off, n, gid_base, out, gids);
+    route_copy_kernel<<<blocks(n, 256), 256, 0, s>>>(g, recs, order, len, off, n, gid_base, out, gids);
     return hipGetLastError();
 }
 
