@@ -116,6 +116,10 @@ hipError_t cq_sort_offsets(void* temp, size_t* temp_bytes, const unsigned long l
 hipError_t cq_launch_route_len(const uint8_t* g, const unsigned long long* recs, uint32_t n,
                                const unsigned long long* codes, const uint32_t* cls, uint32_t nranks, uint32_t* len,
                                uint32_t* dest, hipStream_t s);
+uint32_t cq_rs_blocks(uint64_t n);
+hipError_t cq_launch_rs_count(const uint8_t* g, uint64_t lo, uint64_t n, unsigned long long* counts, hipStream_t s);
+hipError_t cq_launch_rs_write(const uint8_t* g, uint64_t lo, uint64_t n, const unsigned long long* base,
+                              unsigned long long* out, hipStream_t s);
 hipError_t cq_launch_route_bounds(const uint32_t* dsorted, const unsigned long long* off,
                                   const unsigned long long* lens, uint32_t n, uint32_t nranks,
                                   unsigned long long* starts, hipStream_t s);
@@ -1853,6 +1857,31 @@ bool is_row_query(cq_node* q);
 
 // every data record of t, file order (csv_load's rows)
 uint32_t all_records(DevCtx& c, const cqgpu_table* t, DevBuf& out) {
+    // record starts in file order (route.hip rs_*: count, scan, write; no atomics)
+    const uint32_t nb = cq_rs_blocks(t->n);
+    DevBuf counts((size_t)nb * 8), base((size_t)nb * 8);
+    HIPCHECK(cq_launch_rs_count(t->g, t->data_begin, t->n, counts.as<unsigned long long>(), c.stream));
+    size_t tb = 0;
+    HIPCHECK(cq_excl_sum_u64(nullptr, &tb, counts.as<unsigned long long>(), base.as<unsigned long long>(), nb, c.stream));
+    DevBuf temp(tb);
+    HIPCHECK(cq_excl_sum_u64(temp.p, &tb, counts.as<unsigned long long>(), base.as<unsigned long long>(), nb, c.stream));
+    unsigned long long last[2] = {0, 0};
+    HIPCHECK(hipMemcpyAsync(&last[0], base.as<unsigned long long>() + nb - 1, 8, hipMemcpyDeviceToHost, c.stream));
+    HIPCHECK(hipMemcpyAsync(&last[1], counts.as<unsigned long long>() + nb - 1, 8, hipMemcpyDeviceToHost, c.stream));
+    HIPCHECK(hipStreamSynchronize(c.stream));
+    const unsigned long long n = last[0] + last[1];
+    if (n >= (1ull << 32)) throw Ineligible{"join side over 2^32 rows"};
+    DevBuf recs(std::max<unsigned long long>(n, 1) * 8);
+    HIPCHECK(cq_launch_rs_write(t->g, t->data_begin, t->n, base.as<unsigned long long>(), recs.as<unsigned long long>(),
+                                c.stream));
+    HIPCHECK(hipStreamSynchronize(c.stream));
+    std::swap(out.p, recs.p);
+    return (uint32_t)n;
+}
+
+// record starts through the general scan path (kept for cqgpu_debug_all_records'
+// cross-check against the two-pass kernels)
+uint32_t all_records_scan(DevCtx& c, const cqgpu_table* t, DevBuf& out) {
     Compiled C;
     memset(&C.P, 0, sizeof C.P);
     C.P.group_slot = -1;
@@ -2707,6 +2736,28 @@ int cqgpu_explain(cq_node* q, const char* header, cq_csv_config cfg, char* out, 
 }
 
 // record start offsets of every data record, in file order (tokenizer check)
+size_t cqgpu_debug_all_records(cqgpu_table* t, int method, unsigned long long* out, size_t cap) {
+    g_err.clear();
+    try {
+        DevCtx& c = ctx();
+        if (!t) throw HipError{"no table"};
+        DevBuf recs;
+        const uint32_t n = method == 1 ? all_records_scan(c, t, recs) : all_records(c, t, recs);
+        const size_t m = std::min<size_t>(n, cap);
+        if (m && out) {
+            HIPCHECK(hipMemcpyAsync(out, recs.p, m * 8, hipMemcpyDeviceToHost, c.stream));
+            HIPCHECK(hipStreamSynchronize(c.stream));
+        }
+        return n;
+    } catch (Ineligible& e) {
+        set_err("cq_amd: %s", e.why.c_str());
+        return (size_t)-1;
+    } catch (HipError& e) {
+        set_err("cq_amd: %s", e.msg.c_str());
+        return (size_t)-1;
+    }
+}
+
 size_t cqgpu_debug_records(cqgpu_table* t, unsigned long long* out, size_t cap) {
     try {
         DevCtx& c = ctx();

@@ -104,6 +104,70 @@ __global__ void pair_gid_kernel(const uint2* __restrict__ pairs, const unsigned 
     out[i] = (lg[pr.x] << 32) | rg[pr.y];
 }
 
+// ---- record starts of a whole table (csv_load's line split, reference
+// csv_reader.c:403-427: a record is a maximal non-empty run of bytes other than
+// '\n' / '\r'; the header record ends at data_begin).  Two bandwidth passes over
+// the bytes, no atomics: per-block counts, an exclusive scan, then each block
+// writes its starts in file order.  Each thread owns 16 bytes; the byte before
+// them comes from the previous lane (or memory: the table is padded with '\n').
+constexpr uint32_t RS_T = 256;                  // threads per block
+constexpr uint32_t RS_B = RS_T * 16;            // bytes per block
+
+__device__ __forceinline__ uint32_t start_mask(const uint8_t* __restrict__ g, uint64_t p0, uint64_t lo, uint64_t n) {
+    const uint4 v = *(const uint4*)(g + p0);
+    const uint32_t w[4] = {v.x, v.y, v.z, v.w};
+    uint32_t term = 0;                           // bit b: byte p0+b is a terminator
+    for (int q = 0; q < 4; q++)
+        for (int b = 0; b < 4; b++) {
+            const uint32_t ch = (w[q] >> (8 * b)) & 0xff;
+            term |= (uint32_t)(ch == '\n' || ch == '\r') << (4 * q + b);
+        }
+    const uint8_t prev = g[(int64_t)p0 - 1];
+    const uint32_t prev_term = (term << 1) | (uint32_t)(prev == '\n' || prev == '\r');
+    uint32_t m = ~term & prev_term & 0xffffu;
+    // only positions in [lo, n)
+    for (int b = 0; b < 16; b++)
+        if (p0 + b < lo || p0 + b >= n) m &= ~(1u << b);
+    return m;
+}
+
+__global__ void rs_count_kernel(const uint8_t* __restrict__ g, uint64_t lo, uint64_t n,
+                                unsigned long long* __restrict__ counts) {
+    const uint64_t p0 = (uint64_t)blockIdx.x * RS_B + threadIdx.x * 16;
+    const uint32_t c = p0 < n ? (uint32_t)__popc(start_mask(g, p0, lo, n)) : 0u;
+    __shared__ uint32_t part[RS_T / 64];
+    uint32_t s = c;
+    for (int o = 32; o > 0; o >>= 1) s += __shfl_down(s, o, 64);
+    if ((threadIdx.x & 63) == 0) part[threadIdx.x / 64] = s;
+    __syncthreads();
+    if (threadIdx.x == 0) {
+        unsigned long long t = 0;
+        for (uint32_t k = 0; k < RS_T / 64; k++) t += part[k];
+        counts[blockIdx.x] = t;
+    }
+}
+
+__global__ void rs_write_kernel(const uint8_t* __restrict__ g, uint64_t lo, uint64_t n,
+                                const unsigned long long* __restrict__ base, unsigned long long* __restrict__ out) {
+    const uint64_t p0 = (uint64_t)blockIdx.x * RS_B + threadIdx.x * 16;
+    const uint32_t m = p0 < n ? start_mask(g, p0, lo, n) : 0u;
+    const uint32_t c = (uint32_t)__popc(m);
+    // block exclusive scan of c
+    const uint32_t lane = threadIdx.x & 63, wv = threadIdx.x / 64;
+    uint32_t inc = c;
+    for (int o = 1; o < 64; o <<= 1) {
+        const uint32_t y = __shfl_up(inc, o, 64);
+        if (lane >= (uint32_t)o) inc += y;
+    }
+    __shared__ uint32_t wt[RS_T / 64];
+    if (lane == 63) wt[wv] = inc;
+    __syncthreads();
+    uint32_t before = 0;
+    for (uint32_t k = 0; k < wv; k++) before += wt[k];
+    unsigned long long pos = base[blockIdx.x] + before + inc - c;
+    for (uint32_t mm = m; mm; mm &= mm - 1) out[pos++] = p0 + (uint32_t)__builtin_ctz(mm);
+}
+
 inline uint32_t blocks(uint64_t n, uint32_t b) { return (uint32_t)((n + b - 1) / b); }
 
 }  // namespace
@@ -146,6 +210,19 @@ hipError_t cq_launch_route_copy(const uint8_t* g, const unsigned long long* recs
                                 uint8_t* out, unsigned long long* gids, hipStream_t s) {
     if (!n) return hipSuccess;
     route_copy_kernel<<<blocks(n, 256), 256, 0, s>>>(g, recs, order, len, off, n, gid_base, out, gids);
+    return hipGetLastError();
+}
+
+// record starts of g[lo, n) in file order: first call with out == nullptr returns
+// the block count (scratch: counts/base of that many u64); see all_records
+uint32_t cq_rs_blocks(uint64_t n) { return blocks(n ? n : 1, RS_B); }
+hipError_t cq_launch_rs_count(const uint8_t* g, uint64_t lo, uint64_t n, unsigned long long* counts, hipStream_t s) {
+    rs_count_kernel<<<cq_rs_blocks(n), RS_T, 0, s>>>(g, lo, n, counts);
+    return hipGetLastError();
+}
+hipError_t cq_launch_rs_write(const uint8_t* g, uint64_t lo, uint64_t n, const unsigned long long* base,
+                              unsigned long long* out, hipStream_t s) {
+    rs_write_kernel<<<cq_rs_blocks(n), RS_T, 0, s>>>(g, lo, n, base, out);
     return hipGetLastError();
 }
 

@@ -123,6 +123,10 @@ const char* cqgpu_last_ineligible(void);
 size_t cqgpu_debug_records(cqgpu_table* t, unsigned long long* out, size_t cap);
 cq_table* cqgpu_debug_cells(cqgpu_table* t, const int* cols, int ncols,
                             const unsigned long long* recs, size_t nrec);
+/* every data record's start offset in file order, as the join and the key
+ * routing see them: method 0 = the two-pass record-start kernels (route.hip),
+ * 1 = through the general scan path; returns the count ((size_t)-1 on error) */
+size_t cqgpu_debug_all_records(cqgpu_table* t, int method, unsigned long long* out, size_t cap);
 /* the fused scan kernel's own parse of ascending columns `cols` for every
  * record (rows in arbitrary order, their record offsets in recs_out) */
 cq_table* cqgpu_debug_scan_cells(cqgpu_table* t, const int* cols, int ncols,
