@@ -139,6 +139,9 @@ __device__ __forceinline__ GKey raw_key(uint32_t len, uint64_t w0, uint64_t w1) 
     return k;
 }
 
+#ifndef LEAN_PF
+#define LEAN_PF 1          // windows in flight per wave (1 or 2; 2 measured 2.58 vs 2.52 ms on config 3)
+#endif
 struct Win {            // one window in flight
     v4u a, b;           // staged bytes [32l, 32l + 32)
 };
@@ -557,9 +560,18 @@ __global__ __launch_bounds__(LT) void lean_kernel(const uint8_t* __restrict__ g,
     uint64_t clk_[8] = {0, 0, 0, 0, 0, 0, 0, 0};
     uint64_t clk_last_ = __builtin_amdgcn_s_memtime();
 #endif
+    // LEAN_PF windows in flight per wave (the one being processed + LEAN_PF - 1
+    // prefetched): 4 waves per SIMD with one 2 KiB window each leave too few bytes
+    // in flight to cover HBM latency at full bandwidth (Little's law)
     Win nx;
+#if LEAN_PF >= 2
+    Win nx2;
+#endif
     uint64_t w = LP.first_win + (uint64_t)blockIdx.x * NWV + wv;
     if (w < last_win) load_win(g, w, wstr_b, nx);
+#if LEAN_PF >= 2
+    if (w + wstep < last_win) load_win(g, w + wstep, wstr_b, nx2);
+#endif
     for (uint32_t round = 0; w < last_win; round++, w += wstep) {
         const uint64_t ws = w * wstr_b;
 #ifdef LEAN_CLK
@@ -568,7 +580,12 @@ __global__ __launch_bounds__(LT) void lean_kernel(const uint8_t* __restrict__ g,
         const Win cur = nx;
         LCLK(0);
 #ifndef LEAN_NOMEM   // profiling build LEAN_NOMEM: every window re-processes the first one (no HBM reads)
+#if LEAN_PF >= 2
+        nx = nx2;
+        if (w + 2 * wstep < last_win) load_win(g, w + 2 * wstep, wstr_b, nx2);
+#else
         if (w + wstep < last_win) load_win(g, w + wstep, wstr_b, nx);
+#endif
 #endif
 
         // ---- stage and classify
