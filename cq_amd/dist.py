@@ -63,27 +63,32 @@ def exclusive_base(count: int, device: torch.device | str = "cpu") -> int:
     return sum(int(x.item()) for x in allc[: dist.get_rank()])
 
 
-def join_partitioned(ast, lshard, rshard, lheader: bytes, rheader: bytes, device: torch.device | str):
+def join_partitioned(ast, lshard, rshard, lheader: bytes, rheader: bytes, device: torch.device | str,
+                     comm_device: torch.device | str | None = None):
     """Repartitioned INNER JOIN over this rank's shards of both inputs.
 
     Returns the merged result pointer on rank 0 (free with cq_amd.result_free)
-    and None elsewhere.  Every rank must call it (collectives inside)."""
+    and None elsewhere.  Every rank must call it (collectives inside).
+    comm_device: where the collectives run -- `device` for RCCL (default); "cpu"
+    stages the exchange through host memory for a gloo group (tests)."""
     import cq_amd
     world, rank = dist.get_world_size(), dist.get_rank()
+    comm = torch.device(comm_device) if comm_device is not None else torch.device(device)
     routed = []
     for side, (tab, header) in enumerate(((lshard, lheader), (rshard, rheader))):
         nbytes, nrecs = cq_amd.route_plan(ast, [lshard, rshard], side, world)
-        base = exclusive_base(sum(nrecs), device)
+        base = exclusive_base(sum(nrecs), comm)
         sb = torch.empty(max(sum(nbytes), 1), dtype=torch.uint8, device=device)
         sg = torch.empty(max(sum(nrecs), 1), dtype=torch.int64, device=device)
         cq_amd.route_fill(tab, base, sb.data_ptr(), sg.data_ptr())
         torch.cuda.synchronize(device)
-        rb, _ = exchange(sb[: sum(nbytes)], nbytes)
-        rg, _ = exchange(sg[: sum(nrecs)], nrecs)
+        rb, _ = exchange(sb[: sum(nbytes)].to(comm), nbytes)
+        rg, _ = exchange(sg[: sum(nrecs)].to(comm), nrecs)
+        rb, rg = rb.to(device), rg.to(device)
         torch.cuda.synchronize(device)
         routed.append(cq_amd.table_from_routed(rb.data_ptr(), rb.numel(), rg.data_ptr(), rg.numel(), header))
     blob = cq_amd.query_partial(ast, routed)
-    blobs = gather_blobs(blob, device)
+    blobs = gather_blobs(blob, comm)
     if rank != 0:
         return None
     return cq_amd.merge_partials(ast, blobs)

@@ -170,3 +170,68 @@ def test_route_counts(files):
         assert [recs[i] for i in gids] == got
         lt.close()
         rt.close()
+
+
+def _dist_worker(rank, world, port, lpath, rpath, sql, q):
+    """one rank of cq_amd.dist.join_partitioned; gloo group, shared GPU 0"""
+    import os
+    import torch.distributed as dist
+    os.environ["MASTER_ADDR"] = "127.0.0.1"
+    os.environ["MASTER_PORT"] = str(port)
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    try:
+        import cqtest as ct
+        import cq_amd as ca
+        from cq_amd import abi as ab
+        from cq_amd.dist import join_partitioned
+        shards = []
+        for path in (lpath, rpath):
+            data = open(path, "rb").read()
+            header, body = data.split(b"\n", 1)
+            header += b"\n"
+            cuts = [0] + [body.index(b"\n", len(body) * (k + 1) // world) + 1 for k in range(world - 1)] + [len(body)]
+            pc = body[cuts[rank]:cuts[rank + 1]]
+            t = ca.Table.from_bytes(header + pc) if rank == 0 else ca.Table.from_bytes(pc, header=header)
+            shards.append((t, header))
+        with ct.Parsed(sql) as ast:
+            tp = join_partitioned(ast, shards[0][0], shards[1][0], shards[0][1], shards[1][1], "cuda", "cpu")
+            res = None
+            if rank == 0:
+                res = ab.table_to_py(tp) if tp else ca.last_error()
+                if tp:
+                    ca.result_free(tp)
+        q.put((rank, res))
+        for t, _ in shards:
+            t.close()
+    finally:
+        dist.destroy_process_group()
+
+
+def test_join_partitioned_two_processes(files):
+    """the real driver (route, all_to_all, routed tables, partial, gather, merge)
+    in two processes over gloo, vs the oracle"""
+    import socket
+    import torch.multiprocessing as mp
+    data, paths = files
+    sql = (f"SELECT u.role, COUNT(*), SUM(o.price), MAX(o.quantity) FROM '{paths['du']}' AS u "
+           f"JOIN '{paths['do']}' AS o ON u.id = o.customer_id GROUP BY u.role")
+    want, unsup = cqtest.oracle_query(sql)
+    assert not unsup
+    s = socket.socket()
+    s.bind(("127.0.0.1", 0))
+    port = s.getsockname()[1]
+    s.close()
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    procs = [ctx.Process(target=_dist_worker, args=(r, 2, port, paths["du"], paths["do"], sql, q)) for r in range(2)]
+    for p in procs:
+        p.start()
+    res = dict(q.get(timeout=150) for _ in range(2))
+    for p in procs:
+        p.join(timeout=60)
+        assert p.exitcode == 0
+    got = res[0]
+    assert isinstance(got, dict), got
+    with cqtest.Parsed(sql) as ast:
+        tol = tolerant_columns(ast)
+    compare(got, want, tol, sql + " @ 2 processes")
