@@ -72,6 +72,35 @@ def orders_shard(n: int, first_id: int, n_users_total: int, rng) -> bytes:
     return m.tobytes()
 
 
+def cpu_baseline(n: int, seed: int):
+    """The unmodified reference (oracle/_ref/ref_probe, 1 core) on an n x n sample of
+    the same generators.  Its nested-loop join is O(L x R) (evaluator_joins.c:63-181),
+    so the sample is small and the figure is row-pairs/s: non-comparable with the
+    GPU's rows/s, reported beside it as SURVEY.md 8d asks."""
+    import subprocess
+    import tempfile
+    probe = os.path.join(ROOT, "oracle", "_ref", "ref_probe")
+    if not os.path.exists(probe):
+        return None
+    rng = np.random.default_rng([seed, 99])
+    with tempfile.TemporaryDirectory() as d:
+        up, op = os.path.join(d, "users.csv"), os.path.join(d, "orders.csv")
+        with open(up, "wb") as fh:
+            fh.write(b"id,name,age,role\n" + users_shard(n, 0, rng))
+        with open(op, "wb") as fh:
+            fh.write(b"id,price,quantity,customer_id\n" + orders_shard(n, 0, n, rng))
+        sql = (f"SELECT u.role, COUNT(*), SUM(o.price) FROM '{up}' AS u JOIN '{op}' AS o "
+               f"ON u.id = o.customer_id GROUP BY u.role")
+        out = subprocess.run(["taskset", "-c", "0", probe, "time", sql], capture_output=True, timeout=600)
+        if out.returncode != 0:
+            out = subprocess.run([probe, "time", sql], capture_output=True, timeout=600)
+        secs = json.loads(out.stdout.decode())["seconds"]
+    return {"value": n * n / secs, "unit": "row-pairs/s", "cores": 1, "kind": "reference",
+            "rows_per_s": 2 * n / secs, "seconds": secs, "comparable": False,
+            "sample": f"{n} users x {n} orders of the same generators; reference parse + evaluate_query "
+                      f"(nested-loop join incl. csv_load) = {secs:.2f} s"}
+
+
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
@@ -80,6 +109,8 @@ def main():
     ap.add_argument("--users", type=int, default=20_000_000, help="users rows per GPU")
     ap.add_argument("--orders", type=int, default=20_000_000, help="orders rows per GPU")
     ap.add_argument("--seed", type=int, default=42)
+    ap.add_argument("--cpu-rows", type=int, default=5000, help="n of the reference's n x n join sample")
+    ap.add_argument("--no-cpu", action="store_true")
     args = ap.parse_args()
     rank = int(os.environ.get("RANK", "0"))
     world = int(os.environ.get("WORLD_SIZE", "1"))
@@ -179,6 +210,12 @@ def main():
         elapsed = float(t.item())
     rows_total = (args.users + args.orders) * world
     if rank == 0:
+        cpu = None
+        if world == 1 and not args.no_cpu:
+            try:
+                cpu = cpu_baseline(args.cpu_rows, args.seed)
+            except Exception as e:  # reported, never fatal
+                print(f"cpu baseline failed: {e}", file=sys.stderr)
         if pairs != args.orders * world:
             print(f"warning: {pairs} joined pairs, expected {args.orders * world}", file=sys.stderr)
         line = {
@@ -204,6 +241,7 @@ def main():
                 "parallelism": f"dp{world} (hash repartition all_to_all over RCCL)",
             },
             "phases_ms": {k: sum(v) / len(v) for k, v in phase.items()},
+            "cpu_baseline": cpu,
             "setup_s": gen_s,
         }
         print(json.dumps(line), flush=True)
