@@ -2407,10 +2407,129 @@ cqgpu_table* open_table(const char* path, cq_csv_config cfg) {
     return t;
 }
 
+// ---- device-resident table cache of the drop-in entry point -----------------
+// The reference re-reads and re-parses the file on every query (csv_load per
+// evaluate_query, evaluator_joins.c:219 for joins).  evaluate_query keeps the
+// uploaded bytes resident in HBM between calls instead, keyed by path and the
+// file's identity (device, inode, size, mtime in ns) plus the CSV config; a
+// changed file misses and is re-uploaded, so results equal a fresh load.
+// LRU within a byte budget (CQGPU_TABLE_CACHE_BYTES, default 32 GiB of the 288 GB
+// HBM; 0 disables).
+struct CacheEnt {
+    std::string path;
+    uint64_t dev = 0, ino = 0, size = 0;
+    int64_t mtime_ns = 0;
+    char delim = ',', quote = '"';
+    bool header = true;
+    cqgpu_table* t = nullptr;
+    uint64_t tick = 0;
+};
+std::vector<CacheEnt> g_cache;
+uint64_t g_cache_tick = 0, g_cache_hits = 0;
+long long g_cache_limit = -1;           // -1: not read from the environment yet
+
+uint64_t cache_limit() {
+    if (g_cache_limit < 0) {
+        const char* e = getenv("CQGPU_TABLE_CACHE_BYTES");
+        g_cache_limit = e ? (long long)strtoull(e, nullptr, 10) : (32ll << 30);
+    }
+    return (uint64_t)g_cache_limit;
+}
+
+void cache_drop(size_t i) {
+    cqgpu_table* t = g_cache[i].t;
+    g_cache.erase(g_cache.begin() + (long)i);
+    if (t->dbuf) (void)hipFree(t->dbuf);
+    if (t->gids) (void)hipFree(t->gids);
+    delete t;
+}
+
+// *owned: the caller frees the table (not cached)
+cqgpu_table* cached_open(const char* path, cq_csv_config cfg, bool* owned) {
+    *owned = true;
+    const uint64_t lim = cache_limit();
+    if (!lim) return open_table(path, cfg);
+    struct stat sb;
+    if (stat(path, &sb) != 0) return open_table(path, cfg);
+    const int64_t mt = (int64_t)sb.st_mtim.tv_sec * 1000000000ll + sb.st_mtim.tv_nsec;
+    int dev = 0;
+    (void)hipGetDevice(&dev);
+    for (size_t i = 0; i < g_cache.size(); i++) {
+        CacheEnt& e = g_cache[i];
+        if (e.path != path) continue;
+        if (e.dev == (uint64_t)sb.st_dev && e.ino == (uint64_t)sb.st_ino && e.size == (uint64_t)sb.st_size &&
+            e.mtime_ns == mt && e.delim == cfg.delimiter && e.quote == cfg.quote && e.header == cfg.has_header &&
+            e.t->device == dev) {
+            e.tick = ++g_cache_tick;
+            g_cache_hits++;
+            *owned = false;
+            return e.t;
+        }
+        if (e.dev != (uint64_t)sb.st_dev || e.ino != (uint64_t)sb.st_ino || e.size != (uint64_t)sb.st_size ||
+            e.mtime_ns != mt) {
+            cache_drop(i);          // the file changed: its bytes are stale
+            i--;
+        }
+    }
+    cqgpu_table* t = open_table(path, cfg);
+    if (!t || t->n > lim) return t;
+    uint64_t used = 0;
+    for (auto& e : g_cache) used += e.t->n;
+    while (!g_cache.empty() && used + t->n > lim) {
+        size_t v = 0;
+        for (size_t i = 1; i < g_cache.size(); i++)
+            if (g_cache[i].tick < g_cache[v].tick) v = i;
+        used -= g_cache[v].t->n;
+        cache_drop(v);
+    }
+    CacheEnt e;
+    e.path = path;
+    e.dev = (uint64_t)sb.st_dev;
+    e.ino = (uint64_t)sb.st_ino;
+    e.size = (uint64_t)sb.st_size;
+    e.mtime_ns = mt;
+    e.delim = cfg.delimiter;
+    e.quote = cfg.quote;
+    e.header = cfg.has_header;
+    e.t = t;
+    e.tick = ++g_cache_tick;
+    g_cache.push_back(e);
+    *owned = false;
+    return t;
+}
+
 }  // namespace
 
 // ================================================================== C ABI
 extern "C" {
+
+void cqgpu_cache_clear(void) {
+    while (!g_cache.empty()) cache_drop(g_cache.size() - 1);
+}
+
+long long cqgpu_set_cache_limit(long long bytes) {
+    const long long prev = (long long)cache_limit();
+    g_cache_limit = bytes < 0 ? 0 : bytes;
+    uint64_t used = 0;
+    for (auto& e : g_cache) used += e.t->n;
+    while (!g_cache.empty() && used > (uint64_t)g_cache_limit) {
+        size_t v = 0;
+        for (size_t i = 1; i < g_cache.size(); i++)
+            if (g_cache[i].tick < g_cache[v].tick) v = i;
+        used -= g_cache[v].t->n;
+        cache_drop(v);
+    }
+    return prev;
+}
+
+int cqgpu_cache_info(uint64_t* entries, uint64_t* bytes, uint64_t* hits) {
+    uint64_t used = 0;
+    for (auto& e : g_cache) used += e.t->n;
+    if (entries) *entries = g_cache.size();
+    if (bytes) *bytes = used;
+    if (hits) *hits = g_cache_hits;
+    return 0;
+}
 
 cqgpu_table* cqgpu_table_open(const char* path, cq_csv_config cfg) {
     try {
@@ -2642,19 +2761,33 @@ cq_table* evaluate_query(cq_node* q) {
         return nullptr;
     }
     std::vector<cqgpu_table*> tables;
-    cqgpu_table* base = cqgpu_table_open(f->u.from.path, global_csv_config);
-    if (!base) {
+    std::vector<bool> owned;
+    auto open_one = [&](const char* path) -> cqgpu_table* {
+        bool own = true;
+        cqgpu_table* t = nullptr;
+        try {
+            t = cached_open(path, global_csv_config, &own);
+        } catch (HipError& e) {
+            set_err("cq_amd: %s", e.msg.c_str());
+            t = nullptr;
+        }
+        if (!t) set_err("Error loading file: %s", path);
+        tables.push_back(t);
+        owned.push_back(own);
+        return t;
+    };
+    if (!open_one(f->u.from.path)) {
         fprintf(stderr, "Failed to load table from '%s'\n", f->u.from.path);
         return nullptr;
     }
-    tables.push_back(base);
     for (int j = 0; j < q->u.q.join_count; j++) {
         cq_node* jn = q->u.q.joins[j];
-        cqgpu_table* tj = (jn && jn->u.join.path) ? cqgpu_table_open(jn->u.join.path, global_csv_config) : nullptr;
-        tables.push_back(tj);
+        if (jn && jn->u.join.path) open_one(jn->u.join.path);
+        else { tables.push_back(nullptr); owned.push_back(true); }
     }
     cq_table* r = cqgpu_query(q, tables.data(), (int)tables.size());
-    for (auto* t : tables) cqgpu_table_free(t);
+    for (size_t i = 0; i < tables.size(); i++)
+        if (owned[i]) cqgpu_table_free(tables[i]);
     return r;
 }
 

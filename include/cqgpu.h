@@ -38,6 +38,16 @@ cq_table* evaluate_query(cq_node* query_ast);
 /* replaces the reference global (evaluator.c:23), written by main.c:99-101 */
 extern cq_csv_config global_csv_config;
 
+/* ---- device-resident table cache of evaluate_query ------------------------
+ * evaluate_query keeps each file's uploaded bytes in HBM between calls (the
+ * reference re-reads the file per query), keyed by path + device/inode/size/
+ * mtime + CSV config, so a changed file is re-read; LRU within a byte budget
+ * (env CQGPU_TABLE_CACHE_BYTES, default 32 GiB; 0 disables). */
+void cqgpu_cache_clear(void);
+/* new budget in bytes (0 disables and empties); returns the previous budget */
+long long cqgpu_set_cache_limit(long long bytes);
+int cqgpu_cache_info(uint64_t* entries, uint64_t* bytes, uint64_t* hits);
+
 /* ---- resident tables (replace csv_load on the GPU path) ------------------- */
 typedef struct cqgpu_table cqgpu_table;
 /* mmap + upload to the current HIP device (reference mmap.c:78-108 + csv_load) */
