@@ -2015,7 +2015,6 @@ cq_table* run_join(DevCtx& c, cq_node* q, const cqgpu_table* L, const cqgpu_tabl
     }
     const bool keyed = kl >= 0 && kr >= 0;
     if (part) {
-        if (kind != CQ_JOIN_INNER) throw Ineligible{"outer JOIN across partials"};
         if (!keyed) throw Ineligible{"JOIN without an `ident = ident` ON across partials"};
     }
     // the joined table's schema: alias.col names (evaluator_joins.c:30-37)
@@ -2565,7 +2564,6 @@ int cqgpu_route_plan(cq_node* q, cqgpu_table* const* tables, int ntables, int si
         if (!q || q->kind != CQ_N_QUERY || q->u.q.join_count != 1 || !q->u.q.joins[0]) throw Ineligible{"not one JOIN"};
         check_plan_shape(q, tables[0], true);
         cq_node* jn = q->u.q.joins[0];
-        if (jn->u.join.kind != CQ_JOIN_INNER) throw Ineligible{"outer JOIN across partials"};
         cq_node* on = jn->u.join.on;
         const cqgpu_table* L = tables[0];
         const cqgpu_table* R = tables[1];
@@ -2651,7 +2649,7 @@ int cqgpu_route_fill(cqgpu_table* t, uint64_t gid_base, void* dev_bytes, uint64_
         DevCtx& c = ctx();
         if (!t || !t->route) throw HipError{"route_fill without route_plan"};
         RouteState& st = *t->route;
-        if (gid_base + st.n > (1ull << 32)) throw HipError{"route: more than 2^32 records on a join side"};
+        if (gid_base + st.n >= (1ull << 32)) throw HipError{"route: 2^32 - 1 or more records on a join side"};
         if (st.n) {
             if (!dev_bytes || !dev_gids) throw HipError{"route_fill: null output buffer"};
             HIPCHECK(cq_launch_route_copy(t->g, st.recs.as<unsigned long long>(), st.order.as<uint32_t>(),

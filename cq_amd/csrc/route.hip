@@ -94,14 +94,21 @@ __global__ void route_copy_kernel(const uint8_t* __restrict__ g, const unsigned 
     }
 }
 
-// (l, r) pair -> (global left id << 32 | global right id); ids < 2^32 (checked on the host)
+// (l, r) pair -> its position key in the reference's output order (perform_join,
+// evaluator_joins.c:63-171): (global left id << 32 | global right id) for matched
+// pairs, (left id << 32) for an unmatched left row (it is its row's only output),
+// (2^32 - 1) << 32 | right id for an unmatched right row (appended after every
+// left-driven row, in right-row order).  Ids < 2^32 - 1 (checked on the host).
+constexpr uint32_t PAIR_NONE = 0xFFFFFFFFu;       // scan.hip JOIN_NONE
 __global__ void pair_gid_kernel(const uint2* __restrict__ pairs, const unsigned long long* __restrict__ pidx,
                                 uint32_t n, const unsigned long long* __restrict__ lg,
                                 const unsigned long long* __restrict__ rg, unsigned long long* __restrict__ out) {
     const uint32_t i = blockIdx.x * blockDim.x + threadIdx.x;
     if (i >= n) return;
     const uint2 pr = pairs[pidx[i]];
-    out[i] = (lg[pr.x] << 32) | rg[pr.y];
+    const unsigned long long l = pr.x == PAIR_NONE ? 0xFFFFFFFFull : lg[pr.x];
+    const unsigned long long r = pr.y == PAIR_NONE ? 0ull : rg[pr.y];
+    out[i] = (l << 32) | r;
 }
 
 // ---- record starts of a whole table (csv_load's line split, reference

@@ -80,8 +80,8 @@ cq_table* cqgpu_merge_partials(cq_node* query_ast, const void* const* blobs, con
                                int nblobs);
 
 /* ---- join-key repartition for the multi-GPU JOIN ---
- * One INNER JOIN with an `ident = ident` ON (reference evaluator_joins.c:40-60,
- * :63-181) over range-partitioned inputs: every rank routes each record of its
+ * One INNER / LEFT / RIGHT / FULL JOIN with an `ident = ident` ON (reference
+ * evaluator_joins.c:40-60, :63-181) over range-partitioned inputs: every rank routes each record of its
  * shard of side `side` (0 = FROM table, 1 = JOIN table) to rank
  * hash(key value class, key code) mod nranks, exchanges the records with an
  * all-to-all (RCCL over xGMI), rebuilds each side from what it received

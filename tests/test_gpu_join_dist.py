@@ -118,6 +118,16 @@ QUERIES = [
                  "WHERE o.price > 300 GROUP BY u.name HAVING COUNT(*) > 5 ORDER BY u.name LIMIT 20"),
     ("sa", "sb", "SELECT a.k, COUNT(*), SUM(b.w), MIN(a.v) FROM '{L}' AS a JOIN '{R}' AS b ON a.k = b.k GROUP BY a.k"),
     ("sa", "sb", "SELECT COUNT(*), MAX(b.w) FROM '{L}' AS a JOIN '{R}' AS b ON a.k = b.k WHERE a.v > 5000"),
+    # outer joins (evaluator_joins.c:128-171): unmatched rows are exact per rank after the
+    # repartition; their global positions come from the pair position keys
+    ("du", "do", "SELECT COUNT(*), SUM(o.price) FROM '{L}' AS u LEFT JOIN '{R}' AS o ON u.id = o.customer_id"),
+    ("du", "do", "SELECT u.role, COUNT(*), MAX(o.id), MIN(u.name) FROM '{L}' AS u LEFT JOIN '{R}' AS o "
+                 "ON u.id = o.customer_id GROUP BY u.role"),
+    ("du", "do", "SELECT o.quantity, COUNT(*), MIN(u.age) FROM '{L}' AS u RIGHT JOIN '{R}' AS o "
+                 "ON u.id = o.customer_id GROUP BY o.quantity"),
+    ("du", "do", "SELECT u.age, COUNT(*), SUM(o.price) FROM '{L}' AS u FULL JOIN '{R}' AS o "
+                 "ON u.id = o.customer_id GROUP BY u.age"),
+    ("sa", "sb", "SELECT b.k, COUNT(*), SUM(a.v) FROM '{L}' AS a FULL JOIN '{R}' AS b ON a.k = b.k GROUP BY b.k"),
 ]
 
 
