@@ -1483,6 +1483,9 @@ __global__ __launch_bounds__(256) void join_agg_kernel(const uint2* __restrict__
     const GroupTable& gt = c_gt;
     const int nneed = P.nneed, nacc = P.nacc;
     unsigned long long my_pass = 0;
+    uint32_t my_cls[MAX_ACC];             // value classes seen per MIN/MAX argument, flushed once per wave
+#pragma unroll
+    for (int a = 0; a < MAX_ACC; a++) my_cls[a] = 0;
     for (unsigned long long b0 = (unsigned long long)blockIdx.x * blockDim.x; b0 < np;
          b0 += (unsigned long long)gridDim.x * blockDim.x) {
         const unsigned long long i = b0 + threadIdx.x;
@@ -1498,11 +1501,9 @@ __global__ __launch_bounds__(256) void join_agg_kernel(const uint2* __restrict__
         }
         if (pass) {
             my_pass++;
-            for (int a = 0; a < nacc; a++)
-                if (P.acc[a].kind != ACC_SUM) {
-                    const uint32_t m = class_bit(get_cell(cs, P.acc[a].slot, nneed));
-                    if (m) atomicOr(&stats->acc_classes[a], m);
-                }
+#pragma unroll
+            for (int a = 0; a < MAX_ACC; a++)
+                if (a < nacc && P.acc[a].kind != ACC_SUM) my_cls[a] |= class_bit(get_cell(cs, P.acc[a].slot, nneed));
         }
         GKey key;
         key.cls = GK_ALL; key.len = 0; key.w0 = 0; key.w1 = 0;
@@ -1537,6 +1538,13 @@ __global__ __launch_bounds__(256) void join_agg_kernel(const uint2* __restrict__
     }
     for (int o = 32; o > 0; o >>= 1) my_pass += __shfl_down(my_pass, o, 64);
     if ((threadIdx.x & 63) == 0 && my_pass) atomicAdd(&stats->passed, my_pass);
+#pragma unroll
+    for (int a = 0; a < MAX_ACC; a++) {
+        if (a >= nacc) break;
+        uint32_t m = my_cls[a];
+        for (int o = 32; o > 0; o >>= 1) m |= (uint32_t)__shfl_xor((int)m, o, 64);
+        if ((threadIdx.x & 63) == 0 && m) atomicOr(&stats->acc_classes[a], m);
+    }
 }
 
 // WHERE over the joined rows of a row-returning query: 1 / 0 per pair
