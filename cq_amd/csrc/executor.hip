@@ -256,13 +256,73 @@ struct Scratch {
 };
 
 // owned device allocation
+// Device scratch blocks are recycled instead of hipFree'd: hipFree synchronises
+// the device and cost ~140 us per call (74 calls per repartitioned-join step,
+// ~10 ms).  Every kernel and copy of the library runs on the one DevCtx stream, so
+// a block released here and handed out again is only touched by work enqueued
+// after everything that used it before.  Released blocks are kept up to
+// DEVPOOL_KEEP bytes; a failed hipMalloc empties the pool and retries.
+constexpr size_t DEVPOOL_KEEP = 8ull << 30;
+struct DevPool {
+    std::multimap<size_t, void*> idle;
+    std::unordered_map<void*, size_t> live;
+    size_t idle_bytes = 0;
+};
+DevPool& devpool() {
+    static DevPool* P = new DevPool;      // never destroyed: blocks outlive static teardown
+    return *P;
+}
+size_t devpool_class(size_t n) {          // 4 size classes per power of two
+    n = std::max<size_t>(n, 256);
+    if (n <= 4096) return (n + 255) & ~(size_t)255;
+    int k = 63 - __builtin_clzll((unsigned long long)n);
+    const size_t step = (size_t)1 << (k - 2);
+    return (n + step - 1) & ~(step - 1);
+}
+void devpool_trim(size_t keep) {
+    DevPool& P = devpool();
+    while (P.idle_bytes > keep && !P.idle.empty()) {
+        auto it = std::prev(P.idle.end());   // largest first
+        P.idle_bytes -= it->first;
+        (void)hipFree(it->second);
+        P.idle.erase(it);
+    }
+}
+void* devpool_get(size_t bytes) {
+    DevPool& P = devpool();
+    const size_t sz = devpool_class(bytes);
+    auto it = P.idle.find(sz);
+    void* p = nullptr;
+    if (it != P.idle.end()) {
+        p = it->second;
+        P.idle.erase(it);
+        P.idle_bytes -= sz;
+    } else if (hipMalloc(&p, sz) != hipSuccess) {
+        (void)hipGetLastError();
+        devpool_trim(0);
+        HIPCHECK(hipMalloc(&p, sz));
+    }
+    P.live[p] = sz;
+    return p;
+}
+void devpool_put(void* p) {
+    DevPool& P = devpool();
+    auto it = P.live.find(p);
+    if (it == P.live.end()) { (void)hipFree(p); return; }
+    const size_t sz = it->second;
+    P.live.erase(it);
+    P.idle.emplace(sz, p);
+    P.idle_bytes += sz;
+    devpool_trim(DEVPOOL_KEEP);
+}
+
 struct DevBuf {
     void* p = nullptr;
     DevBuf() = default;
-    explicit DevBuf(size_t bytes) { HIPCHECK(hipMalloc(&p, std::max<size_t>(bytes, 256))); }
+    explicit DevBuf(size_t bytes) { p = devpool_get(bytes); }
     DevBuf(const DevBuf&) = delete;
     DevBuf& operator=(const DevBuf&) = delete;
-    ~DevBuf() { if (p) (void)hipFree(p); }
+    ~DevBuf() { if (p) devpool_put(p); }
     template <class T> T* as() const { return (T*)p; }
 };
 
