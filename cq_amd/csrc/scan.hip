@@ -1517,7 +1517,7 @@ __global__ __launch_bounds__(256) void join_agg_kernel(const uint2* __restrict__
             gi = g_insert(gt, key, h, stats);
             if (gi >= 0) {
                 atomicAdd(&gt.cnt[gi], 1ULL);
-                atomicMin(&gt.first[gi], i);
+                if (__atomic_load_n(&gt.first[gi], __ATOMIC_RELAXED) > i) atomicMin(&gt.first[gi], i);   // first only decreases
                 for (int a = 0; a < nacc; a++) {
                     const Cell c = get_cell(cs, P.acc[a].slot, nneed);
                     if (P.acc[a].kind == ACC_SUM && is_num(c)) {
