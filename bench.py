@@ -1,22 +1,30 @@
 #!/usr/bin/env python3
 """Benchmark: rows/s of cq's SELECT hot path (CSV scan + WHERE + GROUP BY) on MI355X.
 
-Workload (BASELINE.json configs[2] per GPU; configs[3] shape when N > 1):
-  synthetic Shape A+role CSV (reference utils/generate_big_dataset.py columns +
-  role_%03d, 1,000 groups), 100M rows per GPU, resident in HBM, and
-      SELECT role, COUNT(*), SUM(height), AVG(height) FROM 'big.csv'
-      WHERE age > 30 GROUP BY role
+Workload (BASELINE.json): the logical Shape A+role CSV of cq_amd/datagen.py
+(reference utils/generate_big_dataset.py columns + role_%03d, 1,000 groups,
+seed 42), resident in HBM, and
+    SELECT role, COUNT(*), SUM(height), AVG(height) FROM 'big.csv'
+    WHERE age > 30 GROUP BY role
+  * N = 1: configs[2] -- rows [0, 1e8) on one GPU (3.89 GB);
+  * N > 1: configs[3] -- rows [0, 1e9) range-partitioned over the N ranks (each
+    rank generates and uploads only its own rows; ~38.9 GB in all).
 One step = one full query over the resident bytes: the fused scan kernel
 (tokenize + type + filter + LDS hash aggregate), compaction, first-row gather,
-result materialisation; with N > 1 each rank scans its own row-range shard of
-one N x 100M-row file, partial group states are exchanged over RCCL
-(torch.distributed all_gather) and merged on rank 0 (weak scaling).
+result table; with N > 1 each rank scans its shard (cqgpu_query_partial), the
+partial group states are exchanged over RCCL and merged on rank 0.
+
+The last step's result is checked against tests/golden/big.json (the reference
+itself at 1e8 rows; the generator's draws at 1e9) or, for other sizes, against
+datagen.expected_filter_groupby; a mismatch exits non-zero.
 
     python bench.py [--gpus N] [--steps K] [--warmup W]
     torchrun --nproc-per-node N bench.py --gpus N ...
 
-Prints one JSON line (rank 0) with roofline (scan kernel HBM bytes/s vs 8 TB/s)
-and a CPU baseline: the unmodified reference (oracle/_ref/ref_probe built from
+Prints one JSON line (rank 0) with the roofline of the scan kernel (file bytes /
+HIP-event kernel time vs 8 TB/s), an end-to-end evaluate_query timing on the same
+file (mmap + H2D + scan), config 2 (filter + COUNT) as an extra key, and a CPU
+baseline: the unmodified reference (oracle/_ref/ref_probe built from
 /root/reference by oracle/ref.mk) timed on a bounded sample of the same workload.
 """
 import argparse
@@ -27,19 +35,20 @@ import subprocess
 import sys
 import tempfile
 import time
+from concurrent.futures import ProcessPoolExecutor
 
 import torch  # first: libcqgpu binds to the HIP runtime torch loads
 
 ROOT = os.path.dirname(os.path.abspath(__file__))
 sys.path.insert(0, ROOT)
+from cq_amd import datagen  # noqa: E402  (numpy only: safe before the GPU is touched)
 
 METRIC = "rows/sec scanned (filter+GROUP BY) at 1/2/4/8 GPUs; % of HBM read peak"
 QUERY = ("SELECT role, COUNT(*), SUM(height), AVG(height) FROM '{path}' "
          "WHERE age > 30 GROUP BY role")
-# --config 2 (not the bench line; a measurement of BASELINE configs[1]):
-# Shape A without role, filter + COUNT
 QUERY2 = "SELECT COUNT(*) FROM '{path}' WHERE age > 30"
 HBM_PEAK_GBS = 8000.0   # MI355X HBM3E spec (MI355X_MICROARCH.md, chip-level parameters)
+GOLDEN = os.path.join(ROOT, "tests", "golden", "big.json")
 
 
 def parse_args():
@@ -47,14 +56,18 @@ def parse_args():
     ap.add_argument("--gpus", type=int, default=1)
     ap.add_argument("--steps", type=int, default=20)
     ap.add_argument("--warmup", type=int, default=3)
-    ap.add_argument("--rows", type=int, default=100_000_000, help="data rows per GPU")
+    ap.add_argument("--rows", type=int, default=None,
+                    help="data rows of the logical file (default 1e8 at N=1, 1e9 at N>1)")
     ap.add_argument("--seed", type=int, default=42)
     ap.add_argument("--cpu-rows", type=int, default=8_000_000,
                     help="rows of the CPU-baseline sample (reference evaluator)")
     ap.add_argument("--no-cpu", action="store_true")
+    ap.add_argument("--no-e2e", action="store_true", help="skip the end-to-end evaluate_query timing")
+    ap.add_argument("--no-config2", action="store_true", help="skip the config-2 (filter + COUNT) key")
+    ap.add_argument("--gen-workers", type=int, default=4, help="processes generating this rank's rows")
     ap.add_argument("--traffic", default=os.path.join(ROOT, "profiles", "hbm_traffic.json"))
     ap.add_argument("--config", type=int, default=3, choices=(2, 3),
-                    help="3: the bench line (filter + GROUP BY); 2: Shape A filter + COUNT")
+                    help="3: the bench line (filter + GROUP BY); 2: Shape A filter + COUNT as the line")
     return ap.parse_args()
 
 
@@ -70,26 +83,85 @@ def build_plan(path, config=3):
     return P, q
 
 
+def _gen(args):
+    seed, lo, hi, role = args
+    return datagen.logical_rows(seed, lo, hi, role)
+
+
+def gen_rows(seed, lo, hi, role, workers):
+    """rows [lo, hi) of the logical file, generated chunk-parallel (before any GPU call)"""
+    step = datagen.CHUNK_ROWS
+    parts = [(seed, a, min(hi, (a // step + 1) * step), role) for a in
+             [lo] + list(range((lo // step + 1) * step, hi, step))] if hi > lo else []
+    if workers <= 1 or len(parts) <= 1:
+        return b"".join(_gen(p) for p in parts)
+    with ProcessPoolExecutor(max_workers=workers) as ex:
+        return b"".join(ex.map(_gen, parts))
+
+
+def expected_for(config, rows, seed):
+    """(expected answer, source) for the whole logical file rows [0, rows)"""
+    try:
+        with open(GOLDEN) as fh:
+            gj = json.load(fh)
+        if gj.get("seed") == seed:
+            for key in ("config3", "config4") if config == 3 else ("config2",):
+                ent = gj.get(key)
+                if ent and ent["rows"] == rows:
+                    src = ("reference (tests/golden/big.json %s)" % key if "reference" in ent
+                           else "generator draws (tests/golden/big.json %s)" % key)
+                    return ent["expected"], src
+    except FileNotFoundError:
+        pass
+    return datagen.expected_filter_groupby(seed, 0, rows, with_role=config == 3), "generator draws (computed)"
+
+
+def verify(res, exp, config):
+    """res: abi.table_to_py of the result; exp: expected_filter_groupby layout"""
+    rows = res["rows"]
+    if config == 2:
+        return len(rows) == 1 and rows[0][0] == ("I", exp["count"][0])
+    if len(rows) != len(exp["count"]):
+        return False
+    for r, name, cnt, cents in zip(rows, exp["groups"], exp["count"], exp["sum_cents"]):
+        if r[0] != ("S", name.encode()) or r[1] != ("I", cnt):
+            return False
+        s, a = r[2][1], r[3][1]
+        want = cents / 100.0
+        if abs(s - want) > 1e-6 * want or abs(a - want / cnt) > 1e-6 * (want / cnt):
+            return False
+    return True
+
+
 def cpu_baseline(rows, seed, config=3):
     """Reference evaluator (single-threaded C, -O2) on a bounded sample, 1 core."""
-    from cq_amd import datagen
     probe = os.path.join(ROOT, "oracle", "_ref", "ref_probe")
-    kind = "reference"
     if not os.path.exists(probe):
         return None
     with tempfile.TemporaryDirectory() as d:
         path = os.path.join(d, "sample.csv")
-        datagen.write_shape_a(path, rows, seed=seed, with_role=config == 3)
+        datagen.write_logical(path, rows, seed=seed, with_role=config == 3)
         query = (QUERY if config == 3 else QUERY2).format(path=path)
         out = subprocess.run(["taskset", "-c", "0", probe, "time", query], capture_output=True, timeout=600)
         if out.returncode != 0:
             out = subprocess.run([probe, "time", query], capture_output=True, timeout=600)
         res = json.loads(out.stdout.decode())
     secs = res["seconds"]
-    return {"value": rows / secs, "unit": "rows/s", "cores": 1, "kind": kind,
-            "sample": f"{rows} rows of the same workload (same generator, seed {seed}); "
-                      f"reference parse+evaluate_query wall time incl. csv_load = {secs:.2f} s",
-            "seconds": secs, "host_cores": os.cpu_count()}
+    cpu = {"value": rows / secs, "unit": "rows/s", "cores": 1, "kind": "reference",
+           "sample": f"rows [0, {rows}) of the same logical file (seed {seed}); reference parse + "
+                     f"evaluate_query wall time incl. csv_load = {secs:.2f} s, 1 core (taskset)",
+           "seconds": secs, "host_cores": os.cpu_count()}
+    try:
+        with open(GOLDEN) as fh:
+            g = json.load(fh)["config%d" % config]
+        cpu["full_size_reference"] = {
+            "rows": g["rows"], "seconds": g["reference_seconds"], "rows_per_s": g["rows"] / g["reference_seconds"],
+            "where": "build container (8 vCPU Xeon), tests/golden/make_big_golden.py",
+            "why_not_here": "a 1e8-row reference run takes ~6 min and ~35 GB RSS: outside the bench's "
+                            "few-minute budget, so the same-run number is the bounded sample above"}
+    except Exception:
+        pass
+    return cpu
 
 
 def main():
@@ -99,6 +171,21 @@ def main():
     local = int(os.environ.get("LOCAL_RANK", "0"))
     if world != args.gpus and "WORLD_SIZE" in os.environ:
         print(f"warning: WORLD_SIZE={world} but --gpus={args.gpus}", file=sys.stderr)
+    role = args.config == 3
+    total = args.rows if args.rows is not None else (100_000_000 if world == 1 else 1_000_000_000)
+
+    # ---- this rank's rows of the logical file, generated before the GPU is touched
+    t0 = time.time()
+    lo, hi = total * rank // world, total * (rank + 1) // world
+    header = datagen.header_of(role)
+    body = gen_rows(args.seed, lo, hi, role, args.gen_workers)
+    shard = header + body if rank == 0 else body
+    del body
+    data2 = None   # config 2's file (Shape A, no role), also generated before the GPU is touched
+    if world == 1 and args.config == 3 and not args.no_config2:
+        data2 = datagen.header_of(False) + gen_rows(args.seed, 0, 100_000_000, False, args.gen_workers)
+    gen_s = time.time() - t0
+
     torch.cuda.set_device(local)
     torch.zeros(1, device="cuda")
     dist = None
@@ -107,25 +194,11 @@ def main():
         dist.init_process_group("nccl", device_id=torch.device("cuda", local))
 
     import cq_amd
-    from cq_amd import abi, datagen
+    from cq_amd import abi
     from cq_amd.dist import gather_blobs
-    cq_amd.lib()
+    L = cq_amd.lib()
 
-    # ---- synthetic shard of this rank (one N x rows file, row-range partitioned)
     t0 = time.time()
-    role = args.config == 3
-    header = b"name,surname,age,gender,height,role\n" if role else b"name,surname,age,gender,height\n"
-    import numpy as np
-    rng = np.random.default_rng([args.seed, rank])
-    chunks = []
-    left = args.rows
-    while left > 0:
-        n = min(1 << 22, left)
-        chunks.append(datagen.shape_a_chunk(rng, n, role))
-        left -= n
-    body = b"".join(chunks)
-    del chunks
-    shard = header + body if rank == 0 else body
     sizes = [len(shard)]
     if dist is not None:
         allsz = [None] * world
@@ -135,27 +208,23 @@ def main():
     table = cq_amd.Table.from_bytes(shard, abi.csv_config(), base_offset=base,
                                     header=None if rank == 0 else header)
     nbytes = len(shard)
-    del body, shard
-    gen_s = time.time() - t0
+    upload_s = time.time() - t0
 
     P, q = build_plan("big.csv", args.config)
     ast = C.pointer(q)
-    L = cq_amd.lib()
-
     kernel_used = [1]
 
     def step():
+        """one query; returns (result pointer on rank 0 or None, scan ms)"""
         if dist is None:
             tp = L.cqgpu_query(ast, (C.c_void_p * 1)(table.handle.value), 1)
             if not tp:
                 raise RuntimeError(cq_amd.last_error())
-            ng = tp.contents.nrows
-            cq_amd.result_free(tp)
             st = cq_amd.stats()
             if os.environ.get("CQ_BENCH_DEBUG"):
                 print("stats", st, file=sys.stderr)
             kernel_used[0] = st.get("scan_kernel", 0)
-            return ng, st["scan_ms"]
+            return tp, st["scan_ms"]
         blob = C.c_void_p()
         n = L.cqgpu_query_partial(ast, (C.c_void_p * 1)(table.handle.value), 1, C.byref(blob))
         if n == 0:
@@ -164,21 +233,17 @@ def main():
         mine = C.string_at(blob, n)
         C.CDLL(None).free(blob)
         blobs = gather_blobs(mine, device=torch.device("cuda", local))
-        ng = 0
+        tp = None
         if rank == 0:
             tp = cq_amd.merge_partials(ast, blobs)
             if not tp:
                 raise RuntimeError(cq_amd.last_error())
-            ng = tp.contents.nrows
-            cq_amd.result_free(tp)
-        return ng, scan_ms
+        return tp, scan_ms
 
-    ng = None
     for _ in range(args.warmup):
-        ng, _ = step()
-    want_groups = 1000 if role else 1
-    if rank == 0 and ng is not None and ng != want_groups:
-        print(f"warning: {ng} groups (expected {want_groups})", file=sys.stderr)
+        tp, _ = step()
+        if tp:
+            cq_amd.result_free(tp)
 
     def barrier():
         if dist is not None:
@@ -186,11 +251,16 @@ def main():
         torch.cuda.synchronize()
 
     scan_ms = []
+    last = None
     barrier()
     t1 = time.perf_counter()
-    for _ in range(args.steps):
-        _, ms = step()
+    for i in range(args.steps):
+        tp, ms = step()
         scan_ms.append(ms)
+        if tp:
+            if last:
+                cq_amd.result_free(last)
+            last = tp
     barrier()
     elapsed = time.perf_counter() - t1
     if dist is not None:
@@ -198,20 +268,47 @@ def main():
         dist.all_reduce(t, op=dist.ReduceOp.MAX)
         elapsed = float(t.item())
     ms_per_step = elapsed * 1000.0 / args.steps
-    rows_total = args.rows * world
-    value = rows_total / (elapsed / args.steps)
+    value = total / (elapsed / args.steps)
 
+    rc = 0
     if rank == 0:
+        # ---- the last step's answer against the expected one (outside the timed region)
+        res = abi.table_to_py(last)
+        cq_amd.result_free(last)
+        exp, exp_src = expected_for(args.config, total, args.seed)
+        ok = verify(res, exp, args.config)
+        if not ok:
+            print("VERIFY FAILED: result differs from " + exp_src, file=sys.stderr)
+            print("got rows[:3]", res["rows"][:3], file=sys.stderr)
+            rc = 3
         avg_scan_ms = sum(scan_ms) / len(scan_ms)
         achieved = nbytes / (avg_scan_ms * 1e-3) / 1e9
         traffic = None
         try:
             with open(args.traffic) as fh:
                 tj = json.load(fh)
-            if tj.get("rows") == args.rows:
+            if tj.get("rows") == hi - lo:
                 traffic = tj.get("hbm_bytes_per_launch")
         except Exception:
             pass
+
+        # ---- end-to-end: evaluate_query on the file (mmap + H2D + scan + result), cold table cache
+        e2e = None
+        if world == 1 and not args.no_e2e:
+            try:
+                e2e = end_to_end(shard, args.config, L, cq_amd, exp, total)
+            except Exception as e:  # reported, never fatal
+                print(f"end-to-end timing failed: {e}", file=sys.stderr)
+        cfg2 = None
+        if data2 is not None:
+            table.close()
+            del shard
+            try:
+                cfg2 = config2_leg(args, cq_amd, abi, L, data2)
+                if cfg2 and not cfg2["verified"]:
+                    rc = 3
+            except Exception as e:
+                print(f"config 2 leg failed: {e}", file=sys.stderr)
         cpu = None
         if world == 1 and not args.no_cpu:
             try:
@@ -227,21 +324,26 @@ def main():
             "warmup": args.warmup,
             "ms_per_step": ms_per_step,
             "higher_is_better": True,
-            "scaling": "weak",
+            "scaling": "weak" if world == 1 else "strong",
             "vs_baseline": None,
             "dtype": "u8",
-            "data": ("synthetic: Shape A+role CSV (generate_big_dataset.py columns + role_%03d, "
-                     if role else "synthetic: Shape A CSV (generate_big_dataset.py columns, ")
-                    + f"seed {args.seed}), resident in HBM before timing",
+            "data": ("synthetic: logical Shape A+role CSV (generate_big_dataset.py columns + role_%03d, "
+                     if role else "synthetic: logical Shape A CSV (generate_big_dataset.py columns, ")
+                    + f"seed {args.seed}, cq_amd/datagen.py), resident in HBM before timing",
             "config": {
-                "workload": ("config3 per GPU: SELECT role, COUNT(*), SUM(height), AVG(height) "
-                             "FROM 'big.csv' WHERE age > 30 GROUP BY role" if role else
-                             "config2 per GPU: SELECT COUNT(*) FROM 'big.csv' WHERE age > 30"),
-                "rows_per_gpu": args.rows,
+                "workload": (("config3: " if world == 1 else "config4: ") +
+                             "SELECT role, COUNT(*), SUM(height), AVG(height) FROM 'big.csv' "
+                             "WHERE age > 30 GROUP BY role" if role else
+                             "config2: SELECT COUNT(*) FROM 'big.csv' WHERE age > 30"),
+                "rows_total": total,
+                "rows_per_gpu": hi - lo,
                 "bytes_per_gpu": nbytes,
-                "groups": want_groups,
-                "parallelism": f"dp{world} (newline-snapped row ranges, RCCL all_gather of partials)",
+                "groups": 1000 if role else 1,
+                "parallelism": (f"dp{world} (rows [r*T/N, (r+1)*T/N) per rank, RCCL all_gather of partials)"
+                                if world > 1 else "dp1"),
             },
+            "verified": ok,
+            "verified_against": exp_src,
             "roofline": {
                 "bound": "hbm",
                 "achieved": achieved,
@@ -249,20 +351,99 @@ def main():
                 "unit": "GB/s",
                 "frac": achieved / HBM_PEAK_GBS,
                 "traffic": traffic,
-                "kernel": (("cq::lean::lean_kernel<true, LW_NUM, 1> (+ slow_kernel, raw_merge_kernel)" if role
-                            else "cq::lean::lean_kernel<false, LW_NUM, 0> (+ slow_kernel)")
+                "kernel": (("cq::lean::lean_kernel<true, LW_NUM, 1, false> (+ slow_kernel, raw_merge_kernel)"
+                            if role else "cq::lean::lean_kernel<false, LW_NUM, 0, false> (+ slow_kernel)")
                            if kernel_used[0] else "cq::scan_kernel"),
                 "kernel_ms": avg_scan_ms,
                 "bytes_per_launch": nbytes,
             },
+            "end_to_end": e2e,
+            "config2": cfg2,
             "cpu_baseline": cpu,
-            "setup_s": gen_s,
+            "setup_s": {"generate": round(gen_s, 2), "upload": round(upload_s, 2)},
         }
         print(json.dumps(line), flush=True)
-    table.close()
+    else:
+        if last:
+            cq_amd.result_free(last)
+    if table.handle:
+        table.close()
     if dist is not None:
         dist.barrier()
         dist.destroy_process_group()
+    sys.exit(rc)
+
+
+def end_to_end(data, config, L, cq_amd, exp, rows):
+    """evaluate_query (the drop-in entry point) on the same bytes written as a file:
+    mmap + pinned H2D upload + scan + result, the device table cache cleared
+    before every call; median of 3."""
+    from cq_amd import abi
+    d = "/dev/shm" if os.path.isdir("/dev/shm") else tempfile.gettempdir()
+    fd, path = tempfile.mkstemp(suffix=".csv", dir=d)
+    try:
+        with os.fdopen(fd, "wb") as fh:
+            fh.write(data)
+        P, q = build_plan(path, config)
+        times = []
+        ok = True
+        for _ in range(3):
+            L.cqgpu_cache_clear()
+            torch.cuda.synchronize()
+            t0 = time.perf_counter()
+            tp = L.evaluate_query(C.pointer(q))
+            t = time.perf_counter() - t0
+            if not tp:
+                raise RuntimeError(cq_amd.last_error())
+            ok = ok and verify(abi.table_to_py(tp), exp, config)
+            cq_amd.result_free(tp)
+            times.append(t)
+        L.cqgpu_cache_clear()
+        times.sort()
+        t = times[1]
+        return {"seconds": t, "rows_per_s": rows / t, "file_bytes": len(data),
+                "GB_per_s": len(data) / t / 1e9, "verified": ok,
+                "includes": "evaluate_query on a page-cached file (%s): mmap, 64 MiB pinned H2D chunks, "
+                            "scan, result; table cache cleared before each call; median of 3" % d}
+    finally:
+        os.unlink(path)
+
+
+def config2_leg(args, cq_amd, abi, L, data):
+    """configs[1]: 1e8 rows of Shape A (no role), SELECT COUNT(*) ... WHERE age > 30"""
+    rows = 100_000_000
+    t = cq_amd.Table.from_bytes(data, abi.csv_config())
+    nb = len(data)
+    del data
+    P, q = build_plan("big.csv", 2)
+    ast = C.pointer(q)
+    arr = (C.c_void_p * 1)(t.handle.value)
+    for _ in range(args.warmup):
+        cq_amd.result_free(L.cqgpu_query(ast, arr, 1))
+    torch.cuda.synchronize()
+    ms = []
+    t0 = time.perf_counter()
+    last = None
+    for _ in range(args.steps):
+        tp = L.cqgpu_query(ast, arr, 1)
+        if not tp:
+            raise RuntimeError(cq_amd.last_error())
+        ms.append(cq_amd.stats()["scan_ms"])
+        if last:
+            cq_amd.result_free(last)
+        last = tp
+    torch.cuda.synchronize()
+    el = time.perf_counter() - t0
+    res = abi.table_to_py(last)
+    cq_amd.result_free(last)
+    t.close()
+    exp, src = expected_for(2, rows, args.seed)
+    kms = sum(ms) / len(ms)
+    return {"workload": "config2: SELECT COUNT(*) FROM 'big.csv' WHERE age > 30 (Shape A, 1e8 rows)",
+            "value": rows / (el / args.steps), "unit": "rows/s", "ms_per_step": el * 1000 / args.steps,
+            "kernel_ms": kms, "bytes_per_launch": nb,
+            "roofline_frac": nb / (kms * 1e-3) / 1e9 / HBM_PEAK_GBS,
+            "verified": verify(res, exp, 2), "verified_against": src}
 
 
 if __name__ == "__main__":

@@ -35,6 +35,7 @@ using namespace cq;
 
 extern "C" {
 uint32_t cq_lean_pick_ws(const uint8_t* data, uint64_t n);
+uint64_t cq_lean_long_cols(const uint8_t* data, uint64_t n, uint32_t delim);
 uint32_t cq_scan_cand_stride(const ScanPlan* P, int grouped);
 size_t cq_scan_lds_bytes(const ScanPlan* P, int grouped);
 int cq_scan_occupancy(const ScanPlan* P, int grouped);
@@ -142,7 +143,7 @@ cq_csv_config global_csv_config = {',', '"', true};
 
 namespace {
 
-constexpr uint64_t PAD_BEFORE = 64;
+constexpr uint64_t PAD_BEFORE = 256;   // byte 0 lands 256-aligned: lean_kernel windows are 128-byte aligned
 constexpr uint64_t PAD_AFTER = 32768 + 2048 + 256;   // >= WIN + MARGIN of the scan
 constexpr uint64_t NOPOS = ~0ULL;
 
@@ -372,6 +373,7 @@ struct cqgpu_table {
     uint64_t data_begin = 0;
     int device = 0;
     uint32_t lean_ws = 0;            // lean_kernel window stride for this file's record lengths
+    uint64_t long_cols = ~0ull;      // columns with sampled fields over 8 bytes (cq_lean_long_cols)
     unsigned long long* gids = nullptr;   // routed tables: global record id of each record (device)
     uint64_t ngids = 0;
     std::unique_ptr<RouteState> route;    // pending repartition (cqgpu_route_plan)
@@ -452,6 +454,8 @@ cqgpu_table* upload(const uint8_t* host, size_t n, cq_csv_config cfg, uint64_t b
         t->data_begin = cfg.has_header ? (uint64_t)(p - d) : 0;
     }
     t->lean_ws = cq_lean_pick_ws(host + t->data_begin, n - std::min<uint64_t>(n, t->data_begin));
+    t->long_cols = cq_lean_long_cols(host + t->data_begin, n - std::min<uint64_t>(n, t->data_begin),
+                                     (uint8_t)cfg.delimiter);
     size_t total = PAD_BEFORE + n + PAD_AFTER;
     HIPCHECK(hipMalloc(&t->dbuf, total));
     HIPCHECK(hipMemsetAsync(t->dbuf, '\n', PAD_BEFORE, c.stream));
@@ -842,6 +846,10 @@ void finish_plan(const cqgpu_table* t, Compiled& C, Compiler& cc) {
     C.P.range_begin = 0;
     C.P.range_end = t->n;
     C.P.lean_ws = t->lean_ws;
+    if (C.P.group_slot >= 0) {
+        const int gc = C.P.need_col[C.P.group_slot];
+        C.P.lean_k16 = (uint32_t)((t->long_cols >> (gc < 63 ? gc : 63)) & 1);
+    }
 }
 
 // compile the aggregate SELECT (evaluator.c:69-258 + build_aggregated_result)

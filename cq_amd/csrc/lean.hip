@@ -6,42 +6,52 @@
 // for plans whose WHERE is absent or `column op literal` and whose aggregates are
 // COUNT / SUM / AVG (at most 4 parsed columns, 2 distinct SUM arguments).
 //
-// Every wave works on its own windows with no block barrier in the loop, so one
-// wave's byte classification overlaps another's record work on the same SIMD.
-// The record work is arranged as a few batched LDS round trips (record start ->
-// bitmap view -> field bytes -> hash slot) with the arithmetic between them:
+// Every wave works on its own 4 KiB windows with no block barrier in the loop, so
+// one wave's byte classification overlaps another's record work on the same SIMD,
+// and every lane carries TWO records through the record pass (records l and
+// l + 64 of the pass): two independent dependency chains per lane for the LDS
+// round trips to overlap, and one set of wave-uniform tests, ballots and loop
+// control per two records.
 //
-//   load      a window stages 2 KiB, lane l bytes [32l, 32l + 32) (two 16-byte
-//             non-temporal loads, issued one window ahead): the 16 bytes before
-//             the window's own range (record-start context), its WS = 1952 owned
-//             bytes, and 80 bytes after them for the record views.  Windows start
-//             WS bytes apart and own the records that start in their range
-//   classify  per lane two 32-bit masks -- separators (delimiter and record
-//             terminators '\n' '\r') and terminators -- plus a quote mask when
-//             the window holds a quote; stored as the window's LDS bitmaps
-//   starts    record starts owned by the window (previous byte a terminator);
-//             one DPP wave scan numbers them, 64 per pass go to an LDS list
-//   fields    one lane per record: a funnel shift gives the 64 separator and
-//             terminator bits from the record start, field c ends at the c-th
-//             set separator bit.  A record whose needed fields are not all inside
+//   load      a window is 4 KiB of the file starting at a multiple of its stride
+//             (128-byte aligned), lane l bytes [64l, 64l + 64) by four 16-byte
+//             non-temporal loads issued one window ahead, plus the dword before
+//             the window (record-start context).  The window owns the records
+//             that start in its first `ws` bytes (ws <= WS = 3968); the last 128
+//             bytes are the record views' tail and are re-read by the next window
+//   classify  per lane two 64-bit masks -- separators (delimiter and record
+//             terminators '\n' '\r') and terminators -- plus quote presence; the
+//             masks go to LDS as the window's bitmaps (quote bitmap only when the
+//             window holds a quote)
+//   starts    record starts (previous byte a terminator) owned by the window; one
+//             DPP wave scan numbers them, 128 per pass go to an LDS list
+//   fields    per record: 64 separator and terminator bits from the record start
+//             (funnel shifts of three bitmap words); field c ends at the c-th set
+//             separator bit.  A record whose needed fields are not all inside
 //             those 64 bytes, or that has a quote in front of its last needed
 //             field, goes whole to the slow list and slow_kernel (scan.hip)
-//   values    WHERE / SUM fields of 1-7 bytes shaped `digits[.digits]` are typed
-//             in registers: M = the digits, k = digits after the dot, exactly
-//             parse_value's INTEGER M or DOUBLE strtod = RN(M / 10^k).  A WHERE
-//             against a numeric literal L compares INTEGER fields with integer
-//             thresholds ceil(L) / floor(L) and DOUBLE fields as RN(M / 10^k)
-//             against L (value_compare, csv_reader.c:98-130); a short STRING
-//             literal compares big-endian byte words (strcmp).  Any other field
-//             shape runs the exact field typers (scanlib.h) or goes slow
-//   group     the block's LDS open-addressing table is keyed by the RAW bytes of
-//             the GROUP BY field (<= 16 bytes): a raw key partitions the rows at
-//             least as finely as the reference's printf-canonical key.  Blocks
-//             flush (and a full LDS table spills) into an HBM table of raw keys;
-//             raw_merge_kernel then types every distinct raw key once with the
-//             general parser (parse_cell + group_key) and merges it into the
-//             canonical HBM table -- so "1.5" and "1.50" still meet there
-//   aggregate COUNT and SUM are fire-and-forget LDS atomics; the block flushes once
+//   values    WHERE / SUM fields of 1-4 bytes shaped `digits[.digits]` are typed
+//             in registers (right-aligned digit bytes, the dot squeezed out by one
+//             v_perm_b32, a v_dot4 for the value): M and k = digits after the dot,
+//             exactly parse_value's INTEGER M or DOUBLE strtod = RN(M / 10^k); 5-7
+//             byte numerals by an 8-byte variant, anything else by the exact field
+//             typers (scanlib.h) or the slow path.  A WHERE against a numeric
+//             literal L compares INTEGER fields with the integer thresholds
+//             ceil(L) / floor(L) and DOUBLE fields as RN(M / 10^k) against L
+//             (value_compare, csv_reader.c:98-130); a short STRING literal
+//             compares big-endian byte words (strcmp)
+//   group     the block's LDS table is keyed by the RAW bytes of the GROUP BY
+//             field (a raw key partitions rows at least as finely as the
+//             reference's printf-canonical key): buckets of 4 slots, every key
+//             has two candidate buckets (two-choice hashing keeps the fullest
+//             bucket near the mean), and a slot's tag IS the zero-padded key, so
+//             one round trip of four 16-byte LDS reads finds the key with no
+//             fingerprint or second key read.  New keys are claimed by a 64-bit
+//             LDS compare-and-swap of the tag.  COUNT / SUM / first-row are
+//             fire-and-forget LDS atomics.  Blocks flush (and keys that find no
+//             room spill) into an HBM table of raw keys; raw_merge_kernel types
+//             every distinct raw key once with the general parser and merges it
+//             into the canonical table -- so "1.5" and "1.50" still meet there
 //
 // SUM addends of DOUBLE fields are M * RN(10^-k) (within 2 ulp of the reference's
 // RN(M / 10^k); SUM / AVG parity is 1e-6 relative, north_star), INTEGER addends
@@ -55,20 +65,22 @@
 namespace cq {
 namespace lean {
 
-constexpr int LT = 1024;                  // threads per block
+#ifndef LEAN_WAVES
+#define LEAN_WAVES 12   // 3 waves per SIMD: 168 VGPRs, so the prefetched window never spills
+#endif
+constexpr int LT = 64 * LEAN_WAVES;       // threads per block
 constexpr int NWV = LT / 64;              // waves per block
-constexpr int LB = 32;                    // staged bytes per lane
-constexpr int WB = 64 * LB;               // staged window bytes (2 KiB)
-constexpr int HEAD = 16;                  // staged bytes before the owned range
-constexpr int WS = 1952;                  // largest window stride = owned bytes (LeanPlan.ws: the file's)
+constexpr int LB = 64;                    // staged bytes per lane
+constexpr int WB = 64 * LB;               // staged window bytes (4 KiB)
+constexpr int WS = 3968;                  // largest window stride = owned bytes (LeanPlan.ws: the file's)
 constexpr int NMW = WB / 32;              // 32-bit bitmap words per window
 constexpr int WBYTES = WB + 32;           // staged bytes + slack for 16-byte field loads
-constexpr int RSN = 64;                   // record slots per pass
+constexpr int RSN = 128;                  // record slots per pass: two per lane
 constexpr int MAXS = 2;                   // distinct SUM arguments
 constexpr int KN = 4;                     // need slots
 constexpr uint32_t NOFIRST = 0xFFFFFFFFu;
-static_assert(HEAD + WS + 64 + 16 <= WB, "a record view (64 bytes) plus a field load stays in the window");
-static_assert(WS % 16 == 0, "16-byte aligned window loads");
+static_assert(WS + 64 + 16 <= WB, "a record view (64 bytes) plus a field load stays in the window");
+static_assert(WS % 128 == 0, "128-byte aligned windows");
 
 // profiling build LEAN_CLK: shader cycles per phase, summed over waves into ScanStats.clk
 #ifdef LEAN_CLK
@@ -90,13 +102,13 @@ enum : int { LW_NONE = 0, LW_NUM = 1, LW_STR = 2, LW_GEN = 3 };
 // per-wave LDS area
 struct WaveLds {
     uint8_t bytes[WBYTES];
-    uint2 bm[NMW + 2];          // {separator bits, terminator bits} per 32 window bytes
+    uint2 bm[NMW];              // {separator bits, terminator bits} per 32 window bytes
     uint32_t qt[NMW + 4];       // quote bits (written only when the window holds a quote)
     uint16_t rs[RSN];           // record starts of the current pass (window offsets)
 };
 static_assert(sizeof(WaveLds) % 16 == 0, "16-byte aligned wave areas");
 
-// everything the kernel reads from constant memory
+// everything the kernel reads from its arguments
 struct LeanPlan {
     uint64_t lo_ok, hi_ok;       // records starting in [lo_ok, hi_ok) are owned by this launch
     uint64_t first_win, last_win;
@@ -115,7 +127,7 @@ struct LeanPlan {
     int32_t acc_sidx[MAX_ACC];   // accumulator -> SUM index
     uint32_t gcol;               // GROUP BY CSV column
     uint32_t delim, quote;
-    uint32_t ws;                 // window stride: multiple of 16, <= WS
+    uint32_t ws;                 // window stride: multiple of 128, <= WS
     uint32_t rcol[KN];           // the roles' CSV columns, ascending
     uint32_t rrole[KN];          // their roles: R_WHERE, R_SUM0, R_SUM1, R_GROUP
 };
@@ -124,8 +136,7 @@ enum : uint32_t { R_WHERE = 0, R_SUM0 = 1, R_SUM1 = 2, R_GROUP = 3 };
 // kernel arguments (kernarg segment).  The two HBM group tables (canonical keys,
 // shared with slow_kernel, and raw-byte keys for block flushes and LDS spills) are
 // read through a pointer to a device copy instead: only the rare spill path and
-// the final flush touch them, and their ~1 KB of pointers held in scalar
-// registers across the window loop spilled SGPRs into VGPR lanes.
+// the final flush touch them.
 struct LeanArgs {
     LeanPlan lp;
 };
@@ -139,29 +150,25 @@ __device__ __forceinline__ GKey raw_key(uint32_t len, uint64_t w0, uint64_t w1) 
     return k;
 }
 
-#ifndef LEAN_PF
-#define LEAN_PF 1          // windows in flight per wave (1 or 2; 2 measured 2.58 vs 2.52 ms on config 3)
-#endif
 struct Win {            // one window in flight
-    v4u a, b;           // staged bytes [32l, 32l + 32)
+    v4u a[4];           // staged bytes [64l, 64l + 64)
+    uint32_t prev;      // the dword before the window
 };
 
 __device__ __forceinline__ void load_win(const uint8_t* g, uint64_t w, uint32_t ws, Win& x) {
-    const v4u* src = (const v4u*)(g + w * ws - HEAD);   // g has 64 padding bytes before byte 0
+    const uint8_t* base = g + w * ws;                    // 128-byte aligned (g is 256-aligned, ws % 128 == 0)
+    const v4u* src = (const v4u*)base;
     const int lane = threadIdx.x & 63;
-    x.a = __builtin_nontemporal_load(src + 2 * lane);
-    x.b = __builtin_nontemporal_load(src + 2 * lane + 1);
+#pragma unroll
+    for (int i = 0; i < 4; i++) x.a[i] = __builtin_nontemporal_load(src + 4 * lane + i);
+    // the dword before the window (g has 256 bytes of '\n' before byte 0) by a buffer load: a
+    // uniform address would otherwise become a scalar load, whose lgkmcnt the LDS
+    // waits of the whole window would have to drain
+    const __amdgpu_buffer_rsrc_t r = __builtin_amdgcn_make_buffer_rsrc((void*)(base - 4), 0, 4, 0x00020000);
+    x.prev = __builtin_amdgcn_raw_buffer_load_b32(r, 0, 0, 0);
 }
 
-// 0x80 flags -> a nibble (bit i = byte i)
-__device__ __forceinline__ uint32_t nib(uint32_t f) {
-    uint32_t t = f >> 7;
-    t |= t >> 7;
-    t |= t >> 14;
-    return t & 0xFu;
-}
-
-// separator / terminator / quote bits of 32 bytes (bit i = byte i).
+// separator / terminator bits of 32 bytes (bit i = byte i) and quote flags.
 //
 // Byte classes by v_perm_b32 lookups: a selector byte 0-7 picks a table byte,
 // 8-11 the sign of table byte 1/3/5/7, 12 gives 0x00 and 13-255 give 0xFF.  With
@@ -176,9 +183,9 @@ __device__ __forceinline__ uint32_t nib(uint32_t f) {
 __device__ __forceinline__ uint32_t flags40(uint32_t r) {
     return r & ~(r >> 1) & 0x40404040u;
 }
-__device__ __forceinline__ void classify(const v4u a, const v4u b, uint32_t rep_d, uint32_t rep_q, uint32_t& sep,
-                                         uint32_t& nl, uint32_t& qf) {
-    uint32_t us[4], un[4], q = 0;
+__device__ __forceinline__ void classify32(const v4u a, const v4u b, uint32_t rep_d, uint32_t rep_q, uint32_t& sep,
+                                           uint32_t& nl, uint32_t& q) {
+    uint32_t us[4], un[4];
 #pragma unroll
     for (int j = 0; j < 8; j++) {
         const uint32_t x = j < 4 ? a[j & 3] : b[j & 3];
@@ -199,7 +206,13 @@ __device__ __forceinline__ void classify(const v4u a, const v4u b, uint32_t rep_
     // us[p] = 0x40 * (bits of bytes 8p .. 8p + 7)
     sep = (us[0] >> 6) | (us[1] << 2) | (us[2] << 10) | (us[3] << 18);
     nl = (un[0] >> 6) | (un[1] << 2) | (un[2] << 10) | (un[3] << 18);
-    qf = q & 0x80808080u;
+}
+// 0x80 flags -> a nibble (bit i = byte i)
+__device__ __forceinline__ uint32_t nib(uint32_t f) {
+    uint32_t t = f >> 7;
+    t |= t >> 7;
+    t |= t >> 14;
+    return t & 0xFu;
 }
 __device__ __forceinline__ uint32_t byte_bits(const v4u a, const v4u b, uint32_t rep) {
     uint32_t m = 0;
@@ -238,10 +251,10 @@ __device__ __forceinline__ uint64_t qview(const WaveLds& W, uint32_t p) {
 }
 
 // 4 bytes of the tile at byte offset o (any alignment)
-__device__ __forceinline__ void load4(const uint8_t* tile, uint32_t o, uint32_t& e0) {
+__device__ __forceinline__ uint32_t load4(const uint8_t* tile, uint32_t o) {
     const uint32_t* t32 = (const uint32_t*)tile;
     const uint32_t a = o >> 2, sh = o & 3;
-    e0 = __builtin_amdgcn_alignbyte(t32[a + 1], t32[a], sh);
+    return __builtin_amdgcn_alignbyte(t32[a + 1], t32[a], sh);
 }
 
 // bytes [0, len) of two dwords (len <= 8)
@@ -254,14 +267,43 @@ __device__ __forceinline__ void mask8(uint32_t len, uint32_t& d0, uint32_t& d1) 
 // 0x80 in every byte < 0x21 (blank, control, NUL) among the bytes of f-flags
 __device__ __forceinline__ uint32_t low_bytes(uint32_t d, uint32_t f) { return lt_bytes(d, 0x21212121u) & f; }
 
-// A field of 1..7 bytes shaped [digits][.][digits] with at least one digit (no sign,
-// so never date-shaped: parse_date needs 8-10 bytes): infer_type gives INTEGER
-// (no dot) or DOUBLE, parse_value M or strtod = RN(M / 10^k).  d0/d1: the field's
-// first 8 bytes, unmasked.  Branch-free; M, k and dot are meaningful when ok.
+// A numeral field shaped [digits][.][digits] with at least one digit (no sign, at
+// most 7 bytes, so never date-shaped: parse_date needs 8-10 bytes): infer_type
+// gives INTEGER (no dot) or DOUBLE, parse_value M or strtod = RN(M / 10^k).
+// M, k and dot are meaningful when ok.
 struct Num {
     uint32_t M, k;
     bool ok, dot;
 };
+
+// Fields of 1..4 bytes, d = the field's first 4 bytes (unmasked).  The field is
+// right-aligned in the dword with its digits as byte values (bytes before it 0,
+// i.e. leading zeros); with DOT a '.' is squeezed out by one v_perm_b32 whose
+// selector keeps the bytes behind the dot and moves the ones before it up a byte.
+// Then every byte must be a digit value, and M is one v_dot4 (weights 100/10/1)
+// plus the top byte * 1000.  Without DOT a field holding a '.' is simply not ok.
+template <bool DOT>
+__device__ __forceinline__ Num num4(uint32_t d, uint32_t len) {
+    Num r;
+    const uint32_t sh = 32u - 8u * len;                                 // len 1..4 (others: ok false)
+    uint32_t v = (d ^ 0x30303030u) << (sh & 31);
+    r.dot = false;
+    r.k = 0;
+    if (DOT) {
+        const uint32_t fd = ~nonzero_bytes(v ^ 0x1E1E1E1Eu) & 0x80808080u & (0xFFFFFFFFu << (sh & 31));   // '.' ^ '0'
+        const uint32_t low = fd & (0u - fd);                            // the first dot, byte index pd
+        const uint32_t below = ((low << 1) - (low != 0 ? 1u : 0u)) & 0x01010100u;   // bytes 1..pd (none: 0)
+        v = __builtin_amdgcn_perm(0u, v, (low ? 0x0302010Cu : 0x03020100u) - below);   // bytes <= pd up one, byte 0 := 0
+        r.dot = low != 0;
+        r.k = r.dot ? (uint32_t)__builtin_clz(low) >> 3 : 0u;           // 3 - pd = digits after the dot
+    }
+    const bool digits = lt_bytes(v, 0x0A0A0A0Au) == 0x80808080u;
+    r.ok = (len - 1u <= 3u) & digits & (!DOT | (len > 1u) | !r.dot);
+    r.M = __builtin_amdgcn_udot4(v, 0x010A6400u, __umul24(v & 0xFFu, 1000u), false);
+    return r;
+}
+
+// Fields of 1..7 bytes (d0/d1: the field's first 8 bytes, unmasked).
 __device__ __forceinline__ Num num7(uint32_t d0, uint32_t d1, uint32_t len) {
     Num r;
     const uint32_t f0 = len_mask(len, 0) & 0x80808080u, f1 = len_mask(len, 1) & 0x80808080u;
@@ -291,54 +333,6 @@ __device__ __forceinline__ Num num7(uint32_t d0, uint32_t d1, uint32_t len) {
     return r;
 }
 
-// num7 for fields of 1..4 bytes (one dword): the same M, k, dot and ok for every
-// field num7 accepts with len <= 4; ok is false for longer fields.  The kernel
-// takes it when every lane's field of the role fits (a wave-uniform choice).
-__device__ __forceinline__ Num num4(uint32_t d0, uint32_t len) {
-    Num r;
-    const uint32_t f = len_mask(len, 0) & 0x80808080u;
-    const uint32_t x = d0 ^ 0x30303030u;
-    const uint32_t g = lt_bytes(x, 0x0A0A0A0Au) & f;                   // digits
-    const uint32_t t = ~nonzero_bytes(d0 ^ 0x2E2E2E2Eu) & f;            // dots
-    const uint32_t ndot = (uint32_t)__popc(t);
-    r.ok = (len - 1 <= 3u) & ((g | t) == f) & (ndot <= 1) & (g != 0);
-    uint32_t v = x & spread(g);                                         // digit values, dot -> 0
-    uint32_t pd = (uint32_t)__builtin_ctz(t | 0x80000000u) >> 3;        // dot byte (3 when none or last)
-    r.dot = ndot != 0;
-    const uint32_t lo = (1u << (8 * pd)) - 1;
-    v = r.dot ? ((v & lo) | ((v >> 8) & ~lo)) : v;
-    r.k = r.dot ? len - 1 - pd : 0u;
-    r.k = r.k > 3 ? 3u : r.k;
-    uint32_t nd = len - ndot;                                           // digits
-    nd = nd - 1 > 3u ? 1u : nd;
-    v <<= 8 * (4 - nd);                                                 // right-align the digits
-    r.M = __builtin_amdgcn_udot4(v, 0x010A6400u, __umul24(v & 0xFFu, 1000u), false);
-    return r;
-}
-
-// Field `c` of the record at window offset p from its 64-bit separator view sv
-// (delimiters and terminators, bit i = byte p + i) and its end e (the first
-// terminator; 64: beyond the view).  Clearing the c lowest separator bits leaves
-// the field's end as the lowest bit; the cleared bits' highest is its start - 1.
-// A column past the record's end is missing (length 0: NULL); a field the view
-// cannot bound fails the fast path.  The roles' columns come in ascending order,
-// so s and `done` carry the cleared bits from one role to the next (the clears
-// of a record total its largest column, not the sum of the columns).  c is
-// uniform: a scalar loop.
-__device__ __forceinline__ void field_next(uint64_t sv, uint64_t& s, uint32_t& done, uint32_t e, uint32_t c,
-                                           uint32_t p, uint32_t& fp, uint32_t& fl, bool& fail, uint32_t& last) {
-    for (; done < c; done++) s &= s - 1;
-    const uint64_t cl = sv ^ s;
-    const uint32_t start = cl ? 64u - (uint32_t)__builtin_clzll(cl) : 0u;
-    const uint32_t end = ctz64(s);
-    const bool gone = start > e;
-    fail |= gone ? (e == 64) : (end == 64);
-    fp = p + start;
-    fl = gone ? 0u : end - start;
-    const uint32_t l = gone ? e : end;
-    last = l > last ? l : last;
-}
-
 // value_compare outcome through a truth table: bit 0 for <, bit 1 for ==, bit 2 for >
 __device__ __forceinline__ bool tt_result(uint32_t tt, int c) { return (tt >> (c < 0 ? 0 : (c == 0 ? 1 : 2))) & 1; }
 
@@ -353,6 +347,9 @@ __device__ __forceinline__ double inv10(uint32_t k) {
 // exact typing of a field (infer_type + parse_value); false: only the general
 // parser can tell (dates, signs, long numerals, blanks ...)
 __device__ __forceinline__ bool type_field(const uint8_t* bytes, uint32_t o, uint32_t len, Cell& c) {
+#ifdef LEAN_NOGEN
+    return false;
+#endif
     if (len == 0) { c = cell_null(); return true; }
     uint64_t kw;
     if (lean_field(bytes, o, len, true, c, kw)) return true;
@@ -364,107 +361,117 @@ __device__ __forceinline__ uint64_t bswap64(uint32_t d0, uint32_t d1) {
     return ((uint64_t)__builtin_bswap32(d0) << 32) | __builtin_bswap32(d1);
 }
 
-// LDS group table (structure of arrays carved from dynamic LDS), raw-byte keys.
-// Slots are grouped in buckets of BS = 16; a key's home bucket is its hash's top
-// bits, and a bucket's 16 u16 fingerprints (0: free, FP_BUSY: being written) are
-// read with two 16-byte loads.  A lookup is two batched round trips:
-// fingerprints, then the first matching slot's key.  Keys missing from their
-// home bucket's first match (new keys, bucket overflow, fingerprint collisions)
-// take lt_slow: lock-free linear probing over the slots from the home bucket.
-constexpr uint32_t BS = 16;
-constexpr uint32_t FP_BUSY = 0xFFFEu;   // fingerprints are odd
+// ------------------------------------------------------------------ LDS group table
+//
+// Structure of arrays carved from dynamic LDS at compile-time offsets.  Slots come
+// in buckets of BSLOTS = 4; a key may live in either of two buckets (hash bits
+// [0, 16) and [16, 32)).  The tag of a slot is the key itself:
+//   K8  (keys of <= 8 bytes): one u64, the zero-padded key bytes.  Key bytes are
+//       > ' ' (keys with lower bytes take the slow path), so a key's first byte
+//       is nonzero and the zero padding encodes its length; the empty key (NULL
+//       field) is tag 1 << 32 and a free slot is tag 0.
+//   K16 (keys of <= 16 bytes): four u32, words 0-1 as for K8, words 2-3 the key
+//       bytes 8-15.  A free slot is claimed by a CAS of words 0-1 to CLAIM,
+//       words 2-3 written, then words 0-1 published.
+// A key is inserted into the first free slot of the less occupied bucket by CAS;
+// two inserters of one key that race into different buckets leave a duplicate,
+// which is harmless: lookups take either slot and the flush merges by key.
+constexpr uint32_t BSLOTS = 4;
+constexpr uint32_t CLAIM = 0xFFFFFFFFu;       // K16 tag word 1 of a slot being written
 
-// LDS bytes per table slot (fingerprint, key, count, SUM/miss per argument) and
-// the slots of a plan shape: a compile-time constant of each kernel instance, so
-// every table array sits at an immediate LDS offset
-constexpr uint32_t slot_bytes(int ns) { return 2 + 16 + 8 + 4 + (uint32_t)ns * 12; }
+template <bool K16>
+constexpr uint32_t slot_bytes(int ns) { return (K16 ? 16u : 8u) + 4u + 4u + (uint32_t)ns * 12u; }
 constexpr uint32_t fixed_bytes() { return (uint32_t)(sizeof(WaveLds) * NWV); }
+constexpr uint32_t LDS_MAX = 160u * 1024u - 256u;
+template <bool K16>
 constexpr uint32_t slots_for(int ns, bool grouped) {
     if (!grouped) return 0;
-    uint32_t h = 2048;
-    while (h > 64 && fixed_bytes() + h * slot_bytes(ns) + 512 > 160u * 1024u) h >>= 1;
+    uint32_t h = 4096;
+    while (h > 64 && fixed_bytes() + h * slot_bytes<K16>(ns) > LDS_MAX) h >>= 1;
     return h;
 }
+
 struct LTab {
-    uint32_t H;           // slots (multiple of BS)
-    uint32_t NB;          // buckets
-    v4u* F;               // fingerprints: bucket b = F[2b], F[2b + 1]
-    v4u* A;               // {0x80000000 | len, first-row code, key bytes 0-3, key bytes 4-7}
-    uint2* B;             // key bytes 8-15
+    uint8_t* T;           // tags: H * (8 | 16) bytes
     uint32_t* cnt;
+    uint32_t* first;      // smallest first-row code of the slot's passing records
     double* sum[MAXS];
     uint32_t* miss[MAXS]; // SUM arguments that were not numeric
 };
 
-__device__ __forceinline__ uint32_t key_hash(uint32_t len, uint32_t k0, uint32_t k1, uint32_t k2, uint32_t k3) {
-    uint32_t x = k0 ^ rotl(k1, 7) ^ rotl(k2, 13) ^ rotl(k3, 21) ^ (len << 27);
-    x *= 0x9E3779B1u;
-    x ^= x >> 15;
-    x *= 0x85EBCA6Bu;
-    return x ^ (x >> 13);
+__device__ __forceinline__ uint32_t key_hash(uint32_t k0, uint32_t k1, uint32_t k2, uint32_t k3) {
+    uint32_t x = k0 ^ rotl(k1, 11) ^ rotl(k2, 19) ^ rotl(k3, 5);
+    x ^= x >> 16;
+    x = __umul24(x, 0x2F0B3Du) ^ (x >> 7);
+    x ^= x >> 13;
+    return __umul24(x, 0x3C6EF3u) ^ (x >> 11) ^ (x << 16);
 }
-__device__ __forceinline__ uint32_t fp_of(uint32_t h) { return (h & 0xFFFFu) | 1u; }
-__device__ __forceinline__ uint32_t bucket_of(uint32_t h, uint32_t nb) { return __umulhi(h, nb); }
 
-// index of the first of the 16 u16 fingerprints equal to fp (16: none).  Per
-// dword the borrow-based zero-half test (its lowest flag is exact) leaves flags at
-// bits 15 and 31; one v_dot4_u32_u8 per dword weighs them 4^j * {1, 2} into a
-// chained 8-bit mask (times 0x80) per four dwords.
-__device__ __forceinline__ uint32_t fp_first(const v4u q0, const v4u q1, uint32_t fp) {
-    const uint32_t rep = fp * 0x00010001u;
-    uint32_t m0 = 0, m1 = 0;
+// look the key up in its two buckets: the slot, or -1
+template <bool K16>
+__device__ __forceinline__ int lt_find(const LTab& t, uint32_t nb, uint32_t h, uint32_t k0, uint32_t k1, uint32_t k2,
+                                       uint32_t k3) {
+    const uint32_t b1 = h & (nb - 1), b2 = (h >> 16) & (nb - 1);
+    int s = -1;
+    if (!K16) {
+        const v4u* T4 = (const v4u*)t.T;                 // two tags per v4u
+        const v4u a0 = T4[2 * b1], a1 = T4[2 * b1 + 1], c0 = T4[2 * b2], c1 = T4[2 * b2 + 1];
+        const uint64_t k = (uint64_t)k0 | ((uint64_t)k1 << 32);
+#define LT_TRY8(V, HALF, SLOT) \
+        s = (((uint64_t)(HALF ? V.z : V.x) | ((uint64_t)(HALF ? V.w : V.y) << 32)) == k) ? (int)(SLOT) : s;
+        LT_TRY8(c1, 1, 4 * b2 + 3) LT_TRY8(c1, 0, 4 * b2 + 2) LT_TRY8(c0, 1, 4 * b2 + 1) LT_TRY8(c0, 0, 4 * b2)
+        LT_TRY8(a1, 1, 4 * b1 + 3) LT_TRY8(a1, 0, 4 * b1 + 2) LT_TRY8(a0, 1, 4 * b1 + 1) LT_TRY8(a0, 0, 4 * b1)
+#undef LT_TRY8
+    } else {
+        const v4u* T4 = (const v4u*)t.T;                 // one tag per v4u
+        v4u x[8];
 #pragma unroll
-    for (int j = 0; j < 4; j++) {
-        const uint32_t x0 = q0[j] ^ rep, x1 = q1[j] ^ rep;
-        const uint32_t f0 = (x0 - 0x00010001u) & ~x0 & 0x80008000u;
-        const uint32_t f1 = (x1 - 0x00010001u) & ~x1 & 0x80008000u;
-        const uint32_t w = (1u << (2 * j + 8)) | (2u << (2 * j + 24));     // bytes 1 and 3
-        m0 = __builtin_amdgcn_udot4(f0, w, m0, false);
-        m1 = __builtin_amdgcn_udot4(f1, w, m1, false);
+        for (int i = 0; i < 4; i++) { x[i] = T4[4 * b1 + i]; x[4 + i] = T4[4 * b2 + i]; }
+#pragma unroll
+        for (int i = 7; i >= 0; i--) {
+            const bool m = (x[i].x == k0) & (x[i].y == k1) & (x[i].z == k2) & (x[i].w == k3);
+            s = m ? (int)((i < 4 ? 4 * b1 : 4 * b2 - 4) + i) : s;
+        }
     }
-    return (uint32_t)__builtin_ctz((m0 >> 7) | (m1 << 1) | 0x10000u);
+    return s;
 }
 
-// Find the key or insert it: linear probing over slots from the home bucket.  A
-// free fingerprint is claimed FP_BUSY by CAS on its dword, the key written, then
-// the fingerprint published; every inserter of a key probes the same sequence,
-// so two of them meet at the same first free slot and the loser finds the
-// winner's key.  -1: the table is full or a claim never resolved (the HBM raw
-// table takes the record).
-__device__ __forceinline__ int lt_slow(const LTab& t, uint32_t len, uint32_t k0, uint32_t k1, uint32_t k2,
-                                       uint32_t k3, uint32_t h, uint32_t& first) {
-    const uint32_t hd = 0x80000000u | len, fp = fp_of(h);
-    uint32_t slot = bucket_of(h, t.NB) * BS;
-    uint32_t* f32 = (uint32_t*)t.F;
-    uint32_t n = 0;
-    for (uint32_t it = 0; it < 4 * t.H + 4096; it++) {
-        const uint32_t sh = 16 * (slot & 1);
-        const uint32_t d = __hip_atomic_load(f32 + (slot >> 1), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
-        const uint32_t x = (d >> sh) & 0xFFFFu;
-        if (x == 0) {
-            const uint32_t old = atomicCAS(f32 + (slot >> 1), d, d | (FP_BUSY << sh));
-            if (old == d) {                                 // claimed: write the key, publish
-                t.A[slot] = v4u{hd, NOFIRST, k0, k1};
-                t.B[slot] = make_uint2(k2, k3);
+// find or insert (lanes that missed in lt_find); -1: both buckets full (the
+// record spills to the HBM raw table)
+template <bool K16>
+__device__ int lt_insert(const LTab& t, uint32_t nb, uint32_t h, uint32_t k0, uint32_t k1, uint32_t k2, uint32_t k3) {
+    const uint32_t b1 = h & (nb - 1), b2 = (h >> 16) & (nb - 1);
+    for (int attempt = 0; attempt < 64; attempt++) {
+        const int s = lt_find<K16>(t, nb, h, k0, k1, k2, k3);
+        if (s >= 0) return s;
+        // occupancy of the two buckets (slots fill in order)
+        uint32_t n1 = 0, n2 = 0;
+        const uint32_t stride = K16 ? 16u : 8u;
+        for (uint32_t i = 0; i < BSLOTS; i++) {
+            const uint32_t* a = (const uint32_t*)(t.T + (4 * b1 + i) * stride);
+            const uint32_t* c = (const uint32_t*)(t.T + (4 * b2 + i) * stride);
+            n1 += (__hip_atomic_load(a, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP) |
+                   __hip_atomic_load(a + 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP)) != 0;
+            n2 += (__hip_atomic_load(c, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP) |
+                   __hip_atomic_load(c + 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP)) != 0;
+        }
+        if (n1 >= BSLOTS && n2 >= BSLOTS) return -1;
+        const uint32_t slot = (n1 <= n2 || n2 >= BSLOTS) && n1 < BSLOTS ? 4 * b1 + n1 : 4 * b2 + n2;
+        unsigned long long* w01 = (unsigned long long*)(t.T + slot * stride);
+        const unsigned long long key01 = (unsigned long long)k0 | ((unsigned long long)k1 << 32);
+        if (!K16) {
+            if (atomicCAS(w01, 0ull, key01) == 0ull) return (int)slot;
+        } else {
+            if (atomicCAS(w01, 0ull, (unsigned long long)CLAIM << 32) == 0ull) {
+                uint32_t* w = (uint32_t*)w01;
+                w[2] = k2;
+                w[3] = k3;
                 __builtin_amdgcn_fence(__ATOMIC_RELEASE, "workgroup");
-                atomicXor(f32 + (slot >> 1), (FP_BUSY ^ fp) << sh);
-                first = NOFIRST;
-                return (int)slot;
-            }
-            continue;                                       // the dword changed: look again
-        }
-        if (x == FP_BUSY) continue;                         // being written: look again
-        if (x == fp) {
-            __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "workgroup");
-            const v4u a = t.A[slot];
-            const uint2 b = t.B[slot];
-            if (a.x == hd && a.z == k0 && a.w == k1 && b.x == k2 && b.y == k3) {
-                first = a.y;
+                atomicExch(w01, key01);
                 return (int)slot;
             }
         }
-        if (++n == t.H) return -1;
-        slot = slot + 1 == t.H ? 0 : slot + 1;
+        // lost the slot to another inserter: look again
     }
     return -1;
 }
@@ -485,11 +492,94 @@ __device__ __forceinline__ uint8_t* carve(uint8_t*& q, size_t bytes) {
     return r;
 }
 
-// GROUPED: GROUP BY (else one group); WM: LW_*; NS: distinct SUM arguments (0-2)
-template <bool GROUPED, int WM, int NS>
+// a raw key's length from its zero-padded words (key bytes are nonzero)
+__device__ __forceinline__ uint32_t key_len(uint64_t w0, uint64_t w1) {
+    if (w1) return 16u - ((uint32_t)__builtin_clzll(w1) >> 3);
+    if (w0 == (1ull << 32)) return 0u;                  // the empty key's tag
+    return w0 ? 8u - ((uint32_t)__builtin_clzll(w0) >> 3) : 0u;
+}
+
+// a record whose key found no LDS slot (a key longer than the tag, both buckets
+// full): aggregated straight into the HBM raw table; keys over 16 bytes or with
+// low bytes past byte 8 go to the slow list
+__device__ __forceinline__ void spill_record(const uint8_t* bytes, uint32_t gfp, uint32_t kl, uint64_t off,
+                                          const GroupTable* tabs, ScanStats* stats, unsigned long long* slow_list,
+                                          unsigned long long slow_cap, int nacc, const int32_t* acc_sidx, bool n0,
+                                          double v0, bool n1, double v1) {
+    const GroupTable& rt = tabs[TAB_RT];
+    uint32_t a0, a1, a2, a3;
+    load16(bytes, gfp, a0, a1, a2, a3);
+    const uint32_t m0 = len_mask(kl, 0), m1 = len_mask(kl, 1), m2 = len_mask(kl, 2), m3 = len_mask(kl, 3);
+    a0 &= m0; a1 &= m1; a2 &= m2; a3 &= m3;
+    const bool fits = kl <= 16 && (low_bytes(a2, m2 & 0x80808080u) | low_bytes(a3, m3 & 0x80808080u)) == 0;
+    if (!fits) {
+        const unsigned long long i = atomicAdd(&stats->slow_records, 1ull);
+        if (i < slow_cap) slow_list[i] = off;
+        return;
+    }
+    const GKey kk = raw_key(kl, (uint64_t)a0 | ((uint64_t)a1 << 32), (uint64_t)a2 | ((uint64_t)a3 << 32));
+    const int gi = g_insert(rt, kk, gk_hash(kk), stats);
+    if (gi < 0) return;
+    atomicAdd(&rt.cnt[gi], 1ULL);
+    atomicMin(&rt.first[gi], (unsigned long long)off);
+    for (int a = 0; a < nacc; a++) {
+        const bool nm = acc_sidx[a] == 0 ? n0 : n1;
+        if (nm) {
+            atomicAdd(&rt.sum[a][gi], acc_sidx[a] == 0 ? v0 : v1);
+            atomicAdd(&rt.num[a][gi], 1ULL);
+        }
+    }
+}
+
+// one record's role fields
+struct Rec {
+    uint32_t p;                 // window offset of the record start
+    bool valid, fail;
+    uint32_t wfp, wfl, gfp, klen, lastpos;
+    uint32_t sfp[MAXS], sfl[MAXS];
+};
+
+// Field walk of one record from its 64-bit separator view sv and record end e
+// (first terminator bit; 64: beyond the view): the roles' columns come in
+// ascending order, and clearing separator bits one by one visits the field ends
+// in order: before field c's end is cleared, the lowest remaining bit is that
+// end, and the previous one (field c - 1's end) is its start - 1.  A column past
+// the record's end is missing (length 0: NULL); a field the view cannot bound
+// fails the fast path.  The columns are uniform: the clearing loop is scalar.
+template <int NR, int WM, int NS, bool GROUPED>
+__device__ __forceinline__ void walk(Rec& R, uint64_t sv, uint64_t nv, const uint32_t (&rcol)[KN],
+                                     const uint32_t (&rrole)[KN]) {
+    const uint32_t e = ctz64(nv);
+    uint64_t s = sv;
+    uint32_t done = 0, prev_end = 0xFFFFFFFFu;        // position of separator done - 1 (start - 1 of field done)
+#pragma unroll
+    for (int k = 0; k < NR; k++) {
+        const uint32_t c = rcol[k];
+        for (; done < c; done++) {
+            prev_end = ctz64(s);
+            s &= s - 1;
+        }
+        const uint32_t start = prev_end + 1;           // 0 for column 0
+        const uint32_t end = ctz64(s);
+        const bool gone = start > e;
+        R.fail |= gone ? (e == 64) : (end == 64);
+        const uint32_t fp = R.p + start, fl = gone ? 0u : end - start;
+        const uint32_t l = gone ? e : end;
+        R.lastpos = l > R.lastpos ? l : R.lastpos;
+        const uint32_t role = rrole[k];
+        if (WM != LW_NONE && role == R_WHERE) { R.wfp = fp; R.wfl = fl; }
+        if (NS > 0 && role == R_SUM0) { R.sfp[0] = fp; R.sfl[0] = fl; }
+        if (NS > 1 && role == R_SUM1) { R.sfp[MAXS - 1] = fp; R.sfl[MAXS - 1] = fl; }
+        if (GROUPED && role == R_GROUP) { R.gfp = fp; R.klen = fl; }
+    }
+}
+
+// GROUPED: GROUP BY (else one group); WM: LW_*; NS: distinct SUM arguments (0-2);
+// K16: LDS tags of 16 key bytes (else 8)
+template <bool GROUPED, int WM, int NS, bool K16>
 __global__ __launch_bounds__(LT) void lean_kernel(const uint8_t* __restrict__ g, ScanStats* __restrict__ stats,
                                                   unsigned long long* __restrict__ row_out,
-                                                  unsigned long long row_cap, uint32_t lds_h_unused,
+                                                  unsigned long long row_cap,
                                                   unsigned long long* __restrict__ slow_list,
                                                   unsigned long long slow_cap, const LeanArgs args,
                                                   const GroupTable* __restrict__ tabs) {
@@ -500,32 +590,29 @@ __global__ __launch_bounds__(LT) void lean_kernel(const uint8_t* __restrict__ g,
     const int tid = threadIdx.x, lane = tid & 63;
     const int wv = __builtin_amdgcn_readfirstlane(tid >> 6);   // wave-uniform: the window loop is scalar
     WaveLds& W = waves[wv];
-    constexpr uint32_t lds_h = slots_for(NS, GROUPED);
+    constexpr uint32_t H = slots_for<K16>(NS, GROUPED);
+    constexpr uint32_t NB = H / BSLOTS;
+    constexpr uint32_t TSTRIDE = K16 ? 16u : 8u;
     LTab lt;
-    lt.H = lds_h;
-    lt.NB = 0; lt.F = nullptr;
-    lt.A = nullptr; lt.B = nullptr; lt.cnt = nullptr;
+    lt.T = nullptr; lt.cnt = nullptr; lt.first = nullptr;
 #pragma unroll
     for (int s = 0; s < MAXS; s++) { lt.sum[s] = nullptr; lt.miss[s] = nullptr; }
     if (GROUPED) {
-        lt.NB = lds_h / BS;
-        lt.F = (v4u*)carve(q, (size_t)lds_h * 2);
-        lt.A = (v4u*)carve(q, (size_t)lds_h * 16);
-        lt.B = (uint2*)carve(q, (size_t)lds_h * 8);
-        lt.cnt = (uint32_t*)carve(q, (size_t)lds_h * 4);
+        lt.T = carve(q, (size_t)H * TSTRIDE);
+        lt.cnt = (uint32_t*)carve(q, (size_t)H * 4);
+        lt.first = (uint32_t*)carve(q, (size_t)H * 4);
 #pragma unroll
         for (int s = 0; s < NS; s++) {
-            lt.sum[s] = (double*)carve(q, (size_t)lds_h * 8);
-            lt.miss[s] = (uint32_t*)carve(q, (size_t)lds_h * 4);
+            lt.sum[s] = (double*)carve(q, (size_t)H * 8);
+            lt.miss[s] = (uint32_t*)carve(q, (size_t)H * 4);
         }
-        for (uint32_t i = tid; i < lds_h; i += LT) {
-            lt.A[i] = v4u{0u, NOFIRST, 0u, 0u};
-            lt.B[i] = make_uint2(0u, 0u);
+        for (uint32_t i = tid; i < H * TSTRIDE / 16; i += LT) ((v4u*)lt.T)[i] = v4u{0u, 0u, 0u, 0u};
+        for (uint32_t i = tid; i < H; i += LT) {
             lt.cnt[i] = 0;
+            lt.first[i] = NOFIRST;
 #pragma unroll
             for (int s = 0; s < NS; s++) { lt.sum[s][i] = 0.0; lt.miss[s][i] = 0; }
         }
-        for (uint32_t i = tid; i < lt.NB * 2; i += LT) lt.F[i] = v4u{0u, 0u, 0u, 0u};
         __syncthreads();
     }
 
@@ -560,18 +647,9 @@ __global__ __launch_bounds__(LT) void lean_kernel(const uint8_t* __restrict__ g,
     uint64_t clk_[8] = {0, 0, 0, 0, 0, 0, 0, 0};
     uint64_t clk_last_ = __builtin_amdgcn_s_memtime();
 #endif
-    // LEAN_PF windows in flight per wave (the one being processed + LEAN_PF - 1
-    // prefetched): 4 waves per SIMD with one 2 KiB window each leave too few bytes
-    // in flight to cover HBM latency at full bandwidth (Little's law)
     Win nx;
-#if LEAN_PF >= 2
-    Win nx2;
-#endif
     uint64_t w = LP.first_win + (uint64_t)blockIdx.x * NWV + wv;
     if (w < last_win) load_win(g, w, wstr_b, nx);
-#if LEAN_PF >= 2
-    if (w + wstep < last_win) load_win(g, w + wstep, wstr_b, nx2);
-#endif
     for (uint32_t round = 0; w < last_win; round++, w += wstep) {
         const uint64_t ws = w * wstr_b;
 #ifdef LEAN_CLK
@@ -580,44 +658,43 @@ __global__ __launch_bounds__(LT) void lean_kernel(const uint8_t* __restrict__ g,
         const Win cur = nx;
         LCLK(0);
 #ifndef LEAN_NOMEM   // profiling build LEAN_NOMEM: every window re-processes the first one (no HBM reads)
-#if LEAN_PF >= 2
-        nx = nx2;
-        if (w + 2 * wstep < last_win) load_win(g, w + 2 * wstep, wstr_b, nx2);
-#else
         if (w + wstep < last_win) load_win(g, w + wstep, wstr_b, nx);
-#endif
 #endif
 
         // ---- stage and classify
-        ((v4u*)W.bytes)[2 * lane] = cur.a;
-        ((v4u*)W.bytes)[2 * lane + 1] = cur.b;
-#if defined(LEAN_PROF) && LEAN_PROF == 0   // profiling build: loads + staging only
-        if (lane == 0) n_rec += W.bytes[w & 2047];
-        continue;
-#endif
-        uint32_t sep, nl, qf;
-        classify(cur.a, cur.b, rep_d, rep_q, sep, nl, qf);
-        W.bm[lane] = make_uint2(sep, nl);
-        const bool wq = __ballot(qf != 0) != 0;           // window holds a quote (uniform)
-        if (wq) W.qt[lane] = byte_bits(cur.a, cur.b, rep_q);
+#pragma unroll
+        for (int i = 0; i < 4; i++) ((v4u*)W.bytes)[4 * lane + i] = cur.a[i];
+        uint32_t sep0, nl0, sep1, nl1, qf = 0;
+        classify32(cur.a[0], cur.a[1], rep_d, rep_q, sep0, nl0, qf);
+        classify32(cur.a[2], cur.a[3], rep_d, rep_q, sep1, nl1, qf);
+        W.bm[2 * lane] = make_uint2(sep0, nl0);
+        W.bm[2 * lane + 1] = make_uint2(sep1, nl1);
+        const bool wq = __ballot((qf & 0x80808080u) != 0) != 0;   // window holds a quote (uniform)
+        if (wq) {
+            W.qt[2 * lane] = byte_bits(cur.a[0], cur.a[1], rep_q);
+            W.qt[2 * lane + 1] = byte_bits(cur.a[2], cur.a[3], rep_q);
+        }
 
-        // ---- record starts owned by this window: file [ws, ws + WS) within [lo_ok, hi_ok)
-        const uint32_t prevnl = (uint32_t)__builtin_amdgcn_update_dpp(0, (int)(nl >> 31), 0x138, 0xf, 0xf, true);
-        uint32_t starts = ~nl & ((nl << 1) | prevnl);
+        // ---- record starts owned by this window: file [ws, ws + stride) within [lo_ok, hi_ok)
+        const uint64_t nl = (uint64_t)nl0 | ((uint64_t)nl1 << 32);
+        const uint32_t prev_top = (uint32_t)__builtin_amdgcn_update_dpp(0, (int)(nl1 >> 31), 0x138, 0xf, 0xf, true);
+        const uint32_t pb = cur.prev >> 24;                           // the byte before the window
+        const uint32_t prevnl = lane == 0 ? (uint32_t)(pb == '\n' || pb == '\r') : prev_top;
+        uint64_t starts = ~nl & ((nl << 1) | prevnl);
         {
             const uint64_t lo64 = (lo_ok > ws ? lo_ok : ws) - ws;
             const uint64_t hi64 = hi_ok < ws + wstr_b ? hi_ok : ws + wstr_b;
-            const uint32_t lo_s = HEAD + (uint32_t)(lo64 < (uint64_t)wstr_b ? lo64 : (uint64_t)wstr_b);   // staged offsets
-            const uint32_t hi_s = hi64 > ws ? HEAD + (uint32_t)(hi64 - ws) : (uint32_t)HEAD;
+            const uint32_t lo_s = (uint32_t)(lo64 < (uint64_t)wstr_b ? lo64 : (uint64_t)wstr_b);   // window offsets
+            const uint32_t hi_s = hi64 > ws ? (uint32_t)(hi64 - ws) : 0u;
             const uint32_t b0 = (uint32_t)lane * LB;
             if (b0 + LB <= lo_s || b0 >= hi_s) {
                 starts = 0;
             } else {
-                if (lo_s > b0) starts &= ~0u << (lo_s - b0);
-                if (hi_s < b0 + LB) starts &= (1u << (hi_s - b0)) - 1;
+                if (lo_s > b0) starts &= ~0ull << (lo_s - b0);
+                if (hi_s < b0 + LB) starts &= (1ull << (hi_s - b0)) - 1;
             }
         }
-        const uint32_t nst = (uint32_t)__popc(starts);
+        const uint32_t nst = (uint32_t)__popcll(starts);
         const uint32_t incl = wave_incl_scan(nst);
         const uint32_t rbase = incl - nst;
         const uint32_t R = (uint32_t)__builtin_amdgcn_readlane((int)incl, 63);
@@ -630,259 +707,332 @@ __global__ __launch_bounds__(LT) void lean_kernel(const uint8_t* __restrict__ g,
         for (uint32_t pass = 0; pass < R; pass += RSN) {
             // this pass's record starts -> W.rs
             {
-                uint32_t m = starts, r = rbase - pass;
+                uint64_t m = starts;
+                uint32_t r = rbase - pass;
                 while (m) {
-                    const uint32_t b = (uint32_t)__builtin_ctz(m);
+                    const uint32_t b = ctz64(m);
                     m &= m - 1;
                     if (r < (uint32_t)RSN) W.rs[r] = (uint16_t)(lane * LB + b);
                     r++;
                 }
             }
             wave_order();
-            const bool valid = pass + lane < R;
-            const uint32_t p = valid ? W.rs[lane] : (uint32_t)HEAD;
-
+            Rec rec[2];
+#pragma unroll
+            for (int u = 0; u < 2; u++) {
+                Rec& Rr = rec[u];
+                Rr.valid = pass + 64 * u + lane < R;
+                Rr.p = Rr.valid ? W.rs[64 * u + lane] : 0u;
+            }
             // ---- role fields (WHERE, SUM 0/1, GROUP BY): position and length (0: NULL / missing)
-            uint64_t sv, nv;
-            views(W, p, sv, nv);
-            const uint32_t e = ctz64(nv);                  // record end (64: beyond the view)
-            bool fail = !valid;
-            uint32_t lastpos = 0;
-            uint32_t wfp = p, wfl = 0, gfp = p, klen = 0;
-            uint32_t sfp[MAXS], sfl[MAXS];
 #pragma unroll
-            for (int j = 0; j < MAXS; j++) { sfp[j] = p; sfl[j] = 0; }
-            {
-                uint64_t s = sv;
-                uint32_t done = 0;
+            for (int u = 0; u < 2; u++) {
+                Rec& Rr = rec[u];
+                uint64_t sv, nv;
+                views(W, Rr.p, sv, nv);
+                Rr.fail = !Rr.valid;
+                Rr.lastpos = 0;
+                Rr.wfp = Rr.p; Rr.wfl = 0; Rr.gfp = Rr.p; Rr.klen = 0;
 #pragma unroll
-                for (int k = 0; k < NR; k++) {
-                    uint32_t fp_, fl_;
-                    field_next(sv, s, done, e, rcol[k], p, fp_, fl_, fail, lastpos);
-                    const uint32_t role = rrole[k];
-                    if (WM != LW_NONE && role == R_WHERE) { wfp = fp_; wfl = fl_; }
-                    if (NS > 0 && role == R_SUM0) { sfp[0] = fp_; sfl[0] = fl_; }
-                    if (NS > 1 && role == R_SUM1) { sfp[MAXS - 1] = fp_; sfl[MAXS - 1] = fl_; }
-                    if (GROUPED && role == R_GROUP) { gfp = fp_; klen = fl_; }
-                }
+                for (int j = 0; j < MAXS; j++) { Rr.sfp[j] = Rr.p; Rr.sfl[j] = 0; }
+                walk<NR, WM, NS, GROUPED>(Rr, sv, nv, rcol, rrole);
             }
             // a quote at or before the last byte examined may hide separators
-            if (wq) fail |= (qview(W, p) & ((2ULL << (lastpos < 63 ? lastpos : 63)) - 1)) != 0;
-
-            // ---- wave-uniform field-size classes: every lane's numeric WHERE / SUM field
-            //      fits a dword (num4), every GROUP BY key fits 8 bytes (two-word keys)
-            const bool w4 = WM == LW_NUM && __all(!valid | (wfl <= 4u));
-            bool s4 = NS > 0;
+            if (wq) {
 #pragma unroll
-            for (int j = 0; j < NS; j++) s4 = s4 && __all(!valid | (sfl[j] <= 4u));
-            const bool g8 = GROUPED && __all(!valid | (klen <= 8u));
-
-            // ---- field bytes of the roles (one batch of LDS reads)
-            uint32_t wd0 = 0, wd1 = 0;
-            if (WM != LW_NONE) {
-                if (w4) load4(W.bytes, wfp, wd0);
-                else load8(W.bytes, wfp, wd0, wd1);
-            }
-            uint32_t sd0[MAXS], sd1[MAXS];
-#pragma unroll
-            for (int j = 0; j < MAXS; j++) {
-                sd0[j] = sd1[j] = 0;
-                if (j < NS) {
-                    if (s4) load4(W.bytes, sfp[j], sd0[j]);
-                    else load8(W.bytes, sfp[j], sd0[j], sd1[j]);
+                for (int u = 0; u < 2; u++) {
+                    Rec& Rr = rec[u];
+                    Rr.fail |= (qview(W, Rr.p) & ((2ULL << (Rr.lastpos < 63 ? Rr.lastpos : 63)) - 1)) != 0;
                 }
             }
-            uint32_t k0 = 0, k1 = 0, k2 = 0, k3 = 0;
-            if (GROUPED) {
-                if (g8) load8(W.bytes, gfp, k0, k1);
-                else load16(W.bytes, gfp, k0, k1, k2, k3);
+
+            // ---- wave-uniform field-size classes: every lane's numeric WHERE / SUM field
+            //      fits a dword (num4), the GROUP BY keys fit the tag (K8: 8 bytes)
+            bool w4 = WM == LW_NUM, s4 = NS > 0;
+            bool g8 = GROUPED;
+            {
+                bool wb = true, sb = true, gb = true;
+#pragma unroll
+                for (int u = 0; u < 2; u++) {
+                    const Rec& Rr = rec[u];
+                    wb = wb & (!Rr.valid | (Rr.wfl <= 4u));
+#pragma unroll
+                    for (int j = 0; j < NS; j++) sb = sb & (!Rr.valid | (Rr.sfl[j] <= 4u));
+                    gb = gb & (!Rr.valid | (Rr.klen <= 8u));
+                }
+                if (WM == LW_NUM) w4 = __all(wb);
+                if (NS > 0) s4 = __all(sb);
+                if (GROUPED) g8 = __all(gb);
+            }
+
+            // ---- field bytes of the roles (one batch of LDS reads)
+            uint32_t wd0[2] = {0, 0}, wd1[2] = {0, 0};
+            uint32_t sd0[2][MAXS], sd1[2][MAXS];
+            uint32_t k0[2] = {0, 0}, k1[2] = {0, 0}, k2[2] = {0, 0}, k3[2] = {0, 0};
+#pragma unroll
+            for (int u = 0; u < 2; u++) {
+                const Rec& Rr = rec[u];
+                if (WM != LW_NONE) {
+                    if (w4) wd0[u] = load4(W.bytes, Rr.wfp);
+                    else load8(W.bytes, Rr.wfp, wd0[u], wd1[u]);
+                }
+#pragma unroll
+                for (int j = 0; j < MAXS; j++) {
+                    sd0[u][j] = sd1[u][j] = 0;
+                    if (j < NS) {
+                        if (s4) sd0[u][j] = load4(W.bytes, Rr.sfp[j]);
+                        else load8(W.bytes, Rr.sfp[j], sd0[u][j], sd1[u][j]);
+                    }
+                }
+                if (GROUPED) {
+                    if (g8 || !K16) load8(W.bytes, Rr.gfp, k0[u], k1[u]);
+                    else load16(W.bytes, Rr.gfp, k0[u], k1[u], k2[u], k3[u]);
+                }
             }
 
             LCLK(2);
-#if defined(LEAN_PROF) && LEAN_PROF == 2   // profiling build: + record list, field walk, field loads
-            n_rec += __popcll(__ballot(fail || ((wd0 ^ sd0[0] ^ k0 ^ lastpos) & 1)));
+#if defined(LEAN_PROF) && LEAN_PROF == 2   // profiling build: + record list, views, field walk, field loads
+            n_rec += __popcll(__ballot(rec[0].fail ^ rec[1].fail ^ ((wd0[0] ^ wd0[1] ^ sd0[0][0] ^ sd0[1][0] ^ k0[0] ^ k1[1]) & 1)));
             wave_order();
             continue;
 #endif
             // ---- WHERE outcome: numerals and short strings in registers, else the exact typers
-            bool pass_ = true;
+            bool pass_[2] = {true, true};
             if (WM != LW_NONE) {
-                bool outcome = pass_null;                  // missing column / empty field: NULL
-                bool typed = wfl == 0;
-                if (WM == LW_NUM) {
-                    const Num n = w4 ? num4(wd0, wfl) : num7(wd0, wd1, wfl);
-                    int c = (int)n.M < wlo ? -1 : ((int)n.M > whi ? 1 : 0);
-                    if (__any(n.ok & n.dot)) {             // DOUBLE fields: strtod = RN(M / 10^k)
-                        const double d = (double)n.M / p10(n.k);
-                        if (n.dot) c = d < wl ? -1 : (d > wl ? 1 : 0);
+                bool outcome[2], gen[2];
+                Num n[2];
+#pragma unroll
+                for (int u = 0; u < 2; u++) {
+                    const Rec& Rr = rec[u];
+                    outcome[u] = pass_null;                // missing column / empty field: NULL
+                    bool typed = Rr.wfl == 0;
+                    if (WM == LW_NUM) {
+                        n[u] = w4 ? num4<false>(wd0[u], Rr.wfl) : num7(wd0[u], wd1[u], Rr.wfl);
+                        const int c = (int)n[u].M < wlo ? -1 : ((int)n[u].M > whi ? 1 : 0);
+                        if (n[u].ok) outcome[u] = tt_result(wtt, c);
+                        typed |= n[u].ok;
+                    } else if (WM == LW_STR) {
+                        // a STRING field of <= 8 bytes: no leading digit / sign / dot (never a
+                        // numeral or date), no byte <= ' ' (trim_whitespace is a no-op)
+                        uint32_t a0 = wd0[u], a1 = wd1[u];
+                        const uint32_t c0 = a0 & 0xFFu;
+                        mask8(Rr.wfl, a0, a1);
+                        const uint32_t f0 = len_mask(Rr.wfl, 0) & 0x80808080u, f1 = len_mask(Rr.wfl, 1) & 0x80808080u;
+                        const bool ok = (Rr.wfl - 1 < 8u) & !(is_digit(c0) | (c0 == '-') | (c0 == '+') | (c0 == '.')) &
+                                        ((low_bytes(a0, f0) | low_bytes(a1, f1)) == 0);
+                        const uint64_t x = bswap64(a0, a1);
+                        if (ok) outcome[u] = tt_result(wtt, x < wstr ? -1 : (x > wstr ? 1 : 0));
+                        typed |= ok;
                     }
-                    if (n.ok) outcome = tt_result(wtt, c);
-                    typed |= n.ok;
-                } else if (WM == LW_STR) {
-                    // a STRING field of <= 8 bytes: no leading digit / sign / dot (never a
-                    // numeral or date), no byte <= ' ' (trim_whitespace is a no-op)
-                    uint32_t a0 = wd0, a1 = wd1;
-                    const uint32_t c0 = a0 & 0xFFu;
-                    mask8(wfl, a0, a1);
-                    const uint32_t f0 = len_mask(wfl, 0) & 0x80808080u, f1 = len_mask(wfl, 1) & 0x80808080u;
-                    const bool ok = (wfl - 1 < 8u) & !(is_digit(c0) | (c0 == '-') | (c0 == '+') | (c0 == '.')) &
-                                    ((low_bytes(a0, f0) | low_bytes(a1, f1)) == 0);
-                    const uint64_t x = bswap64(a0, a1);
-                    if (ok) outcome = tt_result(wtt, x < wstr ? -1 : (x > wstr ? 1 : 0));
-                    typed |= ok;
+                    gen[u] = !typed & !Rr.fail;
                 }
-                const bool gen = !typed & !fail;
-                if (__any(gen)) {                          // the exact typers (rare shapes)
-                    if (gen) {
-                        Cell c;
-                        if (!type_field(W.bytes, wfp, wfl, c)) {
-                            fail = true;
-                        } else {
-                            if (c.kind == K_STR) c.bits = tile_g + wfp;
-                            outcome = tt_result(wtt, compare(c, LP.wconst));
+                if (WM == LW_NUM && w4) {
+                    // DOUBLE fields of <= 4 bytes (num4<false> declined them): strtod = RN(M / 10^k)
+                    if (__any(gen[0] | gen[1])) {
+#pragma unroll
+                        for (int u = 0; u < 2; u++) {
+                            if (gen[u]) {
+                                const Num d = num4<true>(wd0[u], rec[u].wfl);
+                                if (d.ok) {
+                                    const double v = (double)d.M / p10(d.k);
+                                    outcome[u] = tt_result(wtt, v < wl ? -1 : (v > wl ? 1 : 0));
+                                    gen[u] = false;
+                                }
+                            }
+                        }
+                    }
+                } else if (WM == LW_NUM) {
+                    if (__any(n[0].ok & n[0].dot) || __any(n[1].ok & n[1].dot)) {
+#pragma unroll
+                        for (int u = 0; u < 2; u++) {
+                            if (n[u].ok & n[u].dot) {
+                                const double v = (double)n[u].M / p10(n[u].k);
+                                outcome[u] = tt_result(wtt, v < wl ? -1 : (v > wl ? 1 : 0));
+                            }
                         }
                     }
                 }
-                pass_ = outcome;
+                if (__any(gen[0] | gen[1])) {              // the exact typers (rare shapes)
+#pragma unroll
+                    for (int u = 0; u < 2; u++) {
+                        if (gen[u]) {
+                            Cell c;
+                            if (!type_field(W.bytes, rec[u].wfp, rec[u].wfl, c)) {
+                                rec[u].fail = true;
+                            } else {
+                                if (c.kind == K_STR) c.bits = tile_g + rec[u].wfp;
+                                outcome[u] = tt_result(wtt, compare(c, LP.wconst));
+                            }
+                        }
+                    }
+                }
+                pass_[0] = outcome[0];
+                pass_[1] = outcome[1];
             }
 
             // ---- SUM addends (numeric: true and the value)
-            double sval[MAXS];
-            bool snum[MAXS];
+            double sval[2][MAXS];
+            bool snum[2][MAXS];
 #pragma unroll
             for (int j = 0; j < MAXS; j++) {
-                sval[j] = 0.0;
-                snum[j] = false;
-                if (j >= NS) continue;
-                Num n;
-                if (s4) {
-                    n = num4(sd0[j], sfl[j]);
-                    sval[j] = (double)n.M * (((n.k & 1) ? 0.1 : 1.0) * ((n.k & 2) ? 0.01 : 1.0));   // = inv10(k), k <= 3
-                } else {
-                    n = num7(sd0[j], sd1[j], sfl[j]);
-                    sval[j] = (double)n.M * inv10(n.k);
+                bool gen[2] = {false, false};
+#pragma unroll
+                for (int u = 0; u < 2; u++) {
+                    sval[u][j] = 0.0;
+                    snum[u][j] = false;
+                    if (j >= NS) continue;
+                    const uint32_t len = rec[u].sfl[j];
+                    Num n;
+                    if (s4) {
+                        n = num4<true>(sd0[u][j], len);
+                        sval[u][j] = (double)n.M * (((n.k & 1) ? 0.1 : 1.0) * ((n.k & 2) ? 0.01 : 1.0));   // = inv10(k), k <= 3
+                    } else {
+                        n = num7(sd0[u][j], sd1[u][j], len);
+                        sval[u][j] = (double)n.M * inv10(n.k);
+                    }
+                    snum[u][j] = n.ok;
+                    gen[u] = !n.ok & (len != 0) & !rec[u].fail;
                 }
-                snum[j] = n.ok;
-                const bool gen = !n.ok & (sfl[j] != 0) & !fail;
-                if (__any(gen)) {
-                    if (gen) {
-                        Cell c;
-                        if (!type_field(W.bytes, sfp[j], sfl[j], c)) fail = true;
-                        else if (is_num(c)) { sval[j] = num_of(c); snum[j] = true; }
+                if (j < NS && __any(gen[0] | gen[1])) {
+#pragma unroll
+                    for (int u = 0; u < 2; u++) {
+                        if (gen[u]) {
+                            Cell c;
+                            if (!type_field(W.bytes, rec[u].sfp[j], rec[u].sfl[j], c)) rec[u].fail = true;
+                            else if (is_num(c)) { sval[u][j] = num_of(c); snum[u][j] = true; }
+                        }
                     }
                 }
             }
 
-            // ---- GROUP BY key: the raw field bytes (<= 16, no byte <= ' ')
-            uint32_t h = 0;
+            // ---- GROUP BY key: the raw field bytes (no byte <= ' '), zero padded
+            uint32_t h[2] = {0, 0};
+            bool longk[2] = {false, false};
             if (GROUPED) {
-                if (g8) {
-                    const uint32_t m0 = len_mask(klen, 0), m1 = len_mask(klen, 1);
-                    k0 &= m0; k1 &= m1;
-                    const uint32_t lowb = low_bytes(k0, m0 & 0x80808080u) | low_bytes(k1, m1 & 0x80808080u);
-                    fail |= lowb != 0;
-                    h = key_hash(klen, k0, k1, 0u, 0u);
-                } else {
-                    const uint32_t m0 = len_mask(klen, 0), m1 = len_mask(klen, 1), m2 = len_mask(klen, 2),
-                                   m3 = len_mask(klen, 3);
-                    k0 &= m0; k1 &= m1; k2 &= m2; k3 &= m3;
-                    const uint32_t lowb = low_bytes(k0, m0 & 0x80808080u) | low_bytes(k1, m1 & 0x80808080u) |
-                                          low_bytes(k2, m2 & 0x80808080u) | low_bytes(k3, m3 & 0x80808080u);
-                    fail |= (lowb != 0) | (klen > 16);
-                    h = key_hash(klen, k0, k1, k2, k3);
+#pragma unroll
+                for (int u = 0; u < 2; u++) {
+                    const uint32_t klen = rec[u].klen;
+                    if (g8 || !K16) {
+                        const uint32_t m0 = len_mask(klen, 0), m1 = len_mask(klen, 1);
+                        k0[u] &= m0; k1[u] &= m1;
+                        const uint32_t lowb = low_bytes(k0[u], m0 & 0x80808080u) | low_bytes(k1[u], m1 & 0x80808080u);
+                        rec[u].fail |= lowb != 0;
+                        longk[u] = klen > 8;
+                    } else {
+                        const uint32_t m0 = len_mask(klen, 0), m1 = len_mask(klen, 1), m2 = len_mask(klen, 2),
+                                       m3 = len_mask(klen, 3);
+                        k0[u] &= m0; k1[u] &= m1; k2[u] &= m2; k3[u] &= m3;
+                        const uint32_t lowb = low_bytes(k0[u], m0 & 0x80808080u) | low_bytes(k1[u], m1 & 0x80808080u) |
+                                              low_bytes(k2[u], m2 & 0x80808080u) | low_bytes(k3[u], m3 & 0x80808080u);
+                        rec[u].fail |= lowb != 0;
+                        longk[u] = klen > 16;
+                    }
+                    if (klen == 0) k1[u] = 1u;               // the empty key's tag
+                    h[u] = key_hash(k0[u], k1[u], k2[u], k3[u]);
                 }
             }
 
             LCLK(3);
-            // ---- declined records go whole to slow_kernel
-            const uint64_t rec = ws - HEAD + p;
-            const bool slow = valid && fail;
-            const uint64_t sb = __ballot(slow);
-            if (sb) {
-                unsigned long long base = 0;
-                if (lane == 0) base = atomicAdd(&stats->slow_records, (unsigned long long)__popcll(sb));
-                base = __shfl(base, 0, 64);
-                if (slow) {
-                    const unsigned long long i = base + __popcll(sb & ((1ULL << lane) - 1));
-                    if (i < slow_cap) slow_list[i] = rec;
-                }
-            }
-            const bool ok = valid & !fail;
-            pass_ = pass_ & ok;
-            n_rec += (unsigned long long)__popcll(__ballot(ok));
-            n_pass += (unsigned long long)__popcll(__ballot(pass_));
-            if (row_out) {
-                const unsigned long long slot = wave_slot(pass_, &stats->rows_emitted);
-                if (pass_ && slot < row_cap) row_out[slot] = rec;
-            }
-#if defined(LEAN_PROF) && LEAN_PROF == 3   // profiling build: + values, filter, keys
-            n_rec += __popcll(__ballot((h ^ (uint32_t)sval[0]) & 1));
+#if defined(LEAN_PROF) && LEAN_PROF == 3   // profiling build: + typing, keys and hashes
+            n_rec += __popcll(__ballot(pass_[0] ^ pass_[1] ^ ((h[0] ^ h[1] ^ (uint32_t)sval[0][0] ^ (uint32_t)sval[1][0]) & 1)));
             wave_order();
             continue;
 #endif
+            // ---- declined records go whole to slow_kernel
+#pragma unroll
+            for (int u = 0; u < 2; u++) {
+                const Rec& Rr = rec[u];
+                const uint64_t off = ws + Rr.p;
+                const bool slow = Rr.valid && Rr.fail;
+                const uint64_t sb = __ballot(slow);
+                if (sb) {
+                    unsigned long long base = 0;
+                    if (lane == 0) base = atomicAdd(&stats->slow_records, (unsigned long long)__popcll(sb));
+                    base = __shfl(base, 0, 64);
+                    if (slow) {
+                        const unsigned long long i = base + __popcll(sb & ((1ULL << lane) - 1));
+                        if (i < slow_cap) slow_list[i] = off;
+                    }
+                }
+                const bool ok = Rr.valid & !Rr.fail;
+                pass_[u] = pass_[u] & ok;
+                n_rec += (unsigned long long)__popcll(__ballot(ok));
+                n_pass += (unsigned long long)__popcll(__ballot(pass_[u]));
+                if (row_out) {
+                    const unsigned long long slot = wave_slot(pass_[u], &stats->rows_emitted);
+                    if (pass_[u] && slot < row_cap) row_out[slot] = off;
+                }
+            }
 
             LCLK(4);
             // ---- aggregate
             if (!GROUPED) {
-                my_cnt += pass_ ? 1u : 0u;
-                my_first = pass_ && rec < my_first ? rec : my_first;
 #pragma unroll
-                for (int j = 0; j < NS; j++) {
-                    my_sum[j] += pass_ && snum[j] ? sval[j] : 0.0;
-                    my_num[j] += pass_ && snum[j] ? 1u : 0u;
-                }
-            } else {
-                // home bucket for every lane: fingerprints, then the matching slot's key
-                const uint32_t bk = bucket_of(h, lt.NB);
-                const v4u q0 = lt.F[2 * bk], q1 = lt.F[2 * bk + 1];
-                const uint32_t j = fp_first(q0, q1, fp_of(h));
-                const uint32_t s0 = bk * BS + (j < BS ? j : BS - 1);
-                const v4u a = lt.A[s0];
-                bool hit = (j < BS) & (a.x == (0x80000000u | klen)) & (a.z == k0) & (a.w == k1);
-                if (!g8) {           // a stored key of the same length <= 8 has zero words 2-3
-                    const uint2 b = lt.B[s0];
-                    hit = hit & (b.x == k2) & (b.y == k3);
-                }
-                int slot = hit ? (int)s0 : -1;
-                uint32_t first = a.y;
-                const bool miss = pass_ & !hit;
-                if (__any(miss)) {                         // new keys (rare after the first windows)
-                    if (miss) slot = lt_slow(lt, klen, k0, k1, k2, k3, h, first);
-                }
-                const bool add = pass_ & (slot >= 0);
-                if (add) {
-                    const uint32_t fc = (round << 15) | ((uint32_t)wv << 11) | p;
-                    atomicAdd(&lt.cnt[slot], 1u);
-                    if (fc < first) atomicMin((uint32_t*)(lt.A + slot) + 1, fc);
+                for (int u = 0; u < 2; u++) {
+                    const uint64_t off = ws + rec[u].p;
+                    my_cnt += pass_[u] ? 1u : 0u;
+                    my_first = pass_[u] && off < my_first ? off : my_first;
 #pragma unroll
-                    for (int j = 0; j < NS; j++) atomicAdd(&lt.sum[j][slot], snum[j] ? sval[j] : 0.0);
-                }
-#pragma unroll
-                for (int j = 0; j < NS; j++) {
-                    const bool nn = add & !snum[j];
-                    if (__any(nn)) {
-                        if (nn) atomicAdd(&lt.miss[j][slot], 1u);
+                    for (int j = 0; j < NS; j++) {
+                        my_sum[j] += pass_[u] && snum[u][j] ? sval[u][j] : 0.0;
+                        my_num[j] += pass_[u] && snum[u][j] ? 1u : 0u;
                     }
                 }
-                const bool spill = pass_ && slot < 0;
-                if (__any(spill)) {                        // LDS table full: straight to the HBM raw table
-                    n_spill += (unsigned long long)__popcll(__ballot(spill));
-                    if (spill) {
-                        const GroupTable& rt = tabs[TAB_RT];
-                        const GKey kk = raw_key(klen, (uint64_t)k0 | ((uint64_t)k1 << 32), (uint64_t)k2 | ((uint64_t)k3 << 32));
-                        const int gi = g_insert(rt, kk, gk_hash(kk), stats);
-                        if (gi >= 0) {
-                            atomicAdd(&rt.cnt[gi], 1ULL);
-                            atomicMin(&rt.first[gi], (unsigned long long)rec);
-                            for (int a = 0; a < LP.nacc; a++) {
-                                const int j = LP.acc_sidx[a];
-                                const bool nm = j == 0 ? snum[0] : snum[MAXS - 1];
-                                const double v = j == 0 ? sval[0] : sval[MAXS - 1];
-                                if (nm) {
-                                    atomicAdd(&rt.sum[a][gi], v);
-                                    atomicAdd(&rt.num[a][gi], 1ULL);
-                                }
-                            }
+            } else {
+                int slot[2];
+                bool miss[2];
+#pragma unroll
+                for (int u = 0; u < 2; u++) {
+                    slot[u] = longk[u] ? -1 : lt_find<K16>(lt, NB, h[u], k0[u], k1[u], k2[u], k3[u]);
+                    miss[u] = pass_[u] & (slot[u] < 0) & !longk[u];
+                }
+#if defined(LEAN_PROF) && LEAN_PROF == 4   // profiling build: + table lookups (no atomics)
+                n_rec += __popcll(__ballot((slot[0] ^ slot[1]) & 1));
+                wave_order();
+                continue;
+#endif
+                if (__any(miss[0] | miss[1])) {           // new keys (rare after the first windows)
+#pragma unroll
+                    for (int u = 0; u < 2; u++)
+                        if (miss[u]) slot[u] = lt_insert<K16>(lt, NB, h[u], k0[u], k1[u], k2[u], k3[u]);
+                }
+#pragma unroll
+                for (int u = 0; u < 2; u++) {
+                    const bool add = pass_[u] & (slot[u] >= 0);
+                    if (add) {
+                        const uint32_t fc = (round << 16) | ((uint32_t)wv << 12) | rec[u].p;
+#ifndef LEAN_ATOM
+#define LEAN_ATOM 7
+#endif
+                        if (LEAN_ATOM & 1) atomicAdd(&lt.cnt[slot[u]], 1u);
+                        if (LEAN_ATOM & 32) lt.cnt[slot[u]] = fc;                       // experiment: plain store
+                        if (LEAN_ATOM & 64) atomicAdd(&lt.cnt[(wv * 64 + lane + 128 * u) & (H - 1)], 1u);   // experiment: private
+                        if (LEAN_ATOM & 128) atomicAdd(&lt.cnt[h[u] & (H - 1)], 1u);   // experiment: no lookup dependency
+                        if (LEAN_ATOM & 2) atomicMin(&lt.first[slot[u]], fc);
+#pragma unroll
+                        for (int j = 0; j < NS; j++) {
+                            if (LEAN_ATOM & 4) atomicAdd(&lt.sum[j][slot[u]], snum[u][j] ? sval[u][j] : 0.0);
+                            if (LEAN_ATOM & 8) atomicAdd((unsigned long long*)&lt.sum[j][slot[u]], (unsigned long long)(sval[u][j] * 1000.0));
+                            if (LEAN_ATOM & 16) atomicAdd((uint32_t*)&lt.sum[j][slot[u]], (uint32_t)(sval[u][j] * 1000.0));
+                        }
+                    }
+#pragma unroll
+                    for (int j = 0; j < NS; j++) {
+                        const bool nn = add & !snum[u][j];
+                        if (__any(nn)) {
+                            if (nn) atomicAdd(&lt.miss[j][slot[u]], 1u);
+                        }
+                    }
+                }
+#pragma unroll
+                for (int u = 0; u < 2; u++) {
+                    const bool spill = pass_[u] && slot[u] < 0;
+                    if (__any(spill)) {                    // long key or both buckets full: the HBM raw table
+                        n_spill += (unsigned long long)__popcll(__ballot(spill));
+                        if (spill) {
+                            spill_record(W.bytes, rec[u].gfp, rec[u].klen, ws + rec[u].p, tabs, stats, slow_list,
+                                         slow_cap, LP.nacc, LP.acc_sidx, snum[u][0], sval[u][0], snum[u][MAXS - 1],
+                                         sval[u][MAXS - 1]);
                         }
                     }
                 }
@@ -946,18 +1096,27 @@ __global__ __launch_bounds__(LT) void lean_kernel(const uint8_t* __restrict__ g,
     //      types each distinct raw key once and merges it into the canonical table)
     __syncthreads();
     const GroupTable& rt = tabs[TAB_RT];
-    for (uint32_t i = tid; i < lds_h; i += LT) {
-        const v4u a = lt.A[i];
-        if (a.x < 2) continue;
-        const uint2 b = lt.B[i];
-        const GKey k = raw_key(a.x & 0x1F, (uint64_t)a.z | ((uint64_t)a.w << 32), (uint64_t)b.x | ((uint64_t)b.y << 32));
+    // every block walks its slots from a different start: the blocks' tables hold
+    // the same keys in nearly the same slots, and flushing them in the same order
+    // would send all blocks' atomics for one key to one HBM slot at once
+    const uint32_t rot = (uint32_t)blockIdx.x * (H / 64 + 1);
+    for (uint32_t ii = tid; ii < H; ii += LT) {
+        const uint32_t i = (ii + rot) & (H - 1);
+        const uint32_t* tw = (const uint32_t*)(lt.T + i * TSTRIDE);
+        const uint64_t w0 = (uint64_t)tw[0] | ((uint64_t)tw[1] << 32);
+        const uint64_t w1 = K16 ? ((uint64_t)tw[2] | ((uint64_t)tw[3] << 32)) : 0ull;
+        if (w0 == 0 || (K16 && tw[1] == CLAIM && tw[0] == 0)) continue;   // free (or a never-published claim)
+        const uint32_t n = lt.cnt[i];
+        if (!n) continue;
+        const uint32_t kl = key_len(w0, w1);
+        const GKey k = raw_key(kl, kl ? w0 : 0ull, w1);
         const int gi = g_insert(rt, k, gk_hash(k), stats);
         if (gi < 0) continue;
-        const uint32_t n = lt.cnt[i];
-        if (n) atomicAdd(&rt.cnt[gi], (unsigned long long)n);
-        if (a.y != NOFIRST) {
-            const uint64_t fw = LP.first_win + ((uint64_t)(a.y >> 15) * gridDim.x + blockIdx.x) * NWV + ((a.y >> 11) & 15);
-            atomicMin(&rt.first[gi], (unsigned long long)(fw * LP.ws - HEAD + (a.y & 2047)));
+        atomicAdd(&rt.cnt[gi], (unsigned long long)n);
+        const uint32_t fc = lt.first[i];
+        if (fc != NOFIRST) {
+            const uint64_t fw = LP.first_win + ((uint64_t)(fc >> 16) * gridDim.x + blockIdx.x) * NWV + ((fc >> 12) & 15);
+            atomicMin(&rt.first[gi], (unsigned long long)(fw * LP.ws + (fc & 4095)));
         }
         for (int acc = 0; acc < LP.nacc; acc++) {
             const int j = LP.acc_sidx[acc];
@@ -1071,29 +1230,27 @@ bool lean_shape(const ScanPlan* P, LeanPlan* lp, int* wm) {
 }
 
 int ns_of(const LeanPlan& lp) { return lp.ns; }
-size_t lean_slot_bytes(int ns) { return lean::slot_bytes(ns); }
-size_t lean_fixed_bytes() { return lean::fixed_bytes(); }
 
-uint32_t lean_slots(int ns, int grouped) { return lean::slots_for(ns, grouped != 0); }
-size_t lean_lds(int ns, int grouped) {
-    return lean_fixed_bytes() + (size_t)lean_slots(ns, grouped) * lean_slot_bytes(ns) + 512;
+template <bool K16>
+size_t lean_lds_t(int ns, int grouped) {
+    return lean::fixed_bytes() + (size_t)lean::slots_for<K16>(ns, grouped != 0) * lean::slot_bytes<K16>(ns) + 256;
 }
 
-typedef void (*lean_fn_t)(const uint8_t*, ScanStats*, unsigned long long*, unsigned long long, uint32_t,
-                          unsigned long long*, unsigned long long, const lean::LeanArgs, const GroupTable*);
+typedef void (*lean_fn_t)(const uint8_t*, ScanStats*, unsigned long long*, unsigned long long, unsigned long long*,
+                          unsigned long long, const lean::LeanArgs, const GroupTable*);
 
-template <bool G, int WM>
+template <bool G, int WM, bool K16>
 lean_fn_t pick_ns(int ns) {
-    if (ns == 0) return lean::lean_kernel<G, WM, 0>;
-    return ns == 1 ? lean::lean_kernel<G, WM, 1> : lean::lean_kernel<G, WM, 2>;
+    if (ns == 0) return lean::lean_kernel<G, WM, 0, K16>;
+    return ns == 1 ? lean::lean_kernel<G, WM, 1, K16> : lean::lean_kernel<G, WM, 2, K16>;
 }
-template <bool G>
+template <bool G, bool K16>
 lean_fn_t pick_fn(int wm, int ns) {
     switch (wm) {
-        case lean::LW_NONE: return pick_ns<G, lean::LW_NONE>(ns);
-        case lean::LW_NUM: return pick_ns<G, lean::LW_NUM>(ns);
-        case lean::LW_STR: return pick_ns<G, lean::LW_STR>(ns);
-        default: return pick_ns<G, lean::LW_GEN>(ns);
+        case lean::LW_NONE: return pick_ns<G, lean::LW_NONE, K16>(ns);
+        case lean::LW_NUM: return pick_ns<G, lean::LW_NUM, K16>(ns);
+        case lean::LW_STR: return pick_ns<G, lean::LW_STR, K16>(ns);
+        default: return pick_ns<G, lean::LW_GEN, K16>(ns);
     }
 }
 
@@ -1114,11 +1271,11 @@ uint64_t cq_lean_windows(uint64_t begin, uint64_t end, uint32_t ws) {
     return (end + ws - 1) / ws - begin / ws;
 }
 
-// The window stride for a file: a window's records are handled one per lane, so
-// a stride holding ~58 records of the file's average length fills a wave in one
-// pass instead of spilling a few records into a second, nearly empty pass (and
-// never more than the staged bytes allow).  The average comes from up to 256 KiB
-// of the data bytes (records split on '\n' / '\r' runs, as csv_load does).
+// The window stride for a file: a window's records are handled two per lane, so a
+// stride holding ~120 records of the file's average length fills a wave's 128
+// record slots in one pass (and never more than the staged bytes allow).  The
+// average comes from up to 256 KiB of the data bytes (records split on '\n' /
+// '\r' runs, as csv_load does).
 uint32_t cq_lean_pick_ws(const uint8_t* data, uint64_t n) {
     const uint64_t m = n < (256u << 10) ? n : (256u << 10);
     uint64_t recs = 0;
@@ -1130,18 +1287,42 @@ uint32_t cq_lean_pick_ws(const uint8_t* data, uint64_t n) {
     }
     if (recs < 16) return lean::WS;
     const double avg = (double)m / (double)recs;
-    uint64_t ws = (uint64_t)(58.0 * avg) & ~(uint64_t)15;
+    uint64_t ws = (uint64_t)(120.0 * avg) & ~(uint64_t)127;
     if (ws > (uint64_t)lean::WS) ws = lean::WS;
-    if (ws < 256) ws = 256;
+    if (ws < 512) ws = 512;
     return (uint32_t)ws;
 }
 int cq_lean_waves_per_block() { return lean::NWV; }
+
+// Columns whose sampled fields (up to 256 KiB of records, quote-blind split) are
+// longer than 8 bytes: bit c for column c < 63, bit 63 for every later column.
+// A GROUP BY on such a column runs the K16 tag width.
+uint64_t cq_lean_long_cols(const uint8_t* data, uint64_t n, uint32_t delim) {
+    const uint64_t m = n < (256u << 10) ? n : (256u << 10);
+    uint64_t mask = 1ull << 63, i = 0;
+    while (i < m) {
+        while (i < m && (data[i] == '\n' || data[i] == '\r')) i++;
+        uint32_t c = 0;
+        uint64_t fs = i;
+        while (i <= m) {
+            const bool end = i == m || data[i] == '\n' || data[i] == '\r';
+            if (end || data[i] == delim) {
+                if (i - fs > 8) mask |= 1ull << (c < 63 ? c : 63);
+                c++;
+                fs = i + 1;
+                if (end) break;
+            }
+            i++;
+        }
+    }
+    return mask;
+}
 
 size_t cq_lean_lds_bytes(const cq::ScanPlan* P, int grouped) {
     LeanPlan lp;
     int wm = 0;
     if (!lean_shape(P, &lp, &wm)) return 0;
-    return lean_lds(ns_of(lp), grouped);
+    return P->lean_k16 ? lean_lds_t<true>(ns_of(lp), grouped) : lean_lds_t<false>(ns_of(lp), grouped);
 }
 
 // the lean scan (the caller runs slow_kernel over slow_list afterwards)
@@ -1152,6 +1333,7 @@ hipError_t cq_launch_lean(const uint8_t* g, const cq::ScanPlan* P, const cq::Gro
     LeanPlan lp;
     int wm = 0;
     if (!lean_shape(P, &lp, &wm)) return hipErrorInvalidValue;
+    if (((uintptr_t)g & 255) != 0) return hipErrorInvalidValue;   // 128-byte aligned windows
     if (wm == lean::LW_STR) {   // the literal's bytes (a STRING cell points at device memory)
         const Cell& L = P->consts[P->prog[1].b];
         uint8_t b[8] = {0, 0, 0, 0, 0, 0, 0, 0};
@@ -1171,7 +1353,7 @@ hipError_t cq_launch_lean(const uint8_t* g, const cq::ScanPlan* P, const cq::Gro
     lp.lo_ok = P->data_begin > P->range_begin ? P->data_begin : P->range_begin;
     lp.hi_ok = hi;
     lp.ws = P->lean_ws ? P->lean_ws : (uint32_t)lean::WS;
-    if (lp.ws > (uint32_t)lean::WS || lp.ws % 16) return hipErrorInvalidValue;
+    if (lp.ws > (uint32_t)lean::WS || lp.ws % 128) return hipErrorInvalidValue;
     lp.first_win = P->range_begin / lp.ws;
     lp.last_win = (hi + lp.ws - 1) / lp.ws;
     const int ns = ns_of(lp);
@@ -1191,8 +1373,8 @@ hipError_t cq_launch_lean(const uint8_t* g, const cq::ScanPlan* P, const cq::Gro
         for (int j = 0; j < ns; j++) add(lp.scol[j], j == 0 ? lean::R_SUM0 : lean::R_SUM1);
         if (grouped) add(lp.gcol, lean::R_GROUP);
     }
-    const uint32_t h = lean_slots(ns, grouped);
-    const size_t lds = lean_lds(ns, grouped);
+    const bool k16 = grouped && P->lean_k16;
+    const size_t lds = k16 ? lean_lds_t<true>(ns, grouped) : lean_lds_t<false>(ns, grouped);
     lean::LeanArgs args;
     memset(&args, 0, sizeof args);
     args.lp = lp;
@@ -1209,9 +1391,10 @@ hipError_t cq_launch_lean(const uint8_t* g, const cq::ScanPlan* P, const cq::Gro
         hipError_t e = hipMemcpyAsync(tabs_dev, tabs, sizeof tabs, hipMemcpyHostToDevice, s);
         if (e != hipSuccess) return e;
     }
-    const lean_fn_t fn = grouped ? pick_fn<true>(wm, ns) : pick_fn<false>(wm, ns);
+    const lean_fn_t fn = !grouped ? pick_fn<false, false>(wm, ns) : (k16 ? pick_fn<true, true>(wm, ns)
+                                                                         : pick_fn<true, false>(wm, ns));
     (void)hipFuncSetAttribute((const void*)fn, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds);
-    hipLaunchKernelGGL(fn, dim3(grid), dim3(lean::LT), lds, s, g, stats, row_out, row_cap, h, slow_list, slow_cap,
+    hipLaunchKernelGGL(fn, dim3(grid), dim3(lean::LT), lds, s, g, stats, row_out, row_cap, slow_list, slow_cap,
                        args, (const GroupTable*)tabs_dev);
     return hipGetLastError();
 }

@@ -63,6 +63,7 @@ struct ScanPlan {
     AccSpec acc[MAX_ACC];
     int32_t want_rows;     // 1: also emit matching record offsets (row-returning)
     uint32_t lean_ws;      // lean_kernel window stride (0: the largest, lean::WS)
+    uint32_t lean_k16;     // lean_kernel GROUP BY tags of 16 key bytes (the column's sampled fields exceed 8)
 };
 
 // projection of a row-returning SELECT (device pointers): ncols CSV columns

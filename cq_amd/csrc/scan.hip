@@ -1847,7 +1847,7 @@ hipError_t cq_launch_scan(const uint8_t* g, const cq::ScanPlan* P, const cq::Gro
         uint64_t lg = (wins + per - 1) / per;
         if (lg > (uint64_t)device_cus()) lg = (uint64_t)device_cus();
         if (lg < 1) lg = 1;
-        if ((wins + lg * per - 1) / (lg * per) < (1u << 17)) {   // first-row codes hold 17 bits of round
+        if ((wins + lg * per - 1) / (lg * per) < (1u << 16)) {   // first-row codes hold 16 bits of round
             hipError_t e = cq_launch_lean(g, P, gt, rt, stats, row_out, row_cap, grouped, (int)lg, s, slow_list,
                                           slow_cap);
             if (e != hipSuccess) return e;

@@ -60,13 +60,22 @@ __device__ __forceinline__ uint32_t tag_of(uint64_t h) {
     return t < 2 ? t + 2 : t;
 }
 
+// Lock-free find-or-insert into the HBM group table.  Every access to a slot's
+// tag and key words is a relaxed agent-scope atomic (global_load / global_store
+// sc1: past the CU's L1, coherent across XCDs), so no probe pays an acquire's L1
+// invalidate or an insert a release's L2 write-back: an inserter claims the tag
+// by CAS (0 -> 1), stores the key words, drains them with s_waitcnt vmcnt(0) and
+// only then stores the final tag; a reader that sees that tag issues its key loads
+// after the tag load returned (the compare depends on it), so it sees the words
+// (MI355X_MICROARCH.md, inter-workgroup visibility: sc1 stores drained before
+// the flag, sc1 loads).
 static __device__ int g_insert(const GroupTable& gt, const GKey k, uint64_t h, ScanStats* st) {
     const uint32_t tg = tag_of(h);
     const uint32_t mask = gt.cap - 1;
     const uint32_t cl = gk_clslen(k);
     for (uint32_t probe = 0; probe < gt.cap; probe++) {
         uint32_t i = (uint32_t)(h + probe) & mask;
-        uint32_t t = __hip_atomic_load(&gt.tag[i], __ATOMIC_ACQUIRE, __HIP_MEMORY_SCOPE_AGENT);
+        uint32_t t = __hip_atomic_load(&gt.tag[i], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
         if (t == 0) {
             uint32_t old = atomicCAS(&gt.tag[i], 0u, 1u);
             if (old == 0) {
@@ -75,14 +84,16 @@ static __device__ int g_insert(const GroupTable& gt, const GKey k, uint64_t h, S
                 __hip_atomic_store(&gt.w1[i], k.w1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
                 uint32_t used = atomicAdd(gt.used, 1u) + 1;
                 if (used * 2 > gt.cap) atomicExch(&st->overflow, 1ULL);
-                __hip_atomic_store(&gt.tag[i], tg, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_AGENT);
+                asm volatile("s_waitcnt vmcnt(0)" ::: "memory");   // key words performed before the tag
+                __hip_atomic_store(&gt.tag[i], tg, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
                 return (int)i;
             }
             t = old;
         }
         for (uint32_t spin = 0; t == 1; spin++) {
             if (spin > (1u << 20)) { atomicExch(&st->overflow, 3ULL); return -1; }   // never hang
-            t = __hip_atomic_load(&gt.tag[i], __ATOMIC_ACQUIRE, __HIP_MEMORY_SCOPE_AGENT);
+            __builtin_amdgcn_s_sleep(1);
+            t = __hip_atomic_load(&gt.tag[i], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
         }
         if (t == tg) {
             GKey o;

@@ -1,0 +1,13 @@
+# bench line of each library variant (default: the product build + listed variants)
+#   VARIANTS="base w12" BENCH_ARGS="--rows 100000000" bash scripts/bench_variants.sh
+set -o pipefail
+cd "$GRAFT_REPO_ROOT"
+export TMPDIR=/tmp
+OUT=gpurun_out/${TAG:-variants}
+mkdir -p $OUT
+for v in ${VARIANTS:-base}; do
+  L=$PWD/cq_amd/lib/libcqgpu_$v.so
+  [ $v = base ] && L=$PWD/cq_amd/lib/libcqgpu.so
+  CQ_AMD_LIB=$L timeout -k 10 300 python bench.py --steps 10 --warmup 2 --no-cpu --no-e2e --no-config2 ${BENCH_ARGS:-} > $OUT/$v.json 2> $OUT/$v.err || { tail -5 $OUT/$v.err; exit 1; }
+  python -c "import json; d=json.load(open('$OUT/$v.json')); r=d['roofline']; print('$v', round(r['kernel_ms'],3), 'ms', round(r['frac'],3), 'verified', d['verified'])"
+done
