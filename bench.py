@@ -195,7 +195,7 @@ def main():
 
     import cq_amd
     from cq_amd import abi
-    from cq_amd.dist import gather_blobs
+    from cq_amd.dist import scan_partitioned
     L = cq_amd.lib()
 
     t0 = time.time()
@@ -225,20 +225,8 @@ def main():
                 print("stats", st, file=sys.stderr)
             kernel_used[0] = st.get("scan_kernel", 0)
             return tp, st["scan_ms"]
-        blob = C.c_void_p()
-        n = L.cqgpu_query_partial(ast, (C.c_void_p * 1)(table.handle.value), 1, C.byref(blob))
-        if n == 0:
-            raise RuntimeError(cq_amd.last_error())
-        scan_ms = cq_amd.stats()["scan_ms"]
-        mine = C.string_at(blob, n)
-        C.CDLL(None).free(blob)
-        blobs = gather_blobs(mine, device=torch.device("cuda", local))
-        tp = None
-        if rank == 0:
-            tp = cq_amd.merge_partials(ast, blobs)
-            if not tp:
-                raise RuntimeError(cq_amd.last_error())
-        return tp, scan_ms
+        tp = scan_partitioned(ast, table)      # partial, RCCL gather, merge on rank 0
+        return tp, cq_amd.stats()["scan_ms"]   # the merge runs no scan: still this rank's partial
 
     for _ in range(args.warmup):
         tp, _ = step()

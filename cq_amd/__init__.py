@@ -41,6 +41,14 @@ def lib():
         L.cqgpu_table_from_bytes.restype = C.c_void_p
         L.cqgpu_table_from_bytes.argtypes = [C.c_void_p, C.c_size_t, abi.CsvConfig, C.c_uint64,
                                              C.c_char_p, C.c_size_t]
+        L.cqgpu_table_open_range.restype = C.c_void_p
+        L.cqgpu_table_open_range.argtypes = [C.c_char_p, abi.CsvConfig, C.c_int, C.c_int]
+        L.cqgpu_range_bounds.restype = C.c_int
+        L.cqgpu_range_bounds.argtypes = [C.c_void_p, C.c_size_t, abi.CsvConfig, C.c_int, C.c_int,
+                                         C.POINTER(C.c_uint64), C.POINTER(C.c_uint64),
+                                         C.POINTER(C.c_uint64), C.POINTER(C.c_uint64)]
+        L.cqgpu_table_base_offset.restype = C.c_uint64
+        L.cqgpu_table_base_offset.argtypes = [C.c_void_p]
         L.cqgpu_table_free.argtypes = [C.c_void_p]
         L.cqgpu_table_bytes.restype = C.c_size_t
         L.cqgpu_table_bytes.argtypes = [C.c_void_p]
@@ -95,9 +103,18 @@ class Table:
                                          base_offset, header, len(header) if header else 0)
         return cls(h)
 
+    @classmethod
+    def open_range(cls, path: str, rank: int, nranks: int, cfg: abi.CsvConfig | None = None) -> "Table":
+        """rank's newline-snapped byte range of the file (cqgpu_table_open_range)"""
+        return cls(lib().cqgpu_table_open_range(path.encode(), cfg or abi.csv_config(), rank, nranks))
+
     @property
     def nbytes(self) -> int:
         return lib().cqgpu_table_bytes(self.handle)
+
+    @property
+    def base_offset(self) -> int:
+        return lib().cqgpu_table_base_offset(self.handle)
 
     def close(self):
         if self.handle:
@@ -109,6 +126,16 @@ class Table:
             self.close()
         except Exception:
             pass
+
+
+def range_bounds(data: bytes, rank: int, nranks: int, cfg: abi.CsvConfig | None = None):
+    """(lo, hi, header_lo, header_hi) of rank's range (cqgpu_range_bounds; host code only)"""
+    lo, hi, hl, hh = C.c_uint64(), C.c_uint64(), C.c_uint64(), C.c_uint64()
+    buf = C.c_char_p(data)
+    if lib().cqgpu_range_bounds(C.cast(buf, C.c_void_p), len(data), cfg or abi.csv_config(), rank, nranks,
+                                C.byref(lo), C.byref(hi), C.byref(hl), C.byref(hh)) != 0:
+        raise ValueError("cqgpu_range_bounds: bad arguments")
+    return lo.value, hi.value, hl.value, hh.value
 
 
 def _tables_arg(tables):

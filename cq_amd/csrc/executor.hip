@@ -2474,6 +2474,49 @@ cqgpu_table* open_table(const char* path, cq_csv_config cfg) {
     return t;
 }
 
+// ---- range partition (multi-GPU scans) -----------------
+bool is_term(uint8_t b) { return b == '\n' || b == '\r'; }
+
+// header record [hl, hh) (csv_load: first non-empty line, csv_reader.c:411-419) and
+// the first byte after it and its terminator run (the data region's start)
+void header_span(const uint8_t* d, uint64_t n, uint64_t* hl, uint64_t* hh, uint64_t* data0) {
+    uint64_t p = 0;
+    while (p < n && is_term(d[p])) p++;
+    *hl = p;
+    while (p < n && !is_term(d[p])) p++;
+    *hh = p;
+    while (p < n && is_term(d[p])) p++;
+    *data0 = p;
+}
+
+// the record start at or after the nominal cut c: the byte after the next
+// terminator run (c itself when the byte before it ends a record)
+uint64_t snap_cut(const uint8_t* d, uint64_t n, uint64_t c) {
+    if (c >= n) return n;
+    uint64_t s = c;
+    if (!(s > 0 && is_term(d[s - 1])))
+        while (s < n && !is_term(d[s])) s++;
+    while (s < n && is_term(d[s])) s++;
+    return s;
+}
+
+void range_bounds(const uint8_t* d, uint64_t n, const cq_csv_config& cfg, int rank, int nranks, uint64_t* lo,
+                  uint64_t* hi, uint64_t* hl, uint64_t* hh) {
+    uint64_t data0;
+    header_span(d, n, hl, hh, &data0);
+    if (!cfg.has_header) data0 = 0;          // every line is data; the first one still names the columns
+    const uint64_t span = n - data0;
+    auto cut = [&](int r) -> uint64_t {
+        if (r <= 0) return 0;
+        if (r >= nranks) return n;
+        const uint64_t c = data0 + (uint64_t)((unsigned __int128)span * (unsigned)r / (unsigned)nranks);
+        return std::max(snap_cut(d, n, c), data0);
+    };
+    *lo = cut(rank);
+    *hi = cut(rank + 1);
+    if (*hi < *lo) *hi = *lo;
+}
+
 // ---- device-resident table cache of the drop-in entry point -----------------
 // The reference re-reads and re-parses the file on every query (csv_load per
 // evaluate_query, evaluator_joins.c:219 for joins).  evaluate_query keeps the
@@ -2618,6 +2661,48 @@ cqgpu_table* cqgpu_table_from_bytes(const void* data, size_t n, cq_csv_config cf
         return nullptr;
     }
 }
+
+int cqgpu_range_bounds(const void* data, size_t n, cq_csv_config cfg, int rank, int nranks, uint64_t* lo,
+                       uint64_t* hi, uint64_t* hdr_lo, uint64_t* hdr_hi) {
+    if ((!data && n) || nranks < 1 || rank < 0 || rank >= nranks || !lo || !hi) return -1;
+    uint64_t hl, hh;
+    range_bounds((const uint8_t*)data, n, cfg, rank, nranks, lo, hi, &hl, &hh);
+    if (hdr_lo) *hdr_lo = hl;
+    if (hdr_hi) *hdr_hi = hh;
+    return 0;
+}
+
+cqgpu_table* cqgpu_table_open_range(const char* path, cq_csv_config cfg, int rank, int nranks) {
+    g_err.clear();
+    if (nranks < 1 || rank < 0 || rank >= nranks) {
+        set_err("cq_amd: bad range %d of %d", rank, nranks);
+        return nullptr;
+    }
+    int fd = open(path, O_RDONLY);
+    if (fd < 0) { set_err("Error loading file: %s", path); return nullptr; }
+    struct stat sb;
+    if (fstat(fd, &sb) < 0 || sb.st_size == 0) { close(fd); set_err("Error loading file: %s", path); return nullptr; }
+    const size_t n = (size_t)sb.st_size;
+    void* m = mmap(nullptr, n, PROT_READ, MAP_PRIVATE, fd, 0);
+    close(fd);
+    if (m == MAP_FAILED) { set_err("Error loading file: %s", path); return nullptr; }
+    const uint8_t* d = (const uint8_t*)m;
+    uint64_t lo, hi, hl, hh;
+    range_bounds(d, n, cfg, rank, nranks, &lo, &hi, &hl, &hh);
+    madvise((void*)d, n, MADV_NORMAL);
+    cqgpu_table* t = nullptr;
+    try {
+        if (lo == 0) t = upload(d, hi, cfg, 0, nullptr, 0);
+        else t = upload(d + lo, hi - lo, cfg, lo, (const char*)d + hl, hh - hl);
+    } catch (HipError& e) {
+        set_err("cq_amd: %s", e.msg.c_str());
+        t = nullptr;
+    }
+    munmap(m, n);
+    return t;
+}
+
+uint64_t cqgpu_table_base_offset(const cqgpu_table* t) { return t ? t->base_offset : 0; }
 
 // ---- join-key repartition (multi-GPU JOIN) -----------------------------------
 int cqgpu_route_plan(cq_node* q, cqgpu_table* const* tables, int ntables, int side, int nranks,

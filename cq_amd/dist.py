@@ -63,6 +63,24 @@ def exclusive_base(count: int, device: torch.device | str = "cpu") -> int:
     return sum(int(x.item()) for x in allc[: dist.get_rank()])
 
 
+def scan_partitioned(ast, table, comm_device: torch.device | str | None = None):
+    """One range-partitioned query step (config 4): this rank's partial over its
+    shard (cqgpu_query_partial), the blobs gathered (RCCL all_gather on a device
+    group, gloo with comm_device="cpu"), merged on rank 0 (cqgpu_merge_partials).
+    Returns the result pointer on rank 0 (free with cq_amd.result_free), None on
+    the other ranks.  Every rank must call it (collectives inside)."""
+    import cq_amd
+    comm = torch.device(comm_device) if comm_device is not None else torch.device("cuda", torch.cuda.current_device())
+    blob = cq_amd.query_partial(ast, [table])
+    blobs = gather_blobs(blob, comm)
+    if dist.get_rank() != 0:
+        return None
+    tp = cq_amd.merge_partials(ast, blobs)
+    if not tp:
+        raise RuntimeError(cq_amd.last_error() or "cqgpu_merge_partials failed")
+    return tp
+
+
 def join_partitioned(ast, lshard, rshard, lheader: bytes, rheader: bytes, device: torch.device | str,
                      comm_device: torch.device | str | None = None):
     """Repartitioned INNER JOIN over this rank's shards of both inputs.

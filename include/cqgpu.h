@@ -57,6 +57,24 @@ cqgpu_table* cqgpu_table_open(const char* path, cq_csv_config cfg);
  * when the shard does not start at the file start (NULL otherwise). */
 cqgpu_table* cqgpu_table_from_bytes(const void* data, size_t n, cq_csv_config cfg,
                                     uint64_t base_offset, const char* header, size_t header_len);
+/* ---- range partition of one file over nranks GPUs ---
+ * The data region (after the header record) is cut into nranks equal byte
+ * ranges; every cut is snapped to the byte after the next run of '\n' / '\r'
+ * (records split on any terminator, quote-blind, reference csv_reader.c:404-408),
+ * so each record lies in exactly one range.  Rank 0's range starts at byte 0
+ * (leading blank lines and the header included).  range_bounds is pure host
+ * code (no device); it writes rank `rank`'s [*lo, *hi) and the header record
+ * [*hdr_lo, *hdr_hi) (empty when cfg.has_header is false and the file has no
+ * records).  Returns 0, or -1 on bad arguments. */
+int cqgpu_range_bounds(const void* data, size_t n, cq_csv_config cfg, int rank, int nranks,
+                       uint64_t* lo, uint64_t* hi, uint64_t* hdr_lo, uint64_t* hdr_hi);
+/* mmap `path` and upload rank `rank`'s range of it (with its whole-file base
+ * offset and the header record) to the current HIP device: the shard each rank
+ * scans with cqgpu_query_partial before cqgpu_merge_partials. */
+cqgpu_table* cqgpu_table_open_range(const char* path, cq_csv_config cfg, int rank, int nranks);
+/* whole-file byte offset of a table's first byte (0 unless it is a shard) */
+uint64_t cqgpu_table_base_offset(const cqgpu_table* t);
+
 void cqgpu_table_free(cqgpu_table* t);
 size_t cqgpu_table_bytes(const cqgpu_table* t);
 int cqgpu_table_ncols(const cqgpu_table* t);

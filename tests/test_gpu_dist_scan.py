@@ -1,0 +1,88 @@
+"""bench.py's N > 1 step in real processes: two ranks on one GPU.
+
+Each rank opens its newline-snapped range of one file (cqgpu_table_open_range),
+runs cq_amd.dist.scan_partitioned -- the function bench.py times at N > 1
+(cqgpu_query_partial, gather_blobs, cqgpu_merge_partials on rank 0) -- over a
+gloo group (RCCL needs one GPU per rank), and rank 0's result must equal the
+oracle on the whole file for the config-3 query.
+"""
+import os
+import socket
+
+import pytest
+import torch.multiprocessing as mp
+
+import cqtest
+from cq_amd import datagen
+
+pytestmark = pytest.mark.gpu
+
+SQL = "SELECT role, COUNT(*), SUM(height), AVG(height) FROM '{p}' WHERE age > 30 GROUP BY role"
+
+
+def _free_port():
+    s = socket.socket()
+    s.bind(("127.0.0.1", 0))
+    p = s.getsockname()[1]
+    s.close()
+    return p
+
+
+def _worker(rank, world, port, path, q):
+    import sys
+    sys.path.insert(0, os.path.dirname(os.path.abspath(__file__)))
+    import torch
+    import torch.distributed as dist
+    os.environ["MASTER_ADDR"] = "127.0.0.1"
+    os.environ["MASTER_PORT"] = str(port)
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    try:
+        torch.cuda.set_device(0)
+        import cqtest as ct
+        import cq_amd
+        from cq_amd import abi
+        from cq_amd.dist import scan_partitioned
+        t = cq_amd.Table.open_range(path, rank, world)
+        with ct.Parsed(SQL.format(p=path)) as ast:
+            tp = None
+            for _ in range(2):                 # a warm-up step, then the checked one
+                if tp:
+                    cq_amd.result_free(tp)
+                tp = scan_partitioned(ast, t, "cpu")
+        t.close()
+        if rank == 0:
+            res = abi.table_to_py(tp)
+            cq_amd.result_free(tp)
+            q.put((rank, res, None))
+        else:
+            q.put((rank, tp is None, None))
+    except Exception as e:   # reported to the parent
+        q.put((rank, None, repr(e)))
+    finally:
+        dist.destroy_process_group()
+
+
+@pytest.mark.parametrize("world", [2])
+def test_bench_step_two_processes(tmp_path, world):
+    path = str(tmp_path / "big.csv")
+    datagen.write_logical(path, 400_000, seed=42, with_role=True)
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    port = _free_port()
+    procs = [ctx.Process(target=_worker, args=(r, world, port, path, q)) for r in range(world)]
+    for p in procs:
+        p.start()
+    out = {}
+    for _ in range(world):
+        rank, res, err = q.get(timeout=110)
+        assert err is None, f"rank {rank}: {err}"
+        out[rank] = res
+    for p in procs:
+        p.join(timeout=30)
+        assert p.exitcode == 0
+    assert out[1] is True
+    want, unsup = cqtest.oracle_query(SQL.format(p=path))
+    assert not unsup
+    from test_gpu_parity import compare
+    compare(out[0], want, {2, 3}, "2-process config-3 step")
+    assert len(want["rows"]) == 1000

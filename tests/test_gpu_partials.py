@@ -1,9 +1,15 @@
-"""Range-partitioned aggregation: per-shard cqgpu_query_partial + cqgpu_merge_partials
-must give exactly the whole-table answer (SUM/AVG within 1e-6 relative).
+"""Range-partitioned aggregation (SURVEY.md section 8e, config 4 on one GPU).
 
-The shards split one synthetic file at record boundaries; each is uploaded with
-its whole-file base offset and the header bytes, as bench.py does per rank.
+Every "rank" opens its own newline-snapped byte range of one file with the
+product entry point (cqgpu_table_open_range), runs cqgpu_query_partial on it,
+and cqgpu_merge_partials over all ranks' blobs must equal the ORACLE's answer on
+the whole file (oracle/cq_oracle.c, pinned to the reference): counts, group set,
+first-appearance order, MIN/MAX and representative cells exact, SUM/AVG within
+1e-6 relative.  Files carry CR, CRLF and blank-line runs, so cuts land on them.
 """
+import os
+import random
+
 import pytest
 
 import cqtest
@@ -14,51 +20,101 @@ from test_gpu_parity import compare, tolerant_columns
 pytestmark = pytest.mark.gpu
 
 QUERIES = [
-    "SELECT role, COUNT(*), SUM(height), AVG(height) FROM 'x' WHERE age > 30 GROUP BY role",
-    "SELECT COUNT(*), SUM(height), MIN(height), MAX(age) FROM 'x' WHERE gender = 'f'",
-    "SELECT name, COUNT(*), MIN(role), MAX(role) FROM 'x' GROUP BY name",
-    "SELECT age, COUNT(*) FROM 'x' GROUP BY age HAVING COUNT(*) > 1900 ORDER BY COUNT(*) DESC LIMIT 5",
-    "SELECT gender, AVG(age) FROM 'x' WHERE role LIKE 'role_0%' GROUP BY gender",
+    "SELECT role, COUNT(*), SUM(height), AVG(height) FROM '{p}' WHERE age > 30 GROUP BY role",
+    "SELECT COUNT(*), SUM(height), MIN(height), MAX(age) FROM '{p}' WHERE gender = 'f'",
+    "SELECT name, COUNT(*), MIN(role), MAX(role) FROM '{p}' GROUP BY name",
+    "SELECT age, COUNT(*) FROM '{p}' GROUP BY age HAVING COUNT(*) > 1900 ORDER BY COUNT(*) DESC LIMIT 5",
+    "SELECT gender, AVG(age) FROM '{p}' WHERE role LIKE 'role_0%' GROUP BY gender",
+    "SELECT COUNT(*) FROM '{p}' WHERE age > 30",
 ]
 
 
+def _mixed_terminators(data: bytes, seed: int) -> bytes:
+    """the same records with every terminator replaced by a random run"""
+    rng = random.Random(seed)
+    runs = [b"\n", b"\r\n", b"\r", b"\n\n", b"\r\n\r\n", b"\n\r"]
+    lines = data.split(b"\n")
+    out = []
+    for i, ln in enumerate(lines):
+        out.append(ln)
+        if i + 1 < len(lines):
+            out.append(rng.choice(runs) if i > 0 else b"\n")
+    return b"\r\n\n" + b"".join(out)
+
+
 @pytest.fixture(scope="module")
-def shards():
-    data = datagen.shape_a_bytes(120_000, seed=11, with_role=True)
-    header, body = data.split(b"\n", 1)
-    header += b"\n"
-    cuts = [0]
-    for frac in (0.31, 0.64):
-        i = body.index(b"\n", int(len(body) * frac)) + 1
-        cuts.append(i)
-    cuts.append(len(body))
-    pieces = [body[a:b] for a, b in zip(cuts, cuts[1:])]
-    whole = cq_amd.Table.from_bytes(data)
-    parts = []
-    base = 0
-    for i, pc in enumerate(pieces):
-        if i == 0:
-            parts.append(cq_amd.Table.from_bytes(header + pc))
-            base = len(header) + len(pc)
-        else:
-            parts.append(cq_amd.Table.from_bytes(pc, base_offset=base, header=header))
-            base += len(pc)
-    yield whole, parts
-    whole.close()
-    for p in parts:
-        p.close()
+def files(tmp_path_factory):
+    d = tmp_path_factory.mktemp("ranges")
+    plain = datagen.shape_a_bytes(120_000, seed=11, with_role=True)
+    paths = {}
+    for name, data in (("plain", plain), ("mixed", _mixed_terminators(datagen.shape_a_bytes(30_000, seed=12,
+                                                                                              with_role=True), 3))):
+        p = os.path.join(str(d), name + ".csv")
+        with open(p, "wb") as fh:
+            fh.write(data)
+        paths[name] = p
+    return paths
+
+
+def _merged(ast, path, nranks):
+    tabs = [cq_amd.Table.open_range(path, r, nranks) for r in range(nranks)]
+    try:
+        sizes = [t.nbytes for t in tabs]
+        assert sum(sizes) == os.path.getsize(path)
+        blobs = [cq_amd.query_partial(ast, [t]) for t in tabs]
+    finally:
+        for t in tabs:
+            t.close()
+    tp = cq_amd.merge_partials(ast, blobs)
+    assert tp, cq_amd.last_error()
+    got = abi.table_to_py(tp)
+    cq_amd.result_free(tp)
+    return got
 
 
 @pytest.mark.parametrize("sql", QUERIES)
-def test_merge_equals_whole(shards, sql):
-    whole, parts = shards
-    with cqtest.Parsed(sql) as ast:
-        want = cq_amd.query(ast, [whole])
-        assert want is not None, cq_amd.last_error()
-        blobs = [cq_amd.query_partial(ast, [p]) for p in parts]
-        tp = cq_amd.merge_partials(ast, blobs)
-        assert tp, cq_amd.last_error()
-        got = abi.table_to_py(tp)
-        cq_amd.result_free(tp)
+@pytest.mark.parametrize("nranks", [1, 3, 8])
+def test_merge_equals_oracle(files, sql, nranks):
+    path = files["plain"]
+    q = sql.format(p=path)
+    want, unsup = cqtest.oracle_query(q)
+    assert not unsup and want is not None
+    with cqtest.Parsed(q) as ast:
+        got = _merged(ast, path, nranks)
         tol = tolerant_columns(ast)
-    compare(got, want, tol, sql)
+    compare(got, want, tol, f"{nranks} ranks: {q}")
+
+
+@pytest.mark.parametrize("nranks", [2, 5, 7, 16])
+def test_mixed_terminator_cuts(files, nranks):
+    path = files["mixed"]
+    for sql in QUERIES[:3]:
+        q = sql.format(p=path)
+        want, unsup = cqtest.oracle_query(q)
+        assert not unsup and want is not None
+        with cqtest.Parsed(q) as ast:
+            got = _merged(ast, path, nranks)
+            tol = tolerant_columns(ast)
+        compare(got, want, tol, f"{nranks} ranks: {q}")
+
+
+def test_range_bases_are_record_starts(files):
+    path = files["mixed"]
+    data = open(path, "rb").read()
+    for n in (2, 5, 16):
+        for r in range(n):
+            t = cq_amd.Table.open_range(path, r, n)
+            lo, hi, _, _ = cq_amd.range_bounds(data, r, n)
+            assert t.base_offset == lo and t.nbytes == hi - lo
+            t.close()
+
+
+def test_more_ranks_than_records(tmp_path):
+    p = tmp_path / "tiny.csv"
+    p.write_bytes(b"a,b\n1,x\n2,y\n")
+    q = f"SELECT b, COUNT(*), SUM(a) FROM '{p}' GROUP BY b"
+    want, _ = cqtest.oracle_query(q)
+    with cqtest.Parsed(q) as ast:
+        got = _merged(ast, str(p), 9)
+        tol = tolerant_columns(ast)
+    compare(got, want, tol, q)
