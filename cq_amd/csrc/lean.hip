@@ -539,38 +539,65 @@ struct Rec {
     uint32_t sfp[MAXS], sfl[MAXS];
 };
 
-// Field walk of one record from its 64-bit separator view sv and record end e
-// (first terminator bit; 64: beyond the view): the roles' columns come in
-// ascending order, and clearing separator bits one by one visits the field ends
-// in order: before field c's end is cleared, the lowest remaining bit is that
-// end, and the previous one (field c - 1's end) is its start - 1.  A column past
-// the record's end is missing (length 0: NULL); a field the view cannot bound
-// fails the fast path.  The columns are uniform: the clearing loop is scalar.
+// Field walk of a record from its 64-bit separator view sv and record end e (first
+// terminator bit; 64: beyond the view): the roles' columns come in ascending
+// order, and clearing separator bits one by one visits the field ends in order:
+// before field c's end is cleared, the lowest remaining bit is that end, and the
+// previous one (field c - 1's end) is its start - 1.  A column past the record's
+// end is missing (length 0: NULL); a field the view cannot bound fails the fast
+// path.
+// The same walk for both records of a lane at once, with the roles addressed by
+// their rank in column order: skip[k] = separators between role k - 1's field end
+// and role k's field start (uniform), so both records' bit-clearing chains run in
+// one scalar loop, and each field lands in its role's registers by selects on
+// the uniform role ranks (kw: WHERE, ks: SUM 0/1, kg: GROUP BY) -- no branch
+// depends on which role a column plays.
 template <int NR, int WM, int NS, bool GROUPED>
-__device__ __forceinline__ void walk(Rec& R, uint64_t sv, uint64_t nv, const uint32_t (&rcol)[KN],
-                                     const uint32_t (&rrole)[KN]) {
-    const uint32_t e = ctz64(nv);
-    uint64_t s = sv;
-    uint32_t done = 0, prev_end = 0xFFFFFFFFu;        // position of separator done - 1 (start - 1 of field done)
+__device__ __forceinline__ void walk2(Rec (&rec)[2], const uint64_t (&sv)[2], const uint64_t (&nv)[2],
+                                      const uint32_t (&skip)[KN], uint32_t kw, const uint32_t (&ks)[MAXS],
+                                      uint32_t kg) {
+    uint64_t s0 = sv[0], s1 = sv[1];
+    const uint32_t e0 = ctz64(nv[0]), e1 = ctz64(nv[1]);
+    uint32_t pe0 = 0xFFFFFFFFu, pe1 = 0xFFFFFFFFu;      // start - 1 of the current field
 #pragma unroll
     for (int k = 0; k < NR; k++) {
-        const uint32_t c = rcol[k];
-        for (; done < c; done++) {
-            prev_end = ctz64(s);
-            s &= s - 1;
+        const uint32_t n = skip[k];
+        if (n > 0) {
+            for (uint32_t i = 1; i < n; i++) {          // fields passed over: only their bits go
+                s0 &= s0 - 1;
+                s1 &= s1 - 1;
+            }
+            pe0 = ctz64(s0);
+            pe1 = ctz64(s1);
+            s0 &= s0 - 1;
+            s1 &= s1 - 1;
         }
-        const uint32_t start = prev_end + 1;           // 0 for column 0
-        const uint32_t end = ctz64(s);
-        const bool gone = start > e;
-        R.fail |= gone ? (e == 64) : (end == 64);
-        const uint32_t fp = R.p + start, fl = gone ? 0u : end - start;
-        const uint32_t l = gone ? e : end;
-        R.lastpos = l > R.lastpos ? l : R.lastpos;
-        const uint32_t role = rrole[k];
-        if (WM != LW_NONE && role == R_WHERE) { R.wfp = fp; R.wfl = fl; }
-        if (NS > 0 && role == R_SUM0) { R.sfp[0] = fp; R.sfl[0] = fl; }
-        if (NS > 1 && role == R_SUM1) { R.sfp[MAXS - 1] = fp; R.sfl[MAXS - 1] = fl; }
-        if (GROUPED && role == R_GROUP) { R.gfp = fp; R.klen = fl; }
+#pragma unroll
+        for (int u = 0; u < 2; u++) {
+            Rec& R = rec[u];
+            const uint32_t start = (u ? pe1 : pe0) + 1, end = ctz64(u ? s1 : s0), e = u ? e1 : e0;
+            const bool gone = start > e;
+            R.fail |= gone ? (e == 64) : (end == 64);
+            const uint32_t fp = R.p + start, fl = gone ? 0u : end - start;
+            const uint32_t l = gone ? e : end;
+            R.lastpos = l > R.lastpos ? l : R.lastpos;
+            if (WM != LW_NONE) {
+                R.wfp = kw == (uint32_t)k ? fp : R.wfp;
+                R.wfl = kw == (uint32_t)k ? fl : R.wfl;
+            }
+            if (NS > 0) {
+                R.sfp[0] = ks[0] == (uint32_t)k ? fp : R.sfp[0];
+                R.sfl[0] = ks[0] == (uint32_t)k ? fl : R.sfl[0];
+            }
+            if (NS > 1) {
+                R.sfp[1] = ks[1] == (uint32_t)k ? fp : R.sfp[1];
+                R.sfl[1] = ks[1] == (uint32_t)k ? fl : R.sfl[1];
+            }
+            if (GROUPED) {
+                R.gfp = kg == (uint32_t)k ? fp : R.gfp;
+                R.klen = kg == (uint32_t)k ? fl : R.klen;
+            }
+        }
     }
 }
 
@@ -618,11 +645,20 @@ __global__ __launch_bounds__(LT) void lean_kernel(const uint8_t* __restrict__ g,
 
     // uniform plan facts
     constexpr int NR = (WM != LW_NONE ? 1 : 0) + NS + (GROUPED ? 1 : 0);   // roles
-    uint32_t rcol[KN], rrole[KN];
+    uint32_t skip[KN];                     // separators before role rank k's field (walk2)
+    uint32_t kw = 0, ks[MAXS] = {0, 0}, kg = 0;   // role ranks of WHERE, SUM 0/1, GROUP BY
 #pragma unroll
     for (int k = 0; k < KN; k++) {
-        rcol[k] = __builtin_amdgcn_readfirstlane(LP.rcol[k]);
-        rrole[k] = __builtin_amdgcn_readfirstlane(LP.rrole[k]);
+        const uint32_t c = __builtin_amdgcn_readfirstlane(LP.rcol[k]);
+        const uint32_t pc = k ? __builtin_amdgcn_readfirstlane(LP.rcol[k - 1]) : 0u;
+        skip[k] = k ? c - pc : c;
+        const uint32_t role = __builtin_amdgcn_readfirstlane(LP.rrole[k]);
+        if (k < NR) {
+            kw = role == R_WHERE ? (uint32_t)k : kw;
+            ks[0] = role == R_SUM0 ? (uint32_t)k : ks[0];
+            ks[1] = role == R_SUM1 ? (uint32_t)k : ks[1];
+            kg = role == R_GROUP ? (uint32_t)k : kg;
+        }
     }
     const uint32_t rep_d = LP.delim * 0x01010101u, rep_q = LP.quote * 0x01010101u;
     const uint64_t lo_ok = LP.lo_ok, hi_ok = LP.hi_ok, last_win = LP.last_win;
@@ -650,6 +686,15 @@ __global__ __launch_bounds__(LT) void lean_kernel(const uint8_t* __restrict__ g,
     Win nx;
     uint64_t w = LP.first_win + (uint64_t)blockIdx.x * NWV + wv;
     if (w < last_win) load_win(g, w, wstr_b, nx);
+#ifndef LEAN_L2PF
+#define LEAN_L2PF 0
+#endif
+    // L2 prefetch of the window LEAN_L2PF windows ahead: one dword per lane every
+    // 64 bytes touches every 128-byte line of it, so its HBM read starts that many
+    // windows before the register load of the same bytes (then an L2 hit).  The
+    // dwords are folded into pf_sink two windows later, so the wait for them comes
+    // after the next register window's anyway, and never change a result.
+    uint32_t pf_sink = 0, pf0 = 0, pf1 = 0;
     for (uint32_t round = 0; w < last_win; round++, w += wstep) {
         const uint64_t ws = w * wstr_b;
 #ifdef LEAN_CLK
@@ -659,6 +704,12 @@ __global__ __launch_bounds__(LT) void lean_kernel(const uint8_t* __restrict__ g,
         LCLK(0);
 #ifndef LEAN_NOMEM   // profiling build LEAN_NOMEM: every window re-processes the first one (no HBM reads)
         if (w + wstep < last_win) load_win(g, w + wstep, wstr_b, nx);
+        if (LEAN_L2PF > 0) {
+            const uint64_t wp = w + (uint64_t)LEAN_L2PF * wstep;
+            pf_sink ^= pf1;
+            pf1 = pf0;
+            if (wp < last_win) pf0 = ((const uint32_t*)(g + wp * wstr_b))[16 * lane];
+        }
 #endif
 
         // ---- stage and classify
@@ -725,17 +776,22 @@ __global__ __launch_bounds__(LT) void lean_kernel(const uint8_t* __restrict__ g,
                 Rr.p = Rr.valid ? W.rs[64 * u + lane] : 0u;
             }
             // ---- role fields (WHERE, SUM 0/1, GROUP BY): position and length (0: NULL / missing)
+            {
+                uint64_t sv[2], nv[2];
 #pragma unroll
-            for (int u = 0; u < 2; u++) {
-                Rec& Rr = rec[u];
-                uint64_t sv, nv;
-                views(W, Rr.p, sv, nv);
-                Rr.fail = !Rr.valid;
-                Rr.lastpos = 0;
-                Rr.wfp = Rr.p; Rr.wfl = 0; Rr.gfp = Rr.p; Rr.klen = 0;
+                for (int u = 0; u < 2; u++) {
+                    views(W, rec[u].p, sv[u], nv[u]);
+                    rec[u].fail = !rec[u].valid;
+                    rec[u].lastpos = 0;
+                }
 #pragma unroll
-                for (int j = 0; j < MAXS; j++) { Rr.sfp[j] = Rr.p; Rr.sfl[j] = 0; }
-                walk<NR, WM, NS, GROUPED>(Rr, sv, nv, rcol, rrole);
+                for (int u = 0; u < 2; u++) {
+                    Rec& Rr = rec[u];
+                    Rr.wfp = Rr.p; Rr.wfl = 0; Rr.gfp = Rr.p; Rr.klen = 0;
+#pragma unroll
+                    for (int j = 0; j < MAXS; j++) { Rr.sfp[j] = Rr.p; Rr.sfl[j] = 0; }
+                }
+                walk2<NR, WM, NS, GROUPED>(rec, sv, nv, skip, kw, ks, kg);
             }
             // a quote at or before the last byte examined may hide separators
             if (wq) {
@@ -1042,6 +1098,8 @@ __global__ __launch_bounds__(LT) void lean_kernel(const uint8_t* __restrict__ g,
         }
         LCLK(6);
     }
+    if (LEAN_L2PF > 0 && (pf_sink ^ pf0 ^ pf1) == 0x9E3779B9u && lane == 63 && n_rec == 0x9E3779B9ull)
+        stats->clk[7] = 1;       // keeps the prefetch loads (never true in practice)
 #ifdef LEAN_CLK
     if (lane == 0)
         for (int i = 0; i < 8; i++) atomicAdd(&stats->clk[i], (unsigned long long)clk_[i]);

@@ -26,7 +26,7 @@ for it in range(3):
     st = cq_amd.stats()
     clk = (C.c_ulonglong * 8)()
     L.cqgpu_debug_clocks(clk)
-windows = (len(data) + 1951) // 1952
+windows = (len(data) + 3967) // 3968
 tot = sum(clk)
 print(f"rows {rows} scan_ms {st['scan_ms']:.3f} grid {st['grid']} windows {windows}")
 for i, n in enumerate(names[:7]):

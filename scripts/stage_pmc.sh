@@ -20,7 +20,7 @@ for v in ${VARIANTS:-base}; do
 import collections, csv, glob, json, sys
 out, v = sys.argv[1], sys.argv[2]
 d = json.load(open(f"{out}/{v}.json"))
-nb = d["config"]["bytes_per_gpu"]; wins = nb / 1952.0
+nb = d["config"]["bytes_per_gpu"]; wins = nb / 3968.0
 tot = collections.defaultdict(lambda: collections.defaultdict(float))
 for f in glob.glob(f"{out}/pmc_{v}/**/*counter_collection.csv", recursive=True):
     for r in csv.DictReader(open(f)):
@@ -28,7 +28,7 @@ for f in glob.glob(f"{out}/pmc_{v}/**/*counter_collection.csv", recursive=True):
             tot[r["Counter_Name"]][r["Dispatch_Id"]] += float(r["Counter_Value"])
 a = {c: sum(x.values()) / len(x) / wins for c, x in tot.items()}
 wc = a.get("SQ_WAVE_CYCLES", 1)
-print(f"{v:6s} {d['roofline']['kernel_ms']:.3f} ms | per 1952B: VALU {a.get('SQ_INSTS_VALU',0):.0f} SALU {a.get('SQ_INSTS_SALU',0):.0f} "
+print(f"{v:6s} {d['roofline']['kernel_ms']:.3f} ms | per 3968B: VALU {a.get('SQ_INSTS_VALU',0):.0f} SALU {a.get('SQ_INSTS_SALU',0):.0f} "
       f"LDS {a.get('SQ_INSTS_LDS',0):.1f} bankconf {a.get('SQ_LDS_BANK_CONFLICT',0):.0f} | wait {a.get('SQ_WAIT_ANY',0)/wc:.2f} "
       f"waitinst {a.get('SQ_WAIT_INST_ANY',0)/wc:.2f} active {a.get('SQ_ACTIVE_INST_ANY',0)/wc:.2f} wavecyc {wc:.0f}")
 PY
