@@ -20,9 +20,11 @@
 #if defined(__HIPCC__)
 #include <hip/hip_runtime.h>
 #define CQ_HD __device__ __forceinline__
+#define CQ_HDM __device__ __forceinline__     // member functions
 #define CQ_POW5_ATTR static __device__
 #else
 #define CQ_HD static inline
+#define CQ_HDM inline
 #define CQ_POW5_ATTR static
 #endif
 
@@ -519,7 +521,7 @@ CQ_HD bool like(const uint8_t* s, uint32_t sl, const uint8_t* p, uint32_t pl, bo
 // INT the value, DBL sign + round-half-even(|x|*1e6) below 2^43 where the text
 // is exact, and the value itself above (GK_BIG), where distinct doubles never
 // share a text.
-enum : uint32_t { GK_STR = 0, GK_INT = 1, GK_DBL = 2, GK_BIG = 3, GK_LONG = 5, GK_ALL = 7 };
+enum : uint32_t { GK_STR = 0, GK_INT = 1, GK_DBL = 2, GK_BIG = 3, GK_COMP = 4, GK_LONG = 5, GK_ALL = 7 };
 
 // A group key in 16 bytes + class/length.  Text keys of at most 16 bytes (all
 // NULL and DATE keys, most strings) are stored inline, little-endian, zero
@@ -639,6 +641,48 @@ CQ_HD uint64_t gk_hash(const GKey& k) {
     const uint64_t x = a ^ (a >> 29) ^ (k.w1 * 0x9E3779B97F4A7C15ULL) ^ ((uint64_t)gk_clslen(k) << 7);
     const uint64_t h = x * 0xD6E8FEB86659FD93ULL;
     return (h >> 40) | (h << 24);
+}
+
+// Composite GROUP BY key (evaluator.c:113-212): the reference joins the parts'
+// key texts with '\t' and groups by the joined text.  Here the key is a 128-bit
+// digest of the parts' canonical keys (GK_COMP, len = part count): exact parts
+// (inline text, numbers, dates) enter with their whole identity, long text parts
+// with two independent 64-bit content hashes.  Equal texts give equal digests;
+// unequal ones collide with probability ~2^-128 per pair.  A text part holding a
+// tab could make two different part lists join to the same text, so kernels flag
+// it and the host refuses the plan.
+CQ_HD uint64_t bytes_hash2(const uint8_t* p, uint32_t n) {
+    uint64_t h = 0x2545F4914F6CDD1DULL ^ n;
+    for (uint32_t i = 0; i < n; i++) h = (h ^ p[i]) * 0x100000001B3ULL + (h >> 29);
+    return mix64(h);
+}
+struct CompKey {
+    uint64_t a = 0x6A09E667F3BCC908ULL, b = 0xBB67AE8584CAA73BULL;
+    CQ_HDM void add(const GKey& k) {
+        uint64_t x0 = k.w0, x1 = k.w1;
+        if (k.cls == GK_LONG) x0 = bytes_hash2((const uint8_t*)(uintptr_t)k.w0, k.len);   // w1: FNV of the bytes
+        const uint64_t t = ((uint64_t)gk_clslen(k) << 1) | 1;
+        a = mix64(a ^ t) ^ x0;
+        a = mix64(a ^ (x1 * 0x9E3779B97F4A7C15ULL));
+        b = mix64(b + x1) ^ (t * 0xC2B2AE3D27D4EB4FULL);
+        b = mix64(b ^ (x0 + 0x165667B19E3779F9ULL));
+    }
+};
+CQ_HD GKey comp_key(const CompKey& c, uint32_t nparts) {
+    GKey k;
+    k.cls = GK_COMP;
+    k.len = nparts;
+    k.w0 = c.a;
+    k.w1 = c.b;
+    return k;
+}
+CQ_HD bool text_has_tab(const Cell& c) {
+    if (c.kind != K_STR) return false;
+    const uint8_t* p = (const uint8_t*)(uintptr_t)c.bits;
+    const uint32_t n = c.len < 255 ? c.len : 255;
+    for (uint32_t i = 0; i < n; i++)
+        if (p[i] == '\t') return true;
+    return false;
 }
 
 CQ_HD bool gk_equal(const GKey& a, const GKey& b) {

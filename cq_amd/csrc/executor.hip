@@ -50,6 +50,7 @@ hipError_t cq_launch_gather(const uint8_t* g, const ScanPlan* P, const unsigned 
 hipError_t cq_launch_copy_strings(const Cell* cells, uint32_t n, const unsigned long long* offs,
                                   uint8_t* out, hipStream_t s);
 cq::Cell cq_host_parse_cell(const uint8_t* text, uint32_t len);
+cq::Cell cq_host_eval(const cq::Insn* code, uint32_t n, const cq::Cell* cols, const cq::Cell* consts);
 hipError_t cq_launch_cells(const uint8_t* g, const unsigned long long* recs, uint32_t n, const cq::ColsDesc* D,
                            cq::Cell* out, hipStream_t s);
 hipError_t cq_launch_join_code(const cq::Cell* cells, uint32_t stride, uint32_t kcol, uint32_t n,
@@ -568,7 +569,7 @@ std::vector<HCell> fetch_cells(DevCtx& c, const std::vector<Cell>& cells) {
 }
 
 // ------------------------------------------------------------------ compiled plan
-enum OutKind { OUT_COUNT, OUT_SUM, OUT_AVG, OUT_EXT, OUT_REP, OUT_CONST, OUT_NULL, OUT_VLA };
+enum OutKind { OUT_COUNT, OUT_SUM, OUT_AVG, OUT_EXT, OUT_REP, OUT_CONST, OUT_NULL, OUT_VLA, OUT_HEXPR };
 struct OutCol {
     OutKind kind = OUT_NULL;
     int acc = -1;          // accumulator index for SUM/AVG/EXT
@@ -588,6 +589,10 @@ struct Compiled {
     int max_depth = 0;
     int group_col = -1;              // csv column of the GROUP BY key
     std::vector<std::pair<int, int>> vla;   // STDDEV (0) / MEDIAN (1) and their csv column
+    int where_len = -1;              // WHERE program length when group expressions follow it
+    // expression items evaluated on the host over each group's first-row cells:
+    // OP_COL b = rep slot, OP_CONST b = literal index (C.lits)
+    std::vector<std::vector<Insn>> hexpr;
 };
 
 struct Compiler {
@@ -835,8 +840,10 @@ void finish_plan(const cqgpu_table* t, Compiled& C, Compiler& cc) {
     }
     for (int a = 0; a < C.P.nacc; a++) C.P.acc[a].slot = (uint8_t)remap[C.P.acc[a].slot];
     if (C.P.group_slot >= 0) C.P.group_slot = remap[C.P.group_slot];
+    for (int g = 0; g < C.P.ngpart; g++)
+        if (C.P.gpart_slot[g] >= 0) C.P.gpart_slot[g] = (int16_t)remap[C.P.gpart_slot[g]];
     C.need_cols = sorted;
-    C.P.nprog = (int)cc.code.size();
+    C.P.nprog = C.where_len >= 0 ? C.where_len : (int)cc.code.size();
     std::copy(cc.code.begin(), cc.code.end(), C.P.prog);
     C.P.nconst = (int)C.lits.size();
     C.P.delim = (uint8_t)t->cfg.delimiter;
@@ -860,14 +867,21 @@ void compile_aggregate(const cqgpu_table* t, cq_node* q, Compiled& C) {
     if (q->u.q.where) {
         cc.cond(q->u.q.where);
     }
+    C.where_len = (int)cc.code.size();
     cq_node* gb = q->u.q.group_by;
     C.grouped = gb && gb->kind == CQ_N_GROUP_BY && gb->u.grp.keys && gb->u.grp.nkeys > 0;
     C.P.group_slot = -1;
+    C.P.ngpart = 0;
     if (C.grouped) {
-        if (gb->u.grp.nkeys != 1) throw Ineligible{"multi-column GROUP BY"};
-        const char* key = gb->u.grp.keys[0];
+        // a GROUP BY name matching a SELECT alias groups by that item's expression
+        // (evaluator.c:71-98)
+        const int nk = gb->u.grp.nkeys;
+        if (nk > MAX_GPART) throw Ineligible{"GROUP BY of more than 4 parts"};
+        std::vector<cq_node*> gexpr(nk, nullptr);
         cq_node* sel = q->u.q.select;
-        if (sel && sel->kind == CQ_N_SELECT && sel->u.sel.exprs) {
+        for (int g = 0; g < nk; g++) {
+            const char* key = gb->u.grp.keys[g];
+            if (!key || !sel || sel->kind != CQ_N_SELECT || !sel->u.sel.exprs) continue;
             for (int i = 0; i < sel->u.sel.count; i++) {
                 const char* cs = sel->u.sel.texts[i];
                 if (!cs) continue;
@@ -875,13 +889,34 @@ void compile_aggregate(const cqgpu_table* t, cq_node* q, Compiled& C) {
                 if (!as) continue;
                 const char* a = as + 4;
                 while (*a && is_space((unsigned char)*a)) a++;
-                if (key && !strcasecmp(a, key)) throw Ineligible{"GROUP BY a SELECT alias"};
+                if (!strcasecmp(a, key)) { gexpr[g] = sel->u.sel.exprs[i]; break; }
             }
         }
-        int gc = col_index_fallback(t, key);
-        C.group_col = gc;
-        if (gc < 0) C.group_missing = true;
-        else C.P.group_slot = cc.need(gc);
+        if (nk == 1 && !gexpr[0]) {                     // create_groups (find_column_index_with_fallback)
+            int gc = col_index_fallback(t, gb->u.grp.keys[0]);
+            C.group_col = gc;
+            if (gc < 0) C.group_missing = true;
+            else C.P.group_slot = cc.need(gc);
+        } else {
+            // create_groups_by_expression, or the composite key: expressions by the
+            // WHERE VM (code after the WHERE program), columns by csv_get_column_index
+            // -- no table-prefix fallback on this path (evaluator.c:152), a missing
+            // column is the part "NULL"
+            C.P.ngpart = nk;
+            for (int g = 0; g < nk; g++) {
+                C.P.gcode_off[g] = (uint16_t)cc.code.size();
+                if (gexpr[g]) {
+                    const int d0 = cc.depth;
+                    cc.expr(gexpr[g]);
+                    cc.depth = d0;
+                    C.P.gpart_slot[g] = -1;
+                } else {
+                    const int col = col_index(t, gb->u.grp.keys[g]);
+                    C.P.gpart_slot[g] = (int16_t)(col >= 0 ? cc.need(col) : -2);
+                }
+            }
+            C.P.gcode_off[nk] = (uint16_t)cc.code.size();
+        }
     }
     cq_node* sel = q->u.q.select;
     int nsel = sel ? sel->u.sel.count : 0;
@@ -938,7 +973,29 @@ void compile_aggregate(const cqgpu_table* t, cq_node* q, Compiled& C) {
         cq_node* node = sel->u.sel.exprs ? sel->u.sel.exprs[i] : nullptr;
         if (node && node->kind != CQ_N_IDENTIFIER) {
             if (node->kind == CQ_N_LITERAL) { oc.kind = OUT_CONST; oc.lit = cc.lit(node->u.text); C.outs.push_back(oc); continue; }
-            throw Ineligible{"expression column in an aggregate SELECT"};
+            // an expression on the group's first row (evaluator_aggregates.c:669-677):
+            // compiled by a scratch compiler, its columns become representative cells
+            Compiled T;
+            Compiler tc{t, q, alias, T};
+            tc.lit_cap = MAX_CONST - (int)C.lits.size();
+            tc.need_cap = MAX_NEED;
+            tc.expr(node);
+            std::vector<Insn> code = tc.code;
+            for (auto& in : code) {
+                if (in.op == OP_COL) {
+                    const int col = in.b;
+                    auto it = std::find(C.rep_cols.begin(), C.rep_cols.end(), col);
+                    if (it == C.rep_cols.end()) { C.rep_cols.push_back(col); in.b = (uint16_t)(C.rep_cols.size() - 1); }
+                    else in.b = (uint16_t)(it - C.rep_cols.begin());
+                } else if (in.op == OP_CONST) {
+                    in.b = (uint16_t)cc.lit(T.lits[in.b].c_str());
+                }
+            }
+            oc.kind = OUT_HEXPR;
+            oc.acc = (int)C.hexpr.size();
+            C.hexpr.push_back(std::move(code));
+            C.outs.push_back(oc);
+            continue;
         }
         int col = col_index_fallback(t, cn.c_str());
         if (col < 0) { oc.kind = OUT_NULL; C.outs.push_back(oc); continue; }
@@ -1396,6 +1453,25 @@ cq_table* build_groups(const Compiled& C, const std::vector<HGroup>& groups, con
                     break;
                 case OUT_REP: if (h.cnt > 0 && o.rep < (int)h.reps.size()) v = h.reps[o.rep]; break;
                 case OUT_CONST: if (h.cnt > 0) v = litcells[o.lit]; break;
+                case OUT_HEXPR:
+                    if (h.cnt > 0) {
+                        // host cells -> cells whose STRING bits point at the host strings
+                        std::vector<Cell> cols(h.reps.size()), consts(litcells.size());
+                        auto to_cell = [](const HCell& x) {
+                            Cell y;
+                            y.kind = x.kind; y.len = (uint32_t)x.s.size(); y.bits = x.bits;
+                            if (x.kind == K_STR) y.bits = (uint64_t)(uintptr_t)x.s.c_str();
+                            return y;
+                        };
+                        for (size_t k = 0; k < cols.size(); k++) cols[k] = to_cell(h.reps[k]);
+                        for (size_t k = 0; k < consts.size(); k++) consts[k] = to_cell(litcells[k]);
+                        const auto& code = C.hexpr[o.acc];
+                        const Cell r = cq_host_eval(code.data(), (uint32_t)code.size(), cols.data(), consts.data());
+                        v.kind = r.kind;
+                        v.bits = r.bits;
+                        if (r.kind == K_STR) v.s.assign((const char*)(uintptr_t)r.bits, r.len);
+                    }
+                    break;
                 default: break;
             }
             row.values[i] = to_value(v);
@@ -2062,6 +2138,67 @@ void side_gids(DevCtx& c, const cqgpu_table* t, uint32_t n, DevBuf& own, const u
     *out = own.as<unsigned long long>();
 }
 
+// WHERE + GROUP BY + aggregates over (l, r) pairs of parsed cells (join_agg_kernel),
+// then compaction and the representative cells of each group's first pair
+// (join_finish_kernel): groups in first-pair order, `first` / `extpos` = pair indexes
+std::vector<HGroup> aggregate_pairs(DevCtx& c, Compiled& C, const JoinMap& MA, const JoinMap& MR, const uint2* pairs,
+                                    unsigned long long np, const Cell* Lc, const Cell* Rc, ScanStats& st) {
+    const int grouped = C.grouped ? 1 : 0;
+    constexpr uint32_t SB = 48;
+    const uint32_t ncell = (uint32_t)MR.n + (uint32_t)C.P.nacc + 1;
+    uint32_t cap = grouped ? 8192 : 64;
+    std::vector<GroupOut> outs;
+    std::vector<Cell> fcells;
+    std::vector<uint8_t> fbytes;
+    while (true) {
+        TableArena Ar = make_arena(c, C.P, cap, cap / 2 + 1, 1, cq_scan_cand_stride(&C.P, grouped));
+        const unsigned int cap_out = cap / 2 + 1;
+        Scratch fin(c, (size_t)cap_out * ncell * (sizeof(Cell) + SB) + 64);
+        Cell* dcells = (Cell*)fin.p;
+        uint8_t* dbytes = fin.p + (size_t)cap_out * ncell * sizeof(Cell);
+        HIPCHECK(hipEventRecord(c.ev0, c.stream));
+        HIPCHECK(cq_launch_join_agg(pairs, np, &MA, Lc, Rc, &C.P, &Ar.gt, Ar.stats, grouped, c.stream));
+        HIPCHECK(hipEventRecord(c.ev1, c.stream));
+        HIPCHECK(cq_launch_compact(&Ar.gt, &C.P, Ar.out, Ar.out_count, cap_out, c.stream));
+        HIPCHECK(cq_launch_join_finish(Ar.out, Ar.out_count, cap_out, pairs, &MR, Lc, Rc, C.P.nacc, SB, dcells, dbytes,
+                                       c.stream));
+        unsigned int ng = 0;
+        HIPCHECK(hipMemcpyAsync(&ng, Ar.out_count, 4, hipMemcpyDeviceToHost, c.stream));
+        HIPCHECK(hipMemcpyAsync(&st, Ar.stats, sizeof st, hipMemcpyDeviceToHost, c.stream));
+        HIPCHECK(hipStreamSynchronize(c.stream));
+        float ms = 0;
+        HIPCHECK(hipEventElapsedTime(&ms, c.ev0, c.ev1));
+        g_stats.scan_ms = ms;
+        if (st.overflow >= 2) throw HipError{"join aggregate: lock / insert timeout"};
+        if (st.overflow) {
+            if (cap >= (1u << 30)) throw HipError{"group table overflow"};
+            cap *= 8;
+            continue;
+        }
+        ng = std::min(ng, cap_out);
+        outs.resize(ng);
+        fcells.resize((size_t)ng * ncell);
+        fbytes.resize((size_t)ng * ncell * SB);
+        if (ng) {
+            HIPCHECK(hipMemcpyAsync(outs.data(), Ar.out, ng * sizeof(GroupOut), hipMemcpyDeviceToHost, c.stream));
+            HIPCHECK(hipMemcpyAsync(fcells.data(), dcells, fcells.size() * sizeof(Cell), hipMemcpyDeviceToHost, c.stream));
+            HIPCHECK(hipMemcpyAsync(fbytes.data(), dbytes, fbytes.size(), hipMemcpyDeviceToHost, c.stream));
+        }
+        HIPCHECK(hipStreamSynchronize(c.stream));
+        break;
+    }
+    g_stats.passed = st.passed;
+    if (st.key_flags & 1u) throw Ineligible{"composite GROUP BY key text holding a tab"};
+    for (int a = 0; a < C.P.nacc; a++) {
+        if (C.P.acc[a].kind == ACC_SUM) continue;
+        unsigned m = st.acc_classes[a];
+        if (m & (m - 1)) throw Ineligible{"MIN/MAX over a column mixing numbers, strings and dates"};
+    }
+    std::vector<int> rep_ord(C.rep_cols.size());
+    for (size_t i = 0; i < rep_ord.size(); i++) rep_ord[i] = (int)i;
+    return make_groups(c, C, std::max<unsigned long long>(np, 1), 0, outs, fcells, fbytes, MR.n, rep_ord, SB);
+}
+
 cq_table* run_join(DevCtx& c, cq_node* q, const cqgpu_table* L, const cqgpu_table* R, JoinPartial* part = nullptr) {
     cq_node* jn = q->u.q.joins[0];
     if (q->u.q.join_count != 1 || !jn || jn->kind != CQ_N_JOIN) throw Ineligible{"more than one JOIN"};
@@ -2302,63 +2439,10 @@ cq_table* run_join(DevCtx& c, cq_node* q, const cqgpu_table* L, const cqgpu_tabl
     // aggregates over the pairs
     std::vector<HGroup> groups;
     if (!C.group_missing) {
-        const int grouped = C.grouped ? 1 : 0;
         const JoinMap MA = join_map(C.need_cols, nl, A, B);
         const JoinMap MR = join_map(C.rep_cols, nl, A, B);
-        constexpr uint32_t SB = 48;
-        const uint32_t ncell = (uint32_t)MR.n + (uint32_t)C.P.nacc + 1;
-        uint32_t cap = grouped ? 8192 : 64;
-        std::vector<GroupOut> outs;
-        std::vector<Cell> fcells;
-        std::vector<uint8_t> fbytes;
         ScanStats st;
-        while (true) {
-            TableArena Ar = make_arena(c, C.P, cap, cap / 2 + 1, 1, cq_scan_cand_stride(&C.P, grouped));
-            const unsigned int cap_out = cap / 2 + 1;
-            Scratch fin(c, (size_t)cap_out * ncell * (sizeof(Cell) + SB) + 64);
-            Cell* dcells = (Cell*)fin.p;
-            uint8_t* dbytes = fin.p + (size_t)cap_out * ncell * sizeof(Cell);
-            HIPCHECK(hipEventRecord(c.ev0, c.stream));
-            HIPCHECK(cq_launch_join_agg(pairs.as<uint2>(), np, &MA, A.cells.as<Cell>(), B.cells.as<Cell>(), &C.P, &Ar.gt,
-                                        Ar.stats, grouped, c.stream));
-            HIPCHECK(hipEventRecord(c.ev1, c.stream));
-            HIPCHECK(cq_launch_compact(&Ar.gt, &C.P, Ar.out, Ar.out_count, cap_out, c.stream));
-            HIPCHECK(cq_launch_join_finish(Ar.out, Ar.out_count, cap_out, pairs.as<uint2>(), &MR, A.cells.as<Cell>(),
-                                           B.cells.as<Cell>(), C.P.nacc, SB, dcells, dbytes, c.stream));
-            unsigned int ng = 0;
-            HIPCHECK(hipMemcpyAsync(&ng, Ar.out_count, 4, hipMemcpyDeviceToHost, c.stream));
-            HIPCHECK(hipMemcpyAsync(&st, Ar.stats, sizeof st, hipMemcpyDeviceToHost, c.stream));
-            HIPCHECK(hipStreamSynchronize(c.stream));
-            float ms = 0;
-            HIPCHECK(hipEventElapsedTime(&ms, c.ev0, c.ev1));
-            g_stats.scan_ms = ms;
-            if (st.overflow >= 2) throw HipError{"join aggregate: lock / insert timeout"};
-            if (st.overflow) {
-                if (cap >= (1u << 30)) throw HipError{"group table overflow"};
-                cap *= 8;
-                continue;
-            }
-            ng = std::min(ng, cap_out);
-            outs.resize(ng);
-            fcells.resize((size_t)ng * ncell);
-            fbytes.resize((size_t)ng * ncell * SB);
-            if (ng) {
-                HIPCHECK(hipMemcpyAsync(outs.data(), Ar.out, ng * sizeof(GroupOut), hipMemcpyDeviceToHost, c.stream));
-                HIPCHECK(hipMemcpyAsync(fcells.data(), dcells, fcells.size() * sizeof(Cell), hipMemcpyDeviceToHost, c.stream));
-                HIPCHECK(hipMemcpyAsync(fbytes.data(), dbytes, fbytes.size(), hipMemcpyDeviceToHost, c.stream));
-            }
-            HIPCHECK(hipStreamSynchronize(c.stream));
-            break;
-        }
-        g_stats.passed = st.passed;
-        for (int a = 0; a < C.P.nacc; a++) {
-            if (C.P.acc[a].kind == ACC_SUM) continue;
-            unsigned m = st.acc_classes[a];
-            if (m & (m - 1)) throw Ineligible{"MIN/MAX over a column mixing numbers, strings and dates"};
-        }
-        std::vector<int> rep_ord(C.rep_cols.size());
-        for (size_t i = 0; i < rep_ord.size(); i++) rep_ord[i] = (int)i;
-        groups = make_groups(c, C, std::max<unsigned long long>(np, 1), 0, outs, fcells, fbytes, MR.n, rep_ord, SB);
+        groups = aggregate_pairs(c, C, MA, MR, pairs.as<uint2>(), np, A.cells.as<Cell>(), B.cells.as<Cell>(), st);
         if (part) {
             for (int a = 0; a < C.P.nacc; a++) part->acc_classes[a] = st.acc_classes[a];
             // pair positions -> global (left id, right id) order keys
@@ -2403,6 +2487,60 @@ cq_table* run_join(DevCtx& c, cq_node* q, const cqgpu_table* L, const cqgpu_tabl
     return res;
 }
 
+// Aggregates the fused scan kernels do not cover (composite and expression GROUP
+// BY, evaluator.c:113-212 / evaluator_aggregates.c:179-250): every record's needed
+// columns parsed into cells (record-start kernels + cells_kernel), then the pair
+// aggregation with one "pair" (row, -) per record.  Groups come back in
+// first-appearance order with whole-file byte offsets, like run_aggregate's.
+std::vector<HGroup> run_cells_aggregate(DevCtx& c, const cqgpu_table* t, Compiled& C, Literals& Lit,
+                                        ScanStats* st_out = nullptr) {
+    parse_literals(c, C.lits, Lit);
+    for (size_t i = 0; i < Lit.cells.size(); i++) C.P.consts[i] = Lit.cells[i];
+    std::vector<HGroup> groups;
+    if (C.group_missing) return groups;
+    JoinSide A, B;
+    for (int j : C.need_cols) A.cols.push_back(j);
+    for (int j : C.rep_cols) A.cols.push_back(j);
+    if (A.cols.empty()) A.cols.push_back(0);
+    load_side(c, t, A);
+    const unsigned long long np = A.n;
+    DevBuf pairs(std::max<unsigned long long>(np, 1) * 8), bcells(sizeof(Cell));
+    if (np) HIPCHECK(cq_launch_join_fill(nullptr, nullptr, (uint32_t)np, 0, 0, pairs.as<uint2>(), c.stream));
+    const int nl = (int)t->names.size();
+    const JoinMap MA = join_map(C.need_cols, nl, A, B);
+    const JoinMap MR = join_map(C.rep_cols, nl, A, B);
+    ScanStats st;
+    groups = aggregate_pairs(c, C, MA, MR, pairs.as<uint2>(), np, A.cells.as<Cell>(), bcells.as<Cell>(), st);
+    if (st_out) *st_out = st;
+    g_stats.records = np;
+    g_stats.scan_bytes = t->n;
+    // row indexes -> whole-file byte offsets of the records
+    std::vector<uint32_t> idx;
+    for (const HGroup& h : groups) {
+        if (h.first != NOPOS) idx.push_back((uint32_t)h.first);
+        for (int a = 0; a < C.P.nacc; a++)
+            if (h.extpos[a] != NOPOS) idx.push_back((uint32_t)h.extpos[a]);
+    }
+    for (uint32_t i : idx)
+        if (i >= np) throw HipError{"cells aggregate: row index out of range"};
+    if (!idx.empty()) {
+        DevBuf di(idx.size() * 4), dof(idx.size() * 8);
+        HIPCHECK(hipMemcpyAsync(di.p, idx.data(), idx.size() * 4, hipMemcpyHostToDevice, c.stream));
+        HIPCHECK(cq_launch_gather_codes(A.recs.as<unsigned long long>(), di.as<uint32_t>(), (uint32_t)idx.size(),
+                                        dof.as<unsigned long long>(), c.stream));
+        std::vector<unsigned long long> off(idx.size());
+        HIPCHECK(hipMemcpyAsync(off.data(), dof.p, off.size() * 8, hipMemcpyDeviceToHost, c.stream));
+        HIPCHECK(hipStreamSynchronize(c.stream));
+        size_t k = 0;
+        for (HGroup& h : groups) {
+            if (h.first != NOPOS) h.first = off[k++] + t->base_offset;
+            for (int a = 0; a < C.P.nacc; a++)
+                if (h.extpos[a] != NOPOS) h.extpos[a] = off[k++] + t->base_offset;
+        }
+    }
+    return groups;
+}
+
 // ------------------------------------------------------------------ query dispatch
 void check_plan_shape(cq_node* q, const cqgpu_table* t, bool join_ok = false) {
     if (!q || q->kind != CQ_N_QUERY) throw Ineligible{"not a SELECT query"};
@@ -2445,8 +2583,14 @@ cq_table* query_impl(cq_node* q, cqgpu_table* const* tables, int ntables) {
     Compiled C;
     compile_aggregate(t, q, C);
     Literals L;
-    std::vector<HGroup> groups = run_aggregate(c, t, C, L, nullptr);
-    compute_vla(c, t, C, groups);
+    std::vector<HGroup> groups;
+    if (C.P.ngpart > 0) {
+        if (!C.vla.empty()) throw Ineligible{"STDDEV/MEDIAN with a composite or expression GROUP BY"};
+        groups = run_cells_aggregate(c, t, C, L);
+    } else {
+        groups = run_aggregate(c, t, C, L, nullptr);
+        compute_vla(c, t, C, groups);
+    }
     g_stats.groups = groups.size();
     cq_table* res = build_groups(C, groups, L, c);
     post_ops(c, res, q);
@@ -3232,7 +3376,12 @@ size_t cqgpu_query_partial(cq_node* q, cqgpu_table* const* tables, int ntables, 
         Literals L;
         ScanStats st;
         memset(&st, 0, sizeof st);
-        std::vector<HGroup> groups = run_aggregate(c, t, C, L, &st);
+        std::vector<HGroup> groups;
+        if (C.P.ngpart > 0) {
+            groups = run_cells_aggregate(c, t, C, L, &st);
+        } else {
+            groups = run_aggregate(c, t, C, L, &st);
+        }
         Blob b;
         b.u32(0x31505143u);                          // "CQP1"
         b.u32((uint32_t)t->names.size());
@@ -3337,6 +3486,7 @@ cq_table* cqgpu_merge_partials(cq_node* q, const void* const* blobs, const size_
                 // group identity: class + text for text keys, class + payload otherwise
                 std::string id = std::to_string(h.kcls) + ":";
                 if (h.kcls == GK_STR || h.kcls == GK_LONG) id += h.kbytes;
+                else if (h.kcls == GK_COMP) id += std::to_string(h.kw0) + "/" + std::to_string(h.kw1);
                 else id += std::to_string(h.kw0);
                 auto it = where.find(id);
                 if (it == where.end()) {

@@ -5,3 +5,37 @@
 #include "cell.h"
 
 extern "C" cq::Cell cq_host_parse_cell(const uint8_t* text, uint32_t len) { return cq::parse_cell(text, len); }
+
+#include "plan.h"
+
+// evaluate_expression (evaluator_expressions.c:23-263) on the host over one row of
+// cells: a non-aggregate expression item of an aggregate SELECT, evaluated on the
+// group's first row (build_aggregated_result, evaluator_aggregates.c:669-677).
+// OP_COL b indexes `cols`, OP_CONST b indexes `consts`.
+extern "C" cq::Cell cq_host_eval(const cq::Insn* code, uint32_t n, const cq::Cell* cols, const cq::Cell* consts) {
+    using namespace cq;
+    Cell st[VM_STACK + 1];
+    int sp = 0;
+    for (uint32_t pc = 0; pc < n; pc++) {
+        const Insn in = code[pc];
+        if (sp > VM_STACK) return cell_null();
+        switch (in.op) {
+            case OP_COL: st[sp++] = cols[in.b]; break;
+            case OP_CONST: st[sp++] = consts[in.b]; break;
+            case OP_ARITH: {
+                if (sp < 2) return cell_null();
+                const Cell r = st[--sp], l = st[--sp];
+                st[sp++] = arith(in.a, l, r);
+                break;
+            }
+            case OP_NEG: {
+                if (sp < 1) return cell_null();
+                const Cell x = st[--sp];
+                st[sp++] = negate(x);
+                break;
+            }
+            default: st[sp++] = cell_null(); break;
+        }
+    }
+    return sp > 0 ? st[sp - 1] : cell_null();
+}

@@ -9,6 +9,7 @@ constexpr int MAX_NEED = 8;     // distinct CSV columns one scan parses
 constexpr int MAX_PROG = 128;   // predicate instructions
 constexpr int MAX_CONST = 48;   // literal cells
 constexpr int MAX_ACC = 8;      // accumulators (one per aggregate SELECT item)
+constexpr int MAX_GPART = 4;    // composite GROUP BY parts (the reference's 1024-byte key holds 4)
 constexpr int VM_STACK = 8;
 
 // predicate bytecode (WHERE tree of evaluator_conditions.c:62-164 and
@@ -59,6 +60,13 @@ struct ScanPlan {
     int32_t nconst;
     Cell consts[MAX_CONST];
     int32_t group_slot;    // -1: one group (aggregate query without GROUP BY)
+    // composite / expression GROUP BY (evaluator.c:113-212, evaluator_aggregates.c:179-250):
+    // ngpart > 0 replaces group_slot; part k is need slot gpart_slot[k] (>= 0), the
+    // expression prog[gcode_off[k], gcode_off[k + 1]) (-1, after the WHERE program) or
+    // a column the composite path cannot resolve (-2: the text "NULL")
+    int32_t ngpart;
+    int16_t gpart_slot[MAX_GPART];
+    uint16_t gcode_off[MAX_GPART + 1];
     int32_t nacc;
     AccSpec acc[MAX_ACC];
     int32_t want_rows;     // 1: also emit matching record offsets (row-returning)
@@ -128,6 +136,7 @@ struct ScanStats {
     unsigned int acc_classes[MAX_ACC];  // OR of value classes seen per accumulator (1 num, 2 str, 4 date)
     unsigned long long slow_records;    // records the fast field walk handed to the general parser
     unsigned long long clk[8];          // profiling builds (CQ_CLOCKS): shader cycles per phase, summed over waves
+    unsigned int key_flags;             // composite GROUP BY: 1 = a text part holds a tab (key texts may collide)
 };
 
 // a MIN/MAX candidate published by one block (or wave) for one group

@@ -1190,6 +1190,51 @@ __global__ void gather_kernel(const uint8_t* __restrict__ g,
     parse_record_out(g + recs[i], P, out + (uint64_t)i * P.nneed);
 }
 
+// evaluate_expression (evaluator_expressions.c:23-263) over one record's need
+// slots: a composite / expression GROUP BY part, prog[b, e)
+template <int N>
+__device__ Cell eval_expr_vm(const ScanPlan& P, const Cell* kc, const CellsT<N>& cs, uint32_t b, uint32_t e) {
+    Stack st;
+#pragma unroll
+    for (int j = 0; j < 8; j++) st.s[j] = cell_null();
+    int sp = 0;
+    for (uint32_t pc = b; pc < e; pc++) {
+        const Insn in = P.prog[pc];
+        switch (in.op) {
+            case OP_COL: st.set(sp++, get_cell(cs, in.a)); break;
+            case OP_CONST: st.set(sp++, kc[in.b]); break;
+            case OP_ARITH: {
+                Cell r = st.get(--sp), l = st.get(--sp);
+                st.set(sp++, arith(in.a, l, r));
+                break;
+            }
+            case OP_NEG: { Cell x = st.get(--sp); st.set(sp++, negate(x)); break; }
+            default: st.set(sp++, cell_null()); break;
+        }
+    }
+    return sp > 0 ? st.get(sp - 1) : cell_null();
+}
+
+// the group key of a record: the GROUP BY column's canonical key, one expression's
+// (create_groups_by_expression), or the composite digest of several parts (cell.h
+// CompKey; `tab`: a text part holds a tab)
+template <int N>
+__device__ GKey plan_group_key(const ScanPlan& P, const Cell* kc, const CellsT<N>& cs, int nneed, bool& tab) {
+    if (P.ngpart == 0) return group_key(get_cell(cs, P.group_slot, nneed));
+    CompKey ck;
+    for (int k = 0; k < MAX_GPART; k++) {
+        if (k >= P.ngpart) break;
+        const int s = P.gpart_slot[k];
+        const Cell c = s >= 0 ? get_cell(cs, s, nneed)
+                              : (s == -1 ? eval_expr_vm(P, kc, cs, P.gcode_off[k], P.gcode_off[k + 1]) : cell_null());
+        const GKey pk = group_key(c);
+        if (P.ngpart == 1) return pk;
+        tab = tab || text_has_tab(c);
+        ck.add(pk);
+    }
+    return comp_key(ck, (uint32_t)P.ngpart);
+}
+
 // ------------------------------------------------------------------ projection
 // evaluate_expression (evaluator_expressions.c:23-263) for one SELECT item of a
 // row-returning query (build_result, evaluator_utils.c:249-549): the program's
@@ -1509,7 +1554,9 @@ __global__ __launch_bounds__(256) void join_agg_kernel(const uint2* __restrict__
         key.cls = GK_ALL; key.len = 0; key.w0 = 0; key.w1 = 0;
         uint64_t h = 0x12345678ULL;
         if (grouped && pass) {
-            key = group_key(get_cell(cs, P.group_slot, nneed));
+            bool tab = false;
+            key = plan_group_key(P, P.consts, cs, nneed, tab);
+            if (tab) atomicOr(&stats->key_flags, 1u);
             h = gk_hash(key);
         }
         int gi = -1;
