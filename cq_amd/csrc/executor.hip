@@ -176,6 +176,11 @@ struct HipError {
 struct Ineligible {
     std::string why;
 };
+// a MIN/MAX argument mixes value classes: the fused scans hand the plan to the
+// cells path, whose pair aggregation folds such extremes exactly
+struct MixedExtremes : Ineligible {
+    MixedExtremes() : Ineligible{"MIN/MAX over a column mixing numbers, strings and dates"} {}
+};
 
 // ------------------------------------------------------------------ per-device context
 struct DevCtx {
@@ -1391,11 +1396,11 @@ std::vector<HGroup> run_aggregate(DevCtx& c, const cqgpu_table* t, Compiled& C, 
     g_stats.scan_bytes = t->n;
     if (stats_out) *stats_out = st;
     // MIN/MAX over a column mixing value classes depends on row order in the
-    // reference (incomparable cells compare equal): outside the GPU subset
+    // reference (incomparable cells compare equal): the cells path folds it
     for (int a = 0; a < C.P.nacc; a++) {
         if (C.P.acc[a].kind == ACC_SUM) continue;
         unsigned m = st.acc_classes[a];
-        if (m & (m - 1)) throw Ineligible{"MIN/MAX over a column mixing numbers, strings and dates"};
+        if (m & (m - 1)) throw MixedExtremes{};
     }
     return make_groups(c, C, t->n, t->base_offset, outs, fcells, fbytes, FD.ncols, rep_ord, SB);
 }
@@ -2189,14 +2194,41 @@ std::vector<HGroup> aggregate_pairs(DevCtx& c, Compiled& C, const JoinMap& MA, c
     }
     g_stats.passed = st.passed;
     if (st.key_flags & 1u) throw Ineligible{"composite GROUP BY key text holding a tab"};
-    for (int a = 0; a < C.P.nacc; a++) {
-        if (C.P.acc[a].kind == ACC_SUM) continue;
-        unsigned m = st.acc_classes[a];
-        if (m & (m - 1)) throw Ineligible{"MIN/MAX over a column mixing numbers, strings and dates"};
-    }
     std::vector<int> rep_ord(C.rep_cols.size());
     for (size_t i = 0; i < rep_ord.size(); i++) rep_ord[i] = (int)i;
-    return make_groups(c, C, std::max<unsigned long long>(np, 1), 0, outs, fcells, fbytes, MR.n, rep_ord, SB);
+    std::vector<HGroup> groups =
+        make_groups(c, C, std::max<unsigned long long>(np, 1), 0, outs, fcells, fbytes, MR.n, rep_ord, SB);
+    // MIN/MAX over cells of several value classes (evaluator_aggregates.c:311-326):
+    // a row-order fold under value_compare, where cells of different classes compare
+    // "equal", so the result keeps the class of the group's first non-NULL cell and
+    // is the first occurrence of that class's extreme.  One more pass per such
+    // accumulator computes, per class, the extreme (with its first position) and the
+    // first position of any cell of the class; groups come out in the same order.
+    for (int a = 0; a < C.P.nacc; a++) {
+        if (C.P.acc[a].kind == ACC_SUM || C.P.acc[a].cls) continue;   // (a class-split pass itself)
+        const unsigned m = st.acc_classes[a];
+        if (!(m & (m - 1))) continue;
+        Compiled C2 = C;
+        C2.P.nacc = 6;
+        for (int k = 0; k < 3; k++) {
+            AccSpec& e = C2.P.acc[k];
+            e.kind = C.P.acc[a].kind; e.slot = C.P.acc[a].slot; e.cls = (uint8_t)(1u << k); e.pos_only = 0;
+            AccSpec& f = C2.P.acc[3 + k];
+            f.kind = ACC_MIN; f.slot = C.P.acc[a].slot; f.cls = (uint8_t)(1u << k); f.pos_only = 1;
+        }
+        ScanStats st2;
+        const std::vector<HGroup> split = aggregate_pairs(c, C2, MA, MR, pairs, np, Lc, Rc, st2);
+        if (split.size() != groups.size()) throw HipError{"mixed MIN/MAX: class-split pass disagrees on the groups"};
+        for (size_t g = 0; g < groups.size(); g++) {
+            int best = -1;
+            for (int k = 0; k < 3; k++)
+                if (split[g].extpos[3 + k] != NOPOS && (best < 0 || split[g].extpos[3 + k] < split[g].extpos[3 + best]))
+                    best = k;
+            groups[g].ext[a] = best >= 0 ? split[g].ext[best] : HCell();
+            groups[g].extpos[a] = best >= 0 ? split[g].extpos[best] : NOPOS;
+        }
+    }
+    return groups;
 }
 
 cq_table* run_join(DevCtx& c, cq_node* q, const cqgpu_table* L, const cqgpu_table* R, JoinPartial* part = nullptr) {
@@ -2588,8 +2620,13 @@ cq_table* query_impl(cq_node* q, cqgpu_table* const* tables, int ntables) {
         if (!C.vla.empty()) throw Ineligible{"STDDEV/MEDIAN with a composite or expression GROUP BY"};
         groups = run_cells_aggregate(c, t, C, L);
     } else {
-        groups = run_aggregate(c, t, C, L, nullptr);
-        compute_vla(c, t, C, groups);
+        try {
+            groups = run_aggregate(c, t, C, L, nullptr);
+            compute_vla(c, t, C, groups);
+        } catch (MixedExtremes&) {
+            if (!C.vla.empty()) throw Ineligible{"STDDEV/MEDIAN beside MIN/MAX over mixed value classes"};
+            groups = run_cells_aggregate(c, t, C, L);
+        }
     }
     g_stats.groups = groups.size();
     cq_table* res = build_groups(C, groups, L, c);
@@ -3380,7 +3417,11 @@ size_t cqgpu_query_partial(cq_node* q, cqgpu_table* const* tables, int ntables, 
         if (C.P.ngpart > 0) {
             groups = run_cells_aggregate(c, t, C, L, &st);
         } else {
-            groups = run_aggregate(c, t, C, L, &st);
+            try {
+                groups = run_aggregate(c, t, C, L, &st);
+            } catch (MixedExtremes&) {
+                groups = run_cells_aggregate(c, t, C, L, &st);
+            }
         }
         Blob b;
         b.u32(0x31505143u);                          // "CQP1"

@@ -42,7 +42,8 @@ enum : uint8_t { ACC_SUM = 0, ACC_MIN = 1, ACC_MAX = 2 };
 struct AccSpec {
     uint8_t kind;   // ACC_*
     uint8_t slot;   // need slot of the argument column
-    uint8_t pad[2];
+    uint8_t cls;    // MIN/MAX over the pair path: only cells of these value classes (class_bit; 0 = all)
+    uint8_t pos_only;   // MIN over the pair path: every qualifying cell counts as equal (first position)
 };
 
 struct ScanPlan {

@@ -1529,8 +1529,12 @@ __global__ __launch_bounds__(256) void join_agg_kernel(const uint2* __restrict__
     const int nneed = P.nneed, nacc = P.nacc;
     unsigned long long my_pass = 0;
     uint32_t my_cls[MAX_ACC];             // value classes seen per MIN/MAX argument, flushed once per wave
+    // one group (no GROUP BY): MIN/MAX candidates kept per lane, merged per wave at
+    // the end, so the group's lock is taken once per wave instead of once per pair
+    Cell my_ext[MAX_ACC];
+    unsigned long long my_pos[MAX_ACC];
 #pragma unroll
-    for (int a = 0; a < MAX_ACC; a++) my_cls[a] = 0;
+    for (int a = 0; a < MAX_ACC; a++) { my_cls[a] = 0; my_ext[a] = cell_null(); my_pos[a] = NOPOS; }
     for (unsigned long long b0 = (unsigned long long)blockIdx.x * blockDim.x; b0 < np;
          b0 += (unsigned long long)gridDim.x * blockDim.x) {
         const unsigned long long i = b0 + threadIdx.x;
@@ -1578,9 +1582,44 @@ __global__ __launch_bounds__(256) void join_agg_kernel(const uint2* __restrict__
         for (int a = 0; a < MAX_ACC; a++) {
             if (a >= nacc) break;
             if (P.acc[a].kind == ACC_SUM) continue;      // uniform
-            const Cell c = get_cell(cs, P.acc[a].slot, nneed);
-            g_ext_update(pass && gi >= 0 && c.kind != K_NULL, gt, a, P.acc[a].kind, gi >= 0 ? (uint32_t)gi : 0u,
-                         c, i, stats);
+            Cell c = get_cell(cs, P.acc[a].slot, nneed);
+            const uint32_t cf = P.acc[a].cls;             // class-split MIN/MAX (mixed classes, host fold)
+            const bool in_cls = (cf == 0 || (class_bit(c) & cf) != 0) && c.kind != K_NULL;
+            if (P.acc[a].pos_only) c = cell_int(0);
+            if (!grouped) {
+                if (pass && gi >= 0 && in_cls && ext_better(P.acc[a].kind, c, i, my_ext[a], my_pos[a])) {
+                    my_ext[a] = c;
+                    my_pos[a] = i;
+                }
+            } else {
+                g_ext_update(pass && gi >= 0 && in_cls, gt, a, P.acc[a].kind, gi >= 0 ? (uint32_t)gi : 0u, c, i,
+                             stats);
+            }
+        }
+    }
+    if (!grouped) {
+#pragma unroll
+        for (int a = 0; a < MAX_ACC; a++) {
+            if (a >= nacc) break;
+            if (P.acc[a].kind == ACC_SUM) continue;      // uniform
+            Cell c = my_ext[a];
+            unsigned long long p = my_pos[a];
+            for (int o = 32; o > 0; o >>= 1) {
+                Cell oc;
+                oc.kind = (uint32_t)__shfl_down((int)c.kind, o, 64);
+                oc.len = (uint32_t)__shfl_down((int)c.len, o, 64);
+                oc.bits = __shfl_down(c.bits, o, 64);
+                const unsigned long long op = __shfl_down(p, o, 64);
+                if (op != NOPOS && ext_better(P.acc[a].kind, oc, op, c, p)) { c = oc; p = op; }
+            }
+            int gi = -1;
+            const bool lead = (threadIdx.x & 63) == 0 && p != NOPOS;
+            if (lead) {
+                GKey k;
+                k.cls = GK_ALL; k.len = 0; k.w0 = 0; k.w1 = 0;
+                gi = g_insert(gt, k, 0x12345678ULL, stats);
+            }
+            g_ext_update(lead && gi >= 0, gt, a, P.acc[a].kind, gi >= 0 ? (uint32_t)gi : 0u, c, p, stats);
         }
     }
     for (int o = 32; o > 0; o >>= 1) my_pass += __shfl_down(my_pass, o, 64);

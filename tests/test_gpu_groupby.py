@@ -102,3 +102,29 @@ def test_composite_across_partials(synth):
         cq_amd.result_free(tp)
         tol = tolerant_columns(ast)
     compare(got, want, tol, sql)
+
+
+# ---------------------------------------------------------------- mixed-class MIN/MAX
+def test_mixed_class_min_max(tmp_path):
+    """MIN/MAX over columns mixing numbers, strings and dates: the reference's
+    row-order fold keeps the class of each group's first non-NULL cell
+    (evaluator_aggregates.c:311-326, value_compare calls other classes equal)."""
+    import numpy as np
+    rng = np.random.default_rng(5)
+    shapes = ["12", "-3", "7.5", "abc", "Zed", "2024-02-03", "1999-12-31", "", "0", "b", "10.25", "2001-01-01"]
+    rows = ["g,v,w"]
+    for i in range(30000):
+        rows.append("%d,%s,%s" % (rng.integers(0, 40), shapes[rng.integers(0, len(shapes))],
+                                  shapes[rng.integers(0, len(shapes))]))
+    p = tmp_path / "mixed.csv"
+    p.write_text("\n".join(rows) + "\n")
+    for sql in (f"SELECT g, MIN(v), MAX(v), COUNT(*) FROM '{p}' GROUP BY g",
+                f"SELECT MIN(v), MAX(w), MIN(w), MAX(v) FROM '{p}'",
+                f"SELECT g, MIN(w), MAX(w) FROM '{p}' WHERE v > 5 GROUP BY g",
+                f"SELECT g, v, MIN(w), COUNT(*) FROM '{p}' GROUP BY g, v"):
+        want, unsup = cqtest.oracle_query(sql)
+        assert not unsup
+        with cqtest.Parsed(sql) as ast:
+            got = cq_amd.evaluate(ast)
+        assert not cq_amd.last_ineligible(), (sql, cq_amd.last_ineligible())
+        compare(got, want, set(), sql)

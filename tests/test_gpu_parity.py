@@ -20,9 +20,9 @@ pytestmark = pytest.mark.gpu
 SUMAVG_REL = 1e-6
 QUERIES = cqtest.golden("queries.json")
 
-# golden queries outside the GPU subset of this round (they take the
-# fallback path or return an error): MIN/MAX over a column mixing numbers and strings
-EXPECTED_INELIGIBLE_MARKERS = ("MIN(a), MAX(a), MIN(b), MAX(b), MIN(d) FROM '{D}/edge_numbers.csv'",)
+# golden queries outside the GPU subset (they would take the fallback path or
+# return an error): none this round
+EXPECTED_INELIGIBLE_MARKERS = ()
 
 
 def expected_ineligible(sql):
@@ -223,8 +223,5 @@ def test_field_shape_fuzz(tmp_path):
         with cqtest.Parsed(sql) as ast:
             got = cq_amd.evaluate(ast)
             tol = tolerant_columns(ast)
-        inel = cq_amd.last_ineligible()
-        if inel:
-            assert "MIN/MAX" in inel, inel
-            continue
+        assert not cq_amd.last_ineligible(), (sql, cq_amd.last_ineligible())
         compare(got, want, tol, sql)
