@@ -17,6 +17,7 @@
 #include <cstring>
 #include <string>
 #include <map>
+#include <set>
 #include <memory>
 #include <tuple>
 #include <unordered_map>
@@ -65,6 +66,8 @@ hipError_t cq_launch_join_emit(const cq::Cell* L, uint32_t ls, uint32_t lk, uint
                                uint2* pairs, unsigned int* rmatched, hipStream_t s);
 hipError_t cq_launch_join_fill(const unsigned int* flags, const unsigned int* pos, uint32_t n, unsigned long long base,
                                int right_side, uint2* pairs, hipStream_t s);
+hipError_t cq_launch_join_gather(const uint2* pairs, unsigned long long np, const cq::JoinMap* M, const cq::Cell* L,
+                                 const cq::Cell* R, cq::Cell* out, hipStream_t s);
 hipError_t cq_sort_classes(void* temp, size_t* temp_bytes, const unsigned int* kin, unsigned int* kout,
                            const unsigned int* vin, unsigned int* vout, size_t n, hipStream_t s);
 hipError_t cq_sort_codes_seg(void* temp, size_t* temp_bytes, const unsigned long long* kin, unsigned long long* kout,
@@ -2231,55 +2234,33 @@ std::vector<HGroup> aggregate_pairs(DevCtx& c, Compiled& C, const JoinMap& MA, c
     return groups;
 }
 
-cq_table* run_join(DevCtx& c, cq_node* q, const cqgpu_table* L, const cqgpu_table* R, JoinPartial* part = nullptr) {
-    cq_node* jn = q->u.q.joins[0];
-    if (q->u.q.join_count != 1 || !jn || jn->kind != CQ_N_JOIN) throw Ineligible{"more than one JOIN"};
-    const int kind = jn->u.join.kind;
-    const bool outer_left = kind == CQ_JOIN_LEFT || kind == CQ_JOIN_FULL;
-    const bool outer_right = kind == CQ_JOIN_RIGHT || kind == CQ_JOIN_FULL;
-    if (!R) throw Ineligible{"join table failed to load"};
-    cq_node* on = jn->u.join.on;
-    if (!on) throw Ineligible{"JOIN without ON (cross product)"};
-    const char* la = (q->u.q.from && q->u.q.from->u.from.alias) ? q->u.q.from->u.from.alias : "main";
-    const char* ra = jn->u.join.alias ? jn->u.join.alias : "right";
-    const int nl = (int)L->names.size();
-    // ON operands (anything but `ident = ident` matches no pair)
-    int kl = -1, kr = -1;
-    if (on->kind == CQ_N_CONDITION && on->u.bin.op && !strcmp(on->u.bin.op, "=") && on->u.bin.lhs && on->u.bin.rhs &&
-        on->u.bin.lhs->kind == CQ_N_IDENTIFIER && on->u.bin.rhs->kind == CQ_N_IDENTIFIER) {
-        kl = join_on_index(on->u.bin.lhs->u.text, L, L, la, R, ra);
-        kr = join_on_index(on->u.bin.rhs->u.text, R, L, la, R, ra);
-    }
-    const bool keyed = kl >= 0 && kr >= 0;
-    if (part) {
-        if (!keyed) throw Ineligible{"JOIN without an `ident = ident` ON across partials"};
-    }
-    // the joined table's schema: alias.col names (evaluator_joins.c:30-37)
-    cqgpu_table J;
-    J.cfg = L->cfg;
-    for (auto& nm : L->names) J.names.push_back(std::string(la) + "." + nm);
-    for (auto& nm : R->names) J.names.push_back(std::string(ra) + "." + nm);
-    const bool rows = is_row_query(q);
-    if (part && rows) throw Ineligible{"row-returning SELECT across partials"};
-    Compiled C;
-    RowPlan RP;
-    if (rows) compile_rows(&J, q, C, RP);
-    else compile_aggregate(&J, q, C);
-    if (!C.vla.empty()) throw Ineligible{"STDDEV/MEDIAN over a join"};
-    // the columns each side parses
-    JoinSide A, B;
-    if (keyed) { A.cols.push_back(kl); B.cols.push_back(kr); }
-    auto want = [&](int j) { if (j < nl) A.cols.push_back(j); else B.cols.push_back(j - nl); };
-    for (int j : C.need_cols) want(j);
-    for (int j : C.rep_cols) want(j);
-    for (int j : RP.cols) want(j);
-    if (A.cols.empty()) A.cols.push_back(0);
-    if (B.cols.empty()) B.cols.push_back(0);
-    load_side(c, L, A);
-    load_side(c, R, B);
-    // pairs in (l, r) order
+// key value classes present in a side's key column (bit k: class k, 1 number,
+// 2 string, 3 date): a repartitioned join's ranks report them so the merge can
+// refuse cross-class keys, which value_compare calls "equal" (csv_reader.c:128)
+uint32_t key_class_mask(DevCtx& c, const JoinSide& S, int kcol) {
+    if (!S.n) return 0;
+    const uint32_t stride = (uint32_t)S.cols.size(), k = (uint32_t)S.slot(kcol);
+    DevBuf codes((size_t)S.n * 8), cls((size_t)S.n * 4), pc(64);
+    HIPCHECK(hipMemsetAsync(pc.p, 0, 64, c.stream));
+    HIPCHECK(cq_launch_join_code(S.cells.as<Cell>(), stride, k, S.n, codes.as<unsigned long long>(), cls.as<uint32_t>(),
+                                 nullptr, pc.as<unsigned int>(), c.stream));
+    unsigned int per[4] = {0, 0, 0, 0};
+    HIPCHECK(hipMemcpyAsync(per, pc.p, 16, hipMemcpyDeviceToHost, c.stream));
+    HIPCHECK(hipStreamSynchronize(c.stream));
+    uint32_t m = 0;
+    for (int j = 1; j < 4; j++)
+        if (per[j]) m |= 1u << j;
+    return m;
+}
+
+// (l, r) pairs of one join level in the nested loop's order (perform_join,
+// evaluator_joins.c:63-181): left rows ascending, each with its matching right
+// rows ascending; LEFT / FULL put an unmatched left row (l, -) in its place,
+// RIGHT / FULL append the unmatched right rows (-, r) in row order.  kl / kr:
+// the ON operands' columns of A / B (keyed: both resolved).
+unsigned long long build_pairs(DevCtx& c, JoinSide& A, JoinSide& B, int kl, int kr, bool keyed, bool outer_left,
+                               bool outer_right, DevBuf& pairs) {
     unsigned long long np = 0;
-    DevBuf pairs(8);
     if (keyed && A.n && B.n) {
         const uint32_t ls = (uint32_t)A.cols.size(), rs = (uint32_t)B.cols.size();
         const uint32_t lk = (uint32_t)A.slot(kl), rk = (uint32_t)B.slot(kr);
@@ -2303,20 +2284,6 @@ cq_table* run_join(DevCtx& c, cq_node* q, const cqgpu_table* L, const cqgpu_tabl
         memset(&JR, 0, sizeof JR);
         JR.seg[0] = 0;
         for (int k = 0; k < 4; k++) JR.seg[k + 1] = JR.seg[k] + per[k];
-        if (part) {
-            // key value classes present on each side (cross-class pairs are not routable)
-            DevBuf lc((size_t)A.n * 8), lk2((size_t)A.n * 4), lpc(64);
-            HIPCHECK(hipMemsetAsync(lpc.p, 0, 64, c.stream));
-            HIPCHECK(cq_launch_join_code(A.cells.as<Cell>(), ls, lk, A.n, lc.as<unsigned long long>(),
-                                         lk2.as<uint32_t>(), nullptr, lpc.as<unsigned int>(), c.stream));
-            unsigned int lper[4] = {0, 0, 0, 0};
-            HIPCHECK(hipMemcpyAsync(lper, lpc.p, 16, hipMemcpyDeviceToHost, c.stream));
-            HIPCHECK(hipStreamSynchronize(c.stream));
-            for (int k = 1; k < 4; k++) {
-                if (lper[k]) part->lmask |= 1u << k;
-                if (per[k]) part->rmask |= 1u << k;
-            }
-        }
         int segs[8];
         for (int k = 0; k < 4; k++) { segs[k] = (int)JR.seg[k]; segs[4 + k] = (int)JR.seg[k + 1]; }
         int* dsegs = (int*)((uint8_t*)pc.p + 32);
@@ -2397,6 +2364,128 @@ cq_table* run_join(DevCtx& c, cq_node* q, const cqgpu_table* L, const cqgpu_tabl
         if (nr2) HIPCHECK(cq_launch_join_fill(nullptr, nullptr, (uint32_t)nr2, nl2, 1, pairs.as<uint2>(), c.stream));
         np = nl2 + nr2;
     }
+    return np;
+}
+
+// One JOIN, or a chain of them (process_joins, evaluator_joins.c:237-274): join
+// j's left side is the table joined so far, named "joined" with columns
+// "<alias>.<col>" of the previous level (so a second level names "joined.u.id").
+// Every level runs on the device; between levels only the columns later levels,
+// the WHERE, the groups and the SELECT read are gathered into a cell table of the
+// joined rows (NULL cells for an outer join's missing side).
+cq_table* run_join(DevCtx& c, cq_node* q, const cqgpu_table* L, const cqgpu_table* const* rights, int nrights,
+                   JoinPartial* part = nullptr) {
+    const int nj = q->u.q.join_count;
+    if (nj < 1) throw HipError{"run_join without a JOIN"};
+    if (nrights < nj) throw Ineligible{"join table not given"};
+    if (part && nj != 1) throw Ineligible{"join chains across partials"};
+    struct Level {
+        const cqgpu_table* R;
+        std::string ra;
+        bool outer_left, outer_right, keyed;
+        int kl, kr, nleft;
+        std::set<int> lneed, rneed;
+    };
+    std::vector<Level> lv(nj);
+    std::vector<std::string> wnames = L->names;
+    std::string wa = (q->u.q.from && q->u.q.from->u.from.alias) ? q->u.q.from->u.from.alias : "main";
+    for (int j = 0; j < nj; j++) {
+        cq_node* jn = q->u.q.joins[j];
+        if (!jn || jn->kind != CQ_N_JOIN) throw Ineligible{"malformed JOIN"};
+        Level& v = lv[j];
+        const int kind = jn->u.join.kind;
+        v.outer_left = kind == CQ_JOIN_LEFT || kind == CQ_JOIN_FULL;
+        v.outer_right = kind == CQ_JOIN_RIGHT || kind == CQ_JOIN_FULL;
+        v.R = rights[j];
+        if (!v.R) throw Ineligible{"join table failed to load"};
+        cq_node* on = jn->u.join.on;
+        if (!on) throw Ineligible{"JOIN without ON (cross product)"};
+        v.ra = jn->u.join.alias ? jn->u.join.alias : "right";
+        cqgpu_table W;                       // the left side's schema at this level
+        W.names = wnames;
+        // ON operands (anything but `ident = ident` matches no pair)
+        v.kl = v.kr = -1;
+        if (on->kind == CQ_N_CONDITION && on->u.bin.op && !strcmp(on->u.bin.op, "=") && on->u.bin.lhs &&
+            on->u.bin.rhs && on->u.bin.lhs->kind == CQ_N_IDENTIFIER && on->u.bin.rhs->kind == CQ_N_IDENTIFIER) {
+            v.kl = join_on_index(on->u.bin.lhs->u.text, &W, &W, wa.c_str(), v.R, v.ra.c_str());
+            v.kr = join_on_index(on->u.bin.rhs->u.text, v.R, &W, wa.c_str(), v.R, v.ra.c_str());
+        }
+        v.keyed = v.kl >= 0 && v.kr >= 0;
+        if (part && !v.keyed) throw Ineligible{"JOIN without an `ident = ident` ON across partials"};
+        v.nleft = (int)wnames.size();
+        std::vector<std::string> nn;        // copy_columns_with_prefix (evaluator_joins.c:30-37)
+        for (auto& nm : wnames) nn.push_back(wa + "." + nm);
+        for (auto& nm : v.R->names) nn.push_back(v.ra + "." + nm);
+        wnames.swap(nn);
+        wa = "joined";
+    }
+    // the final joined table's schema
+    cqgpu_table J;
+    J.cfg = L->cfg;
+    J.names = wnames;
+    const bool rows = is_row_query(q);
+    if (part && rows) throw Ineligible{"row-returning SELECT across partials"};
+    Compiled C;
+    RowPlan RP;
+    if (rows) compile_rows(&J, q, C, RP);
+    else compile_aggregate(&J, q, C);
+    if (!C.vla.empty()) throw Ineligible{"STDDEV/MEDIAN over a join"};
+    // columns each level needs, from the last level back
+    {
+        std::set<int> cur(C.need_cols.begin(), C.need_cols.end());
+        cur.insert(C.rep_cols.begin(), C.rep_cols.end());
+        cur.insert(RP.cols.begin(), RP.cols.end());
+        for (int j = nj - 1; j >= 0; j--) {
+            Level& v = lv[j];
+            for (int f : cur) {
+                if (f < v.nleft) v.lneed.insert(f);
+                else v.rneed.insert(f - v.nleft);
+            }
+            if (v.keyed) { v.lneed.insert(v.kl); v.rneed.insert(v.kr); }
+            cur = v.lneed;
+        }
+    }
+    // level 0's left side: the FROM table's columns
+    std::unique_ptr<JoinSide> Ap(new JoinSide);
+    Ap->cols.assign(lv[0].lneed.begin(), lv[0].lneed.end());
+    if (Ap->cols.empty()) Ap->cols.push_back(0);
+    load_side(c, L, *Ap);
+    std::unique_ptr<JoinSide> Bp;
+    DevBuf pairs(8);
+    unsigned long long np = 0;
+    for (int j = 0; j < nj; j++) {
+        Level& v = lv[j];
+        Bp.reset(new JoinSide);
+        Bp->cols.assign(v.rneed.begin(), v.rneed.end());
+        if (Bp->cols.empty()) Bp->cols.push_back(0);
+        load_side(c, v.R, *Bp);
+        DevBuf pb(8);
+        np = build_pairs(c, *Ap, *Bp, v.kl, v.kr, v.keyed, v.outer_left, v.outer_right, pb);
+        std::swap(pairs.p, pb.p);
+        if (part && v.keyed) {               // even when one side is empty on this rank
+            part->lmask |= key_class_mask(c, *Ap, v.kl);
+            part->rmask |= key_class_mask(c, *Bp, v.kr);
+        }
+        if (j + 1 == nj) break;
+        // the joined rows' cells the next levels read: the next left side
+        if (np >= (1ull << 32)) throw Ineligible{"intermediate join over 2^32 rows"};
+        std::unique_ptr<JoinSide> Wn(new JoinSide);
+        Wn->cols.assign(lv[j + 1].lneed.begin(), lv[j + 1].lneed.end());
+        if (Wn->cols.empty()) Wn->cols.push_back(0);
+        if ((int)Wn->cols.size() > MAX_NEED) throw Ineligible{"join: more than 8 columns of one side"};
+        Wn->n = (uint32_t)np;
+        const JoinMap M = join_map(Wn->cols, v.nleft, *Ap, *Bp);
+        DevBuf cells((size_t)std::max<unsigned long long>(np, 1) * Wn->cols.size() * sizeof(Cell));
+        std::swap(Wn->cells.p, cells.p);
+        if (np) HIPCHECK(cq_launch_join_gather(pairs.as<uint2>(), np, &M, Ap->cells.as<Cell>(), Bp->cells.as<Cell>(),
+                                               Wn->cells.as<Cell>(), c.stream));
+        HIPCHECK(hipStreamSynchronize(c.stream));
+        Ap = std::move(Wn);
+    }
+    JoinSide& A = *Ap;
+    JoinSide& B = *Bp;
+    const int nl = lv[nj - 1].nleft;
+    const cqgpu_table* R = lv[nj - 1].R;
     g_stats.records = np;
     Literals Lit;
     parse_literals(c, C.lits, Lit);
@@ -2599,8 +2688,9 @@ cq_table* query_impl(cq_node* q, cqgpu_table* const* tables, int ntables) {
     if (q && q->kind == CQ_N_QUERY && q->u.q.join_count > 0) {
         check_plan_shape(q, t, true);
         if (ntables < 2) throw Ineligible{"join table not given"};
-        if (tables[1]) check_plan_shape(q, tables[1], true);
-        return run_join(c, q, t, tables[1]);
+        for (int j = 1; j < ntables; j++)
+            if (tables[j]) check_plan_shape(q, tables[j], true);
+        return run_join(c, q, t, tables + 1, ntables - 1);
     }
     check_plan_shape(q, t);
     if (is_row_query(q)) {
@@ -3094,7 +3184,19 @@ cq_table* evaluate_query(cq_node* q) {
     }
     std::vector<cqgpu_table*> tables;
     std::vector<bool> owned;
+    std::vector<std::string> paths;
     auto open_one = [&](const char* path) -> cqgpu_table* {
+        // a path named twice (FROM and JOIN, or two JOINs) is opened once: a second
+        // cache lookup could drop the first entry if the file changed in between
+        for (size_t i = 0; i < paths.size(); i++) {
+            if (paths[i] == path && tables[i]) {
+                tables.push_back(tables[i]);
+                owned.push_back(false);
+                paths.push_back(path);
+                return tables[i];
+            }
+        }
+        paths.push_back(path);
         bool own = true;
         cqgpu_table* t = nullptr;
         try {
@@ -3115,7 +3217,7 @@ cq_table* evaluate_query(cq_node* q) {
     for (int j = 0; j < q->u.q.join_count; j++) {
         cq_node* jn = q->u.q.joins[j];
         if (jn && jn->u.join.path) open_one(jn->u.join.path);
-        else { tables.push_back(nullptr); owned.push_back(true); }
+        else { tables.push_back(nullptr); owned.push_back(true); paths.push_back(""); }
     }
     cq_table* r = cqgpu_query(q, tables.data(), (int)tables.size());
     for (size_t i = 0; i < tables.size(); i++)
@@ -3375,7 +3477,7 @@ size_t cqgpu_query_partial(cq_node* q, cqgpu_table* const* tables, int ntables, 
             check_plan_shape(q, t, true);
             if (ntables < 2 || !tables[1]) throw Ineligible{"join table not given"};
             JoinPartial jp;
-            (void)run_join(c, q, t, tables[1], &jp);
+            (void)run_join(c, q, t, tables + 1, ntables - 1, &jp);
             Compiled C;
             cqgpu_table J;
             J.names = jp.names;

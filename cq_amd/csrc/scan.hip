@@ -1491,6 +1491,22 @@ __global__ void join_emit_kernel(const Cell* __restrict__ L, uint32_t ls, uint32
     }
 }
 
+// a join chain's intermediate table: the cells later levels read of every joined
+// row (M: column k from side M.side[k], cell slot M.col[k]; NULL for a missing side)
+__global__ void join_gather_kernel(const uint2* __restrict__ pairs, unsigned long long np, JoinMap M,
+                                   const Cell* __restrict__ L, const Cell* __restrict__ R, Cell* __restrict__ out) {
+    const unsigned long long i = (unsigned long long)blockIdx.x * blockDim.x + threadIdx.x;
+    if (i >= np) return;
+    const uint2 pr = pairs[i];
+    for (int k = 0; k < M.n; k++) {
+        const uint32_t row = M.side[k] ? pr.y : pr.x;
+        Cell c = cell_null();
+        if (row != JOIN_NONE)
+            c = M.side[k] ? R[(uint64_t)row * M.rstride + M.col[k]] : L[(uint64_t)row * M.lstride + M.col[k]];
+        out[i * (uint64_t)M.n + k] = c;
+    }
+}
+
 // outer joins: pairs for the unmatched right rows (flags: 1 = unmatched; RIGHT / FULL, appended after
 // the left-major part in row order), or every row of one side (ON that matches
 // nothing: `ident = ident` not resolvable, or another condition shape)
@@ -2050,6 +2066,12 @@ hipError_t cq_launch_join_emit(const cq::Cell* L, uint32_t ls, uint32_t lk, uint
     if (!nL) return hipSuccess;
     hipLaunchKernelGGL(cq::join_emit_kernel, dim3(grid_of(nL, 256)), dim3(256), 0, s, L, ls, lk, nL, *J, lo, cnt, offs,
                        pairs, rmatched);
+    return hipGetLastError();
+}
+hipError_t cq_launch_join_gather(const uint2* pairs, unsigned long long np, const cq::JoinMap* M, const cq::Cell* L,
+                                 const cq::Cell* R, cq::Cell* out, hipStream_t s) {
+    const unsigned long long blocks = (np + 255) / 256;
+    hipLaunchKernelGGL(cq::join_gather_kernel, dim3((uint32_t)blocks), dim3(256), 0, s, pairs, np, *M, L, R, out);
     return hipGetLastError();
 }
 hipError_t cq_launch_join_fill(const unsigned int* flags, const unsigned int* pos, uint32_t n, unsigned long long base,

@@ -116,6 +116,7 @@ R = "'{D}/synth_role.csv'"
 A = "'{D}/synth_a.csv'"
 SU = "'{D}/synth_users.csv'"
 SO = "'{D}/synth_orders.csv'"
+P = "'{D}/products.csv'"
 QUERIES = [
     # config 1 (plumbing) and filter + COUNT
     f"SELECT COUNT(*) FROM {T} WHERE age > 30",
@@ -200,6 +201,16 @@ QUERIES = [
     f"SELECT COUNT(*) FROM {SU} AS u JOIN {SO} AS o ON u.id = o.customer_id",
     f"SELECT u.role, COUNT(*), SUM(o.price) FROM {SU} AS u JOIN {SO} AS o ON u.id = o.customer_id GROUP BY u.role",
     f"SELECT COUNT(*), SUM(o.price), AVG(o.quantity) FROM {SU} AS u JOIN {SO} AS o ON u.id = o.customer_id WHERE u.age > 40",
+    # join chains (process_joins, evaluator_joins.c:237-274: level 2 joins "joined")
+    f"SELECT COUNT(*) FROM {U} AS u JOIN {O} AS o ON u.id = o.customer_id JOIN {P} AS p ON o.id = p.id",
+    f"SELECT p.name, p.category, o.price FROM {U} AS u JOIN {O} AS o ON u.id = o.customer_id JOIN {P} AS p ON o.id = p.id",
+    f"SELECT p.category, COUNT(*), SUM(p.id), MAX(o.price) FROM {U} AS u JOIN {O} AS o ON u.id = o.customer_id JOIN {P} AS p ON o.id = p.id GROUP BY p.category",
+    f"SELECT COUNT(*) FROM {U} AS u LEFT JOIN {O} AS o ON u.id = o.customer_id LEFT JOIN {P} AS p ON o.id = p.id",
+    f"SELECT COUNT(*) FROM {U} AS u JOIN {O} AS o ON u.id = o.customer_id RIGHT JOIN {P} AS p ON o.id = p.id",
+    f"SELECT COUNT(*), SUM(p.id) FROM {U} AS u JOIN {O} AS o ON u.id = o.customer_id JOIN {P} AS p ON o.id = p.id WHERE p.id > 2",
+    f"SELECT COUNT(*) FROM {SU} AS u JOIN {SO} AS o ON u.id = o.customer_id JOIN {SU} AS v ON o.customer_id = v.id",
+    f"SELECT v.role, COUNT(*), AVG(v.age) FROM {SU} AS u JOIN {SO} AS o ON u.id = o.customer_id JOIN {SU} AS v ON o.customer_id = v.id GROUP BY v.role",
+    f"SELECT COUNT(*) FROM {U} AS u FULL JOIN {O} AS o ON u.id = o.customer_id JOIN {U} AS w ON o.id = w.id",
     # row-returning (build_result)
     f"SELECT name, age FROM {T} WHERE age > 30",
     f"SELECT * FROM {T} WHERE age > 30",

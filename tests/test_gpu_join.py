@@ -149,3 +149,30 @@ def test_join_mixed_classes(files, tmpl):
     """keys of different value classes compare "equal" (csv_reader.c:128): every
     left key meets every right key of another non-NULL class, in row order"""
     _check(tmpl.replace("{M}", str(files["mixed"])).replace("{A}", str(files["sa"])))
+
+
+# ---------------------------------------------------------------- join chains
+CHAINS = [
+    "SELECT COUNT(*) FROM '{users}' AS u JOIN '{orders}' AS o ON u.id = o.customer_id JOIN '{users}' AS v ON o.quantity = v.id",
+    "SELECT v.role, COUNT(*), AVG(v.age) FROM '{users}' AS u JOIN '{orders}' AS o ON u.id = o.customer_id JOIN '{users}' AS v ON o.quantity = v.id GROUP BY v.role",
+    "SELECT COUNT(*) FROM '{users}' AS u LEFT JOIN '{orders}' AS o ON u.id = o.customer_id LEFT JOIN '{sa}' AS s ON o.id = s.v",
+    "SELECT COUNT(*), SUM(s.v) FROM '{users}' AS u JOIN '{orders}' AS o ON u.id = o.customer_id RIGHT JOIN '{sa}' AS s ON o.id = s.v",
+    "SELECT s.k, s.v FROM '{users}' AS u JOIN '{orders}' AS o ON u.id = o.customer_id JOIN '{sa}' AS s ON o.id = s.v WHERE s.v < 40",
+    "SELECT COUNT(*) FROM '{sa}' AS a JOIN '{sb}' AS b ON a.k = b.k JOIN '{sa}' AS c ON b.w = c.v JOIN '{sb}' AS d ON c.v = d.w",
+    "SELECT s.k, COUNT(*) FROM '{users}' AS u FULL JOIN '{orders}' AS o ON u.id = o.customer_id JOIN '{sa}' AS s ON o.quantity = s.v GROUP BY s.k",
+]
+
+
+@pytest.mark.parametrize("tmpl", CHAINS)
+def test_join_chain_vs_oracle(files, tmpl):
+    sql = tmpl.format(**{k: str(v) for k, v in files.items()})
+    want, unsup = cqtest.oracle_query(sql)
+    assert not unsup
+    with cqtest.Parsed(sql) as ast:
+        got = cq_amd.evaluate(ast)
+    assert not cq_amd.last_ineligible(), (sql, cq_amd.last_ineligible())
+    from test_gpu_parity import compare
+    with cqtest.Parsed(sql) as ast:
+        from test_gpu_parity import tolerant_columns
+        tol = tolerant_columns(ast)
+    compare(got, want, tol, sql)
