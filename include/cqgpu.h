@@ -125,6 +125,14 @@ int cqgpu_route_fill(cqgpu_table* t, uint64_t gid_base, void* dev_bytes, uint64_
 cqgpu_table* cqgpu_table_from_routed(const void* dev_bytes, size_t n, const uint64_t* dev_gids, size_t nrec,
                                      cq_csv_config cfg, const char* header, size_t header_len);
 
+/* ---- output ----------------------------------------------------------------
+ * replaces write_csv_file (reference utils.c:220-289, called by main.c:133 for
+ * `-o FILE`): the same bytes for any result table -- header by the host, every
+ * row formatted on the GPU (%lld, %.2f, %04d-%02d-%02d, strings quoted when they
+ * hold the delimiter, a quote or a line break).  Returns 0, or -1 with a message
+ * on stderr. */
+int cqgpu_write_csv(const char* filename, const cq_table* result, char delimiter);
+
 /* ---- introspection -------------------------------------------------------- */
 typedef struct {
     double scan_ms;              /* device time of the last fused scan kernel (HIP events) */

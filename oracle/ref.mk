@@ -8,7 +8,10 @@
 #   cq_ref         the reference CLI (main.c + libcq objects), the CPU baseline
 #   ref_probe      our dump driver (oracle/ref_probe.c) linked against libcqref.so
 #   cq_amd_cli     the reference main.c linked with the front end + OUR libcqgpu.so:
-#                  the drop-in demonstration (built only when libcqgpu.so exists)
+#                  the drop-in demonstration (built only when libcqgpu.so exists);
+#                  main.o's call of write_csv_file (`-o`, main.c:133) is bound to
+#                  libcqgpu's GPU writer cqgpu_write_csv by renaming the undefined
+#                  symbol in a copy of the object (objcopy --redefine-sym)
 #
 # The reference Makefile uses `cc -O2` (Makefile:3); we add -fPIC for the .so.
 # Usage: make -f oracle/ref.mk REF=/root/reference
@@ -49,9 +52,13 @@ $(OUT)/cq_ref: $(MAIN_OBJ) $(FRONT_OBJ) $(EVAL_OBJ)
 $(OUT)/ref_probe: oracle/ref_probe.c $(OUT)/libcqref.so
 	$(CC) -O2 -I$(REF)/include -o $@ oracle/ref_probe.c -L$(OUT) -lcqref -lm -Wl,-rpath,'$$ORIGIN'
 
-# drop-in: unchanged reference CLI + front end, evaluator replaced by libcqgpu.so
-$(OUT)/cq_amd_cli: $(MAIN_OBJ) $(FRONT_OBJ) $(GPU_LIB)
-	$(CC) -o $@ $(MAIN_OBJ) $(FRONT_OBJ) -Lcq_amd/lib -lcqgpu -lm \
+# drop-in: unchanged reference CLI + front end, evaluator (and the -o writer)
+# replaced by libcqgpu.so
+$(OUT)/obj/main_gpu.o: $(MAIN_OBJ)
+	objcopy --redefine-sym write_csv_file=cqgpu_write_csv $< $@
+
+$(OUT)/cq_amd_cli: $(OUT)/obj/main_gpu.o $(FRONT_OBJ) $(GPU_LIB)
+	$(CC) -o $@ $(OUT)/obj/main_gpu.o $(FRONT_OBJ) -Lcq_amd/lib -lcqgpu -lm \
 	    -Wl,-rpath,'$$ORIGIN/../../cq_amd/lib'
 
 clean:
