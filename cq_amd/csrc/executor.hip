@@ -70,9 +70,6 @@ hipError_t cq_launch_join_gather(const uint2* pairs, unsigned long long np, cons
                                  const cq::Cell* R, cq::Cell* out, hipStream_t s);
 hipError_t cq_sort_classes(void* temp, size_t* temp_bytes, const unsigned int* kin, unsigned int* kout,
                            const unsigned int* vin, unsigned int* vout, size_t n, hipStream_t s);
-hipError_t cq_sort_codes_seg(void* temp, size_t* temp_bytes, const unsigned long long* kin, unsigned long long* kout,
-                             const unsigned int* vin, unsigned int* vout, size_t n, const int* seg_begin,
-                             const int* seg_end, int nseg, hipStream_t s);
 hipError_t cq_launch_join_agg(const uint2* pairs, unsigned long long np, const cq::JoinMap* M, const cq::Cell* L,
                               const cq::Cell* R, const cq::ScanPlan* P, const cq::GroupTable* gt,
                               cq::ScanStats* stats, int grouped, hipStream_t s);

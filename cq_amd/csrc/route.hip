@@ -15,7 +15,7 @@
 // join's (l, r) nested-loop order is the global one restricted to this rank.
 // Work is byte copying: HBM-bound, no LDS, no MFMA.
 #include <hip/hip_runtime.h>
-#include <hipcub/hipcub.hpp>
+
 #include <stdint.h>
 
 namespace {
@@ -200,11 +200,6 @@ hipError_t cq_launch_route_bounds(const uint32_t* dsorted, const unsigned long l
 }
 
 // stable sort of record indices by destination rank
-hipError_t cq_sort_dest(void* temp, size_t* temp_bytes, const unsigned int* kin, unsigned int* kout,
-                        const unsigned int* vin, unsigned int* vout, size_t n, int bits, hipStream_t s) {
-    return hipcub::DeviceRadixSort::SortPairs(temp, *temp_bytes, kin, kout, vin, vout, (int)n, 0, bits, s);
-}
-
 hipError_t cq_launch_gather_len(const uint32_t* len, const uint32_t* order, uint32_t n, unsigned long long* out,
                                 hipStream_t s) {
     if (!n) return hipSuccess;
