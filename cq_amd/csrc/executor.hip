@@ -59,6 +59,10 @@ hipError_t cq_launch_join_code(const cq::Cell* cells, uint32_t stride, uint32_t 
                                hipStream_t s);
 hipError_t cq_launch_gather_codes(const unsigned long long* codes, const uint32_t* idx, uint32_t n,
                                   unsigned long long* out, hipStream_t s);
+hipError_t cq_launch_hash_build(const unsigned long long* codes, const uint32_t* cls, uint32_t n, const cq::JoinHashW* H,
+                                uint32_t* sid, unsigned long long* overflow, hipStream_t s);
+hipError_t cq_sort_u32(void* temp, size_t* temp_bytes, const unsigned int* kin, unsigned int* kout,
+                       const unsigned int* vin, unsigned int* vout, size_t n, int bits, hipStream_t s);
 hipError_t cq_launch_join_count(const cq::Cell* L, uint32_t ls, uint32_t lk, uint32_t nL, const cq::JoinRight* J,
                                 int outer_left, uint32_t* lo, unsigned long long* cnt, hipStream_t s);
 hipError_t cq_launch_join_emit(const cq::Cell* L, uint32_t ls, uint32_t lk, uint32_t nL, const cq::JoinRight* J,
@@ -2261,10 +2265,10 @@ unsigned long long build_pairs(DevCtx& c, JoinSide& A, JoinSide& B, int kl, int 
     if (keyed && A.n && B.n) {
         const uint32_t ls = (uint32_t)A.cols.size(), rs = (uint32_t)B.cols.size();
         const uint32_t lk = (uint32_t)A.slot(kl), rk = (uint32_t)B.slot(kr);
-        // right side: codes and classes, rows grouped by class, then sorted by code per class
+        // right side: codes and classes; rows grouped by class (the cross-class
+        // streams); the hash table of distinct keys and the rows sorted by key slot
         DevBuf rcodes((size_t)B.n * 8), rcls((size_t)B.n * 4), ridx((size_t)B.n * 4), ccls((size_t)B.n * 4),
-            ridx_c((size_t)B.n * 4), codes_c((size_t)B.n * 8), scodes((size_t)B.n * 8), sidx((size_t)B.n * 4),
-            pc(64);
+            ridx_c((size_t)B.n * 4), pc(64);
         HIPCHECK(hipMemsetAsync(pc.p, 0, 64, c.stream));
         HIPCHECK(cq_launch_join_code(B.cells.as<Cell>(), rs, rk, B.n, rcodes.as<unsigned long long>(),
                                      rcls.as<uint32_t>(), ridx.as<uint32_t>(), pc.as<unsigned int>(), c.stream));
@@ -2274,41 +2278,46 @@ unsigned long long build_pairs(DevCtx& c, JoinSide& A, JoinSide& B, int kl, int 
         DevBuf temp(tb);
         HIPCHECK(cq_sort_classes(temp.p, &tb, rcls.as<unsigned int>(), ccls.as<unsigned int>(), ridx.as<unsigned int>(),
                                  ridx_c.as<unsigned int>(), B.n, c.stream));
+        int hbits = 6;
+        while (hbits < 31 && (1ull << hbits) < 2ull * B.n) hbits++;
+        const uint32_t cap = 1u << hbits;
+        DevBuf hstate((size_t)cap * 4), hcode((size_t)cap * 8), hcls((size_t)cap * 4), hcnt((size_t)cap * 4),
+            hstart((size_t)cap * 4), sid((size_t)B.n * 4), ssid((size_t)B.n * 4), sidx((size_t)B.n * 4);
+        HIPCHECK(hipMemsetAsync(hstate.p, 0, (size_t)cap * 4, c.stream));
+        HIPCHECK(hipMemsetAsync(hcnt.p, 0, (size_t)cap * 4, c.stream));
+        JoinHashW HW;
+        HW.state = hstate.as<uint32_t>(); HW.code = hcode.as<unsigned long long>(); HW.cls = hcls.as<uint32_t>();
+        HW.cnt = hcnt.as<uint32_t>(); HW.cap = cap;
+        unsigned long long* dovf = (unsigned long long*)((uint8_t*)pc.p + 32);
+        HIPCHECK(hipMemsetAsync(dovf, 0, 8, c.stream));
+        HIPCHECK(cq_launch_hash_build(rcodes.as<unsigned long long>(), rcls.as<uint32_t>(), B.n, &HW, sid.as<uint32_t>(),
+                                      dovf, c.stream));
+        size_t tbs = 0;
+        HIPCHECK(cq_excl_sum_u32(nullptr, &tbs, hcnt.as<unsigned int>(), hstart.as<unsigned int>(), cap, c.stream));
+        size_t tbr = 0;
+        HIPCHECK(cq_sort_u32(nullptr, &tbr, sid.as<unsigned int>(), ssid.as<unsigned int>(), ridx.as<unsigned int>(),
+                             sidx.as<unsigned int>(), B.n, hbits, c.stream));
+        DevBuf temp1(std::max(tbs, tbr));
+        HIPCHECK(cq_excl_sum_u32(temp1.p, &tbs, hcnt.as<unsigned int>(), hstart.as<unsigned int>(), cap, c.stream));
+        tbr = std::max(tbs, tbr);
+        HIPCHECK(cq_sort_u32(temp1.p, &tbr, sid.as<unsigned int>(), ssid.as<unsigned int>(), ridx.as<unsigned int>(),
+                             sidx.as<unsigned int>(), B.n, hbits, c.stream));
         unsigned int per[4] = {0, 0, 0, 0};
+        unsigned long long ovf = 0;
         HIPCHECK(hipMemcpyAsync(per, pc.p, 16, hipMemcpyDeviceToHost, c.stream));
+        HIPCHECK(hipMemcpyAsync(&ovf, dovf, 8, hipMemcpyDeviceToHost, c.stream));
         HIPCHECK(hipStreamSynchronize(c.stream));
+        if (ovf) throw HipError{"join hash build: table full or insert timeout"};
         JoinRight JR;
         memset(&JR, 0, sizeof JR);
         JR.seg[0] = 0;
         for (int k = 0; k < 4; k++) JR.seg[k + 1] = JR.seg[k] + per[k];
-        int segs[8];
-        for (int k = 0; k < 4; k++) { segs[k] = (int)JR.seg[k]; segs[4 + k] = (int)JR.seg[k + 1]; }
-        int* dsegs = (int*)((uint8_t*)pc.p + 32);
-        HIPCHECK(hipMemcpyAsync(dsegs, segs, 32, hipMemcpyHostToDevice, c.stream));
-        HIPCHECK(cq_launch_gather_codes(rcodes.as<unsigned long long>(), ridx_c.as<uint32_t>(), B.n,
-                                        codes_c.as<unsigned long long>(), c.stream));
-        // within each class segment by code (stable); one full-width radix sort per
-        // non-empty segment (a segmented sort runs each segment in one workgroup)
-        size_t tb1 = 0;
-        for (int k = 0; k < 4; k++) {
-            if (!per[k]) continue;
-            size_t tk = 0;
-            HIPCHECK(cq_sort_codes(nullptr, &tk, codes_c.as<unsigned long long>(), scodes.as<unsigned long long>(),
-                                   ridx_c.as<unsigned int>(), sidx.as<unsigned int>(), per[k], c.stream));
-            tb1 = std::max(tb1, tk);
-        }
-        DevBuf temp1(tb1);
-        for (int k = 0; k < 4; k++) {
-            if (!per[k]) continue;
-            const size_t o = JR.seg[k];
-            size_t tk = tb1;
-            HIPCHECK(cq_sort_codes(temp1.p, &tk, codes_c.as<unsigned long long>() + o,
-                                   scodes.as<unsigned long long>() + o, ridx_c.as<unsigned int>() + o,
-                                   sidx.as<unsigned int>() + o, per[k], c.stream));
-        }
-        (void)dsegs;
-        HIPCHECK(hipStreamSynchronize(c.stream));        // segs (host) and the sort's inputs stay alive until here
-        JR.scodes = scodes.as<unsigned long long>();
+        JR.hstate = hstate.as<uint32_t>();
+        JR.hcode = hcode.as<unsigned long long>();
+        JR.hcls = hcls.as<uint32_t>();
+        JR.hstart = hstart.as<uint32_t>();
+        JR.hcnt = hcnt.as<uint32_t>();
+        JR.hcap = cap;
         JR.sidx = sidx.as<uint32_t>();
         JR.ridx_c = ridx_c.as<uint32_t>();
         JR.cells = B.cells.as<Cell>();

@@ -118,12 +118,27 @@ struct JoinMap {
 // the right side of a join, sorted by key class then by key code (scan.hip
 // join_count_kernel / join_emit_kernel)
 struct JoinRight {
-    const unsigned long long* scodes;   // codes, sorted within each class segment
-    const uint32_t* sidx;               // row of each sorted code
+    // open-addressing hash table of the right side's distinct keys (value class, code)
+    const uint32_t* hstate;             // 0 empty, else published
+    const unsigned long long* hcode;
+    const uint32_t* hcls;
+    const uint32_t* hstart;             // the key's first position in sidx
+    const uint32_t* hcnt;               // its rows
+    uint32_t hcap;                      // slots, a power of two
+    const uint32_t* sidx;               // right rows grouped by key slot, row order within a slot
     const uint32_t* ridx_c;             // rows grouped by class, row order within a class
     const Cell* cells;
     uint32_t stride, kcol;
     uint32_t seg[5];                    // class segment bounds (0 NULL, 1 number, 2 string, 3 date)
+};
+
+// the same table while it is built (hash_build_kernel)
+struct JoinHashW {
+    uint32_t* state;
+    unsigned long long* code;
+    uint32_t* cls;
+    uint32_t* cnt;
+    uint32_t cap;
 };
 
 // scan statistics written by the kernel (one per launch)

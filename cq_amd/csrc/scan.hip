@@ -1341,15 +1341,14 @@ __global__ void parse_literals_kernel(const uint8_t* __restrict__ text,
     out[i] = parse_cell(text + offs[i], lens[i]);
 }
 
-// ------------------------------------------------------------------ INNER JOIN
-// perform_join (evaluator_joins.c:63-181) as a hash-free sort join on the device:
-// the right side's key codes are radix-sorted (stable, so equal keys keep row
-// order), every left row binary-searches its run, and the (l, r) pairs come out
-// in the reference's nested-loop order (left rows ascending, then right rows).
-// value_compare (csv_reader.c:98-130) equality is what "matches" means:
-// numbers compare as doubles, strings by strcmp, dates by (y, m, d), NULL = NULL;
-// the host refuses key columns that mix value classes (cross-class pairs
-// compare "equal" in the reference).
+// ------------------------------------------------------------------ JOIN
+// perform_join (evaluator_joins.c:63-181) as a hash join on the device: the
+// right side's keys are built into a hash table (hash_build_kernel) with the
+// rows of each key kept in row order, every left row probes it for its run, and
+// the (l, r) pairs come out in the reference's nested-loop order (left rows
+// ascending, then right rows).  value_compare (csv_reader.c:98-130) equality is
+// what "matches" means: numbers compare as doubles, strings by strcmp, dates by
+// (y, m, d), NULL = NULL, and keys of different non-NULL classes compare "equal".
 
 // the columns of one side, parsed per record (parse_line + parse_value)
 __global__ void cells_kernel(const uint8_t* __restrict__ g, const unsigned long long* __restrict__ recs, uint32_t n,
@@ -1403,23 +1402,82 @@ __global__ void gather_codes_kernel(const unsigned long long* __restrict__ codes
     if (i < n) out[i] = codes[idx[i]];
 }
 
-// The right side after two stable sorts: by class (ridx_c: per-class row lists
-// in row order, segments seg[0..4]) and then by code within each class (scodes /
-// sidx).  A left row's matches: its class's equal-code run (STRING codes are
-// hashes: verified byte for byte) merged by row number with the whole lists of the
-// other non-NULL classes.
+// The right side's build: every distinct key (value class, code) gets one slot of
+// an open-addressing hash table in HBM (linear probing, at most half full); the
+// rows sorted stably by slot (sidx) put each key's rows together in row order,
+// hstart / hcnt delimiting them.  A left row probes the table once for its run;
+// STRING codes are hashes, so their candidates are verified byte for byte.  The
+// other non-NULL classes' rows, which value_compare calls equal to any key of
+// another class (csv_reader.c:128), are the class lists ridx_c.
+__device__ __forceinline__ uint64_t hj_hash(unsigned long long code, uint32_t cls) {
+    return mix64(code ^ ((uint64_t)cls << 62) ^ 0x243F6A8885A308D3ULL);
+}
 
+// slot of every right row's key (inserted when new); row counts per slot.  The
+// probe loop is wave-uniform (it runs while any lane of the wave still looks for
+// its slot, one probe per lane per trip): a lane that finds a slot claimed but
+// not yet published retries it on the next trip instead of spinning, so the
+// claiming lane -- perhaps in the same wave -- always gets to publish.
+__global__ void hash_build_kernel(const unsigned long long* __restrict__ codes, const uint32_t* __restrict__ cls,
+                                  uint32_t n, JoinHashW H, uint32_t* __restrict__ sid,
+                                  unsigned long long* __restrict__ overflow) {
+    const uint32_t r = blockIdx.x * blockDim.x + threadIdx.x;
+    bool pending = r < n;
+    const unsigned long long code = pending ? codes[r] : 0ull;
+    const uint32_t k = pending ? cls[r] : 0u;
+    const uint32_t mask = H.cap - 1;
+    uint32_t i = (uint32_t)hj_hash(code, k) & mask, slot = 0, probes = 0;
+    for (uint32_t trip = 0; __any(pending); trip++) {
+        if (pending) {
+            uint32_t st = __hip_atomic_load(&H.state[i], __ATOMIC_ACQUIRE, __HIP_MEMORY_SCOPE_AGENT);
+            if (st == 0) {
+                const uint32_t old = atomicCAS(&H.state[i], 0u, 1u);
+                if (old == 0) {                          // claimed: key words first, then publish
+                    __hip_atomic_store(&H.code[i], code, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+                    __hip_atomic_store(&H.cls[i], k, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+                    __hip_atomic_store(&H.state[i], 2u, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_AGENT);
+                    slot = i;
+                    pending = false;
+                }
+                st = old;
+            }
+            if (pending && st == 2) {
+                if (__hip_atomic_load(&H.code[i], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) == code &&
+                    __hip_atomic_load(&H.cls[i], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) == k) {
+                    slot = i;
+                    pending = false;
+                } else {
+                    i = (i + 1) & mask;
+                    if (++probes >= H.cap) { atomicExch(overflow, 1ULL); pending = false; }   // full
+                }
+            }
+            // st == 1: claimed, not yet published -- the same slot again next trip
+        }
+        if (trip > (1u << 24)) {                          // never hang: report and stop
+            if (pending) atomicExch(overflow, 3ULL);
+            break;
+        }
+    }
+    if (r < n) {
+        atomicAdd(&H.cnt[slot], 1u);
+        sid[r] = slot;
+    }
+}
 
+// [lo, hi) in sidx of the right rows whose key has this class and code
 __device__ __forceinline__ void eq_run(const JoinRight& J, uint32_t k, unsigned long long code, uint32_t& lo,
                                        uint32_t& hi) {
-    uint32_t a = J.seg[k], b = J.seg[k + 1];
-    while (a < b) {
-        const uint32_t mid = (a + b) >> 1;
-        if (J.scodes[mid] < code) a = mid + 1; else b = mid;
+    lo = hi = 0;
+    const uint32_t mask = J.hcap - 1;
+    uint32_t i = (uint32_t)hj_hash(code, k) & mask;
+    for (uint32_t probe = 0; probe < J.hcap; probe++, i = (i + 1) & mask) {
+        if (J.hstate[i] == 0) return;
+        if (J.hcode[i] == code && J.hcls[i] == k) {
+            lo = J.hstart[i];
+            hi = lo + J.hcnt[i];
+            return;
+        }
     }
-    lo = a;
-    hi = a;
-    while (hi < J.seg[k + 1] && J.scodes[hi] == code) hi++;
 }
 
 __global__ void join_count_kernel(const Cell* __restrict__ L, uint32_t ls, uint32_t lk, uint32_t nL, JoinRight J,
@@ -1456,8 +1514,9 @@ __global__ void join_emit_kernel(const Cell* __restrict__ L, uint32_t ls, uint32
     const uint32_t k = key_class(kc);
     const unsigned long long code = join_code(kc);
     // three row-ordered streams: the equal run, and the other two non-NULL classes
-    uint32_t e = lo_in[l];
-    const uint32_t ee = J.seg[k + 1];
+    uint32_t e, ee;
+    eq_run(J, k, code, e, ee);
+    (void)lo_in;
     uint32_t ya = 0, yb = 0, za = 0, zb = 0;
     if (k != 0) {
         const uint32_t y = k == 1 ? 2 : 1, z = k == 3 ? 2 : 3;
@@ -1468,7 +1527,7 @@ __global__ void join_emit_kernel(const Cell* __restrict__ L, uint32_t ls, uint32
     for (unsigned long long m = 0; m < want; m++) {
         // next verified row of the equal run (~0: exhausted)
         uint32_t re = 0xFFFFFFFFu;
-        while (e < ee && J.scodes[e] == code) {
+        while (e < ee) {
             const uint32_t r = J.sidx[e];
             if (k != 2 || compare(kc, J.cells[(uint64_t)r * J.stride + J.kcol]) == 0) { re = r; break; }
             e++;
@@ -2072,6 +2131,12 @@ hipError_t cq_launch_join_gather(const uint2* pairs, unsigned long long np, cons
                                  const cq::Cell* R, cq::Cell* out, hipStream_t s) {
     const unsigned long long blocks = (np + 255) / 256;
     hipLaunchKernelGGL(cq::join_gather_kernel, dim3((uint32_t)blocks), dim3(256), 0, s, pairs, np, *M, L, R, out);
+    return hipGetLastError();
+}
+hipError_t cq_launch_hash_build(const unsigned long long* codes, const uint32_t* cls, uint32_t n, const cq::JoinHashW* H,
+                                uint32_t* sid, unsigned long long* overflow, hipStream_t s) {
+    if (!n) return hipSuccess;
+    hipLaunchKernelGGL(cq::hash_build_kernel, dim3((n + 255) / 256), dim3(256), 0, s, codes, cls, n, *H, sid, overflow);
     return hipGetLastError();
 }
 hipError_t cq_launch_join_fill(const unsigned int* flags, const unsigned int* pos, uint32_t n, unsigned long long base,
