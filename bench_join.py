@@ -2,9 +2,9 @@
 """Join benchmark: BASELINE.json configs[4] shape (users x orders hash join), weak-scaled.
 
 Per GPU: `--users` users rows and `--orders` orders rows (synthetic, seed 42;
-users id = 10^10 + i, orders customer_id = 10^10 + U[0, N x users), i.e. SURVEY.md
-section 8d's config 5 at a per-GPU size that fits one step in seconds), resident in
-HBM as CSV bytes.  One step = the whole repartitioned join of
+users id = 10^10 + i, orders customer_id = 10^10 + U[0, N x users)), resident in HBM
+as CSV bytes; the default 62.5 M + 62.5 M is one rank's share of SURVEY.md section
+8d's config 5 (500 M x 500 M over 8 GPUs).  One step = the whole repartitioned join of
     SELECT u.role, COUNT(*), SUM(o.price) FROM 'users.csv' AS u
     JOIN 'orders.csv' AS o ON u.id = o.customer_id GROUP BY u.role
 on every rank: device key routing of both shards (route.hip), the record
@@ -15,7 +15,12 @@ the partial-blob all_gather and the merge on rank 0.
     python bench_join.py [--gpus N] [--steps K] [--warmup W] [--users U] [--orders O]
 
 Prints one JSON line (rank 0): rows/s = (users + orders rows, all ranks) / step
-time, plus the joined pair count (= all orders rows: every customer_id exists).
+time; `roofline`: the step's algorithmic HBM bytes (both CSV shards read once, the
+minimum any implementation moves) / step time against 8 TB/s; `verified`: the
+joined pair count (= all orders rows: every customer_id exists) and, at N = 1, the
+per-role COUNT / SUM(price) recomputed from the generators' draws (counts exact,
+sums 1e-6 relative); the reference CPU evaluator timed in the same run on an
+n x n sample (row-pairs/s: its join is a nested loop, so not comparable).
 Not the driver's bench line (bench.py is); a measurement of the join path.
 """
 import argparse
@@ -72,6 +77,20 @@ def orders_shard(n: int, first_id: int, n_users_total: int, rng) -> bytes:
     return m.tobytes()
 
 
+def expected_roles(users: int, orders: int, seed: int):
+    """per-role (COUNT, SUM(price) in cents) of the N = 1 join, from the same draws
+    users_shard / orders_shard make (rank 0's generator)"""
+    rng = np.random.default_rng([seed, 0])
+    rng.integers(65, 81, users)                        # names
+    rng.integers(10, 81, users)                        # ages
+    role = rng.integers(0, 1000, users)
+    price = rng.integers(100, 100000, orders)
+    rng.integers(1, 10, orders)                        # quantities
+    cust = rng.integers(0, users, orders)
+    r = role[cust]
+    return np.bincount(r, minlength=1000), np.bincount(r, weights=price, minlength=1000)
+
+
 def cpu_baseline(n: int, seed: int):
     """The unmodified reference (oracle/_ref/ref_probe, 1 core) on an n x n sample of
     the same generators.  Its nested-loop join is O(L x R) (evaluator_joins.c:63-181),
@@ -106,8 +125,8 @@ def main():
     ap.add_argument("--gpus", type=int, default=1)
     ap.add_argument("--steps", type=int, default=5)
     ap.add_argument("--warmup", type=int, default=1)
-    ap.add_argument("--users", type=int, default=20_000_000, help="users rows per GPU")
-    ap.add_argument("--orders", type=int, default=20_000_000, help="orders rows per GPU")
+    ap.add_argument("--users", type=int, default=62_500_000, help="users rows per GPU")
+    ap.add_argument("--orders", type=int, default=62_500_000, help="orders rows per GPU")
     ap.add_argument("--seed", type=int, default=42)
     ap.add_argument("--cpu-rows", type=int, default=5000, help="n of the reference's n x n join sample")
     ap.add_argument("--no-cpu", action="store_true")
@@ -147,6 +166,7 @@ def main():
                         abi.JOIN_INNER)])
     ast = C.pointer(q)
     phase = {}
+    last_res = [None]
 
     def step():
         ts = time.perf_counter()
@@ -178,6 +198,7 @@ def main():
             res = abi.table_to_py(tp)
             cq_amd.result_free(tp)
             pairs = int(sum(r[1][1] for r in res["rows"]))   # COUNT(*) cells: ("I", n)
+            last_res[0] = res
         for t in routed:
             t.close()
         te = time.perf_counter()
@@ -209,6 +230,7 @@ def main():
         dist.all_reduce(t, op=dist.ReduceOp.MAX)
         elapsed = float(t.item())
     rows_total = (args.users + args.orders) * world
+    verified = True
     if rank == 0:
         cpu = None
         if world == 1 and not args.no_cpu:
@@ -216,10 +238,27 @@ def main():
                 cpu = cpu_baseline(args.cpu_rows, args.seed)
             except Exception as e:  # reported, never fatal
                 print(f"cpu baseline failed: {e}", file=sys.stderr)
-        if pairs != args.orders * world:
-            print(f"warning: {pairs} joined pairs, expected {args.orders * world}", file=sys.stderr)
+        verified = pairs == args.orders * world
+        if not verified:
+            print(f"VERIFY FAILED: {pairs} joined pairs, expected {args.orders * world}", file=sys.stderr)
+        verified_against = "pair count = orders rows"
+        if world == 1 and verified:
+            cnt, cents = expected_roles(args.users, args.orders, args.seed)
+            got = {r[0][1].decode(): (r[1][1], r[2][1]) for r in last_res[0]["rows"]}
+            for k in range(1000):
+                if not cnt[k]:
+                    continue
+                g = got.get("role_%03d" % k)
+                want_sum = cents[k] / 100.0
+                if g is None or g[0] != cnt[k] or abs(g[1] - want_sum) > 1e-6 * want_sum:
+                    verified = False
+                    print(f"VERIFY FAILED: role_{k:03d} got {g} want ({cnt[k]}, {want_sum})", file=sys.stderr)
+                    break
+            verified_against = "per-role COUNT / SUM(price) from the generators' draws (numpy)"
+        step_s = elapsed / args.steps
+        achieved = in_bytes * world / step_s / 1e9 / world
         line = {
-            "metric": "join rows/s (users + orders rows, key-repartitioned hash join + GROUP BY)",
+            "metric": "join rows/s (users + orders rows, key-repartitioned device hash join + GROUP BY)",
             "value": rows_total / (elapsed / args.steps),
             "unit": "rows/s",
             "n_gpus": world,
@@ -240,6 +279,12 @@ def main():
                 "joined_pairs": pairs,
                 "parallelism": f"dp{world} (hash repartition all_to_all over RCCL)",
             },
+            "verified": verified,
+            "verified_against": verified_against,
+            "roofline": {"bound": "hbm", "achieved": achieved, "peak": 8000.0, "unit": "GB/s",
+                         "frac": achieved / 8000.0, "traffic": None,
+                         "algorithmic_bytes": "both CSV shards read once per step (bytes_per_gpu); the "
+                                              "pipeline also writes and re-reads routed copies, cells and pairs"},
             "phases_ms": {k: sum(v) / len(v) for k, v in phase.items()},
             "cpu_baseline": cpu,
             "setup_s": gen_s,
@@ -250,6 +295,8 @@ def main():
     if dist is not None:
         dist.barrier()
         dist.destroy_process_group()
+    if rank == 0 and not verified:
+        sys.exit(3)
 
 
 if __name__ == "__main__":

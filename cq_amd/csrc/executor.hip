@@ -52,13 +52,15 @@ hipError_t cq_launch_copy_strings(const Cell* cells, uint32_t n, const unsigned 
                                   uint8_t* out, hipStream_t s);
 cq::Cell cq_host_parse_cell(const uint8_t* text, uint32_t len);
 cq::Cell cq_host_eval(const cq::Insn* code, uint32_t n, const cq::Cell* cols, const cq::Cell* consts);
-hipError_t cq_launch_cells(const uint8_t* g, const unsigned long long* recs, uint32_t n, const cq::ColsDesc* D,
-                           cq::Cell* out, hipStream_t s);
+hipError_t cq_launch_cells(const uint8_t* g, uint64_t tn, const unsigned long long* recs, uint32_t n,
+                           const cq::ColsDesc* D, cq::Cell* out, hipStream_t s);
 hipError_t cq_launch_join_code(const cq::Cell* cells, uint32_t stride, uint32_t kcol, uint32_t n,
                                unsigned long long* codes, uint32_t* cls, uint32_t* idx, unsigned int* per_class,
                                hipStream_t s);
 hipError_t cq_launch_gather_codes(const unsigned long long* codes, const uint32_t* idx, uint32_t n,
                                   unsigned long long* out, hipStream_t s);
+hipError_t cq_launch_class_mask(const cq::Cell* cells, uint32_t stride, uint32_t kcol, uint32_t n, unsigned int* mask,
+                                hipStream_t s);
 hipError_t cq_launch_hash_build(const unsigned long long* codes, const uint32_t* cls, uint32_t n, const cq::JoinHashW* H,
                                 uint32_t* sid, unsigned long long* overflow, hipStream_t s);
 hipError_t cq_sort_u32(void* temp, size_t* temp_bytes, const unsigned int* kin, unsigned int* kout,
@@ -1919,7 +1921,7 @@ void compute_vla(DevCtx& c, const cqgpu_table* t, const Compiled& C, std::vector
     D.quote = (uint8_t)t->cfg.quote;
     auto slot = [&](int col) { return (int)(std::find(cols.begin(), cols.end(), col) - cols.begin()); };
     DevBuf cells((size_t)std::max<uint32_t>(n, 1) * D.ncols * sizeof(Cell));
-    HIPCHECK(cq_launch_cells(t->g, rows.as<unsigned long long>(), n, &D, cells.as<Cell>(), c.stream));
+    HIPCHECK(cq_launch_cells(t->g, t->n, rows.as<unsigned long long>(), n, &D, cells.as<Cell>(), c.stream));
     // host map: group key -> group (GK_LONG keys by content hash, as the kernel keys them)
     std::map<std::tuple<uint64_t, uint64_t, uint64_t>, size_t> at;
     for (size_t g = 0; g < groups.size(); g++) {
@@ -2104,7 +2106,7 @@ void load_side(DevCtx& c, const cqgpu_table* t, JoinSide& S) {
     D.quote = (uint8_t)t->cfg.quote;
     DevBuf cells((size_t)std::max<uint32_t>(S.n, 1) * std::max(D.ncols, 1) * sizeof(Cell));
     std::swap(S.cells.p, cells.p);
-    HIPCHECK(cq_launch_cells(t->g, S.recs.as<unsigned long long>(), S.n, &D, S.cells.as<Cell>(), c.stream));
+    HIPCHECK(cq_launch_cells(t->g, t->n, S.recs.as<unsigned long long>(), S.n, &D, S.cells.as<Cell>(), c.stream));
 }
 
 // joined column -> (side, cell index)
@@ -2241,17 +2243,13 @@ std::vector<HGroup> aggregate_pairs(DevCtx& c, Compiled& C, const JoinMap& MA, c
 uint32_t key_class_mask(DevCtx& c, const JoinSide& S, int kcol) {
     if (!S.n) return 0;
     const uint32_t stride = (uint32_t)S.cols.size(), k = (uint32_t)S.slot(kcol);
-    DevBuf codes((size_t)S.n * 8), cls((size_t)S.n * 4), pc(64);
-    HIPCHECK(hipMemsetAsync(pc.p, 0, 64, c.stream));
-    HIPCHECK(cq_launch_join_code(S.cells.as<Cell>(), stride, k, S.n, codes.as<unsigned long long>(), cls.as<uint32_t>(),
-                                 nullptr, pc.as<unsigned int>(), c.stream));
-    unsigned int per[4] = {0, 0, 0, 0};
-    HIPCHECK(hipMemcpyAsync(per, pc.p, 16, hipMemcpyDeviceToHost, c.stream));
+    DevBuf dm(64);
+    HIPCHECK(hipMemsetAsync(dm.p, 0, 4, c.stream));
+    HIPCHECK(cq_launch_class_mask(S.cells.as<Cell>(), stride, k, S.n, dm.as<unsigned int>(), c.stream));
+    unsigned int m = 0;
+    HIPCHECK(hipMemcpyAsync(&m, dm.p, 4, hipMemcpyDeviceToHost, c.stream));
     HIPCHECK(hipStreamSynchronize(c.stream));
-    uint32_t m = 0;
-    for (int j = 1; j < 4; j++)
-        if (per[j]) m |= 1u << j;
-    return m;
+    return m & 0xEu;                                   // classes 1-3 (NULL keys match only NULL)
 }
 
 // (l, r) pairs of one join level in the nested loop's order (perform_join,

@@ -1350,12 +1350,64 @@ __global__ void parse_literals_kernel(const uint8_t* __restrict__ text,
 // what "matches" means: numbers compare as doubles, strings by strcmp, dates by
 // (y, m, d), NULL = NULL, and keys of different non-NULL classes compare "equal".
 
-// the columns of one side, parsed per record (parse_line + parse_value)
-__global__ void cells_kernel(const uint8_t* __restrict__ g, const unsigned long long* __restrict__ recs, uint32_t n,
-                             ColsDesc D, Cell* __restrict__ out) {
-    const uint32_t i = blockIdx.x * blockDim.x + threadIdx.x;
+// The columns of one side, parsed per record (parse_line + parse_value).  A block
+// takes 256 consecutive records: their bytes (one contiguous span of the table,
+// the records being in file order) are staged into LDS with coalesced 16-byte
+// loads, and each thread then walks its record there; STRING cells are rebased to
+// their HBM bytes.  A span too long for the buffer walks the record in HBM.
+constexpr uint32_t CELLS_T = 256;
+constexpr uint32_t CELLS_SPAN = 16384;
+__global__ __launch_bounds__(CELLS_T) void cells_kernel(const uint8_t* __restrict__ g, uint64_t tn,
+                                                        const unsigned long long* __restrict__ recs, uint32_t n,
+                                                        ColsDesc D, Cell* __restrict__ out) {
+    __shared__ __align__(16) uint8_t buf[CELLS_SPAN + 64];
+    const uint32_t first = blockIdx.x * CELLS_T;
+    const uint32_t last = first + CELLS_T < n ? first + CELLS_T : n;
+    const uint64_t lo = recs[first] & ~15ull;
+    const uint64_t hi = last < n ? recs[last] : tn + 16;    // the table has '\n' padding after byte tn
+    const uint64_t span = hi - lo + 48;                     // + strtod look-ahead past the last field
+    const bool staged = span <= CELLS_SPAN;
+    if (staged) {
+        const uint32_t nch = (uint32_t)((span + 15) / 16);
+        const v4u* src = (const v4u*)(g + lo);
+        for (uint32_t c = threadIdx.x; c < nch; c += CELLS_T) ((v4u*)buf)[c] = __builtin_nontemporal_load(src + c);
+    }
+    __syncthreads();
+    const uint32_t i = first + threadIdx.x;
     if (i >= n) return;
-    parse_cols_out(g + recs[i], D.cols, D.ncols, D.delim, D.quote, out + (uint64_t)i * D.ncols, 1);
+    const uint64_t r = recs[i];
+    Cell* o = out + (uint64_t)i * D.ncols;
+    if (!staged || r < lo || r - lo >= span - 48) {      // (record lists out of file order stay correct)
+        parse_cols_out(g + r, D.cols, D.ncols, D.delim, D.quote, o, 1);
+        return;
+    }
+    const uint32_t off = (uint32_t)(r - lo);
+    const Src S{buf + off, g + r, (uint32_t)span - off, true};
+    uint32_t j = 0, fs = 0, flen = 0;
+    int col = 0;
+    bool ended = false;
+    for (int k = 0; k < D.ncols; k++) {
+        const int want = D.cols[k];
+        Cell c = cell_null();
+        while (!ended && col < want) {
+            if (!g_field(S, j, D.delim, D.quote, fs, flen) || S.at(j) != D.delim) ended = true;
+            else { j = j + 1; col++; }
+        }
+        if (!ended && col == want) {
+            if (!g_field(S, j, D.delim, D.quote, fs, flen)) {
+                ended = true;
+            } else {
+                c = parse_cell(S.ptr(fs, flen), flen);
+                if (c.kind == K_STR) {                      // point at the HBM copy of the bytes
+                    const uint8_t* p = (const uint8_t*)(uintptr_t)c.bits;
+                    if (p >= S.t && p < S.t + S.lim) c.bits = (uint64_t)(uintptr_t)(S.g + (p - S.t));
+                }
+                if (S.at(j) == D.delim) { j = j + 1; col++; }
+                else ended = true;
+            }
+        }
+        o[k] = c;
+    }
 }
 
 // value class of a key under value_compare: 0 NULL, 1 number, 2 string, 3 date.
@@ -1413,6 +1465,17 @@ __device__ __forceinline__ uint64_t hj_hash(unsigned long long code, uint32_t cl
     return mix64(code ^ ((uint64_t)cls << 62) ^ 0x243F6A8885A308D3ULL);
 }
 
+// value classes present in one column of a cell table (bit k: class k of
+// key_class), OR-reduced per wave: what a repartitioned join's rank reports
+__global__ void class_mask_kernel(const Cell* __restrict__ cells, uint32_t stride, uint32_t kcol, uint32_t n,
+                                  unsigned int* __restrict__ mask) {
+    uint32_t m = 0;
+    for (uint32_t i = blockIdx.x * blockDim.x + threadIdx.x; i < n; i += gridDim.x * blockDim.x)
+        m |= 1u << key_class(cells[(uint64_t)i * stride + kcol]);
+    for (int o = 32; o > 0; o >>= 1) m |= (uint32_t)__shfl_xor((int)m, o, 64);
+    if ((threadIdx.x & 63) == 0 && m) atomicOr(mask, m);
+}
+
 // slot of every right row's key (inserted when new); row counts per slot.  The
 // probe loop is wave-uniform (it runs while any lane of the wave still looks for
 // its slot, one probe per lane per trip): a lane that finds a slot claimed but
@@ -1429,13 +1492,17 @@ __global__ void hash_build_kernel(const unsigned long long* __restrict__ codes, 
     uint32_t i = (uint32_t)hj_hash(code, k) & mask, slot = 0, probes = 0;
     for (uint32_t trip = 0; __any(pending); trip++) {
         if (pending) {
-            uint32_t st = __hip_atomic_load(&H.state[i], __ATOMIC_ACQUIRE, __HIP_MEMORY_SCOPE_AGENT);
+            // relaxed agent-scope atomics (coherent at L2, no cache maintenance); the
+            // publisher drains its key stores (vmcnt) before the state store, and a
+            // reader loads the key only after it has seen the published state
+            uint32_t st = __hip_atomic_load(&H.state[i], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
             if (st == 0) {
                 const uint32_t old = atomicCAS(&H.state[i], 0u, 1u);
                 if (old == 0) {                          // claimed: key words first, then publish
                     __hip_atomic_store(&H.code[i], code, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
                     __hip_atomic_store(&H.cls[i], k, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-                    __hip_atomic_store(&H.state[i], 2u, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_AGENT);
+                    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+                    __hip_atomic_store(&H.state[i], 2u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
                     slot = i;
                     pending = false;
                 }
@@ -2092,10 +2159,12 @@ hipError_t cq_launch_finish(const uint8_t* g, uint64_t n, const cq::GroupOut* ou
 // ---- INNER JOIN kernels (executor.hip run_join)
 static unsigned grid_of(uint64_t n, unsigned b) { return (unsigned)std::max<uint64_t>(1, (n + b - 1) / b); }
 
-hipError_t cq_launch_cells(const uint8_t* g, const unsigned long long* recs, uint32_t n, const cq::ColsDesc* D,
-                           cq::Cell* out, hipStream_t s) {
+hipError_t cq_launch_cells(const uint8_t* g, uint64_t tn, const unsigned long long* recs, uint32_t n,
+                           const cq::ColsDesc* D, cq::Cell* out, hipStream_t s) {
     if (!n) return hipSuccess;
-    hipLaunchKernelGGL(cq::cells_kernel, dim3(grid_of(n, 128)), dim3(128), 0, s, g, recs, n, *D, out);
+    if (((uintptr_t)g & 15) != 0) return hipErrorInvalidValue;     // 16-byte staged loads
+    hipLaunchKernelGGL(cq::cells_kernel, dim3((n + cq::CELLS_T - 1) / cq::CELLS_T), dim3(cq::CELLS_T), 0, s, g, tn,
+                       recs, n, *D, out);
     return hipGetLastError();
 }
 hipError_t cq_launch_join_code(const cq::Cell* cells, uint32_t stride, uint32_t kcol, uint32_t n,
@@ -2131,6 +2200,13 @@ hipError_t cq_launch_join_gather(const uint2* pairs, unsigned long long np, cons
                                  const cq::Cell* R, cq::Cell* out, hipStream_t s) {
     const unsigned long long blocks = (np + 255) / 256;
     hipLaunchKernelGGL(cq::join_gather_kernel, dim3((uint32_t)blocks), dim3(256), 0, s, pairs, np, *M, L, R, out);
+    return hipGetLastError();
+}
+hipError_t cq_launch_class_mask(const cq::Cell* cells, uint32_t stride, uint32_t kcol, uint32_t n, unsigned int* mask,
+                                hipStream_t s) {
+    if (!n) return hipSuccess;
+    const uint32_t grid = std::min<uint32_t>((n + 255) / 256, 4096);
+    hipLaunchKernelGGL(cq::class_mask_kernel, dim3(grid), dim3(256), 0, s, cells, stride, kcol, n, mask);
     return hipGetLastError();
 }
 hipError_t cq_launch_hash_build(const unsigned long long* codes, const uint32_t* cls, uint32_t n, const cq::JoinHashW* H,
