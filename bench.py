@@ -195,7 +195,7 @@ def main():
 
     import cq_amd
     from cq_amd import abi
-    from cq_amd.dist import scan_partitioned
+    from cq_amd.dist import scan_partitioned_dense
     L = cq_amd.lib()
 
     t0 = time.time()
@@ -225,7 +225,9 @@ def main():
                 print("stats", st, file=sys.stderr)
             kernel_used[0] = st.get("scan_kernel", 0)
             return tp, st["scan_ms"]
-        tp = scan_partitioned(ast, table)      # partial, RCCL gather, merge on rank 0
+        # partial groups stay in HBM; key all_gather + dense MIN/SUM reduces over RCCL,
+        # rank 0 finishes (scan_partitioned's blob gather only for plans off the dense path)
+        tp = scan_partitioned_dense(ast, table)
         return tp, cq_amd.stats()["scan_ms"]   # the merge runs no scan: still this rank's partial
 
     for _ in range(args.warmup):

@@ -69,6 +69,20 @@ def lib():
         L.cqgpu_table_from_routed.restype = C.c_void_p
         L.cqgpu_table_from_routed.argtypes = [C.c_void_p, C.c_size_t, C.c_void_p, C.c_size_t, abi.CsvConfig,
                                               C.c_char_p, C.c_size_t]
+        vp = C.c_void_p
+        L.cqgpu_partial_new.restype = vp
+        L.cqgpu_partial_new.argtypes = [C.POINTER(abi.Node), C.POINTER(vp), C.c_int]
+        L.cqgpu_partial_keys.restype = C.c_size_t
+        L.cqgpu_partial_keys.argtypes = [vp, vp, C.POINTER(C.c_uint32)]
+        L.cqgpu_partial_dict.restype = C.c_longlong
+        L.cqgpu_partial_dict.argtypes = [vp, vp, C.c_uint64, C.c_uint64]
+        L.cqgpu_partial_scatter.restype = C.c_int
+        L.cqgpu_partial_scatter.argtypes = [vp, vp, vp, vp]
+        L.cqgpu_partial_mask_reps.restype = C.c_int
+        L.cqgpu_partial_mask_reps.argtypes = [vp, vp, vp]
+        L.cqgpu_partial_finish.restype = TP
+        L.cqgpu_partial_finish.argtypes = [vp, C.POINTER(abi.Node), vp, vp, vp]
+        L.cqgpu_partial_free.argtypes = [vp]
         L.cqgpu_last_stats.argtypes = [C.POINTER(Stats)]
         L.cqgpu_last_error.restype = C.c_char_p
         L.cqgpu_last_ineligible.restype = C.c_char_p

@@ -59,6 +59,16 @@ hipError_t cq_launch_join_code(const cq::Cell* cells, uint32_t stride, uint32_t 
                                hipStream_t s);
 hipError_t cq_launch_gather_codes(const unsigned long long* codes, const uint32_t* idx, uint32_t n,
                                   unsigned long long* out, hipStream_t s);
+hipError_t cq_launch_dict_build(const void* all, uint32_t n, uint32_t* state, uint32_t* rec_of, uint32_t* first_of,
+                                uint32_t cap, uint32_t* slot_of, unsigned int* err, hipStream_t s);
+hipError_t cq_launch_dict_flag(const uint32_t* slot_of, const uint32_t* first_of, uint32_t n, uint32_t* flag,
+                               hipStream_t s);
+hipError_t cq_launch_dict_scatter(const uint32_t* slot_of, const uint32_t* first_of, const uint32_t* dense_of,
+                                  uint32_t mine, uint32_t m, const double* st_sum, const unsigned long long* st_first,
+                                  const unsigned long long* st_rep, uint32_t W, double* dsum,
+                                  unsigned long long* dfirst, unsigned long long* drep, hipStream_t s);
+hipError_t cq_launch_rep_mask(const unsigned long long* mine, const unsigned long long* global, uint32_t g,
+                              unsigned long long* drep, hipStream_t s);
 hipError_t cq_launch_class_mask(const cq::Cell* cells, uint32_t stride, uint32_t kcol, uint32_t n, unsigned int* mask,
                                 hipStream_t s);
 hipError_t cq_launch_hash_build(const unsigned long long* codes, const uint32_t* cls, uint32_t n, const cq::JoinHashW* H,
@@ -271,19 +281,28 @@ struct Scratch {
 // owned device allocation
 // Device scratch blocks are recycled instead of hipFree'd: hipFree synchronises
 // the device and cost ~140 us per call (74 calls per repartitioned-join step,
-// ~10 ms).  Every kernel and copy of the library runs on the one DevCtx stream, so
-// a block released here and handed out again is only touched by work enqueued
-// after everything that used it before.  Released blocks are kept up to
-// DEVPOOL_KEEP bytes; a failed hipMalloc empties the pool and retries.
+// ~10 ms).  Every kernel and copy of the library runs on its device's one DevCtx
+// stream, so a block released here and handed out again ON THE SAME DEVICE is only
+// touched by work enqueued after everything that used it before: the idle lists
+// are per device, and a block goes back to the list of the device it was
+// allocated on.  Released blocks are kept up to DEVPOOL_KEEP bytes per device; a
+// failed hipMalloc empties that device's list and retries.
 constexpr size_t DEVPOOL_KEEP = 8ull << 30;
+constexpr int DEVPOOL_MAXDEV = 64;
 struct DevPool {
-    std::multimap<size_t, void*> idle;
-    std::unordered_map<void*, size_t> live;
-    size_t idle_bytes = 0;
+    std::multimap<size_t, void*> idle[DEVPOOL_MAXDEV];
+    size_t idle_bytes[DEVPOOL_MAXDEV] = {};
+    std::unordered_map<void*, std::pair<size_t, int>> live;     // block -> (size class, device)
 };
 DevPool& devpool() {
     static DevPool* P = new DevPool;      // never destroyed: blocks outlive static teardown
     return *P;
+}
+int devpool_device() {
+    int d = 0;
+    HIPCHECK(hipGetDevice(&d));
+    if (d < 0 || d >= DEVPOOL_MAXDEV) throw HipError{"device index beyond the scratch pool"};
+    return d;
 }
 size_t devpool_class(size_t n) {          // 4 size classes per power of two
     n = std::max<size_t>(n, 256);
@@ -292,41 +311,44 @@ size_t devpool_class(size_t n) {          // 4 size classes per power of two
     const size_t step = (size_t)1 << (k - 2);
     return (n + step - 1) & ~(step - 1);
 }
-void devpool_trim(size_t keep) {
+void devpool_trim(int dev, size_t keep) {   // frees blocks of `dev` (the current device)
     DevPool& P = devpool();
-    while (P.idle_bytes > keep && !P.idle.empty()) {
-        auto it = std::prev(P.idle.end());   // largest first
-        P.idle_bytes -= it->first;
+    while (P.idle_bytes[dev] > keep && !P.idle[dev].empty()) {
+        auto it = std::prev(P.idle[dev].end());   // largest first
+        P.idle_bytes[dev] -= it->first;
         (void)hipFree(it->second);
-        P.idle.erase(it);
+        P.idle[dev].erase(it);
     }
 }
 void* devpool_get(size_t bytes) {
     DevPool& P = devpool();
+    const int dev = devpool_device();
     const size_t sz = devpool_class(bytes);
-    auto it = P.idle.find(sz);
+    auto it = P.idle[dev].find(sz);
     void* p = nullptr;
-    if (it != P.idle.end()) {
+    if (it != P.idle[dev].end()) {
         p = it->second;
-        P.idle.erase(it);
-        P.idle_bytes -= sz;
+        P.idle[dev].erase(it);
+        P.idle_bytes[dev] -= sz;
     } else if (hipMalloc(&p, sz) != hipSuccess) {
         (void)hipGetLastError();
-        devpool_trim(0);
+        devpool_trim(dev, 0);
         HIPCHECK(hipMalloc(&p, sz));
     }
-    P.live[p] = sz;
+    P.live[p] = {sz, dev};
     return p;
 }
 void devpool_put(void* p) {
     DevPool& P = devpool();
     auto it = P.live.find(p);
     if (it == P.live.end()) { (void)hipFree(p); return; }
-    const size_t sz = it->second;
+    const size_t sz = it->second.first;
+    const int dev = it->second.second;
     P.live.erase(it);
-    P.idle.emplace(sz, p);
-    P.idle_bytes += sz;
-    devpool_trim(DEVPOOL_KEEP);
+    P.idle[dev].emplace(sz, p);
+    P.idle_bytes[dev] += sz;
+    int cur = -1;
+    if (hipGetDevice(&cur) == hipSuccess && cur == dev) devpool_trim(dev, DEVPOOL_KEEP);
 }
 
 struct DevBuf {
@@ -3677,5 +3699,265 @@ cq_table* cqgpu_merge_partials(cq_node* q, const void* const* blobs, const size_
         return nullptr;
     }
 }
+
+
+// ---- device-side GROUP BY merge for range-partitioned scans (merge.hip) -------
+// Dense path of SURVEY.md section 8e: plans whose result needs only the group key,
+// COUNT / SUM / AVG (no MIN / MAX, no other plain column, no long text keys).
+struct cqgpu_partial {
+    Compiled C;
+    std::vector<std::string> names;
+    uint32_t W = 1;                 // dense words per group: COUNT, then SUM_a and count_a per accumulator
+    uint32_t m = 0;                 // this rank's groups
+    int rep_slot = -1;              // the group column's rep slot (-1: no plain column)
+    DevBuf keys, st_sum, st_first, st_rep;
+    // the dictionary of the last cqgpu_partial_dict call
+    const void* all = nullptr;
+    uint32_t nall = 0, mine = 0, G = 0, cap = 0;
+    DevBuf state, rec_of, first_of, slot_of, flag, dense_of, my_first;
+};
+
+namespace {
+constexpr uint32_t KEYREC = 32;
+struct HKeyRec { uint32_t clslen, pad; uint64_t w0, w1, pad2; };
+}  // namespace
+
+cqgpu_partial* cqgpu_partial_new(cq_node* q, cqgpu_table* const* tables, int ntables) {
+    g_inel.clear();
+    g_err.clear();
+    std::unique_ptr<cqgpu_partial> p(new cqgpu_partial);
+    try {
+        DevCtx& c = ctx();
+        bump_reset(c);
+        if (ntables < 1 || !tables[0]) throw HipError{"no table"};
+        const cqgpu_table* t = tables[0];
+        check_plan_shape(q, t);
+        if (is_row_query(q)) throw Ineligible{"row-returning SELECT across partials"};
+        Compiled& C = p->C;
+        compile_aggregate(t, q, C);
+        if (!C.vla.empty() || C.P.ngpart > 0) throw Ineligible{"dense merge: STDDEV/MEDIAN or composite GROUP BY"};
+        for (int a = 0; a < C.P.nacc; a++)
+            if (C.P.acc[a].kind != ACC_SUM) throw Ineligible{"dense merge: MIN/MAX"};
+        for (const OutCol& o : C.outs)
+            if (o.kind == OUT_HEXPR) throw Ineligible{"dense merge: expression items"};
+        if (C.rep_cols.size() > 1 || (C.rep_cols.size() == 1 && C.rep_cols[0] != C.group_col))
+            throw Ineligible{"dense merge: plain columns besides the group key"};
+        p->rep_slot = C.rep_cols.empty() ? -1 : 0;
+        p->names = t->names;
+        p->W = 1 + 2 * (uint32_t)C.P.nacc;
+        Literals L;
+        ScanStats st;
+        memset(&st, 0, sizeof st);
+        std::vector<HGroup> groups = run_aggregate(c, t, C, L, &st);
+        const uint32_t m = (uint32_t)groups.size();
+        std::vector<HKeyRec> k(m);
+        std::vector<double> sm((size_t)m * p->W);
+        std::vector<unsigned long long> fi(m), rp(2 * (size_t)m);
+        for (uint32_t j = 0; j < m; j++) {
+            const HGroup& h = groups[j];
+            if (h.kcls == GK_LONG) throw Ineligible{"dense merge: group key text over 16 bytes"};
+            // identity as cqgpu_merge_partials': class + text for text keys, class +
+            // first word for numbers (the second word and length carry nothing there)
+            const bool text = h.kcls == GK_STR || h.kcls == GK_COMP;
+            k[j] = HKeyRec{(h.kcls << 16) | (text ? h.klen : 0u), 0, h.kw0, text ? h.kw1 : 0ull, 0};
+            sm[(size_t)j * p->W] = (double)h.cnt;
+            for (int a = 0; a < C.P.nacc; a++) {
+                sm[(size_t)j * p->W + 1 + 2 * a] = h.sum[a];
+                sm[(size_t)j * p->W + 2 + 2 * a] = (double)h.num[a];
+            }
+            fi[j] = h.first;
+            if (p->rep_slot >= 0 && !h.reps.empty()) {
+                rp[2 * j] = h.reps[0].kind;
+                rp[2 * j + 1] = h.reps[0].kind == K_STR ? 0 : h.reps[0].bits;   // text: the key's bytes
+            }
+        }
+        p->m = m;
+        DevBuf a(std::max<size_t>((size_t)m * KEYREC, 64)), b(std::max<size_t>(sm.size() * 8, 64)),
+            f(std::max<size_t>((size_t)m * 8, 64)), r(std::max<size_t>(rp.size() * 8, 64));
+        std::swap(p->keys.p, a.p); std::swap(p->st_sum.p, b.p); std::swap(p->st_first.p, f.p); std::swap(p->st_rep.p, r.p);
+        if (m) {
+            HIPCHECK(hipMemcpyAsync(p->keys.p, k.data(), (size_t)m * KEYREC, hipMemcpyHostToDevice, c.stream));
+            HIPCHECK(hipMemcpyAsync(p->st_sum.p, sm.data(), sm.size() * 8, hipMemcpyHostToDevice, c.stream));
+            HIPCHECK(hipMemcpyAsync(p->st_first.p, fi.data(), fi.size() * 8, hipMemcpyHostToDevice, c.stream));
+            HIPCHECK(hipMemcpyAsync(p->st_rep.p, rp.data(), rp.size() * 8, hipMemcpyHostToDevice, c.stream));
+        }
+        HIPCHECK(hipStreamSynchronize(c.stream));
+        return p.release();
+    } catch (Ineligible& e) {
+        g_inel = e.why;
+        set_err("cq_amd: query outside the dense merge: %s", e.why.c_str());
+        return nullptr;
+    } catch (HipError& e) {
+        set_err("cq_amd: %s", e.msg.c_str());
+        return nullptr;
+    }
+}
+
+size_t cqgpu_partial_keys(cqgpu_partial* p, void* dev_dst, uint32_t* words_per_group) {
+    if (words_per_group) *words_per_group = p ? p->W : 0;
+    if (!p) return 0;
+    if (dev_dst && p->m) {
+        DevCtx& c = ctx();
+        if (hipMemcpyAsync(dev_dst, p->keys.p, (size_t)p->m * KEYREC, hipMemcpyDeviceToDevice, c.stream) != hipSuccess ||
+            hipStreamSynchronize(c.stream) != hipSuccess) {
+            set_err("cq_amd: partial_keys: copy failed");
+            return 0;
+        }
+    }
+    return p->m;
+}
+
+long long cqgpu_partial_dict(cqgpu_partial* p, const void* dev_all, uint64_t nall, uint64_t mine) {
+    g_err.clear();
+    try {
+        if (!p || (!dev_all && nall) || mine + p->m > nall || nall >= (1ull << 31)) throw HipError{"partial_dict: bad arguments"};
+        DevCtx& c = ctx();
+        const uint32_t n = (uint32_t)nall;
+        uint32_t cap = 64;
+        while (cap < 2 * n) cap <<= 1;
+        p->all = dev_all; p->nall = n; p->mine = (uint32_t)mine; p->cap = cap;
+        DevBuf st((size_t)cap * 4), ro((size_t)cap * 4), fo((size_t)cap * 4), so(std::max<size_t>((size_t)n * 4, 4)),
+            fl(std::max<size_t>((size_t)n * 4, 4)), de(std::max<size_t>((size_t)n * 4, 4)), err(64);
+        HIPCHECK(hipMemsetAsync(st.p, 0, (size_t)cap * 4, c.stream));
+        HIPCHECK(hipMemsetAsync(fo.p, 0xFF, (size_t)cap * 4, c.stream));
+        HIPCHECK(hipMemsetAsync(err.p, 0, 4, c.stream));
+        HIPCHECK(cq_launch_dict_build(dev_all, n, st.as<uint32_t>(), ro.as<uint32_t>(), fo.as<uint32_t>(), cap,
+                                      so.as<uint32_t>(), err.as<unsigned int>(), c.stream));
+        HIPCHECK(cq_launch_dict_flag(so.as<uint32_t>(), fo.as<uint32_t>(), n, fl.as<uint32_t>(), c.stream));
+        size_t tb = 0;
+        HIPCHECK(cq_excl_sum_u32(nullptr, &tb, fl.as<unsigned int>(), de.as<unsigned int>(), n, c.stream));
+        DevBuf temp(tb);
+        HIPCHECK(cq_excl_sum_u32(temp.p, &tb, fl.as<unsigned int>(), de.as<unsigned int>(), n, c.stream));
+        unsigned int e = 0, last[2] = {0, 0};
+        HIPCHECK(hipMemcpyAsync(&e, err.p, 4, hipMemcpyDeviceToHost, c.stream));
+        if (n) {
+            HIPCHECK(hipMemcpyAsync(&last[0], de.as<uint32_t>() + n - 1, 4, hipMemcpyDeviceToHost, c.stream));
+            HIPCHECK(hipMemcpyAsync(&last[1], fl.as<uint32_t>() + n - 1, 4, hipMemcpyDeviceToHost, c.stream));
+        }
+        HIPCHECK(hipStreamSynchronize(c.stream));
+        if (e) throw HipError{"partial_dict: key table full or insert timeout"};
+        std::swap(p->state.p, st.p); std::swap(p->rec_of.p, ro.p); std::swap(p->first_of.p, fo.p);
+        std::swap(p->slot_of.p, so.p); std::swap(p->flag.p, fl.p); std::swap(p->dense_of.p, de.p);
+        p->G = last[0] + last[1];
+        return p->G;
+    } catch (HipError& e) {
+        set_err("cq_amd: %s", e.msg.c_str());
+        return -1;
+    }
+}
+
+int cqgpu_partial_scatter(cqgpu_partial* p, double* dsum, unsigned long long* dfirst, unsigned long long* drep) {
+    g_err.clear();
+    try {
+        if (!p) throw HipError{"partial_scatter: no partial"};
+        DevCtx& c = ctx();
+        const size_t G = p->G;
+        if (G) {
+            HIPCHECK(hipMemsetAsync(dsum, 0, G * p->W * 8, c.stream));
+            HIPCHECK(hipMemsetAsync(dfirst, 0x7F, G * 8, c.stream));   // "absent": above every position,
+                                                                        // also as a signed int64 (MIN reduce)
+            HIPCHECK(hipMemsetAsync(drep, 0, G * 16, c.stream));
+        }
+        HIPCHECK(cq_launch_dict_scatter(p->slot_of.as<uint32_t>(), p->first_of.as<uint32_t>(), p->dense_of.as<uint32_t>(),
+                                        p->mine, p->m, p->st_sum.as<double>(), p->st_first.as<unsigned long long>(),
+                                        p->st_rep.as<unsigned long long>(), p->W, dsum, dfirst, drep, c.stream));
+        DevBuf mf(std::max<size_t>(G * 8, 8));
+        if (G) HIPCHECK(hipMemcpyAsync(mf.p, dfirst, G * 8, hipMemcpyDeviceToDevice, c.stream));
+        std::swap(p->my_first.p, mf.p);
+        HIPCHECK(hipStreamSynchronize(c.stream));
+        return 0;
+    } catch (HipError& e) {
+        set_err("cq_amd: %s", e.msg.c_str());
+        return -1;
+    }
+}
+
+int cqgpu_partial_mask_reps(cqgpu_partial* p, const unsigned long long* dfirst_global, unsigned long long* drep) {
+    g_err.clear();
+    try {
+        if (!p) throw HipError{"partial_mask_reps: no partial"};
+        DevCtx& c = ctx();
+        HIPCHECK(cq_launch_rep_mask(p->my_first.as<unsigned long long>(), dfirst_global, p->G, drep, c.stream));
+        HIPCHECK(hipStreamSynchronize(c.stream));
+        return 0;
+    } catch (HipError& e) {
+        set_err("cq_amd: %s", e.msg.c_str());
+        return -1;
+    }
+}
+
+cq_table* cqgpu_partial_finish(cqgpu_partial* p, cq_node* q, const double* dsum, const unsigned long long* dfirst,
+                               const unsigned long long* drep) {
+    g_inel.clear();
+    g_err.clear();
+    try {
+        if (!p) throw HipError{"partial_finish: no partial"};
+        DevCtx& c = ctx();
+        const uint32_t G = p->G, n = p->nall, W = p->W;
+        std::vector<HKeyRec> all(n);
+        std::vector<uint32_t> flag(n);
+        std::vector<double> sm((size_t)G * W);
+        std::vector<unsigned long long> fi(G), rp(2 * (size_t)G);
+        if (n) {
+            HIPCHECK(hipMemcpyAsync(all.data(), p->all, (size_t)n * KEYREC, hipMemcpyDeviceToHost, c.stream));
+            HIPCHECK(hipMemcpyAsync(flag.data(), p->flag.p, (size_t)n * 4, hipMemcpyDeviceToHost, c.stream));
+        }
+        if (G) {
+            HIPCHECK(hipMemcpyAsync(sm.data(), dsum, sm.size() * 8, hipMemcpyDeviceToHost, c.stream));
+            HIPCHECK(hipMemcpyAsync(fi.data(), dfirst, fi.size() * 8, hipMemcpyDeviceToHost, c.stream));
+            HIPCHECK(hipMemcpyAsync(rp.data(), drep, rp.size() * 8, hipMemcpyDeviceToHost, c.stream));
+        }
+        HIPCHECK(hipStreamSynchronize(c.stream));
+        const Compiled& C = p->C;
+        std::vector<HGroup> groups;
+        uint32_t d = 0;
+        for (uint32_t r = 0; r < n && d < G; r++) {
+            if (!flag[r]) continue;
+            const HKeyRec& k = all[r];
+            HGroup h;
+            h.kcls = k.clslen >> 16;
+            h.klen = k.clslen & 0xffff;
+            h.kw0 = k.w0;
+            h.kw1 = k.w1;
+            if (h.kcls == GK_STR)
+                for (uint32_t i = 0; i < h.klen; i++)
+                    h.kbytes.push_back((char)((i < 8 ? k.w0 >> (8 * i) : k.w1 >> (8 * (i - 8))) & 0xff));
+            h.cnt = (unsigned long long)sm[(size_t)d * W];
+            for (int a = 0; a < C.P.nacc; a++) {
+                h.sum[a] = sm[(size_t)d * W + 1 + 2 * a];
+                h.num[a] = (unsigned long long)sm[(size_t)d * W + 2 + 2 * a];
+            }
+            h.first = fi[d] >= 0x7F7F7F7F7F7F7F7Full ? NOPOS : fi[d];
+            if (p->rep_slot >= 0) {
+                HCell rc;
+                rc.kind = (uint32_t)rp[2 * (size_t)d];
+                rc.bits = rp[2 * (size_t)d + 1];
+                if (rc.kind == K_STR) rc.s = h.kbytes;
+                h.reps.push_back(rc);
+            }
+            groups.push_back(std::move(h));
+            d++;
+        }
+        if (!C.grouped && groups.size() > 1) throw HipError{"partials disagree on the single group"};
+        std::stable_sort(groups.begin(), groups.end(), [](const HGroup& x, const HGroup& y) { return x.first < y.first; });
+        Compiled C2 = C;
+        Literals L;
+        parse_literals(c, C2.lits, L);
+        g_stats.groups = groups.size();
+        cq_table* res = build_groups(C2, groups, L, c);
+        post_ops(c, res, q);
+        g_stats.path = 1;
+        return res;
+    } catch (Ineligible& e) {
+        g_inel = e.why;
+        set_err("cq_amd: query outside the GPU executor's subset: %s", e.why.c_str());
+        return nullptr;
+    } catch (HipError& e) {
+        set_err("cq_amd: %s", e.msg.c_str());
+        return nullptr;
+    }
+}
+
+void cqgpu_partial_free(cqgpu_partial* p) { delete p; }
 
 }  // extern "C"

@@ -81,6 +81,124 @@ def scan_partitioned(ast, table, comm_device: torch.device | str | None = None):
     return tp
 
 
+class DensePartial:
+    """This rank's device-resident partial groups (cqgpu_partial_*): the library
+    side of scan_partitioned_dense, kept behind four calls so the collective
+    choreography can be exercised on CPU with a stand-in (tests/test_dist_gloo.py)."""
+
+    KEYREC = 32
+
+    def __init__(self, ast, table):
+        import ctypes as C
+        import cq_amd
+        self.C, self.L, self.ast = C, cq_amd.lib(), ast
+        arr = (C.c_void_p * 1)(table.handle.value)
+        self.p = self.L.cqgpu_partial_new(ast, arr, 1)
+        w = C.c_uint32(0)
+        self.m = self.L.cqgpu_partial_keys(self.p, None, C.byref(w)) if self.p else 0
+        self.W = w.value
+
+    @property
+    def ok(self) -> bool:
+        return bool(self.p)
+
+    def keys(self, device) -> torch.Tensor:
+        t = torch.empty(max(self.m * self.KEYREC, 1), dtype=torch.uint8, device=device)
+        if self.m:
+            self.L.cqgpu_partial_keys(self.p, t.data_ptr(), None)
+        return t[: self.m * self.KEYREC]
+
+    def dict(self, all_keys: torch.Tensor, nall: int, mine: int) -> int:
+        g = self.L.cqgpu_partial_dict(self.p, all_keys.data_ptr() if nall else None, nall, mine)
+        if g < 0:
+            import cq_amd
+            raise RuntimeError(cq_amd.last_error())
+        return int(g)
+
+    def scatter(self, dsum, dfirst, drep):
+        if self.L.cqgpu_partial_scatter(self.p, dsum.data_ptr(), dfirst.data_ptr(), drep.data_ptr()) != 0:
+            import cq_amd
+            raise RuntimeError(cq_amd.last_error())
+
+    def mask_reps(self, dfirst, drep):
+        if self.L.cqgpu_partial_mask_reps(self.p, dfirst.data_ptr(), drep.data_ptr()) != 0:
+            import cq_amd
+            raise RuntimeError(cq_amd.last_error())
+
+    def finish(self, dsum, dfirst, drep):
+        return self.L.cqgpu_partial_finish(self.p, self.ast, dsum.data_ptr(), dfirst.data_ptr(), drep.data_ptr())
+
+    def free(self):
+        if self.p:
+            self.L.cqgpu_partial_free(self.p)
+            self.p = None
+
+
+def dense_merge(part, device, comm_device=None):
+    """The collective part of the device-side merge: one
+    all_gather of the key records (sizes first), the dictionary and dense arrays
+    on every rank, MIN all-reduce of first positions, SUM reduce of the dense sums
+    and representative cells to rank 0, where `part.finish` builds the result.
+    Returns that on rank 0, None elsewhere.  comm_device: where the collectives run
+    (the device for RCCL; "cpu" stages through host memory for a gloo group)."""
+    world, rank = dist.get_world_size(), dist.get_rank()
+    comm = torch.device(comm_device) if comm_device is not None else torch.device(device)
+    mine = part.keys(device)
+    n = torch.tensor([part.m], dtype=torch.int64, device=comm)
+    sizes = [torch.zeros(1, dtype=torch.int64, device=comm) for _ in range(world)]
+    dist.all_gather(sizes, n)
+    counts = [int(x.item()) for x in sizes]                  # a few integers, not the blobs
+    kb = part.KEYREC
+    mx = max(max(counts), 1) * kb
+    buf = torch.zeros(mx, dtype=torch.uint8, device=comm)
+    buf[: mine.numel()] = mine.to(comm)
+    outs = [torch.empty(mx, dtype=torch.uint8, device=comm) for _ in range(world)]
+    dist.all_gather(outs, buf)
+    all_keys = torch.cat([o[: c * kb] for o, c in zip(outs, counts)]).to(device)
+    nall, off = sum(counts), sum(counts[:rank])
+    g = part.dict(all_keys, nall, off)
+    dsum = torch.empty(max(g * part.W, 1), dtype=torch.float64, device=device)
+    dfirst = torch.empty(max(g, 1), dtype=torch.int64, device=device)
+    drep = torch.empty(max(2 * g, 1), dtype=torch.int64, device=device)
+    part.scatter(dsum, dfirst, drep)
+    f = dfirst.to(comm)
+    dist.all_reduce(f, op=dist.ReduceOp.MIN)
+    dfirst.copy_(f)
+    part.mask_reps(dfirst, drep)
+    s, r = dsum.to(comm), drep.to(comm)
+    dist.reduce(s, 0, op=dist.ReduceOp.SUM)
+    dist.reduce(r, 0, op=dist.ReduceOp.SUM)
+    if rank != 0:
+        return None
+    dsum.copy_(s)
+    drep.copy_(r)
+    return part.finish(dsum, dfirst, drep)
+
+
+def scan_partitioned_dense(ast, table, comm_device=None):
+    """One range-partitioned query step with the merge on the devices (config 4):
+    this rank's scan keeps its groups in HBM (cqgpu_partial_new), the ranks agree
+    on the path (a MIN all-reduce of "eligible"), and dense_merge reduces the
+    groups over RCCL.  Plans outside the dense path (MIN/MAX, plain columns other
+    than the group key, long text keys) take scan_partitioned's blobs."""
+    import cq_amd
+    device = torch.device("cuda", torch.cuda.current_device())
+    comm = torch.device(comm_device) if comm_device is not None else device
+    part = DensePartial(ast, table)
+    try:
+        ok = torch.tensor([1 if part.ok else 0], dtype=torch.int32, device=comm)
+        dist.all_reduce(ok, op=dist.ReduceOp.MIN)
+        if int(ok.item()) == 0:
+            part.free()
+            return scan_partitioned(ast, table, comm_device)
+        tp = dense_merge(part, device, comm_device)
+        if dist.get_rank() == 0 and not tp:
+            raise RuntimeError(cq_amd.last_error() or "cqgpu_partial_finish failed")
+        return tp
+    finally:
+        part.free()
+
+
 def join_partitioned(ast, lshard, rshard, lheader: bytes, rheader: bytes, device: torch.device | str,
                      comm_device: torch.device | str | None = None):
     """Repartitioned INNER JOIN over this rank's shards of both inputs.

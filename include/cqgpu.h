@@ -97,6 +97,30 @@ size_t cqgpu_query_partial(cq_node* query_ast, cqgpu_table* const* tables, int n
 cq_table* cqgpu_merge_partials(cq_node* query_ast, const void* const* blobs, const size_t* sizes,
                                int nblobs);
 
+/* ---- device-side merge of range-partitioned GROUP BY partials --------------
+ *  for plans whose result is the group key with
+ * COUNT / SUM / AVG (the config-3/4 shape; others use the blobs above):
+ *   p = cqgpu_partial_new(q, tables, 1)           this rank's scan, groups kept on the device
+ *   n = cqgpu_partial_keys(p, dst, &W)            n key records of 32 bytes, copied to dst (device; NULL: count only)
+ *   all_gather the key records (RCCL), concatenated in rank order -> all, nall, mine = offset of ours
+ *   G = cqgpu_partial_dict(p, all, nall, mine)    the global dictionary, identical on every rank
+ *   cqgpu_partial_scatter(p, dsum, dfirst, drep)  dense arrays: double[G*W], int64[G] (absent:
+ *                                                 0x7F7F...7F), int64[2G]
+ *   all_reduce(dfirst, MIN); cqgpu_partial_mask_reps(p, dfirst, drep)
+ *   reduce(dsum, SUM) and reduce(drep, SUM) to rank 0
+ *   rank 0: r = cqgpu_partial_finish(p, q, dsum, dfirst, drep); every rank: cqgpu_partial_free(p)
+ * All buffers are device memory.  new returns NULL (cqgpu_last_ineligible set)
+ * for plans outside the dense path; dict returns -1 on error. */
+typedef struct cqgpu_partial cqgpu_partial;
+cqgpu_partial* cqgpu_partial_new(cq_node* query_ast, cqgpu_table* const* tables, int ntables);
+size_t cqgpu_partial_keys(cqgpu_partial* p, void* dev_dst, uint32_t* words_per_group);
+long long cqgpu_partial_dict(cqgpu_partial* p, const void* dev_all, uint64_t nall, uint64_t mine);
+int cqgpu_partial_scatter(cqgpu_partial* p, double* dsum, unsigned long long* dfirst, unsigned long long* drep);
+int cqgpu_partial_mask_reps(cqgpu_partial* p, const unsigned long long* dfirst_global, unsigned long long* drep);
+cq_table* cqgpu_partial_finish(cqgpu_partial* p, cq_node* query_ast, const double* dsum,
+                               const unsigned long long* dfirst, const unsigned long long* drep);
+void cqgpu_partial_free(cqgpu_partial* p);
+
 /* ---- join-key repartition for the multi-GPU JOIN ---
  * One INNER / LEFT / RIGHT / FULL JOIN with an `ident = ident` ON (reference
  * evaluator_joins.c:40-60, :63-181) over range-partitioned inputs: every rank routes each record of its

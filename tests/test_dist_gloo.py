@@ -101,3 +101,107 @@ def test_exchange_gloo(world):
         assert rids == wids, rank
         assert rc == [0 if (s == 0 and rank == 1) else rank + s + 1 for s in range(world)]
         assert base == sum(r + 5 for r in range(rank))
+
+
+# ---------------------------------------------------------------- dense merge choreography
+class _StandInPartial:
+    """numpy stand-in for cq_amd.dist.DensePartial with the library's contract
+    (merge.hip): 32-byte key records, the dictionary numbers distinct keys by first
+    occurrence in the all-gathered concatenation, W dense words per group, first
+    positions MIN-reduced, representative cells kept only where the first row is"""
+    KEYREC = 32
+    W = 3
+
+    def __init__(self, groups):
+        import numpy as np
+        self.np = np
+        self.groups = groups                      # [(key int, cnt, sum, first, rep)]
+        self.m = len(groups)
+
+    def keys(self, device):
+        import torch
+        rec = self.np.zeros((self.m, 4), dtype=self.np.uint64)
+        for j, g in enumerate(self.groups):
+            rec[j, 1] = g[0]
+        return torch.from_numpy(rec.view(self.np.uint8).reshape(-1).copy()).to(device)
+
+    def dict(self, all_keys, nall, mine):
+        keys = all_keys.cpu().numpy().view(self.np.uint64).reshape(nall, 4)[:, 1] if nall else []
+        self.dense = {}
+        for k in keys:
+            self.dense.setdefault(int(k), len(self.dense))
+        self.order = list(self.dense)
+        return len(self.dense)
+
+    def scatter(self, dsum, dfirst, drep):
+        dsum.zero_()
+        dfirst.fill_(0x7F7F7F7F7F7F7F7F)
+        drep.zero_()
+        for k, cnt, sm, first, rep in self.groups:
+            d = self.dense[k]
+            dsum[d * 3], dsum[d * 3 + 1], dsum[d * 3 + 2] = float(cnt), float(sm), float(cnt)
+            dfirst[d] = first
+            drep[2 * d], drep[2 * d + 1] = 1, rep
+        self.my_first = dfirst.clone()
+
+    def mask_reps(self, dfirst, drep):
+        for d in range(len(self.order)):
+            if int(self.my_first[d]) != int(dfirst[d]):
+                drep[2 * d] = drep[2 * d + 1] = 0
+
+    def finish(self, dsum, dfirst, drep):
+        rows = [(k, int(dsum[3 * d]), float(dsum[3 * d + 1]), int(dfirst[d]), int(drep[2 * d + 1]))
+                for d, k in enumerate(self.order)]
+        return sorted(rows, key=lambda r: r[3])
+
+    def free(self):
+        pass
+
+
+def _rank_groups(rank):
+    # keys 0..9 spread unevenly; rank r holds positions [1000r, 1000r + 1000)
+    import random
+    rng = random.Random(rank)
+    out = []
+    for k in rng.sample(range(10), 3 + 2 * rank):
+        out.append((k * 0x1000003 + 7, rng.randint(1, 50), rng.randint(-100, 100),
+                    1000 * rank + rng.randint(0, 999), 10_000 * rank + k))
+    return out
+
+
+def _dworker(rank, world, port, q):
+    import torch.distributed as dist
+    from cq_amd.dist import dense_merge
+    os.environ["MASTER_ADDR"] = "127.0.0.1"
+    os.environ["MASTER_PORT"] = str(port)
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    try:
+        q.put((rank, dense_merge(_StandInPartial(_rank_groups(rank)), "cpu", "cpu")))
+    finally:
+        dist.destroy_process_group()
+
+
+@pytest.mark.parametrize("world", [2, 3])
+def test_dense_merge_choreography_gloo(world):
+    """cq_amd.dist.dense_merge's collectives (sizes + key all_gather, MIN all_reduce
+    of first positions, SUM reduce of dense sums and masked reps) over gloo"""
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    port = _free_port()
+    procs = [ctx.Process(target=_dworker, args=(r, world, port, q)) for r in range(world)]
+    for p in procs:
+        p.start()
+    res = dict(q.get(timeout=120) for _ in range(world))
+    for p in procs:
+        p.join(timeout=60)
+        assert p.exitcode == 0
+    assert all(res[r] is None for r in range(1, world))
+    want = {}
+    for r in range(world):
+        for k, cnt, sm, first, rep in _rank_groups(r):
+            w = want.setdefault(k, [k, 0, 0.0, 1 << 62, 0])
+            w[1] += cnt
+            w[2] += sm
+            if first < w[3]:
+                w[3], w[4] = first, rep
+    assert res[0] == sorted((tuple(w) for w in want.values()), key=lambda r: r[3])

@@ -28,7 +28,7 @@ def _free_port():
     return p
 
 
-def _worker(rank, world, port, path, q):
+def _worker(rank, world, port, path, q, sql=SQL, dense=False):
     import sys
     sys.path.insert(0, os.path.dirname(os.path.abspath(__file__)))
     import torch
@@ -41,14 +41,15 @@ def _worker(rank, world, port, path, q):
         import cqtest as ct
         import cq_amd
         from cq_amd import abi
-        from cq_amd.dist import scan_partitioned
+        from cq_amd.dist import scan_partitioned, scan_partitioned_dense
+        fn = scan_partitioned_dense if dense else scan_partitioned
         t = cq_amd.Table.open_range(path, rank, world)
-        with ct.Parsed(SQL.format(p=path)) as ast:
+        with ct.Parsed(sql.format(p=path)) as ast:
             tp = None
             for _ in range(2):                 # a warm-up step, then the checked one
                 if tp:
                     cq_amd.result_free(tp)
-                tp = scan_partitioned(ast, t, "cpu")
+                tp = fn(ast, t, "cpu")
         t.close()
         if rank == 0:
             res = abi.table_to_py(tp)
@@ -62,14 +63,11 @@ def _worker(rank, world, port, path, q):
         dist.destroy_process_group()
 
 
-@pytest.mark.parametrize("world", [2])
-def test_bench_step_two_processes(tmp_path, world):
-    path = str(tmp_path / "big.csv")
-    datagen.write_logical(path, 400_000, seed=42, with_role=True)
+def _run(path, world, sql, dense):
     ctx = mp.get_context("spawn")
     q = ctx.Queue()
     port = _free_port()
-    procs = [ctx.Process(target=_worker, args=(r, world, port, path, q)) for r in range(world)]
+    procs = [ctx.Process(target=_worker, args=(r, world, port, path, q, sql, dense)) for r in range(world)]
     for p in procs:
         p.start()
     out = {}
@@ -80,9 +78,32 @@ def test_bench_step_two_processes(tmp_path, world):
     for p in procs:
         p.join(timeout=30)
         assert p.exitcode == 0
-    assert out[1] is True
+    assert all(out[r] is True for r in range(1, world))
+    return out[0]
+
+
+@pytest.mark.parametrize("dense", [False, True])
+def test_bench_step_two_processes(tmp_path, dense):
+    """bench.py's N > 1 step: blobs + host merge, and the device-side dense merge"""
+    path = str(tmp_path / "big.csv")
+    datagen.write_logical(path, 400_000, seed=42, with_role=True)
+    got = _run(path, 2, SQL, dense)
     want, unsup = cqtest.oracle_query(SQL.format(p=path))
     assert not unsup
     from test_gpu_parity import compare
-    compare(out[0], want, {2, 3}, "2-process config-3 step")
+    compare(got, want, {2, 3}, f"2-process config-3 step (dense={dense})")
     assert len(want["rows"]) == 1000
+
+
+def test_dense_step_falls_back_together(tmp_path):
+    """a key over 16 bytes on ONE rank only: every rank must leave the dense path
+    (the agreement all-reduce), or the ranks would wait in different collectives"""
+    rows = ["k,v"] + [f"k{i % 7},{i}" for i in range(3000)] + [f"a_key_longer_than_sixteen,{i}" for i in range(40)]
+    path = str(tmp_path / "mixed.csv")
+    with open(path, "w") as fh:
+        fh.write("\n".join(rows) + "\n")
+    sql = "SELECT k, COUNT(*), SUM(v) FROM '{p}' GROUP BY k"
+    got = _run(path, 3, sql, True)
+    want, _ = cqtest.oracle_query(sql.format(p=path))
+    from test_gpu_parity import compare
+    compare(got, want, {2}, "dense fallback")

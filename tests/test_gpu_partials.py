@@ -118,3 +118,95 @@ def test_more_ranks_than_records(tmp_path):
         got = _merged(ast, str(p), 9)
         tol = tolerant_columns(ast)
     compare(got, want, tol, q)
+
+
+# ---------------------------------------------------------------- device-side dense merge
+def _dense_merge_by_hand(ast, tabs):
+    """cqgpu_partial_* over simulated ranks in one process: the all_gather is a
+    concatenation, the reduces are torch reductions over the ranks' dense arrays"""
+    import torch
+    from cq_amd.dist import DensePartial
+    parts = [DensePartial(ast, t) for t in tabs]
+    try:
+        if not all(p.ok for p in parts):
+            return None
+        keys = [p.keys("cuda") for p in parts]
+        counts = [p.m for p in parts]
+        all_keys = torch.cat(keys) if sum(counts) else torch.empty(1, dtype=torch.uint8, device="cuda")
+        dense = []
+        for r, p in enumerate(parts):
+            g = p.dict(all_keys, sum(counts), sum(counts[:r]))
+            ds = torch.empty(max(g * p.W, 1), dtype=torch.float64, device="cuda")
+            df = torch.empty(max(g, 1), dtype=torch.int64, device="cuda")
+            dr = torch.empty(max(2 * g, 1), dtype=torch.int64, device="cuda")
+            p.scatter(ds, df, dr)
+            dense.append((g, ds, df, dr))
+        assert len({g for g, _, _, _ in dense}) == 1            # one dictionary on every rank
+        fmin = torch.stack([d[2] for d in dense]).min(0).values
+        for p, d in zip(parts, dense):
+            d[2].copy_(fmin)
+            p.mask_reps(d[2], d[3])
+        ssum = torch.stack([d[1] for d in dense]).sum(0)
+        rsum = torch.stack([d[3] for d in dense]).sum(0)
+        return parts[0].finish(ssum, fmin, rsum)
+    finally:
+        for p in parts:
+            p.free()
+
+
+DENSE = [q for q in QUERIES if "MIN(" not in q and "MAX(" not in q and "SELECT name" not in q]
+
+
+@pytest.mark.parametrize("sql", DENSE)
+@pytest.mark.parametrize("nranks", [1, 3, 8])
+def test_dense_merge_equals_oracle(files, sql, nranks):
+    path = files["plain"]
+    q = sql.format(p=path)
+    want, unsup = cqtest.oracle_query(q)
+    assert not unsup and want is not None
+    with cqtest.Parsed(q) as ast:
+        tabs = [cq_amd.Table.open_range(path, r, nranks) for r in range(nranks)]
+        try:
+            tp = _dense_merge_by_hand(ast, tabs)
+        finally:
+            for t in tabs:
+                t.close()
+        assert tp, cq_amd.last_error() or cq_amd.last_ineligible()
+        got = abi.table_to_py(tp)
+        cq_amd.result_free(tp)
+        tol = tolerant_columns(ast)
+    compare(got, want, tol, f"dense {nranks} ranks: {q}")
+
+
+def test_dense_merge_typed_keys(tmp_path):
+    """group keys of every class across ranks; a representative cell that is a DATE
+    on one rank and the same text as a STRING on another keeps the first row's kind"""
+    rows = ["k,v"]
+    vals = ["2024-01-05", " 2024-01-05 ", "NULL", "", "7", "7.0", "-0.5", "x", "2024-1-5"]
+    for i in range(9000):
+        rows.append(f"{vals[(i * 5) % len(vals)]},{i % 13}")
+    p = tmp_path / "typed.csv"
+    p.write_text("\n".join(rows) + "\n")
+    q = f"SELECT k, COUNT(*), SUM(v), AVG(v) FROM '{p}' GROUP BY k"
+    want, _ = cqtest.oracle_query(q)
+    for n in (2, 5):
+        with cqtest.Parsed(q) as ast:
+            tabs = [cq_amd.Table.open_range(str(p), r, n) for r in range(n)]
+            tp = _dense_merge_by_hand(ast, tabs)
+            for t in tabs:
+                t.close()
+            got = abi.table_to_py(tp)
+            cq_amd.result_free(tp)
+            tol = tolerant_columns(ast)
+        compare(got, want, tol, f"dense typed keys, {n} ranks")
+
+
+def test_dense_merge_refuses_minmax(files):
+    q = QUERIES[2].format(p=files["plain"])
+    with cqtest.Parsed(q) as ast:
+        t = cq_amd.Table.open_range(files["plain"], 0, 2)
+        from cq_amd.dist import DensePartial
+        part = DensePartial(ast, t)
+        assert not part.ok and "dense merge" in cq_amd.last_ineligible()
+        part.free()
+        t.close()
