@@ -8,28 +8,30 @@
 //
 // Every wave works on its own 4 KiB windows with no block barrier in the loop, so
 // one wave's byte classification overlaps another's record work on the same SIMD,
-// and every lane carries TWO records through the record pass (records l and
-// l + 64 of the pass): two independent dependency chains per lane for the LDS
-// round trips to overlap, and one set of wave-uniform tests, ballots and loop
-// control per two records.
+// and every lane carries TWO records through the record pass: two independent
+// dependency chains per lane for the LDS round trips to overlap, and one set of
+// wave-uniform tests, ballots and loop control per two records.
 //
 //   load      a window is 4 KiB of the file starting at a multiple of its stride
-//             (128-byte aligned), lane l bytes [64l, 64l + 64) by four 16-byte
-//             non-temporal loads issued one window ahead, plus the dword before
-//             the window (record-start context).  The window owns the records
-//             that start in its first `ws` bytes (ws <= WS = 3968); the last 128
-//             bytes are the record views' tail and are re-read by the next window
-//   classify  per lane two 64-bit masks -- separators (delimiter and record
-//             terminators '\n' '\r') and terminators -- plus quote presence; the
-//             masks go to LDS as the window's bitmaps (quote bitmap only when the
+//             (128-byte aligned) by four coalesced 16-byte non-temporal loads per
+//             lane (load i: bytes [1024i, 1024i + 1024)) issued one window ahead,
+//             plus the dword before the window (record-start context).  The window
+//             owns the records that start in its first `ws` bytes (ws <= WS =
+//             3968); the last 128 bytes are the record views' tail and are re-read
+//             by the next window
+//   classify  the window goes to LDS as loaded and comes back lane-contiguous
+//             (lane l: bytes [64l, 64l + 64)); per lane two 64-bit masks --
+//             separators (delimiter and record terminators '\n' '\r') and
+//             terminators -- plus quote presence (quote bitmap in LDS only when the
 //             window holds a quote)
-//   starts    record starts (previous byte a terminator) owned by the window; one
-//             DPP wave scan numbers them, 128 per pass go to an LDS list
-//   fields    per record: 64 separator and terminator bits from the record start
-//             (funnel shifts of three bitmap words); field c ends at the c-th set
-//             separator bit.  A record whose needed fields are not all inside
-//             those 64 bytes, or that has a quote in front of its last needed
-//             field, goes whole to the slow list and slow_kernel (scan.hip)
+//   starts    record starts (previous byte a terminator) owned by the window; each
+//             lane takes the records starting in its own 64 bytes, two per pass
+//   fields    per record: 64 separator and terminator bits from the record start,
+//             funnel-shifted out of the lane's own and the next lane's masks (one
+//             DPP wave shift each, no LDS); field c ends at the c-th set separator
+//             bit.  A record whose needed fields are not all inside those 64 bytes,
+//             or that has a quote in front of its last needed field, goes whole to
+//             the slow list and slow_kernel (scan.hip)
 //   values    WHERE / SUM fields of 1-4 bytes shaped `digits[.digits]` are typed
 //             in registers (right-aligned digit bytes, the dot squeezed out by one
 //             v_perm_b32, a v_dot4 for the value): M and k = digits after the dot,
@@ -73,9 +75,8 @@ constexpr int NWV = LT / 64;              // waves per block
 constexpr int LB = 64;                    // staged bytes per lane
 constexpr int WB = 64 * LB;               // staged window bytes (4 KiB)
 constexpr int WS = 3968;                  // largest window stride = owned bytes (LeanPlan.ws: the file's)
-constexpr int NMW = WB / 32;              // 32-bit bitmap words per window
+constexpr int NMW = WB / 32;              // 32-bit quote-bitmap words per window
 constexpr int WBYTES = WB + 32;           // staged bytes + slack for 16-byte field loads
-constexpr int RSN = 128;                  // record slots per pass: two per lane
 constexpr int MAXS = 2;                   // distinct SUM arguments
 constexpr int KN = 4;                     // need slots
 constexpr uint32_t NOFIRST = 0xFFFFFFFFu;
@@ -102,9 +103,7 @@ enum : int { LW_NONE = 0, LW_NUM = 1, LW_STR = 2, LW_GEN = 3 };
 // per-wave LDS area
 struct WaveLds {
     uint8_t bytes[WBYTES];
-    uint2 bm[NMW];              // {separator bits, terminator bits} per 32 window bytes
     uint32_t qt[NMW + 4];       // quote bits (written only when the window holds a quote)
-    uint16_t rs[RSN];           // record starts of the current pass (window offsets)
 };
 static_assert(sizeof(WaveLds) % 16 == 0, "16-byte aligned wave areas");
 
@@ -159,8 +158,16 @@ __device__ __forceinline__ void load_win(const uint8_t* g, uint64_t w, uint32_t 
     const uint8_t* base = g + w * ws;                    // 128-byte aligned (g is 256-aligned, ws % 128 == 0)
     const v4u* src = (const v4u*)base;
     const int lane = threadIdx.x & 63;
+#ifdef LEAN_TEMPORAL
+#define LEAN_LD(p) (*(p))
+#else
+#define LEAN_LD(p) __builtin_nontemporal_load(p)
+#endif
+    // coalesced: load i is bytes [1024i, 1024i + 1024), lane l its 16 bytes at 16l (one load
+    // per lane of 64 contiguous bytes was 1.5x slower to stream: 64-byte lane strides)
 #pragma unroll
-    for (int i = 0; i < 4; i++) x.a[i] = __builtin_nontemporal_load(src + 4 * lane + i);
+    for (int i = 0; i < 4; i++) x.a[i] = LEAN_LD(src + 64 * i + lane);
+#undef LEAN_LD
     // the dword before the window (g has 256 bytes of '\n' before byte 0) by a buffer load: a
     // uniform address would otherwise become a scalar load, whose lgkmcnt the LDS
     // waits of the whole window would have to drain
@@ -236,13 +243,11 @@ __device__ __forceinline__ uint32_t ctz64(uint64_t x) { return (uint32_t)__built
 __device__ __forceinline__ uint32_t rotl(uint32_t x, int r) { return __builtin_amdgcn_alignbit(x, x, 32 - r); }
 
 // 64 bitmap bits starting at window offset p
-__device__ __forceinline__ void views(const WaveLds& W, uint32_t p, uint64_t& sv, uint64_t& nv) {
-    const uint32_t wi = p >> 5, sh = p & 31;
-    const uint2 b0 = W.bm[wi], b1 = W.bm[wi + 1], b2 = W.bm[wi + 2];
-    sv = (uint64_t)__builtin_amdgcn_alignbit(b1.x, b0.x, sh) |
-         ((uint64_t)__builtin_amdgcn_alignbit(b2.x, b1.x, sh) << 32);
-    nv = (uint64_t)__builtin_amdgcn_alignbit(b1.y, b0.y, sh) |
-         ((uint64_t)__builtin_amdgcn_alignbit(b2.y, b1.y, sh) << 32);
+// 64 bits from bit b (< 64) of the 128 bits w0 | w1 << 32 | w2 << 64 | w3 << 96
+__device__ __forceinline__ uint64_t view128(uint32_t w0, uint32_t w1, uint32_t w2, uint32_t w3, uint32_t b) {
+    const bool hi = b >= 32;
+    const uint32_t sh = b & 31, a = hi ? w1 : w0, c = hi ? w2 : w1, d = hi ? w3 : w2;
+    return (uint64_t)__builtin_amdgcn_alignbit(c, a, sh) | ((uint64_t)__builtin_amdgcn_alignbit(d, c, sh) << 32);
 }
 __device__ __forceinline__ uint64_t qview(const WaveLds& W, uint32_t p) {
     const uint32_t wi = p >> 5, sh = p & 31;
@@ -714,16 +719,18 @@ __global__ __launch_bounds__(LT) void lean_kernel(const uint8_t* __restrict__ g,
 
         // ---- stage and classify
 #pragma unroll
-        for (int i = 0; i < 4; i++) ((v4u*)W.bytes)[4 * lane + i] = cur.a[i];
+        for (int i = 0; i < 4; i++) ((v4u*)W.bytes)[64 * i + lane] = cur.a[i];
+        wave_order();
+        v4u la[4];                                                    // lane l: window bytes [64l, 64l + 64)
+#pragma unroll
+        for (int i = 0; i < 4; i++) la[i] = ((const v4u*)W.bytes)[4 * lane + i];
         uint32_t sep0, nl0, sep1, nl1, qf = 0;
-        classify32(cur.a[0], cur.a[1], rep_d, rep_q, sep0, nl0, qf);
-        classify32(cur.a[2], cur.a[3], rep_d, rep_q, sep1, nl1, qf);
-        W.bm[2 * lane] = make_uint2(sep0, nl0);
-        W.bm[2 * lane + 1] = make_uint2(sep1, nl1);
+        classify32(la[0], la[1], rep_d, rep_q, sep0, nl0, qf);
+        classify32(la[2], la[3], rep_d, rep_q, sep1, nl1, qf);
         const bool wq = __ballot((qf & 0x80808080u) != 0) != 0;   // window holds a quote (uniform)
         if (wq) {
-            W.qt[2 * lane] = byte_bits(cur.a[0], cur.a[1], rep_q);
-            W.qt[2 * lane + 1] = byte_bits(cur.a[2], cur.a[3], rep_q);
+            W.qt[2 * lane] = byte_bits(la[0], la[1], rep_q);
+            W.qt[2 * lane + 1] = byte_bits(la[2], la[3], rep_q);
         }
 
         // ---- record starts owned by this window: file [ws, ws + stride) within [lo_ok, hi_ok)
@@ -745,45 +752,38 @@ __global__ __launch_bounds__(LT) void lean_kernel(const uint8_t* __restrict__ g,
                 if (hi_s < b0 + LB) starts &= (1ull << (hi_s - b0)) - 1;
             }
         }
-        const uint32_t nst = (uint32_t)__popcll(starts);
-        const uint32_t incl = wave_incl_scan(nst);
-        const uint32_t rbase = incl - nst;
-        const uint32_t R = (uint32_t)__builtin_amdgcn_readlane((int)incl, 63);
+        // every lane walks the records that start in its own 64 bytes, two per pass
+        // the next lane's bitmap words (wave_shl:1): a record starting in this lane's
+        // bytes has its 64-byte view inside these 128 bits (lane 63 owns no start:
+        // ws <= 3968)
+        const uint32_t xs0 = (uint32_t)__builtin_amdgcn_update_dpp(0, (int)sep0, 0x130, 0xf, 0xf, true);
+        const uint32_t xs1 = (uint32_t)__builtin_amdgcn_update_dpp(0, (int)sep1, 0x130, 0xf, 0xf, true);
+        const uint32_t xn0 = (uint32_t)__builtin_amdgcn_update_dpp(0, (int)nl0, 0x130, 0xf, 0xf, true);
+        const uint32_t xn1 = (uint32_t)__builtin_amdgcn_update_dpp(0, (int)nl1, 0x130, 0xf, 0xf, true);
+        uint64_t todo = starts;
 
         LCLK(1);
-#if defined(LEAN_PROF) && LEAN_PROF == 1   // profiling build: + classify, bitmaps, record numbering
-        n_rec += R;
+#if defined(LEAN_PROF) && LEAN_PROF == 1   // profiling build: + classify, bitmaps
+        n_rec += (unsigned long long)__popcll(__ballot(((xs0 ^ xs1 ^ xn0 ^ xn1) & 1) != (todo & 1)));
         continue;
 #endif
-        for (uint32_t pass = 0; pass < R; pass += RSN) {
-            // this pass's record starts -> W.rs
-            {
-                uint64_t m = starts;
-                uint32_t r = rbase - pass;
-                while (m) {
-                    const uint32_t b = ctz64(m);
-                    m &= m - 1;
-                    if (r < (uint32_t)RSN) W.rs[r] = (uint16_t)(lane * LB + b);
-                    r++;
-                }
-            }
-            wave_order();
+        while (__any(todo != 0)) {
             Rec rec[2];
+            uint64_t sv[2], nv[2];
 #pragma unroll
             for (int u = 0; u < 2; u++) {
                 Rec& Rr = rec[u];
-                Rr.valid = pass + 64 * u + lane < R;
-                Rr.p = Rr.valid ? W.rs[64 * u + lane] : 0u;
+                Rr.valid = todo != 0;
+                const uint32_t b = Rr.valid ? ctz64(todo) : 0u;
+                todo &= todo - 1;
+                Rr.p = (uint32_t)lane * LB + b;
+                sv[u] = view128(sep0, sep1, xs0, xs1, b);
+                nv[u] = view128(nl0, nl1, xn0, xn1, b);
+                Rr.fail = !Rr.valid;
+                Rr.lastpos = 0;
             }
             // ---- role fields (WHERE, SUM 0/1, GROUP BY): position and length (0: NULL / missing)
             {
-                uint64_t sv[2], nv[2];
-#pragma unroll
-                for (int u = 0; u < 2; u++) {
-                    views(W, rec[u].p, sv[u], nv[u]);
-                    rec[u].fail = !rec[u].valid;
-                    rec[u].lastpos = 0;
-                }
 #pragma unroll
                 for (int u = 0; u < 2; u++) {
                     Rec& Rr = rec[u];
@@ -1093,7 +1093,7 @@ __global__ __launch_bounds__(LT) void lean_kernel(const uint8_t* __restrict__ g,
                     }
                 }
             }
-            wave_order();                                  // W.rs is rewritten by the next pass
+            wave_order();
             LCLK(5);
         }
         LCLK(6);

@@ -10,6 +10,6 @@ for v in ${VARIANTS:-"clk:-DLEAN_CLK" "l1:-DLEAN_PROF=1" "nomem:-DLEAN_NOMEM"}; 
   n=${v%%:*}; d=$(echo "${v#*:}" | tr "+" " ")
   ( /opt/rocm/bin/hipcc $F $d -c lean.hip -o /tmp/lean_$n.o && \
     /opt/rocm/bin/hipcc -shared --offload-arch=gfx950 -o ../lib/libcqgpu_$n.so ../lib/scan.o /tmp/lean_$n.o \
-        ../lib/executor.o ../lib/sort.o ../lib/route.o ../lib/hostcell.o ) &
+        ../lib/executor.o ../lib/route.o ../lib/prim.o ../lib/writer.o ../lib/merge.o ../lib/hostcell.o ) &
 done
 wait
