@@ -1221,6 +1221,25 @@ double now_ms() {
     return std::chrono::duration<double, std::milli>(std::chrono::steady_clock::now().time_since_epoch()).count();
 }
 
+// CQ_AMD_TIMING=1: host-side phase times of each aggregate query on stderr
+struct PhaseClock {
+    bool on;
+    double t;
+    std::string line;
+    PhaseClock() : on(getenv("CQ_AMD_TIMING") != nullptr), t(on ? now_ms() : 0.0) {}
+    void mark(const char* what) {
+        if (!on) return;
+        const double n = now_ms();
+        char b[64];
+        snprintf(b, sizeof b, " %s %.3f", what, n - t);
+        line += b;
+        t = n;
+    }
+    ~PhaseClock() { if (on && !line.empty()) fprintf(stderr, "cq_amd timing ms:%s\n", line.c_str()); }
+};
+PhaseClock* g_phase = nullptr;
+#define PHASE(x) do { if (g_phase) g_phase->mark(x); } while (0)
+
 // compacted groups + finish output -> host groups in first-appearance order
 // (create_groups appends groups in row order); `limit`: first positions are below it
 std::vector<HGroup> make_groups(DevCtx& c, const Compiled& C, uint64_t limit, uint64_t base_offset,
@@ -1265,6 +1284,7 @@ std::vector<HGroup> make_groups(DevCtx& c, const Compiled& C, uint64_t limit, ui
     for (size_t i = 0; i < order.size(); i++) order[i] = (uint32_t)i;
     std::sort(order.begin(), order.end(), [&](uint32_t a, uint32_t b) { return outs[a].first < outs[b].first; });
     const size_t nrep = C.rep_cols.size();
+    groups.reserve(order.size());
     for (uint32_t gi : order) {
         const GroupOut& o = outs[gi];
         const HCell* cs = hcells.data() + (size_t)gi * ncell;
@@ -1304,6 +1324,7 @@ std::vector<HGroup> run_aggregate(DevCtx& c, const cqgpu_table* t, Compiled& C, 
                                   unsigned long long row_cap = 0) {
     parse_literals(c, C.lits, L);
     for (size_t i = 0; i < L.cells.size(); i++) C.P.consts[i] = L.cells[i];
+    PHASE("literals");
     std::vector<HGroup> groups;
     if (C.group_missing) return groups;    // create_groups: unknown column -> no groups
     const int grouped = C.grouped ? 1 : 0;
@@ -1360,12 +1381,18 @@ std::vector<HGroup> run_aggregate(DevCtx& c, const cqgpu_table* t, Compiled& C, 
             if (!chunk) {      // one launch: compact and finish speculatively, one sync for all
                 HIPCHECK(cq_launch_compact(&A.gt, &C.P, A.out, A.out_count, cap_out, c.stream));
                 HIPCHECK(cq_launch_finish(t->g, t->n, A.out, A.out_count, cap_out, &FD, dcells, dbytes, c.stream));
-                HIPCHECK(hipMemcpyAsync(&ng, A.out_count, 4, hipMemcpyDeviceToHost, c.stream));
                 finished = true;
             }
-            ScanStats s1;
-            HIPCHECK(hipMemcpyAsync(&s1, A.stats, sizeof s1, hipMemcpyDeviceToHost, c.stream));
+            // the group count and the scan statistics through pinned memory, one sync
+            uint8_t* hs = (uint8_t*)pinned(c, sizeof(ScanStats) + 16);
+            HIPCHECK(hipMemcpyAsync(hs, A.stats, sizeof(ScanStats), hipMemcpyDeviceToHost, c.stream));
+            if (finished) HIPCHECK(hipMemcpyAsync(hs + sizeof(ScanStats), A.out_count, 4, hipMemcpyDeviceToHost, c.stream));
+            PHASE("launch");
             HIPCHECK(hipStreamSynchronize(c.stream));
+            PHASE("scan+finish");
+            ScanStats s1;
+            memcpy(&s1, hs, sizeof s1);
+            if (finished) memcpy(&ng, hs + sizeof(ScanStats), 4);
             float ms = 0;
             HIPCHECK(hipEventElapsedTime(&ms, c.ev0, c.ev1));
             ms_total += ms;
@@ -1408,12 +1435,18 @@ std::vector<HGroup> run_aggregate(DevCtx& c, const cqgpu_table* t, Compiled& C, 
         outs.resize(ng);
         fcells.resize((size_t)ng * ncell);
         fbytes.resize((size_t)ng * ncell * SB);
-        if (ng) {
-            HIPCHECK(hipMemcpyAsync(outs.data(), A.out, ng * sizeof(GroupOut), hipMemcpyDeviceToHost, c.stream));
-            HIPCHECK(hipMemcpyAsync(fcells.data(), dcells, fcells.size() * sizeof(Cell), hipMemcpyDeviceToHost, c.stream));
-            HIPCHECK(hipMemcpyAsync(fbytes.data(), dbytes, fbytes.size(), hipMemcpyDeviceToHost, c.stream));
+        if (ng) {   // through the pinned staging buffer: three async copies, one sync
+            const size_t b0 = ng * sizeof(GroupOut), b1 = fcells.size() * sizeof(Cell), b2 = fbytes.size();
+            uint8_t* hp = (uint8_t*)pinned(c, b0 + b1 + b2);
+            HIPCHECK(hipMemcpyAsync(hp, A.out, b0, hipMemcpyDeviceToHost, c.stream));
+            HIPCHECK(hipMemcpyAsync(hp + b0, dcells, b1, hipMemcpyDeviceToHost, c.stream));
+            HIPCHECK(hipMemcpyAsync(hp + b0 + b1, dbytes, b2, hipMemcpyDeviceToHost, c.stream));
+            HIPCHECK(hipStreamSynchronize(c.stream));
+            memcpy(outs.data(), hp, b0);
+            memcpy(fcells.data(), hp + b0, b1);
+            memcpy(fbytes.data(), hp + b0 + b1, b2);
         }
-        HIPCHECK(hipStreamSynchronize(c.stream));
+        PHASE("copies");
         break;
     }
     g_stats.retries = retries;
@@ -2218,6 +2251,7 @@ std::vector<HGroup> aggregate_pairs(DevCtx& c, Compiled& C, const JoinMap& MA, c
             HIPCHECK(hipMemcpyAsync(fbytes.data(), dbytes, fbytes.size(), hipMemcpyDeviceToHost, c.stream));
         }
         HIPCHECK(hipStreamSynchronize(c.stream));
+        PHASE("copies");
         break;
     }
     g_stats.passed = st.passed;
@@ -2728,8 +2762,12 @@ cq_table* query_impl(cq_node* q, cqgpu_table* const* tables, int ntables) {
         post_ops(c, res, q, true, limited);
         return res;
     }
+    PhaseClock pc;
+    g_phase = &pc;
+    struct Unset { ~Unset() { g_phase = nullptr; } } unset_;
     Compiled C;
     compile_aggregate(t, q, C);
+    PHASE("compile");
     Literals L;
     std::vector<HGroup> groups;
     if (C.P.ngpart > 0) {
@@ -2744,9 +2782,12 @@ cq_table* query_impl(cq_node* q, cqgpu_table* const* tables, int ntables) {
             groups = run_cells_aggregate(c, t, C, L);
         }
     }
+    PHASE("groups");
     g_stats.groups = groups.size();
     cq_table* res = build_groups(C, groups, L, c);
+    PHASE("build");
     post_ops(c, res, q);
+    PHASE("post");
     return res;
 }
 
