@@ -13,7 +13,7 @@ import os
 from . import abi
 
 HERE = os.path.dirname(os.path.abspath(__file__))
-# CQ_AMD_LIB: profiling builds of the same library (scripts/prof_stages.sh)
+# CQ_AMD_LIB: profiling builds of the same library (scripts/build_lean_variants.sh, scripts/bench_variants.sh)
 LIB_PATH = os.environ.get("CQ_AMD_LIB") or os.path.join(HERE, "lib", "libcqgpu.so")
 
 _lib = None
