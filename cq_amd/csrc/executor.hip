@@ -98,6 +98,10 @@ hipError_t cq_launch_join_project(const uint2* pairs, unsigned long long np, con
 hipError_t cq_launch_join_finish(const cq::GroupOut* out, const unsigned int* count, unsigned int cap_out,
                                  const uint2* pairs, const cq::JoinMap* M, const cq::Cell* L, const cq::Cell* R,
                                  int nacc, uint32_t sb, cq::Cell* cells, uint8_t* bytes, hipStream_t s);
+hipError_t cq_launch_vla_pair_prep(const uint2* pairs, uint32_t n, const cq::JoinMap* M, const cq::JoinMap* V,
+                                   const cq::Cell* L, const cq::Cell* R, const cq::ScanPlan* P, int grouped,
+                                   unsigned long long* kw0, unsigned long long* kw1, unsigned long long* kcl,
+                                   unsigned long long* vkey, unsigned int* flag, hipStream_t s);
 hipError_t cq_launch_vla_prep(const cq::Cell* cells, uint32_t n, uint32_t nc, int gslot, uint32_t vslot,
                               unsigned long long* kw0, unsigned long long* kw1, unsigned long long* kcl,
                               unsigned long long* vkey, unsigned int* flag, hipStream_t s);
@@ -1940,10 +1944,93 @@ cq_table* run_rows(DevCtx& c, const cqgpu_table* t, Compiled& C, RowPlan& R, cq_
     return r;
 }
 
-// STDDEV / MEDIAN (evaluate_aggregate, evaluator_aggregates.c:328-411): the
-// WHERE-passing records' group key and value cells, sorted on the device by
-// (key, value), reduced per group (scan.hip vla_* kernels), matched back to the
-// scan's groups by key
+// STDDEV / MEDIAN (evaluate_aggregate, evaluator_aggregates.c:328-411): per passing
+// row its group key words and the value as an order-preserving key (vla_prep /
+// vla_pair_prep), sorted on the device by (key, value), reduced per group (scan.hip
+// vla_* kernels), matched back to the aggregation's groups by key.
+using VlaAt = std::map<std::tuple<uint64_t, uint64_t, uint64_t>, size_t>;
+VlaAt vla_index(const Compiled& C, const std::vector<HGroup>& groups) {
+    VlaAt at;                            // GK_LONG keys by content hash, as the kernels key them
+    for (size_t g = 0; g < groups.size(); g++) {
+        const HGroup& h = groups[g];
+        const uint64_t cl = C.grouped ? ((uint64_t)h.kcls << 16 | h.klen) : ((uint64_t)GK_ALL << 16);
+        const uint64_t w0 = !C.grouped || h.kcls == GK_LONG ? 0 : h.kw0;
+        const uint64_t w1 = C.grouped ? h.kw1 : 0;
+        at[std::make_tuple(cl, w0, w1)] = g;
+    }
+    return at;
+}
+struct VlaRows {                         // one row per candidate: key words, value key, numeric flag
+    DevBuf kw0, kw1, kcl, vkey, flag;
+    explicit VlaRows(size_t n) : kw0(n * 8), kw1(n * 8), kcl(n * 8), vkey(n * 8), flag(n * 4) {}
+};
+// sort + segment + reduce one value-list aggregate (index vi, kind 0 STDDEV / 1 MEDIAN)
+void vla_finish(DevCtx& c, const VlaAt& at, bool grouped, std::vector<HGroup>& groups, size_t vi, int kind,
+                VlaRows& V, uint32_t n) {
+    if (!n) return;
+    const size_t N = n;
+    DevBuf pos(N * 4), perm(N * 4), perm2(N * 4), keys(N * 8), keys2(N * 8), head(N * 4), sid(N * 4), start(N * 4),
+        out(N * 32);
+    uint32_t m = 0;
+    {
+        size_t tb = 0;
+        HIPCHECK(cq_excl_sum_u32(nullptr, &tb, V.flag.as<unsigned int>(), pos.as<unsigned int>(), n, c.stream));
+        DevBuf temp(tb);
+        HIPCHECK(cq_excl_sum_u32(temp.p, &tb, V.flag.as<unsigned int>(), pos.as<unsigned int>(), n, c.stream));
+        unsigned int last[2] = {0, 0};
+        HIPCHECK(hipMemcpyAsync(&last[0], pos.as<unsigned int>() + n - 1, 4, hipMemcpyDeviceToHost, c.stream));
+        HIPCHECK(hipMemcpyAsync(&last[1], V.flag.as<unsigned int>() + n - 1, 4, hipMemcpyDeviceToHost, c.stream));
+        HIPCHECK(hipStreamSynchronize(c.stream));
+        m = last[0] + last[1];
+    }
+    if (!m) return;                      // no numeric value anywhere: every group NULL
+    HIPCHECK(cq_launch_vla_compact(V.flag.as<unsigned int>(), pos.as<unsigned int>(), n, perm.as<unsigned int>(),
+                                   c.stream));
+    // LSD: value, then the key words (stable sorts keep the value order inside a key)
+    const unsigned long long* passes[4] = {V.vkey.as<unsigned long long>(), V.kcl.as<unsigned long long>(),
+                                           V.kw1.as<unsigned long long>(), V.kw0.as<unsigned long long>()};
+    for (int ps = 0; ps < 4; ps++) {
+        if (ps > 0 && !grouped) break;
+        HIPCHECK(cq_launch_vla_gather(passes[ps], perm.as<unsigned int>(), m, keys.as<unsigned long long>(), c.stream));
+        size_t tb = 0;
+        HIPCHECK(cq_sort_codes(nullptr, &tb, keys.as<unsigned long long>(), keys2.as<unsigned long long>(),
+                               perm.as<unsigned int>(), perm2.as<unsigned int>(), m, c.stream));
+        DevBuf temp(tb);
+        HIPCHECK(cq_sort_codes(temp.p, &tb, keys.as<unsigned long long>(), keys2.as<unsigned long long>(),
+                               perm.as<unsigned int>(), perm2.as<unsigned int>(), m, c.stream));
+        HIPCHECK(hipStreamSynchronize(c.stream));
+        std::swap(perm.p, perm2.p);
+    }
+    HIPCHECK(cq_launch_vla_heads(V.kw0.as<unsigned long long>(), V.kw1.as<unsigned long long>(),
+                                 V.kcl.as<unsigned long long>(), perm.as<unsigned int>(), m, head.as<unsigned int>(),
+                                 c.stream));
+    size_t tb = 0;
+    HIPCHECK(cq_excl_sum_u32(nullptr, &tb, head.as<unsigned int>(), sid.as<unsigned int>(), m, c.stream));
+    DevBuf temp(tb);
+    HIPCHECK(cq_excl_sum_u32(temp.p, &tb, head.as<unsigned int>(), sid.as<unsigned int>(), m, c.stream));
+    unsigned int last[2] = {0, 0};
+    HIPCHECK(hipMemcpyAsync(&last[0], sid.as<unsigned int>() + m - 1, 4, hipMemcpyDeviceToHost, c.stream));
+    HIPCHECK(hipMemcpyAsync(&last[1], head.as<unsigned int>() + m - 1, 4, hipMemcpyDeviceToHost, c.stream));
+    HIPCHECK(hipStreamSynchronize(c.stream));
+    const uint32_t nseg = last[0] + last[1];
+    HIPCHECK(cq_launch_vla_starts(head.as<unsigned int>(), sid.as<unsigned int>(), m, start.as<unsigned int>(), c.stream));
+    HIPCHECK(cq_launch_vla_reduce(V.vkey.as<unsigned long long>(), V.kw0.as<unsigned long long>(),
+                                  V.kw1.as<unsigned long long>(), V.kcl.as<unsigned long long>(), perm.as<unsigned int>(),
+                                  start.as<unsigned int>(), nseg, m, kind, out.as<unsigned long long>(), c.stream));
+    std::vector<unsigned long long> h((size_t)nseg * 4);
+    HIPCHECK(hipMemcpyAsync(h.data(), out.p, h.size() * 8, hipMemcpyDeviceToHost, c.stream));
+    HIPCHECK(hipStreamSynchronize(c.stream));
+    for (uint32_t sg = 0; sg < nseg; sg++) {
+        auto it = at.find(std::make_tuple((uint64_t)h[4 * sg], (uint64_t)h[4 * sg + 1], (uint64_t)h[4 * sg + 2]));
+        if (it == at.end()) continue;
+        HGroup& g = groups[it->second];
+        g.vla[vi] = as_dbl(h[4 * sg + 3]);
+        g.vla_ok[vi] = true;
+    }
+}
+
+// single table, single-column (or no) GROUP BY: the WHERE-passing records' key and
+// value cells from their byte offsets
 void compute_vla(DevCtx& c, const cqgpu_table* t, const Compiled& C, std::vector<HGroup>& groups) {
     if (C.vla.empty() || groups.empty()) return;
     const cqgpu_stats saved = g_stats;
@@ -1977,82 +2064,33 @@ void compute_vla(DevCtx& c, const cqgpu_table* t, const Compiled& C, std::vector
     auto slot = [&](int col) { return (int)(std::find(cols.begin(), cols.end(), col) - cols.begin()); };
     DevBuf cells((size_t)std::max<uint32_t>(n, 1) * D.ncols * sizeof(Cell));
     HIPCHECK(cq_launch_cells(t->g, t->n, rows.as<unsigned long long>(), n, &D, cells.as<Cell>(), c.stream));
-    // host map: group key -> group (GK_LONG keys by content hash, as the kernel keys them)
-    std::map<std::tuple<uint64_t, uint64_t, uint64_t>, size_t> at;
-    for (size_t g = 0; g < groups.size(); g++) {
-        const HGroup& h = groups[g];
-        const uint64_t cl = C.grouped ? ((uint64_t)h.kcls << 16 | h.klen) : ((uint64_t)GK_ALL << 16);
-        const uint64_t w0 = !C.grouped || h.kcls == GK_LONG ? 0 : h.kw0;
-        const uint64_t w1 = C.grouped ? h.kw1 : 0;
-        at[std::make_tuple(cl, w0, w1)] = g;
-    }
-    const size_t N = std::max<uint32_t>(n, 1);
-    DevBuf kw0(N * 8), kw1(N * 8), kcl(N * 8), vkey(N * 8), flag(N * 4), pos(N * 4), perm(N * 4), perm2(N * 4),
-        keys(N * 8), keys2(N * 8), head(N * 4), sid(N * 4), start(N * 4), out(N * 32);
+    const VlaAt at = vla_index(C, groups);
+    VlaRows V(std::max<uint32_t>(n, 1));
     for (size_t vi = 0; vi < C.vla.size(); vi++) {
-        const int kind = C.vla[vi].first;
         HIPCHECK(cq_launch_vla_prep(cells.as<Cell>(), n, (uint32_t)D.ncols, C.grouped ? slot(C.group_col) : -1,
-                                    (uint32_t)slot(C.vla[vi].second), kw0.as<unsigned long long>(),
-                                    kw1.as<unsigned long long>(), kcl.as<unsigned long long>(),
-                                    vkey.as<unsigned long long>(), flag.as<unsigned int>(), c.stream));
-        uint32_t m = 0;
-        if (n) {
-            size_t tb = 0;
-            HIPCHECK(cq_excl_sum_u32(nullptr, &tb, flag.as<unsigned int>(), pos.as<unsigned int>(), n, c.stream));
-            DevBuf temp(tb);
-            HIPCHECK(cq_excl_sum_u32(temp.p, &tb, flag.as<unsigned int>(), pos.as<unsigned int>(), n, c.stream));
-            unsigned int last[2] = {0, 0};
-            HIPCHECK(hipMemcpyAsync(&last[0], pos.as<unsigned int>() + n - 1, 4, hipMemcpyDeviceToHost, c.stream));
-            HIPCHECK(hipMemcpyAsync(&last[1], flag.as<unsigned int>() + n - 1, 4, hipMemcpyDeviceToHost, c.stream));
-            HIPCHECK(hipStreamSynchronize(c.stream));
-            m = last[0] + last[1];
-        }
-        if (!m) continue;                   // no numeric value anywhere: every group NULL
-        HIPCHECK(cq_launch_vla_compact(flag.as<unsigned int>(), pos.as<unsigned int>(), n, perm.as<unsigned int>(),
-                                       c.stream));
-        // LSD: value, then the key words (stable sorts keep the value order inside a key)
-        const unsigned long long* passes[4] = {vkey.as<unsigned long long>(), kcl.as<unsigned long long>(),
-                                               kw1.as<unsigned long long>(), kw0.as<unsigned long long>()};
-        for (int ps = 0; ps < 4; ps++) {
-            if (ps > 0 && !C.grouped) break;
-            HIPCHECK(cq_launch_vla_gather(passes[ps], perm.as<unsigned int>(), m, keys.as<unsigned long long>(),
-                                          c.stream));
-            size_t tb = 0;
-            HIPCHECK(cq_sort_codes(nullptr, &tb, keys.as<unsigned long long>(), keys2.as<unsigned long long>(),
-                                   perm.as<unsigned int>(), perm2.as<unsigned int>(), m, c.stream));
-            DevBuf temp(tb);
-            HIPCHECK(cq_sort_codes(temp.p, &tb, keys.as<unsigned long long>(), keys2.as<unsigned long long>(),
-                                   perm.as<unsigned int>(), perm2.as<unsigned int>(), m, c.stream));
-            HIPCHECK(hipStreamSynchronize(c.stream));
-            std::swap(perm.p, perm2.p);
-        }
-        HIPCHECK(cq_launch_vla_heads(kw0.as<unsigned long long>(), kw1.as<unsigned long long>(),
-                                     kcl.as<unsigned long long>(), perm.as<unsigned int>(), m, head.as<unsigned int>(),
-                                     c.stream));
-        size_t tb = 0;
-        HIPCHECK(cq_excl_sum_u32(nullptr, &tb, head.as<unsigned int>(), sid.as<unsigned int>(), m, c.stream));
-        DevBuf temp(tb);
-        HIPCHECK(cq_excl_sum_u32(temp.p, &tb, head.as<unsigned int>(), sid.as<unsigned int>(), m, c.stream));
-        unsigned int last[2] = {0, 0};
-        HIPCHECK(hipMemcpyAsync(&last[0], sid.as<unsigned int>() + m - 1, 4, hipMemcpyDeviceToHost, c.stream));
-        HIPCHECK(hipMemcpyAsync(&last[1], head.as<unsigned int>() + m - 1, 4, hipMemcpyDeviceToHost, c.stream));
-        HIPCHECK(hipStreamSynchronize(c.stream));
-        const uint32_t nseg = last[0] + last[1];
-        HIPCHECK(cq_launch_vla_starts(head.as<unsigned int>(), sid.as<unsigned int>(), m, start.as<unsigned int>(),
-                                      c.stream));
-        HIPCHECK(cq_launch_vla_reduce(vkey.as<unsigned long long>(), kw0.as<unsigned long long>(),
-                                      kw1.as<unsigned long long>(), kcl.as<unsigned long long>(), perm.as<unsigned int>(),
-                                      start.as<unsigned int>(), nseg, m, kind, out.as<unsigned long long>(), c.stream));
-        std::vector<unsigned long long> h((size_t)nseg * 4);
-        HIPCHECK(hipMemcpyAsync(h.data(), out.p, h.size() * 8, hipMemcpyDeviceToHost, c.stream));
-        HIPCHECK(hipStreamSynchronize(c.stream));
-        for (uint32_t sg = 0; sg < nseg; sg++) {
-            auto it = at.find(std::make_tuple((uint64_t)h[4 * sg], (uint64_t)h[4 * sg + 1], (uint64_t)h[4 * sg + 2]));
-            if (it == at.end()) continue;
-            HGroup& g = groups[it->second];
-            g.vla[vi] = as_dbl(h[4 * sg + 3]);
-            g.vla_ok[vi] = true;
-        }
+                                    (uint32_t)slot(C.vla[vi].second), V.kw0.as<unsigned long long>(),
+                                    V.kw1.as<unsigned long long>(), V.kcl.as<unsigned long long>(),
+                                    V.vkey.as<unsigned long long>(), V.flag.as<unsigned int>(), c.stream));
+        vla_finish(c, at, C.grouped, groups, vi, C.vla[vi].first, V, n);
+    }
+}
+
+// over (l, r) pairs of parsed cells (joins; composite / expression keys over identity
+// pairs): MA the plan's need slots, VM[vi] the value column of C.vla[vi]
+void compute_vla_pairs(DevCtx& c, const Compiled& C, const JoinMap& MA, const std::vector<JoinMap>& VM,
+                       const uint2* pairs, unsigned long long np, const Cell* Lc, const Cell* Rc,
+                       std::vector<HGroup>& groups) {
+    if (C.vla.empty() || groups.empty()) return;
+    if (np >= (1ull << 31)) throw Ineligible{"STDDEV/MEDIAN over more than 2^31 rows"};
+    const uint32_t n = (uint32_t)np;
+    const VlaAt at = vla_index(C, groups);
+    VlaRows V(std::max<uint32_t>(n, 1));
+    for (size_t vi = 0; vi < C.vla.size(); vi++) {
+        HIPCHECK(cq_launch_vla_pair_prep(pairs, n, &MA, &VM[vi], Lc, Rc, &C.P, C.grouped ? 1 : 0,
+                                         V.kw0.as<unsigned long long>(), V.kw1.as<unsigned long long>(),
+                                         V.kcl.as<unsigned long long>(), V.vkey.as<unsigned long long>(),
+                                         V.flag.as<unsigned int>(), c.stream));
+        vla_finish(c, at, C.grouped, groups, vi, C.vla[vi].first, V, n);
     }
 }
 
@@ -2489,11 +2527,12 @@ cq_table* run_join(DevCtx& c, cq_node* q, const cqgpu_table* L, const cqgpu_tabl
     RowPlan RP;
     if (rows) compile_rows(&J, q, C, RP);
     else compile_aggregate(&J, q, C);
-    if (!C.vla.empty()) throw Ineligible{"STDDEV/MEDIAN over a join"};
+    if (!C.vla.empty() && part) throw Ineligible{"STDDEV/MEDIAN across partials (needs every value)"};
     // columns each level needs, from the last level back
     {
         std::set<int> cur(C.need_cols.begin(), C.need_cols.end());
         cur.insert(C.rep_cols.begin(), C.rep_cols.end());
+        for (auto& v : C.vla) cur.insert(v.second);
         cur.insert(RP.cols.begin(), RP.cols.end());
         for (int j = nj - 1; j >= 0; j--) {
             Level& v = lv[j];
@@ -2624,6 +2663,11 @@ cq_table* run_join(DevCtx& c, cq_node* q, const cqgpu_table* L, const cqgpu_tabl
         const JoinMap MR = join_map(C.rep_cols, nl, A, B);
         ScanStats st;
         groups = aggregate_pairs(c, C, MA, MR, pairs.as<uint2>(), np, A.cells.as<Cell>(), B.cells.as<Cell>(), st);
+        if (!C.vla.empty()) {
+            std::vector<JoinMap> VM;
+            for (auto& v : C.vla) VM.push_back(join_map(std::vector<int>{v.second}, nl, A, B));
+            compute_vla_pairs(c, C, MA, VM, pairs.as<uint2>(), np, A.cells.as<Cell>(), B.cells.as<Cell>(), groups);
+        }
         if (part) {
             for (int a = 0; a < C.P.nacc; a++) part->acc_classes[a] = st.acc_classes[a];
             // pair positions -> global (left id, right id) order keys
@@ -2682,6 +2726,9 @@ std::vector<HGroup> run_cells_aggregate(DevCtx& c, const cqgpu_table* t, Compile
     JoinSide A, B;
     for (int j : C.need_cols) A.cols.push_back(j);
     for (int j : C.rep_cols) A.cols.push_back(j);
+    for (auto& v : C.vla) A.cols.push_back(v.second);
+    std::sort(A.cols.begin(), A.cols.end());
+    A.cols.erase(std::unique(A.cols.begin(), A.cols.end()), A.cols.end());
     if (A.cols.empty()) A.cols.push_back(0);
     load_side(c, t, A);
     const unsigned long long np = A.n;
@@ -2692,6 +2739,11 @@ std::vector<HGroup> run_cells_aggregate(DevCtx& c, const cqgpu_table* t, Compile
     const JoinMap MR = join_map(C.rep_cols, nl, A, B);
     ScanStats st;
     groups = aggregate_pairs(c, C, MA, MR, pairs.as<uint2>(), np, A.cells.as<Cell>(), bcells.as<Cell>(), st);
+    if (!C.vla.empty()) {
+        std::vector<JoinMap> VM;
+        for (auto& v : C.vla) VM.push_back(join_map(std::vector<int>{v.second}, nl, A, B));
+        compute_vla_pairs(c, C, MA, VM, pairs.as<uint2>(), np, A.cells.as<Cell>(), bcells.as<Cell>(), groups);
+    }
     if (st_out) *st_out = st;
     g_stats.records = np;
     g_stats.scan_bytes = t->n;
@@ -2771,14 +2823,12 @@ cq_table* query_impl(cq_node* q, cqgpu_table* const* tables, int ntables) {
     Literals L;
     std::vector<HGroup> groups;
     if (C.P.ngpart > 0) {
-        if (!C.vla.empty()) throw Ineligible{"STDDEV/MEDIAN with a composite or expression GROUP BY"};
         groups = run_cells_aggregate(c, t, C, L);
     } else {
         try {
             groups = run_aggregate(c, t, C, L, nullptr);
             compute_vla(c, t, C, groups);
         } catch (MixedExtremes&) {
-            if (!C.vla.empty()) throw Ineligible{"STDDEV/MEDIAN beside MIN/MAX over mixed value classes"};
             groups = run_cells_aggregate(c, t, C, L);
         }
     }

@@ -1872,6 +1872,38 @@ __global__ void vla_prep_kernel(const Cell* __restrict__ cells, uint32_t n, uint
     flag[i] = is_num(v) ? 1u : 0u;
 }
 
+// the same per (l, r) pair of parsed cells (joins, composite / expression keys
+// over identity pairs): WHERE by the plan's VM, the group key as join_agg_kernel
+// computes it (plan_group_key), the value from V's one column
+__global__ void vla_pair_prep_kernel(const uint2* __restrict__ pairs, uint32_t n, JoinMap M, JoinMap V,
+                                     const Cell* __restrict__ L, const Cell* __restrict__ R, int grouped,
+                                     unsigned long long* __restrict__ kw0, unsigned long long* __restrict__ kw1,
+                                     unsigned long long* __restrict__ kcl, unsigned long long* __restrict__ vkey,
+                                     unsigned int* __restrict__ flag) {
+    const ScanPlan& P = c_plan;
+    const uint32_t i = blockIdx.x * blockDim.x + threadIdx.x;
+    if (i >= n) return;
+    const uint2 pr = pairs[i];
+    CellsT<MAX_NEED> cs;
+    join_cells(M, L, R, pr, cs);
+    const bool pass = P.nprog == 0 || eval_where_vm(P, P.consts, cs);
+    GKey k;
+    k.cls = GK_ALL; k.len = 0; k.w0 = 0; k.w1 = 0;
+    if (grouped) {
+        bool tab = false;
+        k = plan_group_key(P, P.consts, cs, P.nneed, tab);
+    }
+    kw0[i] = k.cls == GK_LONG ? 0ull : k.w0;
+    kw1[i] = k.w1;
+    kcl[i] = gk_clslen(k);
+    const uint32_t row = V.side[0] ? pr.y : pr.x;
+    Cell v = cell_null();
+    if (row != JOIN_NONE) v = V.side[0] ? R[(uint64_t)row * V.rstride + V.col[0]] : L[(uint64_t)row * V.lstride + V.col[0]];
+    const uint64_t b = dbl_bits(num_of(v));
+    vkey[i] = (b >> 63) ? ~b : (b | 0x8000000000000000ULL);
+    flag[i] = pass && is_num(v) ? 1u : 0u;
+}
+
 __global__ void vla_compact_kernel(const unsigned int* __restrict__ flag, const unsigned int* __restrict__ pos,
                                    uint32_t n, unsigned int* __restrict__ perm) {
     const uint32_t i = blockIdx.x * blockDim.x + threadIdx.x;
@@ -2257,6 +2289,16 @@ hipError_t cq_launch_join_finish(const cq::GroupOut* out, const unsigned int* co
 }
 
 // ---- STDDEV / MEDIAN kernels (executor.hip compute_vla)
+hipError_t cq_launch_vla_pair_prep(const uint2* pairs, uint32_t n, const cq::JoinMap* M, const cq::JoinMap* V,
+                                   const cq::Cell* L, const cq::Cell* R, const cq::ScanPlan* P, int grouped,
+                                   unsigned long long* kw0, unsigned long long* kw1, unsigned long long* kcl,
+                                   unsigned long long* vkey, unsigned int* flag, hipStream_t s) {
+    hipError_t e = hipMemcpyToSymbolAsync(HIP_SYMBOL(cq::c_plan), P, sizeof *P, 0, hipMemcpyHostToDevice, s);
+    if (e != hipSuccess || !n) return e;
+    hipLaunchKernelGGL(cq::vla_pair_prep_kernel, dim3(grid_of(n, 256)), dim3(256), 0, s, pairs, n, *M, *V, L, R, grouped,
+                       kw0, kw1, kcl, vkey, flag);
+    return hipGetLastError();
+}
 hipError_t cq_launch_vla_prep(const cq::Cell* cells, uint32_t n, uint32_t nc, int gslot, uint32_t vslot,
                               unsigned long long* kw0, unsigned long long* kw1, unsigned long long* kcl,
                               unsigned long long* vkey, unsigned int* flag, hipStream_t s) {

@@ -211,6 +211,14 @@ QUERIES = [
     f"SELECT COUNT(*) FROM {SU} AS u JOIN {SO} AS o ON u.id = o.customer_id JOIN {SU} AS v ON o.customer_id = v.id",
     f"SELECT v.role, COUNT(*), AVG(v.age) FROM {SU} AS u JOIN {SO} AS o ON u.id = o.customer_id JOIN {SU} AS v ON o.customer_id = v.id GROUP BY v.role",
     f"SELECT COUNT(*) FROM {U} AS u FULL JOIN {O} AS o ON u.id = o.customer_id JOIN {U} AS w ON o.id = w.id",
+    # STDDEV / MEDIAN over joins and with composite / expression keys
+    f"SELECT u.role, STDDEV(o.price), MEDIAN(o.price) FROM {SU} AS u JOIN {SO} AS o ON u.id = o.customer_id GROUP BY u.role",
+    f"SELECT STDDEV(o.price), MEDIAN(o.quantity), COUNT(*) FROM {U} AS u JOIN {O} AS o ON u.id = o.customer_id",
+    f"SELECT u.role, MEDIAN(o.price), STDDEV(u.age) FROM {SU} AS u LEFT JOIN {SO} AS o ON u.id = o.customer_id WHERE u.age > 30 GROUP BY u.role",
+    f"SELECT p.category, STDDEV(o.price), MEDIAN(p.id) FROM {U} AS u JOIN {O} AS o ON u.id = o.customer_id JOIN {P} AS p ON o.id = p.id GROUP BY p.category",
+    f"SELECT gender, role, STDDEV(height), MEDIAN(age) FROM {R} GROUP BY gender, role",
+    f"SELECT age / 10 AS decade, MEDIAN(height), STDDEV(height), COUNT(*) FROM {R} WHERE gender = 'm' GROUP BY decade",
+    f"SELECT role, active, MEDIAN(age) FROM {T} GROUP BY role, active",
     # row-returning (build_result)
     f"SELECT name, age FROM {T} WHERE age > 30",
     f"SELECT * FROM {T} WHERE age > 30",

@@ -34,6 +34,10 @@ def files(tmp_path_factory):
     f["mix"].write_text("\n".join(lines) + "\n")
     f["role"] = d / "role.csv"
     datagen.write_shape_a(str(f["role"]), 200_000, seed=5, with_role=True)
+    f["users"] = d / "users.csv"
+    f["users"].write_bytes(datagen.users_bytes(4_000, seed=31))
+    f["orders"] = d / "orders.csv"
+    f["orders"].write_bytes(datagen.orders_bytes(15_000, 4_800, seed=32))
     return f
 
 
@@ -62,9 +66,32 @@ QUERIES = [
     "SELECT s, STDDEV(x) FROM '{M}' WHERE g = 'gnull' GROUP BY s",
     "SELECT role, STDDEV(height), MEDIAN(age) FROM '{R}' WHERE age > 30 GROUP BY role",
     "SELECT MEDIAN(height), STDDEV(age) FROM '{R}'",
+    # composite and expression keys (cells path, compute_vla_pairs over identity pairs)
+    "SELECT gender, role, STDDEV(height), MEDIAN(age) FROM '{R}' WHERE age > 50 GROUP BY gender, role",
+    "SELECT g, y, MEDIAN(x), STDDEV(x) FROM '{M}' GROUP BY g, y",
+    "SELECT age / 7 AS b, MEDIAN(height), COUNT(*) FROM '{R}' GROUP BY b",
+    # MIN/MAX over a column mixing classes beside STDDEV / MEDIAN
+    "SELECT g, MIN(x), MEDIAN(x), STDDEV(x) FROM '{M}' GROUP BY g",
+    # joins (pairs of parsed cells)
+    "SELECT u.role, STDDEV(o.price), MEDIAN(o.quantity), COUNT(*) FROM '{U}' AS u JOIN '{O}' AS o ON u.id = o.customer_id GROUP BY u.role",
+    "SELECT MEDIAN(o.price), STDDEV(u.age) FROM '{U}' AS u JOIN '{O}' AS o ON u.id = o.customer_id WHERE o.quantity > 3",
+    "SELECT u.age, MEDIAN(o.price), STDDEV(o.price) FROM '{U}' AS u LEFT JOIN '{O}' AS o ON u.id = o.customer_id GROUP BY u.age",
+    "SELECT o.quantity, u.role, MEDIAN(u.age) FROM '{U}' AS u JOIN '{O}' AS o ON u.id = o.customer_id GROUP BY o.quantity, u.role",
 ]
 
 
 @pytest.mark.parametrize("tmpl", QUERIES)
 def test_stddev_median(files, tmpl):
-    _check(tmpl.replace("{M}", str(files["mix"])).replace("{R}", str(files["role"])))
+    _check(tmpl.replace("{M}", str(files["mix"])).replace("{R}", str(files["role"]))
+           .replace("{U}", str(files["users"])).replace("{O}", str(files["orders"])))
+
+
+def test_stddev_across_partials_refused(files):
+    """every value of a group is needed: partial merges refuse the plan loudly"""
+    sql = f"SELECT role, MEDIAN(age) FROM '{files['role']}' GROUP BY role"
+    with cqtest.Parsed(sql) as ast:
+        t = cq_amd.Table.open_range(str(files["role"]), 0, 2)
+        with pytest.raises(RuntimeError):
+            cq_amd.query_partial(ast, [t])
+        t.close()
+    assert "STDDEV/MEDIAN" in cq_amd.last_ineligible()
