@@ -98,6 +98,10 @@ hipError_t cq_launch_join_project(const uint2* pairs, unsigned long long np, con
 hipError_t cq_launch_join_finish(const cq::GroupOut* out, const unsigned int* count, unsigned int cap_out,
                                  const uint2* pairs, const cq::JoinMap* M, const cq::Cell* L, const cq::Cell* R,
                                  int nacc, uint32_t sb, cq::Cell* cells, uint8_t* bytes, hipStream_t s);
+size_t cq_join_sum_lds(int nacc);
+hipError_t cq_launch_join_sum(const uint2* pairs, unsigned long long np, const cq::JoinMap* M, const cq::Cell* L,
+                              const cq::Cell* R, const cq::ScanPlan* P, const cq::GroupTable* gt,
+                              cq::ScanStats* stats, int ncu, hipStream_t s);
 hipError_t cq_launch_vla_pair_prep(const uint2* pairs, uint32_t n, const cq::JoinMap* M, const cq::JoinMap* V,
                                    const cq::Cell* L, const cq::Cell* R, const cq::ScanPlan* P, int grouped,
                                    unsigned long long* kw0, unsigned long long* kw1, unsigned long long* kcl,
@@ -2260,8 +2264,13 @@ std::vector<HGroup> aggregate_pairs(DevCtx& c, Compiled& C, const JoinMap& MA, c
         Scratch fin(c, (size_t)cap_out * ncell * (sizeof(Cell) + SB) + 64);
         Cell* dcells = (Cell*)fin.p;
         uint8_t* dbytes = fin.p + (size_t)cap_out * ncell * sizeof(Cell);
+        bool sums_only = grouped && !getenv("CQ_AMD_NO_JOIN_PREAGG");
+        for (int a = 0; a < C.P.nacc; a++) sums_only = sums_only && C.P.acc[a].kind == ACC_SUM;
         HIPCHECK(hipEventRecord(c.ev0, c.stream));
-        HIPCHECK(cq_launch_join_agg(pairs, np, &MA, Lc, Rc, &C.P, &Ar.gt, Ar.stats, grouped, c.stream));
+        if (sums_only)   // COUNT / SUM / AVG by group: block-local LDS pre-aggregation
+            HIPCHECK(cq_launch_join_sum(pairs, np, &MA, Lc, Rc, &C.P, &Ar.gt, Ar.stats, c.ncu, c.stream));
+        else
+            HIPCHECK(cq_launch_join_agg(pairs, np, &MA, Lc, Rc, &C.P, &Ar.gt, Ar.stats, grouped, c.stream));
         HIPCHECK(hipEventRecord(c.ev1, c.stream));
         HIPCHECK(cq_launch_compact(&Ar.gt, &C.P, Ar.out, Ar.out_count, cap_out, c.stream));
         HIPCHECK(cq_launch_join_finish(Ar.out, Ar.out_count, cap_out, pairs, &MR, Lc, Rc, C.P.nacc, SB, dcells, dbytes,

@@ -1775,6 +1775,146 @@ __global__ __launch_bounds__(256) void join_agg_kernel(const uint2* __restrict__
     }
 }
 
+// join_agg_kernel for grouped COUNT / SUM / AVG plans with a block-local LDS
+// pre-aggregation: each pair's group is found (or claimed) in the block's LDS
+// table of JS_SLOTS keys (linear probing, the key words stored beside the tag,
+// a wave-uniform claim loop so a lane never spins on a slot its own wave has yet
+// to publish), COUNT / SUM / numeric count / first pair go to LDS atomics, and the
+// block's groups are flushed into the HBM table once at the end: one HBM insert
+// and a few atomics per (block, group) instead of per pair.  Pairs whose group
+// finds no slot within JS_PROBES probes take join_agg_kernel's HBM path.
+constexpr uint32_t JS_SLOTS = 1024, JS_PROBES = 64;
+__global__ __launch_bounds__(512) void join_sum_kernel(const uint2* __restrict__ pairs, unsigned long long np,
+                                                       JoinMap M, const Cell* __restrict__ L,
+                                                       const Cell* __restrict__ R, ScanStats* __restrict__ stats) {
+    const ScanPlan& P = c_plan;
+    const GroupTable& gt = c_gt;
+    const int nneed = P.nneed, nacc = P.nacc;
+    extern __shared__ __align__(16) uint8_t smem[];
+    uint32_t* tag = (uint32_t*)smem;                                  // 0 free, 1 claimed, else lds_hdr
+    v4u* kw = (v4u*)(smem + JS_SLOTS * 4);
+    uint32_t* cnt = (uint32_t*)(smem + JS_SLOTS * 20);
+    unsigned long long* first = (unsigned long long*)(smem + JS_SLOTS * 24);
+    double* sum = (double*)(smem + JS_SLOTS * 32);                    // [nacc][JS_SLOTS]
+    uint32_t* num = (uint32_t*)(smem + JS_SLOTS * (32 + 8 * (uint32_t)nacc));
+    for (uint32_t i = threadIdx.x; i < JS_SLOTS; i += blockDim.x) {
+        tag[i] = 0;
+        cnt[i] = 0;
+        first[i] = ~0ull;
+        for (int a = 0; a < nacc; a++) { sum[a * JS_SLOTS + i] = 0.0; num[a * JS_SLOTS + i] = 0; }
+    }
+    __syncthreads();
+    unsigned long long my_pass = 0;
+    for (unsigned long long b0 = (unsigned long long)blockIdx.x * blockDim.x; b0 < np;
+         b0 += (unsigned long long)gridDim.x * blockDim.x) {
+        const unsigned long long i = b0 + threadIdx.x;
+        const bool valid = i < np;
+        CellsT<MAX_NEED> cs;
+        bool pass = false;
+        if (valid) {
+            join_cells(M, L, R, pairs[i], cs);
+            pass = P.nprog == 0 || eval_where_vm(P, P.consts, cs);
+        } else {
+#pragma unroll
+            for (int k = 0; k < MAX_NEED; k++) cs.c[k] = cell_null();
+        }
+        GKey key;
+        key.cls = GK_ALL; key.len = 0; key.w0 = 0; key.w1 = 0;
+        uint64_t h = 0;
+        if (pass) {
+            my_pass++;
+            bool tab = false;
+            key = plan_group_key(P, P.consts, cs, nneed, tab);
+            if (tab) atomicOr(&stats->key_flags, 1u);
+            h = gk_hash(key);
+        }
+        // the block's slot of the key (wave-uniform loop: claims publish within the trip)
+        const uint32_t hd = lds_hdr(key, h);
+        const v4u mine = key_words(key);
+        uint32_t pos = (uint32_t)h & (JS_SLOTS - 1), probes = 0;
+        int s = -1;
+        bool pending = pass;
+        for (uint32_t trip = 0; __any(pending); trip++) {
+            if (pending) {
+                uint32_t t = __hip_atomic_load(&tag[pos], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
+                if (t == 0) {
+                    const uint32_t old = atomicCAS(&tag[pos], 0u, 1u);
+                    if (old == 0) {
+                        kw[pos] = mine;
+                        __builtin_amdgcn_fence(__ATOMIC_RELEASE, "workgroup");
+                        __hip_atomic_store(&tag[pos], hd, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
+                        s = (int)pos;
+                        pending = false;
+                    }
+                    t = old;
+                }
+                if (pending && t != 1) {                       // a published key: compare
+                    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "workgroup");
+                    if (t == hd && key_match(key, mine, kw[pos])) {
+                        s = (int)pos;
+                        pending = false;
+                    } else if (++probes >= JS_PROBES) {
+                        pending = false;                          // no room: the HBM path
+                    } else {
+                        pos = (pos + 1) & (JS_SLOTS - 1);
+                    }
+                }
+            }
+            if (trip > (1u << 20)) break;                          // never hang (s stays -1)
+        }
+        if (s >= 0) {
+            atomicAdd(&cnt[s], 1u);
+            atomicMin(&first[s], i);
+            for (int a = 0; a < nacc; a++) {
+                const Cell c = get_cell(cs, P.acc[a].slot, nneed);
+                if (is_num(c)) {
+                    atomicAdd(&sum[a * JS_SLOTS + s], num_of(c));
+                    atomicAdd(&num[a * JS_SLOTS + s], 1u);
+                }
+            }
+        } else if (pass) {
+            const int gi = g_insert(gt, key, h, stats);
+            if (gi >= 0) {
+                atomicAdd(&gt.cnt[gi], 1ULL);
+                if (__atomic_load_n(&gt.first[gi], __ATOMIC_RELAXED) > i) atomicMin(&gt.first[gi], i);
+                for (int a = 0; a < nacc; a++) {
+                    const Cell c = get_cell(cs, P.acc[a].slot, nneed);
+                    if (is_num(c)) {
+                        atomicAdd(&gt.sum[a][gi], num_of(c));
+                        atomicAdd(&gt.num[a][gi], 1ULL);
+                    }
+                }
+            }
+        }
+    }
+    for (int o = 32; o > 0; o >>= 1) my_pass += __shfl_down(my_pass, o, 64);
+    if ((threadIdx.x & 63) == 0 && my_pass) atomicAdd(&stats->passed, my_pass);
+    __syncthreads();
+    // flush: one HBM insert and a few atomics per group of this block
+    for (uint32_t i = threadIdx.x; i < JS_SLOTS; i += blockDim.x) {
+        const uint32_t t = tag[i];
+        if (t < 0x80000000u || !cnt[i]) continue;
+        const v4u w = kw[i];
+        GKey k;
+        k.cls = (t >> 16) & 7u;
+        k.len = t & 0xFFFFu;
+        k.w0 = (uint64_t)w.x | ((uint64_t)w.y << 32);
+        k.w1 = (uint64_t)w.z | ((uint64_t)w.w << 32);
+        const int gi = g_insert(gt, k, gk_hash(k), stats);
+        if (gi < 0) continue;
+        atomicAdd(&gt.cnt[gi], (unsigned long long)cnt[i]);
+        const unsigned long long f = first[i];
+        if (__atomic_load_n(&gt.first[gi], __ATOMIC_RELAXED) > f) atomicMin(&gt.first[gi], f);
+        for (int a = 0; a < nacc; a++) {
+            const uint32_t nn = num[a * JS_SLOTS + i];
+            if (nn) {
+                atomicAdd(&gt.sum[a][gi], sum[a * JS_SLOTS + i]);
+                atomicAdd(&gt.num[a][gi], (unsigned long long)nn);
+            }
+        }
+    }
+}
+
 // WHERE over the joined rows of a row-returning query: 1 / 0 per pair
 __global__ void join_filter_kernel(const uint2* __restrict__ pairs, unsigned long long np, JoinMap M,
                                    const Cell* __restrict__ L, const Cell* __restrict__ R,
@@ -2262,6 +2402,18 @@ hipError_t cq_launch_join_agg(const uint2* pairs, unsigned long long np, const c
     if (e != hipSuccess || !np) return e;
     const unsigned grid = (unsigned)std::min<uint64_t>(grid_of(np, 256), 4096);
     hipLaunchKernelGGL(cq::join_agg_kernel, dim3(grid), dim3(256), 0, s, pairs, np, *M, L, R, stats, grouped);
+    return hipGetLastError();
+}
+size_t cq_join_sum_lds(int nacc) { return (size_t)cq::JS_SLOTS * (32 + 12 * (size_t)nacc); }
+hipError_t cq_launch_join_sum(const uint2* pairs, unsigned long long np, const cq::JoinMap* M, const cq::Cell* L,
+                              const cq::Cell* R, const cq::ScanPlan* P, const cq::GroupTable* gt,
+                              cq::ScanStats* stats, int ncu, hipStream_t s) {
+    hipError_t e = hipMemcpyToSymbolAsync(HIP_SYMBOL(cq::c_plan), P, sizeof *P, 0, hipMemcpyHostToDevice, s);
+    if (e == hipSuccess) e = hipMemcpyToSymbolAsync(HIP_SYMBOL(cq::c_gt), gt, sizeof *gt, 0, hipMemcpyHostToDevice, s);
+    if (e != hipSuccess || !np) return e;
+    const size_t lds = cq_join_sum_lds(P->nacc);
+    const unsigned grid = (unsigned)std::min<uint64_t>(grid_of(np, 512), (uint64_t)std::max(ncu, 1) * 2);
+    hipLaunchKernelGGL(cq::join_sum_kernel, dim3(grid), dim3(512), lds, s, pairs, np, *M, L, R, stats);
     return hipGetLastError();
 }
 hipError_t cq_launch_join_filter(const uint2* pairs, unsigned long long np, const cq::JoinMap* M, const cq::Cell* L,
