@@ -1355,6 +1355,13 @@ __global__ void parse_literals_kernel(const uint8_t* __restrict__ text,
 // the records being in file order) are staged into LDS with coalesced 16-byte
 // loads, and each thread then walks its record there; STRING cells are rebased to
 // their HBM bytes.  A span too long for the buffer walks the record in HBM.
+// 0x80 flags of a dword -> 4 bits (bit i = byte i)
+__device__ __forceinline__ uint32_t flag_nib(uint32_t f) {
+    uint32_t t = f >> 7;
+    t |= t >> 7;
+    t |= t >> 14;
+    return t & 0xFu;
+}
 constexpr uint32_t CELLS_T = 256;
 constexpr uint32_t CELLS_SPAN = 16384;
 __global__ __launch_bounds__(CELLS_T) void cells_kernel(const uint8_t* __restrict__ g, uint64_t tn,
@@ -1383,6 +1390,109 @@ __global__ __launch_bounds__(CELLS_T) void cells_kernel(const uint8_t* __restric
     }
     const uint32_t off = (uint32_t)(r - lo);
     const Src S{buf + off, g + r, (uint32_t)span - off, true};
+    // fast path (delimiter above ' ', so blank skipping never meets a delimiter):
+    // the record's first 64 bytes from LDS as separator / terminator / quote masks,
+    // fields found by clearing separator bits, each field typed from its exact bytes
+    // -- short numerals and plain strings in registers, anything else by parse_cell.
+    // A quote before the terminator, no terminator in the view, or a needed field
+    // starting with a blank falls back to the byte walk below.
+    if (D.delim > 0x20u) {
+        const uint32_t* b32 = (const uint32_t*)buf;
+        const uint32_t a = off >> 2, sh = off & 3;
+        const uint32_t rep_d = D.delim * 0x01010101u, rep_q = D.quote * 0x01010101u;
+        uint64_t sv = 0, nv = 0, qv = 0;
+        uint32_t prev = b32[a];
+#pragma unroll
+        for (int jj = 0; jj < 16; jj++) {
+            const uint32_t nx = b32[a + jj + 1];
+            const uint32_t x = __builtin_amdgcn_alignbyte(nx, prev, sh);
+            prev = nx;
+            const uint32_t fn = (~nonzero_bytes(x ^ 0x0A0A0A0Au) | ~nonzero_bytes(x ^ 0x0D0D0D0Du)) & 0x80808080u;
+            const uint32_t fd = ~nonzero_bytes(x ^ rep_d) & 0x80808080u;
+            const uint32_t fq = ~nonzero_bytes(x ^ rep_q) & 0x80808080u;
+            sv |= (uint64_t)flag_nib(fd | fn) << (4 * jj);
+            nv |= (uint64_t)flag_nib(fn) << (4 * jj);
+            qv |= (uint64_t)flag_nib(fq) << (4 * jj);
+        }
+        const uint32_t e = nv ? (uint32_t)__builtin_ctzll(nv) : 64u;
+        bool ok = e < 64 && (qv & ((2ull << e) - 1)) == 0;
+        if (ok) {
+            uint64_t sm = sv;
+            uint32_t start = 0;
+            int col = 0;
+            bool gone = false;
+            for (int k = 0; k < D.ncols && ok; k++) {
+                const int want = D.cols[k];
+                while (!gone && col < want) {
+                    const uint32_t b = (uint32_t)__builtin_ctzll(sm);       // sm holds the terminator bit e
+                    if (b >= e) gone = true;
+                    else { start = b + 1; sm &= sm - 1; col++; }
+                }
+                Cell c = cell_null();
+                if (!gone) {
+                    const uint32_t end = (uint32_t)__builtin_ctzll(sm), fl = end - start;
+                    if (fl) {
+                        uint32_t e0, e1, e2, e3;
+                        load16(buf, off + start, e0, e1, e2, e3);
+                        const uint32_t c0 = e0 & 0xFFu;
+                        if (c0 <= 0x20u) { ok = false; break; }            // leading blank: the byte walk
+                        bool done = false;
+                        if (fl <= 16) {
+                            const uint32_t m0 = len_mask(fl, 0), m1 = len_mask(fl, 1), m2 = len_mask(fl, 2),
+                                           m3 = len_mask(fl, 3);
+                            const uint32_t low = lt_bytes(e0 | ~m0, 0x21212121u) | lt_bytes(e1 | ~m1, 0x21212121u) |
+                                                 lt_bytes(e2 | ~m2, 0x21212121u) | lt_bytes(e3 | ~m3, 0x21212121u);
+                            if (!low) {
+                                const uint32_t f0 = m0 & 0x80808080u, f1 = m1 & 0x80808080u, f2 = m2 & 0x80808080u,
+                                               f3 = m3 & 0x80808080u;
+                                const uint32_t g0 = digit_bytes(e0) & f0, g1 = digit_bytes(e1) & f1,
+                                               g2 = digit_bytes(e2) & f2, g3 = digit_bytes(e3) & f3;
+                                const uint32_t t0 = ~nonzero_bytes(e0 ^ 0x2E2E2E2Eu) & f0,
+                                               t1 = ~nonzero_bytes(e1 ^ 0x2E2E2E2Eu) & f1,
+                                               t2 = ~nonzero_bytes(e2 ^ 0x2E2E2E2Eu) & f2,
+                                               t3 = ~nonzero_bytes(e3 ^ 0x2E2E2E2Eu) & f3;
+                                const uint32_t ndot = __popc(t0) + __popc(t1) + __popc(t2) + __popc(t3);
+                                const bool allnum = (g0 | t0) == f0 && (g1 | t1) == f1 && (g2 | t2) == f2 &&
+                                                    (g3 | t3) == f3;
+                                // digits with at most one dot, not 8-10 bytes (parse_date's lengths),
+                                // at most 15 digits: INTEGER exactly, DOUBLE = RN(M / 10^k)
+                                if (allnum && ndot <= 1 && fl - ndot >= 1 && fl - ndot <= 15 && (fl < 8 || fl > 10)) {
+                                    const uint32_t w[4] = {e0, e1, e2, e3};
+                                    unsigned long long M = 0;
+                                    uint32_t kd = 0;
+                                    bool seen = false;
+#pragma unroll
+                                    for (uint32_t bi = 0; bi < 16; bi++) {
+                                        const uint32_t ch = (w[bi >> 2] >> (8 * (bi & 3))) & 0xFFu;
+                                        if (bi < fl) {
+                                            if (ch == '.') seen = true;
+                                            else { M = M * 10 + (ch - '0'); kd += seen ? 1u : 0u; }
+                                        }
+                                    }
+                                    c = ndot ? cell_dbl((double)M / pow10_exact(kd)) : cell_int((int64_t)M);
+                                    done = true;
+                                } else if (!is_digit(c0) && c0 != '+' && c0 != '-' && c0 != '.') {
+                                    c.kind = K_STR;                             // a plain string (never a date)
+                                    c.len = fl;
+                                    c.bits = (uint64_t)(uintptr_t)(g + r + start);
+                                    done = true;
+                                }
+                            }
+                        }
+                        if (!done) {
+                            c = parse_cell(S.ptr(start, fl), fl);
+                            if (c.kind == K_STR) {
+                                const uint8_t* p = (const uint8_t*)(uintptr_t)c.bits;
+                                if (p >= S.t && p < S.t + S.lim) c.bits = (uint64_t)(uintptr_t)(S.g + (p - S.t));
+                            }
+                        }
+                    }
+                }
+                o[k] = c;
+            }
+            if (ok) return;
+        }
+    }
     uint32_t j = 0, fs = 0, flen = 0;
     int col = 0;
     bool ended = false;
