@@ -33,10 +33,32 @@ __global__ void route_len_kernel(const uint8_t* __restrict__ g, const unsigned l
                                  uint32_t* __restrict__ dest) {
     const uint32_t i = blockIdx.x * blockDim.x + threadIdx.x;
     if (i >= n) return;
-    const uint8_t* p = g + recs[i];
-    uint32_t k = 0;
-    while (p[k] != '\n' && p[k] != '\r') k++;       // the table is padded with '\n' after its end
-    len[i] = k + 1;
+    // the first terminator at or after the start, 16 aligned bytes at a time (the
+    // table is padded with '\n' after its end, and 256-byte aligned)
+    const uint64_t st = recs[i];
+    uint64_t a = st & ~15ull;
+    uint32_t drop = (uint32_t)(st - a);                // bytes before the record in the first chunk
+    uint64_t pos = 0;
+    for (;;) {
+        const uint4 v = *(const uint4*)(g + a);
+        const uint32_t w[4] = {v.x, v.y, v.z, v.w};
+        uint32_t m = 0;
+#pragma unroll
+        for (int q = 0; q < 4; q++) {
+            const uint32_t x = w[q], t1 = x ^ 0x0A0A0A0Au, t2 = x ^ 0x0D0D0D0Du;
+            const uint32_t z = ~((((t1 & 0x7F7F7F7Fu) + 0x7F7F7F7Fu) | t1) & (((t2 & 0x7F7F7F7Fu) + 0x7F7F7F7Fu) | t2))
+                               & 0x80808080u;              // 0x80 in every terminator byte
+            uint32_t nb = z >> 7;
+            nb |= nb >> 7;
+            nb |= nb >> 14;
+            m |= (nb & 0xFu) << (4 * q);
+        }
+        m &= 0xFFFFu << drop;
+        if (m) { pos = a + (uint32_t)__builtin_ctz(m); break; }
+        a += 16;
+        drop = 0;
+    }
+    len[i] = (uint32_t)(pos - st) + 1;
     dest[i] = (uint32_t)(mix64(codes[i] ^ ((uint64_t)cls[i] << 62)) % nranks);
 }
 
@@ -67,8 +89,8 @@ __global__ void gather_len_kernel(const uint32_t* __restrict__ len, const uint32
 }
 
 // one wave per 64 consecutive output records: each lane loads one record's
-// (source, destination, length) coalesced, then the wave copies the records one
-// after another with lane k moving byte k (records are ~30-40 B: one pass each)
+// (source, destination, length) coalesced, then the wave copies them four at a
+// time, 16 lanes per record (records are ~30-40 B: two or three bytes per lane)
 __global__ void route_copy_kernel(const uint8_t* __restrict__ g, const unsigned long long* __restrict__ recs,
                                   const uint32_t* __restrict__ order, const uint32_t* __restrict__ len,
                                   const unsigned long long* __restrict__ off, uint32_t n, uint64_t gid_base,
@@ -85,12 +107,14 @@ __global__ void route_copy_kernel(const uint8_t* __restrict__ g, const unsigned 
         m = len[i];
         gids[j] = gid_base + i;
     }
-    const uint32_t cnt = (uint32_t)((uint64_t)n - j0 < 64 ? (uint64_t)n - j0 : 64);
-    for (uint32_t r = 0; r < cnt; r++) {
-        const unsigned long long s = __shfl(src, (int)r);
-        const unsigned long long d = __shfl(dst, (int)r);
-        const uint32_t mm = (uint32_t)__shfl((int)m, (int)r);
-        for (uint32_t k = lane; k < mm; k += 64) out[d + k] = k + 1 == mm ? (uint8_t)'\n' : g[s + k];
+    // four records at a time, 16 lanes each (lane k of a group moves bytes k, k + 16, ...)
+    const uint32_t grp = lane >> 4, sub = lane & 15;
+    for (uint32_t r = 0; r < 64; r += 4) {
+        const int from = (int)(r + grp);
+        const unsigned long long s = __shfl(src, from);
+        const unsigned long long d = __shfl(dst, from);
+        const uint32_t mm = (uint32_t)__shfl((int)m, from);     // 0 past n
+        for (uint32_t k = sub; k < mm; k += 16) out[d + k] = k + 1 == mm ? (uint8_t)'\n' : g[s + k];
     }
 }
 
