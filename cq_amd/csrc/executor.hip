@@ -128,6 +128,10 @@ hipError_t cq_excl_sum_u64(void* temp, size_t* temp_bytes, const unsigned long l
                            size_t n, hipStream_t s);
 hipError_t cq_excl_sum_u32(void* temp, size_t* temp_bytes, const unsigned int* in, unsigned int* out, size_t n,
                            hipStream_t s);
+size_t cq_pack_result_bytes(unsigned int ng, int nacc, uint32_t ncell, uint32_t sb);
+hipError_t cq_launch_pack_result(const cq::GroupOut* out, const unsigned int* count, unsigned int cap_out, int nacc,
+                                 const cq::Cell* cells, const uint8_t* bytes, uint32_t ncell, uint32_t sb,
+                                 uint8_t* dst, hipStream_t s);
 hipError_t cq_launch_finish(const uint8_t* g, uint64_t n, const cq::GroupOut* out, const unsigned int* count,
                             unsigned int cap_out, const cq::FinishDesc* D, cq::Cell* cells, uint8_t* bytes,
                             hipStream_t s);
@@ -1287,16 +1291,21 @@ std::vector<HGroup> make_groups(DevCtx& c, const Compiled& C, uint64_t limit, ui
         std::vector<HCell> hl = fetch_cells(c, longs);
         for (size_t i = 0; i < longs.size(); i++) hcells[long_at[i]] = hl[i];
     }
+    PHASE("hcells");
     // first-appearance order (create_groups appends groups in row order)
+    std::vector<std::pair<unsigned long long, uint32_t>> fo(outs.size());
+    for (size_t i = 0; i < fo.size(); i++) fo[i] = {outs[i].first, (uint32_t)i};
+    std::sort(fo.begin(), fo.end());       // (first, index): ties keep the index order
     std::vector<uint32_t> order(outs.size());
-    for (size_t i = 0; i < order.size(); i++) order[i] = (uint32_t)i;
-    std::sort(order.begin(), order.end(), [&](uint32_t a, uint32_t b) { return outs[a].first < outs[b].first; });
+    for (size_t i = 0; i < fo.size(); i++) order[i] = fo[i].second;
     const size_t nrep = C.rep_cols.size();
+    PHASE("order");
     groups.reserve(order.size());
     for (uint32_t gi : order) {
         const GroupOut& o = outs[gi];
         const HCell* cs = hcells.data() + (size_t)gi * ncell;
-        HGroup h;
+        groups.emplace_back();
+        HGroup& h = groups.back();
         h.kcls = o.clslen >> 16;
         h.klen = o.clslen & 0xffff;
         h.kw0 = o.w0;
@@ -1319,7 +1328,6 @@ std::vector<HGroup> make_groups(DevCtx& c, const Compiled& C, uint64_t limit, ui
         }
         h.reps.resize(nrep);
         for (size_t i = 0; i < rep_ord.size(); i++) h.reps[rep_ord[i]] = cs[i];
-        groups.push_back(std::move(h));
     }
     return groups;
 }
@@ -1368,6 +1376,8 @@ std::vector<HGroup> run_aggregate(DevCtx& c, const cqgpu_table* t, Compiled& C, 
         Scratch fin(c, (size_t)cap_out * ncell * (sizeof(Cell) + SB) + 64);
         Cell* dcells = (Cell*)fin.p;
         uint8_t* dbytes = fin.p + (size_t)cap_out * ncell * sizeof(Cell);
+        DevBuf packed(cq_pack_result_bytes(cap_out, C.P.nacc, ncell, SB) + 64);
+        bool is_packed = false;
         memset(&st, 0, sizeof st);
         unsigned long long last_clk[8] = {0, 0, 0, 0, 0, 0, 0, 0};
         float ms_total = 0;
@@ -1389,7 +1399,10 @@ std::vector<HGroup> run_aggregate(DevCtx& c, const cqgpu_table* t, Compiled& C, 
             if (!chunk) {      // one launch: compact and finish speculatively, one sync for all
                 HIPCHECK(cq_launch_compact(&A.gt, &C.P, A.out, A.out_count, cap_out, c.stream));
                 HIPCHECK(cq_launch_finish(t->g, t->n, A.out, A.out_count, cap_out, &FD, dcells, dbytes, c.stream));
+                HIPCHECK(cq_launch_pack_result(A.out, A.out_count, cap_out, C.P.nacc, dcells, dbytes, ncell, SB,
+                                               packed.as<uint8_t>(), c.stream));
                 finished = true;
+                is_packed = true;
             }
             // the group count and the scan statistics through pinned memory, one sync
             uint8_t* hs = (uint8_t*)pinned(c, sizeof(ScanStats) + 16);
@@ -1443,7 +1456,34 @@ std::vector<HGroup> run_aggregate(DevCtx& c, const cqgpu_table* t, Compiled& C, 
         outs.resize(ng);
         fcells.resize((size_t)ng * ncell);
         fbytes.resize((size_t)ng * ncell * SB);
-        if (ng) {   // through the pinned staging buffer: three async copies, one sync
+        if (ng && is_packed) {   // one copy of the packed result (pack_result_kernel's layout)
+            const size_t rec = 40 + 40 * (size_t)C.P.nacc, b1 = fcells.size() * sizeof(Cell), b2 = fbytes.size();
+            const size_t tot = cq_pack_result_bytes(ng, C.P.nacc, ncell, SB);
+            uint8_t* hp = (uint8_t*)pinned(c, tot);
+            HIPCHECK(hipMemcpyAsync(hp, packed.p, tot, hipMemcpyDeviceToHost, c.stream));
+            HIPCHECK(hipStreamSynchronize(c.stream));
+            memset(outs.data(), 0, ng * sizeof(GroupOut));
+            for (unsigned int i = 0; i < ng; i++) {
+                const uint8_t* r = hp + i * rec;
+                GroupOut& o = outs[i];
+                o.clslen = ((const uint32_t*)r)[0];
+                o.w0 = ((const uint64_t*)r)[1];
+                o.w1 = ((const uint64_t*)r)[2];
+                o.cnt = ((const unsigned long long*)r)[3];
+                o.first = ((const unsigned long long*)r)[4];
+                const uint64_t* q = (const uint64_t*)(r + 40);
+                for (int a = 0; a < C.P.nacc; a++) {
+                    o.sum[a] = as_dbl(q[5 * a]);
+                    o.num[a] = q[5 * a + 1];
+                    o.ext[a].kind = (uint32_t)q[5 * a + 2];
+                    o.ext[a].len = (uint32_t)(q[5 * a + 2] >> 32);
+                    o.ext[a].bits = q[5 * a + 3];
+                    o.extpos[a] = q[5 * a + 4];
+                }
+            }
+            memcpy(fcells.data(), hp + ng * rec, b1);
+            memcpy(fbytes.data(), hp + ng * rec + b1, b2);
+        } else if (ng) {   // through the pinned staging buffer: three async copies, one sync
             const size_t b0 = ng * sizeof(GroupOut), b1 = fcells.size() * sizeof(Cell), b2 = fbytes.size();
             uint8_t* hp = (uint8_t*)pinned(c, b0 + b1 + b2);
             HIPCHECK(hipMemcpyAsync(hp, A.out, b0, hipMemcpyDeviceToHost, c.stream));

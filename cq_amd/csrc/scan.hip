@@ -2430,6 +2430,55 @@ hipError_t cq_launch_project(const uint8_t* g, const unsigned long long* recs, u
     return hipGetLastError();
 }
 
+namespace cq {
+// the aggregate result in one contiguous buffer for a single device-to-host copy:
+// per group its key, COUNT, first row and the plan's accumulators only
+// (40 + 40 * nacc bytes instead of the whole GroupOut), then the finish cells,
+// then their inline string bytes -- sections laid out by the device's group count
+__global__ void pack_result_kernel(const GroupOut* __restrict__ out, const unsigned int* __restrict__ count,
+                                   unsigned int cap_out, int nacc, const Cell* __restrict__ cells,
+                                   const uint8_t* __restrict__ bytes, uint32_t ncell, uint32_t sb,
+                                   uint8_t* __restrict__ dst) {
+    const uint32_t ng = min(*count, cap_out);
+    const uint32_t rec = 40u + 40u * (uint32_t)nacc;
+    const uint32_t i = blockIdx.x * blockDim.x + threadIdx.x;
+    if (i >= ng) return;
+    const GroupOut& o = out[i];
+    uint8_t* r = dst + (size_t)i * rec;
+    ((uint32_t*)r)[0] = o.clslen;
+    ((uint32_t*)r)[1] = 0;
+    ((uint64_t*)r)[1] = o.w0;
+    ((uint64_t*)r)[2] = o.w1;
+    ((unsigned long long*)r)[3] = o.cnt;
+    ((unsigned long long*)r)[4] = o.first;
+    uint64_t* q = (uint64_t*)(r + 40);
+    for (int a = 0; a < nacc; a++) {
+        q[5 * a + 0] = dbl_bits(o.sum[a]);
+        q[5 * a + 1] = o.num[a];
+        q[5 * a + 2] = ((uint64_t)o.ext[a].len << 32) | o.ext[a].kind;
+        q[5 * a + 3] = o.ext[a].bits;
+        q[5 * a + 4] = o.extpos[a];
+    }
+    Cell* dc = (Cell*)(dst + (size_t)ng * rec);
+    for (uint32_t k = 0; k < ncell; k++) dc[(size_t)i * ncell + k] = cells[(size_t)i * ncell + k];
+    uint8_t* db = (uint8_t*)(dc + (size_t)ng * ncell);
+    const uint4* sbs = (const uint4*)(bytes + (size_t)i * ncell * sb);
+    uint4* dbs = (uint4*)(db + (size_t)i * ncell * sb);
+    for (uint32_t k = 0; k < ncell * sb / 16; k++) dbs[k] = sbs[k];
+}
+}  // namespace cq
+
+size_t cq_pack_result_bytes(unsigned int ng, int nacc, uint32_t ncell, uint32_t sb) {
+    return (size_t)ng * (40u + 40u * (uint32_t)nacc + ncell * (uint32_t)sizeof(cq::Cell) + ncell * sb);
+}
+hipError_t cq_launch_pack_result(const cq::GroupOut* out, const unsigned int* count, unsigned int cap_out, int nacc,
+                                 const cq::Cell* cells, const uint8_t* bytes, uint32_t ncell, uint32_t sb,
+                                 uint8_t* dst, hipStream_t s) {
+    if (sb % 16) return hipErrorInvalidValue;
+    hipLaunchKernelGGL(cq::pack_result_kernel, dim3((cap_out + 127) / 128), dim3(128), 0, s, out, count, cap_out, nacc,
+                       cells, bytes, ncell, sb, dst);
+    return hipGetLastError();
+}
 hipError_t cq_launch_finish(const uint8_t* g, uint64_t n, const cq::GroupOut* out, const unsigned int* count,
                             unsigned int cap_out, const cq::FinishDesc* D, cq::Cell* cells, uint8_t* bytes,
                             hipStream_t s) {
