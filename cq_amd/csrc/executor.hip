@@ -165,6 +165,9 @@ hipError_t cq_launch_route_copy(const uint8_t* g, const unsigned long long* recs
 hipError_t cq_launch_pair_gid(const uint2* pairs, const unsigned long long* pidx, uint32_t n,
                               const unsigned long long* lg, const unsigned long long* rg, unsigned long long* out,
                               hipStream_t s);
+hipError_t cq_launch_pair_gid_flagged(const uint2* pairs, unsigned long long np, const unsigned int* flags,
+                                      const unsigned int* pos, const unsigned long long* lg,
+                                      const unsigned long long* rg, unsigned long long* out, hipStream_t s);
 }
 
 // reference evaluator.c:23
@@ -580,6 +583,20 @@ cq_value to_value(const HCell& h) {
         default: v.kind = CQ_V_NULL; break;
     }
     return v;
+}
+
+HCell from_value(const cq_value& v) {              // to_value's inverse (result rows -> blob cells)
+    HCell h;
+    h.kind = (uint32_t)v.kind;
+    switch (v.kind) {
+        case K_INT: h.bits = (uint64_t)v.u.i; break;
+        case K_DBL: h.bits = dbl_bits(v.u.f); break;
+        case K_DATE: h.bits = ((uint64_t)(uint32_t)v.u.date.y << 32) | ((uint64_t)(v.u.date.m & 0xffff) << 16) |
+                              (uint64_t)(v.u.date.d & 0xffff); break;
+        case K_STR: h.s = v.u.s ? v.u.s : ""; break;
+        default: h.kind = K_NULL; break;
+    }
+    return h;
 }
 
 // device cells -> host cells (strings copied back with one kernel)
@@ -2268,6 +2285,11 @@ struct JoinPartial {
     std::vector<HGroup> groups;       // first / extpos: (global left id << 32) | global right id
     uint32_t acc_classes[MAX_ACC] = {};
     uint32_t lmask = 0, rmask = 0;    // bit k: a key of value class k (1 number, 2 string, 3 date)
+    // row-returning joins: the projected rows of the passing pairs, in local pair
+    // order, with their global order keys ((global left id << 32) | global right id)
+    cq_table* rows = nullptr;
+    std::vector<unsigned long long> row_keys;
+    ~JoinPartial() { if (rows) cqgpu_result_free(rows); }
 };
 
 // global record ids of a join side: the routed ids, or the local row index
@@ -2571,7 +2593,6 @@ cq_table* run_join(DevCtx& c, cq_node* q, const cqgpu_table* L, const cqgpu_tabl
     J.cfg = L->cfg;
     J.names = wnames;
     const bool rows = is_row_query(q);
-    if (part && rows) throw Ineligible{"row-returning SELECT across partials"};
     Compiled C;
     RowPlan RP;
     if (rows) compile_rows(&J, q, C, RP);
@@ -2659,13 +2680,25 @@ cq_table* run_join(DevCtx& c, cq_node* q, const cqgpu_table* L, const cqgpu_tabl
         }
         if (npass > (unsigned long long)INT32_MAX) throw Ineligible{"more than 2^31-1 result rows"};
         g_stats.groups = npass;
+        std::vector<unsigned long long> keys;
+        if (part) {   // every passing row with its global order key; the merge sorts, ORDER / LIMIT after
+            DevBuf lown, rown, dk(std::max<unsigned long long>(npass, 1) * 8);
+            const unsigned long long *lg = nullptr, *rg = nullptr;
+            side_gids(c, L, A.n, lown, &lg);
+            side_gids(c, R, B.n, rown, &rg);
+            HIPCHECK(cq_launch_pair_gid_flagged(pairs.as<uint2>(), np, flags.as<unsigned int>(), pos.as<unsigned int>(),
+                                                lg, rg, dk.as<unsigned long long>(), c.stream));
+            keys.resize(npass);
+            if (npass) HIPCHECK(hipMemcpyAsync(keys.data(), dk.p, npass * 8, hipMemcpyDeviceToHost, c.stream));
+            HIPCHECK(hipStreamSynchronize(c.stream));
+        }
         unsigned long long lo = 0, hi = npass;
         cq_node* sel = q->u.q.select;
         cq_node* ob = q->u.q.order_by;
         const bool ordered = ob && ob->kind == CQ_N_ORDER_BY && ob->u.ord.key;
         const bool distinct = sel && sel->u.sel.distinct;
         bool limited = false;
-        if (!ordered && !distinct && (q->u.q.limit >= 0 || q->u.q.offset >= 0)) {
+        if (!part && !ordered && !distinct && (q->u.q.limit >= 0 || q->u.q.offset >= 0)) {
             const unsigned long long off = q->u.q.offset >= 0 ? (unsigned long long)q->u.q.offset : 0;
             const unsigned long long lim = q->u.q.limit >= 0 ? (unsigned long long)q->u.q.limit : npass;
             lo = std::min(off, npass);
@@ -2701,6 +2734,12 @@ cq_table* run_join(DevCtx& c, cq_node* q, const cqgpu_table* L, const cqgpu_tabl
                 HIPCHECK(hipStreamSynchronize(c.stream));
                 append_rows(c, res, b, hcells, nout, m);
             }
+        }
+        if (part) {
+            part->names = RP.names;
+            part->rows = res;
+            part->row_keys.swap(keys);
+            return nullptr;
         }
         post_ops(c, res, q, true, limited);
         return res;
@@ -3644,6 +3683,25 @@ size_t cqgpu_query_partial(cq_node* q, cqgpu_table* const* tables, int ntables, 
             if (ntables < 2 || !tables[1]) throw Ineligible{"join table not given"};
             JoinPartial jp;
             (void)run_join(c, q, t, tables + 1, ntables - 1, &jp);
+            if (jp.rows) {                           // "CQR1": names, then per row its order key and cells
+                Blob b;
+                b.u32(0x31525143u);
+                b.u32((uint32_t)jp.names.size());
+                for (auto& nm : jp.names) b.str(nm);
+                b.u32(jp.lmask);
+                b.u32(jp.rmask);
+                const cq_table* r = jp.rows;
+                b.u64((uint64_t)r->nrows);
+                for (int i = 0; i < r->nrows; i++) {
+                    b.u64(jp.row_keys[i]);
+                    for (int k = 0; k < r->ncols; k++) b.cell(from_value(r->rows[i].values[k]));
+                }
+                void* out = malloc(std::max<size_t>(b.d.size(), 1));
+                if (!out) throw HipError{"out of host memory"};
+                memcpy(out, b.d.data(), b.d.size());
+                *blob_out = out;
+                return b.d.size();
+            }
             Compiled C;
             cqgpu_table J;
             J.names = jp.names;
@@ -3736,6 +3794,48 @@ cq_table* cqgpu_merge_partials(cq_node* q, const void* const* blobs, const size_
         };
         std::vector<Part> parts(nblobs);
         uint32_t nacc = 0, nrep = 0, magic0 = 0, lmask = 0, rmask = 0;
+        if (sizes[0] >= 4 && *(const uint32_t*)blobs[0] == 0x31525143u) {
+            // "CQR1": a row-returning join's rows from every rank, merged in the
+            // reference's nested-loop order by their global (left id, right id) keys
+            std::vector<std::string> names;
+            struct Row { unsigned long long key; std::vector<HCell> cells; };
+            std::vector<Row> all;
+            for (int bi = 0; bi < nblobs; bi++) {
+                Reader r{(const uint8_t*)blobs[bi], sizes[bi], 0};
+                if (r.u32() != 0x31525143u) throw HipError{"partials from different plans"};
+                std::vector<std::string> nm(r.u32());
+                for (auto& x : nm) x = r.str();
+                if (bi == 0) names = nm;
+                else if (nm != names) throw HipError{"partials from different plans"};
+                lmask |= r.u32();
+                rmask |= r.u32();
+                const uint64_t nr = r.u64();
+                for (uint64_t i = 0; i < nr; i++) {
+                    Row row;
+                    row.key = r.u64();
+                    row.cells.resize(names.size());
+                    for (auto& cc : row.cells) cc = r.cell();
+                    all.push_back(std::move(row));
+                }
+            }
+            for (int x = 1; x < 4; x++)           // value_compare's cross-class "equal" (csv_reader.c:128)
+                for (int y = 1; y < 4; y++)
+                    if (x != y && (lmask >> x & 1) && (rmask >> y & 1))
+                        throw Ineligible{"join keys of different value classes across partials"};
+            if (all.size() > (size_t)INT32_MAX) throw Ineligible{"more than 2^31-1 result rows"};
+            std::stable_sort(all.begin(), all.end(), [](const Row& a, const Row& b) { return a.key < b.key; });
+            cq_table* res = new_result(names);
+            res->nrows = res->row_capacity = (int)all.size();
+            res->rows = (cq_row*)calloc(std::max<size_t>(all.size(), 1), sizeof(cq_row));
+            for (size_t i = 0; i < all.size(); i++) {
+                res->rows[i].ncols = (int)names.size();
+                res->rows[i].values = (cq_value*)calloc(std::max<size_t>(names.size(), 1), sizeof(cq_value));
+                for (size_t k = 0; k < names.size(); k++) res->rows[i].values[k] = to_value(all[i].cells[k]);
+            }
+            post_ops(c, res, q, true, false);
+            g_stats.path = 1;
+            return res;
+        }
         for (int bi = 0; bi < nblobs; bi++) {
             Reader r{(const uint8_t*)blobs[bi], sizes[bi], 0};
             const uint32_t magic = r.u32();

@@ -674,7 +674,6 @@ __global__ __launch_bounds__(LT) void lean_kernel(const uint8_t* __restrict__ g,
     const uint32_t wtt = __builtin_amdgcn_readfirstlane(LP.wtt);
     const double wl = WM == LW_NUM ? LP.wl : 0.0;
     const uint64_t wstr = WM == LW_STR ? LP.wstr : 0ull;
-    const uint64_t tile_g = (uint64_t)(uintptr_t)W.bytes;
     const uint64_t wstep = (uint64_t)gridDim.x * NWV;
 
     // per-lane single-group partials and per-wave statistics
@@ -682,7 +681,9 @@ __global__ __launch_bounds__(LT) void lean_kernel(const uint8_t* __restrict__ g,
     unsigned long long my_first = ~0ULL;
     double my_sum[MAXS] = {0.0, 0.0};
     uint32_t my_num[MAXS] = {0u, 0u};
-    unsigned long long n_rec = 0, n_pass = 0, n_spill = 0;
+    // record / passing counts per lane (vector registers: the scalar file is full)
+    uint32_t v_rec = 0, v_pass = 0;
+    unsigned long long n_rec = 0, n_spill = 0;
 
 #ifdef LEAN_CLK
     uint64_t clk_[8] = {0, 0, 0, 0, 0, 0, 0, 0};
@@ -916,7 +917,7 @@ __global__ __launch_bounds__(LT) void lean_kernel(const uint8_t* __restrict__ g,
                             if (!type_field(W.bytes, rec[u].wfp, rec[u].wfl, c)) {
                                 rec[u].fail = true;
                             } else {
-                                if (c.kind == K_STR) c.bits = tile_g + rec[u].wfp;
+                                if (c.kind == K_STR) c.bits = (uint64_t)(uintptr_t)(W.bytes + rec[u].wfp);
                                 outcome[u] = tt_result(wtt, compare(c, LP.wconst));
                             }
                         }
@@ -1012,9 +1013,9 @@ __global__ __launch_bounds__(LT) void lean_kernel(const uint8_t* __restrict__ g,
                 }
                 const bool ok = Rr.valid & !Rr.fail;
                 pass_[u] = pass_[u] & ok;
-                n_rec += (unsigned long long)__popcll(__ballot(ok));
-                n_pass += (unsigned long long)__popcll(__ballot(pass_[u]));
-                if (row_out) {
+                v_rec += ok ? 1u : 0u;
+                v_pass += pass_[u] ? 1u : 0u;
+                if (!GROUPED && row_out) {                 // (grouped launches never emit rows)
                     const unsigned long long slot = wave_slot(pass_[u], &stats->rows_emitted);
                     if (pass_[u] && slot < row_cap) row_out[slot] = off;
                 }
@@ -1106,6 +1107,12 @@ __global__ __launch_bounds__(LT) void lean_kernel(const uint8_t* __restrict__ g,
 #endif
 
     // ---- statistics
+    unsigned long long n_pass = v_pass;
+    n_rec = (lane == 0 ? n_rec : 0ull) + v_rec;     // (profiling builds count uniformly in n_rec)
+    for (int o = 32; o > 0; o >>= 1) {
+        n_rec += __shfl_down(n_rec, o, 64);
+        n_pass += __shfl_down(n_pass, o, 64);
+    }
     if (lane == 0) {
         if (n_rec) atomicAdd(&stats->records, n_rec);
         if (n_pass) atomicAdd(&stats->passed, n_pass);
@@ -1449,6 +1456,7 @@ hipError_t cq_launch_lean(const uint8_t* g, const cq::ScanPlan* P, const cq::Gro
         hipError_t e = hipMemcpyAsync(tabs_dev, tabs, sizeof tabs, hipMemcpyHostToDevice, s);
         if (e != hipSuccess) return e;
     }
+    if (grouped && row_out) return hipErrorInvalidValue;   // the grouped kernels emit no rows
     const lean_fn_t fn = !grouped ? pick_fn<false, false>(wm, ns) : (k16 ? pick_fn<true, true>(wm, ns)
                                                                          : pick_fn<true, false>(wm, ns));
     (void)hipFuncSetAttribute((const void*)fn, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds);

@@ -135,6 +135,20 @@ __global__ void pair_gid_kernel(const uint2* __restrict__ pairs, const unsigned 
     out[i] = (l << 32) | r;
 }
 
+// the same for the pairs passing a row-returning WHERE (flags), written at their
+// output positions (pos: exclusive scan of flags)
+__global__ void pair_gid_flagged_kernel(const uint2* __restrict__ pairs, unsigned long long np,
+                                        const unsigned int* __restrict__ flags, const unsigned int* __restrict__ pos,
+                                        const unsigned long long* __restrict__ lg,
+                                        const unsigned long long* __restrict__ rg, unsigned long long* __restrict__ out) {
+    const unsigned long long i = (unsigned long long)blockIdx.x * blockDim.x + threadIdx.x;
+    if (i >= np || !flags[i]) return;
+    const uint2 pr = pairs[i];
+    const unsigned long long l = pr.x == PAIR_NONE ? 0xFFFFFFFFull : lg[pr.x];
+    const unsigned long long r = pr.y == PAIR_NONE ? 0ull : rg[pr.y];
+    out[pos[i]] = (l << 32) | r;
+}
+
 // ---- record starts of a whole table (csv_load's line split, reference
 // csv_reader.c:403-427: a record is a maximal non-empty run of bytes other than
 // '\n' / '\r'; the header record ends at data_begin).  Two bandwidth passes over
@@ -252,6 +266,13 @@ hipError_t cq_launch_rs_write(const uint8_t* g, uint64_t lo, uint64_t n, const u
     return hipGetLastError();
 }
 
+hipError_t cq_launch_pair_gid_flagged(const uint2* pairs, unsigned long long np, const unsigned int* flags,
+                                      const unsigned int* pos, const unsigned long long* lg,
+                                      const unsigned long long* rg, unsigned long long* out, hipStream_t s) {
+    if (!np) return hipSuccess;
+    pair_gid_flagged_kernel<<<(unsigned)((np + 255) / 256), 256, 0, s>>>(pairs, np, flags, pos, lg, rg, out);
+    return hipGetLastError();
+}
 hipError_t cq_launch_pair_gid(const uint2* pairs, const unsigned long long* pidx, uint32_t n,
                               const unsigned long long* lg, const unsigned long long* rg, unsigned long long* out,
                               hipStream_t s) {

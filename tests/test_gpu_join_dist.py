@@ -128,6 +128,18 @@ QUERIES = [
     ("du", "do", "SELECT u.age, COUNT(*), SUM(o.price) FROM '{L}' AS u FULL JOIN '{R}' AS o "
                  "ON u.id = o.customer_id GROUP BY u.age"),
     ("sa", "sb", "SELECT b.k, COUNT(*), SUM(a.v) FROM '{L}' AS a FULL JOIN '{R}' AS b ON a.k = b.k GROUP BY b.k"),
+    # row-returning joins (build_result over the joined table): every rank's rows with
+    # their global (left id, right id) keys, merged in nested-loop order, then the
+    # host's ORDER BY / DISTINCT / LIMIT
+    ("du", "do", "SELECT u.name, o.price, o.quantity FROM '{L}' AS u JOIN '{R}' AS o "
+                 "ON u.id = o.customer_id WHERE o.quantity > 3"),
+    ("du", "do", "SELECT u.role, o.id FROM '{L}' AS u LEFT JOIN '{R}' AS o ON u.id = o.customer_id"),
+    ("sa", "sb", "SELECT a.k, b.w FROM '{L}' AS a FULL JOIN '{R}' AS b ON a.k = b.k"),
+    ("du", "do", "SELECT o.id, u.name, o.price FROM '{L}' AS u JOIN '{R}' AS o ON u.id = o.customer_id "
+                 "ORDER BY o.id DESC LIMIT 20"),
+    ("du", "do", "SELECT o.id, u.age FROM '{L}' AS u JOIN '{R}' AS o ON u.id = o.customer_id LIMIT 15 OFFSET 5"),
+    ("du", "do", "SELECT DISTINCT u.role FROM '{L}' AS u JOIN '{R}' AS o ON u.id = o.customer_id"),
+    ("sa", "sb", "SELECT * FROM '{L}' AS a JOIN '{R}' AS b ON a.k = b.k WHERE b.w < 100"),
 ]
 
 
