@@ -134,6 +134,13 @@ class DensePartial:
             self.p = None
 
 
+def _sync(device):
+    """order torch's stream (collectives, copies) before the library's own stream"""
+    d = torch.device(device)
+    if d.type == "cuda":
+        torch.cuda.synchronize(d)
+
+
 def dense_merge(part, device, comm_device=None):
     """The collective part of the device-side merge: one
     all_gather of the key records (sizes first), the dictionary and dense arrays
@@ -156,6 +163,7 @@ def dense_merge(part, device, comm_device=None):
     dist.all_gather(outs, buf)
     all_keys = torch.cat([o[: c * kb] for o, c in zip(outs, counts)]).to(device)
     nall, off = sum(counts), sum(counts[:rank])
+    _sync(device)          # the library's stream reads what torch's stream wrote
     g = part.dict(all_keys, nall, off)
     dsum = torch.empty(max(g * part.W, 1), dtype=torch.float64, device=device)
     dfirst = torch.empty(max(g, 1), dtype=torch.int64, device=device)
@@ -164,6 +172,7 @@ def dense_merge(part, device, comm_device=None):
     f = dfirst.to(comm)
     dist.all_reduce(f, op=dist.ReduceOp.MIN)
     dfirst.copy_(f)
+    _sync(device)
     part.mask_reps(dfirst, drep)
     s, r = dsum.to(comm), drep.to(comm)
     dist.reduce(s, 0, op=dist.ReduceOp.SUM)
@@ -172,6 +181,7 @@ def dense_merge(part, device, comm_device=None):
         return None
     dsum.copy_(s)
     drep.copy_(r)
+    _sync(device)
     return part.finish(dsum, dfirst, drep)
 
 

@@ -133,6 +133,7 @@ def _dense_merge_by_hand(ast, tabs):
         keys = [p.keys("cuda") for p in parts]
         counts = [p.m for p in parts]
         all_keys = torch.cat(keys) if sum(counts) else torch.empty(1, dtype=torch.uint8, device="cuda")
+        torch.cuda.synchronize()
         dense = []
         for r, p in enumerate(parts):
             g = p.dict(all_keys, sum(counts), sum(counts[:r]))
@@ -143,11 +144,14 @@ def _dense_merge_by_hand(ast, tabs):
             dense.append((g, ds, df, dr))
         assert len({g for g, _, _, _ in dense}) == 1            # one dictionary on every rank
         fmin = torch.stack([d[2] for d in dense]).min(0).values
-        for p, d in zip(parts, dense):
+        for d in dense:
             d[2].copy_(fmin)
+        torch.cuda.synchronize()
+        for p, d in zip(parts, dense):
             p.mask_reps(d[2], d[3])
         ssum = torch.stack([d[1] for d in dense]).sum(0)
         rsum = torch.stack([d[3] for d in dense]).sum(0)
+        torch.cuda.synchronize()
         return parts[0].finish(ssum, fmin, rsum)
     finally:
         for p in parts:
