@@ -59,6 +59,7 @@ def _run(ast, ldata: bytes, rdata: bytes, nranks: int):
             rb = torch.cat([sb[bo[d]:bo[d + 1]] for sb, _, bo, _ in sends])
             rg = torch.cat([sg[ro[d]:ro[d + 1]] for _, sg, _, ro in sends])
             keep += [rb, rg]
+            torch.cuda.synchronize()          # torch's copies before the library's stream reads them
             routed[d][side] = cq_amd.table_from_routed(rb.data_ptr(), rb.numel(), rg.data_ptr(), rg.numel(), hdr)
     blobs = [cq_amd.query_partial(ast, routed[d]) for d in range(nranks)]
     tp = cq_amd.merge_partials(ast, blobs)
