@@ -393,8 +393,9 @@ def end_to_end(data, config, L, cq_amd, exp, rows):
         t = times[1]
         return {"seconds": t, "rows_per_s": rows / t, "file_bytes": len(data),
                 "GB_per_s": len(data) / t / 1e9, "verified": ok,
-                "includes": "evaluate_query on a page-cached file (%s): mmap, 64 MiB pinned H2D chunks, "
-                            "scan, result; table cache cleared before each call; median of 3" % d}
+                "includes": "evaluate_query on a page-cached file (%s): mmap, 32 MiB pinned chunks filled by up "
+                            "to 8 host threads while earlier chunks copy to the device, scan, result; table "
+                            "cache cleared before each call; median of 3" % d}
     finally:
         os.unlink(path)
 
