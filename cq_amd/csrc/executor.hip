@@ -122,7 +122,7 @@ hipError_t cq_launch_vla_starts(const unsigned int* head, const unsigned int* si
 hipError_t cq_launch_vla_reduce(const unsigned long long* vkey, const unsigned long long* kw0,
                                 const unsigned long long* kw1, const unsigned long long* kcl, const unsigned int* perm,
                                 const unsigned int* start, uint32_t nseg, uint32_t m, int kind, unsigned long long* out,
-                                hipStream_t s);
+                                double* aux, hipStream_t s);
 hipError_t cq_sort_codes(void* temp, size_t* temp_bytes, const unsigned long long* kin, unsigned long long* kout,
                          const unsigned int* vin, unsigned int* vout, size_t n, hipStream_t s);
 hipError_t cq_excl_sum_u64(void* temp, size_t* temp_bytes, const unsigned long long* in, unsigned long long* out,
@@ -1108,6 +1108,9 @@ struct HGroup {
     std::vector<HCell> reps;            // representative cells (first row)
     double vla[MAX_ACC] = {};           // STDDEV / MEDIAN results
     bool vla_ok[MAX_ACC] = {};          // false: no numeric value (NULL)
+    // across partials, STDDEV's state: sum, squared deviations from the partial's
+    // mean and the numeric count (merged exactly by the parallel-variance rule)
+    double vsum[MAX_ACC] = {}, vm2[MAX_ACC] = {}, vn[MAX_ACC] = {};
 };
 
 // little-endian byte writer / reader of the partial-aggregation blobs
@@ -2052,7 +2055,8 @@ struct VlaRows {                         // one row per candidate: key words, va
 };
 // sort + segment + reduce one value-list aggregate (index vi, kind 0 STDDEV / 1 MEDIAN)
 void vla_finish(DevCtx& c, const VlaAt& at, bool grouped, std::vector<HGroup>& groups, size_t vi, int kind,
-                VlaRows& V, uint32_t n) {
+                VlaRows& V, uint32_t n, bool partial = false) {
+    if (partial && kind != 0) throw Ineligible{"MEDIAN across partials (needs every value)"};
     if (!n) return;
     const size_t N = n;
     DevBuf pos(N * 4), perm(N * 4), perm2(N * 4), keys(N * 8), keys2(N * 8), head(N * 4), sid(N * 4), start(N * 4),
@@ -2100,16 +2104,27 @@ void vla_finish(DevCtx& c, const VlaAt& at, bool grouped, std::vector<HGroup>& g
     HIPCHECK(hipStreamSynchronize(c.stream));
     const uint32_t nseg = last[0] + last[1];
     HIPCHECK(cq_launch_vla_starts(head.as<unsigned int>(), sid.as<unsigned int>(), m, start.as<unsigned int>(), c.stream));
+    DevBuf aux(partial ? (size_t)nseg * 16 : 16);
     HIPCHECK(cq_launch_vla_reduce(V.vkey.as<unsigned long long>(), V.kw0.as<unsigned long long>(),
                                   V.kw1.as<unsigned long long>(), V.kcl.as<unsigned long long>(), perm.as<unsigned int>(),
-                                  start.as<unsigned int>(), nseg, m, kind, out.as<unsigned long long>(), c.stream));
+                                  start.as<unsigned int>(), nseg, m, partial ? 2 : kind, out.as<unsigned long long>(),
+                                  aux.as<double>(), c.stream));
     std::vector<unsigned long long> h((size_t)nseg * 4);
+    std::vector<double> ha(partial ? (size_t)nseg * 2 : 0);
     HIPCHECK(hipMemcpyAsync(h.data(), out.p, h.size() * 8, hipMemcpyDeviceToHost, c.stream));
+    if (partial) HIPCHECK(hipMemcpyAsync(ha.data(), aux.p, ha.size() * 8, hipMemcpyDeviceToHost, c.stream));
     HIPCHECK(hipStreamSynchronize(c.stream));
     for (uint32_t sg = 0; sg < nseg; sg++) {
         auto it = at.find(std::make_tuple((uint64_t)h[4 * sg], (uint64_t)h[4 * sg + 1], (uint64_t)h[4 * sg + 2]));
         if (it == at.end()) continue;
         HGroup& g = groups[it->second];
+        if (partial) {
+            g.vsum[vi] = as_dbl(h[4 * sg + 3]);
+            g.vm2[vi] = ha[2 * sg];
+            g.vn[vi] = ha[2 * sg + 1];
+            g.vla_ok[vi] = true;
+            continue;
+        }
         g.vla[vi] = as_dbl(h[4 * sg + 3]);
         g.vla_ok[vi] = true;
     }
@@ -2117,7 +2132,8 @@ void vla_finish(DevCtx& c, const VlaAt& at, bool grouped, std::vector<HGroup>& g
 
 // single table, single-column (or no) GROUP BY: the WHERE-passing records' key and
 // value cells from their byte offsets
-void compute_vla(DevCtx& c, const cqgpu_table* t, const Compiled& C, std::vector<HGroup>& groups) {
+void compute_vla(DevCtx& c, const cqgpu_table* t, const Compiled& C, std::vector<HGroup>& groups,
+                 bool partial = false) {
     if (C.vla.empty() || groups.empty()) return;
     const cqgpu_stats saved = g_stats;
     Compiled W = C;                          // the WHERE alone, matching records out
@@ -2157,7 +2173,7 @@ void compute_vla(DevCtx& c, const cqgpu_table* t, const Compiled& C, std::vector
                                     (uint32_t)slot(C.vla[vi].second), V.kw0.as<unsigned long long>(),
                                     V.kw1.as<unsigned long long>(), V.kcl.as<unsigned long long>(),
                                     V.vkey.as<unsigned long long>(), V.flag.as<unsigned int>(), c.stream));
-        vla_finish(c, at, C.grouped, groups, vi, C.vla[vi].first, V, n);
+        vla_finish(c, at, C.grouped, groups, vi, C.vla[vi].first, V, n, partial);
     }
 }
 
@@ -2165,7 +2181,7 @@ void compute_vla(DevCtx& c, const cqgpu_table* t, const Compiled& C, std::vector
 // pairs): MA the plan's need slots, VM[vi] the value column of C.vla[vi]
 void compute_vla_pairs(DevCtx& c, const Compiled& C, const JoinMap& MA, const std::vector<JoinMap>& VM,
                        const uint2* pairs, unsigned long long np, const Cell* Lc, const Cell* Rc,
-                       std::vector<HGroup>& groups) {
+                       std::vector<HGroup>& groups, bool partial = false) {
     if (C.vla.empty() || groups.empty()) return;
     if (np >= (1ull << 31)) throw Ineligible{"STDDEV/MEDIAN over more than 2^31 rows"};
     const uint32_t n = (uint32_t)np;
@@ -2176,7 +2192,7 @@ void compute_vla_pairs(DevCtx& c, const Compiled& C, const JoinMap& MA, const st
                                          V.kw0.as<unsigned long long>(), V.kw1.as<unsigned long long>(),
                                          V.kcl.as<unsigned long long>(), V.vkey.as<unsigned long long>(),
                                          V.flag.as<unsigned int>(), c.stream));
-        vla_finish(c, at, C.grouped, groups, vi, C.vla[vi].first, V, n);
+        vla_finish(c, at, C.grouped, groups, vi, C.vla[vi].first, V, n, partial);
     }
 }
 
@@ -2622,7 +2638,9 @@ cq_table* run_join(DevCtx& c, cq_node* q, const cqgpu_table* L, const cqgpu_tabl
     RowPlan RP;
     if (rows) compile_rows(&J, q, C, RP);
     else compile_aggregate(&J, q, C);
-    if (!C.vla.empty() && part) throw Ineligible{"STDDEV/MEDIAN across partials (needs every value)"};
+    if (part)
+        for (auto& v : C.vla)
+            if (v.first != 0) throw Ineligible{"MEDIAN across partials (needs every value)"};
     // columns each level needs, from the last level back
     {
         std::set<int> cur(C.need_cols.begin(), C.need_cols.end());
@@ -2779,7 +2797,8 @@ cq_table* run_join(DevCtx& c, cq_node* q, const cqgpu_table* L, const cqgpu_tabl
         if (!C.vla.empty()) {
             std::vector<JoinMap> VM;
             for (auto& v : C.vla) VM.push_back(join_map(std::vector<int>{v.second}, nl, A, B));
-            compute_vla_pairs(c, C, MA, VM, pairs.as<uint2>(), np, A.cells.as<Cell>(), B.cells.as<Cell>(), groups);
+            compute_vla_pairs(c, C, MA, VM, pairs.as<uint2>(), np, A.cells.as<Cell>(), B.cells.as<Cell>(), groups,
+                              part != nullptr);
         }
         if (part) {
             for (int a = 0; a < C.P.nacc; a++) part->acc_classes[a] = st.acc_classes[a];
@@ -2831,7 +2850,7 @@ cq_table* run_join(DevCtx& c, cq_node* q, const cqgpu_table* L, const cqgpu_tabl
 // aggregation with one "pair" (row, -) per record.  Groups come back in
 // first-appearance order with whole-file byte offsets, like run_aggregate's.
 std::vector<HGroup> run_cells_aggregate(DevCtx& c, const cqgpu_table* t, Compiled& C, Literals& Lit,
-                                        ScanStats* st_out = nullptr) {
+                                        ScanStats* st_out = nullptr, bool partial = false) {
     parse_literals(c, C.lits, Lit);
     for (size_t i = 0; i < Lit.cells.size(); i++) C.P.consts[i] = Lit.cells[i];
     std::vector<HGroup> groups;
@@ -2855,7 +2874,7 @@ std::vector<HGroup> run_cells_aggregate(DevCtx& c, const cqgpu_table* t, Compile
     if (!C.vla.empty()) {
         std::vector<JoinMap> VM;
         for (auto& v : C.vla) VM.push_back(join_map(std::vector<int>{v.second}, nl, A, B));
-        compute_vla_pairs(c, C, MA, VM, pairs.as<uint2>(), np, A.cells.as<Cell>(), bcells.as<Cell>(), groups);
+        compute_vla_pairs(c, C, MA, VM, pairs.as<uint2>(), np, A.cells.as<Cell>(), bcells.as<Cell>(), groups, partial);
     }
     if (st_out) *st_out = st;
     g_stats.records = np;
@@ -3739,6 +3758,7 @@ size_t cqgpu_query_partial(cq_node* q, cqgpu_table* const* tables, int ntables, 
             for (int a = 0; a < C.P.nacc; a++) b.u32(jp.acc_classes[a]);
             const uint32_t nrep = (uint32_t)C.rep_cols.size();
             b.u32(nrep);
+            b.u32((uint32_t)C.vla.size());
             b.u32(jp.lmask);
             b.u32(jp.rmask);
             b.u64(jp.groups.size());
@@ -3749,6 +3769,7 @@ size_t cqgpu_query_partial(cq_node* q, cqgpu_table* const* tables, int ntables, 
                     b.f64(h.sum[a]); b.u64(h.num[a]); b.u64(h.extpos[a]); b.cell(h.ext[a]);
                 }
                 for (uint32_t r = 0; r < nrep; r++) b.cell(r < h.reps.size() ? h.reps[r] : HCell());
+                for (size_t v = 0; v < C.vla.size(); v++) { b.f64(h.vsum[v]); b.f64(h.vm2[v]); b.f64(h.vn[v]); }
             }
             void* out = malloc(std::max<size_t>(b.d.size(), 1));
             if (!out) throw HipError{"out of host memory"};
@@ -3760,18 +3781,20 @@ size_t cqgpu_query_partial(cq_node* q, cqgpu_table* const* tables, int ntables, 
         if (is_row_query(q)) throw Ineligible{"row-returning SELECT across partials"};
         Compiled C;
         compile_aggregate(t, q, C);
-        if (!C.vla.empty()) throw Ineligible{"STDDEV/MEDIAN across partials (needs every value)"};
+        for (auto& v : C.vla)
+            if (v.first != 0) throw Ineligible{"MEDIAN across partials (needs every value)"};
         Literals L;
         ScanStats st;
         memset(&st, 0, sizeof st);
         std::vector<HGroup> groups;
         if (C.P.ngpart > 0) {
-            groups = run_cells_aggregate(c, t, C, L, &st);
+            groups = run_cells_aggregate(c, t, C, L, &st, true);
         } else {
             try {
                 groups = run_aggregate(c, t, C, L, &st);
+                compute_vla(c, t, C, groups, true);
             } catch (MixedExtremes&) {
-                groups = run_cells_aggregate(c, t, C, L, &st);
+                groups = run_cells_aggregate(c, t, C, L, &st, true);
             }
         }
         Blob b;
@@ -3782,6 +3805,7 @@ size_t cqgpu_query_partial(cq_node* q, cqgpu_table* const* tables, int ntables, 
         for (int a = 0; a < C.P.nacc; a++) b.u32(st.acc_classes[a]);
         const uint32_t nrep = (uint32_t)C.rep_cols.size();
         b.u32(nrep);
+        b.u32((uint32_t)C.vla.size());
         b.u64(groups.size());
         for (const HGroup& h : groups) {
             b.u32(h.kcls); b.u32(h.klen); b.u64(h.kw0); b.u64(h.kw1); b.str(h.kbytes);
@@ -3790,6 +3814,7 @@ size_t cqgpu_query_partial(cq_node* q, cqgpu_table* const* tables, int ntables, 
                 b.f64(h.sum[a]); b.u64(h.num[a]); b.u64(h.extpos[a]); b.cell(h.ext[a]);
             }
             for (uint32_t r = 0; r < nrep; r++) b.cell(r < h.reps.size() ? h.reps[r] : HCell());
+            for (size_t v = 0; v < C.vla.size(); v++) { b.f64(h.vsum[v]); b.f64(h.vm2[v]); b.f64(h.vn[v]); }
         }
         void* out = malloc(std::max<size_t>(b.d.size(), 1));
         if (!out) throw HipError{"out of host memory"};
@@ -3818,7 +3843,7 @@ cq_table* cqgpu_merge_partials(cq_node* q, const void* const* blobs, const size_
             std::vector<HGroup> groups;
         };
         std::vector<Part> parts(nblobs);
-        uint32_t nacc = 0, nrep = 0, magic0 = 0, lmask = 0, rmask = 0;
+        uint32_t nacc = 0, nrep = 0, nvla = 0, magic0 = 0, lmask = 0, rmask = 0;
         if (sizes[0] >= 4 && *(const uint32_t*)blobs[0] == 0x31525143u) {
             // "CQR1": a row-returning join's rows from every rank, merged in the
             // reference's nested-loop order by their global (left id, right id) keys
@@ -3873,10 +3898,12 @@ cq_table* cqgpu_merge_partials(cq_node* q, const void* const* blobs, const size_
             const uint32_t na = r.u32();
             for (uint32_t a = 0; a < na; a++) pt.classes.push_back(r.u32());
             const uint32_t nr = r.u32();
+            const uint32_t nv = r.u32();
             if (magic == 0x314a5143u) { lmask |= r.u32(); rmask |= r.u32(); }
-            if (bi == 0) { nacc = na; nrep = nr; }
-            else if (pt.names != parts[0].names || na != nacc || nr != nrep)
+            if (bi == 0) { nacc = na; nrep = nr; nvla = nv; }
+            else if (pt.names != parts[0].names || na != nacc || nr != nrep || nv != nvla)
                 throw HipError{"partials from different plans"};
+            if (nv > (uint32_t)MAX_ACC) throw HipError{"bad partial blob"};
             const uint64_t ng = r.u64();
             for (uint64_t gi = 0; gi < ng; gi++) {
                 HGroup h;
@@ -3886,6 +3913,7 @@ cq_table* cqgpu_merge_partials(cq_node* q, const void* const* blobs, const size_
                     h.sum[a] = r.f64(); h.num[a] = r.u64(); h.extpos[a] = r.u64(); h.ext[a] = r.cell();
                 }
                 for (uint32_t k = 0; k < nrep; k++) h.reps.push_back(r.cell());
+                for (uint32_t v = 0; v < nvla; v++) { h.vsum[v] = r.f64(); h.vm2[v] = r.f64(); h.vn[v] = r.f64(); }
                 pt.groups.push_back(std::move(h));
             }
         }
@@ -3942,10 +3970,25 @@ cq_table* cqgpu_merge_partials(cq_node* q, const void* const* blobs, const size_
                     }
                     if (better) { m.ext[a] = h.ext[a]; m.extpos[a] = h.extpos[a]; }
                 }
+                for (uint32_t v = 0; v < nvla; v++) {   // parallel variance: counts, sums, squared deviations
+                    if (h.vn[v] == 0) continue;
+                    if (m.vn[v] == 0) { m.vsum[v] = h.vsum[v]; m.vm2[v] = h.vm2[v]; m.vn[v] = h.vn[v]; continue; }
+                    const double na = m.vn[v], nb = h.vn[v], n = na + nb;
+                    const double d = h.vsum[v] / nb - m.vsum[v] / na;
+                    m.vm2[v] += h.vm2[v] + d * d * (na * nb / n);
+                    m.vsum[v] += h.vsum[v];
+                    m.vn[v] = n;
+                }
             }
         }
         // one group without GROUP BY, present even with no rows
         if (!C.grouped && merged.size() > 1) throw HipError{"partials disagree on the single group"};
+        if (C.vla.size() != nvla) throw HipError{"partials do not match the plan"};
+        for (HGroup& h : merged)           // population STDDEV of the merged state
+            for (uint32_t v = 0; v < nvla; v++) {
+                h.vla_ok[v] = h.vn[v] > 0;
+                h.vla[v] = h.vn[v] > 0 ? sqrt(h.vm2[v] / h.vn[v]) : 0.0;
+            }
         std::stable_sort(merged.begin(), merged.end(),
                          [](const HGroup& x, const HGroup& y) { return x.first < y.first; });
         Literals L;

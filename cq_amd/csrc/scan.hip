@@ -2196,13 +2196,26 @@ __device__ __forceinline__ double vla_value(unsigned long long k) {
 __global__ void vla_reduce_kernel(const unsigned long long* __restrict__ vkey, const unsigned long long* __restrict__ kw0,
                                   const unsigned long long* __restrict__ kw1, const unsigned long long* __restrict__ kcl,
                                   const unsigned int* __restrict__ perm, const unsigned int* __restrict__ start,
-                                  uint32_t nseg, uint32_t m, int kind, unsigned long long* __restrict__ out) {
+                                  uint32_t nseg, uint32_t m, int kind, unsigned long long* __restrict__ out,
+                                  double* __restrict__ aux) {
     const uint32_t s = blockIdx.x * blockDim.x + threadIdx.x;
     if (s >= nseg) return;
     const uint32_t a = start[s], b = s + 1 < nseg ? start[s + 1] : m;
     const uint32_t n = b - a;
     double r;
-    if (kind == 0) {
+    if (kind == 2) {          // a partial's STDDEV state: sum (out), squared deviations and count (aux)
+        double sum = 0;
+        for (uint32_t i = a; i < b; i++) sum += vla_value(vkey[perm[i]]);
+        const double mean = sum / n;
+        double vs = 0;
+        for (uint32_t i = a; i < b; i++) {
+            const double d = vla_value(vkey[perm[i]]) - mean;
+            vs += d * d;
+        }
+        r = sum;
+        aux[2 * (uint64_t)s] = vs;
+        aux[2 * (uint64_t)s + 1] = (double)n;
+    } else if (kind == 0) {
         double sum = 0;
         for (uint32_t i = a; i < b; i++) sum += vla_value(vkey[perm[i]]);
         const double mean = sum / n;
@@ -2646,10 +2659,10 @@ hipError_t cq_launch_vla_starts(const unsigned int* head, const unsigned int* si
 hipError_t cq_launch_vla_reduce(const unsigned long long* vkey, const unsigned long long* kw0,
                                 const unsigned long long* kw1, const unsigned long long* kcl, const unsigned int* perm,
                                 const unsigned int* start, uint32_t nseg, uint32_t m, int kind, unsigned long long* out,
-                                hipStream_t s) {
+                                double* aux, hipStream_t s) {
     if (!nseg) return hipSuccess;
     hipLaunchKernelGGL(cq::vla_reduce_kernel, dim3(grid_of(nseg, 64)), dim3(64), 0, s, vkey, kw0, kw1, kcl, perm, start,
-                       nseg, m, kind, out);
+                       nseg, m, kind, out, aux);
     return hipGetLastError();
 }
 

@@ -141,6 +141,9 @@ QUERIES = [
     ("du", "do", "SELECT o.id, u.age FROM '{L}' AS u JOIN '{R}' AS o ON u.id = o.customer_id LIMIT 15 OFFSET 5"),
     ("du", "do", "SELECT DISTINCT u.role FROM '{L}' AS u JOIN '{R}' AS o ON u.id = o.customer_id"),
     ("sa", "sb", "SELECT * FROM '{L}' AS a JOIN '{R}' AS b ON a.k = b.k WHERE b.w < 100"),
+    # STDDEV across partials: per-rank (sum, squared deviations, count), merged exactly
+    ("du", "do", "SELECT u.role, STDDEV(o.price), COUNT(*) FROM '{L}' AS u JOIN '{R}' AS o "
+                 "ON u.id = o.customer_id GROUP BY u.role"),
 ]
 
 

@@ -11,7 +11,7 @@ import pytest
 
 import cqtest
 import cq_amd
-from cq_amd import datagen
+from cq_amd import abi, datagen
 
 pytestmark = pytest.mark.gpu
 REL = 1e-6
@@ -86,12 +86,50 @@ def test_stddev_median(files, tmpl):
            .replace("{U}", str(files["users"])).replace("{O}", str(files["orders"])))
 
 
-def test_stddev_across_partials_refused(files):
-    """every value of a group is needed: partial merges refuse the plan loudly"""
+def test_median_across_partials_refused(files):
+    """MEDIAN needs every value of a group: partial merges refuse it loudly"""
     sql = f"SELECT role, MEDIAN(age) FROM '{files['role']}' GROUP BY role"
     with cqtest.Parsed(sql) as ast:
         t = cq_amd.Table.open_range(str(files["role"]), 0, 2)
         with pytest.raises(RuntimeError):
             cq_amd.query_partial(ast, [t])
         t.close()
-    assert "STDDEV/MEDIAN" in cq_amd.last_ineligible()
+    assert "MEDIAN across partials" in cq_amd.last_ineligible()
+
+
+PARTIAL_STDDEV = [
+    "SELECT role, STDDEV(height), COUNT(*) FROM '{R}' WHERE age > 30 GROUP BY role",
+    "SELECT STDDEV(age), STDDEV(height), AVG(age) FROM '{R}'",
+    "SELECT g, STDDEV(x), STDDEV_POP(y) FROM '{M}' GROUP BY g",
+    "SELECT gender, role, STDDEV(age) FROM '{R}' GROUP BY gender, role",
+    "SELECT g, MIN(y), MAX(y), STDDEV(x) FROM '{M}' GROUP BY g",
+]
+
+
+@pytest.mark.parametrize("nranks", [1, 3, 8])
+@pytest.mark.parametrize("tmpl", PARTIAL_STDDEV)
+def test_stddev_across_partials(files, tmpl, nranks):
+    """per range: (sum, squared deviations, count) per group, merged by the
+    parallel-variance rule; population STDDEV within 1e-6 of the oracle"""
+    path = str(files["mix"]) if "{M}" in tmpl else str(files["role"])
+    sql = tmpl.replace("{M}", path).replace("{R}", path)
+    want, unsup = cqtest.oracle_query(sql)
+    assert not unsup
+    with cqtest.Parsed(sql) as ast:
+        tabs = [cq_amd.Table.open_range(path, r, nranks) for r in range(nranks)]
+        try:
+            blobs = [cq_amd.query_partial(ast, [t]) for t in tabs]
+        finally:
+            for t in tabs:
+                t.close()
+        tp = cq_amd.merge_partials(ast, blobs)
+        assert tp, cq_amd.last_error()
+        got = abi.table_to_py(tp)
+        cq_amd.result_free(tp)
+    sel = sql.split(" FROM ")[0][len("SELECT "):]
+    tol = {i for i, t in enumerate(x.strip().upper() for x in sel.split(",")) if t.startswith(("STDDEV", "SUM", "AVG"))}
+    assert got["columns"] == want["columns"]
+    assert len(got["rows"]) == len(want["rows"])
+    for i, (g, w) in enumerate(zip(got["rows"], want["rows"])):
+        for j, (x, y) in enumerate(zip(g, w)):
+            assert cqtest.cell_equal(x, y, REL if j in tol else 0.0), f"{sql} @ {nranks}: row {i} col {j}: {x} vs {y}"
