@@ -72,6 +72,7 @@ hipError_t cq_launch_rep_mask(const unsigned long long* mine, const unsigned lon
                               unsigned long long* drep, hipStream_t s);
 hipError_t cq_launch_class_mask(const cq::Cell* cells, uint32_t stride, uint32_t kcol, uint32_t n, unsigned int* mask,
                                 hipStream_t s);
+hipError_t cq_launch_run_bounds(const uint32_t* ssid, uint32_t n, cq::HSlot* slots, hipStream_t s);
 hipError_t cq_launch_hash_build(const unsigned long long* codes, const uint32_t* cls, uint32_t n, const cq::JoinHashW* H,
                                 uint32_t* sid, unsigned long long* overflow, hipStream_t s);
 hipError_t cq_sort_u32(void* temp, size_t* temp_bytes, const unsigned int* kin, unsigned int* kout,
@@ -2485,27 +2486,22 @@ unsigned long long build_pairs(DevCtx& c, JoinSide& A, JoinSide& B, int kl, int 
         int hbits = 6;
         while (hbits < 31 && (1ull << hbits) < 2ull * B.n) hbits++;
         const uint32_t cap = 1u << hbits;
-        DevBuf hstate((size_t)cap * 4), hcode((size_t)cap * 8), hcls((size_t)cap * 4), hcnt((size_t)cap * 4),
-            hstart((size_t)cap * 4), sid((size_t)B.n * 4), ssid((size_t)B.n * 4), sidx((size_t)B.n * 4);
-        HIPCHECK(hipMemsetAsync(hstate.p, 0, (size_t)cap * 4, c.stream));
-        HIPCHECK(hipMemsetAsync(hcnt.p, 0, (size_t)cap * 4, c.stream));
+        DevBuf hslot((size_t)cap * sizeof(HSlot)), sid((size_t)B.n * 4), ssid((size_t)B.n * 4), sidx((size_t)B.n * 4);
+        HIPCHECK(hipMemsetAsync(hslot.p, 0, (size_t)cap * sizeof(HSlot), c.stream));
         JoinHashW HW;
-        HW.state = hstate.as<uint32_t>(); HW.code = hcode.as<unsigned long long>(); HW.cls = hcls.as<uint32_t>();
-        HW.cnt = hcnt.as<uint32_t>(); HW.cap = cap;
+        HW.slot = hslot.as<HSlot>();
+        HW.cap = cap;
         unsigned long long* dovf = (unsigned long long*)((uint8_t*)pc.p + 32);
         HIPCHECK(hipMemsetAsync(dovf, 0, 8, c.stream));
         HIPCHECK(cq_launch_hash_build(rcodes.as<unsigned long long>(), rcls.as<uint32_t>(), B.n, &HW, sid.as<uint32_t>(),
                                       dovf, c.stream));
-        size_t tbs = 0;
-        HIPCHECK(cq_excl_sum_u32(nullptr, &tbs, hcnt.as<unsigned int>(), hstart.as<unsigned int>(), cap, c.stream));
         size_t tbr = 0;
         HIPCHECK(cq_sort_u32(nullptr, &tbr, sid.as<unsigned int>(), ssid.as<unsigned int>(), ridx.as<unsigned int>(),
                              sidx.as<unsigned int>(), B.n, hbits, c.stream));
-        DevBuf temp1(std::max(tbs, tbr));
-        HIPCHECK(cq_excl_sum_u32(temp1.p, &tbs, hcnt.as<unsigned int>(), hstart.as<unsigned int>(), cap, c.stream));
-        tbr = std::max(tbs, tbr);
+        DevBuf temp1(tbr);
         HIPCHECK(cq_sort_u32(temp1.p, &tbr, sid.as<unsigned int>(), ssid.as<unsigned int>(), ridx.as<unsigned int>(),
                              sidx.as<unsigned int>(), B.n, hbits, c.stream));
+        HIPCHECK(cq_launch_run_bounds(ssid.as<uint32_t>(), B.n, hslot.as<HSlot>(), c.stream));
         unsigned int per[4] = {0, 0, 0, 0};
         unsigned long long ovf = 0;
         HIPCHECK(hipMemcpyAsync(per, pc.p, 16, hipMemcpyDeviceToHost, c.stream));
@@ -2516,11 +2512,7 @@ unsigned long long build_pairs(DevCtx& c, JoinSide& A, JoinSide& B, int kl, int 
         memset(&JR, 0, sizeof JR);
         JR.seg[0] = 0;
         for (int k = 0; k < 4; k++) JR.seg[k + 1] = JR.seg[k] + per[k];
-        JR.hstate = hstate.as<uint32_t>();
-        JR.hcode = hcode.as<unsigned long long>();
-        JR.hcls = hcls.as<uint32_t>();
-        JR.hstart = hstart.as<uint32_t>();
-        JR.hcnt = hcnt.as<uint32_t>();
+        JR.hslot = hslot.as<HSlot>();
         JR.hcap = cap;
         JR.sidx = sidx.as<uint32_t>();
         JR.ridx_c = ridx_c.as<uint32_t>();

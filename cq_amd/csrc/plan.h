@@ -115,15 +115,21 @@ struct JoinMap {
     uint32_t lstride, rstride;
 };
 
-// the right side of a join, sorted by key class then by key code (scan.hip
-// join_count_kernel / join_emit_kernel)
+// one slot of a join's hash table of right-side keys: the key (code, value
+// class) and, once the rows are sorted by slot, the slot's run [start, end) in
+// sidx -- one 24-byte record, so a build or a probe touches one line, not five
+struct HSlot {
+    unsigned long long code;
+    uint32_t st;                        // 0 empty, 1 claimed, 2 + class published
+    uint32_t start, end;
+    uint32_t pad;
+};
+static_assert(sizeof(HSlot) == 24, "24-byte hash slots");
+
+// the right side of a join (scan.hip join_count_kernel / join_emit_kernel)
 struct JoinRight {
     // open-addressing hash table of the right side's distinct keys (value class, code)
-    const uint32_t* hstate;             // 0 empty, else published
-    const unsigned long long* hcode;
-    const uint32_t* hcls;
-    const uint32_t* hstart;             // the key's first position in sidx
-    const uint32_t* hcnt;               // its rows
+    const HSlot* hslot;
     uint32_t hcap;                      // slots, a power of two
     const uint32_t* sidx;               // right rows grouped by key slot, row order within a slot
     const uint32_t* ridx_c;             // rows grouped by class, row order within a class
@@ -134,10 +140,7 @@ struct JoinRight {
 
 // the same table while it is built (hash_build_kernel)
 struct JoinHashW {
-    uint32_t* state;
-    unsigned long long* code;
-    uint32_t* cls;
-    uint32_t* cnt;
+    HSlot* slot;
     uint32_t cap;
 };
 

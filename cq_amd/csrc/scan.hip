@@ -1603,24 +1603,23 @@ __global__ void hash_build_kernel(const unsigned long long* __restrict__ codes, 
     for (uint32_t trip = 0; __any(pending); trip++) {
         if (pending) {
             // relaxed agent-scope atomics (coherent at L2, no cache maintenance); the
-            // publisher drains its key stores (vmcnt) before the state store, and a
-            // reader loads the key only after it has seen the published state
-            uint32_t st = __hip_atomic_load(&H.state[i], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+            // publisher drains its code store (vmcnt) before the state store, and a
+            // reader loads the code only after it has seen the published state
+            HSlot& S = H.slot[i];
+            uint32_t st = __hip_atomic_load(&S.st, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
             if (st == 0) {
-                const uint32_t old = atomicCAS(&H.state[i], 0u, 1u);
-                if (old == 0) {                          // claimed: key words first, then publish
-                    __hip_atomic_store(&H.code[i], code, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-                    __hip_atomic_store(&H.cls[i], k, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+                const uint32_t old = atomicCAS(&S.st, 0u, 1u);
+                if (old == 0) {                          // claimed: the code first, then publish
+                    __hip_atomic_store(&S.code, code, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
                     asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-                    __hip_atomic_store(&H.state[i], 2u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+                    __hip_atomic_store(&S.st, 2u + k, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
                     slot = i;
                     pending = false;
                 }
                 st = old;
             }
-            if (pending && st == 2) {
-                if (__hip_atomic_load(&H.code[i], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) == code &&
-                    __hip_atomic_load(&H.cls[i], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) == k) {
+            if (pending && st >= 2) {
+                if (st == 2u + k && __hip_atomic_load(&S.code, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) == code) {
                     slot = i;
                     pending = false;
                 } else {
@@ -1635,10 +1634,16 @@ __global__ void hash_build_kernel(const unsigned long long* __restrict__ codes, 
             break;
         }
     }
-    if (r < n) {
-        atomicAdd(&H.cnt[slot], 1u);
-        sid[r] = slot;
-    }
+    if (r < n) sid[r] = slot;
+}
+
+// each slot's run [start, end) in the rows sorted by slot (ssid: the sorted slots)
+__global__ void run_bounds_kernel(const uint32_t* __restrict__ ssid, uint32_t n, HSlot* __restrict__ slots) {
+    const uint32_t j = blockIdx.x * blockDim.x + threadIdx.x;
+    if (j >= n) return;
+    const uint32_t s = ssid[j];
+    if (j == 0 || ssid[j - 1] != s) slots[s].start = j;
+    if (j + 1 == n || ssid[j + 1] != s) slots[s].end = j + 1;
 }
 
 // [lo, hi) in sidx of the right rows whose key has this class and code
@@ -1648,10 +1653,11 @@ __device__ __forceinline__ void eq_run(const JoinRight& J, uint32_t k, unsigned 
     const uint32_t mask = J.hcap - 1;
     uint32_t i = (uint32_t)hj_hash(code, k) & mask;
     for (uint32_t probe = 0; probe < J.hcap; probe++, i = (i + 1) & mask) {
-        if (J.hstate[i] == 0) return;
-        if (J.hcode[i] == code && J.hcls[i] == k) {
-            lo = J.hstart[i];
-            hi = lo + J.hcnt[i];
+        const HSlot S = J.hslot[i];
+        if (S.st == 0) return;
+        if (S.st == 2u + k && S.code == code) {
+            lo = S.start;
+            hi = S.end;
             return;
         }
     }
@@ -2551,6 +2557,11 @@ hipError_t cq_launch_class_mask(const cq::Cell* cells, uint32_t stride, uint32_t
     if (!n) return hipSuccess;
     const uint32_t grid = std::min<uint32_t>((n + 255) / 256, 4096);
     hipLaunchKernelGGL(cq::class_mask_kernel, dim3(grid), dim3(256), 0, s, cells, stride, kcol, n, mask);
+    return hipGetLastError();
+}
+hipError_t cq_launch_run_bounds(const uint32_t* ssid, uint32_t n, cq::HSlot* slots, hipStream_t s) {
+    if (!n) return hipSuccess;
+    hipLaunchKernelGGL(cq::run_bounds_kernel, dim3((n + 255) / 256), dim3(256), 0, s, ssid, n, slots);
     return hipGetLastError();
 }
 hipError_t cq_launch_hash_build(const unsigned long long* codes, const uint32_t* cls, uint32_t n, const cq::JoinHashW* H,
