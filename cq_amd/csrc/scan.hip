@@ -1900,7 +1900,7 @@ __global__ __launch_bounds__(256) void join_agg_kernel(const uint2* __restrict__
 // and a few atomics per (block, group) instead of per pair.  Pairs whose group
 // finds no slot within JS_PROBES probes take join_agg_kernel's HBM path.
 constexpr uint32_t JS_SLOTS = 1024, JS_PROBES = 64;
-__global__ __launch_bounds__(512) void join_sum_kernel(const uint2* __restrict__ pairs, unsigned long long np,
+__global__ __launch_bounds__(512) __attribute__((amdgpu_waves_per_eu(4))) void join_sum_kernel(const uint2* __restrict__ pairs, unsigned long long np,
                                                        JoinMap M, const Cell* __restrict__ L,
                                                        const Cell* __restrict__ R, ScanStats* __restrict__ stats) {
     const ScanPlan& P = c_plan;
