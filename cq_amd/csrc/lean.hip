@@ -67,8 +67,15 @@
 namespace cq {
 namespace lean {
 
+#ifndef LEAN_REGPF
+#define LEAN_DMA 1      // the next window arrives in LDS by LDS-DMA (no registers held for it)
+#endif
 #ifndef LEAN_WAVES
+#ifdef LEAN_DMA
+#define LEAN_WAVES 16   // 4 waves per SIMD at 128 VGPRs: no register prefetch to spill
+#else
 #define LEAN_WAVES 12   // 3 waves per SIMD: 168 VGPRs, so the prefetched window never spills
+#endif
 #endif
 constexpr int LT = 64 * LEAN_WAVES;       // threads per block
 constexpr int NWV = LT / 64;              // waves per block
@@ -150,11 +157,48 @@ __device__ __forceinline__ GKey raw_key(uint32_t len, uint64_t w0, uint64_t w1) 
 }
 
 struct Win {            // one window in flight
+#ifndef LEAN_DMA
     v4u a[4];           // staged bytes [64l, 64l + 64)
+#endif
     uint32_t prev;      // the dword before the window
 };
 
-__device__ __forceinline__ void load_win(const uint8_t* g, uint64_t w, uint32_t ws, Win& x) {
+// the dword before the window (g has 256 bytes of '\n' before byte 0) by a buffer load: a
+// uniform address would otherwise become a scalar load, whose lgkmcnt the LDS waits of the
+// whole window would have to drain
+__device__ __forceinline__ uint32_t load_prev(const uint8_t* base) {
+    const __amdgpu_buffer_rsrc_t r = __builtin_amdgcn_make_buffer_rsrc((void*)(base - 4), 0, 4, 0x00020000);
+    return __builtin_amdgcn_raw_buffer_load_b32(r, 0, 0, 0);
+}
+
+#ifdef LEAN_DMA
+#if defined(LEAN_DMA_NT) && LEAN_DMA_NT   // cache policy bits of the window loads
+#define LEAN_DMA_CPOL " nt"
+#else
+#define LEAN_DMA_CPOL ""
+#endif
+// the window's 4 KiB straight into the wave's LDS bytes (lds: their wave-uniform LDS
+// address) by four LDS-DMA loads, 1 KiB each, lane l's 16 bytes at 16l.  The caller waits
+// for them with vmcnt(0) before reading the bytes; the lgkmcnt(0) first retires this
+// wave's LDS reads of the window the loads overwrite.  M0 (the LDS base of an LDS-DMA
+// load) is set and restored inside the one statement (the compiler owns M0).
+__device__ __forceinline__ void load_win(const uint8_t* g, uint64_t w, uint32_t ws, uint32_t lds, Win& x) {
+    const uint8_t* base = g + w * ws;                    // 128-byte aligned (g is 256-aligned, ws % 128 == 0)
+    const int lane = threadIdx.x & 63;
+    asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+#pragma unroll
+    for (int i = 0; i < 4; i++) {
+        uint32_t keep;
+        asm volatile("s_mov_b32 %0, m0\n\ts_mov_b32 m0, %2\n\ts_nop 0\n\tglobal_load_lds_dwordx4 %1, off" LEAN_DMA_CPOL
+                     "\n\ts_mov_b32 m0, %0"
+                     : "=&s"(keep)
+                     : "v"(base + 1024 * i + 16 * lane), "s"(lds + 1024u * i)
+                     : "memory");
+    }
+    x.prev = load_prev(base);
+}
+#else
+__device__ __forceinline__ void load_win(const uint8_t* g, uint64_t w, uint32_t ws, uint32_t, Win& x) {
     const uint8_t* base = g + w * ws;                    // 128-byte aligned (g is 256-aligned, ws % 128 == 0)
     const v4u* src = (const v4u*)base;
     const int lane = threadIdx.x & 63;
@@ -168,12 +212,9 @@ __device__ __forceinline__ void load_win(const uint8_t* g, uint64_t w, uint32_t 
 #pragma unroll
     for (int i = 0; i < 4; i++) x.a[i] = LEAN_LD(src + 64 * i + lane);
 #undef LEAN_LD
-    // the dword before the window (g has 256 bytes of '\n' before byte 0) by a buffer load: a
-    // uniform address would otherwise become a scalar load, whose lgkmcnt the LDS
-    // waits of the whole window would have to drain
-    const __amdgpu_buffer_rsrc_t r = __builtin_amdgcn_make_buffer_rsrc((void*)(base - 4), 0, 4, 0x00020000);
-    x.prev = __builtin_amdgcn_raw_buffer_load_b32(r, 0, 0, 0);
+    x.prev = load_prev(base);
 }
+#endif
 
 // separator / terminator bits of 32 bytes (bit i = byte i) and quote flags.
 //
@@ -507,13 +548,11 @@ __device__ __forceinline__ uint32_t key_len(uint64_t w0, uint64_t w1) {
 // a record whose key found no LDS slot (a key longer than the tag, both buckets
 // full): aggregated straight into the HBM raw table; keys over 16 bytes or with
 // low bytes past byte 8 go to the slow list
-__device__ __forceinline__ void spill_record(const uint8_t* bytes, uint32_t gfp, uint32_t kl, uint64_t off,
-                                          const GroupTable* tabs, ScanStats* stats, unsigned long long* slow_list,
-                                          unsigned long long slow_cap, int nacc, const int32_t* acc_sidx, bool n0,
-                                          double v0, bool n1, double v1) {
+__device__ __forceinline__ void spill_record(uint32_t a0, uint32_t a1, uint32_t a2, uint32_t a3, uint32_t kl,
+                                          uint64_t off, const GroupTable* tabs, ScanStats* stats,
+                                          unsigned long long* slow_list, unsigned long long slow_cap, int nacc,
+                                          const int32_t* acc_sidx, bool n0, double v0, bool n1, double v1) {
     const GroupTable& rt = tabs[TAB_RT];
-    uint32_t a0, a1, a2, a3;
-    load16(bytes, gfp, a0, a1, a2, a3);
     const uint32_t m0 = len_mask(kl, 0), m1 = len_mask(kl, 1), m2 = len_mask(kl, 2), m3 = len_mask(kl, 3);
     a0 &= m0; a1 &= m1; a2 &= m2; a3 &= m3;
     const bool fits = kl <= 16 && (low_bytes(a2, m2 & 0x80808080u) | low_bytes(a3, m3 & 0x80808080u)) == 0;
@@ -690,8 +729,11 @@ __global__ __launch_bounds__(LT) void lean_kernel(const uint8_t* __restrict__ g,
     uint64_t clk_last_ = __builtin_amdgcn_s_memtime();
 #endif
     Win nx;
+    // the wave's LDS window bytes as an LDS address (the LDS-DMA base)
+    const uint32_t wlds = __builtin_amdgcn_readfirstlane(
+        (uint32_t)(uintptr_t)(__attribute__((address_space(3))) uint8_t*)W.bytes);
     uint64_t w = LP.first_win + (uint64_t)blockIdx.x * NWV + wv;
-    if (w < last_win) load_win(g, w, wstr_b, nx);
+    if (w < last_win) load_win(g, w, wstr_b, wlds, nx);
 #ifndef LEAN_L2PF
 #define LEAN_L2PF 0
 #endif
@@ -703,13 +745,29 @@ __global__ __launch_bounds__(LT) void lean_kernel(const uint8_t* __restrict__ g,
     uint32_t pf_sink = 0, pf0 = 0, pf1 = 0;
     for (uint32_t round = 0; w < last_win; round++, w += wstep) {
         const uint64_t ws = w * wstr_b;
-#ifdef LEAN_CLK
-        asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+#if defined(LEAN_CLK) || defined(LEAN_DMA)
+        asm volatile("s_waitcnt vmcnt(0)" ::: "memory");   // (LEAN_DMA: the window's bytes are in LDS)
 #endif
         const Win cur = nx;
         LCLK(0);
-#ifndef LEAN_NOMEM   // profiling build LEAN_NOMEM: every window re-processes the first one (no HBM reads)
-        if (w + wstep < last_win) load_win(g, w + wstep, wstr_b, nx);
+#ifdef LEAN_DMA
+        // the next window's DMA goes out once this window's bytes are read for the last
+        // time: after the key loads of the last pass (LEAN_ISSUE), or after the passes
+#ifdef LEAN_NOMEM
+        bool issued = true;
+#else
+        bool issued = false;
+#endif
+#define LEAN_ISSUE()                                                                \
+    do {                                                                            \
+        if (!issued && w + wstep < last_win) load_win(g, w + wstep, wstr_b, wlds, nx); \
+        issued = true;                                                              \
+    } while (0)
+#else
+#define LEAN_ISSUE() do {} while (0)
+#endif
+#if !defined(LEAN_NOMEM) && !defined(LEAN_DMA)   // LEAN_NOMEM: every window re-processes the first one (no HBM reads)
+        if (w + wstep < last_win) load_win(g, w + wstep, wstr_b, wlds, nx);
         if (LEAN_L2PF > 0) {
             const uint64_t wp = w + (uint64_t)LEAN_L2PF * wstep;
             pf_sink ^= pf1;
@@ -719,9 +777,11 @@ __global__ __launch_bounds__(LT) void lean_kernel(const uint8_t* __restrict__ g,
 #endif
 
         // ---- stage and classify
+#ifndef LEAN_DMA
 #pragma unroll
         for (int i = 0; i < 4; i++) ((v4u*)W.bytes)[64 * i + lane] = cur.a[i];
         wave_order();
+#endif
         v4u la[4];                                                    // lane l: window bytes [64l, 64l + 64)
 #pragma unroll
         for (int i = 0; i < 4; i++) la[i] = ((const v4u*)W.bytes)[4 * lane + i];
@@ -766,6 +826,7 @@ __global__ __launch_bounds__(LT) void lean_kernel(const uint8_t* __restrict__ g,
         LCLK(1);
 #if defined(LEAN_PROF) && LEAN_PROF == 1   // profiling build: + classify, bitmaps
         n_rec += (unsigned long long)__popcll(__ballot(((xs0 ^ xs1 ^ xn0 ^ xn1) & 1) != (todo & 1)));
+        LEAN_ISSUE();
         continue;
 #endif
         while (__any(todo != 0)) {
@@ -783,6 +844,7 @@ __global__ __launch_bounds__(LT) void lean_kernel(const uint8_t* __restrict__ g,
                 Rr.fail = !Rr.valid;
                 Rr.lastpos = 0;
             }
+            const bool last_pass = !__any(todo != 0);
             // ---- role fields (WHERE, SUM 0/1, GROUP BY): position and length (0: NULL / missing)
             {
 #pragma unroll
@@ -972,6 +1034,8 @@ __global__ __launch_bounds__(LT) void lean_kernel(const uint8_t* __restrict__ g,
                     if (g8 || !K16) {
                         const uint32_t m0 = len_mask(klen, 0), m1 = len_mask(klen, 1);
                         k0[u] &= m0; k1[u] &= m1;
+                        if (!K16 && __any(klen - 9u < 8u) && klen - 9u < 8u)   // a 9-16 byte key: its spill
+                            load16(W.bytes, rec[u].gfp, k0[u], k1[u], k2[u], k3[u]);   // needs bytes 8-15
                         const uint32_t lowb = low_bytes(k0[u], m0 & 0x80808080u) | low_bytes(k1[u], m1 & 0x80808080u);
                         rec[u].fail |= lowb != 0;
                         longk[u] = klen > 8;
@@ -989,6 +1053,7 @@ __global__ __launch_bounds__(LT) void lean_kernel(const uint8_t* __restrict__ g,
                 }
             }
 
+            if (last_pass) LEAN_ISSUE();                  // (spills take the key from registers)
             LCLK(3);
 #if defined(LEAN_PROF) && LEAN_PROF == 3   // profiling build: + typing, keys and hashes
             n_rec += __popcll(__ballot(pass_[0] ^ pass_[1] ^ ((h[0] ^ h[1] ^ (uint32_t)sval[0][0] ^ (uint32_t)sval[1][0]) & 1)));
@@ -1087,9 +1152,9 @@ __global__ __launch_bounds__(LT) void lean_kernel(const uint8_t* __restrict__ g,
                     if (__any(spill)) {                    // long key or both buckets full: the HBM raw table
                         n_spill += (unsigned long long)__popcll(__ballot(spill));
                         if (spill) {
-                            spill_record(W.bytes, rec[u].gfp, rec[u].klen, ws + rec[u].p, tabs, stats, slow_list,
-                                         slow_cap, LP.nacc, LP.acc_sidx, snum[u][0], sval[u][0], snum[u][MAXS - 1],
-                                         sval[u][MAXS - 1]);
+                            spill_record(k0[u], k1[u], k2[u], k3[u], rec[u].klen, ws + rec[u].p, tabs, stats,
+                                         slow_list, slow_cap, LP.nacc, LP.acc_sidx, snum[u][0], sval[u][0],
+                                         snum[u][MAXS - 1], sval[u][MAXS - 1]);
                         }
                     }
                 }
@@ -1097,8 +1162,10 @@ __global__ __launch_bounds__(LT) void lean_kernel(const uint8_t* __restrict__ g,
             wave_order();
             LCLK(5);
         }
+        LEAN_ISSUE();                                     // (a window without owned records)
         LCLK(6);
     }
+#undef LEAN_ISSUE
     if (LEAN_L2PF > 0 && (pf_sink ^ pf0 ^ pf1) == 0x9E3779B9u && lane == 63 && n_rec == 0x9E3779B9ull)
         stats->clk[7] = 1;       // keeps the prefetch loads (never true in practice)
 #ifdef LEAN_CLK
