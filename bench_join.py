@@ -171,7 +171,9 @@ def main():
     def step():
         ts = time.perf_counter()
         routed = []
-        for side, (tab, hdr) in enumerate(((ut, uh), (ot, oh))):
+        # one rank routes every record to itself in its own order: the shards are the
+        # routed tables (cq_amd.dist.join_partitioned does the same)
+        for side, (tab, hdr) in enumerate(((ut, uh), (ot, oh)) if world > 1 else ()):
             nb, nr = cq_amd.route_plan(ast, [ut, ot], side, world)
             base = exclusive_base(sum(nr), dev) if dist is not None else 0
             sb = torch.empty(max(sum(nb), 1), dtype=torch.uint8, device=dev)
@@ -186,7 +188,7 @@ def main():
             routed.append(cq_amd.table_from_routed(rb.data_ptr(), rb.numel(), rg.data_ptr(), rg.numel(), hdr))
             del sb, sg, rb, rg
         tr = time.perf_counter()
-        blob = cq_amd.query_partial(ast, routed)
+        blob = cq_amd.query_partial(ast, routed if world > 1 else [ut, ot])
         st = cq_amd.stats()
         tj = time.perf_counter()
         blobs = gather_blobs(blob, dev) if dist is not None else [blob]
@@ -277,7 +279,8 @@ def main():
                 "orders_per_gpu": args.orders,
                 "bytes_per_gpu": in_bytes,
                 "joined_pairs": pairs,
-                "parallelism": f"dp{world} (hash repartition all_to_all over RCCL)",
+                "parallelism": (f"dp{world} (hash repartition all_to_all over RCCL)" if world > 1
+                                else "dp1 (one rank: no repartition)"),
             },
             "verified": verified,
             "verified_against": verified_against,

@@ -159,6 +159,7 @@ hipError_t cq_sort_codes(void* temp, size_t* temp_bytes, const unsigned long lon
                          const unsigned int* vin, unsigned int* vout, size_t n, hipStream_t s);
 hipError_t cq_sort_dest(void* temp, size_t* temp_bytes, const unsigned int* kin, unsigned int* kout,
                         const unsigned int* vin, unsigned int* vout, size_t n, int bits, hipStream_t s);
+hipError_t cq_launch_iota_u64(uint32_t n, unsigned long long* out, hipStream_t s);
 hipError_t cq_launch_gather_len(const uint32_t* len, const uint32_t* order, uint32_t n, unsigned long long* out,
                                 hipStream_t s);
 hipError_t cq_launch_route_copy(const uint8_t* g, const unsigned long long* recs, const uint32_t* order,
@@ -2341,12 +2342,9 @@ void side_gids(DevCtx& c, const cqgpu_table* t, uint32_t n, DevBuf& own, const u
         *out = t->gids;
         return;
     }
-    std::vector<unsigned long long> h(std::max<uint32_t>(n, 1));
-    for (uint32_t i = 0; i < n; i++) h[i] = i;
-    DevBuf b(h.size() * 8);
+    DevBuf b((size_t)std::max<uint32_t>(n, 1) * 8);
     std::swap(own.p, b.p);
-    HIPCHECK(hipMemcpyAsync(own.p, h.data(), h.size() * 8, hipMemcpyHostToDevice, c.stream));
-    HIPCHECK(hipStreamSynchronize(c.stream));
+    HIPCHECK(cq_launch_iota_u64(n, own.as<unsigned long long>(), c.stream));
     *out = own.as<unsigned long long>();
 }
 

@@ -237,6 +237,17 @@ hipError_t cq_launch_route_bounds(const uint32_t* dsorted, const unsigned long l
     return hipGetLastError();
 }
 
+// out[i] = i (the record ids of an unrouted join side)
+__global__ void iota_u64_kernel(uint32_t n, unsigned long long* __restrict__ out) {
+    const uint32_t i = blockIdx.x * blockDim.x + threadIdx.x;
+    if (i < n) out[i] = i;
+}
+hipError_t cq_launch_iota_u64(uint32_t n, unsigned long long* out, hipStream_t s) {
+    if (!n) return hipSuccess;
+    iota_u64_kernel<<<blocks(n, 256), 256, 0, s>>>(n, out);
+    return hipGetLastError();
+}
+
 // stable sort of record indices by destination rank
 hipError_t cq_launch_gather_len(const uint32_t* len, const uint32_t* order, uint32_t n, unsigned long long* out,
                                 hipStream_t s) {

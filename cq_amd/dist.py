@@ -219,6 +219,11 @@ def join_partitioned(ast, lshard, rshard, lheader: bytes, rheader: bytes, device
     stages the exchange through host memory for a gloo group (tests)."""
     import cq_amd
     world, rank = dist.get_world_size(), dist.get_rank()
+    if world == 1:
+        # one rank: every record routes to itself in its own order (the stable sort by
+        # destination is the identity), so the shards are already the routed tables
+        # and their record ids the local row indexes
+        return cq_amd.merge_partials(ast, [cq_amd.query_partial(ast, [lshard, rshard])])
     comm = torch.device(comm_device) if comm_device is not None else torch.device(device)
     routed = []
     for side, (tab, header) in enumerate(((lshard, lheader), (rshard, rheader))):

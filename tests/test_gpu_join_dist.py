@@ -233,9 +233,11 @@ def _dist_worker(rank, world, port, lpath, rpath, sql, q):
         dist.destroy_process_group()
 
 
-def test_join_partitioned_two_processes(files):
+@pytest.mark.parametrize("world", [1, 2])
+def test_join_partitioned_processes(files, world):
     """the real driver (route, all_to_all, routed tables, partial, gather, merge)
-    in two processes over gloo, vs the oracle"""
+    in two processes over gloo, vs the oracle; one process takes the no-repartition
+    path (its shards are the routed tables)"""
     import socket
     import torch.multiprocessing as mp
     data, paths = files
@@ -249,10 +251,11 @@ def test_join_partitioned_two_processes(files):
     s.close()
     ctx = mp.get_context("spawn")
     q = ctx.Queue()
-    procs = [ctx.Process(target=_dist_worker, args=(r, 2, port, paths["du"], paths["do"], sql, q)) for r in range(2)]
+    procs = [ctx.Process(target=_dist_worker, args=(r, world, port, paths["du"], paths["do"], sql, q))
+             for r in range(world)]
     for p in procs:
         p.start()
-    res = dict(q.get(timeout=150) for _ in range(2))
+    res = dict(q.get(timeout=150) for _ in range(world))
     for p in procs:
         p.join(timeout=60)
         assert p.exitcode == 0
@@ -260,4 +263,4 @@ def test_join_partitioned_two_processes(files):
     assert isinstance(got, dict), got
     with cqtest.Parsed(sql) as ast:
         tol = tolerant_columns(ast)
-    compare(got, want, tol, sql + " @ 2 processes")
+    compare(got, want, tol, sql + f" @ {world} processes")
