@@ -2470,17 +2470,28 @@ unsigned long long build_pairs(DevCtx& c, JoinSide& A, JoinSide& B, int kl, int 
         const uint32_t lk = (uint32_t)A.slot(kl), rk = (uint32_t)B.slot(kr);
         // right side: codes and classes; rows grouped by class (the cross-class
         // streams); the hash table of distinct keys and the rows sorted by key slot
-        DevBuf rcodes((size_t)B.n * 8), rcls((size_t)B.n * 4), ridx((size_t)B.n * 4), ccls((size_t)B.n * 4),
-            ridx_c((size_t)B.n * 4), pc(64);
+        DevBuf rcodes((size_t)B.n * 8), rcls((size_t)B.n * 4), ridx((size_t)B.n * 4), ridx_c, pc(64);
         HIPCHECK(hipMemsetAsync(pc.p, 0, 64, c.stream));
         HIPCHECK(cq_launch_join_code(B.cells.as<Cell>(), rs, rk, B.n, rcodes.as<unsigned long long>(),
                                      rcls.as<uint32_t>(), ridx.as<uint32_t>(), pc.as<unsigned int>(), c.stream));
-        size_t tb = 0;
-        HIPCHECK(cq_sort_classes(nullptr, &tb, rcls.as<unsigned int>(), ccls.as<unsigned int>(), ridx.as<unsigned int>(),
-                                 ridx_c.as<unsigned int>(), B.n, c.stream));
-        DevBuf temp(tb);
-        HIPCHECK(cq_sort_classes(temp.p, &tb, rcls.as<unsigned int>(), ccls.as<unsigned int>(), ridx.as<unsigned int>(),
-                                 ridx_c.as<unsigned int>(), B.n, c.stream));
+        unsigned int per[4] = {0, 0, 0, 0};
+        HIPCHECK(hipMemcpyAsync(per, pc.p, 16, hipMemcpyDeviceToHost, c.stream));
+        HIPCHECK(hipStreamSynchronize(c.stream));
+        // rows grouped by class, row order within a class: with one class present that
+        // is the identity ridx (join_code's idx), so the class sort runs only for mixes
+        const int nclass = (per[0] != 0) + (per[1] != 0) + (per[2] != 0) + (per[3] != 0);
+        if (nclass > 1) {
+            DevBuf ccls((size_t)B.n * 4), rc((size_t)B.n * 4);
+            size_t tb = 0;
+            HIPCHECK(cq_sort_classes(nullptr, &tb, rcls.as<unsigned int>(), ccls.as<unsigned int>(),
+                                     ridx.as<unsigned int>(), rc.as<unsigned int>(), B.n, c.stream));
+            DevBuf temp(tb);
+            HIPCHECK(cq_sort_classes(temp.p, &tb, rcls.as<unsigned int>(), ccls.as<unsigned int>(),
+                                     ridx.as<unsigned int>(), rc.as<unsigned int>(), B.n, c.stream));
+            HIPCHECK(hipStreamSynchronize(c.stream));   // (temp / ccls freed on scope exit)
+            std::swap(ridx_c.p, rc.p);
+        }
+        const uint32_t* ridx_cp = nclass > 1 ? ridx_c.as<uint32_t>() : ridx.as<uint32_t>();
         int hbits = 6;
         while (hbits < 31 && (1ull << hbits) < 2ull * B.n) hbits++;
         const uint32_t cap = 1u << hbits;
@@ -2500,9 +2511,7 @@ unsigned long long build_pairs(DevCtx& c, JoinSide& A, JoinSide& B, int kl, int 
         HIPCHECK(cq_sort_u32(temp1.p, &tbr, sid.as<unsigned int>(), ssid.as<unsigned int>(), ridx.as<unsigned int>(),
                              sidx.as<unsigned int>(), B.n, hbits, c.stream));
         HIPCHECK(cq_launch_run_bounds(ssid.as<uint32_t>(), B.n, hslot.as<HSlot>(), c.stream));
-        unsigned int per[4] = {0, 0, 0, 0};
         unsigned long long ovf = 0;
-        HIPCHECK(hipMemcpyAsync(per, pc.p, 16, hipMemcpyDeviceToHost, c.stream));
         HIPCHECK(hipMemcpyAsync(&ovf, dovf, 8, hipMemcpyDeviceToHost, c.stream));
         HIPCHECK(hipStreamSynchronize(c.stream));
         if (ovf) throw HipError{"join hash build: table full or insert timeout"};
@@ -2513,7 +2522,7 @@ unsigned long long build_pairs(DevCtx& c, JoinSide& A, JoinSide& B, int kl, int 
         JR.hslot = hslot.as<HSlot>();
         JR.hcap = cap;
         JR.sidx = sidx.as<uint32_t>();
-        JR.ridx_c = ridx_c.as<uint32_t>();
+        JR.ridx_c = ridx_cp;
         JR.cells = B.cells.as<Cell>();
         JR.stride = rs;
         JR.kcol = rk;

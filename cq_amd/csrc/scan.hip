@@ -1540,22 +1540,31 @@ __device__ __forceinline__ uint64_t join_code(const Cell& c) {
 __global__ void join_code_kernel(const Cell* __restrict__ cells, uint32_t stride, uint32_t kcol, uint32_t n,
                                  unsigned long long* __restrict__ codes, uint32_t* __restrict__ cls,
                                  uint32_t* __restrict__ idx, unsigned int* __restrict__ per_class) {
-    // per-class counts: block-local LDS counters, one global atomic per class per block
-    // (a global atomic per row serialises 10^7 rows on four addresses)
-    __shared__ unsigned int cnt[4];
-    if (threadIdx.x < 4) cnt[threadIdx.x] = 0;
-    __syncthreads();
-    const uint32_t i = blockIdx.x * blockDim.x + threadIdx.x;
-    if (i < n) {
+    // per-class counts: per-lane counters over a grid-stride loop, one global atomic per
+    // class per block (one per block of 256 rows put 2.4*10^5 atomics per class of a
+    // 62.5 M-row side on four addresses: 2.8 ms of serialised atomics)
+    uint32_t mine[4] = {0u, 0u, 0u, 0u};
+    for (uint32_t i = blockIdx.x * blockDim.x + threadIdx.x; i < n; i += gridDim.x * blockDim.x) {
         const Cell c = cells[(uint64_t)i * stride + kcol];
         codes[i] = join_code(c);
         const uint32_t k = key_class(c);
         cls[i] = k;
         if (idx) idx[i] = i;
-        if (per_class) atomicAdd(&cnt[k], 1u);
+#pragma unroll
+        for (int j = 0; j < 4; j++) mine[j] += k == (uint32_t)j ? 1u : 0u;
+    }
+    if (!per_class) return;
+    __shared__ unsigned int cnt[4];
+    if (threadIdx.x < 4) cnt[threadIdx.x] = 0;
+    __syncthreads();
+#pragma unroll
+    for (int j = 0; j < 4; j++) {
+        uint32_t v = mine[j];
+        for (int o = 32; o > 0; o >>= 1) v += (uint32_t)__shfl_xor((int)v, o, 64);
+        if ((threadIdx.x & 63) == 0 && v) atomicAdd(&cnt[j], v);
     }
     __syncthreads();
-    if (per_class && threadIdx.x < 4 && cnt[threadIdx.x]) atomicAdd(&per_class[threadIdx.x], cnt[threadIdx.x]);
+    if (threadIdx.x < 4 && cnt[threadIdx.x]) atomicAdd(&per_class[threadIdx.x], cnt[threadIdx.x]);
 }
 
 __global__ void gather_codes_kernel(const unsigned long long* __restrict__ codes, const uint32_t* __restrict__ idx,
@@ -2521,7 +2530,8 @@ hipError_t cq_launch_join_code(const cq::Cell* cells, uint32_t stride, uint32_t 
                                unsigned long long* codes, uint32_t* cls, uint32_t* idx, unsigned int* per_class,
                                hipStream_t s) {
     if (!n) return hipSuccess;
-    hipLaunchKernelGGL(cq::join_code_kernel, dim3(grid_of(n, 256)), dim3(256), 0, s, cells, stride, kcol, n, codes,
+    hipLaunchKernelGGL(cq::join_code_kernel, dim3(std::min(grid_of(n, 256), 8192u)), dim3(256), 0, s, cells, stride,
+                       kcol, n, codes,
                        cls, idx, per_class);
     return hipGetLastError();
 }
