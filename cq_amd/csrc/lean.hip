@@ -647,7 +647,9 @@ __device__ __forceinline__ void walk2(Rec (&rec)[2], const uint64_t (&sv)[2], co
 
 // GROUPED: GROUP BY (else one group); WM: LW_*; NS: distinct SUM arguments (0-2);
 // K16: LDS tags of 16 key bytes (else 8)
-template <bool GROUPED, int WM, int NS, bool K16>
+// CANON: the roles' column order is their canonical order (WHERE, SUM 0, SUM 1, GROUP
+// BY, as present), so the walk's role ranks are compile-time constants (no selects)
+template <bool GROUPED, int WM, int NS, bool K16, bool CANON>
 __global__ __launch_bounds__(LT) void lean_kernel(const uint8_t* __restrict__ g, ScanStats* __restrict__ stats,
                                                   unsigned long long* __restrict__ row_out,
                                                   unsigned long long row_cap,
@@ -691,6 +693,7 @@ __global__ __launch_bounds__(LT) void lean_kernel(const uint8_t* __restrict__ g,
     constexpr int NR = (WM != LW_NONE ? 1 : 0) + NS + (GROUPED ? 1 : 0);   // roles
     uint32_t skip[KN];                     // separators before role rank k's field (walk2)
     uint32_t kw = 0, ks[MAXS] = {0, 0}, kg = 0;   // role ranks of WHERE, SUM 0/1, GROUP BY
+    constexpr uint32_t CKW = 0, CKS0 = WM != LW_NONE ? 1u : 0u, CKS1 = CKS0 + 1, CKG = (uint32_t)NR - 1;
 #pragma unroll
     for (int k = 0; k < KN; k++) {
         const uint32_t c = __builtin_amdgcn_readfirstlane(LP.rcol[k]);
@@ -704,6 +707,7 @@ __global__ __launch_bounds__(LT) void lean_kernel(const uint8_t* __restrict__ g,
             kg = role == R_GROUP ? (uint32_t)k : kg;
         }
     }
+    if (CANON) { kw = CKW; ks[0] = CKS0; ks[1] = CKS1; kg = CKG; }
     const uint32_t rep_d = LP.delim * 0x01010101u, rep_q = LP.quote * 0x01010101u;
     const uint64_t lo_ok = LP.lo_ok, hi_ok = LP.hi_ok, last_win = LP.last_win;
     const uint32_t wstr_b = __builtin_amdgcn_readfirstlane(LP.ws);   // window stride
@@ -1371,19 +1375,23 @@ size_t lean_lds_t(int ns, int grouped) {
 typedef void (*lean_fn_t)(const uint8_t*, ScanStats*, unsigned long long*, unsigned long long, unsigned long long*,
                           unsigned long long, const lean::LeanArgs, const GroupTable*);
 
-template <bool G, int WM, bool K16>
+template <bool G, int WM, bool K16, bool CANON>
 lean_fn_t pick_ns(int ns) {
-    if (ns == 0) return lean::lean_kernel<G, WM, 0, K16>;
-    return ns == 1 ? lean::lean_kernel<G, WM, 1, K16> : lean::lean_kernel<G, WM, 2, K16>;
+    if (ns == 0) return lean::lean_kernel<G, WM, 0, K16, CANON>;
+    return ns == 1 ? lean::lean_kernel<G, WM, 1, K16, CANON> : lean::lean_kernel<G, WM, 2, K16, CANON>;
+}
+template <bool G, bool K16, bool CANON>
+lean_fn_t pick_wm(int wm, int ns) {
+    switch (wm) {
+        case lean::LW_NONE: return pick_ns<G, lean::LW_NONE, K16, CANON>(ns);
+        case lean::LW_NUM: return pick_ns<G, lean::LW_NUM, K16, CANON>(ns);
+        case lean::LW_STR: return pick_ns<G, lean::LW_STR, K16, CANON>(ns);
+        default: return pick_ns<G, lean::LW_GEN, K16, CANON>(ns);
+    }
 }
 template <bool G, bool K16>
-lean_fn_t pick_fn(int wm, int ns) {
-    switch (wm) {
-        case lean::LW_NONE: return pick_ns<G, lean::LW_NONE, K16>(ns);
-        case lean::LW_NUM: return pick_ns<G, lean::LW_NUM, K16>(ns);
-        case lean::LW_STR: return pick_ns<G, lean::LW_STR, K16>(ns);
-        default: return pick_ns<G, lean::LW_GEN, K16>(ns);
-    }
+lean_fn_t pick_fn(int wm, int ns, bool canon) {
+    return canon ? pick_wm<G, K16, true>(wm, ns) : pick_wm<G, K16, false>(wm, ns);
 }
 
 }  // namespace
@@ -1489,6 +1497,7 @@ hipError_t cq_launch_lean(const uint8_t* g, const cq::ScanPlan* P, const cq::Gro
     lp.first_win = P->range_begin / lp.ws;
     lp.last_win = (hi + lp.ws - 1) / lp.ws;
     const int ns = ns_of(lp);
+    bool canon = true;
     {   // the roles in ascending column order (lean_kernel's field walk)
         uint32_t nr = 0;
         auto add = [&](uint32_t col, uint32_t role) {
@@ -1504,6 +1513,12 @@ hipError_t cq_launch_lean(const uint8_t* g, const cq::ScanPlan* P, const cq::Gro
         if (wm != lean::LW_NONE) add(lp.wcol, lean::R_WHERE);
         for (int j = 0; j < ns; j++) add(lp.scol[j], j == 0 ? lean::R_SUM0 : lean::R_SUM1);
         if (grouped) add(lp.gcol, lean::R_GROUP);
+        // canonical: the walk meets the roles in the order they were added
+        uint32_t want[lean::KN], nw = 0;
+        if (wm != lean::LW_NONE) want[nw++] = lean::R_WHERE;
+        for (int j = 0; j < ns; j++) want[nw++] = j == 0 ? lean::R_SUM0 : lean::R_SUM1;
+        if (grouped) want[nw++] = lean::R_GROUP;
+        for (uint32_t i = 0; i < nr; i++) canon = canon && lp.rrole[i] == want[i];
     }
     const bool k16 = grouped && P->lean_k16;
     const size_t lds = k16 ? lean_lds_t<true>(ns, grouped) : lean_lds_t<false>(ns, grouped);
@@ -1524,8 +1539,8 @@ hipError_t cq_launch_lean(const uint8_t* g, const cq::ScanPlan* P, const cq::Gro
         if (e != hipSuccess) return e;
     }
     if (grouped && row_out) return hipErrorInvalidValue;   // the grouped kernels emit no rows
-    const lean_fn_t fn = !grouped ? pick_fn<false, false>(wm, ns) : (k16 ? pick_fn<true, true>(wm, ns)
-                                                                         : pick_fn<true, false>(wm, ns));
+    const lean_fn_t fn = !grouped ? pick_fn<false, false>(wm, ns, canon)
+                                  : (k16 ? pick_fn<true, true>(wm, ns, canon) : pick_fn<true, false>(wm, ns, canon));
     (void)hipFuncSetAttribute((const void*)fn, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds);
     hipLaunchKernelGGL(fn, dim3(grid), dim3(lean::LT), lds, s, g, stats, row_out, row_cap, slow_list, slow_cap,
                        args, (const GroupTable*)tabs_dev);
