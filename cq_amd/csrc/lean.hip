@@ -726,7 +726,8 @@ __global__ __launch_bounds__(LT) void lean_kernel(const uint8_t* __restrict__ g,
     uint32_t my_num[MAXS] = {0u, 0u};
     // record / passing counts per lane (vector registers: the scalar file is full)
     uint32_t v_rec = 0, v_pass = 0;
-    unsigned long long n_rec = 0, n_spill = 0;
+    unsigned long long n_rec = 0;
+    uint32_t v_spill = 0;                  // LDS-table misses of this lane (a vector register too)
 
 #ifdef LEAN_CLK
     uint64_t clk_[8] = {0, 0, 0, 0, 0, 0, 0, 0};
@@ -1154,7 +1155,7 @@ __global__ __launch_bounds__(LT) void lean_kernel(const uint8_t* __restrict__ g,
                 for (int u = 0; u < 2; u++) {
                     const bool spill = pass_[u] && slot[u] < 0;
                     if (__any(spill)) {                    // long key or both buckets full: the HBM raw table
-                        n_spill += (unsigned long long)__popcll(__ballot(spill));
+                        v_spill += spill ? 1u : 0u;
                         if (spill) {
                             spill_record(k0[u], k1[u], k2[u], k3[u], rec[u].klen, ws + rec[u].p, tabs, stats,
                                          slow_list, slow_cap, LP.nacc, LP.acc_sidx, snum[u][0], sval[u][0],
@@ -1178,11 +1179,12 @@ __global__ __launch_bounds__(LT) void lean_kernel(const uint8_t* __restrict__ g,
 #endif
 
     // ---- statistics
-    unsigned long long n_pass = v_pass;
+    unsigned long long n_pass = v_pass, n_spill = v_spill;
     n_rec = (lane == 0 ? n_rec : 0ull) + v_rec;     // (profiling builds count uniformly in n_rec)
     for (int o = 32; o > 0; o >>= 1) {
         n_rec += __shfl_down(n_rec, o, 64);
         n_pass += __shfl_down(n_pass, o, 64);
+        n_spill += __shfl_down(n_spill, o, 64);
     }
     if (lane == 0) {
         if (n_rec) atomicAdd(&stats->records, n_rec);
