@@ -228,32 +228,36 @@ __device__ __forceinline__ void load_win(const uint8_t* g, uint64_t w, uint32_t 
 // The 0x40 flags of two dwords become a byte of bits with one v_dot4_u32_u8
 // each (weights 1..128), four such bytes the 32-bit mask.  Quote presence is
 // the borrow-based zero-byte test (exact for "any").
+// r & ~(r >> 1) & 0x40404040 as one v_bitop3_b32 (truth table 0x20: a & ~b & c) after
+// the shift; the compiler's own form takes a v_not more
 __device__ __forceinline__ uint32_t flags40(uint32_t r) {
-    return r & ~(r >> 1) & 0x40404040u;
+    return __builtin_amdgcn_bitop3_b32(r, r >> 1, 0x40404040u, 0x20);
 }
+// The delimiter and terminator flags are packed separately and the separator mask
+// is their OR per 32 bytes (one op there instead of an AND per dword).
 __device__ __forceinline__ void classify32(const v4u a, const v4u b, uint32_t rep_d, uint32_t rep_q, uint32_t& sep,
                                            uint32_t& nl, uint32_t& q) {
-    uint32_t us[4], un[4];
+    uint32_t ud[4], un[4];
 #pragma unroll
     for (int j = 0; j < 8; j++) {
         const uint32_t x = j < 4 ? a[j & 3] : b[j & 3];
         const uint32_t rn = __builtin_amdgcn_perm(0x00004000u, 0x00400000u, x ^ 0x08080808u);
         const uint32_t rd = __builtin_amdgcn_perm(0u, 0x00000040u, x ^ rep_d);
-        const uint32_t fs = flags40(rn & rd), fn = flags40(rn);
+        const uint32_t fd = flags40(rd), fn = flags40(rn);
         const uint32_t w = (j & 1) ? 0x80402010u : 0x08040201u;
         if (j & 1) {
-            us[j >> 1] = __builtin_amdgcn_udot4(fs, w, us[j >> 1], false);
+            ud[j >> 1] = __builtin_amdgcn_udot4(fd, w, ud[j >> 1], false);
             un[j >> 1] = __builtin_amdgcn_udot4(fn, w, un[j >> 1], false);
         } else {
-            us[j >> 1] = __builtin_amdgcn_udot4(fs, w, 0u, false);
+            ud[j >> 1] = __builtin_amdgcn_udot4(fd, w, 0u, false);
             un[j >> 1] = __builtin_amdgcn_udot4(fn, w, 0u, false);
         }
         const uint32_t t = x ^ rep_q;
         q |= (t - 0x01010101u) & ~t;
     }
-    // us[p] = 0x40 * (bits of bytes 8p .. 8p + 7)
-    sep = (us[0] >> 6) | (us[1] << 2) | (us[2] << 10) | (us[3] << 18);
+    // ud[p] = 0x40 * (bits of bytes 8p .. 8p + 7)
     nl = (un[0] >> 6) | (un[1] << 2) | (un[2] << 10) | (un[3] << 18);
+    sep = nl | (ud[0] >> 6) | (ud[1] << 2) | (ud[2] << 10) | (ud[3] << 18);
 }
 // 0x80 flags -> a nibble (bit i = byte i)
 __device__ __forceinline__ uint32_t nib(uint32_t f) {
