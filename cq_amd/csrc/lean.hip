@@ -600,17 +600,37 @@ struct Rec {
 // one scalar loop, and each field lands in its role's registers by selects on
 // the uniform role ranks (kw: WHERE, ks: SUM 0/1, kg: GROUP BY) -- no branch
 // depends on which role a column plays.
-template <int NR, int WM, int NS, bool GROUPED>
+// DISTINCT (the roles' columns strictly ascending): skip[k] >= 1 for k >= 1, so the
+// first bit role k clears is role k - 1's field end, already known -- a role in the
+// column right after the previous one costs no bit search for its start.
+template <int NR, int WM, int NS, bool GROUPED, bool DISTINCT>
 __device__ __forceinline__ void walk2(Rec (&rec)[2], const uint64_t (&sv)[2], const uint64_t (&nv)[2],
                                       const uint32_t (&skip)[KN], uint32_t kw, const uint32_t (&ks)[MAXS],
                                       uint32_t kg) {
     uint64_t s0 = sv[0], s1 = sv[1];
     const uint32_t e0 = ctz64(nv[0]), e1 = ctz64(nv[1]);
     uint32_t pe0 = 0xFFFFFFFFu, pe1 = 0xFFFFFFFFu;      // start - 1 of the current field
+    uint32_t en0 = 0, en1 = 0;                          // the previous role's field end
 #pragma unroll
     for (int k = 0; k < NR; k++) {
         const uint32_t n = skip[k];
-        if (n > 0) {
+        if (DISTINCT && k > 0) {
+            s0 &= s0 - 1;                               // role k - 1's end
+            s1 &= s1 - 1;
+            if (n == 1) {
+                pe0 = en0;
+                pe1 = en1;
+            } else {
+                for (uint32_t i = 2; i < n; i++) {
+                    s0 &= s0 - 1;
+                    s1 &= s1 - 1;
+                }
+                pe0 = ctz64(s0);
+                pe1 = ctz64(s1);
+                s0 &= s0 - 1;
+                s1 &= s1 - 1;
+            }
+        } else if (n > 0) {
             for (uint32_t i = 1; i < n; i++) {          // fields passed over: only their bits go
                 s0 &= s0 - 1;
                 s1 &= s1 - 1;
@@ -620,10 +640,12 @@ __device__ __forceinline__ void walk2(Rec (&rec)[2], const uint64_t (&sv)[2], co
             s0 &= s0 - 1;
             s1 &= s1 - 1;
         }
+        en0 = ctz64(s0);
+        en1 = ctz64(s1);
 #pragma unroll
         for (int u = 0; u < 2; u++) {
             Rec& R = rec[u];
-            const uint32_t start = (u ? pe1 : pe0) + 1, end = ctz64(u ? s1 : s0), e = u ? e1 : e0;
+            const uint32_t start = (u ? pe1 : pe0) + 1, end = u ? en1 : en0, e = u ? e1 : e0;
             const bool gone = start > e;
             R.fail |= gone ? (e == 64) : (end == 64);
             const uint32_t fp = R.p + start, fl = gone ? 0u : end - start;
@@ -652,7 +674,8 @@ __device__ __forceinline__ void walk2(Rec (&rec)[2], const uint64_t (&sv)[2], co
 // GROUPED: GROUP BY (else one group); WM: LW_*; NS: distinct SUM arguments (0-2);
 // K16: LDS tags of 16 key bytes (else 8)
 // CANON: the roles' column order is their canonical order (WHERE, SUM 0, SUM 1, GROUP
-// BY, as present), so the walk's role ranks are compile-time constants (no selects)
+// BY, as present) over distinct columns, so the walk's role ranks are compile-time
+// constants (no selects) and every later role skips at least one separator
 template <bool GROUPED, int WM, int NS, bool K16, bool CANON>
 __global__ __launch_bounds__(LT) void lean_kernel(const uint8_t* __restrict__ g, ScanStats* __restrict__ stats,
                                                   unsigned long long* __restrict__ row_out,
@@ -863,7 +886,7 @@ __global__ __launch_bounds__(LT) void lean_kernel(const uint8_t* __restrict__ g,
 #pragma unroll
                     for (int j = 0; j < MAXS; j++) { Rr.sfp[j] = Rr.p; Rr.sfl[j] = 0; }
                 }
-                walk2<NR, WM, NS, GROUPED>(rec, sv, nv, skip, kw, ks, kg);
+                walk2<NR, WM, NS, GROUPED, CANON>(rec, sv, nv, skip, kw, ks, kg);
             }
             // a quote at or before the last byte examined may hide separators
             if (wq) {
@@ -1524,7 +1547,8 @@ hipError_t cq_launch_lean(const uint8_t* g, const cq::ScanPlan* P, const cq::Gro
         if (wm != lean::LW_NONE) want[nw++] = lean::R_WHERE;
         for (int j = 0; j < ns; j++) want[nw++] = j == 0 ? lean::R_SUM0 : lean::R_SUM1;
         if (grouped) want[nw++] = lean::R_GROUP;
-        for (uint32_t i = 0; i < nr; i++) canon = canon && lp.rrole[i] == want[i];
+        // and the columns are distinct (walk2's DISTINCT: every later role skips >= 1 separator)
+        for (uint32_t i = 0; i < nr; i++) canon = canon && lp.rrole[i] == want[i] && (i == 0 || lp.rcol[i] > lp.rcol[i - 1]);
     }
     const bool k16 = grouped && P->lean_k16;
     const size_t lds = k16 ? lean_lds_t<true>(ns, grouped) : lean_lds_t<false>(ns, grouped);
