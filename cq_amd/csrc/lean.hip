@@ -1081,7 +1081,9 @@ __global__ __launch_bounds__(LT) void lean_kernel(const uint8_t* __restrict__ g,
                         longk[u] = klen > 16;
                     }
                     if (klen == 0) k1[u] = 1u;               // the empty key's tag
-                    h[u] = key_hash(k0[u], k1[u], k2[u], k3[u]);
+                    // 8-byte tags: only keys of <= 8 bytes are looked up (longer ones spill
+                    // with their own hash), so words 2-3 never enter the tag hash
+                    h[u] = K16 ? key_hash(k0[u], k1[u], k2[u], k3[u]) : key_hash(k0[u], k1[u], 0u, 0u);
                 }
             }
 
