@@ -240,7 +240,8 @@ def stats() -> dict:
 
 
 def set_scan_kernel(mode: int) -> int:
-    """0: automatic (lean_kernel where it applies), 1: always the general scan_kernel."""
+    """0: automatic (fast_kernel, else lean_kernel, else scan_kernel by plan shape),
+    1: always the general scan_kernel, 2: never fast_kernel.  Returns the old mode."""
     return lib().cqgpu_set_scan_kernel(mode)
 
 

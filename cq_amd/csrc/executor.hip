@@ -143,6 +143,10 @@ hipError_t cq_launch_project(const uint8_t* g, const unsigned long long* recs, u
                              const ProjDesc* D, Cell* scratch, Cell* out, hipStream_t s);
 int cq_set_scan_mode(int mode);
 int cq_scan_uses_lean(const cq::ScanPlan* P, int with_cells);
+int cq_scan_kernel_kind(const cq::ScanPlan* P, int grouped, int want_rows, int with_cells);
+uint32_t cq_fast_seed(const uint8_t* data, uint64_t n, uint32_t delim, uint32_t quote, uint32_t col,
+                      unsigned long long* tags);
+size_t cq_fast_seed_slots();
 hipError_t cq_sort_offsets(void* temp, size_t* temp_bytes, const unsigned long long* in,
                            unsigned long long* out, size_t n, int bits, hipStream_t s);
 hipError_t cq_launch_route_len(const uint8_t* g, const unsigned long long* recs, uint32_t n,
@@ -416,6 +420,8 @@ struct RouteState {
     uint64_t bytes = 0;
 };
 
+constexpr uint64_t SAMPLE_BYTES = 256u << 10;   // bytes a table keeps for plan-time sampling
+
 struct cqgpu_table {
     uint8_t* dbuf = nullptr;
     const uint8_t* g = nullptr;      // device byte 0
@@ -427,6 +433,8 @@ struct cqgpu_table {
     int device = 0;
     uint32_t lean_ws = 0;            // lean_kernel window stride for this file's record lengths
     uint64_t long_cols = ~0ull;      // columns with sampled fields over 8 bytes (cq_lean_long_cols)
+    std::string sample;              // the first data bytes (plan-time sampling: fast_kernel's key seed)
+    std::map<int, std::unique_ptr<DevBuf>> fast_seed;   // per GROUP BY column: seeded LDS tags (device)
     unsigned long long* gids = nullptr;   // routed tables: global record id of each record (device)
     uint64_t ngids = 0;
     std::unique_ptr<RouteState> route;    // pending repartition (cqgpu_route_plan)
@@ -509,6 +517,10 @@ cqgpu_table* upload(const uint8_t* host, size_t n, cq_csv_config cfg, uint64_t b
     t->lean_ws = cq_lean_pick_ws(host + t->data_begin, n - std::min<uint64_t>(n, t->data_begin));
     t->long_cols = cq_lean_long_cols(host + t->data_begin, n - std::min<uint64_t>(n, t->data_begin),
                                      (uint8_t)cfg.delimiter);
+    {
+        const uint64_t db = std::min<uint64_t>(n, t->data_begin);
+        t->sample.assign((const char*)host + db, (size_t)std::min<uint64_t>(n - db, SAMPLE_BYTES));
+    }
     size_t total = PAD_BEFORE + n + PAD_AFTER;
     HIPCHECK(hipMalloc(&t->dbuf, total));
     HIPCHECK(hipMemsetAsync(t->dbuf, '\n', PAD_BEFORE, c.stream));
@@ -910,6 +922,27 @@ std::string agg_display_name(const char* cs) {
 
 // order the need slots by column so one left-to-right pass parses them all,
 // and fill the table-dependent plan fields
+
+// fast_kernel's LDS table seed for GROUP BY column `col` of table t: the distinct
+// keys of the table's sample placed by cq_fast_seed (fast.hip), built on first use
+// and kept with the table (const: a cache, not table state)
+const void* fast_seed_of(const cqgpu_table* tc, int col) {
+    cqgpu_table* t = const_cast<cqgpu_table*>(tc);
+    auto it = t->fast_seed.find(col);
+    if (it != t->fast_seed.end()) return it->second->p;
+    if (t->sample.empty()) return nullptr;
+    std::vector<unsigned long long> tags(cq_fast_seed_slots());
+    cq_fast_seed((const uint8_t*)t->sample.data(), t->sample.size(), (uint8_t)t->cfg.delimiter, (uint8_t)t->cfg.quote,
+                 (uint32_t)col, tags.data());
+    std::unique_ptr<DevBuf> b(new DevBuf(tags.size() * 8));
+    DevCtx& c = ctx();
+    HIPCHECK(hipMemcpyAsync(b->p, tags.data(), tags.size() * 8, hipMemcpyHostToDevice, c.stream));
+    HIPCHECK(hipStreamSynchronize(c.stream));
+    const void* r = b->p;
+    t->fast_seed[col] = std::move(b);
+    return r;
+}
+
 void finish_plan(const cqgpu_table* t, Compiled& C, Compiler& cc) {
     std::vector<int> order(C.need_cols.size());
     for (size_t i = 0; i < order.size(); i++) order[i] = (int)i;
@@ -942,9 +975,11 @@ void finish_plan(const cqgpu_table* t, Compiled& C, Compiler& cc) {
     C.P.range_begin = 0;
     C.P.range_end = t->n;
     C.P.lean_ws = t->lean_ws;
+    C.P.fast_seed = 0;
     if (C.P.group_slot >= 0) {
         const int gc = C.P.need_col[C.P.group_slot];
         C.P.lean_k16 = (uint32_t)((t->long_cols >> (gc < 63 ? gc : 63)) & 1);
+        if (!C.P.lean_k16) C.P.fast_seed = (uint64_t)(uintptr_t)fast_seed_of(t, gc);
     }
 }
 
@@ -1478,7 +1513,7 @@ std::vector<HGroup> run_aggregate(DevCtx& c, const cqgpu_table* t, Compiled& C, 
         }
         g_stats.scan_ms = ms_total;
         g_stats.grid = grid;
-        g_stats.scan_kernel = cq_scan_uses_lean(&C.P, 0);
+        g_stats.scan_kernel = cq_scan_kernel_kind(&C.P, grouped, row_out != nullptr, 0);
         for (int i = 0; i < 8; i++) g_clk[i] = last_clk[i];
         if (st.overflow >= 2)   // a bounded spin gave up: a kernel bug, never a data property
             throw HipError{st.overflow == 2 ? "scan kernel: MIN/MAX lock timeout" : "scan kernel: group insert timeout"};
@@ -4018,8 +4053,9 @@ struct cqgpu_partial {
     uint32_t m = 0;                 // this rank's groups
     int rep_slot = -1;              // the group column's rep slot (-1: no plain column)
     DevBuf keys, st_sum, st_first, st_rep;
-    // the dictionary of the last cqgpu_partial_dict call
-    const void* all = nullptr;
+    // the dictionary of the last cqgpu_partial_dict call (the gathered key records,
+    // copied: the caller's buffer need not outlive the call)
+    DevBuf all;
     uint32_t nall = 0, mine = 0, G = 0, cap = 0;
     DevBuf state, rec_of, first_of, slot_of, flag, dense_of, my_first;
 };
@@ -4072,7 +4108,9 @@ cqgpu_partial* cqgpu_partial_new(cq_node* q, cqgpu_table* const* tables, int nta
                 sm[(size_t)j * p->W + 1 + 2 * a] = h.sum[a];
                 sm[(size_t)j * p->W + 2 + 2 * a] = (double)h.num[a];
             }
-            fi[j] = h.first;
+            // a group with no first row here (NOPOS = -1 as a signed int64) must lose the
+            // MIN all-reduce of first positions: the "absent" sentinel scatter uses
+            fi[j] = h.first == NOPOS ? 0x7F7F7F7F7F7F7F7Full : h.first;
             if (p->rep_slot >= 0 && !h.reps.empty()) {
                 rp[2 * j] = h.reps[0].kind;
                 rp[2 * j + 1] = h.reps[0].kind == K_STR ? 0 : h.reps[0].bits;   // text: the key's bytes
@@ -4117,12 +4155,19 @@ size_t cqgpu_partial_keys(cqgpu_partial* p, void* dev_dst, uint32_t* words_per_g
 long long cqgpu_partial_dict(cqgpu_partial* p, const void* dev_all, uint64_t nall, uint64_t mine) {
     g_err.clear();
     try {
-        if (!p || (!dev_all && nall) || mine + p->m > nall || nall >= (1ull << 31)) throw HipError{"partial_dict: bad arguments"};
+        if (!p || (!dev_all && nall) || mine + p->m > nall) throw HipError{"partial_dict: bad arguments"};
+        // the table holds 2 * nall slots of 32-bit indexes: beyond 2^29 keys the caller
+        // takes the blob path (cqgpu_query_partial) instead
+        if (nall >= (1ull << 29)) throw HipError{"partial_dict: too many keys for the device dictionary"};
         DevCtx& c = ctx();
         const uint32_t n = (uint32_t)nall;
-        uint32_t cap = 64;
-        while (cap < 2 * n) cap <<= 1;
-        p->all = dev_all; p->nall = n; p->mine = (uint32_t)mine; p->cap = cap;
+        uint64_t cap = 64;
+        while (cap < 2 * (uint64_t)n) cap <<= 1;
+        DevBuf owned(std::max<size_t>((size_t)n * KEYREC, 64));
+        if (n) HIPCHECK(hipMemcpyAsync(owned.p, dev_all, (size_t)n * KEYREC, hipMemcpyDeviceToDevice, c.stream));
+        dev_all = owned.p;
+        std::swap(p->all.p, owned.p);
+        p->nall = n; p->mine = (uint32_t)mine; p->cap = (uint32_t)cap;
         DevBuf st((size_t)cap * 4), ro((size_t)cap * 4), fo((size_t)cap * 4), so(std::max<size_t>((size_t)n * 4, 4)),
             fl(std::max<size_t>((size_t)n * 4, 4)), de(std::max<size_t>((size_t)n * 4, 4)), err(64);
         HIPCHECK(hipMemsetAsync(st.p, 0, (size_t)cap * 4, c.stream));
@@ -4206,7 +4251,7 @@ cq_table* cqgpu_partial_finish(cqgpu_partial* p, cq_node* q, const double* dsum,
         std::vector<double> sm((size_t)G * W);
         std::vector<unsigned long long> fi(G), rp(2 * (size_t)G);
         if (n) {
-            HIPCHECK(hipMemcpyAsync(all.data(), p->all, (size_t)n * KEYREC, hipMemcpyDeviceToHost, c.stream));
+            HIPCHECK(hipMemcpyAsync(all.data(), p->all.p, (size_t)n * KEYREC, hipMemcpyDeviceToHost, c.stream));
             HIPCHECK(hipMemcpyAsync(flag.data(), p->flag.p, (size_t)n * 4, hipMemcpyDeviceToHost, c.stream));
         }
         if (G) {

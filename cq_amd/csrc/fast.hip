@@ -1,0 +1,1066 @@
+// fast.hip -- the scan kernel for the plan shape of the benchmark queries.
+//
+// Same job and semantics as lean_kernel (lean.hip) -- csv_load + filter_rows +
+// create_groups + evaluate_aggregate in one pass over the HBM-resident bytes
+// (reference csv_reader.c:375-465, evaluator_utils.c:986-1006,
+// evaluator_aggregates.c:108-414) -- for the narrower shape the benchmark and most
+// aggregate queries have:
+//   WHERE absent or `column op numeric-literal`; COUNT / SUM / AVG over at most two
+//   distinct columns; GROUP BY absent or one column whose keys fit 8 bytes; the
+//   roles' columns strictly ascending in the order WHERE, SUM 0, SUM 1, GROUP BY.
+// Everything a record needs is decided on one straight path; any record the path
+// cannot type exactly (a quote in front of its fields, a field of another shape, a
+// short row, a key with a blank) goes whole to the slow list and slow_kernel
+// (scan.hip), which runs the general parser.  That keeps the kernel's vector
+// instruction stream short: on gfx950 a wave64 integer VALU instruction holds its
+// SIMD for four cycles, and lean_kernel was bound by that stream
+// (profiles/r3_valu_rate.txt).
+//
+// Structure (one 1024-thread block per CU, each wave streaming its own windows):
+//   load      4 KiB windows by LDS-DMA straight into the wave's LDS bytes
+//   classify  lane l: bytes [64l, 64l+64) -> 64-bit separator and terminator masks
+//             (two v_perm_b32 lookups per dword); with the default ',' and '"' the
+//             delimiter lookup also flags quotes (its table maps '"' to 0x00, whose
+//             zero-byte test costs two instructions per dword)
+//   records   each lane walks the records starting in its own 64 bytes, two at a time
+//   fields    the roles' field ends by clearing separator bits; compile-time role ranks
+//   values    numerals of 1-4 bytes in registers (v_perm + v_dot4); wider ones by a
+//             uniform side path
+//   SUM       addends of <= 3 decimals as exact fixed-point integers (scale 10^3)
+//             accumulated with 64-bit LDS integer atomics; other numerals in doubles
+//   GROUP BY  LDS table of 2048 slots in 1024 two-slot buckets; a key lives in one of
+//             its two buckets.  The host seeds the table from a sample of the file
+//             with a cuckoo placement (no bucket overflows for the sampled keys), so a
+//             lookup is two 16-byte LDS reads and four compares; unseen keys take a
+//             free slot of their buckets by CAS, or spill to the HBM raw table
+#include <hip/hip_runtime.h>
+#include <cmath>
+#include <cstring>
+#include <vector>
+#include <unordered_set>
+#include "plan.h"
+#include "scanlib.h"
+
+namespace cq {
+namespace fast {
+
+constexpr int NWV = 16;                   // waves per block
+constexpr int LT = 64 * NWV;              // threads per block
+constexpr int LB = 64;                    // window bytes per lane
+constexpr int WB = 64 * LB;               // window bytes (4 KiB)
+constexpr int WS = 3968;                  // largest window stride (records owned per window)
+constexpr int NMW = WB / 32;
+constexpr int WBYTES = WB + 32;
+constexpr int MAXS = 2;
+constexpr uint32_t NOFIRST = 0xFFFFFFFFu;
+constexpr uint32_t TSLOTS = 2048;         // LDS table slots
+constexpr uint32_t TBUCKETS = TSLOTS / 2; // two-slot buckets
+static_assert(WS + 64 + 16 <= WB, "a record view plus a field load stays in the window");
+
+struct WaveLds {
+    uint8_t bytes[WBYTES];
+    uint32_t qt[NMW + 4];       // quote bits (written only when the window holds a quote)
+};
+static_assert(sizeof(WaveLds) % 16 == 0, "16-byte aligned wave areas");
+
+struct FastPlan {
+    uint64_t lo_ok, hi_ok;      // records starting in [lo_ok, hi_ok) are owned by this launch
+    uint64_t first_win, last_win;
+    uint32_t ws;                // window stride (multiple of 128, <= WS)
+    uint32_t delim, quote;
+    uint32_t skip[4];           // field k's column minus field k-1's (field 0: its column); fields = the
+                                // roles' columns ascending (equal columns: skip 0)
+    uint32_t rank[4];           // field index of WHERE, SUM 0, SUM 1, GROUP BY
+    uint32_t wtt;               // WHERE truth table (bit 0 <, 1 ==, 2 >)
+    int32_t wlo, whi;           // INTEGER field M: M < L <=> M < wlo; M > L <=> M > whi
+    double wl;                  // the literal
+    uint32_t pass_null;         // WHERE outcome of a NULL (empty) field
+    int32_t nacc;
+    uint32_t acc1;              // bit a: accumulator a sums SUM argument 1 (else 0)
+    const unsigned long long* seed;   // TSLOTS host-placed tags, or null
+};
+
+// HBM tables: canonical keys (TAB_GT), raw keys (TAB_RT)
+enum : int { TAB_GT = 0, TAB_RT = 1 };
+__device__ GroupTable g_fast_tabs[2];
+constexpr uint32_t GK_RAW = 6;       // raw field bytes as key (lean.hip's class)
+
+// ------------------------------------------------------------------ helpers
+__device__ __forceinline__ uint32_t ctz64(uint64_t x) { return (uint32_t)__builtin_ctzg(x, 64); }
+
+__device__ __forceinline__ void load_win(const uint8_t* g, uint64_t w, uint32_t ws, uint32_t lds, uint32_t& prev) {
+    const uint8_t* base = g + w * ws;
+    const int lane = threadIdx.x & 63;
+    asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+#pragma unroll
+    for (int i = 0; i < 4; i++) {
+        uint32_t keep;
+        asm volatile("s_mov_b32 %0, m0\n\ts_mov_b32 m0, %2\n\ts_nop 0\n\tglobal_load_lds_dwordx4 %1, off\n\ts_mov_b32 m0, %0"
+                     : "=&s"(keep)
+                     : "v"(base + 1024 * i + 16 * lane), "s"(lds + 1024u * i)
+                     : "memory");
+    }
+    const __amdgpu_buffer_rsrc_t r = __builtin_amdgcn_make_buffer_rsrc((void*)(base - 4), 0, 4, 0x00020000);
+    prev = __builtin_amdgcn_raw_buffer_load_b32(r, 0, 0, 0);
+}
+
+__device__ __forceinline__ uint32_t flags40(uint32_t r) { return __builtin_amdgcn_bitop3_b32(r, r >> 1, 0x40404040u, 0x20); }
+
+// 32 bytes -> separator and terminator bits; quote presence accumulated in q
+// (COMMA: the delimiter lookup's zero bytes, else the quote byte's zero test)
+template <bool COMMA>
+__device__ __forceinline__ void classify32(const v4u a, const v4u b, uint32_t rep_d, uint32_t rep_q, uint32_t& sep,
+                                           uint32_t& nl, uint32_t& q) {
+    uint32_t ud[4], un[4];
+#pragma unroll
+    for (int j = 0; j < 8; j++) {
+        const uint32_t x = j < 4 ? a[j & 3] : b[j & 3];
+        const uint32_t rn = __builtin_amdgcn_perm(0x00004000u, 0x00400000u, x ^ 0x08080808u);
+        uint32_t rd;
+        if (COMMA) {
+            // x ^ '*': ',' -> 6 (0x40); '"' -> 8 = sign of table byte 1 (0x20) -> 0x00; '&' -> 12 -> 0x00;
+            // '+' -> 1 (0x20); the other selectors 0-7 -> 0x80, 9-11 -> signs of 0x80 bytes, >= 13 -> 0xFF
+            rd = __builtin_amdgcn_perm(0x80408080u, 0x80802080u, x ^ 0x2A2A2A2Au);
+            q = __builtin_amdgcn_bitop3_b32(rd - 0x01010101u, rd, q, 0xBA);   // (t & ~rd) | q
+        } else {
+            rd = __builtin_amdgcn_perm(0u, 0x00000040u, x ^ rep_d);
+            const uint32_t t = x ^ rep_q;
+            q = __builtin_amdgcn_bitop3_b32(t - 0x01010101u, t, q, 0xBA);
+        }
+        const uint32_t fd = flags40(rd), fn = flags40(rn);
+        const uint32_t w = (j & 1) ? 0x80402010u : 0x08040201u;
+        if (j & 1) {
+            ud[j >> 1] = __builtin_amdgcn_udot4(fd, w, ud[j >> 1], false);
+            un[j >> 1] = __builtin_amdgcn_udot4(fn, w, un[j >> 1], false);
+        } else {
+            ud[j >> 1] = __builtin_amdgcn_udot4(fd, w, 0u, false);
+            un[j >> 1] = __builtin_amdgcn_udot4(fn, w, 0u, false);
+        }
+    }
+    nl = (un[0] >> 6) | (un[1] << 2) | (un[2] << 10) | (un[3] << 18);
+    sep = nl | (ud[0] >> 6) | (ud[1] << 2) | (ud[2] << 10) | (ud[3] << 18);
+}
+
+// exact quote bits of 32 bytes (only for windows that hold a quote)
+__device__ __forceinline__ uint32_t nib(uint32_t f) {
+    uint32_t t = f >> 7;
+    t |= t >> 7;
+    t |= t >> 14;
+    return t & 0xFu;
+}
+__device__ __forceinline__ uint32_t quote_bits(const v4u a, const v4u b, uint32_t rep) {
+    uint32_t m = 0;
+#pragma unroll
+    for (int v = 0; v < 2; v++) {
+#pragma unroll
+        for (int j = 0; j < 4; j++) m |= nib(~nonzero_bytes((v ? b[j] : a[j]) ^ rep) & 0x80808080u) << ((v * 4 + j) * 4);
+    }
+    return m;
+}
+
+// 64 bits from bit b (< 64) of the 128 bits w0 | w1 << 32 | w2 << 64 | w3 << 96
+__device__ __forceinline__ uint64_t view128(uint32_t w0, uint32_t w1, uint32_t w2, uint32_t w3, uint32_t b) {
+    const bool hi = b >= 32;
+    const uint32_t sh = b & 31, a = hi ? w1 : w0, c = hi ? w2 : w1, d = hi ? w3 : w2;
+    return (uint64_t)__builtin_amdgcn_alignbit(c, a, sh) | ((uint64_t)__builtin_amdgcn_alignbit(d, c, sh) << 32);
+}
+__device__ __forceinline__ uint64_t qview(const WaveLds& W, uint32_t p) {
+    const uint32_t wi = p >> 5, sh = p & 31;
+    const uint32_t q0 = W.qt[wi], q1 = W.qt[wi + 1], q2 = W.qt[wi + 2];
+    return (uint64_t)__builtin_amdgcn_alignbit(q1, q0, sh) | ((uint64_t)__builtin_amdgcn_alignbit(q2, q1, sh) << 32);
+}
+
+// 4 / 8 bytes of the window at byte offset o (one ds_read2_b32 [+ ds_read_b32])
+__device__ __forceinline__ uint32_t ld4(const uint8_t* w, uint32_t o) {
+    const uint32_t* t = (const uint32_t*)w;
+    const uint32_t a = o >> 2;
+    return __builtin_amdgcn_alignbyte(t[a + 1], t[a], o & 3);
+}
+__device__ __forceinline__ void ld8(const uint8_t* w, uint32_t o, uint32_t& d0, uint32_t& d1) {
+    const uint32_t* t = (const uint32_t*)w;
+    const uint32_t a = o >> 2;
+    const uint32_t x0 = t[a], x1 = t[a + 1], x2 = t[a + 2];
+    d0 = __builtin_amdgcn_alignbyte(x1, x0, o & 3);
+    d1 = __builtin_amdgcn_alignbyte(x2, x1, o & 3);
+}
+
+// A numeral of 1-4 bytes shaped [digits][.][digits] with at least one digit: M and
+// k (digits after the dot), exactly parse_value's INTEGER M (no dot) or strtod's
+// RN(M / 10^k) (csv_reader.c:133-240; never date-shaped: parse_date needs 8-10
+// bytes).  d: the field's first 4 bytes, unmasked.  DOT: a dot is allowed.
+struct Num {
+    uint32_t M, k;
+    bool ok, dot;
+};
+template <bool DOT>
+__device__ __forceinline__ Num num4(uint32_t d, uint32_t len) {
+    Num r;
+    const uint32_t sh = 32u - 8u * len;
+    uint32_t v = (d ^ 0x30303030u) << (sh & 31);
+    r.dot = false;
+    r.k = 0;
+    if (DOT) {
+        const uint32_t fd = ~nonzero_bytes(v ^ 0x1E1E1E1Eu) & 0x80808080u & (0xFFFFFFFFu << (sh & 31));   // '.' ^ '0'
+        const uint32_t low = fd & (0u - fd);
+        const uint32_t below = ((low << 1) - (low != 0 ? 1u : 0u)) & 0x01010100u;
+        v = __builtin_amdgcn_perm(0u, v, (low ? 0x0302010Cu : 0x03020100u) - below);
+        r.dot = low != 0;
+        r.k = r.dot ? (uint32_t)__builtin_clz(low) >> 3 : 0u;
+    }
+    const bool digits = lt_bytes(v, 0x0A0A0A0Au) == 0x80808080u;
+    r.ok = (len - 1u <= 3u) & digits & (!DOT | (len > 1u) | !r.dot);
+    r.M = __builtin_amdgcn_udot4(v, 0x010A6400u, __umul24(v & 0xFFu, 1000u), false);
+    return r;
+}
+// 1-7 bytes (d0/d1: the field's first 8 bytes, unmasked)
+__device__ __forceinline__ Num num7(uint32_t d0, uint32_t d1, uint32_t len) {
+    Num r;
+    const uint32_t f0 = len_mask(len, 0) & 0x80808080u, f1 = len_mask(len, 1) & 0x80808080u;
+    const uint32_t x0 = d0 ^ 0x30303030u, x1 = d1 ^ 0x30303030u;
+    const uint32_t g0 = lt_bytes(x0, 0x0A0A0A0Au) & f0, g1 = lt_bytes(x1, 0x0A0A0A0Au) & f1;
+    const uint32_t t0 = ~nonzero_bytes(d0 ^ 0x2E2E2E2Eu) & f0, t1 = ~nonzero_bytes(d1 ^ 0x2E2E2E2Eu) & f1;
+    const uint32_t ndot = (uint32_t)__popc(t0) + (uint32_t)__popc(t1);
+    r.ok = (len - 1 <= 6u) & ((g0 | t0) == f0) & ((g1 | t1) == f1) & (ndot <= 1) & ((g0 | g1) != 0);
+    uint64_t v = ((uint64_t)(x0 & spread(g0)) | ((uint64_t)(x1 & spread(g1)) << 32));
+    const uint64_t tm = (uint64_t)t0 | ((uint64_t)t1 << 32);
+    uint32_t pd = ctz64(tm) >> 3;
+    pd = pd > 7 ? 7u : pd;
+    r.dot = ndot != 0;
+    const uint64_t lo = (1ULL << (8 * pd)) - 1;
+    v = r.dot ? ((v & lo) | ((v >> 8) & ~lo)) : v;
+    r.k = r.dot ? len - 1 - pd : 0u;
+    r.k = r.k > 7 ? 7u : r.k;
+    uint32_t nd2 = len - ndot;
+    nd2 = nd2 - 1 > 7u ? 1u : nd2;
+    v <<= 8 * (8 - nd2);
+    const uint32_t vl = (uint32_t)v, vh = (uint32_t)(v >> 32);
+    const uint32_t e1 = __builtin_amdgcn_udot4(vl, 0x00010A64u, 0u, false);
+    const uint32_t e2 = __builtin_amdgcn_udot4(__builtin_amdgcn_alignbyte(vh, vl, 3), 0x00010A64u, 0u, false);
+    const uint32_t e3 = __builtin_amdgcn_udot4(vh, 0x010A0000u, 0u, false);
+    r.M = __umul24(__umul24(e1, 1000u) + e2, 100u) + e3;
+    return r;
+}
+
+__device__ __forceinline__ bool tt_result(uint32_t tt, int c) { return (tt >> (c < 0 ? 0 : (c == 0 ? 1 : 2))) & 1; }
+__device__ __forceinline__ double p10(uint32_t k) {
+    return ((k & 1) ? 10.0 : 1.0) * ((k & 2) ? 100.0 : 1.0) * ((k & 4) ? 1e4 : 1.0);
+}
+
+// 0x80 in every byte < 0x21 (blank, control, NUL) among the f-flagged bytes
+__device__ __forceinline__ uint32_t low_bytes(uint32_t d, uint32_t f) { return lt_bytes(d, 0x21212121u) & f; }
+
+}  // namespace fast
+
+// the bucket hash of an 8-byte key tag (shared with the host's seed placement)
+__host__ __device__ __forceinline__ uint32_t fast_key_hash(uint32_t k0, uint32_t k1) {
+    uint32_t x = k0 ^ ((k1 << 11) | (k1 >> 21));
+    x ^= x >> 16;
+    x = ((x & 0xFFFFFFu) * 0x2F0B3Du) ^ (x >> 7);
+    x ^= x >> 13;
+    return ((x & 0xFFFFFFu) * 0x3C6EF3u) ^ (x >> 11);
+}
+
+namespace fast {
+
+__device__ __forceinline__ GKey raw_key(uint32_t len, uint64_t w0) {
+    GKey k;
+    k.cls = GK_RAW; k.len = len; k.w0 = w0; k.w1 = 0;
+    return k;
+}
+__device__ __forceinline__ uint32_t key_len8(uint64_t w0) {
+    if (w0 == (1ull << 32)) return 0u;                 // the empty key's tag
+    return w0 ? 8u - ((uint32_t)__builtin_clzll(w0) >> 3) : 0u;
+}
+
+// a record whose key found no LDS slot: straight into the HBM raw table
+// (acc1: bit a set when accumulator a sums SUM argument 1, else argument 0)
+__device__ __noinline__ void spill8(uint64_t tag, uint64_t off, const GroupTable* tabs, ScanStats* stats, int nacc,
+                                    uint32_t acc1, bool n0, double v0, bool n1, double v1) {
+    const GroupTable& rt = tabs[TAB_RT];
+    const uint32_t kl = key_len8(tag);
+    const GKey kk = raw_key(kl, kl ? tag : 0ull);
+    const int gi = g_insert(rt, kk, gk_hash(kk), stats);
+    if (gi < 0) return;
+    atomicAdd(&rt.cnt[gi], 1ULL);
+    atomicMin(&rt.first[gi], (unsigned long long)off);
+    for (int a = 0; a < nacc; a++) {
+        const bool s1 = (acc1 >> a) & 1;
+        const bool nm = s1 ? n1 : n0;
+        if (nm) {
+            atomicAdd(&rt.sum[a][gi], s1 ? v1 : v0);
+            atomicAdd(&rt.num[a][gi], 1ULL);
+        }
+    }
+}
+
+__device__ __forceinline__ uint8_t* carve(uint8_t*& q, size_t bytes) {
+    uint8_t* r = q;
+    q += (bytes + 15) & ~(size_t)15;
+    return r;
+}
+
+template <int NS>
+constexpr uint32_t table_bytes(bool grouped) {
+    // tags, COUNT, first row; per SUM argument the fixed-point sum and the non-numeric
+    // count; one double sum only with one SUM argument (two would not fit the LDS)
+    return grouped ? TSLOTS * (8u + 4u + 4u + (uint32_t)NS * (8u + 4u) + (NS == 1 ? 8u : 0u)) : 0u;
+}
+constexpr uint32_t fixed_bytes() { return (uint32_t)(sizeof(WaveLds) * NWV); }
+
+// GROUPED: GROUP BY one column (else one group); WHERE: `col op numeric literal`
+// (else none); NS: distinct SUM arguments; COMMA: delimiter ',' and quote '"';
+// CANON: the roles' columns ascend in the order WHERE, SUM 0, SUM 1, GROUP BY (the
+// walk's ranks are compile-time), else rank[] says which field each role reads
+template <bool GROUPED, bool WHERE, int NS, bool COMMA, bool CANON>
+__global__ __launch_bounds__(LT) void fast_kernel(const uint8_t* __restrict__ g, ScanStats* __restrict__ stats,
+                                                  unsigned long long* __restrict__ slow_list,
+                                                  unsigned long long slow_cap, const FastPlan fp,
+                                                  const GroupTable* __restrict__ tabs) {
+    extern __shared__ __align__(16) uint8_t smem[];
+    uint8_t* q = smem;
+    WaveLds* waves = (WaveLds*)carve(q, sizeof(WaveLds) * NWV);
+    const int tid = threadIdx.x, lane = tid & 63;
+    const int wv = __builtin_amdgcn_readfirstlane(tid >> 6);
+    WaveLds& W = waves[wv];
+    // LDS table (structure of arrays)
+    unsigned long long* T = nullptr;     // tags, bucket b = slots 2b, 2b + 1
+    uint32_t* tcnt = nullptr;
+    uint32_t* tfirst = nullptr;
+    unsigned long long* tfix[MAXS] = {nullptr, nullptr};   // SUM in units of 10^-3 (exact)
+    double* tdbl[MAXS] = {nullptr, nullptr};               // SUM addends outside the fixed-point path
+    uint32_t* tmiss[MAXS] = {nullptr, nullptr};            // non-numeric SUM arguments
+    if (GROUPED) {
+        T = (unsigned long long*)carve(q, TSLOTS * 8);
+        tcnt = (uint32_t*)carve(q, TSLOTS * 4);
+        tfirst = (uint32_t*)carve(q, TSLOTS * 4);
+#pragma unroll
+        for (int s = 0; s < NS; s++) {
+            tfix[s] = (unsigned long long*)carve(q, TSLOTS * 8);
+            if (NS == 1) tdbl[s] = (double*)carve(q, TSLOTS * 8);
+            tmiss[s] = (uint32_t*)carve(q, TSLOTS * 4);
+        }
+        const unsigned long long* seed = fp.seed;
+        for (uint32_t i = tid; i < TSLOTS; i += LT) {
+            T[i] = seed ? seed[i] : 0ull;
+            tcnt[i] = 0;
+            tfirst[i] = NOFIRST;
+#pragma unroll
+            for (int s = 0; s < NS; s++) {
+                tfix[s][i] = 0;
+                if (NS == 1) tdbl[s][i] = 0.0;
+                tmiss[s][i] = 0;
+            }
+        }
+        __syncthreads();
+    }
+
+    constexpr int NR = (WHERE ? 1 : 0) + NS + (GROUPED ? 1 : 0);   // roles, in column order
+    constexpr int KW = 0, KS0 = WHERE ? 1 : 0, KG = NR - 1;
+    uint32_t skip[4], rk[4];
+#pragma unroll
+    for (int k = 0; k < 4; k++) {
+        skip[k] = __builtin_amdgcn_readfirstlane(fp.skip[k]);
+        rk[k] = __builtin_amdgcn_readfirstlane(fp.rank[k]);
+    }
+    const uint32_t rep_d = fp.delim * 0x01010101u, rep_q = fp.quote * 0x01010101u;
+    const uint64_t lo_ok = fp.lo_ok, hi_ok = fp.hi_ok, last_win = fp.last_win, first_win = fp.first_win;
+    const uint32_t wsb = __builtin_amdgcn_readfirstlane(fp.ws);
+    const bool pass_null = __builtin_amdgcn_readfirstlane(fp.pass_null) != 0;
+    const int wlo = __builtin_amdgcn_readfirstlane(fp.wlo), whi = __builtin_amdgcn_readfirstlane(fp.whi);
+    const uint32_t wtt = __builtin_amdgcn_readfirstlane(fp.wtt);
+    const double wl = fp.wl;
+    const int nacc = __builtin_amdgcn_readfirstlane(fp.nacc);
+    const uint32_t acc1 = __builtin_amdgcn_readfirstlane(fp.acc1);
+    const uint64_t wstep = (uint64_t)gridDim.x * NWV;
+
+    uint32_t my_cnt = 0;                       // ungrouped partials (per lane)
+    unsigned long long my_first = ~0ULL;
+    unsigned long long my_fix[MAXS] = {0ull, 0ull};
+    double my_dbl[MAXS] = {0.0, 0.0};
+    uint32_t my_num[MAXS] = {0u, 0u};
+    uint32_t v_rec = 0, v_pass = 0, v_spill = 0;
+
+    uint32_t prev_next = 0;
+    const uint32_t wlds = __builtin_amdgcn_readfirstlane(
+        (uint32_t)(uintptr_t)(__attribute__((address_space(3))) uint8_t*)W.bytes);
+    uint64_t w = first_win + (uint64_t)blockIdx.x * NWV + wv;
+    if (w < last_win) load_win(g, w, wsb, wlds, prev_next);
+    for (uint32_t round = 0; w < last_win; round++, w += wstep) {
+        const uint64_t ws = w * wsb;
+        asm volatile("s_waitcnt vmcnt(0)" ::: "memory");   // the window's bytes are in LDS
+        const uint32_t prevw = prev_next;
+        bool issued = false;
+#define FAST_ISSUE()                                                               \
+    do {                                                                           \
+        if (!issued && w + wstep < last_win) load_win(g, w + wstep, wsb, wlds, prev_next); \
+        issued = true;                                                             \
+    } while (0)
+
+        // ---- classify lane l's 64 bytes
+        v4u la[4];
+#pragma unroll
+        for (int i = 0; i < 4; i++) la[i] = ((const v4u*)W.bytes)[4 * lane + i];
+        uint32_t sep0, nl0, sep1, nl1, qf = 0;
+        classify32<COMMA>(la[0], la[1], rep_d, rep_q, sep0, nl0, qf);
+        classify32<COMMA>(la[2], la[3], rep_d, rep_q, sep1, nl1, qf);
+        const bool wq = __ballot((qf & 0x80808080u) != 0) != 0;   // window may hold a quote (uniform)
+        if (wq) {
+            W.qt[2 * lane] = quote_bits(la[0], la[1], rep_q);
+            W.qt[2 * lane + 1] = quote_bits(la[2], la[3], rep_q);
+        }
+
+        // ---- record starts owned by this window
+        const uint64_t nl = (uint64_t)nl0 | ((uint64_t)nl1 << 32);
+        const uint32_t prev_top = (uint32_t)__builtin_amdgcn_update_dpp(0, (int)(nl1 >> 31), 0x138, 0xf, 0xf, true);
+        const uint32_t pb = prevw >> 24;
+        const uint32_t prevnl = lane == 0 ? (uint32_t)(pb == '\n' || pb == '\r') : prev_top;
+        uint64_t todo = ~nl & ((nl << 1) | prevnl);
+        {
+            const uint64_t lo64 = (lo_ok > ws ? lo_ok : ws) - ws;
+            const uint64_t hi64 = hi_ok < ws + wsb ? hi_ok : ws + wsb;
+            const uint32_t lo_s = (uint32_t)(lo64 < (uint64_t)wsb ? lo64 : (uint64_t)wsb);
+            const uint32_t hi_s = hi64 > ws ? (uint32_t)(hi64 - ws) : 0u;
+            const uint32_t b0 = (uint32_t)lane * LB;
+            const uint32_t a = lo_s > b0 ? lo_s - b0 : 0u, e = hi_s > b0 ? hi_s - b0 : 0u;
+            const uint64_t keep_lo = a >= 64 ? 0ull : (~0ull << a);
+            const uint64_t keep_hi = e >= 64 ? ~0ull : ((1ull << e) - 1);
+            todo &= keep_lo & keep_hi;
+        }
+        const uint32_t xs0 = (uint32_t)__builtin_amdgcn_update_dpp(0, (int)sep0, 0x130, 0xf, 0xf, true);
+        const uint32_t xs1 = (uint32_t)__builtin_amdgcn_update_dpp(0, (int)sep1, 0x130, 0xf, 0xf, true);
+        const uint32_t xn0 = (uint32_t)__builtin_amdgcn_update_dpp(0, (int)nl0, 0x130, 0xf, 0xf, true);
+        const uint32_t xn1 = (uint32_t)__builtin_amdgcn_update_dpp(0, (int)nl1, 0x130, 0xf, 0xf, true);
+
+        while (__any(todo != 0)) {
+            // ---- two records of this lane
+            uint32_t p[2], fst[2][4], fen[2][4];
+            bool valid[2], fail[2];
+#pragma unroll
+            for (int u = 0; u < 2; u++) {
+                valid[u] = todo != 0;
+                const uint32_t b = valid[u] ? ctz64(todo) : 0u;
+                todo &= todo - 1;
+                p[u] = (uint32_t)lane * LB + b;
+                uint64_t s = view128(sep0, sep1, xs0, xs1, b);
+                const uint32_t e = ctz64(view128(nl0, nl1, xn0, xn1, b));   // record end (64: past the view)
+                // the roles' fields in column order: clearing separator bits visits field
+                // ends in order (skip 0 after the first role: the same column again)
+                uint32_t en_prev = 0, st_prev = 0;
+#pragma unroll
+                for (int k = 0; k < NR; k++) {
+                    const uint32_t n = skip[k];
+                    uint32_t st, en;
+                    if (k > 0 && n == 0) {
+                        st = st_prev;
+                        en = en_prev;
+                    } else {
+                        if (k == 0) {
+                            if (n == 0) {
+                                st = 0;
+                            } else {
+                                for (uint32_t i = 1; i < n; i++) s &= s - 1;
+                                st = ctz64(s) + 1;
+                                s &= s - 1;
+                            }
+                        } else {
+                            s &= s - 1;                              // the previous field's end
+                            if (n == 1) {
+                                st = en_prev + 1;
+                            } else {
+                                for (uint32_t i = 2; i < n; i++) s &= s - 1;
+                                st = ctz64(s) + 1;
+                                s &= s - 1;
+                            }
+                        }
+                        en = ctz64(s);
+                    }
+                    fst[u][k] = st;
+                    fen[u][k] = en;
+                    en_prev = en;
+                    st_prev = st;
+                }
+                // the last role's field must end inside the view and at or before the
+                // record's terminator (else the row is short or longer than the view)
+                fail[u] = !valid[u] | (en_prev >= 64u) | (en_prev > e);
+            }
+            const bool last_pass = !__any(todo != 0);
+            if (wq) {                                                // a quote in front of a needed field
+#pragma unroll
+                for (int u = 0; u < 2; u++) {
+                    const uint32_t lp = fen[u][NR - 1] < 63 ? fen[u][NR - 1] : 63u;
+                    fail[u] |= (qview(W, p[u]) & ((2ULL << lp) - 1)) != 0;
+                }
+            }
+
+            // ---- each role's field: compile-time ranks (CANON) or the plan's (uniform selects)
+            uint32_t wst[2] = {0, 0}, wen[2] = {0, 0}, gst[2] = {0, 0}, gen[2] = {0, 0};
+            uint32_t sst[2][MAXS] = {{0, 0}, {0, 0}}, sen[2][MAXS] = {{0, 0}, {0, 0}};
+#pragma unroll
+            for (int u = 0; u < 2; u++) {
+                auto pick = [&](uint32_t r, uint32_t& a, uint32_t& b) {
+                    a = fst[u][0];
+                    b = fen[u][0];
+#pragma unroll
+                    for (int k = 1; k < NR; k++) {
+                        a = r == (uint32_t)k ? fst[u][k] : a;
+                        b = r == (uint32_t)k ? fen[u][k] : b;
+                    }
+                };
+                if (CANON) {
+                    if (WHERE) { wst[u] = fst[u][KW]; wen[u] = fen[u][KW]; }
+#pragma unroll
+                    for (int j = 0; j < NS; j++) { sst[u][j] = fst[u][KS0 + j]; sen[u][j] = fen[u][KS0 + j]; }
+                    if (GROUPED) { gst[u] = fst[u][KG]; gen[u] = fen[u][KG]; }
+                } else {
+                    if (WHERE) pick(rk[0], wst[u], wen[u]);
+#pragma unroll
+                    for (int j = 0; j < NS; j++) pick(rk[1 + j], sst[u][j], sen[u][j]);
+                    if (GROUPED) pick(rk[3], gst[u], gen[u]);
+                }
+            }
+
+            // ---- field bytes (one batch of LDS reads)
+            uint32_t wd[2], sd[2][MAXS], k0[2], k1[2];
+#pragma unroll
+            for (int u = 0; u < 2; u++) {
+                if (WHERE) wd[u] = ld4(W.bytes, p[u] + wst[u]);
+#pragma unroll
+                for (int j = 0; j < NS; j++) sd[u][j] = ld4(W.bytes, p[u] + sst[u][j]);
+                if (GROUPED) ld8(W.bytes, p[u] + gst[u], k0[u], k1[u]);
+            }
+
+            // ---- WHERE outcome (wu: a field the 4-byte numeral path could not type)
+            bool pass[2] = {true, true};
+            bool wu[2] = {false, false};
+            if (WHERE) {
+                bool wide = false;
+#pragma unroll
+                for (int u = 0; u < 2; u++) {
+                    const uint32_t len = wen[u] - wst[u];
+                    const Num n = num4<false>(wd[u], len);
+                    const int c = (int)n.M < wlo ? -1 : ((int)n.M > whi ? 1 : 0);
+                    pass[u] = len == 0 ? pass_null : tt_result(wtt, c);
+                    wu[u] = !n.ok & (len != 0) & !fail[u];
+                    wide |= wu[u];
+                }
+                if (__any(wide)) {                                   // DOUBLE or 5-7 byte numerals
+#pragma unroll
+                    for (int u = 0; u < 2; u++) {
+                        if (wu[u]) {
+                            const uint32_t len = wen[u] - wst[u];
+                            uint32_t d0, d1;
+                            ld8(W.bytes, p[u] + wst[u], d0, d1);
+                            const Num n = num7(d0, d1, len);
+                            if (n.ok) {
+                                int c;
+                                if (n.dot) {
+                                    const double v = (double)n.M / p10(n.k);   // strtod: exact operands, one rounding
+                                    c = v < wl ? -1 : (v > wl ? 1 : 0);
+                                } else {
+                                    c = (int)n.M < wlo ? -1 : ((int)n.M > whi ? 1 : 0);
+                                }
+                                pass[u] = tt_result(wtt, c);
+                                wu[u] = false;
+                            }
+                        }
+                    }
+                }
+            }
+
+            // ---- SUM addends: fixed point (10^-3) for numerals of <= 4 bytes (<= 3 decimals);
+            //      5-7 byte numerals as strtod's double; su: not typed here
+            uint64_t sfix[2][MAXS];
+            double sdbl[2][MAXS];
+            bool hspill[2] = {false, false};   // an addend only the HBM table can take (NS == 2, > 3 decimals)
+            bool snum[2][MAXS], sfx[2][MAXS], su[2] = {false, false};
+#pragma unroll
+            for (int j = 0; j < NS; j++) {
+                bool wide = false, sw[2];
+#pragma unroll
+                for (int u = 0; u < 2; u++) {
+                    const uint32_t len = sen[u][j] - sst[u][j];
+                    const Num n = num4<true>(sd[u][j], len);
+                    const uint32_t mul = (n.k & 2) ? ((n.k & 1) ? 1u : 10u) : ((n.k & 1) ? 100u : 1000u);
+                    sfix[u][j] = __umul24(n.M, mul);   // < 10^7
+                    sdbl[u][j] = 0.0;
+                    snum[u][j] = n.ok;
+                    sfx[u][j] = true;
+                    sw[u] = !n.ok & (len != 0) & !fail[u];
+                    wide |= sw[u];
+                }
+                if (__any(wide)) {
+#pragma unroll
+                    for (int u = 0; u < 2; u++) {
+                        if (sw[u]) {
+                            const uint32_t len = sen[u][j] - sst[u][j];
+                            uint32_t d0, d1;
+                            ld8(W.bytes, p[u] + sst[u][j], d0, d1);
+                            const Num n = num7(d0, d1, len);
+                            if (n.ok) {
+                                snum[u][j] = true;
+                                sw[u] = false;
+                                if (n.k <= 3) {                          // exact: M * 10^(3 - k) < 10^10
+                                    const uint32_t mul = (n.k & 2) ? ((n.k & 1) ? 1u : 10u) : ((n.k & 1) ? 100u : 1000u);
+                                    sfix[u][j] = (uint64_t)n.M * mul;
+                                } else {
+                                    sdbl[u][j] = (double)n.M / p10(n.k);   // strtod: RN(M / 10^k), exact operands
+                                    sfx[u][j] = false;
+                                    hspill[u] |= NS == 2;
+                                }
+                            }
+                        }
+                    }
+                }
+#pragma unroll
+                for (int u = 0; u < 2; u++) su[u] |= sw[u];
+            }
+#pragma unroll
+            for (int u = 0; u < 2; u++) fail[u] |= wu[u] | su[u];
+
+            // ---- GROUP BY key: the raw field bytes (<= 8, none <= ' '), zero padded
+            uint64_t tag[2] = {0, 0};
+            uint32_t hb[2] = {0, 0};
+            if (GROUPED) {
+#pragma unroll
+                for (int u = 0; u < 2; u++) {
+                    const uint32_t klen = gen[u] - gst[u];
+                    const uint32_t m0 = len_mask(klen, 0), m1 = len_mask(klen, 1);
+                    const uint32_t a0 = k0[u] & m0, a1 = k1[u] & m1;
+                    fail[u] |= (klen > 8u) | ((low_bytes(a0, m0 & 0x80808080u) | low_bytes(a1, m1 & 0x80808080u)) != 0);
+                    tag[u] = klen ? ((uint64_t)a0 | ((uint64_t)a1 << 32)) : (1ull << 32);
+                    hb[u] = fast_key_hash((uint32_t)tag[u], (uint32_t)(tag[u] >> 32));
+                }
+            }
+            if (last_pass) FAST_ISSUE();                             // the window's bytes are read
+
+            // ---- declined records go whole to slow_kernel
+#pragma unroll
+            for (int u = 0; u < 2; u++) {
+                const bool slow = valid[u] & fail[u];
+                const uint64_t sb = __ballot(slow);
+                if (sb) {
+                    unsigned long long base = 0;
+                    if (lane == 0) base = atomicAdd(&stats->slow_records, (unsigned long long)__popcll(sb));
+                    base = __shfl(base, 0, 64);
+                    if (slow) {
+                        const unsigned long long i = base + __popcll(sb & ((1ULL << lane) - 1));
+                        if (i < slow_cap) slow_list[i] = ws + p[u];
+                    }
+                }
+                const bool ok = valid[u] & !fail[u];
+                pass[u] = pass[u] & ok;
+                v_rec += ok ? 1u : 0u;
+                v_pass += pass[u] ? 1u : 0u;
+            }
+
+            // ---- aggregate
+            if (!GROUPED) {
+#pragma unroll
+                for (int u = 0; u < 2; u++) {
+                    const uint64_t off = ws + p[u];
+                    my_cnt += pass[u] ? 1u : 0u;
+                    my_first = pass[u] && off < my_first ? off : my_first;
+#pragma unroll
+                    for (int j = 0; j < NS; j++) {
+                        const bool on = pass[u] & snum[u][j];
+                        my_fix[j] += on & sfx[u][j] ? sfix[u][j] : 0u;
+                        my_dbl[j] += on & !sfx[u][j] ? sdbl[u][j] : 0.0;
+                        my_num[j] += on ? 1u : 0u;
+                    }
+                }
+            } else {
+                int slot[2];
+                bool miss[2];
+#pragma unroll
+                for (int u = 0; u < 2; u++) {
+                    const uint32_t b1 = hb[u] & (TBUCKETS - 1), b2 = (hb[u] >> 16) & (TBUCKETS - 1);
+                    const v4u x = ((const v4u*)T)[b1], y = ((const v4u*)T)[b2];
+                    const uint64_t t0 = (uint64_t)x.x | ((uint64_t)x.y << 32), t1 = (uint64_t)x.z | ((uint64_t)x.w << 32);
+                    const uint64_t t2 = (uint64_t)y.x | ((uint64_t)y.y << 32), t3 = (uint64_t)y.z | ((uint64_t)y.w << 32);
+                    int s = -1;
+                    s = t3 == tag[u] ? (int)(2 * b2 + 1) : s;
+                    s = t2 == tag[u] ? (int)(2 * b2) : s;
+                    s = t1 == tag[u] ? (int)(2 * b1 + 1) : s;
+                    s = t0 == tag[u] ? (int)(2 * b1) : s;
+                    slot[u] = hspill[u] ? -1 : s;
+                    miss[u] = pass[u] & (s < 0) & !hspill[u];
+                }
+                if (__any(miss[0] | miss[1])) {                      // keys the seed did not place
+#pragma unroll
+                    for (int u = 0; u < 2; u++) {
+                        if (miss[u]) {
+                            const uint32_t b1 = hb[u] & (TBUCKETS - 1), b2 = (hb[u] >> 16) & (TBUCKETS - 1);
+                            const uint32_t cand[4] = {2 * b1, 2 * b1 + 1, 2 * b2, 2 * b2 + 1};
+                            for (int c = 0; c < 4 && slot[u] < 0; c++) {
+                                const unsigned long long old = atomicCAS(&T[cand[c]], 0ull, (unsigned long long)tag[u]);
+                                if (old == 0ull || old == tag[u]) slot[u] = (int)cand[c];
+                            }
+                        }
+                    }
+                }
+#pragma unroll
+                for (int u = 0; u < 2; u++) {
+                    const bool add = pass[u] & (slot[u] >= 0);
+                    if (add) {
+                        const uint32_t fc = (round << 16) | ((uint32_t)wv << 12) | p[u];
+                        atomicAdd(&tcnt[slot[u]], 1u);
+                        atomicMin(&tfirst[slot[u]], fc);
+#pragma unroll
+                        for (int j = 0; j < NS; j++) {
+                            if (snum[u][j]) {
+                                if (sfx[u][j]) atomicAdd(&tfix[j][slot[u]], (unsigned long long)sfix[u][j]);
+                                else if (NS == 1) atomicAdd(&tdbl[j][slot[u]], sdbl[u][j]);
+                            }
+                        }
+                    }
+#pragma unroll
+                    for (int j = 0; j < NS; j++) {
+                        const bool nn = add & !snum[u][j];
+                        if (__any(nn)) {
+                            if (nn) atomicAdd(&tmiss[j][slot[u]], 1u);
+                        }
+                    }
+                    const bool spill = pass[u] & (slot[u] < 0);
+                    if (__any(spill)) {                              // both buckets full
+                        v_spill += spill ? 1u : 0u;
+                        if (spill) {
+                            double v0 = 0.0, v1 = 0.0;
+                            bool n0 = false, n1 = false;
+                            if (NS > 0) { n0 = snum[u][0]; v0 = sfx[u][0] ? sfix[u][0] / 1000.0 : sdbl[u][0]; }
+                            if (NS > 1) { n1 = snum[u][1]; v1 = sfx[u][1] ? sfix[u][1] / 1000.0 : sdbl[u][1]; }
+                            spill8(tag[u], ws + p[u], tabs, stats, nacc, acc1, n0, v0, n1, v1);
+                        }
+                    }
+                }
+            }
+            asm volatile("" ::: "memory");
+            __builtin_amdgcn_wave_barrier();
+            asm volatile("" ::: "memory");
+        }
+        FAST_ISSUE();                                                // (a window without owned records)
+#undef FAST_ISSUE
+    }
+
+    // ---- statistics
+    unsigned long long n_rec = v_rec, n_pass = v_pass, n_spill = v_spill;
+    for (int o = 32; o > 0; o >>= 1) {
+        n_rec += __shfl_down(n_rec, o, 64);
+        n_pass += __shfl_down(n_pass, o, 64);
+        n_spill += __shfl_down(n_spill, o, 64);
+    }
+    if (lane == 0) {
+        if (n_rec) atomicAdd(&stats->records, n_rec);
+        if (n_pass) atomicAdd(&stats->passed, n_pass);
+        if (n_spill) atomicAdd(&stats->lds_spills, n_spill);
+    }
+
+    if (!GROUPED) {
+        unsigned long long c = my_cnt, f = my_first;
+        double sm[MAXS];
+        unsigned long long nm[MAXS];
+#pragma unroll
+        for (int j = 0; j < MAXS; j++) { sm[j] = (double)my_fix[j] / 1000.0 + my_dbl[j]; nm[j] = my_num[j]; }
+        for (int o = 32; o > 0; o >>= 1) {
+            c += __shfl_down(c, o, 64);
+            const unsigned long long ff = __shfl_down(f, o, 64);
+            f = ff < f ? ff : f;
+#pragma unroll
+            for (int j = 0; j < MAXS; j++) {
+                sm[j] += __shfl_down(sm[j], o, 64);
+                nm[j] += __shfl_down(nm[j], o, 64);
+            }
+        }
+        if (lane == 0) {
+            const GroupTable& gt = tabs[TAB_GT];
+            GKey k;
+            k.cls = GK_ALL; k.len = 0; k.w0 = 0; k.w1 = 0;
+            const int gi = g_insert(gt, k, 0x12345678ULL, stats);
+            if (gi >= 0) {
+                if (c) atomicAdd(&gt.cnt[gi], c);
+                if (f != ~0ULL) atomicMin(&gt.first[gi], f);
+                for (int a = 0; a < nacc; a++) {
+                    const bool j1 = (acc1 >> a) & 1;
+                    const double sa = j1 ? sm[MAXS - 1] : sm[0];
+                    const unsigned long long na = j1 ? nm[MAXS - 1] : nm[0];
+                    if (na) {
+                        atomicAdd(&gt.sum[a][gi], sa);
+                        atomicAdd(&gt.num[a][gi], na);
+                    }
+                }
+            }
+        }
+        return;
+    }
+
+    // ---- flush the block's raw keys into the HBM raw table (raw_merge_kernel types
+    //      every distinct raw key once and merges it into the canonical table)
+    __syncthreads();
+    const GroupTable& rt = tabs[TAB_RT];
+    const uint32_t rot = (uint32_t)blockIdx.x * (TSLOTS / 64 + 1);
+    for (uint32_t ii = tid; ii < TSLOTS; ii += LT) {
+        const uint32_t i = (ii + rot) & (TSLOTS - 1);
+        const uint32_t n = tcnt[i];
+        if (!n) continue;
+        const uint64_t w0 = T[i];
+        const uint32_t kl = key_len8(w0);
+        const GKey k = raw_key(kl, kl ? w0 : 0ull);
+        const int gi = g_insert(rt, k, gk_hash(k), stats);
+        if (gi < 0) continue;
+        atomicAdd(&rt.cnt[gi], (unsigned long long)n);
+        const uint32_t fc = tfirst[i];
+        if (fc != NOFIRST) {
+            const uint64_t fw = first_win + ((uint64_t)(fc >> 16) * gridDim.x + blockIdx.x) * NWV + ((fc >> 12) & 15);
+            atomicMin(&rt.first[gi], (unsigned long long)(fw * wsb + (fc & 4095)));
+        }
+        for (int acc = 0; acc < nacc; acc++) {
+            const bool j1 = (acc1 >> acc) & 1;
+            const double sa = j1 ? (double)tfix[MAXS - 1][i] / 1000.0
+                                 : (double)tfix[0][i] / 1000.0 + (NS == 1 ? tdbl[0][i] : 0.0);
+            const uint32_t ms = j1 ? tmiss[MAXS - 1][i] : tmiss[0][i];
+            const uint32_t num = n - ms;
+            if (num) {
+                atomicAdd(&rt.sum[acc][gi], sa);
+                atomicAdd(&rt.num[acc][gi], (unsigned long long)num);
+            }
+        }
+    }
+}
+
+}  // namespace fast
+}  // namespace cq
+
+// ------------------------------------------------------------------ host side
+namespace {
+
+using namespace cq;
+using fast::FastPlan;
+
+bool fcmp_result(uint32_t op, int c) {
+    switch (op) {
+        case CMP_EQ: return c == 0;
+        case CMP_NE: return c != 0;
+        case CMP_LT: return c < 0;
+        case CMP_GT: return c > 0;
+        case CMP_LE: return c <= 0;
+        default: return c >= 0;
+    }
+}
+
+// fast_kernel's plan shape (see the file comment); fills the FastPlan fields that
+// depend on the plan only
+bool fast_shape(const ScanPlan* P, int grouped, FastPlan* fp, int* ns, bool* where, bool* canonical) {
+    if (P->nacc > MAX_ACC || P->ngpart > 0) return false;
+    const uint32_t d = P->delim;
+    if ((d - '0') < 10u || d == '.' || ((d | 32) >= 'a' && (d | 32) <= 'z') || d == '+' || d == '-') return false;
+    if (d == '\n' || d == '\r' || d <= ' ') return false;
+    if (P->quote == d || P->quote == '\n' || P->quote == '\r') return false;
+    *fp = FastPlan{};
+    fp->delim = d;
+    fp->quote = P->quote;
+    fp->nacc = P->nacc;
+    int sslot[2] = {-1, -1};
+    *ns = 0;
+    for (int a = 0; a < P->nacc; a++) {
+        if (P->acc[a].kind != ACC_SUM) return false;
+        const int slot = P->acc[a].slot;
+        int j = 0;
+        while (j < *ns && sslot[j] != slot) j++;
+        if (j == *ns) {
+            if (*ns == 2) return false;
+            sslot[(*ns)++] = slot;
+        }
+        if (j) fp->acc1 |= 1u << a;
+    }
+    int wcol = -1;
+    if (P->nprog == 0) {
+        *where = false;
+    } else if (P->nprog == 3 && P->prog[0].op == OP_COL && P->prog[1].op == OP_CONST && P->prog[2].op == OP_CMP) {
+        const Cell& L = P->consts[P->prog[1].b];
+        if (L.kind != K_INT && L.kind != K_DBL) return false;
+        *where = true;
+        wcol = P->need_col[P->prog[0].a];
+        const uint32_t op = P->prog[2].a;
+        fp->wtt = (fcmp_result(op, -1) ? 1u : 0u) | (fcmp_result(op, 0) ? 2u : 0u) | (fcmp_result(op, 1) ? 4u : 0u);
+        fp->pass_null = fcmp_result(op, -1) ? 1u : 0u;             // NULL < any non-NULL
+        double lv;
+        if (L.kind == K_INT) lv = (double)(int64_t)L.bits;
+        else memcpy(&lv, &L.bits, 8);
+        if (!std::isfinite(lv)) return false;
+        fp->wl = lv;
+        const double c = std::ceil(lv), f = std::floor(lv);
+        fp->wlo = c >= 2147483647.0 ? 2147483647 : (c <= -2147483648.0 ? (-2147483647 - 1) : (int32_t)c);
+        fp->whi = f >= 2147483647.0 ? 2147483647 : (f <= -2147483648.0 ? (-2147483647 - 1) : (int32_t)f);
+    } else {
+        return false;
+    }
+    if (grouped && (P->group_slot < 0 || P->lean_k16)) return false;
+    // the roles' fields in column order (equal columns share a field; ties keep the
+    // role order WHERE, SUM 0, SUM 1, GROUP BY)
+    int cols[4], roles[4], nr = 0;
+    if (*where) { cols[nr] = wcol; roles[nr++] = 0; }
+    for (int j = 0; j < *ns; j++) { cols[nr] = P->need_col[sslot[j]]; roles[nr++] = 1 + j; }
+    if (grouped) { cols[nr] = P->need_col[P->group_slot]; roles[nr++] = 3; }
+    for (int a = 1; a < nr; a++)
+        for (int b = a; b > 0 && cols[b - 1] > cols[b]; b--) {
+            std::swap(cols[b - 1], cols[b]);
+            std::swap(roles[b - 1], roles[b]);
+        }
+    bool canon = true;
+    for (int k = 0; k < nr; k++) {
+        if (cols[k] < 0) return false;
+        fp->skip[k] = (uint32_t)(k ? cols[k] - cols[k - 1] : cols[k]);
+        fp->rank[roles[k]] = (uint32_t)k;
+        // compile-time ranks: WHERE 0, SUM j (WHERE ? 1 : 0) + j, GROUP BY the last
+        const int want = roles[k] == 0 ? 0 : (roles[k] == 3 ? nr - 1 : (*where ? 1 : 0) + roles[k] - 1);
+        canon = canon && k == want;
+    }
+    *canonical = canon;
+    return true;
+}
+
+typedef void (*fast_fn_t)(const uint8_t*, ScanStats*, unsigned long long*, unsigned long long, const FastPlan,
+                          const GroupTable*);
+
+template <bool G, bool WH, bool COMMA, bool CANON>
+fast_fn_t pick_ns(int ns) {
+    if (ns == 0) return fast::fast_kernel<G, WH, 0, COMMA, CANON>;
+    return ns == 1 ? fast::fast_kernel<G, WH, 1, COMMA, CANON> : fast::fast_kernel<G, WH, 2, COMMA, CANON>;
+}
+template <bool G, bool CANON>
+fast_fn_t pick_wc(bool where, int ns, bool comma) {
+    if (where) return comma ? pick_ns<G, true, true, CANON>(ns) : pick_ns<G, true, false, CANON>(ns);
+    return comma ? pick_ns<G, false, true, CANON>(ns) : pick_ns<G, false, false, CANON>(ns);
+}
+template <bool G>
+fast_fn_t pick_fast(bool where, int ns, bool comma, bool canon) {
+    return canon ? pick_wc<G, true>(where, ns, comma) : pick_wc<G, false>(where, ns, comma);
+}
+
+size_t fast_lds(int grouped, int ns) {
+    const size_t t = !grouped ? 0 : (ns == 0 ? fast::table_bytes<0>(true) : (ns == 1 ? fast::table_bytes<1>(true)
+                                                                                     : fast::table_bytes<2>(true)));
+    return fast::fixed_bytes() + t + 256;
+}
+
+}  // namespace
+
+extern "C" {
+
+// 1 when fast_kernel handles this plan (grouped: GROUP BY one column; want_rows:
+// the launch must also emit matching record offsets, which fast_kernel does not)
+int cq_fast_eligible(const cq::ScanPlan* P, int grouped, int want_rows) {
+    if (want_rows) return 0;
+    FastPlan fp;
+    int ns = 0;
+    bool where = false, canon = false;
+    if (!fast_shape(P, grouped, &fp, &ns, &where, &canon)) return 0;
+    return fast_lds(grouped, ns) <= 160 * 1024 ? 1 : 0;
+}
+
+// the scan (the caller runs slow_kernel over slow_list, then raw_merge_kernel)
+hipError_t cq_launch_fast(const uint8_t* g, const cq::ScanPlan* P, const cq::GroupTable* gt,
+                          const cq::GroupTable* rt, cq::ScanStats* stats, int grouped, int grid, hipStream_t s,
+                          unsigned long long* slow_list, unsigned long long slow_cap) {
+    FastPlan fp;
+    int ns = 0;
+    bool where = false, canon = false;
+    if (!fast_shape(P, grouped, &fp, &ns, &where, &canon)) return hipErrorInvalidValue;
+    if (((uintptr_t)g & 255) != 0) return hipErrorInvalidValue;
+    const uint64_t hi = P->range_end < P->n ? P->range_end : P->n;
+    fp.lo_ok = P->data_begin > P->range_begin ? P->data_begin : P->range_begin;
+    fp.hi_ok = hi;
+    fp.ws = P->lean_ws ? P->lean_ws : (uint32_t)fast::WS;
+    if (fp.ws > (uint32_t)fast::WS || fp.ws % 128) return hipErrorInvalidValue;
+    fp.first_win = P->range_begin / fp.ws;
+    fp.last_win = (hi + fp.ws - 1) / fp.ws;
+    fp.seed = grouped ? (const unsigned long long*)(uintptr_t)P->fast_seed : nullptr;
+    static GroupTable* tabs_dev[64];
+    int dev = 0;
+    (void)hipGetDevice(&dev);
+    if (!tabs_dev[dev & 63]) {
+        hipError_t e = hipGetSymbolAddress((void**)&tabs_dev[dev & 63], HIP_SYMBOL(fast::g_fast_tabs));
+        if (e != hipSuccess) return e;
+    }
+    static GroupTable tabs[2];
+    tabs[0] = *gt;
+    if (rt) tabs[1] = *rt;
+    else memset(&tabs[1], 0, sizeof tabs[1]);
+    hipError_t e = hipMemcpyAsync(tabs_dev[dev & 63], tabs, sizeof tabs, hipMemcpyHostToDevice, s);
+    if (e != hipSuccess) return e;
+    const bool comma = P->delim == ',' && P->quote == '"';
+    const fast_fn_t fn = grouped ? pick_fast<true>(where, ns, comma, canon) : pick_fast<false>(where, ns, comma, canon);
+    const size_t lds = fast_lds(grouped, ns);
+    (void)hipFuncSetAttribute((const void*)fn, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds);
+    hipLaunchKernelGGL(fn, dim3(grid), dim3(fast::LT), lds, s, g, stats, slow_list, slow_cap, fp,
+                       (const GroupTable*)tabs_dev[dev & 63]);
+    return hipGetLastError();
+}
+
+int cq_fast_waves_per_block() { return fast::NWV; }
+
+// The LDS table seed of a GROUP BY column: the distinct raw keys of the sampled
+// records (records split on '\n' / '\r' runs, fields on the delimiter, quote-blind;
+// records holding a quote skipped), placed into the 1024 two-slot buckets by cuckoo
+// insertion with fast_key_hash's two bucket choices.  tags: TSLOTS words (0: free).
+// Returns the number of keys placed (keys that do not fit are left to the kernel's
+// own insertion).
+uint32_t cq_fast_seed(const uint8_t* data, uint64_t n, uint32_t delim, uint32_t quote, uint32_t col,
+                      unsigned long long* tags) {
+    using fast::TSLOTS;
+    using fast::TBUCKETS;
+    memset(tags, 0, TSLOTS * sizeof(unsigned long long));
+    std::unordered_set<unsigned long long> keys;
+    uint64_t i = 0;
+    while (i < n && keys.size() < TSLOTS) {
+        while (i < n && (data[i] == '\n' || data[i] == '\r')) i++;
+        const uint64_t rs = i;
+        while (i < n && data[i] != '\n' && data[i] != '\r') i++;
+        if (i >= n) break;                               // the sample's last record may be cut
+        const uint8_t* r = data + rs;
+        const uint64_t rl = i - rs;
+        if (memchr(r, (int)quote, rl)) continue;
+        uint32_t c = 0;
+        uint64_t fs = 0;
+        bool found = false;
+        uint64_t kf = 0, kl = 0;
+        for (uint64_t j = 0; j <= rl; j++) {
+            if (j == rl || r[j] == delim) {
+                if (c == col) { kf = fs; kl = j - fs; found = true; break; }
+                c++;
+                fs = j + 1;
+            }
+        }
+        if (!found || kl > 8) continue;
+        bool ok = true;
+        unsigned long long t = 0;
+        for (uint64_t j = 0; j < kl; j++) {
+            if (r[kf + j] <= ' ') ok = false;
+            t |= (unsigned long long)r[kf + j] << (8 * j);
+        }
+        if (!ok) continue;
+        keys.insert(kl ? t : (1ull << 32));
+    }
+    uint32_t placed = 0;
+    uint64_t rng = 0x9E3779B97F4A7C15ull;
+    for (unsigned long long k : keys) {
+        unsigned long long cur = k;
+        bool done = false;
+        for (int kick = 0; kick < 512 && !done; kick++) {
+            const uint32_t h = fast_key_hash((uint32_t)cur, (uint32_t)(cur >> 32));
+            const uint32_t b[2] = {h & (TBUCKETS - 1), (h >> 16) & (TBUCKETS - 1)};
+            for (int x = 0; x < 2 && !done; x++)
+                for (int y = 0; y < 2 && !done; y++)
+                    if (!tags[2 * b[x] + y]) { tags[2 * b[x] + y] = cur; done = true; }
+            if (done) break;
+            rng ^= rng << 13; rng ^= rng >> 7; rng ^= rng << 17;
+            const uint32_t v = 2 * b[(rng >> 1) & 1] + (uint32_t)(rng & 1);
+            std::swap(cur, tags[v]);
+        }
+        if (done) placed++;                              // else the carried key is left out
+    }
+    return placed;
+}
+
+size_t cq_fast_seed_slots() { return fast::TSLOTS; }
+
+}  // extern "C"

@@ -2333,27 +2333,39 @@ hipError_t cq_launch_lean(const uint8_t* g, const cq::ScanPlan* P, const cq::Gro
                           unsigned long long* slow_list, unsigned long long slow_cap);
 hipError_t cq_launch_raw_merge(const cq::GroupTable* gt, const cq::GroupTable* rt, int nacc, cq::ScanStats* stats,
                                hipStream_t s);
+int cq_fast_eligible(const cq::ScanPlan* P, int grouped, int want_rows);
+int cq_fast_waves_per_block();
+hipError_t cq_launch_fast(const uint8_t* g, const cq::ScanPlan* P, const cq::GroupTable* gt,
+                          const cq::GroupTable* rt, cq::ScanStats* stats, int grouped, int grid, hipStream_t s,
+                          unsigned long long* slow_list, unsigned long long slow_cap);
 
-// cqgpu_set_scan_kernel(1) or CQ_SCAN_KERNEL=general: scan_kernel for every plan
-// (A/B runs, parity tests of both kernels)
+// cqgpu_set_scan_kernel / CQ_SCAN_KERNEL: 0 (default) fast_kernel, else lean_kernel,
+// else scan_kernel, by plan shape; 1 ("general"): scan_kernel for every plan; 2
+// ("lean"): never fast_kernel (A/B runs, parity tests of every kernel)
 static int g_scan_mode = -1;
-static bool lean_enabled() {
+static int scan_mode() {
     if (g_scan_mode < 0) {
         const char* v = getenv("CQ_SCAN_KERNEL");
-        g_scan_mode = (v && strcmp(v, "general") == 0) ? 1 : 0;
+        g_scan_mode = (v && strcmp(v, "general") == 0) ? 1 : ((v && strcmp(v, "lean") == 0) ? 2 : 0);
     }
-    return g_scan_mode == 0;
+    return g_scan_mode;
 }
+static bool lean_enabled() { return scan_mode() != 1; }
 int cq_set_scan_mode(int mode) {
-    lean_enabled();
-    const int old = g_scan_mode;
-    g_scan_mode = mode ? 1 : 0;
+    const int old = scan_mode();
+    g_scan_mode = mode == 1 ? 1 : (mode == 2 ? 2 : 0);
     return old;
 }
 
-// 1 when cq_launch_scan runs lean_kernel for this plan
+// 1 when cq_launch_scan runs lean_kernel or fast_kernel for this plan
 int cq_scan_uses_lean(const cq::ScanPlan* P, int with_cells) {
     return !with_cells && lean_enabled() && cq_lean_eligible(P);
+}
+// 2 when it runs fast_kernel, 1 lean_kernel, 0 scan_kernel
+int cq_scan_kernel_kind(const cq::ScanPlan* P, int grouped, int want_rows, int with_cells) {
+    if (with_cells || !lean_enabled()) return 0;
+    if (scan_mode() == 0 && cq_fast_eligible(P, grouped, want_rows)) return 2;
+    return cq_lean_eligible(P) ? 1 : 0;
 }
 
 static int device_cus() {
@@ -2381,13 +2393,15 @@ hipError_t cq_launch_scan(const uint8_t* g, const cq::ScanPlan* P, const cq::Gro
         // one 16-wave block per CU, each wave streaming its own windows
         const uint64_t hi = P->range_end < P->n ? P->range_end : P->n;
         const uint64_t wins = cq_lean_windows(P->range_begin, hi, P->lean_ws) + 1;
-        const uint64_t per = (uint64_t)cq_lean_waves_per_block();
+        const bool fast = scan_mode() == 0 && cq_fast_eligible(P, grouped, row_out != nullptr);
+        const uint64_t per = (uint64_t)(fast ? cq_fast_waves_per_block() : cq_lean_waves_per_block());
         uint64_t lg = (wins + per - 1) / per;
         if (lg > (uint64_t)device_cus()) lg = (uint64_t)device_cus();
         if (lg < 1) lg = 1;
         if ((wins + lg * per - 1) / (lg * per) < (1u << 16)) {   // first-row codes hold 16 bits of round
-            hipError_t e = cq_launch_lean(g, P, gt, rt, stats, row_out, row_cap, grouped, (int)lg, s, slow_list,
-                                          slow_cap);
+            hipError_t e = fast ? cq_launch_fast(g, P, gt, rt, stats, grouped, (int)lg, s, slow_list, slow_cap)
+                                : cq_launch_lean(g, P, gt, rt, stats, row_out, row_cap, grouped, (int)lg, s,
+                                                 slow_list, slow_cap);
             if (e != hipSuccess) return e;
             if (grouped)
                 hipLaunchKernelGGL(cq::slow_kernel<true>, dim3(256), dim3(256), 0, s, g, stats, row_out, row_cap,

@@ -18,6 +18,29 @@ import torch
 import torch.distributed as dist
 
 
+class PeerFailure(RuntimeError):
+    """A rank-local step failed on this rank or on a peer; every rank raises it
+    together, after the same collectives, so no rank is left waiting in one."""
+
+
+def agree(err, comm) -> None:
+    """One MAX all-reduce of "this rank failed": raises PeerFailure on every rank
+    when any rank's local step raised (err: that exception, or None)."""
+    flag = torch.tensor([0 if err is None else 1], dtype=torch.int32, device=comm)
+    dist.all_reduce(flag, op=dist.ReduceOp.MAX)
+    if int(flag.item()):
+        msg = f"rank {dist.get_rank()}: {err}" if err is not None else f"rank {dist.get_rank()}: a peer rank failed"
+        raise PeerFailure(msg) from err
+
+
+def _local(fn, *a):
+    """(result, None) or (None, exception) of a rank-local step"""
+    try:
+        return fn(*a), None
+    except Exception as e:  # reported to every rank by agree()
+        return None, e
+
+
 def gather_blobs(blob: bytes, device: torch.device | str = "cpu") -> list[bytes]:
     """all_gather of variable-size byte strings; every rank gets every rank's blob."""
     world = dist.get_world_size()
@@ -71,7 +94,8 @@ def scan_partitioned(ast, table, comm_device: torch.device | str | None = None):
     the other ranks.  Every rank must call it (collectives inside)."""
     import cq_amd
     comm = torch.device(comm_device) if comm_device is not None else torch.device("cuda", torch.cuda.current_device())
-    blob = cq_amd.query_partial(ast, [table])
+    blob, err = _local(cq_amd.query_partial, ast, [table])
+    agree(err, comm)
     blobs = gather_blobs(blob, comm)
     if dist.get_rank() != 0:
         return None
@@ -150,11 +174,14 @@ def dense_merge(part, device, comm_device=None):
     (the device for RCCL; "cpu" stages through host memory for a gloo group)."""
     world, rank = dist.get_world_size(), dist.get_rank()
     comm = torch.device(comm_device) if comm_device is not None else torch.device(device)
-    mine = part.keys(device)
+    mine, err = _local(part.keys, device)
+    agree(err, comm)
     n = torch.tensor([part.m], dtype=torch.int64, device=comm)
     sizes = [torch.zeros(1, dtype=torch.int64, device=comm) for _ in range(world)]
     dist.all_gather(sizes, n)
     counts = [int(x.item()) for x in sizes]                  # a few integers, not the blobs
+    if sum(counts) >= DICT_MAX_KEYS:
+        return NOT_DENSE                                     # every rank sees the same total
     kb = part.KEYREC
     mx = max(max(counts), 1) * kb
     buf = torch.zeros(mx, dtype=torch.uint8, device=comm)
@@ -164,16 +191,23 @@ def dense_merge(part, device, comm_device=None):
     all_keys = torch.cat([o[: c * kb] for o, c in zip(outs, counts)]).to(device)
     nall, off = sum(counts), sum(counts[:rank])
     _sync(device)          # the library's stream reads what torch's stream wrote
-    g = part.dict(all_keys, nall, off)
-    dsum = torch.empty(max(g * part.W, 1), dtype=torch.float64, device=device)
-    dfirst = torch.empty(max(g, 1), dtype=torch.int64, device=device)
-    drep = torch.empty(max(2 * g, 1), dtype=torch.int64, device=device)
-    part.scatter(dsum, dfirst, drep)
+
+    def local_dense():
+        g = part.dict(all_keys, nall, off)
+        ds = torch.empty(max(g * part.W, 1), dtype=torch.float64, device=device)
+        df = torch.empty(max(g, 1), dtype=torch.int64, device=device)
+        dr = torch.empty(max(2 * g, 1), dtype=torch.int64, device=device)
+        part.scatter(ds, df, dr)
+        return ds, df, dr
+    out, err = _local(local_dense)
+    agree(err, comm)
+    dsum, dfirst, drep = out
     f = dfirst.to(comm)
     dist.all_reduce(f, op=dist.ReduceOp.MIN)
     dfirst.copy_(f)
     _sync(device)
-    part.mask_reps(dfirst, drep)
+    _, err = _local(part.mask_reps, dfirst, drep)
+    agree(err, comm)
     s, r = dsum.to(comm), drep.to(comm)
     dist.reduce(s, 0, op=dist.ReduceOp.SUM)
     dist.reduce(r, 0, op=dist.ReduceOp.SUM)
@@ -185,6 +219,10 @@ def dense_merge(part, device, comm_device=None):
     return part.finish(dsum, dfirst, drep)
 
 
+DICT_MAX_KEYS = 1 << 29      # cqgpu_partial_dict's limit: more keys take the blob path
+NOT_DENSE = object()
+
+
 def scan_partitioned_dense(ast, table, comm_device=None):
     """One range-partitioned query step with the merge on the devices (config 4):
     this rank's scan keeps its groups in HBM (cqgpu_partial_new), the ranks agree
@@ -194,7 +232,8 @@ def scan_partitioned_dense(ast, table, comm_device=None):
     import cq_amd
     device = torch.device("cuda", torch.cuda.current_device())
     comm = torch.device(comm_device) if comm_device is not None else device
-    part = DensePartial(ast, table)
+    part, err = _local(DensePartial, ast, table)
+    agree(err, comm)
     try:
         ok = torch.tensor([1 if part.ok else 0], dtype=torch.int32, device=comm)
         dist.all_reduce(ok, op=dist.ReduceOp.MIN)
@@ -202,6 +241,9 @@ def scan_partitioned_dense(ast, table, comm_device=None):
             part.free()
             return scan_partitioned(ast, table, comm_device)
         tp = dense_merge(part, device, comm_device)
+        if tp is NOT_DENSE:
+            part.free()
+            return scan_partitioned(ast, table, comm_device)
         if dist.get_rank() == 0 and not tp:
             raise RuntimeError(cq_amd.last_error() or "cqgpu_partial_finish failed")
         return tp
@@ -227,18 +269,29 @@ def join_partitioned(ast, lshard, rshard, lheader: bytes, rheader: bytes, device
     comm = torch.device(comm_device) if comm_device is not None else torch.device(device)
     routed = []
     for side, (tab, header) in enumerate(((lshard, lheader), (rshard, rheader))):
-        nbytes, nrecs = cq_amd.route_plan(ast, [lshard, rshard], side, world)
+        plan, err = _local(cq_amd.route_plan, ast, [lshard, rshard], side, world)
+        agree(err, comm)
+        nbytes, nrecs = plan
         base = exclusive_base(sum(nrecs), comm)
-        sb = torch.empty(max(sum(nbytes), 1), dtype=torch.uint8, device=device)
-        sg = torch.empty(max(sum(nrecs), 1), dtype=torch.int64, device=device)
-        cq_amd.route_fill(tab, base, sb.data_ptr(), sg.data_ptr())
-        torch.cuda.synchronize(device)
+
+        def fill():
+            b = torch.empty(max(sum(nbytes), 1), dtype=torch.uint8, device=device)
+            g = torch.empty(max(sum(nrecs), 1), dtype=torch.int64, device=device)
+            cq_amd.route_fill(tab, base, b.data_ptr(), g.data_ptr())
+            torch.cuda.synchronize(device)
+            return b, g
+        out, err = _local(fill)
+        agree(err, comm)
+        sb, sg = out
         rb, _ = exchange(sb[: sum(nbytes)].to(comm), nbytes)
         rg, _ = exchange(sg[: sum(nrecs)].to(comm), nrecs)
         rb, rg = rb.to(device), rg.to(device)
         torch.cuda.synchronize(device)
-        routed.append(cq_amd.table_from_routed(rb.data_ptr(), rb.numel(), rg.data_ptr(), rg.numel(), header))
-    blob = cq_amd.query_partial(ast, routed)
+        t, err = _local(cq_amd.table_from_routed, rb.data_ptr(), rb.numel(), rg.data_ptr(), rg.numel(), header)
+        agree(err, comm)
+        routed.append(t)
+    blob, err = _local(cq_amd.query_partial, ast, routed)
+    agree(err, comm)
     blobs = gather_blobs(blob, comm)
     if rank != 0:
         return None

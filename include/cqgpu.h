@@ -104,6 +104,8 @@ cq_table* cqgpu_merge_partials(cq_node* query_ast, const void* const* blobs, con
  *   n = cqgpu_partial_keys(p, dst, &W)            n key records of 32 bytes, copied to dst (device; NULL: count only)
  *   all_gather the key records (RCCL), concatenated in rank order -> all, nall, mine = offset of ours
  *   G = cqgpu_partial_dict(p, all, nall, mine)    the global dictionary, identical on every rank
+ *                                                 (copies `all`: the caller may free it on return;
+ *                                                 nall >= 2^29 returns -1: take the blob path)
  *   cqgpu_partial_scatter(p, dsum, dfirst, drep)  dense arrays: double[G*W], int64[G] (absent:
  *                                                 0x7F7F...7F), int64[2G]
  *   all_reduce(dfirst, MIN); cqgpu_partial_mask_reps(p, dfirst, drep)
@@ -170,7 +172,7 @@ typedef struct {
     int retries;                 /* global group table regrowths */
     uint64_t slow_records;       /* records the fast field path handed to the general parser */
     uint64_t passed;             /* records that passed WHERE */
-    int scan_kernel;             /* 1 = lean_kernel (wave-autonomous), 0 = general scan_kernel */
+    int scan_kernel;             /* 2 = fast_kernel, 1 = lean_kernel (both wave-autonomous), 0 = general scan_kernel */
 } cqgpu_stats;
 int cqgpu_last_stats(cqgpu_stats* out);
 const char* cqgpu_last_error(void);
@@ -198,10 +200,10 @@ int cqgpu_explain(cq_node* query_ast, const char* header, cq_csv_config cfg, cha
  * summed over waves (all zero in the normal build) */
 int cqgpu_debug_clocks(unsigned long long* out8);
 
-/* Scan kernel choice: 0 = automatic (lean_kernel for the plan shapes it covers,
- * the general scan_kernel otherwise), 1 = always scan_kernel.  Returns the
- * previous mode.  Both produce identical results; the knob exists for A/B
- * measurements and for parity tests of both kernels. */
+/* Scan kernel choice: 0 = automatic (fast_kernel, else lean_kernel, else the
+ * general scan_kernel, by the plan shapes each covers), 1 = always scan_kernel,
+ * 2 = never fast_kernel.  Returns the previous mode.  All produce identical
+ * results; the knob exists for A/B measurements and parity tests of every kernel. */
 int cqgpu_set_scan_kernel(int mode);
 
 /* Optional fallback for plans outside the GPU subset: the reference evaluator

@@ -1,0 +1,171 @@
+"""Parity of fast_kernel (cq_amd/csrc/fast.hip) with the oracle, lean_kernel and the
+general scan_kernel on inputs aimed at its own edges.
+
+fast_kernel covers WHERE `col op numeric-literal` (or none), COUNT / SUM / AVG over
+at most two columns, and GROUP BY one column of <= 8-byte keys, with the roles'
+columns ascending.  Its own edges, on top of lean_kernel's (test_gpu_lean.py):
+  * the ',' / '"' classifier flags '&' bytes as possible quotes (whole windows then
+    take the exact quote-bitmap path) and must never miss a real quote;
+  * the LDS table is seeded from the first 256 KiB: keys that first appear later
+    are inserted by the kernel, and beyond the table's room they spill to HBM;
+  * SUM addends of <= 4 bytes are summed as exact 10^-3 fixed point, wider
+    numerals as doubles, in the same group;
+  * records the straight path cannot type (blanks, signs, short rows, 9+ byte
+    keys, long records) go whole to slow_kernel.
+Counts, group sets / order bit-exact; SUM / AVG 1e-6 relative (north_star)."""
+import numpy as np
+import pytest
+
+import cqtest
+import cq_amd
+
+pytestmark = pytest.mark.gpu
+REL = 1e-6
+
+
+def _run(sql, mode):
+    old = cq_amd.set_scan_kernel(mode)
+    try:
+        with cqtest.Parsed(sql) as ast:
+            got = cq_amd.evaluate(ast)
+        return got, cq_amd.stats(), cq_amd.last_ineligible()
+    finally:
+        cq_amd.set_scan_kernel(old)
+
+
+def _tol(sql):
+    sel = sql.split(" FROM ")[0]
+    items = [s.strip() for s in sel[len("SELECT "):].split(",")]
+    return {i for i, s in enumerate(items) if s.upper().startswith(("SUM(", "AVG("))}
+
+
+def _cmp(got, want, tol, ctx):
+    assert (got is None) == (want is None), ctx
+    if want is None:
+        return
+    assert got["columns"] == want["columns"], ctx
+    assert len(got["rows"]) == len(want["rows"]), (ctx, len(got["rows"]), len(want["rows"]))
+    for i, (g, w) in enumerate(zip(got["rows"], want["rows"])):
+        for j, (x, y) in enumerate(zip(g, w)):
+            assert cqtest.cell_equal(x, y, REL if j in tol else 0.0), f"{ctx}: row {i} col {j}: {x} vs {y}"
+
+
+def check(sql, fast=True):
+    want, unsup = cqtest.oracle_query(sql)
+    assert not unsup, sql
+    tol = _tol(sql)
+    got, st, inel = _run(sql, 0)
+    assert not inel, (sql, inel)
+    if fast:
+        assert st["scan_kernel"] == 2, (sql, "fast_kernel did not run", st)
+    _cmp(got, want, tol, "auto: " + sql)
+    lean, _, _ = _run(sql, 2)
+    _cmp(lean, want, tol, "lean: " + sql)
+    return st
+
+
+def _write(path, header, rows, term="\n"):
+    path.write_text(header + term + term.join(rows) + term)
+    return str(path)
+
+
+@pytest.fixture(scope="module")
+def d(tmp_path_factory):
+    return tmp_path_factory.mktemp("fast")
+
+
+def test_fast_bench_shape(d):
+    rng = np.random.default_rng(1)
+    rows = ["n%d,s,%d,%s,%d.%02d,role_%03d" % (i % 7, rng.integers(10, 81), "fm"[i % 2], rng.integers(1, 3),
+                                                rng.integers(0, 100), rng.integers(0, 1000)) for i in range(200_000)]
+    p = _write(d / "bench.csv", "name,surname,age,gender,height,role", rows)
+    st = check(f"SELECT role, COUNT(*), SUM(height), AVG(height) FROM '{p}' WHERE age > 30 GROUP BY role")
+    assert st["slow_records"] == 0 and st["lds_spills"] == 0, st
+    check(f"SELECT COUNT(*) FROM '{p}' WHERE age > 30")
+    check(f"SELECT COUNT(*), SUM(age), AVG(height) FROM '{p}' WHERE age <= 45.5")
+    check(f"SELECT role, COUNT(*) FROM '{p}' GROUP BY role")
+    check(f"SELECT role, SUM(age), SUM(height), AVG(age) FROM '{p}' WHERE age != 50 GROUP BY role")
+
+
+def test_fast_late_keys_and_spill(d):
+    """keys absent from the sample (first 256 KiB) and more keys than the table holds"""
+    rows = ["k%05d,%d,%d" % (i % 40, i % 13, i % 100) for i in range(60_000)]          # 40 keys seeded
+    rows += ["L%06d,%d,%d" % (i % 5000, i % 7, i % 9) for i in range(120_000)]         # 5000 late keys
+    p = _write(d / "late.csv", "a,b,c", rows)
+    st = check(f"SELECT c, COUNT(*) FROM '{p}' WHERE b >= 3 GROUP BY c")
+    st = check(f"SELECT a, COUNT(*), SUM(c) FROM '{p}' GROUP BY a")
+    assert st["lds_spills"] > 0, st
+
+
+def test_fast_quotes_and_ampersands(d):
+    """'&' looks like a quote to the ',' classifier; real quotes in front of needed fields"""
+    rng = np.random.default_rng(3)
+    rows = []
+    for i in range(50_000):
+        a = ["a&b", "plain", '"q,uoted"', "x+y", "&", '"'][rng.integers(0, 6)]
+        rows.append("%s,%d,g%d,%d.%d" % (a, rng.integers(0, 99), rng.integers(0, 30), rng.integers(0, 9),
+                                         rng.integers(0, 9)))
+    p = _write(d / "quotes.csv", "a,b,c,e", rows)
+    check(f"SELECT c, COUNT(*), SUM(e) FROM '{p}' WHERE b > 40 GROUP BY c")
+    check(f"SELECT COUNT(*), SUM(e) FROM '{p}' WHERE b < 10")
+
+
+def test_fast_numeral_shapes(d):
+    """wide and odd numerals in WHERE / SUM fields: 5-7 byte numerals, doubles, signs,
+    blanks, exponents, empty fields, dates -- typed in place or sent to slow_kernel"""
+    rng = np.random.default_rng(4)
+    shapes = ["%d" % rng.integers(0, 99), "%d.%d" % (rng.integers(0, 99), rng.integers(0, 9)), "123456",
+              "12.3456", "-5", "+7", " 8", "1e3", "", "2024-01-15", "0.001", ".5", "5.", "abc"]
+    rows = []
+    for i in range(80_000):
+        b = shapes[rng.integers(0, len(shapes))] if rng.integers(0, 4) == 0 else str(rng.integers(0, 60))
+        c = shapes[rng.integers(0, len(shapes))] if rng.integers(0, 4) == 0 else "%d.%02d" % (rng.integers(0, 9),
+                                                                                            rng.integers(0, 99))
+        rows.append("x%d,%s,%s,k%d" % (i % 3, b, c, rng.integers(0, 50)))
+    p = _write(d / "shapes.csv", "a,b,c,d", rows)
+    check(f"SELECT d, COUNT(*), SUM(c), AVG(c) FROM '{p}' WHERE b > 20 GROUP BY d")
+    check(f"SELECT COUNT(*), SUM(b), SUM(c) FROM '{p}' WHERE b <= 30.5")
+    check(f"SELECT d, COUNT(*), AVG(b) FROM '{p}' GROUP BY d")
+
+
+def test_fast_keys(d):
+    """empty keys, 8-byte keys, keys with blanks (slow), numerals as keys, CRLF; and
+    9-byte keys that appear only after the sampled bytes (the plan chose 8-byte tags:
+    those records go to slow_kernel)"""
+    rng = np.random.default_rng(5)
+    keys = ["", "abcdefgh", "k 1", "z", "12345678", "1.5", "1.50", "NULL", " z"]
+    rows = ["%d,%d,%s" % (rng.integers(0, 50), rng.integers(0, 9), keys[rng.integers(0, len(keys))])
+            for _ in range(40_000)]
+    p = _write(d / "keys.csv", "v,w,k", rows, term="\r\n")
+    check(f"SELECT k, COUNT(*), SUM(w) FROM '{p}' WHERE v > 10 GROUP BY k")
+    late = rows + ["%d,%d,%s" % (rng.integers(0, 50), rng.integers(0, 9), ["abcdefghi", "z", "toolongkey1"][i % 3])
+                   for i in range(30_000)]
+    p2 = _write(d / "latelong.csv", "v,w,k", late)
+    st = check(f"SELECT k, COUNT(*), SUM(w) FROM '{p2}' WHERE v > 10 GROUP BY k")
+    assert st["slow_records"] > 0, st
+    rows3 = ["%d,%s" % (i % 50, ["abcdefghi", "x"][i % 2]) for i in range(5000)]
+    p3 = _write(d / "long.csv", "v,k", rows3)
+    st = check(f"SELECT k, COUNT(*) FROM '{p3}' WHERE v > 10 GROUP BY k", fast=False)   # 16-byte tags: lean_kernel
+    assert st["scan_kernel"] == 1, st
+
+
+def test_fast_role_orders(d):
+    """roles in any column order and sharing columns (runtime ranks, skip 0)"""
+    rng = np.random.default_rng(6)
+    rows = ["k%d,%d,%d.%d,%d" % (rng.integers(0, 90), rng.integers(0, 99), rng.integers(0, 9), rng.integers(0, 9),
+                                 rng.integers(0, 5)) for _ in range(60_000)]
+    p = _write(d / "orders.csv", "a,b,c,e", rows)
+    check(f"SELECT a, COUNT(*), SUM(c) FROM '{p}' WHERE e > 1 GROUP BY a")       # GROUP first
+    check(f"SELECT e, COUNT(*), SUM(b), AVG(b) FROM '{p}' WHERE b > 20 GROUP BY e")   # WHERE = SUM column
+    check(f"SELECT b, SUM(c), SUM(b) FROM '{p}' WHERE c < 4.5 GROUP BY b")         # GROUP = SUM column
+    check(f"SELECT COUNT(*), SUM(e), SUM(b) FROM '{p}' WHERE c >= 2")                # SUM columns reversed
+
+
+def test_fast_not_for_other_shapes(d):
+    rows = ["%d,%d,k%d" % (i % 9, i % 4, i % 3) for i in range(1000)]
+    p = _write(d / "other.csv", "a,b,c", rows)
+    # a STRING literal in WHERE and row-returning SELECTs are lean_kernel's shapes
+    st = check(f"SELECT c, COUNT(*) FROM '{p}' WHERE c != 'x' GROUP BY c", fast=False)
+    assert st["scan_kernel"] != 2, st
+    st = check(f"SELECT a, b FROM '{p}' WHERE b > 1", fast=False)
+    assert st["scan_kernel"] != 2, st

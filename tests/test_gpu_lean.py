@@ -1,5 +1,6 @@
-"""Parity of lean_kernel (cq_amd/csrc/lean.hip), the wave-autonomous scan, with the
-oracle -- and with the general scan_kernel -- on inputs aimed at its edges.
+"""Parity of the wave-autonomous scans -- fast_kernel (cq_amd/csrc/fast.hip) where the
+plan has its shape, lean_kernel (lean.hip) forced, and the general scan_kernel --
+with the oracle on inputs aimed at their edges.
 
 lean_kernel splits the file into 2 KiB windows, one wave each, and sees only the
 first 64 bytes of a record through its separator bitmaps; records it cannot type
@@ -130,9 +131,12 @@ def _check(sql):
     want, unsup = cqtest.oracle_query(sql)
     assert not unsup, sql
     tol = _tol(sql)
-    lean, st, inel = _run(sql, 0)
+    auto, st, inel = _run(sql, 0)                 # fast_kernel where the plan has its shape
     assert not inel, (sql, inel)
-    assert st["scan_kernel"] == 1, (sql, "lean_kernel did not run")
+    assert st["scan_kernel"] in (1, 2), (sql, "neither fast_kernel nor lean_kernel ran")
+    _cmp(auto, want, tol, "auto: " + sql)
+    lean, st1, _ = _run(sql, 2)                   # lean_kernel forced
+    assert st1["scan_kernel"] == 1, (sql, "lean_kernel did not run")
     _cmp(lean, want, tol, "lean: " + sql)
     general, st2, _ = _run(sql, 1)
     assert st2["scan_kernel"] == 0
@@ -184,7 +188,7 @@ def test_lean_resident_rescans(files):
     try:
         with cqtest.Parsed(sql) as ast:
             ref = cq_amd.query(ast, [t])
-            for mode in (0, 1, 0):
+            for mode in (0, 1, 2, 0):
                 old = cq_amd.set_scan_kernel(mode)
                 got = cq_amd.query(ast, [t])
                 cq_amd.set_scan_kernel(old)
