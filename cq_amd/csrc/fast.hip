@@ -64,8 +64,9 @@ struct WaveLds {
 static_assert(sizeof(WaveLds) % 16 == 0, "16-byte aligned wave areas");
 
 struct FastPlan {
-    uint64_t lo_ok, hi_ok;      // records starting in [lo_ok, hi_ok) are owned by this launch
-    uint64_t first_win, last_win;
+    uint64_t first_win;         // the first window holding an owned record start
+    uint32_t nwin;              // windows [first_win, first_win + nwin) hold the owned starts
+    uint32_t lo_s, hi_s;        // owned starts: from lo_s in the first window, below hi_s in the last
     uint32_t ws;                // window stride (multiple of 128, <= WS)
     uint32_t delim, quote;
     uint32_t skip[4];           // field k's column minus field k-1's (field 0: its column); fields = the
@@ -88,47 +89,67 @@ constexpr uint32_t GK_RAW = 6;       // raw field bytes as key (lean.hip's class
 // ------------------------------------------------------------------ helpers
 __device__ __forceinline__ uint32_t ctz64(uint64_t x) { return (uint32_t)__builtin_ctzg(x, 64); }
 
-__device__ __forceinline__ void load_win(const uint8_t* g, uint64_t w, uint32_t ws, uint32_t lds, uint32_t& prev) {
+// The window's 4 KiB straight into the wave's LDS bytes by four LDS-DMA loads, 1 KiB
+// each (lane l's 16 bytes at 16l), addressed by a scalar base plus the lane's constant
+// offset `voff` (16 * lane), so the window costs no vector address arithmetic.  The
+// caller waits with vmcnt(0); the lgkmcnt(0) first retires this wave's LDS reads of the
+// window the loads overwrite.  M0 (the LDS base of an LDS-DMA load) is set and restored
+// inside the statement (the compiler owns M0).
+__device__ __forceinline__ void load_win(const uint8_t* g, uint64_t w, uint32_t ws, uint32_t lds, uint32_t voff,
+                                         uint32_t& prev) {
     const uint8_t* base = g + w * ws;
-    const int lane = threadIdx.x & 63;
     asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
 #pragma unroll
     for (int i = 0; i < 4; i++) {
         uint32_t keep;
-        asm volatile("s_mov_b32 %0, m0\n\ts_mov_b32 m0, %2\n\ts_nop 0\n\tglobal_load_lds_dwordx4 %1, off\n\ts_mov_b32 m0, %0"
+        asm volatile("s_mov_b32 %0, m0\n\ts_mov_b32 m0, %3\n\ts_nop 0\n\tglobal_load_lds_dwordx4 %1, %2\n\ts_mov_b32 m0, %0"
                      : "=&s"(keep)
-                     : "v"(base + 1024 * i + 16 * lane), "s"(lds + 1024u * i)
+                     : "v"(voff), "s"(base + 1024 * i), "s"(lds + 1024u * i)
                      : "memory");
     }
     const __amdgpu_buffer_rsrc_t r = __builtin_amdgcn_make_buffer_rsrc((void*)(base - 4), 0, 4, 0x00020000);
     prev = __builtin_amdgcn_raw_buffer_load_b32(r, 0, 0, 0);
 }
 
-__device__ __forceinline__ uint32_t flags40(uint32_t r) { return __builtin_amdgcn_bitop3_b32(r, r >> 1, 0x40404040u, 0x20); }
+// A VGPR-resident copy of a (uniform or constant) value: on gfx950 a VALU instruction
+// reading an SGPR operand issues at half rate, and VOP3 instructions cannot take a
+// literal, so the constants of the hot VOP3 operations live in VGPRs
+__device__ __forceinline__ uint32_t vreg(uint32_t x) {
+    asm volatile("" : "+v"(x));
+    return x;
+}
+// the classifier's constants (VGPRs)
+struct CK {
+    uint32_t tn1, tn0, td1, td0;   // v_perm tables: terminators, delimiter
+    uint32_t m40;                  // 0x40404040
+    uint32_t w0, w1;               // v_dot4 bit weights
+    uint32_t rd, rq;               // delimiter / quote bytes x 4 (non-COMMA)
+};
+__device__ __forceinline__ uint32_t flags40(uint32_t r, uint32_t m40) { return __builtin_amdgcn_bitop3_b32(r, r >> 1, m40, 0x20); }
 
 // 32 bytes -> separator and terminator bits; quote presence accumulated in q
 // (COMMA: the delimiter lookup's zero bytes, else the quote byte's zero test)
 template <bool COMMA>
-__device__ __forceinline__ void classify32(const v4u a, const v4u b, uint32_t rep_d, uint32_t rep_q, uint32_t& sep,
-                                           uint32_t& nl, uint32_t& q) {
+__device__ __forceinline__ void classify32(const v4u a, const v4u b, const CK& k, uint32_t& sep, uint32_t& nl,
+                                           uint32_t& q) {
     uint32_t ud[4], un[4];
 #pragma unroll
     for (int j = 0; j < 8; j++) {
         const uint32_t x = j < 4 ? a[j & 3] : b[j & 3];
-        const uint32_t rn = __builtin_amdgcn_perm(0x00004000u, 0x00400000u, x ^ 0x08080808u);
+        const uint32_t rn = __builtin_amdgcn_perm(k.tn1, k.tn0, x ^ 0x08080808u);
         uint32_t rd;
         if (COMMA) {
             // x ^ '*': ',' -> 6 (0x40); '"' -> 8 = sign of table byte 1 (0x20) -> 0x00; '&' -> 12 -> 0x00;
             // '+' -> 1 (0x20); the other selectors 0-7 -> 0x80, 9-11 -> signs of 0x80 bytes, >= 13 -> 0xFF
-            rd = __builtin_amdgcn_perm(0x80408080u, 0x80802080u, x ^ 0x2A2A2A2Au);
+            rd = __builtin_amdgcn_perm(k.td1, k.td0, x ^ 0x2A2A2A2Au);
             q = __builtin_amdgcn_bitop3_b32(rd - 0x01010101u, rd, q, 0xBA);   // (t & ~rd) | q
         } else {
-            rd = __builtin_amdgcn_perm(0u, 0x00000040u, x ^ rep_d);
-            const uint32_t t = x ^ rep_q;
+            rd = __builtin_amdgcn_perm(k.td1, k.td0, x ^ k.rd);
+            const uint32_t t = x ^ k.rq;
             q = __builtin_amdgcn_bitop3_b32(t - 0x01010101u, t, q, 0xBA);
         }
-        const uint32_t fd = flags40(rd), fn = flags40(rn);
-        const uint32_t w = (j & 1) ? 0x80402010u : 0x08040201u;
+        const uint32_t fd = flags40(rd, k.m40), fn = flags40(rn, k.m40);
+        const uint32_t w = (j & 1) ? k.w1 : k.w0;
         if (j & 1) {
             ud[j >> 1] = __builtin_amdgcn_udot4(fd, w, ud[j >> 1], false);
             un[j >> 1] = __builtin_amdgcn_udot4(fn, w, un[j >> 1], false);
@@ -362,8 +383,19 @@ __global__ __launch_bounds__(LT) void fast_kernel(const uint8_t* __restrict__ g,
         skip[k] = __builtin_amdgcn_readfirstlane(fp.skip[k]);
         rk[k] = __builtin_amdgcn_readfirstlane(fp.rank[k]);
     }
-    const uint32_t rep_d = fp.delim * 0x01010101u, rep_q = fp.quote * 0x01010101u;
-    const uint64_t lo_ok = fp.lo_ok, hi_ok = fp.hi_ok, last_win = fp.last_win, first_win = fp.first_win;
+    const uint32_t rep_q = fp.quote * 0x01010101u;
+    CK ck;
+    ck.tn1 = vreg(0x00004000u);
+    ck.tn0 = vreg(0x00400000u);
+    ck.td1 = vreg(COMMA ? 0x80408080u : 0u);
+    ck.td0 = vreg(COMMA ? 0x80802080u : 0x40u);
+    ck.m40 = vreg(0x40404040u);
+    ck.w0 = vreg(0x08040201u);
+    ck.w1 = vreg(0x80402010u);
+    ck.rd = vreg(fp.delim * 0x01010101u);
+    ck.rq = vreg(rep_q);
+    const uint64_t first_win = fp.first_win;
+    const uint32_t nwin = __builtin_amdgcn_readfirstlane(fp.nwin);
     const uint32_t wsb = __builtin_amdgcn_readfirstlane(fp.ws);
     const bool pass_null = __builtin_amdgcn_readfirstlane(fp.pass_null) != 0;
     const int wlo = __builtin_amdgcn_readfirstlane(fp.wlo), whi = __builtin_amdgcn_readfirstlane(fp.whi);
@@ -371,28 +403,32 @@ __global__ __launch_bounds__(LT) void fast_kernel(const uint8_t* __restrict__ g,
     const double wl = fp.wl;
     const int nacc = __builtin_amdgcn_readfirstlane(fp.nacc);
     const uint32_t acc1 = __builtin_amdgcn_readfirstlane(fp.acc1);
-    const uint64_t wstep = (uint64_t)gridDim.x * NWV;
+    const uint32_t wstep = gridDim.x * NWV;
+    // interior windows own the records starting in their first ws bytes: the lanes below ws / 64
+    const uint32_t lane_full = (uint32_t)lane * LB < wsb ? ~0u : 0u;
 
     uint32_t my_cnt = 0;                       // ungrouped partials (per lane)
-    unsigned long long my_first = ~0ULL;
+    uint32_t my_first = NOFIRST;               // first-row code (round, wave, window offset)
     unsigned long long my_fix[MAXS] = {0ull, 0ull};
     double my_dbl[MAXS] = {0.0, 0.0};
     uint32_t my_num[MAXS] = {0u, 0u};
     uint32_t v_rec = 0, v_pass = 0, v_spill = 0;
 
     uint32_t prev_next = 0;
+    const uint32_t voff = vreg(16u * (uint32_t)lane);
     const uint32_t wlds = __builtin_amdgcn_readfirstlane(
         (uint32_t)(uintptr_t)(__attribute__((address_space(3))) uint8_t*)W.bytes);
-    uint64_t w = first_win + (uint64_t)blockIdx.x * NWV + wv;
-    if (w < last_win) load_win(g, w, wsb, wlds, prev_next);
-    for (uint32_t round = 0; w < last_win; round++, w += wstep) {
-        const uint64_t ws = w * wsb;
+    // window i (0 .. nwin - 1) of the range: file window first_win + i
+    uint32_t i = blockIdx.x * NWV + wv;
+    if (i < nwin) load_win(g, first_win + i, wsb, wlds, voff, prev_next);
+    for (uint32_t round = 0; i < nwin; round++, i += wstep) {
+        const uint32_t fcw = (round << 16) | ((uint32_t)wv << 12);   // first-row code of this window
         asm volatile("s_waitcnt vmcnt(0)" ::: "memory");   // the window's bytes are in LDS
         const uint32_t prevw = prev_next;
         bool issued = false;
 #define FAST_ISSUE()                                                               \
     do {                                                                           \
-        if (!issued && w + wstep < last_win) load_win(g, w + wstep, wsb, wlds, prev_next); \
+        if (!issued && i + wstep < nwin) load_win(g, first_win + i + wstep, wsb, wlds, voff, prev_next); \
         issued = true;                                                             \
     } while (0)
 
@@ -401,8 +437,8 @@ __global__ __launch_bounds__(LT) void fast_kernel(const uint8_t* __restrict__ g,
 #pragma unroll
         for (int i = 0; i < 4; i++) la[i] = ((const v4u*)W.bytes)[4 * lane + i];
         uint32_t sep0, nl0, sep1, nl1, qf = 0;
-        classify32<COMMA>(la[0], la[1], rep_d, rep_q, sep0, nl0, qf);
-        classify32<COMMA>(la[2], la[3], rep_d, rep_q, sep1, nl1, qf);
+        classify32<COMMA>(la[0], la[1], ck, sep0, nl0, qf);
+        classify32<COMMA>(la[2], la[3], ck, sep1, nl1, qf);
         const bool wq = __ballot((qf & 0x80808080u) != 0) != 0;   // window may hold a quote (uniform)
         if (wq) {
             W.qt[2 * lane] = quote_bits(la[0], la[1], rep_q);
@@ -415,22 +451,26 @@ __global__ __launch_bounds__(LT) void fast_kernel(const uint8_t* __restrict__ g,
         const uint32_t pb = prevw >> 24;
         const uint32_t prevnl = lane == 0 ? (uint32_t)(pb == '\n' || pb == '\r') : prev_top;
         uint64_t todo = ~nl & ((nl << 1) | prevnl);
-        {
-            const uint64_t lo64 = (lo_ok > ws ? lo_ok : ws) - ws;
-            const uint64_t hi64 = hi_ok < ws + wsb ? hi_ok : ws + wsb;
-            const uint32_t lo_s = (uint32_t)(lo64 < (uint64_t)wsb ? lo64 : (uint64_t)wsb);
-            const uint32_t hi_s = hi64 > ws ? (uint32_t)(hi64 - ws) : 0u;
+        if (i == 0 || i == nwin - 1) {                      // the range's first / last window: clip
+            const uint32_t lo_s = i == 0 ? fp.lo_s : 0u, hi_s = i == nwin - 1 ? fp.hi_s : wsb;
             const uint32_t b0 = (uint32_t)lane * LB;
             const uint32_t a = lo_s > b0 ? lo_s - b0 : 0u, e = hi_s > b0 ? hi_s - b0 : 0u;
             const uint64_t keep_lo = a >= 64 ? 0ull : (~0ull << a);
             const uint64_t keep_hi = e >= 64 ? ~0ull : ((1ull << e) - 1);
             todo &= keep_lo & keep_hi;
+        } else {
+            todo &= ((uint64_t)lane_full << 32) | lane_full;
         }
         const uint32_t xs0 = (uint32_t)__builtin_amdgcn_update_dpp(0, (int)sep0, 0x130, 0xf, 0xf, true);
         const uint32_t xs1 = (uint32_t)__builtin_amdgcn_update_dpp(0, (int)sep1, 0x130, 0xf, 0xf, true);
         const uint32_t xn0 = (uint32_t)__builtin_amdgcn_update_dpp(0, (int)nl0, 0x130, 0xf, 0xf, true);
         const uint32_t xn1 = (uint32_t)__builtin_amdgcn_update_dpp(0, (int)nl1, 0x130, 0xf, 0xf, true);
 
+#if defined(FAST_PROF) && FAST_PROF == 1      // profiling build: load + classify + record starts only
+        v_rec += (uint32_t)__popcll(todo) + ((xs0 ^ xs1 ^ xn0 ^ xn1) & 1);
+        FAST_ISSUE();
+        continue;
+#endif
         while (__any(todo != 0)) {
             // ---- two records of this lane
             uint32_t p[2], fst[2][4], fen[2][4];
@@ -519,6 +559,11 @@ __global__ __launch_bounds__(LT) void fast_kernel(const uint8_t* __restrict__ g,
                 }
             }
 
+#if defined(FAST_PROF) && FAST_PROF == 2      // + record views and the field walk
+            v_rec += (wst[0] ^ sst[1][0] ^ gen[0] ^ gst[1] ^ (uint32_t)fail[0] ^ (uint32_t)fail[1]) & 1;
+            if (last_pass) FAST_ISSUE();
+            continue;
+#endif
             // ---- field bytes (one batch of LDS reads)
             uint32_t wd[2], sd[2][MAXS], k0[2], k1[2];
 #pragma unroll
@@ -632,6 +677,10 @@ __global__ __launch_bounds__(LT) void fast_kernel(const uint8_t* __restrict__ g,
                 }
             }
             if (last_pass) FAST_ISSUE();                             // the window's bytes are read
+#if defined(FAST_PROF) && FAST_PROF == 3      // + field loads, typing, keys and hashes
+            v_rec += (hb[0] ^ hb[1] ^ (uint32_t)pass[0] ^ (uint32_t)fail[1] ^ (uint32_t)sfix[0][0]) & 1;
+            continue;
+#endif
 
             // ---- declined records go whole to slow_kernel
 #pragma unroll
@@ -643,8 +692,8 @@ __global__ __launch_bounds__(LT) void fast_kernel(const uint8_t* __restrict__ g,
                     if (lane == 0) base = atomicAdd(&stats->slow_records, (unsigned long long)__popcll(sb));
                     base = __shfl(base, 0, 64);
                     if (slow) {
-                        const unsigned long long i = base + __popcll(sb & ((1ULL << lane) - 1));
-                        if (i < slow_cap) slow_list[i] = ws + p[u];
+                        const unsigned long long si = base + __popcll(sb & ((1ULL << lane) - 1));
+                        if (si < slow_cap) slow_list[si] = (first_win + i) * wsb + p[u];
                     }
                 }
                 const bool ok = valid[u] & !fail[u];
@@ -657,9 +706,8 @@ __global__ __launch_bounds__(LT) void fast_kernel(const uint8_t* __restrict__ g,
             if (!GROUPED) {
 #pragma unroll
                 for (int u = 0; u < 2; u++) {
-                    const uint64_t off = ws + p[u];
                     my_cnt += pass[u] ? 1u : 0u;
-                    my_first = pass[u] && off < my_first ? off : my_first;
+                    my_first = pass[u] ? min(my_first, fcw | p[u]) : my_first;
 #pragma unroll
                     for (int j = 0; j < NS; j++) {
                         const bool on = pass[u] & snum[u][j];
@@ -682,6 +730,9 @@ __global__ __launch_bounds__(LT) void fast_kernel(const uint8_t* __restrict__ g,
                     s = t2 == tag[u] ? (int)(2 * b2) : s;
                     s = t1 == tag[u] ? (int)(2 * b1 + 1) : s;
                     s = t0 == tag[u] ? (int)(2 * b1) : s;
+#ifdef FAST_NOLOOKUP                                          // experiment: no table reads
+                    s = (int)(hb[u] & (TSLOTS - 1));
+#endif
                     slot[u] = hspill[u] ? -1 : s;
                     miss[u] = pass[u] & (s < 0) & !hspill[u];
                 }
@@ -702,12 +753,15 @@ __global__ __launch_bounds__(LT) void fast_kernel(const uint8_t* __restrict__ g,
                 for (int u = 0; u < 2; u++) {
                     const bool add = pass[u] & (slot[u] >= 0);
                     if (add) {
-                        const uint32_t fc = (round << 16) | ((uint32_t)wv << 12) | p[u];
-                        atomicAdd(&tcnt[slot[u]], 1u);
-                        atomicMin(&tfirst[slot[u]], fc);
+                        const uint32_t fc = fcw | p[u];
+#ifndef FAST_ATOM
+#define FAST_ATOM 7                                                  // experiment: which LDS atomics run
+#endif
+                        if (FAST_ATOM & 1) atomicAdd(&tcnt[slot[u]], 1u);
+                        if (FAST_ATOM & 2) atomicMin(&tfirst[slot[u]], fc);
 #pragma unroll
                         for (int j = 0; j < NS; j++) {
-                            if (snum[u][j]) {
+                            if (snum[u][j] && (FAST_ATOM & 4)) {
                                 if (sfx[u][j]) atomicAdd(&tfix[j][slot[u]], (unsigned long long)sfix[u][j]);
                                 else if (NS == 1) atomicAdd(&tdbl[j][slot[u]], sdbl[u][j]);
                             }
@@ -728,7 +782,7 @@ __global__ __launch_bounds__(LT) void fast_kernel(const uint8_t* __restrict__ g,
                             bool n0 = false, n1 = false;
                             if (NS > 0) { n0 = snum[u][0]; v0 = sfx[u][0] ? sfix[u][0] / 1000.0 : sdbl[u][0]; }
                             if (NS > 1) { n1 = snum[u][1]; v1 = sfx[u][1] ? sfix[u][1] / 1000.0 : sdbl[u][1]; }
-                            spill8(tag[u], ws + p[u], tabs, stats, nacc, acc1, n0, v0, n1, v1);
+                            spill8(tag[u], (first_win + i) * wsb + p[u], tabs, stats, nacc, acc1, n0, v0, n1, v1);
                         }
                     }
                 }
@@ -755,14 +809,15 @@ __global__ __launch_bounds__(LT) void fast_kernel(const uint8_t* __restrict__ g,
     }
 
     if (!GROUPED) {
-        unsigned long long c = my_cnt, f = my_first;
+        unsigned long long c = my_cnt;
+        uint32_t f = my_first;
         double sm[MAXS];
         unsigned long long nm[MAXS];
 #pragma unroll
         for (int j = 0; j < MAXS; j++) { sm[j] = (double)my_fix[j] / 1000.0 + my_dbl[j]; nm[j] = my_num[j]; }
         for (int o = 32; o > 0; o >>= 1) {
             c += __shfl_down(c, o, 64);
-            const unsigned long long ff = __shfl_down(f, o, 64);
+            const uint32_t ff = __shfl_down(f, o, 64);
             f = ff < f ? ff : f;
 #pragma unroll
             for (int j = 0; j < MAXS; j++) {
@@ -777,7 +832,10 @@ __global__ __launch_bounds__(LT) void fast_kernel(const uint8_t* __restrict__ g,
             const int gi = g_insert(gt, k, 0x12345678ULL, stats);
             if (gi >= 0) {
                 if (c) atomicAdd(&gt.cnt[gi], c);
-                if (f != ~0ULL) atomicMin(&gt.first[gi], f);
+                if (f != NOFIRST) {
+                    const uint64_t fw = first_win + ((uint64_t)(f >> 16) * gridDim.x + blockIdx.x) * NWV + ((f >> 12) & 15);
+                    atomicMin(&gt.first[gi], (unsigned long long)(fw * wsb + (f & 4095)));
+                }
                 for (int a = 0; a < nacc; a++) {
                     const bool j1 = (acc1 >> a) & 1;
                     const double sa = j1 ? sm[MAXS - 1] : sm[0];
@@ -967,12 +1025,17 @@ hipError_t cq_launch_fast(const uint8_t* g, const cq::ScanPlan* P, const cq::Gro
     if (!fast_shape(P, grouped, &fp, &ns, &where, &canon)) return hipErrorInvalidValue;
     if (((uintptr_t)g & 255) != 0) return hipErrorInvalidValue;
     const uint64_t hi = P->range_end < P->n ? P->range_end : P->n;
-    fp.lo_ok = P->data_begin > P->range_begin ? P->data_begin : P->range_begin;
-    fp.hi_ok = hi;
+    const uint64_t lo = P->data_begin > P->range_begin ? P->data_begin : P->range_begin;
     fp.ws = P->lean_ws ? P->lean_ws : (uint32_t)fast::WS;
     if (fp.ws > (uint32_t)fast::WS || fp.ws % 128) return hipErrorInvalidValue;
-    fp.first_win = P->range_begin / fp.ws;
-    fp.last_win = (hi + fp.ws - 1) / fp.ws;
+    if (hi > lo) {
+        const uint64_t wl = lo / fp.ws, wh = (hi - 1) / fp.ws;
+        if (wh - wl + 1 >= (1ull << 31)) return hipErrorInvalidValue;
+        fp.first_win = wl;
+        fp.nwin = (uint32_t)(wh - wl + 1);
+        fp.lo_s = (uint32_t)(lo - wl * fp.ws);
+        fp.hi_s = (uint32_t)(hi - wh * fp.ws);
+    }
     fp.seed = grouped ? (const unsigned long long*)(uintptr_t)P->fast_seed : nullptr;
     static GroupTable* tabs_dev[64];
     int dev = 0;

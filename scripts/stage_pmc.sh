@@ -24,7 +24,7 @@ nb = d["config"]["bytes_per_gpu"]; wins = nb / 3968.0
 tot = collections.defaultdict(lambda: collections.defaultdict(float))
 for f in glob.glob(f"{out}/pmc_{v}/**/*counter_collection.csv", recursive=True):
     for r in csv.DictReader(open(f)):
-        if "lean_kernel" in r["Kernel_Name"]:
+        if "lean_kernel" in r["Kernel_Name"] or "fast_kernel" in r["Kernel_Name"]:
             tot[r["Counter_Name"]][r["Dispatch_Id"]] += float(r["Counter_Value"])
 a = {c: sum(x.values()) / len(x) / wins for c, x in tot.items()}
 wc = a.get("SQ_WAVE_CYCLES", 1)
