@@ -87,7 +87,18 @@ __device__ GroupTable g_fast_tabs[2];
 constexpr uint32_t GK_RAW = 6;       // raw field bytes as key (lean.hip's class)
 
 // ------------------------------------------------------------------ helpers
-__device__ __forceinline__ uint32_t ctz64(uint64_t x) { return (uint32_t)__builtin_ctzg(x, 64); }
+// trailing zeros of x, or >= 64 (0xFFFFFFFF) when x == 0: v_ffbl of each half (all
+// ones for a zero half), the high half's index | 32, the smaller (v_ffbl as written:
+// the compiler's cttz lowering adds zero tests)
+__device__ __forceinline__ uint32_t ffbl(uint32_t x) {
+    uint32_t r;
+    asm("v_ffbl_b32 %0, %1" : "=v"(r) : "v"(x));
+    return r;
+}
+__device__ __forceinline__ uint32_t ctz64(uint64_t x) {
+    const uint32_t lo = ffbl((uint32_t)x), hi = ffbl((uint32_t)(x >> 32)) | 32u;
+    return lo < hi ? lo : hi;
+}
 
 // The window's 4 KiB straight into the wave's LDS bytes by four LDS-DMA loads, 1 KiB
 // each (lane l's 16 bytes at 16l), addressed by a scalar base plus the lane's constant
@@ -179,11 +190,11 @@ __device__ __forceinline__ uint32_t quote_bits(const v4u a, const v4u b, uint32_
     return m;
 }
 
-// 64 bits from bit b (< 64) of the 128 bits w0 | w1 << 32 | w2 << 64 | w3 << 96
-__device__ __forceinline__ uint64_t view128(uint32_t w0, uint32_t w1, uint32_t w2, uint32_t w3, uint32_t b) {
-    const bool hi = b >= 32;
-    const uint32_t sh = b & 31, a = hi ? w1 : w0, c = hi ? w2 : w1, d = hi ? w3 : w2;
-    return (uint64_t)__builtin_amdgcn_alignbit(c, a, sh) | ((uint64_t)__builtin_amdgcn_alignbit(d, c, sh) << 32);
+// 64 bits from bit b (< 64) of the 128 bits lo | hi << 64, given hi2 = hi << 1 and
+// nb = 63 - b: two 64-bit shifts and an or (the view of both bit planes of a record
+// shares nb)
+__device__ __forceinline__ uint64_t view128(uint64_t lo, uint64_t hi2, uint32_t b, uint32_t nb) {
+    return (lo >> b) | (hi2 << nb);
 }
 __device__ __forceinline__ uint64_t qview(const WaveLds& W, uint32_t p) {
     const uint32_t wi = p >> 5, sh = p & 31;
@@ -320,11 +331,16 @@ __device__ __forceinline__ uint8_t* carve(uint8_t*& q, size_t bytes) {
     return r;
 }
 
+// A slot's accumulators, one 32-byte record (one address for all of a record's LDS
+// atomics): COUNT, first-row code, per SUM argument the fixed-point sum (10^-3) and the
+// non-numeric count; with one SUM argument a double sum for the addends outside the
+// fixed-point path (two SUM arguments: such addends take the HBM table)
+constexpr uint32_t SLOT_BYTES = 32;
+enum SlotOff : uint32_t { SO_CNT = 0, SO_FIRST = 4, SO_FIX0 = 8, SO_FIX1 = 16, SO_DBL = 16, SO_MISS0 = 24, SO_MISS1 = 28 };
 template <int NS>
 constexpr uint32_t table_bytes(bool grouped) {
-    // tags, COUNT, first row; per SUM argument the fixed-point sum and the non-numeric
-    // count; one double sum only with one SUM argument (two would not fit the LDS)
-    return grouped ? TSLOTS * (8u + 4u + 4u + (uint32_t)NS * (8u + 4u) + (NS == 1 ? 8u : 0u)) : 0u;
+    // the tags, and a 32-byte slot record (see SlotOff) per slot
+    return grouped ? TSLOTS * (8u + SLOT_BYTES) : 0u;
 }
 constexpr uint32_t fixed_bytes() { return (uint32_t)(sizeof(WaveLds) * NWV); }
 
@@ -339,38 +355,26 @@ __global__ __launch_bounds__(LT) void fast_kernel(const uint8_t* __restrict__ g,
                                                   const GroupTable* __restrict__ tabs) {
     extern __shared__ __align__(16) uint8_t smem[];
     uint8_t* q = smem;
+    // LDS table: slot records first (LDS address 0: field offsets fold into the
+    // atomics), then the tags (bucket b = slots 2b, 2b + 1), then the wave windows
+    uint8_t* S = nullptr;
+    unsigned long long* T = nullptr;
+    if (GROUPED) {
+        S = carve(q, TSLOTS * SLOT_BYTES);
+        T = (unsigned long long*)carve(q, TSLOTS * 8);
+    }
     WaveLds* waves = (WaveLds*)carve(q, sizeof(WaveLds) * NWV);
     const int tid = threadIdx.x, lane = tid & 63;
     const int wv = __builtin_amdgcn_readfirstlane(tid >> 6);
     WaveLds& W = waves[wv];
-    // LDS table (structure of arrays)
-    unsigned long long* T = nullptr;     // tags, bucket b = slots 2b, 2b + 1
-    uint32_t* tcnt = nullptr;
-    uint32_t* tfirst = nullptr;
-    unsigned long long* tfix[MAXS] = {nullptr, nullptr};   // SUM in units of 10^-3 (exact)
-    double* tdbl[MAXS] = {nullptr, nullptr};               // SUM addends outside the fixed-point path
-    uint32_t* tmiss[MAXS] = {nullptr, nullptr};            // non-numeric SUM arguments
     if (GROUPED) {
-        T = (unsigned long long*)carve(q, TSLOTS * 8);
-        tcnt = (uint32_t*)carve(q, TSLOTS * 4);
-        tfirst = (uint32_t*)carve(q, TSLOTS * 4);
-#pragma unroll
-        for (int s = 0; s < NS; s++) {
-            tfix[s] = (unsigned long long*)carve(q, TSLOTS * 8);
-            if (NS == 1) tdbl[s] = (double*)carve(q, TSLOTS * 8);
-            tmiss[s] = (uint32_t*)carve(q, TSLOTS * 4);
-        }
         const unsigned long long* seed = fp.seed;
         for (uint32_t i = tid; i < TSLOTS; i += LT) {
             T[i] = seed ? seed[i] : 0ull;
-            tcnt[i] = 0;
-            tfirst[i] = NOFIRST;
+            uint32_t* r = (uint32_t*)(S + i * SLOT_BYTES);
 #pragma unroll
-            for (int s = 0; s < NS; s++) {
-                tfix[s][i] = 0;
-                if (NS == 1) tdbl[s][i] = 0.0;
-                tmiss[s][i] = 0;
-            }
+            for (int w = 0; w < 8; w++) r[w] = 0u;
+            r[SO_FIRST / 4] = NOFIRST;
         }
         __syncthreads();
     }
@@ -412,7 +416,7 @@ __global__ __launch_bounds__(LT) void fast_kernel(const uint8_t* __restrict__ g,
     unsigned long long my_fix[MAXS] = {0ull, 0ull};
     double my_dbl[MAXS] = {0.0, 0.0};
     uint32_t my_num[MAXS] = {0u, 0u};
-    uint32_t v_rec = 0, v_pass = 0, v_spill = 0;
+    uint32_t n_rec = 0, n_pass = 0, n_spill = 0;   // wave totals (uniform)
 
     uint32_t prev_next = 0;
     const uint32_t voff = vreg(16u * (uint32_t)lane);
@@ -465,63 +469,72 @@ __global__ __launch_bounds__(LT) void fast_kernel(const uint8_t* __restrict__ g,
         const uint32_t xs1 = (uint32_t)__builtin_amdgcn_update_dpp(0, (int)sep1, 0x130, 0xf, 0xf, true);
         const uint32_t xn0 = (uint32_t)__builtin_amdgcn_update_dpp(0, (int)nl0, 0x130, 0xf, 0xf, true);
         const uint32_t xn1 = (uint32_t)__builtin_amdgcn_update_dpp(0, (int)nl1, 0x130, 0xf, 0xf, true);
+        const uint64_t sep64 = (uint64_t)sep0 | ((uint64_t)sep1 << 32);
+        const uint64_t xsep2 = ((uint64_t)xs0 | ((uint64_t)xs1 << 32)) << 1;   // the next lane's bits, << 1
+        const uint64_t xnl2 = ((uint64_t)xn0 | ((uint64_t)xn1 << 32)) << 1;
 
 #if defined(FAST_PROF) && FAST_PROF == 1      // profiling build: load + classify + record starts only
-        v_rec += (uint32_t)__popcll(todo) + ((xs0 ^ xs1 ^ xn0 ^ xn1) & 1);
+        n_rec += (uint32_t)__popcll(__ballot(((uint32_t)__popcll(todo) + ((xs0 ^ xs1 ^ xn0 ^ xn1) & 1)) & 1));
         FAST_ISSUE();
         continue;
 #endif
         while (__any(todo != 0)) {
             // ---- two records of this lane
-            uint32_t p[2], fst[2][4], fen[2][4];
+            uint32_t p[2], fst[2][4], fen[2][4], e[2];
+            uint64_t sv[2];
             bool valid[2], fail[2];
 #pragma unroll
             for (int u = 0; u < 2; u++) {
                 valid[u] = todo != 0;
-                const uint32_t b = valid[u] ? ctz64(todo) : 0u;
+                const uint32_t b = ctz64(todo) & 63u;               // (no start left: any byte of the lane)
                 todo &= todo - 1;
                 p[u] = (uint32_t)lane * LB + b;
-                uint64_t s = view128(sep0, sep1, xs0, xs1, b);
-                const uint32_t e = ctz64(view128(nl0, nl1, xn0, xn1, b));   // record end (64: past the view)
-                // the roles' fields in column order: clearing separator bits visits field
-                // ends in order (skip 0 after the first role: the same column again)
-                uint32_t en_prev = 0, st_prev = 0;
+                const uint32_t nb = b ^ 63u;
+                sv[u] = view128(sep64, xsep2, b, nb);
+                e[u] = ctz64(view128(nl, xnl2, b, nb));            // record end (>= 64: past the view)
+            }
+            // the roles' fields in column order, both records at once: clearing separator
+            // bits visits field ends in order (skip 0 after the first role: the same
+            // column again).  ctz64 of an exhausted view is >= 64, and so is every later end.
 #pragma unroll
-                for (int k = 0; k < NR; k++) {
-                    const uint32_t n = skip[k];
-                    uint32_t st, en;
-                    if (k > 0 && n == 0) {
-                        st = st_prev;
-                        en = en_prev;
-                    } else {
-                        if (k == 0) {
-                            if (n == 0) {
-                                st = 0;
-                            } else {
-                                for (uint32_t i = 1; i < n; i++) s &= s - 1;
-                                st = ctz64(s) + 1;
-                                s &= s - 1;
-                            }
-                        } else {
-                            s &= s - 1;                              // the previous field's end
-                            if (n == 1) {
-                                st = en_prev + 1;
-                            } else {
-                                for (uint32_t i = 2; i < n; i++) s &= s - 1;
-                                st = ctz64(s) + 1;
-                                s &= s - 1;
-                            }
-                        }
-                        en = ctz64(s);
-                    }
-                    fst[u][k] = st;
-                    fen[u][k] = en;
-                    en_prev = en;
-                    st_prev = st;
+            for (int k = 0; k < NR; k++) {
+                uint32_t n = skip[k];
+                asm volatile("" : "+s"(n));                         // tested here, not hoisted as lane masks
+                if (k > 0 && n == 0) {
+#pragma unroll
+                    for (int u = 0; u < 2; u++) { fst[u][k] = fst[u][k - 1]; fen[u][k] = fen[u][k - 1]; }
+                    continue;
                 }
+                if (k > 0) {
+#pragma unroll
+                    for (int u = 0; u < 2; u++) sv[u] &= sv[u] - 1;  // the previous field's end
+                }
+                if (k == 0 && n == 0) {
+#pragma unroll
+                    for (int u = 0; u < 2; u++) fst[u][k] = 0;
+                } else if (k > 0 && n == 1) {
+#pragma unroll
+                    for (int u = 0; u < 2; u++) fst[u][k] = fen[u][k - 1] + 1;
+                } else {
+                    for (uint32_t i = k == 0 ? 1u : 2u; i < n; i++) {
+#pragma unroll
+                        for (int u = 0; u < 2; u++) sv[u] &= sv[u] - 1;
+                    }
+#pragma unroll
+                    for (int u = 0; u < 2; u++) {
+                        fst[u][k] = ctz64(sv[u]) + 1;
+                        sv[u] &= sv[u] - 1;
+                    }
+                }
+#pragma unroll
+                for (int u = 0; u < 2; u++) fen[u][k] = ctz64(sv[u]);
+            }
+#pragma unroll
+            for (int u = 0; u < 2; u++) {
                 // the last role's field must end inside the view and at or before the
                 // record's terminator (else the row is short or longer than the view)
-                fail[u] = !valid[u] | (en_prev >= 64u) | (en_prev > e);
+                const uint32_t en = fen[u][NR - 1];
+                fail[u] = !valid[u] | (en >= 64u) | (en > e[u]);
             }
             const bool last_pass = !__any(todo != 0);
             if (wq) {                                                // a quote in front of a needed field
@@ -560,7 +573,7 @@ __global__ __launch_bounds__(LT) void fast_kernel(const uint8_t* __restrict__ g,
             }
 
 #if defined(FAST_PROF) && FAST_PROF == 2      // + record views and the field walk
-            v_rec += (wst[0] ^ sst[1][0] ^ gen[0] ^ gst[1] ^ (uint32_t)fail[0] ^ (uint32_t)fail[1]) & 1;
+            n_rec += (uint32_t)__popcll(__ballot((wst[0] ^ sst[1][0] ^ gen[0] ^ gst[1] ^ (uint32_t)fail[0] ^ (uint32_t)fail[1]) & 1));
             if (last_pass) FAST_ISSUE();
             continue;
 #endif
@@ -678,7 +691,7 @@ __global__ __launch_bounds__(LT) void fast_kernel(const uint8_t* __restrict__ g,
             }
             if (last_pass) FAST_ISSUE();                             // the window's bytes are read
 #if defined(FAST_PROF) && FAST_PROF == 3      // + field loads, typing, keys and hashes
-            v_rec += (hb[0] ^ hb[1] ^ (uint32_t)pass[0] ^ (uint32_t)fail[1] ^ (uint32_t)sfix[0][0]) & 1;
+            n_rec += (uint32_t)__popcll(__ballot((hb[0] ^ hb[1] ^ (uint32_t)pass[0] ^ (uint32_t)fail[1] ^ (uint32_t)sfix[0][0]) & 1));
             continue;
 #endif
 
@@ -698,8 +711,8 @@ __global__ __launch_bounds__(LT) void fast_kernel(const uint8_t* __restrict__ g,
                 }
                 const bool ok = valid[u] & !fail[u];
                 pass[u] = pass[u] & ok;
-                v_rec += ok ? 1u : 0u;
-                v_pass += pass[u] ? 1u : 0u;
+                n_rec += (uint32_t)__popcll(__ballot(ok));
+                n_pass += (uint32_t)__popcll(__ballot(pass[u]));
             }
 
             // ---- aggregate
@@ -717,6 +730,7 @@ __global__ __launch_bounds__(LT) void fast_kernel(const uint8_t* __restrict__ g,
                     }
                 }
             } else {
+                // lookup: the key's two buckets (one 16-byte LDS read each)
                 int slot[2];
                 bool miss[2];
 #pragma unroll
@@ -733,7 +747,7 @@ __global__ __launch_bounds__(LT) void fast_kernel(const uint8_t* __restrict__ g,
 #ifdef FAST_NOLOOKUP                                          // experiment: no table reads
                     s = (int)(hb[u] & (TSLOTS - 1));
 #endif
-                    slot[u] = hspill[u] ? -1 : s;
+                    slot[u] = s;
                     miss[u] = pass[u] & (s < 0) & !hspill[u];
                 }
                 if (__any(miss[0] | miss[1])) {                      // keys the seed did not place
@@ -751,19 +765,21 @@ __global__ __launch_bounds__(LT) void fast_kernel(const uint8_t* __restrict__ g,
                 }
 #pragma unroll
                 for (int u = 0; u < 2; u++) {
+                    slot[u] = hspill[u] ? -1 : slot[u];
                     const bool add = pass[u] & (slot[u] >= 0);
+                    uint8_t* r = S + (uint32_t)slot[u] * SLOT_BYTES;
                     if (add) {
                         const uint32_t fc = fcw | p[u];
 #ifndef FAST_ATOM
 #define FAST_ATOM 7                                                  // experiment: which LDS atomics run
 #endif
-                        if (FAST_ATOM & 1) atomicAdd(&tcnt[slot[u]], 1u);
-                        if (FAST_ATOM & 2) atomicMin(&tfirst[slot[u]], fc);
+                        if (FAST_ATOM & 1) atomicAdd((uint32_t*)(r + SO_CNT), 1u);
+                        if (FAST_ATOM & 2) atomicMin((uint32_t*)(r + SO_FIRST), fc);
 #pragma unroll
                         for (int j = 0; j < NS; j++) {
                             if (snum[u][j] && (FAST_ATOM & 4)) {
-                                if (sfx[u][j]) atomicAdd(&tfix[j][slot[u]], (unsigned long long)sfix[u][j]);
-                                else if (NS == 1) atomicAdd(&tdbl[j][slot[u]], sdbl[u][j]);
+                                if (sfx[u][j]) atomicAdd((unsigned long long*)(r + (j ? SO_FIX1 : SO_FIX0)), (unsigned long long)sfix[u][j]);
+                                else if (NS == 1) atomicAdd((double*)(r + SO_DBL), sdbl[u][j]);
                             }
                         }
                     }
@@ -771,12 +787,13 @@ __global__ __launch_bounds__(LT) void fast_kernel(const uint8_t* __restrict__ g,
                     for (int j = 0; j < NS; j++) {
                         const bool nn = add & !snum[u][j];
                         if (__any(nn)) {
-                            if (nn) atomicAdd(&tmiss[j][slot[u]], 1u);
+                            if (nn) atomicAdd((uint32_t*)(r + (j ? SO_MISS1 : SO_MISS0)), 1u);
                         }
                     }
                     const bool spill = pass[u] & (slot[u] < 0);
-                    if (__any(spill)) {                              // both buckets full
-                        v_spill += spill ? 1u : 0u;
+                    const uint64_t spb = __ballot(spill);
+                    if (spb) {                                       // both buckets full
+                        n_spill += (uint32_t)__popcll(spb);
                         if (spill) {
                             double v0 = 0.0, v1 = 0.0;
                             bool n0 = false, n1 = false;
@@ -796,16 +813,10 @@ __global__ __launch_bounds__(LT) void fast_kernel(const uint8_t* __restrict__ g,
     }
 
     // ---- statistics
-    unsigned long long n_rec = v_rec, n_pass = v_pass, n_spill = v_spill;
-    for (int o = 32; o > 0; o >>= 1) {
-        n_rec += __shfl_down(n_rec, o, 64);
-        n_pass += __shfl_down(n_pass, o, 64);
-        n_spill += __shfl_down(n_spill, o, 64);
-    }
     if (lane == 0) {
-        if (n_rec) atomicAdd(&stats->records, n_rec);
-        if (n_pass) atomicAdd(&stats->passed, n_pass);
-        if (n_spill) atomicAdd(&stats->lds_spills, n_spill);
+        if (n_rec) atomicAdd(&stats->records, (unsigned long long)n_rec);
+        if (n_pass) atomicAdd(&stats->passed, (unsigned long long)n_pass);
+        if (n_spill) atomicAdd(&stats->lds_spills, (unsigned long long)n_spill);
     }
 
     if (!GROUPED) {
@@ -857,7 +868,8 @@ __global__ __launch_bounds__(LT) void fast_kernel(const uint8_t* __restrict__ g,
     const uint32_t rot = (uint32_t)blockIdx.x * (TSLOTS / 64 + 1);
     for (uint32_t ii = tid; ii < TSLOTS; ii += LT) {
         const uint32_t i = (ii + rot) & (TSLOTS - 1);
-        const uint32_t n = tcnt[i];
+        const uint8_t* r = S + i * SLOT_BYTES;
+        const uint32_t n = *(const uint32_t*)(r + SO_CNT);
         if (!n) continue;
         const uint64_t w0 = T[i];
         const uint32_t kl = key_len8(w0);
@@ -865,16 +877,17 @@ __global__ __launch_bounds__(LT) void fast_kernel(const uint8_t* __restrict__ g,
         const int gi = g_insert(rt, k, gk_hash(k), stats);
         if (gi < 0) continue;
         atomicAdd(&rt.cnt[gi], (unsigned long long)n);
-        const uint32_t fc = tfirst[i];
+        const uint32_t fc = *(const uint32_t*)(r + SO_FIRST);
         if (fc != NOFIRST) {
             const uint64_t fw = first_win + ((uint64_t)(fc >> 16) * gridDim.x + blockIdx.x) * NWV + ((fc >> 12) & 15);
             atomicMin(&rt.first[gi], (unsigned long long)(fw * wsb + (fc & 4095)));
         }
         for (int acc = 0; acc < nacc; acc++) {
             const bool j1 = (acc1 >> acc) & 1;
-            const double sa = j1 ? (double)tfix[MAXS - 1][i] / 1000.0
-                                 : (double)tfix[0][i] / 1000.0 + (NS == 1 ? tdbl[0][i] : 0.0);
-            const uint32_t ms = j1 ? tmiss[MAXS - 1][i] : tmiss[0][i];
+            const double sa = j1 ? (double)*(const unsigned long long*)(r + SO_FIX1) / 1000.0
+                                 : (double)*(const unsigned long long*)(r + SO_FIX0) / 1000.0 +
+                                       (NS == 1 ? *(const double*)(r + SO_DBL) : 0.0);
+            const uint32_t ms = *(const uint32_t*)(r + (j1 ? SO_MISS1 : SO_MISS0));
             const uint32_t num = n - ms;
             if (num) {
                 atomicAdd(&rt.sum[acc][gi], sa);
