@@ -74,6 +74,7 @@ struct FastPlan {
     uint32_t rank[4];           // field index of WHERE, SUM 0, SUM 1, GROUP BY
     uint32_t wtt;               // WHERE truth table (bit 0 <, 1 ==, 2 >)
     int32_t wlo, whi;           // INTEGER field M: M < L <=> M < wlo; M > L <=> M > whi
+    uint32_t wa, ww, wneg;      // a 1-4 digit INTEGER M passes <=> ((M - wa) <=u ww) != wneg
     double wl;                  // the literal
     uint32_t pass_null;         // WHERE outcome of a NULL (empty) field
     int32_t nacc;
@@ -101,25 +102,29 @@ __device__ __forceinline__ uint32_t ctz64(uint64_t x) {
 }
 
 // The window's 4 KiB straight into the wave's LDS bytes by four LDS-DMA loads, 1 KiB
-// each (lane l's 16 bytes at 16l), addressed by a scalar base plus the lane's constant
-// offset `voff` (16 * lane), so the window costs no vector address arithmetic.  The
-// caller waits with vmcnt(0); the lgkmcnt(0) first retires this wave's LDS reads of the
-// window the loads overwrite.  M0 (the LDS base of an LDS-DMA load) is set and restored
-// inside the statement (the compiler owns M0).
+// each (lane l's 16 bytes at 16l): one scalar base, the lane's constant offset `voff`
+// (16 * lane) and the instruction offsets 0 / 1024 / 2048 / 3072, which step the LDS
+// destination (M0 + offset + 16 * lane) with the source, so the window costs no vector
+// address arithmetic and keeps one scalar pair live.  The caller waits with vmcnt(0);
+// the lgkmcnt(0) first retires this wave's LDS reads of the window the loads
+// overwrite.  M0 is set and restored inside the statement (the compiler owns M0).
+// `prev`: the 4 bytes before the window.
 __device__ __forceinline__ void load_win(const uint8_t* g, uint64_t w, uint32_t ws, uint32_t lds, uint32_t voff,
                                          uint32_t& prev) {
     const uint8_t* base = g + w * ws;
     asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
-#pragma unroll
-    for (int i = 0; i < 4; i++) {
-        uint32_t keep;
-        asm volatile("s_mov_b32 %0, m0\n\ts_mov_b32 m0, %3\n\ts_nop 0\n\tglobal_load_lds_dwordx4 %1, %2\n\ts_mov_b32 m0, %0"
-                     : "=&s"(keep)
-                     : "v"(voff), "s"(base + 1024 * i), "s"(lds + 1024u * i)
-                     : "memory");
-    }
-    const __amdgpu_buffer_rsrc_t r = __builtin_amdgcn_make_buffer_rsrc((void*)(base - 4), 0, 4, 0x00020000);
-    prev = __builtin_amdgcn_raw_buffer_load_b32(r, 0, 0, 0);
+    uint32_t keep;
+    asm volatile(
+        "s_mov_b32 %0, m0\n\ts_mov_b32 m0, %3\n\ts_nop 0\n\t"
+        "global_load_lds_dwordx4 %1, %2\n\t"
+        "global_load_lds_dwordx4 %1, %2 offset:1024\n\t"
+        "global_load_lds_dwordx4 %1, %2 offset:2048\n\t"
+        "global_load_lds_dwordx4 %1, %2 offset:3072\n\t"
+        "s_mov_b32 m0, %0"
+        : "=&s"(keep)
+        : "v"(voff), "s"(base), "s"(lds)
+        : "memory");
+    prev = *(const uint32_t*)(base - 4);
 }
 
 // A VGPR-resident copy of a (uniform or constant) value: on gfx950 a VALU instruction
@@ -202,6 +207,19 @@ __device__ __forceinline__ uint64_t qview(const WaveLds& W, uint32_t p) {
     return (uint64_t)__builtin_amdgcn_alignbit(q1, q0, sh) | ((uint64_t)__builtin_amdgcn_alignbit(q2, q1, sh) << 32);
 }
 
+// 4 / 8 bytes at LDS byte address a (any alignment; one ds_read2_b32 [+ ds_read_b32]):
+// the record positions are absolute LDS addresses, so a field load adds no base
+typedef const __attribute__((address_space(3))) uint32_t* lds_u32p;
+__device__ __forceinline__ uint32_t ld4a(uint32_t a) {
+    const lds_u32p t = (lds_u32p)(size_t)(a & ~3u);
+    return __builtin_amdgcn_alignbyte(t[1], t[0], a);   // (v_alignbyte uses the low 2 bits)
+}
+__device__ __forceinline__ void ld8a(uint32_t a, uint32_t& d0, uint32_t& d1) {
+    const lds_u32p t = (lds_u32p)(size_t)(a & ~3u);
+    const uint32_t x0 = t[0], x1 = t[1], x2 = t[2];
+    d0 = __builtin_amdgcn_alignbyte(x1, x0, a);
+    d1 = __builtin_amdgcn_alignbyte(x2, x1, a);
+}
 // 4 / 8 bytes of the window at byte offset o (one ds_read2_b32 [+ ds_read_b32])
 __device__ __forceinline__ uint32_t ld4(const uint8_t* w, uint32_t o) {
     const uint32_t* t = (const uint32_t*)w;
@@ -404,6 +422,8 @@ __global__ __launch_bounds__(LT) void fast_kernel(const uint8_t* __restrict__ g,
     const bool pass_null = __builtin_amdgcn_readfirstlane(fp.pass_null) != 0;
     const int wlo = __builtin_amdgcn_readfirstlane(fp.wlo), whi = __builtin_amdgcn_readfirstlane(fp.whi);
     const uint32_t wtt = __builtin_amdgcn_readfirstlane(fp.wtt);
+    const uint32_t wa = vreg(fp.wa), ww = vreg(fp.ww);
+    const bool wneg = __builtin_amdgcn_readfirstlane(fp.wneg) != 0;
     const double wl = fp.wl;
     const int nacc = __builtin_amdgcn_readfirstlane(fp.nacc);
     const uint32_t acc1 = __builtin_amdgcn_readfirstlane(fp.acc1);
@@ -423,6 +443,7 @@ __global__ __launch_bounds__(LT) void fast_kernel(const uint8_t* __restrict__ g,
     const uint32_t wlds = __builtin_amdgcn_readfirstlane(
         (uint32_t)(uintptr_t)(__attribute__((address_space(3))) uint8_t*)W.bytes);
     // window i (0 .. nwin - 1) of the range: file window first_win + i
+    const uint32_t lane_lds = vreg(wlds + (uint32_t)lane * LB);   // the LDS address of the lane's bytes
     uint32_t i = blockIdx.x * NWV + wv;
     if (i < nwin) load_win(g, first_win + i, wsb, wlds, voff, prev_next);
     for (uint32_t round = 0; i < nwin; round++, i += wstep) {
@@ -432,7 +453,11 @@ __global__ __launch_bounds__(LT) void fast_kernel(const uint8_t* __restrict__ g,
         bool issued = false;
 #define FAST_ISSUE()                                                               \
     do {                                                                           \
-        if (!issued && i + wstep < nwin) load_win(g, first_win + i + wstep, wsb, wlds, voff, prev_next); \
+        if (!issued && i + wstep < nwin) {                                          \
+            uint32_t ni = i + wstep;                                               \
+            asm volatile("" : "+s"(ni)); /* the address is formed here, not hoisted */ \
+            load_win(g, first_win + ni, wsb, wlds, voff, prev_next);               \
+        }                                                                          \
         issued = true;                                                             \
     } while (0)
 
@@ -480,7 +505,7 @@ __global__ __launch_bounds__(LT) void fast_kernel(const uint8_t* __restrict__ g,
 #endif
         while (__any(todo != 0)) {
             // ---- two records of this lane
-            uint32_t p[2], fst[2][4], fen[2][4], e[2];
+            uint32_t p[2], pa[2], fst[2][4], fen[2][4], e[2];   // p: window offset, pa: LDS address
             uint64_t sv[2];
             bool valid[2], fail[2];
 #pragma unroll
@@ -488,7 +513,8 @@ __global__ __launch_bounds__(LT) void fast_kernel(const uint8_t* __restrict__ g,
                 valid[u] = todo != 0;
                 const uint32_t b = ctz64(todo) & 63u;               // (no start left: any byte of the lane)
                 todo &= todo - 1;
-                p[u] = (uint32_t)lane * LB + b;
+                pa[u] = lane_lds + b;
+                p[u] = pa[u] - wlds;
                 const uint32_t nb = b ^ 63u;
                 sv[u] = view128(sep64, xsep2, b, nb);
                 e[u] = ctz64(view128(nl, xnl2, b, nb));            // record end (>= 64: past the view)
@@ -581,10 +607,10 @@ __global__ __launch_bounds__(LT) void fast_kernel(const uint8_t* __restrict__ g,
             uint32_t wd[2], sd[2][MAXS], k0[2], k1[2];
 #pragma unroll
             for (int u = 0; u < 2; u++) {
-                if (WHERE) wd[u] = ld4(W.bytes, p[u] + wst[u]);
+                if (WHERE) wd[u] = ld4a(pa[u] + wst[u]);
 #pragma unroll
-                for (int j = 0; j < NS; j++) sd[u][j] = ld4(W.bytes, p[u] + sst[u][j]);
-                if (GROUPED) ld8(W.bytes, p[u] + gst[u], k0[u], k1[u]);
+                for (int j = 0; j < NS; j++) sd[u][j] = ld4a(pa[u] + sst[u][j]);
+                if (GROUPED) ld8a(pa[u] + gst[u], k0[u], k1[u]);
             }
 
             // ---- WHERE outcome (wu: a field the 4-byte numeral path could not type)
@@ -596,8 +622,7 @@ __global__ __launch_bounds__(LT) void fast_kernel(const uint8_t* __restrict__ g,
                 for (int u = 0; u < 2; u++) {
                     const uint32_t len = wen[u] - wst[u];
                     const Num n = num4<false>(wd[u], len);
-                    const int c = (int)n.M < wlo ? -1 : ((int)n.M > whi ? 1 : 0);
-                    pass[u] = len == 0 ? pass_null : tt_result(wtt, c);
+                    pass[u] = len == 0 ? pass_null : ((n.M - wa <= ww) != wneg);
                     wu[u] = !n.ok & (len != 0) & !fail[u];
                     wide |= wu[u];
                 }
@@ -607,7 +632,7 @@ __global__ __launch_bounds__(LT) void fast_kernel(const uint8_t* __restrict__ g,
                         if (wu[u]) {
                             const uint32_t len = wen[u] - wst[u];
                             uint32_t d0, d1;
-                            ld8(W.bytes, p[u] + wst[u], d0, d1);
+                            ld8a(pa[u] + wst[u], d0, d1);
                             const Num n = num7(d0, d1, len);
                             if (n.ok) {
                                 int c;
@@ -652,7 +677,7 @@ __global__ __launch_bounds__(LT) void fast_kernel(const uint8_t* __restrict__ g,
                         if (sw[u]) {
                             const uint32_t len = sen[u][j] - sst[u][j];
                             uint32_t d0, d1;
-                            ld8(W.bytes, p[u] + sst[u][j], d0, d1);
+                            ld8a(pa[u] + sst[u][j], d0, d1);
                             const Num n = num7(d0, d1, len);
                             if (n.ok) {
                                 snum[u][j] = true;
@@ -961,6 +986,23 @@ bool fast_shape(const ScanPlan* P, int grouped, FastPlan* fp, int* ns, bool* whe
         const double c = std::ceil(lv), f = std::floor(lv);
         fp->wlo = c >= 2147483647.0 ? 2147483647 : (c <= -2147483648.0 ? (-2147483647 - 1) : (int32_t)c);
         fp->whi = f >= 2147483647.0 ? 2147483647 : (f <= -2147483648.0 ? (-2147483647 - 1) : (int32_t)f);
+        // the outcome over M in [0, 9999] (num4's INTEGER range) as one interval test:
+        // the parts M < L, M == L, M > L are consecutive intervals, so any selection of
+        // them is an interval or (< and > without ==) the complement of one
+        const bool lt = fp->wtt & 1, eq = fp->wtt & 2, gt = fp->wtt & 4;
+        const int64_t lo_eq = fp->wlo, hi_eq = fp->whi;
+        int64_t A, B;
+        fp->wneg = 0;
+        if (lt && !eq && gt) { fp->wneg = 1; A = lo_eq; B = hi_eq; }
+        else if (!lt && !eq && !gt) { A = 1; B = 0; }
+        else {
+            A = lt ? INT64_MIN : (eq ? lo_eq : hi_eq + 1);
+            B = gt ? INT64_MAX : (eq ? hi_eq : lo_eq - 1);
+        }
+        A = A < 0 ? 0 : A;
+        B = B > 9999 ? 9999 : B;
+        if (A > B) { fp->wa = 0xFFFFFFFFu; fp->ww = 0; }     // empty: M - wa = M + 1 > 0
+        else { fp->wa = (uint32_t)A; fp->ww = (uint32_t)(B - A); }
     } else {
         return false;
     }
