@@ -47,6 +47,12 @@ METRIC = "rows/sec scanned (filter+GROUP BY) at 1/2/4/8 GPUs; % of HBM read peak
 QUERY = ("SELECT role, COUNT(*), SUM(height), AVG(height) FROM '{path}' "
          "WHERE age > 30 GROUP BY role")
 QUERY2 = "SELECT COUNT(*) FROM '{path}' WHERE age > 30"
+KERNEL_NAMES = {
+    (2, True): "cq::fast::fast_kernel<true, true, 1, true, true> (+ slow_kernel, raw_merge_kernel)",
+    (2, False): "cq::fast::fast_kernel<false, true, 0, true, true> (+ slow_kernel)",
+    (1, True): "cq::lean::lean_kernel<true, LW_NUM, 1, false> (+ slow_kernel, raw_merge_kernel)",
+    (1, False): "cq::lean::lean_kernel<false, LW_NUM, 0, false> (+ slow_kernel)",
+}
 HBM_PEAK_GBS = 8000.0   # MI355X HBM3E spec (MI355X_MICROARCH.md, chip-level parameters)
 GOLDEN = os.path.join(ROOT, "tests", "golden", "big.json")
 
@@ -213,6 +219,7 @@ def main():
     P, q = build_plan("big.csv", args.config)
     ast = C.pointer(q)
     kernel_used = [1]
+    last_stats = [{}]
 
     def step():
         """one query; returns (result pointer on rank 0 or None, scan ms)"""
@@ -224,11 +231,15 @@ def main():
             if os.environ.get("CQ_BENCH_DEBUG"):
                 print("stats", st, file=sys.stderr)
             kernel_used[0] = st.get("scan_kernel", 0)
+            last_stats[0] = st
             return tp, st["scan_ms"]
         # partial groups stay in HBM; key all_gather + dense MIN/SUM reduces over RCCL,
         # rank 0 finishes (scan_partitioned's blob gather only for plans off the dense path)
         tp = scan_partitioned_dense(ast, table)
-        return tp, cq_amd.stats()["scan_ms"]   # the merge runs no scan: still this rank's partial
+        st = cq_amd.stats()                   # the merge runs no scan: still this rank's partial
+        kernel_used[0] = st.get("scan_kernel", 0)
+        last_stats[0] = st
+        return tp, st["scan_ms"]
 
     for _ in range(args.warmup):
         tp, _ = step()
@@ -314,7 +325,10 @@ def main():
             "warmup": args.warmup,
             "ms_per_step": ms_per_step,
             "higher_is_better": True,
-            "scaling": "weak" if world == 1 else "strong",
+            "scaling": "strong",
+            "scaling_note": ("total rows fixed per run: --rows (default 1e8 at N=1, config 3; 1e9 at N>1, "
+                             "config 4, range-partitioned); `--gpus 1 --rows 1000000000` runs config 4's "
+                             "own file on one GPU, the N=1 point of the same curve"),
             "vs_baseline": None,
             "dtype": "u8",
             "data": ("synthetic: logical Shape A+role CSV (generate_big_dataset.py columns + role_%03d, "
@@ -341,11 +355,17 @@ def main():
                 "unit": "GB/s",
                 "frac": achieved / HBM_PEAK_GBS,
                 "traffic": traffic,
-                "kernel": (("cq::lean::lean_kernel<true, LW_NUM, 1, false> (+ slow_kernel, raw_merge_kernel)"
-                            if role else "cq::lean::lean_kernel<false, LW_NUM, 0, false> (+ slow_kernel)")
-                           if kernel_used[0] else "cq::scan_kernel"),
+                "kernel": KERNEL_NAMES.get((kernel_used[0], role), "cq::scan_kernel"),
                 "kernel_ms": avg_scan_ms,
                 "bytes_per_launch": nbytes,
+            },
+            "plan_sample": {
+                # the plan's choices come from the first 256 KiB (group-key seed, tag width,
+                # window stride); records they do not cover show up here
+                "slow_records": last_stats[0].get("slow_records"),
+                "lds_spills": last_stats[0].get("lds_spills"),
+                "retries": last_stats[0].get("retries"),
+                "records": last_stats[0].get("records"),
             },
             "end_to_end": e2e,
             "config2": cfg2,
@@ -415,11 +435,13 @@ def config2_leg(args, cq_amd, abi, L, data):
     ms = []
     t0 = time.perf_counter()
     last = None
+    st = {}
     for _ in range(args.steps):
         tp = L.cqgpu_query(ast, arr, 1)
         if not tp:
             raise RuntimeError(cq_amd.last_error())
-        ms.append(cq_amd.stats()["scan_ms"])
+        st = cq_amd.stats()
+        ms.append(st["scan_ms"])
         if last:
             cq_amd.result_free(last)
         last = tp
@@ -433,6 +455,8 @@ def config2_leg(args, cq_amd, abi, L, data):
     return {"workload": "config2: SELECT COUNT(*) FROM 'big.csv' WHERE age > 30 (Shape A, 1e8 rows)",
             "value": rows / (el / args.steps), "unit": "rows/s", "ms_per_step": el * 1000 / args.steps,
             "kernel_ms": kms, "bytes_per_launch": nb,
+            "kernel": KERNEL_NAMES.get((st.get("scan_kernel", 0), False), "cq::scan_kernel"),
+            "plan_sample": {"slow_records": st.get("slow_records"), "lds_spills": st.get("lds_spills")},
             "roofline_frac": nb / (kms * 1e-3) / 1e9 / HBM_PEAK_GBS,
             "verified": verify(res, exp, 2), "verified_against": src}
 

@@ -133,7 +133,8 @@ hipError_t cq_excl_sum_u32(void* temp, size_t* temp_bytes, const unsigned int* i
 size_t cq_pack_result_bytes(unsigned int ng, int nacc, uint32_t ncell, uint32_t sb);
 hipError_t cq_launch_pack_result(const cq::GroupOut* out, const unsigned int* count, unsigned int cap_out, int nacc,
                                  const cq::Cell* cells, const uint8_t* bytes, uint32_t ncell, uint32_t sb,
-                                 uint8_t* dst, hipStream_t s);
+                                 uint8_t* dst, const cq::ScanStats* stats, uint8_t* hdr, int order, hipStream_t s);
+unsigned int cq_pack_order_max();
 hipError_t cq_launch_finish(const uint8_t* g, uint64_t n, const cq::GroupOut* out, const unsigned int* count,
                             unsigned int cap_out, const cq::FinishDesc* D, cq::Cell* cells, uint8_t* bytes,
                             hipStream_t s);
@@ -231,11 +232,14 @@ struct DevCtx {
     size_t ws_size = 0;
     void* pinned = nullptr;
     size_t pinned_size = 0;
+    uint8_t* mail = nullptr;           // host-mapped, coherent: kernels write results here directly
+    size_t mail_size = 0;
     // per-query scratch (literals, gathers, string fetches): a bump region reset at
     // the start of every query, so the query path makes no hipMalloc / hipFree
     uint8_t* bump = nullptr;
     size_t bump_size = 0, bump_used = 0;
     hipEvent_t up_ev[2] = {nullptr, nullptr};   // table upload: staging-buffer reuse
+    uint64_t query_gen = 1;            // bumped at every query (literal cache lifetimes)
 };
 DevCtx g_ctx[64];
 
@@ -268,7 +272,7 @@ void* workspace(DevCtx& c, size_t bytes) {
 // per-query device scratch: from the context's bump region when it fits, else an
 // owned allocation freed with the object
 constexpr size_t BUMP_BYTES = 8u << 20;
-void bump_reset(DevCtx& c) { c.bump_used = 0; }
+void bump_reset(DevCtx& c) { c.bump_used = 0; c.query_gen++; }
 struct Scratch {
     uint8_t* p = nullptr;
     bool owned = false;
@@ -392,6 +396,19 @@ void* pinned(DevCtx& c, size_t bytes) {
         c.pinned_size = sz;
     }
     return c.pinned;
+}
+
+// the result mailbox: host memory the device writes over PCIe (fine-grained,
+// coherent), read by the host after the stream's one synchronisation
+uint8_t* mailbox(DevCtx& c, size_t bytes) {
+    if (bytes > c.mail_size) {
+        if (c.mail) HIPCHECK(hipHostFree(c.mail));
+        c.mail = nullptr;
+        size_t sz = std::max(bytes, std::max<size_t>(c.mail_size * 2, 4 << 20));
+        HIPCHECK(hipHostMalloc((void**)&c.mail, sz, hipHostMallocMapped | hipHostMallocCoherent));
+        c.mail_size = sz;
+    }
+    return c.mail;
 }
 
 double as_dbl(uint64_t b) { double d; memcpy(&d, &b, 8); return d; }
@@ -1189,6 +1206,21 @@ struct Literals {
     std::vector<HCell> host;          // the same cells with host strings
 };
 
+// A query's literals repeat from step to step: their typed cells and device copy are
+// kept per device (up to LIT_CACHE entries) and reused when the texts are the same.
+// An entry that some Literals of the running query uses is never replaced.
+constexpr size_t LIT_CACHE = 8;
+struct LitEntry {
+    std::string key;
+    uint8_t* dev = nullptr;
+    size_t cap = 0;
+    std::vector<Cell> cells;
+    std::vector<HCell> host;
+    size_t cell_off = 0;
+    uint64_t gen = 0;                  // the last query that used it
+};
+std::vector<LitEntry> g_litcache[64];
+
 // typed on the host by cell.h's parser (hostcell.cpp, the kernels' own typing
 // code); STRING literals get a device copy of their bytes for the kernels
 void parse_literals(DevCtx& c, const std::vector<std::string>& texts, Literals& L) {
@@ -1198,6 +1230,22 @@ void parse_literals(DevCtx& c, const std::vector<std::string>& texts, Literals& 
     L.cells.clear();
     L.host.clear();
     if (!n) return;
+    std::string key;
+    for (size_t i = 0; i < n; i++) {
+        const uint32_t k = (uint32_t)texts[i].size();
+        key.append((const char*)&k, 4);
+        key += texts[i];
+    }
+    std::vector<LitEntry>& cache = g_litcache[c.device & 63];
+    for (LitEntry& e : cache) {
+        if (e.dev && e.key == key) {
+            e.gen = c.query_gen;
+            L.cells = e.cells;
+            L.host = e.host;
+            L.dcells = (Cell*)(e.dev + e.cell_off);
+            return;
+        }
+    }
     std::vector<size_t> offs(n);
     std::string blob;
     for (size_t i = 0; i < n; i++) {
@@ -1207,7 +1255,6 @@ void parse_literals(DevCtx& c, const std::vector<std::string>& texts, Literals& 
     }
     L.cells.resize(n);
     L.host.resize(n);
-    bool any_str = false;
     for (size_t i = 0; i < n; i++) {
         const uint8_t* t = (const uint8_t*)blob.data() + offs[i];
         Cell x = cq_host_parse_cell(t, (uint32_t)texts[i].size());
@@ -1217,21 +1264,49 @@ void parse_literals(DevCtx& c, const std::vector<std::string>& texts, Literals& 
             const size_t off = (size_t)((const uint8_t*)(uintptr_t)x.bits - (const uint8_t*)blob.data());
             L.host[i].s.assign(blob.data() + off, x.len);
             x.bits = off;                  // relocated to the device copy below
-            any_str = true;
         }
         L.cells[i] = x;
     }
     const size_t cell_off = (blob.size() + 15) & ~(size_t)15;
-    L.dev.get(c, cell_off + n * sizeof(Cell));
+    const size_t bytes = cell_off + n * sizeof(Cell);
+    // a cache entry no Literals of this query holds (else the query's scratch)
+    LitEntry* slot = nullptr;
+    if (cache.size() < LIT_CACHE) {
+        cache.emplace_back();
+        slot = &cache.back();
+    } else {
+        for (LitEntry& e : cache)
+            if (e.gen < c.query_gen && (!slot || e.gen < slot->gen)) slot = &e;
+    }
+    uint8_t* dst;
+    if (slot) {
+        if (slot->cap < bytes) {
+            if (slot->dev) HIPCHECK(hipFree(slot->dev));
+            slot->dev = nullptr;
+            slot->cap = 0;
+            HIPCHECK(hipMalloc((void**)&slot->dev, std::max<size_t>(bytes, 4096)));
+            slot->cap = std::max<size_t>(bytes, 4096);
+        }
+        dst = slot->dev;
+    } else {
+        L.dev.get(c, bytes);
+        dst = L.dev.p;
+    }
     for (size_t i = 0; i < n; i++)
-        if (L.cells[i].kind == K_STR) L.cells[i].bits += (uint64_t)(uintptr_t)L.dev.p;
-    std::vector<uint8_t> up(cell_off + n * sizeof(Cell), 0);
+        if (L.cells[i].kind == K_STR) L.cells[i].bits += (uint64_t)(uintptr_t)dst;
+    std::vector<uint8_t> up(bytes, 0);
     memcpy(up.data(), blob.data(), blob.size());
     memcpy(up.data() + cell_off, L.cells.data(), n * sizeof(Cell));
-    (void)any_str;
-    HIPCHECK(hipMemcpyAsync(L.dev.p, up.data(), up.size(), hipMemcpyHostToDevice, c.stream));
-    L.dcells = (Cell*)(L.dev.p + cell_off);
+    HIPCHECK(hipMemcpyAsync(dst, up.data(), up.size(), hipMemcpyHostToDevice, c.stream));
+    L.dcells = (Cell*)(dst + cell_off);
     HIPCHECK(hipStreamSynchronize(c.stream));   // the staging vector goes out of scope
+    if (slot) {
+        slot->key = key;
+        slot->cells = L.cells;
+        slot->host = L.host;
+        slot->cell_off = cell_off;
+        slot->gen = c.query_gen;
+    }
 }
 
 // group table arena in the device workspace
@@ -1246,6 +1321,23 @@ struct TableArena {
 };
 
 size_t align256(size_t x) { return (x + 255) & ~(size_t)255; }
+
+// one launch initialises an arena: bytes [0, n) zero except the 0xff regions
+// (every region 256-byte aligned; the slow list past n needs no initialisation)
+constexpr int ARENA_FILLS = 32;
+struct ArenaFills {
+    uint32_t n;
+    uint64_t off[ARENA_FILLS], end[ARENA_FILLS];
+};
+__global__ void arena_init_kernel(uint4* __restrict__ base, uint64_t n16, ArenaFills F) {
+    for (uint64_t i = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x; i < n16; i += (uint64_t)gridDim.x * blockDim.x) {
+        const uint64_t b = i * 16;
+        bool ff = false;
+        for (uint32_t k = 0; k < F.n; k++) ff |= (b >= F.off[k]) & (b < F.end[k]);
+        const uint32_t v = ff ? 0xffffffffu : 0u;
+        base[i] = make_uint4(v, v, v, v);
+    }
+}
 
 TableArena make_arena(DevCtx& c, const ScanPlan& P, uint32_t cap, size_t out_cap, size_t cand_blocks = 0,
                       uint32_t cand_stride = 16, unsigned long long slow_cap = 1ull << 20) {
@@ -1301,12 +1393,30 @@ TableArena make_arena(DevCtx& c, const ScanPlan& P, uint32_t cap, size_t out_cap
     for (auto& p : parts) total += align256(p.bytes);
     uint8_t* base = (uint8_t*)workspace(c, total);
     size_t off = 0;
-    // zero everything in one memset, then the 0xff regions
-    HIPCHECK(hipMemsetAsync(base, 0, total, c.stream));
+    ArenaFills F;
+    F.n = 0;
+    bool fits = true;
     for (auto& p : parts) {
         *p.p = base + off;
-        if (p.fill) HIPCHECK(hipMemsetAsync(base + off, p.fill, p.bytes, c.stream));
+        if (p.fill) {
+            if (p.fill != 0xff || F.n == ARENA_FILLS) fits = false;
+            else { F.off[F.n] = off; F.end[F.n] = off + align256(p.bytes); F.n++; }
+        }
         off += align256(p.bytes);
+    }
+    const size_t init = total - align256(slow_cap * 8ull);   // the slow list is the last part
+    if (fits) {
+        const uint64_t n16 = init / 16;
+        const unsigned grid = (unsigned)std::min<uint64_t>((n16 + 255) / 256, 2048);
+        hipLaunchKernelGGL(arena_init_kernel, dim3(std::max(grid, 1u)), dim3(256), 0, c.stream, (uint4*)base, n16, F);
+        HIPCHECK(hipGetLastError());
+    } else {             // zero everything in one memset, then the fill regions
+        HIPCHECK(hipMemsetAsync(base, 0, init, c.stream));
+        off = 0;
+        for (auto& p : parts) {
+            if (p.fill) HIPCHECK(hipMemsetAsync(base + off, p.fill, p.bytes, c.stream));
+            off += align256(p.bytes);
+        }
     }
     return A;
 }
@@ -1338,7 +1448,8 @@ PhaseClock* g_phase = nullptr;
 // (create_groups appends groups in row order); `limit`: first positions are below it
 std::vector<HGroup> make_groups(DevCtx& c, const Compiled& C, uint64_t limit, uint64_t base_offset,
                                 std::vector<GroupOut>& outs, std::vector<Cell>& fcells, std::vector<uint8_t>& fbytes,
-                                int nrep_sorted, const std::vector<int>& rep_ord, uint32_t SB) {
+                                int nrep_sorted, const std::vector<int>& rep_ord, uint32_t SB,
+                                bool presorted = false) {
     std::vector<HGroup> groups;
     const uint32_t ncell = (uint32_t)nrep_sorted + (uint32_t)C.P.nacc + 1;
     // single group: always present (evaluator.c:232-247), even with no rows
@@ -1375,11 +1486,15 @@ std::vector<HGroup> make_groups(DevCtx& c, const Compiled& C, uint64_t limit, ui
     }
     PHASE("hcells");
     // first-appearance order (create_groups appends groups in row order)
-    std::vector<std::pair<unsigned long long, uint32_t>> fo(outs.size());
-    for (size_t i = 0; i < fo.size(); i++) fo[i] = {outs[i].first, (uint32_t)i};
-    std::sort(fo.begin(), fo.end());       // (first, index): ties keep the index order
     std::vector<uint32_t> order(outs.size());
-    for (size_t i = 0; i < fo.size(); i++) order[i] = fo[i].second;
+    if (presorted) {                       // pack_result_kernel placed them in this order
+        for (size_t i = 0; i < order.size(); i++) order[i] = (uint32_t)i;
+    } else {
+        std::vector<std::pair<unsigned long long, uint32_t>> fo(outs.size());
+        for (size_t i = 0; i < fo.size(); i++) fo[i] = {outs[i].first, (uint32_t)i};
+        std::sort(fo.begin(), fo.end());   // (first, index): ties keep the index order
+        for (size_t i = 0; i < fo.size(); i++) order[i] = fo[i].second;
+    }
     const size_t nrep = C.rep_cols.size();
     PHASE("order");
     groups.reserve(order.size());
@@ -1417,9 +1532,14 @@ std::vector<HGroup> make_groups(DevCtx& c, const Compiled& C, uint64_t limit, ui
 // run the fused scan (with regrowth on overflow) and return the groups
 // row_out (optional): offsets of the records passing WHERE, unordered; entries
 // past row_cap are counted in ScanStats.rows_emitted but not written
+cq_table* build_direct(const Compiled& C, const uint8_t* hp, uint32_t ng, uint32_t ncell, uint32_t SB,
+                       const std::vector<int>& rep_ord, const Literals& L, uint64_t limit);
+
+// direct (optional): for plans build_direct handles, the result table built straight
+// from the packed result (no HGroup per group); the returned vector is then empty
 std::vector<HGroup> run_aggregate(DevCtx& c, const cqgpu_table* t, Compiled& C, Literals& L,
                                   ScanStats* stats_out, unsigned long long* row_out = nullptr,
-                                  unsigned long long row_cap = 0) {
+                                  unsigned long long row_cap = 0, cq_table** direct = nullptr) {
     parse_literals(c, C.lits, L);
     for (size_t i = 0; i < L.cells.size(); i++) C.P.consts[i] = L.cells[i];
     PHASE("literals");
@@ -1452,13 +1572,17 @@ std::vector<HGroup> run_aggregate(DevCtx& c, const cqgpu_table* t, Compiled& C, 
     std::vector<Cell> fcells;
     std::vector<uint8_t> fbytes;
     uint64_t chunk = 0;          // 0: the whole table in one launch
+    bool presorted = false;
     while (true) {
         TableArena A = make_arena(c, C.P, cap, cap / 2 + 1, (size_t)grid, cq_scan_cand_stride(&C.P, grouped));
         const unsigned int cap_out = cap / 2 + 1;
         Scratch fin(c, (size_t)cap_out * ncell * (sizeof(Cell) + SB) + 64);
         Cell* dcells = (Cell*)fin.p;
         uint8_t* dbytes = fin.p + (size_t)cap_out * ncell * sizeof(Cell);
-        DevBuf packed(cq_pack_result_bytes(cap_out, C.P.nacc, ncell, SB) + 64);
+        // the mailbox: scan statistics and group count, then the packed result
+        constexpr size_t MAIL_HDR = 1024;
+        static_assert(sizeof(ScanStats) + 4 <= MAIL_HDR, "mailbox header");
+        uint8_t* mail = mailbox(c, MAIL_HDR + cq_pack_result_bytes(cap_out, C.P.nacc, ncell, SB) + 64);
         bool is_packed = false;
         memset(&st, 0, sizeof st);
         unsigned long long last_clk[8] = {0, 0, 0, 0, 0, 0, 0, 0};
@@ -1482,14 +1606,14 @@ std::vector<HGroup> run_aggregate(DevCtx& c, const cqgpu_table* t, Compiled& C, 
                 HIPCHECK(cq_launch_compact(&A.gt, &C.P, A.out, A.out_count, cap_out, c.stream));
                 HIPCHECK(cq_launch_finish(t->g, t->n, A.out, A.out_count, cap_out, &FD, dcells, dbytes, c.stream));
                 HIPCHECK(cq_launch_pack_result(A.out, A.out_count, cap_out, C.P.nacc, dcells, dbytes, ncell, SB,
-                                               packed.as<uint8_t>(), c.stream));
+                                               mail + MAIL_HDR, A.stats, mail, 1, c.stream));
                 finished = true;
                 is_packed = true;
             }
             // the group count and the scan statistics through pinned memory, one sync
-            uint8_t* hs = (uint8_t*)pinned(c, sizeof(ScanStats) + 16);
-            HIPCHECK(hipMemcpyAsync(hs, A.stats, sizeof(ScanStats), hipMemcpyDeviceToHost, c.stream));
-            if (finished) HIPCHECK(hipMemcpyAsync(hs + sizeof(ScanStats), A.out_count, 4, hipMemcpyDeviceToHost, c.stream));
+            // (one launch: pack_result_kernel wrote both into the mailbox)
+            uint8_t* hs = finished ? mail : (uint8_t*)pinned(c, sizeof(ScanStats) + 16);
+            if (!finished) HIPCHECK(hipMemcpyAsync(hs, A.stats, sizeof(ScanStats), hipMemcpyDeviceToHost, c.stream));
             PHASE("launch");
             HIPCHECK(hipStreamSynchronize(c.stream));
             PHASE("scan+finish");
@@ -1535,15 +1659,39 @@ std::vector<HGroup> run_aggregate(DevCtx& c, const cqgpu_table* t, Compiled& C, 
             HIPCHECK(hipStreamSynchronize(c.stream));
         }
         ng = std::min(ng, cap_out);
+        if (direct && is_packed && ng && ng <= cq_pack_order_max() && C.grouped) {
+            // the stats checks below run first; then the table straight from the mailbox
+            for (int a = 0; a < C.P.nacc; a++) {
+                if (C.P.acc[a].kind == ACC_SUM) continue;
+                unsigned m = st.acc_classes[a];
+                if (m & (m - 1)) throw MixedExtremes{};
+            }
+            // (one sequential copy out of the PCIe-written mailbox, then cached reads)
+            static thread_local std::vector<uint8_t> hbuf;
+            const size_t pb = cq_pack_result_bytes(ng, C.P.nacc, ncell, SB);
+            if (hbuf.size() < pb) hbuf.resize(pb);
+            memcpy(hbuf.data(), mail + MAIL_HDR, pb);
+            PHASE("mcopy");
+            *direct = build_direct(C, hbuf.data(), ng, ncell, SB, rep_ord, L, t->n);
+            if (*direct) {
+                g_stats.retries = retries;
+                g_stats.records = st.records;
+                g_stats.lds_spills = st.lds_spills;
+                g_stats.slow_records = st.slow_records;
+                g_stats.passed = st.passed;
+                g_stats.scan_bytes = t->n;
+                g_stats.groups = ng;
+                if (stats_out) *stats_out = st;
+                PHASE("direct");
+                return {};
+            }
+        }
         outs.resize(ng);
         fcells.resize((size_t)ng * ncell);
         fbytes.resize((size_t)ng * ncell * SB);
         if (ng && is_packed) {   // one copy of the packed result (pack_result_kernel's layout)
             const size_t rec = 40 + 40 * (size_t)C.P.nacc, b1 = fcells.size() * sizeof(Cell), b2 = fbytes.size();
-            const size_t tot = cq_pack_result_bytes(ng, C.P.nacc, ncell, SB);
-            uint8_t* hp = (uint8_t*)pinned(c, tot);
-            HIPCHECK(hipMemcpyAsync(hp, packed.p, tot, hipMemcpyDeviceToHost, c.stream));
-            HIPCHECK(hipStreamSynchronize(c.stream));
+            const uint8_t* hp = mail + MAIL_HDR;   // written by pack_result_kernel, synchronised above
             memset(outs.data(), 0, ng * sizeof(GroupOut));
             for (unsigned int i = 0; i < ng; i++) {
                 const uint8_t* r = hp + i * rec;
@@ -1576,6 +1724,7 @@ std::vector<HGroup> run_aggregate(DevCtx& c, const cqgpu_table* t, Compiled& C, 
             memcpy(fcells.data(), hp + b0, b1);
             memcpy(fbytes.data(), hp + b0 + b1, b2);
         }
+        presorted = is_packed && ng <= cq_pack_order_max();
         PHASE("copies");
         break;
     }
@@ -1593,7 +1742,8 @@ std::vector<HGroup> run_aggregate(DevCtx& c, const cqgpu_table* t, Compiled& C, 
         unsigned m = st.acc_classes[a];
         if (m & (m - 1)) throw MixedExtremes{};
     }
-    return make_groups(c, C, t->n, t->base_offset, outs, fcells, fbytes, FD.ncols, rep_ord, SB);
+    return make_groups(c, C, t->n, t->base_offset, outs, fcells, fbytes, FD.ncols, rep_ord, SB,
+                       presorted);
 }
 
 // ------------------------------------------------------------------ result tables
@@ -1671,6 +1821,89 @@ cq_table* build_groups(const Compiled& C, const std::vector<HGroup>& groups, con
                 default: break;
             }
             row.values[i] = to_value(v);
+        }
+    }
+    return r;
+}
+
+// build_groups' rows straight from pack_result_kernel's output in first-appearance
+// order, for plans whose items are COUNT / SUM / AVG / representative cells /
+// constants and whose STRING cells are inline: one calloc per row and one strdup
+// per string, nothing else per group.  nullptr: the plan or the data needs
+// make_groups + build_groups.
+cq_table* build_direct(const Compiled& C, const uint8_t* hp, uint32_t ng, uint32_t ncell, uint32_t SB,
+                       const std::vector<int>& rep_ord, const Literals& L, uint64_t limit) {
+    for (const OutCol& o : C.outs)
+        if (o.kind != OUT_COUNT && o.kind != OUT_SUM && o.kind != OUT_AVG && o.kind != OUT_REP &&
+            o.kind != OUT_CONST && o.kind != OUT_NULL)
+            return nullptr;
+    const int nacc = C.P.nacc;
+    const size_t rec = 40 + 40 * (size_t)nacc;
+    const Cell* cells = (const Cell*)(hp + (size_t)ng * rec);
+    const uint8_t* bytes = (const uint8_t*)(cells + (size_t)ng * ncell);
+    std::vector<int> rep_at(C.rep_cols.size(), -1);   // rep slot -> finish cell index
+    for (size_t i = 0; i < rep_ord.size(); i++) rep_at[rep_ord[i]] = (int)i;
+    for (uint32_t g = 0; g < ng; g++) {
+        const unsigned long long first = ((const unsigned long long*)(hp + g * rec))[4];
+        if (first != NOPOS && first >= limit) throw HipError{"scan kernel: group first-row offset out of range"};
+        for (const OutCol& o : C.outs) {
+            if (o.kind != OUT_REP || o.rep < 0 || o.rep >= (int)rep_at.size()) continue;
+            const Cell& x = cells[(size_t)g * ncell + rep_at[o.rep]];
+            if (x.kind == K_STR && x.len > SB) return nullptr;          // long text: fetched by make_groups
+        }
+    }
+    PHASE("dcheck");
+    cq_table* r = new_result(C.names);
+    r->nrows = r->row_capacity = (int)ng;
+    r->rows = (cq_row*)malloc(sizeof(cq_row) * std::max<size_t>(ng, 1));
+    for (uint32_t g = 0; g < ng; g++) {
+        const uint8_t* rp = hp + g * rec;
+        const unsigned long long cnt = ((const unsigned long long*)rp)[3];
+        const uint64_t* q = (const uint64_t*)(rp + 40);
+        cq_row& row = r->rows[g];
+        row.ncols = r->ncols;
+        row.values = (cq_value*)calloc(std::max(r->ncols, 1), sizeof(cq_value));
+        for (int i = 0; i < r->ncols; i++) {
+            const OutCol& o = C.outs[i];
+            cq_value& v = row.values[i];
+            v.kind = CQ_V_NULL;
+            switch (o.kind) {
+                case OUT_COUNT: v.kind = K_INT; v.u.i = (long long)cnt; break;
+                case OUT_SUM: {
+                    const unsigned long long num = q[5 * o.acc + 1];
+                    v.kind = K_DBL;
+                    v.u.f = num ? as_dbl(q[5 * o.acc]) : 0.0;
+                    break;
+                }
+                case OUT_AVG: {
+                    const unsigned long long num = q[5 * o.acc + 1];
+                    v.kind = K_DBL;
+                    v.u.f = num ? as_dbl(q[5 * o.acc]) / (double)num : 0.0;
+                    break;
+                }
+                case OUT_REP:
+                    if (cnt > 0 && o.rep >= 0 && o.rep < (int)rep_at.size()) {
+                        const size_t k = (size_t)g * ncell + rep_at[o.rep];
+                        const Cell& x = cells[k];
+                        if (x.kind == K_STR) {             // to_value's strdup: up to the first NUL
+                            const char* src = (const char*)bytes + k * SB;
+                            const size_t n = strnlen(src, x.len);
+                            char* d = (char*)malloc(n + 1);
+                            memcpy(d, src, n);
+                            d[n] = 0;
+                            v.kind = K_STR;
+                            v.u.s = d;
+                        } else {
+                            HCell h;
+                            h.kind = x.kind;
+                            h.bits = x.bits;
+                            v = to_value(h);
+                        }
+                    }
+                    break;
+                case OUT_CONST: if (cnt > 0) v = to_value(L.host[o.lit]); break;
+                default: break;
+            }
         }
     }
     return r;
@@ -2992,7 +3225,13 @@ cq_table* query_impl(cq_node* q, cqgpu_table* const* tables, int ntables) {
         groups = run_cells_aggregate(c, t, C, L);
     } else {
         try {
-            groups = run_aggregate(c, t, C, L, nullptr);
+            cq_table* direct = nullptr;
+            groups = run_aggregate(c, t, C, L, nullptr, nullptr, 0, &direct);
+            if (direct) {
+                post_ops(c, direct, q);
+                PHASE("post");
+                return direct;
+            }
             compute_vla(c, t, C, groups);
         } catch (MixedExtremes&) {
             groups = run_cells_aggregate(c, t, C, L);

@@ -40,6 +40,7 @@
 #include <unordered_set>
 #include "plan.h"
 #include "scanlib.h"
+#include "upload.h"
 
 namespace cq {
 namespace fast {
@@ -1103,12 +1104,12 @@ hipError_t cq_launch_fast(const uint8_t* g, const cq::ScanPlan* P, const cq::Gro
     tabs[0] = *gt;
     if (rt) tabs[1] = *rt;
     else memset(&tabs[1], 0, sizeof tabs[1]);
-    hipError_t e = hipMemcpyAsync(tabs_dev[dev & 63], tabs, sizeof tabs, hipMemcpyHostToDevice, s);
+    hipError_t e = cq::upload_buffer(tabs_dev[dev & 63], tabs, sizeof tabs, s);
     if (e != hipSuccess) return e;
     const bool comma = P->delim == ',' && P->quote == '"';
     const fast_fn_t fn = grouped ? pick_fast<true>(where, ns, comma, canon) : pick_fast<false>(where, ns, comma, canon);
     const size_t lds = fast_lds(grouped, ns);
-    (void)hipFuncSetAttribute((const void*)fn, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds);
+    cq::set_max_lds((const void*)fn, (int)lds);
     hipLaunchKernelGGL(fn, dim3(grid), dim3(fast::LT), lds, s, g, stats, slow_list, slow_cap, fp,
                        (const GroupTable*)tabs_dev[dev & 63]);
     return hipGetLastError();

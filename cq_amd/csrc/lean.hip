@@ -63,6 +63,7 @@
 #include <cstring>
 #include "plan.h"
 #include "scanlib.h"
+#include "upload.h"
 
 namespace cq {
 namespace lean {
@@ -1567,13 +1568,13 @@ hipError_t cq_launch_lean(const uint8_t* g, const cq::ScanPlan* P, const cq::Gro
     if (rt) tabs[1] = *rt;
     else memset(&tabs[1], 0, sizeof tabs[1]);
     {
-        hipError_t e = hipMemcpyAsync(tabs_dev, tabs, sizeof tabs, hipMemcpyHostToDevice, s);
+        hipError_t e = cq::upload_buffer(tabs_dev, tabs, sizeof tabs, s);
         if (e != hipSuccess) return e;
     }
     if (grouped && row_out) return hipErrorInvalidValue;   // the grouped kernels emit no rows
     const lean_fn_t fn = !grouped ? pick_fn<false, false>(wm, ns, canon)
                                   : (k16 ? pick_fn<true, true>(wm, ns, canon) : pick_fn<true, false>(wm, ns, canon));
-    (void)hipFuncSetAttribute((const void*)fn, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds);
+    cq::set_max_lds((const void*)fn, (int)lds);
     hipLaunchKernelGGL(fn, dim3(grid), dim3(lean::LT), lds, s, g, stats, row_out, row_cap, slow_list, slow_cap,
                        args, (const GroupTable*)tabs_dev);
     return hipGetLastError();

@@ -40,8 +40,12 @@
 #include <algorithm>
 #include <cstdlib>
 #include <cstring>
+#include <map>
+#include <mutex>
+#include <tuple>
 #include "plan.h"
 #include "scanlib.h"
+#include "upload.h"
 
 namespace cq {
 
@@ -2386,9 +2390,9 @@ hipError_t cq_launch_scan(const uint8_t* g, const cq::ScanPlan* P, const cq::Gro
                           cq::Cell* cells_out, unsigned long long* slow_list, unsigned long long slow_cap) {
     if (cq_scan_uses_lean(P, cells_out != nullptr) && (!grouped || rt)) {
         // slow_kernel reads this file's plan and table symbols
-        hipError_t e0 = hipMemcpyToSymbolAsync(HIP_SYMBOL(cq::c_plan), P, sizeof *P, 0, hipMemcpyHostToDevice, s);
+        hipError_t e0 = cq::upload_symbol((const void*)&HIP_SYMBOL(cq::c_plan), P, sizeof *P, s);
         if (e0 == hipSuccess)
-            e0 = hipMemcpyToSymbolAsync(HIP_SYMBOL(cq::c_gt), gt, sizeof *gt, 0, hipMemcpyHostToDevice, s);
+            e0 = cq::upload_symbol((const void*)&HIP_SYMBOL(cq::c_gt), gt, sizeof *gt, s);
         if (e0 != hipSuccess) return e0;
         // one 16-wave block per CU, each wave streaming its own windows
         const uint64_t hi = P->range_end < P->n ? P->range_end : P->n;
@@ -2415,12 +2419,12 @@ hipError_t cq_launch_scan(const uint8_t* g, const cq::ScanPlan* P, const cq::Gro
         }
     }
     const size_t lds = cq_scan_lds_bytes(P, grouped);
-    hipError_t e = hipMemcpyToSymbolAsync(HIP_SYMBOL(cq::c_plan), P, sizeof *P, 0, hipMemcpyHostToDevice, s);
-    if (e == hipSuccess) e = hipMemcpyToSymbolAsync(HIP_SYMBOL(cq::c_gt), gt, sizeof *gt, 0, hipMemcpyHostToDevice, s);
+    hipError_t e = cq::upload_symbol((const void*)&HIP_SYMBOL(cq::c_plan), P, sizeof *P, s);
+    if (e == hipSuccess) e = cq::upload_symbol((const void*)&HIP_SYMBOL(cq::c_gt), gt, sizeof *gt, s);
     if (e != hipSuccess) return e;
     const uint32_t h = cq_scan_lds_slots(P, grouped);
     const scan_fn_t fn = scan_fn(P, grouped);
-    (void)hipFuncSetAttribute((const void*)fn, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds);
+    cq::set_max_lds((const void*)fn, (int)lds);
     hipLaunchKernelGGL(fn, dim3(grid), dim3(cq::SCAN_T), lds, s, g, stats, row_out, row_cap, h, cells_out,
                        slow_list, slow_cap);
     e = hipGetLastError();
@@ -2438,9 +2442,23 @@ int cq_scan_occupancy(const cq::ScanPlan* P, int grouped) {
     const size_t lds = cq_scan_lds_bytes(P, grouped);
     int blocks = 0;
     const void* fn = (const void*)scan_fn(P, grouped);
-    (void)hipFuncSetAttribute(fn, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds);
+    cq::set_max_lds((const void*)fn, (int)lds);
+    // (per step otherwise: the occupancy query is a slow runtime call)
+    static std::mutex mu;
+    static std::map<std::tuple<const void*, size_t, int>, int> memo;
+    int dev = 0;
+    (void)hipGetDevice(&dev);
+    const auto key = std::make_tuple(fn, lds, dev);
+    {
+        std::lock_guard<std::mutex> g(mu);
+        auto it = memo.find(key);
+        if (it != memo.end()) return it->second;
+    }
     if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&blocks, fn, cq::SCAN_T, lds) != hipSuccess) return 1;
-    return blocks > 0 ? blocks : 1;
+    blocks = blocks > 0 ? blocks : 1;
+    std::lock_guard<std::mutex> g(mu);
+    memo[key] = blocks;
+    return blocks;
 }
 
 hipError_t cq_launch_compact(const cq::GroupTable* gt, const cq::ScanPlan* P, cq::GroupOut* out,
@@ -2449,7 +2467,7 @@ hipError_t cq_launch_compact(const cq::GroupTable* gt, const cq::ScanPlan* P, cq
     uint32_t kinds = 0;
     for (int a = 0; a < nacc; a++) kinds |= (uint32_t)P->acc[a].kind << (2 * a);
     const dim3 grid((gt->cap + 255) / 256);
-    hipError_t e = hipMemcpyToSymbolAsync(HIP_SYMBOL(cq::c_gt), gt, sizeof *gt, 0, hipMemcpyHostToDevice, s);
+    hipError_t e = cq::upload_symbol((const void*)&HIP_SYMBOL(cq::c_gt), gt, sizeof *gt, s);
     if (e != hipSuccess) return e;
     hipLaunchKernelGGL(cq::compact_kernel, grid, dim3(256), 0, s, nacc, kinds, out, count, cap_out);
     return hipGetLastError();
@@ -2458,7 +2476,7 @@ hipError_t cq_launch_compact(const cq::GroupTable* gt, const cq::ScanPlan* P, cq
 hipError_t cq_launch_gather(const uint8_t* g, const cq::ScanPlan* P, const unsigned long long* recs,
                             uint32_t nrec, cq::Cell* out, hipStream_t s) {
     if (!nrec) return hipSuccess;
-    hipError_t e = hipMemcpyToSymbolAsync(HIP_SYMBOL(cq::c_plan), P, sizeof *P, 0, hipMemcpyHostToDevice, s);
+    hipError_t e = cq::upload_symbol((const void*)&HIP_SYMBOL(cq::c_plan), P, sizeof *P, s);
     if (e != hipSuccess) return e;
     hipLaunchKernelGGL(cq::gather_kernel, dim3((nrec + 127) / 128), dim3(128), 0, s, g, recs, nrec, out);
     return hipGetLastError();
@@ -2473,27 +2491,55 @@ hipError_t cq_launch_project(const uint8_t* g, const unsigned long long* recs, u
 }
 
 namespace cq {
-// the aggregate result in one contiguous buffer for a single device-to-host copy:
-// per group its key, COUNT, first row and the plan's accumulators only
-// (40 + 40 * nacc bytes instead of the whole GroupOut), then the finish cells,
-// then their inline string bytes -- sections laid out by the device's group count
+// the aggregate result in one contiguous buffer (host-mapped: no copy, one sync):
+// per group its key, COUNT, first row and the plan's accumulators only (40 + 40 *
+// nacc bytes instead of the whole GroupOut), then the finish cells, then their
+// inline string bytes -- sections laid out by the device's group count.  With
+// `order` and at most PACK_ORDER_MAX groups, group i lands at its rank in (first
+// row, index) order: create_groups' first-appearance order, so the host does not
+// sort.  `hdr` (optional) receives the scan statistics and the group count.
+constexpr uint32_t PACK_ORDER_MAX = 8192;
 __global__ void pack_result_kernel(const GroupOut* __restrict__ out, const unsigned int* __restrict__ count,
                                    unsigned int cap_out, int nacc, const Cell* __restrict__ cells,
                                    const uint8_t* __restrict__ bytes, uint32_t ncell, uint32_t sb,
-                                   uint8_t* __restrict__ dst) {
+                                   uint8_t* __restrict__ dst, const ScanStats* __restrict__ stats,
+                                   uint8_t* __restrict__ hdr, int order) {
     const uint32_t ng = min(*count, cap_out);
     const uint32_t rec = 40u + 40u * (uint32_t)nacc;
     const uint32_t i = blockIdx.x * blockDim.x + threadIdx.x;
+    if (hdr && blockIdx.x == 0) {
+        const uint32_t nw = (uint32_t)(sizeof(ScanStats) / 4);
+        for (uint32_t k = threadIdx.x; k < nw; k += blockDim.x) ((uint32_t*)hdr)[k] = ((const uint32_t*)stats)[k];
+        if (threadIdx.x == 0) *(uint32_t*)(hdr + sizeof(ScanStats)) = ng;
+    }
+    uint32_t r = i;
+    if (order && ng <= PACK_ORDER_MAX) {
+        __shared__ unsigned long long tile[1024];
+        const unsigned long long fi = i < ng ? out[i].first : 0ull;
+        uint32_t below = 0;
+        for (uint32_t base = 0; base < ng; base += 1024) {
+            const uint32_t m = min(1024u, ng - base);
+            __syncthreads();
+            for (uint32_t k = threadIdx.x; k < m; k += blockDim.x) tile[k] = out[base + k].first;
+            __syncthreads();
+            if (i < ng)
+                for (uint32_t k = 0; k < m; k++) {
+                    const unsigned long long f = tile[k];
+                    below += (f < fi) | ((f == fi) & (base + k < i));
+                }
+        }
+        r = below;
+    }
     if (i >= ng) return;
     const GroupOut& o = out[i];
-    uint8_t* r = dst + (size_t)i * rec;
-    ((uint32_t*)r)[0] = o.clslen;
-    ((uint32_t*)r)[1] = 0;
-    ((uint64_t*)r)[1] = o.w0;
-    ((uint64_t*)r)[2] = o.w1;
-    ((unsigned long long*)r)[3] = o.cnt;
-    ((unsigned long long*)r)[4] = o.first;
-    uint64_t* q = (uint64_t*)(r + 40);
+    uint8_t* rp = dst + (size_t)r * rec;
+    ((uint32_t*)rp)[0] = o.clslen;
+    ((uint32_t*)rp)[1] = 0;
+    ((uint64_t*)rp)[1] = o.w0;
+    ((uint64_t*)rp)[2] = o.w1;
+    ((unsigned long long*)rp)[3] = o.cnt;
+    ((unsigned long long*)rp)[4] = o.first;
+    uint64_t* q = (uint64_t*)(rp + 40);
     for (int a = 0; a < nacc; a++) {
         q[5 * a + 0] = dbl_bits(o.sum[a]);
         q[5 * a + 1] = o.num[a];
@@ -2502,10 +2548,10 @@ __global__ void pack_result_kernel(const GroupOut* __restrict__ out, const unsig
         q[5 * a + 4] = o.extpos[a];
     }
     Cell* dc = (Cell*)(dst + (size_t)ng * rec);
-    for (uint32_t k = 0; k < ncell; k++) dc[(size_t)i * ncell + k] = cells[(size_t)i * ncell + k];
+    for (uint32_t k = 0; k < ncell; k++) dc[(size_t)r * ncell + k] = cells[(size_t)i * ncell + k];
     uint8_t* db = (uint8_t*)(dc + (size_t)ng * ncell);
     const uint4* sbs = (const uint4*)(bytes + (size_t)i * ncell * sb);
-    uint4* dbs = (uint4*)(db + (size_t)i * ncell * sb);
+    uint4* dbs = (uint4*)(db + (size_t)r * ncell * sb);
     for (uint32_t k = 0; k < ncell * sb / 16; k++) dbs[k] = sbs[k];
 }
 }  // namespace cq
@@ -2515,12 +2561,13 @@ size_t cq_pack_result_bytes(unsigned int ng, int nacc, uint32_t ncell, uint32_t 
 }
 hipError_t cq_launch_pack_result(const cq::GroupOut* out, const unsigned int* count, unsigned int cap_out, int nacc,
                                  const cq::Cell* cells, const uint8_t* bytes, uint32_t ncell, uint32_t sb,
-                                 uint8_t* dst, hipStream_t s) {
+                                 uint8_t* dst, const cq::ScanStats* stats, uint8_t* hdr, int order, hipStream_t s) {
     if (sb % 16) return hipErrorInvalidValue;
     hipLaunchKernelGGL(cq::pack_result_kernel, dim3((cap_out + 127) / 128), dim3(128), 0, s, out, count, cap_out, nacc,
-                       cells, bytes, ncell, sb, dst);
+                       cells, bytes, ncell, sb, dst, stats, hdr, order);
     return hipGetLastError();
 }
+unsigned int cq_pack_order_max() { return cq::PACK_ORDER_MAX; }
 hipError_t cq_launch_finish(const uint8_t* g, uint64_t n, const cq::GroupOut* out, const unsigned int* count,
                             unsigned int cap_out, const cq::FinishDesc* D, cq::Cell* cells, uint8_t* bytes,
                             hipStream_t s) {
@@ -2604,8 +2651,8 @@ hipError_t cq_launch_join_fill(const unsigned int* flags, const unsigned int* po
 hipError_t cq_launch_join_agg(const uint2* pairs, unsigned long long np, const cq::JoinMap* M, const cq::Cell* L,
                               const cq::Cell* R, const cq::ScanPlan* P, const cq::GroupTable* gt,
                               cq::ScanStats* stats, int grouped, hipStream_t s) {
-    hipError_t e = hipMemcpyToSymbolAsync(HIP_SYMBOL(cq::c_plan), P, sizeof *P, 0, hipMemcpyHostToDevice, s);
-    if (e == hipSuccess) e = hipMemcpyToSymbolAsync(HIP_SYMBOL(cq::c_gt), gt, sizeof *gt, 0, hipMemcpyHostToDevice, s);
+    hipError_t e = cq::upload_symbol((const void*)&HIP_SYMBOL(cq::c_plan), P, sizeof *P, s);
+    if (e == hipSuccess) e = cq::upload_symbol((const void*)&HIP_SYMBOL(cq::c_gt), gt, sizeof *gt, s);
     if (e != hipSuccess || !np) return e;
     const unsigned grid = (unsigned)std::min<uint64_t>(grid_of(np, 256), 4096);
     hipLaunchKernelGGL(cq::join_agg_kernel, dim3(grid), dim3(256), 0, s, pairs, np, *M, L, R, stats, grouped);
@@ -2615,8 +2662,8 @@ size_t cq_join_sum_lds(int nacc) { return (size_t)cq::JS_SLOTS * (32 + 12 * (siz
 hipError_t cq_launch_join_sum(const uint2* pairs, unsigned long long np, const cq::JoinMap* M, const cq::Cell* L,
                               const cq::Cell* R, const cq::ScanPlan* P, const cq::GroupTable* gt,
                               cq::ScanStats* stats, int ncu, hipStream_t s) {
-    hipError_t e = hipMemcpyToSymbolAsync(HIP_SYMBOL(cq::c_plan), P, sizeof *P, 0, hipMemcpyHostToDevice, s);
-    if (e == hipSuccess) e = hipMemcpyToSymbolAsync(HIP_SYMBOL(cq::c_gt), gt, sizeof *gt, 0, hipMemcpyHostToDevice, s);
+    hipError_t e = cq::upload_symbol((const void*)&HIP_SYMBOL(cq::c_plan), P, sizeof *P, s);
+    if (e == hipSuccess) e = cq::upload_symbol((const void*)&HIP_SYMBOL(cq::c_gt), gt, sizeof *gt, s);
     if (e != hipSuccess || !np) return e;
     const size_t lds = cq_join_sum_lds(P->nacc);
     const unsigned grid = (unsigned)std::min<uint64_t>(grid_of(np, 512), (uint64_t)std::max(ncu, 1) * 2);
@@ -2625,7 +2672,7 @@ hipError_t cq_launch_join_sum(const uint2* pairs, unsigned long long np, const c
 }
 hipError_t cq_launch_join_filter(const uint2* pairs, unsigned long long np, const cq::JoinMap* M, const cq::Cell* L,
                                  const cq::Cell* R, const cq::ScanPlan* P, unsigned int* flags, hipStream_t s) {
-    hipError_t e = hipMemcpyToSymbolAsync(HIP_SYMBOL(cq::c_plan), P, sizeof *P, 0, hipMemcpyHostToDevice, s);
+    hipError_t e = cq::upload_symbol((const void*)&HIP_SYMBOL(cq::c_plan), P, sizeof *P, s);
     if (e != hipSuccess || !np) return e;
     hipLaunchKernelGGL(cq::join_filter_kernel, dim3(grid_of(np, 256)), dim3(256), 0, s, pairs, np, *M, L, R, flags);
     return hipGetLastError();
@@ -2652,7 +2699,7 @@ hipError_t cq_launch_vla_pair_prep(const uint2* pairs, uint32_t n, const cq::Joi
                                    const cq::Cell* L, const cq::Cell* R, const cq::ScanPlan* P, int grouped,
                                    unsigned long long* kw0, unsigned long long* kw1, unsigned long long* kcl,
                                    unsigned long long* vkey, unsigned int* flag, hipStream_t s) {
-    hipError_t e = hipMemcpyToSymbolAsync(HIP_SYMBOL(cq::c_plan), P, sizeof *P, 0, hipMemcpyHostToDevice, s);
+    hipError_t e = cq::upload_symbol((const void*)&HIP_SYMBOL(cq::c_plan), P, sizeof *P, s);
     if (e != hipSuccess || !n) return e;
     hipLaunchKernelGGL(cq::vla_pair_prep_kernel, dim3(grid_of(n, 256)), dim3(256), 0, s, pairs, n, *M, *V, L, R, grouped,
                        kw0, kw1, kcl, vkey, flag);
