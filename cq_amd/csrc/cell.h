@@ -685,6 +685,79 @@ CQ_HD bool text_has_tab(const Cell& c) {
     return false;
 }
 
+// A composite key whose text parts hold a tab (evaluator.c:124 joins the parts with
+// '\t', so two different part lists can join to the same text): the joined text
+// itself, rendered as evaluator.c:127-170 renders each part (NULL "NULL", %lld,
+// %.6f, %04d-%02d-%02d, the string up to its first NUL or 255 bytes), hashed as one
+// byte stream into two independent 64-bit lanes.  A list with a tab inside a part
+// never joins to the same text as a list without one (its text has more tabs), so
+// these keys (GK_COMP, len = part count | COMPT_FLAG) never meet the per-part
+// digests.  false: a DOUBLE part of 2^43 or more (its %.6f text is not rendered here).
+constexpr uint32_t COMPT_FLAG = 0x8000;
+struct TextHash {
+    uint64_t a = 0xCBF29CE484222325ULL, b = 0x84222325CBF29CE4ULL;
+    CQ_HDM void byte(uint8_t c) {
+        a = (a ^ c) * 0x100000001B3ULL;
+        b = (b ^ (c + 0x5Bu)) * 0x1000000000000B3ULL;
+    }
+    CQ_HDM void bytes(const uint8_t* p, uint32_t n) { for (uint32_t i = 0; i < n; i++) byte(p[i]); }
+    CQ_HDM void dec(uint64_t v, int mind) {          // decimal digits, zero padded to mind
+        uint8_t t[20];
+        int n = 0;
+        do { t[n++] = (uint8_t)('0' + v % 10); v /= 10; } while (v);
+        while (n < mind) t[n++] = '0';
+        while (n) byte(t[--n]);
+    }
+};
+CQ_HD bool joined_text_add(TextHash& h, const Cell& c, bool first) {
+    if (!first) h.byte('\t');
+    switch (c.kind) {
+        case K_NULL: h.bytes((const uint8_t*)"NULL", 4); break;
+        case K_INT: {
+            const int64_t v = (int64_t)c.bits;
+            if (v < 0) h.byte('-');
+            h.dec(v < 0 ? 0ULL - (uint64_t)v : (uint64_t)v, 1);
+            break;
+        }
+        case K_DBL: {
+            const double x = as_dbl(c.bits), ax = x < 0 ? -x : x;
+            if (!(ax < 8796093022208.0)) return false;
+            const uint64_t u = micro_units(ax);
+            if (c.bits >> 63) h.byte('-');
+            h.dec(u / 1000000ULL, 1);
+            h.byte('.');
+            h.dec(u % 1000000ULL, 6);
+            break;
+        }
+        case K_DATE: {
+            const int32_t y = (int32_t)(c.bits >> 32);
+            const uint32_t m = (uint32_t)((c.bits >> 16) & 0xffff), d = (uint32_t)(c.bits & 0xffff);
+            if (y < 0) h.byte('-');
+            h.dec(y < 0 ? (uint64_t)(-(int64_t)y) : (uint64_t)y, y < 0 ? 3 : 4);
+            h.byte('-');
+            h.dec(m, 2);
+            h.byte('-');
+            h.dec(d, 2);
+            break;
+        }
+        default: {
+            const uint8_t* p = (const uint8_t*)(uintptr_t)c.bits;
+            const uint32_t n = c.len < 255 ? c.len : 255;
+            for (uint32_t i = 0; i < n && p[i]; i++) h.byte(p[i]);
+            break;
+        }
+    }
+    return true;
+}
+CQ_HD GKey joined_text_key(const TextHash& h, uint32_t nparts) {
+    GKey k;
+    k.cls = GK_COMP;
+    k.len = nparts | COMPT_FLAG;
+    k.w0 = mix64(h.a ^ (h.b >> 17));
+    k.w1 = mix64(h.b + 0x9E3779B97F4A7C15ULL * h.a);
+    return k;
+}
+
 CQ_HD bool gk_equal(const GKey& a, const GKey& b) {
     if (a.cls != b.cls || a.len != b.len || a.w1 != b.w1) return false;
     if (a.w0 == b.w0) return true;

@@ -1017,7 +1017,7 @@ void compile_aggregate(const cqgpu_table* t, cq_node* q, Compiled& C) {
         // a GROUP BY name matching a SELECT alias groups by that item's expression
         // (evaluator.c:71-98)
         const int nk = gb->u.grp.nkeys;
-        if (nk > MAX_GPART) throw Ineligible{"GROUP BY of more than 4 parts"};
+        if (nk > MAX_GPART) throw Ineligible{"GROUP BY of more than 8 parts"};
         std::vector<cq_node*> gexpr(nk, nullptr);
         cq_node* sel = q->u.q.select;
         for (int g = 0; g < nk; g++) {
@@ -2672,7 +2672,7 @@ std::vector<HGroup> aggregate_pairs(DevCtx& c, Compiled& C, const JoinMap& MA, c
         break;
     }
     g_stats.passed = st.passed;
-    if (st.key_flags & 1u) throw Ineligible{"composite GROUP BY key text holding a tab"};
+    if (st.key_flags & 2u) throw Ineligible{"composite GROUP BY: a part list with a tab and a DOUBLE of 2^43 or more"};
     std::vector<int> rep_ord(C.rep_cols.size());
     for (size_t i = 0; i < rep_ord.size(); i++) rep_ord[i] = (int)i;
     std::vector<HGroup> groups =

@@ -9,7 +9,7 @@ constexpr int MAX_NEED = 8;     // distinct CSV columns one scan parses
 constexpr int MAX_PROG = 128;   // predicate instructions
 constexpr int MAX_CONST = 48;   // literal cells
 constexpr int MAX_ACC = 8;      // accumulators (one per aggregate SELECT item)
-constexpr int MAX_GPART = 4;    // composite GROUP BY parts (the reference's 1024-byte key holds 4)
+constexpr int MAX_GPART = 8;    // composite GROUP BY parts (the reference's list grows without bound)
 constexpr int VM_STACK = 8;
 
 // predicate bytecode (WHERE tree of evaluator_conditions.c:62-164 and
@@ -156,7 +156,7 @@ struct ScanStats {
     unsigned int acc_classes[MAX_ACC];  // OR of value classes seen per accumulator (1 num, 2 str, 4 date)
     unsigned long long slow_records;    // records the fast field walk handed to the general parser
     unsigned long long clk[8];          // profiling builds (CQ_CLOCKS): shader cycles per phase, summed over waves
-    unsigned int key_flags;             // composite GROUP BY: 1 = a text part holds a tab (key texts may collide)
+    unsigned int key_flags;             // composite GROUP BY: 2 = a tab list with a DOUBLE part >= 2^43 (refused)
 };
 
 // a MIN/MAX candidate published by one block (or wave) for one group

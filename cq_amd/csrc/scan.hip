@@ -1221,20 +1221,37 @@ __device__ Cell eval_expr_vm(const ScanPlan& P, const Cell* kc, const CellsT<N>&
 
 // the group key of a record: the GROUP BY column's canonical key, one expression's
 // (create_groups_by_expression), or the composite digest of several parts (cell.h
-// CompKey; `tab`: a text part holds a tab)
+// CompKey); a part list with a tab inside a text part keys on its joined text
+// (cell.h joined_text_key).  `tab`: such a list held a DOUBLE part the joined
+// text cannot render (the plan is refused)
+template <int N>
+__device__ Cell plan_group_part(const ScanPlan& P, const Cell* kc, const CellsT<N>& cs, int nneed, int k) {
+    const int s = P.gpart_slot[k];
+    return s >= 0 ? get_cell(cs, s, nneed)
+                  : (s == -1 ? eval_expr_vm(P, kc, cs, P.gcode_off[k], P.gcode_off[k + 1]) : cell_null());
+}
 template <int N>
 __device__ GKey plan_group_key(const ScanPlan& P, const Cell* kc, const CellsT<N>& cs, int nneed, bool& tab) {
     if (P.ngpart == 0) return group_key(get_cell(cs, P.group_slot, nneed));
     CompKey ck;
+    bool has_tab = false;
     for (int k = 0; k < MAX_GPART; k++) {
         if (k >= P.ngpart) break;
-        const int s = P.gpart_slot[k];
-        const Cell c = s >= 0 ? get_cell(cs, s, nneed)
-                              : (s == -1 ? eval_expr_vm(P, kc, cs, P.gcode_off[k], P.gcode_off[k + 1]) : cell_null());
+        const Cell c = plan_group_part(P, kc, cs, nneed, k);
         const GKey pk = group_key(c);
         if (P.ngpart == 1) return pk;
-        tab = tab || text_has_tab(c);
+        has_tab = has_tab || text_has_tab(c);
         ck.add(pk);
+    }
+    if (has_tab) {                                      // rare: the joined text
+        TextHash h;
+        bool ok = true;
+        for (int k = 0; k < MAX_GPART; k++) {
+            if (k >= P.ngpart) break;
+            ok = joined_text_add(h, plan_group_part(P, kc, cs, nneed, k), k == 0) && ok;
+        }
+        tab = tab || !ok;
+        return joined_text_key(h, (uint32_t)P.ngpart);
     }
     return comp_key(ck, (uint32_t)P.ngpart);
 }
@@ -1831,7 +1848,7 @@ __global__ __launch_bounds__(256) void join_agg_kernel(const uint2* __restrict__
         if (grouped && pass) {
             bool tab = false;
             key = plan_group_key(P, P.consts, cs, nneed, tab);
-            if (tab) atomicOr(&stats->key_flags, 1u);
+            if (tab) atomicOr(&stats->key_flags, 2u);
             h = gk_hash(key);
         }
         int gi = -1;
@@ -1954,7 +1971,7 @@ __global__ __launch_bounds__(512) __attribute__((amdgpu_waves_per_eu(4))) void j
             my_pass++;
             bool tab = false;
             key = plan_group_key(P, P.consts, cs, nneed, tab);
-            if (tab) atomicOr(&stats->key_flags, 1u);
+            if (tab) atomicOr(&stats->key_flags, 2u);
             h = gk_hash(key);
         }
         // the block's slot of the key (wave-uniform loop: claims publish within the trip)

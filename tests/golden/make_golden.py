@@ -66,6 +66,20 @@ EDGE = {
         b"\"1234\"\"\",\"1.5\"\"\",r,s\n"
         b"  \"lead\" ,\"trail\"  ,  plain  ,\"a\"\"b\"\"c\"\n"
     ),
+    # composite GROUP BY text parts holding a tab (evaluator.c:124 joins parts with '\t')
+    "edge_tabs.csv": (
+        b"t1,t2,t3,n\n"
+        b"a\tb,c,x,1\n"
+        b"a,b\tc,x,2\n"
+        b"a,b,c,3\n"
+        b"a\tb,c,y,4\n"
+        b"p\tq\tr,s,x,5\n"
+        b"p,q\tr\ts,x,6\n"
+        b"p\tq,r\ts,x,7\n"
+        b"a,b,c,8\n"
+        b"1\t2,3,x,9\n"
+        b"1,2\t3,x,10\n"
+    ),
     # whitespace and field splitting (csv_reader.c:285-338)
     "edge_ws.csv": (
         b"w1,w2,w3,w4\n"
@@ -219,6 +233,24 @@ QUERIES = [
     f"SELECT gender, role, STDDEV(height), MEDIAN(age) FROM {R} GROUP BY gender, role",
     f"SELECT age / 10 AS decade, MEDIAN(height), STDDEV(height), COUNT(*) FROM {R} WHERE gender = 'm' GROUP BY decade",
     f"SELECT role, active, MEDIAN(age) FROM {T} GROUP BY role, active",
+    # GROUP BY on a joined table by unqualified names: single-column through
+    # find_column_index_with_fallback against the joined header (0 groups,
+    # evaluator_aggregates.c:114 / evaluator.c:108), composite through
+    # csv_get_column_index where a missing name is the part "NULL" (evaluator.c:152)
+    f"SELECT role, COUNT(*) FROM {U} AS u JOIN {O} AS o ON u.id = o.customer_id GROUP BY role",
+    f"SELECT COUNT(*), SUM(o.price) FROM {SU} AS u JOIN {SO} AS o ON u.id = o.customer_id GROUP BY role",
+    f"SELECT u.role, COUNT(*) FROM {U} AS u JOIN {O} AS o ON u.id = o.customer_id GROUP BY role, u.active",
+    f"SELECT u.role, COUNT(*), SUM(o.price) FROM {SU} AS u JOIN {SO} AS o ON u.id = o.customer_id WHERE u.age > 70 GROUP BY u.role, quantity",
+    # composite GROUP BY beyond four parts (parser_clauses.c:241-246 grows the list)
+    # (at most 4 SELECT items: a 5th overflows the reference's parser)
+    f"SELECT name, role, COUNT(*) FROM {T} GROUP BY name, age, role, height, active",
+    f"SELECT name, COUNT(*), SUM(age) FROM {T} GROUP BY id, name, age, role, height, active",
+    f"SELECT gender, role, COUNT(*), SUM(height) FROM {R} WHERE age > 77 GROUP BY gender, role, age, height, name",
+    f"SELECT role, COUNT(*) FROM {R} WHERE age > 78 GROUP BY gender, role, age, height, name, age, gender",
+    # composite parts holding a tab: the joined text is the key
+    "SELECT t1, t2, COUNT(*), SUM(n) FROM '{D}/edge_tabs.csv' GROUP BY t1, t2",
+    "SELECT t1, t2, t3, COUNT(*) FROM '{D}/edge_tabs.csv' GROUP BY t1, t2, t3",
+    "SELECT t2, t1, COUNT(*) FROM '{D}/edge_tabs.csv' WHERE n > 1 GROUP BY t2, t1",
     # row-returning (build_result)
     f"SELECT name, age FROM {T} WHERE age > 30",
     f"SELECT * FROM {T} WHERE age > 30",

@@ -79,12 +79,65 @@ def test_composite_typed_parts(tmp_path):
         compare(got, want, tol, sql)
 
 
-def test_tab_in_composite_part_refused(tmp_path):
-    p = tmp_path / "tab.csv"
-    p.write_bytes(b"a,b\nx\ty,1\nx,y\t1\n")
-    with cqtest.Parsed(f"SELECT a, b, COUNT(*) FROM '{p}' GROUP BY a, b") as ast:
+def test_tab_in_composite_parts(tmp_path):
+    """text parts holding a tab key on the joined text (evaluator.c:124): ("x\ty", 1)
+    and ("x", "y\t1") are one group; numbers, dates, NULL and expressions render as
+    the reference renders them (%lld, %.6f, %04d-%02d-%02d, "NULL"); also across
+    range partials"""
+    import random
+    rng = random.Random(5)
+    a_vals = ["x\ty", "x", "1\t2", "1", "", "2024-01-05\tz", "2024-01-05", "p\tq\tr", "p", "0.5\t1"]
+    b_vals = ["1", "y\t1", "2", "2\t3", "", "z", "q\tr", "1.5", "2024-01-05", "1\t0.500000"]
+    rows = ["a,b,c"] + ["%s,%s,%d" % (rng.choice(a_vals), rng.choice(b_vals), rng.randrange(9))
+                        for _ in range(4000)]
+    p = tmp_path / "tabs.csv"
+    p.write_text("\n".join(rows) + "\n")
+    sqls = (f"SELECT a, b, COUNT(*), SUM(c) FROM '{p}' GROUP BY a, b",
+            f"SELECT b, COUNT(*) FROM '{p}' GROUP BY b, a, c",
+            f"SELECT a, c / 2 AS h, COUNT(*) FROM '{p}' WHERE c > 2 GROUP BY a, h",
+            f"SELECT a, COUNT(*) FROM '{p}' GROUP BY a, b, nosuch")
+    for sql in sqls:
+        want, unsup = cqtest.oracle_query(sql)
+        assert not unsup
+        with cqtest.Parsed(sql) as ast:
+            got = cq_amd.evaluate(ast)
+            tol = tolerant_columns(ast)
+            assert not cq_amd.last_ineligible(), (sql, cq_amd.last_ineligible())
+            compare(got, want, tol, sql)
+            tabs = [cq_amd.Table.open_range(str(p), r, 3) for r in range(3)]
+            blobs = [cq_amd.query_partial(ast, [t]) for t in tabs]
+            for t in tabs:
+                t.close()
+            from cq_amd import abi
+            tp = cq_amd.merge_partials(ast, blobs)
+            assert tp, cq_amd.last_error()
+            merged = abi.table_to_py(tp)
+            cq_amd.result_free(tp)
+        compare(merged, want, tol, sql + " (3 partials)")
+
+
+def test_many_parts_across_partials(synth):
+    """GROUP BY of 6 parts (the reference's list grows without bound,
+    parser_clauses.c:241-246) on one GPU and over 4 range partials"""
+    sql = (f"SELECT role, COUNT(*), SUM(height) FROM '{synth}' WHERE age > 70 "
+           f"GROUP BY gender, role, age, name, height, surname")
+    want, unsup = cqtest.oracle_query(sql)
+    assert not unsup
+    with cqtest.Parsed(sql) as ast:
         got = cq_amd.evaluate(ast)
-    assert got is None and "tab" in cq_amd.last_ineligible()
+        tol = tolerant_columns(ast)
+        assert not cq_amd.last_ineligible(), cq_amd.last_ineligible()
+        compare(got, want, tol, sql)
+        tabs = [cq_amd.Table.open_range(synth, r, 4) for r in range(4)]
+        blobs = [cq_amd.query_partial(ast, [t]) for t in tabs]
+        for t in tabs:
+            t.close()
+        from cq_amd import abi
+        tp = cq_amd.merge_partials(ast, blobs)
+        assert tp, cq_amd.last_error()
+        merged = abi.table_to_py(tp)
+        cq_amd.result_free(tp)
+    compare(merged, want, tol, sql + " (4 partials)")
 
 
 def test_composite_across_partials(synth):

@@ -176,3 +176,20 @@ def test_join_chain_vs_oracle(files, tmpl):
         from test_gpu_parity import tolerant_columns
         tol = tolerant_columns(ast)
     compare(got, want, tol, sql)
+
+
+def test_hash_build_high_contention(tmp_path):
+    """hash_build_kernel's relaxed publish (memory model) under
+    contention: a build side of 120,000 rows over only 48 distinct keys (about 2,500
+    copies of each, inserted concurrently from every CU) joined with a probe side;
+    counts, per-key groups and sums must equal the oracle's nested-loop join"""
+    rng = np.random.default_rng(23)
+    b = ["k,w"] + [f"{int(rng.integers(0, 48))},{i % 1000}" for i in range(120_000)]
+    a = ["k,v"] + [f"{int(rng.integers(0, 64))},{i}" for i in range(300)]
+    pa, pb = tmp_path / "a.csv", tmp_path / "b.csv"
+    pa.write_text("\n".join(a) + "\n")
+    pb.write_text("\n".join(b) + "\n")
+    for sql in (f"SELECT COUNT(*) FROM '{pa}' AS a JOIN '{pb}' AS b ON a.k = b.k",
+                f"SELECT a.k, COUNT(*), SUM(b.w) FROM '{pa}' AS a JOIN '{pb}' AS b ON a.k = b.k GROUP BY a.k",
+                f"SELECT b.k, COUNT(*), SUM(a.v) FROM '{pb}' AS b JOIN '{pa}' AS a ON b.k = a.k GROUP BY b.k"):
+        _check(sql, expect_rows=1)

@@ -205,6 +205,50 @@ def test_dense_merge_typed_keys(tmp_path):
         compare(got, want, tol, f"dense typed keys, {n} ranks")
 
 
+def test_dict_build_high_contention(tmp_path):
+    """dict_build_kernel's relaxed publish (memory model) under
+    contention: one rank's 1,000 keys, then 63 more copies of them with each key's
+    copies adjacent (63,000 inserts of the same 1,000 keys from every CU, lanes of a
+    wave racing for one slot) must build exactly the 1,000-entry dictionary, and the
+    merge through it must equal the oracle's answer"""
+    import torch
+    from cq_amd.dist import DensePartial
+    p = tmp_path / "role.csv"
+    datagen.write_shape_a(str(p), 60_000, seed=31, with_role=True)
+    q = f"SELECT role, COUNT(*), SUM(height), AVG(height) FROM '{p}' GROUP BY role"
+    want, unsup = cqtest.oracle_query(q)
+    assert not unsup
+    with cqtest.Parsed(q) as ast:
+        t = cq_amd.Table.open_range(str(p), 0, 1)
+        part = DensePartial(ast, t)
+        try:
+            assert part.ok, cq_amd.last_ineligible()
+            m = part.m
+            assert m == len(want["rows"]) == 1000
+            keys = part.keys("cuda").view(m, DensePartial.KEYREC)
+            dups = keys.unsqueeze(1).expand(m, 63, DensePartial.KEYREC).reshape(-1)
+            all_keys = torch.cat([keys.reshape(-1), dups]).contiguous()
+            torch.cuda.synchronize()
+            for _ in range(3):
+                g = part.dict(all_keys, 64 * m, 0)
+                assert g == m
+            ds = torch.empty(g * part.W, dtype=torch.float64, device="cuda")
+            df = torch.empty(g, dtype=torch.int64, device="cuda")
+            dr = torch.empty(2 * g, dtype=torch.int64, device="cuda")
+            part.scatter(ds, df, dr)
+            part.mask_reps(df, dr)
+            torch.cuda.synchronize()
+            tp = part.finish(ds, df, dr)
+            assert tp, cq_amd.last_error()
+            got = abi.table_to_py(tp)
+            cq_amd.result_free(tp)
+            tol = tolerant_columns(ast)
+        finally:
+            part.free()
+            t.close()
+    compare(got, want, tol, "dictionary under contention")
+
+
 def test_dense_merge_refuses_minmax(files):
     q = QUERIES[2].format(p=files["plain"])
     with cqtest.Parsed(q) as ast:
