@@ -146,7 +146,7 @@ def main():
     import cq_amd
     from cq_amd import abi
     from cq_amd.dist import exchange, exclusive_base, gather_blobs
-    cq_amd.lib()
+    L = cq_amd.lib()
 
     t0 = time.time()
     rng = np.random.default_rng([args.seed, rank])
@@ -188,15 +188,20 @@ def main():
             routed.append(cq_amd.table_from_routed(rb.data_ptr(), rb.numel(), rg.data_ptr(), rg.numel(), hdr))
             del sb, sg, rb, rg
         tr = time.perf_counter()
-        blob = cq_amd.query_partial(ast, routed if world > 1 else [ut, ot])
-        st = cq_amd.stats()
-        tj = time.perf_counter()
-        blobs = gather_blobs(blob, dev) if dist is not None else [blob]
+        if world == 1:     # one rank: the whole join is local (the fused aggregate join)
+            tp = L.cqgpu_query(ast, (C.c_void_p * 2)(ut.handle.value, ot.handle.value), 2)
+            st = cq_amd.stats()
+            tj = time.perf_counter()
+        else:
+            blob = cq_amd.query_partial(ast, routed)
+            st = cq_amd.stats()
+            tj = time.perf_counter()
+            blobs = gather_blobs(blob, dev)
+            tp = cq_amd.merge_partials(ast, blobs) if rank == 0 else None
         pairs = 0
         if rank == 0:
-            tp = cq_amd.merge_partials(ast, blobs)
             if not tp:
-                raise RuntimeError(cq_amd.last_error())
+                raise RuntimeError(cq_amd.last_error() or cq_amd.last_ineligible())
             res = abi.table_to_py(tp)
             cq_amd.result_free(tp)
             pairs = int(sum(r[1][1] for r in res["rows"]))   # COUNT(*) cells: ("I", n)

@@ -131,6 +131,25 @@ hipError_t cq_excl_sum_u64(void* temp, size_t* temp_bytes, const unsigned long l
 hipError_t cq_excl_sum_u32(void* temp, size_t* temp_bytes, const unsigned int* in, unsigned int* out, size_t n,
                            hipStream_t s);
 size_t cq_pack_result_bytes(unsigned int ng, int nacc, uint32_t ncell, uint32_t sb);
+hipError_t cq_launch_raw_merge(const cq::GroupTable* gt, const cq::GroupTable* rt, int nacc, cq::ScanStats* stats,
+                               hipStream_t s);
+uint64_t cq_jx_windows(uint64_t lo, uint64_t hi, uint32_t ws);
+hipError_t cq_jx_extract(const uint8_t* g, uint64_t lo, uint64_t hi, uint32_t ws, uint32_t delim, uint32_t quote,
+                         int kcol, int pcol, int build, int pass, unsigned long long* key, unsigned long long* pay,
+                         uint32_t* off, unsigned int* wcount, const unsigned int* wbase, unsigned int cap,
+                         unsigned int* flag, unsigned long long* krange, int grid, hipStream_t s);
+hipError_t cq_jx_build(const unsigned long long* key, uint32_t n, void* table, uint64_t tcap, unsigned int* flag,
+                       int grid, hipStream_t s);
+size_t cq_jx_entry_bytes();
+hipError_t cq_jx_build_direct(const unsigned long long* key, const unsigned long long* pay, const uint32_t* off,
+                              uint32_t n, unsigned long long kmin, unsigned long long range, void* D,
+                              unsigned int* flag, int grid, hipStream_t s);
+size_t cq_jx_direct_bytes();
+hipError_t cq_jx_probe(int grouped, int value, int direct, const unsigned long long* pkey,
+                       const unsigned long long* ppay, const uint32_t* poff, uint32_t n, unsigned long long kmin,
+                       const void* table, uint64_t tcap, const unsigned long long* bpay, const uint32_t* boff,
+                       const cq::GroupTable* rt, int nacc, cq::ScanStats* stats, unsigned int* flag, int grid,
+                       hipStream_t s);
 hipError_t cq_launch_pack_result(const cq::GroupOut* out, const unsigned int* count, unsigned int cap_out, int nacc,
                                  const cq::Cell* cells, const uint8_t* bytes, uint32_t ncell, uint32_t sb,
                                  uint8_t* dst, const cq::ScanStats* stats, uint8_t* hdr, int order, hipStream_t s);
@@ -2844,6 +2863,221 @@ unsigned long long build_pairs(DevCtx& c, JoinSide& A, JoinSide& B, int kl, int 
     return np;
 }
 
+// The fused aggregate join: one INNER JOIN on `ident = ident`
+// without WHERE, COUNT / SUM / AVG of one probe-side (right) column, GROUP BY one
+// build-side (left) column or none, every other item a left column.  No record-start
+// pass, no cell tables, no pair array: both sides stream through jx_extract_kernel
+// (ON key + one payload per record), the left side's keys go into an HBM hash table,
+// and every right record probes it and aggregates its pairs into LDS group tables
+// (jx_probe_kernel), then raw_merge / compact / finish (the group's first pair's left
+// record) / pack as run_aggregate.  Same groups, order and cells as aggregate_pairs:
+// a pair's order key is (left byte offset, right byte offset), the nested loop's
+// (l, r) order.  nullptr: outside this shape, or the data (a quote, a short row, a key
+// that is not a canonical INTEGER below 10^15 or NULL, a wider numeral) needs the
+// general pipeline.
+cq_table* run_fast_join(DevCtx& c, cq_node* q, Compiled& C, const cqgpu_table* L, const cqgpu_table* R, int kl,
+                        int kr, int nl) {
+    if (getenv("CQ_AMD_NO_FAST_JOIN")) return nullptr;
+    if (C.group_missing || C.P.nprog != 0 || C.P.ngpart != 0 || !C.vla.empty()) return nullptr;
+    if (L->n >= (1ull << 32) - 4096 || R->n >= (1ull << 32) - 4096) return nullptr;
+    if (L->cfg.delimiter != R->cfg.delimiter || L->cfg.quote != R->cfg.quote) return nullptr;
+    const uint32_t d = (uint8_t)L->cfg.delimiter;
+    if ((d - '0') < 10u || d == '.' || ((d | 32) >= 'a' && (d | 32) <= 'z') || d == '+' || d == '-' || d <= ' ')
+        return nullptr;
+    if ((uint8_t)L->cfg.quote == d || L->cfg.quote == '\n' || L->cfg.quote == '\r') return nullptr;
+    const bool grouped = C.grouped;
+    int gcol = -1, vcol = -1;
+    if (grouped) {
+        if (C.P.group_slot < 0) return nullptr;
+        gcol = C.need_cols[C.P.group_slot];
+        if (gcol >= nl) return nullptr;
+    }
+    for (int a = 0; a < C.P.nacc; a++) {
+        if (C.P.acc[a].kind != ACC_SUM) return nullptr;
+        const int col = C.need_cols[C.P.acc[a].slot];
+        if (col < nl) return nullptr;
+        if (vcol >= 0 && col - nl != vcol) return nullptr;
+        vcol = col - nl;
+    }
+    for (int rc : C.rep_cols)
+        if (rc >= nl) return nullptr;
+    for (const OutCol& o : C.outs)
+        if (o.kind != OUT_COUNT && o.kind != OUT_SUM && o.kind != OUT_AVG && o.kind != OUT_REP && o.kind != OUT_CONST &&
+            o.kind != OUT_NULL)
+            return nullptr;
+    if (C.rep_cols.size() > (size_t)MAX_NEED) return nullptr;
+    const uint32_t ws = L->lean_ws ? L->lean_ws : 3968u, wsr = R->lean_ws ? R->lean_ws : 3968u;
+    // pass 0: records per window; exclusive scans give every window's first record index
+    const uint64_t nwl = cq_jx_windows(L->data_begin, L->n, ws), nwr = cq_jx_windows(R->data_begin, R->n, wsr);
+    if (nwl >= (1ull << 31) || nwr >= (1ull << 31)) return nullptr;
+    DevBuf wcl(std::max<size_t>(nwl, 1) * 4), wbl(std::max<size_t>(nwl, 1) * 4);
+    DevBuf wcr(std::max<size_t>(nwr, 1) * 4), wbr(std::max<size_t>(nwr, 1) * 4), ctl(256);
+    unsigned int* dctl = ctl.as<unsigned int>();      // [2] extract flags, [3] direct-build flags
+    unsigned long long* krange = (unsigned long long*)(dctl + 4);   // build keys' min, max; [2..3] probe's
+    HIPCHECK(hipMemsetAsync(ctl.p, 0, 256, c.stream));
+    HIPCHECK(hipMemsetAsync(krange, 0xff, 8, c.stream));
+    HIPCHECK(hipMemsetAsync(krange + 2, 0xff, 8, c.stream));
+    const int xgrid = c.ncu;
+    const uint8_t dq = (uint8_t)L->cfg.quote;
+    HIPCHECK(hipEventRecord(c.ev0, c.stream));
+    HIPCHECK(cq_jx_extract(L->g, L->data_begin, L->n, ws, d, dq, kl, gcol, 1, 0, nullptr, nullptr, nullptr,
+                           wcl.as<unsigned int>(), nullptr, 0, dctl + 2, krange, xgrid, c.stream));
+    HIPCHECK(cq_jx_extract(R->g, R->data_begin, R->n, wsr, d, dq, kr, vcol, 0, 0, nullptr, nullptr, nullptr,
+                           wcr.as<unsigned int>(), nullptr, 0, dctl + 2, krange + 2, xgrid, c.stream));
+    size_t tbl = 0, tbr = 0;
+    HIPCHECK(cq_excl_sum_u32(nullptr, &tbl, wcl.as<unsigned int>(), wbl.as<unsigned int>(), nwl, c.stream));
+    HIPCHECK(cq_excl_sum_u32(nullptr, &tbr, wcr.as<unsigned int>(), wbr.as<unsigned int>(), nwr, c.stream));
+    DevBuf tmp(std::max(tbl, tbr) + 16);
+    if (nwl) HIPCHECK(cq_excl_sum_u32(tmp.p, &tbl, wcl.as<unsigned int>(), wbl.as<unsigned int>(), nwl, c.stream));
+    if (nwr) HIPCHECK(cq_excl_sum_u32(tmp.p, &tbr, wcr.as<unsigned int>(), wbr.as<unsigned int>(), nwr, c.stream));
+    unsigned int tail[4] = {0, 0, 0, 0};
+    if (nwl) {
+        HIPCHECK(hipMemcpyAsync(&tail[0], wbl.as<unsigned int>() + nwl - 1, 4, hipMemcpyDeviceToHost, c.stream));
+        HIPCHECK(hipMemcpyAsync(&tail[1], wcl.as<unsigned int>() + nwl - 1, 4, hipMemcpyDeviceToHost, c.stream));
+    }
+    if (nwr) {
+        HIPCHECK(hipMemcpyAsync(&tail[2], wbr.as<unsigned int>() + nwr - 1, 4, hipMemcpyDeviceToHost, c.stream));
+        HIPCHECK(hipMemcpyAsync(&tail[3], wcr.as<unsigned int>() + nwr - 1, 4, hipMemcpyDeviceToHost, c.stream));
+    }
+    HIPCHECK(hipStreamSynchronize(c.stream));
+    const uint64_t nL = (uint64_t)tail[0] + tail[1], nR = (uint64_t)tail[2] + tail[3];
+    if (nL >= (1ull << 31) || nR >= (1ull << 31)) return nullptr;
+    // pass 1: the records, in file order
+    DevBuf lkey(std::max<size_t>(nL, 1) * 8), lpay(std::max<size_t>(nL, 1) * 8), loff(std::max<size_t>(nL, 1) * 4);
+    DevBuf rkey(std::max<size_t>(nR, 1) * 8), rpay(std::max<size_t>(nR, 1) * 8), roff(std::max<size_t>(nR, 1) * 4);
+    HIPCHECK(cq_jx_extract(L->g, L->data_begin, L->n, ws, d, dq, kl, gcol, 1, 1, lkey.as<unsigned long long>(),
+                           lpay.as<unsigned long long>(), loff.as<uint32_t>(), nullptr, wbl.as<unsigned int>(),
+                           (unsigned int)nL, dctl + 2, krange, xgrid, c.stream));
+    HIPCHECK(cq_jx_extract(R->g, R->data_begin, R->n, wsr, d, dq, kr, vcol, 0, 1, rkey.as<unsigned long long>(),
+                           rpay.as<unsigned long long>(), roff.as<uint32_t>(), nullptr, wbr.as<unsigned int>(),
+                           (unsigned int)nR, dctl + 2, krange + 2, xgrid, c.stream));
+    unsigned long long kr2[2] = {~0ull, 0ull};
+    unsigned int fl0 = 0;
+    HIPCHECK(hipMemcpyAsync(&fl0, dctl + 2, 4, hipMemcpyDeviceToHost, c.stream));
+    HIPCHECK(hipMemcpyAsync(kr2, krange, 16, hipMemcpyDeviceToHost, c.stream));
+    HIPCHECK(hipStreamSynchronize(c.stream));
+    if (fl0) return nullptr;
+    // the build side's keys: a direct array over a dense key range (primary keys), else
+    // the hash table
+    DevBuf table(8);
+    uint64_t tcap = 0;
+    bool direct = false;
+    if (nL && kr2[0] <= kr2[1] && kr2[1] - kr2[0] < 4 * nL + 1024) {
+        tcap = kr2[1] - kr2[0] + 1;
+        DevBuf t2(tcap * cq_jx_direct_bytes());
+        std::swap(table.p, t2.p);
+        HIPCHECK(hipMemsetAsync(table.p, 0, tcap * cq_jx_direct_bytes(), c.stream));
+        HIPCHECK(cq_jx_build_direct(lkey.as<unsigned long long>(), lpay.as<unsigned long long>(), loff.as<uint32_t>(),
+                                    (uint32_t)nL, kr2[0], tcap, table.p, dctl + 3, c.ncu * 8, c.stream));
+        unsigned int fl1 = 0;
+        HIPCHECK(hipMemcpyAsync(&fl1, dctl + 3, 4, hipMemcpyDeviceToHost, c.stream));
+        HIPCHECK(hipStreamSynchronize(c.stream));
+        direct = fl1 == 0;                  // (a NULL or repeated key: the hash table)
+    }
+    if (!direct) {
+        tcap = 1024;
+        while (tcap < 2 * nL) tcap <<= 1;
+        DevBuf t2((size_t)tcap * cq_jx_entry_bytes());
+        std::swap(table.p, t2.p);
+        HIPCHECK(hipMemsetAsync(table.p, 0, (size_t)tcap * cq_jx_entry_bytes(), c.stream));
+        HIPCHECK(cq_jx_build(lkey.as<unsigned long long>(), (uint32_t)nL, table.p, tcap, dctl + 2, c.ncu * 8, c.stream));
+    }
+    Literals Lit;
+    parse_literals(c, C.lits, Lit);
+    // finish: the representative (left) columns of each group's first pair's left record
+    constexpr uint32_t SB = 48;
+    FinishDesc FD;
+    memset(&FD, 0, sizeof FD);
+    std::vector<int> rep_ord(C.rep_cols.size());
+    for (size_t i = 0; i < rep_ord.size(); i++) rep_ord[i] = (int)i;
+    std::sort(rep_ord.begin(), rep_ord.end(), [&](int a, int b) { return C.rep_cols[a] < C.rep_cols[b]; });
+    FD.ncols = (int32_t)rep_ord.size();
+    for (size_t i = 0; i < rep_ord.size(); i++) FD.cols[i] = (int16_t)C.rep_cols[rep_ord[i]];
+    FD.delim = d;
+    FD.quote = (uint8_t)L->cfg.quote;
+    FD.nacc = C.P.nacc;
+    FD.sb = SB;
+    FD.first_shift = 32;
+    const uint32_t ncell = (uint32_t)FD.ncols + (uint32_t)FD.nacc + 1;
+    uint32_t cap = grouped ? 8192 : 64;
+    for (int attempt = 0; attempt < 4; attempt++, cap *= 8) {
+        TableArena A = make_arena(c, C.P, cap, cap / 2 + 1, 1, 16);
+        const unsigned int cap_out = cap / 2 + 1;
+        Scratch fin(c, (size_t)cap_out * ncell * (sizeof(Cell) + SB) + 64);
+        Cell* dcells = (Cell*)fin.p;
+        uint8_t* dbytes = fin.p + (size_t)cap_out * ncell * sizeof(Cell);
+        HIPCHECK(cq_jx_probe(grouped ? 1 : 0, vcol >= 0 ? 1 : 0, direct ? 1 : 0, rkey.as<unsigned long long>(),
+                             rpay.as<unsigned long long>(), roff.as<uint32_t>(), (uint32_t)nR, kr2[0], table.p, tcap,
+                             lpay.as<unsigned long long>(), loff.as<uint32_t>(), grouped ? &A.rt : &A.gt, C.P.nacc,
+                             A.stats, dctl + 2, c.ncu * 2, c.stream));
+        if (grouped) HIPCHECK(cq_launch_raw_merge(&A.gt, &A.rt, C.P.nacc, A.stats, c.stream));
+        HIPCHECK(hipEventRecord(c.ev1, c.stream));
+        HIPCHECK(cq_launch_compact(&A.gt, &C.P, A.out, A.out_count, cap_out, c.stream));
+        HIPCHECK(cq_launch_finish(L->g, L->n, A.out, A.out_count, cap_out, &FD, dcells, dbytes, c.stream));
+        constexpr size_t MAIL_HDR = 1024;
+        uint8_t* mail = mailbox(c, MAIL_HDR + cq_pack_result_bytes(cap_out, C.P.nacc, ncell, SB) + 64);
+        HIPCHECK(cq_launch_pack_result(A.out, A.out_count, cap_out, C.P.nacc, dcells, dbytes, ncell, SB,
+                                       mail + MAIL_HDR, A.stats, mail, 1, c.stream));
+        unsigned int fl = 0;
+        HIPCHECK(hipMemcpyAsync(&fl, dctl + 2, 4, hipMemcpyDeviceToHost, c.stream));
+        HIPCHECK(hipStreamSynchronize(c.stream));
+        if (fl) return nullptr;
+        ScanStats st;
+        memcpy(&st, mail, sizeof st);
+        unsigned int ng = 0;
+        memcpy(&ng, mail + sizeof(ScanStats), 4);
+        if (st.overflow >= 2) throw HipError{"fused join: group insert timeout"};
+        if (st.overflow) continue;
+        float ms = 0;
+        HIPCHECK(hipEventElapsedTime(&ms, c.ev0, c.ev1));
+        g_stats.scan_ms = ms;
+        g_stats.records = nL + nR;
+        g_stats.passed = st.passed;
+        g_stats.scan_kernel = 3;
+        ng = std::min(ng, cap_out);
+        const bool presorted = ng <= cq_pack_order_max();
+        static thread_local std::vector<uint8_t> hbuf;
+        const size_t pb = cq_pack_result_bytes(ng, C.P.nacc, ncell, SB);
+        if (hbuf.size() < pb + 8) hbuf.resize(pb + 8);
+        memcpy(hbuf.data(), mail + MAIL_HDR, pb);
+        cq_table* res = nullptr;
+        if (grouped && presorted && ng) res = build_direct(C, hbuf.data(), ng, ncell, SB, rep_ord, Lit, ~0ull);
+        if (!res) {
+            std::vector<GroupOut> outs(ng);
+            std::vector<Cell> fcells((size_t)ng * ncell);
+            std::vector<uint8_t> fbytes((size_t)ng * ncell * SB);
+            const size_t rec = 40 + 40 * (size_t)C.P.nacc;
+            memset(outs.data(), 0, ng * sizeof(GroupOut));
+            for (unsigned int i = 0; i < ng; i++) {
+                const uint8_t* r = hbuf.data() + i * rec;
+                GroupOut& o = outs[i];
+                o.clslen = ((const uint32_t*)r)[0];
+                o.w0 = ((const uint64_t*)r)[1];
+                o.w1 = ((const uint64_t*)r)[2];
+                o.cnt = ((const unsigned long long*)r)[3];
+                o.first = ((const unsigned long long*)r)[4];
+                const uint64_t* qq = (const uint64_t*)(r + 40);
+                for (int a = 0; a < C.P.nacc; a++) {
+                    o.sum[a] = as_dbl(qq[5 * a]);
+                    o.num[a] = qq[5 * a + 1];
+                    o.extpos[a] = NOPOS;
+                }
+            }
+            memcpy(fcells.data(), hbuf.data() + ng * rec, fcells.size() * sizeof(Cell));
+            memcpy(fbytes.data(), hbuf.data() + ng * rec + fcells.size() * sizeof(Cell), fbytes.size());
+            std::vector<HGroup> groups = make_groups(c, C, ~0ull, 0, outs, fcells, fbytes, FD.ncols, rep_ord, SB,
+                                                     presorted);
+            g_stats.groups = groups.size();
+            res = build_groups(C, groups, Lit, c);
+        } else {
+            g_stats.groups = ng;
+        }
+        post_ops(c, res, q);
+        return res;
+    }
+    return nullptr;
+}
+
 // One JOIN, or a chain of them (process_joins, evaluator_joins.c:237-274): join
 // j's left side is the table joined so far, named "joined" with columns
 // "<alias>.<col>" of the previous level (so a second level names "joined.u.id").
@@ -2908,6 +3142,10 @@ cq_table* run_join(DevCtx& c, cq_node* q, const cqgpu_table* L, const cqgpu_tabl
     if (part)
         for (auto& v : C.vla)
             if (v.first != 0) throw Ineligible{"MEDIAN across partials (needs every value)"};
+    if (!part && !rows && nj == 1 && lv[0].keyed && !lv[0].outer_left && !lv[0].outer_right) {
+        cq_table* fj = run_fast_join(c, q, C, L, lv[0].R, lv[0].kl, lv[0].kr, lv[0].nleft);
+        if (fj) return fj;
+    }
     // columns each level needs, from the last level back
     {
         std::set<int> cur(C.need_cols.begin(), C.need_cols.end());

@@ -34,6 +34,7 @@
 //             lookup is two 16-byte LDS reads and four compares; unseen keys take a
 //             free slot of their buckets by CAS, or spill to the HBM raw table
 #include <hip/hip_runtime.h>
+#include <algorithm>
 #include <cmath>
 #include <cstring>
 #include <vector>
@@ -923,6 +924,442 @@ __global__ __launch_bounds__(LT) void fast_kernel(const uint8_t* __restrict__ g,
     }
 }
 
+
+// ------------------------------------------------------------------ fused join: extraction
+// One side of an aggregate-only equi-join (perform_join, evaluator_joins.c:63-181,
+// feeding evaluate_aggregate) streamed like fast_kernel: per record the ON key as a
+// canonical non-negative INTEGER below 10^15 (then value_compare's double equality is
+// integer equality) or NULL, and one payload: BUILD the GROUP BY field's raw bytes
+// (<= 8, none <= ' ', as fast_kernel's tags), else the SUM argument in units of 10^-3
+// (fast_kernel's fixed-point path; NULL: JX_NOVAL).  Every record lands, in no particular
+// order, at a slot reserved per wave: key[], pay[], off[] (its byte offset, the join's
+// order key).  A record outside this shape (a quote in the window, a short row, another
+// key spelling, a wider numeral) sets *flag: the caller runs the general join instead.
+constexpr unsigned long long JX_NULLKEY = ~0ull;
+constexpr unsigned long long JX_NOVAL = 0x8000000000000000ull;
+struct JxPlan {
+    uint64_t first_win;
+    uint32_t nwin, lo_s, hi_s, ws;
+    uint32_t delim, quote;
+    uint32_t skip[2];          // field k's column minus field k-1's (the roles in column order)
+    uint32_t rank_key;         // field index of the key (the payload's: 1 - rank_key)
+};
+struct JxOut {
+    unsigned long long* key;
+    unsigned long long* pay;
+    uint32_t* off;
+    unsigned int* wcount;      // COUNT pass: records owned by window i
+    const unsigned int* wbase; // emit pass: the first record index of window i (exclusive scan)
+    unsigned int cap;
+    unsigned int* flag;
+    unsigned long long* krange;   // [0] min, [1] max of the non-NULL keys
+};
+
+// the canonical INTEGER key of a field (16 bytes d0..d3 from its start, len bytes):
+// digits only, no leading zero, at most 15 digits and not 8-10; NULL (empty) -> JX_NULLKEY
+__device__ __forceinline__ bool jx_key(uint32_t d0, uint32_t d1, uint32_t d2, uint32_t d3, uint32_t len,
+                                       unsigned long long& key) {
+    if (len == 0) { key = JX_NULLKEY; return true; }
+    const uint32_t dd[4] = {d0, d1, d2, d3};
+    // (8-10 digits may type as a DATE, infer_type csv_reader.c:139: such keys take the
+    // general join, whose class rules pair DATE with every number)
+    bool ok = len <= 15u && (len < 8u || len > 10u) && ((d0 & 0xFFu) != '0' || len == 1u);
+    unsigned long long v = 0;
+#pragma unroll
+    for (int j = 0; j < 15; j++) {
+        const uint32_t c = (dd[j >> 2] >> (8 * (j & 3))) & 0xFFu;
+        const uint32_t dg = c - '0';
+        if ((uint32_t)j < len) {
+            ok = ok && dg < 10u;
+            v = v * 10ull + dg;
+        }
+    }
+    key = v;
+    return ok;
+}
+
+template <bool BUILD, bool COMMA, int NR, bool COUNT>
+__global__ __launch_bounds__(LT) void jx_extract_kernel(const uint8_t* __restrict__ g, const JxPlan jp, const JxOut jo) {
+    extern __shared__ __align__(16) uint8_t smem[];
+    WaveLds* waves = (WaveLds*)smem;
+    const int tid = threadIdx.x, lane = tid & 63;
+    const int wv = __builtin_amdgcn_readfirstlane(tid >> 6);
+    WaveLds& W = waves[wv];
+    const uint32_t rep_q = jp.quote * 0x01010101u;
+    CK ck;
+    ck.tn1 = vreg(0x00004000u);
+    ck.tn0 = vreg(0x00400000u);
+    ck.td1 = vreg(COMMA ? 0x80408080u : 0u);
+    ck.td0 = vreg(COMMA ? 0x80802080u : 0x40u);
+    ck.m40 = vreg(0x40404040u);
+    ck.w0 = vreg(0x08040201u);
+    ck.w1 = vreg(0x80402010u);
+    ck.rd = vreg(jp.delim * 0x01010101u);
+    ck.rq = vreg(rep_q);
+    const uint64_t first_win = jp.first_win;
+    const uint32_t nwin = __builtin_amdgcn_readfirstlane(jp.nwin);
+    const uint32_t wsb = __builtin_amdgcn_readfirstlane(jp.ws);
+    const uint32_t rkey = __builtin_amdgcn_readfirstlane(jp.rank_key);
+    const uint32_t wstep = gridDim.x * NWV;
+    const uint32_t lane_full = (uint32_t)lane * LB < wsb ? ~0u : 0u;
+    uint32_t prev_next = 0;
+    const uint32_t voff = vreg(16u * (uint32_t)lane);
+    const uint32_t wlds = __builtin_amdgcn_readfirstlane(
+        (uint32_t)(uintptr_t)(__attribute__((address_space(3))) uint8_t*)W.bytes);
+    const uint32_t lane_lds = vreg(wlds + (uint32_t)lane * LB);
+    bool bad = false;
+    unsigned long long kmin = ~0ull, kmax = 0ull;
+    uint32_t i = blockIdx.x * NWV + wv;
+    if (i < nwin) load_win(g, first_win + i, wsb, wlds, voff, prev_next);
+    for (; i < nwin; i += wstep) {
+        asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+        const uint32_t prevw = prev_next;
+        v4u la[4];
+#pragma unroll
+        for (int k = 0; k < 4; k++) la[k] = ((const v4u*)W.bytes)[4 * lane + k];
+        uint32_t sep0, nl0, sep1, nl1, qf = 0;
+        classify32<COMMA>(la[0], la[1], ck, sep0, nl0, qf);
+        classify32<COMMA>(la[2], la[3], ck, sep1, nl1, qf);
+        bad = bad || __ballot((qf & 0x80808080u) != 0) != 0;      // a quote: the general join
+        const uint64_t nl = (uint64_t)nl0 | ((uint64_t)nl1 << 32);
+        const uint32_t prev_top = (uint32_t)__builtin_amdgcn_update_dpp(0, (int)(nl1 >> 31), 0x138, 0xf, 0xf, true);
+        const uint32_t pb = prevw >> 24;
+        const uint32_t prevnl = lane == 0 ? (uint32_t)(pb == '\n' || pb == '\r') : prev_top;
+        uint64_t todo = ~nl & ((nl << 1) | prevnl);
+        if (i == 0 || i == nwin - 1) {
+            const uint32_t lo_s = i == 0 ? jp.lo_s : 0u, hi_s = i == nwin - 1 ? jp.hi_s : wsb;
+            const uint32_t b0 = (uint32_t)lane * LB;
+            const uint32_t a = lo_s > b0 ? lo_s - b0 : 0u, e = hi_s > b0 ? hi_s - b0 : 0u;
+            const uint64_t keep_lo = a >= 64 ? 0ull : (~0ull << a);
+            const uint64_t keep_hi = e >= 64 ? ~0ull : ((1ull << e) - 1);
+            todo &= keep_lo & keep_hi;
+        } else {
+            todo &= ((uint64_t)lane_full << 32) | lane_full;
+        }
+        const uint32_t xs0 = (uint32_t)__builtin_amdgcn_update_dpp(0, (int)sep0, 0x130, 0xf, 0xf, true);
+        const uint32_t xs1 = (uint32_t)__builtin_amdgcn_update_dpp(0, (int)sep1, 0x130, 0xf, 0xf, true);
+        const uint32_t xn0 = (uint32_t)__builtin_amdgcn_update_dpp(0, (int)nl0, 0x130, 0xf, 0xf, true);
+        const uint32_t xn1 = (uint32_t)__builtin_amdgcn_update_dpp(0, (int)nl1, 0x130, 0xf, 0xf, true);
+        const uint64_t sep64 = (uint64_t)sep0 | ((uint64_t)sep1 << 32);
+        const uint64_t xsep2 = ((uint64_t)xs0 | ((uint64_t)xs1 << 32)) << 1;
+        const uint64_t xnl2 = ((uint64_t)xn0 | ((uint64_t)xn1 << 32)) << 1;
+        const uint64_t wbase = (first_win + i) * wsb;
+        if (COUNT) {                       // records owned by this window (the emit pass's layout)
+            const uint32_t tot = __builtin_amdgcn_readlane(wave_incl_scan((uint32_t)__popcll(todo)), 63);
+            if (lane == 0) jo.wcount[i] = tot;
+            if (i + wstep < nwin) {
+                uint32_t ni = i + wstep;
+                asm volatile("" : "+s"(ni));
+                load_win(g, first_win + ni, wsb, wlds, voff, prev_next);
+            }
+            continue;
+        }
+        // record j of this lane in this window lands at wbase[i] + (the lanes below's
+        // records) + j: file order
+        const uint32_t nmine = (uint32_t)__popcll(todo);
+        uint32_t at_next = jo.wbase[i] + wave_incl_scan(nmine) - nmine;
+        bool issued = false;
+        while (__any(todo != 0)) {
+            uint32_t p[2], pa[2], fst[2][2], fen[2][2], e[2];
+            uint64_t sv[2];
+            bool valid[2], fail[2];
+#pragma unroll
+            for (int u = 0; u < 2; u++) {
+                valid[u] = todo != 0;
+                const uint32_t b = ctz64(todo) & 63u;
+                todo &= todo - 1;
+                pa[u] = lane_lds + b;
+                p[u] = pa[u] - wlds;
+                const uint32_t nb = b ^ 63u;
+                sv[u] = view128(sep64, xsep2, b, nb);
+                e[u] = ctz64(view128(nl, xnl2, b, nb));
+            }
+#pragma unroll
+            for (int k = 0; k < NR; k++) {
+                uint32_t n = jp.skip[k];
+                n = __builtin_amdgcn_readfirstlane(n);
+                asm volatile("" : "+s"(n));
+                if (k > 0 && n == 0) {
+#pragma unroll
+                    for (int u = 0; u < 2; u++) { fst[u][k] = fst[u][k - 1]; fen[u][k] = fen[u][k - 1]; }
+                    continue;
+                }
+                if (k > 0) {
+#pragma unroll
+                    for (int u = 0; u < 2; u++) sv[u] &= sv[u] - 1;
+                }
+                if (k == 0 && n == 0) {
+#pragma unroll
+                    for (int u = 0; u < 2; u++) fst[u][k] = 0;
+                } else if (k > 0 && n == 1) {
+#pragma unroll
+                    for (int u = 0; u < 2; u++) fst[u][k] = fen[u][k - 1] + 1;
+                } else {
+                    for (uint32_t j = k == 0 ? 1u : 2u; j < n; j++) {
+#pragma unroll
+                        for (int u = 0; u < 2; u++) sv[u] &= sv[u] - 1;
+                    }
+#pragma unroll
+                    for (int u = 0; u < 2; u++) {
+                        fst[u][k] = ctz64(sv[u]) + 1;
+                        sv[u] &= sv[u] - 1;
+                    }
+                }
+#pragma unroll
+                for (int u = 0; u < 2; u++) fen[u][k] = ctz64(sv[u]);
+            }
+            const bool last_pass = !__any(todo != 0);
+            unsigned long long key[2], pay[2];
+#pragma unroll
+            for (int u = 0; u < 2; u++) {
+                const uint32_t en = fen[u][NR - 1];
+                fail[u] = (en >= 64u) | (en > e[u]);
+                const uint32_t ks = NR == 1 || rkey == 0 ? fst[u][0] : fst[u][1];
+                const uint32_t ke = NR == 1 || rkey == 0 ? fen[u][0] : fen[u][1];
+                uint32_t d0, d1, d2, d3;
+                ld8a(pa[u] + ks, d0, d1);
+                ld8a(pa[u] + ks + 8, d2, d3);
+                fail[u] |= !jx_key(d0, d1, d2, d3, ke - ks, key[u]);
+                pay[u] = 0;
+                if (NR == 2) {
+                    const uint32_t ps = rkey == 0 ? fst[u][1] : fst[u][0];
+                    const uint32_t pe = rkey == 0 ? fen[u][1] : fen[u][0];
+                    const uint32_t plen = pe - ps;
+                    uint32_t q0, q1;
+                    ld8a(pa[u] + ps, q0, q1);
+                    if (BUILD) {                                      // the group field's raw bytes
+                        const uint32_t m0 = len_mask(plen, 0), m1 = len_mask(plen, 1);
+                        const uint32_t a0 = q0 & m0, a1 = q1 & m1;
+                        fail[u] |= (plen > 8u) | ((low_bytes(a0, m0 & 0x80808080u) | low_bytes(a1, m1 & 0x80808080u)) != 0);
+                        pay[u] = plen ? ((uint64_t)a0 | ((uint64_t)a1 << 32)) : (1ull << 32);
+                    } else if (plen == 0) {
+                        pay[u] = JX_NOVAL;                            // NULL: counted, not summed
+                    } else {                                          // the SUM argument, 10^-3 units
+                        // (a leading '-': the rest parsed, then negated; two's complement sums)
+                        const bool neg = (q0 & 0xFFu) == '-' && plen > 1u;
+                        uint32_t v0 = q0, v1 = q1, vl = plen;
+                        if (neg) {
+                            ld8a(pa[u] + ps + 1, v0, v1);
+                            vl = plen - 1;
+                        }
+                        unsigned long long fx;
+                        const Num n4 = num4<true>(v0, vl);
+                        if (n4.ok) {
+                            const uint32_t mul = (n4.k & 2) ? ((n4.k & 1) ? 1u : 10u) : ((n4.k & 1) ? 100u : 1000u);
+                            fx = (unsigned long long)__umul24(n4.M, mul);
+                        } else {
+                            const Num n7 = num7(v0, v1, vl);
+                            fail[u] |= !n7.ok | (n7.k > 3u);
+                            const uint32_t mul = (n7.k & 2) ? ((n7.k & 1) ? 1u : 10u) : ((n7.k & 1) ? 100u : 1000u);
+                            fx = (unsigned long long)n7.M * mul;
+                        }
+                        pay[u] = neg ? 0ull - fx : fx;
+                    }
+                }
+                bad = bad || (valid[u] && fail[u]);
+            }
+            if (last_pass && !issued) {                               // the window's bytes are read
+                if (i + wstep < nwin) {
+                    uint32_t ni = i + wstep;
+                    asm volatile("" : "+s"(ni));
+                    load_win(g, first_win + ni, wsb, wlds, voff, prev_next);
+                }
+                issued = true;
+            }
+#pragma unroll
+            for (int u = 0; u < 2; u++) {
+                if (valid[u]) {
+                    const uint32_t at = at_next++;
+                    if (at < jo.cap) {
+                        jo.key[at] = key[u];
+                        jo.pay[at] = pay[u];
+                        jo.off[at] = (uint32_t)(wbase + p[u]);
+                    }
+                    if (key[u] != JX_NULLKEY) {
+                        kmin = key[u] < kmin ? key[u] : kmin;
+                        kmax = key[u] > kmax ? key[u] : kmax;
+                    }
+                }
+            }
+        }
+        if (!issued && i + wstep < nwin) {
+            uint32_t ni = i + wstep;
+            asm volatile("" : "+s"(ni));
+            load_win(g, first_win + ni, wsb, wlds, voff, prev_next);
+        }
+    }
+    if (COUNT) return;
+    if (__any(bad) && lane == 0) atomicOr(jo.flag, 1u);
+    for (int o = 32; o > 0; o >>= 1) {
+        const unsigned long long a = __shfl_down(kmin, o, 64), b = __shfl_down(kmax, o, 64);
+        kmin = a < kmin ? a : kmin;
+        kmax = b > kmax ? b : kmax;
+    }
+    if (lane == 0 && kmin != ~0ull) {
+        atomicMin(&jo.krange[0], kmin);
+        atomicMax(&jo.krange[1], kmax);
+    }
+}
+
+
+// ------------------------------------------------------------------ fused join: build, probe + aggregate
+// The build side's keys into an open-addressing table of 16-byte entries (stored key
+// + 2, so 0 is free; the build record's index), every record its own entry (equal keys
+// occupy consecutive probes: many-to-many pairs are all found).
+struct JxEntry {
+    unsigned long long k;
+    uint32_t idx, pad;
+};
+__device__ __forceinline__ uint64_t jx_hash(unsigned long long k) {
+    uint64_t x = k * 0x9E3779B97F4A7C15ull;
+    return x ^ (x >> 29);
+}
+__global__ void jx_build_kernel(const unsigned long long* __restrict__ key, uint32_t n, JxEntry* __restrict__ T,
+                                uint64_t mask, unsigned int* __restrict__ flag) {
+    for (uint32_t i = blockIdx.x * blockDim.x + threadIdx.x; i < n; i += gridDim.x * blockDim.x) {
+        const unsigned long long k = key[i], sk = k + 2ull;
+        uint64_t h = jx_hash(k) & mask;
+        for (uint64_t probes = 0;; probes++) {
+            if (probes > mask) { atomicOr(flag, 2u); break; }
+            const unsigned long long old = atomicCAS(&T[h].k, 0ull, sk);
+            if (old == 0ull) { T[h].idx = i; break; }
+            h = (h + 1) & mask;
+        }
+    }
+}
+
+// Build keys of a dense range (the usual primary key): entry D[key - kmin] holds the
+// build record's payload and byte offset, so a probe reads one 16-byte entry.  A NULL
+// key or a repeated key (flag 8) sends the caller to the hash table.
+struct JxDirect {
+    unsigned long long pay;
+    uint32_t off, used;
+};
+__global__ void jx_build_direct_kernel(const unsigned long long* __restrict__ key,
+                                       const unsigned long long* __restrict__ pay, const uint32_t* __restrict__ off,
+                                       uint32_t n, unsigned long long kmin, unsigned long long range,
+                                       JxDirect* __restrict__ D, unsigned int* __restrict__ flag) {
+    for (uint32_t i = blockIdx.x * blockDim.x + threadIdx.x; i < n; i += gridDim.x * blockDim.x) {
+        const unsigned long long k = key[i];
+        if (k == JX_NULLKEY || k - kmin >= range) { atomicOr(flag, 8u); continue; }
+        JxDirect& e = D[k - kmin];
+        if (atomicCAS(&e.used, 0u, 1u) != 0u) { atomicOr(flag, 8u); continue; }
+        e.pay = pay[i];
+        e.off = off[i];
+    }
+}
+
+// Probe side records: every pair (build record l, probe record r) with equal keys,
+// in any order, aggregated per GROUP BY raw tag (the build record's payload) into a
+// block-local LDS table: COUNT, the SUM argument's fixed-point sum and count (the
+// probe record's payload), and the first pair in (l, r) order as the key
+// (l byte offset << 32) | r byte offset.  Flushed into the HBM raw-key table, which
+// raw_merge_kernel canonicalises (GROUP BY typing) like fast_kernel's.
+constexpr uint32_t JX_SLOTS = 2048;
+template <bool GROUPED, bool VALUE, bool DIRECT>
+__global__ __launch_bounds__(1024) void jx_probe_kernel(const unsigned long long* __restrict__ pkey,
+                                                        const unsigned long long* __restrict__ ppay,
+                                                        const uint32_t* __restrict__ poff,
+                                                        uint32_t n, unsigned long long kmin,
+                                                        const JxEntry* __restrict__ T, uint64_t mask,
+                                                        const unsigned long long* __restrict__ bpay,
+                                                        const uint32_t* __restrict__ boff, GroupTable rt, int nacc,
+                                                        ScanStats* __restrict__ stats, unsigned int* __restrict__ flag) {
+    __shared__ unsigned long long stag[JX_SLOTS], sfix[JX_SLOTS], sfirst[JX_SLOTS];
+    __shared__ uint32_t scnt[JX_SLOTS], snum[JX_SLOTS];
+    constexpr uint32_t NS = GROUPED ? JX_SLOTS : 1;
+    for (uint32_t s = threadIdx.x; s < NS; s += blockDim.x) {
+        stag[s] = 0; sfix[s] = 0; sfirst[s] = ~0ull; scnt[s] = 0; snum[s] = 0;
+    }
+    __syncthreads();
+    bool full = false;
+    unsigned long long npairs = 0;
+    for (uint32_t r = blockIdx.x * blockDim.x + threadIdx.x; r < n; r += gridDim.x * blockDim.x) {
+        const unsigned long long k = pkey[r], sk = k + 2ull;
+        const unsigned long long v = VALUE ? ppay[r] : 0ull;
+        const uint32_t ro = poff[r];
+        uint64_t h = DIRECT ? k - kmin : jx_hash(k) & mask;
+        for (uint64_t probes = 0; probes <= mask; probes++) {
+            uint32_t l = 0;
+            bool hit;
+            unsigned long long btag = 0;
+            uint32_t boffv = 0;
+            if (DIRECT) {                    // one entry per key: T is the JxDirect array D
+                if (k != JX_NULLKEY && h <= mask) {
+                    const JxDirect e = ((const JxDirect*)T)[h];
+                    hit = e.used != 0u;
+                    btag = e.pay;
+                    boffv = e.off;
+                } else {
+                    hit = false;
+                }
+            } else {
+                const JxEntry e = T[h];
+                if (e.k == 0ull) break;
+                hit = e.k == sk;
+                l = e.idx;
+            }
+            if (hit) {
+                if (!DIRECT) {
+                    btag = GROUPED ? bpay[l] : 0ull;
+                    boffv = boff[l];
+                }
+                const unsigned long long pk = ((unsigned long long)boffv << 32) | ro;
+                uint32_t s = 0;
+                if (GROUPED) {
+                    const unsigned long long tag = btag;
+                    s = fast_key_hash((uint32_t)tag, (uint32_t)(tag >> 32)) & (JX_SLOTS - 1);
+                    for (uint32_t q = 0;; q++) {
+                        if (q == JX_SLOTS) { full = true; break; }
+                        const unsigned long long t = stag[s];
+                        if (t == tag) break;
+                        if (t == 0ull) {
+                            const unsigned long long old = atomicCAS(&stag[s], 0ull, tag);
+                            if (old == 0ull || old == tag) break;
+                        }
+                        s = (s + 1) & (JX_SLOTS - 1);
+                    }
+                    if (full) break;
+                }
+                atomicAdd(&scnt[s], 1u);
+                if (pk < sfirst[s]) atomicMin(&sfirst[s], pk);   // (the first pair is found early)
+                if (VALUE && v != JX_NOVAL) {
+                    atomicAdd(&sfix[s], v);
+                    atomicAdd(&snum[s], 1u);
+                }
+                npairs++;
+            }
+            if (DIRECT) break;
+            h = (h + 1) & mask;
+        }
+    }
+    if (full) atomicOr(flag, 4u);
+    for (int o = 32; o > 0; o >>= 1) npairs += __shfl_down(npairs, o, 64);
+    if ((threadIdx.x & 63) == 0 && npairs) atomicAdd(&stats->passed, npairs);
+    __syncthreads();
+    for (uint32_t s = threadIdx.x; s < NS; s += blockDim.x) {
+        if (!scnt[s]) continue;
+        GKey kk;
+        if (GROUPED) {
+            const unsigned long long w0 = stag[s];
+            const uint32_t kl = key_len8(w0);
+            kk = raw_key(kl, kl ? w0 : 0ull);
+        } else {
+            kk.cls = GK_ALL; kk.len = 0; kk.w0 = 0; kk.w1 = 0;
+        }
+        const int gi = g_insert(rt, kk, GROUPED ? gk_hash(kk) : 0x12345678ULL, stats);
+        if (gi < 0) continue;
+        atomicAdd(&rt.cnt[gi], (unsigned long long)scnt[s]);
+        atomicMin(&rt.first[gi], sfirst[s]);
+        if (VALUE && snum[s]) {                 // every accumulator sums the one probe-side argument
+            for (int a = 0; a < nacc; a++) {
+                atomicAdd(&rt.sum[a][gi], (double)(long long)sfix[s] / 1000.0);
+                atomicAdd(&rt.num[a][gi], (unsigned long long)snum[s]);
+            }
+        }
+    }
+}
+
 }  // namespace fast
 }  // namespace cq
 
@@ -1116,6 +1553,101 @@ hipError_t cq_launch_fast(const uint8_t* g, const cq::ScanPlan* P, const cq::Gro
 }
 
 int cq_fast_waves_per_block() { return fast::NWV; }
+
+// ---- fused aggregate join (executor.hip run_fast_join)
+// windows of the table's bytes [lo, hi) at stride ws
+uint64_t cq_jx_windows(uint64_t lo, uint64_t hi, uint32_t ws) { return hi > lo ? (hi - 1) / ws - lo / ws + 1 : 0; }
+// extraction of one side, records of the table's bytes [lo, hi) (lo at a record start);
+// kcol the ON key's column, pcol the payload's (-1: none); build: the payload is the
+// GROUP BY field's raw bytes, else the SUM argument.  pass 0 counts each window's
+// records into wcount; pass 1 emits every record at wbase[window] + its rank (file order)
+hipError_t cq_jx_extract(const uint8_t* g, uint64_t lo, uint64_t hi, uint32_t ws, uint32_t delim, uint32_t quote,
+                         int kcol, int pcol, int build, int pass, unsigned long long* key, unsigned long long* pay,
+                         uint32_t* off, unsigned int* wcount, const unsigned int* wbase, unsigned int cap,
+                         unsigned int* flag, unsigned long long* krange, int grid, hipStream_t s) {
+    using namespace cq::fast;
+    if (((uintptr_t)g & 255) != 0 || kcol < 0 || ws > (uint32_t)WS || ws % 128) return hipErrorInvalidValue;
+    JxPlan jp;
+    memset(&jp, 0, sizeof jp);
+    jp.ws = ws;
+    jp.delim = delim;
+    jp.quote = quote;
+    if (hi > lo) {
+        const uint64_t wl = lo / ws, wh = (hi - 1) / ws;
+        if (wh - wl + 1 >= (1ull << 31)) return hipErrorInvalidValue;
+        jp.first_win = wl;
+        jp.nwin = (uint32_t)(wh - wl + 1);
+        jp.lo_s = (uint32_t)(lo - wl * ws);
+        jp.hi_s = (uint32_t)(hi - wh * ws);
+    }
+    const int nr = pcol >= 0 ? 2 : 1;
+    if (nr == 1) {
+        jp.skip[0] = (uint32_t)kcol;
+        jp.rank_key = 0;
+    } else {
+        const int c0 = std::min(kcol, pcol), c1 = std::max(kcol, pcol);
+        jp.skip[0] = (uint32_t)c0;
+        jp.skip[1] = (uint32_t)(c1 - c0);
+        jp.rank_key = kcol <= pcol ? 0u : 1u;
+    }
+    const bool comma = delim == ',' && quote == '"';
+    typedef void (*xfn_t)(const uint8_t*, const JxPlan, const JxOut);
+    static const xfn_t tab[2][2][2][2] = {
+        {{{jx_extract_kernel<false, false, 1, false>, jx_extract_kernel<false, false, 1, true>},
+          {jx_extract_kernel<false, false, 2, false>, jx_extract_kernel<false, false, 2, true>}},
+         {{jx_extract_kernel<false, true, 1, false>, jx_extract_kernel<false, true, 1, true>},
+          {jx_extract_kernel<false, true, 2, false>, jx_extract_kernel<false, true, 2, true>}}},
+        {{{jx_extract_kernel<true, false, 1, false>, jx_extract_kernel<true, false, 1, true>},
+          {jx_extract_kernel<true, false, 2, false>, jx_extract_kernel<true, false, 2, true>}},
+         {{jx_extract_kernel<true, true, 1, false>, jx_extract_kernel<true, true, 1, true>},
+          {jx_extract_kernel<true, true, 2, false>, jx_extract_kernel<true, true, 2, true>}}}};
+    const xfn_t fn = tab[build ? 1 : 0][comma ? 1 : 0][nr - 1][pass == 0 ? 1 : 0];
+    JxOut jo;
+    jo.key = key; jo.pay = pay; jo.off = off; jo.wcount = wcount; jo.wbase = wbase; jo.cap = cap; jo.flag = flag;
+    jo.krange = krange;
+    const size_t lds = sizeof(WaveLds) * NWV;
+    cq::set_max_lds((const void*)fn, (int)lds);
+    if (jp.nwin == 0) return hipSuccess;
+    hipLaunchKernelGGL(fn, dim3(grid), dim3(LT), lds, s, g, jp, jo);
+    return hipGetLastError();
+}
+hipError_t cq_jx_build(const unsigned long long* key, uint32_t n, void* table, uint64_t tcap, unsigned int* flag,
+                       int grid, hipStream_t s) {
+    if (tcap & (tcap - 1)) return hipErrorInvalidValue;
+    hipLaunchKernelGGL(cq::fast::jx_build_kernel, dim3(grid), dim3(256), 0, s, key, n, (cq::fast::JxEntry*)table,
+                       tcap - 1, flag);
+    return hipGetLastError();
+}
+size_t cq_jx_entry_bytes() { return sizeof(cq::fast::JxEntry); }
+hipError_t cq_jx_build_direct(const unsigned long long* key, const unsigned long long* pay, const uint32_t* off,
+                              uint32_t n, unsigned long long kmin, unsigned long long range, void* D,
+                              unsigned int* flag, int grid, hipStream_t s) {
+    hipLaunchKernelGGL(cq::fast::jx_build_direct_kernel, dim3(grid), dim3(256), 0, s, key, pay, off, n, kmin, range,
+                       (cq::fast::JxDirect*)D, flag);
+    return hipGetLastError();
+}
+size_t cq_jx_direct_bytes() { return sizeof(cq::fast::JxDirect); }
+// direct: table is jx_build_direct's D of `tcap` entries (keys kmin ..), else the hash
+// table of tcap (a power of two) entries
+hipError_t cq_jx_probe(int grouped, int value, int direct, const unsigned long long* pkey,
+                       const unsigned long long* ppay, const uint32_t* poff, uint32_t n, unsigned long long kmin,
+                       const void* table, uint64_t tcap, const unsigned long long* bpay, const uint32_t* boff,
+                       const cq::GroupTable* rt, int nacc, cq::ScanStats* stats, unsigned int* flag, int grid,
+                       hipStream_t s) {
+    using namespace cq::fast;
+    typedef void (*pfn_t)(const unsigned long long*, const unsigned long long*, const uint32_t*, uint32_t,
+                          unsigned long long, const JxEntry*, uint64_t, const unsigned long long*, const uint32_t*,
+                          GroupTable, int, ScanStats*, unsigned int*);
+    static const pfn_t tab[2][2][2] = {
+        {{jx_probe_kernel<false, false, false>, jx_probe_kernel<false, false, true>},
+         {jx_probe_kernel<false, true, false>, jx_probe_kernel<false, true, true>}},
+        {{jx_probe_kernel<true, false, false>, jx_probe_kernel<true, false, true>},
+         {jx_probe_kernel<true, true, false>, jx_probe_kernel<true, true, true>}}};
+    const pfn_t fn = tab[grouped ? 1 : 0][value ? 1 : 0][direct ? 1 : 0];
+    hipLaunchKernelGGL(fn, dim3(grid), dim3(1024), 0, s, pkey, ppay, poff, n, kmin, (const JxEntry*)table, tcap - 1,
+                       bpay, boff, *rt, nacc, stats, flag);
+    return hipGetLastError();
+}
 
 // The LDS table seed of a GROUP BY column: the distinct raw keys of the sampled
 // records (records split on '\n' / '\r' runs, fields on the delimiter, quote-blind;

@@ -97,6 +97,7 @@ struct FinishDesc {
     uint32_t quote;
     int32_t nacc;
     uint32_t sb;              // inline STRING bytes per cell
+    uint32_t first_shift;     // the record offset is first >> first_shift (a join's pair key: 32)
 };
 
 // INNER JOIN (evaluator_joins.c:63-181) on the device: columns of one side parsed

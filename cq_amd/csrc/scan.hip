@@ -1318,7 +1318,7 @@ __global__ void finish_kernel(const uint8_t* __restrict__ g, uint64_t n, const G
     const uint32_t ng = *count < cap_out ? *count : cap_out;
     if (i >= ng) return;
     Cell* cs = cells + (size_t)i * ncell;
-    const unsigned long long first = out[i].first;
+    const unsigned long long first = out[i].first == NOPOS ? NOPOS : out[i].first >> D.first_shift;
     if (D.ncols) {
         if (first != NOPOS && first < n) {
             parse_cols_out(g + first, D.cols, D.ncols, D.delim, D.quote, cs, 1);

@@ -174,6 +174,35 @@ def test_mixed_key_classes_refused(files):
         assert "value classes" in cq_amd.last_ineligible()
 
 
+def test_mixed_key_classes_refused_empty_side():
+    """ADVICE r1 layout: 5 ranks, a right side of three INTEGER keys, a left side of
+    the same INTEGER keys plus many STRING keys.  The routing sends the STRING rows
+    to ranks that receive no right rows; those ranks must still record their left
+    key classes, so the merge sees STRING (left) against INTEGER (right) and refuses
+    (value_compare's cross-class "equal" pairs cannot be hash-routed)"""
+    left = b"k,v\n" + b"".join(b"%s,%d\n" % ((b"%d" % (i % 3 + 1)) if i % 4 == 0 else (b"s%02d" % (i % 40)), i)
+                                 for i in range(400))
+    right = b"k,w\n1,10\n2,20\n3,30\n"
+    sql = "SELECT COUNT(*) FROM 'l' AS a JOIN 'r' AS b ON a.k = b.k"
+    with cqtest.Parsed(sql) as ast:
+        lh, ls = _shards(left, 5, 1)
+        rh, rs = _shards(right, 5, 2)
+        recv = []
+        for side, sh in ((0, ls), (1, rs)):
+            per = np.zeros(5, dtype=int)
+            for r in range(5):
+                _, nr = cq_amd.route_plan(ast, [ls[r], rs[r]], side, 5)
+                per += np.array(nr)
+            recv.append(per)
+        for t in ls + rs:
+            t.close()
+        # the layout the advice describes: some rank gets left rows (only STRING keys) and no right rows
+        assert any(recv[0][d] > 0 and recv[1][d] == 0 for d in range(5)), recv
+        tp = _run(ast, left, right, 5)
+        assert not tp
+        assert "value classes" in cq_amd.last_ineligible(), cq_amd.last_ineligible()
+
+
 def test_route_counts(files):
     """every record is routed exactly once; bytes = record bytes + one newline each"""
     data, _ = files
