@@ -38,17 +38,29 @@ def main():
     stats = glob.glob(os.path.join(a.src, "kt", "**", "*kernel_stats.csv"), recursive=True)
     if stats:
         shutil.copy(stats[0], a.prefix + "_kernel_stats.csv")
-    counters = {}
-    for sub in ("fetch", "write", "sq"):
-        counters.update(pmc(os.path.join(a.src, sub)))
-    json.dump(counters, open(a.prefix + "_pmc.json", "w"), indent=1, sort_keys=True)
-    if "FETCH_SIZE" in counters:
-        fetch = counters["FETCH_SIZE"] * 1024 * 2          # KiB, half-counted on gfx950
-        write = counters.get("WRITE_SIZE", 0.0) * 1024
+    # counters per kernel class: config 3's and config 2's fast_kernel, config 5's jx kernels
+    classes = {"config3": "fast_kernel<true", "config2": "fast_kernel<false", "config5_probe": "jx_probe_kernel",
+               "config5_extract_build": "jx_extract_kernel<true", "config5_extract_probe": "jx_extract_kernel<false",
+               "config5_build": "jx_build"}
+    out = {}
+    for name, pat in classes.items():
+        counters = {}
+        for sub in ("fetch", "write", "sq", "sq2"):
+            counters.update(pmc(os.path.join(a.src, sub), pat))
+        if counters:
+            if "FETCH_SIZE" in counters:
+                counters["hbm_bytes_per_launch"] = counters["FETCH_SIZE"] * 1024 * 2 + counters.get("WRITE_SIZE", 0.0) * 1024
+            out[name] = counters
+    json.dump(out, open(a.prefix + "_pmc.json", "w"), indent=1, sort_keys=True)
+    c3 = out.get("config3", {})
+    if "FETCH_SIZE" in c3:
+        fetch = c3["FETCH_SIZE"] * 1024 * 2          # KiB, half-counted on gfx950
+        write = c3.get("WRITE_SIZE", 0.0) * 1024
         traffic = {"rows": a.rows, "hbm_bytes_per_launch": fetch + write, "fetch_bytes": fetch,
                    "write_bytes": write, "source": a.prefix + "_pmc.json",
                    "correction": "FETCH_SIZE(KiB)*1024*2 + WRITE_SIZE(KiB)*1024 (MI355X_MICROARCH.md HBM)"}
         json.dump(traffic, open(os.path.join(os.path.dirname(a.prefix), "hbm_traffic.json"), "w"), indent=1)
+    counters = out
     stats2 = glob.glob(os.path.join(a.src, "kt2", "**", "*kernel_stats.csv"), recursive=True)
     if stats2:
         shutil.copy(stats2[0], a.prefix + "_config2_kernel_stats.csv")
