@@ -1169,6 +1169,14 @@ void compile_aggregate(const cqgpu_table* t, cq_node* q, Compiled& C) {
 }
 
 // ------------------------------------------------------------------ host groups
+// vla_prep_kernel's order-preserving value key back to the double (scan.hip vla_value)
+inline double vkey_value(unsigned long long k) {
+    const uint64_t b = (k >> 63) ? (k & 0x7FFFFFFFFFFFFFFFULL) : ~k;
+    double d;
+    memcpy(&d, &b, 8);
+    return d;
+}
+
 struct HGroup {
     uint32_t kcls = 0, klen = 0;        // cell.h GKey class and text length
     uint64_t kw0 = 0, kw1 = 0;          // key words (GK_LONG: w1 = content hash)
@@ -1184,6 +1192,18 @@ struct HGroup {
     // across partials, STDDEV's state: sum, squared deviations from the partial's
     // mean and the numeric count (merged exactly by the parallel-variance rule)
     double vsum[MAX_ACC] = {}, vm2[MAX_ACC] = {}, vn[MAX_ACC] = {};
+    // across partials, MEDIAN's state: the group's numeric values as order-preserving
+    // keys, ascending (mvals[v] for value-list aggregate v; empty for STDDEV)
+    std::vector<std::vector<unsigned long long>> mvals;
+    // MIN/MAX over several value classes: per class (0 number, 1 string, 2 date) the
+    // extreme with its position and the class's first position, so range partials
+    // can fold the whole file's row order (aggregate_pairs' class-split pass)
+    struct ClassSplit {
+        int acc = 0;
+        HCell ext[3];
+        unsigned long long extpos[3] = {NOPOS, NOPOS, NOPOS}, first[3] = {NOPOS, NOPOS, NOPOS};
+    };
+    std::vector<ClassSplit> split;
 };
 
 // little-endian byte writer / reader of the partial-aggregation blobs
@@ -1195,6 +1215,17 @@ struct Blob {
     void f64(double v) { raw(&v, 8); }
     void str(const std::string& s) { u32((uint32_t)s.size()); raw(s.data(), s.size()); }
     void cell(const HCell& h) { u32(h.kind); u64(h.bits); str(h.s); }
+    void split(const std::vector<HGroup::ClassSplit>& v) {
+        u32((uint32_t)v.size());
+        for (const HGroup::ClassSplit& cs : v) {
+            u32((uint32_t)cs.acc);
+            for (int k = 0; k < 3; k++) { cell(cs.ext[k]); u64(cs.extpos[k]); u64(cs.first[k]); }
+        }
+    }
+    void mvals(const std::vector<unsigned long long>* v) {
+        u64(v ? v->size() : 0);
+        if (v && !v->empty()) raw(v->data(), v->size() * 8);
+    }
 };
 struct Reader {
     const uint8_t* p;
@@ -2226,7 +2257,11 @@ void append_rows(DevCtx& c, cq_table* r, int at, const std::vector<Cell>& cells,
     }
 }
 
-cq_table* run_rows(DevCtx& c, const cqgpu_table* t, Compiled& C, RowPlan& R, cq_node* q, bool* limited) {
+// keys: when given (a range partial, cqgpu_query_partial), the rank's rows are all
+// kept in file order -- OFFSET is global, so only the first OFFSET+LIMIT rows of the
+// shard can matter -- and each row's whole-file byte position is returned with it
+cq_table* run_rows(DevCtx& c, const cqgpu_table* t, Compiled& C, RowPlan& R, cq_node* q, bool* limited,
+                   std::vector<unsigned long long>* keys = nullptr) {
     const int nout = (int)R.names.size();
     *limited = false;
     // 1. scan: WHERE over every record, matching record offsets out (unordered)
@@ -2272,12 +2307,25 @@ cq_table* run_rows(DevCtx& c, const cqgpu_table* t, Compiled& C, RowPlan& R, cq_
     if (!ordered && !distinct && (q->u.q.limit >= 0 || q->u.q.offset >= 0)) {
         const unsigned long long off = q->u.q.offset >= 0 ? (unsigned long long)q->u.q.offset : 0;
         const unsigned long long lim = q->u.q.limit >= 0 ? (unsigned long long)q->u.q.limit : n;
-        lo = std::min(off, n);
-        hi = std::min(n, lo + lim);
-        *limited = true;
+        if (keys) {
+            hi = std::min(n, off + std::min(lim, n));
+        } else {
+            lo = std::min(off, n);
+            hi = std::min(n, lo + lim);
+            *limited = true;
+        }
     }
     cq_table* r = new_result(R.names);
     const int nr = (int)(hi - lo);
+    if (keys) {
+        keys->resize(hi - lo);
+        if (hi > lo) {
+            HIPCHECK(hipMemcpyAsync(keys->data(), sorted.as<unsigned long long>() + lo, (hi - lo) * 8,
+                                    hipMemcpyDeviceToHost, c.stream));
+            HIPCHECK(hipStreamSynchronize(c.stream));
+        }
+        for (auto& k : *keys) k += t->base_offset;
+    }
     r->nrows = r->row_capacity = nr;
     r->rows = (cq_row*)calloc(std::max(nr, 1), sizeof(cq_row));
     if (!nr || !nout) {
@@ -2345,7 +2393,6 @@ struct VlaRows {                         // one row per candidate: key words, va
 // sort + segment + reduce one value-list aggregate (index vi, kind 0 STDDEV / 1 MEDIAN)
 void vla_finish(DevCtx& c, const VlaAt& at, bool grouped, std::vector<HGroup>& groups, size_t vi, int kind,
                 VlaRows& V, uint32_t n, bool partial = false) {
-    if (partial && kind != 0) throw Ineligible{"MEDIAN across partials (needs every value)"};
     if (!n) return;
     const size_t N = n;
     DevBuf pos(N * 4), perm(N * 4), perm2(N * 4), keys(N * 8), keys2(N * 8), head(N * 4), sid(N * 4), start(N * 4),
@@ -2393,21 +2440,40 @@ void vla_finish(DevCtx& c, const VlaAt& at, bool grouped, std::vector<HGroup>& g
     HIPCHECK(hipStreamSynchronize(c.stream));
     const uint32_t nseg = last[0] + last[1];
     HIPCHECK(cq_launch_vla_starts(head.as<unsigned int>(), sid.as<unsigned int>(), m, start.as<unsigned int>(), c.stream));
-    DevBuf aux(partial ? (size_t)nseg * 16 : 16);
+    // a partial's MEDIAN keeps every value: the (key, value)-sorted value keys and the
+    // segment starts come back, each group's run becomes its mvals
+    const bool values = partial && kind == 1;
+    const bool moments = partial && kind == 0;
+    DevBuf aux(moments ? (size_t)nseg * 16 : 16);
     HIPCHECK(cq_launch_vla_reduce(V.vkey.as<unsigned long long>(), V.kw0.as<unsigned long long>(),
                                   V.kw1.as<unsigned long long>(), V.kcl.as<unsigned long long>(), perm.as<unsigned int>(),
-                                  start.as<unsigned int>(), nseg, m, partial ? 2 : kind, out.as<unsigned long long>(),
+                                  start.as<unsigned int>(), nseg, m, moments ? 2 : kind, out.as<unsigned long long>(),
                                   aux.as<double>(), c.stream));
     std::vector<unsigned long long> h((size_t)nseg * 4);
-    std::vector<double> ha(partial ? (size_t)nseg * 2 : 0);
+    std::vector<double> ha(moments ? (size_t)nseg * 2 : 0);
+    std::vector<unsigned long long> hv(values ? m : 0);
+    std::vector<unsigned int> hs(values ? nseg : 0);
     HIPCHECK(hipMemcpyAsync(h.data(), out.p, h.size() * 8, hipMemcpyDeviceToHost, c.stream));
-    if (partial) HIPCHECK(hipMemcpyAsync(ha.data(), aux.p, ha.size() * 8, hipMemcpyDeviceToHost, c.stream));
+    if (moments) HIPCHECK(hipMemcpyAsync(ha.data(), aux.p, ha.size() * 8, hipMemcpyDeviceToHost, c.stream));
+    if (values) {
+        HIPCHECK(cq_launch_vla_gather(V.vkey.as<unsigned long long>(), perm.as<unsigned int>(), m,
+                                      keys.as<unsigned long long>(), c.stream));
+        HIPCHECK(hipMemcpyAsync(hv.data(), keys.p, (size_t)m * 8, hipMemcpyDeviceToHost, c.stream));
+        HIPCHECK(hipMemcpyAsync(hs.data(), start.p, (size_t)nseg * 4, hipMemcpyDeviceToHost, c.stream));
+    }
     HIPCHECK(hipStreamSynchronize(c.stream));
     for (uint32_t sg = 0; sg < nseg; sg++) {
         auto it = at.find(std::make_tuple((uint64_t)h[4 * sg], (uint64_t)h[4 * sg + 1], (uint64_t)h[4 * sg + 2]));
         if (it == at.end()) continue;
         HGroup& g = groups[it->second];
-        if (partial) {
+        if (values) {
+            const uint32_t e = sg + 1 < nseg ? hs[sg + 1] : m;
+            if (g.mvals.size() <= vi) g.mvals.resize(vi + 1);
+            g.mvals[vi].assign(hv.begin() + hs[sg], hv.begin() + e);
+            g.vla_ok[vi] = true;
+            continue;
+        }
+        if (moments) {
             g.vsum[vi] = as_dbl(h[4 * sg + 3]);
             g.vm2[vi] = ha[2 * sg];
             g.vn[vi] = ha[2 * sg + 1];
@@ -2724,6 +2790,14 @@ std::vector<HGroup> aggregate_pairs(DevCtx& c, Compiled& C, const JoinMap& MA, c
                     best = k;
             groups[g].ext[a] = best >= 0 ? split[g].ext[best] : HCell();
             groups[g].extpos[a] = best >= 0 ? split[g].extpos[best] : NOPOS;
+            HGroup::ClassSplit cs;
+            cs.acc = a;
+            for (int k = 0; k < 3; k++) {
+                cs.ext[k] = split[g].ext[k];
+                cs.extpos[k] = split[g].extpos[k];
+                cs.first[k] = split[g].extpos[3 + k];
+            }
+            groups[g].split.push_back(cs);
         }
     }
     return groups;
@@ -3140,8 +3214,6 @@ cq_table* run_join(DevCtx& c, cq_node* q, const cqgpu_table* L, const cqgpu_tabl
     if (rows) compile_rows(&J, q, C, RP);
     else compile_aggregate(&J, q, C);
     if (part)
-        for (auto& v : C.vla)
-            if (v.first != 0) throw Ineligible{"MEDIAN across partials (needs every value)"};
     if (!part && !rows && nj == 1 && lv[0].keyed && !lv[0].outer_left && !lv[0].outer_right) {
         cq_table* fj = run_fast_join(c, q, C, L, lv[0].R, lv[0].kl, lv[0].kr, lv[0].nleft);
         if (fj) return fj;
@@ -3390,6 +3462,11 @@ std::vector<HGroup> run_cells_aggregate(DevCtx& c, const cqgpu_table* t, Compile
         if (h.first != NOPOS) idx.push_back((uint32_t)h.first);
         for (int a = 0; a < C.P.nacc; a++)
             if (h.extpos[a] != NOPOS) idx.push_back((uint32_t)h.extpos[a]);
+        for (const HGroup::ClassSplit& cs : h.split)
+            for (int k = 0; k < 3; k++) {
+                if (cs.extpos[k] != NOPOS) idx.push_back((uint32_t)cs.extpos[k]);
+                if (cs.first[k] != NOPOS) idx.push_back((uint32_t)cs.first[k]);
+            }
     }
     for (uint32_t i : idx)
         if (i >= np) throw HipError{"cells aggregate: row index out of range"};
@@ -3406,6 +3483,11 @@ std::vector<HGroup> run_cells_aggregate(DevCtx& c, const cqgpu_table* t, Compile
             if (h.first != NOPOS) h.first = off[k++] + t->base_offset;
             for (int a = 0; a < C.P.nacc; a++)
                 if (h.extpos[a] != NOPOS) h.extpos[a] = off[k++] + t->base_offset;
+            for (HGroup::ClassSplit& cs : h.split)
+                for (int j = 0; j < 3; j++) {
+                    if (cs.extpos[j] != NOPOS) cs.extpos[j] = off[k++] + t->base_offset;
+                    if (cs.first[j] != NOPOS) cs.first[j] = off[k++] + t->base_offset;
+                }
         }
     }
     return groups;
@@ -4280,7 +4362,11 @@ size_t cqgpu_query_partial(cq_node* q, cqgpu_table* const* tables, int ntables, 
                     b.f64(h.sum[a]); b.u64(h.num[a]); b.u64(h.extpos[a]); b.cell(h.ext[a]);
                 }
                 for (uint32_t r = 0; r < nrep; r++) b.cell(r < h.reps.size() ? h.reps[r] : HCell());
-                for (size_t v = 0; v < C.vla.size(); v++) { b.f64(h.vsum[v]); b.f64(h.vm2[v]); b.f64(h.vn[v]); }
+                for (size_t v = 0; v < C.vla.size(); v++) {
+                    b.f64(h.vsum[v]); b.f64(h.vm2[v]); b.f64(h.vn[v]);
+                    b.mvals(v < h.mvals.size() ? &h.mvals[v] : nullptr);
+                }
+                b.split(h.split);
             }
             void* out = malloc(std::max<size_t>(b.d.size(), 1));
             if (!out) throw HipError{"out of host memory"};
@@ -4289,11 +4375,37 @@ size_t cqgpu_query_partial(cq_node* q, cqgpu_table* const* tables, int ntables, 
             return b.d.size();
         }
         check_plan_shape(q, t);
-        if (is_row_query(q)) throw Ineligible{"row-returning SELECT across partials"};
+        if (is_row_query(q)) {
+            // "CQR1" as for joins: this shard's projected rows in file order, each keyed
+            // by its record's whole-file byte position; cqgpu_merge_partials orders all
+            // ranks' rows by that key (the whole file's record order, build_result's
+            // row order) before ORDER BY / DISTINCT / LIMIT
+            Compiled C;
+            RowPlan R;
+            compile_rows(t, q, C, R);
+            bool limited = false;
+            std::vector<unsigned long long> keys;
+            cq_table* r = run_rows(c, t, C, R, q, &limited, &keys);
+            struct Free { cq_table* r; ~Free() { cqgpu_result_free(r); } } free_{r};
+            Blob b;
+            b.u32(0x31525143u);
+            b.u32((uint32_t)R.names.size());
+            for (auto& nm : R.names) b.str(nm);
+            b.u32(0);
+            b.u32(0);
+            b.u64((uint64_t)r->nrows);
+            for (int i = 0; i < r->nrows; i++) {
+                b.u64(keys[i]);
+                for (int k = 0; k < (int)R.names.size(); k++) b.cell(from_value(r->rows[i].values[k]));
+            }
+            void* out = malloc(std::max<size_t>(b.d.size(), 1));
+            if (!out) throw HipError{"out of host memory"};
+            memcpy(out, b.d.data(), b.d.size());
+            *blob_out = out;
+            return b.d.size();
+        }
         Compiled C;
         compile_aggregate(t, q, C);
-        for (auto& v : C.vla)
-            if (v.first != 0) throw Ineligible{"MEDIAN across partials (needs every value)"};
         Literals L;
         ScanStats st;
         memset(&st, 0, sizeof st);
@@ -4325,7 +4437,11 @@ size_t cqgpu_query_partial(cq_node* q, cqgpu_table* const* tables, int ntables, 
                 b.f64(h.sum[a]); b.u64(h.num[a]); b.u64(h.extpos[a]); b.cell(h.ext[a]);
             }
             for (uint32_t r = 0; r < nrep; r++) b.cell(r < h.reps.size() ? h.reps[r] : HCell());
-            for (size_t v = 0; v < C.vla.size(); v++) { b.f64(h.vsum[v]); b.f64(h.vm2[v]); b.f64(h.vn[v]); }
+            for (size_t v = 0; v < C.vla.size(); v++) {
+                b.f64(h.vsum[v]); b.f64(h.vm2[v]); b.f64(h.vn[v]);
+                b.mvals(v < h.mvals.size() ? &h.mvals[v] : nullptr);
+            }
+            b.split(h.split);
         }
         void* out = malloc(std::max<size_t>(b.d.size(), 1));
         if (!out) throw HipError{"out of host memory"};
@@ -4424,7 +4540,25 @@ cq_table* cqgpu_merge_partials(cq_node* q, const void* const* blobs, const size_
                     h.sum[a] = r.f64(); h.num[a] = r.u64(); h.extpos[a] = r.u64(); h.ext[a] = r.cell();
                 }
                 for (uint32_t k = 0; k < nrep; k++) h.reps.push_back(r.cell());
-                for (uint32_t v = 0; v < nvla; v++) { h.vsum[v] = r.f64(); h.vm2[v] = r.f64(); h.vn[v] = r.f64(); }
+                for (uint32_t v = 0; v < nvla; v++) {
+                    h.vsum[v] = r.f64(); h.vm2[v] = r.f64(); h.vn[v] = r.f64();
+                    const uint64_t nv = r.u64();
+                    if (nv > (r.n - r.o) / 8) throw HipError{"truncated partial blob"};
+                    if (nv) {
+                        if (h.mvals.size() <= v) h.mvals.resize(v + 1);
+                        h.mvals[v].resize(nv);
+                        for (auto& x : h.mvals[v]) x = r.u64();
+                    }
+                }
+                const uint32_t ns = r.u32();
+                if (ns > nacc) throw HipError{"bad partial blob"};
+                for (uint32_t j = 0; j < ns; j++) {
+                    HGroup::ClassSplit cs;
+                    cs.acc = (int)r.u32();
+                    if (cs.acc < 0 || cs.acc >= (int)nacc) throw HipError{"bad partial blob"};
+                    for (int k = 0; k < 3; k++) { cs.ext[k] = r.cell(); cs.extpos[k] = r.u64(); cs.first[k] = r.u64(); }
+                    h.split.push_back(cs);
+                }
                 pt.groups.push_back(std::move(h));
             }
         }
@@ -4446,12 +4580,41 @@ cq_table* cqgpu_merge_partials(cq_node* q, const void* const* blobs, const size_
         compile_aggregate(&meta, q, C);
         if ((uint32_t)C.P.nacc != nacc || (uint32_t)C.rep_cols.size() != nrep)
             throw HipError{"partials do not match the plan"};
+        // MIN/MAX over several value classes: value_compare calls cells of different
+        // classes "equal" (csv_reader.c:128), so the row-order fold keeps the class of
+        // the first non-NULL cell and that class's first extreme.  Range partials carry
+        // per class the extreme and first position (HGroup::split); a partial that saw
+        // one class has that class's extreme only, whose position stands in for the
+        // class's first -- ranges are disjoint and ordered, so only the order between
+        // partials matters there.  Hash-repartitioned join partials interleave
+        // positions across ranks and are refused.
+        bool mixed[MAX_ACC] = {};
         for (uint32_t a = 0; a < nacc; a++) {
             if (C.P.acc[a].kind == ACC_SUM) continue;
             uint32_t m = 0;
             for (auto& pt : parts) m |= pt.classes[a];
-            if (m & (m - 1)) throw Ineligible{"MIN/MAX over a column mixing numbers, strings and dates"};
+            mixed[a] = (m & (m - 1)) != 0;
+            if (mixed[a] && joined) throw Ineligible{"MIN/MAX over a column mixing numbers, strings and dates"};
         }
+        auto split_of = [](HGroup& h, int a) -> HGroup::ClassSplit& {
+            for (auto& cs : h.split)
+                if (cs.acc == a) return cs;
+            HGroup::ClassSplit cs;
+            cs.acc = a;
+            if (h.extpos[a] != NOPOS) {
+                const int k = h.ext[a].kind == K_STR ? 1 : h.ext[a].kind == K_DATE ? 2 : 0;
+                cs.ext[k] = h.ext[a];
+                cs.extpos[k] = cs.first[k] = h.extpos[a];
+            }
+            h.split.push_back(cs);
+            return h.split.back();
+        };
+        auto better_ext = [&](int a, const HCell& x, unsigned long long xp, const HCell& y, unsigned long long yp) {
+            if (xp == NOPOS) return false;
+            if (yp == NOPOS) return true;
+            const int cv = hcompare(x, y);     // first strictly better wins (evaluator_aggregates.c:311-326)
+            return (C.P.acc[a].kind == ACC_MIN ? cv < 0 : cv > 0) || (cv == 0 && xp < yp);
+        };
         std::vector<HGroup> merged;
         std::unordered_map<std::string, size_t> where;
         for (auto& pt : parts) {
@@ -4461,6 +4624,8 @@ cq_table* cqgpu_merge_partials(cq_node* q, const void* const* blobs, const size_
                 if (h.kcls == GK_STR || h.kcls == GK_LONG) id += h.kbytes;
                 else if (h.kcls == GK_COMP) id += std::to_string(h.kw0) + "/" + std::to_string(h.kw1);
                 else id += std::to_string(h.kw0);
+                for (uint32_t a = 0; a < nacc; a++)
+                    if (mixed[a]) (void)split_of(h, (int)a);
                 auto it = where.find(id);
                 if (it == where.end()) {
                     where.emplace(id, merged.size());
@@ -4473,13 +4638,28 @@ cq_table* cqgpu_merge_partials(cq_node* q, const void* const* blobs, const size_
                 for (uint32_t a = 0; a < nacc; a++) {
                     m.sum[a] += h.sum[a];
                     m.num[a] += h.num[a];
-                    if (C.P.acc[a].kind == ACC_SUM || h.extpos[a] == NOPOS) continue;
-                    bool better = m.extpos[a] == NOPOS;
-                    if (!better) {   // first strictly better wins (evaluator_aggregates.c:311-326)
-                        const int cv = hcompare(h.ext[a], m.ext[a]);
-                        better = (C.P.acc[a].kind == ACC_MIN ? cv < 0 : cv > 0) || (cv == 0 && h.extpos[a] < m.extpos[a]);
+                    if (C.P.acc[a].kind == ACC_SUM) continue;
+                    if (mixed[a]) {
+                        HGroup::ClassSplit& ms = split_of(m, (int)a);
+                        const HGroup::ClassSplit& hs = split_of(h, (int)a);
+                        for (int k = 0; k < 3; k++) {
+                            ms.first[k] = std::min(ms.first[k], hs.first[k]);
+                            if (better_ext((int)a, hs.ext[k], hs.extpos[k], ms.ext[k], ms.extpos[k])) {
+                                ms.ext[k] = hs.ext[k];
+                                ms.extpos[k] = hs.extpos[k];
+                            }
+                        }
+                        continue;
                     }
-                    if (better) { m.ext[a] = h.ext[a]; m.extpos[a] = h.extpos[a]; }
+                    if (better_ext((int)a, h.ext[a], h.extpos[a], m.ext[a], m.extpos[a])) {
+                        m.ext[a] = h.ext[a];
+                        m.extpos[a] = h.extpos[a];
+                    }
+                }
+                for (uint32_t v = 0; v < nvla; v++) {   // MEDIAN: every value
+                    if (v >= h.mvals.size() || h.mvals[v].empty()) continue;
+                    if (m.mvals.size() <= v) m.mvals.resize(v + 1);
+                    m.mvals[v].insert(m.mvals[v].end(), h.mvals[v].begin(), h.mvals[v].end());
                 }
                 for (uint32_t v = 0; v < nvla; v++) {   // parallel variance: counts, sums, squared deviations
                     if (h.vn[v] == 0) continue;
@@ -4492,11 +4672,31 @@ cq_table* cqgpu_merge_partials(cq_node* q, const void* const* blobs, const size_
                 }
             }
         }
+        for (HGroup& h : merged)           // the mixed-class fold: the first class's extreme
+            for (uint32_t a = 0; a < nacc; a++) {
+                if (!mixed[a]) continue;
+                const HGroup::ClassSplit& cs = split_of(h, (int)a);
+                int best = -1;
+                for (int k = 0; k < 3; k++)
+                    if (cs.first[k] != NOPOS && (best < 0 || cs.first[k] < cs.first[best])) best = k;
+                h.ext[a] = best >= 0 ? cs.ext[best] : HCell();
+                h.extpos[a] = best >= 0 ? cs.extpos[best] : NOPOS;
+            }
         // one group without GROUP BY, present even with no rows
         if (!C.grouped && merged.size() > 1) throw HipError{"partials disagree on the single group"};
         if (C.vla.size() != nvla) throw HipError{"partials do not match the plan"};
-        for (HGroup& h : merged)           // population STDDEV of the merged state
+        for (HGroup& h : merged)           // population STDDEV / MEDIAN of the merged state
             for (uint32_t v = 0; v < nvla; v++) {
+                if (C.vla[v].first == 1) {      // vla_reduce_kernel's MEDIAN over all ranks' values
+                    std::vector<unsigned long long> e;
+                    if (v < h.mvals.size()) e.swap(h.mvals[v]);
+                    std::sort(e.begin(), e.end());
+                    const size_t n = e.size();
+                    h.vla_ok[v] = n > 0;
+                    h.vla[v] = !n ? 0.0 : (n & 1) ? vkey_value(e[n / 2])
+                                                  : (vkey_value(e[n / 2 - 1]) + vkey_value(e[n / 2])) / 2.0;
+                    continue;
+                }
                 h.vla_ok[v] = h.vn[v] > 0;
                 h.vla[v] = h.vn[v] > 0 ? sqrt(h.vm2[v] / h.vn[v]) : 0.0;
             }

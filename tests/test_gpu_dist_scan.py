@@ -107,3 +107,21 @@ def test_dense_step_falls_back_together(tmp_path):
     want, _ = cqtest.oracle_query(sql.format(p=path))
     from test_gpu_parity import compare
     compare(got, want, {2}, "dense fallback")
+
+
+@pytest.mark.parametrize("sql", [
+    "SELECT name, age, height FROM '{p}' WHERE height > 198 AND age > 60",
+    "SELECT * FROM '{p}' WHERE role = 'role_042' ORDER BY height DESC LIMIT 30 OFFSET 2",
+    "SELECT role, MEDIAN(height), STDDEV(height) FROM '{p}' WHERE age < 20 GROUP BY role",
+])
+def test_rows_and_median_two_processes(tmp_path, sql):
+    """row-returning SELECTs and MEDIAN over real ranks: each rank's rows / values
+    travel in its blob, rank 0 orders them by whole-file position"""
+    path = str(tmp_path / "rows.csv")
+    datagen.write_logical(path, 200_000, seed=7, with_role=True)
+    for dense in (False, True):          # the dense path must decline them on every rank
+        got = _run(path, 2, sql, dense)
+        want, unsup = cqtest.oracle_query(sql.format(p=path))
+        assert not unsup
+        from test_gpu_parity import compare
+        compare(got, want, {2} if "STDDEV" in sql else set(), f"2-process: {sql} (dense={dense})")

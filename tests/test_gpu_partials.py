@@ -1,4 +1,4 @@
-"""Range-partitioned aggregation (SURVEY.md section 8e, config 4 on one GPU).
+"""Range-partitioned aggregation and row SELECTs (SURVEY.md section 8e, config 4 on one GPU).
 
 Every "rank" opens its own newline-snapped byte range of one file with the
 product entry point (cqgpu_table_open_range), runs cqgpu_query_partial on it,
@@ -258,3 +258,103 @@ def test_dense_merge_refuses_minmax(files):
         assert not part.ok and "dense merge" in cq_amd.last_ineligible()
         part.free()
         t.close()
+
+
+# ---------------------------------------------------------------- row-returning SELECT across ranges
+# Every rank projects its shard's matching rows, each keyed by its record's whole-file
+# byte position ("CQR1"); the merge orders all ranks' rows by position -- build_result's
+# row order over the whole file -- before ORDER BY / DISTINCT / LIMIT / OFFSET.
+ROW_QUERIES = [
+    "SELECT name, age FROM '{p}' WHERE age > 62 AND height < 150",
+    "SELECT * FROM '{p}' WHERE height > 195 LIMIT 40 OFFSET 17",
+    "SELECT name, age * 2 AS a2, height FROM '{p}' WHERE role = 'role_003' ORDER BY age DESC LIMIT 25",
+    "SELECT DISTINCT gender, role FROM '{p}' WHERE age < 19 AND role LIKE 'role_00%'",
+    "SELECT surname FROM '{p}' LIMIT 9 OFFSET 3000",
+    "SELECT name, height FROM '{p}' WHERE name LIKE 'Zz%'",          # no row anywhere
+]
+
+
+@pytest.mark.parametrize("sql", ROW_QUERIES)
+@pytest.mark.parametrize("nranks", [1, 3, 8])
+def test_row_select_across_ranges(files, sql, nranks):
+    path = files["plain"]
+    q = sql.format(p=path)
+    want, unsup = cqtest.oracle_query(q)
+    assert not unsup and want is not None
+    with cqtest.Parsed(q) as ast:
+        got = _merged(ast, path, nranks)
+        tol = tolerant_columns(ast)
+    compare(got, want, tol, f"{nranks} ranks: {q}")
+
+
+@pytest.mark.parametrize("nranks", [2, 5, 16])
+def test_row_select_mixed_terminator_cuts(files, nranks):
+    """CR / CRLF / blank-line runs at the cuts: no record lost, none twice, file order"""
+    path = files["mixed"]
+    for sql in ROW_QUERIES[:3] + ["SELECT * FROM '{p}' WHERE age > 70"]:
+        q = sql.format(p=path)
+        want, unsup = cqtest.oracle_query(q)
+        assert not unsup and want is not None
+        with cqtest.Parsed(q) as ast:
+            got = _merged(ast, path, nranks)
+            tol = tolerant_columns(ast)
+        compare(got, want, tol, f"{nranks} ranks: {q}")
+
+
+# ---------------------------------------------------------------- MEDIAN / mixed-class MIN/MAX across ranges
+VLA_QUERIES = [
+    "SELECT role, MEDIAN(height), STDDEV(age), COUNT(*) FROM '{p}' WHERE age > 40 GROUP BY role",
+    "SELECT MEDIAN(age), MEDIAN(height) FROM '{p}'",
+    "SELECT gender, MEDIAN(age) FROM '{p}' WHERE role LIKE 'role_01%' GROUP BY gender",
+]
+
+
+@pytest.mark.parametrize("sql", VLA_QUERIES)
+@pytest.mark.parametrize("nranks", [1, 3, 8])
+def test_median_across_ranges(files, sql, nranks):
+    path = files["plain"]
+    q = sql.format(p=path)
+    want, unsup = cqtest.oracle_query(q)
+    assert not unsup and want is not None
+    with cqtest.Parsed(q) as ast:
+        got = _merged(ast, path, nranks)
+        tol = tolerant_columns(ast)
+    compare(got, want, tol, f"{nranks} ranks: {q}")
+
+
+@pytest.fixture(scope="module")
+def mixed_classes(tmp_path_factory):
+    """a column whose cells mix numbers, strings and dates, with groups whose first
+    non-NULL cell is of each class, and shards that see only one class of a group"""
+    rng = random.Random(5)
+    vals = {"num": ["7", "-3.5", "12", "0", "100", "2.25"],
+            "str": ["pear", "apple", "zeta", "Apple", "m"],
+            "date": ["2024-01-05", "1999-12-31", "2030-06-01", "2001-02-03"]}
+    rows = ["g,v"]
+    for i in range(6000):
+        g = f"g{i % 23}"
+        # each group's first cells come from a group-dependent class, later ones from any
+        if i < 23 * 3:
+            cls = ("num", "str", "date")[(i % 23) % 3]
+        elif i % 23 == 5 and i < 3000:
+            cls = "str"
+        else:
+            cls = rng.choice(("num", "str", "date", "null"))
+        rows.append(f"{g}," + ("" if cls == "null" else rng.choice(vals[cls])))
+    p = tmp_path_factory.mktemp("mixed_cls") / "mixed.csv"
+    p.write_text("\n".join(rows) + "\n")
+    return str(p)
+
+
+@pytest.mark.parametrize("nranks", [1, 2, 3, 5, 8])
+def test_mixed_class_minmax_across_ranges(mixed_classes, nranks):
+    for sql in ("SELECT g, MIN(v), MAX(v), COUNT(*) FROM '{p}' GROUP BY g",
+                "SELECT MIN(v), MAX(v) FROM '{p}'",
+                "SELECT g, MAX(v), MEDIAN(v) FROM '{p}' WHERE g = 'g5' OR g = 'g7' GROUP BY g"):
+        q = sql.format(p=mixed_classes)
+        want, unsup = cqtest.oracle_query(q)
+        assert not unsup and want is not None
+        with cqtest.Parsed(q) as ast:
+            got = _merged(ast, mixed_classes, nranks)
+            tol = tolerant_columns(ast)
+        compare(got, want, tol, f"{nranks} ranks: {q}")

@@ -86,23 +86,17 @@ def test_stddev_median(files, tmpl):
            .replace("{U}", str(files["users"])).replace("{O}", str(files["orders"])))
 
 
-def test_median_across_partials_refused(files):
-    """MEDIAN needs every value of a group: partial merges refuse it loudly"""
-    sql = f"SELECT role, MEDIAN(age) FROM '{files['role']}' GROUP BY role"
-    with cqtest.Parsed(sql) as ast:
-        t = cq_amd.Table.open_range(str(files["role"]), 0, 2)
-        with pytest.raises(RuntimeError):
-            cq_amd.query_partial(ast, [t])
-        t.close()
-    assert "MEDIAN across partials" in cq_amd.last_ineligible()
-
-
 PARTIAL_STDDEV = [
     "SELECT role, STDDEV(height), COUNT(*) FROM '{R}' WHERE age > 30 GROUP BY role",
     "SELECT STDDEV(age), STDDEV(height), AVG(age) FROM '{R}'",
     "SELECT g, STDDEV(x), STDDEV_POP(y) FROM '{M}' GROUP BY g",
     "SELECT gender, role, STDDEV(age) FROM '{R}' GROUP BY gender, role",
     "SELECT g, MIN(y), MAX(y), STDDEV(x) FROM '{M}' GROUP BY g",
+    # MEDIAN: every rank ships its groups' numeric values, the merge sorts them
+    "SELECT role, MEDIAN(age) FROM '{R}' GROUP BY role",
+    "SELECT g, MEDIAN(x), STDDEV(x), MIN(x) FROM '{M}' GROUP BY g",
+    "SELECT gender, role, MEDIAN(height), MEDIAN(age) FROM '{R}' WHERE age > 50 GROUP BY gender, role",
+    "SELECT MEDIAN(height) FROM '{R}' WHERE age > 200",
 ]
 
 
@@ -110,7 +104,8 @@ PARTIAL_STDDEV = [
 @pytest.mark.parametrize("tmpl", PARTIAL_STDDEV)
 def test_stddev_across_partials(files, tmpl, nranks):
     """per range: (sum, squared deviations, count) per group, merged by the
-    parallel-variance rule; population STDDEV within 1e-6 of the oracle"""
+    parallel-variance rule; population STDDEV within 1e-6 of the oracle; MEDIAN
+    from every rank's values, exact"""
     path = str(files["mix"]) if "{M}" in tmpl else str(files["role"])
     sql = tmpl.replace("{M}", path).replace("{R}", path)
     want, unsup = cqtest.oracle_query(sql)
