@@ -19,6 +19,11 @@ LIB_PATH = os.environ.get("CQ_AMD_LIB") or os.path.join(HERE, "lib", "libcqgpu.s
 _lib = None
 
 
+class Coll(C.Structure):
+    """cqgpu_coll: the next collective of the device-side merge (cqgpu.h)"""
+    _fields_ = [("op", C.c_int32), ("pad", C.c_int32), ("count", C.c_uint64)]
+
+
 class Stats(C.Structure):
     _fields_ = [("scan_ms", C.c_double), ("total_ms", C.c_double), ("scan_bytes", C.c_uint64),
                 ("records", C.c_uint64), ("groups", C.c_uint64), ("lds_spills", C.c_uint64),
@@ -72,16 +77,12 @@ def lib():
         vp = C.c_void_p
         L.cqgpu_partial_new.restype = vp
         L.cqgpu_partial_new.argtypes = [C.POINTER(abi.Node), C.POINTER(vp), C.c_int]
-        L.cqgpu_partial_keys.restype = C.c_size_t
-        L.cqgpu_partial_keys.argtypes = [vp, vp, C.POINTER(C.c_uint32)]
-        L.cqgpu_partial_dict.restype = C.c_longlong
-        L.cqgpu_partial_dict.argtypes = [vp, vp, C.c_uint64, C.c_uint64]
-        L.cqgpu_partial_scatter.restype = C.c_int
-        L.cqgpu_partial_scatter.argtypes = [vp, vp, vp, vp]
-        L.cqgpu_partial_mask_reps.restype = C.c_int
-        L.cqgpu_partial_mask_reps.argtypes = [vp, vp, vp]
-        L.cqgpu_partial_finish.restype = TP
-        L.cqgpu_partial_finish.argtypes = [vp, C.POINTER(abi.Node), vp, vp, vp]
+        L.cqgpu_partial_next.restype = C.c_int
+        L.cqgpu_partial_next.argtypes = [vp, vp, C.POINTER(C.c_uint64), C.c_int, C.c_int, C.POINTER(Coll)]
+        L.cqgpu_partial_put.restype = C.c_int
+        L.cqgpu_partial_put.argtypes = [vp, vp]
+        L.cqgpu_partial_result.restype = TP
+        L.cqgpu_partial_result.argtypes = [vp, C.POINTER(abi.Node)]
         L.cqgpu_partial_free.argtypes = [vp]
         L.cqgpu_last_stats.argtypes = [C.POINTER(Stats)]
         L.cqgpu_last_error.restype = C.c_char_p

@@ -60,16 +60,24 @@ hipError_t cq_launch_join_code(const cq::Cell* cells, uint32_t stride, uint32_t 
                                hipStream_t s);
 hipError_t cq_launch_gather_codes(const unsigned long long* codes, const uint32_t* idx, uint32_t n,
                                   unsigned long long* out, hipStream_t s);
-hipError_t cq_launch_dict_build(const void* all, uint32_t n, uint32_t* state, uint32_t* rec_of, uint32_t* first_of,
-                                uint32_t cap, uint32_t* slot_of, unsigned int* err, hipStream_t s);
+hipError_t cq_launch_dict_build(const void* all, const void* text, uint32_t n, uint32_t* state, uint32_t* rec_of,
+                                uint32_t* first_of, uint32_t cap, uint32_t* slot_of, unsigned int* err, hipStream_t s);
 hipError_t cq_launch_dict_flag(const uint32_t* slot_of, const uint32_t* first_of, uint32_t n, uint32_t* flag,
                                hipStream_t s);
+hipError_t cq_launch_rebase(void* recs, uint32_t n, uint64_t add, hipStream_t s);
+hipError_t cq_launch_fill_rows(unsigned long long* dst, uint64_t g, uint32_t w, const unsigned long long* row,
+                               hipStream_t s);
 hipError_t cq_launch_dict_scatter(const uint32_t* slot_of, const uint32_t* first_of, const uint32_t* dense_of,
-                                  uint32_t mine, uint32_t m, const double* st_sum, const unsigned long long* st_first,
-                                  const unsigned long long* st_rep, uint32_t W, double* dsum,
-                                  unsigned long long* dfirst, unsigned long long* drep, hipStream_t s);
-hipError_t cq_launch_rep_mask(const unsigned long long* mine, const unsigned long long* global, uint32_t g,
-                              unsigned long long* drep, hipStream_t s);
+                                  uint32_t mine, uint32_t m, const unsigned long long* st_sum,
+                                  const unsigned long long* st_min, const unsigned long long* st_priv, uint32_t W,
+                                  uint32_t P, uint32_t Q, unsigned long long* dsum, unsigned long long* dmin,
+                                  unsigned long long* dpriv, uint32_t* dense_id, hipStream_t s);
+hipError_t cq_launch_ext_mask(const unsigned long long* dmin, const unsigned long long* dpriv, uint64_t g, uint32_t P,
+                              uint32_t Q, uint32_t nmm, unsigned long long* dext, hipStream_t s);
+hipError_t cq_launch_cell_mask(const unsigned long long* dmin, const unsigned long long* dext,
+                               const unsigned long long* dpriv, const double* dsum, uint64_t g, uint32_t P, uint32_t Q,
+                               uint32_t W, uint32_t nmm, uint32_t R, uint32_t nv, uint32_t vsum0,
+                               unsigned long long* dcell, double* dvla, hipStream_t s);
 hipError_t cq_launch_class_mask(const cq::Cell* cells, uint32_t stride, uint32_t kcol, uint32_t n, unsigned int* mask,
                                 hipStream_t s);
 hipError_t cq_launch_run_bounds(const uint32_t* ssid, uint32_t n, cq::HSlot* slots, hipStream_t s);
@@ -1624,7 +1632,11 @@ std::vector<HGroup> run_aggregate(DevCtx& c, const cqgpu_table* t, Compiled& C, 
     uint64_t chunk = 0;          // 0: the whole table in one launch
     bool presorted = false;
     while (true) {
-        TableArena A = make_arena(c, C.P, cap, cap / 2 + 1, (size_t)grid, cq_scan_cand_stride(&C.P, grouped));
+        // test knob CQGPU_SLOW_CAP: a smaller slow-record list, to force the chunked rescan
+        unsigned long long slow_cap = 1ull << 20;
+        if (const char* e = getenv("CQGPU_SLOW_CAP"))
+            if (atoll(e) >= 64) slow_cap = std::min<unsigned long long>(slow_cap, (unsigned long long)atoll(e));
+        TableArena A = make_arena(c, C.P, cap, cap / 2 + 1, (size_t)grid, cq_scan_cand_stride(&C.P, grouped), slow_cap);
         const unsigned int cap_out = cap / 2 + 1;
         Scratch fin(c, (size_t)cap_out * ncell * (sizeof(Cell) + SB) + 64);
         Cell* dcells = (Cell*)fin.p;
@@ -4721,26 +4733,120 @@ cq_table* cqgpu_merge_partials(cq_node* q, const void* const* blobs, const size_
 
 
 // ---- device-side GROUP BY merge for range-partitioned scans (merge.hip) -------
-// Dense path of SURVEY.md section 8e: plans whose result needs only the group key,
-// COUNT / SUM / AVG (no MIN / MAX, no other plain column, no long text keys).
-struct cqgpu_partial {
-    Compiled C;
-    std::vector<std::string> names;
-    uint32_t W = 1;                 // dense words per group: COUNT, then SUM_a and count_a per accumulator
-    uint32_t m = 0;                 // this rank's groups
-    int rep_slot = -1;              // the group column's rep slot (-1: no plain column)
-    DevBuf keys, st_sum, st_first, st_rep;
-    // the dictionary of the last cqgpu_partial_dict call (the gathered key records,
-    // copied: the caller's buffer need not outlive the call)
-    DevBuf all;
-    uint32_t nall = 0, mine = 0, G = 0, cap = 0;
-    DevBuf state, rec_of, first_of, slot_of, flag, dense_of, my_first;
-};
-
+// SURVEY.md section 8e, "RCCL reduce for the final aggregate merge".  The library
+// drives the merge as a fixed sequence of collectives that the caller runs over
+// RCCL (cqgpu_partial_next / cqgpu_partial_put, cqgpu.h); the sequence depends on
+// the plan only, so every rank issues the same collectives.
+//   KEYS  all_gather of [m][m key records][long key texts]   -> dictionary (G groups)
+//   MIN   all_reduce MIN of the MIN plane  (first positions, per-class firsts, order keys)
+//   SUM   all_reduce SUM of the SUM plane  (STDDEV plans: ranks need the global means)
+//   STRS  all_gather of the string extremes of groups whose MIN/MAX keeps the string
+//         class (text has no fixed-width order key: every rank picks the winner)
+//   EXT   all_reduce MIN of masked extreme positions      (MIN/MAX plans)
+//   CELL  reduce SUM of the owners' cells to rank 0         (representative / extreme cells)
+//   VLA   reduce SUM of the pooled squared deviations      (STDDEV plans)
+//   SUMR  reduce SUM of the SUM plane to rank 0            (plans without STDDEV)
+//   SIDE  all_gather of the owners' cell texts over 8 bytes (plans with cells)
+// Out of this path (blob merge instead): MEDIAN (needs every value), more than 2^29 keys.
 namespace {
 constexpr uint32_t KEYREC = 32;
 struct HKeyRec { uint32_t clslen, pad; uint64_t w0, w1, pad2; };
+constexpr unsigned long long ABS64 = 0x7FFFFFFFFFFFFFFFull;        // merge.hip ABSENT
+constexpr unsigned long long CELL_PRESENT = 1ull << 63, CELL_LONG = 1ull << 62;
+enum : int32_t { COLL_DONE = 0, COLL_ALLGATHER = 1, COLL_ALLREDUCE_MIN_I64 = 2, COLL_ALLREDUCE_SUM_F64 = 3,
+                 COLL_REDUCE_SUM_I64 = 4, COLL_REDUCE_SUM_F64 = 5, COLL_DECLINE = 6 };
+enum Stage { ST_KEYS, ST_MIN, ST_SUM, ST_STRS, ST_EXT, ST_CELL, ST_VLA, ST_SUMR, ST_SIDE };
+
+// two independent hashes of a long key's bytes (the dictionary's filter before the
+// byte compare; identical on every rank)
+uint64_t text_hash(const uint8_t* b, uint32_t n, uint64_t seed) {
+    uint64_t h = seed ^ n;
+    for (uint32_t i = 0; i < n; i++) h = (h ^ b[i]) * 0x100000001B3ull + (h >> 29);
+    h ^= h >> 33; h *= 0xff51afd7ed558ccdull; h ^= h >> 33;
+    return h;
+}
+
+int cell_class(const HCell& x) { return x.kind == K_STR ? 1 : x.kind == K_DATE ? 2 : 0; }
+
+// per-class state of MIN/MAX accumulator a (HGroup::split, or the one class a
+// single-class partial saw, whose extreme position stands in for its first)
+HGroup::ClassSplit class_split(const HGroup& h, int a) {
+    for (const auto& cs : h.split)
+        if (cs.acc == a) return cs;
+    HGroup::ClassSplit cs;
+    cs.acc = a;
+    if (h.extpos[a] != NOPOS) {
+        const int k = cell_class(h.ext[a]);
+        cs.ext[k] = h.ext[a];
+        cs.extpos[k] = cs.first[k] = h.extpos[a];
+    }
+    return cs;
+}
+
+// MIN-reduce order key of an extreme cell: value_compare's order within its class
+// (numbers as doubles, dates by (y, m, d)), negated for MAX, as a signed 64-bit
+// integer.  Strings get a constant: their winner is picked from the gathered texts.
+unsigned long long ext_order_key(const HCell& x, bool is_max) {
+    const unsigned long long SIGN = 1ull << 63;
+    unsigned long long ku = 0;
+    switch (cell_class(x)) {
+        case 0: {
+            double d = x.kind == K_INT ? (double)(long long)x.bits : as_dbl(x.bits);
+            if (d == 0) d = 0.0;                             // -0 and 0 compare equal
+            const unsigned long long u = dbl_bits(d);
+            ku = (u >> 63) ? ~u : (u | SIGN);
+            break;
+        }
+        case 1: return 0;
+        default: ku = x.bits; break;                         // (y << 32) | (m << 16) | d
+    }
+    if (is_max) ku = ~ku;
+    return ku ^ SIGN;
+}
+
+void enc_cell(const HCell& x, std::string& ltext, unsigned long long* w) {
+    const uint64_t len = x.kind == K_STR ? x.s.size() : 0;
+    w[0] = CELL_PRESENT | x.kind | (len << 8);
+    w[1] = x.bits;
+    if (x.kind == K_STR) {
+        w[1] = 0;
+        if (len <= 8) {
+            for (size_t i = 0; i < len; i++) w[1] |= (unsigned long long)(uint8_t)x.s[i] << (8 * i);
+        } else {
+            w[0] |= CELL_LONG;
+            w[1] = ltext.size();
+            ltext += x.s;
+        }
+    }
+}
 }  // namespace
+
+struct cqgpu_partial {
+    Compiled C;
+    std::vector<int> mm;                 // MIN/MAX accumulator indexes
+    uint32_t W = 1, P = 1, Q = 1, R = 0, NV = 0, VS0 = 0;
+    uint32_t m = 0;                      // this rank's groups
+    std::vector<uint8_t> keyblob;        // [u64 m][m key records][long key texts]
+    std::string ltext;                   // this rank's cell texts over 8 bytes
+    DevBuf st_sum, st_min, st_priv;      // this rank's planes, m rows
+    std::vector<Stage> stages;
+    size_t at = 0;                       // stages[at] is the next to issue
+    int32_t op = COLL_DONE;
+    uint64_t count = 0;
+    bool masked = false;
+    // the dictionary (from the gathered key blobs)
+    uint32_t nall = 0, G = 0;
+    DevBuf all, text, slot_of, first_of, dense_of, flag;
+    uint64_t text_bytes = 0;
+    DevBuf dsum, dmin, dpriv, dext, dcell, dvla;
+    std::vector<uint8_t> side;           // [u32 d][u32 cell][u32 len][bytes] of owned long cells
+    std::vector<uint8_t> side_all;       // everyone's, gathered
+    std::vector<std::string> mystr;      // per local group and MIN/MAX: its string-class extreme
+    std::vector<unsigned long long> mystrpos;
+    std::vector<uint32_t> dense_id;      // per local group: its dense id
+    std::vector<uint8_t> strs;           // [u32 d][u32 i][u32 len][u64 pos][bytes] candidates
+    std::unordered_map<uint64_t, unsigned long long> str_best;   // d * nmm + i -> winner position
+};
 
 cqgpu_partial* cqgpu_partial_new(cq_node* q, cqgpu_table* const* tables, int ntables) {
     g_inel.clear();
@@ -4752,58 +4858,116 @@ cqgpu_partial* cqgpu_partial_new(cq_node* q, cqgpu_table* const* tables, int nta
         if (ntables < 1 || !tables[0]) throw HipError{"no table"};
         const cqgpu_table* t = tables[0];
         check_plan_shape(q, t);
-        if (is_row_query(q)) throw Ineligible{"row-returning SELECT across partials"};
+        if (is_row_query(q)) throw Ineligible{"dense merge: row-returning SELECT"};
         Compiled& C = p->C;
         compile_aggregate(t, q, C);
-        if (!C.vla.empty() || C.P.ngpart > 0) throw Ineligible{"dense merge: STDDEV/MEDIAN or composite GROUP BY"};
+        for (auto& v : C.vla)
+            if (v.first != 0) throw Ineligible{"dense merge: MEDIAN (needs every value)"};
         for (int a = 0; a < C.P.nacc; a++)
-            if (C.P.acc[a].kind != ACC_SUM) throw Ineligible{"dense merge: MIN/MAX"};
-        for (const OutCol& o : C.outs)
-            if (o.kind == OUT_HEXPR) throw Ineligible{"dense merge: expression items"};
-        if (C.rep_cols.size() > 1 || (C.rep_cols.size() == 1 && C.rep_cols[0] != C.group_col))
-            throw Ineligible{"dense merge: plain columns besides the group key"};
-        p->rep_slot = C.rep_cols.empty() ? -1 : 0;
-        p->names = t->names;
-        p->W = 1 + 2 * (uint32_t)C.P.nacc;
+            if (C.P.acc[a].kind != ACC_SUM) p->mm.push_back(a);
+        const uint32_t nacc = (uint32_t)C.P.nacc, nmm = (uint32_t)p->mm.size();
+        p->R = (uint32_t)C.rep_cols.size();
+        p->NV = (uint32_t)C.vla.size();
+        p->VS0 = 1 + 2 * nacc;
+        p->W = p->VS0 + 2 * p->NV;
+        p->P = 1 + 6 * nmm;
+        p->Q = 1 + 12 * nmm + 2 * p->R + 3 * p->NV;
         Literals L;
         ScanStats st;
         memset(&st, 0, sizeof st);
-        std::vector<HGroup> groups = run_aggregate(c, t, C, L, &st);
+        std::vector<HGroup> groups;
+        if (C.P.ngpart > 0) {
+            groups = run_cells_aggregate(c, t, C, L, &st, true);
+        } else {
+            try {
+                groups = run_aggregate(c, t, C, L, &st);
+                compute_vla(c, t, C, groups, true);
+            } catch (MixedExtremes&) {
+                groups = run_cells_aggregate(c, t, C, L, &st, true);
+            }
+        }
         const uint32_t m = (uint32_t)groups.size();
+        p->m = m;
+        const uint32_t W = p->W, P = p->P, Q = p->Q, R = p->R, NV = p->NV;
         std::vector<HKeyRec> k(m);
-        std::vector<double> sm((size_t)m * p->W);
-        std::vector<unsigned long long> fi(m), rp(2 * (size_t)m);
+        std::string ktext;
+        std::vector<unsigned long long> hs((size_t)m * W), hm((size_t)m * P), hp((size_t)m * Q);
+        p->mystr.assign((size_t)m * nmm, std::string());
+        p->mystrpos.assign((size_t)m * nmm, NOPOS);
         for (uint32_t j = 0; j < m; j++) {
             const HGroup& h = groups[j];
-            if (h.kcls == GK_LONG) throw Ineligible{"dense merge: group key text over 16 bytes"};
             // identity as cqgpu_merge_partials': class + text for text keys, class +
-            // first word for numbers (the second word and length carry nothing there)
-            const bool text = h.kcls == GK_STR || h.kcls == GK_COMP;
-            k[j] = HKeyRec{(h.kcls << 16) | (text ? h.klen : 0u), 0, h.kw0, text ? h.kw1 : 0ull, 0};
-            sm[(size_t)j * p->W] = (double)h.cnt;
-            for (int a = 0; a < C.P.nacc; a++) {
-                sm[(size_t)j * p->W + 1 + 2 * a] = h.sum[a];
-                sm[(size_t)j * p->W + 2 + 2 * a] = (double)h.num[a];
+            // first word for numbers; long text keys carry their bytes in the blob
+            if (h.kcls == GK_LONG) {
+                const uint8_t* b = (const uint8_t*)h.kbytes.data();
+                const uint32_t n = (uint32_t)h.kbytes.size();
+                k[j] = HKeyRec{(GK_LONG << 16) | n, 0, text_hash(b, n, 0x9E3779B97F4A7C15ull), text_hash(b, n, 0x2545F4914F6CDD1Dull),
+                               8 + (uint64_t)m * KEYREC + ktext.size()};
+                ktext += h.kbytes;
+            } else {
+                const bool txt = h.kcls == GK_STR || h.kcls == GK_COMP;
+                k[j] = HKeyRec{(h.kcls << 16) | (txt ? h.klen : 0u), 0, h.kw0, txt ? h.kw1 : 0ull, 0};
             }
-            // a group with no first row here (NOPOS = -1 as a signed int64) must lose the
-            // MIN all-reduce of first positions: the "absent" sentinel scatter uses
-            fi[j] = h.first == NOPOS ? 0x7F7F7F7F7F7F7F7Full : h.first;
-            if (p->rep_slot >= 0 && !h.reps.empty()) {
-                rp[2 * j] = h.reps[0].kind;
-                rp[2 * j + 1] = h.reps[0].kind == K_STR ? 0 : h.reps[0].bits;   // text: the key's bytes
+            unsigned long long* s = &hs[(size_t)j * W];
+            s[0] = dbl_bits((double)h.cnt);
+            for (uint32_t a = 0; a < nacc; a++) {
+                s[1 + 2 * a] = dbl_bits(h.sum[a]);
+                s[2 + 2 * a] = dbl_bits((double)h.num[a]);
+            }
+            for (uint32_t v = 0; v < NV; v++) {
+                s[p->VS0 + 2 * v] = dbl_bits(h.vn[v]);
+                s[p->VS0 + 2 * v + 1] = dbl_bits(h.vsum[v]);
+            }
+            unsigned long long* mn = &hm[(size_t)j * P];
+            unsigned long long* pv = &hp[(size_t)j * Q];
+            mn[0] = pv[0] = h.first == NOPOS ? ABS64 : h.first;
+            for (uint32_t i = 0; i < nmm; i++) {
+                const int a = p->mm[i];
+                const HGroup::ClassSplit cs = class_split(h, a);
+                for (int kk = 0; kk < 3; kk++) {
+                    const bool here = cs.extpos[kk] != NOPOS;
+                    const unsigned long long key = here ? ext_order_key(cs.ext[kk], C.P.acc[a].kind == ACC_MAX) : ABS64;
+                    mn[1 + 6 * i + kk] = cs.first[kk] == NOPOS ? ABS64 : cs.first[kk];
+                    mn[1 + 6 * i + 3 + kk] = key;
+                    pv[1 + 12 * i + kk] = key;
+                    pv[1 + 12 * i + 3 + kk] = here ? cs.extpos[kk] : ABS64;
+                    if (here) enc_cell(cs.ext[kk], p->ltext, &pv[1 + 12 * i + 6 + 2 * kk]);
+                    if (here && kk == 1) {
+                        p->mystr[(size_t)j * nmm + i] = cs.ext[1].s;
+                        p->mystrpos[(size_t)j * nmm + i] = cs.extpos[1];
+                    }
+                }
+            }
+            for (uint32_t r = 0; r < R; r++)
+                if (r < h.reps.size()) enc_cell(h.reps[r], p->ltext, &pv[1 + 12 * nmm + 2 * r]);
+            for (uint32_t v = 0; v < NV; v++) {
+                pv[1 + 12 * nmm + 2 * R + 3 * v] = dbl_bits(h.vn[v]);
+                pv[1 + 12 * nmm + 2 * R + 3 * v + 1] = dbl_bits(h.vsum[v]);
+                pv[1 + 12 * nmm + 2 * R + 3 * v + 2] = dbl_bits(h.vm2[v]);
             }
         }
-        p->m = m;
-        DevBuf a(std::max<size_t>((size_t)m * KEYREC, 64)), b(std::max<size_t>(sm.size() * 8, 64)),
-            f(std::max<size_t>((size_t)m * 8, 64)), r(std::max<size_t>(rp.size() * 8, 64));
-        std::swap(p->keys.p, a.p); std::swap(p->st_sum.p, b.p); std::swap(p->st_first.p, f.p); std::swap(p->st_rep.p, r.p);
+        p->keyblob.resize(8 + (size_t)m * KEYREC + ktext.size());
+        const uint64_t m64 = m;
+        memcpy(p->keyblob.data(), &m64, 8);
+        if (m) memcpy(p->keyblob.data() + 8, k.data(), (size_t)m * KEYREC);
+        if (!ktext.empty()) memcpy(p->keyblob.data() + 8 + (size_t)m * KEYREC, ktext.data(), ktext.size());
+        DevBuf a(std::max<size_t>(hs.size() * 8, 64)), b(std::max<size_t>(hm.size() * 8, 64)),
+            r(std::max<size_t>(hp.size() * 8, 64));
+        std::swap(p->st_sum.p, a.p); std::swap(p->st_min.p, b.p); std::swap(p->st_priv.p, r.p);
         if (m) {
-            HIPCHECK(hipMemcpyAsync(p->keys.p, k.data(), (size_t)m * KEYREC, hipMemcpyHostToDevice, c.stream));
-            HIPCHECK(hipMemcpyAsync(p->st_sum.p, sm.data(), sm.size() * 8, hipMemcpyHostToDevice, c.stream));
-            HIPCHECK(hipMemcpyAsync(p->st_first.p, fi.data(), fi.size() * 8, hipMemcpyHostToDevice, c.stream));
-            HIPCHECK(hipMemcpyAsync(p->st_rep.p, rp.data(), rp.size() * 8, hipMemcpyHostToDevice, c.stream));
+            HIPCHECK(hipMemcpyAsync(p->st_sum.p, hs.data(), hs.size() * 8, hipMemcpyHostToDevice, c.stream));
+            HIPCHECK(hipMemcpyAsync(p->st_min.p, hm.data(), hm.size() * 8, hipMemcpyHostToDevice, c.stream));
+            HIPCHECK(hipMemcpyAsync(p->st_priv.p, hp.data(), hp.size() * 8, hipMemcpyHostToDevice, c.stream));
         }
         HIPCHECK(hipStreamSynchronize(c.stream));
+        p->stages = {ST_KEYS, ST_MIN};
+        if (NV) p->stages.push_back(ST_SUM);
+        if (nmm) p->stages.push_back(ST_STRS);
+        if (nmm) p->stages.push_back(ST_EXT);
+        if (R + nmm) p->stages.push_back(ST_CELL);
+        if (NV) p->stages.push_back(ST_VLA);
+        if (!NV) p->stages.push_back(ST_SUMR);
+        if (R + nmm) p->stages.push_back(ST_SIDE);
         return p.release();
     } catch (Ineligible& e) {
         g_inel = e.why;
@@ -4815,84 +4979,301 @@ cqgpu_partial* cqgpu_partial_new(cq_node* q, cqgpu_table* const* tables, int nta
     }
 }
 
-size_t cqgpu_partial_keys(cqgpu_partial* p, void* dev_dst, uint32_t* words_per_group) {
-    if (words_per_group) *words_per_group = p ? p->W : 0;
-    if (!p) return 0;
-    if (dev_dst && p->m) {
+namespace {
+// the dictionary from the gathered key blobs: records compacted in rank order,
+// long-key text offsets rebased into the concatenation, then merge.hip's build
+// (dense id = rank of a key's first occurrence) and this rank's planes scattered
+// into G-row dense planes (rows of absent groups hold the planes' identities)
+bool build_dictionary(DevCtx& c, cqgpu_partial* p, const uint8_t* cat, const uint64_t* sizes, int rank, int world) {
+    std::vector<uint64_t> off(world + 1, 0), ms(world, 0);
+    for (int r = 0; r < world; r++) off[r + 1] = off[r] + sizes[r];
+    for (int r = 0; r < world; r++) {
+        if (sizes[r] < 8) throw HipError{"partial_next: bad key blob"};
+        HIPCHECK(hipMemcpyAsync(&ms[r], cat + off[r], 8, hipMemcpyDeviceToHost, c.stream));
+    }
+    HIPCHECK(hipStreamSynchronize(c.stream));
+    uint64_t nall = 0, mine = 0;
+    for (int r = 0; r < world; r++) {
+        if (8 + ms[r] * KEYREC > sizes[r]) throw HipError{"partial_next: bad key blob"};
+        if (r < rank) mine += ms[r];
+        nall += ms[r];
+    }
+    if (ms[rank] != p->m) throw HipError{"partial_next: the gathered blob of this rank is not its own"};
+    // the table holds 2 * nall slots of 32-bit indexes
+    if (nall >= (1ull << 29)) return false;
+    const uint32_t n = (uint32_t)nall;
+    DevBuf all(std::max<size_t>((size_t)n * KEYREC, 64)), text(std::max<uint64_t>(off[world], 64));
+    HIPCHECK(hipMemcpyAsync(text.p, cat, off[world], hipMemcpyDeviceToDevice, c.stream));
+    uint64_t at = 0;
+    for (int r = 0; r < world; r++) {
+        if (!ms[r]) continue;
+        uint8_t* dst = all.as<uint8_t>() + at * KEYREC;
+        HIPCHECK(hipMemcpyAsync(dst, cat + off[r] + 8, ms[r] * KEYREC, hipMemcpyDeviceToDevice, c.stream));
+        HIPCHECK(cq_launch_rebase(dst, (uint32_t)ms[r], off[r], c.stream));
+        at += ms[r];
+    }
+    uint64_t cap = 64;
+    while (cap < 2 * (uint64_t)n) cap <<= 1;
+    DevBuf st((size_t)cap * 4), ro((size_t)cap * 4), fo((size_t)cap * 4), so(std::max<size_t>((size_t)n * 4, 4)),
+        fl(std::max<size_t>((size_t)n * 4, 4)), de(std::max<size_t>((size_t)n * 4, 4)), err(64);
+    HIPCHECK(hipMemsetAsync(st.p, 0, (size_t)cap * 4, c.stream));
+    HIPCHECK(hipMemsetAsync(fo.p, 0xFF, (size_t)cap * 4, c.stream));
+    HIPCHECK(hipMemsetAsync(err.p, 0, 4, c.stream));
+    HIPCHECK(cq_launch_dict_build(all.p, text.p, n, st.as<uint32_t>(), ro.as<uint32_t>(), fo.as<uint32_t>(),
+                                  (uint32_t)cap, so.as<uint32_t>(), err.as<unsigned int>(), c.stream));
+    HIPCHECK(cq_launch_dict_flag(so.as<uint32_t>(), fo.as<uint32_t>(), n, fl.as<uint32_t>(), c.stream));
+    size_t tb = 0;
+    HIPCHECK(cq_excl_sum_u32(nullptr, &tb, fl.as<unsigned int>(), de.as<unsigned int>(), n, c.stream));
+    DevBuf temp(std::max<size_t>(tb, 16));
+    HIPCHECK(cq_excl_sum_u32(temp.p, &tb, fl.as<unsigned int>(), de.as<unsigned int>(), n, c.stream));
+    unsigned int e = 0, last[2] = {0, 0};
+    HIPCHECK(hipMemcpyAsync(&e, err.p, 4, hipMemcpyDeviceToHost, c.stream));
+    if (n) {
+        HIPCHECK(hipMemcpyAsync(&last[0], de.as<uint32_t>() + n - 1, 4, hipMemcpyDeviceToHost, c.stream));
+        HIPCHECK(hipMemcpyAsync(&last[1], fl.as<uint32_t>() + n - 1, 4, hipMemcpyDeviceToHost, c.stream));
+    }
+    HIPCHECK(hipStreamSynchronize(c.stream));
+    if (e) throw HipError{"partial_next: key table full or insert timeout"};
+    const uint32_t G = last[0] + last[1];
+    p->nall = n;
+    p->G = G;
+    p->text_bytes = off[world];
+    std::swap(p->all.p, all.p); std::swap(p->text.p, text.p); std::swap(p->slot_of.p, so.p);
+    std::swap(p->first_of.p, fo.p); std::swap(p->dense_of.p, de.p); std::swap(p->flag.p, fl.p);
+    // G-row planes: identities first, then this rank's rows
+    const uint32_t W = p->W, P = p->P, Q = p->Q, nmm = (uint32_t)p->mm.size(), C = p->R + nmm;
+    DevBuf ds(std::max<size_t>((size_t)G * W * 8, 64)), dm(std::max<size_t>((size_t)G * P * 8, 64)),
+        dp(std::max<size_t>((size_t)G * Q * 8, 64)), dx(std::max<size_t>((size_t)G * nmm * 8, 64)),
+        dc(std::max<size_t>((size_t)G * C * 16, 64)), dv(std::max<size_t>((size_t)G * p->NV * 8, 64));
+    std::vector<unsigned long long> rows(W + P + Q, 0);
+    for (uint32_t w = 0; w < P; w++) rows[W + w] = ABS64;
+    rows[W + P] = ABS64;                                     // private: first, then per MIN/MAX keys
+    for (uint32_t i = 0; i < nmm; i++)                       // and positions absent, cells / moments 0
+        for (int kk = 0; kk < 6; kk++) rows[W + P + 1 + 12 * i + kk] = ABS64;
+    DevBuf drow(rows.size() * 8), did(std::max<size_t>((size_t)p->m * 4, 64));
+    HIPCHECK(hipMemcpyAsync(drow.p, rows.data(), rows.size() * 8, hipMemcpyHostToDevice, c.stream));
+    HIPCHECK(cq_launch_fill_rows(ds.as<unsigned long long>(), G, W, drow.as<unsigned long long>(), c.stream));
+    HIPCHECK(cq_launch_fill_rows(dm.as<unsigned long long>(), G, P, drow.as<unsigned long long>() + W, c.stream));
+    HIPCHECK(cq_launch_fill_rows(dp.as<unsigned long long>(), G, Q, drow.as<unsigned long long>() + W + P, c.stream));
+    HIPCHECK(cq_launch_dict_scatter(p->slot_of.as<uint32_t>(), p->first_of.as<uint32_t>(), p->dense_of.as<uint32_t>(),
+                                    (uint32_t)mine, p->m, p->st_sum.as<unsigned long long>(),
+                                    p->st_min.as<unsigned long long>(), p->st_priv.as<unsigned long long>(), W, P, Q,
+                                    ds.as<unsigned long long>(), dm.as<unsigned long long>(),
+                                    dp.as<unsigned long long>(), did.as<uint32_t>(), c.stream));
+    p->dense_id.resize(p->m);
+    if (p->m)
+        HIPCHECK(hipMemcpyAsync(p->dense_id.data(), did.p, (size_t)p->m * 4, hipMemcpyDeviceToHost, c.stream));
+    HIPCHECK(hipStreamSynchronize(c.stream));
+    std::swap(p->dsum.p, ds.p); std::swap(p->dmin.p, dm.p); std::swap(p->dpriv.p, dp.p);
+    std::swap(p->dext.p, dx.p); std::swap(p->dcell.p, dc.p); std::swap(p->dvla.p, dv.p);
+    return true;
+}
+
+// the owners' cells and STDDEV terms (merge.hip cell_mask_kernel), and the side blob
+// of this rank's owned cell texts over 8 bytes
+void mask_cells(DevCtx& c, cqgpu_partial* p) {
+    if (p->masked) return;
+    const uint32_t nmm = (uint32_t)p->mm.size(), C = p->R + nmm;
+    HIPCHECK(cq_launch_cell_mask(p->dmin.as<unsigned long long>(), p->dext.as<unsigned long long>(),
+                                 p->dpriv.as<unsigned long long>(), p->dsum.as<double>(), p->G, p->P, p->Q, p->W, nmm,
+                                 p->R, p->NV, p->VS0, p->dcell.as<unsigned long long>(), p->dvla.as<double>(),
+                                 c.stream));
+    std::vector<unsigned long long> cells((size_t)p->G * C * 2);
+    if (!cells.empty())
+        HIPCHECK(hipMemcpyAsync(cells.data(), p->dcell.p, cells.size() * 8, hipMemcpyDeviceToHost, c.stream));
+    HIPCHECK(hipStreamSynchronize(c.stream));
+    p->side.clear();
+    auto u32 = [&](uint32_t v) { p->side.insert(p->side.end(), (uint8_t*)&v, (uint8_t*)&v + 4); };
+    for (size_t i = 0; i < cells.size() / 2; i++) {
+        const unsigned long long w0 = cells[2 * i], w1 = cells[2 * i + 1];
+        if (!(w0 & CELL_PRESENT) || !(w0 & CELL_LONG)) continue;
+        const uint32_t len = (uint32_t)((w0 >> 8) & 0xFFFFFFFFull);
+        if (w1 + len > p->ltext.size()) throw HipError{"partial_next: bad cell text offset"};
+        u32((uint32_t)(i / C));
+        u32((uint32_t)(i % C));
+        u32(len);
+        p->side.insert(p->side.end(), p->ltext.begin() + w1, p->ltext.begin() + w1 + len);
+    }
+    p->masked = true;
+}
+}  // namespace
+
+namespace {
+// this rank's string-class extremes of the (group, MIN/MAX) pairs whose result keeps
+// the string class (the class whose first cell comes first, from the global MIN plane)
+void string_candidates(DevCtx& c, cqgpu_partial* p) {
+    const uint32_t nmm = (uint32_t)p->mm.size(), P = p->P;
+    std::vector<unsigned long long> mn((size_t)p->G * P);
+    if (!mn.empty()) HIPCHECK(hipMemcpyAsync(mn.data(), p->dmin.p, mn.size() * 8, hipMemcpyDeviceToHost, c.stream));
+    HIPCHECK(hipStreamSynchronize(c.stream));
+    p->strs.clear();
+    for (uint32_t j = 0; j < p->m; j++)
+        for (uint32_t i = 0; i < nmm; i++) {
+            if (p->mystrpos[(size_t)j * nmm + i] == NOPOS) continue;
+            const uint32_t d = p->dense_id[j];
+            const unsigned long long* cf = &mn[(size_t)d * P + 1 + 6 * i];
+            int best = -1;
+            for (int k = 0; k < 3; k++)
+                if (cf[k] != ABS64 && (best < 0 || (long long)cf[k] < (long long)cf[best])) best = k;
+            if (best != 1) continue;
+            const std::string& t = p->mystr[(size_t)j * nmm + i];
+            const uint32_t h[3] = {d, i, (uint32_t)t.size()};
+            const unsigned long long pos = p->mystrpos[(size_t)j * nmm + i];
+            p->strs.insert(p->strs.end(), (const uint8_t*)h, (const uint8_t*)h + 12);
+            p->strs.insert(p->strs.end(), (const uint8_t*)&pos, (const uint8_t*)&pos + 8);
+            p->strs.insert(p->strs.end(), t.begin(), t.end());
+        }
+}
+
+// every rank's candidates -> per (group, MIN/MAX) the winner: strcmp order (value_compare
+// on strings), the first position among equals (evaluator_aggregates.c:311-326)
+void string_winners(cqgpu_partial* p, const uint8_t* all, size_t n) {
+    const uint32_t nmm = (uint32_t)p->mm.size();
+    struct Best { HCell v; unsigned long long pos; };
+    std::unordered_map<uint64_t, Best> best;
+    for (size_t o = 0; o + 20 <= n;) {
+        uint32_t h[3];
+        unsigned long long pos;
+        memcpy(h, all + o, 12);
+        memcpy(&pos, all + o + 12, 8);
+        o += 20;
+        if (o + h[2] > n || h[0] >= p->G || h[1] >= nmm) throw HipError{"partial_next: bad string candidates"};
+        HCell x;
+        x.kind = K_STR;
+        x.s.assign((const char*)all + o, h[2]);
+        o += h[2];
+        const bool is_max = p->C.P.acc[p->mm[h[1]]].kind == ACC_MAX;
+        const uint64_t key = (uint64_t)h[0] * nmm + h[1];
+        auto it = best.find(key);
+        if (it == best.end()) { best.emplace(key, Best{x, pos}); continue; }
+        const int cv = hcompare(x, it->second.v);
+        if ((is_max ? cv > 0 : cv < 0) || (cv == 0 && pos < it->second.pos)) it->second = Best{x, pos};
+    }
+    p->str_best.clear();
+    for (auto& kv : best) p->str_best[kv.first] = kv.second.pos;
+}
+}  // namespace
+
+int cqgpu_partial_next(cqgpu_partial* p, const void* result, const uint64_t* result_sizes, int rank, int world,
+                       cqgpu_coll* next) {
+    g_err.clear();
+    try {
+        if (!p || !next || world < 1 || rank < 0 || rank >= world) throw HipError{"partial_next: bad arguments"};
         DevCtx& c = ctx();
-        if (hipMemcpyAsync(dev_dst, p->keys.p, (size_t)p->m * KEYREC, hipMemcpyDeviceToDevice, c.stream) != hipSuccess ||
-            hipStreamSynchronize(c.stream) != hipSuccess) {
-            set_err("cq_amd: partial_keys: copy failed");
+        const uint32_t G = p->G, nmm = (uint32_t)p->mm.size(), C = p->R + nmm;
+        // 1. take the result of the collective issued last
+        if (p->at > 0) {
+            const Stage done = p->stages[p->at - 1];
+            const size_t bytes = p->count * (done == ST_KEYS || done == ST_SIDE || done == ST_STRS ? 1 : 8);
+            if (!result && bytes) throw HipError{"partial_next: no result buffer"};
+            DevBuf* into = nullptr;
+            switch (done) {
+                case ST_KEYS:
+                    if (!result_sizes) throw HipError{"partial_next: no gathered sizes"};
+                    if (!build_dictionary(c, p, (const uint8_t*)result, result_sizes, rank, world)) {
+                        next->op = COLL_DECLINE;
+                        next->count = 0;
+                        p->op = COLL_DECLINE;
+                        return 0;
+                    }
+                    break;
+                case ST_MIN: into = &p->dmin; break;
+                case ST_SUM: case ST_SUMR: into = &p->dsum; break;
+                case ST_EXT: into = &p->dext; break;
+                case ST_CELL: into = &p->dcell; break;
+                case ST_VLA: into = &p->dvla; break;
+                case ST_STRS: {
+                    if (!result_sizes) throw HipError{"partial_next: no gathered sizes"};
+                    uint64_t tot = 0;
+                    for (int r = 0; r < world; r++) tot += result_sizes[r];
+                    std::vector<uint8_t> h(tot);
+                    if (tot) HIPCHECK(hipMemcpyAsync(h.data(), result, tot, hipMemcpyDeviceToHost, c.stream));
+                    HIPCHECK(hipStreamSynchronize(c.stream));
+                    string_winners(p, h.data(), h.size());
+                    break;
+                }
+                case ST_SIDE: {
+                    if (!result_sizes) throw HipError{"partial_next: no gathered sizes"};
+                    uint64_t tot = 0;
+                    for (int r = 0; r < world; r++) tot += result_sizes[r];
+                    p->side_all.resize(tot);
+                    if (tot) HIPCHECK(hipMemcpyAsync(p->side_all.data(), result, tot, hipMemcpyDeviceToHost, c.stream));
+                    HIPCHECK(hipStreamSynchronize(c.stream));
+                    break;
+                }
+            }
+            if (into && bytes) {
+                HIPCHECK(hipMemcpyAsync(into->p, result, bytes, hipMemcpyDeviceToDevice, c.stream));
+                HIPCHECK(hipStreamSynchronize(c.stream));
+            }
+        }
+        // 2. the next collective
+        if (p->at >= p->stages.size()) {
+            p->op = next->op = COLL_DONE;
+            p->count = next->count = 0;
             return 0;
         }
-    }
-    return p->m;
-}
-
-long long cqgpu_partial_dict(cqgpu_partial* p, const void* dev_all, uint64_t nall, uint64_t mine) {
-    g_err.clear();
-    try {
-        if (!p || (!dev_all && nall) || mine + p->m > nall) throw HipError{"partial_dict: bad arguments"};
-        // the table holds 2 * nall slots of 32-bit indexes: beyond 2^29 keys the caller
-        // takes the blob path (cqgpu_query_partial) instead
-        if (nall >= (1ull << 29)) throw HipError{"partial_dict: too many keys for the device dictionary"};
-        DevCtx& c = ctx();
-        const uint32_t n = (uint32_t)nall;
-        uint64_t cap = 64;
-        while (cap < 2 * (uint64_t)n) cap <<= 1;
-        DevBuf owned(std::max<size_t>((size_t)n * KEYREC, 64));
-        if (n) HIPCHECK(hipMemcpyAsync(owned.p, dev_all, (size_t)n * KEYREC, hipMemcpyDeviceToDevice, c.stream));
-        dev_all = owned.p;
-        std::swap(p->all.p, owned.p);
-        p->nall = n; p->mine = (uint32_t)mine; p->cap = (uint32_t)cap;
-        DevBuf st((size_t)cap * 4), ro((size_t)cap * 4), fo((size_t)cap * 4), so(std::max<size_t>((size_t)n * 4, 4)),
-            fl(std::max<size_t>((size_t)n * 4, 4)), de(std::max<size_t>((size_t)n * 4, 4)), err(64);
-        HIPCHECK(hipMemsetAsync(st.p, 0, (size_t)cap * 4, c.stream));
-        HIPCHECK(hipMemsetAsync(fo.p, 0xFF, (size_t)cap * 4, c.stream));
-        HIPCHECK(hipMemsetAsync(err.p, 0, 4, c.stream));
-        HIPCHECK(cq_launch_dict_build(dev_all, n, st.as<uint32_t>(), ro.as<uint32_t>(), fo.as<uint32_t>(), cap,
-                                      so.as<uint32_t>(), err.as<unsigned int>(), c.stream));
-        HIPCHECK(cq_launch_dict_flag(so.as<uint32_t>(), fo.as<uint32_t>(), n, fl.as<uint32_t>(), c.stream));
-        size_t tb = 0;
-        HIPCHECK(cq_excl_sum_u32(nullptr, &tb, fl.as<unsigned int>(), de.as<unsigned int>(), n, c.stream));
-        DevBuf temp(tb);
-        HIPCHECK(cq_excl_sum_u32(temp.p, &tb, fl.as<unsigned int>(), de.as<unsigned int>(), n, c.stream));
-        unsigned int e = 0, last[2] = {0, 0};
-        HIPCHECK(hipMemcpyAsync(&e, err.p, 4, hipMemcpyDeviceToHost, c.stream));
-        if (n) {
-            HIPCHECK(hipMemcpyAsync(&last[0], de.as<uint32_t>() + n - 1, 4, hipMemcpyDeviceToHost, c.stream));
-            HIPCHECK(hipMemcpyAsync(&last[1], fl.as<uint32_t>() + n - 1, 4, hipMemcpyDeviceToHost, c.stream));
+        const uint32_t g = p->G;
+        (void)G;
+        switch (p->stages[p->at]) {
+            case ST_KEYS: p->op = COLL_ALLGATHER; p->count = p->keyblob.size(); break;
+            case ST_MIN: p->op = COLL_ALLREDUCE_MIN_I64; p->count = (uint64_t)g * p->P; break;
+            case ST_SUM: p->op = COLL_ALLREDUCE_SUM_F64; p->count = (uint64_t)g * p->W; break;
+            case ST_STRS:
+                string_candidates(c, p);
+                p->op = COLL_ALLGATHER;
+                p->count = p->strs.size();
+                break;
+            case ST_EXT:
+                HIPCHECK(cq_launch_ext_mask(p->dmin.as<unsigned long long>(), p->dpriv.as<unsigned long long>(), g, p->P,
+                                            p->Q, nmm, p->dext.as<unsigned long long>(), c.stream));
+                if (!p->str_best.empty()) {       // string winners: every rank already knows the position
+                    std::vector<unsigned long long> ex((size_t)g * nmm);
+                    HIPCHECK(hipMemcpyAsync(ex.data(), p->dext.p, ex.size() * 8, hipMemcpyDeviceToHost, c.stream));
+                    HIPCHECK(hipStreamSynchronize(c.stream));
+                    for (auto& kv : p->str_best) ex[kv.first] = kv.second;
+                    HIPCHECK(hipMemcpyAsync(p->dext.p, ex.data(), ex.size() * 8, hipMemcpyHostToDevice, c.stream));
+                }
+                HIPCHECK(hipStreamSynchronize(c.stream));
+                p->op = COLL_ALLREDUCE_MIN_I64;
+                p->count = (uint64_t)g * nmm;
+                break;
+            case ST_CELL: mask_cells(c, p); p->op = COLL_REDUCE_SUM_I64; p->count = (uint64_t)g * C * 2; break;
+            case ST_VLA: mask_cells(c, p); p->op = COLL_REDUCE_SUM_F64; p->count = (uint64_t)g * p->NV; break;
+            case ST_SUMR: p->op = COLL_REDUCE_SUM_F64; p->count = (uint64_t)g * p->W; break;
+            case ST_SIDE: mask_cells(c, p); p->op = COLL_ALLGATHER; p->count = p->side.size(); break;
         }
-        HIPCHECK(hipStreamSynchronize(c.stream));
-        if (e) throw HipError{"partial_dict: key table full or insert timeout"};
-        std::swap(p->state.p, st.p); std::swap(p->rec_of.p, ro.p); std::swap(p->first_of.p, fo.p);
-        std::swap(p->slot_of.p, so.p); std::swap(p->flag.p, fl.p); std::swap(p->dense_of.p, de.p);
-        p->G = last[0] + last[1];
-        return p->G;
+        p->at++;
+        next->op = p->op;
+        next->count = p->count;
+        return 0;
     } catch (HipError& e) {
         set_err("cq_amd: %s", e.msg.c_str());
         return -1;
     }
 }
 
-int cqgpu_partial_scatter(cqgpu_partial* p, double* dsum, unsigned long long* dfirst, unsigned long long* drep) {
+int cqgpu_partial_put(cqgpu_partial* p, void* dev_dst) {
     g_err.clear();
     try {
-        if (!p) throw HipError{"partial_scatter: no partial"};
+        if (!p || p->at == 0 || p->op == COLL_DONE || p->op == COLL_DECLINE) throw HipError{"partial_put: nothing pending"};
+        if (!p->count) return 0;
+        if (!dev_dst) throw HipError{"partial_put: no buffer"};
         DevCtx& c = ctx();
-        const size_t G = p->G;
-        if (G) {
-            HIPCHECK(hipMemsetAsync(dsum, 0, G * p->W * 8, c.stream));
-            HIPCHECK(hipMemsetAsync(dfirst, 0x7F, G * 8, c.stream));   // "absent": above every position,
-                                                                        // also as a signed int64 (MIN reduce)
-            HIPCHECK(hipMemsetAsync(drep, 0, G * 16, c.stream));
+        const void* src = nullptr;
+        hipMemcpyKind kind = hipMemcpyDeviceToDevice;
+        switch (p->stages[p->at - 1]) {
+            case ST_KEYS: src = p->keyblob.data(); kind = hipMemcpyHostToDevice; break;
+            case ST_SIDE: src = p->side.data(); kind = hipMemcpyHostToDevice; break;
+            case ST_STRS: src = p->strs.data(); kind = hipMemcpyHostToDevice; break;
+            case ST_MIN: src = p->dmin.p; break;
+            case ST_SUM: case ST_SUMR: src = p->dsum.p; break;
+            case ST_EXT: src = p->dext.p; break;
+            case ST_CELL: src = p->dcell.p; break;
+            case ST_VLA: src = p->dvla.p; break;
         }
-        HIPCHECK(cq_launch_dict_scatter(p->slot_of.as<uint32_t>(), p->first_of.as<uint32_t>(), p->dense_of.as<uint32_t>(),
-                                        p->mine, p->m, p->st_sum.as<double>(), p->st_first.as<unsigned long long>(),
-                                        p->st_rep.as<unsigned long long>(), p->W, dsum, dfirst, drep, c.stream));
-        DevBuf mf(std::max<size_t>(G * 8, 8));
-        if (G) HIPCHECK(hipMemcpyAsync(mf.p, dfirst, G * 8, hipMemcpyDeviceToDevice, c.stream));
-        std::swap(p->my_first.p, mf.p);
+        const size_t bytes = p->count * (p->op == COLL_ALLGATHER ? 1 : 8);
+        HIPCHECK(hipMemcpyAsync(dev_dst, src, bytes, kind, c.stream));
         HIPCHECK(hipStreamSynchronize(c.stream));
         return 0;
     } catch (HipError& e) {
@@ -4901,43 +5282,63 @@ int cqgpu_partial_scatter(cqgpu_partial* p, double* dsum, unsigned long long* df
     }
 }
 
-int cqgpu_partial_mask_reps(cqgpu_partial* p, const unsigned long long* dfirst_global, unsigned long long* drep) {
-    g_err.clear();
-    try {
-        if (!p) throw HipError{"partial_mask_reps: no partial"};
-        DevCtx& c = ctx();
-        HIPCHECK(cq_launch_rep_mask(p->my_first.as<unsigned long long>(), dfirst_global, p->G, drep, c.stream));
-        HIPCHECK(hipStreamSynchronize(c.stream));
-        return 0;
-    } catch (HipError& e) {
-        set_err("cq_amd: %s", e.msg.c_str());
-        return -1;
-    }
-}
-
-cq_table* cqgpu_partial_finish(cqgpu_partial* p, cq_node* q, const double* dsum, const unsigned long long* dfirst,
-                               const unsigned long long* drep) {
+cq_table* cqgpu_partial_result(cqgpu_partial* p, cq_node* q) {
     g_inel.clear();
     g_err.clear();
     try {
-        if (!p) throw HipError{"partial_finish: no partial"};
+        if (!p || p->op != COLL_DONE || p->at != p->stages.size()) throw HipError{"partial_result: merge not finished"};
         DevCtx& c = ctx();
-        const uint32_t G = p->G, n = p->nall, W = p->W;
+        const uint32_t G = p->G, n = p->nall, W = p->W, P = p->P, nmm = (uint32_t)p->mm.size(), R = p->R;
+        const uint32_t C = R + nmm, NV = p->NV;
         std::vector<HKeyRec> all(n);
         std::vector<uint32_t> flag(n);
-        std::vector<double> sm((size_t)G * W);
-        std::vector<unsigned long long> fi(G), rp(2 * (size_t)G);
+        std::vector<uint8_t> text(p->text_bytes);
+        std::vector<double> sm((size_t)G * W), vla((size_t)G * NV);
+        std::vector<unsigned long long> mn((size_t)G * P), ex((size_t)G * nmm), cells((size_t)G * C * 2);
         if (n) {
             HIPCHECK(hipMemcpyAsync(all.data(), p->all.p, (size_t)n * KEYREC, hipMemcpyDeviceToHost, c.stream));
             HIPCHECK(hipMemcpyAsync(flag.data(), p->flag.p, (size_t)n * 4, hipMemcpyDeviceToHost, c.stream));
         }
-        if (G) {
-            HIPCHECK(hipMemcpyAsync(sm.data(), dsum, sm.size() * 8, hipMemcpyDeviceToHost, c.stream));
-            HIPCHECK(hipMemcpyAsync(fi.data(), dfirst, fi.size() * 8, hipMemcpyDeviceToHost, c.stream));
-            HIPCHECK(hipMemcpyAsync(rp.data(), drep, rp.size() * 8, hipMemcpyDeviceToHost, c.stream));
-        }
+        if (!text.empty()) HIPCHECK(hipMemcpyAsync(text.data(), p->text.p, text.size(), hipMemcpyDeviceToHost, c.stream));
+        auto get = [&](void* dst, const DevBuf& b, size_t bytes) {
+            if (bytes) HIPCHECK(hipMemcpyAsync(dst, b.p, bytes, hipMemcpyDeviceToHost, c.stream));
+        };
+        get(sm.data(), p->dsum, sm.size() * 8);
+        get(vla.data(), p->dvla, vla.size() * 8);
+        get(mn.data(), p->dmin, mn.size() * 8);
+        get(ex.data(), p->dext, ex.size() * 8);
+        get(cells.data(), p->dcell, cells.size() * 8);
         HIPCHECK(hipStreamSynchronize(c.stream));
-        const Compiled& C = p->C;
+        // the owners' texts over 8 bytes
+        std::unordered_map<uint64_t, std::string> longs;
+        for (size_t o = 0; o + 12 <= p->side_all.size();) {
+            uint32_t h[3];
+            memcpy(h, p->side_all.data() + o, 12);
+            o += 12;
+            if (o + h[2] > p->side_all.size() || h[0] >= G || h[1] >= C) throw HipError{"partial_result: bad side blob"};
+            longs[(uint64_t)h[0] * C + h[1]].assign((const char*)p->side_all.data() + o, h[2]);
+            o += h[2];
+        }
+        auto dec = [&](uint64_t d, uint32_t ci) {
+            HCell x;
+            const unsigned long long w0 = cells[(d * C + ci) * 2], w1 = cells[(d * C + ci) * 2 + 1];
+            if (!(w0 & CELL_PRESENT)) return x;
+            x.kind = (uint32_t)(w0 & 0xff);
+            x.bits = w1;
+            if (x.kind == K_STR) {
+                const uint32_t len = (uint32_t)((w0 >> 8) & 0xFFFFFFFFull);
+                x.bits = 0;
+                if (w0 & CELL_LONG) {
+                    auto it = longs.find(d * C + ci);
+                    if (it == longs.end()) throw HipError{"partial_result: a long cell's text is missing"};
+                    x.s = it->second;
+                } else {
+                    for (uint32_t i = 0; i < len; i++) x.s.push_back((char)((w1 >> (8 * i)) & 0xff));
+                }
+            }
+            return x;
+        };
+        const Compiled& Cp = p->C;
         std::vector<HGroup> groups;
         uint32_t d = 0;
         for (uint32_t r = 0; r < n && d < G; r++) {
@@ -4951,25 +5352,35 @@ cq_table* cqgpu_partial_finish(cqgpu_partial* p, cq_node* q, const double* dsum,
             if (h.kcls == GK_STR)
                 for (uint32_t i = 0; i < h.klen; i++)
                     h.kbytes.push_back((char)((i < 8 ? k.w0 >> (8 * i) : k.w1 >> (8 * (i - 8))) & 0xff));
+            if (h.kcls == GK_LONG) {
+                if (k.pad2 + h.klen > text.size()) throw HipError{"partial_result: bad key text offset"};
+                h.kbytes.assign((const char*)text.data() + k.pad2, h.klen);
+            }
             h.cnt = (unsigned long long)sm[(size_t)d * W];
-            for (int a = 0; a < C.P.nacc; a++) {
+            for (int a = 0; a < Cp.P.nacc; a++) {
                 h.sum[a] = sm[(size_t)d * W + 1 + 2 * a];
                 h.num[a] = (unsigned long long)sm[(size_t)d * W + 2 + 2 * a];
             }
-            h.first = fi[d] >= 0x7F7F7F7F7F7F7F7Full ? NOPOS : fi[d];
-            if (p->rep_slot >= 0) {
-                HCell rc;
-                rc.kind = (uint32_t)rp[2 * (size_t)d];
-                rc.bits = rp[2 * (size_t)d + 1];
-                if (rc.kind == K_STR) rc.s = h.kbytes;
-                h.reps.push_back(rc);
+            h.first = mn[(size_t)d * P] == ABS64 ? NOPOS : mn[(size_t)d * P];
+            for (uint32_t r2 = 0; r2 < R; r2++) h.reps.push_back(dec(d, r2));
+            for (uint32_t i = 0; i < nmm; i++) {
+                const int a = p->mm[i];
+                const unsigned long long pos = ex[(size_t)d * nmm + i];
+                if (pos == ABS64) continue;
+                h.ext[a] = dec(d, R + i);
+                h.extpos[a] = pos;
+            }
+            for (uint32_t v = 0; v < NV; v++) {
+                const double nv = sm[(size_t)d * W + p->VS0 + 2 * v];
+                h.vla_ok[v] = nv > 0;
+                h.vla[v] = nv > 0 ? sqrt(vla[(size_t)d * NV + v] / nv) : 0.0;
             }
             groups.push_back(std::move(h));
             d++;
         }
-        if (!C.grouped && groups.size() > 1) throw HipError{"partials disagree on the single group"};
+        if (!Cp.grouped && groups.size() > 1) throw HipError{"partials disagree on the single group"};
         std::stable_sort(groups.begin(), groups.end(), [](const HGroup& x, const HGroup& y) { return x.first < y.first; });
-        Compiled C2 = C;
+        Compiled C2 = Cp;
         Literals L;
         parse_literals(c, C2.lits, L);
         g_stats.groups = groups.size();

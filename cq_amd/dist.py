@@ -105,52 +105,45 @@ def scan_partitioned(ast, table, comm_device: torch.device | str | None = None):
     return tp
 
 
+# cqgpu_coll ops (cqgpu.h)
+DONE, ALLGATHER, ALLREDUCE_MIN_I64, ALLREDUCE_SUM_F64, REDUCE_SUM_I64, REDUCE_SUM_F64, DECLINE = range(7)
+NOT_DENSE = object()
+
+
 class DensePartial:
     """This rank's device-resident partial groups (cqgpu_partial_*): the library
-    side of scan_partitioned_dense, kept behind four calls so the collective
-    choreography can be exercised on CPU with a stand-in (tests/test_dist_gloo.py)."""
-
-    KEYREC = 32
+    asks for one collective at a time (next), fills its payload (put) and takes
+    the result on the following next; kept behind these calls so the collective
+    loop can be exercised on CPU with a stand-in (tests/test_dist_gloo.py)."""
 
     def __init__(self, ast, table):
         import ctypes as C
         import cq_amd
-        self.C, self.L, self.ast = C, cq_amd.lib(), ast
+        self.C, self.L, self.ast, self.cq = C, cq_amd.lib(), ast, cq_amd
         arr = (C.c_void_p * 1)(table.handle.value)
         self.p = self.L.cqgpu_partial_new(ast, arr, 1)
-        w = C.c_uint32(0)
-        self.m = self.L.cqgpu_partial_keys(self.p, None, C.byref(w)) if self.p else 0
-        self.W = w.value
 
     @property
     def ok(self) -> bool:
         return bool(self.p)
 
-    def keys(self, device) -> torch.Tensor:
-        t = torch.empty(max(self.m * self.KEYREC, 1), dtype=torch.uint8, device=device)
-        if self.m:
-            self.L.cqgpu_partial_keys(self.p, t.data_ptr(), None)
-        return t[: self.m * self.KEYREC]
+    def next(self, result, sizes, rank, world):
+        """(op, count) of the next collective, after taking `result` (a device
+        tensor, or None) of the last one; `sizes`: per-rank byte counts of an ALLGATHER"""
+        C = self.C
+        c = self.cq.Coll()
+        arr = (C.c_uint64 * world)(*sizes) if sizes is not None else None
+        ptr = result.data_ptr() if result is not None and result.numel() else None
+        if self.L.cqgpu_partial_next(self.p, ptr, arr, rank, world, C.byref(c)) != 0:
+            raise RuntimeError(self.cq.last_error() or "cqgpu_partial_next failed")
+        return c.op, c.count
 
-    def dict(self, all_keys: torch.Tensor, nall: int, mine: int) -> int:
-        g = self.L.cqgpu_partial_dict(self.p, all_keys.data_ptr() if nall else None, nall, mine)
-        if g < 0:
-            import cq_amd
-            raise RuntimeError(cq_amd.last_error())
-        return int(g)
+    def put(self, buf):
+        if self.L.cqgpu_partial_put(self.p, buf.data_ptr() if buf.numel() else None) != 0:
+            raise RuntimeError(self.cq.last_error() or "cqgpu_partial_put failed")
 
-    def scatter(self, dsum, dfirst, drep):
-        if self.L.cqgpu_partial_scatter(self.p, dsum.data_ptr(), dfirst.data_ptr(), drep.data_ptr()) != 0:
-            import cq_amd
-            raise RuntimeError(cq_amd.last_error())
-
-    def mask_reps(self, dfirst, drep):
-        if self.L.cqgpu_partial_mask_reps(self.p, dfirst.data_ptr(), drep.data_ptr()) != 0:
-            import cq_amd
-            raise RuntimeError(cq_amd.last_error())
-
-    def finish(self, dsum, dfirst, drep):
-        return self.L.cqgpu_partial_finish(self.p, self.ast, dsum.data_ptr(), dfirst.data_ptr(), drep.data_ptr())
+    def result(self):
+        return self.L.cqgpu_partial_result(self.p, self.ast)
 
     def free(self):
         if self.p:
@@ -165,70 +158,75 @@ def _sync(device):
         torch.cuda.synchronize(d)
 
 
-def dense_merge(part, device, comm_device=None):
-    """The collective part of the device-side merge: one
-    all_gather of the key records (sizes first), the dictionary and dense arrays
-    on every rank, MIN all-reduce of first positions, SUM reduce of the dense sums
-    and representative cells to rank 0, where `part.finish` builds the result.
-    Returns that on rank 0, None elsewhere.  comm_device: where the collectives run
-    (the device for RCCL; "cpu" stages through host memory for a gloo group)."""
-    world, rank = dist.get_world_size(), dist.get_rank()
-    comm = torch.device(comm_device) if comm_device is not None else torch.device(device)
-    mine, err = _local(part.keys, device)
-    agree(err, comm)
-    n = torch.tensor([part.m], dtype=torch.int64, device=comm)
+def allgather_var(buf: torch.Tensor, comm) -> tuple[torch.Tensor, list[int]]:
+    """all_gather of a variable-length uint8 tensor: the ranks' payloads
+    concatenated in rank order, and their lengths"""
+    world = dist.get_world_size()
+    n = torch.tensor([buf.numel()], dtype=torch.int64, device=comm)
     sizes = [torch.zeros(1, dtype=torch.int64, device=comm) for _ in range(world)]
     dist.all_gather(sizes, n)
-    counts = [int(x.item()) for x in sizes]                  # a few integers, not the blobs
-    if sum(counts) >= DICT_MAX_KEYS:
-        return NOT_DENSE                                     # every rank sees the same total
-    kb = part.KEYREC
-    mx = max(max(counts), 1) * kb
-    buf = torch.zeros(mx, dtype=torch.uint8, device=comm)
-    buf[: mine.numel()] = mine.to(comm)
+    lens = [int(x.item()) for x in sizes]
+    mx = max(max(lens), 1)
+    pad = torch.zeros(mx, dtype=torch.uint8, device=comm)
+    pad[: buf.numel()] = buf.to(comm)
     outs = [torch.empty(mx, dtype=torch.uint8, device=comm) for _ in range(world)]
-    dist.all_gather(outs, buf)
-    all_keys = torch.cat([o[: c * kb] for o, c in zip(outs, counts)]).to(device)
-    nall, off = sum(counts), sum(counts[:rank])
-    _sync(device)          # the library's stream reads what torch's stream wrote
+    dist.all_gather(outs, pad)
+    return torch.cat([o[:k] for o, k in zip(outs, lens)]), lens
 
-    def local_dense():
-        g = part.dict(all_keys, nall, off)
-        ds = torch.empty(max(g * part.W, 1), dtype=torch.float64, device=device)
-        df = torch.empty(max(g, 1), dtype=torch.int64, device=device)
-        dr = torch.empty(max(2 * g, 1), dtype=torch.int64, device=device)
-        part.scatter(ds, df, dr)
-        return ds, df, dr
-    out, err = _local(local_dense)
-    agree(err, comm)
-    dsum, dfirst, drep = out
-    f = dfirst.to(comm)
-    dist.all_reduce(f, op=dist.ReduceOp.MIN)
-    dfirst.copy_(f)
-    _sync(device)
-    _, err = _local(part.mask_reps, dfirst, drep)
-    agree(err, comm)
-    s, r = dsum.to(comm), drep.to(comm)
-    dist.reduce(s, 0, op=dist.ReduceOp.SUM)
-    dist.reduce(r, 0, op=dist.ReduceOp.SUM)
+
+_DTYPES = {ALLGATHER: torch.uint8, ALLREDUCE_MIN_I64: torch.int64, ALLREDUCE_SUM_F64: torch.float64,
+           REDUCE_SUM_I64: torch.int64, REDUCE_SUM_F64: torch.float64}
+
+
+def dense_merge(part, device, comm_device=None):
+    """Run the collectives the library asks for: the key
+    all_gather, MIN all-reduces of positions and order keys, SUM reduces of the
+    dense planes and the owners' cells, over RCCL on device tensors (or gloo
+    through host memory with comm_device="cpu").  Returns cqgpu_partial_result on
+    rank 0, None elsewhere, NOT_DENSE when the library declines (every rank
+    declines together: the decision depends on the gathered keys only)."""
+    world, rank = dist.get_world_size(), dist.get_rank()
+    comm = torch.device(comm_device) if comm_device is not None else torch.device(device)
+    result, sizes = None, None
+    while True:
+        out, err = _local(part.next, result, sizes, rank, world)
+        agree(err, comm)
+        op, count = out
+        if op == DONE:
+            break
+        if op == DECLINE:
+            return NOT_DENSE
+        buf = torch.empty(max(count, 1), dtype=_DTYPES[op], device=device)[:count]
+        _, err = _local(part.put, buf)
+        agree(err, comm)
+        _sync(device)
+        sizes = None
+        if op == ALLGATHER:
+            result, sizes = allgather_var(buf, comm)
+        elif count == 0:                     # every rank has the same G: skip together
+            result = buf
+        else:
+            x = buf.to(comm)
+            if op == ALLREDUCE_MIN_I64:
+                dist.all_reduce(x, op=dist.ReduceOp.MIN)
+            elif op == ALLREDUCE_SUM_F64:
+                dist.all_reduce(x, op=dist.ReduceOp.SUM)
+            else:
+                dist.reduce(x, 0, op=dist.ReduceOp.SUM)
+            result = x
+        result = result.to(device)
+        _sync(device)
     if rank != 0:
         return None
-    dsum.copy_(s)
-    drep.copy_(r)
-    _sync(device)
-    return part.finish(dsum, dfirst, drep)
-
-
-DICT_MAX_KEYS = 1 << 29      # cqgpu_partial_dict's limit: more keys take the blob path
-NOT_DENSE = object()
+    return part.result()
 
 
 def scan_partitioned_dense(ast, table, comm_device=None):
     """One range-partitioned query step with the merge on the devices (config 4):
     this rank's scan keeps its groups in HBM (cqgpu_partial_new), the ranks agree
     on the path (a MIN all-reduce of "eligible"), and dense_merge reduces the
-    groups over RCCL.  Plans outside the dense path (MIN/MAX, plain columns other
-    than the group key, long text keys) take scan_partitioned's blobs."""
+    groups over RCCL.  Plans outside the dense path (MEDIAN, MIN/MAX over long
+    text, too many keys) take scan_partitioned's blobs."""
     import cq_amd
     device = torch.device("cuda", torch.cuda.current_device())
     comm = torch.device(comm_device) if comm_device is not None else device
@@ -245,7 +243,7 @@ def scan_partitioned_dense(ast, table, comm_device=None):
             part.free()
             return scan_partitioned(ast, table, comm_device)
         if dist.get_rank() == 0 and not tp:
-            raise RuntimeError(cq_amd.last_error() or "cqgpu_partial_finish failed")
+            raise RuntimeError(cq_amd.last_error() or "cqgpu_partial_result failed")
         return tp
     finally:
         part.free()

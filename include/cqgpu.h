@@ -98,29 +98,43 @@ cq_table* cqgpu_merge_partials(cq_node* query_ast, const void* const* blobs, con
                                int nblobs);
 
 /* ---- device-side merge of range-partitioned GROUP BY partials --------------
- *  for plans whose result is the group key with
- * COUNT / SUM / AVG (the config-3/4 shape; others use the blobs above):
- *   p = cqgpu_partial_new(q, tables, 1)           this rank's scan, groups kept on the device
- *   n = cqgpu_partial_keys(p, dst, &W)            n key records of 32 bytes, copied to dst (device; NULL: count only)
- *   all_gather the key records (RCCL), concatenated in rank order -> all, nall, mine = offset of ours
- *   G = cqgpu_partial_dict(p, all, nall, mine)    the global dictionary, identical on every rank
- *                                                 (copies `all`: the caller may free it on return;
- *                                                 nall >= 2^29 returns -1: take the blob path)
- *   cqgpu_partial_scatter(p, dsum, dfirst, drep)  dense arrays: double[G*W], int64[G] (absent:
- *                                                 0x7F7F...7F), int64[2G]
- *   all_reduce(dfirst, MIN); cqgpu_partial_mask_reps(p, dfirst, drep)
- *   reduce(dsum, SUM) and reduce(drep, SUM) to rank 0
- *   rank 0: r = cqgpu_partial_finish(p, q, dsum, dfirst, drep); every rank: cqgpu_partial_free(p)
- * All buffers are device memory.  new returns NULL (cqgpu_last_ineligible set)
- * for plans outside the dense path; dict returns -1 on error. */
+ * ("RCCL reduce for the final aggregate merge").  The
+ * library keeps this rank's partial groups on the device and asks the caller
+ * for one collective at a time; the sequence depends on the plan only, so every
+ * rank asks for the same ones:
+ *   p = cqgpu_partial_new(q, tables, 1)          this rank's scan (NULL + cqgpu_last_ineligible:
+ *                                                plan outside the dense path -> blobs above)
+ *   result = NULL, sizes = NULL
+ *   loop:
+ *     cqgpu_partial_next(p, result, sizes, rank, world, &c)   takes the last result, returns the next
+ *     c.op == CQGPU_COLL_DONE: stop;  CQGPU_COLL_DECLINE: too many keys, take the blob path
+ *     buf = device buffer of c.count elements (bytes for ALLGATHER, 8-byte words otherwise)
+ *     cqgpu_partial_put(p, buf)                   this rank's payload into buf
+ *     run c.op on buf (ALLGATHER: result = the ranks' payloads concatenated in rank
+ *     order, sizes = their byte counts; the reduces in place: result = buf)
+ *   rank 0: r = cqgpu_partial_result(p, q); every rank: cqgpu_partial_free(p)
+ * All buffers are device memory; the library copies what it keeps, so the caller
+ * may free `result` once next returns.  Returns 0 / -1 (cqgpu_last_error). */
 typedef struct cqgpu_partial cqgpu_partial;
+enum {
+    CQGPU_COLL_DONE = 0,
+    CQGPU_COLL_ALLGATHER = 1,          /* uint8, variable size per rank */
+    CQGPU_COLL_ALLREDUCE_MIN_I64 = 2,  /* int64 (signed) */
+    CQGPU_COLL_ALLREDUCE_SUM_F64 = 3,  /* double */
+    CQGPU_COLL_REDUCE_SUM_I64 = 4,     /* int64, to rank 0 */
+    CQGPU_COLL_REDUCE_SUM_F64 = 5,     /* double, to rank 0 */
+    CQGPU_COLL_DECLINE = 6
+};
+typedef struct {
+    int32_t op;
+    int32_t pad;
+    uint64_t count;
+} cqgpu_coll;
 cqgpu_partial* cqgpu_partial_new(cq_node* query_ast, cqgpu_table* const* tables, int ntables);
-size_t cqgpu_partial_keys(cqgpu_partial* p, void* dev_dst, uint32_t* words_per_group);
-long long cqgpu_partial_dict(cqgpu_partial* p, const void* dev_all, uint64_t nall, uint64_t mine);
-int cqgpu_partial_scatter(cqgpu_partial* p, double* dsum, unsigned long long* dfirst, unsigned long long* drep);
-int cqgpu_partial_mask_reps(cqgpu_partial* p, const unsigned long long* dfirst_global, unsigned long long* drep);
-cq_table* cqgpu_partial_finish(cqgpu_partial* p, cq_node* query_ast, const double* dsum,
-                               const unsigned long long* dfirst, const unsigned long long* drep);
+int cqgpu_partial_next(cqgpu_partial* p, const void* result, const uint64_t* result_sizes, int rank, int world,
+                       cqgpu_coll* next);
+int cqgpu_partial_put(cqgpu_partial* p, void* dev_dst);
+cq_table* cqgpu_partial_result(cqgpu_partial* p, cq_node* query_ast);
 void cqgpu_partial_free(cqgpu_partial* p);
 
 /* ---- join-key repartition for the multi-GPU JOIN ---

@@ -106,51 +106,77 @@ def test_exchange_gloo(world):
 # ---------------------------------------------------------------- dense merge choreography
 class _StandInPartial:
     """numpy stand-in for cq_amd.dist.DensePartial with the library's contract
-    (merge.hip): 32-byte key records, the dictionary numbers distinct keys by first
-    occurrence in the all-gathered concatenation, W dense words per group, first
-    positions MIN-reduced, representative cells kept only where the first row is"""
-    KEYREC = 32
-    W = 3
+    (cqgpu.h, cqgpu_partial_next): it asks for the key all_gather (8-byte count,
+    then 8-byte keys), numbers distinct keys by first occurrence in the
+    concatenation, asks for a MIN all-reduce of first positions, a SUM reduce of
+    the representative cells masked to the rank holding the first row, a SUM
+    reduce of the dense sums, and an all_gather of an (empty) side blob"""
+    STAGES = ["keys", "min", "cell", "sumr", "side"]
+    ABS = 0x7FFFFFFFFFFFFFFF
 
     def __init__(self, groups):
         import numpy as np
         self.np = np
         self.groups = groups                      # [(key int, cnt, sum, first, rep)]
-        self.m = len(groups)
+        self.at = 0
+        self.payload = None
 
-    def keys(self, device):
+    def next(self, result, sizes, rank, world):
+        np = self.np
+        if self.at > 0:
+            done = self.STAGES[self.at - 1]
+            r = result.cpu().numpy() if result is not None else None
+            if done == "keys":
+                assert sizes is not None and sum(sizes) == r.size
+                keys, o = [], 0
+                for sz in sizes:
+                    m = int(r[o:o + 8].view(np.int64)[0])
+                    keys += [int(x) for x in r[o + 8:o + 8 + 8 * m].view(np.int64)]
+                    o += sz
+                self.dense = {}
+                for k in keys:
+                    self.dense.setdefault(k, len(self.dense))
+                self.order = list(self.dense)
+                G = len(self.order)
+                self.sum = np.zeros(3 * G)
+                self.first = np.full(G, self.ABS, dtype=np.int64)
+                self.rep = np.zeros(G, dtype=np.int64)
+                for k, cnt, sm, first, rep in self.groups:
+                    d = self.dense[k]
+                    self.sum[3 * d:3 * d + 3] = (cnt, sm, cnt)
+                    self.first[d], self.rep[d] = first, rep
+                self.my_first = self.first.copy()
+            elif done == "min":
+                self.first = r.copy()
+            elif done == "cell":
+                self.rep = r.copy()
+            elif done == "sumr":
+                self.sum = r.copy()
+        if self.at == len(self.STAGES):
+            return 0, 0
+        st = self.STAGES[self.at]
+        self.at += 1
+        if st == "keys":
+            self.payload = np.array([len(self.groups)] + [g[0] for g in self.groups], dtype=np.int64).view(np.uint8)
+            return 1, self.payload.size
+        if st == "min":
+            self.payload = self.first
+            return 2, self.payload.size
+        if st == "cell":
+            self.payload = np.where(self.my_first == self.first, self.rep, 0)
+            return 4, self.payload.size
+        if st == "sumr":
+            self.payload = self.sum
+            return 5, self.payload.size
+        self.payload = np.zeros(0, dtype=np.uint8)
+        return 1, 0
+
+    def put(self, buf):
         import torch
-        rec = self.np.zeros((self.m, 4), dtype=self.np.uint64)
-        for j, g in enumerate(self.groups):
-            rec[j, 1] = g[0]
-        return torch.from_numpy(rec.view(self.np.uint8).reshape(-1).copy()).to(device)
+        buf.copy_(torch.from_numpy(self.payload.copy()))
 
-    def dict(self, all_keys, nall, mine):
-        keys = all_keys.cpu().numpy().view(self.np.uint64).reshape(nall, 4)[:, 1] if nall else []
-        self.dense = {}
-        for k in keys:
-            self.dense.setdefault(int(k), len(self.dense))
-        self.order = list(self.dense)
-        return len(self.dense)
-
-    def scatter(self, dsum, dfirst, drep):
-        dsum.zero_()
-        dfirst.fill_(0x7F7F7F7F7F7F7F7F)
-        drep.zero_()
-        for k, cnt, sm, first, rep in self.groups:
-            d = self.dense[k]
-            dsum[d * 3], dsum[d * 3 + 1], dsum[d * 3 + 2] = float(cnt), float(sm), float(cnt)
-            dfirst[d] = first
-            drep[2 * d], drep[2 * d + 1] = 1, rep
-        self.my_first = dfirst.clone()
-
-    def mask_reps(self, dfirst, drep):
-        for d in range(len(self.order)):
-            if int(self.my_first[d]) != int(dfirst[d]):
-                drep[2 * d] = drep[2 * d + 1] = 0
-
-    def finish(self, dsum, dfirst, drep):
-        rows = [(k, int(dsum[3 * d]), float(dsum[3 * d + 1]), int(dfirst[d]), int(drep[2 * d + 1]))
+    def result(self):
+        rows = [(k, int(self.sum[3 * d]), float(self.sum[3 * d + 1]), int(self.first[d]), int(self.rep[d]))
                 for d, k in enumerate(self.order)]
         return sorted(rows, key=lambda r: r[3])
 
@@ -183,8 +209,8 @@ def _dworker(rank, world, port, q):
 
 @pytest.mark.parametrize("world", [2, 3])
 def test_dense_merge_choreography_gloo(world):
-    """cq_amd.dist.dense_merge's collectives (sizes + key all_gather, MIN all_reduce
-    of first positions, SUM reduce of dense sums and masked reps) over gloo"""
+    """cq_amd.dist.dense_merge's collective loop (variable-size all_gathers, MIN
+    all_reduce, SUM reduces to rank 0, as the library asks for them) over gloo"""
     ctx = mp.get_context("spawn")
     q = ctx.Queue()
     port = _free_port()

@@ -169,3 +169,45 @@ def test_fast_not_for_other_shapes(d):
     assert st["scan_kernel"] != 2, st
     st = check(f"SELECT a, b FROM '{p}' WHERE b > 1", fast=False)
     assert st["scan_kernel"] != 2, st
+
+
+def test_plan_sample_misses(d):
+    """The plan (tag width, window stride, seeded keys) comes from the first 256 KiB.
+    A file whose keys grow past 16 bytes and whose records grow 10x only after that
+    must still give the oracle's answer: the records the chosen plan cannot take go
+    to slow_kernel (counted in stats), nothing is dropped."""
+    rng = np.random.default_rng(8)
+    rows = ["%d,k%d,%d.%d" % (rng.integers(0, 99), rng.integers(0, 20), rng.integers(0, 9), rng.integers(0, 9))
+            for _ in range(40_000)]                                   # ~0.5 MB of short records
+    rows += ["%d,%s,%d.%d" % (rng.integers(0, 99), "a_key_of_more_than_sixteen_bytes_%d" % (i % 30),
+                              rng.integers(0, 9), rng.integers(0, 9)) + ",pad" + "x" * int(rng.integers(100, 400))
+             for i in range(20_000)]                                  # late long keys, long records
+    p = _write(d / "drift.csv", "v,k,h", rows)
+    for sql in (f"SELECT k, COUNT(*), SUM(h), AVG(h) FROM '{p}' WHERE v > 30 GROUP BY k",
+                f"SELECT COUNT(*), SUM(h) FROM '{p}' WHERE v < 50"):
+        want, unsup = cqtest.oracle_query(sql)
+        assert not unsup
+        got, st, inel = _run(sql, 0)
+        assert not inel, inel
+        _cmp(got, want, _tol(sql), "drift: " + sql)
+    assert st["records"] == 60_000, st
+
+
+def test_slow_list_overflow_rescan(d, monkeypatch):
+    """more slow records than the slow list holds (CQGPU_SLOW_CAP shrinks it from
+    2^20 to 512): the scan reruns in byte-range chunks and still equals the oracle"""
+    rng = np.random.default_rng(9)
+    rows = []
+    for i in range(30_000):
+        a = '"q,%d"' % (i % 11) if i % 3 == 0 else "p%d" % (i % 11)      # a third quoted: slow records
+        rows.append("%s,%d,%d.%d" % (a, rng.integers(0, 99), rng.integers(0, 9), rng.integers(0, 9)))
+    p = _write(d / "slowcap.csv", "a,b,c", rows)
+    monkeypatch.setenv("CQGPU_SLOW_CAP", "512")
+    for sql in (f"SELECT a, COUNT(*), SUM(c) FROM '{p}' WHERE b > 20 GROUP BY a",
+                f"SELECT COUNT(*), AVG(c) FROM '{p}'"):
+        want, unsup = cqtest.oracle_query(sql)
+        assert not unsup
+        got, st, inel = _run(sql, 0)
+        assert not inel, inel
+        _cmp(got, want, _tol(sql), "slow cap: " + sql)
+        assert st["slow_records"] > 512, st

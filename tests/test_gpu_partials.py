@@ -121,44 +121,83 @@ def test_more_ranks_than_records(tmp_path):
 
 
 # ---------------------------------------------------------------- device-side dense merge
-def _dense_merge_by_hand(ast, tabs):
-    """cqgpu_partial_* over simulated ranks in one process: the all_gather is a
-    concatenation, the reduces are torch reductions over the ranks' dense arrays"""
+# (queries keep at most 4 SELECT items: the reference parser corrupts its heap on more,
+# SURVEY appendix A Q13 -- the parse itself, before any evaluation)
+def _collectives_by_hand(parts):
+    """cqgpu_partial_next / put over simulated ranks in one process: an all_gather
+    is a concatenation, the reduces are torch reductions over the ranks' buffers
+    (a reduce to rank 0 leaves the other ranks' buffers as they were)"""
     import torch
+    from cq_amd import dist as D
+    n = len(parts)
+    results, sizes = [None] * n, None
+    while True:
+        colls = [p.next(results[r], sizes, r, n) for r, p in enumerate(parts)]
+        ops = {op for op, _ in colls}
+        assert len(ops) == 1, colls                 # every rank asks for the same collective
+        op = ops.pop()
+        if op == D.DONE:
+            return parts[0].result()
+        if op == D.DECLINE:
+            return None
+        bufs = []
+        for (o, cnt), p in zip(colls, parts):
+            b = torch.empty(max(cnt, 1), dtype=D._DTYPES[op], device="cuda")[:cnt]
+            p.put(b)
+            bufs.append(b)
+        torch.cuda.synchronize()
+        sizes = None
+        if op == D.ALLGATHER:
+            cat = torch.cat(bufs)
+            sizes = [b.numel() for b in bufs]
+            results = [cat] * n
+        else:
+            assert len({b.numel() for b in bufs}) == 1
+            st = torch.stack(bufs)
+            red = st.min(0).values if op == D.ALLREDUCE_MIN_I64 else st.sum(0)
+            if op in (D.ALLREDUCE_MIN_I64, D.ALLREDUCE_SUM_F64):
+                results = [red] * n
+            else:
+                results = [red] + bufs[1:]
+        torch.cuda.synchronize()
+
+
+def _dense_merge_by_hand(ast, tabs):
     from cq_amd.dist import DensePartial
     parts = [DensePartial(ast, t) for t in tabs]
     try:
         if not all(p.ok for p in parts):
             return None
-        keys = [p.keys("cuda") for p in parts]
-        counts = [p.m for p in parts]
-        all_keys = torch.cat(keys) if sum(counts) else torch.empty(1, dtype=torch.uint8, device="cuda")
-        torch.cuda.synchronize()
-        dense = []
-        for r, p in enumerate(parts):
-            g = p.dict(all_keys, sum(counts), sum(counts[:r]))
-            ds = torch.empty(max(g * p.W, 1), dtype=torch.float64, device="cuda")
-            df = torch.empty(max(g, 1), dtype=torch.int64, device="cuda")
-            dr = torch.empty(max(2 * g, 1), dtype=torch.int64, device="cuda")
-            p.scatter(ds, df, dr)
-            dense.append((g, ds, df, dr))
-        assert len({g for g, _, _, _ in dense}) == 1            # one dictionary on every rank
-        fmin = torch.stack([d[2] for d in dense]).min(0).values
-        for d in dense:
-            d[2].copy_(fmin)
-        torch.cuda.synchronize()
-        for p, d in zip(parts, dense):
-            p.mask_reps(d[2], d[3])
-        ssum = torch.stack([d[1] for d in dense]).sum(0)
-        rsum = torch.stack([d[3] for d in dense]).sum(0)
-        torch.cuda.synchronize()
-        return parts[0].finish(ssum, fmin, rsum)
+        return _collectives_by_hand(parts)
     finally:
         for p in parts:
             p.free()
 
 
-DENSE = [q for q in QUERIES if "MIN(" not in q and "MAX(" not in q and "SELECT name" not in q]
+def _dense(ast, path, nranks):
+    tabs = [cq_amd.Table.open_range(path, r, nranks) for r in range(nranks)]
+    try:
+        tp = _dense_merge_by_hand(ast, tabs)
+    finally:
+        for t in tabs:
+            t.close()
+    assert tp, cq_amd.last_error() or cq_amd.last_ineligible()
+    got = abi.table_to_py(tp)
+    cq_amd.result_free(tp)
+    return got
+
+
+DENSE = QUERIES + [
+    "SELECT role, MIN(height), MAX(age), STDDEV(height) FROM '{p}' WHERE age > 30 GROUP BY role",
+    "SELECT gender, role, COUNT(*), AVG(age) FROM '{p}' WHERE height > 1.8 GROUP BY gender, role",
+    "SELECT name, surname, COUNT(*), MAX(height) FROM '{p}' WHERE age < 22 GROUP BY role",
+    "SELECT age / 10 AS decade, COUNT(*), MIN(surname), MAX(role) FROM '{p}' GROUP BY decade",
+    "SELECT role, height * 100 AS hc, COUNT(*) FROM '{p}' GROUP BY role HAVING COUNT(*) > 100 "
+    "ORDER BY role DESC LIMIT 7",
+    "SELECT role, age + 1 AS a1, name, COUNT(*) FROM '{p}' WHERE age > 50 GROUP BY role",
+    "SELECT STDDEV(age), STDDEV(height), MIN(gender), MAX(surname) FROM '{p}'",
+    "SELECT role, MIN(name), MAX(name), COUNT(*) FROM '{p}' WHERE age > 60 GROUP BY role",
+]
 
 
 @pytest.mark.parametrize("sql", DENSE)
@@ -169,17 +208,22 @@ def test_dense_merge_equals_oracle(files, sql, nranks):
     want, unsup = cqtest.oracle_query(q)
     assert not unsup and want is not None
     with cqtest.Parsed(q) as ast:
-        tabs = [cq_amd.Table.open_range(path, r, nranks) for r in range(nranks)]
-        try:
-            tp = _dense_merge_by_hand(ast, tabs)
-        finally:
-            for t in tabs:
-                t.close()
-        assert tp, cq_amd.last_error() or cq_amd.last_ineligible()
-        got = abi.table_to_py(tp)
-        cq_amd.result_free(tp)
+        got = _dense(ast, path, nranks)
         tol = tolerant_columns(ast)
     compare(got, want, tol, f"dense {nranks} ranks: {q}")
+
+
+def test_dense_merge_mixed_terminators(files):
+    path = files["mixed"]
+    for sql in DENSE[:3] + DENSE[6:9]:
+        q = sql.format(p=path)
+        want, unsup = cqtest.oracle_query(q)
+        assert not unsup and want is not None
+        for n in (2, 5):
+            with cqtest.Parsed(q) as ast:
+                got = _dense(ast, path, n)
+                tol = tolerant_columns(ast)
+            compare(got, want, tol, f"dense {n} ranks: {q}")
 
 
 def test_dense_merge_typed_keys(tmp_path):
@@ -191,73 +235,94 @@ def test_dense_merge_typed_keys(tmp_path):
         rows.append(f"{vals[(i * 5) % len(vals)]},{i % 13}")
     p = tmp_path / "typed.csv"
     p.write_text("\n".join(rows) + "\n")
-    q = f"SELECT k, COUNT(*), SUM(v), AVG(v) FROM '{p}' GROUP BY k"
-    want, _ = cqtest.oracle_query(q)
-    for n in (2, 5):
-        with cqtest.Parsed(q) as ast:
-            tabs = [cq_amd.Table.open_range(str(p), r, n) for r in range(n)]
-            tp = _dense_merge_by_hand(ast, tabs)
-            for t in tabs:
-                t.close()
-            got = abi.table_to_py(tp)
-            cq_amd.result_free(tp)
-            tol = tolerant_columns(ast)
-        compare(got, want, tol, f"dense typed keys, {n} ranks")
+    for q in (f"SELECT k, COUNT(*), SUM(v), AVG(v) FROM '{p}' GROUP BY k",
+              f"SELECT k, MIN(v), MAX(k) FROM '{p}' GROUP BY k"):
+        want, _ = cqtest.oracle_query(q)
+        for n in (2, 5):
+            with cqtest.Parsed(q) as ast:
+                got = _dense(ast, str(p), n)
+                tol = tolerant_columns(ast)
+            compare(got, want, tol, f"dense typed keys, {n} ranks: {q}")
+
+
+def test_dense_merge_long_text(tmp_path):
+    """group keys over 16 bytes (gathered with their bytes, compared exactly) and
+    representative / extreme texts over 8 bytes (the owners' side gather)"""
+    rng = random.Random(9)
+    rows = ["k,name,v"]
+    keys = [f"a_group_key_longer_than_sixteen_{i:03d}" for i in range(40)] + ["short", "mid_len_key_1234"]
+    for i in range(12000):
+        k = keys[rng.randrange(len(keys))]
+        rows.append(f"{k},person_{rng.randrange(10**6)}_{'x' * rng.randrange(0, 12)},{rng.randrange(-50, 50)}")
+    p = tmp_path / "long.csv"
+    p.write_text("\n".join(rows) + "\n")
+    for sql in (f"SELECT k, name, COUNT(*), SUM(v) FROM '{p}' GROUP BY k",
+                f"SELECT k, MIN(v), MAX(v) FROM '{p}' WHERE v < 40 GROUP BY k",
+                f"SELECT k, COUNT(*), STDDEV(v) FROM '{p}' WHERE v > 0 GROUP BY k ORDER BY k"):
+        want, _ = cqtest.oracle_query(sql)
+        for n in (1, 3, 8):
+            with cqtest.Parsed(sql) as ast:
+                got = _dense(ast, str(p), n)
+                tol = tolerant_columns(ast)
+            compare(got, want, tol, f"dense long text, {n} ranks: {sql}")
+
+
+def test_dense_merge_mixed_classes(mixed_classes):
+    for sql in ("SELECT g, MIN(v), MAX(v), COUNT(*) FROM '{p}' GROUP BY g",
+                "SELECT MIN(v), MAX(v) FROM '{p}'"):
+        q = sql.format(p=mixed_classes)
+        want, _ = cqtest.oracle_query(q)
+        for n in (1, 2, 3, 5, 8):
+            with cqtest.Parsed(q) as ast:
+                got = _dense(ast, mixed_classes, n)
+                tol = tolerant_columns(ast)
+            compare(got, want, tol, f"dense mixed classes, {n} ranks: {q}")
 
 
 def test_dict_build_high_contention(tmp_path):
     """dict_build_kernel's relaxed publish (memory model) under
-    contention: one rank's 1,000 keys, then 63 more copies of them with each key's
-    copies adjacent (63,000 inserts of the same 1,000 keys from every CU, lanes of a
-    wave racing for one slot) must build exactly the 1,000-entry dictionary, and the
-    merge through it must equal the oracle's answer"""
-    import torch
-    from cq_amd.dist import DensePartial
+    contention: 64 simulated ranks holding the same 1,000 keys (64,000 inserts of
+    the same keys from every CU, lanes of a wave racing for one slot) must build
+    exactly the 1,000-entry dictionary: COUNT and SUM come out 64 times the oracle's,
+    AVG equal, groups in the same order"""
     p = tmp_path / "role.csv"
     datagen.write_shape_a(str(p), 60_000, seed=31, with_role=True)
-    q = f"SELECT role, COUNT(*), SUM(height), AVG(height) FROM '{p}' GROUP BY role"
+    q = f"SELECT COUNT(*), SUM(height), AVG(height) FROM '{p}' GROUP BY role"
     want, unsup = cqtest.oracle_query(q)
-    assert not unsup
+    assert not unsup and len(want["rows"]) == 1000
+    from cq_amd.dist import DensePartial
     with cqtest.Parsed(q) as ast:
         t = cq_amd.Table.open_range(str(p), 0, 1)
-        part = DensePartial(ast, t)
+        parts = [DensePartial(ast, t) for _ in range(64)]
         try:
-            assert part.ok, cq_amd.last_ineligible()
-            m = part.m
-            assert m == len(want["rows"]) == 1000
-            keys = part.keys("cuda").view(m, DensePartial.KEYREC)
-            dups = keys.unsqueeze(1).expand(m, 63, DensePartial.KEYREC).reshape(-1)
-            all_keys = torch.cat([keys.reshape(-1), dups]).contiguous()
-            torch.cuda.synchronize()
-            for _ in range(3):
-                g = part.dict(all_keys, 64 * m, 0)
-                assert g == m
-            ds = torch.empty(g * part.W, dtype=torch.float64, device="cuda")
-            df = torch.empty(g, dtype=torch.int64, device="cuda")
-            dr = torch.empty(2 * g, dtype=torch.int64, device="cuda")
-            part.scatter(ds, df, dr)
-            part.mask_reps(df, dr)
-            torch.cuda.synchronize()
-            tp = part.finish(ds, df, dr)
+            assert all(x.ok for x in parts), cq_amd.last_ineligible()
+            tp = _collectives_by_hand(parts)
             assert tp, cq_amd.last_error()
             got = abi.table_to_py(tp)
             cq_amd.result_free(tp)
-            tol = tolerant_columns(ast)
         finally:
+            for x in parts:
+                x.free()
+            t.close()
+    assert len(got["rows"]) == 1000
+    for g, w in zip(got["rows"], want["rows"]):
+        assert g[0] == ("I", 64 * w[0][1])
+        assert cqtest.cell_equal(g[1], ("D", 64 * w[1][1]), 1e-9)
+        assert cqtest.cell_equal(g[2], w[2], 1e-9)
+
+
+def test_dense_merge_refusals(files):
+    """MEDIAN needs every value: it leaves the dense path (the blob merge takes it)"""
+    from cq_amd.dist import DensePartial
+    for sql, why in (("SELECT role, MEDIAN(age) FROM '{p}' GROUP BY role", "MEDIAN"),):
+        q = sql.format(p=files["plain"])
+        with cqtest.Parsed(q) as ast:
+            t = cq_amd.Table.open_range(files["plain"], 0, 2)
+            part = DensePartial(ast, t)
+            ok = part.ok
             part.free()
             t.close()
-    compare(got, want, tol, "dictionary under contention")
-
-
-def test_dense_merge_refuses_minmax(files):
-    q = QUERIES[2].format(p=files["plain"])
-    with cqtest.Parsed(q) as ast:
-        t = cq_amd.Table.open_range(files["plain"], 0, 2)
-        from cq_amd.dist import DensePartial
-        part = DensePartial(ast, t)
-        assert not part.ok and "dense merge" in cq_amd.last_ineligible()
-        part.free()
-        t.close()
+        assert not ok and why in cq_amd.last_ineligible(), (sql, cq_amd.last_ineligible())
 
 
 # ---------------------------------------------------------------- row-returning SELECT across ranges
