@@ -1312,11 +1312,14 @@ __global__ __launch_bounds__(256) void raw_merge_kernel(ScanStats* __restrict__ 
     if (gi < 0) return;
     atomicAdd(&gt.cnt[gi], rt.cnt[i]);
     atomicMin(&gt.first[gi], rt.first[i]);
-    for (int a = 0; a < nacc; a++) {
+    rt.cnt[i] = 0;                    // consumed: a chunked rescan merges each chunk's
+    for (int a = 0; a < nacc; a++) {  // raw state once (first offsets merge by MIN)
         const unsigned long long n = rt.num[a][i];
         if (n) {
             atomicAdd(&gt.sum[a][gi], rt.sum[a][i]);
             atomicAdd(&gt.num[a][gi], n);
+            rt.sum[a][i] = 0;
+            rt.num[a][i] = 0;
         }
     }
 }
