@@ -3225,7 +3225,6 @@ cq_table* run_join(DevCtx& c, cq_node* q, const cqgpu_table* L, const cqgpu_tabl
     RowPlan RP;
     if (rows) compile_rows(&J, q, C, RP);
     else compile_aggregate(&J, q, C);
-    if (part)
     if (!part && !rows && nj == 1 && lv[0].keyed && !lv[0].outer_left && !lv[0].outer_right) {
         cq_table* fj = run_fast_join(c, q, C, L, lv[0].R, lv[0].kl, lv[0].kr, lv[0].nleft);
         if (fj) return fj;
