@@ -109,6 +109,9 @@ hipError_t cq_launch_join_finish(const cq::GroupOut* out, const unsigned int* co
                                  const uint2* pairs, const cq::JoinMap* M, const cq::Cell* L, const cq::Cell* R,
                                  int nacc, uint32_t sb, cq::Cell* cells, uint8_t* bytes, hipStream_t s);
 size_t cq_join_sum_lds(int nacc);
+hipError_t cq_launch_comp_verify(const uint2* pairs, unsigned long long np, const cq::JoinMap* M, const cq::Cell* L,
+                                 const cq::Cell* R, const cq::ScanPlan* P, const cq::GroupTable* gt, unsigned int* bad,
+                                 hipStream_t s);
 hipError_t cq_launch_join_sum(const uint2* pairs, unsigned long long np, const cq::JoinMap* M, const cq::Cell* L,
                               const cq::Cell* R, const cq::ScanPlan* P, const cq::GroupTable* gt,
                               cq::ScanStats* stats, int ncu, hipStream_t s);
@@ -1071,6 +1074,7 @@ void compile_aggregate(const cqgpu_table* t, cq_node* q, Compiled& C) {
             // -- no table-prefix fallback on this path (evaluator.c:152), a missing
             // column is the part "NULL"
             C.P.ngpart = nk;
+            if (const char* e = getenv("CQGPU_TEST_DIGEST_BITS")) C.P.test_digest_bits = (uint32_t)std::min(atoi(e), 63);
             for (int g = 0; g < nk; g++) {
                 C.P.gcode_off[g] = (uint16_t)cc.code.size();
                 if (gexpr[g]) {
@@ -2739,11 +2743,19 @@ std::vector<HGroup> aggregate_pairs(DevCtx& c, Compiled& C, const JoinMap& MA, c
         else
             HIPCHECK(cq_launch_join_agg(pairs, np, &MA, Lc, Rc, &C.P, &Ar.gt, Ar.stats, grouped, c.stream));
         HIPCHECK(hipEventRecord(c.ev1, c.stream));
+        // composite keys: every pair's parts against its group's first pair's parts
+        const bool verify = grouped && C.P.ngpart > 1;
+        DevBuf vbad(64);
+        if (verify) {
+            HIPCHECK(hipMemsetAsync(vbad.p, 0, 4, c.stream));
+            HIPCHECK(cq_launch_comp_verify(pairs, np, &MA, Lc, Rc, &C.P, &Ar.gt, vbad.as<unsigned int>(), c.stream));
+        }
         HIPCHECK(cq_launch_compact(&Ar.gt, &C.P, Ar.out, Ar.out_count, cap_out, c.stream));
         HIPCHECK(cq_launch_join_finish(Ar.out, Ar.out_count, cap_out, pairs, &MR, Lc, Rc, C.P.nacc, SB, dcells, dbytes,
                                        c.stream));
-        unsigned int ng = 0;
+        unsigned int ng = 0, bad = 0;
         HIPCHECK(hipMemcpyAsync(&ng, Ar.out_count, 4, hipMemcpyDeviceToHost, c.stream));
+        if (verify) HIPCHECK(hipMemcpyAsync(&bad, vbad.p, 4, hipMemcpyDeviceToHost, c.stream));
         HIPCHECK(hipMemcpyAsync(&st, Ar.stats, sizeof st, hipMemcpyDeviceToHost, c.stream));
         HIPCHECK(hipStreamSynchronize(c.stream));
         float ms = 0;
@@ -2755,6 +2767,7 @@ std::vector<HGroup> aggregate_pairs(DevCtx& c, Compiled& C, const JoinMap& MA, c
             cap *= 8;
             continue;
         }
+        if (bad) throw HipError{"composite GROUP BY: two different part lists share a 128-bit key digest"};
         ng = std::min(ng, cap_out);
         outs.resize(ng);
         fcells.resize((size_t)ng * ncell);

@@ -247,7 +247,12 @@ struct Num {
 template <bool DOT>
 __device__ __forceinline__ Num num4(uint32_t d, uint32_t len) {
     Num r;
-    const uint32_t sh = 32u - 8u * len;
+    // (32 - 8 len) mod 32: LLVM folds it into 24 * len, a full-width v_mul_lo_u32
+    uint32_t l8 = len << 3;
+#ifndef FAST_OLD_SH
+    asm volatile("" : "+v"(l8));
+#endif
+    const uint32_t sh = 32u - l8;
     uint32_t v = (d ^ 0x30303030u) << (sh & 31);
     r.dot = false;
     r.k = 0;
@@ -447,9 +452,44 @@ __global__ __launch_bounds__(LT) void fast_kernel(const uint8_t* __restrict__ g,
     // window i (0 .. nwin - 1) of the range: file window first_win + i
     const uint32_t lane_lds = vreg(wlds + (uint32_t)lane * LB);   // the LDS address of the lane's bytes
     uint32_t i = blockIdx.x * NWV + wv;
+#ifdef FAST_PF_PLAIN
+#define FAST_PFLOAD(p) (*(p))
+#else
+#define FAST_PFLOAD(p) __builtin_nontemporal_load(p)
+#endif
+#ifdef FAST_REGPF
+    // register prefetch: lane l's 64 bytes of the NEXT window are loaded into VGPRs
+    // while this window is processed (a whole window of work hides the load), then
+    // stored to the wave's LDS bytes for the record pass
+    v4u nx[4];
+    const v4u* gl = (const v4u*)(g + (size_t)lane * LB);
+    if (i < nwin) {
+        const v4u* a = (const v4u*)((const uint8_t*)gl + (first_win + i) * wsb);
+#pragma unroll
+        for (int k = 0; k < 4; k++) nx[k] = FAST_PFLOAD(a + k);
+        prev_next = *(const uint32_t*)(g + (first_win + i) * wsb - 4);
+    }
+#else
     if (i < nwin) load_win(g, first_win + i, wsb, wlds, voff, prev_next);
+#endif
     for (uint32_t round = 0; i < nwin; round++, i += wstep) {
         const uint32_t fcw = (round << 16) | ((uint32_t)wv << 12);   // first-row code of this window
+#ifdef FAST_REGPF
+        v4u la[4];
+#pragma unroll
+        for (int k = 0; k < 4; k++) {
+            la[k] = nx[k];
+            ((v4u*)W.bytes)[4 * lane + k] = la[k];
+        }
+        const uint32_t prevw = prev_next;
+        if (i + wstep < nwin) {
+            const v4u* a = (const v4u*)((const uint8_t*)gl + (first_win + i + wstep) * wsb);
+#pragma unroll
+            for (int k = 0; k < 4; k++) nx[k] = FAST_PFLOAD(a + k);
+            prev_next = *(const uint32_t*)(g + (first_win + i + wstep) * wsb - 4);
+        }
+#define FAST_ISSUE() do {} while (0)
+#else
         asm volatile("s_waitcnt vmcnt(0)" ::: "memory");   // the window's bytes are in LDS
         const uint32_t prevw = prev_next;
         bool issued = false;
@@ -467,6 +507,7 @@ __global__ __launch_bounds__(LT) void fast_kernel(const uint8_t* __restrict__ g,
         v4u la[4];
 #pragma unroll
         for (int i = 0; i < 4; i++) la[i] = ((const v4u*)W.bytes)[4 * lane + i];
+#endif
         uint32_t sep0, nl0, sep1, nl1, qf = 0;
         classify32<COMMA>(la[0], la[1], ck, sep0, nl0, qf);
         classify32<COMMA>(la[2], la[3], ck, sep1, nl1, qf);

@@ -74,6 +74,7 @@ struct ScanPlan {
     uint32_t lean_ws;      // lean_kernel window stride (0: the largest, lean::WS)
     uint32_t lean_k16;     // lean_kernel GROUP BY tags of 16 key bytes (the column's sampled fields exceed 8)
     uint64_t fast_seed;    // fast_kernel: device address of the GROUP BY column's seeded LDS tags (0: none)
+    uint32_t test_digest_bits;   // test knob CQGPU_TEST_DIGEST_BITS: composite digests cut to this many bits (0: all 128)
 };
 
 // projection of a row-returning SELECT (device pointers): ncols CSV columns

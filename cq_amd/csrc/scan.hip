@@ -1253,7 +1253,12 @@ __device__ GKey plan_group_key(const ScanPlan& P, const Cell* kc, const CellsT<N
         tab = tab || !ok;
         return joined_text_key(h, (uint32_t)P.ngpart);
     }
-    return comp_key(ck, (uint32_t)P.ngpart);
+    GKey k = comp_key(ck, (uint32_t)P.ngpart);
+    if (P.test_digest_bits) {                          // test knob: force digest collisions
+        k.w0 &= (1ULL << P.test_digest_bits) - 1;
+        k.w1 = 0;
+    }
+    return k;
 }
 
 // ------------------------------------------------------------------ projection
@@ -1802,6 +1807,62 @@ __device__ __forceinline__ void join_cells(const JoinMap& M, const Cell* L, cons
             if (row != JOIN_NONE)
                 cs.c[k] = M.side[k] ? R[(uint64_t)row * M.rstride + M.col[k]] : L[(uint64_t)row * M.lstride + M.col[k]];
         }
+    }
+}
+
+// Exactness of composite GROUP BY keys (evaluator.c:113-212 groups by the parts' key
+// texts joined with '\t'; the kernels key such groups by a 128-bit digest of the
+// parts).  After the aggregation every passing pair looks its digest up and compares
+// its parts, one by one under the canonical key equality, with the parts of its
+// group's first pair: a digest shared by two different part lists (a collision)
+// sets *bad and the host fails the query instead of merging them.  Joined-text keys
+// (a part holding a tab, COMPT_FLAG) are not re-checked here.
+static __device__ int g_find(const GroupTable& gt, const GKey k, uint64_t h) {
+    const uint32_t tg = tag_of(h), mask = gt.cap - 1;
+    for (uint32_t probe = 0; probe < gt.cap; probe++) {
+        const uint32_t i = (uint32_t)(h + probe) & mask;
+        const uint32_t t = gt.tag[i];
+        if (t == 0) return -1;
+        if (t != tg) continue;
+        GKey o;
+        const uint32_t ocl = gt.clslen[i];
+        o.cls = ocl >> 16;
+        o.len = ocl & 0xffff;
+        o.w0 = gt.w0[i];
+        o.w1 = gt.w1[i];
+        if (gk_equal(o, k)) return (int)i;
+    }
+    return -1;
+}
+__global__ __launch_bounds__(256) void comp_verify_kernel(const uint2* __restrict__ pairs, unsigned long long np,
+                                                          JoinMap M, const Cell* __restrict__ L,
+                                                          const Cell* __restrict__ R, unsigned int* __restrict__ bad) {
+    const ScanPlan& P = c_plan;
+    const GroupTable& gt = c_gt;
+    const int nneed = P.nneed;
+    for (unsigned long long i = (unsigned long long)blockIdx.x * blockDim.x + threadIdx.x; i < np;
+         i += (unsigned long long)gridDim.x * blockDim.x) {
+        CellsT<MAX_NEED> cs;
+        join_cells(M, L, R, pairs[i], cs);
+        if (P.nprog != 0 && !eval_where_vm(P, P.consts, cs)) continue;
+        bool tab = false;
+        const GKey key = plan_group_key(P, P.consts, cs, nneed, tab);
+        if (key.cls != GK_COMP || (key.len & COMPT_FLAG)) continue;
+        const int gi = g_find(gt, key, gk_hash(key));
+        if (gi < 0) { atomicOr(bad, 2u); continue; }
+        const unsigned long long f = gt.first[gi];
+        if (f == i) continue;
+        if (f >= np) { atomicOr(bad, 2u); continue; }
+        CellsT<MAX_NEED> cf;
+        join_cells(M, L, R, pairs[f], cf);
+        bool same = true;
+        for (int k = 0; k < MAX_GPART; k++) {
+            if (k >= P.ngpart) break;
+            const GKey a = group_key(plan_group_part(P, P.consts, cs, nneed, k));
+            const GKey b = group_key(plan_group_part(P, P.consts, cf, nneed, k));
+            same = same && gk_equal(a, b);
+        }
+        if (!same) atomicOr(bad, 1u);
     }
 }
 
@@ -2673,6 +2734,16 @@ hipError_t cq_launch_join_agg(const uint2* pairs, unsigned long long np, const c
     if (e != hipSuccess || !np) return e;
     const unsigned grid = (unsigned)std::min<uint64_t>(grid_of(np, 256), 4096);
     hipLaunchKernelGGL(cq::join_agg_kernel, dim3(grid), dim3(256), 0, s, pairs, np, *M, L, R, stats, grouped);
+    return hipGetLastError();
+}
+hipError_t cq_launch_comp_verify(const uint2* pairs, unsigned long long np, const cq::JoinMap* M, const cq::Cell* L,
+                                 const cq::Cell* R, const cq::ScanPlan* P, const cq::GroupTable* gt, unsigned int* bad,
+                                 hipStream_t s) {
+    hipError_t e = cq::upload_symbol((const void*)&HIP_SYMBOL(cq::c_plan), P, sizeof *P, s);
+    if (e == hipSuccess) e = cq::upload_symbol((const void*)&HIP_SYMBOL(cq::c_gt), gt, sizeof *gt, s);
+    if (e != hipSuccess || !np) return e;
+    const unsigned grid = (unsigned)std::min<uint64_t>(grid_of(np, 256), 4096);
+    hipLaunchKernelGGL(cq::comp_verify_kernel, dim3(grid), dim3(256), 0, s, pairs, np, *M, L, R, bad);
     return hipGetLastError();
 }
 size_t cq_join_sum_lds(int nacc) { return (size_t)cq::JS_SLOTS * (32 + 12 * (size_t)nacc); }

@@ -181,3 +181,24 @@ def test_mixed_class_min_max(tmp_path):
             got = cq_amd.evaluate(ast)
         assert not cq_amd.last_ineligible(), (sql, cq_amd.last_ineligible())
         compare(got, want, set(), sql)
+
+
+def test_composite_digest_collision_fails_loudly(synth, monkeypatch):
+    """Composite keys are grouped by a 128-bit digest of the parts; every passing
+    row's parts are then checked against its group's first row's parts
+    (evaluator.c:113-212 groups by the exact joined key text).  The test knob
+    CQGPU_TEST_DIGEST_BITS cuts the digest to 2 bits, so different part lists must
+    collide: the query has to fail with the collision named, never merge them.
+    Full digests on the same query: exact against the oracle."""
+    sql = f"SELECT role, gender, COUNT(*) FROM '{synth}' GROUP BY role, gender"
+    monkeypatch.setenv("CQGPU_TEST_DIGEST_BITS", "2")
+    with cqtest.Parsed(sql) as ast:
+        got = cq_amd.evaluate(ast)
+    assert got is None
+    assert "digest" in cq_amd.last_error(), cq_amd.last_error()
+    monkeypatch.delenv("CQGPU_TEST_DIGEST_BITS")
+    want, _ = cqtest.oracle_query(sql)
+    with cqtest.Parsed(sql) as ast:
+        got = cq_amd.evaluate(ast)
+        tol = tolerant_columns(ast)
+    compare(got, want, tol, sql)
