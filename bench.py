@@ -198,7 +198,9 @@ def main():
     torch.cuda.set_device(local)
     torch.zeros(1, device="cuda")
     dist = None
-    if world > 1:
+    # CQ_BENCH_FORCE_DIST=1 under torchrun: the N > 1 step (range partial + dense RCCL
+    # merge) even at world size 1, so one-GPU boxes exercise the collective path
+    if world > 1 or (os.environ.get("CQ_BENCH_FORCE_DIST") and "WORLD_SIZE" in os.environ):
         import torch.distributed as dist
         dist.init_process_group("nccl", device_id=torch.device("cuda", local))
 

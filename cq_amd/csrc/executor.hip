@@ -161,6 +161,8 @@ hipError_t cq_jx_probe(int grouped, int value, int direct, const unsigned long l
                        const void* table, uint64_t tcap, const unsigned long long* bpay, const uint32_t* boff,
                        const cq::GroupTable* rt, int nacc, cq::ScanStats* stats, unsigned int* flag, int grid,
                        hipStream_t s);
+hipError_t cq_launch_mail_copy(const void* src, const unsigned int* count, unsigned int cap_out, int nacc, uint32_t ncell,
+                               uint32_t sb, void* dst, hipStream_t s);
 hipError_t cq_launch_pack_result(const cq::GroupOut* out, const unsigned int* count, unsigned int cap_out, int nacc,
                                  const cq::Cell* cells, const uint8_t* bytes, uint32_t ncell, uint32_t sb,
                                  uint8_t* dst, const cq::ScanStats* stats, uint8_t* hdr, int order, hipStream_t s);
@@ -1649,6 +1651,7 @@ std::vector<HGroup> run_aggregate(DevCtx& c, const cqgpu_table* t, Compiled& C, 
         constexpr size_t MAIL_HDR = 1024;
         static_assert(sizeof(ScanStats) + 4 <= MAIL_HDR, "mailbox header");
         uint8_t* mail = mailbox(c, MAIL_HDR + cq_pack_result_bytes(cap_out, C.P.nacc, ncell, SB) + 64);
+        Scratch pk;                               // the packed result in HBM (until the sync below)
         bool is_packed = false;
         memset(&st, 0, sizeof st);
         unsigned long long last_clk[8] = {0, 0, 0, 0, 0, 0, 0, 0};
@@ -1671,8 +1674,16 @@ std::vector<HGroup> run_aggregate(DevCtx& c, const cqgpu_table* t, Compiled& C, 
             if (!chunk) {      // one launch: compact and finish speculatively, one sync for all
                 HIPCHECK(cq_launch_compact(&A.gt, &C.P, A.out, A.out_count, cap_out, c.stream));
                 HIPCHECK(cq_launch_finish(t->g, t->n, A.out, A.out_count, cap_out, &FD, dcells, dbytes, c.stream));
-                HIPCHECK(cq_launch_pack_result(A.out, A.out_count, cap_out, C.P.nacc, dcells, dbytes, ncell, SB,
-                                               mail + MAIL_HDR, A.stats, mail, 1, c.stream));
+                if (getenv("CQGPU_PACK_MAPPED")) {   // A/B knob: pack straight into the mapped mailbox
+                    HIPCHECK(cq_launch_pack_result(A.out, A.out_count, cap_out, C.P.nacc, dcells, dbytes, ncell, SB,
+                                                   mail + MAIL_HDR, A.stats, mail, 1, c.stream));
+                } else {                             // pack in HBM, then coalesced copy into the mailbox
+                    pk.get(c, cq_pack_result_bytes(cap_out, C.P.nacc, ncell, SB) + 64);
+                    HIPCHECK(cq_launch_pack_result(A.out, A.out_count, cap_out, C.P.nacc, dcells, dbytes, ncell, SB,
+                                                   pk.p, A.stats, mail, 1, c.stream));
+                    HIPCHECK(cq_launch_mail_copy(pk.p, A.out_count, cap_out, C.P.nacc, ncell, SB, mail + MAIL_HDR,
+                                                 c.stream));
+                }
                 finished = true;
                 is_packed = true;
             }

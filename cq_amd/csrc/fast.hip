@@ -259,10 +259,22 @@ __device__ __forceinline__ Num num4(uint32_t d, uint32_t len) {
     if (DOT) {
         const uint32_t fd = ~nonzero_bytes(v ^ 0x1E1E1E1Eu) & 0x80808080u & (0xFFFFFFFFu << (sh & 31));   // '.' ^ '0'
         const uint32_t low = fd & (0u - fd);
+#ifdef FAST_OLD_NUMK
         const uint32_t below = ((low << 1) - (low != 0 ? 1u : 0u)) & 0x01010100u;
         v = __builtin_amdgcn_perm(0u, v, (low ? 0x0302010Cu : 0x03020100u) - below);
         r.dot = low != 0;
         r.k = r.dot ? (uint32_t)__builtin_clz(low) >> 3 : 0u;
+#else
+        // branch-free: t1 = the bytes up to the dot (all ones without a dot); the
+        // digits after the dot are the sign bits above it; the bytes below the dot
+        // move up one place (the dot's byte drops out, byte 0 becomes zero)
+        const uint32_t t1 = (low << 1) - 1u;
+        const uint32_t nzm = low ? 0xFFFFFFFFu : 0u;
+        const uint32_t below = t1 & 0x01010100u & nzm;
+        v = __builtin_amdgcn_perm(0u, v, 0x03020100u - below + (nzm & 12u));
+        r.dot = low != 0;
+        r.k = (uint32_t)__popc(~t1 & 0x80808080u);
+#endif
     }
     const bool digits = lt_bytes(v, 0x0A0A0A0Au) == 0x80808080u;
     r.ok = (len - 1u <= 3u) & digits & (!DOT | (len > 1u) | !r.dot);
@@ -706,7 +718,12 @@ __global__ __launch_bounds__(LT) void fast_kernel(const uint8_t* __restrict__ g,
                 for (int u = 0; u < 2; u++) {
                     const uint32_t len = sen[u][j] - sst[u][j];
                     const Num n = num4<true>(sd[u][j], len);
+#ifdef FAST_OLD_NUMK
                     const uint32_t mul = (n.k & 2) ? ((n.k & 1) ? 1u : 10u) : ((n.k & 1) ? 100u : 1000u);
+#else
+                    // 10^(3 - k), k <= 3: a 16-bit entry of one 64-bit constant
+                    const uint32_t mul = (uint32_t)(0x0001000A006403E8ull >> (n.k << 4)) & 0xFFFFu;
+#endif
                     sfix[u][j] = __umul24(n.M, mul);   // < 10^7
                     sdbl[u][j] = 0.0;
                     snum[u][j] = n.ok;

@@ -74,6 +74,13 @@ static_assert(NW == SCAN_T, "one mask word per lane");
 // per-lane scratch, because the kernel indexes their arrays at run time.
 __constant__ ScanPlan c_plan;
 __constant__ GroupTable c_gt;
+// slow_kernel's grid: the slow list's length is only known on the device and is 0
+// on well-formed data, where a 256-block launch of this register- and
+// scratch-heavy kernel costs ~15 us for nothing; 64 blocks (16 K lanes, grid-stride)
+// cost ~4 us and still drain a full 1 Mi-record list
+#ifndef SLOW_GRID
+#define SLOW_GRID 64
+#endif
 __device__ __forceinline__ const ScanPlan& c_plan_ref() { return c_plan; }
 
 
@@ -2486,10 +2493,10 @@ hipError_t cq_launch_scan(const uint8_t* g, const cq::ScanPlan* P, const cq::Gro
                                                  slow_list, slow_cap);
             if (e != hipSuccess) return e;
             if (grouped)
-                hipLaunchKernelGGL(cq::slow_kernel<true>, dim3(256), dim3(256), 0, s, g, stats, row_out, row_cap,
+                hipLaunchKernelGGL(cq::slow_kernel<true>, dim3(SLOW_GRID), dim3(256), 0, s, g, stats, row_out, row_cap,
                                    cells_out, slow_list, slow_cap);
             else
-                hipLaunchKernelGGL(cq::slow_kernel<false>, dim3(256), dim3(256), 0, s, g, stats, row_out, row_cap,
+                hipLaunchKernelGGL(cq::slow_kernel<false>, dim3(SLOW_GRID), dim3(256), 0, s, g, stats, row_out, row_cap,
                                    cells_out, slow_list, slow_cap);
             e = hipGetLastError();
             if (e == hipSuccess && grouped) e = cq_launch_raw_merge(gt, rt, P->nacc, stats, s);
@@ -2508,10 +2515,10 @@ hipError_t cq_launch_scan(const uint8_t* g, const cq::ScanPlan* P, const cq::Gro
     e = hipGetLastError();
     if (e != hipSuccess) return e;
     if (grouped)
-        hipLaunchKernelGGL(cq::slow_kernel<true>, dim3(256), dim3(256), 0, s, g, stats, row_out, row_cap, cells_out,
+        hipLaunchKernelGGL(cq::slow_kernel<true>, dim3(SLOW_GRID), dim3(256), 0, s, g, stats, row_out, row_cap, cells_out,
                            slow_list, slow_cap);
     else
-        hipLaunchKernelGGL(cq::slow_kernel<false>, dim3(256), dim3(256), 0, s, g, stats, row_out, row_cap, cells_out,
+        hipLaunchKernelGGL(cq::slow_kernel<false>, dim3(SLOW_GRID), dim3(256), 0, s, g, stats, row_out, row_cap, cells_out,
                            slow_list, slow_cap);
     return hipGetLastError();
 }
@@ -2626,14 +2633,48 @@ __global__ void pack_result_kernel(const GroupOut* __restrict__ out, const unsig
         q[5 * a + 4] = o.extpos[a];
     }
     Cell* dc = (Cell*)(dst + (size_t)ng * rec);
-    for (uint32_t k = 0; k < ncell; k++) dc[(size_t)r * ncell + k] = cells[(size_t)i * ncell + k];
     uint8_t* db = (uint8_t*)(dc + (size_t)ng * ncell);
-    const uint4* sbs = (const uint4*)(bytes + (size_t)i * ncell * sb);
-    uint4* dbs = (uint4*)(db + (size_t)r * ncell * sb);
-    for (uint32_t k = 0; k < ncell * sb / 16; k++) dbs[k] = sbs[k];
+    for (uint32_t k = 0; k < ncell; k++) {
+        const Cell c = cells[(size_t)i * ncell + k];
+        dc[(size_t)r * ncell + k] = c;
+        // only a STRING's own bytes cross to the host (it reads len <= sb of them)
+        const uint32_t nb = c.kind == K_STR ? (min(c.len, sb) + 15u) / 16u : 0u;
+        const uint4* sbs = (const uint4*)(bytes + ((size_t)i * ncell + k) * sb);
+        uint4* dbs = (uint4*)(db + ((size_t)r * ncell + k) * sb);
+        for (uint32_t w = 0; w < nb; w++) dbs[w] = sbs[w];
+    }
 }
 }  // namespace cq
 
+namespace cq {
+// the packed result's records and cells, device buffer -> host-mapped mailbox in
+// coalesced 16-byte lanes (pack_result_kernel's own writes are one thread per group
+// at its rank: scattered 8-byte PCIe writes); the string-byte section follows
+// sparsely, only a STRING's own bytes
+__global__ void mail_copy_kernel(const uint4* __restrict__ src, const unsigned int* __restrict__ count,
+                                 unsigned int cap_out, int nacc, uint32_t ncell, uint32_t sb, uint4* __restrict__ dst) {
+    const uint32_t ng = min(*count, cap_out);
+    const size_t head = (size_t)ng * (40u + 40u * (uint32_t)nacc + ncell * (uint32_t)sizeof(Cell));
+    const size_t n16 = head / 16;
+    for (size_t i = (size_t)blockIdx.x * blockDim.x + threadIdx.x; i < n16; i += (size_t)gridDim.x * blockDim.x)
+        dst[i] = src[i];
+    const Cell* cells = (const Cell*)((const uint8_t*)src + (size_t)ng * (40u + 40u * (uint32_t)nacc));
+    const uint8_t* sbytes = (const uint8_t*)src + head;
+    uint8_t* dbytes = (uint8_t*)dst + head;
+    for (size_t k = (size_t)blockIdx.x * blockDim.x + threadIdx.x; k < (size_t)ng * ncell;
+         k += (size_t)gridDim.x * blockDim.x) {
+        const Cell c = cells[k];
+        const uint32_t nb = c.kind == K_STR ? (min(c.len, sb) + 15u) / 16u : 0u;
+        for (uint32_t w = 0; w < nb; w++) ((uint4*)(dbytes + k * sb))[w] = ((const uint4*)(sbytes + k * sb))[w];
+    }
+}
+}  // namespace cq
+hipError_t cq_launch_mail_copy(const void* src, const unsigned int* count, unsigned int cap_out, int nacc, uint32_t ncell,
+                               uint32_t sb, void* dst, hipStream_t s) {
+    hipLaunchKernelGGL(cq::mail_copy_kernel, dim3(64), dim3(256), 0, s, (const uint4*)src, count, cap_out, nacc, ncell,
+                       sb, (uint4*)dst);
+    return hipGetLastError();
+}
 size_t cq_pack_result_bytes(unsigned int ng, int nacc, uint32_t ncell, uint32_t sb) {
     return (size_t)ng * (40u + 40u * (uint32_t)nacc + ncell * (uint32_t)sizeof(cq::Cell) + ncell * sb);
 }
