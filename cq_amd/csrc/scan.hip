@@ -1158,9 +1158,8 @@ __global__ __launch_bounds__(256) void slow_kernel(const uint8_t* __restrict__ g
 }
 
 // ------------------------------------------------------------------ compaction
-__global__ void compact_kernel(int nacc, uint32_t kinds, GroupOut* out, unsigned int* count,
+__global__ void compact_kernel(const GroupTable gt, int nacc, uint32_t kinds, GroupOut* out, unsigned int* count,
                                unsigned int cap_out) {
-    const GroupTable& gt = c_gt;
     uint8_t kind_of[MAX_ACC];
 #pragma unroll
     for (int a = 0; a < MAX_ACC; a++) kind_of[a] = (uint8_t)((kinds >> (2 * a)) & 3);
@@ -2552,9 +2551,7 @@ hipError_t cq_launch_compact(const cq::GroupTable* gt, const cq::ScanPlan* P, cq
     uint32_t kinds = 0;
     for (int a = 0; a < nacc; a++) kinds |= (uint32_t)P->acc[a].kind << (2 * a);
     const dim3 grid((gt->cap + 255) / 256);
-    hipError_t e = cq::upload_symbol((const void*)&HIP_SYMBOL(cq::c_gt), gt, sizeof *gt, s);
-    if (e != hipSuccess) return e;
-    hipLaunchKernelGGL(cq::compact_kernel, grid, dim3(256), 0, s, nacc, kinds, out, count, cap_out);
+    hipLaunchKernelGGL(cq::compact_kernel, grid, dim3(256), 0, s, *gt, nacc, kinds, out, count, cap_out);
     return hipGetLastError();
 }
 
@@ -2607,11 +2604,22 @@ __global__ void pack_result_kernel(const GroupOut* __restrict__ out, const unsig
             __syncthreads();
             for (uint32_t k = threadIdx.x; k < m; k += blockDim.x) tile[k] = out[base + k].first;
             __syncthreads();
-            if (i < ng)
-                for (uint32_t k = 0; k < m; k++) {
+            if (i < ng) {
+                // eight independent LDS reads in flight per trip (a one-at-a-time loop
+                // waits out the LDS latency per element: ~30 us for 1,000 groups)
+                uint32_t k = 0;
+                for (; k + 8 <= m; k += 8) {
+                    unsigned long long f[8];
+#pragma unroll
+                    for (int u = 0; u < 8; u++) f[u] = tile[k + u];
+#pragma unroll
+                    for (int u = 0; u < 8; u++) below += (f[u] < fi) | ((f[u] == fi) & (base + k + u < i));
+                }
+                for (; k < m; k++) {
                     const unsigned long long f = tile[k];
                     below += (f < fi) | ((f == fi) & (base + k < i));
                 }
+            }
         }
         r = below;
     }
