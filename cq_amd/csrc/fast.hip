@@ -147,9 +147,45 @@ __device__ __forceinline__ uint32_t flags40(uint32_t r, uint32_t m40) { return _
 
 // 32 bytes -> separator and terminator bits; quote presence accumulated in q
 // (COMMA: the delimiter lookup's zero bytes, else the quote byte's zero test)
+#ifndef FAST_OLD_CLS
+// COMMA tables with the match in bit 0 (v_perm output & 0x01010101 is 0 exactly
+// for the matched bytes, so no flag extraction before v_dot4):
+//   terminators: x ^ 0x06 -> '\n' selector 12 (always 0x00), '\r' selector 11 (sign
+//     of table byte 7 = 0x01 -> 0x00); byte 0x01 selects table byte 7 itself (0x01);
+//     every other table byte 0xFF, selectors >= 13 0xFF: exact, no false match
+//   delimiter: x ^ 0x2E -> ',' selector 2 (0x80), '"' selector 12 (0x00: a separator
+//     here, and the one zero byte, so the zero-byte test flags exactly the quotes);
+//     every other table byte 0xFF (the sign selectors 8-11 give 0xFF)
+constexpr uint32_t CLS2_TN1 = 0x01FFFFFFu, CLS2_TN0 = 0xFFFFFFFFu, CLS2_TD1 = 0xFFFFFFFFu, CLS2_TD0 = 0xFF80FFFFu;
+#endif
 template <bool COMMA>
 __device__ __forceinline__ void classify32(const v4u a, const v4u b, const CK& k, uint32_t& sep, uint32_t& nl,
                                            uint32_t& q) {
+#ifndef FAST_OLD_CLS
+    if (COMMA) {
+        uint32_t us[4], un[4];
+#pragma unroll
+        for (int j = 0; j < 8; j++) {
+            const uint32_t x = j < 4 ? a[j & 3] : b[j & 3];
+            const uint32_t rn = __builtin_amdgcn_perm(k.tn1, k.tn0, x ^ 0x06060606u);
+            const uint32_t rd = __builtin_amdgcn_perm(k.td1, k.td0, x ^ 0x2E2E2E2Eu);
+            q = __builtin_amdgcn_bitop3_b32(rd - 0x01010101u, rd, q, 0xBA);   // (t & ~rd) | q: quotes
+            const uint32_t fn = rn & k.m40;                                    // 1: not a terminator
+            const uint32_t fs = __builtin_amdgcn_bitop3_b32(rn, rd, k.m40, 0x80);   // 1: not a separator
+            const uint32_t w = (j & 1) ? k.w1 : k.w0;
+            if (j & 1) {
+                us[j >> 1] = __builtin_amdgcn_udot4(fs, w, us[j >> 1], false);
+                un[j >> 1] = __builtin_amdgcn_udot4(fn, w, un[j >> 1], false);
+            } else {
+                us[j >> 1] = __builtin_amdgcn_udot4(fs, w, 0u, false);
+                un[j >> 1] = __builtin_amdgcn_udot4(fn, w, 0u, false);
+            }
+        }
+        nl = ~(un[0] | (un[1] << 8) | (un[2] << 16) | (un[3] << 24));
+        sep = ~(us[0] | (us[1] << 8) | (us[2] << 16) | (us[3] << 24));
+        return;
+    }
+#endif
     uint32_t ud[4], un[4];
 #pragma unroll
     for (int j = 0; j < 8; j++) {
@@ -426,11 +462,19 @@ __global__ __launch_bounds__(LT) void fast_kernel(const uint8_t* __restrict__ g,
     }
     const uint32_t rep_q = fp.quote * 0x01010101u;
     CK ck;
+#ifndef FAST_OLD_CLS
+    ck.tn1 = vreg(COMMA ? CLS2_TN1 : 0x00004000u);
+    ck.tn0 = vreg(COMMA ? CLS2_TN0 : 0x00400000u);
+    ck.td1 = vreg(COMMA ? CLS2_TD1 : 0u);
+    ck.td0 = vreg(COMMA ? CLS2_TD0 : 0x40u);
+    ck.m40 = vreg(COMMA ? 0x01010101u : 0x40404040u);   // (COMMA: the bit-0 mask)
+#else
     ck.tn1 = vreg(0x00004000u);
     ck.tn0 = vreg(0x00400000u);
     ck.td1 = vreg(COMMA ? 0x80408080u : 0u);
     ck.td0 = vreg(COMMA ? 0x80802080u : 0x40u);
     ck.m40 = vreg(0x40404040u);
+#endif
     ck.w0 = vreg(0x08040201u);
     ck.w1 = vreg(0x80402010u);
     ck.rd = vreg(fp.delim * 0x01010101u);
@@ -1045,11 +1089,19 @@ __global__ __launch_bounds__(LT) void jx_extract_kernel(const uint8_t* __restric
     WaveLds& W = waves[wv];
     const uint32_t rep_q = jp.quote * 0x01010101u;
     CK ck;
+#ifndef FAST_OLD_CLS
+    ck.tn1 = vreg(COMMA ? CLS2_TN1 : 0x00004000u);
+    ck.tn0 = vreg(COMMA ? CLS2_TN0 : 0x00400000u);
+    ck.td1 = vreg(COMMA ? CLS2_TD1 : 0u);
+    ck.td0 = vreg(COMMA ? CLS2_TD0 : 0x40u);
+    ck.m40 = vreg(COMMA ? 0x01010101u : 0x40404040u);   // (COMMA: the bit-0 mask)
+#else
     ck.tn1 = vreg(0x00004000u);
     ck.tn0 = vreg(0x00400000u);
     ck.td1 = vreg(COMMA ? 0x80408080u : 0u);
     ck.td0 = vreg(COMMA ? 0x80802080u : 0x40u);
     ck.m40 = vreg(0x40404040u);
+#endif
     ck.w0 = vreg(0x08040201u);
     ck.w1 = vreg(0x80402010u);
     ck.rd = vreg(jp.delim * 0x01010101u);
