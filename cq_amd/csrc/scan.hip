@@ -249,6 +249,34 @@ __device__ void parse_cols_out(const uint8_t* rec, const int16_t* cols, int ncol
     }
 }
 
+// the same from a staged copy: the record's first `lim` bytes in `tile` (LDS), the
+// rest (and every cell's bytes) in HBM at `rec`
+__device__ void parse_cols_out_staged(const uint8_t* tile, uint32_t lim, const uint8_t* rec, const int16_t* cols,
+                                      int ncols, uint32_t delim, uint32_t quote, Cell* out) {
+    const Src S{tile, rec, lim, false};
+    uint32_t i = 0, fs = 0, flen = 0;
+    int col = 0;
+    bool ended = false;
+    for (int k = 0; k < ncols; k++) {
+        const int want = cols[k];
+        Cell c = cell_null();
+        while (!ended && col < want) {
+            if (!g_field(S, i, delim, quote, fs, flen) || S.at(i) != delim) ended = true;
+            else { i = i + 1; col++; }
+        }
+        if (!ended && col == want) {
+            if (!g_field(S, i, delim, quote, fs, flen)) {
+                ended = true;
+            } else {
+                c = parse_cell(rec + fs, flen);
+                if (S.at(i) == delim) { i = i + 1; col++; }
+                else ended = true;
+            }
+        }
+        out[k] = c;
+    }
+}
+
 __device__ void parse_record_out(const uint8_t* rec, const ScanPlan& P, Cell* out) {
     parse_cols_out(rec, P.need_col, P.nneed, P.delim, P.quote, out, 1);
 }
@@ -1321,7 +1349,8 @@ __global__ __launch_bounds__(256) void project_kernel(const uint8_t* __restrict_
 // (build_aggregated_result's non-aggregate columns, evaluator_aggregates.c:679-689),
 // its MIN/MAX cells and its long-key text, with the first `sb` bytes of every
 // STRING inline -- so the host fetches a whole aggregate result in one copy.
-__global__ void finish_kernel(const uint8_t* __restrict__ g, uint64_t n, const GroupOut* __restrict__ out,
+constexpr int FINISH_T = 128;
+__global__ __launch_bounds__(FINISH_T) void finish_kernel(const uint8_t* __restrict__ g, uint64_t n, const GroupOut* __restrict__ out,
                               const unsigned int* __restrict__ count, unsigned int cap_out, FinishDesc D,
                               Cell* __restrict__ cells, uint8_t* __restrict__ bytes) {
     const uint32_t ncell = (uint32_t)(D.ncols + D.nacc + 1);
@@ -1332,7 +1361,19 @@ __global__ void finish_kernel(const uint8_t* __restrict__ g, uint64_t n, const G
     const unsigned long long first = out[i].first == NOPOS ? NOPOS : out[i].first >> D.first_shift;
     if (D.ncols) {
         if (first != NOPOS && first < n) {
-            parse_cols_out(g + first, D.cols, D.ncols, D.delim, D.quote, cs, 1);
+            // the record's first 128 bytes staged in LDS by nine independent 16-byte
+            // loads (the byte walk from HBM was one dependent load per byte; the
+            // table's tail padding covers the over-read)
+            __shared__ uint4 stage[FINISH_T][9];
+            const uint8_t* rec = g + first;
+            const uint4* src = (const uint4*)((uintptr_t)rec & ~(uintptr_t)15);
+            uint4 v[9];
+#pragma unroll
+            for (int w = 0; w < 9; w++) v[w] = src[w];
+#pragma unroll
+            for (int w = 0; w < 9; w++) stage[threadIdx.x][w] = v[w];
+            const uint8_t* tile = (const uint8_t*)stage[threadIdx.x] + ((uintptr_t)rec & 15);
+            parse_cols_out_staged(tile, 128, rec, D.cols, D.ncols, D.delim, D.quote, cs);
         } else {
             for (int k = 0; k < D.ncols; k++) cs[k] = cell_null();
         }
@@ -2602,7 +2643,20 @@ __global__ void pack_result_kernel(const GroupOut* __restrict__ out, const unsig
         for (uint32_t base = 0; base < ng; base += 1024) {
             const uint32_t m = min(1024u, ng - base);
             __syncthreads();
-            for (uint32_t k = threadIdx.x; k < m; k += blockDim.x) tile[k] = out[base + k].first;
+            {   // eight independent loads in flight per thread (GroupOut rows are 360 bytes apart)
+                unsigned long long t[8];
+#pragma unroll
+                for (int u = 0; u < 8; u++) {
+                    const uint32_t k = threadIdx.x + u * blockDim.x;
+                    t[u] = k < m ? out[base + k].first : 0ull;
+                }
+#pragma unroll
+                for (int u = 0; u < 8; u++) {
+                    const uint32_t k = threadIdx.x + u * blockDim.x;
+                    if (k < m) tile[k] = t[u];
+                }
+                for (uint32_t k = threadIdx.x + 8 * blockDim.x; k < m; k += blockDim.x) tile[k] = out[base + k].first;
+            }
             __syncthreads();
             if (i < ng) {
                 // eight independent LDS reads in flight per trip (a one-at-a-time loop
@@ -2624,7 +2678,9 @@ __global__ void pack_result_kernel(const GroupOut* __restrict__ out, const unsig
         r = below;
     }
     if (i >= ng) return;
-    const GroupOut& o = out[i];
+    // every load of the group's record first, then the stores (interleaved, each
+    // store waited on its load)
+    const GroupOut o = out[i];
     uint8_t* rp = dst + (size_t)r * rec;
     ((uint32_t*)rp)[0] = o.clslen;
     ((uint32_t*)rp)[1] = 0;
@@ -2633,7 +2689,9 @@ __global__ void pack_result_kernel(const GroupOut* __restrict__ out, const unsig
     ((unsigned long long*)rp)[3] = o.cnt;
     ((unsigned long long*)rp)[4] = o.first;
     uint64_t* q = (uint64_t*)(rp + 40);
-    for (int a = 0; a < nacc; a++) {
+#pragma unroll
+    for (int a = 0; a < MAX_ACC; a++) {
+        if (a >= nacc) break;
         q[5 * a + 0] = dbl_bits(o.sum[a]);
         q[5 * a + 1] = o.num[a];
         q[5 * a + 2] = ((uint64_t)o.ext[a].len << 32) | o.ext[a].kind;
@@ -2698,7 +2756,8 @@ unsigned int cq_pack_order_max() { return cq::PACK_ORDER_MAX; }
 hipError_t cq_launch_finish(const uint8_t* g, uint64_t n, const cq::GroupOut* out, const unsigned int* count,
                             unsigned int cap_out, const cq::FinishDesc* D, cq::Cell* cells, uint8_t* bytes,
                             hipStream_t s) {
-    hipLaunchKernelGGL(cq::finish_kernel, dim3((cap_out + 127) / 128), dim3(128), 0, s, g, n, out, count, cap_out, *D,
+    hipLaunchKernelGGL(cq::finish_kernel, dim3((cap_out + cq::FINISH_T - 1) / cq::FINISH_T), dim3(cq::FINISH_T), 0, s,
+                       g, n, out, count, cap_out, *D,
                        cells, bytes);
     return hipGetLastError();
 }
