@@ -862,10 +862,24 @@ __global__ __launch_bounds__(LT) void fast_kernel(const uint8_t* __restrict__ g,
                 // lookup: the key's two buckets (one 16-byte LDS read each)
                 int slot[2];
                 bool miss[2];
+#ifndef FAST_OLD_LK
+                // both records' bucket reads issued before any compare (one LDS wait per pass)
+                v4u xs[2], ys[2];
 #pragma unroll
                 for (int u = 0; u < 2; u++) {
                     const uint32_t b1 = hb[u] & (TBUCKETS - 1), b2 = (hb[u] >> 16) & (TBUCKETS - 1);
+                    xs[u] = ((const v4u*)T)[b1];
+                    ys[u] = ((const v4u*)T)[b2];
+                }
+#endif
+#pragma unroll
+                for (int u = 0; u < 2; u++) {
+                    const uint32_t b1 = hb[u] & (TBUCKETS - 1), b2 = (hb[u] >> 16) & (TBUCKETS - 1);
+#ifndef FAST_OLD_LK
+                    const v4u x = xs[u], y = ys[u];
+#else
                     const v4u x = ((const v4u*)T)[b1], y = ((const v4u*)T)[b2];
+#endif
                     const uint64_t t0 = (uint64_t)x.x | ((uint64_t)x.y << 32), t1 = (uint64_t)x.z | ((uint64_t)x.w << 32);
                     const uint64_t t2 = (uint64_t)y.x | ((uint64_t)y.y << 32), t3 = (uint64_t)y.z | ((uint64_t)y.w << 32);
                     int s = -1;
