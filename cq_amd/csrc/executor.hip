@@ -4875,6 +4875,9 @@ cqgpu_partial* cqgpu_partial_new(cq_node* q, cqgpu_table* const* tables, int nta
     g_inel.clear();
     g_err.clear();
     std::unique_ptr<cqgpu_partial> p(new cqgpu_partial);
+    PhaseClock pc;
+    g_phase = &pc;
+    struct Unset { ~Unset() { g_phase = nullptr; } } unset_;
     try {
         DevCtx& c = ctx();
         bump_reset(c);
@@ -4909,6 +4912,7 @@ cqgpu_partial* cqgpu_partial_new(cq_node* q, cqgpu_table* const* tables, int nta
                 groups = run_cells_aggregate(c, t, C, L, &st, true);
             }
         }
+        PHASE("partial scan");
         const uint32_t m = (uint32_t)groups.size();
         p->m = m;
         const uint32_t W = p->W, P = p->P, Q = p->Q, R = p->R, NV = p->NV;
@@ -4983,6 +4987,7 @@ cqgpu_partial* cqgpu_partial_new(cq_node* q, cqgpu_table* const* tables, int nta
             HIPCHECK(hipMemcpyAsync(p->st_priv.p, hp.data(), hp.size() * 8, hipMemcpyHostToDevice, c.stream));
         }
         HIPCHECK(hipStreamSynchronize(c.stream));
+        PHASE("partial planes");
         p->stages = {ST_KEYS, ST_MIN};
         if (NV) p->stages.push_back(ST_SUM);
         if (nmm) p->stages.push_back(ST_STRS);
@@ -5308,6 +5313,9 @@ int cqgpu_partial_put(cqgpu_partial* p, void* dev_dst) {
 cq_table* cqgpu_partial_result(cqgpu_partial* p, cq_node* q) {
     g_inel.clear();
     g_err.clear();
+    PhaseClock pc;
+    g_phase = &pc;
+    struct Unset { ~Unset() { g_phase = nullptr; } } unset_;
     try {
         if (!p || p->op != COLL_DONE || p->at != p->stages.size()) throw HipError{"partial_result: merge not finished"};
         DevCtx& c = ctx();
@@ -5318,20 +5326,26 @@ cq_table* cqgpu_partial_result(cqgpu_partial* p, cq_node* q) {
         std::vector<uint8_t> text(p->text_bytes);
         std::vector<double> sm((size_t)G * W), vla((size_t)G * NV);
         std::vector<unsigned long long> mn((size_t)G * P), ex((size_t)G * nmm), cells((size_t)G * C * 2);
-        if (n) {
-            HIPCHECK(hipMemcpyAsync(all.data(), p->all.p, (size_t)n * KEYREC, hipMemcpyDeviceToHost, c.stream));
-            HIPCHECK(hipMemcpyAsync(flag.data(), p->flag.p, (size_t)n * 4, hipMemcpyDeviceToHost, c.stream));
-        }
-        if (!text.empty()) HIPCHECK(hipMemcpyAsync(text.data(), p->text.p, text.size(), hipMemcpyDeviceToHost, c.stream));
-        auto get = [&](void* dst, const DevBuf& b, size_t bytes) {
-            if (bytes) HIPCHECK(hipMemcpyAsync(dst, b.p, bytes, hipMemcpyDeviceToHost, c.stream));
-        };
-        get(sm.data(), p->dsum, sm.size() * 8);
-        get(vla.data(), p->dvla, vla.size() * 8);
-        get(mn.data(), p->dmin, mn.size() * 8);
-        get(ex.data(), p->dext, ex.size() * 8);
-        get(cells.data(), p->dcell, cells.size() * 8);
+        // every plane into one pinned staging buffer (pageable copies are staged one
+        // by one by the runtime), one sync, then host copies out
+        struct Piece { void* dst; const void* src; size_t bytes; size_t at; };
+        Piece pieces[] = {{all.data(), p->all.p, n ? (size_t)n * KEYREC : 0, 0},
+                          {flag.data(), p->flag.p, n ? (size_t)n * 4 : 0, 0},
+                          {text.data(), p->text.p, text.size(), 0},
+                          {sm.data(), p->dsum.p, sm.size() * 8, 0},
+                          {vla.data(), p->dvla.p, vla.size() * 8, 0},
+                          {mn.data(), p->dmin.p, mn.size() * 8, 0},
+                          {ex.data(), p->dext.p, ex.size() * 8, 0},
+                          {cells.data(), p->dcell.p, cells.size() * 8, 0}};
+        size_t tot = 0;
+        for (Piece& pc2 : pieces) { pc2.at = tot; tot += (pc2.bytes + 15) & ~(size_t)15; }
+        uint8_t* stage = (uint8_t*)pinned(c, std::max<size_t>(tot, 16));
+        for (Piece& pc2 : pieces)
+            if (pc2.bytes) HIPCHECK(hipMemcpyAsync(stage + pc2.at, pc2.src, pc2.bytes, hipMemcpyDeviceToHost, c.stream));
         HIPCHECK(hipStreamSynchronize(c.stream));
+        for (Piece& pc2 : pieces)
+            if (pc2.bytes) memcpy(pc2.dst, stage + pc2.at, pc2.bytes);
+        PHASE("result copies");
         // the owners' texts over 8 bytes
         std::unordered_map<uint64_t, std::string> longs;
         for (size_t o = 0; o + 12 <= p->side_all.size();) {
@@ -5362,19 +5376,34 @@ cq_table* cqgpu_partial_result(cqgpu_partial* p, cq_node* q) {
             return x;
         };
         const Compiled& Cp = p->C;
-        std::vector<HGroup> groups;
-        uint32_t d = 0;
-        for (uint32_t r = 0; r < n && d < G; r++) {
-            if (!flag[r]) continue;
+        // dense id d <-> its key record r (the d-th flagged record), then the groups
+        // built straight in first-row order (a stable sort of (first, d) pairs instead
+        // of moving whole HGroups)
+        std::vector<uint32_t> rec_of;
+        rec_of.reserve(G);
+        for (uint32_t r = 0; r < n && rec_of.size() < G; r++)
+            if (flag[r]) rec_of.push_back(r);
+        std::vector<std::pair<unsigned long long, uint32_t>> ord(rec_of.size());
+        for (uint32_t d = 0; d < (uint32_t)rec_of.size(); d++) {
+            const unsigned long long f = mn[(size_t)d * P];
+            ord[d] = {f == ABS64 ? NOPOS : f, d};
+        }
+        std::sort(ord.begin(), ord.end());      // (first, d): ties keep dense order, as the stable sort did
+        std::vector<HGroup> groups(ord.size());
+        for (size_t gi = 0; gi < ord.size(); gi++) {
+            const uint32_t d = ord[gi].second, r = rec_of[d];
             const HKeyRec& k = all[r];
-            HGroup h;
+            HGroup& h = groups[gi];
             h.kcls = k.clslen >> 16;
             h.klen = k.clslen & 0xffff;
             h.kw0 = k.w0;
             h.kw1 = k.w1;
-            if (h.kcls == GK_STR)
-                for (uint32_t i = 0; i < h.klen; i++)
-                    h.kbytes.push_back((char)((i < 8 ? k.w0 >> (8 * i) : k.w1 >> (8 * (i - 8))) & 0xff));
+            if (h.kcls == GK_STR) {
+                char kb[16];
+                for (uint32_t i = 0; i < h.klen && i < 16; i++)
+                    kb[i] = (char)((i < 8 ? k.w0 >> (8 * i) : k.w1 >> (8 * (i - 8))) & 0xff);
+                h.kbytes.assign(kb, std::min<uint32_t>(h.klen, 16));
+            }
             if (h.kcls == GK_LONG) {
                 if (k.pad2 + h.klen > text.size()) throw HipError{"partial_result: bad key text offset"};
                 h.kbytes.assign((const char*)text.data() + k.pad2, h.klen);
@@ -5398,17 +5427,17 @@ cq_table* cqgpu_partial_result(cqgpu_partial* p, cq_node* q) {
                 h.vla_ok[v] = nv > 0;
                 h.vla[v] = nv > 0 ? sqrt(vla[(size_t)d * NV + v] / nv) : 0.0;
             }
-            groups.push_back(std::move(h));
-            d++;
         }
         if (!Cp.grouped && groups.size() > 1) throw HipError{"partials disagree on the single group"};
-        std::stable_sort(groups.begin(), groups.end(), [](const HGroup& x, const HGroup& y) { return x.first < y.first; });
+        PHASE("result groups");
         Compiled C2 = Cp;
         Literals L;
         parse_literals(c, C2.lits, L);
+        PHASE("result literals");
         g_stats.groups = groups.size();
         cq_table* res = build_groups(C2, groups, L, c);
         post_ops(c, res, q);
+        PHASE("result table");
         g_stats.path = 1;
         return res;
     } catch (Ineligible& e) {

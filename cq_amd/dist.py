@@ -165,7 +165,7 @@ def allgather_var(buf: torch.Tensor, comm) -> tuple[torch.Tensor, list[int]]:
     n = torch.tensor([buf.numel()], dtype=torch.int64, device=comm)
     sizes = [torch.zeros(1, dtype=torch.int64, device=comm) for _ in range(world)]
     dist.all_gather(sizes, n)
-    lens = [int(x.item()) for x in sizes]
+    lens = torch.cat(sizes).tolist()          # one device-to-host transfer, not one per rank
     mx = max(max(lens), 1)
     pad = torch.zeros(mx, dtype=torch.uint8, device=comm)
     pad[: buf.numel()] = buf.to(comm)
@@ -188,18 +188,26 @@ def dense_merge(part, device, comm_device=None):
     world, rank = dist.get_world_size(), dist.get_rank()
     comm = torch.device(comm_device) if comm_device is not None else torch.device(device)
     result, sizes = None, None
+
+    def step(result, sizes):
+        """take the last result, learn the next collective and fill its payload (one
+        rank-local step, so one agreement per collective; cqgpu_partial_put returns
+        after its copy has completed, so the payload is ready for torch's stream)"""
+        op, count = part.next(result, sizes, rank, world)
+        if op in (DONE, DECLINE):
+            return op, count, None
+        buf = torch.empty(max(count, 1), dtype=_DTYPES[op], device=device)[:count]
+        part.put(buf)
+        return op, count, buf
+
     while True:
-        out, err = _local(part.next, result, sizes, rank, world)
+        out, err = _local(step, result, sizes)
         agree(err, comm)
-        op, count = out
+        op, count, buf = out
         if op == DONE:
             break
         if op == DECLINE:
             return NOT_DENSE
-        buf = torch.empty(max(count, 1), dtype=_DTYPES[op], device=device)[:count]
-        _, err = _local(part.put, buf)
-        agree(err, comm)
-        _sync(device)
         sizes = None
         if op == ALLGATHER:
             result, sizes = allgather_var(buf, comm)
@@ -231,11 +239,18 @@ def scan_partitioned_dense(ast, table, comm_device=None):
     device = torch.device("cuda", torch.cuda.current_device())
     comm = torch.device(comm_device) if comm_device is not None else device
     part, err = _local(DensePartial, ast, table)
-    agree(err, comm)
+    # one MAX all-reduce for both questions: did any rank fail, is any rank off the dense path
+    flags = torch.tensor([0 if err is None else 1, 0 if (err is None and part.ok) else 1], dtype=torch.int32,
+                         device=comm)
+    dist.all_reduce(flags, op=dist.ReduceOp.MAX)
+    failed, declined = flags.tolist()
+    if failed:
+        if part is not None:
+            part.free()
+        msg = f"rank {dist.get_rank()}: {err}" if err is not None else f"rank {dist.get_rank()}: a peer rank failed"
+        raise PeerFailure(msg) from err
     try:
-        ok = torch.tensor([1 if part.ok else 0], dtype=torch.int32, device=comm)
-        dist.all_reduce(ok, op=dist.ReduceOp.MIN)
-        if int(ok.item()) == 0:
+        if declined:
             part.free()
             return scan_partitioned(ast, table, comm_device)
         tp = dense_merge(part, device, comm_device)

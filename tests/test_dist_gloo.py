@@ -231,3 +231,52 @@ def test_dense_merge_choreography_gloo(world):
             if first < w[3]:
                 w[3], w[4] = first, rep
     assert res[0] == sorted((tuple(w) for w in want.values()), key=lambda r: r[3])
+
+
+class _FailingPartial(_StandInPartial):
+    """the stand-in, but this rank's payload step for the cell reduce raises (a
+    rank-local failure such as a HIP out-of-memory on that rank only)"""
+
+    def put(self, buf):
+        if self.STAGES[self.at - 1] == "cell":
+            raise RuntimeError("injected rank-local failure")
+        super().put(buf)
+
+
+def _fworker(rank, world, port, q, bad):
+    import torch.distributed as dist
+    from cq_amd.dist import PeerFailure, dense_merge
+    os.environ["MASTER_ADDR"] = "127.0.0.1"
+    os.environ["MASTER_PORT"] = str(port)
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    try:
+        cls = _FailingPartial if rank == bad else _StandInPartial
+        try:
+            dense_merge(cls(_rank_groups(rank)), "cpu", "cpu")
+            q.put((rank, "returned"))
+        except PeerFailure as e:
+            q.put((rank, "peer-failure: " + str(e)))
+        # every rank still reaches the same next collective (nobody was left inside one)
+        dist.barrier()
+    finally:
+        dist.destroy_process_group()
+
+
+@pytest.mark.parametrize("world,bad", [(2, 1), (3, 0)])
+def test_dense_merge_rank_local_failure_raises_everywhere(world, bad):
+    """a rank-local failure inside the merge loop must not leave the other
+    ranks blocked in a collective -- every rank raises PeerFailure after the same
+    agreement, the failing rank naming its own error"""
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    port = _free_port()
+    procs = [ctx.Process(target=_fworker, args=(r, world, port, q, bad)) for r in range(world)]
+    for p in procs:
+        p.start()
+    res = dict(q.get(timeout=120) for _ in range(world))
+    for p in procs:
+        p.join(timeout=60)
+        assert p.exitcode == 0
+    for r in range(world):
+        assert res[r].startswith("peer-failure"), res
+    assert "injected rank-local failure" in res[bad]
