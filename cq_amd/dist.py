@@ -163,15 +163,17 @@ def allgather_var(buf: torch.Tensor, comm) -> tuple[torch.Tensor, list[int]]:
     concatenated in rank order, and their lengths"""
     world = dist.get_world_size()
     n = torch.tensor([buf.numel()], dtype=torch.int64, device=comm)
-    sizes = [torch.zeros(1, dtype=torch.int64, device=comm) for _ in range(world)]
-    dist.all_gather(sizes, n)
-    lens = torch.cat(sizes).tolist()          # one device-to-host transfer, not one per rank
+    sizes = torch.empty(world, dtype=torch.int64, device=comm)
+    dist.all_gather_into_tensor(sizes, n)
+    lens = sizes.tolist()                     # one device-to-host transfer
     mx = max(max(lens), 1)
-    pad = torch.zeros(mx, dtype=torch.uint8, device=comm)
-    pad[: buf.numel()] = buf.to(comm)
-    outs = [torch.empty(mx, dtype=torch.uint8, device=comm) for _ in range(world)]
-    dist.all_gather(outs, pad)
-    return torch.cat([o[:k] for o, k in zip(outs, lens)]), lens
+    pad = torch.empty(mx, dtype=torch.uint8, device=comm)
+    pad[: buf.numel()] = buf.to(comm)         # (bytes past a rank's length are never read)
+    out = torch.empty(world * mx, dtype=torch.uint8, device=comm)
+    dist.all_gather_into_tensor(out, pad)
+    if all(k == mx for k in lens):
+        return out, lens
+    return torch.cat([out[r * mx:r * mx + k] for r, k in enumerate(lens)]), lens
 
 
 _DTYPES = {ALLGATHER: torch.uint8, ALLREDUCE_MIN_I64: torch.int64, ALLREDUCE_SUM_F64: torch.float64,
