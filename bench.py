@@ -202,7 +202,19 @@ def main():
     # merge) even at world size 1, so one-GPU boxes exercise the collective path
     if world > 1 or (os.environ.get("CQ_BENCH_FORCE_DIST") and "WORLD_SIZE" in os.environ):
         import torch.distributed as dist
-        dist.init_process_group("nccl", device_id=torch.device("cuda", local))
+        # RCCL prints a version banner on stdout when its communicator comes up: keep
+        # stdout for the one JSON line (the banner goes to stderr)
+        sys.stdout.flush()
+        saved = os.dup(1)
+        os.dup2(2, 1)
+        try:
+            dist.init_process_group("nccl", device_id=torch.device("cuda", local))
+            dist.barrier()
+            torch.cuda.synchronize()
+        finally:
+            sys.stdout.flush()
+            os.dup2(saved, 1)
+            os.close(saved)
 
     import cq_amd
     from cq_amd import abi

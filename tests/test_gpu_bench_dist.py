@@ -29,7 +29,8 @@ def test_bench_dense_merge_over_rccl_one_rank():
            "--no-config5", "--gen-workers", "4"]
     p = subprocess.run(cmd, cwd=ROOT, env=env, capture_output=True, text=True, timeout=110)
     assert p.returncode == 0, p.stderr[-3000:]
-    line = [l for l in p.stdout.splitlines() if l.startswith("{")][-1]
-    d = json.loads(line)
+    lines = [l for l in p.stdout.splitlines() if l.strip()]
+    assert len(lines) == 1, p.stdout[-2000:]          # one JSON line on stdout (no RCCL banner)
+    d = json.loads(lines[0])
     assert d["verified"] is True
     assert d["config"]["rows_total"] == 3_000_000
