@@ -421,7 +421,7 @@ constexpr uint32_t fixed_bytes() { return (uint32_t)(sizeof(WaveLds) * NWV); }
 // (else none); NS: distinct SUM arguments; COMMA: delimiter ',' and quote '"';
 // CANON: the roles' columns ascend in the order WHERE, SUM 0, SUM 1, GROUP BY (the
 // walk's ranks are compile-time), else rank[] says which field each role reads
-template <bool GROUPED, bool WHERE, int NS, bool COMMA, bool CANON>
+template <bool GROUPED, bool WHERE, int NS, bool COMMA, bool CANON, int RP>
 __global__ __launch_bounds__(LT) void fast_kernel(const uint8_t* __restrict__ g, ScanStats* __restrict__ stats,
                                                   unsigned long long* __restrict__ slow_list,
                                                   unsigned long long slow_cap, const FastPlan fp,
@@ -604,11 +604,11 @@ __global__ __launch_bounds__(LT) void fast_kernel(const uint8_t* __restrict__ g,
 #endif
         while (__any(todo != 0)) {
             // ---- two records of this lane
-            uint32_t p[2], pa[2], fst[2][4], fen[2][4], e[2];   // p: window offset, pa: LDS address
-            uint64_t sv[2];
-            bool valid[2], fail[2];
+            uint32_t p[RP], pa[RP], fst[RP][4], fen[RP][4], e[RP];   // p: window offset, pa: LDS address
+            uint64_t sv[RP];
+            bool valid[RP], fail[RP];
 #pragma unroll
-            for (int u = 0; u < 2; u++) {
+            for (int u = 0; u < RP; u++) {
                 valid[u] = todo != 0;
                 const uint32_t b = ctz64(todo) & 63u;               // (no start left: any byte of the lane)
                 todo &= todo - 1;
@@ -627,35 +627,35 @@ __global__ __launch_bounds__(LT) void fast_kernel(const uint8_t* __restrict__ g,
                 asm volatile("" : "+s"(n));                         // tested here, not hoisted as lane masks
                 if (k > 0 && n == 0) {
 #pragma unroll
-                    for (int u = 0; u < 2; u++) { fst[u][k] = fst[u][k - 1]; fen[u][k] = fen[u][k - 1]; }
+                    for (int u = 0; u < RP; u++) { fst[u][k] = fst[u][k - 1]; fen[u][k] = fen[u][k - 1]; }
                     continue;
                 }
                 if (k > 0) {
 #pragma unroll
-                    for (int u = 0; u < 2; u++) sv[u] &= sv[u] - 1;  // the previous field's end
+                    for (int u = 0; u < RP; u++) sv[u] &= sv[u] - 1;  // the previous field's end
                 }
                 if (k == 0 && n == 0) {
 #pragma unroll
-                    for (int u = 0; u < 2; u++) fst[u][k] = 0;
+                    for (int u = 0; u < RP; u++) fst[u][k] = 0;
                 } else if (k > 0 && n == 1) {
 #pragma unroll
-                    for (int u = 0; u < 2; u++) fst[u][k] = fen[u][k - 1] + 1;
+                    for (int u = 0; u < RP; u++) fst[u][k] = fen[u][k - 1] + 1;
                 } else {
                     for (uint32_t i = k == 0 ? 1u : 2u; i < n; i++) {
 #pragma unroll
-                        for (int u = 0; u < 2; u++) sv[u] &= sv[u] - 1;
+                        for (int u = 0; u < RP; u++) sv[u] &= sv[u] - 1;
                     }
 #pragma unroll
-                    for (int u = 0; u < 2; u++) {
+                    for (int u = 0; u < RP; u++) {
                         fst[u][k] = ctz64(sv[u]) + 1;
                         sv[u] &= sv[u] - 1;
                     }
                 }
 #pragma unroll
-                for (int u = 0; u < 2; u++) fen[u][k] = ctz64(sv[u]);
+                for (int u = 0; u < RP; u++) fen[u][k] = ctz64(sv[u]);
             }
 #pragma unroll
-            for (int u = 0; u < 2; u++) {
+            for (int u = 0; u < RP; u++) {
                 // the last role's field must end inside the view and at or before the
                 // record's terminator (else the row is short or longer than the view)
                 const uint32_t en = fen[u][NR - 1];
@@ -664,17 +664,17 @@ __global__ __launch_bounds__(LT) void fast_kernel(const uint8_t* __restrict__ g,
             const bool last_pass = !__any(todo != 0);
             if (wq) {                                                // a quote in front of a needed field
 #pragma unroll
-                for (int u = 0; u < 2; u++) {
+                for (int u = 0; u < RP; u++) {
                     const uint32_t lp = fen[u][NR - 1] < 63 ? fen[u][NR - 1] : 63u;
                     fail[u] |= (qview(W, p[u]) & ((2ULL << lp) - 1)) != 0;
                 }
             }
 
             // ---- each role's field: compile-time ranks (CANON) or the plan's (uniform selects)
-            uint32_t wst[2] = {0, 0}, wen[2] = {0, 0}, gst[2] = {0, 0}, gen[2] = {0, 0};
-            uint32_t sst[2][MAXS] = {{0, 0}, {0, 0}}, sen[2][MAXS] = {{0, 0}, {0, 0}};
+            uint32_t wst[RP] = {}, wen[RP] = {}, gst[RP] = {}, gen[RP] = {};
+            uint32_t sst[RP][MAXS] = {}, sen[RP][MAXS] = {};
 #pragma unroll
-            for (int u = 0; u < 2; u++) {
+            for (int u = 0; u < RP; u++) {
                 auto pick = [&](uint32_t r, uint32_t& a, uint32_t& b) {
                     a = fst[u][0];
                     b = fen[u][0];
@@ -703,9 +703,9 @@ __global__ __launch_bounds__(LT) void fast_kernel(const uint8_t* __restrict__ g,
             continue;
 #endif
             // ---- field bytes (one batch of LDS reads)
-            uint32_t wd[2], sd[2][MAXS], k0[2], k1[2];
+            uint32_t wd[RP], sd[RP][MAXS], k0[RP], k1[RP];
 #pragma unroll
-            for (int u = 0; u < 2; u++) {
+            for (int u = 0; u < RP; u++) {
                 if (WHERE) wd[u] = ld4a(pa[u] + wst[u]);
 #pragma unroll
                 for (int j = 0; j < NS; j++) sd[u][j] = ld4a(pa[u] + sst[u][j]);
@@ -713,12 +713,14 @@ __global__ __launch_bounds__(LT) void fast_kernel(const uint8_t* __restrict__ g,
             }
 
             // ---- WHERE outcome (wu: a field the 4-byte numeral path could not type)
-            bool pass[2] = {true, true};
-            bool wu[2] = {false, false};
+            bool pass[RP];
+            bool wu[RP];
+#pragma unroll
+            for (int u = 0; u < RP; u++) { pass[u] = true; wu[u] = false; }
             if (WHERE) {
                 bool wide = false;
 #pragma unroll
-                for (int u = 0; u < 2; u++) {
+                for (int u = 0; u < RP; u++) {
                     const uint32_t len = wen[u] - wst[u];
                     const Num n = num4<false>(wd[u], len);
                     pass[u] = len == 0 ? pass_null : ((n.M - wa <= ww) != wneg);
@@ -727,7 +729,7 @@ __global__ __launch_bounds__(LT) void fast_kernel(const uint8_t* __restrict__ g,
                 }
                 if (__any(wide)) {                                   // DOUBLE or 5-7 byte numerals
 #pragma unroll
-                    for (int u = 0; u < 2; u++) {
+                    for (int u = 0; u < RP; u++) {
                         if (wu[u]) {
                             const uint32_t len = wen[u] - wst[u];
                             uint32_t d0, d1;
@@ -751,15 +753,15 @@ __global__ __launch_bounds__(LT) void fast_kernel(const uint8_t* __restrict__ g,
 
             // ---- SUM addends: fixed point (10^-3) for numerals of <= 4 bytes (<= 3 decimals);
             //      5-7 byte numerals as strtod's double; su: not typed here
-            uint64_t sfix[2][MAXS];
-            double sdbl[2][MAXS];
-            bool hspill[2] = {false, false};   // an addend only the HBM table can take (NS == 2, > 3 decimals)
-            bool snum[2][MAXS], sfx[2][MAXS], su[2] = {false, false};
+            uint64_t sfix[RP][MAXS];
+            double sdbl[RP][MAXS];
+            bool hspill[RP] = {};   // an addend only the HBM table can take (NS == 2, > 3 decimals)
+            bool snum[RP][MAXS], sfx[RP][MAXS], su[RP] = {};
 #pragma unroll
             for (int j = 0; j < NS; j++) {
-                bool wide = false, sw[2];
+                bool wide = false, sw[RP];
 #pragma unroll
-                for (int u = 0; u < 2; u++) {
+                for (int u = 0; u < RP; u++) {
                     const uint32_t len = sen[u][j] - sst[u][j];
                     const Num n = num4<true>(sd[u][j], len);
 #ifdef FAST_OLD_NUMK
@@ -777,7 +779,7 @@ __global__ __launch_bounds__(LT) void fast_kernel(const uint8_t* __restrict__ g,
                 }
                 if (__any(wide)) {
 #pragma unroll
-                    for (int u = 0; u < 2; u++) {
+                    for (int u = 0; u < RP; u++) {
                         if (sw[u]) {
                             const uint32_t len = sen[u][j] - sst[u][j];
                             uint32_t d0, d1;
@@ -799,17 +801,17 @@ __global__ __launch_bounds__(LT) void fast_kernel(const uint8_t* __restrict__ g,
                     }
                 }
 #pragma unroll
-                for (int u = 0; u < 2; u++) su[u] |= sw[u];
+                for (int u = 0; u < RP; u++) su[u] |= sw[u];
             }
 #pragma unroll
-            for (int u = 0; u < 2; u++) fail[u] |= wu[u] | su[u];
+            for (int u = 0; u < RP; u++) fail[u] |= wu[u] | su[u];
 
             // ---- GROUP BY key: the raw field bytes (<= 8, none <= ' '), zero padded
-            uint64_t tag[2] = {0, 0};
-            uint32_t hb[2] = {0, 0};
+            uint64_t tag[RP] = {};
+            uint32_t hb[RP] = {};
             if (GROUPED) {
 #pragma unroll
-                for (int u = 0; u < 2; u++) {
+                for (int u = 0; u < RP; u++) {
                     const uint32_t klen = gen[u] - gst[u];
                     const uint32_t m0 = len_mask(klen, 0), m1 = len_mask(klen, 1);
                     const uint32_t a0 = k0[u] & m0, a1 = k1[u] & m1;
@@ -826,7 +828,7 @@ __global__ __launch_bounds__(LT) void fast_kernel(const uint8_t* __restrict__ g,
 
             // ---- declined records go whole to slow_kernel
 #pragma unroll
-            for (int u = 0; u < 2; u++) {
+            for (int u = 0; u < RP; u++) {
                 const bool slow = valid[u] & fail[u];
                 const uint64_t sb = __ballot(slow);
                 if (sb) {
@@ -847,7 +849,7 @@ __global__ __launch_bounds__(LT) void fast_kernel(const uint8_t* __restrict__ g,
             // ---- aggregate
             if (!GROUPED) {
 #pragma unroll
-                for (int u = 0; u < 2; u++) {
+                for (int u = 0; u < RP; u++) {
                     my_cnt += pass[u] ? 1u : 0u;
                     my_first = pass[u] ? min(my_first, fcw | p[u]) : my_first;
 #pragma unroll
@@ -860,20 +862,20 @@ __global__ __launch_bounds__(LT) void fast_kernel(const uint8_t* __restrict__ g,
                 }
             } else {
                 // lookup: the key's two buckets (one 16-byte LDS read each)
-                int slot[2];
-                bool miss[2];
+                int slot[RP];
+                bool miss[RP];
 #ifndef FAST_OLD_LK
                 // both records' bucket reads issued before any compare (one LDS wait per pass)
-                v4u xs[2], ys[2];
+                v4u xs[RP], ys[RP];
 #pragma unroll
-                for (int u = 0; u < 2; u++) {
+                for (int u = 0; u < RP; u++) {
                     const uint32_t b1 = hb[u] & (TBUCKETS - 1), b2 = (hb[u] >> 16) & (TBUCKETS - 1);
                     xs[u] = ((const v4u*)T)[b1];
                     ys[u] = ((const v4u*)T)[b2];
                 }
 #endif
 #pragma unroll
-                for (int u = 0; u < 2; u++) {
+                for (int u = 0; u < RP; u++) {
                     const uint32_t b1 = hb[u] & (TBUCKETS - 1), b2 = (hb[u] >> 16) & (TBUCKETS - 1);
 #ifndef FAST_OLD_LK
                     const v4u x = xs[u], y = ys[u];
@@ -893,9 +895,12 @@ __global__ __launch_bounds__(LT) void fast_kernel(const uint8_t* __restrict__ g,
                     slot[u] = s;
                     miss[u] = pass[u] & (s < 0) & !hspill[u];
                 }
-                if (__any(miss[0] | miss[1])) {                      // keys the seed did not place
+                bool anym = false;
 #pragma unroll
-                    for (int u = 0; u < 2; u++) {
+                for (int u = 0; u < RP; u++) anym |= miss[u];
+                if (__any(anym)) {                                   // keys the seed did not place
+#pragma unroll
+                    for (int u = 0; u < RP; u++) {
                         if (miss[u]) {
                             const uint32_t b1 = hb[u] & (TBUCKETS - 1), b2 = (hb[u] >> 16) & (TBUCKETS - 1);
                             const uint32_t cand[4] = {2 * b1, 2 * b1 + 1, 2 * b2, 2 * b2 + 1};
@@ -907,7 +912,7 @@ __global__ __launch_bounds__(LT) void fast_kernel(const uint8_t* __restrict__ g,
                     }
                 }
 #pragma unroll
-                for (int u = 0; u < 2; u++) {
+                for (int u = 0; u < RP; u++) {
                     slot[u] = hspill[u] ? -1 : slot[u];
                     const bool add = pass[u] & (slot[u] >= 0);
                     uint8_t* r = S + (uint32_t)slot[u] * SLOT_BYTES;
@@ -1596,19 +1601,29 @@ bool fast_shape(const ScanPlan* P, int grouped, FastPlan* fp, int* ns, bool* whe
 typedef void (*fast_fn_t)(const uint8_t*, ScanStats*, unsigned long long*, unsigned long long, const FastPlan,
                           const GroupTable*);
 
+// rp3: three records per lane pass (records shorter than ~33 bytes: a lane's 64
+// bytes usually hold three starts, and a two-record pass would run a second pass
+// for the few lanes with a third); ungrouped plans only, the grouped kernels keep
+// two (register budget of the lookup and atomics)
 template <bool G, bool WH, bool COMMA, bool CANON>
-fast_fn_t pick_ns(int ns) {
-    if (ns == 0) return fast::fast_kernel<G, WH, 0, COMMA, CANON>;
-    return ns == 1 ? fast::fast_kernel<G, WH, 1, COMMA, CANON> : fast::fast_kernel<G, WH, 2, COMMA, CANON>;
+fast_fn_t pick_ns(int ns, bool rp3) {
+    if constexpr (!G) {
+        if (rp3) {
+            if (ns == 0) return fast::fast_kernel<G, WH, 0, COMMA, CANON, 3>;
+            return ns == 1 ? fast::fast_kernel<G, WH, 1, COMMA, CANON, 3> : fast::fast_kernel<G, WH, 2, COMMA, CANON, 3>;
+        }
+    }
+    if (ns == 0) return fast::fast_kernel<G, WH, 0, COMMA, CANON, 2>;
+    return ns == 1 ? fast::fast_kernel<G, WH, 1, COMMA, CANON, 2> : fast::fast_kernel<G, WH, 2, COMMA, CANON, 2>;
 }
 template <bool G, bool CANON>
-fast_fn_t pick_wc(bool where, int ns, bool comma) {
-    if (where) return comma ? pick_ns<G, true, true, CANON>(ns) : pick_ns<G, true, false, CANON>(ns);
-    return comma ? pick_ns<G, false, true, CANON>(ns) : pick_ns<G, false, false, CANON>(ns);
+fast_fn_t pick_wc(bool where, int ns, bool comma, bool rp3) {
+    if (where) return comma ? pick_ns<G, true, true, CANON>(ns, rp3) : pick_ns<G, true, false, CANON>(ns, rp3);
+    return comma ? pick_ns<G, false, true, CANON>(ns, rp3) : pick_ns<G, false, false, CANON>(ns, rp3);
 }
 template <bool G>
-fast_fn_t pick_fast(bool where, int ns, bool comma, bool canon) {
-    return canon ? pick_wc<G, true>(where, ns, comma) : pick_wc<G, false>(where, ns, comma);
+fast_fn_t pick_fast(bool where, int ns, bool comma, bool canon, bool rp3) {
+    return canon ? pick_wc<G, true>(where, ns, comma, rp3) : pick_wc<G, false>(where, ns, comma, rp3);
 }
 
 size_t fast_lds(int grouped, int ns) {
@@ -1645,6 +1660,11 @@ hipError_t cq_launch_fast(const uint8_t* g, const cq::ScanPlan* P, const cq::Gro
     const uint64_t lo = P->data_begin > P->range_begin ? P->data_begin : P->range_begin;
     fp.ws = P->lean_ws ? P->lean_ws : (uint32_t)fast::WS;
     if (fp.ws > (uint32_t)fast::WS || fp.ws % 128) return hipErrorInvalidValue;
+    // the sampled stride is 120 records' worth (lean_kernel's choice): below the
+    // largest stride the records average under 33 bytes -> the three-record pass,
+    // over windows of the largest stride (test knob CQGPU_FAST_RP2: keep two)
+    const bool rp3 = !grouped && fp.ws < (uint32_t)fast::WS && !getenv("CQGPU_FAST_RP2");
+    if (rp3) fp.ws = (uint32_t)fast::WS;
     if (hi > lo) {
         const uint64_t wl = lo / fp.ws, wh = (hi - 1) / fp.ws;
         if (wh - wl + 1 >= (1ull << 31)) return hipErrorInvalidValue;
@@ -1668,7 +1688,8 @@ hipError_t cq_launch_fast(const uint8_t* g, const cq::ScanPlan* P, const cq::Gro
     hipError_t e = cq::upload_buffer(tabs_dev[dev & 63], tabs, sizeof tabs, s);
     if (e != hipSuccess) return e;
     const bool comma = P->delim == ',' && P->quote == '"';
-    const fast_fn_t fn = grouped ? pick_fast<true>(where, ns, comma, canon) : pick_fast<false>(where, ns, comma, canon);
+    const fast_fn_t fn = grouped ? pick_fast<true>(where, ns, comma, canon, false)
+                                 : pick_fast<false>(where, ns, comma, canon, rp3);
     const size_t lds = fast_lds(grouped, ns);
     cq::set_max_lds((const void*)fn, (int)lds);
     hipLaunchKernelGGL(fn, dim3(grid), dim3(fast::LT), lds, s, g, stats, slow_list, slow_cap, fp,
