@@ -211,3 +211,32 @@ def test_slow_list_overflow_rescan(d, monkeypatch):
         assert not inel, inel
         _cmp(got, want, _tol(sql), "slow cap: " + sql)
         assert st["slow_records"] > 512, st
+
+
+@pytest.mark.parametrize("rp2", [False, True])
+def test_fast_three_record_pass(d, monkeypatch, rp2):
+    """ungrouped plans over records shorter than ~33 bytes take the three-records-per-
+    lane pass over windows of the largest stride (config 2's Shape A is 29.9 B/row);
+    CQGPU_FAST_RP2 keeps the two-record pass: both must match the oracle, including
+    lanes with four record starts (18-byte records), mixed with long records and a
+    window whose records a chunk cut splits"""
+    from cq_amd import datagen
+    if rp2:
+        monkeypatch.setenv("CQGPU_FAST_RP2", "1")
+    p = d / "shape_a.csv"
+    p.write_bytes(datagen.shape_a_bytes(150_000, seed=5, with_role=False))
+    for sql in (f"SELECT COUNT(*) FROM '{p}' WHERE age > 30",
+                f"SELECT COUNT(*), SUM(height), AVG(height) FROM '{p}' WHERE age <= 44",
+                f"SELECT COUNT(*), SUM(age) FROM '{p}'"):
+        check(sql)
+    rng = np.random.default_rng(9)
+    rows = []
+    for i in range(120_000):
+        if i % 97 == 0:
+            rows.append("x" * int(rng.integers(40, 90)) + ",%d,1.5" % rng.integers(0, 99))
+        else:
+            rows.append("%s,%d,%d.%d" % ("ab"[i % 2] * int(rng.integers(1, 6)), rng.integers(0, 99),
+                                         rng.integers(0, 9), rng.integers(0, 9)))
+    q = _write(d / "tiny.csv", "name,age,height", rows)
+    check(f"SELECT COUNT(*), SUM(height), AVG(height) FROM '{q}' WHERE age > 50")
+    check(f"SELECT COUNT(*) FROM '{q}'")
