@@ -3797,6 +3797,12 @@ cqgpu_table* cqgpu_table_open(const char* path, cq_csv_config cfg) {
     } catch (HipError& e) {
         set_err("cq_amd: %s", e.msg.c_str());
         return nullptr;
+    } catch (std::exception& e) {
+        set_err("cq_amd: %s", e.what());
+        return nullptr;
+    } catch (...) {
+        set_err("cq_amd: %s", "unexpected C++ exception");
+        return nullptr;
     }
 }
 
@@ -3806,6 +3812,12 @@ cqgpu_table* cqgpu_table_from_bytes(const void* data, size_t n, cq_csv_config cf
         return upload((const uint8_t*)data, n, cfg, base_offset, header, header_len);
     } catch (HipError& e) {
         set_err("cq_amd: %s", e.msg.c_str());
+        return nullptr;
+    } catch (std::exception& e) {
+        set_err("cq_amd: %s", e.what());
+        return nullptr;
+    } catch (...) {
+        set_err("cq_amd: %s", "unexpected C++ exception");
         return nullptr;
     }
 }
@@ -3844,6 +3856,12 @@ cqgpu_table* cqgpu_table_open_range(const char* path, cq_csv_config cfg, int ran
         else t = upload(d + lo, hi - lo, cfg, lo, (const char*)d + hl, hh - hl);
     } catch (HipError& e) {
         set_err("cq_amd: %s", e.msg.c_str());
+        t = nullptr;
+    } catch (std::exception& e) {
+        set_err("cq_amd: %s", e.what());
+        t = nullptr;
+    } catch (...) {
+        set_err("cq_amd: %s", "unexpected C++ exception");
         t = nullptr;
     }
     munmap(m, n);
@@ -3941,6 +3959,12 @@ int cqgpu_route_plan(cq_node* q, cqgpu_table* const* tables, int ntables, int si
     } catch (HipError& e) {
         set_err("cq_amd: %s", e.msg.c_str());
         return -1;
+    } catch (std::exception& e) {
+        set_err("cq_amd: %s", e.what());
+        return -1;
+    } catch (...) {
+        set_err("cq_amd: %s", "unexpected C++ exception");
+        return -1;
     }
 }
 
@@ -3962,6 +3986,12 @@ int cqgpu_route_fill(cqgpu_table* t, uint64_t gid_base, void* dev_bytes, uint64_
         return 0;
     } catch (HipError& e) {
         set_err("cq_amd: %s", e.msg.c_str());
+        return -1;
+    } catch (std::exception& e) {
+        set_err("cq_amd: %s", e.what());
+        return -1;
+    } catch (...) {
+        set_err("cq_amd: %s", "unexpected C++ exception");
         return -1;
     }
 }
@@ -3991,6 +4021,14 @@ cqgpu_table* cqgpu_table_from_routed(const void* dev_bytes, size_t n, const uint
         return t;
     } catch (HipError& e) {
         set_err("cq_amd: %s", e.msg.c_str());
+        cqgpu_table_free(t);
+        return nullptr;
+    } catch (std::exception& e) {
+        set_err("cq_amd: %s", e.what());
+        cqgpu_table_free(t);
+        return nullptr;
+    } catch (...) {
+        set_err("cq_amd: %s", "unexpected C++ exception");
         cqgpu_table_free(t);
         return nullptr;
     }
@@ -4037,6 +4075,12 @@ cq_table* cqgpu_query(cq_node* q, cqgpu_table* const* tables, int ntables) {
     } catch (HipError& e) {
         set_err("cq_amd: %s", e.msg.c_str());
         return nullptr;
+    } catch (std::exception& e) {
+        set_err("cq_amd: %s", e.what());
+        return nullptr;
+    } catch (...) {
+        set_err("cq_amd: %s", "unexpected C++ exception");
+        return nullptr;
     }
 }
 
@@ -4080,6 +4124,12 @@ cq_table* evaluate_query(cq_node* q) {
             t = cached_open(path, global_csv_config, &own);
         } catch (HipError& e) {
             set_err("cq_amd: %s", e.msg.c_str());
+            t = nullptr;
+        } catch (std::exception& e) {
+            set_err("cq_amd: %s", e.what());
+            t = nullptr;
+        } catch (...) {
+            set_err("cq_amd: %s", "unexpected C++ exception");
             t = nullptr;
         }
         if (!t) set_err("Error loading file: %s", path);
@@ -4176,6 +4226,12 @@ int cqgpu_explain(cq_node* q, const char* header, cq_csv_config cfg, char* out, 
     } catch (HipError& e) {
         snprintf(out, cap, "error: %s\n", e.msg.c_str());
         return 2;
+    } catch (std::exception& e) {
+        snprintf(out, cap, "error: %s\n", e.what());
+        return 2;
+    } catch (...) {
+        snprintf(out, cap, "error: %s\n", "unexpected C++ exception");
+        return 2;
     }
 }
 
@@ -4198,6 +4254,12 @@ size_t cqgpu_debug_all_records(cqgpu_table* t, int method, unsigned long long* o
         return (size_t)-1;
     } catch (HipError& e) {
         set_err("cq_amd: %s", e.msg.c_str());
+        return (size_t)-1;
+    } catch (std::exception& e) {
+        set_err("cq_amd: %s", e.what());
+        return (size_t)-1;
+    } catch (...) {
+        set_err("cq_amd: %s", "unexpected C++ exception");
         return (size_t)-1;
     }
 }
@@ -4230,6 +4292,12 @@ size_t cqgpu_debug_records(cqgpu_table* t, unsigned long long* out, size_t cap) 
         return (size_t)st.rows_emitted;
     } catch (HipError& e) {
         set_err("cq_amd: %s", e.msg.c_str());
+        return 0;
+    } catch (std::exception& e) {
+        set_err("cq_amd: %s", e.what());
+        return 0;
+    } catch (...) {
+        set_err("cq_amd: %s", "unexpected C++ exception");
         return 0;
     }
 }
@@ -4283,6 +4351,12 @@ cq_table* cqgpu_debug_scan_cells(cqgpu_table* t, const int* cols, int ncols, uns
     } catch (HipError& e) {
         set_err("cq_amd: %s", e.msg.c_str());
         return nullptr;
+    } catch (std::exception& e) {
+        set_err("cq_amd: %s", e.what());
+        return nullptr;
+    } catch (...) {
+        set_err("cq_amd: %s", "unexpected C++ exception");
+        return nullptr;
     }
 }
 
@@ -4329,6 +4403,12 @@ cq_table* cqgpu_debug_cells(cqgpu_table* t, const int* cols, int ncols, const un
         return r;
     } catch (HipError& e) {
         set_err("cq_amd: %s", e.msg.c_str());
+        return nullptr;
+    } catch (std::exception& e) {
+        set_err("cq_amd: %s", e.what());
+        return nullptr;
+    } catch (...) {
+        set_err("cq_amd: %s", "unexpected C++ exception");
         return nullptr;
     }
 }
@@ -4489,6 +4569,12 @@ size_t cqgpu_query_partial(cq_node* q, cqgpu_table* const* tables, int ntables, 
         return 0;
     } catch (HipError& e) {
         set_err("cq_amd: %s", e.msg.c_str());
+        return 0;
+    } catch (std::exception& e) {
+        set_err("cq_amd: %s", e.what());
+        return 0;
+    } catch (...) {
+        set_err("cq_amd: %s", "unexpected C++ exception");
         return 0;
     }
 }
@@ -4751,6 +4837,12 @@ cq_table* cqgpu_merge_partials(cq_node* q, const void* const* blobs, const size_
     } catch (HipError& e) {
         set_err("cq_amd: %s", e.msg.c_str());
         return nullptr;
+    } catch (std::exception& e) {
+        set_err("cq_amd: %s", e.what());
+        return nullptr;
+    } catch (...) {
+        set_err("cq_amd: %s", "unexpected C++ exception");
+        return nullptr;
     }
 }
 
@@ -5003,6 +5095,12 @@ cqgpu_partial* cqgpu_partial_new(cq_node* q, cqgpu_table* const* tables, int nta
         return nullptr;
     } catch (HipError& e) {
         set_err("cq_amd: %s", e.msg.c_str());
+        return nullptr;
+    } catch (std::exception& e) {
+        set_err("cq_amd: %s", e.what());
+        return nullptr;
+    } catch (...) {
+        set_err("cq_amd: %s", "unexpected C++ exception");
         return nullptr;
     }
 }
@@ -5278,6 +5376,12 @@ int cqgpu_partial_next(cqgpu_partial* p, const void* result, const uint64_t* res
     } catch (HipError& e) {
         set_err("cq_amd: %s", e.msg.c_str());
         return -1;
+    } catch (std::exception& e) {
+        set_err("cq_amd: %s", e.what());
+        return -1;
+    } catch (...) {
+        set_err("cq_amd: %s", "unexpected C++ exception");
+        return -1;
     }
 }
 
@@ -5306,6 +5410,12 @@ int cqgpu_partial_put(cqgpu_partial* p, void* dev_dst) {
         return 0;
     } catch (HipError& e) {
         set_err("cq_amd: %s", e.msg.c_str());
+        return -1;
+    } catch (std::exception& e) {
+        set_err("cq_amd: %s", e.what());
+        return -1;
+    } catch (...) {
+        set_err("cq_amd: %s", "unexpected C++ exception");
         return -1;
     }
 }
@@ -5446,6 +5556,12 @@ cq_table* cqgpu_partial_result(cqgpu_partial* p, cq_node* q) {
         return nullptr;
     } catch (HipError& e) {
         set_err("cq_amd: %s", e.msg.c_str());
+        return nullptr;
+    } catch (std::exception& e) {
+        set_err("cq_amd: %s", e.what());
+        return nullptr;
+    } catch (...) {
+        set_err("cq_amd: %s", "unexpected C++ exception");
         return nullptr;
     }
 }

@@ -657,15 +657,22 @@ __global__ __launch_bounds__(LT) void fast_kernel(const uint8_t* __restrict__ g,
 #pragma unroll
             for (int u = 0; u < RP; u++) {
                 // the last role's field must end inside the view and at or before the
-                // record's terminator (else the row is short or longer than the view)
-                const uint32_t en = fen[u][NR - 1];
-                fail[u] = !valid[u] | (en >= 64u) | (en > e[u]);
+                // record's terminator (else the row is short or longer than the view);
+                // with no role at all (COUNT(*), no WHERE) every record counts as it is
+                // (record splitting is quote-blind, csv_reader.c:404-408)
+                if constexpr (NR == 0) {
+                    fail[u] = !valid[u];
+                } else {
+                    const uint32_t en = fen[u][NR - 1];
+                    fail[u] = !valid[u] | (en >= 64u) | (en > e[u]);
+                }
             }
             const bool last_pass = !__any(todo != 0);
-            if (wq) {                                                // a quote in front of a needed field
+            if (NR > 0 && wq) {                                      // a quote in front of a needed field
 #pragma unroll
                 for (int u = 0; u < RP; u++) {
-                    const uint32_t lp = fen[u][NR - 1] < 63 ? fen[u][NR - 1] : 63u;
+                    const uint32_t lr = fen[u][NR > 0 ? NR - 1 : 0];
+                    const uint32_t lp = lr < 63 ? lr : 63u;
                     fail[u] |= (qview(W, p[u]) & ((2ULL << lp) - 1)) != 0;
                 }
             }
@@ -855,8 +862,8 @@ __global__ __launch_bounds__(LT) void fast_kernel(const uint8_t* __restrict__ g,
 #pragma unroll
                     for (int j = 0; j < NS; j++) {
                         const bool on = pass[u] & snum[u][j];
-                        my_fix[j] += on & sfx[u][j] ? sfix[u][j] : 0u;
-                        my_dbl[j] += on & !sfx[u][j] ? sdbl[u][j] : 0.0;
+                        my_fix[j] += (on & sfx[u][j]) ? sfix[u][j] : 0u;
+                        my_dbl[j] += (on & !sfx[u][j]) ? sdbl[u][j] : 0.0;
                         my_num[j] += on ? 1u : 0u;
                     }
                 }

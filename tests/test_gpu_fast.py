@@ -240,3 +240,19 @@ def test_fast_three_record_pass(d, monkeypatch, rp2):
     q = _write(d / "tiny.csv", "name,age,height", rows)
     check(f"SELECT COUNT(*), SUM(height), AVG(height) FROM '{q}' WHERE age > 50")
     check(f"SELECT COUNT(*) FROM '{q}'")
+
+
+def test_fast_count_star_no_roles(d):
+    """`SELECT COUNT(*) FROM f` with no WHERE has no role at all (NR = 0): every
+    record counts as it is -- quotes, records longer than the 64-byte view, short
+    and ragged rows, blank lines, CR / CRLF runs -- and none goes to slow_kernel"""
+    rng = np.random.default_rng(12)
+    rows = []
+    for i in range(200_000):
+        r = int(rng.integers(0, 8))
+        rows.append(['a,1', '"q,x",2', 'x' * int(rng.integers(70, 200)) + ',3', 'z', '"', ',,', ' ', 'k,"y"'][r])
+    body = "h1,h2\n" + "\n".join(rows[:100_000]) + "\r\n\r\n" + "\r".join(rows[100_000:]) + "\n\n"
+    p = d / "nroles.csv"
+    p.write_text(body)
+    st = check(f"SELECT COUNT(*) FROM '{p}'")
+    assert st["slow_records"] == 0, st
