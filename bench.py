@@ -211,6 +211,11 @@ def main():
             dist.init_process_group("nccl", device_id=torch.device("cuda", local))
             dist.barrier()
             torch.cuda.synchronize()
+            if not os.environ.get("CQ_BENCH_DIST_PY"):
+                # the library's own RCCL communicator (the whole N > 1 step runs inside it)
+                from cq_amd.dist import init_library_comm
+                init_library_comm()
+                torch.cuda.synchronize()
         finally:
             sys.stdout.flush()
             os.dup2(saved, 1)
@@ -218,7 +223,7 @@ def main():
 
     import cq_amd
     from cq_amd import abi
-    from cq_amd.dist import scan_partitioned_dense
+    from cq_amd.dist import scan_partitioned_dense, scan_partitioned_rccl
     L = cq_amd.lib()
 
     t0 = time.time()
@@ -237,6 +242,7 @@ def main():
     ast = C.pointer(q)
     kernel_used = [1]
     last_stats = [{}]
+    merge_path = [None]
 
     def step():
         """one query; returns (result pointer on rank 0 or None, scan ms)"""
@@ -250,9 +256,14 @@ def main():
             kernel_used[0] = st.get("scan_kernel", 0)
             last_stats[0] = st
             return tp, st["scan_ms"]
-        # partial groups stay in HBM; key all_gather + dense MIN/SUM reduces over RCCL,
-        # rank 0 finishes (scan_partitioned's blob gather only for plans off the dense path)
-        tp = scan_partitioned_dense(ast, table)
+        if os.environ.get("CQ_BENCH_DIST_PY"):
+            # A/B: round 3's Python-driven dense merge (torch.distributed collectives)
+            tp = scan_partitioned_dense(ast, table)
+            merge_path[0] = "dense (python-driven)"
+        else:
+            # the whole step inside the library over its RCCL communicator: config 4's
+            # plan takes the gather-merge (one grouped send/recv to rank 0, device merge)
+            tp, merge_path[0] = scan_partitioned_rccl(ast, table)
         st = cq_amd.stats()                   # the merge runs no scan: still this rank's partial
         kernel_used[0] = st.get("scan_kernel", 0)
         last_stats[0] = st
@@ -370,8 +381,8 @@ def main():
                 "rows_per_gpu": hi - lo,
                 "bytes_per_gpu": nbytes,
                 "groups": 1000 if role else 1,
-                "parallelism": (f"dp{world} (rows [r*T/N, (r+1)*T/N) per rank, RCCL all_gather of partials)"
-                                if world > 1 else "dp1"),
+                "parallelism": (f"dp{world} (rows [r*T/N, (r+1)*T/N) per rank; merge inside libcqgpu over "
+                                "RCCL: " + str(merge_path[0]) + ")" if dist is not None else "dp1"),
             },
             "verified": ok,
             "verified_against": exp_src,

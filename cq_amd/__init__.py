@@ -28,7 +28,8 @@ class Stats(C.Structure):
     _fields_ = [("scan_ms", C.c_double), ("total_ms", C.c_double), ("scan_bytes", C.c_uint64),
                 ("records", C.c_uint64), ("groups", C.c_uint64), ("lds_spills", C.c_uint64),
                 ("grid", C.c_int), ("path", C.c_int), ("retries", C.c_int),
-                ("slow_records", C.c_uint64), ("passed", C.c_uint64), ("scan_kernel", C.c_int)]
+                ("slow_records", C.c_uint64), ("passed", C.c_uint64), ("scan_kernel", C.c_int),
+                ("wide", C.c_int)]
 
 
 def lib():
@@ -84,6 +85,15 @@ def lib():
         L.cqgpu_partial_result.restype = TP
         L.cqgpu_partial_result.argtypes = [vp, C.POINTER(abi.Node)]
         L.cqgpu_partial_free.argtypes = [vp]
+        L.cqgpu_comm_unique_id.restype = C.c_int
+        L.cqgpu_comm_unique_id.argtypes = [vp]
+        L.cqgpu_comm_init.restype = C.c_int
+        L.cqgpu_comm_init.argtypes = [vp, C.c_int, C.c_int]
+        L.cqgpu_comm_destroy.argtypes = []
+        L.cqgpu_dist_query.restype = TP
+        L.cqgpu_dist_query.argtypes = [C.POINTER(abi.Node), vp, C.POINTER(C.c_int), C.POINTER(C.c_int)]
+        L.cqgpu_gm_local.restype = TP
+        L.cqgpu_gm_local.argtypes = [C.POINTER(abi.Node), C.POINTER(vp), C.c_int]
         L.cqgpu_last_stats.argtypes = [C.POINTER(Stats)]
         L.cqgpu_last_error.restype = C.c_char_p
         L.cqgpu_last_ineligible.restype = C.c_char_p
@@ -252,3 +262,47 @@ def last_error() -> str:
 
 def last_ineligible() -> str:
     return (lib().cqgpu_last_ineligible() or b"").decode("latin-1")
+
+
+# ---- the N > 1 step inside the library over RCCL (cqgpu.h cqgpu_dist_query)
+COMM_ID_BYTES = 128
+DIST_PATHS = {1: "gather-merge", 2: "dense", 3: "blobs"}
+
+
+def comm_unique_id() -> bytes:
+    """rank 0: a fresh RCCL unique id (to broadcast to the other ranks)"""
+    buf = C.create_string_buffer(COMM_ID_BYTES)
+    if lib().cqgpu_comm_unique_id(buf) != 0:
+        raise RuntimeError(last_error() or "cqgpu_comm_unique_id failed")
+    return buf.raw
+
+
+def comm_init(uid: bytes, rank: int, world: int) -> None:
+    """every rank, once: the library's RCCL communicator on the current HIP device"""
+    buf = C.create_string_buffer(bytes(uid), COMM_ID_BYTES)
+    if lib().cqgpu_comm_init(buf, rank, world) != 0:
+        raise RuntimeError(last_error() or "cqgpu_comm_init failed")
+
+
+def comm_destroy() -> None:
+    lib().cqgpu_comm_destroy()
+
+
+def dist_query_raw(ast, table: "Table"):
+    """(result pointer or None, status, path): rank 0 gets the result; status -1
+    on every rank when any rank failed"""
+    st, path = C.c_int(0), C.c_int(0)
+    tp = lib().cqgpu_dist_query(ast, table.handle, C.byref(st), C.byref(path))
+    return (tp if tp else None), st.value, path.value
+
+
+def gm_local(ast, shards):
+    """test entry: the gather-merge over shards held by this process (simulated ranks)"""
+    arr, n = _tables_arg(shards)
+    tp = lib().cqgpu_gm_local(ast, arr, n)
+    if not tp:
+        return None
+    out = abi.table_to_py(tp)
+    lib().cqgpu_result_free(tp)
+    return out
+

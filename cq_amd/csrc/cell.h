@@ -709,7 +709,28 @@ struct TextHash {
         while (n) byte(t[--n]);
     }
 };
-CQ_HD bool joined_text_add(TextHash& h, const Cell& c, bool first) {
+// bytes [lo, lo + 16) of a rendered joined text and its whole length: two joined
+// texts are compared exactly window by window (scan.hip joined_text_equal)
+struct TextWindow {
+    uint64_t lo, pos = 0, w0 = 0, w1 = 0;
+    CQ_HDM explicit TextWindow(uint64_t l) : lo(l) {}
+    CQ_HDM void byte(uint8_t c) {
+        const uint64_t k = pos - lo;                  // (wraps above 16 before the window)
+        if (k < 8) w0 |= (uint64_t)c << (8 * k);
+        else if (k < 16) w1 |= (uint64_t)c << (8 * (k - 8));
+        pos++;
+    }
+    CQ_HDM void bytes(const uint8_t* p, uint32_t n) { for (uint32_t i = 0; i < n; i++) byte(p[i]); }
+    CQ_HDM void dec(uint64_t v, int mind) {
+        uint8_t t[20];
+        int n = 0;
+        do { t[n++] = (uint8_t)('0' + v % 10); v /= 10; } while (v);
+        while (n < mind) t[n++] = '0';
+        while (n) byte(t[--n]);
+    }
+};
+template <class H>
+CQ_HD bool joined_text_add(H& h, const Cell& c, bool first) {
     if (!first) h.byte('\t');
     switch (c.kind) {
         case K_NULL: h.bytes((const uint8_t*)"NULL", 4); break;

@@ -30,6 +30,8 @@
 #include <sys/stat.h>
 #include <unistd.h>
 
+#include <rccl/rccl.h>
+
 #include "../../include/cqgpu.h"
 #include "plan.h"
 
@@ -142,6 +144,15 @@ hipError_t cq_excl_sum_u64(void* temp, size_t* temp_bytes, const unsigned long l
 hipError_t cq_excl_sum_u32(void* temp, size_t* temp_bytes, const unsigned int* in, unsigned int* out, size_t n,
                            hipStream_t s);
 size_t cq_pack_result_bytes(unsigned int ng, int nacc, uint32_t ncell, uint32_t sb);
+hipError_t cq_launch_gm_pack(const cq::GroupOut* out, const unsigned int* count, unsigned int cap_out, int nacc,
+                             uint32_t R, const cq::Cell* cells, const uint8_t* bytes, uint32_t sb, uint32_t maxg,
+                             uint8_t* dst, const cq::ScanStats* stats, uint8_t* hdr, hipStream_t s);
+size_t cq_gm_scan_bytes(uint32_t T);
+hipError_t cq_launch_gm_merge(const uint8_t* buf, uint64_t B, uint32_t N, uint32_t maxg, int nacc, uint32_t R,
+                              int grouped, uint32_t sb, uint32_t* state, uint32_t* rec_of, uint32_t* first_of, uint32_t cap,
+                              uint32_t* slot_of, uint32_t* flag, uint32_t* dense, uint32_t* idx, void* scan_temp,
+                              size_t scan_temp_bytes, unsigned int* err, uint8_t* dst, unsigned int* gcount,
+                              uint8_t* mail, hipStream_t s);
 hipError_t cq_launch_raw_merge(const cq::GroupTable* gt, const cq::GroupTable* rt, int nacc, cq::ScanStats* stats,
                                hipStream_t s);
 uint64_t cq_jx_windows(uint64_t lo, uint64_t hi, uint32_t ws);
@@ -743,6 +754,9 @@ struct Compiled {
     // expression items evaluated on the host over each group's first-row cells:
     // OP_COL b = rep slot, OP_CONST b = literal index (C.lits)
     std::vector<std::vector<Insn>> hexpr;
+    // more than MAX_NEED distinct columns: the fused scans (registers per need slot)
+    // cannot take the plan; it runs on the cells path (parsed cell tables + PairView)
+    bool wide = false;
 };
 
 struct Compiler {
@@ -752,13 +766,14 @@ struct Compiler {
     Compiled& C;
     std::vector<Insn> code;
     int depth = 0, bdepth = 0;
-    int need_cap = MAX_NEED;         // distinct columns one plan may reference
+    int need_cap = MAX_WIDE;         // distinct columns one plan may reference (> MAX_NEED: the cells path)
     int lit_cap = MAX_CONST;
 
     int need(int col) {
         auto it = std::find(C.need_cols.begin(), C.need_cols.end(), col);
         if (it != C.need_cols.end()) return (int)(it - C.need_cols.begin());
-        if ((int)C.need_cols.size() >= need_cap) throw Ineligible{"more than 8 referenced columns"};
+        if ((int)C.need_cols.size() >= need_cap)
+            throw Ineligible{"more than " + std::to_string(need_cap) + " referenced columns"};
         C.need_cols.push_back(col);
         return (int)C.need_cols.size() - 1;
     }
@@ -1001,7 +1016,9 @@ void finish_plan(const cqgpu_table* t, Compiled& C, Compiler& cc) {
     std::vector<int> sorted(order.size());
     for (size_t i = 0; i < order.size(); i++) sorted[remap[i]] = C.need_cols[i];
     C.P.nneed = (int)sorted.size();
-    for (int i = 0; i < C.P.nneed; i++) C.P.need_col[i] = (int16_t)sorted[i];
+    C.wide = C.P.nneed > MAX_NEED;
+    if (C.wide) g_stats.wide = 1;
+    for (int i = 0; i < C.P.nneed && i < MAX_NEED; i++) C.P.need_col[i] = (int16_t)sorted[i];
     C.P.max_col = C.P.nneed ? sorted.back() : -1;
     for (auto& in : cc.code) {
         if (in.op == OP_COL) {
@@ -1025,7 +1042,7 @@ void finish_plan(const cqgpu_table* t, Compiled& C, Compiler& cc) {
     C.P.range_end = t->n;
     C.P.lean_ws = t->lean_ws;
     C.P.fast_seed = 0;
-    if (C.P.group_slot >= 0) {
+    if (C.P.group_slot >= 0 && !C.wide) {
         const int gc = C.P.need_col[C.P.group_slot];
         C.P.lean_k16 = (uint32_t)((t->long_cols >> (gc < 63 ? gc : 63)) & 1);
         if (!C.P.lean_k16) C.P.fast_seed = (uint64_t)(uintptr_t)fast_seed_of(t, gc);
@@ -1049,7 +1066,7 @@ void compile_aggregate(const cqgpu_table* t, cq_node* q, Compiled& C) {
         // a GROUP BY name matching a SELECT alias groups by that item's expression
         // (evaluator.c:71-98)
         const int nk = gb->u.grp.nkeys;
-        if (nk > MAX_GPART) throw Ineligible{"GROUP BY of more than 8 parts"};
+        if (nk > MAX_GPART) throw Ineligible{"GROUP BY of more than " + std::to_string(MAX_GPART) + " parts"};
         std::vector<cq_node*> gexpr(nk, nullptr);
         cq_node* sel = q->u.q.select;
         for (int g = 0; g < nk; g++) {
@@ -1152,7 +1169,7 @@ void compile_aggregate(const cqgpu_table* t, cq_node* q, Compiled& C) {
             Compiled T;
             Compiler tc{t, q, alias, T};
             tc.lit_cap = MAX_CONST - (int)C.lits.size();
-            tc.need_cap = MAX_NEED;
+            tc.need_cap = MAX_WIDE;
             tc.expr(node);
             std::vector<Insn> code = tc.code;
             for (auto& in : code) {
@@ -1599,11 +1616,21 @@ std::vector<HGroup> make_groups(DevCtx& c, const Compiled& C, uint64_t limit, ui
 cq_table* build_direct(const Compiled& C, const uint8_t* hp, uint32_t ng, uint32_t ncell, uint32_t SB,
                        const std::vector<int>& rep_ord, const Literals& L, uint64_t limit);
 
+// gather-merge output of one rank (dist_query): its groups packed in the GM
+// layout (plan.h) into `dst` (header first; the caller zeroes the header's status)
+struct GmSend {
+    uint8_t* dst = nullptr;
+    uint32_t maxg = 0;
+    uint32_t ng = 0;                 // out: the rank's groups (may exceed maxg: declined)
+};
+
 // direct (optional): for plans build_direct handles, the result table built straight
-// from the packed result (no HGroup per group); the returned vector is then empty
+// from the packed result (no HGroup per group); the returned vector is then empty.
+// gm (optional): the groups packed for the gather-merge instead, nothing returned
 std::vector<HGroup> run_aggregate(DevCtx& c, const cqgpu_table* t, Compiled& C, Literals& L,
                                   ScanStats* stats_out, unsigned long long* row_out = nullptr,
-                                  unsigned long long row_cap = 0, cq_table** direct = nullptr) {
+                                  unsigned long long row_cap = 0, cq_table** direct = nullptr,
+                                  GmSend* gm = nullptr) {
     parse_literals(c, C.lits, L);
     for (size_t i = 0; i < L.cells.size(); i++) C.P.consts[i] = L.cells[i];
     PHASE("literals");
@@ -1625,7 +1652,8 @@ std::vector<HGroup> run_aggregate(DevCtx& c, const cqgpu_table* t, Compiled& C, 
     std::vector<int> rep_ord(C.rep_cols.size());
     for (size_t i = 0; i < rep_ord.size(); i++) rep_ord[i] = (int)i;
     std::sort(rep_ord.begin(), rep_ord.end(), [&](int a, int b) { return C.rep_cols[a] < C.rep_cols[b]; });
-    if (rep_ord.size() > (size_t)MAX_NEED) throw Ineligible{"too many representative columns"};
+    if (C.wide) throw HipError{"internal: a wide plan reached the fused scan"};
+    if (rep_ord.size() > (size_t)MAX_WIDE) throw Ineligible{"too many representative columns"};
     FD.ncols = (int32_t)rep_ord.size();
     for (size_t i = 0; i < rep_ord.size(); i++) FD.cols[i] = (int16_t)C.rep_cols[rep_ord[i]];
     FD.delim = C.P.delim;
@@ -1674,7 +1702,10 @@ std::vector<HGroup> run_aggregate(DevCtx& c, const cqgpu_table* t, Compiled& C, 
             if (!chunk) {      // one launch: compact and finish speculatively, one sync for all
                 HIPCHECK(cq_launch_compact(&A.gt, &C.P, A.out, A.out_count, cap_out, c.stream));
                 HIPCHECK(cq_launch_finish(t->g, t->n, A.out, A.out_count, cap_out, &FD, dcells, dbytes, c.stream));
-                if (getenv("CQGPU_PACK_MAPPED")) {   // A/B knob: pack straight into the mapped mailbox
+                if (gm) {                            // the rank's records for the root (header: mailbox)
+                    HIPCHECK(cq_launch_gm_pack(A.out, A.out_count, cap_out, C.P.nacc, (uint32_t)FD.ncols, dcells,
+                                               dbytes, SB, gm->maxg, gm->dst, A.stats, mail, c.stream));
+                } else if (getenv("CQGPU_PACK_MAPPED")) {   // A/B knob: pack straight into the mapped mailbox
                     HIPCHECK(cq_launch_pack_result(A.out, A.out_count, cap_out, C.P.nacc, dcells, dbytes, ncell, SB,
                                                    mail + MAIL_HDR, A.stats, mail, 1, c.stream));
                 } else {                             // pack in HBM, then coalesced copy into the mailbox
@@ -1685,7 +1716,7 @@ std::vector<HGroup> run_aggregate(DevCtx& c, const cqgpu_table* t, Compiled& C, 
                                                  c.stream));
                 }
                 finished = true;
-                is_packed = true;
+                is_packed = !gm;
             }
             // the group count and the scan statistics through pinned memory, one sync
             // (one launch: pack_result_kernel wrote both into the mailbox)
@@ -1732,10 +1763,24 @@ std::vector<HGroup> run_aggregate(DevCtx& c, const cqgpu_table* t, Compiled& C, 
         if (!finished) {
             HIPCHECK(cq_launch_compact(&A.gt, &C.P, A.out, A.out_count, cap_out, c.stream));
             HIPCHECK(cq_launch_finish(t->g, t->n, A.out, A.out_count, cap_out, &FD, dcells, dbytes, c.stream));
+            if (gm)
+                HIPCHECK(cq_launch_gm_pack(A.out, A.out_count, cap_out, C.P.nacc, (uint32_t)FD.ncols, dcells, dbytes,
+                                           SB, gm->maxg, gm->dst, A.stats, nullptr, c.stream));
             HIPCHECK(hipMemcpyAsync(&ng, A.out_count, 4, hipMemcpyDeviceToHost, c.stream));
             HIPCHECK(hipStreamSynchronize(c.stream));
         }
         ng = std::min(ng, cap_out);
+        if (gm) {                   // packed for the root: statistics only
+            gm->ng = ng;
+            g_stats.retries = retries;
+            g_stats.records = st.records;
+            g_stats.lds_spills = st.lds_spills;
+            g_stats.slow_records = st.slow_records;
+            g_stats.passed = st.passed;
+            g_stats.scan_bytes = t->n;
+            if (stats_out) *stats_out = st;
+            return {};
+        }
         if (direct && is_packed && ng && ng <= cq_pack_order_max() && C.grouped) {
             // the stats checks below run first; then the table straight from the mailbox
             for (int a = 0; a < C.P.nacc; a++) {
@@ -2284,6 +2329,14 @@ void append_rows(DevCtx& c, cq_table* r, int at, const std::vector<Cell>& cells,
     }
 }
 
+uint32_t all_records(DevCtx& c, const cqgpu_table* t, DevBuf& out);
+struct JoinSide;
+void load_side(DevCtx& c, const cqgpu_table* t, JoinSide& S);
+
+// filter_rows (evaluator_utils.c:986-1006) for a WHERE over more than MAX_NEED
+// columns: the byte offsets of the passing records, in file order, into `out`
+unsigned long long wide_filter(DevCtx& c, const cqgpu_table* t, Compiled& C, DevBuf& out);
+
 // keys: when given (a range partial, cqgpu_query_partial), the rank's rows are all
 // kept in file order -- OFFSET is global, so only the first OFFSET+LIMIT rows of the
 // shard can matter -- and each row's whole-file byte position is returned with it
@@ -2298,21 +2351,33 @@ cq_table* run_rows(DevCtx& c, const cqgpu_table* t, Compiled& C, RowPlan& R, cq_
     const char* cap_env = getenv("CQGPU_ROW_CAP0");
     unsigned long long cap = std::min<unsigned long long>(t->n / 2 + 2, 1ull << 24);
     if (cap_env && atoll(cap_env) > 0) cap = std::min<unsigned long long>(cap, (unsigned long long)atoll(cap_env));
-    DevBuf rows(cap * 8);
-    (void)run_aggregate(c, t, C, L, &st, rows.as<unsigned long long>(), cap);
-    if (st.rows_emitted > cap) {          // exact count known now: rescan into a buffer that fits
-        cap = st.rows_emitted;
-        DevBuf bigger(cap * 8);
-        std::swap(rows.p, bigger.p);
+    DevBuf rows(8), sorted(8);
+    unsigned long long n = 0;
+    if (C.wide) {
+        // a WHERE over more than MAX_NEED columns: every record's needed cells, the
+        // WHERE per record (join_filter over identity pairs), the passing records'
+        // offsets compacted in file order -- no sort
+        n = wide_filter(c, t, C, sorted);
+    } else {
+        DevBuf r0(cap * 8);
+        std::swap(rows.p, r0.p);
         (void)run_aggregate(c, t, C, L, &st, rows.as<unsigned long long>(), cap);
-        if (st.rows_emitted != cap) throw HipError{"row scan: matching-row count changed between passes"};
+        if (st.rows_emitted > cap) {          // exact count known now: rescan into a buffer that fits
+            cap = st.rows_emitted;
+            DevBuf bigger(cap * 8);
+            std::swap(rows.p, bigger.p);
+            (void)run_aggregate(c, t, C, L, &st, rows.as<unsigned long long>(), cap);
+            if (st.rows_emitted != cap) throw HipError{"row scan: matching-row count changed between passes"};
+        }
+        n = st.rows_emitted;
+        DevBuf s0(n * 8);
+        std::swap(sorted.p, s0.p);
     }
-    const unsigned long long n = st.rows_emitted;
     if (n > (unsigned long long)INT32_MAX) throw Ineligible{"more than 2^31-1 result rows"};
     g_stats.groups = n;
     // 2. file order: radix sort of the byte offsets
-    DevBuf sorted(n * 8);
-    if (n > 1) {
+    if (C.wide) {
+    } else if (n > 1) {
         int bits = 1;
         while (bits < 64 && (1ull << bits) <= t->n) bits++;
         size_t tb = 0;
@@ -2673,7 +2738,7 @@ struct JoinSide {
 void load_side(DevCtx& c, const cqgpu_table* t, JoinSide& S) {
     std::sort(S.cols.begin(), S.cols.end());
     S.cols.erase(std::unique(S.cols.begin(), S.cols.end()), S.cols.end());
-    if ((int)S.cols.size() > MAX_NEED) throw Ineligible{"join: more than 8 columns of one side"};
+    if ((int)S.cols.size() > MAX_WIDE) throw Ineligible{"join: more than " + std::to_string(MAX_WIDE) + " columns of one side"};
     S.n = all_records(c, t, S.recs);
     ColsDesc D;
     memset(&D, 0, sizeof D);
@@ -2690,12 +2755,12 @@ void load_side(DevCtx& c, const cqgpu_table* t, JoinSide& S) {
 JoinMap join_map(const std::vector<int>& jcols, int nl, const JoinSide& A, const JoinSide& B) {
     JoinMap M;
     memset(&M, 0, sizeof M);
-    if ((int)jcols.size() > MAX_NEED) throw Ineligible{"join: too many columns"};
+    if ((int)jcols.size() > MAX_WIDE) throw Ineligible{"join: more than " + std::to_string(MAX_WIDE) + " joined columns"};
     M.n = (int)jcols.size();
     for (int k = 0; k < M.n; k++) {
         const int j = jcols[k];
         M.side[k] = j < nl ? 0 : 1;
-        M.col[k] = (int8_t)(j < nl ? A.slot(j) : B.slot(j - nl));
+        M.col[k] = (int16_t)(j < nl ? A.slot(j) : B.slot(j - nl));
     }
     M.lstride = (uint32_t)std::max<size_t>(A.cols.size(), 1);
     M.rstride = (uint32_t)std::max<size_t>(B.cols.size(), 1);
@@ -3015,7 +3080,7 @@ cq_table* run_fast_join(DevCtx& c, cq_node* q, Compiled& C, const cqgpu_table* L
         if (o.kind != OUT_COUNT && o.kind != OUT_SUM && o.kind != OUT_AVG && o.kind != OUT_REP && o.kind != OUT_CONST &&
             o.kind != OUT_NULL)
             return nullptr;
-    if (C.rep_cols.size() > (size_t)MAX_NEED) return nullptr;
+    if (C.wide || C.rep_cols.size() > (size_t)MAX_WIDE) return nullptr;
     const uint32_t ws = L->lean_ws ? L->lean_ws : 3968u, wsr = R->lean_ws ? R->lean_ws : 3968u;
     // pass 0: records per window; exclusive scans give every window's first record index
     const uint64_t nwl = cq_jx_windows(L->data_begin, L->n, ws), nwr = cq_jx_windows(R->data_begin, R->n, wsr);
@@ -3296,7 +3361,7 @@ cq_table* run_join(DevCtx& c, cq_node* q, const cqgpu_table* L, const cqgpu_tabl
         std::unique_ptr<JoinSide> Wn(new JoinSide);
         Wn->cols.assign(lv[j + 1].lneed.begin(), lv[j + 1].lneed.end());
         if (Wn->cols.empty()) Wn->cols.push_back(0);
-        if ((int)Wn->cols.size() > MAX_NEED) throw Ineligible{"join: more than 8 columns of one side"};
+        if ((int)Wn->cols.size() > MAX_WIDE) throw Ineligible{"join: more than " + std::to_string(MAX_WIDE) + " columns of one side"};
         Wn->n = (uint32_t)np;
         const JoinMap M = join_map(Wn->cols, v.nleft, *Ap, *Bp);
         DevBuf cells((size_t)std::max<unsigned long long>(np, 1) * Wn->cols.size() * sizeof(Cell));
@@ -3528,6 +3593,46 @@ std::vector<HGroup> run_cells_aggregate(DevCtx& c, const cqgpu_table* t, Compile
     return groups;
 }
 
+unsigned long long wide_filter(DevCtx& c, const cqgpu_table* t, Compiled& C, DevBuf& out) {
+    Literals Lit;
+    parse_literals(c, C.lits, Lit);
+    for (size_t i = 0; i < Lit.cells.size(); i++) C.P.consts[i] = Lit.cells[i];
+    JoinSide A, B;
+    A.cols = C.need_cols;
+    if (A.cols.empty()) A.cols.push_back(0);
+    load_side(c, t, A);
+    const uint32_t n = A.n;
+    g_stats.records = n;
+    g_stats.scan_bytes = t->n;
+    g_stats.scan_kernel = 0;
+    if (!n) return 0;
+    DevBuf pairs((size_t)n * 8), bcells(sizeof(Cell)), flags((size_t)n * 4), pos((size_t)n * 4);
+    HIPCHECK(cq_launch_join_fill(nullptr, nullptr, n, 0, 0, pairs.as<uint2>(), c.stream));
+    const JoinMap MW = join_map(C.need_cols, (int)t->names.size(), A, B);
+    HIPCHECK(cq_launch_join_filter(pairs.as<uint2>(), n, &MW, A.cells.as<Cell>(), bcells.as<Cell>(), &C.P,
+                                   flags.as<unsigned int>(), c.stream));
+    size_t tb = 0;
+    HIPCHECK(cq_excl_sum_u32(nullptr, &tb, flags.as<unsigned int>(), pos.as<unsigned int>(), n, c.stream));
+    DevBuf temp(tb);
+    HIPCHECK(cq_excl_sum_u32(temp.p, &tb, flags.as<unsigned int>(), pos.as<unsigned int>(), n, c.stream));
+    unsigned int last[2] = {0, 0};
+    HIPCHECK(hipMemcpyAsync(&last[0], pos.as<unsigned int>() + n - 1, 4, hipMemcpyDeviceToHost, c.stream));
+    HIPCHECK(hipMemcpyAsync(&last[1], flags.as<unsigned int>() + n - 1, 4, hipMemcpyDeviceToHost, c.stream));
+    HIPCHECK(hipStreamSynchronize(c.stream));
+    const uint32_t npass = last[0] + last[1];
+    g_stats.passed = npass;
+    DevBuf perm((size_t)std::max(npass, 1u) * 4), o((size_t)std::max(npass, 1u) * 8);
+    if (npass) {
+        HIPCHECK(cq_launch_vla_compact(flags.as<unsigned int>(), pos.as<unsigned int>(), n, perm.as<unsigned int>(),
+                                       c.stream));
+        HIPCHECK(cq_launch_gather_codes(A.recs.as<unsigned long long>(), perm.as<uint32_t>(), npass,
+                                        o.as<unsigned long long>(), c.stream));
+    }
+    HIPCHECK(hipStreamSynchronize(c.stream));
+    std::swap(out.p, o.p);
+    return npass;
+}
+
 // ------------------------------------------------------------------ query dispatch
 void check_plan_shape(cq_node* q, const cqgpu_table* t, bool join_ok = false) {
     if (!q || q->kind != CQ_N_QUERY) throw Ineligible{"not a SELECT query"};
@@ -3576,7 +3681,7 @@ cq_table* query_impl(cq_node* q, cqgpu_table* const* tables, int ntables) {
     PHASE("compile");
     Literals L;
     std::vector<HGroup> groups;
-    if (C.P.ngpart > 0) {
+    if (C.P.ngpart > 0 || C.wide) {
         groups = run_cells_aggregate(c, t, C, L);
     } else {
         try {
@@ -4182,7 +4287,7 @@ int cqgpu_explain(cq_node* q, const char* header, cq_csv_config cfg, char* out, 
             RowPlan R;
             compile_rows(&t, q, C, R);
             s = "rows\nneed:";
-            for (int i = 0; i < C.P.nneed; i++) s += " " + std::to_string(C.P.need_col[i]);
+            for (int col : C.need_cols) s += " " + std::to_string(col);
             s += "\ncols:";
             for (int cidx : R.cols) s += " " + std::to_string(cidx);
             s += "\nnames:";
@@ -4201,7 +4306,7 @@ int cqgpu_explain(cq_node* q, const char* header, cq_csv_config cfg, char* out, 
         }
         compile_aggregate(&t, q, C);
         s = "need:";
-        for (int i = 0; i < C.P.nneed; i++) s += " " + std::to_string(C.P.need_col[i]);
+        for (int col : C.need_cols) s += " " + std::to_string(col);
         s += "\nprog:";
         for (int i = 0; i < C.P.nprog; i++)
             s += " " + std::to_string(C.P.prog[i].op) + "/" + std::to_string(C.P.prog[i].a) + "/" +
@@ -4525,7 +4630,7 @@ size_t cqgpu_query_partial(cq_node* q, cqgpu_table* const* tables, int ntables, 
         ScanStats st;
         memset(&st, 0, sizeof st);
         std::vector<HGroup> groups;
-        if (C.P.ngpart > 0) {
+        if (C.P.ngpart > 0 || C.wide) {
             groups = run_cells_aggregate(c, t, C, L, &st, true);
         } else {
             try {
@@ -4994,7 +5099,7 @@ cqgpu_partial* cqgpu_partial_new(cq_node* q, cqgpu_table* const* tables, int nta
         ScanStats st;
         memset(&st, 0, sizeof st);
         std::vector<HGroup> groups;
-        if (C.P.ngpart > 0) {
+        if (C.P.ngpart > 0 || C.wide) {
             groups = run_cells_aggregate(c, t, C, L, &st, true);
         } else {
             try {
@@ -5567,5 +5672,622 @@ cq_table* cqgpu_partial_result(cqgpu_partial* p, cq_node* q) {
 }
 
 void cqgpu_partial_free(cqgpu_partial* p) { delete p; }
+
+}  // extern "C"
+
+// ==================================================================== N > 1 over RCCL
+// The whole range-partitioned step inside the library (cqgpu.h cqgpu_dist_query):
+// one communicator per device, every collective on the device context's stream,
+// rank-local failures carried as status words in the payloads.  Three merges, chosen
+// from the plan alone (so every rank takes the same one):
+//   gather-merge  COUNT / SUM / AVG / group columns / constants over <= 1 GROUP BY
+//                 column: each rank's groups (first-appearance order) to rank 0 in
+//                 one grouped send / recv, merged by merge.hip gm_* on its device;
+//                 then rank 0's status to every rank (ncclBroadcast)
+//   dense         other aggregates but MEDIAN: the cqgpu_partial stage sequence
+//                 (KEYS all_gather, MIN / SUM all-reduces, SUM reduces to rank 0)
+//   blobs         MEDIAN, row-returning SELECT: cqgpu_query_partial blobs to rank 0
+// A gather-merge the data declines (more than GM_MAXG groups on a rank, texts over
+// GM_TEXT bytes) falls to the dense merge, a dense merge over 2^29 keys to blobs.
+namespace {
+
+#define NCCLCHECK(x)                                                                  \
+    do {                                                                              \
+        ncclResult_t r_ = (x);                                                        \
+        if (r_ != ncclSuccess) throw HipError{std::string(#x) + ": " + ncclGetErrorString(r_)}; \
+    } while (0)
+
+struct DistComm {
+    ncclComm_t comm = nullptr;
+    int rank = 0, world = 1;
+};
+DistComm g_comm[64];
+
+DistComm& dist_comm() {
+    int dev = 0;
+    HIPCHECK(hipGetDevice(&dev));
+    DistComm& m = g_comm[dev & 63];
+    if (!m.comm) throw HipError{"dist_query: no communicator on this device (cqgpu_comm_init)"};
+    return m;
+}
+
+// a rank-local step failed on some rank: every rank throws it after the same collectives
+struct PeerFail {
+    std::string msg;
+};
+
+constexpr uint32_t GM_MAXG = 4096;      // groups one rank may send (above: the dense merge)
+constexpr uint32_t GM_SB = 48;          // finish_kernel's inline string bytes (run_aggregate SB)
+constexpr size_t DIST_MAIL_HDR = 1024;
+
+enum DistPath { DP_GM = 1, DP_DENSE = 2, DP_BLOB = 3 };
+
+bool gm_eligible(const Compiled& C) {
+    if (C.wide || C.P.ngpart > 0 || !C.vla.empty()) return false;
+    for (int a = 0; a < C.P.nacc; a++)
+        if (C.P.acc[a].kind != ACC_SUM) return false;
+    for (const OutCol& o : C.outs)
+        if (o.kind != OUT_COUNT && o.kind != OUT_SUM && o.kind != OUT_AVG && o.kind != OUT_REP && o.kind != OUT_CONST &&
+            o.kind != OUT_NULL)
+            return false;
+    return true;
+}
+bool dense_eligible(const Compiled& C) {
+    for (auto& v : C.vla)
+        if (v.first != 0) return false;      // MEDIAN needs every value
+    return true;
+}
+
+// per-device buffers of the N > 1 step, kept across steps (grown as needed)
+struct DistBufs {
+    DevBuf send, recv, scratch, word;
+    size_t send_b = 0, recv_b = 0, scratch_b = 0;
+    uint32_t* hword = nullptr;           // pinned: status words read back
+};
+DistBufs g_dbuf[64];
+DistBufs& dist_bufs() {
+    int dev = 0;
+    HIPCHECK(hipGetDevice(&dev));
+    DistBufs& b = g_dbuf[dev & 63];
+    if (!b.word.p) {
+        DevBuf w(256);
+        std::swap(b.word.p, w.p);
+        HIPCHECK(hipHostMalloc((void**)&b.hword, 256, hipHostMallocDefault));
+    }
+    return b;
+}
+uint8_t* grow(DevBuf& b, size_t& have, size_t need) {
+    if (need > have || !b.p) {
+        DevBuf nb(std::max<size_t>(need, 256));
+        std::swap(b.p, nb.p);
+        have = std::max<size_t>(need, 256);
+    }
+    return (uint8_t*)b.p;
+}
+
+// one MAX all-reduce of this rank's flag (0 / 1); true when any rank set it
+bool agree_any(DevCtx& c, DistComm& m, bool bad) {
+    DistBufs& b = dist_bufs();
+    b.hword[0] = bad ? 1u : 0u;
+    uint32_t* dw = b.word.as<uint32_t>();
+    HIPCHECK(hipMemcpyAsync(dw, b.hword, 4, hipMemcpyHostToDevice, c.stream));
+    NCCLCHECK(ncclAllReduce(dw, dw, 1, ncclUint32, ncclMax, m.comm, c.stream));
+    HIPCHECK(hipMemcpyAsync(b.hword + 1, dw, 4, hipMemcpyDeviceToHost, c.stream));
+    HIPCHECK(hipStreamSynchronize(c.stream));
+    return b.hword[1] != 0;
+}
+
+// rank 0's status word (device, `dsrc` on rank 0) to every rank; returns it
+uint32_t bcast_status(DevCtx& c, DistComm& m, const uint32_t* dsrc) {
+    DistBufs& b = dist_bufs();
+    uint32_t* dw = b.word.as<uint32_t>() + 4;
+    NCCLCHECK(ncclBroadcast(m.rank == 0 ? (const void*)dsrc : (const void*)dw, dw, 1, ncclUint32, 0, m.comm, c.stream));
+    HIPCHECK(hipMemcpyAsync(b.hword + 2, dw, 4, hipMemcpyDeviceToHost, c.stream));
+    HIPCHECK(hipStreamSynchronize(c.stream));
+    return b.hword[2];
+}
+
+// ---- gather-merge
+uint64_t gm_rank_bytes(const Compiled& C) {
+    const uint64_t B = GM_HDR + (uint64_t)GM_MAXG * gm_rec_bytes(C.P.nacc, (uint32_t)C.rep_cols.size());
+    return (B + 255) & ~255ull;
+}
+
+// this rank's scan packed into dst (header + records); GM_OK or GM_FAILED (the
+// header says which either way)
+uint32_t gm_local_part(DevCtx& c, const cqgpu_table* t, Compiled& C, uint8_t* dst, std::string& err) {
+    GmHdr h;
+    memset(&h, 0, sizeof h);
+    try {
+        HIPCHECK(hipMemsetAsync(dst, 0, GM_HDR, c.stream));
+        Literals L;
+        ScanStats st;
+        GmSend gs;
+        gs.dst = dst;
+        gs.maxg = GM_MAXG;
+        (void)run_aggregate(c, t, C, L, &st, nullptr, 0, nullptr, &gs);
+        h.base = t->base_offset;
+        h.records = st.records;
+        h.passed = st.passed;
+        h.slow_records = st.slow_records;
+        h.lds_spills = st.lds_spills;
+        // bytes [8, 48): base and statistics (status and ng are gm_pack_kernel's)
+        HIPCHECK(hipMemcpyAsync(dst + 8, (const uint8_t*)&h + 8, 40, hipMemcpyHostToDevice, c.stream));
+        return GM_OK;
+    } catch (HipError& e) {
+        err = e.msg;
+    } catch (Ineligible& e) {
+        err = e.why;
+    } catch (std::exception& e) {
+        err = e.what();
+    }
+    (void)hipGetLastError();
+    memset(&h, 0, sizeof h);
+    h.status = GM_FAILED;
+    (void)hipMemcpyAsync(dst, &h, GM_HDR, hipMemcpyHostToDevice, c.stream);
+    return GM_FAILED;
+}
+
+struct GmRoot {
+    uint32_t* dstatus = nullptr;         // device: the merge's status word
+    uint8_t* mail = nullptr;
+};
+// rank 0: the merge kernels over N ranks' records, the result into the mailbox
+GmRoot gm_merge_launch(DevCtx& c, const Compiled& C, const uint8_t* recv, uint64_t B, uint32_t N) {
+    DistBufs& db = dist_bufs();
+    const uint32_t T = N * GM_MAXG;
+    uint32_t cap = 64;
+    while (cap < 2 * T) cap <<= 1;
+    const uint32_t R = (uint32_t)C.rep_cols.size(), nacc = (uint32_t)C.P.nacc, ncell = R + nacc + 1;
+    const size_t scan_b = cq_gm_scan_bytes(T);
+    const size_t out_b = cq_pack_result_bytes(T, (int)nacc, ncell, GM_SB);
+    size_t off = 0;
+    auto part = [&](size_t bytes) { const size_t o = off; off += (bytes + 255) & ~(size_t)255; return o; };
+    const size_t o_state = part((size_t)cap * 4), o_first = part((size_t)cap * 4), o_idx = part((size_t)N * T * 4);
+    const size_t o_rec = part((size_t)cap * 4), o_slot = part((size_t)T * 4), o_flag = part((size_t)T * 4),
+                 o_dense = part((size_t)T * 4), o_err = part(64), o_scan = part(scan_b), o_out = part(out_b);
+    uint8_t* S = grow(db.scratch, db.scratch_b, off);
+    // zero: state, err; 0xFF: first_of, idx (contiguous: one memset each)
+    HIPCHECK(hipMemsetAsync(S + o_state, 0, o_first - o_state, c.stream));
+    HIPCHECK(hipMemsetAsync(S + o_first, 0xFF, o_rec - o_first, c.stream));
+    HIPCHECK(hipMemsetAsync(S + o_err, 0, 64, c.stream));
+    GmRoot g;
+    g.mail = mailbox(c, DIST_MAIL_HDR + out_b + 64);
+    unsigned int* gcount = (unsigned int*)(S + o_err + 16);
+    HIPCHECK(cq_launch_gm_merge(recv, B, N, GM_MAXG, (int)nacc, R, C.grouped ? 1 : 0, GM_SB, (uint32_t*)(S + o_state),
+                                (uint32_t*)(S + o_rec), (uint32_t*)(S + o_first), cap, (uint32_t*)(S + o_slot),
+                                (uint32_t*)(S + o_flag), (uint32_t*)(S + o_dense), (uint32_t*)(S + o_idx), S + o_scan,
+                                scan_b, (unsigned int*)(S + o_err), S + o_out, gcount, g.mail, c.stream));
+    HIPCHECK(cq_launch_mail_copy(S + o_out, gcount, T, (int)nacc, ncell, GM_SB, g.mail + DIST_MAIL_HDR, c.stream));
+    g.dstatus = gcount + 1;
+    return g;
+}
+
+// rank 0, after the stream's sync: the result table from the mailbox
+cq_table* gm_finish_root(DevCtx& c, cq_node* q, Compiled& C, const uint8_t* mail) {
+    ScanStats st;
+    memcpy(&st, mail, sizeof st);
+    uint32_t G = 0;
+    memcpy(&G, mail + sizeof(ScanStats), 4);
+    const uint32_t R = (uint32_t)C.rep_cols.size(), ncell = R + (uint32_t)C.P.nacc + 1;
+    std::vector<int> rep_ord(R);
+    for (uint32_t i = 0; i < R; i++) rep_ord[i] = (int)i;
+    std::sort(rep_ord.begin(), rep_ord.end(), [&](int a, int b) { return C.rep_cols[a] < C.rep_cols[b]; });
+    Literals L;
+    parse_literals(c, C.lits, L);
+    static thread_local std::vector<uint8_t> hbuf;
+    const size_t pb = cq_pack_result_bytes(G, C.P.nacc, ncell, GM_SB);
+    if (hbuf.size() < pb + 8) hbuf.resize(pb + 8);
+    memcpy(hbuf.data(), mail + DIST_MAIL_HDR, pb);
+    g_stats.records = st.records;
+    g_stats.passed = st.passed;
+    g_stats.slow_records = st.slow_records;
+    g_stats.lds_spills = st.lds_spills;
+    g_stats.groups = G;
+    cq_table* res = build_direct(C, hbuf.data(), G, ncell, GM_SB, rep_ord, L, ~0ull);
+    if (!res) throw HipError{"gather-merge: a result cell is not inline"};
+    post_ops(c, res, q);
+    g_stats.path = 1;
+    return res;
+}
+
+// the gather-merge step; returns GM_OK (rank 0: *res), GM_DECLINE, or throws PeerFail
+uint32_t dist_gm(DevCtx& c, DistComm& m, cq_node* q, const cqgpu_table* t, cq_table** res) {
+    Compiled C;
+    std::string err;
+    uint32_t mine = GM_OK;
+    try {
+        compile_aggregate(t, q, C);
+    } catch (Ineligible& e) {
+        err = e.why;
+        mine = GM_FAILED;
+    } catch (HipError& e) {
+        err = e.msg;
+        mine = GM_FAILED;
+    }
+    const uint32_t N = (uint32_t)m.world;
+    const uint64_t B = gm_rank_bytes(C);
+    DistBufs& db = dist_bufs();
+    uint8_t* recv = m.rank == 0 ? grow(db.recv, db.recv_b, B * N) : nullptr;
+    uint8_t* dst = m.rank == 0 ? recv : grow(db.send, db.send_b, B);
+    if (mine == GM_OK) {
+        mine = gm_local_part(c, t, C, dst, err);
+    } else {
+        GmHdr h;
+        memset(&h, 0, sizeof h);
+        h.status = GM_FAILED;
+        HIPCHECK(hipMemcpyAsync(dst, &h, GM_HDR, hipMemcpyHostToDevice, c.stream));
+    }
+    NCCLCHECK(ncclGroupStart());
+    if (m.rank == 0) {
+        for (uint32_t r = 1; r < N; r++) NCCLCHECK(ncclRecv(recv + r * B, B, ncclUint8, (int)r, m.comm, c.stream));
+    } else {
+        NCCLCHECK(ncclSend(dst, B, ncclUint8, 0, m.comm, c.stream));
+    }
+    NCCLCHECK(ncclGroupEnd());
+    GmRoot g;
+    if (m.rank == 0) g = gm_merge_launch(c, C, recv, B, N);
+    const uint32_t st = bcast_status(c, m, g.dstatus);
+    if (st == GM_FAILED)
+        throw PeerFail{mine == GM_FAILED ? err : std::string("a peer rank failed")};
+    if (st == GM_DECLINE) return GM_DECLINE;
+    if (m.rank == 0) *res = gm_finish_root(c, q, C, g.mail);
+    return GM_OK;
+}
+
+// ---- dense merge: the cqgpu_partial stage sequence issued here over RCCL
+// the collective a rank that failed mid-loop still issues at stage `at` (counts of
+// the reduces follow from G, known on every rank after the KEYS agreement; its
+// all-gathers send nothing and report the failure in the size exchange)
+cqgpu_coll expected_coll(const cqgpu_partial* p, size_t at) {
+    cqgpu_coll x;
+    memset(&x, 0, sizeof x);
+    if (!p || at >= p->stages.size()) { x.op = COLL_DONE; return x; }
+    const uint64_t g = p->G, nmm = p->mm.size(), C = p->R + nmm;
+    switch (p->stages[at]) {
+        case ST_KEYS: case ST_STRS: case ST_SIDE: x.op = COLL_ALLGATHER; x.count = 0; break;
+        case ST_MIN: x.op = COLL_ALLREDUCE_MIN_I64; x.count = g * p->P; break;
+        case ST_SUM: x.op = COLL_ALLREDUCE_SUM_F64; x.count = g * p->W; break;
+        case ST_EXT: x.op = COLL_ALLREDUCE_MIN_I64; x.count = g * nmm; break;
+        case ST_CELL: x.op = COLL_REDUCE_SUM_I64; x.count = g * C * 2; break;
+        case ST_VLA: x.op = COLL_REDUCE_SUM_F64; x.count = g * p->NV; break;
+        case ST_SUMR: x.op = COLL_REDUCE_SUM_F64; x.count = g * p->W; break;
+    }
+    return x;
+}
+
+// all-gather of a variable-length device byte buffer: sizes (with this rank's failure
+// flag) first -- the one host synchronisation a data-dependent size needs -- then
+// the payloads padded to the largest; *out holds them concatenated in rank order
+bool allgather_var(DevCtx& c, DistComm& m, const void* buf, uint64_t n, bool bad, DevBuf& out,
+                   std::vector<uint64_t>& sizes) {
+    const int N = m.world;
+    DevBuf pair((size_t)N * 16 + 16);
+    uint64_t* dp = pair.as<uint64_t>();
+    uint64_t mine[2] = {bad ? 0 : n, bad ? 1ull : 0ull};
+    HIPCHECK(hipMemcpyAsync(dp + 2 * N, mine, 16, hipMemcpyHostToDevice, c.stream));
+    NCCLCHECK(ncclAllGather(dp + 2 * N, dp, 2, ncclUint64, m.comm, c.stream));
+    std::vector<uint64_t> all((size_t)2 * N);
+    HIPCHECK(hipMemcpyAsync(all.data(), dp, all.size() * 8, hipMemcpyDeviceToHost, c.stream));
+    HIPCHECK(hipStreamSynchronize(c.stream));
+    bool any = false;
+    uint64_t mx = 1, tot = 0;
+    sizes.assign(N, 0);
+    for (int r = 0; r < N; r++) {
+        any = any || all[2 * r + 1] != 0;
+        sizes[r] = all[2 * r];
+        mx = std::max(mx, sizes[r]);
+        tot += sizes[r];
+    }
+    if (any) return false;
+    DevBuf pad(mx), gathered(mx * N);
+    if (n) HIPCHECK(hipMemcpyAsync(pad.p, buf, n, hipMemcpyDeviceToDevice, c.stream));
+    NCCLCHECK(ncclAllGather(pad.p, gathered.p, mx, ncclUint8, m.comm, c.stream));
+    DevBuf cat(std::max<uint64_t>(tot, 16));
+    uint64_t at = 0;
+    for (int r = 0; r < N; r++) {
+        if (sizes[r])
+            HIPCHECK(hipMemcpyAsync(cat.as<uint8_t>() + at, gathered.as<uint8_t>() + (uint64_t)r * mx, sizes[r],
+                                    hipMemcpyDeviceToDevice, c.stream));
+        at += sizes[r];
+    }
+    std::swap(out.p, cat.p);
+    HIPCHECK(hipStreamSynchronize(c.stream));      // before pad / gathered go back to the pool
+    return true;
+}
+
+// returns 0 (rank 0: *res), 1 declined (blobs); throws PeerFail
+int dist_dense(DevCtx& c, DistComm& m, cq_node* q, cqgpu_table* t, cq_table** res) {
+    std::string err;
+    cqgpu_partial* p = cqgpu_partial_new(q, &t, 1);
+    const bool inel = !p && !g_inel.empty();
+    bool bad = !p && !inel;
+    if (bad) err = g_err;
+    // entry: did any rank fail, is any rank off the dense path (one MAX all-reduce of two words)
+    {
+        DistBufs& b = dist_bufs();
+        b.hword[0] = bad ? 1u : 0u;
+        b.hword[1] = inel ? 1u : 0u;
+        uint32_t* dw = b.word.as<uint32_t>() + 8;
+        HIPCHECK(hipMemcpyAsync(dw, b.hword, 8, hipMemcpyHostToDevice, c.stream));
+        NCCLCHECK(ncclAllReduce(dw, dw, 2, ncclUint32, ncclMax, m.comm, c.stream));
+        HIPCHECK(hipMemcpyAsync(b.hword + 4, dw, 8, hipMemcpyDeviceToHost, c.stream));
+        HIPCHECK(hipStreamSynchronize(c.stream));
+        if (b.hword[4]) {
+            if (p) cqgpu_partial_free(p);
+            throw PeerFail{bad ? err : std::string("a peer rank failed")};
+        }
+        if (b.hword[5]) {
+            if (p) cqgpu_partial_free(p);
+            return 1;
+        }
+    }
+    std::unique_ptr<cqgpu_partial> own(p);
+    DevBuf result;
+    std::vector<uint64_t> sizes;
+    bool have_sizes = false, have_result = false;
+    size_t cur = 0;
+    while (true) {
+        cqgpu_coll nx;
+        memset(&nx, 0, sizeof nx);
+        const size_t before = cur;
+        if (!bad) {
+            if (cqgpu_partial_next(p, have_result ? result.p : nullptr, have_sizes ? sizes.data() : nullptr, m.rank,
+                                   m.world, &nx) != 0) {
+                bad = true;
+                err = g_err;
+            }
+        }
+        if (bad) nx = expected_coll(p, before);
+        cur = before + 1;
+        // the KEYS result just built the dictionary (G): agree before counts depend on it
+        if (before == 1 && agree_any(c, m, bad)) throw PeerFail{bad ? err : std::string("a peer rank failed")};
+        if (nx.op == COLL_DONE) break;
+        if (nx.op == COLL_DECLINE) return 1;            // (every rank: it depends on the gathered keys)
+        const size_t elem = nx.op == COLL_ALLGATHER ? 1 : 8;
+        DevBuf buf(std::max<size_t>(nx.count * elem, 16));
+        if (!bad && nx.count && cqgpu_partial_put(p, buf.p) != 0) {
+            bad = true;
+            err = g_err;
+        }
+        have_sizes = false;
+        if (nx.op == COLL_ALLGATHER) {
+            if (!allgather_var(c, m, buf.p, bad ? 0 : nx.count, bad, result, sizes))
+                throw PeerFail{bad ? err : std::string("a peer rank failed")};
+            have_sizes = true;
+        } else {
+            if (nx.count) {
+                const ncclDataType_t ty = (nx.op == COLL_ALLREDUCE_SUM_F64 || nx.op == COLL_REDUCE_SUM_F64) ? ncclFloat64
+                                                                                                           : ncclInt64;
+                if (nx.op == COLL_ALLREDUCE_MIN_I64 || nx.op == COLL_ALLREDUCE_SUM_F64)
+                    NCCLCHECK(ncclAllReduce(buf.p, buf.p, nx.count, ty, nx.op == COLL_ALLREDUCE_MIN_I64 ? ncclMin : ncclSum,
+                                            m.comm, c.stream));
+                else
+                    NCCLCHECK(ncclReduce(buf.p, buf.p, nx.count, ty, ncclSum, 0, m.comm, c.stream));
+            }
+            std::swap(result.p, buf.p);
+        }
+        have_result = true;
+    }
+    if (agree_any(c, m, bad)) throw PeerFail{bad ? err : std::string("a peer rank failed")};
+    // rank 0's result, then its status to every rank
+    DistBufs& b = dist_bufs();
+    std::string rerr;
+    if (m.rank == 0) {
+        *res = cqgpu_partial_result(p, q);
+        if (!*res) rerr = g_err;
+        b.hword[8] = *res ? 0u : 1u;
+        HIPCHECK(hipMemcpyAsync(b.word.as<uint32_t>() + 12, b.hword + 8, 4, hipMemcpyHostToDevice, c.stream));
+    }
+    if (bcast_status(c, m, b.word.as<uint32_t>() + 12)) {
+        if (*res) { cqgpu_result_free(*res); *res = nullptr; }
+        throw PeerFail{m.rank == 0 ? rerr : std::string("rank 0 failed to finish the merge")};
+    }
+    return 0;
+}
+
+// ---- blobs: every rank's cqgpu_query_partial to rank 0, merged there
+void dist_blob(DevCtx& c, DistComm& m, cq_node* q, cqgpu_table* t, cq_table** res) {
+    void* blob = nullptr;
+    const size_t n = cqgpu_query_partial(q, &t, 1, &blob);
+    const bool bad = n == 0;
+    std::string err = bad ? (g_err.empty() ? g_inel : g_err) : std::string();
+    struct Free { void* b; ~Free() { free(b); } } fr{blob};
+    const int N = m.world;
+    DevBuf pair((size_t)N * 16 + 16), dblob(std::max<size_t>(n, 16));
+    uint64_t* dp = pair.as<uint64_t>();
+    uint64_t mine[2] = {bad ? 0 : (uint64_t)n, bad ? 1ull : 0ull};
+    HIPCHECK(hipMemcpyAsync(dp + 2 * N, mine, 16, hipMemcpyHostToDevice, c.stream));
+    NCCLCHECK(ncclAllGather(dp + 2 * N, dp, 2, ncclUint64, m.comm, c.stream));
+    std::vector<uint64_t> all((size_t)2 * N);
+    HIPCHECK(hipMemcpyAsync(all.data(), dp, all.size() * 8, hipMemcpyDeviceToHost, c.stream));
+    if (n) HIPCHECK(hipMemcpyAsync(dblob.p, blob, n, hipMemcpyHostToDevice, c.stream));
+    HIPCHECK(hipStreamSynchronize(c.stream));
+    for (int r = 0; r < N; r++)
+        if (all[2 * r + 1]) throw PeerFail{bad ? err : std::string("a peer rank failed")};
+    std::vector<uint64_t> off(N + 1, 0);
+    for (int r = 0; r < N; r++) off[r + 1] = off[r] + all[2 * r];
+    DevBuf gathered(m.rank == 0 ? std::max<uint64_t>(off[N], 16) : 16);
+    NCCLCHECK(ncclGroupStart());
+    if (m.rank == 0) {
+        for (int r = 1; r < N; r++)
+            if (all[2 * r]) NCCLCHECK(ncclRecv(gathered.as<uint8_t>() + off[r], all[2 * r], ncclUint8, r, m.comm, c.stream));
+    } else {
+        NCCLCHECK(ncclSend(dblob.p, n, ncclUint8, 0, m.comm, c.stream));
+    }
+    NCCLCHECK(ncclGroupEnd());
+    DistBufs& b = dist_bufs();
+    std::string rerr;
+    if (m.rank == 0) {
+        std::vector<uint8_t> h(off[N]);
+        if (off[N] > off[1])
+            HIPCHECK(hipMemcpyAsync(h.data() + off[1], gathered.as<uint8_t>() + off[1], off[N] - off[1],
+                                    hipMemcpyDeviceToHost, c.stream));
+        HIPCHECK(hipStreamSynchronize(c.stream));
+        memcpy(h.data(), blob, n);
+        std::vector<const void*> ptrs(N);
+        std::vector<size_t> sz(N);
+        for (int r = 0; r < N; r++) { ptrs[r] = h.data() + off[r]; sz[r] = all[2 * r]; }
+        *res = cqgpu_merge_partials(q, ptrs.data(), sz.data(), N);
+        if (!*res) rerr = g_err;
+        b.hword[8] = *res ? 0u : 1u;
+        HIPCHECK(hipMemcpyAsync(b.word.as<uint32_t>() + 12, b.hword + 8, 4, hipMemcpyHostToDevice, c.stream));
+    }
+    if (bcast_status(c, m, b.word.as<uint32_t>() + 12)) {
+        if (*res) { cqgpu_result_free(*res); *res = nullptr; }
+        throw PeerFail{m.rank == 0 ? rerr : std::string("rank 0 failed to finish the merge")};
+    }
+}
+
+// the merge the plan takes, decided from the AST and the header alone (no device
+// work: a table copy without its sample), so every rank decides the same
+int dist_path(cq_node* q, const cqgpu_table* t) {
+    cqgpu_table shadow;
+    shadow.names = t->names;
+    shadow.cfg = t->cfg;
+    check_plan_shape(q, &shadow);
+    if (is_row_query(q)) return DP_BLOB;
+    Compiled D;
+    compile_aggregate(&shadow, q, D);
+    if (gm_eligible(D)) return DP_GM;
+    return dense_eligible(D) ? DP_DENSE : DP_BLOB;
+}
+
+}  // namespace
+
+extern "C" {
+
+int cqgpu_comm_unique_id(void* id_out) {
+    g_err.clear();
+    if (!id_out) return -1;
+    ncclUniqueId id;
+    const ncclResult_t r = ncclGetUniqueId(&id);
+    if (r != ncclSuccess) {
+        set_err("cq_amd: ncclGetUniqueId: %s", ncclGetErrorString(r));
+        return -1;
+    }
+    static_assert(sizeof(ncclUniqueId) == CQGPU_COMM_ID_BYTES, "RCCL unique id size");
+    memcpy(id_out, &id, sizeof id);
+    return 0;
+}
+
+int cqgpu_comm_init(const void* id, int rank, int world) {
+    g_err.clear();
+    try {
+        if (!id || world < 1 || rank < 0 || rank >= world) throw HipError{"comm_init: bad arguments"};
+        int dev = 0;
+        HIPCHECK(hipGetDevice(&dev));
+        DistComm& m = g_comm[dev & 63];
+        if (m.comm) {
+            (void)ncclCommDestroy(m.comm);
+            m.comm = nullptr;
+        }
+        ncclUniqueId uid;
+        memcpy(&uid, id, sizeof uid);
+        (void)ctx();                                   // the device context (stream) first
+        NCCLCHECK(ncclCommInitRank(&m.comm, world, uid, rank));
+        m.rank = rank;
+        m.world = world;
+        return 0;
+    } catch (HipError& e) {
+        set_err("cq_amd: %s", e.msg.c_str());
+        return -1;
+    } catch (std::exception& e) {
+        set_err("cq_amd: %s", e.what());
+        return -1;
+    } catch (...) {
+        set_err("cq_amd: %s", "unexpected C++ exception");
+        return -1;
+    }
+}
+
+void cqgpu_comm_destroy(void) {
+    int dev = 0;
+    if (hipGetDevice(&dev) != hipSuccess) return;
+    DistComm& m = g_comm[dev & 63];
+    if (m.comm) (void)ncclCommDestroy(m.comm);
+    m.comm = nullptr;
+    m.rank = 0;
+    m.world = 1;
+}
+
+cq_table* cqgpu_dist_query(cq_node* q, cqgpu_table* t, int* status, int* path) {
+    g_err.clear();
+    g_inel.clear();
+    memset(&g_stats, 0, sizeof g_stats);
+    if (status) *status = 0;
+    if (path) *path = 0;
+    cq_table* res = nullptr;
+    try {
+        if (!t) throw HipError{"dist_query: no table"};
+        DevCtx& c = ctx();
+        DistComm& m = dist_comm();
+        bump_reset(c);
+        const double t0 = now_ms();
+        int dp = dist_path(q, t);                        // Ineligible: the same on every rank
+        if (dp == DP_GM && dist_gm(c, m, q, t, &res) == GM_DECLINE) dp = DP_DENSE;
+        if (dp == DP_DENSE && dist_dense(c, m, q, t, &res) != 0) dp = DP_BLOB;
+        if (dp == DP_BLOB) dist_blob(c, m, q, t, &res);
+        if (path) *path = dp;
+        g_stats.total_ms = now_ms() - t0;
+        if (m.rank == 0) g_stats.path = 1;
+        return res;
+    } catch (PeerFail& e) {
+        set_err("cq_amd: %s", e.msg.c_str());
+    } catch (Ineligible& e) {
+        g_inel = e.why;
+        set_err("cq_amd: query outside the GPU executor's subset: %s", e.why.c_str());
+    } catch (HipError& e) {
+        set_err("cq_amd: %s", e.msg.c_str());
+    } catch (std::exception& e) {
+        set_err("cq_amd: %s", e.what());
+    } catch (...) {
+        set_err("cq_amd: %s", "unexpected C++ exception");
+    }
+    if (res) cqgpu_result_free(res);
+    if (status) *status = -1;
+    return nullptr;
+}
+
+// simulated ranks in one process: every shard's pack, then the root's merge
+cq_table* cqgpu_gm_local(cq_node* q, cqgpu_table* const* shards, int n) {
+    g_err.clear();
+    g_inel.clear();
+    memset(&g_stats, 0, sizeof g_stats);
+    try {
+        if (n < 1 || !shards) throw HipError{"gm_local: no shards"};
+        DevCtx& c = ctx();
+        bump_reset(c);
+        if (dist_path(q, shards[0]) != DP_GM) throw Ineligible{"gather-merge: plan outside it"};
+        Compiled C;
+        compile_aggregate(shards[0], q, C);
+        const uint64_t B = gm_rank_bytes(C);
+        DevBuf recv(B * (uint64_t)n);
+        for (int r = 0; r < n; r++) {
+            Compiled Cr;
+            compile_aggregate(shards[r], q, Cr);
+            std::string err;
+            if (gm_local_part(c, shards[r], Cr, recv.as<uint8_t>() + (uint64_t)r * B, err) != GM_OK)
+                throw HipError{"gm_local: shard " + std::to_string(r) + ": " + err};
+        }
+        GmRoot g = gm_merge_launch(c, C, recv.as<uint8_t>(), B, (uint32_t)n);
+        HIPCHECK(hipStreamSynchronize(c.stream));
+        uint32_t st = 0;
+        memcpy(&st, g.mail + sizeof(ScanStats) + 4, 4);
+        if (st == GM_DECLINE) throw Ineligible{"gather-merge: declined by the data"};
+        if (st != GM_OK) throw HipError{"gm_local: merge failed"};
+        return gm_finish_root(c, q, C, g.mail);
+    } catch (Ineligible& e) {
+        g_inel = e.why;
+        set_err("cq_amd: %s", e.why.c_str());
+    } catch (HipError& e) {
+        set_err("cq_amd: %s", e.msg.c_str());
+    } catch (std::exception& e) {
+        set_err("cq_amd: %s", e.what());
+    } catch (...) {
+        set_err("cq_amd: %s", "unexpected C++ exception");
+    }
+    return nullptr;
+}
 
 }  // extern "C"

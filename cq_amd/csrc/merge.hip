@@ -203,10 +203,257 @@ __global__ void cell_mask_kernel(const unsigned long long* __restrict__ dmin, co
     }
 }
 
+// ---- gather-merge on the root (executor.hip dist_query): every rank's records
+// (plan.h GM layout) side by side, rank r's at buf + r * B.  Record i = r * maxg + j
+// (rank-major = file order, the ranges being ordered); a key's dense id is the rank
+// of its first occurrence, which is also the group's global first-appearance order
+// (create_groups, evaluator_aggregates.c:152-164), and that occurrence holds the
+// group's first row -- its representative cells are the result's.
+struct GmView {
+    const uint8_t* buf;
+    uint64_t B;          // bytes per rank
+    uint32_t N, maxg, rec, nacc, R;
+    __device__ __forceinline__ const GmHdr& hdr(uint32_t r) const { return *(const GmHdr*)(buf + (uint64_t)r * B); }
+    __device__ __forceinline__ const uint8_t* rec_at(uint32_t r, uint32_t j) const {
+        return buf + (uint64_t)r * B + GM_HDR + (uint64_t)j * rec;
+    }
+    __device__ __forceinline__ const uint8_t* key_text(const uint8_t* rp) const {
+        return rp + 40 + 16 * nacc + (uint64_t)R * GM_CELL + 16;
+    }
+};
+__device__ __forceinline__ bool gm_key_eq(const GmView& V, const uint8_t* a, const uint8_t* b) {
+    const uint32_t ca = *(const uint32_t*)a, cb = *(const uint32_t*)b;
+    if (ca != cb || ((const uint64_t*)a)[1] != ((const uint64_t*)b)[1] || ((const uint64_t*)a)[2] != ((const uint64_t*)b)[2])
+        return false;
+    if ((ca >> 16) != 5u) return true;                              // GK_LONG: the bytes
+    const uint32_t n = ca & 0xffffu;
+    const uint8_t* x = V.key_text(a);
+    const uint8_t* y = V.key_text(b);
+    for (uint32_t k = 0; k < n; k++)
+        if (x[k] != y[k]) return false;
+    return true;
+}
+
+__global__ void gm_dict_kernel(GmView V, uint32_t* __restrict__ state, uint32_t* __restrict__ rec_of,
+                               uint32_t* __restrict__ first_of, uint32_t cap, uint32_t* __restrict__ slot_of,
+                               unsigned int* __restrict__ err) {
+    const uint32_t i = blockIdx.x * blockDim.x + threadIdx.x;
+    const uint32_t T = V.N * V.maxg;
+    const uint32_t r = i / V.maxg, j = i - r * V.maxg;
+    bool pending = i < T && j < min(V.hdr(r).ng, V.maxg);
+    const bool valid = pending;
+    const uint8_t* rp = pending ? V.rec_at(r, j) : nullptr;
+    uint64_t h = 0;
+    if (pending)
+        h = mix64(((const uint64_t*)rp)[1] ^ mix64(((const uint64_t*)rp)[2] + 0x9E3779B97F4A7C15ULL) ^
+                  ((uint64_t)*(const uint32_t*)rp << 17));
+    const uint32_t mask = cap - 1;
+    uint32_t s = (uint32_t)h & mask, probes = 0, slot = 0;
+    for (uint32_t trip = 0; __any(pending); trip++) {
+        if (pending) {
+            uint32_t st = __hip_atomic_load(&state[s], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+            if (st == 0) {
+                const uint32_t old = atomicCAS(&state[s], 0u, 1u);
+                if (old == 0) {
+                    __hip_atomic_store(&rec_of[s], i, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+                    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+                    __hip_atomic_store(&state[s], 2u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+                    slot = s;
+                    pending = false;
+                }
+                st = old;
+            }
+            if (pending && st == 2) {
+                const uint32_t o = __hip_atomic_load(&rec_of[s], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+                const uint32_t orr = o / V.maxg;
+                if (gm_key_eq(V, V.rec_at(orr, o - orr * V.maxg), rp)) {
+                    slot = s;
+                    pending = false;
+                } else {
+                    s = (s + 1) & mask;
+                    if (++probes >= cap) { atomicOr(err, 1u); pending = false; }
+                }
+            }
+        }
+        if (trip > (1u << 22)) {
+            if (pending) atomicOr(err, 2u);
+            break;
+        }
+    }
+    if (valid) {
+        atomicMin(&first_of[slot], i);
+        slot_of[i] = slot;
+    }
+}
+
+// 1 where record i is its key's first occurrence (0 for the empty record slots)
+__global__ void gm_flag_kernel(GmView V, const uint32_t* __restrict__ slot_of, const uint32_t* __restrict__ first_of,
+                               uint32_t* __restrict__ flag) {
+    const uint32_t i = blockIdx.x * blockDim.x + threadIdx.x;
+    const uint32_t T = V.N * V.maxg;
+    if (i >= T) return;
+    const uint32_t r = i / V.maxg, j = i - r * V.maxg;
+    flag[i] = (j < min(V.hdr(r).ng, V.maxg) && first_of[slot_of[i]] == i) ? 1u : 0u;
+}
+
+// idx[r * T + d] = j: rank r's record of dense group d
+__global__ void gm_scatter_kernel(GmView V, const uint32_t* __restrict__ slot_of, const uint32_t* __restrict__ first_of,
+                                  const uint32_t* __restrict__ dense, uint32_t* __restrict__ idx) {
+    const uint32_t i = blockIdx.x * blockDim.x + threadIdx.x;
+    const uint32_t T = V.N * V.maxg;
+    if (i >= T) return;
+    const uint32_t r = i / V.maxg, j = i - r * V.maxg;
+    if (j >= min(V.hdr(r).ng, V.maxg)) return;
+    idx[(uint64_t)r * T + dense[first_of[slot_of[i]]]] = j;
+}
+
+// one thread per dense group (its first occurrence h): COUNT / SUM / numeric counts
+// added over the ranks in rank order (a fixed order: the same sums every run), the
+// representative cells and first row (made whole-file) from the first occurrence;
+// written in pack_result_kernel's layout (executor.hip build_direct reads it).  The
+// header of `mail` gets the summed statistics, the group count and the status.
+__global__ void gm_combine_kernel(GmView V, const uint32_t* __restrict__ flag, const uint32_t* __restrict__ dense,
+                                  const uint32_t* __restrict__ idx, int grouped, uint32_t sb, uint8_t* __restrict__ dst,
+                                  unsigned int* __restrict__ gcount, uint8_t* __restrict__ mail,
+                                  const unsigned int* __restrict__ err) {
+    const uint32_t i = blockIdx.x * blockDim.x + threadIdx.x;
+    const uint32_t T = V.N * V.maxg;
+    uint32_t status = *err ? GM_FAILED : GM_OK;
+    for (uint32_t r = 0; r < V.N; r++) status = max(status, V.hdr(r).status);
+    uint32_t G = T ? dense[T - 1] + flag[T - 1] : 0u;
+    const bool zero = !grouped && G == 0;                 // no row anywhere: the one empty group
+    if (zero) G = 1;
+    const uint32_t nacc = V.nacc, R = V.R, ncell = R + nacc + 1;
+    const uint32_t orec = 40u + 40u * nacc;
+    if (i == 0) {
+        ScanStats st;
+        memset(&st, 0, sizeof st);
+        for (uint32_t r = 0; r < V.N; r++) {
+            st.records += V.hdr(r).records;
+            st.passed += V.hdr(r).passed;
+            st.slow_records += V.hdr(r).slow_records;
+            st.lds_spills += V.hdr(r).lds_spills;
+        }
+        memcpy(mail, &st, sizeof st);
+        *(uint32_t*)(mail + sizeof(ScanStats)) = status == GM_OK ? G : 0u;
+        *(uint32_t*)(mail + sizeof(ScanStats) + 4) = status;
+        gcount[0] = status == GM_OK ? G : 0u;
+        gcount[1] = status;
+    }
+    if (status != GM_OK) return;
+    uint32_t d = 0, hr = 0, hj = 0;
+    if (zero) {
+        if (i != 0) return;
+    } else {
+        if (i >= T || !flag[i]) return;
+        d = dense[i];
+        hr = i / V.maxg;
+        hj = i - hr * V.maxg;
+    }
+    uint8_t* op = dst + (uint64_t)d * orec;
+    Cell* oc = (Cell*)(dst + (uint64_t)G * orec) + (uint64_t)d * ncell;
+    uint8_t* ob = dst + (uint64_t)G * orec + (uint64_t)G * ncell * sizeof(Cell) + (uint64_t)d * ncell * sb;
+    uint64_t* oq = (uint64_t*)(op + 40);
+    if (zero) {
+        ((uint32_t*)op)[0] = (uint32_t)GK_ALL << 16;
+        ((uint32_t*)op)[1] = 0;
+        ((uint64_t*)op)[1] = 0;
+        ((uint64_t*)op)[2] = 0;
+        ((unsigned long long*)op)[3] = 0;
+        ((unsigned long long*)op)[4] = ~0ull;
+        for (uint32_t a = 0; a < nacc; a++) {
+            oq[5 * a] = 0; oq[5 * a + 1] = 0; oq[5 * a + 2] = 0; oq[5 * a + 3] = 0; oq[5 * a + 4] = ~0ull;
+        }
+        for (uint32_t k = 0; k < ncell; k++) oc[k] = cell_null();
+        return;
+    }
+    const uint8_t* hp = V.rec_at(hr, hj);
+    unsigned long long cnt = 0;
+    for (uint32_t r = 0; r < V.N; r++) {
+        const uint32_t j = idx[(uint64_t)r * T + d];
+        if (j == 0xFFFFFFFFu) continue;
+        const uint8_t* rp = V.rec_at(r, j);
+        cnt += ((const unsigned long long*)rp)[3];
+    }
+    ((uint32_t*)op)[0] = *(const uint32_t*)hp;
+    ((uint32_t*)op)[1] = 0;
+    ((uint64_t*)op)[1] = ((const uint64_t*)hp)[1];
+    ((uint64_t*)op)[2] = ((const uint64_t*)hp)[2];
+    ((unsigned long long*)op)[3] = cnt;
+    const unsigned long long f = ((const unsigned long long*)hp)[4];
+    ((unsigned long long*)op)[4] = f == ~0ull ? ~0ull : f + V.hdr(hr).base;
+    for (uint32_t a = 0; a < nacc; a++) {
+        double sum = 0.0;
+        unsigned long long num = 0;
+        for (uint32_t r = 0; r < V.N; r++) {
+            const uint32_t j = idx[(uint64_t)r * T + d];
+            if (j == 0xFFFFFFFFu) continue;
+            const uint64_t* q = (const uint64_t*)(V.rec_at(r, j) + 40);
+            if (q[2 * a + 1]) {
+                sum += __longlong_as_double((long long)q[2 * a]);
+                num += q[2 * a + 1];
+            }
+        }
+        oq[5 * a] = (uint64_t)__double_as_longlong(sum);
+        oq[5 * a + 1] = num;
+        oq[5 * a + 2] = 0;
+        oq[5 * a + 3] = 0;
+        oq[5 * a + 4] = ~0ull;
+    }
+    // cells: [R representative][nacc extremes (none here)][the key text]
+    const uint8_t* hc = hp + 40 + 16 * nacc;
+    for (uint32_t k = 0; k < ncell; k++) {
+        Cell c = cell_null();
+        const uint8_t* cc = nullptr;
+        if (k < R) cc = hc + (uint64_t)k * GM_CELL;
+        else if (k == ncell - 1) cc = hc + (uint64_t)R * GM_CELL;
+        if (cc) {
+            c.kind = ((const uint32_t*)cc)[0];
+            c.len = ((const uint32_t*)cc)[1];
+            c.bits = ((const uint64_t*)cc)[1];
+            if (c.kind == K_STR) {
+                const uint32_t nb = min(c.len, sb);
+                for (uint32_t w = 0; w < nb; w++) ob[(uint64_t)k * sb + w] = cc[16 + w];
+            }
+        }
+        oc[k] = c;
+    }
+}
+
 }  // namespace mg
 }  // namespace cq
 
 extern "C" {
+
+hipError_t cq_excl_sum_u32(void* temp, size_t* temp_bytes, const unsigned int* in, unsigned int* out, size_t n,
+                           hipStream_t s);
+
+// the root's whole gather-merge: dictionary, dense ids, per-rank index, combine.
+// state / first_of (cap slots) and idx (N * N * maxg words) must hold 0 / 0xFF bytes
+// on entry (cq_gm_merge_scratch sizes them); err zero
+size_t cq_gm_scan_bytes(uint32_t T) {
+    size_t tb = 0;
+    cq_excl_sum_u32(nullptr, &tb, nullptr, nullptr, T, nullptr);
+    return tb;
+}
+hipError_t cq_launch_gm_merge(const uint8_t* buf, uint64_t B, uint32_t N, uint32_t maxg, int nacc, uint32_t R,
+                              int grouped, uint32_t sb, uint32_t* state, uint32_t* rec_of, uint32_t* first_of, uint32_t cap,
+                              uint32_t* slot_of, uint32_t* flag, uint32_t* dense, uint32_t* idx, void* scan_temp,
+                              size_t scan_temp_bytes, unsigned int* err, uint8_t* dst, unsigned int* gcount,
+                              uint8_t* mail, hipStream_t s) {
+    cq::mg::GmView V{buf, B, N, maxg, cq::gm_rec_bytes(nacc, R), (uint32_t)nacc, R};
+    const uint32_t T = N * maxg;
+    const unsigned g = (T + 255) / 256;
+    hipLaunchKernelGGL(cq::mg::gm_dict_kernel, dim3(g), dim3(256), 0, s, V, state, rec_of, first_of, cap, slot_of, err);
+    hipLaunchKernelGGL(cq::mg::gm_flag_kernel, dim3(g), dim3(256), 0, s, V, slot_of, first_of, flag);
+    size_t tb = scan_temp_bytes;
+    hipError_t e = cq_excl_sum_u32(scan_temp, &tb, flag, dense, T, s);
+    if (e != hipSuccess) return e;
+    hipLaunchKernelGGL(cq::mg::gm_scatter_kernel, dim3(g), dim3(256), 0, s, V, slot_of, first_of, dense, idx);
+    hipLaunchKernelGGL(cq::mg::gm_combine_kernel, dim3(g), dim3(256), 0, s, V, flag, dense, idx, grouped, sb, dst, gcount,
+                       mail, err);
+    return hipGetLastError();
+}
 
 hipError_t cq_launch_dict_build(const void* all, const void* text, uint32_t n, uint32_t* state, uint32_t* rec_of,
                                 uint32_t* first_of, uint32_t cap, uint32_t* slot_of, unsigned int* err, hipStream_t s) {

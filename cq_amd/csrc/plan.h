@@ -9,7 +9,11 @@ constexpr int MAX_NEED = 8;     // distinct CSV columns one scan parses
 constexpr int MAX_PROG = 128;   // predicate instructions
 constexpr int MAX_CONST = 48;   // literal cells
 constexpr int MAX_ACC = 8;      // accumulators (one per aggregate SELECT item)
-constexpr int MAX_GPART = 8;    // composite GROUP BY parts (the reference's list grows without bound)
+constexpr int MAX_GPART = 64;   // composite GROUP BY parts (the reference's list grows without bound)
+// distinct columns of a plan, a join side or a projection on the cells path: plans
+// over more than MAX_NEED columns ("wide") read their cells from the parsed cell
+// tables (scan.hip PairView) instead of registers
+constexpr int MAX_WIDE = 256;
 constexpr int VM_STACK = 8;
 
 // predicate bytecode (WHERE tree of evaluator_conditions.c:62-164 and
@@ -92,7 +96,7 @@ struct ProjDesc {
 
 // finish_kernel (scan.hip): what to gather for every compacted group
 struct FinishDesc {
-    int16_t cols[MAX_NEED];   // representative columns, ascending
+    int16_t cols[MAX_WIDE];   // representative columns, ascending
     int32_t ncols;
     uint32_t delim;
     uint32_t quote;
@@ -104,7 +108,7 @@ struct FinishDesc {
 // INNER JOIN (evaluator_joins.c:63-181) on the device: columns of one side parsed
 // per record into a row-major cell array (ncols cells per row)
 struct ColsDesc {
-    int16_t cols[MAX_NEED];   // CSV columns, ascending
+    int16_t cols[MAX_WIDE];   // CSV columns, ascending
     int32_t ncols;
     uint32_t delim;
     uint32_t quote;
@@ -112,8 +116,8 @@ struct ColsDesc {
 // where each need slot of a plan over the joined row lives: side 0 = left cells,
 // 1 = right cells, col = index within that side's row of cells
 struct JoinMap {
-    int8_t side[MAX_NEED];
-    int8_t col[MAX_NEED];
+    int8_t side[MAX_WIDE];
+    int16_t col[MAX_WIDE];
     int32_t n;
     uint32_t lstride, rstride;
 };
@@ -201,5 +205,25 @@ struct GroupOut {
     Cell ext[MAX_ACC];
     unsigned long long extpos[MAX_ACC];
 };
+
+// gather-merge of range partials (multi-GPU, scan.hip gm_pack_kernel -> merge.hip
+// gm_*): per rank a GM_HDR-byte header, then up to maxg group records of
+// gm_rec_bytes(nacc, R): clslen u32, pad, w0, w1, COUNT, first (local offset),
+// per accumulator (SUM f64, numeric count), then R + 1 cells of GM_CELL bytes
+// (kind u32, len u32, bits, GM_TEXT bytes of STRING text; the last one is a long
+// key's text)
+constexpr uint32_t GM_HDR = 64, GM_CELL = 64, GM_TEXT = 48;
+enum : uint32_t { GM_OK = 0, GM_FAILED = 1, GM_DECLINE = 2 };
+struct GmHdr {
+    uint32_t status;        // GM_OK / GM_FAILED / GM_DECLINE
+    uint32_t ng;            // groups in this rank's records
+    uint64_t base;          // the rank's whole-file byte offset
+    uint64_t records, passed, slow_records, lds_spills;
+    uint64_t pad[2];
+};
+static_assert(sizeof(GmHdr) == GM_HDR, "gather-merge header");
+__host__ __device__ constexpr uint32_t gm_rec_bytes(int nacc, uint32_t R) {
+    return 40u + 16u * (uint32_t)nacc + GM_CELL * (R + 1u);
+}
 
 }  // namespace cq

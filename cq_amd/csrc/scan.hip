@@ -37,6 +37,7 @@
 // [range_begin, range_end) can be scanned independently: that is also how the
 // multi-GPU path shards a file.
 #include <hip/hip_runtime.h>
+#include <type_traits>
 #include <algorithm>
 #include <cstdlib>
 #include <cstring>
@@ -131,6 +132,23 @@ __device__ __forceinline__ Cell get_cell(const CellsT<N>& cs, int a, int n = N) 
         r = sel_cell(k == a, cs.c[k], r);
     }
     return r;
+}
+
+// A joined (or identity) pair's cells read in place from the sides' parsed cell
+// tables: plans over more than MAX_NEED columns ("wide") keep no register copy;
+// need slot a lives on side M->side[a] at cell M->col[a] of its row
+constexpr uint32_t JOIN_NONE = 0xFFFFFFFFu;      // pair side absent (outer joins): NULL cells
+struct PairView {
+    const JoinMap* M;
+    const Cell* L;
+    const Cell* R;
+    uint2 pr;
+};
+__device__ __forceinline__ Cell get_cell(const PairView& v, int a, int = 0) {
+    const bool right = v.M->side[a] != 0;
+    const uint32_t row = right ? v.pr.y : v.pr.x;
+    if (row == JOIN_NONE) return cell_null();
+    return right ? v.R[(uint64_t)row * v.M->rstride + v.M->col[a]] : v.L[(uint64_t)row * v.M->lstride + v.M->col[a]];
 }
 
 // the general cell parser (cell.h parse_cell) kept out of line: it carries the
@@ -300,8 +318,8 @@ struct Stack {
 
 // evaluate_condition (evaluator_conditions.c:62-164) over the flattened WHERE tree;
 // kc: the literal cells (LDS copy, string bytes staged in LDS)
-template <int N>
-__device__ __forceinline__ bool eval_where_vm(const ScanPlan& P, const Cell* kc, const CellsT<N>& cs) {
+template <class CS>
+__device__ __forceinline__ bool eval_where_vm(const ScanPlan& P, const Cell* kc, const CS& cs) {
     Stack st;
 #pragma unroll
     for (int j = 0; j < 8; j++) st.s[j] = cell_null();
@@ -1230,8 +1248,8 @@ __global__ void gather_kernel(const uint8_t* __restrict__ g,
 
 // evaluate_expression (evaluator_expressions.c:23-263) over one record's need
 // slots: a composite / expression GROUP BY part, prog[b, e)
-template <int N>
-__device__ Cell eval_expr_vm(const ScanPlan& P, const Cell* kc, const CellsT<N>& cs, uint32_t b, uint32_t e) {
+template <class CS>
+__device__ Cell eval_expr_vm(const ScanPlan& P, const Cell* kc, const CS& cs, uint32_t b, uint32_t e) {
     Stack st;
 #pragma unroll
     for (int j = 0; j < 8; j++) st.s[j] = cell_null();
@@ -1258,14 +1276,14 @@ __device__ Cell eval_expr_vm(const ScanPlan& P, const Cell* kc, const CellsT<N>&
 // CompKey); a part list with a tab inside a text part keys on its joined text
 // (cell.h joined_text_key).  `tab`: such a list held a DOUBLE part the joined
 // text cannot render (the plan is refused)
-template <int N>
-__device__ Cell plan_group_part(const ScanPlan& P, const Cell* kc, const CellsT<N>& cs, int nneed, int k) {
+template <class CS>
+__device__ Cell plan_group_part(const ScanPlan& P, const Cell* kc, const CS& cs, int nneed, int k) {
     const int s = P.gpart_slot[k];
     return s >= 0 ? get_cell(cs, s, nneed)
                   : (s == -1 ? eval_expr_vm(P, kc, cs, P.gcode_off[k], P.gcode_off[k + 1]) : cell_null());
 }
-template <int N>
-__device__ GKey plan_group_key(const ScanPlan& P, const Cell* kc, const CellsT<N>& cs, int nneed, bool& tab) {
+template <class CS>
+__device__ GKey plan_group_key(const ScanPlan& P, const Cell* kc, const CS& cs, int nneed, bool& tab) {
     if (P.ngpart == 0) return group_key(get_cell(cs, P.group_slot, nneed));
     CompKey ck;
     bool has_tab = false;
@@ -1285,7 +1303,12 @@ __device__ GKey plan_group_key(const ScanPlan& P, const Cell* kc, const CellsT<N
             ok = joined_text_add(h, plan_group_part(P, kc, cs, nneed, k), k == 0) && ok;
         }
         tab = tab || !ok;
-        return joined_text_key(h, (uint32_t)P.ngpart);
+        GKey k = joined_text_key(h, (uint32_t)P.ngpart);
+        if (P.test_digest_bits) {                      // test knob: force collisions
+            k.w0 &= (1ULL << P.test_digest_bits) - 1;
+            k.w1 = 0;
+        }
+        return k;
     }
     GKey k = comp_key(ck, (uint32_t)P.ngpart);
     if (P.test_digest_bits) {                          // test knob: force digest collisions
@@ -1765,8 +1788,6 @@ __global__ void join_count_kernel(const Cell* __restrict__ L, uint32_t ls, uint3
     cnt[l] = (outer_left && n == 0) ? 1 : n;             // LEFT / FULL: the unmatched row, NULL-padded
 }
 
-constexpr uint32_t JOIN_NONE = 0xFFFFFFFFu;      // pair side absent (outer joins): NULL cells
-
 __global__ void join_emit_kernel(const Cell* __restrict__ L, uint32_t ls, uint32_t lk, uint32_t nL, JoinRight J,
                                  const uint32_t* __restrict__ lo_in, const unsigned long long* __restrict__ cnt,
                                  const unsigned long long* __restrict__ offs, uint2* __restrict__ pairs,
@@ -1843,7 +1864,8 @@ __global__ void join_fill_kernel(const unsigned int* __restrict__ flags, const u
     pairs[at] = right_side ? make_uint2(JOIN_NONE, i) : make_uint2(i, JOIN_NONE);
 }
 
-// the plan's need slots of one joined row
+// the plan's need slots of one joined row: in registers (plans over <= MAX_NEED
+// columns), or a view of the cell tables (wide plans)
 __device__ __forceinline__ void join_cells(const JoinMap& M, const Cell* L, const Cell* R, uint2 pr,
                                            CellsT<MAX_NEED>& cs) {
 #pragma unroll
@@ -1856,6 +1878,14 @@ __device__ __forceinline__ void join_cells(const JoinMap& M, const Cell* L, cons
         }
     }
 }
+__device__ __forceinline__ void join_cells(const JoinMap& M, const Cell* L, const Cell* R, uint2 pr, PairView& v) {
+    v.M = &M;
+    v.L = L;
+    v.R = R;
+    v.pr = pr;
+}
+template <bool WIDE>
+using PairCells = typename std::conditional<WIDE, PairView, CellsT<MAX_NEED>>::type;
 
 // Exactness of composite GROUP BY keys (evaluator.c:113-212 groups by the parts' key
 // texts joined with '\t'; the kernels key such groups by a 128-bit digest of the
@@ -1863,7 +1893,7 @@ __device__ __forceinline__ void join_cells(const JoinMap& M, const Cell* L, cons
 // its parts, one by one under the canonical key equality, with the parts of its
 // group's first pair: a digest shared by two different part lists (a collision)
 // sets *bad and the host fails the query instead of merging them.  Joined-text keys
-// (a part holding a tab, COMPT_FLAG) are not re-checked here.
+// (a part holding a tab, COMPT_FLAG) compare the two joined texts byte for byte.
 static __device__ int g_find(const GroupTable& gt, const GKey k, uint64_t h) {
     const uint32_t tg = tag_of(h), mask = gt.cap - 1;
     for (uint32_t probe = 0; probe < gt.cap; probe++) {
@@ -1881,6 +1911,25 @@ static __device__ int g_find(const GroupTable& gt, const GKey k, uint64_t h) {
     }
     return -1;
 }
+
+// two part lists' joined texts (evaluator.c:113-212), compared exactly: lengths, then
+// 16-byte windows rendered from the parts again (joined-text keys are rare: a text
+// part holding a tab)
+template <class CS>
+__device__ bool joined_text_equal(const ScanPlan& P, const Cell* kc, const CS& a, const CS& b, int nneed) {
+    for (uint64_t lo = 0;; lo += 16) {
+        TextWindow x(lo), y(lo);
+        for (int k = 0; k < MAX_GPART; k++) {
+            if (k >= P.ngpart) break;
+            joined_text_add(x, plan_group_part(P, kc, a, nneed, k), k == 0);
+            joined_text_add(y, plan_group_part(P, kc, b, nneed, k), k == 0);
+        }
+        if (x.pos != y.pos || x.w0 != y.w0 || x.w1 != y.w1) return false;
+        if (lo + 16 >= x.pos) return true;
+    }
+}
+
+template <bool WIDE>
 __global__ __launch_bounds__(256) void comp_verify_kernel(const uint2* __restrict__ pairs, unsigned long long np,
                                                           JoinMap M, const Cell* __restrict__ L,
                                                           const Cell* __restrict__ R, unsigned int* __restrict__ bad) {
@@ -1889,19 +1938,23 @@ __global__ __launch_bounds__(256) void comp_verify_kernel(const uint2* __restric
     const int nneed = P.nneed;
     for (unsigned long long i = (unsigned long long)blockIdx.x * blockDim.x + threadIdx.x; i < np;
          i += (unsigned long long)gridDim.x * blockDim.x) {
-        CellsT<MAX_NEED> cs;
+        PairCells<WIDE> cs;
         join_cells(M, L, R, pairs[i], cs);
         if (P.nprog != 0 && !eval_where_vm(P, P.consts, cs)) continue;
         bool tab = false;
         const GKey key = plan_group_key(P, P.consts, cs, nneed, tab);
-        if (key.cls != GK_COMP || (key.len & COMPT_FLAG)) continue;
+        if (key.cls != GK_COMP) continue;
         const int gi = g_find(gt, key, gk_hash(key));
         if (gi < 0) { atomicOr(bad, 2u); continue; }
         const unsigned long long f = gt.first[gi];
         if (f == i) continue;
         if (f >= np) { atomicOr(bad, 2u); continue; }
-        CellsT<MAX_NEED> cf;
+        PairCells<WIDE> cf;
         join_cells(M, L, R, pairs[f], cf);
+        if (key.len & COMPT_FLAG) {                    // the joined text itself
+            if (!joined_text_equal(P, P.consts, cs, cf, nneed)) atomicOr(bad, 1u);
+            continue;
+        }
         bool same = true;
         for (int k = 0; k < MAX_GPART; k++) {
             if (k >= P.ngpart) break;
@@ -1916,6 +1969,7 @@ __global__ __launch_bounds__(256) void comp_verify_kernel(const uint2* __restric
 // WHERE + GROUP BY + aggregates over the joined rows (filter_rows, create_groups,
 // evaluate_aggregate over perform_join's table); a group's `first` is its first
 // pair's index, i.e. its first row of the joined table
+template <bool WIDE>
 __global__ __launch_bounds__(256) void join_agg_kernel(const uint2* __restrict__ pairs, unsigned long long np,
                                                        JoinMap M, const Cell* __restrict__ L,
                                                        const Cell* __restrict__ R, ScanStats* __restrict__ stats,
@@ -1935,15 +1989,10 @@ __global__ __launch_bounds__(256) void join_agg_kernel(const uint2* __restrict__
          b0 += (unsigned long long)gridDim.x * blockDim.x) {
         const unsigned long long i = b0 + threadIdx.x;
         const bool valid = i < np;
-        CellsT<MAX_NEED> cs;
+        PairCells<WIDE> cs;
         bool pass = false;
-        if (valid) {
-            join_cells(M, L, R, pairs[i], cs);
-            pass = P.nprog == 0 || eval_where_vm(P, P.consts, cs);
-        } else {
-#pragma unroll
-            for (int k = 0; k < MAX_NEED; k++) cs.c[k] = cell_null();
-        }
+        join_cells(M, L, R, valid ? pairs[i] : make_uint2(JOIN_NONE, JOIN_NONE), cs);
+        if (valid) pass = P.nprog == 0 || eval_where_vm(P, P.consts, cs);
         if (pass) {
             my_pass++;
 #pragma unroll
@@ -2038,6 +2087,7 @@ __global__ __launch_bounds__(256) void join_agg_kernel(const uint2* __restrict__
 // and a few atomics per (block, group) instead of per pair.  Pairs whose group
 // finds no slot within JS_PROBES probes take join_agg_kernel's HBM path.
 constexpr uint32_t JS_SLOTS = 1024, JS_PROBES = 64;
+template <bool WIDE>
 __global__ __launch_bounds__(512) __attribute__((amdgpu_waves_per_eu(4))) void join_sum_kernel(const uint2* __restrict__ pairs, unsigned long long np,
                                                        JoinMap M, const Cell* __restrict__ L,
                                                        const Cell* __restrict__ R, ScanStats* __restrict__ stats) {
@@ -2063,15 +2113,10 @@ __global__ __launch_bounds__(512) __attribute__((amdgpu_waves_per_eu(4))) void j
          b0 += (unsigned long long)gridDim.x * blockDim.x) {
         const unsigned long long i = b0 + threadIdx.x;
         const bool valid = i < np;
-        CellsT<MAX_NEED> cs;
+        PairCells<WIDE> cs;
         bool pass = false;
-        if (valid) {
-            join_cells(M, L, R, pairs[i], cs);
-            pass = P.nprog == 0 || eval_where_vm(P, P.consts, cs);
-        } else {
-#pragma unroll
-            for (int k = 0; k < MAX_NEED; k++) cs.c[k] = cell_null();
-        }
+        join_cells(M, L, R, valid ? pairs[i] : make_uint2(JOIN_NONE, JOIN_NONE), cs);
+        if (valid) pass = P.nprog == 0 || eval_where_vm(P, P.consts, cs);
         GKey key;
         key.cls = GK_ALL; key.len = 0; key.w0 = 0; key.w1 = 0;
         uint64_t h = 0;
@@ -2170,13 +2215,14 @@ __global__ __launch_bounds__(512) __attribute__((amdgpu_waves_per_eu(4))) void j
 }
 
 // WHERE over the joined rows of a row-returning query: 1 / 0 per pair
+template <bool WIDE>
 __global__ void join_filter_kernel(const uint2* __restrict__ pairs, unsigned long long np, JoinMap M,
                                    const Cell* __restrict__ L, const Cell* __restrict__ R,
                                    unsigned int* __restrict__ flags) {
     const ScanPlan& P = c_plan;
     const unsigned long long i = (unsigned long long)blockIdx.x * blockDim.x + threadIdx.x;
     if (i >= np) return;
-    CellsT<MAX_NEED> cs;
+    PairCells<WIDE> cs;
     join_cells(M, L, R, pairs[i], cs);
     flags[i] = (P.nprog == 0 || eval_where_vm(P, P.consts, cs)) ? 1u : 0u;
 }
@@ -2269,6 +2315,7 @@ __global__ void vla_prep_kernel(const Cell* __restrict__ cells, uint32_t n, uint
 // the same per (l, r) pair of parsed cells (joins, composite / expression keys
 // over identity pairs): WHERE by the plan's VM, the group key as join_agg_kernel
 // computes it (plan_group_key), the value from V's one column
+template <bool WIDE>
 __global__ void vla_pair_prep_kernel(const uint2* __restrict__ pairs, uint32_t n, JoinMap M, JoinMap V,
                                      const Cell* __restrict__ L, const Cell* __restrict__ R, int grouped,
                                      unsigned long long* __restrict__ kw0, unsigned long long* __restrict__ kw1,
@@ -2278,7 +2325,7 @@ __global__ void vla_pair_prep_kernel(const uint2* __restrict__ pairs, uint32_t n
     const uint32_t i = blockIdx.x * blockDim.x + threadIdx.x;
     if (i >= n) return;
     const uint2 pr = pairs[i];
-    CellsT<MAX_NEED> cs;
+    PairCells<WIDE> cs;
     join_cells(M, L, R, pr, cs);
     const bool pass = P.nprog == 0 || eval_where_vm(P, P.consts, cs);
     GKey k;
@@ -2622,6 +2669,50 @@ namespace cq {
 // row, index) order: create_groups' first-appearance order, so the host does not
 // sort.  `hdr` (optional) receives the scan statistics and the group count.
 constexpr uint32_t PACK_ORDER_MAX = 8192;
+// group i's rank in first-appearance order (by first-row offset, ties by index):
+// an LDS-tiled count of the groups before it; every thread of the block calls it
+__device__ uint32_t first_rank(const GroupOut* __restrict__ out, uint32_t ng, uint32_t i) {
+    __shared__ unsigned long long tile[1024];
+    const unsigned long long fi = i < ng ? out[i].first : 0ull;
+    uint32_t below = 0;
+    for (uint32_t base = 0; base < ng; base += 1024) {
+        const uint32_t m = min(1024u, ng - base);
+        __syncthreads();
+        {   // eight independent loads in flight per thread (GroupOut rows are 360 bytes apart)
+            unsigned long long t[8];
+#pragma unroll
+            for (int u = 0; u < 8; u++) {
+                const uint32_t k = threadIdx.x + u * blockDim.x;
+                t[u] = k < m ? out[base + k].first : 0ull;
+            }
+#pragma unroll
+            for (int u = 0; u < 8; u++) {
+                const uint32_t k = threadIdx.x + u * blockDim.x;
+                if (k < m) tile[k] = t[u];
+            }
+            for (uint32_t k = threadIdx.x + 8 * blockDim.x; k < m; k += blockDim.x) tile[k] = out[base + k].first;
+        }
+        __syncthreads();
+        if (i < ng) {
+            // eight independent LDS reads in flight per trip (a one-at-a-time loop
+            // waits out the LDS latency per element: ~30 us for 1,000 groups)
+            uint32_t k = 0;
+            for (; k + 8 <= m; k += 8) {
+                unsigned long long f[8];
+#pragma unroll
+                for (int u = 0; u < 8; u++) f[u] = tile[k + u];
+#pragma unroll
+                for (int u = 0; u < 8; u++) below += (f[u] < fi) | ((f[u] == fi) & (base + k + u < i));
+            }
+            for (; k < m; k++) {
+                const unsigned long long f = tile[k];
+                below += (f < fi) | ((f == fi) & (base + k < i));
+            }
+        }
+    }
+    return below;
+}
+
 __global__ void pack_result_kernel(const GroupOut* __restrict__ out, const unsigned int* __restrict__ count,
                                    unsigned int cap_out, int nacc, const Cell* __restrict__ cells,
                                    const uint8_t* __restrict__ bytes, uint32_t ncell, uint32_t sb,
@@ -2635,48 +2726,7 @@ __global__ void pack_result_kernel(const GroupOut* __restrict__ out, const unsig
         for (uint32_t k = threadIdx.x; k < nw; k += blockDim.x) ((uint32_t*)hdr)[k] = ((const uint32_t*)stats)[k];
         if (threadIdx.x == 0) *(uint32_t*)(hdr + sizeof(ScanStats)) = ng;
     }
-    uint32_t r = i;
-    if (order && ng <= PACK_ORDER_MAX) {
-        __shared__ unsigned long long tile[1024];
-        const unsigned long long fi = i < ng ? out[i].first : 0ull;
-        uint32_t below = 0;
-        for (uint32_t base = 0; base < ng; base += 1024) {
-            const uint32_t m = min(1024u, ng - base);
-            __syncthreads();
-            {   // eight independent loads in flight per thread (GroupOut rows are 360 bytes apart)
-                unsigned long long t[8];
-#pragma unroll
-                for (int u = 0; u < 8; u++) {
-                    const uint32_t k = threadIdx.x + u * blockDim.x;
-                    t[u] = k < m ? out[base + k].first : 0ull;
-                }
-#pragma unroll
-                for (int u = 0; u < 8; u++) {
-                    const uint32_t k = threadIdx.x + u * blockDim.x;
-                    if (k < m) tile[k] = t[u];
-                }
-                for (uint32_t k = threadIdx.x + 8 * blockDim.x; k < m; k += blockDim.x) tile[k] = out[base + k].first;
-            }
-            __syncthreads();
-            if (i < ng) {
-                // eight independent LDS reads in flight per trip (a one-at-a-time loop
-                // waits out the LDS latency per element: ~30 us for 1,000 groups)
-                uint32_t k = 0;
-                for (; k + 8 <= m; k += 8) {
-                    unsigned long long f[8];
-#pragma unroll
-                    for (int u = 0; u < 8; u++) f[u] = tile[k + u];
-#pragma unroll
-                    for (int u = 0; u < 8; u++) below += (f[u] < fi) | ((f[u] == fi) & (base + k + u < i));
-                }
-                for (; k < m; k++) {
-                    const unsigned long long f = tile[k];
-                    below += (f < fi) | ((f == fi) & (base + k < i));
-                }
-            }
-        }
-        r = below;
-    }
+    const uint32_t r = (order && ng <= PACK_ORDER_MAX) ? first_rank(out, ng, i) : i;
     if (i >= ng) return;
     // every load of the group's record first, then the stores (interleaved, each
     // store waited on its load)
@@ -2753,6 +2803,80 @@ hipError_t cq_launch_pack_result(const cq::GroupOut* out, const unsigned int* co
     return hipGetLastError();
 }
 unsigned int cq_pack_order_max() { return cq::PACK_ORDER_MAX; }
+
+namespace cq {
+// ---- gather-merge (multi-GPU, executor.hip dist_query): this rank's groups in its
+// own first-appearance order as self-contained records (no table addresses) for the
+// root's merge (merge.hip gm_*).  Send buffer: a 64-byte header, then maxg records
+// of gm_rec_bytes(nacc, R) (layout in plan.h GmHdr / GM_* offsets).  A group the
+// format cannot carry (more than maxg groups, a representative STRING or long key
+// over GM_TEXT bytes) sets the header's status to GM_DECLINE.
+__global__ void gm_pack_kernel(const GroupOut* __restrict__ out, const unsigned int* __restrict__ count,
+                               unsigned int cap_out, int nacc, uint32_t R, const Cell* __restrict__ cells,
+                               const uint8_t* __restrict__ bytes, uint32_t sb, uint32_t maxg, uint8_t* __restrict__ dst,
+                               const ScanStats* __restrict__ stats, uint8_t* __restrict__ hdr) {
+    const uint32_t ng = min(*count, cap_out);
+    const uint32_t i = blockIdx.x * blockDim.x + threadIdx.x;
+    GmHdr* H = (GmHdr*)dst;
+    if (blockIdx.x == 0) {
+        if (hdr) {   // the local mailbox header (statistics and group count, as pack_result)
+            const uint32_t nw = (uint32_t)(sizeof(ScanStats) / 4);
+            for (uint32_t k = threadIdx.x; k < nw; k += blockDim.x) ((uint32_t*)hdr)[k] = ((const uint32_t*)stats)[k];
+            if (threadIdx.x == 0) *(uint32_t*)(hdr + sizeof(ScanStats)) = ng;
+        }
+        if (threadIdx.x == 0) {
+            H->ng = min(ng, maxg);
+            H->records = stats->records;
+            H->passed = stats->passed;
+            H->slow_records = stats->slow_records;
+            H->lds_spills = stats->lds_spills;
+            if (ng > maxg) atomicMax(&H->status, GM_DECLINE);
+        }
+    }
+    if (ng > maxg) return;
+    const uint32_t r = first_rank(out, ng, i);
+    if (i >= ng) return;
+    const uint32_t ncell = R + (uint32_t)nacc + 1;
+    const GroupOut o = out[i];
+    uint8_t* rp = dst + GM_HDR + (size_t)r * gm_rec_bytes(nacc, R);
+    const bool longk = (o.clslen >> 16) == GK_LONG;
+    ((uint32_t*)rp)[0] = o.clslen;
+    ((uint32_t*)rp)[1] = 0;
+    ((uint64_t*)rp)[1] = longk ? 0ull : o.w0;       // (GK_LONG: w0 is a table address; the text follows)
+    ((uint64_t*)rp)[2] = o.w1;
+    ((unsigned long long*)rp)[3] = o.cnt;
+    ((unsigned long long*)rp)[4] = o.first;
+    uint64_t* q = (uint64_t*)(rp + 40);
+    for (int a = 0; a < nacc; a++) {
+        q[2 * a] = dbl_bits(o.sum[a]);
+        q[2 * a + 1] = o.num[a];
+    }
+    uint8_t* cp = rp + 40 + 16 * (uint32_t)nacc;
+    for (uint32_t k = 0; k <= R; k++) {
+        // representative cells, then the key text of a long key (finish_kernel's last cell)
+        const uint32_t src = k < R ? k : ncell - 1;
+        Cell c = cells[(size_t)i * ncell + src];
+        if (k == R && !longk) c = cell_null();
+        uint8_t* cc = cp + (size_t)k * GM_CELL;
+        ((uint32_t*)cc)[0] = c.kind;
+        ((uint32_t*)cc)[1] = c.len;
+        ((uint64_t*)cc)[1] = c.kind == K_STR ? 0ull : c.bits;
+        if (c.kind == K_STR) {
+            if (c.len > GM_TEXT || c.len > sb) atomicMax(&H->status, GM_DECLINE);
+            const uint8_t* sbs = bytes + ((size_t)i * ncell + src) * sb;
+            const uint32_t nb = min(min(c.len, (uint32_t)GM_TEXT), sb);
+            for (uint32_t w = 0; w < nb; w++) cc[16 + w] = sbs[w];
+        }
+    }
+}
+}  // namespace cq
+hipError_t cq_launch_gm_pack(const cq::GroupOut* out, const unsigned int* count, unsigned int cap_out, int nacc,
+                             uint32_t R, const cq::Cell* cells, const uint8_t* bytes, uint32_t sb, uint32_t maxg,
+                             uint8_t* dst, const cq::ScanStats* stats, uint8_t* hdr, hipStream_t s) {
+    hipLaunchKernelGGL(cq::gm_pack_kernel, dim3((cap_out + 127) / 128), dim3(128), 0, s, out, count, cap_out, nacc, R,
+                       cells, bytes, sb, maxg, dst, stats, hdr);
+    return hipGetLastError();
+}
 hipError_t cq_launch_finish(const uint8_t* g, uint64_t n, const cq::GroupOut* out, const unsigned int* count,
                             unsigned int cap_out, const cq::FinishDesc* D, cq::Cell* cells, uint8_t* bytes,
                             hipStream_t s) {
@@ -2841,7 +2965,10 @@ hipError_t cq_launch_join_agg(const uint2* pairs, unsigned long long np, const c
     if (e == hipSuccess) e = cq::upload_symbol((const void*)&HIP_SYMBOL(cq::c_gt), gt, sizeof *gt, s);
     if (e != hipSuccess || !np) return e;
     const unsigned grid = (unsigned)std::min<uint64_t>(grid_of(np, 256), 4096);
-    hipLaunchKernelGGL(cq::join_agg_kernel, dim3(grid), dim3(256), 0, s, pairs, np, *M, L, R, stats, grouped);
+    if (M->n > cq::MAX_NEED)
+        hipLaunchKernelGGL(cq::join_agg_kernel<true>, dim3(grid), dim3(256), 0, s, pairs, np, *M, L, R, stats, grouped);
+    else
+        hipLaunchKernelGGL(cq::join_agg_kernel<false>, dim3(grid), dim3(256), 0, s, pairs, np, *M, L, R, stats, grouped);
     return hipGetLastError();
 }
 hipError_t cq_launch_comp_verify(const uint2* pairs, unsigned long long np, const cq::JoinMap* M, const cq::Cell* L,
@@ -2851,7 +2978,10 @@ hipError_t cq_launch_comp_verify(const uint2* pairs, unsigned long long np, cons
     if (e == hipSuccess) e = cq::upload_symbol((const void*)&HIP_SYMBOL(cq::c_gt), gt, sizeof *gt, s);
     if (e != hipSuccess || !np) return e;
     const unsigned grid = (unsigned)std::min<uint64_t>(grid_of(np, 256), 4096);
-    hipLaunchKernelGGL(cq::comp_verify_kernel, dim3(grid), dim3(256), 0, s, pairs, np, *M, L, R, bad);
+    if (M->n > cq::MAX_NEED)
+        hipLaunchKernelGGL(cq::comp_verify_kernel<true>, dim3(grid), dim3(256), 0, s, pairs, np, *M, L, R, bad);
+    else
+        hipLaunchKernelGGL(cq::comp_verify_kernel<false>, dim3(grid), dim3(256), 0, s, pairs, np, *M, L, R, bad);
     return hipGetLastError();
 }
 size_t cq_join_sum_lds(int nacc) { return (size_t)cq::JS_SLOTS * (32 + 12 * (size_t)nacc); }
@@ -2863,14 +2993,20 @@ hipError_t cq_launch_join_sum(const uint2* pairs, unsigned long long np, const c
     if (e != hipSuccess || !np) return e;
     const size_t lds = cq_join_sum_lds(P->nacc);
     const unsigned grid = (unsigned)std::min<uint64_t>(grid_of(np, 512), (uint64_t)std::max(ncu, 1) * 2);
-    hipLaunchKernelGGL(cq::join_sum_kernel, dim3(grid), dim3(512), lds, s, pairs, np, *M, L, R, stats);
+    if (M->n > cq::MAX_NEED)
+        hipLaunchKernelGGL(cq::join_sum_kernel<true>, dim3(grid), dim3(512), lds, s, pairs, np, *M, L, R, stats);
+    else
+        hipLaunchKernelGGL(cq::join_sum_kernel<false>, dim3(grid), dim3(512), lds, s, pairs, np, *M, L, R, stats);
     return hipGetLastError();
 }
 hipError_t cq_launch_join_filter(const uint2* pairs, unsigned long long np, const cq::JoinMap* M, const cq::Cell* L,
                                  const cq::Cell* R, const cq::ScanPlan* P, unsigned int* flags, hipStream_t s) {
     hipError_t e = cq::upload_symbol((const void*)&HIP_SYMBOL(cq::c_plan), P, sizeof *P, s);
     if (e != hipSuccess || !np) return e;
-    hipLaunchKernelGGL(cq::join_filter_kernel, dim3(grid_of(np, 256)), dim3(256), 0, s, pairs, np, *M, L, R, flags);
+    if (M->n > cq::MAX_NEED)
+        hipLaunchKernelGGL(cq::join_filter_kernel<true>, dim3(grid_of(np, 256)), dim3(256), 0, s, pairs, np, *M, L, R, flags);
+    else
+        hipLaunchKernelGGL(cq::join_filter_kernel<false>, dim3(grid_of(np, 256)), dim3(256), 0, s, pairs, np, *M, L, R, flags);
     return hipGetLastError();
 }
 hipError_t cq_launch_join_project(const uint2* pairs, unsigned long long np, const unsigned int* flags,
@@ -2897,8 +3033,12 @@ hipError_t cq_launch_vla_pair_prep(const uint2* pairs, uint32_t n, const cq::Joi
                                    unsigned long long* vkey, unsigned int* flag, hipStream_t s) {
     hipError_t e = cq::upload_symbol((const void*)&HIP_SYMBOL(cq::c_plan), P, sizeof *P, s);
     if (e != hipSuccess || !n) return e;
-    hipLaunchKernelGGL(cq::vla_pair_prep_kernel, dim3(grid_of(n, 256)), dim3(256), 0, s, pairs, n, *M, *V, L, R, grouped,
-                       kw0, kw1, kcl, vkey, flag);
+    if (M->n > cq::MAX_NEED)
+        hipLaunchKernelGGL(cq::vla_pair_prep_kernel<true>, dim3(grid_of(n, 256)), dim3(256), 0, s, pairs, n, *M, *V, L, R,
+                           grouped, kw0, kw1, kcl, vkey, flag);
+    else
+        hipLaunchKernelGGL(cq::vla_pair_prep_kernel<false>, dim3(grid_of(n, 256)), dim3(256), 0, s, pairs, n, *M, *V, L,
+                           R, grouped, kw0, kw1, kcl, vkey, flag);
     return hipGetLastError();
 }
 hipError_t cq_launch_vla_prep(const cq::Cell* cells, uint32_t n, uint32_t nc, int gslot, uint32_t vslot,

@@ -266,6 +266,35 @@ def scan_partitioned_dense(ast, table, comm_device=None):
         part.free()
 
 
+def init_library_comm(device: torch.device | str | None = None) -> None:
+    """Create the library's own RCCL communicator on this rank's device (once per
+    process, before the first scan_partitioned_rccl): rank 0's unique id reaches
+    the other ranks through the torch.distributed group (any backend)."""
+    import cq_amd
+    rank, world = dist.get_rank(), dist.get_world_size()
+    dev = torch.device(device) if device is not None else torch.device("cuda", torch.cuda.current_device())
+    comm = dev if dist.get_backend() == "nccl" else torch.device("cpu")
+    uid = cq_amd.comm_unique_id() if rank == 0 else bytes(cq_amd.COMM_ID_BYTES)
+    t = torch.frombuffer(bytearray(uid), dtype=torch.uint8).to(comm)
+    dist.broadcast(t, 0)
+    cq_amd.comm_init(bytes(t.cpu().numpy()), rank, world)
+
+
+def scan_partitioned_rccl(ast, table):
+    """One range-partitioned query step with the whole merge inside the library
+    (cqgpu_dist_query over its own RCCL communicator, init_library_comm): no
+    Python collective, no per-stage host agreement.  Returns (result pointer on
+    rank 0 / None elsewhere, path name); raises PeerFailure on EVERY rank when any
+    rank failed.  Every rank must call it."""
+    import cq_amd
+    tp, status, path = cq_amd.dist_query_raw(ast, table)
+    if status != 0:
+        raise PeerFailure(f"rank {dist.get_rank()}: {cq_amd.last_error()}")
+    if dist.get_rank() == 0 and tp is None:
+        raise RuntimeError(cq_amd.last_error() or cq_amd.last_ineligible() or "cqgpu_dist_query failed")
+    return tp, cq_amd.DIST_PATHS.get(path, str(path))
+
+
 def join_partitioned(ast, lshard, rshard, lheader: bytes, rheader: bytes, device: torch.device | str,
                      comm_device: torch.device | str | None = None):
     """Repartitioned INNER JOIN over this rank's shards of both inputs.

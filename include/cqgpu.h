@@ -137,6 +137,39 @@ int cqgpu_partial_put(cqgpu_partial* p, void* dev_dst);
 cq_table* cqgpu_partial_result(cqgpu_partial* p, cq_node* query_ast);
 void cqgpu_partial_free(cqgpu_partial* p);
 
+/* ---- the whole N > 1 step inside the library, over RCCL ---
+ * One process per GPU.  The launcher creates the communicator once: rank 0 calls
+ * cqgpu_comm_unique_id, broadcasts the CQGPU_COMM_ID_BYTES bytes to the other ranks
+ * by any means (bench.py / cq_amd.dist: torch.distributed), then every rank calls
+ * cqgpu_comm_init on its current HIP device.  Replaces the caller-driven
+ * cqgpu_partial_next / put loop (kept above for the CPU choreography tests):
+ * every collective runs on the library's own stream, a rank-local failure travels
+ * as a status word inside the payloads, and the host synchronises only where a
+ * size is data-dependent.
+ *
+ * cqgpu_dist_query: this rank's range shard (cqgpu_table_open_range) of the FROM
+ * table.  Every rank calls it with the same query.  Plans whose items are COUNT /
+ * SUM / AVG / group columns / constants over a one-column (or no) GROUP BY take the
+ * gather-merge: each rank packs its groups (first-appearance order, no table
+ * addresses) and sends them to rank 0, whose device merges them (dictionary of
+ * first occurrences = the global first-appearance order, sums in rank order,
+ * representative cells of the first occurrence) -- one collective plus the final
+ * status broadcast.  Other aggregates run the dense merge above over RCCL
+ * (all_gather of keys, MIN / SUM all-reduces, SUM reduces to rank 0); MEDIAN and
+ * row-returning SELECTs the partial blobs (one all_gather).  Rank 0 returns the
+ * result (evaluate_query's contract), the other ranks NULL.  *status: 0, or -1 on
+ * EVERY rank when any rank failed (cqgpu_last_error: this rank's message or "a
+ * peer rank failed"). *path (optional): 1 gather-merge, 2 dense, 3 blobs. */
+#define CQGPU_COMM_ID_BYTES 128
+int cqgpu_comm_unique_id(void* id_out);
+int cqgpu_comm_init(const void* id, int rank, int world);
+void cqgpu_comm_destroy(void);
+cq_table* cqgpu_dist_query(cq_node* query_ast, cqgpu_table* shard, int* status, int* path);
+/* test entry: the gather-merge of `n` shards held by this one process (simulated
+ * ranks, no RCCL): every shard's pack, then rank 0's merge kernels; NULL +
+ * cqgpu_last_ineligible when the plan or the data leaves the gather-merge */
+cq_table* cqgpu_gm_local(cq_node* query_ast, cqgpu_table* const* shards, int n);
+
 /* ---- join-key repartition for the multi-GPU JOIN ---
  * One INNER / LEFT / RIGHT / FULL JOIN with an `ident = ident` ON (reference
  * evaluator_joins.c:40-60, :63-181) over range-partitioned inputs: every rank routes each record of its
@@ -187,6 +220,7 @@ typedef struct {
     uint64_t slow_records;       /* records the fast field path handed to the general parser */
     uint64_t passed;             /* records that passed WHERE */
     int scan_kernel;             /* 2 = fast_kernel, 1 = lean_kernel (both wave-autonomous), 0 = general scan_kernel */
+    int wide;                    /* 1 = a plan over more than 8 distinct columns (cells path, scan.hip PairView) */
 } cqgpu_stats;
 int cqgpu_last_stats(cqgpu_stats* out);
 const char* cqgpu_last_error(void);

@@ -1,0 +1,54 @@
+"""Worker for tests/test_gpu_dist_rccl.py (run under torch.distributed.run): the
+library's own RCCL communicator (cq_amd.dist.init_library_comm), then every query
+of argv through cqgpu_dist_query on this rank's range shard; rank 0 writes the
+results (and the merge path each took) as JSON to the output file."""
+import json
+import os
+import sys
+
+import torch
+import torch.distributed as dist
+
+sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
+sys.path.insert(0, os.path.dirname(os.path.abspath(__file__)))
+
+
+def main():
+    path, out, sqls = sys.argv[1], sys.argv[2], json.loads(sys.argv[3])
+    rank, world = int(os.environ["RANK"]), int(os.environ["WORLD_SIZE"])
+    local = int(os.environ.get("LOCAL_RANK", "0"))
+    torch.cuda.set_device(local)
+    dist.init_process_group("nccl", device_id=torch.device("cuda", local))
+    import cqtest
+    import cq_amd
+    from cq_amd import abi
+    from cq_amd.dist import init_library_comm
+    init_library_comm()
+    t = cq_amd.Table.open_range(path, rank, world)
+    results = []
+    for sql in sqls:
+        with cqtest.Parsed(sql.format(p=path)) as ast:
+            got = None
+            for _ in range(2):                      # a warm-up step, then the kept one
+                tp, status, p = cq_amd.dist_query_raw(ast, t)
+                if got is not None or status != 0:
+                    break
+                if tp:
+                    got = abi.table_to_py(tp)
+                    cq_amd.result_free(tp)
+                else:
+                    got = "none"
+            results.append({"sql": sql, "status": status, "path": p, "error": cq_amd.last_error(),
+                            "result": None if got in (None, "none") else
+                            {"columns": got["columns"], "rows": [[list(c) for c in r] for r in got["rows"]]}})
+    t.close()
+    cq_amd.comm_destroy()
+    if rank == 0:
+        with open(out, "w") as fh:
+            json.dump(results, fh, default=lambda b: b.decode("latin-1") if isinstance(b, bytes) else str(b))
+    dist.barrier()
+    dist.destroy_process_group()
+
+
+if __name__ == "__main__":
+    main()

@@ -104,6 +104,24 @@ EDGE = {
 }
 
 
+def wide_bytes(rows=600, seed=12):
+    """12 columns (more than a fused scan's 8 need slots): ints, decimals, short
+    strings, a key column, NULL (empty) cells in c10"""
+    import numpy as np
+    rng = np.random.default_rng(seed)
+    out = ["c0,c1,c2,c3,c4,c5,c6,c7,c8,c9,c10,c11"]
+    for i in range(rows):
+        c = [str(int(rng.integers(0, 100))) for _ in range(4)]
+        c.append("%d.%02d" % (rng.integers(0, 9), rng.integers(0, 100)))
+        c.append(["x", "yy", "zz", "w w", "alpha"][int(rng.integers(0, 5))])
+        c += [str(int(rng.integers(-50, 1000))) for _ in range(3)]
+        c.append("k%d" % rng.integers(0, 7))
+        c.append("" if rng.integers(0, 30) == 0 else str(int(rng.integers(0, 5000))))
+        c.append("%d.%d" % (rng.integers(0, 300), rng.integers(0, 10)))
+        out.append(",".join(c))
+    return ("\n".join(out) + "\n").encode()
+
+
 def write_fixtures():
     os.makedirs(DATA, exist_ok=True)
     for f in sorted(os.listdir(os.path.join(REF, "data"))):
@@ -120,6 +138,8 @@ def write_fixtures():
         fh.write(datagen.users_bytes(1500, seed=9))
     with open(os.path.join(DATA, "synth_orders.csv"), "wb") as fh:
         fh.write(datagen.orders_bytes(2500, 1800, seed=10))
+    with open(os.path.join(DATA, "synth_wide.csv"), "wb") as fh:
+        fh.write(wide_bytes())
 
 
 # ---------------------------------------------------------------- query corpus
@@ -131,6 +151,8 @@ A = "'{D}/synth_a.csv'"
 SU = "'{D}/synth_users.csv'"
 SO = "'{D}/synth_orders.csv'"
 P = "'{D}/products.csv'"
+W = "'{D}/synth_wide.csv'"
+WIDE9 = "c0 > 5 AND c1 < 95 AND c2 != 50 AND c3 >= 3 AND c4 > 0.5 AND c5 != 'yy' AND c6 < 900 AND c7 > -40 AND c8 > 0"
 QUERIES = [
     # config 1 (plumbing) and filter + COUNT
     f"SELECT COUNT(*) FROM {T} WHERE age > 30",
@@ -190,14 +212,16 @@ QUERIES = [
     f"SELECT name, COUNT(*) FROM {A} WHERE age > 30 GROUP BY name",
     f"SELECT COUNT(*) FROM {A} WHERE age > 30",
     f"SELECT COUNT(*) FROM {R} WHERE age > 30",
-    f"SELECT COUNT(*), SUM(height), AVG(height), MIN(age), MAX(age) FROM {R} WHERE age > 30",
+    f"SELECT COUNT(*), SUM(height), MIN(age), MAX(age) FROM {R} WHERE age > 30",
+    f"SELECT COUNT(*), AVG(height) FROM {R} WHERE age > 30",
     # edge typing through queries
     "SELECT COUNT(*) FROM '{D}/edge_numbers.csv' WHERE a > 0",
     "SELECT a, COUNT(*) FROM '{D}/edge_numbers.csv' GROUP BY a",
     "SELECT b, COUNT(*) FROM '{D}/edge_numbers.csv' GROUP BY b",
     "SELECT d, COUNT(*) FROM '{D}/edge_numbers.csv' GROUP BY d",
     "SELECT SUM(a), SUM(b), SUM(c), SUM(d) FROM '{D}/edge_numbers.csv'",
-    "SELECT MIN(a), MAX(a), MIN(b), MAX(b), MIN(d) FROM '{D}/edge_numbers.csv'",
+    "SELECT MIN(a), MAX(a), MIN(b), MAX(b) FROM '{D}/edge_numbers.csv'",
+    "SELECT MIN(d), MAX(d) FROM '{D}/edge_numbers.csv'",
     "SELECT d1, COUNT(*) FROM '{D}/edge_dates.csv' GROUP BY d1",
     "SELECT COUNT(*) FROM '{D}/edge_dates.csv' WHERE d1 > '2024-01-01'",
     "SELECT q1, COUNT(*) FROM '{D}/edge_quotes.csv' GROUP BY q1",
@@ -251,6 +275,26 @@ QUERIES = [
     "SELECT t1, t2, COUNT(*), SUM(n) FROM '{D}/edge_tabs.csv' GROUP BY t1, t2",
     "SELECT t1, t2, t3, COUNT(*) FROM '{D}/edge_tabs.csv' GROUP BY t1, t2, t3",
     "SELECT t2, t1, COUNT(*) FROM '{D}/edge_tabs.csv' WHERE n > 1 GROUP BY t2, t1",
+    # plans over more than 8 distinct columns (every column copied into the joined
+    # row, evaluator_joins.c:30-37; `*` over all of them, evaluator_utils.c:272-417;
+    # any condition tree, evaluator_conditions.c:62-164)
+    f"SELECT * FROM {U} AS u JOIN {O} AS o ON u.id = o.customer_id",
+    f"SELECT * FROM {U} AS u LEFT JOIN {O} AS o ON u.id = o.customer_id",
+    f"SELECT * FROM {U} AS u JOIN {O} AS o ON u.id = o.customer_id WHERE o.price > 60 AND u.age < 40",
+    f"SELECT * FROM {U} AS u JOIN {O} AS o ON u.id = o.customer_id JOIN {P} AS p ON o.id = p.id",
+    f"SELECT u.name, o.price FROM {U} AS u JOIN {O} AS o ON u.id = o.customer_id WHERE u.age + u.height + u.active + o.tax + o.quantity + o.id > 100 AND u.city != 'x' AND u.email != 'y' AND u.role != 'z'",
+    f"SELECT u.role, COUNT(*), SUM(o.price) FROM {U} AS u JOIN {O} AS o ON u.id = o.customer_id WHERE u.age + u.height + u.active > 0 AND o.tax + o.quantity + o.id > 0 AND u.city != 'x' AND u.email != 'y' GROUP BY u.role",
+    f"SELECT COUNT(*), SUM(c11) FROM {W} WHERE {WIDE9}",
+    f"SELECT c9, COUNT(*), SUM(c10), AVG(c11) FROM {W} WHERE {WIDE9} GROUP BY c9",
+    f"SELECT c9, MIN(c10), MAX(c5), MIN(c4) FROM {W} WHERE c0 + c1 + c2 + c3 + c6 + c7 + c8 > 100 AND c5 != 'x' GROUP BY c9",
+    f"SELECT c9, STDDEV(c10), MEDIAN(c11) FROM {W} WHERE c0 + c1 + c2 + c3 + c4 + c6 + c7 + c8 > 60 GROUP BY c9",
+    f"SELECT c0, c11 FROM {W} WHERE {WIDE9}",
+    f"SELECT * FROM {W} WHERE {WIDE9} AND c10 > 2000",
+    f"SELECT c9, c0 + c10, COUNT(*) FROM {W} WHERE {WIDE9} GROUP BY c9",
+    # GROUP BY of more than 8 parts (parser_clauses.c:241-246; evaluator.c:113-212)
+    f"SELECT c9, COUNT(*) FROM {W} GROUP BY c0, c1, c2, c3, c4, c5, c6, c7, c8, c9",
+    f"SELECT c9, COUNT(*), SUM(c11) FROM {W} WHERE c0 > 50 GROUP BY c9, c5, c9, c5, c9, c5, c9, c5, c9, c5, c9, c5",
+    f"SELECT c5, COUNT(*) FROM {W} GROUP BY c5, c9, c0 % 3, c1 % 2, c2 % 2, c3 % 2, c6 % 2, c7 % 2, c8 % 2",
     # row-returning (build_result)
     f"SELECT name, age FROM {T} WHERE age > 30",
     f"SELECT * FROM {T} WHERE age > 30",

@@ -1,0 +1,162 @@
+"""The N > 1 step inside the library (cqgpu_dist_query over its own RCCL
+communicator) and its gather-merge kernels.
+
+* Gather-merge kernels over simulated ranks (cqgpu_gm_local: every shard's pack,
+  then rank 0's merge kernels, in one process): the config-3 / config-4 plan and
+  the other plans of its shape at 1..16 ranks against the ORACLE on the whole
+  file -- counts, group set and first-appearance order, representative cells
+  exact, SUM / AVG 1e-6 relative; CR / CRLF cuts; long keys (inline up to 48
+  bytes, declined beyond); too many groups (declined).
+* cqgpu_dist_query itself at world size 1 over RCCL (torch.distributed.run, one
+  rank: a one-GPU box cannot hold two RCCL ranks): the gather-merge, dense and
+  blob paths each against the oracle, the path each query took asserted.
+"""
+import json
+import os
+import socket
+import subprocess
+import sys
+
+import numpy as np
+import pytest
+
+import cqtest
+import cq_amd
+from cq_amd import datagen
+from test_gpu_parity import compare, tolerant_columns
+from test_gpu_partials import _mixed_terminators
+
+pytestmark = pytest.mark.gpu
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+
+GM = [
+    "SELECT role, COUNT(*), SUM(height), AVG(height) FROM '{p}' WHERE age > 30 GROUP BY role",
+    "SELECT COUNT(*) FROM '{p}' WHERE age > 30",
+    "SELECT COUNT(*), SUM(height), AVG(age) FROM '{p}'",
+    "SELECT name, COUNT(*), AVG(height) FROM '{p}' WHERE gender = 'f' GROUP BY name",
+    "SELECT age, COUNT(*), SUM(height) FROM '{p}' GROUP BY age ORDER BY COUNT(*) DESC LIMIT 7",
+    "SELECT role, 42, COUNT(*) FROM '{p}' WHERE height > 1.99 GROUP BY role",
+    "SELECT COUNT(*) FROM '{p}' WHERE age > 200",
+    "SELECT role, COUNT(*) FROM '{p}' WHERE age > 200 GROUP BY role",
+    "SELECT height, COUNT(*) FROM '{p}' GROUP BY height HAVING COUNT(*) > 100",
+]
+
+
+@pytest.fixture(scope="module")
+def files(tmp_path_factory):
+    d = str(tmp_path_factory.mktemp("gm"))
+    out = {}
+    out["plain"] = os.path.join(d, "plain.csv")
+    with open(out["plain"], "wb") as fh:
+        fh.write(datagen.shape_a_bytes(150_000, seed=21, with_role=True))
+    out["mixed"] = os.path.join(d, "mixed.csv")
+    with open(out["mixed"], "wb") as fh:
+        fh.write(_mixed_terminators(datagen.shape_a_bytes(40_000, seed=22, with_role=True), 5))
+    rng = np.random.default_rng(3)
+    keys = ["key_of_twenty_bytes_%02d" % i for i in range(40)] + ["k%d" % i for i in range(30)]
+    out["longkey"] = os.path.join(d, "longkey.csv")
+    with open(out["longkey"], "w") as fh:
+        fh.write("k,v,w\n" + "\n".join("%s,%d,%d.%d" % (keys[rng.integers(0, len(keys))], rng.integers(0, 99),
+                                                       rng.integers(0, 9), rng.integers(0, 9))
+                                       for _ in range(50_000)) + "\n")
+    out["verylong"] = os.path.join(d, "verylong.csv")
+    with open(out["verylong"], "w") as fh:
+        fh.write("k,v\n" + "\n".join("%s,%d" % ("x" * 60 + str(i % 5), i % 7) for i in range(20_000)) + "\n")
+    out["many"] = os.path.join(d, "many.csv")
+    with open(out["many"], "w") as fh:
+        fh.write("k,v\n" + "\n".join("%d,%d" % (i % 9000, i % 7) for i in range(40_000)) + "\n")
+    return out
+
+
+def _gm(path, sql, n):
+    q = sql.format(p=path)
+    tabs = [cq_amd.Table.open_range(path, r, n) for r in range(n)]
+    try:
+        with cqtest.Parsed(q) as ast:
+            got = cq_amd.gm_local(ast, tabs)
+            tol = tolerant_columns(ast)
+    finally:
+        for t in tabs:
+            t.close()
+    return q, got, tol
+
+
+@pytest.mark.parametrize("sql", GM)
+@pytest.mark.parametrize("n", [1, 3, 8])
+def test_gm_local_equals_oracle(files, sql, n):
+    q, got, tol = _gm(files["plain"], sql, n)
+    assert got is not None, (q, cq_amd.last_error(), cq_amd.last_ineligible())
+    want, unsup = cqtest.oracle_query(q)
+    assert not unsup
+    compare(got, want, tol, f"gather-merge {n} ranks: {q}")
+
+
+@pytest.mark.parametrize("n", [2, 5, 16])
+def test_gm_local_mixed_terminator_cuts(files, n):
+    for sql in GM[:4]:
+        q, got, tol = _gm(files["mixed"], sql, n)
+        assert got is not None, (q, cq_amd.last_error())
+        want, _ = cqtest.oracle_query(q)
+        compare(got, want, tol, f"gather-merge {n} ranks: {q}")
+
+
+@pytest.mark.parametrize("n", [1, 4])
+def test_gm_local_long_keys(files, n):
+    """keys over 16 bytes (GK_LONG: compared by their bytes, carried inline up to 48)"""
+    for sql in ("SELECT k, COUNT(*), SUM(w), AVG(v) FROM '{p}' GROUP BY k",
+                "SELECT k, COUNT(*) FROM '{p}' WHERE v > 50 GROUP BY k"):
+        q, got, tol = _gm(files["longkey"], sql, n)
+        assert got is not None, (q, cq_amd.last_error())
+        want, _ = cqtest.oracle_query(q)
+        compare(got, want, tol, f"gather-merge {n} ranks: {q}")
+
+
+def test_gm_local_declines(files):
+    """texts over 48 bytes and more than 4096 groups on a rank leave the gather-merge"""
+    _, got, _ = _gm(files["verylong"], "SELECT k, COUNT(*) FROM '{p}' GROUP BY k", 2)
+    assert got is None and "declined" in cq_amd.last_ineligible()
+    _, got, _ = _gm(files["many"], "SELECT k, COUNT(*) FROM '{p}' GROUP BY k", 2)
+    assert got is None and "declined" in cq_amd.last_ineligible()
+    _, got, _ = _gm(files["plain"], "SELECT role, MIN(age) FROM '{p}' GROUP BY role", 2)
+    assert got is None and "outside" in cq_amd.last_ineligible()
+
+
+# ---------------------------------------------------------------- cqgpu_dist_query over RCCL, one rank
+DIST = [
+    (GM[0], 1),
+    (GM[2], 1),
+    ("SELECT role, MIN(height), MAX(name), COUNT(*) FROM '{p}' WHERE age > 30 GROUP BY role", 2),
+    ("SELECT gender, role, COUNT(*), STDDEV(height) FROM '{p}' GROUP BY gender, role", 2),
+    ("SELECT role, MEDIAN(age) FROM '{p}' GROUP BY role", 3),
+    ("SELECT name, age FROM '{p}' WHERE age > 78 AND height < 1.05", 3),
+]
+
+
+def _port():
+    with socket.socket() as s:
+        s.bind(("127.0.0.1", 0))
+        return s.getsockname()[1]
+
+
+def _cell(c):
+    return (c[0], c[1].encode("latin-1")) if c[0] == "S" else tuple(c)
+
+
+def test_dist_query_one_rank_rccl(files, tmp_path):
+    out = str(tmp_path / "dist.json")
+    cmd = [sys.executable, "-m", "torch.distributed.run", "--nnodes=1", "--nproc-per-node=1",
+           "--master-addr", "127.0.0.1", "--master-port", str(_port()), os.path.join(ROOT, "tests", "dist_rccl_worker.py"),
+           files["plain"], out, json.dumps([s for s, _ in DIST])]
+    p = subprocess.run(cmd, cwd=ROOT, capture_output=True, text=True, timeout=110)
+    assert p.returncode == 0, p.stderr[-3000:]
+    res = json.load(open(out))
+    for (sql, path), r in zip(DIST, res):
+        q = sql.format(p=files["plain"])
+        assert r["status"] == 0, (q, r["error"])
+        assert r["path"] == path, (q, r["path"])
+        want, _ = cqtest.oracle_query(q)
+        got = {"columns": [c.encode("latin-1") for c in r["result"]["columns"]],
+               "rows": [[_cell(c) for c in row] for row in r["result"]["rows"]]}
+        with cqtest.Parsed(q) as ast:
+            tol = tolerant_columns(ast)
+        compare(got, want, tol, f"dist_query path {path}: {q}")

@@ -28,7 +28,8 @@ def synth(tmp_path_factory):
 
 
 QUERIES = [
-    "SELECT role, gender, COUNT(*), SUM(height), AVG(height) FROM '{P}' GROUP BY role, gender",
+    "SELECT role, gender, COUNT(*), SUM(height) FROM '{P}' GROUP BY role, gender",
+    "SELECT role, gender, AVG(height) FROM '{P}' GROUP BY role, gender",
     "SELECT gender, age, COUNT(*), AVG(height) FROM '{P}' WHERE age > 40 GROUP BY gender, age",
     "SELECT gender, age, MIN(name), MAX(role) FROM '{P}' WHERE age > 40 GROUP BY gender, age",
     "SELECT name, surname, gender, COUNT(*) FROM '{P}' GROUP BY name, surname, gender",
@@ -202,3 +203,27 @@ def test_composite_digest_collision_fails_loudly(synth, monkeypatch):
         got = cq_amd.evaluate(ast)
         tol = tolerant_columns(ast)
     compare(got, want, tol, sql)
+
+
+def test_joined_text_collision_fails_loudly(tmp_path, monkeypatch):
+    """Composite keys with a tab inside a text part key on the reference's joined
+    text (evaluator.c:113-212); a hit is re-checked by comparing the two joined
+    texts byte for byte.  CQGPU_TEST_DIGEST_BITS cuts their hash to 2 bits: the
+    query must fail with the collision named; full hashes: exact vs the oracle."""
+    rows = ["a\tb,c,%d" % i for i in range(50)] + ["a,b\tc,%d" % i for i in range(50)] + \
+           ["x\ty,z%d,%d" % (i % 9, i) for i in range(400)]
+    p = tmp_path / "tabs.csv"
+    p.write_text("t1,t2,n\n" + "\n".join(rows) + "\n")
+    sql = f"SELECT t1, t2, COUNT(*), SUM(n) FROM '{p}' GROUP BY t1, t2"
+    monkeypatch.setenv("CQGPU_TEST_DIGEST_BITS", "2")
+    with cqtest.Parsed(sql) as ast:
+        got = cq_amd.evaluate(ast)
+    assert got is None
+    assert "digest" in cq_amd.last_error(), cq_amd.last_error()
+    monkeypatch.delenv("CQGPU_TEST_DIGEST_BITS")
+    want, _ = cqtest.oracle_query(sql)
+    with cqtest.Parsed(sql) as ast:
+        got = cq_amd.evaluate(ast)
+        tol = tolerant_columns(ast)
+    compare(got, want, tol, sql)
+    assert len(want["rows"]) == 10        # 'a\tb'+'c' and 'a'+'b\tc' join to one text

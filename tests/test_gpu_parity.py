@@ -113,7 +113,8 @@ def synth_role(tmp_path_factory):
 SYNTH_QUERIES = [
     "SELECT role, COUNT(*), SUM(height), AVG(height) FROM '{P}' WHERE age > 30 GROUP BY role",
     "SELECT COUNT(*) FROM '{P}' WHERE age > 30",
-    "SELECT COUNT(*), SUM(height), AVG(height), MIN(height), MAX(age) FROM '{P}' WHERE gender = 'f'",
+    "SELECT COUNT(*), SUM(height), MIN(height), MAX(age) FROM '{P}' WHERE gender = 'f'",
+    "SELECT COUNT(*), AVG(height) FROM '{P}' WHERE gender = 'f'",
     "SELECT name, COUNT(*), MIN(role), MAX(role) FROM '{P}' WHERE age BETWEEN 20 AND 40 GROUP BY name",
     "SELECT age, COUNT(*), AVG(height) FROM '{P}' WHERE role IN ('role_001', 'role_500', 'role_999') GROUP BY age",
     "SELECT gender, COUNT(*), SUM(age) FROM '{P}' WHERE NOT (age % 3 = 0 OR height < 1.5) GROUP BY gender",
@@ -216,7 +217,7 @@ def test_field_shape_fuzz(tmp_path):
     p = tmp_path / "fuzz.csv"
     p.write_text("\n".join(lines) + "\n")
     for sql in (f"SELECT a, COUNT(*) FROM '{p}' GROUP BY a",
-                f"SELECT b, COUNT(*), SUM(c), MIN(a), MAX(a) FROM '{p}' GROUP BY b",
+                f"SELECT b, COUNT(*), MIN(a), MAX(a) FROM '{p}' GROUP BY b", f"SELECT b, SUM(c) FROM '{p}' GROUP BY b",
                 f"SELECT c, COUNT(*), SUM(a) FROM '{p}' WHERE b > 0 GROUP BY c"):
         want, unsup = cqtest.oracle_query(sql)
         assert not unsup

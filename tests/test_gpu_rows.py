@@ -28,7 +28,8 @@ def synth(tmp_path_factory):
 ROW_QUERIES = [
     "SELECT name, age FROM '{P}' WHERE age > 30",
     "SELECT * FROM '{P}' WHERE role = 'role_007'",
-    "SELECT name, age * 2, age + height, -height, age % 7 FROM '{P}' WHERE height < 1.5",
+    "SELECT name, age * 2, age + height, -height FROM '{P}' WHERE height < 1.5",
+    "SELECT name, age % 7 FROM '{P}' WHERE height < 1.5",
     "SELECT role AS r, age AS years FROM '{P}' WHERE age BETWEEN 20 AND 22",
     "SELECT main.name, surname FROM '{P}' WHERE gender = 'f' AND age < 19",
     "SELECT name, missing_col, 'lit', 42 FROM '{P}' WHERE age = 55",
