@@ -263,7 +263,8 @@ def main():
         else:
             # the whole step inside the library over its RCCL communicator: config 4's
             # plan takes the gather-merge (one grouped send/recv to rank 0, device merge)
-            tp, merge_path[0] = scan_partitioned_rccl(ast, table)
+            tp, path = scan_partitioned_rccl(ast, table)
+            merge_path[0] = path + " inside libcqgpu over RCCL"
         st = cq_amd.stats()                   # the merge runs no scan: still this rank's partial
         kernel_used[0] = st.get("scan_kernel", 0)
         last_stats[0] = st
@@ -381,8 +382,8 @@ def main():
                 "rows_per_gpu": hi - lo,
                 "bytes_per_gpu": nbytes,
                 "groups": 1000 if role else 1,
-                "parallelism": (f"dp{world} (rows [r*T/N, (r+1)*T/N) per rank; merge inside libcqgpu over "
-                                "RCCL: " + str(merge_path[0]) + ")" if dist is not None else "dp1"),
+                "parallelism": (f"dp{world} (rows [r*T/N, (r+1)*T/N) per rank; merge: " + str(merge_path[0]) +
+                                ")" if dist is not None else "dp1"),
             },
             "verified": ok,
             "verified_against": exp_src,
