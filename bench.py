@@ -533,8 +533,10 @@ def config5_leg(args, cq_amd, L):
             "users": n, "orders": n, "bytes": nb,
             "value": 2 * n / step_s, "unit": "rows/s (users + orders rows)", "ms_per_step": step_s * 1e3,
             "kernel_ms": kms,
-            "kernel": "cq::fast::jx_extract_kernel x 4, jx_build_direct_kernel, jx_probe_kernel (+ raw_merge)"
-                      if st.get("scan_kernel") == 3 else "general join pipeline",
+            "kernel": {4: "cq::fast::jx_extract_kernel<STAR> build + probe, jx_star_first_kernel, jx_star_flush_kernel "
+                          "(+ raw_merge)",
+                       3: "cq::fast::jx_extract_kernel x 4, jx_build_direct_kernel, jx_probe_kernel (+ raw_merge)"}
+                      .get(st.get("scan_kernel"), "general join pipeline"),
             "roofline": {"bound": "hbm", "achieved": nb / step_s / 1e9, "peak": HBM_PEAK_GBS, "unit": "GB/s",
                          "frac": nb / step_s / 1e9 / HBM_PEAK_GBS, "traffic": None,
                          "algorithmic_bytes": "both CSV files read once (SURVEY.md 8d; one rank: no repartition)"},

@@ -38,6 +38,14 @@ def lib():
     if _lib is None:
         if not os.path.exists(LIB_PATH):
             raise RuntimeError(f"cq_amd native library missing: {LIB_PATH} (run __graft_entry__.build())")
+        # One HIP runtime per process: the torch wheel ships its own libamdhip64 /
+        # libhsa-runtime64 / librccl.  Loaded first, they also serve libcqgpu's
+        # dependencies (same sonames); loaded after libcqgpu pulled in /opt/rocm's,
+        # both runtimes live in the process and their teardown frees twice at exit.
+        try:
+            import torch  # noqa: F401
+        except ImportError:
+            pass
         L = C.CDLL(LIB_PATH, mode=C.RTLD_GLOBAL)
         TP = C.POINTER(abi.Table)
         L.evaluate_query.restype = TP
@@ -72,6 +80,8 @@ def lib():
                                        C.POINTER(C.c_uint64), C.POINTER(C.c_uint64)]
         L.cqgpu_route_fill.restype = C.c_int
         L.cqgpu_route_fill.argtypes = [C.c_void_p, C.c_uint64, C.c_void_p, C.c_void_p]
+        L.cqgpu_table_set_record_total.restype = C.c_int
+        L.cqgpu_table_set_record_total.argtypes = [C.c_void_p, C.c_uint64]
         L.cqgpu_table_from_routed.restype = C.c_void_p
         L.cqgpu_table_from_routed.argtypes = [C.c_void_p, C.c_size_t, C.c_void_p, C.c_size_t, abi.CsvConfig,
                                               C.c_char_p, C.c_size_t]
@@ -234,6 +244,12 @@ def table_from_routed(dev_bytes_ptr: int, nbytes: int, dev_gids_ptr: int, nrec: 
     """A join side rebuilt from received records (device memory) and their global ids."""
     return Table(lib().cqgpu_table_from_routed(dev_bytes_ptr, nbytes, dev_gids_ptr, nrec,
                                                cfg or abi.csv_config(), header, len(header)))
+
+
+def table_set_record_total(table: "Table", total: int) -> None:
+    """The whole input's record count for a routed table (cqgpu_table_set_record_total)."""
+    if lib().cqgpu_table_set_record_total(table.handle, total) != 0:
+        raise RuntimeError(last_error() or "cqgpu_table_set_record_total failed")
 
 
 def merge_partials(ast, blobs):

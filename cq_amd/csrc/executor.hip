@@ -17,6 +17,7 @@
 #include <cstring>
 #include <string>
 #include <map>
+#include <functional>
 #include <set>
 #include <memory>
 #include <thread>
@@ -40,6 +41,7 @@ using namespace cq;
 extern "C" {
 uint32_t cq_lean_pick_ws(const uint8_t* data, uint64_t n);
 uint64_t cq_lean_long_cols(const uint8_t* data, uint64_t n, uint32_t delim);
+uint64_t cq_cols_longer_than(const uint8_t* data, uint64_t n, uint32_t delim, uint32_t limit);
 uint32_t cq_scan_cand_stride(const ScanPlan* P, int grouped);
 size_t cq_scan_lds_bytes(const ScanPlan* P, int grouped);
 int cq_scan_occupancy(const ScanPlan* P, int grouped);
@@ -167,6 +169,17 @@ hipError_t cq_jx_build_direct(const unsigned long long* key, const unsigned long
                               uint32_t n, unsigned long long kmin, unsigned long long range, void* D,
                               unsigned int* flag, int grid, hipStream_t s);
 size_t cq_jx_direct_bytes();
+hipError_t cq_jx_star_extract(const uint8_t* g, uint64_t lo, uint64_t hi, uint32_t ws, uint32_t delim, uint32_t quote,
+                              int kcol, int pcol, int build, unsigned long long kmin, unsigned long long range,
+                              uint16_t* d16, uint32_t* l32, uint8_t* m8, unsigned long long* ttab,
+                              unsigned long long* gsum, unsigned long long* counter, unsigned int* flag,
+                              unsigned long long* krange, int grid, hipStream_t s);
+hipError_t cq_jx_star_first(const uint16_t* d16, const uint32_t* l32, const uint8_t* m8, unsigned long long range,
+                            uint32_t* gfirst, unsigned long long* nocc, int grid, hipStream_t s);
+hipError_t cq_jx_star_flush(int grouped, int value, const unsigned long long* ttab, const unsigned long long* gsum,
+                            const uint32_t* gfirst, const unsigned long long* cnts, const cq::GroupTable* rt, int nacc,
+                            cq::ScanStats* stats, unsigned int* flag, hipStream_t s);
+uint32_t cq_jx_star_groups();
 hipError_t cq_jx_probe(int grouped, int value, int direct, const unsigned long long* pkey,
                        const unsigned long long* ppay, const uint32_t* poff, uint32_t n, unsigned long long kmin,
                        const void* table, uint64_t tcap, const unsigned long long* bpay, const uint32_t* boff,
@@ -213,6 +226,13 @@ hipError_t cq_launch_gather_len(const uint32_t* len, const uint32_t* order, uint
 hipError_t cq_launch_route_copy(const uint8_t* g, const unsigned long long* recs, const uint32_t* order,
                                 const uint32_t* len, const unsigned long long* off, uint32_t n, uint64_t gid_base,
                                 uint8_t* out, unsigned long long* gids, hipStream_t s);
+hipError_t cq_launch_chain_key(const uint2* pairs, unsigned long long np, const unsigned long long* prev,
+                               unsigned long long prev_none, unsigned long long radix, const unsigned long long* rg,
+                               unsigned long long r_none, unsigned long long* out, hipStream_t s);
+hipError_t cq_launch_key_pick(const unsigned long long* key, const unsigned long long* pidx, uint32_t n,
+                              unsigned long long* out, hipStream_t s);
+hipError_t cq_launch_key_flagged(const unsigned long long* key, unsigned long long np, const unsigned int* flags,
+                                 const unsigned int* pos, unsigned long long* out, hipStream_t s);
 hipError_t cq_launch_pair_gid(const uint2* pairs, const unsigned long long* pidx, uint32_t n,
                               const unsigned long long* lg, const unsigned long long* rg, unsigned long long* out,
                               hipStream_t s);
@@ -493,10 +513,15 @@ struct cqgpu_table {
     int device = 0;
     uint32_t lean_ws = 0;            // lean_kernel window stride for this file's record lengths
     uint64_t long_cols = ~0ull;      // columns with sampled fields over 8 bytes (cq_lean_long_cols)
+    uint64_t wide4_cols = ~0ull;     // columns with sampled fields over 4 bytes (fast_kernel's numerals)
     std::string sample;              // the first data bytes (plan-time sampling: fast_kernel's key seed)
     std::map<int, std::unique_ptr<DevBuf>> fast_seed;   // per GROUP BY column: seeded LDS tags (device)
+    // per join-key column: its canonical INTEGER keys' [min, max], learned by a STAR
+    // join's build pass (the table is immutable) -- the next build sizes its arrays by it
+    std::map<int, std::pair<uint64_t, uint64_t>> key_range;
     unsigned long long* gids = nullptr;   // routed tables: global record id of each record (device)
     uint64_t ngids = 0;
+    uint64_t gid_total = 0;               // routed tables: records of the whole input (every rank's share)
     std::unique_ptr<RouteState> route;    // pending repartition (cqgpu_route_plan)
 };
 
@@ -577,6 +602,8 @@ cqgpu_table* upload(const uint8_t* host, size_t n, cq_csv_config cfg, uint64_t b
     t->lean_ws = cq_lean_pick_ws(host + t->data_begin, n - std::min<uint64_t>(n, t->data_begin));
     t->long_cols = cq_lean_long_cols(host + t->data_begin, n - std::min<uint64_t>(n, t->data_begin),
                                      (uint8_t)cfg.delimiter);
+    t->wide4_cols = cq_cols_longer_than(host + t->data_begin, n - std::min<uint64_t>(n, t->data_begin),
+                                        (uint8_t)cfg.delimiter, 4);
     {
         const uint64_t db = std::min<uint64_t>(n, t->data_begin);
         t->sample.assign((const char*)host + db, (size_t)std::min<uint64_t>(n - db, SAMPLE_BYTES));
@@ -1041,6 +1068,7 @@ void finish_plan(const cqgpu_table* t, Compiled& C, Compiler& cc) {
     C.P.range_begin = 0;
     C.P.range_end = t->n;
     C.P.lean_ws = t->lean_ws;
+    C.P.fast_wide_cols = t->wide4_cols;
     C.P.fast_seed = 0;
     if (C.P.group_slot >= 0 && !C.wide) {
         const int gc = C.P.need_col[C.P.group_slot];
@@ -1610,6 +1638,54 @@ std::vector<HGroup> make_groups(DevCtx& c, const Compiled& C, uint64_t limit, ui
     return groups;
 }
 
+// Result-table blocks allocated while the device works: the host waits ~1 ms in the
+// stream synchronisation of every scan, and the result rows csv_free releases
+// (reference csv_reader.c:467-490: every row's values array and every string is its
+// own malloc block) cost ~50 us of calloc / malloc per 1,000 groups after it.  The
+// pool keeps calloc'd value arrays and malloc'd string blocks of POOL_STR bytes,
+// refilled during the wait to the previous result's size; build_direct takes from
+// it (any malloc block of the needed size is what csv_free expects).
+struct RowPool {
+    int ncols = -1;
+    std::vector<cq_value*> vals;
+    std::vector<char*> strs;
+    uint32_t hint = 0;                 // rows of the last direct result
+};
+constexpr size_t POOL_STR = 32;
+thread_local RowPool g_rowpool;
+const bool g_rowpool_off = getenv("CQGPU_NO_ROWPOOL") != nullptr;   // A/B knob
+void rowpool_fill(int ncols, uint32_t nstr_per_row) {
+    if (g_rowpool_off) return;
+    RowPool& P = g_rowpool;
+    if (P.ncols != ncols) {
+        for (cq_value* v : P.vals) free(v);
+        P.vals.clear();
+        P.ncols = ncols;
+    }
+    const size_t want = std::min<size_t>(P.hint, 1u << 16);
+    while (P.vals.size() < want) P.vals.push_back((cq_value*)calloc(std::max(ncols, 1), sizeof(cq_value)));
+    const size_t ws = std::min<size_t>(want * nstr_per_row, 1u << 17);
+    while (P.strs.size() < ws) P.strs.push_back((char*)malloc(POOL_STR));
+}
+cq_value* rowpool_vals(int ncols) {
+    RowPool& P = g_rowpool;
+    if (P.ncols == ncols && !P.vals.empty()) {
+        cq_value* v = P.vals.back();
+        P.vals.pop_back();
+        return v;
+    }
+    return (cq_value*)calloc(std::max(ncols, 1), sizeof(cq_value));
+}
+char* rowpool_str(size_t bytes) {
+    RowPool& P = g_rowpool;
+    if (bytes <= POOL_STR && !P.strs.empty()) {
+        char* s = P.strs.back();
+        P.strs.pop_back();
+        return s;
+    }
+    return (char*)malloc(bytes);
+}
+
 // run the fused scan (with regrowth on overflow) and return the groups
 // row_out (optional): offsets of the records passing WHERE, unordered; entries
 // past row_cap are counted in ScanStats.rows_emitted but not written
@@ -1723,6 +1799,12 @@ std::vector<HGroup> run_aggregate(DevCtx& c, const cqgpu_table* t, Compiled& C, 
             uint8_t* hs = finished ? mail : (uint8_t*)pinned(c, sizeof(ScanStats) + 16);
             if (!finished) HIPCHECK(hipMemcpyAsync(hs, A.stats, sizeof(ScanStats), hipMemcpyDeviceToHost, c.stream));
             PHASE("launch");
+            if (direct && finished && C.grouped) {      // the result's blocks, while the device works
+                uint32_t nstr = 0;
+                for (const OutCol& o : C.outs) nstr += o.kind == OUT_REP || o.kind == OUT_CONST;
+                rowpool_fill((int)C.outs.size(), nstr);
+                PHASE("pool");
+            }
             HIPCHECK(hipStreamSynchronize(c.stream));
             PHASE("scan+finish");
             ScanStats s1;
@@ -1978,13 +2060,14 @@ cq_table* build_direct(const Compiled& C, const uint8_t* hp, uint32_t ng, uint32
     cq_table* r = new_result(C.names);
     r->nrows = r->row_capacity = (int)ng;
     r->rows = (cq_row*)malloc(sizeof(cq_row) * std::max<size_t>(ng, 1));
+    g_rowpool.hint = ng;
     for (uint32_t g = 0; g < ng; g++) {
         const uint8_t* rp = hp + g * rec;
         const unsigned long long cnt = ((const unsigned long long*)rp)[3];
         const uint64_t* q = (const uint64_t*)(rp + 40);
         cq_row& row = r->rows[g];
         row.ncols = r->ncols;
-        row.values = (cq_value*)calloc(std::max(r->ncols, 1), sizeof(cq_value));
+        row.values = rowpool_vals(r->ncols);
         for (int i = 0; i < r->ncols; i++) {
             const OutCol& o = C.outs[i];
             cq_value& v = row.values[i];
@@ -2010,7 +2093,7 @@ cq_table* build_direct(const Compiled& C, const uint8_t* hp, uint32_t ng, uint32
                         if (x.kind == K_STR) {             // to_value's strdup: up to the first NUL
                             const char* src = (const char*)bytes + k * SB;
                             const size_t n = strnlen(src, x.len);
-                            char* d = (char*)malloc(n + 1);
+                            char* d = rowpool_str(n + 1);
                             memcpy(d, src, n);
                             d[n] = 0;
                             v.kind = K_STR;
@@ -3038,6 +3121,51 @@ unsigned long long build_pairs(DevCtx& c, JoinSide& A, JoinSide& B, int kl, int 
     return np;
 }
 
+// The canonical INTEGER keys (jx_key's shape) of column `col` in the table's sampled
+// bytes: their [min, max] widened to cover the records the whole table is estimated to
+// hold (a guess: a key outside it only costs the STAR join a second round)
+bool sample_key_range(const cqgpu_table* t, int col, uint64_t* kmin, uint64_t* kmax, uint64_t* est) {
+    const std::string& s = t->sample;
+    const char delim = (char)t->cfg.delimiter;
+    uint64_t lo = ~0ull, hi = 0, nrec = 0, used = 0;
+    size_t i = 0;
+    while (i < s.size()) {
+        while (i < s.size() && (s[i] == '\n' || s[i] == '\r')) i++;
+        const size_t rs = i;
+        while (i < s.size() && s[i] != '\n' && s[i] != '\r') i++;
+        if (i >= s.size()) break;                    // a record cut by the sample's end
+        nrec++;
+        used = i;
+        size_t f = rs;
+        for (int k = 0; k < col && f < i; k++) {
+            while (f < i && s[f] != delim) f++;
+            if (f < i) f++;
+        }
+        size_t e = f;
+        while (e < i && s[e] != delim) e++;
+        const size_t len = e - f;
+        if (len == 0 || len > 15 || (len >= 8 && len <= 10) || (s[f] == '0' && len > 1)) continue;
+        uint64_t v = 0;
+        bool ok = true;
+        for (size_t k = f; k < e; k++) {
+            const unsigned dg = (unsigned)(unsigned char)s[k] - '0';
+            ok = ok && dg < 10;
+            v = v * 10 + dg;
+        }
+        if (!ok) continue;
+        lo = std::min(lo, v);
+        hi = std::max(hi, v);
+    }
+    if (!nrec || lo > hi || !used) return false;
+    const uint64_t n = t->n > t->data_begin ? t->n - t->data_begin : 0;
+    *est = (uint64_t)((double)n * (double)nrec / (double)used) + 1;
+    const uint64_t span = std::max<uint64_t>(hi - lo, *est);
+    const uint64_t pad = span / 8 + 16;
+    *kmin = lo > pad ? lo - pad : 0;
+    *kmax = std::max(hi, *kmin + span + span / 4 + 1024);
+    return true;
+}
+
 // The fused aggregate join: one INNER JOIN on `ident = ident`
 // without WHERE, COUNT / SUM / AVG of one probe-side (right) column, GROUP BY one
 // build-side (left) column or none, every other item a left column.  No record-start
@@ -3050,6 +3178,8 @@ unsigned long long build_pairs(DevCtx& c, JoinSide& A, JoinSide& B, int kl, int 
 // (l, r) order.  nullptr: outside this shape, or the data (a quote, a short row, a key
 // that is not a canonical INTEGER below 10^15 or NULL, a wider numeral) needs the
 // general pipeline.
+// test knob CQ_AMD_JX_DEBUG: why a fused join handed a query on (stderr)
+#define JXDBG(...) do { if (getenv("CQ_AMD_JX_DEBUG")) fprintf(stderr, "cq_amd jx: " __VA_ARGS__); } while (0)
 cq_table* run_fast_join(DevCtx& c, cq_node* q, Compiled& C, const cqgpu_table* L, const cqgpu_table* R, int kl,
                         int kr, int nl) {
     if (getenv("CQ_AMD_NO_FAST_JOIN")) return nullptr;
@@ -3082,6 +3212,181 @@ cq_table* run_fast_join(DevCtx& c, cq_node* q, Compiled& C, const cqgpu_table* L
             return nullptr;
     if (C.wide || C.rep_cols.size() > (size_t)MAX_WIDE) return nullptr;
     const uint32_t ws = L->lean_ws ? L->lean_ws : 3968u, wsr = R->lean_ws ? R->lean_ws : 3968u;
+    const int xgrid = c.ncu;
+    const uint8_t dq = (uint8_t)L->cfg.quote;
+    Literals Lit;
+    parse_literals(c, C.lits, Lit);
+    // finish: the representative (left) columns of each group's first pair's left record
+    constexpr uint32_t SB = 48;
+    FinishDesc FD;
+    memset(&FD, 0, sizeof FD);
+    std::vector<int> rep_ord(C.rep_cols.size());
+    for (size_t i = 0; i < rep_ord.size(); i++) rep_ord[i] = (int)i;
+    std::sort(rep_ord.begin(), rep_ord.end(), [&](int a, int b) { return C.rep_cols[a] < C.rep_cols[b]; });
+    FD.ncols = (int32_t)rep_ord.size();
+    for (size_t i = 0; i < rep_ord.size(); i++) FD.cols[i] = (int16_t)C.rep_cols[rep_ord[i]];
+    FD.delim = d;
+    FD.quote = (uint8_t)L->cfg.quote;
+    FD.nacc = C.P.nacc;
+    FD.sb = SB;
+    FD.first_shift = 32;
+    const uint32_t ncell = (uint32_t)FD.ncols + (uint32_t)FD.nacc + 1;
+    // the groups `fill` puts into an arena's table (raw tags when grouped) -> the result:
+    // raw_merge / compact / finish / pack, one synchronisation; *fallback when the
+    // flags at dflag ask for another path (nothing returned then)
+    auto results = [&](const std::function<void(TableArena&)>& fill, const unsigned int* dflag, uint64_t records,
+                       int kind, bool* fallback) -> cq_table* {
+        *fallback = false;
+        uint32_t cap = grouped ? 8192 : 64;
+        for (int attempt = 0; attempt < 4; attempt++, cap *= 8) {
+            TableArena A = make_arena(c, C.P, cap, cap / 2 + 1, 1, 16);
+            const unsigned int cap_out = cap / 2 + 1;
+            Scratch fin(c, (size_t)cap_out * ncell * (sizeof(Cell) + SB) + 64);
+            Cell* dcells = (Cell*)fin.p;
+            uint8_t* dbytes = fin.p + (size_t)cap_out * ncell * sizeof(Cell);
+            fill(A);
+            if (grouped) HIPCHECK(cq_launch_raw_merge(&A.gt, &A.rt, C.P.nacc, A.stats, c.stream));
+            HIPCHECK(hipEventRecord(c.ev1, c.stream));
+            HIPCHECK(cq_launch_compact(&A.gt, &C.P, A.out, A.out_count, cap_out, c.stream));
+            HIPCHECK(cq_launch_finish(L->g, L->n, A.out, A.out_count, cap_out, &FD, dcells, dbytes, c.stream));
+            constexpr size_t MAIL_HDR = 1024;
+            uint8_t* mail = mailbox(c, MAIL_HDR + cq_pack_result_bytes(cap_out, C.P.nacc, ncell, SB) + 64);
+            HIPCHECK(cq_launch_pack_result(A.out, A.out_count, cap_out, C.P.nacc, dcells, dbytes, ncell, SB,
+                                           mail + MAIL_HDR, A.stats, mail, 1, c.stream));
+            unsigned int fl = 0;
+            HIPCHECK(hipMemcpyAsync(&fl, dflag, 4, hipMemcpyDeviceToHost, c.stream));
+            HIPCHECK(hipStreamSynchronize(c.stream));
+            if (fl) { JXDBG("flags %#x\n", fl); *fallback = true; return nullptr; }
+            ScanStats st;
+            memcpy(&st, mail, sizeof st);
+            unsigned int ng = 0;
+            memcpy(&ng, mail + sizeof(ScanStats), 4);
+            if (st.overflow >= 2) throw HipError{"fused join: group insert timeout"};
+            if (st.overflow) continue;
+            float ms = 0;
+            HIPCHECK(hipEventElapsedTime(&ms, c.ev0, c.ev1));
+            g_stats.scan_ms = ms;
+            g_stats.records = records;
+            g_stats.passed = st.passed;
+            g_stats.scan_kernel = kind;
+            ng = std::min(ng, cap_out);
+            const bool presorted = ng <= cq_pack_order_max();
+            static thread_local std::vector<uint8_t> hbuf;
+            const size_t pb = cq_pack_result_bytes(ng, C.P.nacc, ncell, SB);
+            if (hbuf.size() < pb + 8) hbuf.resize(pb + 8);
+            memcpy(hbuf.data(), mail + MAIL_HDR, pb);
+            cq_table* res = nullptr;
+            if (grouped && presorted && ng) res = build_direct(C, hbuf.data(), ng, ncell, SB, rep_ord, Lit, ~0ull);
+            if (!res) {
+                std::vector<GroupOut> outs(ng);
+                std::vector<Cell> fcells((size_t)ng * ncell);
+                std::vector<uint8_t> fbytes((size_t)ng * ncell * SB);
+                const size_t rec = 40 + 40 * (size_t)C.P.nacc;
+                memset(outs.data(), 0, ng * sizeof(GroupOut));
+                for (unsigned int i = 0; i < ng; i++) {
+                    const uint8_t* r = hbuf.data() + i * rec;
+                    GroupOut& o = outs[i];
+                    o.clslen = ((const uint32_t*)r)[0];
+                    o.w0 = ((const uint64_t*)r)[1];
+                    o.w1 = ((const uint64_t*)r)[2];
+                    o.cnt = ((const unsigned long long*)r)[3];
+                    o.first = ((const unsigned long long*)r)[4];
+                    const uint64_t* qq = (const uint64_t*)(r + 40);
+                    for (int a = 0; a < C.P.nacc; a++) {
+                        o.sum[a] = as_dbl(qq[5 * a]);
+                        o.num[a] = qq[5 * a + 1];
+                        o.extpos[a] = NOPOS;
+                    }
+                }
+                memcpy(fcells.data(), hbuf.data() + ng * rec, fcells.size() * sizeof(Cell));
+                memcpy(fbytes.data(), hbuf.data() + ng * rec + fcells.size() * sizeof(Cell), fbytes.size());
+                std::vector<HGroup> groups = make_groups(c, C, ~0ull, 0, outs, fcells, fbytes, FD.ncols, rep_ord, SB,
+                                                         presorted);
+                g_stats.groups = groups.size();
+                res = build_groups(C, groups, Lit, c);
+            } else {
+                g_stats.groups = ng;
+            }
+            post_ops(c, res, q);
+            return res;
+        }
+        *fallback = true;
+        return nullptr;
+    };
+
+    // ---- STAR: the build side's keys span a dense range (a primary key): both sides
+    // stream once, the build records straight into key-indexed arrays (group id + 1,
+    // byte offset), every probe record looks its key up, marks it and adds its pair
+    // into per-block group sums; no record arrays, no count pass (fast.hip jx_star_*).
+    // The range comes from the table's learned key range, else the sampled bytes; a
+    // key outside it, a NULL or repeated build key, or more than JX_G GROUP BY values
+    // sends the query on to the record-array path below.
+    if (!getenv("CQ_AMD_NO_STAR_JOIN")) {
+        cqgpu_table* Lm = const_cast<cqgpu_table*>(L);
+        for (int round = 0; round < 2; round++) {
+            uint64_t kmin = 0, kmax = 0, est = 0;
+            auto it = Lm->key_range.find(kl);
+            const bool learned = it != Lm->key_range.end();
+            if (learned) {
+                kmin = it->second.first;
+                kmax = it->second.second;
+                est = kmax - kmin + 1;
+            } else if (!sample_key_range(L, kl, &kmin, &kmax, &est)) {
+                JXDBG("star: no sampled keys\n");
+                break;
+            }
+            const uint64_t range = kmax - kmin + 1;
+            JXDBG("star round %d: keys [%llu, %llu] est %llu learned %d\n", round, (unsigned long long)kmin,
+                  (unsigned long long)kmax, (unsigned long long)est, (int)learned);
+            if (kmax < kmin || range >= (1ull << 31) || range > 4 * est + 1024) break;
+            const size_t b16 = (range * 2 + 15) & ~(size_t)15, b8 = (range + 15) & ~(size_t)15;
+            DevBuf big(b16 + b8), l32(range * 4);
+            const uint32_t G = cq_jx_star_groups();
+            const size_t o_gsum = (size_t)G * 8, o_first = o_gsum + (size_t)G * 24, o_ctl = o_first + (size_t)G * 4;
+            DevBuf small(o_ctl + 64);
+            uint16_t* d16 = big.as<uint16_t>();
+            uint8_t* m8 = big.as<uint8_t>() + b16;
+            unsigned long long* ttab = small.as<unsigned long long>();
+            unsigned long long* gsum = (unsigned long long*)(small.as<uint8_t>() + o_gsum);
+            uint32_t* gfirst = (uint32_t*)(small.as<uint8_t>() + o_first);
+            unsigned int* sflag = (unsigned int*)(small.as<uint8_t>() + o_ctl);
+            unsigned long long* cnts = (unsigned long long*)(small.as<uint8_t>() + o_ctl + 8);   // placed, pairs, occupied
+            unsigned long long* skr = cnts + 3;                                                  // build keys' min, max
+            HIPCHECK(hipMemsetAsync(big.p, 0, b16 + b8, c.stream));
+            HIPCHECK(hipMemsetAsync(small.p, 0, o_ctl + 64, c.stream));
+            HIPCHECK(hipMemsetAsync(gfirst, 0xff, (size_t)G * 4, c.stream));
+            HIPCHECK(hipMemsetAsync(skr, 0xff, 8, c.stream));
+            HIPCHECK(hipEventRecord(c.ev0, c.stream));
+            HIPCHECK(cq_jx_star_extract(L->g, L->data_begin, L->n, ws, d, dq, kl, grouped ? gcol : -1, 1, kmin, range, d16,
+                                        l32.as<uint32_t>(), m8, ttab, gsum, cnts, sflag, skr, xgrid, c.stream));
+            HIPCHECK(cq_jx_star_extract(R->g, R->data_begin, R->n, wsr, d, dq, kr, vcol, 0, kmin, range, d16,
+                                        l32.as<uint32_t>(), m8, ttab, gsum, cnts + 1, sflag, nullptr, xgrid, c.stream));
+            HIPCHECK(cq_jx_star_first(d16, l32.as<uint32_t>(), m8, range, gfirst, cnts + 2, c.ncu * 4, c.stream));
+            bool fb = false;
+            cq_table* res = results([&](TableArena& A) {
+                HIPCHECK(cq_jx_star_flush(grouped ? 1 : 0, vcol >= 0 ? 1 : 0, ttab, gsum, gfirst, cnts,
+                                          grouped ? &A.rt : &A.gt, C.P.nacc, A.stats, sflag, c.stream));
+            }, sflag, 0, 4, &fb);
+            if (res || !fb) {
+                if (res && !learned) {           // the exact range, for the next query on this table
+                    unsigned long long kr2[2] = {~0ull, 0ull};
+                    HIPCHECK(hipMemcpyAsync(kr2, skr, 16, hipMemcpyDeviceToHost, c.stream));
+                    HIPCHECK(hipStreamSynchronize(c.stream));
+                    if (kr2[0] <= kr2[1]) Lm->key_range[kl] = {kr2[0], kr2[1]};
+                }
+                return res;
+            }
+            unsigned int fl = 0;
+            unsigned long long kr2[2] = {~0ull, 0ull};
+            HIPCHECK(hipMemcpyAsync(&fl, sflag, 4, hipMemcpyDeviceToHost, c.stream));
+            HIPCHECK(hipMemcpyAsync(kr2, skr, 16, hipMemcpyDeviceToHost, c.stream));
+            HIPCHECK(hipStreamSynchronize(c.stream));
+            // only a range miss is worth a second round (with the range the build saw)
+            if (fl != 16u || kr2[0] > kr2[1] || learned) break;
+            Lm->key_range[kl] = {kr2[0], kr2[1]};
+        }
+    }
+
     // pass 0: records per window; exclusive scans give every window's first record index
     const uint64_t nwl = cq_jx_windows(L->data_begin, L->n, ws), nwr = cq_jx_windows(R->data_begin, R->n, wsr);
     if (nwl >= (1ull << 31) || nwr >= (1ull << 31)) return nullptr;
@@ -3092,8 +3397,6 @@ cq_table* run_fast_join(DevCtx& c, cq_node* q, Compiled& C, const cqgpu_table* L
     HIPCHECK(hipMemsetAsync(ctl.p, 0, 256, c.stream));
     HIPCHECK(hipMemsetAsync(krange, 0xff, 8, c.stream));
     HIPCHECK(hipMemsetAsync(krange + 2, 0xff, 8, c.stream));
-    const int xgrid = c.ncu;
-    const uint8_t dq = (uint8_t)L->cfg.quote;
     HIPCHECK(hipEventRecord(c.ev0, c.stream));
     HIPCHECK(cq_jx_extract(L->g, L->data_begin, L->n, ws, d, dq, kl, gcol, 1, 0, nullptr, nullptr, nullptr,
                            wcl.as<unsigned int>(), nullptr, 0, dctl + 2, krange, xgrid, c.stream));
@@ -3131,7 +3434,7 @@ cq_table* run_fast_join(DevCtx& c, cq_node* q, Compiled& C, const cqgpu_table* L
     HIPCHECK(hipMemcpyAsync(&fl0, dctl + 2, 4, hipMemcpyDeviceToHost, c.stream));
     HIPCHECK(hipMemcpyAsync(kr2, krange, 16, hipMemcpyDeviceToHost, c.stream));
     HIPCHECK(hipStreamSynchronize(c.stream));
-    if (fl0) return nullptr;
+    if (fl0) { JXDBG("record arrays: extract flags %#x\n", fl0); return nullptr; }
     // the build side's keys: a direct array over a dense key range (primary keys), else
     // the hash table
     DevBuf table(8);
@@ -3157,100 +3460,13 @@ cq_table* run_fast_join(DevCtx& c, cq_node* q, Compiled& C, const cqgpu_table* L
         HIPCHECK(hipMemsetAsync(table.p, 0, (size_t)tcap * cq_jx_entry_bytes(), c.stream));
         HIPCHECK(cq_jx_build(lkey.as<unsigned long long>(), (uint32_t)nL, table.p, tcap, dctl + 2, c.ncu * 8, c.stream));
     }
-    Literals Lit;
-    parse_literals(c, C.lits, Lit);
-    // finish: the representative (left) columns of each group's first pair's left record
-    constexpr uint32_t SB = 48;
-    FinishDesc FD;
-    memset(&FD, 0, sizeof FD);
-    std::vector<int> rep_ord(C.rep_cols.size());
-    for (size_t i = 0; i < rep_ord.size(); i++) rep_ord[i] = (int)i;
-    std::sort(rep_ord.begin(), rep_ord.end(), [&](int a, int b) { return C.rep_cols[a] < C.rep_cols[b]; });
-    FD.ncols = (int32_t)rep_ord.size();
-    for (size_t i = 0; i < rep_ord.size(); i++) FD.cols[i] = (int16_t)C.rep_cols[rep_ord[i]];
-    FD.delim = d;
-    FD.quote = (uint8_t)L->cfg.quote;
-    FD.nacc = C.P.nacc;
-    FD.sb = SB;
-    FD.first_shift = 32;
-    const uint32_t ncell = (uint32_t)FD.ncols + (uint32_t)FD.nacc + 1;
-    uint32_t cap = grouped ? 8192 : 64;
-    for (int attempt = 0; attempt < 4; attempt++, cap *= 8) {
-        TableArena A = make_arena(c, C.P, cap, cap / 2 + 1, 1, 16);
-        const unsigned int cap_out = cap / 2 + 1;
-        Scratch fin(c, (size_t)cap_out * ncell * (sizeof(Cell) + SB) + 64);
-        Cell* dcells = (Cell*)fin.p;
-        uint8_t* dbytes = fin.p + (size_t)cap_out * ncell * sizeof(Cell);
+    bool fb = false;
+    return results([&](TableArena& A) {
         HIPCHECK(cq_jx_probe(grouped ? 1 : 0, vcol >= 0 ? 1 : 0, direct ? 1 : 0, rkey.as<unsigned long long>(),
                              rpay.as<unsigned long long>(), roff.as<uint32_t>(), (uint32_t)nR, kr2[0], table.p, tcap,
                              lpay.as<unsigned long long>(), loff.as<uint32_t>(), grouped ? &A.rt : &A.gt, C.P.nacc,
                              A.stats, dctl + 2, c.ncu * 2, c.stream));
-        if (grouped) HIPCHECK(cq_launch_raw_merge(&A.gt, &A.rt, C.P.nacc, A.stats, c.stream));
-        HIPCHECK(hipEventRecord(c.ev1, c.stream));
-        HIPCHECK(cq_launch_compact(&A.gt, &C.P, A.out, A.out_count, cap_out, c.stream));
-        HIPCHECK(cq_launch_finish(L->g, L->n, A.out, A.out_count, cap_out, &FD, dcells, dbytes, c.stream));
-        constexpr size_t MAIL_HDR = 1024;
-        uint8_t* mail = mailbox(c, MAIL_HDR + cq_pack_result_bytes(cap_out, C.P.nacc, ncell, SB) + 64);
-        HIPCHECK(cq_launch_pack_result(A.out, A.out_count, cap_out, C.P.nacc, dcells, dbytes, ncell, SB,
-                                       mail + MAIL_HDR, A.stats, mail, 1, c.stream));
-        unsigned int fl = 0;
-        HIPCHECK(hipMemcpyAsync(&fl, dctl + 2, 4, hipMemcpyDeviceToHost, c.stream));
-        HIPCHECK(hipStreamSynchronize(c.stream));
-        if (fl) return nullptr;
-        ScanStats st;
-        memcpy(&st, mail, sizeof st);
-        unsigned int ng = 0;
-        memcpy(&ng, mail + sizeof(ScanStats), 4);
-        if (st.overflow >= 2) throw HipError{"fused join: group insert timeout"};
-        if (st.overflow) continue;
-        float ms = 0;
-        HIPCHECK(hipEventElapsedTime(&ms, c.ev0, c.ev1));
-        g_stats.scan_ms = ms;
-        g_stats.records = nL + nR;
-        g_stats.passed = st.passed;
-        g_stats.scan_kernel = 3;
-        ng = std::min(ng, cap_out);
-        const bool presorted = ng <= cq_pack_order_max();
-        static thread_local std::vector<uint8_t> hbuf;
-        const size_t pb = cq_pack_result_bytes(ng, C.P.nacc, ncell, SB);
-        if (hbuf.size() < pb + 8) hbuf.resize(pb + 8);
-        memcpy(hbuf.data(), mail + MAIL_HDR, pb);
-        cq_table* res = nullptr;
-        if (grouped && presorted && ng) res = build_direct(C, hbuf.data(), ng, ncell, SB, rep_ord, Lit, ~0ull);
-        if (!res) {
-            std::vector<GroupOut> outs(ng);
-            std::vector<Cell> fcells((size_t)ng * ncell);
-            std::vector<uint8_t> fbytes((size_t)ng * ncell * SB);
-            const size_t rec = 40 + 40 * (size_t)C.P.nacc;
-            memset(outs.data(), 0, ng * sizeof(GroupOut));
-            for (unsigned int i = 0; i < ng; i++) {
-                const uint8_t* r = hbuf.data() + i * rec;
-                GroupOut& o = outs[i];
-                o.clslen = ((const uint32_t*)r)[0];
-                o.w0 = ((const uint64_t*)r)[1];
-                o.w1 = ((const uint64_t*)r)[2];
-                o.cnt = ((const unsigned long long*)r)[3];
-                o.first = ((const unsigned long long*)r)[4];
-                const uint64_t* qq = (const uint64_t*)(r + 40);
-                for (int a = 0; a < C.P.nacc; a++) {
-                    o.sum[a] = as_dbl(qq[5 * a]);
-                    o.num[a] = qq[5 * a + 1];
-                    o.extpos[a] = NOPOS;
-                }
-            }
-            memcpy(fcells.data(), hbuf.data() + ng * rec, fcells.size() * sizeof(Cell));
-            memcpy(fbytes.data(), hbuf.data() + ng * rec + fcells.size() * sizeof(Cell), fbytes.size());
-            std::vector<HGroup> groups = make_groups(c, C, ~0ull, 0, outs, fcells, fbytes, FD.ncols, rep_ord, SB,
-                                                     presorted);
-            g_stats.groups = groups.size();
-            res = build_groups(C, groups, Lit, c);
-        } else {
-            g_stats.groups = ng;
-        }
-        post_ops(c, res, q);
-        return res;
-    }
-    return nullptr;
+    }, dctl + 2, nL + nR, 3, &fb);
 }
 
 // One JOIN, or a chain of them (process_joins, evaluator_joins.c:237-274): join
@@ -3264,7 +3480,11 @@ cq_table* run_join(DevCtx& c, cq_node* q, const cqgpu_table* L, const cqgpu_tabl
     const int nj = q->u.q.join_count;
     if (nj < 1) throw HipError{"run_join without a JOIN"};
     if (nrights < nj) throw Ineligible{"join table not given"};
-    if (part && nj != 1) throw Ineligible{"join chains across partials"};
+    // across partials the first level runs on the key-routed sides; a chain's later
+    // levels join each rank's joined rows with the whole next table (every joined
+    // row lives on one rank, so INNER and LEFT need nothing global; the unmatched
+    // right rows of a later RIGHT / FULL level would)
+    const bool chain = part && nj > 1;
     struct Level {
         const cqgpu_table* R;
         std::string ra;
@@ -3297,7 +3517,9 @@ cq_table* run_join(DevCtx& c, cq_node* q, const cqgpu_table* L, const cqgpu_tabl
             v.kr = join_on_index(on->u.bin.rhs->u.text, v.R, &W, wa.c_str(), v.R, v.ra.c_str());
         }
         v.keyed = v.kl >= 0 && v.kr >= 0;
-        if (part && !v.keyed) throw Ineligible{"JOIN without an `ident = ident` ON across partials"};
+        if (part && j == 0 && !v.keyed) throw Ineligible{"JOIN without an `ident = ident` ON across partials"};
+        if (part && j > 0 && v.outer_right) throw Ineligible{"RIGHT/FULL JOIN after the first level across partials"};
+        if (part && j > 0 && v.R->gids) throw HipError{"join chain across partials: a later level's table must be whole"};
         v.nleft = (int)wnames.size();
         std::vector<std::string> nn;        // copy_columns_with_prefix (evaluator_joins.c:30-37)
         for (auto& nm : wnames) nn.push_back(wa + "." + nm);
@@ -3342,6 +3564,8 @@ cq_table* run_join(DevCtx& c, cq_node* q, const cqgpu_table* L, const cqgpu_tabl
     std::unique_ptr<JoinSide> Bp;
     DevBuf pairs(8);
     unsigned long long np = 0;
+    DevBuf ckey;                             // chain across partials: each joined row's order key
+    unsigned long long kspace = 0;           // one past every key of the level so far
     for (int j = 0; j < nj; j++) {
         Level& v = lv[j];
         Bp.reset(new JoinSide);
@@ -3351,9 +3575,37 @@ cq_table* run_join(DevCtx& c, cq_node* q, const cqgpu_table* L, const cqgpu_tabl
         DevBuf pb(8);
         np = build_pairs(c, *Ap, *Bp, v.kl, v.kr, v.keyed, v.outer_left, v.outer_right, pb);
         std::swap(pairs.p, pb.p);
-        if (part && v.keyed) {               // even when one side is empty on this rank
+        if (part && j == 0 && v.keyed) {     // even when one side is empty on this rank
             part->lmask |= key_class_mask(c, *Ap, v.kl);
             part->rmask |= key_class_mask(c, *Bp, v.kr);
+        }
+        if (chain) {                         // route.hip chain_key_kernel
+            DevBuf nk((size_t)std::max<unsigned long long>(np, 1) * 8);
+            if (j == 0) {
+                if ((L->gids && !L->gid_total) || (v.R->gids && !v.R->gid_total))
+                    throw HipError{"routed join side without its record total (cqgpu_table_set_record_total)"};
+                const unsigned long long nl0 = L->gids ? L->gid_total : Ap->n;
+                const unsigned long long nr0 = v.R->gids ? v.R->gid_total : Bp->n;
+                if ((unsigned __int128)(nl0 + 1) * (nr0 + 1) >= ((unsigned __int128)1 << 64))
+                    throw Ineligible{"join chain across partials: order keys over 64 bits"};
+                DevBuf lown, rown;
+                const unsigned long long *lg = nullptr, *rg = nullptr;
+                side_gids(c, L, Ap->n, lown, &lg);
+                side_gids(c, v.R, Bp->n, rown, &rg);
+                HIPCHECK(cq_launch_chain_key(pairs.as<uint2>(), np, lg, nl0, nr0 + 1, rg, nr0,
+                                             nk.as<unsigned long long>(), c.stream));
+                HIPCHECK(hipStreamSynchronize(c.stream));     // lown / rown go out of scope
+                kspace = (nl0 + 1) * (nr0 + 1);
+            } else {
+                const unsigned long long nr = Bp->n;
+                if ((unsigned __int128)(kspace + 1) * (nr + 1) >= ((unsigned __int128)1 << 64))
+                    throw Ineligible{"join chain across partials: order keys over 64 bits"};
+                HIPCHECK(cq_launch_chain_key(pairs.as<uint2>(), np, ckey.as<unsigned long long>(), kspace, nr + 1,
+                                             nullptr, nr, nk.as<unsigned long long>(), c.stream));
+                HIPCHECK(hipStreamSynchronize(c.stream));     // the previous keys are released below
+                kspace = (kspace + 1) * (nr + 1);
+            }
+            std::swap(ckey.p, nk.p);
         }
         if (j + 1 == nj) break;
         // the joined rows' cells the next levels read: the next left side
@@ -3403,11 +3655,17 @@ cq_table* run_join(DevCtx& c, cq_node* q, const cqgpu_table* L, const cqgpu_tabl
         std::vector<unsigned long long> keys;
         if (part) {   // every passing row with its global order key; the merge sorts, ORDER / LIMIT after
             DevBuf lown, rown, dk(std::max<unsigned long long>(npass, 1) * 8);
-            const unsigned long long *lg = nullptr, *rg = nullptr;
-            side_gids(c, L, A.n, lown, &lg);
-            side_gids(c, R, B.n, rown, &rg);
-            HIPCHECK(cq_launch_pair_gid_flagged(pairs.as<uint2>(), np, flags.as<unsigned int>(), pos.as<unsigned int>(),
-                                                lg, rg, dk.as<unsigned long long>(), c.stream));
+            if (chain) {
+                HIPCHECK(cq_launch_key_flagged(ckey.as<unsigned long long>(), np, flags.as<unsigned int>(),
+                                               pos.as<unsigned int>(), dk.as<unsigned long long>(), c.stream));
+            } else {
+                const unsigned long long *lg = nullptr, *rg = nullptr;
+                side_gids(c, L, A.n, lown, &lg);
+                side_gids(c, R, B.n, rown, &rg);
+                HIPCHECK(cq_launch_pair_gid_flagged(pairs.as<uint2>(), np, flags.as<unsigned int>(),
+                                                    pos.as<unsigned int>(), lg, rg, dk.as<unsigned long long>(),
+                                                    c.stream));
+            }
             keys.resize(npass);
             if (npass) HIPCHECK(hipMemcpyAsync(keys.data(), dk.p, npass * 8, hipMemcpyDeviceToHost, c.stream));
             HIPCHECK(hipStreamSynchronize(c.stream));
@@ -3490,13 +3748,18 @@ cq_table* run_join(DevCtx& c, cq_node* q, const cqgpu_table* L, const cqgpu_tabl
                 if (p >= np) throw HipError{"join partial: pair position out of range"};
             if (!pidx.empty()) {
                 DevBuf lown, rown;
-                const unsigned long long *lg = nullptr, *rg = nullptr;
-                side_gids(c, L, A.n, lown, &lg);
-                side_gids(c, R, B.n, rown, &rg);
                 DevBuf dp(pidx.size() * 8), dk(pidx.size() * 8);
                 HIPCHECK(hipMemcpyAsync(dp.p, pidx.data(), pidx.size() * 8, hipMemcpyHostToDevice, c.stream));
-                HIPCHECK(cq_launch_pair_gid(pairs.as<uint2>(), dp.as<unsigned long long>(), (uint32_t)pidx.size(), lg,
-                                            rg, dk.as<unsigned long long>(), c.stream));
+                if (chain) {
+                    HIPCHECK(cq_launch_key_pick(ckey.as<unsigned long long>(), dp.as<unsigned long long>(),
+                                                (uint32_t)pidx.size(), dk.as<unsigned long long>(), c.stream));
+                } else {
+                    const unsigned long long *lg = nullptr, *rg = nullptr;
+                    side_gids(c, L, A.n, lown, &lg);
+                    side_gids(c, R, B.n, rown, &rg);
+                    HIPCHECK(cq_launch_pair_gid(pairs.as<uint2>(), dp.as<unsigned long long>(), (uint32_t)pidx.size(),
+                                                lg, rg, dk.as<unsigned long long>(), c.stream));
+                }
                 std::vector<unsigned long long> keys(pidx.size());
                 HIPCHECK(hipMemcpyAsync(keys.data(), dk.p, keys.size() * 8, hipMemcpyDeviceToHost, c.stream));
                 HIPCHECK(hipStreamSynchronize(c.stream));
@@ -3985,7 +4248,8 @@ int cqgpu_route_plan(cq_node* q, cqgpu_table* const* tables, int ntables, int si
         bump_reset(c);
         if (ntables < 2 || !tables[0] || !tables[1] || (side != 0 && side != 1)) throw HipError{"route: bad tables"};
         if (nranks < 1 || nranks > 4096) throw HipError{"route: bad rank count"};
-        if (!q || q->kind != CQ_N_QUERY || q->u.q.join_count != 1 || !q->u.q.joins[0]) throw Ineligible{"not one JOIN"};
+        // the first JOIN's ON keys route both its sides; a chain's later tables stay whole
+        if (!q || q->kind != CQ_N_QUERY || q->u.q.join_count < 1 || !q->u.q.joins[0]) throw Ineligible{"no JOIN"};
         check_plan_shape(q, tables[0], true);
         cq_node* jn = q->u.q.joins[0];
         cq_node* on = jn->u.join.on;
@@ -4137,6 +4401,16 @@ cqgpu_table* cqgpu_table_from_routed(const void* dev_bytes, size_t n, const uint
         cqgpu_table_free(t);
         return nullptr;
     }
+}
+
+int cqgpu_table_set_record_total(cqgpu_table* t, uint64_t total) {
+    g_err.clear();
+    if (!t || total < t->ngids) {
+        set_err("cq_amd: %s", "record total below the table's own records");
+        return -1;
+    }
+    t->gid_total = total;
+    return 0;
 }
 
 void cqgpu_table_free(cqgpu_table* t) {

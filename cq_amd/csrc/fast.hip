@@ -140,6 +140,7 @@ __device__ __forceinline__ uint32_t vreg(uint32_t x) {
 struct CK {
     uint32_t tn1, tn0, td1, td0;   // v_perm tables: terminators, delimiter
     uint32_t m40;                  // 0x40404040
+    uint32_t m80;                  // 0x80808080
     uint32_t w0, w1;               // v_dot4 bit weights
     uint32_t rd, rq;               // delimiter / quote bytes x 4 (non-COMMA)
 };
@@ -169,7 +170,11 @@ __device__ __forceinline__ void classify32(const v4u a, const v4u b, const CK& k
             const uint32_t x = j < 4 ? a[j & 3] : b[j & 3];
             const uint32_t rn = __builtin_amdgcn_perm(k.tn1, k.tn0, x ^ 0x06060606u);
             const uint32_t rd = __builtin_amdgcn_perm(k.td1, k.td0, x ^ 0x2E2E2E2Eu);
+#ifdef FAST_OLD_Q
             q = __builtin_amdgcn_bitop3_b32(rd - 0x01010101u, rd, q, 0xBA);   // (t & ~rd) | q: quotes
+#else
+            q = __builtin_amdgcn_bitop3_b32(rd, q, k.m80, 0xCE);                // q | (~rd & 0x80): quotes (rd 0x00)
+#endif
             const uint32_t fn = rn & k.m40;                                    // 1: not a terminator
             const uint32_t fs = __builtin_amdgcn_bitop3_b32(rn, rd, k.m40, 0x80);   // 1: not a separator
             const uint32_t w = (j & 1) ? k.w1 : k.w0;
@@ -379,7 +384,12 @@ __device__ __forceinline__ uint32_t key_len8(uint64_t w0) {
 
 // a record whose key found no LDS slot: straight into the HBM raw table
 // (acc1: bit a set when accumulator a sums SUM argument 1, else argument 0)
-__device__ __noinline__ void spill8(uint64_t tag, uint64_t off, const GroupTable* tabs, ScanStats* stats, int nacc,
+#ifdef FAST_SPILL_INL
+#define FAST_SPILL_ATTR __forceinline__
+#else
+#define FAST_SPILL_ATTR __noinline__
+#endif
+__device__ FAST_SPILL_ATTR void spill8(uint64_t tag, uint64_t off, const GroupTable* tabs, ScanStats* stats, int nacc,
                                     uint32_t acc1, bool n0, double v0, bool n1, double v1) {
     const GroupTable& rt = tabs[TAB_RT];
     const uint32_t kl = key_len8(tag);
@@ -421,7 +431,10 @@ constexpr uint32_t fixed_bytes() { return (uint32_t)(sizeof(WaveLds) * NWV); }
 // (else none); NS: distinct SUM arguments; COMMA: delimiter ',' and quote '"';
 // CANON: the roles' columns ascend in the order WHERE, SUM 0, SUM 1, GROUP BY (the
 // walk's ranks are compile-time), else rank[] says which field each role reads
-template <bool GROUPED, bool WHERE, int NS, bool COMMA, bool CANON, int RP>
+// WN: numerals of 5-7 bytes / over 3 decimals are typed here (a side path); without
+// it (the plan's sampled WHERE / SUM fields are all <= 4 bytes) such a record goes
+// whole to slow_kernel, and the kernel keeps only the fixed-point SUM
+template <bool GROUPED, bool WHERE, int NS, bool COMMA, bool CANON, int RP, bool WN>
 __global__ __launch_bounds__(LT) void fast_kernel(const uint8_t* __restrict__ g, ScanStats* __restrict__ stats,
                                                   unsigned long long* __restrict__ slow_list,
                                                   unsigned long long slow_cap, const FastPlan fp,
@@ -468,6 +481,7 @@ __global__ __launch_bounds__(LT) void fast_kernel(const uint8_t* __restrict__ g,
     ck.td1 = vreg(COMMA ? CLS2_TD1 : 0u);
     ck.td0 = vreg(COMMA ? CLS2_TD0 : 0x40u);
     ck.m40 = vreg(COMMA ? 0x01010101u : 0x40404040u);   // (COMMA: the bit-0 mask)
+    ck.m80 = vreg(0x80808080u);
 #else
     ck.tn1 = vreg(0x00004000u);
     ck.tn0 = vreg(0x00400000u);
@@ -482,6 +496,18 @@ __global__ __launch_bounds__(LT) void fast_kernel(const uint8_t* __restrict__ g,
     const uint64_t first_win = fp.first_win;
     const uint32_t nwin = __builtin_amdgcn_readfirstlane(fp.nwin);
     const uint32_t wsb = __builtin_amdgcn_readfirstlane(fp.ws);
+#ifndef FAST_SR
+    // uniform plan values of the cold paths (and the WHERE's NULL / negation bits)
+    // held in VGPRs: the loop's scalar registers stay for its own state
+    const bool pass_null = vreg(fp.pass_null) != 0;
+    const int wlo = (int)vreg((uint32_t)fp.wlo), whi = (int)vreg((uint32_t)fp.whi);
+    const uint32_t wtt = vreg(fp.wtt);
+    const uint32_t wa = vreg(fp.wa), ww = vreg(fp.ww);
+    const bool wneg = vreg(fp.wneg) != 0;
+    const double wl = fp.wl;
+    const int nacc = (int)vreg((uint32_t)fp.nacc);
+    const uint32_t acc1 = vreg(fp.acc1);
+#else
     const bool pass_null = __builtin_amdgcn_readfirstlane(fp.pass_null) != 0;
     const int wlo = __builtin_amdgcn_readfirstlane(fp.wlo), whi = __builtin_amdgcn_readfirstlane(fp.whi);
     const uint32_t wtt = __builtin_amdgcn_readfirstlane(fp.wtt);
@@ -490,6 +516,7 @@ __global__ __launch_bounds__(LT) void fast_kernel(const uint8_t* __restrict__ g,
     const double wl = fp.wl;
     const int nacc = __builtin_amdgcn_readfirstlane(fp.nacc);
     const uint32_t acc1 = __builtin_amdgcn_readfirstlane(fp.acc1);
+#endif
     const uint32_t wstep = gridDim.x * NWV;
     // interior windows own the records starting in their first ws bytes: the lanes below ws / 64
     const uint32_t lane_full = (uint32_t)lane * LB < wsb ? ~0u : 0u;
@@ -734,7 +761,7 @@ __global__ __launch_bounds__(LT) void fast_kernel(const uint8_t* __restrict__ g,
                     wu[u] = !n.ok & (len != 0) & !fail[u];
                     wide |= wu[u];
                 }
-                if (__any(wide)) {                                   // DOUBLE or 5-7 byte numerals
+                if (WN && __any(wide)) {                             // DOUBLE or 5-7 byte numerals
 #pragma unroll
                     for (int u = 0; u < RP; u++) {
                         if (wu[u]) {
@@ -784,7 +811,7 @@ __global__ __launch_bounds__(LT) void fast_kernel(const uint8_t* __restrict__ g,
                     sw[u] = !n.ok & (len != 0) & !fail[u];
                     wide |= sw[u];
                 }
-                if (__any(wide)) {
+                if (WN && __any(wide)) {
 #pragma unroll
                     for (int u = 0; u < RP; u++) {
                         if (sw[u]) {
@@ -1081,7 +1108,37 @@ struct JxOut {
     unsigned int cap;
     unsigned int* flag;
     unsigned long long* krange;   // [0] min, [1] max of the non-NULL keys
+    // STAR passes (jx_star_*): no record arrays; the build side goes straight into
+    // key-indexed arrays over [kmin, kmin + range), the probe side aggregates in place
+    unsigned long long kmin, range;
+    uint16_t* d16;             // build: group id + 1 of key kmin + i (0: no build record)
+    uint32_t* l32;             // build: that record's byte offset
+    uint8_t* m8;               // probe: 1 when key kmin + i met a probe record
+    unsigned long long* ttab;  // build: GROUP BY raw tags, slot = group id (0: free)
+    unsigned long long* gsum;  // probe: per group id COUNT, fixed-point SUM, SUM count
+    unsigned long long* nbuilt;   // build: records placed
 };
+// STAR flags (JxOut.flag): 8 a NULL build key, 16 a key outside [kmin, kmin + range),
+// 32 more GROUP BY tags than JX_G, 64 a repeated build key (placed != occupied)
+constexpr uint32_t JX_G = 2048;           // group ids of a STAR join (LDS sums per block)
+
+// a GROUP BY raw tag's group id: its slot in the tag table (linear probing; a stale
+// 0 read only leads to the CAS, a set slot never changes)
+__device__ __forceinline__ uint32_t jx_tag_gid(unsigned long long* __restrict__ tt, unsigned long long tag,
+                                               bool& full) {
+    uint32_t s = fast_key_hash((uint32_t)tag, (uint32_t)(tag >> 32)) & (JX_G - 1);
+    for (uint32_t q = 0; q < JX_G; q++) {
+        const unsigned long long t = tt[s];
+        if (t == tag) return s;
+        if (t == 0ull) {
+            const unsigned long long old = atomicCAS(&tt[s], 0ull, tag);
+            if (old == 0ull || old == tag) return s;
+        }
+        s = (s + 1) & (JX_G - 1);
+    }
+    full = true;
+    return 0;
+}
 
 // the canonical INTEGER key of a field (16 bytes d0..d3 from its start, len bytes):
 // digits only, no leading zero, at most 15 digits and not 8-10; NULL (empty) -> JX_NULLKEY
@@ -1106,10 +1163,22 @@ __device__ __forceinline__ bool jx_key(uint32_t d0, uint32_t d1, uint32_t d2, ui
     return ok;
 }
 
-template <bool BUILD, bool COMMA, int NR, bool COUNT>
+template <bool BUILD, bool COMMA, int NR, bool COUNT, bool STAR = false>
 __global__ __launch_bounds__(LT) void jx_extract_kernel(const uint8_t* __restrict__ g, const JxPlan jp, const JxOut jo) {
     extern __shared__ __align__(16) uint8_t smem[];
     WaveLds* waves = (WaveLds*)smem;
+    // STAR probe: per group id COUNT / fixed-point SUM / SUM count of this block
+    constexpr bool SPROBE = STAR && !BUILD;
+    constexpr uint32_t NG = SPROBE ? JX_G : 1;
+    unsigned long long* sfix = (unsigned long long*)(smem + sizeof(WaveLds) * NWV);
+    uint32_t* scnt = (uint32_t*)(sfix + NG);
+    uint32_t* snum = scnt + NG;
+    if constexpr (SPROBE) {
+        for (uint32_t k = threadIdx.x; k < NG; k += LT) { sfix[k] = 0; scnt[k] = 0; snum[k] = 0; }
+        __syncthreads();
+    }
+    uint32_t sflag = 0;
+    unsigned long long nstar = 0;
     const int tid = threadIdx.x, lane = tid & 63;
     const int wv = __builtin_amdgcn_readfirstlane(tid >> 6);
     WaveLds& W = waves[wv];
@@ -1121,6 +1190,7 @@ __global__ __launch_bounds__(LT) void jx_extract_kernel(const uint8_t* __restric
     ck.td1 = vreg(COMMA ? CLS2_TD1 : 0u);
     ck.td0 = vreg(COMMA ? CLS2_TD0 : 0x40u);
     ck.m40 = vreg(COMMA ? 0x01010101u : 0x40404040u);   // (COMMA: the bit-0 mask)
+    ck.m80 = vreg(0x80808080u);
 #else
     ck.tn1 = vreg(0x00004000u);
     ck.tn0 = vreg(0x00400000u);
@@ -1193,7 +1263,7 @@ __global__ __launch_bounds__(LT) void jx_extract_kernel(const uint8_t* __restric
         // record j of this lane in this window lands at wbase[i] + (the lanes below's
         // records) + j: file order
         const uint32_t nmine = (uint32_t)__popcll(todo);
-        uint32_t at_next = jo.wbase[i] + wave_incl_scan(nmine) - nmine;
+        uint32_t at_next = STAR ? 0u : jo.wbase[i] + wave_incl_scan(nmine) - nmine;
         bool issued = false;
         while (__any(todo != 0)) {
             uint32_t p[2], pa[2], fst[2][2], fen[2][2], e[2];
@@ -1302,18 +1372,50 @@ __global__ __launch_bounds__(LT) void jx_extract_kernel(const uint8_t* __restric
                 }
                 issued = true;
             }
+            if constexpr (STAR) {
 #pragma unroll
-            for (int u = 0; u < 2; u++) {
-                if (valid[u]) {
-                    const uint32_t at = at_next++;
-                    if (at < jo.cap) {
-                        jo.key[at] = key[u];
-                        jo.pay[at] = pay[u];
-                        jo.off[at] = (uint32_t)(wbase + p[u]);
+                for (int u = 0; u < 2; u++) {
+                    if (!valid[u] || fail[u]) continue;
+                    const unsigned long long k = key[u];
+                    const unsigned long long ix = k - jo.kmin;
+                    if (BUILD) {
+                        if (k == JX_NULLKEY) { sflag |= 8u; continue; }
+                        kmin = k < kmin ? k : kmin;
+                        kmax = k > kmax ? k : kmax;
+                        if (ix >= jo.range) { sflag |= 16u; continue; }
+                        bool full = false;
+                        const uint32_t gid = NR == 2 ? jx_tag_gid(jo.ttab, pay[u], full) : 0u;
+                        if (full) sflag |= 32u;
+                        jo.d16[ix] = (uint16_t)(gid + 1u);
+                        jo.l32[ix] = (uint32_t)(wbase + p[u]);
+                        nstar++;
+                    } else if (k != JX_NULLKEY && ix < jo.range) {
+                        const uint32_t gp = jo.d16[ix];
+                        if (gp) {
+                            jo.m8[ix] = 1;
+                            atomicAdd(&scnt[gp - 1u], 1u);
+                            if (NR == 2 && pay[u] != JX_NOVAL) {
+                                atomicAdd(&sfix[gp - 1u], pay[u]);
+                                atomicAdd(&snum[gp - 1u], 1u);
+                            }
+                            nstar++;
+                        }
                     }
-                    if (key[u] != JX_NULLKEY) {
-                        kmin = key[u] < kmin ? key[u] : kmin;
-                        kmax = key[u] > kmax ? key[u] : kmax;
+                }
+            } else {
+#pragma unroll
+                for (int u = 0; u < 2; u++) {
+                    if (valid[u]) {
+                        const uint32_t at = at_next++;
+                        if (at < jo.cap) {
+                            jo.key[at] = key[u];
+                            jo.pay[at] = pay[u];
+                            jo.off[at] = (uint32_t)(wbase + p[u]);
+                        }
+                        if (key[u] != JX_NULLKEY) {
+                            kmin = key[u] < kmin ? key[u] : kmin;
+                            kmax = key[u] > kmax ? key[u] : kmax;
+                        }
                     }
                 }
             }
@@ -1326,6 +1428,26 @@ __global__ __launch_bounds__(LT) void jx_extract_kernel(const uint8_t* __restric
     }
     if (COUNT) return;
     if (__any(bad) && lane == 0) atomicOr(jo.flag, 1u);
+    if constexpr (STAR) {
+        for (int o = 32; o > 0; o >>= 1) {
+            sflag |= (uint32_t)__shfl_down((int)sflag, o, 64);
+            nstar += __shfl_down(nstar, o, 64);
+        }
+        if (lane == 0 && sflag) atomicOr(jo.flag, sflag);
+        if (lane == 0 && nstar) atomicAdd(jo.nbuilt, nstar);   // build: placed; probe: pairs
+    }
+    if constexpr (SPROBE) {
+        __syncthreads();
+        for (uint32_t k = threadIdx.x; k < NG; k += LT) {
+            if (!scnt[k]) continue;
+            atomicAdd(&jo.gsum[3 * k], (unsigned long long)scnt[k]);
+            if (snum[k]) {
+                atomicAdd(&jo.gsum[3 * k + 1], sfix[k]);
+                atomicAdd(&jo.gsum[3 * k + 2], (unsigned long long)snum[k]);
+            }
+        }
+        return;
+    }
     for (int o = 32; o > 0; o >>= 1) {
         const unsigned long long a = __shfl_down(kmin, o, 64), b = __shfl_down(kmax, o, 64);
         kmin = a < kmin ? a : kmin;
@@ -1334,6 +1456,84 @@ __global__ __launch_bounds__(LT) void jx_extract_kernel(const uint8_t* __restric
     if (lane == 0 && kmin != ~0ull) {
         atomicMin(&jo.krange[0], kmin);
         atomicMax(&jo.krange[1], kmax);
+    }
+}
+
+// STAR: each group's first pair in (l, r) order has the group's smallest matched build
+// record l (its records' keys are distinct); its byte offset per group id.  Also counts
+// the occupied keys: fewer than the records placed means a repeated build key.
+__global__ __launch_bounds__(1024) void jx_star_first_kernel(const uint16_t* __restrict__ d16,
+                                                             const uint32_t* __restrict__ l32,
+                                                             const uint8_t* __restrict__ m8, uint64_t range,
+                                                             uint32_t* __restrict__ gfirst,
+                                                             unsigned long long* __restrict__ nocc) {
+    __shared__ uint32_t sf[JX_G];
+    for (uint32_t k = threadIdx.x; k < JX_G; k += blockDim.x) sf[k] = ~0u;
+    __syncthreads();
+    unsigned long long occ = 0;
+    const uint64_t n8 = range / 8;
+    for (uint64_t w = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x; w < n8; w += (uint64_t)gridDim.x * blockDim.x) {
+        const uint4 dv = ((const uint4*)d16)[w];             // 8 group ids
+        const uint2 mv = ((const uint2*)m8)[w];              // 8 match bytes
+        const uint32_t dw[4] = {dv.x, dv.y, dv.z, dv.w};
+#pragma unroll
+        for (int j = 0; j < 8; j++) {
+            const uint32_t gp = (dw[j >> 1] >> (16 * (j & 1))) & 0xFFFFu;
+            const uint32_t mb = ((j < 4 ? mv.x : mv.y) >> (8 * (j & 3))) & 0xFFu;
+            occ += gp != 0u;
+            if (gp && mb) atomicMin(&sf[gp - 1u], l32[w * 8 + j]);
+        }
+    }
+    for (uint64_t ix = n8 * 8 + (uint64_t)blockIdx.x * blockDim.x + threadIdx.x; ix < range;
+         ix += (uint64_t)gridDim.x * blockDim.x) {
+        const uint32_t gp = d16[ix];
+        occ += gp != 0u;
+        if (gp && m8[ix]) atomicMin(&sf[gp - 1u], l32[ix]);
+    }
+    for (int o = 32; o > 0; o >>= 1) occ += __shfl_down(occ, o, 64);
+    if ((threadIdx.x & 63) == 0 && occ) atomicAdd(nocc, occ);
+    __syncthreads();
+    for (uint32_t k = threadIdx.x; k < JX_G; k += blockDim.x)
+        if (sf[k] != ~0u) atomicMin(&gfirst[k], sf[k]);
+}
+
+// STAR: the per-group sums into the join's group table (raw tags -> raw_merge_kernel,
+// as jx_probe_kernel's flush; ungrouped: the one GK_ALL group); a repeated build key
+// (occupied keys != records placed) sets flag 64 and nothing is written
+template <bool GROUPED, bool VALUE>
+__global__ __launch_bounds__(1024) void jx_star_flush_kernel(const unsigned long long* __restrict__ ttab,
+                                                             const unsigned long long* __restrict__ gsum,
+                                                             const uint32_t* __restrict__ gfirst,
+                                                             const unsigned long long* __restrict__ cnts,
+                                                             GroupTable rt, int nacc, ScanStats* __restrict__ stats,
+                                                             unsigned int* __restrict__ flag) {
+    // cnts: [0] build records placed, [1] pairs, [2] occupied keys
+    if (cnts[0] != cnts[2]) {
+        if (threadIdx.x == 0) atomicOr(flag, 64u);
+        return;
+    }
+    if (threadIdx.x == 0 && cnts[1]) atomicAdd(&stats->passed, cnts[1]);
+    for (uint32_t s = threadIdx.x; s < (GROUPED ? JX_G : 1u); s += blockDim.x) {
+        const unsigned long long cnt = gsum[3 * s];
+        if (!cnt) continue;
+        GKey kk;
+        if (GROUPED) {
+            const unsigned long long w0 = ttab[s];
+            const uint32_t kl = key_len8(w0);
+            kk = raw_key(kl, kl ? w0 : 0ull);
+        } else {
+            kk.cls = GK_ALL; kk.len = 0; kk.w0 = 0; kk.w1 = 0;
+        }
+        const int gi = g_insert(rt, kk, GROUPED ? gk_hash(kk) : 0x12345678ULL, stats);
+        if (gi < 0) continue;
+        atomicAdd(&rt.cnt[gi], cnt);
+        atomicMin(&rt.first[gi], (unsigned long long)gfirst[s] << 32);
+        if (VALUE && gsum[3 * s + 2]) {
+            for (int a = 0; a < nacc; a++) {
+                atomicAdd(&rt.sum[a][gi], (double)(long long)gsum[3 * s + 1] / 1000.0);
+                atomicAdd(&rt.num[a][gi], gsum[3 * s + 2]);
+            }
+        }
     }
 }
 
@@ -1518,7 +1718,8 @@ bool fcmp_result(uint32_t op, int c) {
 
 // fast_kernel's plan shape (see the file comment); fills the FastPlan fields that
 // depend on the plan only
-bool fast_shape(const ScanPlan* P, int grouped, FastPlan* fp, int* ns, bool* where, bool* canonical) {
+bool fast_shape(const ScanPlan* P, int grouped, FastPlan* fp, int* ns, bool* where, bool* canonical,
+                bool* wide_num = nullptr) {
     if (P->nacc > MAX_ACC || P->ngpart > 0) return false;
     const uint32_t d = P->delim;
     if ((d - '0') < 10u || d == '.' || ((d | 32) >= 'a' && (d | 32) <= 'z') || d == '+' || d == '-') return false;
@@ -1602,6 +1803,12 @@ bool fast_shape(const ScanPlan* P, int grouped, FastPlan* fp, int* ns, bool* whe
         canon = canon && k == want;
     }
     *canonical = canon;
+    if (wide_num) {       // a WHERE / SUM column whose sampled fields exceed 4 bytes
+        bool wn = false;
+        for (int k = 0; k < nr; k++)
+            if (roles[k] != 3) wn = wn || ((P->fast_wide_cols >> (cols[k] < 63 ? cols[k] : 63)) & 1);
+        *wide_num = wn || getenv("CQGPU_FAST_WN") != nullptr;
+    }
     return true;
 }
 
@@ -1612,25 +1819,59 @@ typedef void (*fast_fn_t)(const uint8_t*, ScanStats*, unsigned long long*, unsig
 // bytes usually hold three starts, and a two-record pass would run a second pass
 // for the few lanes with a third); ungrouped plans only, the grouped kernels keep
 // two (register budget of the lookup and atomics)
-template <bool G, bool WH, bool COMMA, bool CANON>
+template <bool G, bool WH, bool COMMA, bool CANON, bool WN>
 fast_fn_t pick_ns(int ns, bool rp3) {
     if constexpr (!G) {
         if (rp3) {
-            if (ns == 0) return fast::fast_kernel<G, WH, 0, COMMA, CANON, 3>;
-            return ns == 1 ? fast::fast_kernel<G, WH, 1, COMMA, CANON, 3> : fast::fast_kernel<G, WH, 2, COMMA, CANON, 3>;
+            if (ns == 0) return fast::fast_kernel<G, WH, 0, COMMA, CANON, 3, WN>;
+            return ns == 1 ? fast::fast_kernel<G, WH, 1, COMMA, CANON, 3, WN> : fast::fast_kernel<G, WH, 2, COMMA, CANON, 3, WN>;
         }
     }
-    if (ns == 0) return fast::fast_kernel<G, WH, 0, COMMA, CANON, 2>;
-    return ns == 1 ? fast::fast_kernel<G, WH, 1, COMMA, CANON, 2> : fast::fast_kernel<G, WH, 2, COMMA, CANON, 2>;
+    if (ns == 0) return fast::fast_kernel<G, WH, 0, COMMA, CANON, 2, WN>;
+    return ns == 1 ? fast::fast_kernel<G, WH, 1, COMMA, CANON, 2, WN> : fast::fast_kernel<G, WH, 2, COMMA, CANON, 2, WN>;
 }
+// (the narrow-numeral kernels for the ',' / '"' canonical plans only: the others keep
+// the side path)
 template <bool G, bool CANON>
-fast_fn_t pick_wc(bool where, int ns, bool comma, bool rp3) {
-    if (where) return comma ? pick_ns<G, true, true, CANON>(ns, rp3) : pick_ns<G, true, false, CANON>(ns, rp3);
-    return comma ? pick_ns<G, false, true, CANON>(ns, rp3) : pick_ns<G, false, false, CANON>(ns, rp3);
+fast_fn_t pick_wc(bool where, int ns, bool comma, bool rp3, bool wn) {
+    if (where) {
+        if (!comma) return pick_ns<G, true, false, CANON, true>(ns, rp3);
+        return (CANON && !wn) ? pick_ns<G, true, true, CANON, false>(ns, rp3) : pick_ns<G, true, true, CANON, true>(ns, rp3);
+    }
+    if (!comma) return pick_ns<G, false, false, CANON, true>(ns, rp3);
+    return (CANON && !wn) ? pick_ns<G, false, true, CANON, false>(ns, rp3) : pick_ns<G, false, true, CANON, true>(ns, rp3);
 }
 template <bool G>
-fast_fn_t pick_fast(bool where, int ns, bool comma, bool canon, bool rp3) {
-    return canon ? pick_wc<G, true>(where, ns, comma, rp3) : pick_wc<G, false>(where, ns, comma, rp3);
+fast_fn_t pick_fast(bool where, int ns, bool comma, bool canon, bool rp3, bool wn) {
+    return canon ? pick_wc<G, true>(where, ns, comma, rp3, wn) : pick_wc<G, false>(where, ns, comma, rp3, wn);
+}
+
+// the window range and the key / payload field walk of a join side (jx_extract_kernel)
+bool jx_plan(const uint8_t* g, uint64_t lo, uint64_t hi, uint32_t ws, uint32_t delim, uint32_t quote, int kcol,
+             int pcol, fast::JxPlan* jp) {
+    if (((uintptr_t)g & 255) != 0 || kcol < 0 || ws > (uint32_t)fast::WS || ws % 128 || ws == 0) return false;
+    memset(jp, 0, sizeof *jp);
+    jp->ws = ws;
+    jp->delim = delim;
+    jp->quote = quote;
+    if (hi > lo) {
+        const uint64_t wl = lo / ws, wh = (hi - 1) / ws;
+        if (wh - wl + 1 >= (1ull << 31)) return false;
+        jp->first_win = wl;
+        jp->nwin = (uint32_t)(wh - wl + 1);
+        jp->lo_s = (uint32_t)(lo - wl * ws);
+        jp->hi_s = (uint32_t)(hi - wh * ws);
+    }
+    if (pcol < 0) {
+        jp->skip[0] = (uint32_t)kcol;
+        jp->rank_key = 0;
+    } else {
+        const int c0 = std::min(kcol, pcol), c1 = std::max(kcol, pcol);
+        jp->skip[0] = (uint32_t)c0;
+        jp->skip[1] = (uint32_t)(c1 - c0);
+        jp->rank_key = kcol <= pcol ? 0u : 1u;
+    }
+    return true;
 }
 
 size_t fast_lds(int grouped, int ns) {
@@ -1661,7 +1902,8 @@ hipError_t cq_launch_fast(const uint8_t* g, const cq::ScanPlan* P, const cq::Gro
     FastPlan fp;
     int ns = 0;
     bool where = false, canon = false;
-    if (!fast_shape(P, grouped, &fp, &ns, &where, &canon)) return hipErrorInvalidValue;
+    bool wn = true;
+    if (!fast_shape(P, grouped, &fp, &ns, &where, &canon, &wn)) return hipErrorInvalidValue;
     if (((uintptr_t)g & 255) != 0) return hipErrorInvalidValue;
     const uint64_t hi = P->range_end < P->n ? P->range_end : P->n;
     const uint64_t lo = P->data_begin > P->range_begin ? P->data_begin : P->range_begin;
@@ -1695,8 +1937,8 @@ hipError_t cq_launch_fast(const uint8_t* g, const cq::ScanPlan* P, const cq::Gro
     hipError_t e = cq::upload_buffer(tabs_dev[dev & 63], tabs, sizeof tabs, s);
     if (e != hipSuccess) return e;
     const bool comma = P->delim == ',' && P->quote == '"';
-    const fast_fn_t fn = grouped ? pick_fast<true>(where, ns, comma, canon, false)
-                                 : pick_fast<false>(where, ns, comma, canon, rp3);
+    const fast_fn_t fn = grouped ? pick_fast<true>(where, ns, comma, canon, false, wn)
+                                 : pick_fast<false>(where, ns, comma, canon, rp3, wn);
     const size_t lds = fast_lds(grouped, ns);
     cq::set_max_lds((const void*)fn, (int)lds);
     hipLaunchKernelGGL(fn, dim3(grid), dim3(fast::LT), lds, s, g, stats, slow_list, slow_cap, fp,
@@ -1718,30 +1960,9 @@ hipError_t cq_jx_extract(const uint8_t* g, uint64_t lo, uint64_t hi, uint32_t ws
                          uint32_t* off, unsigned int* wcount, const unsigned int* wbase, unsigned int cap,
                          unsigned int* flag, unsigned long long* krange, int grid, hipStream_t s) {
     using namespace cq::fast;
-    if (((uintptr_t)g & 255) != 0 || kcol < 0 || ws > (uint32_t)WS || ws % 128) return hipErrorInvalidValue;
     JxPlan jp;
-    memset(&jp, 0, sizeof jp);
-    jp.ws = ws;
-    jp.delim = delim;
-    jp.quote = quote;
-    if (hi > lo) {
-        const uint64_t wl = lo / ws, wh = (hi - 1) / ws;
-        if (wh - wl + 1 >= (1ull << 31)) return hipErrorInvalidValue;
-        jp.first_win = wl;
-        jp.nwin = (uint32_t)(wh - wl + 1);
-        jp.lo_s = (uint32_t)(lo - wl * ws);
-        jp.hi_s = (uint32_t)(hi - wh * ws);
-    }
+    if (!jx_plan(g, lo, hi, ws, delim, quote, kcol, pcol, &jp)) return hipErrorInvalidValue;
     const int nr = pcol >= 0 ? 2 : 1;
-    if (nr == 1) {
-        jp.skip[0] = (uint32_t)kcol;
-        jp.rank_key = 0;
-    } else {
-        const int c0 = std::min(kcol, pcol), c1 = std::max(kcol, pcol);
-        jp.skip[0] = (uint32_t)c0;
-        jp.skip[1] = (uint32_t)(c1 - c0);
-        jp.rank_key = kcol <= pcol ? 0u : 1u;
-    }
     const bool comma = delim == ',' && quote == '"';
     typedef void (*xfn_t)(const uint8_t*, const JxPlan, const JxOut);
     static const xfn_t tab[2][2][2][2] = {
@@ -1755,6 +1976,7 @@ hipError_t cq_jx_extract(const uint8_t* g, uint64_t lo, uint64_t hi, uint32_t ws
           {jx_extract_kernel<true, true, 2, false>, jx_extract_kernel<true, true, 2, true>}}}};
     const xfn_t fn = tab[build ? 1 : 0][comma ? 1 : 0][nr - 1][pass == 0 ? 1 : 0];
     JxOut jo;
+    memset(&jo, 0, sizeof jo);
     jo.key = key; jo.pay = pay; jo.off = off; jo.wcount = wcount; jo.wbase = wbase; jo.cap = cap; jo.flag = flag;
     jo.krange = krange;
     const size_t lds = sizeof(WaveLds) * NWV;
@@ -1763,6 +1985,67 @@ hipError_t cq_jx_extract(const uint8_t* g, uint64_t lo, uint64_t hi, uint32_t ws
     hipLaunchKernelGGL(fn, dim3(grid), dim3(LT), lds, s, g, jp, jo);
     return hipGetLastError();
 }
+
+// STAR join passes (jx_extract_kernel<..., STAR>): build -- every record's key straight
+// into d16 / l32 at key - kmin, its GROUP BY tag's id through ttab; probe -- every
+// record's key looked up in d16, m8 set, COUNT / SUM per group id into gsum.
+// counter: build records placed (build) / pairs (probe).
+hipError_t cq_jx_star_extract(const uint8_t* g, uint64_t lo, uint64_t hi, uint32_t ws, uint32_t delim, uint32_t quote,
+                              int kcol, int pcol, int build, unsigned long long kmin, unsigned long long range,
+                              uint16_t* d16, uint32_t* l32, uint8_t* m8, unsigned long long* ttab,
+                              unsigned long long* gsum, unsigned long long* counter, unsigned int* flag,
+                              unsigned long long* krange, int grid, hipStream_t s) {
+    using namespace cq::fast;
+    JxPlan jp;
+    if (!jx_plan(g, lo, hi, ws, delim, quote, kcol, pcol, &jp)) return hipErrorInvalidValue;
+    const int nr = pcol >= 0 ? 2 : 1;
+    const bool comma = delim == ',' && quote == '"';
+    typedef void (*xfn_t)(const uint8_t*, const JxPlan, const JxOut);
+    static const xfn_t tab[2][2][2] = {
+        {{jx_extract_kernel<false, false, 1, false, true>, jx_extract_kernel<false, false, 2, false, true>},
+         {jx_extract_kernel<false, true, 1, false, true>, jx_extract_kernel<false, true, 2, false, true>}},
+        {{jx_extract_kernel<true, false, 1, false, true>, jx_extract_kernel<true, false, 2, false, true>},
+         {jx_extract_kernel<true, true, 1, false, true>, jx_extract_kernel<true, true, 2, false, true>}}};
+    const xfn_t fn = tab[build ? 1 : 0][comma ? 1 : 0][nr - 1];
+    JxOut jo;
+    memset(&jo, 0, sizeof jo);
+    jo.flag = flag;
+    jo.krange = krange;
+    jo.kmin = kmin;
+    jo.range = range;
+    jo.d16 = d16;
+    jo.l32 = l32;
+    jo.m8 = m8;
+    jo.ttab = ttab;
+    jo.gsum = gsum;
+    jo.nbuilt = counter;
+    const size_t lds = sizeof(WaveLds) * NWV + (build ? 0 : (size_t)JX_G * 16);
+    cq::set_max_lds((const void*)fn, (int)lds);
+    if (jp.nwin == 0) return hipSuccess;
+    hipLaunchKernelGGL(fn, dim3(grid), dim3(LT), lds, s, g, jp, jo);
+    return hipGetLastError();
+}
+hipError_t cq_jx_star_first(const uint16_t* d16, const uint32_t* l32, const uint8_t* m8, unsigned long long range,
+                            uint32_t* gfirst, unsigned long long* nocc, int grid, hipStream_t s) {
+    if (((uintptr_t)d16 & 15) || ((uintptr_t)m8 & 7)) return hipErrorInvalidValue;
+    hipLaunchKernelGGL(cq::fast::jx_star_first_kernel, dim3(grid), dim3(1024), 0, s, d16, l32, m8, (uint64_t)range,
+                       gfirst, nocc);
+    return hipGetLastError();
+}
+hipError_t cq_jx_star_flush(int grouped, int value, const unsigned long long* ttab, const unsigned long long* gsum,
+                            const uint32_t* gfirst, const unsigned long long* cnts, const cq::GroupTable* rt, int nacc,
+                            cq::ScanStats* stats, unsigned int* flag, hipStream_t s) {
+    using namespace cq::fast;
+    typedef void (*ffn_t)(const unsigned long long*, const unsigned long long*, const uint32_t*,
+                          const unsigned long long*, GroupTable, int, ScanStats*, unsigned int*);
+    static const ffn_t tab[2][2] = {{jx_star_flush_kernel<false, false>, jx_star_flush_kernel<false, true>},
+                                    {jx_star_flush_kernel<true, false>, jx_star_flush_kernel<true, true>}};
+    hipLaunchKernelGGL(tab[grouped ? 1 : 0][value ? 1 : 0], dim3(1), dim3(1024), 0, s, ttab, gsum, gfirst, cnts, *rt,
+                       nacc, stats, flag);
+    return hipGetLastError();
+}
+uint32_t cq_jx_star_groups() { return cq::fast::JX_G; }
+
 hipError_t cq_jx_build(const unsigned long long* key, uint32_t n, void* table, uint64_t tcap, unsigned int* flag,
                        int grid, hipStream_t s) {
     if (tcap & (tcap - 1)) return hipErrorInvalidValue;

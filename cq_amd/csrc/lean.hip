@@ -1472,7 +1472,13 @@ int cq_lean_waves_per_block() { return lean::NWV; }
 // Columns whose sampled fields (up to 256 KiB of records, quote-blind split) are
 // longer than 8 bytes: bit c for column c < 63, bit 63 for every later column.
 // A GROUP BY on such a column runs the K16 tag width.
+uint64_t cq_cols_longer_than(const uint8_t* data, uint64_t n, uint32_t delim, uint32_t limit);
 uint64_t cq_lean_long_cols(const uint8_t* data, uint64_t n, uint32_t delim) {
+    return cq_cols_longer_than(data, n, delim, 8);
+}
+// bit c: a sampled field of column c (the first 256 KiB) is longer than `limit`
+// bytes (bit 63 for every column from 63 on, and always set)
+uint64_t cq_cols_longer_than(const uint8_t* data, uint64_t n, uint32_t delim, uint32_t limit) {
     const uint64_t m = n < (256u << 10) ? n : (256u << 10);
     uint64_t mask = 1ull << 63, i = 0;
     while (i < m) {
@@ -1482,7 +1488,7 @@ uint64_t cq_lean_long_cols(const uint8_t* data, uint64_t n, uint32_t delim) {
         while (i <= m) {
             const bool end = i == m || data[i] == '\n' || data[i] == '\r';
             if (end || data[i] == delim) {
-                if (i - fs > 8) mask |= 1ull << (c < 63 ? c : 63);
+                if (i - fs > limit) mask |= 1ull << (c < 63 ? c : 63);
                 c++;
                 fs = i + 1;
                 if (end) break;

@@ -78,6 +78,7 @@ struct ScanPlan {
     uint32_t lean_ws;      // lean_kernel window stride (0: the largest, lean::WS)
     uint32_t lean_k16;     // lean_kernel GROUP BY tags of 16 key bytes (the column's sampled fields exceed 8)
     uint64_t fast_seed;    // fast_kernel: device address of the GROUP BY column's seeded LDS tags (0: none)
+    uint64_t fast_wide_cols;   // bit c: sampled fields of column c over 4 bytes (bit 63: columns >= 63)
     uint32_t test_digest_bits;   // test knob CQGPU_TEST_DIGEST_BITS: composite digests cut to this many bits (0: all 128)
 };
 
@@ -222,7 +223,10 @@ struct GmHdr {
     uint64_t pad[2];
 };
 static_assert(sizeof(GmHdr) == GM_HDR, "gather-merge header");
-__host__ __device__ constexpr uint32_t gm_rec_bytes(int nacc, uint32_t R) {
+#if defined(__HIPCC__)
+__host__ __device__
+#endif
+constexpr uint32_t gm_rec_bytes(int nacc, uint32_t R) {
     return 40u + 16u * (uint32_t)nacc + GM_CELL * (R + 1u);
 }
 

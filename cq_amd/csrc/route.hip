@@ -149,6 +149,40 @@ __global__ void pair_gid_flagged_kernel(const uint2* __restrict__ pairs, unsigne
     out[pos[i]] = (l << 32) | r;
 }
 
+// A chain of joins across partials (process_joins, evaluator_joins.c:237-274): the
+// reference's output order at level j is the order of the working row, then the
+// right row (nested loops), with an outer join's unmatched right rows appended in
+// right-row order.  As one 64-bit mixed-radix key: K_j = K_{j-1} * (n_j + 1) + r,
+// r = n_j for a NULL right side, and K_{j-1} = S_{j-1} (one past every real key of
+// the level before) for an unmatched right row; level 0's key is the global left
+// record id.  The host checks that the key space S_j = (S_{j-1} + 1) * (n_j + 1)
+// stays below 2^64.  prev / rg null: the row index itself.
+__global__ void chain_key_kernel(const uint2* __restrict__ pairs, unsigned long long np,
+                                 const unsigned long long* __restrict__ prev, unsigned long long prev_none,
+                                 unsigned long long radix, const unsigned long long* __restrict__ rg,
+                                 unsigned long long r_none, unsigned long long* __restrict__ out) {
+    const unsigned long long i = (unsigned long long)blockIdx.x * blockDim.x + threadIdx.x;
+    if (i >= np) return;
+    const uint2 pr = pairs[i];
+    const unsigned long long w = pr.x == PAIR_NONE ? prev_none : (prev ? prev[pr.x] : (unsigned long long)pr.x);
+    const unsigned long long r = pr.y == PAIR_NONE ? r_none : (rg ? rg[pr.y] : (unsigned long long)pr.y);
+    out[i] = w * radix + r;
+}
+
+// keys of selected pairs: out[i] = key[pidx[i]], or the flagged pairs' keys at their
+// output positions (pos: exclusive scan of flags)
+__global__ void key_pick_kernel(const unsigned long long* __restrict__ key, const unsigned long long* __restrict__ pidx,
+                                uint32_t n, unsigned long long* __restrict__ out) {
+    const uint32_t i = blockIdx.x * blockDim.x + threadIdx.x;
+    if (i < n) out[i] = key[pidx[i]];
+}
+__global__ void key_flagged_kernel(const unsigned long long* __restrict__ key, unsigned long long np,
+                                   const unsigned int* __restrict__ flags, const unsigned int* __restrict__ pos,
+                                   unsigned long long* __restrict__ out) {
+    const unsigned long long i = (unsigned long long)blockIdx.x * blockDim.x + threadIdx.x;
+    if (i < np && flags[i]) out[pos[i]] = key[i];
+}
+
 // ---- record starts of a whole table (csv_load's line split, reference
 // csv_reader.c:403-427: a record is a maximal non-empty run of bytes other than
 // '\n' / '\r'; the header record ends at data_begin).  Two bandwidth passes over
@@ -289,6 +323,26 @@ hipError_t cq_launch_pair_gid(const uint2* pairs, const unsigned long long* pidx
                               hipStream_t s) {
     if (!n) return hipSuccess;
     pair_gid_kernel<<<blocks(n, 256), 256, 0, s>>>(pairs, pidx, n, lg, rg, out);
+    return hipGetLastError();
+}
+
+hipError_t cq_launch_chain_key(const uint2* pairs, unsigned long long np, const unsigned long long* prev,
+                               unsigned long long prev_none, unsigned long long radix, const unsigned long long* rg,
+                               unsigned long long r_none, unsigned long long* out, hipStream_t s) {
+    if (!np) return hipSuccess;
+    chain_key_kernel<<<(unsigned)((np + 255) / 256), 256, 0, s>>>(pairs, np, prev, prev_none, radix, rg, r_none, out);
+    return hipGetLastError();
+}
+hipError_t cq_launch_key_pick(const unsigned long long* key, const unsigned long long* pidx, uint32_t n,
+                              unsigned long long* out, hipStream_t s) {
+    if (!n) return hipSuccess;
+    key_pick_kernel<<<blocks(n, 256), 256, 0, s>>>(key, pidx, n, out);
+    return hipGetLastError();
+}
+hipError_t cq_launch_key_flagged(const unsigned long long* key, unsigned long long np, const unsigned int* flags,
+                                 const unsigned int* pos, unsigned long long* out, hipStream_t s) {
+    if (!np) return hipSuccess;
+    key_flagged_kernel<<<(unsigned)((np + 255) / 256), 256, 0, s>>>(key, np, flags, pos, out);
     return hipGetLastError();
 }
 

@@ -1379,6 +1379,11 @@ __global__ __launch_bounds__(FINISH_T) void finish_kernel(const uint8_t* __restr
     const uint32_t ncell = (uint32_t)(D.ncols + D.nacc + 1);
     const uint32_t i = blockIdx.x * blockDim.x + threadIdx.x;
     const uint32_t ng = *count < cap_out ? *count : cap_out;
+    // the column list through LDS (a pointer into the by-value descriptor would put
+    // the whole descriptor in every lane's scratch)
+    __shared__ int16_t scols[MAX_WIDE];
+    for (int k = threadIdx.x; k < D.ncols; k += blockDim.x) scols[k] = D.cols[k];
+    __syncthreads();
     if (i >= ng) return;
     Cell* cs = cells + (size_t)i * ncell;
     const unsigned long long first = out[i].first == NOPOS ? NOPOS : out[i].first >> D.first_shift;
@@ -1396,7 +1401,7 @@ __global__ __launch_bounds__(FINISH_T) void finish_kernel(const uint8_t* __restr
 #pragma unroll
             for (int w = 0; w < 9; w++) stage[threadIdx.x][w] = v[w];
             const uint8_t* tile = (const uint8_t*)stage[threadIdx.x] + ((uintptr_t)rec & 15);
-            parse_cols_out_staged(tile, 128, rec, D.cols, D.ncols, D.delim, D.quote, cs);
+            parse_cols_out_staged(tile, 128, rec, scols, D.ncols, D.delim, D.quote, cs);
         } else {
             for (int k = 0; k < D.ncols; k++) cs[k] = cell_null();
         }

@@ -77,13 +77,20 @@ def exchange(send: torch.Tensor, send_counts: list[int]) -> tuple[torch.Tensor, 
     return recv, recv_counts
 
 
-def exclusive_base(count: int, device: torch.device | str = "cpu") -> int:
-    """sum of `count` over lower ranks (global record id of this rank's first record)"""
+def base_and_total(count: int, device: torch.device | str = "cpu") -> tuple[int, int]:
+    """(sum of `count` over lower ranks, sum over all ranks): the global record id of
+    this rank's first record and the whole input's record count"""
     world = dist.get_world_size()
     t = torch.tensor([count], dtype=torch.int64, device=device)
     allc = [torch.zeros(1, dtype=torch.int64, device=device) for _ in range(world)]
     dist.all_gather(allc, t)
-    return sum(int(x.item()) for x in allc[: dist.get_rank()])
+    counts = [int(x) for x in torch.cat(allc).cpu().tolist()]
+    return sum(counts[: dist.get_rank()]), sum(counts)
+
+
+def exclusive_base(count: int, device: torch.device | str = "cpu") -> int:
+    """sum of `count` over lower ranks (global record id of this rank's first record)"""
+    return base_and_total(count, device)[0]
 
 
 def scan_partitioned(ast, table, comm_device: torch.device | str | None = None):
@@ -296,9 +303,12 @@ def scan_partitioned_rccl(ast, table):
 
 
 def join_partitioned(ast, lshard, rshard, lheader: bytes, rheader: bytes, device: torch.device | str,
-                     comm_device: torch.device | str | None = None):
-    """Repartitioned INNER JOIN over this rank's shards of both inputs.
+                     comm_device: torch.device | str | None = None, rest=()):
+    """Repartitioned JOIN over this rank's shards of both inputs of the first JOIN.
 
+    rest: a chain's later JOIN tables, each whole on every rank (the joined rows of
+    the first level are spread over the ranks by its key; each rank joins its own
+    with the whole next table).
     Returns the merged result pointer on rank 0 (free with cq_amd.result_free)
     and None elsewhere.  Every rank must call it (collectives inside).
     comm_device: where the collectives run -- `device` for RCCL (default); "cpu"
@@ -309,14 +319,14 @@ def join_partitioned(ast, lshard, rshard, lheader: bytes, rheader: bytes, device
         # one rank: every record routes to itself in its own order (the stable sort by
         # destination is the identity), so the shards are already the routed tables
         # and their record ids the local row indexes
-        return cq_amd.merge_partials(ast, [cq_amd.query_partial(ast, [lshard, rshard])])
+        return cq_amd.merge_partials(ast, [cq_amd.query_partial(ast, [lshard, rshard, *rest])])
     comm = torch.device(comm_device) if comm_device is not None else torch.device(device)
     routed = []
     for side, (tab, header) in enumerate(((lshard, lheader), (rshard, rheader))):
         plan, err = _local(cq_amd.route_plan, ast, [lshard, rshard], side, world)
         agree(err, comm)
         nbytes, nrecs = plan
-        base = exclusive_base(sum(nrecs), comm)
+        base, total = base_and_total(sum(nrecs), comm)
 
         def fill():
             b = torch.empty(max(sum(nbytes), 1), dtype=torch.uint8, device=device)
@@ -332,9 +342,12 @@ def join_partitioned(ast, lshard, rshard, lheader: bytes, rheader: bytes, device
         rb, rg = rb.to(device), rg.to(device)
         torch.cuda.synchronize(device)
         t, err = _local(cq_amd.table_from_routed, rb.data_ptr(), rb.numel(), rg.data_ptr(), rg.numel(), header)
+        if t is not None:
+            _, e2 = _local(cq_amd.table_set_record_total, t, total)
+            err = err or e2
         agree(err, comm)
         routed.append(t)
-    blob, err = _local(cq_amd.query_partial, ast, routed)
+    blob, err = _local(cq_amd.query_partial, ast, routed + list(rest))
     agree(err, comm)
     blobs = gather_blobs(blob, comm)
     if rank != 0:

@@ -197,6 +197,11 @@ int cqgpu_route_fill(cqgpu_table* t, uint64_t gid_base, void* dev_bytes, uint64_
  * the side's header record */
 cqgpu_table* cqgpu_table_from_routed(const void* dev_bytes, size_t n, const uint64_t* dev_gids, size_t nrec,
                                      cq_csv_config cfg, const char* header, size_t header_len);
+/* the record count of the whole input a routed table came from (the sum of every
+ * rank's route_plan records): a chain of JOINs across partials orders its rows by
+ * mixed-radix keys over it (route.hip chain_key_kernel).  -1 if below the table's
+ * own record count.  A chain's later tables are passed whole to query_partial. */
+int cqgpu_table_set_record_total(cqgpu_table* t, uint64_t total);
 
 /* ---- output ----------------------------------------------------------------
  * replaces write_csv_file (reference utils.c:220-289, called by main.c:133 for

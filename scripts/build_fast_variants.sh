@@ -9,6 +9,6 @@ for v in ${VARIANTS:-"f1:-DFAST_PROF=1" "f2:-DFAST_PROF=2" "f3:-DFAST_PROF=3"}; 
   n=${v%%:*}; d=$(echo "${v#*:}" | tr "+" " ")
   ( /opt/rocm/bin/hipcc $F $d -c fast.hip -o /tmp/fast_$n.o && \
     /opt/rocm/bin/hipcc -shared --offload-arch=gfx950 -o ../lib/libcqgpu_$n.so ../lib/scan.o ../lib/lean.o /tmp/fast_$n.o \
-        ../lib/executor.o ../lib/route.o ../lib/prim.o ../lib/writer.o ../lib/merge.o ../lib/hostcell.o ) &
+        ../lib/executor.o ../lib/route.o ../lib/prim.o ../lib/writer.o ../lib/merge.o ../lib/hostcell.o -L/opt/rocm/lib -lrccl -Wl,-rpath,/opt/rocm/lib ) &
 done
 wait

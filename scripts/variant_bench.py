@@ -33,7 +33,7 @@ class Stats(C.Structure):
     _fields_ = [("scan_ms", C.c_double), ("total_ms", C.c_double), ("scan_bytes", C.c_uint64),
                 ("records", C.c_uint64), ("groups", C.c_uint64), ("lds_spills", C.c_uint64),
                 ("grid", C.c_int), ("path", C.c_int), ("retries", C.c_int),
-                ("slow_records", C.c_uint64), ("passed", C.c_uint64), ("scan_kernel", C.c_int)]
+                ("slow_records", C.c_uint64), ("passed", C.c_uint64), ("scan_kernel", C.c_int), ("wide", C.c_int)]
 
 
 libs = {}

@@ -256,3 +256,27 @@ def test_fast_count_star_no_roles(d):
     p.write_text(body)
     st = check(f"SELECT COUNT(*) FROM '{p}'")
     assert st["slow_records"] == 0, st
+
+
+@pytest.mark.parametrize("wn", [False, True])
+def test_fast_narrow_numerals_late_wide(d, monkeypatch, wn):
+    """When the sampled WHERE / SUM fields (first 256 KiB) are all <= 4 bytes the plan
+    takes the narrow-numeral kernel (no 5-7 byte / double side path): numerals wider
+    than that which appear only later go whole to slow_kernel.  CQGPU_FAST_WN keeps
+    the side path (typed in place, no slow record).  Both equal the oracle."""
+    if wn:
+        monkeypatch.setenv("CQGPU_FAST_WN", "1")
+    rng = np.random.default_rng(13)
+    rows = ["%d,%d.%d,k%d" % (rng.integers(0, 99), rng.integers(0, 9), rng.integers(0, 9), i % 37)
+            for i in range(60_000)]
+    rows += ["%s,%s,k%d" % (["12345", "7", "12.50", "3"][i % 4], ["1.2345", "99999", "2.5", "0.125"][i % 4], i % 37)
+             for i in range(40_000)]
+    # (the roles in canonical column order: WHERE, SUM, GROUP BY)
+    p = _write(d / "latewide.csv", "v,h,k", rows)
+    for sql in (f"SELECT k, COUNT(*), SUM(h), AVG(h) FROM '{p}' WHERE v > 30 GROUP BY k",
+                f"SELECT COUNT(*), SUM(h), AVG(h) FROM '{p}' WHERE v < 50"):
+        st = check(sql)
+        if wn:
+            assert st["slow_records"] == 0, st
+        else:
+            assert st["slow_records"] > 0, st

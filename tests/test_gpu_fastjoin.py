@@ -1,9 +1,11 @@
 """The fused aggregate join (executor.hip run_fast_join, fast.hip jx_* kernels) against
 the oracle's nested-loop join (reference evaluator_joins.c:63-181 feeding
 evaluate_aggregate): counts, group sets and first-pair order exact, SUM/AVG within
-1e-6 relative.  Each case also checks which path ran: stats()["scan_kernel"] == 3 is
-the fused path; shapes it must decline (a quote, a short row, a non-canonical key, a
-wide numeral) still give the oracle's answer through the general pipeline.
+1e-6 relative.  Each case also checks which path ran: stats()["scan_kernel"] == 4 is
+the STAR path (a dense build-key range: key-indexed arrays, no record arrays), 3 the
+record-array path (repeated or NULL build keys: the hash table); shapes both must
+decline (a quote, a short row, a non-canonical key, a wide numeral) still give the
+oracle's answer through the general pipeline.
 """
 import numpy as np
 import pytest
@@ -95,11 +97,60 @@ def test_fused_join(tables, case):
     sql = tmpl.replace("{L}", tables[lk]).replace("{R}", tables[rk])
     kind = _run(sql)
     # "ON o.cid = u.id" resolves each operand against its own side first (the ON quirk)
-    assert kind == 3 or "o.cid = u.id" in sql, (sql, kind)
+    want = 4 if lk == "u" else 3          # dense unique keys: STAR; repeats / NULLs: the hash table
+    assert kind == want or "o.cid = u.id" in sql, (sql, kind)
 
 
 @pytest.mark.parametrize("case", range(len(DECLINED)))
 def test_declined_shapes_match_oracle(tables, case):
     lk, rk, tmpl = DECLINED[case]
     sql = tmpl.replace("{L}", tables[lk]).replace("{R}", tables[rk])
-    assert _run(sql) != 3, sql
+    assert _run(sql) not in (3, 4), sql
+
+
+def _star_tables(tmp_path, n, order, seed, ntags=40, late_dup=False, late_null=False):
+    rng = np.random.default_rng(seed)
+    ids = np.arange(n) + 10**10 + 200          # (11-digit keys: 8-10 digits may type as DATEs)
+    if order == "shuffled":
+        ids = rng.permutation(ids)
+    elif order == "descending":
+        ids = ids[::-1]
+    rows = [f"{i},n{i % 91},{18 + i % 60},r{int(rng.integers(0, ntags)):04d}" for i in ids]
+    if late_dup:
+        rows.append(f"{ids[5]},dupname,33,r0001")
+    if late_null:
+        rows.append(",nullname,34,r0002")
+    u = _write(tmp_path, f"su_{order}_{n}_{ntags}_{late_dup}_{late_null}.csv", "id,name,age,role", rows)
+    o = _write(tmp_path, f"so_{order}_{n}.csv", "id,price,quantity,customer_id",
+               [f"{j},{rng.integers(100, 99999) / 100:.2f},{rng.integers(1, 9)},{int(rng.integers(0, n + 500)) + 10**10}"
+                for j in range(400)])   # (the oracle joins by nested loops)
+    return u, o
+
+
+@pytest.mark.parametrize("order", ["ascending", "shuffled", "descending"])
+def test_star_join_key_orders(tmp_path, order):
+    """STAR over 12 K build records (the sampled 256 KiB covers about 2/3): ascending
+    ids (the sampled range holds), shuffled and descending ids (the sampled range
+    misses: a second round with the build's own range); then the same query again on
+    the same tables (the learned range)"""
+    u, o = _star_tables(tmp_path, 12_000, order, 11)
+    sql = (f"SELECT u.role, COUNT(*), SUM(o.price), AVG(o.price) FROM '{u}' AS u JOIN '{o}' AS o "
+           "ON u.id = o.customer_id GROUP BY u.role")
+    assert _run(sql) == 4
+    assert _run(sql) == 4
+    sql2 = f"SELECT COUNT(*), SUM(o.quantity) FROM '{u}' AS u JOIN '{o}' AS o ON u.id = o.customer_id"
+    assert _run(sql2) == 4
+    sql3 = f"SELECT u.name, u.age, COUNT(*) FROM '{u}' AS u JOIN '{o}' AS o ON u.id = o.customer_id GROUP BY u.name"
+    assert _run(sql3) == 4
+
+
+def test_star_join_declines(tmp_path):
+    """a build key repeated after the sample, a NULL build key, more GROUP BY values
+    than the STAR join's 2048 group ids: the record-array path answers"""
+    sqlt = "SELECT u.role, COUNT(*), SUM(o.price) FROM '{u}' AS u JOIN '{o}' AS o ON u.id = o.customer_id GROUP BY u.role"
+    u, o = _star_tables(tmp_path, 12_000, "ascending", 12, late_dup=True)
+    assert _run(sqlt.format(u=u, o=o)) == 3
+    u, o = _star_tables(tmp_path, 12_000, "ascending", 13, late_null=True)
+    assert _run(sqlt.format(u=u, o=o)) == 3
+    u, o = _star_tables(tmp_path, 12_000, "shuffled", 14, ntags=5000)
+    assert _run(sqlt.format(u=u, o=o)) == 3

@@ -37,13 +37,15 @@ def _shards(data: bytes, nranks: int, seed: int):
     return header, tabs
 
 
-def _run(ast, ldata: bytes, rdata: bytes, nranks: int):
+def _run(ast, ldata: bytes, rdata: bytes, nranks: int, rest=()):
+    """rest: a chain's later JOIN tables, whole on every rank"""
     lh, ls = _shards(ldata, nranks, 1)
     rh, rs = _shards(rdata, nranks, 2)
     routed = [[None, None] for _ in range(nranks)]
     keep = []
     for side, (hdr, sh) in enumerate(((lh, ls), (rh, rs))):
         plans = [cq_amd.route_plan(ast, [ls[r], rs[r]], side, nranks) for r in range(nranks)]
+        total = sum(sum(nr) for _, nr in plans)
         sends, base = [], 0
         for r in range(nranks):
             nb, nr = plans[r]
@@ -61,10 +63,14 @@ def _run(ast, ldata: bytes, rdata: bytes, nranks: int):
             keep += [rb, rg]
             torch.cuda.synchronize()          # torch's copies before the library's stream reads them
             routed[d][side] = cq_amd.table_from_routed(rb.data_ptr(), rb.numel(), rg.data_ptr(), rg.numel(), hdr)
-    blobs = [cq_amd.query_partial(ast, routed[d]) for d in range(nranks)]
-    tp = cq_amd.merge_partials(ast, blobs)
-    for t in ls + rs + [x for pr in routed for x in pr]:
-        t.close()
+            cq_amd.table_set_record_total(routed[d][side], total)
+    whole = [[cq_amd.Table.from_bytes(x) for x in rest] for _ in range(nranks)]
+    try:
+        blobs = [cq_amd.query_partial(ast, routed[d] + whole[d]) for d in range(nranks)]
+        tp = cq_amd.merge_partials(ast, blobs)
+    finally:
+        for t in ls + rs + [x for pr in routed for x in pr] + [x for w in whole for x in w]:
+            t.close()
     return tp
 
 
@@ -97,6 +103,11 @@ def files(tmp_path_factory):
     f["sb"] = ("k,w\n" + "".join(f"{'' if i % 53 == 0 else 'key%03d' % (i % 170)},{i * 3}\n"
                                   for i in range(700))).encode()
     f["mixed"] = b"k,z\n1,a\nx,b\n2,c\n,d\n2020-01-02,e\nx,f\n1.0,g\n"
+    # chain tables: roles of "du" (role_20..22 missing, role_05 twice, a NULL role) and
+    # labels of the order quantities
+    f["rl"] = ("role,dept,grade\n" + "".join(f"role_{i:02d},dept{i % 4},{i % 3}\n" for i in range(20))
+               + "role_05,dept9,7\n,deptx,0\n").encode()
+    f["qt"] = b"q,label\n0,lab0\n2,lab2\n1,lab1\n2,lab2b\n9,lab9\n"
     paths = {}
     for k, v in f.items():
         p = d / f"{k}.csv"
@@ -164,6 +175,72 @@ def test_repartitioned_join(files, case, nranks):
     compare(got, want, tol, f"{sql} @ {nranks} ranks")
 
 
+CHAINS = [
+    # (the reference resolves a chained table's columns by their exact joined names:
+    # the last level's "r.x" / "q.x"; earlier levels' "o.x" / "u.x" read NULL -- kept
+    # in two queries as a parity check of that rule)
+    (["rl"], "SELECT r.dept, COUNT(*), SUM(r.grade), AVG(r.grade) FROM '{L}' AS u JOIN '{R}' AS o "
+             "ON u.id = o.customer_id JOIN '{X}' AS r ON u.role = r.role GROUP BY r.dept"),
+    (["rl"], "SELECT COUNT(*), MIN(r.grade), MAX(r.dept), SUM(o.price) FROM '{L}' AS u JOIN '{R}' AS o "
+             "ON u.id = o.customer_id LEFT JOIN '{X}' AS r ON u.role = r.role"),
+    (["rl"], "SELECT r.role, r.dept, r.grade FROM '{L}' AS u JOIN '{R}' AS o ON u.id = o.customer_id "
+             "JOIN '{X}' AS r ON u.role = r.role WHERE r.grade > 1"),
+    (["rl"], "SELECT r.role, r.grade, o.id FROM '{L}' AS u JOIN '{R}' AS o ON u.id = o.customer_id "
+             "LEFT JOIN '{X}' AS r ON u.role = r.role LIMIT 25 OFFSET 10"),
+    (["rl"], "SELECT r.dept, COUNT(*), MAX(r.grade), MIN(r.role) FROM '{L}' AS u LEFT JOIN '{R}' AS o "
+             "ON u.id = o.customer_id JOIN '{X}' AS r ON u.role = r.role GROUP BY r.dept"),
+    (["rl"], "SELECT r.grade, COUNT(*), SUM(r.grade) FROM '{L}' AS u FULL JOIN '{R}' AS o "
+             "ON u.id = o.customer_id LEFT JOIN '{X}' AS r ON u.role = r.role GROUP BY r.grade"),
+    (["rl"], "SELECT r.role, r.dept FROM '{L}' AS u RIGHT JOIN '{R}' AS o ON u.id = o.customer_id "
+             "LEFT JOIN '{X}' AS r ON u.role = r.role WHERE r.grade = 2 ORDER BY r.dept DESC LIMIT 30"),
+    (["rl", "qt"], "SELECT q.label, COUNT(*), SUM(q.q), MIN(q.label) FROM '{L}' AS u JOIN '{R}' AS o "
+                   "ON u.id = o.customer_id JOIN '{X}' AS r ON u.role = r.role "
+                   "JOIN '{Y}' AS q ON r.grade = q.q GROUP BY q.label"),
+    (["rl", "qt"], "SELECT q.label, q.q FROM '{L}' AS u JOIN '{R}' AS o ON u.id = o.customer_id "
+                   "LEFT JOIN '{X}' AS r ON u.role = r.role LEFT JOIN '{Y}' AS q ON r.grade = q.q "
+                   "LIMIT 40 OFFSET 500"),
+]
+
+
+def _chain_sql(paths, rest, tmpl):
+    sql = tmpl.replace("{L}", paths["du"]).replace("{R}", paths["do"])
+    for ph, k in zip(("{X}", "{Y}"), rest):
+        sql = sql.replace(ph, paths[k])
+    return sql
+
+
+@pytest.mark.parametrize("nranks", [1, 3, 8])
+@pytest.mark.parametrize("case", range(len(CHAINS)))
+def test_join_chain_across_partials(files, case, nranks):
+    """process_joins (evaluator_joins.c:237-274) across partials: the first JOIN on
+    the key-routed sides, the later ones against the whole next table on every
+    rank; rows and groups in the reference's nested-loop order through the
+    mixed-radix chain keys (route.hip chain_key_kernel)"""
+    data, paths = files
+    rest, tmpl = CHAINS[case]
+    sql = _chain_sql(paths, rest, tmpl)
+    want, unsup = cqtest.oracle_query(sql)
+    assert not unsup, sql
+    with cqtest.Parsed(sql) as ast:
+        tp = _run(ast, data["du"], data["do"], nranks, [data[k] for k in rest])
+        assert tp, (sql, cq_amd.last_error())
+        got = abi.table_to_py(tp)
+        cq_amd.result_free(tp)
+        tol = tolerant_columns(ast)
+    compare(got, want, tol, f"{sql} @ {nranks} ranks")
+
+
+def test_join_chain_right_later_refused(files):
+    """a later level's RIGHT / FULL JOIN needs every rank's matches: refused, not approximated"""
+    data, paths = files
+    sql = _chain_sql(paths, ["rl"], "SELECT COUNT(*) FROM '{L}' AS u JOIN '{R}' AS o ON u.id = o.customer_id "
+                                     "RIGHT JOIN '{X}' AS r ON u.role = r.role")
+    with cqtest.Parsed(sql) as ast:
+        with pytest.raises(RuntimeError):
+            _run(ast, data["du"], data["do"], 3, [data["rl"]])
+        assert "RIGHT/FULL JOIN after the first level" in cq_amd.last_ineligible()
+
+
 def test_mixed_key_classes_refused(files):
     """value_compare's cross-class "equal" pairs cannot be hash-routed: the merge refuses"""
     data, paths = files
@@ -227,7 +304,7 @@ def test_route_counts(files):
         rt.close()
 
 
-def _dist_worker(rank, world, port, lpath, rpath, sql, q):
+def _dist_worker(rank, world, port, lpath, rpath, sql, q, rest=()):
     """one rank of cq_amd.dist.join_partitioned; gloo group, shared GPU 0"""
     import os
     import torch.distributed as dist
@@ -249,7 +326,10 @@ def _dist_worker(rank, world, port, lpath, rpath, sql, q):
             t = ca.Table.from_bytes(header + pc) if rank == 0 else ca.Table.from_bytes(pc, header=header)
             shards.append((t, header))
         with ct.Parsed(sql) as ast:
-            tp = join_partitioned(ast, shards[0][0], shards[1][0], shards[0][1], shards[1][1], "cuda", "cpu")
+            whole = [ca.Table.from_bytes(open(p, "rb").read()) for p in rest]
+            tp = join_partitioned(ast, shards[0][0], shards[1][0], shards[0][1], shards[1][1], "cuda", "cpu", whole)
+            for t in whole:
+                t.close()
             res = None
             if rank == 0:
                 res = ab.table_to_py(tp) if tp else ca.last_error()
@@ -281,6 +361,37 @@ def test_join_partitioned_processes(files, world):
     ctx = mp.get_context("spawn")
     q = ctx.Queue()
     procs = [ctx.Process(target=_dist_worker, args=(r, world, port, paths["du"], paths["do"], sql, q))
+             for r in range(world)]
+    for p in procs:
+        p.start()
+    res = dict(q.get(timeout=150) for _ in range(world))
+    for p in procs:
+        p.join(timeout=60)
+        assert p.exitcode == 0
+    got = res[0]
+    assert isinstance(got, dict), got
+    with cqtest.Parsed(sql) as ast:
+        tol = tolerant_columns(ast)
+    compare(got, want, tol, sql + f" @ {world} processes")
+
+
+@pytest.mark.parametrize("world", [1, 2])
+def test_join_chain_processes(files, world):
+    """a three-table chain through cq_amd.dist.join_partitioned in separate processes
+    (gloo): routed first level, whole third table, merged on rank 0 vs the oracle"""
+    import socket
+    import torch.multiprocessing as mp
+    data, paths = files
+    sql = _chain_sql(paths, ["rl"], CHAINS[0][1])
+    want, unsup = cqtest.oracle_query(sql)
+    assert not unsup
+    s = socket.socket()
+    s.bind(("127.0.0.1", 0))
+    port = s.getsockname()[1]
+    s.close()
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    procs = [ctx.Process(target=_dist_worker, args=(r, world, port, paths["du"], paths["do"], sql, q, [paths["rl"]]))
              for r in range(world)]
     for p in procs:
         p.start()
