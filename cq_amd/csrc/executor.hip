@@ -171,14 +171,17 @@ hipError_t cq_jx_build_direct(const unsigned long long* key, const unsigned long
 size_t cq_jx_direct_bytes();
 hipError_t cq_jx_star_extract(const uint8_t* g, uint64_t lo, uint64_t hi, uint32_t ws, uint32_t delim, uint32_t quote,
                               int kcol, int pcol, int build, unsigned long long kmin, unsigned long long range,
-                              uint16_t* d16, uint32_t* l32, uint8_t* m8, unsigned long long* ttab,
+                              uint16_t* d16, uint32_t* l32, unsigned long long* ttab,
                               unsigned long long* gsum, unsigned long long* counter, unsigned int* flag,
-                              unsigned long long* krange, int grid, hipStream_t s);
-hipError_t cq_jx_star_first(const uint16_t* d16, const uint32_t* l32, const uint8_t* m8, unsigned long long range,
+                              unsigned long long* krange, uint32_t* notmono, unsigned long long* wfl,
+                              uint32_t* gminix, int grid, hipStream_t s);
+hipError_t cq_jx_star_order(const unsigned long long* wfl, unsigned long long nwin, uint32_t* notmono, hipStream_t s);
+hipError_t cq_jx_star_first(const uint16_t* d16, const uint32_t* l32, unsigned long long range, const uint32_t* notmono,
                             uint32_t* gfirst, unsigned long long* nocc, int grid, hipStream_t s);
 hipError_t cq_jx_star_flush(int grouped, int value, const unsigned long long* ttab, const unsigned long long* gsum,
-                            const uint32_t* gfirst, const unsigned long long* cnts, const cq::GroupTable* rt, int nacc,
-                            cq::ScanStats* stats, unsigned int* flag, hipStream_t s);
+                            const uint32_t* gfirst, const uint32_t* gminix, const uint32_t* l32, const uint32_t* notmono,
+                            const unsigned long long* cnts, const cq::GroupTable* rt, int nacc, cq::ScanStats* stats,
+                            unsigned int* flag, hipStream_t s);
 uint32_t cq_jx_star_groups();
 hipError_t cq_jx_probe(int grouped, int value, int direct, const unsigned long long* pkey,
                        const unsigned long long* ppay, const uint32_t* poff, uint32_t n, unsigned long long kmin,
@@ -3339,33 +3342,42 @@ cq_table* run_fast_join(DevCtx& c, cq_node* q, Compiled& C, const cqgpu_table* L
             JXDBG("star round %d: keys [%llu, %llu] est %llu learned %d\n", round, (unsigned long long)kmin,
                   (unsigned long long)kmax, (unsigned long long)est, (int)learned);
             if (kmax < kmin || range >= (1ull << 31) || range > 4 * est + 1024) break;
-            const size_t b16 = (range * 2 + 15) & ~(size_t)15, b8 = (range + 15) & ~(size_t)15;
-            DevBuf big(b16 + b8), l32(range * 4);
+            const size_t b16 = (range * 2 + 15) & ~(size_t)15;
+            DevBuf big(b16), l32(range * 4 + 16);
             const uint32_t G = cq_jx_star_groups();
-            const size_t o_gsum = (size_t)G * 8, o_first = o_gsum + (size_t)G * 24, o_ctl = o_first + (size_t)G * 4;
+            // ttab | gsum | gfirst | gminix | control words; the build windows' first / last keys
+            const size_t o_gsum = (size_t)G * 8, o_first = o_gsum + (size_t)G * 24, o_minix = o_first + (size_t)G * 4,
+                         o_ctl = o_minix + (size_t)G * 4;
             DevBuf small(o_ctl + 64);
+            const uint64_t nwb = cq_jx_windows(L->data_begin, L->n, ws);
+            DevBuf wfl(std::max<uint64_t>(nwb, 1) * 16);
             uint16_t* d16 = big.as<uint16_t>();
-            uint8_t* m8 = big.as<uint8_t>() + b16;
             unsigned long long* ttab = small.as<unsigned long long>();
             unsigned long long* gsum = (unsigned long long*)(small.as<uint8_t>() + o_gsum);
             uint32_t* gfirst = (uint32_t*)(small.as<uint8_t>() + o_first);
+            uint32_t* gminix = (uint32_t*)(small.as<uint8_t>() + o_minix);
             unsigned int* sflag = (unsigned int*)(small.as<uint8_t>() + o_ctl);
             unsigned long long* cnts = (unsigned long long*)(small.as<uint8_t>() + o_ctl + 8);   // placed, pairs, occupied
             unsigned long long* skr = cnts + 3;                                                  // build keys' min, max
-            HIPCHECK(hipMemsetAsync(big.p, 0, b16 + b8, c.stream));
+            uint32_t* snotmono = (uint32_t*)(skr + 2);
+            HIPCHECK(hipMemsetAsync(big.p, 0, b16, c.stream));
             HIPCHECK(hipMemsetAsync(small.p, 0, o_ctl + 64, c.stream));
-            HIPCHECK(hipMemsetAsync(gfirst, 0xff, (size_t)G * 4, c.stream));
+            HIPCHECK(hipMemsetAsync(gfirst, 0xff, (size_t)G * 8, c.stream));          // gfirst and gminix
             HIPCHECK(hipMemsetAsync(skr, 0xff, 8, c.stream));
             HIPCHECK(hipEventRecord(c.ev0, c.stream));
             HIPCHECK(cq_jx_star_extract(L->g, L->data_begin, L->n, ws, d, dq, kl, grouped ? gcol : -1, 1, kmin, range, d16,
-                                        l32.as<uint32_t>(), m8, ttab, gsum, cnts, sflag, skr, xgrid, c.stream));
+                                        l32.as<uint32_t>(), ttab, gsum, cnts, sflag, skr, snotmono,
+                                        wfl.as<unsigned long long>(), nullptr, xgrid, c.stream));
+            HIPCHECK(cq_jx_star_order(wfl.as<unsigned long long>(), nwb, snotmono, c.stream));
             HIPCHECK(cq_jx_star_extract(R->g, R->data_begin, R->n, wsr, d, dq, kr, vcol, 0, kmin, range, d16,
-                                        l32.as<uint32_t>(), m8, ttab, gsum, cnts + 1, sflag, nullptr, xgrid, c.stream));
-            HIPCHECK(cq_jx_star_first(d16, l32.as<uint32_t>(), m8, range, gfirst, cnts + 2, c.ncu * 4, c.stream));
+                                        l32.as<uint32_t>(), ttab, gsum, cnts + 1, sflag, nullptr, snotmono, nullptr,
+                                        gminix, xgrid, c.stream));
+            HIPCHECK(cq_jx_star_first(d16, l32.as<uint32_t>(), range, snotmono, gfirst, cnts + 2, c.ncu * 4, c.stream));
             bool fb = false;
             cq_table* res = results([&](TableArena& A) {
-                HIPCHECK(cq_jx_star_flush(grouped ? 1 : 0, vcol >= 0 ? 1 : 0, ttab, gsum, gfirst, cnts,
-                                          grouped ? &A.rt : &A.gt, C.P.nacc, A.stats, sflag, c.stream));
+                HIPCHECK(cq_jx_star_flush(grouped ? 1 : 0, vcol >= 0 ? 1 : 0, ttab, gsum, gfirst, gminix,
+                                          l32.as<uint32_t>(), snotmono, cnts, grouped ? &A.rt : &A.gt, C.P.nacc,
+                                          A.stats, sflag, c.stream));
             }, sflag, 0, 4, &fb);
             if (res || !fb) {
                 if (res && !learned) {           // the exact range, for the next query on this table

@@ -86,7 +86,7 @@ struct FastPlan {
 
 // HBM tables: canonical keys (TAB_GT), raw keys (TAB_RT)
 enum : int { TAB_GT = 0, TAB_RT = 1 };
-__device__ GroupTable g_fast_tabs[2];
+// (the pair itself: a per-thread device buffer, cq_launch_fast)
 constexpr uint32_t GK_RAW = 6;       // raw field bytes as key (lean.hip's class)
 
 // ------------------------------------------------------------------ helpers
@@ -1111,12 +1111,16 @@ struct JxOut {
     // STAR passes (jx_star_*): no record arrays; the build side goes straight into
     // key-indexed arrays over [kmin, kmin + range), the probe side aggregates in place
     unsigned long long kmin, range;
-    uint16_t* d16;             // build: group id + 1 of key kmin + i (0: no build record)
+    uint16_t* d16;             // build: group id + 1 of key kmin + i (0: no build record);
+                               // probe: | 0x8000 once a probe record met it
     uint32_t* l32;             // build: that record's byte offset
-    uint8_t* m8;               // probe: 1 when key kmin + i met a probe record
     unsigned long long* ttab;  // build: GROUP BY raw tags, slot = group id (0: free)
     unsigned long long* gsum;  // probe: per group id COUNT, fixed-point SUM, SUM count
     unsigned long long* nbuilt;   // build: records placed
+    uint32_t* notmono;         // build / order check: nonzero unless the build keys rise in file order
+                               // (probe: zero -> per group the smallest matched key index, no flags)
+    unsigned long long* wfl;   // build: per window its first and last key (order check)
+    uint32_t* gminix;          // probe: per group id the smallest matched key index
 };
 // STAR flags (JxOut.flag): 8 a NULL build key, 16 a key outside [kmin, kmin + range),
 // 32 more GROUP BY tags than JX_G, 64 a repeated build key (placed != occupied)
@@ -1139,16 +1143,33 @@ __device__ __forceinline__ uint32_t jx_tag_gid(unsigned long long* __restrict__ 
     full = true;
     return 0;
 }
+// the same through a block's LDS mirror of the tag table (slots as the global table's;
+// a slot the mirror has not seen yet ends the walk there and asks the global table)
+__device__ __forceinline__ uint32_t jx_tag_gid_lds(unsigned long long* __restrict__ lt,
+                                                   unsigned long long* __restrict__ tt, unsigned long long tag,
+                                                   bool& full) {
+    uint32_t s = fast_key_hash((uint32_t)tag, (uint32_t)(tag >> 32)) & (JX_G - 1);
+    for (uint32_t q = 0; q < 8u; q++) {
+        const unsigned long long t = lt[s];
+        if (t == tag) return s;
+        if (t == 0ull) break;
+        s = (s + 1) & (JX_G - 1);
+    }
+    const uint32_t g = jx_tag_gid(tt, tag, full);
+    if (!full) lt[g] = tag;
+    return g;
+}
 
 // the canonical INTEGER key of a field (16 bytes d0..d3 from its start, len bytes):
 // digits only, no leading zero, at most 15 digits and not 8-10; NULL (empty) -> JX_NULLKEY
 __device__ __forceinline__ bool jx_key(uint32_t d0, uint32_t d1, uint32_t d2, uint32_t d3, uint32_t len,
                                        unsigned long long& key) {
     if (len == 0) { key = JX_NULLKEY; return true; }
-    const uint32_t dd[4] = {d0, d1, d2, d3};
     // (8-10 digits may type as a DATE, infer_type csv_reader.c:139: such keys take the
     // general join, whose class rules pair DATE with every number)
     bool ok = len <= 15u && (len < 8u || len > 10u) && ((d0 & 0xFFu) != '0' || len == 1u);
+#ifdef JX_OLD_KEY
+    const uint32_t dd[4] = {d0, d1, d2, d3};
     unsigned long long v = 0;
 #pragma unroll
     for (int j = 0; j < 15; j++) {
@@ -1161,20 +1182,65 @@ __device__ __forceinline__ bool jx_key(uint32_t d0, uint32_t d1, uint32_t d2, ui
     }
     key = v;
     return ok;
+#else
+    // the 16 bytes right-aligned (the digits end at byte 15, '0' fill below): a
+    // 128-bit shift left by 16 - len bytes drops the bytes past the field
+    const uint32_t sb = (16u - (len & 15u)) * 8u;          // 8 .. 120 (len 1 .. 15)
+    const unsigned long long lo = (unsigned long long)d0 | ((unsigned long long)d1 << 32);
+    const unsigned long long hi = (unsigned long long)d2 | ((unsigned long long)d3 << 32);
+    unsigned long long ylo, yhi, fill_lo, fill_hi;
+    if (sb < 64u) {
+        ylo = lo << sb;
+        yhi = (hi << sb) | (lo >> (64u - sb));
+        fill_lo = 0x3030303030303030ull & ((1ull << sb) - 1ull);
+        fill_hi = 0ull;
+    } else {
+        ylo = 0ull;
+        yhi = lo << (sb - 64u);
+        fill_lo = 0x3030303030303030ull;
+        fill_hi = 0x3030303030303030ull & ((1ull << (sb - 64u)) - 1ull);
+    }
+    const unsigned long long dl = (ylo | fill_lo) - 0x3030303030303030ull;   // byte 0: the 10^15 digit
+    const unsigned long long dh = (yhi | fill_hi) - 0x3030303030303030ull;
+    // every byte < 10 (a byte >= 10 sets bit 7 of itself or of itself + 0x76)
+    ok = ok && (((dl + 0x7676767676767676ull) | dl | (dh + 0x7676767676767676ull) | dh) & 0x8080808080808080ull) == 0;
+    // four digits per 32-bit word (most significant first): (b0 10 + b1) 100 + b2 10 + b3
+    const auto g4 = [](uint32_t w) {
+        const uint32_t p = __builtin_amdgcn_udot4(w, 0x0000010Au, 0u, false);
+        const uint32_t q = __builtin_amdgcn_udot4(w, 0x010A0000u, 0u, false);
+        return __umul24(p, 100u) + q;
+    };
+    const uint32_t h0 = __umul24(g4((uint32_t)dl), 10000u) + g4((uint32_t)(dl >> 32));
+    const uint32_t h1 = __umul24(g4((uint32_t)dh), 10000u) + g4((uint32_t)(dh >> 32));
+    key = (unsigned long long)h0 * 100000000ull + h1;
+    return ok;
+#endif
 }
 
 template <bool BUILD, bool COMMA, int NR, bool COUNT, bool STAR = false>
 __global__ __launch_bounds__(LT) void jx_extract_kernel(const uint8_t* __restrict__ g, const JxPlan jp, const JxOut jo) {
     extern __shared__ __align__(16) uint8_t smem[];
     WaveLds* waves = (WaveLds*)smem;
-    // STAR probe: per group id COUNT / fixed-point SUM / SUM count of this block
+    // STAR probe: per group id COUNT / fixed-point SUM / SUM count of this block;
+    // STAR build: the block's mirror of the GROUP BY tag table
     constexpr bool SPROBE = STAR && !BUILD;
+    constexpr bool SBUILD = STAR && BUILD && NR == 2;
     constexpr uint32_t NG = SPROBE ? JX_G : 1;
     unsigned long long* sfix = (unsigned long long*)(smem + sizeof(WaveLds) * NWV);
     uint32_t* scnt = (uint32_t*)(sfix + NG);
     uint32_t* snum = scnt + NG;
+    uint32_t* smix = snum + NG;
+    unsigned long long* stt = (unsigned long long*)(smem + sizeof(WaveLds) * NWV);
+    // (probe: with rising offsets the first pair's build record is the smallest matched
+    // key's: no match flags written into d16)
+    uint32_t mono = 0;
     if constexpr (SPROBE) {
-        for (uint32_t k = threadIdx.x; k < NG; k += LT) { sfix[k] = 0; scnt[k] = 0; snum[k] = 0; }
+        for (uint32_t k = threadIdx.x; k < NG; k += LT) { sfix[k] = 0; scnt[k] = 0; snum[k] = 0; smix[k] = ~0u; }
+        mono = __builtin_amdgcn_readfirstlane(*jo.notmono) == 0u ? 1u : 0u;
+        __syncthreads();
+    }
+    if constexpr (SBUILD) {
+        for (uint32_t k = threadIdx.x; k < JX_G; k += LT) stt[k] = 0ull;
         __syncthreads();
     }
     uint32_t sflag = 0;
@@ -1265,6 +1331,9 @@ __global__ __launch_bounds__(LT) void jx_extract_kernel(const uint8_t* __restric
         const uint32_t nmine = (uint32_t)__popcll(todo);
         uint32_t at_next = STAR ? 0u : jo.wbase[i] + wave_incl_scan(nmine) - nmine;
         bool issued = false;
+        // STAR build: this lane's first and last key (its records come in file order)
+        unsigned long long lfirst = ~0ull, llast = 0ull;
+        bool lany = false, lbad = false;
         while (__any(todo != 0)) {
             uint32_t p[2], pa[2], fst[2][2], fen[2][2], e[2];
             uint64_t sv[2];
@@ -1382,21 +1451,41 @@ __global__ __launch_bounds__(LT) void jx_extract_kernel(const uint8_t* __restric
                         if (k == JX_NULLKEY) { sflag |= 8u; continue; }
                         kmin = k < kmin ? k : kmin;
                         kmax = k > kmax ? k : kmax;
+                        lbad = lbad || (lany && k <= llast);
+                        lfirst = lany ? lfirst : k;
+                        llast = k;
+                        lany = true;
                         if (ix >= jo.range) { sflag |= 16u; continue; }
                         bool full = false;
-                        const uint32_t gid = NR == 2 ? jx_tag_gid(jo.ttab, pay[u], full) : 0u;
+                        uint32_t gid = 0;
+                        if constexpr (SBUILD) gid = jx_tag_gid_lds(stt, jo.ttab, pay[u], full);
                         if (full) sflag |= 32u;
+#ifndef JX_AB_NOSTORE
                         jo.d16[ix] = (uint16_t)(gid + 1u);
                         jo.l32[ix] = (uint32_t)(wbase + p[u]);
                         nstar++;
+#else
+                        sflag |= gid == 12345u ? 1u : 0u;
+#endif
                     } else if (k != JX_NULLKEY && ix < jo.range) {
-                        const uint32_t gp = jo.d16[ix];
-                        if (gp) {
-                            jo.m8[ix] = 1;
-                            atomicAdd(&scnt[gp - 1u], 1u);
+#ifndef JX_AB_NOLOOK
+                        const uint32_t gv = jo.d16[ix];
+#else
+                        const uint32_t gv = 1u + (uint32_t)(ix & 1023u);
+#endif
+                        if (gv) {
+                            const uint32_t gi = (gv & 0x7FFFu) - 1u;
+#if !defined(JX_AB_NOLOOK) && !defined(JX_AB_NOFLAG)
+                            if (mono) {
+                                if ((uint32_t)ix < smix[gi]) atomicMin(&smix[gi], (uint32_t)ix);
+                            } else if (!(gv & 0x8000u)) {
+                                jo.d16[ix] = (uint16_t)(gv | 0x8000u);   // (every writer: the same value)
+                            }
+#endif
+                            atomicAdd(&scnt[gi], 1u);
                             if (NR == 2 && pay[u] != JX_NOVAL) {
-                                atomicAdd(&sfix[gp - 1u], pay[u]);
-                                atomicAdd(&snum[gp - 1u], 1u);
+                                atomicAdd(&sfix[gi], pay[u]);
+                                atomicAdd(&snum[gi], 1u);
                             }
                             nstar++;
                         }
@@ -1425,6 +1514,21 @@ __global__ __launch_bounds__(LT) void jx_extract_kernel(const uint8_t* __restric
             asm volatile("" : "+s"(ni));
             load_win(g, first_win + ni, wsb, wlds, voff, prev_next);
         }
+        if constexpr (STAR && BUILD) {
+            // keys rising across the lanes too; the window's first and last for the
+            // order check between windows (an empty window: not checked, not rising)
+            const uint64_t am = __ballot(lany);
+            const uint64_t above = lane < 63 ? am >> (lane + 1) : 0ull;
+            const unsigned long long nfirst = __shfl(lfirst, above ? (int)(lane + 1 + __builtin_ctzll(above)) : lane, 64);
+            lbad = lbad || (lany && above && llast >= nfirst);
+            const unsigned long long wf = __shfl(lfirst, am ? __builtin_ctzll(am) : 0, 64);
+            const unsigned long long wl = __shfl(llast, am ? 63 - __builtin_clzll(am) : 0, 64);
+            if (lane == 0) {
+                jo.wfl[2 * (uint64_t)i] = am ? wf : ~0ull;
+                jo.wfl[2 * (uint64_t)i + 1] = am ? wl : 0ull;
+            }
+            if ((__any(lbad) || !am) && lane == 0) atomicOr(jo.notmono, 1u);
+        }
     }
     if (COUNT) return;
     if (__any(bad) && lane == 0) atomicOr(jo.flag, 1u);
@@ -1440,6 +1544,7 @@ __global__ __launch_bounds__(LT) void jx_extract_kernel(const uint8_t* __restric
         __syncthreads();
         for (uint32_t k = threadIdx.x; k < NG; k += LT) {
             if (!scnt[k]) continue;
+            if (mono) atomicMin(&jo.gminix[k], smix[k]);
             atomicAdd(&jo.gsum[3 * k], (unsigned long long)scnt[k]);
             if (snum[k]) {
                 atomicAdd(&jo.gsum[3 * k + 1], sfix[k]);
@@ -1459,37 +1564,54 @@ __global__ __launch_bounds__(LT) void jx_extract_kernel(const uint8_t* __restric
     }
 }
 
-// STAR: each group's first pair in (l, r) order has the group's smallest matched build
-// record l (its records' keys are distinct); its byte offset per group id.  Also counts
-// the occupied keys: fewer than the records placed means a repeated build key.
+// STAR, after the build: the windows' keys in file order (first of window i + 1 above
+// the last of window i); a fall sets *notmono (then the probe flags the matched keys)
+__global__ void jx_star_order_kernel(const unsigned long long* __restrict__ wfl, uint64_t nwin,
+                                     uint32_t* __restrict__ notmono) {
+    bool bad = false;
+    for (uint64_t w = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x; w + 1 < nwin;
+         w += (uint64_t)gridDim.x * blockDim.x)
+        bad = bad || wfl[2 * w + 1] >= wfl[2 * (w + 1)];
+    if (__any(bad) && (threadIdx.x & 63) == 0) atomicOr(notmono, 1u);
+}
+
+// STAR without rising build keys: each group's first pair in (l, r) order has the
+// group's smallest matched build record l (the probe flagged the matched keys in d16).
+// Also counts the occupied keys: fewer than the records placed means a repeated key.
 __global__ __launch_bounds__(1024) void jx_star_first_kernel(const uint16_t* __restrict__ d16,
-                                                             const uint32_t* __restrict__ l32,
-                                                             const uint8_t* __restrict__ m8, uint64_t range,
+                                                             const uint32_t* __restrict__ l32, uint64_t range,
+                                                             const uint32_t* __restrict__ notmono,
                                                              uint32_t* __restrict__ gfirst,
                                                              unsigned long long* __restrict__ nocc) {
+    if (!*notmono) return;
     __shared__ uint32_t sf[JX_G];
     for (uint32_t k = threadIdx.x; k < JX_G; k += blockDim.x) sf[k] = ~0u;
     __syncthreads();
     unsigned long long occ = 0;
+    const auto take = [&](uint32_t gv, uint32_t l) {
+        occ += gv != 0u;
+        if (gv & 0x8000u) {
+            const uint32_t gi = (gv & 0x7FFFu) - 1u;
+            if (l < sf[gi]) atomicMin(&sf[gi], l);        // (an atomic only when it lowers)
+        }
+    };
     const uint64_t n8 = range / 8;
     for (uint64_t w = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x; w < n8; w += (uint64_t)gridDim.x * blockDim.x) {
         const uint4 dv = ((const uint4*)d16)[w];             // 8 group ids
-        const uint2 mv = ((const uint2*)m8)[w];              // 8 match bytes
         const uint32_t dw[4] = {dv.x, dv.y, dv.z, dv.w};
+        if (((dv.x | dv.y | dv.z | dv.w) & 0x80008000u) == 0u) {   // nothing matched here
 #pragma unroll
-        for (int j = 0; j < 8; j++) {
-            const uint32_t gp = (dw[j >> 1] >> (16 * (j & 1))) & 0xFFFFu;
-            const uint32_t mb = ((j < 4 ? mv.x : mv.y) >> (8 * (j & 3))) & 0xFFu;
-            occ += gp != 0u;
-            if (gp && mb) atomicMin(&sf[gp - 1u], l32[w * 8 + j]);
+            for (int j = 0; j < 4; j++) occ += ((dw[j] & 0xFFFFu) != 0u) + ((dw[j] >> 16) != 0u);
+            continue;
         }
+        const uint4 la = ((const uint4*)l32)[2 * w], lb = ((const uint4*)l32)[2 * w + 1];
+        const uint32_t lv[8] = {la.x, la.y, la.z, la.w, lb.x, lb.y, lb.z, lb.w};
+#pragma unroll
+        for (int j = 0; j < 8; j++) take((dw[j >> 1] >> (16 * (j & 1))) & 0xFFFFu, lv[j]);
     }
     for (uint64_t ix = n8 * 8 + (uint64_t)blockIdx.x * blockDim.x + threadIdx.x; ix < range;
-         ix += (uint64_t)gridDim.x * blockDim.x) {
-        const uint32_t gp = d16[ix];
-        occ += gp != 0u;
-        if (gp && m8[ix]) atomicMin(&sf[gp - 1u], l32[ix]);
-    }
+         ix += (uint64_t)gridDim.x * blockDim.x)
+        take(d16[ix], l32[ix]);
     for (int o = 32; o > 0; o >>= 1) occ += __shfl_down(occ, o, 64);
     if ((threadIdx.x & 63) == 0 && occ) atomicAdd(nocc, occ);
     __syncthreads();
@@ -1504,11 +1626,16 @@ template <bool GROUPED, bool VALUE>
 __global__ __launch_bounds__(1024) void jx_star_flush_kernel(const unsigned long long* __restrict__ ttab,
                                                              const unsigned long long* __restrict__ gsum,
                                                              const uint32_t* __restrict__ gfirst,
+                                                             const uint32_t* __restrict__ gminix,
+                                                             const uint32_t* __restrict__ l32,
+                                                             const uint32_t* __restrict__ notmono,
                                                              const unsigned long long* __restrict__ cnts,
                                                              GroupTable rt, int nacc, ScanStats* __restrict__ stats,
                                                              unsigned int* __restrict__ flag) {
-    // cnts: [0] build records placed, [1] pairs, [2] occupied keys
-    if (cnts[0] != cnts[2]) {
+    // cnts: [0] build records placed, [1] pairs, [2] occupied keys (counted when the
+    // build keys do not rise in file order; rising keys are distinct)
+    const bool mono = *notmono == 0u;
+    if (!mono && cnts[0] != cnts[2]) {
         if (threadIdx.x == 0) atomicOr(flag, 64u);
         return;
     }
@@ -1527,7 +1654,8 @@ __global__ __launch_bounds__(1024) void jx_star_flush_kernel(const unsigned long
         const int gi = g_insert(rt, kk, GROUPED ? gk_hash(kk) : 0x12345678ULL, stats);
         if (gi < 0) continue;
         atomicAdd(&rt.cnt[gi], cnt);
-        atomicMin(&rt.first[gi], (unsigned long long)gfirst[s] << 32);
+        const uint32_t first = mono ? l32[gminix[s]] : gfirst[s];
+        atomicMin(&rt.first[gi], (unsigned long long)first << 32);
         if (VALUE && gsum[3 * s + 2]) {
             for (int a = 0; a < nacc; a++) {
                 atomicAdd(&rt.sum[a][gi], (double)(long long)gsum[3 * s + 1] / 1000.0);
@@ -1923,14 +2051,16 @@ hipError_t cq_launch_fast(const uint8_t* g, const cq::ScanPlan* P, const cq::Gro
         fp.hi_s = (uint32_t)(hi - wh * fp.ws);
     }
     fp.seed = grouped ? (const unsigned long long*)(uintptr_t)P->fast_seed : nullptr;
-    static GroupTable* tabs_dev[64];
+    // the launch's table pair in device memory of this thread and device (one pair
+    // per thread: concurrent callers never share it)
+    thread_local GroupTable* tabs_dev[64] = {};
     int dev = 0;
     (void)hipGetDevice(&dev);
     if (!tabs_dev[dev & 63]) {
-        hipError_t e = hipGetSymbolAddress((void**)&tabs_dev[dev & 63], HIP_SYMBOL(fast::g_fast_tabs));
+        hipError_t e = hipMalloc((void**)&tabs_dev[dev & 63], 2 * sizeof(GroupTable));
         if (e != hipSuccess) return e;
     }
-    static GroupTable tabs[2];
+    GroupTable tabs[2];
     tabs[0] = *gt;
     if (rt) tabs[1] = *rt;
     else memset(&tabs[1], 0, sizeof tabs[1]);
@@ -1992,9 +2122,10 @@ hipError_t cq_jx_extract(const uint8_t* g, uint64_t lo, uint64_t hi, uint32_t ws
 // counter: build records placed (build) / pairs (probe).
 hipError_t cq_jx_star_extract(const uint8_t* g, uint64_t lo, uint64_t hi, uint32_t ws, uint32_t delim, uint32_t quote,
                               int kcol, int pcol, int build, unsigned long long kmin, unsigned long long range,
-                              uint16_t* d16, uint32_t* l32, uint8_t* m8, unsigned long long* ttab,
+                              uint16_t* d16, uint32_t* l32, unsigned long long* ttab,
                               unsigned long long* gsum, unsigned long long* counter, unsigned int* flag,
-                              unsigned long long* krange, int grid, hipStream_t s) {
+                              unsigned long long* krange, uint32_t* notmono, unsigned long long* wfl,
+                              uint32_t* gminix, int grid, hipStream_t s) {
     using namespace cq::fast;
     JxPlan jp;
     if (!jx_plan(g, lo, hi, ws, delim, quote, kcol, pcol, &jp)) return hipErrorInvalidValue;
@@ -2015,33 +2146,43 @@ hipError_t cq_jx_star_extract(const uint8_t* g, uint64_t lo, uint64_t hi, uint32
     jo.range = range;
     jo.d16 = d16;
     jo.l32 = l32;
-    jo.m8 = m8;
     jo.ttab = ttab;
     jo.gsum = gsum;
     jo.nbuilt = counter;
-    const size_t lds = sizeof(WaveLds) * NWV + (build ? 0 : (size_t)JX_G * 16);
+    jo.notmono = notmono;
+    jo.wfl = wfl;
+    jo.gminix = gminix;
+    const size_t lds = sizeof(WaveLds) * NWV + (build ? (nr == 2 ? (size_t)JX_G * 8 : 0) : (size_t)JX_G * 20);
     cq::set_max_lds((const void*)fn, (int)lds);
     if (jp.nwin == 0) return hipSuccess;
     hipLaunchKernelGGL(fn, dim3(grid), dim3(LT), lds, s, g, jp, jo);
     return hipGetLastError();
 }
-hipError_t cq_jx_star_first(const uint16_t* d16, const uint32_t* l32, const uint8_t* m8, unsigned long long range,
+hipError_t cq_jx_star_order(const unsigned long long* wfl, unsigned long long nwin, uint32_t* notmono, hipStream_t s) {
+    if (nwin < 2) return hipSuccess;
+    hipLaunchKernelGGL(cq::fast::jx_star_order_kernel, dim3((unsigned)std::min<unsigned long long>((nwin + 255) / 256, 1024)),
+                       dim3(256), 0, s, wfl, (uint64_t)nwin, notmono);
+    return hipGetLastError();
+}
+hipError_t cq_jx_star_first(const uint16_t* d16, const uint32_t* l32, unsigned long long range, const uint32_t* notmono,
                             uint32_t* gfirst, unsigned long long* nocc, int grid, hipStream_t s) {
-    if (((uintptr_t)d16 & 15) || ((uintptr_t)m8 & 7)) return hipErrorInvalidValue;
-    hipLaunchKernelGGL(cq::fast::jx_star_first_kernel, dim3(grid), dim3(1024), 0, s, d16, l32, m8, (uint64_t)range,
+    if (((uintptr_t)d16 & 15) || ((uintptr_t)l32 & 15)) return hipErrorInvalidValue;
+    hipLaunchKernelGGL(cq::fast::jx_star_first_kernel, dim3(grid), dim3(1024), 0, s, d16, l32, (uint64_t)range, notmono,
                        gfirst, nocc);
     return hipGetLastError();
 }
 hipError_t cq_jx_star_flush(int grouped, int value, const unsigned long long* ttab, const unsigned long long* gsum,
-                            const uint32_t* gfirst, const unsigned long long* cnts, const cq::GroupTable* rt, int nacc,
-                            cq::ScanStats* stats, unsigned int* flag, hipStream_t s) {
+                            const uint32_t* gfirst, const uint32_t* gminix, const uint32_t* l32, const uint32_t* notmono,
+                            const unsigned long long* cnts, const cq::GroupTable* rt, int nacc, cq::ScanStats* stats,
+                            unsigned int* flag, hipStream_t s) {
     using namespace cq::fast;
-    typedef void (*ffn_t)(const unsigned long long*, const unsigned long long*, const uint32_t*,
-                          const unsigned long long*, GroupTable, int, ScanStats*, unsigned int*);
+    typedef void (*ffn_t)(const unsigned long long*, const unsigned long long*, const uint32_t*, const uint32_t*,
+                          const uint32_t*, const uint32_t*, const unsigned long long*, GroupTable, int, ScanStats*,
+                          unsigned int*);
     static const ffn_t tab[2][2] = {{jx_star_flush_kernel<false, false>, jx_star_flush_kernel<false, true>},
                                     {jx_star_flush_kernel<true, false>, jx_star_flush_kernel<true, true>}};
-    hipLaunchKernelGGL(tab[grouped ? 1 : 0][value ? 1 : 0], dim3(1), dim3(1024), 0, s, ttab, gsum, gfirst, cnts, *rt,
-                       nacc, stats, flag);
+    hipLaunchKernelGGL(tab[grouped ? 1 : 0][value ? 1 : 0], dim3(1), dim3(1024), 0, s, ttab, gsum, gfirst, gminix, l32,
+                       notmono, cnts, *rt, nacc, stats, flag);
     return hipGetLastError();
 }
 uint32_t cq_jx_star_groups() { return cq::fast::JX_G; }

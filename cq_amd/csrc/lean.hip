@@ -148,7 +148,7 @@ struct LeanArgs {
     LeanPlan lp;
 };
 enum : int { TAB_GT = 0, TAB_RT = 1 };
-__device__ GroupTable g_lean_tabs[2];
+// (the pair itself: a per-thread device buffer, cq_launch_lean)
 
 constexpr uint32_t GK_RAW = 6;       // raw field bytes as key (cell.h GK_* never produce 6)
 __device__ __forceinline__ GKey raw_key(uint32_t len, uint64_t w0, uint64_t w1) {
@@ -1567,12 +1567,16 @@ hipError_t cq_launch_lean(const uint8_t* g, const cq::ScanPlan* P, const cq::Gro
     lean::LeanArgs args;
     memset(&args, 0, sizeof args);
     args.lp = lp;
-    static GroupTable* tabs_dev = nullptr;
+    // the launch's table pair in device memory of this thread and device (as fast.hip)
+    thread_local GroupTable* tabs_devs[64] = {};
+    int dev = 0;
+    (void)hipGetDevice(&dev);
+    GroupTable*& tabs_dev = tabs_devs[dev & 63];
     if (!tabs_dev) {
-        hipError_t e = hipGetSymbolAddress((void**)&tabs_dev, HIP_SYMBOL(lean::g_lean_tabs));
+        hipError_t e = hipMalloc((void**)&tabs_dev, 2 * sizeof(GroupTable));
         if (e != hipSuccess) return e;
     }
-    static GroupTable tabs[2];
+    GroupTable tabs[2];
     tabs[0] = *gt;
     if (rt) tabs[1] = *rt;
     else memset(&tabs[1], 0, sizeof tabs[1]);
