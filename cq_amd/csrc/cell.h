@@ -363,7 +363,12 @@ CQ_HD uint64_t date_bits(int y, int m, int d) {
 // strtoll/strtod do in the reference; the buffer is '\n'-padded past its end.
 CQ_HD Cell parse_cell(const uint8_t* f, uint32_t len) {
     if (len == 0) return cell_null();
-    if (len >= 8 && len <= 10) {
+    // every date format starts with sscanf's %d: [space*][+-]digit (a field that
+    // cannot is not copied into the NUL-terminated scratch buffer at all)
+    uint32_t d0 = 0;
+    while (d0 < len && is_space(f[d0])) d0++;
+    if (d0 < len && (f[d0] == '+' || f[d0] == '-')) d0++;
+    if (len >= 8 && len <= 10 && d0 < len && is_digit(f[d0])) {
         char b[11];
         uint32_t n = 0;
         for (uint32_t i = 0; i < len; i++) { b[i] = (char)f[i]; if (!f[i]) break; n = i + 1; }

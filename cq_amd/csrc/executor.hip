@@ -26,6 +26,7 @@
 #include <vector>
 
 #include <fcntl.h>
+#include <malloc.h>
 #include <strings.h>
 #include <sys/mman.h>
 #include <sys/stat.h>
@@ -49,8 +50,12 @@ hipError_t cq_launch_scan(const uint8_t* g, const ScanPlan* P, const GroupTable*
                           ScanStats* stats, unsigned long long* row_out, unsigned long long row_cap, int grouped,
                           int grid, hipStream_t s, Cell* cells_out, unsigned long long* slow_list,
                           unsigned long long slow_cap);
+hipError_t cq_launch_finish_pack(const uint8_t* g, uint64_t n, const GroupOut* out, const unsigned long long* ofirst,
+                                 const unsigned int* count, unsigned int cap_out, const FinishDesc* D, uint8_t* dst,
+                                 const ScanStats* stats, uint8_t* hdr, hipStream_t s);
+unsigned int cq_finish_pack_max();
 hipError_t cq_launch_compact(const GroupTable* gt, const ScanPlan* P, GroupOut* out, unsigned int* count,
-                             unsigned int cap_out, hipStream_t s);
+                             unsigned int cap_out, hipStream_t s, unsigned long long* ofirst);
 hipError_t cq_launch_gather(const uint8_t* g, const ScanPlan* P, const unsigned long long* recs,
                             uint32_t nrec, Cell* out, hipStream_t s);
 hipError_t cq_launch_copy_strings(const Cell* cells, uint32_t n, const unsigned long long* offs,
@@ -1758,7 +1763,7 @@ std::vector<HGroup> run_aggregate(DevCtx& c, const cqgpu_table* t, Compiled& C, 
         constexpr size_t MAIL_HDR = 1024;
         static_assert(sizeof(ScanStats) + 4 <= MAIL_HDR, "mailbox header");
         uint8_t* mail = mailbox(c, MAIL_HDR + cq_pack_result_bytes(cap_out, C.P.nacc, ncell, SB) + 64);
-        Scratch pk;                               // the packed result in HBM (until the sync below)
+        Scratch pk, ofs;                          // the packed result in HBM (until the sync below)
         bool is_packed = false;
         memset(&st, 0, sizeof st);
         unsigned long long last_clk[8] = {0, 0, 0, 0, 0, 0, 0, 0};
@@ -1778,8 +1783,21 @@ std::vector<HGroup> run_aggregate(DevCtx& c, const cqgpu_table* t, Compiled& C, 
                                     row_cap > done ? row_cap - done : 0, grouped, g2, c.stream, nullptr,
                                     A.slow_list, A.slow_cap));
             HIPCHECK(hipEventRecord(c.ev1, c.stream));
-            if (!chunk) {      // one launch: compact and finish speculatively, one sync for all
-                HIPCHECK(cq_launch_compact(&A.gt, &C.P, A.out, A.out_count, cap_out, c.stream));
+            // finish + pack in one launch (finish_pack_kernel) for the mailbox path
+            const bool fp = !chunk && !gm && cap_out <= cq_finish_pack_max() && !getenv("CQGPU_PACK_MAPPED") &&
+                            !getenv("CQGPU_NO_FINISH_PACK");
+            if (fp) {
+                ofs.get(c, (size_t)cap_out * 8 + 64);
+                pk.get(c, cq_pack_result_bytes(cap_out, C.P.nacc, ncell, SB) + 64);
+                HIPCHECK(cq_launch_compact(&A.gt, &C.P, A.out, A.out_count, cap_out, c.stream,
+                                           (unsigned long long*)ofs.p));
+                HIPCHECK(cq_launch_finish_pack(t->g, t->n, A.out, (const unsigned long long*)ofs.p, A.out_count,
+                                               cap_out, &FD, pk.p, A.stats, mail, c.stream));
+                HIPCHECK(cq_launch_mail_copy(pk.p, A.out_count, cap_out, C.P.nacc, ncell, SB, mail + MAIL_HDR, c.stream));
+                finished = true;
+                is_packed = true;
+            } else if (!chunk) {      // one launch: compact and finish speculatively, one sync for all
+                HIPCHECK(cq_launch_compact(&A.gt, &C.P, A.out, A.out_count, cap_out, c.stream, nullptr));
                 HIPCHECK(cq_launch_finish(t->g, t->n, A.out, A.out_count, cap_out, &FD, dcells, dbytes, c.stream));
                 if (gm) {                            // the rank's records for the root (header: mailbox)
                     HIPCHECK(cq_launch_gm_pack(A.out, A.out_count, cap_out, C.P.nacc, (uint32_t)FD.ncols, dcells,
@@ -1846,7 +1864,7 @@ std::vector<HGroup> run_aggregate(DevCtx& c, const cqgpu_table* t, Compiled& C, 
             continue;
         }
         if (!finished) {
-            HIPCHECK(cq_launch_compact(&A.gt, &C.P, A.out, A.out_count, cap_out, c.stream));
+            HIPCHECK(cq_launch_compact(&A.gt, &C.P, A.out, A.out_count, cap_out, c.stream, nullptr));
             HIPCHECK(cq_launch_finish(t->g, t->n, A.out, A.out_count, cap_out, &FD, dcells, dbytes, c.stream));
             if (gm)
                 HIPCHECK(cq_launch_gm_pack(A.out, A.out_count, cap_out, C.P.nacc, (uint32_t)FD.ncols, dcells, dbytes,
@@ -2912,7 +2930,7 @@ std::vector<HGroup> aggregate_pairs(DevCtx& c, Compiled& C, const JoinMap& MA, c
             HIPCHECK(hipMemsetAsync(vbad.p, 0, 4, c.stream));
             HIPCHECK(cq_launch_comp_verify(pairs, np, &MA, Lc, Rc, &C.P, &Ar.gt, vbad.as<unsigned int>(), c.stream));
         }
-        HIPCHECK(cq_launch_compact(&Ar.gt, &C.P, Ar.out, Ar.out_count, cap_out, c.stream));
+        HIPCHECK(cq_launch_compact(&Ar.gt, &C.P, Ar.out, Ar.out_count, cap_out, c.stream, nullptr));
         HIPCHECK(cq_launch_join_finish(Ar.out, Ar.out_count, cap_out, pairs, &MR, Lc, Rc, C.P.nacc, SB, dcells, dbytes,
                                        c.stream));
         unsigned int ng = 0, bad = 0;
@@ -3250,12 +3268,24 @@ cq_table* run_fast_join(DevCtx& c, cq_node* q, Compiled& C, const cqgpu_table* L
             fill(A);
             if (grouped) HIPCHECK(cq_launch_raw_merge(&A.gt, &A.rt, C.P.nacc, A.stats, c.stream));
             HIPCHECK(hipEventRecord(c.ev1, c.stream));
-            HIPCHECK(cq_launch_compact(&A.gt, &C.P, A.out, A.out_count, cap_out, c.stream));
-            HIPCHECK(cq_launch_finish(L->g, L->n, A.out, A.out_count, cap_out, &FD, dcells, dbytes, c.stream));
             constexpr size_t MAIL_HDR = 1024;
             uint8_t* mail = mailbox(c, MAIL_HDR + cq_pack_result_bytes(cap_out, C.P.nacc, ncell, SB) + 64);
-            HIPCHECK(cq_launch_pack_result(A.out, A.out_count, cap_out, C.P.nacc, dcells, dbytes, ncell, SB,
-                                           mail + MAIL_HDR, A.stats, mail, 1, c.stream));
+            Scratch pk, ofs;
+            if (cap_out <= cq_finish_pack_max()) {      // finish + pack in one launch, then the mailbox copy
+                ofs.get(c, (size_t)cap_out * 8 + 64);
+                pk.get(c, cq_pack_result_bytes(cap_out, C.P.nacc, ncell, SB) + 64);
+                HIPCHECK(cq_launch_compact(&A.gt, &C.P, A.out, A.out_count, cap_out, c.stream,
+                                           (unsigned long long*)ofs.p));
+                HIPCHECK(cq_launch_finish_pack(L->g, L->n, A.out, (const unsigned long long*)ofs.p, A.out_count,
+                                               cap_out, &FD, pk.p, A.stats, mail, c.stream));
+                HIPCHECK(cq_launch_mail_copy(pk.p, A.out_count, cap_out, C.P.nacc, ncell, SB, mail + MAIL_HDR,
+                                             c.stream));
+            } else {
+                HIPCHECK(cq_launch_compact(&A.gt, &C.P, A.out, A.out_count, cap_out, c.stream, nullptr));
+                HIPCHECK(cq_launch_finish(L->g, L->n, A.out, A.out_count, cap_out, &FD, dcells, dbytes, c.stream));
+                HIPCHECK(cq_launch_pack_result(A.out, A.out_count, cap_out, C.P.nacc, dcells, dbytes, ncell, SB,
+                                               mail + MAIL_HDR, A.stats, mail, 1, c.stream));
+            }
             unsigned int fl = 0;
             HIPCHECK(hipMemcpyAsync(&fl, dflag, 4, hipMemcpyDeviceToHost, c.stream));
             HIPCHECK(hipStreamSynchronize(c.stream));
@@ -4437,7 +4467,24 @@ int cqgpu_table_ncols(const cqgpu_table* t) { return t ? (int)t->names.size() : 
 
 void cqgpu_result_free(cq_table* r) {
     if (!r) return;
-    for (int i = 0; i < r->nrows; i++) free_row(r->rows[i]);
+    // rows and short strings back into this thread's pool (build_direct takes them
+    // again: no free / malloc per group and step); the rest to free()
+    RowPool& P = g_rowpool;
+    for (int i = 0; i < r->nrows; i++) {
+        cq_row& row = r->rows[i];
+        if (g_rowpool_off || row.ncols != P.ncols || P.vals.size() >= (1u << 16)) {
+            free_row(row);
+            continue;
+        }
+        for (int j = 0; j < row.ncols; j++) {
+            if (row.values[j].kind != CQ_V_STRING) continue;
+            char* sp = row.values[j].u.s;
+            if (sp && P.strs.size() < (1u << 17) && malloc_usable_size(sp) >= POOL_STR) P.strs.push_back(sp);
+            else free(sp);
+        }
+        memset(row.values, 0, sizeof(cq_value) * (size_t)std::max(row.ncols, 1));
+        P.vals.push_back(row.values);
+    }
     free(r->rows);
     for (int i = 0; i < r->ncols; i++) free(r->columns[i].name);
     free(r->columns);

@@ -397,13 +397,28 @@ __device__ __forceinline__ uint32_t class_bit(const Cell& c) {
 __device__ void g_ext_update(bool need, const GroupTable& gt, int a, uint8_t kind, uint32_t i,
                              const Cell c, uint64_t pos, ScanStats* st) {
     if (pos == NOPOS) need = false;
+    // the lock word is a sequence number (even free, odd held, +2 per update): a
+    // candidate that loses against a consistent snapshot drops out without the lock
+    // (the extreme only improves), so a hot group serialises only its improvements
+    uint32_t* lk = &gt.lock[a][i];
+    Cell* ec = &gt.ext[a][i];
+    if (need) {
+        const uint32_t v1 = __hip_atomic_load(lk, __ATOMIC_ACQUIRE, __HIP_MEMORY_SCOPE_AGENT);
+        Cell cur;
+        cur.kind = __hip_atomic_load(&ec->kind, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        cur.len = __hip_atomic_load(&ec->len, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        cur.bits = __hip_atomic_load(&ec->bits, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        const uint64_t cp = __hip_atomic_load(&gt.extpos[a][i], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");
+        const uint32_t v2 = __hip_atomic_load(lk, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        if (!(v1 & 1u) && v1 == v2 && !ext_better(kind, c, pos, cur, cp)) need = false;
+    }
     uint32_t trips = 0;
     while (__any(need)) {
         if (need) {
-            uint32_t* lk = &gt.lock[a][i];
-            if (atomicCAS(lk, 0u, 1u) == 0u) {
+            const uint32_t v = __hip_atomic_load(lk, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+            if (!(v & 1u) && atomicCAS(lk, v, v + 1u) == v) {
                 __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");
-                Cell* ec = &gt.ext[a][i];
                 Cell cur;
                 cur.kind = __hip_atomic_load(&ec->kind, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
                 cur.len = __hip_atomic_load(&ec->len, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
@@ -416,7 +431,7 @@ __device__ void g_ext_update(bool need, const GroupTable& gt, int a, uint8_t kin
                     __hip_atomic_store(&gt.extpos[a][i], (unsigned long long)pos, __ATOMIC_RELAXED,
                                        __HIP_MEMORY_SCOPE_AGENT);
                 }
-                __hip_atomic_store(lk, 0u, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_AGENT);
+                __hip_atomic_store(lk, v + 2u, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_AGENT);
                 need = false;
             }
         }
@@ -463,7 +478,7 @@ struct LdsAcc {         // ACC_SUM
 };
 struct ExtLds {         // ACC_MIN / ACC_MAX
     Cell* c;
-    unsigned long long* pos;
+    uint32_t* pos;      // the extreme's row as LdsTable.first codes it (~0u: none)
     uint32_t* lock;
 };
 
@@ -472,8 +487,10 @@ struct ExtLds {         // ACC_MIN / ACC_MAX
 __device__ __forceinline__ int l_insert(const LdsTable& t, const GKey& k, uint64_t h) {
     const uint32_t hd = lds_hdr(k, h);
     const v4u kk = key_words(k);
-    for (uint32_t probe = 0; probe < 32; probe++) {
-        const uint32_t i = (uint32_t)(h + probe) & (t.H - 1);
+    // H need not be a power of two (the host fits as many slots as LDS holds): the
+    // window starts at the hash's low 24 bits (gk_hash's best mixed) scaled into [0, H)
+    uint32_t i = __umulhi((uint32_t)h << 8, t.H);
+    for (uint32_t probe = 0; probe < 32; probe++, i = i + 1 == t.H ? 0u : i + 1) {
         uint32_t cur = __hip_atomic_load(&t.hdr[i], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
         if (cur == hd && key_match(k, kk, t.key[i])) return (int)i;   // the common case: one round trip
         if (cur == 0) {
@@ -497,18 +514,42 @@ __device__ __forceinline__ int l_insert(const LdsTable& t, const GKey& k, uint64
     return -1;
 }
 
-// wave-uniform LDS MIN/MAX update (see g_ext_update)
+// wave-uniform LDS MIN/MAX update (see g_ext_update).  The slot's lock word is a
+// sequence number: even = free, odd = held, +2 per update.  A candidate first
+// compares against a consistent snapshot (the same even number read before and
+// after the cell) and drops out without the lock when it cannot win -- the extreme
+// only ever improves, so most candidates lose against any snapshot, and only the
+// few that improve it serialise.  The fences order LDS only: a workgroup fence
+// over every address space would also wait for the window prefetch in flight.
+__device__ __forceinline__ uint64_t lds_pos(uint32_t code) { return code == 0xFFFFFFFFu ? NOPOS : code; }
 __device__ __forceinline__ void lds_ext_update(bool need, const ExtLds& e, uint32_t s, uint8_t kind,
-                                               const Cell c, uint64_t pos) {
+                                               const Cell c, uint32_t pos) {
+#ifdef CQ_AB_EXT_SKIP   // A/B build: no MIN/MAX update at all (results wrong)
+    return;
+#endif
+    uint32_t* lk = &e.lock[s];
+#ifndef CQ_AB_EXT_NOSNAP
+    if (need) {
+        const uint32_t v1 = __hip_atomic_load(lk, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
+        __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "workgroup", "local");
+        const Cell cur = e.c[s];
+        const uint64_t cp = lds_pos(e.pos[s]);
+        __builtin_amdgcn_fence(__ATOMIC_ACQ_REL, "workgroup", "local");
+        const uint32_t v2 = __hip_atomic_load(lk, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
+        if (!(v1 & 1u) && v1 == v2 && !ext_better(kind, c, pos, cur, cp)) need = false;
+    }
+#endif
     while (__any(need)) {
         if (need) {
-            if (atomicCAS(&e.lock[s], 0u, 1u) == 0u) {
-                __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "workgroup");
-                if (ext_better(kind, c, pos, e.c[s], e.pos[s])) {
+            const uint32_t v = __hip_atomic_load(lk, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
+            if (!(v & 1u) && atomicCAS(lk, v, v + 1u) == v) {
+                __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "workgroup", "local");
+                if (ext_better(kind, c, pos, e.c[s], lds_pos(e.pos[s]))) {
                     e.c[s] = c;
                     e.pos[s] = pos;
                 }
-                __hip_atomic_store(&e.lock[s], 0u, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_WORKGROUP);
+                __builtin_amdgcn_fence(__ATOMIC_RELEASE, "workgroup", "local");
+                __hip_atomic_store(lk, v + 2u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
                 need = false;
             }
         }
@@ -626,7 +667,7 @@ __global__ __launch_bounds__(SCAN_T) void scan_kernel(const uint8_t* __restrict_
             la[a].miss = (uint32_t*)carve(q, H * 4);
         } else {
             le[a].c = (Cell*)carve(q, H * sizeof(Cell));
-            le[a].pos = (unsigned long long*)carve(q, H * 8);
+            le[a].pos = (uint32_t*)carve(q, H * 4);
             le[a].lock = (uint32_t*)carve(q, H * 4);
         }
     }
@@ -639,7 +680,7 @@ __global__ __launch_bounds__(SCAN_T) void scan_kernel(const uint8_t* __restrict_
             for (int a = 0; a < KA; a++) {
                 if (a >= P.nacc) break;
                 if (la[a].sum) { la[a].sum[i] = 0.0; la[a].miss[i] = 0; }
-                if (EXT && le[a].c) { le[a].pos[i] = NOPOS; le[a].lock[i] = 0; le[a].c[i] = cell_null(); }
+                if (EXT && le[a].c) { le[a].pos[i] = 0xFFFFFFFFu; le[a].lock[i] = 0; le[a].c[i] = cell_null(); }
             }
         }
     }
@@ -900,7 +941,7 @@ __global__ __launch_bounds__(SCAN_T) void scan_kernel(const uint8_t* __restrict_
                     if (pass) {
                         h = gk_hash(key);
 #ifdef CQ_NO_INSERT   // profiling build: direct-mapped slot, results wrong
-                        s = (int)(h & (H - 1));
+                        s = (int)__umulhi((uint32_t)h << 8, H);
 #else
                         s = l_insert(lt, key, h);
 #endif
@@ -927,7 +968,7 @@ __global__ __launch_bounds__(SCAN_T) void scan_kernel(const uint8_t* __restrict_
                             Cell c = av[a];
                             if (c.kind == K_STR) c.bits = c.bits - tile_g + gt0;
                             lds_ext_update(in_lds && c.kind != K_NULL, le[a], in_lds ? (uint32_t)s : 0u,
-                                           P.acc[a].kind, c, rec);
+                                           P.acc[a].kind, c, (iter << 15) | pos);
                         }
                     }
                     if (__any(spill)) {
@@ -1099,10 +1140,12 @@ __global__ __launch_bounds__(SCAN_T) void scan_kernel(const uint8_t* __restrict_
 #pragma unroll
             for (int a = 0; a < KA; a++) {
                 if (a >= nacc) break;
-                if (!le[a].c || le[a].pos[i] == NOPOS) continue;
+                if (!le[a].c || le[a].pos[i] == 0xFFFFFFFFu) continue;
                 const uint64_t idx = (uint64_t)blockIdx.x * gt.cand_stride + i;
                 ExtCand ec;
-                ec.c = le[a].c[i]; ec.pos = le[a].pos[i]; ec.pad = 0;
+                const uint32_t pc = le[a].pos[i];
+                const uint64_t pw = first_win + blockIdx.x + (uint64_t)(pc >> 15) * gridDim.x;
+                ec.c = le[a].c[i]; ec.pos = pw * WSTRIDE - PREB + (pc & 0x7FFF); ec.pad = 0;
                 gt.cand[a][idx] = ec;
                 __threadfence();
                 g_ext_swing(gt, a, P.acc[a].kind, (uint32_t)gi, idx);
@@ -1205,7 +1248,7 @@ __global__ __launch_bounds__(256) void slow_kernel(const uint8_t* __restrict__ g
 
 // ------------------------------------------------------------------ compaction
 __global__ void compact_kernel(const GroupTable gt, int nacc, uint32_t kinds, GroupOut* out, unsigned int* count,
-                               unsigned int cap_out) {
+                               unsigned int cap_out, unsigned long long* ofirst) {
     uint8_t kind_of[MAX_ACC];
 #pragma unroll
     for (int a = 0; a < MAX_ACC; a++) kind_of[a] = (uint8_t)((kinds >> (2 * a)) & 3);
@@ -1232,6 +1275,7 @@ __global__ void compact_kernel(const GroupTable gt, int nacc, uint32_t kinds, Gr
         }
     }
     out[o] = r;
+    if (ofirst) ofirst[o] = r.first;                   // (finish_pack_kernel's dense order keys)
 }
 
 // ------------------------------------------------------------------ gather cells
@@ -2438,7 +2482,7 @@ __global__ void vla_reduce_kernel(const unsigned long long* __restrict__ vkey, c
 extern "C" {
 static size_t lds_slot_bytes(const cq::ScanPlan* P) {
     size_t b = 16 + 4 + 4 + 4;   // key, hdr, cnt, first
-    for (int a = 0; a < P->nacc; a++) b += P->acc[a].kind == cq::ACC_SUM ? 12 : sizeof(cq::Cell) + 12;
+    for (int a = 0; a < P->nacc; a++) b += P->acc[a].kind == cq::ACC_SUM ? 12 : sizeof(cq::Cell) + 8;
     return b;
 }
 static size_t lds_fixed_bytes() {
@@ -2448,13 +2492,15 @@ static size_t lds_fixed_bytes() {
            r16(cq::KSTR);
 }
 
-// group-table capacity: the largest power of two <= 2048 that fits the budget
-// (each carved array is rounded to 16 bytes: 16 arrays at most -> 256 bytes slack)
+// group-table capacity: the largest multiple of 64 <= 2048 that fits the budget
+// (each carved array is rounded to 16 bytes: 16 arrays at most -> 256 bytes slack).
+// Not a power of two: a MIN/MAX plan's wider slots would otherwise halve the table
+// to 1024 slots, which 1000 groups fill to the point that inserts overflow to HBM.
 uint32_t cq_scan_lds_slots(const cq::ScanPlan* P, int grouped) {
     if (!grouped) return 0;
     const size_t per = lds_slot_bytes(P);
     uint32_t h = 2048;
-    while (h > 64 && lds_fixed_bytes() + (size_t)h * per + 512 > (size_t)cq::LDS_BUDGET) h >>= 1;
+    while (h > 64 && lds_fixed_bytes() + (size_t)h * per + 512 > (size_t)cq::LDS_BUDGET) h -= 64;
     return h;
 }
 
@@ -2639,12 +2685,12 @@ int cq_scan_occupancy(const cq::ScanPlan* P, int grouped) {
 }
 
 hipError_t cq_launch_compact(const cq::GroupTable* gt, const cq::ScanPlan* P, cq::GroupOut* out,
-                             unsigned int* count, unsigned int cap_out, hipStream_t s) {
+                             unsigned int* count, unsigned int cap_out, hipStream_t s, unsigned long long* ofirst) {
     const int nacc = P->nacc;
     uint32_t kinds = 0;
     for (int a = 0; a < nacc; a++) kinds |= (uint32_t)P->acc[a].kind << (2 * a);
     const dim3 grid((gt->cap + 255) / 256);
-    hipLaunchKernelGGL(cq::compact_kernel, grid, dim3(256), 0, s, *gt, nacc, kinds, out, count, cap_out);
+    hipLaunchKernelGGL(cq::compact_kernel, grid, dim3(256), 0, s, *gt, nacc, kinds, out, count, cap_out, ofirst);
     return hipGetLastError();
 }
 
@@ -2766,6 +2812,118 @@ __global__ void pack_result_kernel(const GroupOut* __restrict__ out, const unsig
     }
 }
 }  // namespace cq
+
+extern "C++" {
+namespace cq {
+// ---- finish_kernel + pack_result_kernel in one launch: one wave per group.  The
+// wave counts the groups ahead of its own in (first row, index) order over
+// compact_kernel's dense `ofirst` (8 bytes per group instead of a 360-byte GroupOut
+// row each; 64 lanes share the count) -- create_groups' first-appearance order --
+// then lane 0 writes the group's packed record, representative / extreme /
+// long-key cells and STRING bytes at that rank in pack_result_kernel's layout, into
+// HBM (mail_copy_kernel then moves it into the mailbox in coalesced 16-byte stores).
+constexpr uint32_t FP_T = 256, FP_W = FP_T / 64, FP_MAX = 1u << 20;
+__global__ __launch_bounds__(FP_T) void finish_pack_kernel(const uint8_t* __restrict__ g, uint64_t n,
+                                                           const GroupOut* __restrict__ out,
+                                                           const unsigned long long* __restrict__ ofirst,
+                                                           const unsigned int* __restrict__ count,
+                                                           unsigned int cap_out, const FinishDesc D,
+                                                           uint8_t* __restrict__ dst,
+                                                           const ScanStats* __restrict__ stats,
+                                                           uint8_t* __restrict__ hdr) {
+    __shared__ uint4 stage[FP_W][9];
+    __shared__ int16_t scols[MAX_WIDE];
+    __shared__ Cell wcell[FP_W][MAX_WIDE + MAX_ACC + 1];
+    const uint32_t ng = min(*count, cap_out);
+    const uint32_t tid = threadIdx.x, lane = tid & 63, wv = tid >> 6;
+    const uint32_t i = blockIdx.x * FP_W + wv;                  // this wave's group
+    if (blockIdx.x == 0 && tid == 0) {
+        const uint32_t nw = (uint32_t)(sizeof(ScanStats) / 4);
+        for (uint32_t k = 0; k < nw; k++) ((uint32_t*)hdr)[k] = ((const uint32_t*)stats)[k];
+        *(uint32_t*)(hdr + sizeof(ScanStats)) = ng;
+    }
+    if (blockIdx.x * FP_W >= ng) return;                       // (uniform)
+    for (int k = (int)tid; k < D.ncols; k += FP_T) scols[k] = D.cols[k];
+    __syncthreads();
+    if (i >= ng) return;                                        // (wave-uniform)
+    const unsigned long long fi = ofirst[i];
+    uint32_t r = 0;
+    for (uint32_t k = lane; k < ng; k += 64) {
+        const unsigned long long f = ofirst[k];
+        r += (f < fi) | ((f == fi) & (k < i));
+    }
+    for (int o = 32; o > 0; o >>= 1) r += (uint32_t)__shfl_xor((int)r, o, 64);
+    const int nacc = D.nacc;
+    const uint32_t rec = 40u + 40u * (uint32_t)nacc;
+    const uint32_t ncell = (uint32_t)(D.ncols + nacc + 1);
+    // the first record's bytes staged by the wave (lanes 0..8: one 16-byte load each)
+    const unsigned long long fr = fi == NOPOS ? NOPOS : fi >> D.first_shift;
+    const bool have = D.ncols && fr != NOPOS && fr < n;
+    const uint8_t* recp = have ? g + fr : g;
+    if (have && lane < 9) stage[wv][lane] = ((const uint4*)((uintptr_t)recp & ~(uintptr_t)15))[lane];
+    __builtin_amdgcn_wave_barrier();
+    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+    Cell* wcs = wcell[wv];
+    // lane 1: the row's record, extreme cells and long-key cell; lane 0: the
+    // representative cells (a call: nothing of the row's is live across it)
+    if (lane == 1) {
+        const GroupOut& o = out[i];
+        uint64_t* rp = (uint64_t*)(dst + (size_t)r * rec);
+        const uint32_t cl = o.clslen;
+        const uint64_t w0 = o.w0;
+        rp[0] = (uint64_t)cl;
+        rp[1] = w0;
+        rp[2] = o.w1;
+        rp[3] = o.cnt;
+        rp[4] = fi;
+#pragma unroll
+        for (int a = 0; a < MAX_ACC; a++) {
+            if (a >= nacc) break;
+            const Cell e = o.ext[a];
+            rp[5 + 5 * a + 0] = dbl_bits(o.sum[a]);
+            rp[5 + 5 * a + 1] = o.num[a];
+            rp[5 + 5 * a + 2] = ((uint64_t)e.len << 32) | e.kind;
+            rp[5 + 5 * a + 3] = e.bits;
+            rp[5 + 5 * a + 4] = o.extpos[a];
+            wcs[D.ncols + a] = e;
+        }
+        Cell kc = cell_null();
+        if ((cl >> 16) == GK_LONG) { kc.kind = K_STR; kc.len = cl & 0xffff; kc.bits = w0; }
+        wcs[D.ncols + nacc] = kc;
+    }
+    if (lane == 0 && D.ncols) {
+        if (have) {
+            const uint8_t* tile = (const uint8_t*)stage[wv] + ((uintptr_t)recp & 15);
+            parse_cols_out_staged(tile, 128, recp, scols, D.ncols, D.delim, D.quote, wcs);
+        } else {
+            for (int c = 0; c < D.ncols; c++) wcs[c] = cell_null();
+        }
+    }
+    __builtin_amdgcn_wave_barrier();
+    __builtin_amdgcn_fence(__ATOMIC_ACQ_REL, "wavefront", "local");
+    // the wave stores the cells and copies the STRING bytes, one byte per lane
+    Cell* cs = (Cell*)(dst + (size_t)ng * rec) + (size_t)r * ncell;
+    uint8_t* db = dst + (size_t)ng * rec + (size_t)ng * ncell * sizeof(Cell) + (size_t)r * ncell * D.sb;
+    for (uint32_t c = lane; c < ncell; c += 64) cs[c] = wcs[c];
+    for (uint32_t c = 0; c < ncell; c++) {
+        const Cell x = wcs[c];
+        if (x.kind != K_STR) continue;
+        const uint8_t* sp = (const uint8_t*)(uintptr_t)x.bits;
+        const uint32_t m = x.len < D.sb ? x.len : D.sb;
+        for (uint32_t j = lane; j < m; j += 64) db[(size_t)c * D.sb + j] = sp[j];
+    }
+}
+}  // namespace cq
+}  // extern "C++"
+hipError_t cq_launch_finish_pack(const uint8_t* g, uint64_t n, const cq::GroupOut* out, const unsigned long long* ofirst,
+                                 const unsigned int* count, unsigned int cap_out, const cq::FinishDesc* D, uint8_t* dst,
+                                 const cq::ScanStats* stats, uint8_t* hdr, hipStream_t s) {
+    if (cap_out > cq::FP_MAX || D->sb % 16) return hipErrorInvalidValue;
+    hipLaunchKernelGGL(cq::finish_pack_kernel, dim3((cap_out + cq::FP_W - 1) / cq::FP_W), dim3(cq::FP_T), 0, s, g, n,
+                       out, ofirst, count, cap_out, *D, dst, stats, hdr);
+    return hipGetLastError();
+}
+unsigned int cq_finish_pack_max() { return cq::FP_MAX; }
 
 namespace cq {
 // the packed result's records and cells, device buffer -> host-mapped mailbox in
