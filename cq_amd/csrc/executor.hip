@@ -3286,9 +3286,20 @@ cq_table* run_fast_join(DevCtx& c, cq_node* q, Compiled& C, const cqgpu_table* L
                 HIPCHECK(cq_launch_pack_result(A.out, A.out_count, cap_out, C.P.nacc, dcells, dbytes, ncell, SB,
                                                mail + MAIL_HDR, A.stats, mail, 1, c.stream));
             }
-            unsigned int fl = 0;
-            HIPCHECK(hipMemcpyAsync(&fl, dflag, 4, hipMemcpyDeviceToHost, c.stream));
+            // the flags through pinned memory (a pageable destination would block here);
+            // the result rows' pool refilled while the device works
+            unsigned int* hfl = (unsigned int*)pinned(c, 16);
+            HIPCHECK(hipMemcpyAsync(hfl, dflag, 4, hipMemcpyDeviceToHost, c.stream));
+            PHASE("results launch");
+            if (grouped) {
+                uint32_t nstr = 0;
+                for (const OutCol& o : C.outs) nstr += o.kind == OUT_REP || o.kind == OUT_CONST;
+                rowpool_fill((int)C.outs.size(), nstr);
+                PHASE("pool");
+            }
             HIPCHECK(hipStreamSynchronize(c.stream));
+            const unsigned int fl = *hfl;
+            PHASE("sync");
             if (fl) { JXDBG("flags %#x\n", fl); *fallback = true; return nullptr; }
             ScanStats st;
             memcpy(&st, mail, sizeof st);
@@ -3308,8 +3319,10 @@ cq_table* run_fast_join(DevCtx& c, cq_node* q, Compiled& C, const cqgpu_table* L
             const size_t pb = cq_pack_result_bytes(ng, C.P.nacc, ncell, SB);
             if (hbuf.size() < pb + 8) hbuf.resize(pb + 8);
             memcpy(hbuf.data(), mail + MAIL_HDR, pb);
+            PHASE("mcopy");
             cq_table* res = nullptr;
             if (grouped && presorted && ng) res = build_direct(C, hbuf.data(), ng, ncell, SB, rep_ord, Lit, ~0ull);
+            PHASE("direct");
             if (!res) {
                 std::vector<GroupOut> outs(ng);
                 std::vector<Cell> fcells((size_t)ng * ncell);
@@ -3390,10 +3403,16 @@ cq_table* run_fast_join(DevCtx& c, cq_node* q, Compiled& C, const cqgpu_table* L
             unsigned long long* cnts = (unsigned long long*)(small.as<uint8_t>() + o_ctl + 8);   // placed, pairs, occupied
             unsigned long long* skr = cnts + 3;                                                  // build keys' min, max
             uint32_t* snotmono = (uint32_t*)(skr + 2);
+            PHASE("star setup");
             HIPCHECK(hipMemsetAsync(big.p, 0, b16, c.stream));
             HIPCHECK(hipMemsetAsync(small.p, 0, o_ctl + 64, c.stream));
             HIPCHECK(hipMemsetAsync(gfirst, 0xff, (size_t)G * 8, c.stream));          // gfirst and gminix
             HIPCHECK(hipMemsetAsync(skr, 0xff, 8, c.stream));
+            // the GROUP BY tag table seeded with the build side's sampled tags (fast_kernel's
+            // placement): the build's lookups hit without walking
+            if (grouped)
+                if (const void* seed = fast_seed_of(L, gcol))
+                    HIPCHECK(hipMemcpyAsync(ttab, seed, (size_t)G * 8, hipMemcpyDeviceToDevice, c.stream));
             HIPCHECK(hipEventRecord(c.ev0, c.stream));
             HIPCHECK(cq_jx_star_extract(L->g, L->data_begin, L->n, ws, d, dq, kl, grouped ? gcol : -1, 1, kmin, range, d16,
                                         l32.as<uint32_t>(), ttab, gsum, cnts, sflag, skr, snotmono,
@@ -3403,6 +3422,7 @@ cq_table* run_fast_join(DevCtx& c, cq_node* q, Compiled& C, const cqgpu_table* L
                                         l32.as<uint32_t>(), ttab, gsum, cnts + 1, sflag, nullptr, snotmono, nullptr,
                                         gminix, xgrid, c.stream));
             HIPCHECK(cq_jx_star_first(d16, l32.as<uint32_t>(), range, snotmono, gfirst, cnts + 2, c.ncu * 4, c.stream));
+            PHASE("star launch");
             bool fb = false;
             cq_table* res = results([&](TableArena& A) {
                 HIPCHECK(cq_jx_star_flush(grouped ? 1 : 0, vcol >= 0 ? 1 : 0, ttab, gsum, gfirst, gminix,
@@ -3521,6 +3541,9 @@ cq_table* run_join(DevCtx& c, cq_node* q, const cqgpu_table* L, const cqgpu_tabl
                    JoinPartial* part = nullptr) {
     const int nj = q->u.q.join_count;
     if (nj < 1) throw HipError{"run_join without a JOIN"};
+    PhaseClock pc;
+    g_phase = &pc;
+    struct Unset { ~Unset() { g_phase = nullptr; } } unset_;
     if (nrights < nj) throw Ineligible{"join table not given"};
     // across partials the first level runs on the key-routed sides; a chain's later
     // levels join each rank's joined rows with the whole next table (every joined

@@ -1160,6 +1160,39 @@ __device__ __forceinline__ uint32_t jx_tag_gid_lds(unsigned long long* __restric
     return g;
 }
 
+// the same with fast_kernel's two-choice buckets (slots 2b, 2b + 1 of buckets
+// b1, b2 of fast_key_hash), the table seeded by the host's cuckoo placement of the
+// build side's sampled tags (cq_fast_seed): a hit is two 16-byte LDS reads and
+// four compares, no walk; a tag the sample missed claims a free candidate slot in
+// the global table (every block agrees on its slot) and enters the block's mirror.
+// No free candidate: `full` (the record-array join takes the query).
+static_assert(TSLOTS == JX_G, "the STAR tag table is fast_kernel's seeded layout");
+__device__ __forceinline__ uint32_t jx_tag_slot(unsigned long long* __restrict__ lt,
+                                                unsigned long long* __restrict__ tt, unsigned long long tag,
+                                                bool& full) {
+    const uint32_t h = fast_key_hash((uint32_t)tag, (uint32_t)(tag >> 32));
+    const uint32_t b1 = h & (TBUCKETS - 1), b2 = (h >> 16) & (TBUCKETS - 1);
+    const v4u x = ((const v4u*)lt)[b1], y = ((const v4u*)lt)[b2];
+    const unsigned long long t0 = (unsigned long long)x.x | ((unsigned long long)x.y << 32);
+    const unsigned long long t1 = (unsigned long long)x.z | ((unsigned long long)x.w << 32);
+    const unsigned long long t2 = (unsigned long long)y.x | ((unsigned long long)y.y << 32);
+    const unsigned long long t3 = (unsigned long long)y.z | ((unsigned long long)y.w << 32);
+    int sl = -1;
+    sl = t3 == tag ? (int)(2 * b2 + 1) : sl;
+    sl = t2 == tag ? (int)(2 * b2) : sl;
+    sl = t1 == tag ? (int)(2 * b1 + 1) : sl;
+    sl = t0 == tag ? (int)(2 * b1) : sl;
+    if (sl >= 0) return (uint32_t)sl;
+    const uint32_t cand[4] = {2 * b1, 2 * b1 + 1, 2 * b2, 2 * b2 + 1};
+    for (int c = 0; c < 4 && sl < 0; c++) {
+        const unsigned long long old = atomicCAS(&tt[cand[c]], 0ull, tag);
+        if (old == 0ull || old == tag) sl = (int)cand[c];
+    }
+    if (sl < 0) { full = true; return 0; }
+    lt[sl] = tag;                                  // (every writer: the same tag)
+    return (uint32_t)sl;
+}
+
 // the canonical INTEGER key of a field (16 bytes d0..d3 from its start, len bytes):
 // digits only, no leading zero, at most 15 digits and not 8-10; NULL (empty) -> JX_NULLKEY
 __device__ __forceinline__ bool jx_key(uint32_t d0, uint32_t d1, uint32_t d2, uint32_t d3, uint32_t len,
@@ -1239,8 +1272,8 @@ __global__ __launch_bounds__(LT) void jx_extract_kernel(const uint8_t* __restric
         mono = __builtin_amdgcn_readfirstlane(*jo.notmono) == 0u ? 1u : 0u;
         __syncthreads();
     }
-    if constexpr (SBUILD) {
-        for (uint32_t k = threadIdx.x; k < JX_G; k += LT) stt[k] = 0ull;
+    if constexpr (SBUILD) {                       // the mirror starts as the seeded global table
+        for (uint32_t k = threadIdx.x; k < JX_G; k += LT) stt[k] = jo.ttab[k];
         __syncthreads();
     }
     uint32_t sflag = 0;
@@ -1458,7 +1491,11 @@ __global__ __launch_bounds__(LT) void jx_extract_kernel(const uint8_t* __restric
                         if (ix >= jo.range) { sflag |= 16u; continue; }
                         bool full = false;
                         uint32_t gid = 0;
-                        if constexpr (SBUILD) gid = jx_tag_gid_lds(stt, jo.ttab, pay[u], full);
+#ifndef JX_AB_NOTAG
+                        if constexpr (SBUILD) gid = jx_tag_slot(stt, jo.ttab, pay[u], full);
+#else
+                        gid = (uint32_t)(pay[u] >> 40) & 1023u;
+#endif
                         if (full) sflag |= 32u;
 #ifndef JX_AB_NOSTORE
                         jo.d16[ix] = (uint16_t)(gid + 1u);
@@ -1482,11 +1519,15 @@ __global__ __launch_bounds__(LT) void jx_extract_kernel(const uint8_t* __restric
                                 jo.d16[ix] = (uint16_t)(gv | 0x8000u);   // (every writer: the same value)
                             }
 #endif
+#ifndef JX_AB_NOAGG
                             atomicAdd(&scnt[gi], 1u);
                             if (NR == 2 && pay[u] != JX_NOVAL) {
                                 atomicAdd(&sfix[gi], pay[u]);
                                 atomicAdd(&snum[gi], 1u);
                             }
+#else
+                            sflag |= gi == 12345u ? 1u : 0u;
+#endif
                             nstar++;
                         }
                     }
