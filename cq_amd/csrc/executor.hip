@@ -179,8 +179,10 @@ hipError_t cq_jx_star_extract(const uint8_t* g, uint64_t lo, uint64_t hi, uint32
                               uint16_t* d16, uint32_t* l32, unsigned long long* ttab,
                               unsigned long long* gsum, unsigned long long* counter, unsigned int* flag,
                               unsigned long long* krange, uint32_t* notmono, unsigned long long* wfl,
-                              uint32_t* gminix, int grid, hipStream_t s);
+                              uint32_t* gminix, int rp, int grid, hipStream_t s);
 hipError_t cq_jx_star_order(const unsigned long long* wfl, unsigned long long nwin, uint32_t* notmono, hipStream_t s);
+hipError_t cq_jx_star_init(void* d16, size_t d16_bytes, void* small, size_t small_bytes, uint32_t ff0, uint32_t ff1,
+                           uint32_t ffw, const void* seed, size_t seed_bytes, int grid, hipStream_t s);
 hipError_t cq_jx_star_first(const uint16_t* d16, const uint32_t* l32, unsigned long long range, const uint32_t* notmono,
                             uint32_t* gfirst, unsigned long long* nocc, int grid, hipStream_t s);
 hipError_t cq_jx_star_flush(int grouped, int value, const unsigned long long* ttab, const unsigned long long* gsum,
@@ -3389,10 +3391,17 @@ cq_table* run_fast_join(DevCtx& c, cq_node* q, Compiled& C, const cqgpu_table* L
             DevBuf big(b16), l32(range * 4 + 16);
             const uint32_t G = cq_jx_star_groups();
             // ttab | gsum | gfirst | gminix | control words; the build windows' first / last keys
+            // (control words: [0] flags, [8..32) placed / pairs / occupied, [32..48) the build
+            // keys' min (0xFF..) and max, [48..52) not-rising)
             const size_t o_gsum = (size_t)G * 8, o_first = o_gsum + (size_t)G * 24, o_minix = o_first + (size_t)G * 4,
                          o_ctl = o_minix + (size_t)G * 4;
             DevBuf small(o_ctl + 64);
-            const uint64_t nwb = cq_jx_windows(L->data_begin, L->n, ws);
+            // records averaging under ~33 bytes (a sampled stride below the largest):
+            // three records per lane pass over windows of the largest stride (fast_kernel's rule)
+            const bool rp2 = getenv("CQGPU_FAST_RP2") != nullptr;
+            const int rpl = ws < 3968u && !rp2 ? 3 : 2, rpr = wsr < 3968u && !rp2 ? 3 : 2;
+            const uint32_t wsl3 = rpl == 3 ? 3968u : ws, wsr3 = rpr == 3 ? 3968u : wsr;
+            const uint64_t nwb = cq_jx_windows(L->data_begin, L->n, wsl3);
             DevBuf wfl(std::max<uint64_t>(nwb, 1) * 16);
             uint16_t* d16 = big.as<uint16_t>();
             unsigned long long* ttab = small.as<unsigned long long>();
@@ -3404,23 +3413,20 @@ cq_table* run_fast_join(DevCtx& c, cq_node* q, Compiled& C, const cqgpu_table* L
             unsigned long long* skr = cnts + 3;                                                  // build keys' min, max
             uint32_t* snotmono = (uint32_t*)(skr + 2);
             PHASE("star setup");
-            HIPCHECK(hipMemsetAsync(big.p, 0, b16, c.stream));
-            HIPCHECK(hipMemsetAsync(small.p, 0, o_ctl + 64, c.stream));
-            HIPCHECK(hipMemsetAsync(gfirst, 0xff, (size_t)G * 8, c.stream));          // gfirst and gminix
-            HIPCHECK(hipMemsetAsync(skr, 0xff, 8, c.stream));
-            // the GROUP BY tag table seeded with the build side's sampled tags (fast_kernel's
-            // placement): the build's lookups hit without walking
-            if (grouped)
-                if (const void* seed = fast_seed_of(L, gcol))
-                    HIPCHECK(hipMemcpyAsync(ttab, seed, (size_t)G * 8, hipMemcpyDeviceToDevice, c.stream));
+            // one launch: d16 zero, gfirst / gminix and the keys' min 0xFF.., the rest of
+            // the small block zero, the GROUP BY tag table seeded with the build side's
+            // sampled tags (fast_kernel's placement: the build's lookups hit without walking)
+            const void* seed = grouped ? fast_seed_of(L, gcol) : nullptr;
+            HIPCHECK(cq_jx_star_init(big.p, b16, small.p, o_ctl + 64, (uint32_t)o_first, (uint32_t)o_ctl,
+                                     (uint32_t)o_ctl + 32, seed, seed ? (size_t)G * 8 : 0, c.ncu * 4, c.stream));
             HIPCHECK(hipEventRecord(c.ev0, c.stream));
-            HIPCHECK(cq_jx_star_extract(L->g, L->data_begin, L->n, ws, d, dq, kl, grouped ? gcol : -1, 1, kmin, range, d16,
+            HIPCHECK(cq_jx_star_extract(L->g, L->data_begin, L->n, wsl3, d, dq, kl, grouped ? gcol : -1, 1, kmin, range, d16,
                                         l32.as<uint32_t>(), ttab, gsum, cnts, sflag, skr, snotmono,
-                                        wfl.as<unsigned long long>(), nullptr, xgrid, c.stream));
+                                        wfl.as<unsigned long long>(), nullptr, rpl, xgrid, c.stream));
             HIPCHECK(cq_jx_star_order(wfl.as<unsigned long long>(), nwb, snotmono, c.stream));
-            HIPCHECK(cq_jx_star_extract(R->g, R->data_begin, R->n, wsr, d, dq, kr, vcol, 0, kmin, range, d16,
+            HIPCHECK(cq_jx_star_extract(R->g, R->data_begin, R->n, wsr3, d, dq, kr, vcol, 0, kmin, range, d16,
                                         l32.as<uint32_t>(), ttab, gsum, cnts + 1, sflag, nullptr, snotmono, nullptr,
-                                        gminix, xgrid, c.stream));
+                                        gminix, rpr, xgrid, c.stream));
             HIPCHECK(cq_jx_star_first(d16, l32.as<uint32_t>(), range, snotmono, gfirst, cnts + 2, c.ncu * 4, c.stream));
             PHASE("star launch");
             bool fb = false;

@@ -1250,7 +1250,7 @@ __device__ __forceinline__ bool jx_key(uint32_t d0, uint32_t d1, uint32_t d2, ui
 #endif
 }
 
-template <bool BUILD, bool COMMA, int NR, bool COUNT, bool STAR = false>
+template <bool BUILD, bool COMMA, int NR, bool COUNT, bool STAR = false, int RP = 2>
 __global__ __launch_bounds__(LT) void jx_extract_kernel(const uint8_t* __restrict__ g, const JxPlan jp, const JxOut jo) {
     extern __shared__ __align__(16) uint8_t smem[];
     WaveLds* waves = (WaveLds*)smem;
@@ -1368,11 +1368,11 @@ __global__ __launch_bounds__(LT) void jx_extract_kernel(const uint8_t* __restric
         unsigned long long lfirst = ~0ull, llast = 0ull;
         bool lany = false, lbad = false;
         while (__any(todo != 0)) {
-            uint32_t p[2], pa[2], fst[2][2], fen[2][2], e[2];
-            uint64_t sv[2];
-            bool valid[2], fail[2];
+            uint32_t p[RP], pa[RP], fst[RP][2], fen[RP][2], e[RP];
+            uint64_t sv[RP];
+            bool valid[RP], fail[RP];
 #pragma unroll
-            for (int u = 0; u < 2; u++) {
+            for (int u = 0; u < RP; u++) {
                 valid[u] = todo != 0;
                 const uint32_t b = ctz64(todo) & 63u;
                 todo &= todo - 1;
@@ -1389,37 +1389,38 @@ __global__ __launch_bounds__(LT) void jx_extract_kernel(const uint8_t* __restric
                 asm volatile("" : "+s"(n));
                 if (k > 0 && n == 0) {
 #pragma unroll
-                    for (int u = 0; u < 2; u++) { fst[u][k] = fst[u][k - 1]; fen[u][k] = fen[u][k - 1]; }
+                    for (int u = 0; u < RP; u++) { fst[u][k] = fst[u][k - 1]; fen[u][k] = fen[u][k - 1]; }
                     continue;
                 }
                 if (k > 0) {
 #pragma unroll
-                    for (int u = 0; u < 2; u++) sv[u] &= sv[u] - 1;
+                    for (int u = 0; u < RP; u++) sv[u] &= sv[u] - 1;
                 }
                 if (k == 0 && n == 0) {
 #pragma unroll
-                    for (int u = 0; u < 2; u++) fst[u][k] = 0;
+                    for (int u = 0; u < RP; u++) fst[u][k] = 0;
                 } else if (k > 0 && n == 1) {
 #pragma unroll
-                    for (int u = 0; u < 2; u++) fst[u][k] = fen[u][k - 1] + 1;
+                    for (int u = 0; u < RP; u++) fst[u][k] = fen[u][k - 1] + 1;
                 } else {
                     for (uint32_t j = k == 0 ? 1u : 2u; j < n; j++) {
 #pragma unroll
-                        for (int u = 0; u < 2; u++) sv[u] &= sv[u] - 1;
+                        for (int u = 0; u < RP; u++) sv[u] &= sv[u] - 1;
                     }
 #pragma unroll
-                    for (int u = 0; u < 2; u++) {
+                    for (int u = 0; u < RP; u++) {
                         fst[u][k] = ctz64(sv[u]) + 1;
                         sv[u] &= sv[u] - 1;
                     }
                 }
 #pragma unroll
-                for (int u = 0; u < 2; u++) fen[u][k] = ctz64(sv[u]);
+                for (int u = 0; u < RP; u++) fen[u][k] = ctz64(sv[u]);
             }
             const bool last_pass = !__any(todo != 0);
-            unsigned long long key[2], pay[2];
+            unsigned long long key[RP], pay[RP];
+            uint32_t gpre[RP] = {};   // STAR probe: d16 of the key, loaded before the payload is typed
 #pragma unroll
-            for (int u = 0; u < 2; u++) {
+            for (int u = 0; u < RP; u++) {
                 const uint32_t en = fen[u][NR - 1];
                 fail[u] = (en >= 64u) | (en > e[u]);
                 const uint32_t ks = NR == 1 || rkey == 0 ? fst[u][0] : fst[u][1];
@@ -1428,6 +1429,12 @@ __global__ __launch_bounds__(LT) void jx_extract_kernel(const uint8_t* __restric
                 ld8a(pa[u] + ks, d0, d1);
                 ld8a(pa[u] + ks + 8, d2, d3);
                 fail[u] |= !jx_key(d0, d1, d2, d3, ke - ks, key[u]);
+#ifndef JX_LATE_LOOK
+                if constexpr (SPROBE) {    // (out of range or NULL: slot 0, not used)
+                    const unsigned long long ix = key[u] - jo.kmin;
+                    gpre[u] = jo.d16[ix < jo.range ? ix : 0ull];
+                }
+#endif
                 pay[u] = 0;
                 if (NR == 2) {
                     const uint32_t ps = rkey == 0 ? fst[u][1] : fst[u][0];
@@ -1443,6 +1450,10 @@ __global__ __launch_bounds__(LT) void jx_extract_kernel(const uint8_t* __restric
                     } else if (plen == 0) {
                         pay[u] = JX_NOVAL;                            // NULL: counted, not summed
                     } else {                                          // the SUM argument, 10^-3 units
+#ifdef JX_AB_NOPAY
+                        pay[u] = q0 & 0xFFFu;
+                        continue;
+#endif
                         // (a leading '-': the rest parsed, then negated; two's complement sums)
                         const bool neg = (q0 & 0xFFu) == '-' && plen > 1u;
                         uint32_t v0 = q0, v1 = q1, vl = plen;
@@ -1450,17 +1461,12 @@ __global__ __launch_bounds__(LT) void jx_extract_kernel(const uint8_t* __restric
                             ld8a(pa[u] + ps + 1, v0, v1);
                             vl = plen - 1;
                         }
-                        unsigned long long fx;
-                        const Num n4 = num4<true>(v0, vl);
-                        if (n4.ok) {
-                            const uint32_t mul = (n4.k & 2) ? ((n4.k & 1) ? 1u : 10u) : ((n4.k & 1) ? 100u : 1000u);
-                            fx = (unsigned long long)__umul24(n4.M, mul);
-                        } else {
-                            const Num n7 = num7(v0, v1, vl);
-                            fail[u] |= !n7.ok | (n7.k > 3u);
-                            const uint32_t mul = (n7.k & 2) ? ((n7.k & 1) ? 1u : 10u) : ((n7.k & 1) ? 100u : 1000u);
-                            fx = (unsigned long long)n7.M * mul;
-                        }
+                        // (1-7 bytes in one typing: num7 is exact for the 4-byte shapes too,
+                        // and a mix of widths in one wave would run both)
+                        const Num n7 = num7(v0, v1, vl);
+                        fail[u] |= !n7.ok | (n7.k > 3u);
+                        const uint32_t mul = (uint32_t)(0x0001000A006403E8ull >> ((n7.k & 3u) << 4)) & 0xFFFFu;
+                        const unsigned long long fx = (unsigned long long)n7.M * mul;
                         pay[u] = neg ? 0ull - fx : fx;
                     }
                 }
@@ -1476,7 +1482,7 @@ __global__ __launch_bounds__(LT) void jx_extract_kernel(const uint8_t* __restric
             }
             if constexpr (STAR) {
 #pragma unroll
-                for (int u = 0; u < 2; u++) {
+                for (int u = 0; u < RP; u++) {
                     if (!valid[u] || fail[u]) continue;
                     const unsigned long long k = key[u];
                     const unsigned long long ix = k - jo.kmin;
@@ -1505,14 +1511,18 @@ __global__ __launch_bounds__(LT) void jx_extract_kernel(const uint8_t* __restric
                         sflag |= gid == 12345u ? 1u : 0u;
 #endif
                     } else if (k != JX_NULLKEY && ix < jo.range) {
-#ifndef JX_AB_NOLOOK
+#if defined(JX_AB_NOLOOK)
+#elif defined(JX_LATE_LOOK)
                         const uint32_t gv = jo.d16[ix];
 #else
+                        const uint32_t gv = gpre[u];
+#endif
+#ifdef JX_AB_NOLOOK
                         const uint32_t gv = 1u + (uint32_t)(ix & 1023u);
 #endif
                         if (gv) {
                             const uint32_t gi = (gv & 0x7FFFu) - 1u;
-#if !defined(JX_AB_NOLOOK) && !defined(JX_AB_NOFLAG)
+#if !defined(JX_AB_NOFLAG)
                             if (mono) {
                                 if ((uint32_t)ix < smix[gi]) atomicMin(&smix[gi], (uint32_t)ix);
                             } else if (!(gv & 0x8000u)) {
@@ -1534,7 +1544,7 @@ __global__ __launch_bounds__(LT) void jx_extract_kernel(const uint8_t* __restric
                 }
             } else {
 #pragma unroll
-                for (int u = 0; u < 2; u++) {
+                for (int u = 0; u < RP; u++) {
                     if (valid[u]) {
                         const uint32_t at = at_next++;
                         if (at < jo.cap) {
@@ -1614,6 +1624,25 @@ __global__ void jx_star_order_kernel(const unsigned long long* __restrict__ wfl,
          w += (uint64_t)gridDim.x * blockDim.x)
         bad = bad || wfl[2 * w + 1] >= wfl[2 * (w + 1)];
     if (__any(bad) && (threadIdx.x & 63) == 0) atomicOr(notmono, 1u);
+}
+
+// STAR, before the build: every per-query array in one launch (instead of a fill
+// per array and a copy of the tag seed): d16 zero over the key range, the small
+// block zero except its 0xFF run [ff0, ff1) (16-byte granular) and the 8-byte word
+// at ffw, the tag table from the seed when there is one
+__global__ void jx_star_init_kernel(uint4* __restrict__ d16, uint64_t n16, uint4* __restrict__ small, uint32_t nsmall16,
+                                    uint32_t ff0, uint32_t ff1, uint32_t ffw, const uint4* __restrict__ seed,
+                                    uint32_t nseed16) {
+    const uint64_t t = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x, nt = (uint64_t)gridDim.x * blockDim.x;
+    const uint4 z = make_uint4(0u, 0u, 0u, 0u), f = make_uint4(~0u, ~0u, ~0u, ~0u);
+    for (uint64_t i = t; i < nsmall16; i += nt) {
+        const uint32_t b = (uint32_t)i * 16u;
+        uint4 v = (b >= ff0 && b < ff1) ? f : (seed && i < nseed16 ? seed[i] : z);
+        if (ffw == b) { v.x = ~0u; v.y = ~0u; }
+        if (ffw == b + 8u) { v.z = ~0u; v.w = ~0u; }
+        small[i] = v;
+    }
+    for (uint64_t i = t; i < n16; i += nt) d16[i] = z;
 }
 
 // STAR without rising build keys: each group's first pair in (l, r) order has the
@@ -2166,19 +2195,25 @@ hipError_t cq_jx_star_extract(const uint8_t* g, uint64_t lo, uint64_t hi, uint32
                               uint16_t* d16, uint32_t* l32, unsigned long long* ttab,
                               unsigned long long* gsum, unsigned long long* counter, unsigned int* flag,
                               unsigned long long* krange, uint32_t* notmono, unsigned long long* wfl,
-                              uint32_t* gminix, int grid, hipStream_t s) {
+                              uint32_t* gminix, int rp, int grid, hipStream_t s) {
     using namespace cq::fast;
     JxPlan jp;
     if (!jx_plan(g, lo, hi, ws, delim, quote, kcol, pcol, &jp)) return hipErrorInvalidValue;
     const int nr = pcol >= 0 ? 2 : 1;
     const bool comma = delim == ',' && quote == '"';
     typedef void (*xfn_t)(const uint8_t*, const JxPlan, const JxOut);
-    static const xfn_t tab[2][2][2] = {
-        {{jx_extract_kernel<false, false, 1, false, true>, jx_extract_kernel<false, false, 2, false, true>},
-         {jx_extract_kernel<false, true, 1, false, true>, jx_extract_kernel<false, true, 2, false, true>}},
-        {{jx_extract_kernel<true, false, 1, false, true>, jx_extract_kernel<true, false, 2, false, true>},
-         {jx_extract_kernel<true, true, 1, false, true>, jx_extract_kernel<true, true, 2, false, true>}}};
-    const xfn_t fn = tab[build ? 1 : 0][comma ? 1 : 0][nr - 1];
+    // [build][comma][roles - 1][three records per pass: records under ~33 bytes, where
+    // two per pass leave a second, mostly idle pass for the lanes holding a third start]
+    static const xfn_t tab[2][2][2][2] = {
+        {{{jx_extract_kernel<false, false, 1, false, true>, jx_extract_kernel<false, false, 1, false, true, 3>},
+          {jx_extract_kernel<false, false, 2, false, true>, jx_extract_kernel<false, false, 2, false, true, 3>}},
+         {{jx_extract_kernel<false, true, 1, false, true>, jx_extract_kernel<false, true, 1, false, true, 3>},
+          {jx_extract_kernel<false, true, 2, false, true>, jx_extract_kernel<false, true, 2, false, true, 3>}}},
+        {{{jx_extract_kernel<true, false, 1, false, true>, jx_extract_kernel<true, false, 1, false, true, 3>},
+          {jx_extract_kernel<true, false, 2, false, true>, jx_extract_kernel<true, false, 2, false, true, 3>}},
+         {{jx_extract_kernel<true, true, 1, false, true>, jx_extract_kernel<true, true, 1, false, true, 3>},
+          {jx_extract_kernel<true, true, 2, false, true>, jx_extract_kernel<true, true, 2, false, true, 3>}}}};
+    const xfn_t fn = tab[build ? 1 : 0][comma ? 1 : 0][nr - 1][rp == 3 ? 1 : 0];
     JxOut jo;
     memset(&jo, 0, sizeof jo);
     jo.flag = flag;
@@ -2203,6 +2238,16 @@ hipError_t cq_jx_star_order(const unsigned long long* wfl, unsigned long long nw
     if (nwin < 2) return hipSuccess;
     hipLaunchKernelGGL(cq::fast::jx_star_order_kernel, dim3((unsigned)std::min<unsigned long long>((nwin + 255) / 256, 1024)),
                        dim3(256), 0, s, wfl, (uint64_t)nwin, notmono);
+    return hipGetLastError();
+}
+hipError_t cq_jx_star_init(void* d16, size_t d16_bytes, void* small, size_t small_bytes, uint32_t ff0, uint32_t ff1,
+                           uint32_t ffw, const void* seed, size_t seed_bytes, int grid, hipStream_t s) {
+    if (((uintptr_t)d16 | (uintptr_t)small | (uintptr_t)seed | d16_bytes | small_bytes | seed_bytes | ffw) & 7 ||
+        ((uintptr_t)d16 | (uintptr_t)small | (uintptr_t)seed | d16_bytes | small_bytes | seed_bytes | ff0 | ff1) & 15)
+        return hipErrorInvalidValue;
+    hipLaunchKernelGGL(cq::fast::jx_star_init_kernel, dim3(grid), dim3(1024), 0, s, (uint4*)d16, (uint64_t)(d16_bytes / 16),
+                       (uint4*)small, (uint32_t)(small_bytes / 16), ff0, ff1, ffw, (const uint4*)seed,
+                       (uint32_t)(seed_bytes / 16));
     return hipGetLastError();
 }
 hipError_t cq_jx_star_first(const uint16_t* d16, const uint32_t* l32, unsigned long long range, const uint32_t* notmono,
