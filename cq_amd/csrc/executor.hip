@@ -241,6 +241,8 @@ hipError_t cq_launch_chain_key(const uint2* pairs, unsigned long long np, const 
                                unsigned long long r_none, unsigned long long* out, hipStream_t s);
 hipError_t cq_launch_key_pick(const unsigned long long* key, const unsigned long long* pidx, uint32_t n,
                               unsigned long long* out, hipStream_t s);
+hipError_t cq_launch_offset_gid(const unsigned long long* starts, unsigned long long n, const unsigned long long* q,
+                               uint32_t nq, const unsigned long long* gids, unsigned long long* out, hipStream_t s);
 hipError_t cq_launch_key_flagged(const unsigned long long* key, unsigned long long np, const unsigned int* flags,
                                  const unsigned int* pos, unsigned long long* out, hipStream_t s);
 hipError_t cq_launch_pair_gid(const uint2* pairs, const unsigned long long* pidx, uint32_t n,
@@ -533,6 +535,8 @@ struct cqgpu_table {
     uint64_t ngids = 0;
     uint64_t gid_total = 0;               // routed tables: records of the whole input (every rank's share)
     std::unique_ptr<RouteState> route;    // pending repartition (cqgpu_route_plan)
+    std::unique_ptr<DevBuf> rec_starts;   // record start offsets, file order (built on first need; immutable table)
+    uint32_t nrec_starts = 0;
 };
 
 namespace {
@@ -3203,9 +3207,13 @@ bool sample_key_range(const cqgpu_table* t, int col, uint64_t* kmin, uint64_t* k
 // general pipeline.
 // test knob CQ_AMD_JX_DEBUG: why a fused join handed a query on (stderr)
 #define JXDBG(...) do { if (getenv("CQ_AMD_JX_DEBUG")) fprintf(stderr, "cq_amd jx: " __VA_ARGS__); } while (0)
+// run_fast_join's answer when it filled a JoinPartial (a range / routed partial)
+cq_table* const JOIN_PART_DONE = reinterpret_cast<cq_table*>(uintptr_t(1));
+
 cq_table* run_fast_join(DevCtx& c, cq_node* q, Compiled& C, const cqgpu_table* L, const cqgpu_table* R, int kl,
-                        int kr, int nl) {
+                        int kr, int nl, JoinPartial* part = nullptr, const std::vector<std::string>* jnames = nullptr) {
     if (getenv("CQ_AMD_NO_FAST_JOIN")) return nullptr;
+    if (part && !C.grouped) return nullptr;  // (an ungrouped partial reports its one group even when empty)
     if (C.group_missing || C.P.nprog != 0 || C.P.ngpart != 0 || !C.vla.empty()) return nullptr;
     if (L->n >= (1ull << 32) - 4096 || R->n >= (1ull << 32) - 4096) return nullptr;
     if (L->cfg.delimiter != R->cfg.delimiter || L->cfg.quote != R->cfg.quote) return nullptr;
@@ -3323,7 +3331,7 @@ cq_table* run_fast_join(DevCtx& c, cq_node* q, Compiled& C, const cqgpu_table* L
             memcpy(hbuf.data(), mail + MAIL_HDR, pb);
             PHASE("mcopy");
             cq_table* res = nullptr;
-            if (grouped && presorted && ng) res = build_direct(C, hbuf.data(), ng, ncell, SB, rep_ord, Lit, ~0ull);
+            if (!part && grouped && presorted && ng) res = build_direct(C, hbuf.data(), ng, ncell, SB, rep_ord, Lit, ~0ull);
             PHASE("direct");
             if (!res) {
                 std::vector<GroupOut> outs(ng);
@@ -3351,6 +3359,10 @@ cq_table* run_fast_join(DevCtx& c, cq_node* q, Compiled& C, const cqgpu_table* L
                 std::vector<HGroup> groups = make_groups(c, C, ~0ull, 0, outs, fcells, fbytes, FD.ncols, rep_ord, SB,
                                                          presorted);
                 g_stats.groups = groups.size();
+                if (part) {                       // the groups themselves; run_fast_join globalises them
+                    part->groups = std::move(groups);
+                    return JOIN_PART_DONE;
+                }
                 res = build_groups(C, groups, Lit, c);
             } else {
                 g_stats.groups = ng;
@@ -3435,6 +3447,44 @@ cq_table* run_fast_join(DevCtx& c, cq_node* q, Compiled& C, const cqgpu_table* L
                                           l32.as<uint32_t>(), snotmono, cnts, grouped ? &A.rt : &A.gt, C.P.nacc,
                                           A.stats, sflag, c.stream));
             }, sflag, 0, 4, &fb);
+            if (res == JOIN_PART_DONE) {
+                // a partial: each group's first pair as (global left id << 32) -- the left
+                // record's byte offset to its row (binary search over the table's record
+                // starts) to its global id; the right id is left 0: a left record belongs
+                // to one group and lives on one rank, so the left id alone orders groups,
+                // here and in the merge
+                cqgpu_table* Lw = const_cast<cqgpu_table*>(L);
+                if (!Lw->rec_starts) {
+                    std::unique_ptr<DevBuf> b(new DevBuf());
+                    Lw->nrec_starts = all_records(c, L, *b);
+                    Lw->rec_starts = std::move(b);
+                }
+                if (L->gids && L->ngids != Lw->nrec_starts) throw HipError{"routed table: record count differs from its ids"};
+                std::vector<unsigned long long> qo;
+                for (const HGroup& h : part->groups)
+                    if (h.first != NOPOS) qo.push_back(h.first >> 32);
+                if (!qo.empty()) {
+                    DevBuf dq(qo.size() * 8), dk(qo.size() * 8);
+                    HIPCHECK(hipMemcpyAsync(dq.p, qo.data(), qo.size() * 8, hipMemcpyHostToDevice, c.stream));
+                    HIPCHECK(cq_launch_offset_gid(Lw->rec_starts->as<unsigned long long>(), Lw->nrec_starts,
+                                                  dq.as<unsigned long long>(), (uint32_t)qo.size(), L->gids,
+                                                  dk.as<unsigned long long>(), c.stream));
+                    HIPCHECK(hipMemcpyAsync(qo.data(), dk.p, qo.size() * 8, hipMemcpyDeviceToHost, c.stream));
+                    HIPCHECK(hipStreamSynchronize(c.stream));
+                    size_t k = 0;
+                    for (HGroup& h : part->groups) {
+                        if (h.first == NOPOS) continue;
+                        if (qo[k] >= (1ull << 32)) throw HipError{"fused join partial: left id out of range"};
+                        h.first = qo[k++] << 32;
+                    }
+                }
+                if (jnames) part->names = *jnames;
+                for (int a = 0; a < MAX_ACC; a++) part->acc_classes[a] = 0;    // SUM only
+                // key classes (bit 1: numbers): every build key is a canonical INTEGER (else the
+                // STAR flags declined); the probe side reported as numbers whenever it has rows
+                part->lmask |= Lw->nrec_starts ? 2u : 0u;
+                part->rmask |= R->n > R->data_begin ? 2u : 0u;
+            }
             if (res || !fb) {
                 if (res && !learned) {           // the exact range, for the next query on this table
                     unsigned long long kr2[2] = {~0ull, 0ull};
@@ -3455,6 +3505,7 @@ cq_table* run_fast_join(DevCtx& c, cq_node* q, Compiled& C, const cqgpu_table* L
         }
     }
 
+    if (part) return nullptr;              // (partials: the general join below the caller)
     // pass 0: records per window; exclusive scans give every window's first record index
     const uint64_t nwl = cq_jx_windows(L->data_begin, L->n, ws), nwr = cq_jx_windows(R->data_begin, R->n, wsr);
     if (nwl >= (1ull << 31) || nwr >= (1ull << 31)) return nullptr;
@@ -3607,8 +3658,11 @@ cq_table* run_join(DevCtx& c, cq_node* q, const cqgpu_table* L, const cqgpu_tabl
     RowPlan RP;
     if (rows) compile_rows(&J, q, C, RP);
     else compile_aggregate(&J, q, C);
-    if (!part && !rows && nj == 1 && lv[0].keyed && !lv[0].outer_left && !lv[0].outer_right) {
-        cq_table* fj = run_fast_join(c, q, C, L, lv[0].R, lv[0].kl, lv[0].kr, lv[0].nleft);
+    if (!rows && nj == 1 && lv[0].keyed && !lv[0].outer_left && !lv[0].outer_right &&
+        !(part && getenv("CQ_AMD_NO_PART_FAST_JOIN"))) {
+        // (partials: the STAR form only, its groups globalised into *part)
+        cq_table* fj = run_fast_join(c, q, C, L, lv[0].R, lv[0].kl, lv[0].kr, lv[0].nleft, part, &J.names);
+        if (fj == JOIN_PART_DONE) return nullptr;
         if (fj) return fj;
     }
     // columns each level needs, from the last level back
@@ -4457,6 +4511,11 @@ cqgpu_table* cqgpu_table_from_routed(const void* dev_bytes, size_t n, const uint
         HIPCHECK(hipMalloc((void**)&t->gids, std::max<size_t>(nrec, 1) * 8));
         if (nrec) HIPCHECK(hipMemcpyAsync(t->gids, dev_gids, nrec * 8, hipMemcpyDeviceToDevice, c.stream));
         t->ngids = nrec;
+        // the plan-time sample (a STAR join's key range guess and tag seed)
+        if (n) {
+            t->sample.resize((size_t)std::min<uint64_t>(n, SAMPLE_BYTES));
+            HIPCHECK(hipMemcpyAsync(&t->sample[0], dev_bytes, t->sample.size(), hipMemcpyDeviceToHost, c.stream));
+        }
         HIPCHECK(hipStreamSynchronize(c.stream));
         return t;
     } catch (HipError& e) {

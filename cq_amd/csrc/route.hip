@@ -176,6 +176,23 @@ __global__ void key_pick_kernel(const unsigned long long* __restrict__ key, cons
     const uint32_t i = blockIdx.x * blockDim.x + threadIdx.x;
     if (i < n) out[i] = key[pidx[i]];
 }
+// the record holding byte offset q[i] (its start: the last record start <= q[i], by
+// binary search over the file-order starts) -> its global id (routed tables) or index
+__global__ void offset_gid_kernel(const unsigned long long* __restrict__ starts, unsigned long long n,
+                                  const unsigned long long* __restrict__ q, uint32_t nq,
+                                  const unsigned long long* __restrict__ gids, unsigned long long* __restrict__ out) {
+    const uint32_t i = blockIdx.x * blockDim.x + threadIdx.x;
+    if (i >= nq) return;
+    const unsigned long long o = q[i];
+    unsigned long long lo = 0, hi = n;                  // first start > o
+    while (lo < hi) {
+        const unsigned long long mid = (lo + hi) >> 1;
+        if (starts[mid] <= o) lo = mid + 1;
+        else hi = mid;
+    }
+    const unsigned long long idx = lo ? lo - 1 : 0;
+    out[i] = n == 0 ? ~0ull : (gids ? gids[idx] : idx);
+}
 __global__ void key_flagged_kernel(const unsigned long long* __restrict__ key, unsigned long long np,
                                    const unsigned int* __restrict__ flags, const unsigned int* __restrict__ pos,
                                    unsigned long long* __restrict__ out) {
@@ -337,6 +354,12 @@ hipError_t cq_launch_key_pick(const unsigned long long* key, const unsigned long
                               unsigned long long* out, hipStream_t s) {
     if (!n) return hipSuccess;
     key_pick_kernel<<<blocks(n, 256), 256, 0, s>>>(key, pidx, n, out);
+    return hipGetLastError();
+}
+hipError_t cq_launch_offset_gid(const unsigned long long* starts, unsigned long long n, const unsigned long long* q,
+                               uint32_t nq, const unsigned long long* gids, unsigned long long* out, hipStream_t s) {
+    if (!nq) return hipSuccess;
+    offset_gid_kernel<<<blocks(nq, 256), 256, 0, s>>>(starts, n, q, nq, gids, out);
     return hipGetLastError();
 }
 hipError_t cq_launch_key_flagged(const unsigned long long* key, unsigned long long np, const unsigned int* flags,

@@ -37,6 +37,9 @@ def _shards(data: bytes, nranks: int, seed: int):
     return header, tabs
 
 
+LAST_KINDS = []   # per rank, the scan kernel kind of its partial (4: the STAR fused join)
+
+
 def _run(ast, ldata: bytes, rdata: bytes, nranks: int, rest=()):
     """rest: a chain's later JOIN tables, whole on every rank"""
     lh, ls = _shards(ldata, nranks, 1)
@@ -66,7 +69,11 @@ def _run(ast, ldata: bytes, rdata: bytes, nranks: int, rest=()):
             cq_amd.table_set_record_total(routed[d][side], total)
     whole = [[cq_amd.Table.from_bytes(x) for x in rest] for _ in range(nranks)]
     try:
-        blobs = [cq_amd.query_partial(ast, routed[d] + whole[d]) for d in range(nranks)]
+        blobs = []
+        LAST_KINDS.clear()
+        for d in range(nranks):
+            blobs.append(cq_amd.query_partial(ast, routed[d] + whole[d]))
+            LAST_KINDS.append(cq_amd.stats().get("scan_kernel"))
         tp = cq_amd.merge_partials(ast, blobs)
     finally:
         for t in ls + rs + [x for pr in routed for x in pr] + [x for w in whole for x in w]:
@@ -173,6 +180,27 @@ def test_repartitioned_join(files, case, nranks):
         cq_amd.result_free(tp)
         tol = tolerant_columns(ast)
     compare(got, want, tol, f"{sql} @ {nranks} ranks")
+
+
+@pytest.mark.parametrize("nranks", [1, 2, 3, 8])
+def test_repartitioned_fused_join(files, nranks):
+    """config 5's shape after the key repartition: every rank joins its routed sides
+    with the STAR fused join (key-indexed build, no pair array) and reports its groups'
+    first pairs by global left id; the merge must equal the oracle's nested loop"""
+    data, paths = files
+    sql = (f"SELECT u.role, COUNT(*), SUM(o.price), AVG(o.price) FROM '{paths['users']}' AS u "
+           f"JOIN '{paths['orders']}' AS o ON u.id = o.customer_id GROUP BY u.role")
+    want, unsup = cqtest.oracle_query(sql)
+    assert not unsup
+    with cqtest.Parsed(sql) as ast:
+        tp = _run(ast, data["users"], data["orders"], nranks)
+        assert tp, cq_amd.last_error()
+        kinds = list(LAST_KINDS)
+        got = abi.table_to_py(tp)
+        cq_amd.result_free(tp)
+        tol = tolerant_columns(ast)
+    compare(got, want, tol, f"{sql} @ {nranks} ranks")
+    assert all(k == 4 for k in kinds), kinds
 
 
 CHAINS = [
