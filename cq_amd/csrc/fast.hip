@@ -136,6 +136,15 @@ __device__ __forceinline__ uint32_t vreg(uint32_t x) {
     asm volatile("" : "+v"(x));
     return x;
 }
+// the same for a 64-bit value or a pointer (cold-path operands: the loop's scalar
+// registers stay for its own state instead of spilling into VGPR lanes)
+__device__ __forceinline__ uint64_t vreg64(uint64_t x) {
+    uint32_t lo = (uint32_t)x, hi = (uint32_t)(x >> 32);
+    asm volatile("" : "+v"(lo), "+v"(hi));
+    return (uint64_t)lo | ((uint64_t)hi << 32);
+}
+template <class T>
+__device__ __forceinline__ T* vptr(T* p) { return (T*)(uintptr_t)vreg64((uint64_t)(uintptr_t)p); }
 // the classifier's constants (VGPRs)
 struct CK {
     uint32_t tn1, tn0, td1, td0;   // v_perm tables: terminators, delimiter
@@ -493,7 +502,17 @@ __global__ __launch_bounds__(LT) void fast_kernel(const uint8_t* __restrict__ g,
     ck.w1 = vreg(0x80402010u);
     ck.rd = vreg(fp.delim * 0x01010101u);
     ck.rq = vreg(rep_q);
-    const uint64_t first_win = fp.first_win;
+    const uint64_t first_win = fp.first_win;    // (scalar: the window loads' base)
+#ifndef FAST_SR
+#ifdef FAST_VPTR   // experiment (round 4): 17 -> 10 SGPR spills, +8 VGPRs, ~1 % slower in a same-box A/B
+    if constexpr (!WN) {     // (the wide-numeral builds need those VGPRs themselves)
+        stats = vptr(stats);
+        slow_list = vptr(slow_list);
+        slow_cap = vreg64(slow_cap);
+        tabs = vptr(tabs);
+    }
+#endif
+#endif
     const uint32_t nwin = __builtin_amdgcn_readfirstlane(fp.nwin);
     const uint32_t wsb = __builtin_amdgcn_readfirstlane(fp.ws);
 #ifndef FAST_SR

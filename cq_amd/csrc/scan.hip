@@ -286,7 +286,11 @@ __device__ void parse_cols_out_staged(const uint8_t* tile, uint32_t lim, const u
             if (!g_field(S, i, delim, quote, fs, flen)) {
                 ended = true;
             } else {
-                c = parse_cell(rec + fs, flen);
+                // typed from the staged copy when the field and the byte after it are
+                // staged (the number scans stop there); a STRING keeps its HBM address
+                const bool st = fs + flen < lim;
+                c = parse_cell(st ? tile + fs : rec + fs, flen);
+                if (st && c.kind == K_STR) c.bits = c.bits - (uint64_t)(uintptr_t)tile + (uint64_t)(uintptr_t)rec;
                 if (S.at(i) == delim) { i = i + 1; col++; }
                 else ended = true;
             }
@@ -2836,21 +2840,33 @@ __global__ __launch_bounds__(FP_T) void finish_pack_kernel(const uint8_t* __rest
     __shared__ Cell wcell[FP_W][MAX_WIDE + MAX_ACC + 1];
     const uint32_t ng = min(*count, cap_out);
     const uint32_t tid = threadIdx.x, lane = tid & 63, wv = tid >> 6;
-    const uint32_t i = blockIdx.x * FP_W + wv;                  // this wave's group
-    if (blockIdx.x == 0 && tid == 0) {
-        const uint32_t nw = (uint32_t)(sizeof(ScanStats) / 4);
-        for (uint32_t k = 0; k < nw; k++) ((uint32_t*)hdr)[k] = ((const uint32_t*)stats)[k];
-        *(uint32_t*)(hdr + sizeof(ScanStats)) = ng;
+    {   // the mailbox header (host memory over PCIe): one store instruction across lanes,
+        // not a serial loop of small writes the wave must drain before it ends
+        constexpr uint32_t nw = (uint32_t)(sizeof(ScanStats) / 4);
+        static_assert(nw + 1 <= 64, "mailbox header in one wave store");
+        if (blockIdx.x == 0 && tid <= nw)
+            ((uint32_t*)hdr)[tid] = tid < nw ? ((const uint32_t*)stats)[tid] : ng;
     }
     if (blockIdx.x * FP_W >= ng) return;                       // (uniform)
     for (int k = (int)tid; k < D.ncols; k += FP_T) scols[k] = D.cols[k];
     __syncthreads();
-    if (i >= ng) return;                                        // (wave-uniform)
+    // grid-stride over the groups, one wave each (a bounded grid: every launched wave
+    // reserves the kernel's scratch, which the rare exact-strtod path needs)
+    for (uint32_t i = blockIdx.x * FP_W + wv; i < ng; i += gridDim.x * FP_W) {
     const unsigned long long fi = ofirst[i];
     uint32_t r = 0;
-    for (uint32_t k = lane; k < ng; k += 64) {
-        const unsigned long long f = ofirst[k];
-        r += (f < fi) | ((f == fi) & (k < i));
+    for (uint32_t k0 = 0; k0 < ng; k0 += 64 * 8) {      // eight loads in flight per lane
+        unsigned long long f[8];
+#pragma unroll
+        for (int j = 0; j < 8; j++) {
+            const uint32_t k = k0 + 64u * j + lane;
+            f[j] = k < ng ? ofirst[k] : ~0ull;
+        }
+#pragma unroll
+        for (int j = 0; j < 8; j++) {
+            const uint32_t k = k0 + 64u * j + lane;
+            r += (k < ng) & ((f[j] < fi) | ((f[j] == fi) & (k < i)));
+        }
     }
     for (int o = 32; o > 0; o >>= 1) r += (uint32_t)__shfl_xor((int)r, o, 64);
     const int nacc = D.nacc;
@@ -2912,6 +2928,8 @@ __global__ __launch_bounds__(FP_T) void finish_pack_kernel(const uint8_t* __rest
         const uint32_t m = x.len < D.sb ? x.len : D.sb;
         for (uint32_t j = lane; j < m; j += 64) db[(size_t)c * D.sb + j] = sp[j];
     }
+    __builtin_amdgcn_wave_barrier();
+    }
 }
 }  // namespace cq
 }  // extern "C++"
@@ -2919,7 +2937,8 @@ hipError_t cq_launch_finish_pack(const uint8_t* g, uint64_t n, const cq::GroupOu
                                  const unsigned int* count, unsigned int cap_out, const cq::FinishDesc* D, uint8_t* dst,
                                  const cq::ScanStats* stats, uint8_t* hdr, hipStream_t s) {
     if (cap_out > cq::FP_MAX || D->sb % 16) return hipErrorInvalidValue;
-    hipLaunchKernelGGL(cq::finish_pack_kernel, dim3((cap_out + cq::FP_W - 1) / cq::FP_W), dim3(cq::FP_T), 0, s, g, n,
+    const unsigned quads = (cap_out + cq::FP_W - 1) / cq::FP_W;
+    hipLaunchKernelGGL(cq::finish_pack_kernel, dim3(quads < 512u ? quads : 512u), dim3(cq::FP_T), 0, s, g, n,
                        out, ofirst, count, cap_out, *D, dst, stats, hdr);
     return hipGetLastError();
 }
