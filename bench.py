@@ -72,7 +72,8 @@ def parse_args():
     ap.add_argument("--no-config2", action="store_true", help="skip the config-2 (filter + COUNT) key")
     ap.add_argument("--no-config5", action="store_true", help="skip the config-5 (users x orders join) key")
     ap.add_argument("--join-rows", type=int, default=62_500_000,
-                    help="users and orders rows of the config-5 leg (one rank's share of 500 M x 500 M over 8)")
+                    help="users and orders rows per rank of the config-5 leg (500 M x 500 M over 8)")
+    ap.add_argument("--join-ranks", type=int, default=8, help="ranks the config-5 inputs are routed over")
     ap.add_argument("--gen-workers", type=int, default=4, help="processes generating this rank's rows")
     ap.add_argument("--traffic", default=os.path.join(ROOT, "profiles", "hbm_traffic.json"))
     ap.add_argument("--config", type=int, default=3, choices=(2, 3),
@@ -461,65 +462,35 @@ def end_to_end(data, config, L, cq_amd, exp, rows):
 
 
 def config5_leg(args, cq_amd, L):
-    """configs[4] at one rank's share: users x orders, `--join-rows` rows each (62.5 M:
-    500 M x 500 M over 8 GPUs), SELECT u.role, COUNT(*), SUM(o.price) ... JOIN ... GROUP BY
-    u.role through cqgpu_query (the fused aggregate join), verified per role against the
-    generators' draws; roofline bytes = both CSVs (SURVEY.md 8d: no repartition at one rank);
-    CPU baseline: the reference's nested-loop join at 5 K x 5 K and 20 K x 20 K."""
+    """configs[4] as one rank of the 8-GPU node runs it: users x orders of 500 M rows
+    each (`--join-rows` x `--join-ranks`), generated on the device, routed by the
+    product's key routing (whole keys by key mod N) into 8 shards on this one GPU, each
+    shard rebuilt as its rank receives it; rank 0's cqgpu_query_partial (the STAR fused
+    join over its routed 62.5 M + 62.5 M rows with key stride 8) is the timed step.
+    Every rank's partial runs once and their merge is verified against the exact
+    per-role COUNT / SUM(price) and group order of the generators' draws.  Roofline
+    bytes: the rank's two routed CSV shards, HBM traffic from
+    profiles/config5_traffic.json when it was measured for this shape.  CPU baseline:
+    the reference's nested-loop join at 5 K x 5 K and 20 K x 20 K."""
     import ctypes as C
-    import numpy as np
     import bench_join as bj
     from cq_amd import abi
-    n = args.join_rows
-    t0 = time.time()
-    rng = np.random.default_rng([args.seed, 0])
-    uh, oh = b"id,name,age,role\n", b"id,price,quantity,customer_id\n"
-    ub = uh + bj.users_shard(n, 0, rng)
-    ob = oh + bj.orders_shard(n, 0, n, rng)
-    ut = cq_amd.Table.from_bytes(ub)
-    ot = cq_amd.Table.from_bytes(ob)
-    nb = len(ub) + len(ob)
-    del ub, ob
-    gen_s = time.time() - t0
+    n, N = args.join_rows, args.join_ranks
     P = abi.Plan()
     q = P.query([P.ident("u.role"), P.func("COUNT", P.lit("*")), P.func("SUM", P.ident("o.price"))],
                 "users.csv", alias="u", group_by=["u.role"],
                 joins=[("orders.csv", "o", P.cond("=", P.ident("u.id"), P.ident("o.customer_id")), abi.JOIN_INNER)])
     ast = C.pointer(q)
-    arr = (C.c_void_p * 2)(ut.handle.value, ot.handle.value)
-    for _ in range(args.warmup):
-        cq_amd.result_free(L.cqgpu_query(ast, arr, 2))
-    torch.cuda.synchronize()
-    ms, last, st = [], None, {}
-    t1 = time.perf_counter()
-    for _ in range(args.steps):
-        tp = L.cqgpu_query(ast, arr, 2)
-        if not tp:
-            raise RuntimeError(cq_amd.last_error() or cq_amd.last_ineligible())
-        st = cq_amd.stats()
-        ms.append(st["scan_ms"])
-        if last:
-            cq_amd.result_free(last)
-        last = tp
-    torch.cuda.synchronize()
-    el = time.perf_counter() - t1
-    res = abi.table_to_py(last)
-    cq_amd.result_free(last)
-    ut.close()
-    ot.close()
-    cnt, cents = bj.expected_roles(n, n, args.seed)
-    got = {r[0][1].decode(): (r[1][1], r[2][1]) for r in res["rows"]}
-    ok = len(got) == int((cnt > 0).sum())
-    for k in range(1000):
-        if not cnt[k]:
-            continue
-        g = got.get("role_%03d" % k)
-        want = cents[k] / 100.0
-        if g is None or g[0] != cnt[k] or abs(g[1] - want) > 1e-6 * want:
-            ok = False
-            break
-    step_s = el / args.steps
-    kms = sum(ms) / len(ms)
+    r = bj.routed_share_leg(n * N, N, args.steps, args.warmup, args.seed, torch.device("cuda"), ast)
+    step_s = r["step_s"]
+    traffic = None
+    try:
+        with open(os.path.join(ROOT, "profiles", "config5_traffic.json")) as fh:
+            tj = json.load(fh)
+        if tj.get("rows_total") == n * N and tj.get("ranks") == N:
+            traffic = tj.get("hbm_bytes_per_step")
+    except Exception:
+        pass
     cpu = None
     if not args.no_cpu:
         cpu = {}
@@ -528,21 +499,26 @@ def config5_leg(args, cq_amd, L):
                 cpu["%dx%d" % (m, m)] = bj.cpu_baseline(m, args.seed)
             except Exception as e:
                 cpu["%dx%d" % (m, m)] = {"error": str(e)}
-    return {"workload": "config5 (one rank's share): SELECT u.role, COUNT(*), SUM(o.price) FROM users u "
-                        "JOIN orders o ON u.id = o.customer_id GROUP BY u.role",
-            "users": n, "orders": n, "bytes": nb,
-            "value": 2 * n / step_s, "unit": "rows/s (users + orders rows)", "ms_per_step": step_s * 1e3,
-            "kernel_ms": kms,
-            "kernel": {4: "cq::fast::jx_extract_kernel<STAR> build + probe, jx_star_first_kernel, jx_star_flush_kernel "
-                          "(+ raw_merge)",
-                       3: "cq::fast::jx_extract_kernel x 4, jx_build_direct_kernel, jx_probe_kernel (+ raw_merge)"}
-                      .get(st.get("scan_kernel"), "general join pipeline"),
-            "roofline": {"bound": "hbm", "achieved": nb / step_s / 1e9, "peak": HBM_PEAK_GBS, "unit": "GB/s",
-                         "frac": nb / step_s / 1e9 / HBM_PEAK_GBS, "traffic": None,
-                         "algorithmic_bytes": "both CSV files read once (SURVEY.md 8d; one rank: no repartition)"},
-            "joined_pairs": int(cnt.sum()),
-            "verified": ok, "verified_against": "per-role COUNT / SUM(price) from the generators' draws (numpy)",
-            "cpu_baseline": cpu, "setup_s": round(gen_s, 2)}
+    return {"workload": "config5 (rank 0 of %d after the key repartition): SELECT u.role, COUNT(*), SUM(o.price) "
+                        "FROM users u JOIN orders o ON u.id = o.customer_id GROUP BY u.role" % N,
+            "users_total": n * N, "orders_total": n * N, "ranks": N,
+            "rank_rows": r["rows"], "rank_bytes": r["bytes"], "rows_per_rank": r["rank_rows"],
+            "value": r["rows"] / step_s, "unit": "rows/s (rank 0's routed users + orders rows)",
+            "ms_per_step": step_s * 1e3, "kernel_ms": r["kernel_ms"],
+            "step": "cqgpu_query_partial on rank 0's routed shards (STAR join build + probe + flush, "
+                    "first-pair global ids, partial blob); not included: the all-to-all and the merge",
+            "kernel": {4: "cq::fast::jx_extract_kernel<STAR> build + probe (key stride %d), jx_star_first_kernel, "
+                          "jx_star_flush_kernel (+ raw_merge)" % N}.get(r["kinds"][0], "general join pipeline"),
+            "kernel_kinds_per_rank": r["kinds"],
+            "roofline": {"bound": "hbm", "achieved": r["bytes"] / step_s / 1e9, "peak": HBM_PEAK_GBS, "unit": "GB/s",
+                         "frac": r["bytes"] / step_s / 1e9 / HBM_PEAK_GBS, "traffic": traffic,
+                         "algorithmic_bytes": "rank 0's routed users + orders CSV shards read once (SURVEY.md 8d)"},
+            "route_whole_inputs_s": r["route_s"],
+            "joined_pairs": r["joined_pairs"],
+            "verified": r["verified"],
+            "verified_against": "every rank's partial merged (cqgpu_merge_partials) vs the exact per-role COUNT / "
+                                "SUM(price) and first-appearance order of the generators' draws (torch, on device)",
+            "cpu_baseline": cpu, "setup_s": round(r["gen_s"], 2)}
 
 
 def config2_leg(args, cq_amd, abi, L, data):

@@ -91,6 +91,160 @@ def expected_roles(users: int, orders: int, seed: int):
     return np.bincount(r, minlength=1000), np.bincount(r, weights=price, minlength=1000)
 
 
+def _digits_t(v, w: int):
+    """int64 tensor -> [n, w] uint8 ASCII digits (zero padded), on v's device"""
+    import torch
+    out = torch.empty((v.numel(), w), dtype=torch.uint8, device=v.device)
+    x = v.clone()
+    for k in range(w - 1, -1, -1):
+        out[:, k] = (torch.remainder(x, 10) + 48).to(torch.uint8)
+        x = torch.div(x, 10, rounding_mode="floor")
+    return out
+
+
+def gen_config5_device(n: int, seed: int, device):
+    """BASELINE config 5's whole inputs on the device (torch's Philox generator):
+    n users `10^10+i,<6 letters>,<10-80>,role_<000-999>` and n orders
+    `10^10+i,<ddd.dd>,<1-9>,10^10+U[0, n)` as '\n'-terminated records (no header),
+    plus per role the exact COUNT and SUM(price) in cents of the join and the
+    first matched user of each role (the groups' first-appearance order)."""
+    import torch
+    g = torch.Generator(device=device)
+    g.manual_seed(seed)
+    ri = lambda lo, hi: torch.randint(lo, hi, (n,), generator=g, device=device, dtype=torch.int64)  # noqa: E731
+    ids = torch.arange(n, dtype=torch.int64, device=device) + 10**10
+    u = torch.empty((n, 31), dtype=torch.uint8, device=device)
+    u[:, 0:11] = _digits_t(ids, 11)
+    u[:, 11] = 44
+    u[:, 12:18] = ri(65, 81).to(torch.uint8)[:, None]
+    u[:, 18] = 44
+    u[:, 19:21] = _digits_t(ri(10, 81), 2)
+    u[:, 21] = 44
+    u[:, 22:27] = torch.tensor(list(b"role_"), dtype=torch.uint8, device=device)
+    role = ri(0, 1000)
+    u[:, 27:30] = _digits_t(role, 3)
+    u[:, 30] = 10
+    o = torch.empty((n, 33), dtype=torch.uint8, device=device)
+    o[:, 0:11] = _digits_t(ids, 11)
+    o[:, 11] = 44
+    price = ri(100, 100000)
+    o[:, 12:15] = _digits_t(torch.div(price, 100, rounding_mode="floor"), 3)
+    o[:, 15] = 46
+    o[:, 16:18] = _digits_t(torch.remainder(price, 100), 2)
+    o[:, 18] = 44
+    o[:, 19] = (ri(1, 10) + 48).to(torch.uint8)
+    o[:, 20] = 44
+    cust = ri(0, n)
+    o[:, 21:32] = _digits_t(cust + 10**10, 11)
+    o[:, 32] = 10
+    del ids
+    r = role[cust]
+    cnt = torch.bincount(r, minlength=1000).cpu().numpy()
+    cents = torch.bincount(r, weights=price.to(torch.float64), minlength=1000).cpu().numpy()
+    matched = torch.zeros(n, dtype=torch.bool, device=device)
+    matched[cust] = True
+    idx = torch.nonzero(matched).squeeze(1)
+    first = torch.full((1000,), n, dtype=torch.int64, device=device)
+    first.scatter_reduce_(0, role[idx], idx, reduce="amin")
+    first = first.cpu().numpy()
+    del r, matched, idx, cust, price, role
+    return u.reshape(-1), o.reshape(-1), cnt, cents, first
+
+
+def routed_share_leg(n_total: int, nranks: int, steps: int, warmup: int, seed: int, device, ast, check_order=True):
+    """BASELINE config 5 as a rank of an `nranks`-GPU node runs it, on one GPU: the whole
+    n_total x n_total inputs are generated on the device, routed with the product's
+    own key routing (cqgpu_route_plan / cqgpu_route_fill: whole keys by key mod N)
+    into `nranks` shards, and each shard is rebuilt as that rank would receive it
+    (cqgpu_table_from_routed: its records in file order with global ids, key stride N,
+    record total).  Rank 0's cqgpu_query_partial is timed (warmup + steps; everything
+    but the exchange and the merge); every rank's partial runs once and
+    cqgpu_merge_partials must reproduce the exact per-role answer and group order."""
+    import ctypes as C
+    import torch
+    import cq_amd
+    from cq_amd import abi
+    uh, oh = b"id,name,age,role\n", b"id,price,quantity,customer_id\n"
+    t0 = time.time()
+    ub, ob, cnt, cents, first = gen_config5_device(n_total, seed, device)
+    torch.cuda.synchronize(device)
+    gen_s = time.time() - t0
+    gids = torch.arange(n_total, dtype=torch.int64, device=device)
+    U = cq_amd.table_from_routed(ub.data_ptr(), ub.numel(), gids.data_ptr(), n_total, uh)
+    O = cq_amd.table_from_routed(ob.data_ptr(), ob.numel(), gids.data_ptr(), n_total, oh)
+    if not U or not O:
+        raise RuntimeError(cq_amd.last_error())
+    del ub, ob, gids
+    torch.cuda.empty_cache()
+    sends = []
+    t0 = time.perf_counter()
+    for side, tab in enumerate((U, O)):
+        nb, nr = cq_amd.route_plan(ast, [U, O], side, nranks)
+        sb = torch.empty(max(sum(nb), 1), dtype=torch.uint8, device=device)
+        sg = torch.empty(max(sum(nr), 1), dtype=torch.int64, device=device)
+        cq_amd.route_fill(tab, 0, sb.data_ptr(), sg.data_ptr())
+        torch.cuda.synchronize(device)
+        sends.append((sb, sg, np.concatenate([[0], np.cumsum(nb)]).astype(np.int64),
+                      np.concatenate([[0], np.cumsum(nr)]).astype(np.int64)))
+    route_s = time.perf_counter() - t0
+    U.close()
+    O.close()
+    rank_rows = [int(sends[0][3][d + 1] - sends[0][3][d]) + int(sends[1][3][d + 1] - sends[1][3][d])
+                 for d in range(nranks)]
+    blobs, kinds, rank_bytes = [], [], []
+    ms = []
+    step_s = None
+    for d in range(nranks):
+        tabs = []
+        nbytes = 0
+        for (sb, sg, bo, ro), hdr in zip(sends, (uh, oh)):
+            rb, rg = sb[int(bo[d]):int(bo[d + 1])], sg[int(ro[d]):int(ro[d + 1])]
+            t = cq_amd.table_from_routed(rb.data_ptr(), rb.numel(), rg.data_ptr(), rg.numel(), hdr)
+            if not t:
+                raise RuntimeError(cq_amd.last_error())
+            cq_amd.table_set_record_total(t, n_total)
+            cq_amd.table_set_key_stride(t, nranks)
+            tabs.append(t)
+            nbytes += rb.numel()
+        rank_bytes.append(nbytes)
+        if d == 0:
+            for _ in range(warmup):
+                cq_amd.query_partial(ast, tabs)
+            torch.cuda.synchronize(device)
+            t1 = time.perf_counter()
+            for _ in range(steps):
+                blob = cq_amd.query_partial(ast, tabs)
+                ms.append(cq_amd.stats()["scan_ms"])
+            torch.cuda.synchronize(device)
+            step_s = (time.perf_counter() - t1) / steps
+        else:
+            blob = cq_amd.query_partial(ast, tabs)
+        kinds.append(cq_amd.stats()["scan_kernel"])
+        blobs.append(blob)
+        for t in tabs:
+            t.close()
+    del sends
+    torch.cuda.empty_cache()
+    tp = cq_amd.merge_partials(ast, blobs)
+    if not tp:
+        raise RuntimeError(cq_amd.last_error())
+    res = abi.table_to_py(tp)
+    cq_amd.result_free(tp)
+    ok = all(k == 4 for k in kinds)
+    rows = res["rows"]
+    want = [r for r in np.argsort(first, kind="stable") if cnt[r] > 0]
+    ok = ok and len(rows) == len(want)
+    for row, r in zip(rows, want if ok else []):
+        name = row[0][1].decode() if isinstance(row[0][1], bytes) else row[0][1]
+        ws = cents[r] / 100.0
+        if (check_order and name != "role_%03d" % r) or row[1][1] != cnt[r] or abs(row[2][1] - ws) > 1e-6 * ws:
+            ok = False
+            break
+    return {"step_s": step_s, "kernel_ms": sum(ms) / len(ms), "rows": rank_rows[0], "bytes": rank_bytes[0],
+            "rank_rows": rank_rows, "kinds": kinds, "verified": ok, "route_s": route_s, "gen_s": gen_s,
+            "joined_pairs": int(cnt.sum())}
+
+
 def cpu_baseline(n: int, seed: int):
     """The unmodified reference (oracle/_ref/ref_probe, 1 core) on an n x n sample of
     the same generators.  Its nested-loop join is O(L x R) (evaluator_joins.c:63-181),

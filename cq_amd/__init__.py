@@ -82,6 +82,8 @@ def lib():
         L.cqgpu_route_fill.argtypes = [C.c_void_p, C.c_uint64, C.c_void_p, C.c_void_p]
         L.cqgpu_table_set_record_total.restype = C.c_int
         L.cqgpu_table_set_record_total.argtypes = [C.c_void_p, C.c_uint64]
+        L.cqgpu_table_set_key_stride.restype = C.c_int
+        L.cqgpu_table_set_key_stride.argtypes = [C.c_void_p, C.c_uint32]
         L.cqgpu_table_from_routed.restype = C.c_void_p
         L.cqgpu_table_from_routed.argtypes = [C.c_void_p, C.c_size_t, C.c_void_p, C.c_size_t, abi.CsvConfig,
                                               C.c_char_p, C.c_size_t]
@@ -244,6 +246,13 @@ def table_from_routed(dev_bytes_ptr: int, nbytes: int, dev_gids_ptr: int, nrec: 
     """A join side rebuilt from received records (device memory) and their global ids."""
     return Table(lib().cqgpu_table_from_routed(dev_bytes_ptr, nbytes, dev_gids_ptr, nrec,
                                                cfg or abi.csv_config(), header, len(header)))
+
+
+def table_set_key_stride(table: "Table", stride: int) -> None:
+    """A routed table's join-key stride: the rank count of the key-mod-N routing
+    (cqgpu_table_set_key_stride; the STAR join then indexes keys by (key - kmin) / N)."""
+    if lib().cqgpu_table_set_key_stride(table.handle, stride) != 0:
+        raise RuntimeError(last_error() or "cqgpu_table_set_key_stride failed")
 
 
 def table_set_record_total(table: "Table", total: int) -> None:

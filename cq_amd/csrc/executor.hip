@@ -176,7 +176,7 @@ hipError_t cq_jx_build_direct(const unsigned long long* key, const unsigned long
 size_t cq_jx_direct_bytes();
 hipError_t cq_jx_star_extract(const uint8_t* g, uint64_t lo, uint64_t hi, uint32_t ws, uint32_t delim, uint32_t quote,
                               int kcol, int pcol, int build, unsigned long long kmin, unsigned long long range,
-                              uint16_t* d16, uint32_t* l32, unsigned long long* ttab,
+                              uint32_t stride, uint16_t* d16, uint32_t* l32, unsigned long long* ttab,
                               unsigned long long* gsum, unsigned long long* counter, unsigned int* flag,
                               unsigned long long* krange, uint32_t* notmono, unsigned long long* wfl,
                               uint32_t* gminix, int rp, int grid, hipStream_t s);
@@ -531,6 +531,10 @@ struct cqgpu_table {
     // per join-key column: its canonical INTEGER keys' [min, max], learned by a STAR
     // join's build pass (the table is immutable) -- the next build sizes its arrays by it
     std::map<int, std::pair<uint64_t, uint64_t>> key_range;
+    // routed tables (cqgpu_table_set_key_stride): the canonical INTEGER join keys were
+    // routed by key mod key_stride, so this rank's keys are one residue class -- a
+    // STAR join indexes them by (key - kmin) / key_stride
+    uint32_t key_stride = 1;
     unsigned long long* gids = nullptr;   // routed tables: global record id of each record (device)
     uint64_t ngids = 0;
     uint64_t gid_total = 0;               // routed tables: records of the whole input (every rank's share)
@@ -3150,8 +3154,11 @@ unsigned long long build_pairs(DevCtx& c, JoinSide& A, JoinSide& B, int kl, int 
 
 // The canonical INTEGER keys (jx_key's shape) of column `col` in the table's sampled
 // bytes: their [min, max] widened to cover the records the whole table is estimated to
-// hold (a guess: a key outside it only costs the STAR join a second round)
-bool sample_key_range(const cqgpu_table* t, int col, uint64_t* kmin, uint64_t* kmax, uint64_t* est) {
+// hold (a guess: a key outside it only costs the STAR join a second round).  S: the
+// table's key stride (1, or N on a rank of a key-mod-N repartition): the keys are one
+// residue class mod S, so the estimated records span est * S key units, and kmin
+// stays in the sampled keys' class
+bool sample_key_range(const cqgpu_table* t, int col, uint64_t S, uint64_t* kmin, uint64_t* kmax, uint64_t* est) {
     const std::string& s = t->sample;
     const char delim = (char)t->cfg.delimiter;
     uint64_t lo = ~0ull, hi = 0, nrec = 0, used = 0;
@@ -3183,13 +3190,13 @@ bool sample_key_range(const cqgpu_table* t, int col, uint64_t* kmin, uint64_t* k
         lo = std::min(lo, v);
         hi = std::max(hi, v);
     }
-    if (!nrec || lo > hi || !used) return false;
+    if (!nrec || lo > hi || !used || S == 0) return false;
     const uint64_t n = t->n > t->data_begin ? t->n - t->data_begin : 0;
     *est = (uint64_t)((double)n * (double)nrec / (double)used) + 1;
-    const uint64_t span = std::max<uint64_t>(hi - lo, *est);
-    const uint64_t pad = span / 8 + 16;
-    *kmin = lo > pad ? lo - pad : 0;
-    *kmax = std::max(hi, *kmin + span + span / 4 + 1024);
+    const uint64_t span = std::max<uint64_t>(hi - lo, *est * S);
+    const uint64_t pad = (span / 8 / S + 16) * S;
+    *kmin = lo > pad ? lo - pad : lo % S;
+    *kmax = std::max(hi, *kmin + span + span / 4 + 1024 * S);
     return true;
 }
 
@@ -3385,20 +3392,23 @@ cq_table* run_fast_join(DevCtx& c, cq_node* q, Compiled& C, const cqgpu_table* L
         cqgpu_table* Lm = const_cast<cqgpu_table*>(L);
         for (int round = 0; round < 2; round++) {
             uint64_t kmin = 0, kmax = 0, est = 0;
+            const uint64_t S = L->key_stride ? L->key_stride : 1;
             auto it = Lm->key_range.find(kl);
             const bool learned = it != Lm->key_range.end();
             if (learned) {
                 kmin = it->second.first;
                 kmax = it->second.second;
-                est = kmax - kmin + 1;
-            } else if (!sample_key_range(L, kl, &kmin, &kmax, &est)) {
+                est = kmax >= kmin ? (kmax - kmin) / S + 1 : 0;
+            } else if (!sample_key_range(L, kl, S, &kmin, &kmax, &est)) {
                 JXDBG("star: no sampled keys\n");
                 break;
             }
-            const uint64_t range = kmax - kmin + 1;
-            JXDBG("star round %d: keys [%llu, %llu] est %llu learned %d\n", round, (unsigned long long)kmin,
-                  (unsigned long long)kmax, (unsigned long long)est, (int)learned);
-            if (kmax < kmin || range >= (1ull << 31) || range > 4 * est + 1024) break;
+            // key slots: kmin, kmin + S, ... (the table's keys are one residue class mod S)
+            const uint64_t range = kmax >= kmin ? (kmax - kmin) / S + 1 : 0;
+            JXDBG("star round %d: keys [%llu, %llu] stride %llu slots %llu est %llu learned %d\n", round,
+                  (unsigned long long)kmin, (unsigned long long)kmax, (unsigned long long)S, (unsigned long long)range,
+                  (unsigned long long)est, (int)learned);
+            if (kmax < kmin || range >= (1ull << 31) || range * S >= (1ull << 32) || range > 4 * est + 1024) break;
             const size_t b16 = (range * 2 + 15) & ~(size_t)15;
             DevBuf big(b16), l32(range * 4 + 16);
             const uint32_t G = cq_jx_star_groups();
@@ -3432,11 +3442,11 @@ cq_table* run_fast_join(DevCtx& c, cq_node* q, Compiled& C, const cqgpu_table* L
             HIPCHECK(cq_jx_star_init(big.p, b16, small.p, o_ctl + 64, (uint32_t)o_first, (uint32_t)o_ctl,
                                      (uint32_t)o_ctl + 32, seed, seed ? (size_t)G * 8 : 0, c.ncu * 4, c.stream));
             HIPCHECK(hipEventRecord(c.ev0, c.stream));
-            HIPCHECK(cq_jx_star_extract(L->g, L->data_begin, L->n, wsl3, d, dq, kl, grouped ? gcol : -1, 1, kmin, range, d16,
+            HIPCHECK(cq_jx_star_extract(L->g, L->data_begin, L->n, wsl3, d, dq, kl, grouped ? gcol : -1, 1, kmin, range, (uint32_t)S, d16,
                                         l32.as<uint32_t>(), ttab, gsum, cnts, sflag, skr, snotmono,
                                         wfl.as<unsigned long long>(), nullptr, rpl, xgrid, c.stream));
             HIPCHECK(cq_jx_star_order(wfl.as<unsigned long long>(), nwb, snotmono, c.stream));
-            HIPCHECK(cq_jx_star_extract(R->g, R->data_begin, R->n, wsr3, d, dq, kr, vcol, 0, kmin, range, d16,
+            HIPCHECK(cq_jx_star_extract(R->g, R->data_begin, R->n, wsr3, d, dq, kr, vcol, 0, kmin, range, (uint32_t)S, d16,
                                         l32.as<uint32_t>(), ttab, gsum, cnts + 1, sflag, nullptr, snotmono, nullptr,
                                         gminix, rpr, xgrid, c.stream));
             HIPCHECK(cq_jx_star_first(d16, l32.as<uint32_t>(), range, snotmono, gfirst, cnts + 2, c.ncu * 4, c.stream));
@@ -4533,6 +4543,17 @@ cqgpu_table* cqgpu_table_from_routed(const void* dev_bytes, size_t n, const uint
     }
 }
 
+int cqgpu_table_set_key_stride(cqgpu_table* t, uint32_t stride) {
+    g_err.clear();
+    if (!t || stride == 0) {
+        set_err("cq_amd: %s", "key stride must be at least 1");
+        return -1;
+    }
+    t->key_stride = stride;
+    t->key_range.clear();                   // learned ranges assumed the old stride
+    return 0;
+}
+
 int cqgpu_table_set_record_total(cqgpu_table* t, uint64_t total) {
     g_err.clear();
     if (!t || total < t->ngids) {
@@ -4950,6 +4971,7 @@ size_t cqgpu_query_partial(cq_node* q, cqgpu_table* const* tables, int ntables, 
     if (blob_out) *blob_out = nullptr;
     g_inel.clear();
     g_err.clear();
+    memset(&g_stats, 0, sizeof g_stats);     // per call: a caller reads this call's path / kernel kind
     try {
         DevCtx& c = ctx();
         bump_reset(c);
@@ -5106,6 +5128,7 @@ size_t cqgpu_query_partial(cq_node* q, cqgpu_table* const* tables, int ntables, 
 }
 
 cq_table* cqgpu_merge_partials(cq_node* q, const void* const* blobs, const size_t* sizes, int nblobs) {
+    memset(&g_stats, 0, sizeof g_stats);
     g_inel.clear();
     g_err.clear();
     try {
@@ -5490,6 +5513,7 @@ struct cqgpu_partial {
 };
 
 cqgpu_partial* cqgpu_partial_new(cq_node* q, cqgpu_table* const* tables, int ntables) {
+    memset(&g_stats, 0, sizeof g_stats);
     g_inel.clear();
     g_err.clear();
     std::unique_ptr<cqgpu_partial> p(new cqgpu_partial);
@@ -6223,6 +6247,7 @@ uint32_t gm_local_part(DevCtx& c, const cqgpu_table* t, Compiled& C, uint8_t* ds
         HIPCHECK(hipMemsetAsync(dst, 0, GM_HDR, c.stream));
         Literals L;
         ScanStats st;
+        memset(&st, 0, sizeof st);   // run_aggregate returns early (group_missing) without writing it
         GmSend gs;
         gs.dst = dst;
         gs.maxg = GM_MAXG;
@@ -6312,13 +6337,21 @@ cq_table* gm_finish_root(DevCtx& c, cq_node* q, Compiled& C, const uint8_t* mail
     return res;
 }
 
-// the gather-merge step; returns GM_OK (rank 0: *res), GM_DECLINE, or throws PeerFail
-uint32_t dist_gm(DevCtx& c, DistComm& m, cq_node* q, const cqgpu_table* t, cq_table** res) {
+// the gather-merge step; returns GM_OK (rank 0: *res), GM_DECLINE, or throws PeerFail.
+// `D` is the plan-only compile of dist_path -- identical on every rank -- so every
+// rank derives the same per-rank send size B from it (a rank whose own compile threw
+// partway still sends and receives exactly B bytes).  Rank 0 runs the merge AND
+// builds the result before it broadcasts its final status, so a throw anywhere on
+// rank 0 (merge launch, literals, result table, post-ops) becomes GM_FAILED on every
+// rank after the same collectives, never a hang or a one-sided failure.
+uint32_t dist_gm(DevCtx& c, DistComm& m, cq_node* q, const cqgpu_table* t, const Compiled& D, cq_table** res) {
     Compiled C;
     std::string err;
     uint32_t mine = GM_OK;
     try {
         compile_aggregate(t, q, C);
+        if (C.P.nacc != D.P.nacc || C.rep_cols.size() != D.rep_cols.size())
+            throw HipError{"gather-merge: the table's compile differs from the plan's"};
     } catch (Ineligible& e) {
         err = e.why;
         mine = GM_FAILED;
@@ -6327,10 +6360,14 @@ uint32_t dist_gm(DevCtx& c, DistComm& m, cq_node* q, const cqgpu_table* t, cq_ta
         mine = GM_FAILED;
     }
     const uint32_t N = (uint32_t)m.world;
-    const uint64_t B = gm_rank_bytes(C);
+    const uint64_t B = gm_rank_bytes(D);
     DistBufs& db = dist_bufs();
     uint8_t* recv = m.rank == 0 ? grow(db.recv, db.recv_b, B * N) : nullptr;
     uint8_t* dst = m.rank == 0 ? recv : grow(db.send, db.send_b, B);
+    if (mine == GM_OK && getenv("CQGPU_TEST_GM_FAIL_PART")) {      // test knob: this rank's part fails
+        err = "gather-merge: injected local failure (CQGPU_TEST_GM_FAIL_PART)";
+        mine = GM_FAILED;
+    }
     if (mine == GM_OK) {
         mine = gm_local_part(c, t, C, dst, err);
     } else {
@@ -6346,13 +6383,41 @@ uint32_t dist_gm(DevCtx& c, DistComm& m, cq_node* q, const cqgpu_table* t, cq_ta
         NCCLCHECK(ncclSend(dst, B, ncclUint8, 0, m.comm, c.stream));
     }
     NCCLCHECK(ncclGroupEnd());
-    GmRoot g;
-    if (m.rank == 0) g = gm_merge_launch(c, C, recv, B, N);
-    const uint32_t st = bcast_status(c, m, g.dstatus);
-    if (st == GM_FAILED)
-        throw PeerFail{mine == GM_FAILED ? err : std::string("a peer rank failed")};
+    uint32_t fin = GM_OK;                               // rank 0: the final status
+    std::string rerr;
+    if (m.rank == 0) {
+        try {
+            GmRoot g = gm_merge_launch(c, D, recv, B, N);   // (D: every rank's layout, even if C threw)
+            HIPCHECK(hipStreamSynchronize(c.stream));
+            memcpy(&fin, g.mail + sizeof(ScanStats) + 4, 4);   // the merge's status word (mailbox)
+            if (fin == GM_OK) {
+                if (getenv("CQGPU_TEST_GM_FAIL_FINISH")) throw HipError{"gather-merge: injected finish failure"};
+                *res = gm_finish_root(c, q, C, g.mail);
+            } else if (fin != GM_DECLINE) {
+                fin = GM_FAILED;
+                rerr = mine == GM_FAILED ? err : std::string("a peer rank failed");
+            }
+        } catch (HipError& e) {
+            fin = GM_FAILED;
+            rerr = e.msg;
+        } catch (Ineligible& e) {
+            fin = GM_FAILED;
+            rerr = e.why;
+        } catch (std::exception& e) {
+            fin = GM_FAILED;
+            rerr = e.what();
+        }
+        (void)hipGetLastError();
+        if (fin != GM_OK && *res) { cqgpu_result_free(*res); *res = nullptr; }
+        db.hword[8] = fin;
+        HIPCHECK(hipMemcpyAsync(db.word.as<uint32_t>() + 12, db.hword + 8, 4, hipMemcpyHostToDevice, c.stream));
+    }
+    const uint32_t st = bcast_status(c, m, db.word.as<uint32_t>() + 12);
+    if (st == GM_FAILED) {
+        if (*res) { cqgpu_result_free(*res); *res = nullptr; }
+        throw PeerFail{m.rank == 0 ? rerr : (mine == GM_FAILED ? err : std::string("a peer rank failed"))};
+    }
     if (st == GM_DECLINE) return GM_DECLINE;
-    if (m.rank == 0) *res = gm_finish_root(c, q, C, g.mail);
     return GM_OK;
 }
 
@@ -6562,13 +6627,12 @@ void dist_blob(DevCtx& c, DistComm& m, cq_node* q, cqgpu_table* t, cq_table** re
 
 // the merge the plan takes, decided from the AST and the header alone (no device
 // work: a table copy without its sample), so every rank decides the same
-int dist_path(cq_node* q, const cqgpu_table* t) {
+int dist_path(cq_node* q, const cqgpu_table* t, Compiled& D) {
     cqgpu_table shadow;
     shadow.names = t->names;
     shadow.cfg = t->cfg;
     check_plan_shape(q, &shadow);
     if (is_row_query(q)) return DP_BLOB;
-    Compiled D;
     compile_aggregate(&shadow, q, D);
     if (gm_eligible(D)) return DP_GM;
     return dense_eligible(D) ? DP_DENSE : DP_BLOB;
@@ -6645,8 +6709,9 @@ cq_table* cqgpu_dist_query(cq_node* q, cqgpu_table* t, int* status, int* path) {
         DistComm& m = dist_comm();
         bump_reset(c);
         const double t0 = now_ms();
-        int dp = dist_path(q, t);                        // Ineligible: the same on every rank
-        if (dp == DP_GM && dist_gm(c, m, q, t, &res) == GM_DECLINE) dp = DP_DENSE;
+        Compiled D;
+        int dp = dist_path(q, t, D);                     // Ineligible: the same on every rank
+        if (dp == DP_GM && dist_gm(c, m, q, t, D, &res) == GM_DECLINE) dp = DP_DENSE;
         if (dp == DP_DENSE && dist_dense(c, m, q, t, &res) != 0) dp = DP_BLOB;
         if (dp == DP_BLOB) dist_blob(c, m, q, t, &res);
         if (path) *path = dp;
@@ -6679,7 +6744,8 @@ cq_table* cqgpu_gm_local(cq_node* q, cqgpu_table* const* shards, int n) {
         if (n < 1 || !shards) throw HipError{"gm_local: no shards"};
         DevCtx& c = ctx();
         bump_reset(c);
-        if (dist_path(q, shards[0]) != DP_GM) throw Ineligible{"gather-merge: plan outside it"};
+        Compiled D;
+        if (dist_path(q, shards[0], D) != DP_GM) throw Ineligible{"gather-merge: plan outside it"};
         Compiled C;
         compile_aggregate(shards[0], q, C);
         const uint64_t B = gm_rank_bytes(C);

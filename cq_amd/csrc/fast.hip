@@ -1130,7 +1130,11 @@ struct JxOut {
     // STAR passes (jx_star_*): no record arrays; the build side goes straight into
     // key-indexed arrays over [kmin, kmin + range), the probe side aggregates in place
     unsigned long long kmin, range;
-    uint16_t* d16;             // build: group id + 1 of key kmin + i (0: no build record);
+    // key stride S = 2^sshift * m (m odd, sinv = m^-1 mod 2^32): slot i holds key
+    // kmin + i S.  A table routed by key mod N (route.hip) holds on rank d only keys
+    // = d (mod N): dense with stride N.  S = 1: sshift 0, smask 0, sinv 1.
+    uint32_t sshift, smask, sinv;
+    uint16_t* d16;             // build: group id + 1 of key kmin + i S (0: no build record);
                                // probe: | 0x8000 once a probe record met it
     uint32_t* l32;             // build: that record's byte offset
     unsigned long long* ttab;  // build: GROUP BY raw tags, slot = group id (0: free)
@@ -1141,6 +1145,17 @@ struct JxOut {
     unsigned long long* wfl;   // build: per window its first and last key (order check)
     uint32_t* gminix;          // probe: per group id the smallest matched key index
 };
+// a key's STAR slot (k - kmin) / S when k = kmin (mod S) and the slot is below 2^32,
+// else ~0 (never < range: the host keeps range * S < 2^32).  Exact division by the
+// odd part through its inverse: for x divisible by m, (x * m^-1) mod 2^32 = x / m;
+// for any other x it is above (2^32 - 1) / m >= range (Granlund-Montgomery)
+__device__ __forceinline__ unsigned long long jx_slot(unsigned long long k, const JxOut& jo) {
+    const unsigned long long x = k - jo.kmin;
+    const uint32_t lo = (uint32_t)x;
+    const uint32_t q = (lo >> jo.sshift) * jo.sinv;
+    return ((x >> 32) == 0ull && (lo & jo.smask) == 0u) ? (unsigned long long)q : ~0ull;
+}
+
 // STAR flags (JxOut.flag): 8 a NULL build key, 16 a key outside [kmin, kmin + range),
 // 32 more GROUP BY tags than JX_G, 64 a repeated build key (placed != occupied)
 constexpr uint32_t JX_G = 2048;           // group ids of a STAR join (LDS sums per block)
@@ -1450,7 +1465,7 @@ __global__ __launch_bounds__(LT) void jx_extract_kernel(const uint8_t* __restric
                 fail[u] |= !jx_key(d0, d1, d2, d3, ke - ks, key[u]);
 #ifndef JX_LATE_LOOK
                 if constexpr (SPROBE) {    // (out of range or NULL: slot 0, not used)
-                    const unsigned long long ix = key[u] - jo.kmin;
+                    const unsigned long long ix = jx_slot(key[u], jo);
                     gpre[u] = jo.d16[ix < jo.range ? ix : 0ull];
                 }
 #endif
@@ -1504,7 +1519,7 @@ __global__ __launch_bounds__(LT) void jx_extract_kernel(const uint8_t* __restric
                 for (int u = 0; u < RP; u++) {
                     if (!valid[u] || fail[u]) continue;
                     const unsigned long long k = key[u];
-                    const unsigned long long ix = k - jo.kmin;
+                    const unsigned long long ix = jx_slot(k, jo);
                     if (BUILD) {
                         if (k == JX_NULLKEY) { sflag |= 8u; continue; }
                         kmin = k < kmin ? k : kmin;
@@ -2211,7 +2226,7 @@ hipError_t cq_jx_extract(const uint8_t* g, uint64_t lo, uint64_t hi, uint32_t ws
 // counter: build records placed (build) / pairs (probe).
 hipError_t cq_jx_star_extract(const uint8_t* g, uint64_t lo, uint64_t hi, uint32_t ws, uint32_t delim, uint32_t quote,
                               int kcol, int pcol, int build, unsigned long long kmin, unsigned long long range,
-                              uint16_t* d16, uint32_t* l32, unsigned long long* ttab,
+                              uint32_t stride, uint16_t* d16, uint32_t* l32, unsigned long long* ttab,
                               unsigned long long* gsum, unsigned long long* counter, unsigned int* flag,
                               unsigned long long* krange, uint32_t* notmono, unsigned long long* wfl,
                               uint32_t* gminix, int rp, int grid, hipStream_t s) {
@@ -2239,6 +2254,15 @@ hipError_t cq_jx_star_extract(const uint8_t* g, uint64_t lo, uint64_t hi, uint32
     jo.krange = krange;
     jo.kmin = kmin;
     jo.range = range;
+    if (stride == 0 || (unsigned long long)stride * range >= (1ull << 32)) return hipErrorInvalidValue;
+    jo.sshift = (uint32_t)__builtin_ctz(stride);
+    jo.smask = (1u << jo.sshift) - 1u;
+    {
+        const uint32_t m = stride >> jo.sshift;     // odd: Newton's iteration for m^-1 mod 2^32
+        uint32_t inv = m;                           // (correct to 3 bits; each step doubles them)
+        for (int k = 0; k < 4; k++) inv *= 2u - m * inv;
+        jo.sinv = inv;
+    }
     jo.d16 = d16;
     jo.l32 = l32;
     jo.ttab = ttab;

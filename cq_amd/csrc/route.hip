@@ -1,7 +1,8 @@
 // route.hip -- join-key repartition for the multi-GPU JOIN.
 //
 // Each rank holds a contiguous byte range of both join inputs.  Every record is
-// sent to rank hash(key class, key code) mod N, so all records whose keys can be
+// sent to rank (whole number key) mod N or hash(key class, key code) mod N
+// (route_dest), so all records whose keys can be
 // equal under value_compare (reference csv_reader.c:98-130, evaluator_joins.c:40-60)
 // meet on one rank: the code is join_code (scan.hip) -- the double bits for
 // INTEGER/DOUBLE (they compare as doubles), the (y, m, d) word for DATE, the FNV
@@ -24,6 +25,19 @@ __device__ __forceinline__ uint64_t mix64(uint64_t x) {      // splitmix64 final
     x ^= x >> 30; x *= 0xbf58476d1ce4e5b9ull;
     x ^= x >> 27; x *= 0x94d049bb133111ebull;
     return x ^ (x >> 31);
+}
+
+// A key's rank.  Numbers that are whole, non-negative and below 2^53 go to
+// (value mod N): every rank then holds one residue class of the integer keys, so a
+// dense key range (a primary key) stays dense with stride N on every rank and the
+// STAR join indexes it directly (cqgpu_table_set_key_stride).  INTEGER 7 and DOUBLE
+// 7.0 have the same code (join_code: the double bits), so they still meet.  Every
+// other key (strings, dates, fractions, negatives) by a hash of (class, code).
+__device__ __forceinline__ uint32_t route_dest(uint64_t code, uint32_t cls, uint32_t nranks) {
+    const double v = __longlong_as_double((long long)code);
+    if (cls == 1u && v >= 0.0 && v < 9007199254740992.0 && v == __builtin_floor(v))
+        return (uint32_t)((uint64_t)v % nranks);
+    return (uint32_t)(mix64(code ^ ((uint64_t)cls << 62)) % nranks);
 }
 
 // record length (through the terminator, which becomes '\n') and destination rank
@@ -59,7 +73,7 @@ __global__ void route_len_kernel(const uint8_t* __restrict__ g, const unsigned l
         drop = 0;
     }
     len[i] = (uint32_t)(pos - st) + 1;
-    dest[i] = (uint32_t)(mix64(codes[i] ^ ((uint64_t)cls[i] << 62)) % nranks);
+    dest[i] = route_dest(codes[i], cls[i], nranks);
 }
 
 // per-destination record and byte starts from the destination-sorted layout

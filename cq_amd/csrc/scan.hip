@@ -487,35 +487,50 @@ struct ExtLds {         // ACC_MIN / ACC_MAX
 };
 
 
-// find or insert the slot of key k (hash h); -1 if the probe window is full
-__device__ __forceinline__ int l_insert(const LdsTable& t, const GKey& k, uint64_t h) {
+// find or insert the slot of key k (hash h) for the lanes with `need`; -1 if the
+// probe window is full (the HBM table takes the record).  Wave-uniform (the rule
+// above): a slot another lane has claimed but not yet published is retried on
+// the next trip instead of spun on, so a lane never waits on a lane of its own
+// wave -- a per-lane spin here could run its full bound whenever the compiler
+// schedules the waiting lanes before the claiming one.  A claimer publishes in
+// the trip it claims, so every pending lane advances within a few trips; the
+// trip bound only turns a kernel bug into spilled records, never into a hang.
+__device__ __forceinline__ int l_insert(bool need, const LdsTable& t, const GKey& k, uint64_t h) {
     const uint32_t hd = lds_hdr(k, h);
     const v4u kk = key_words(k);
     // H need not be a power of two (the host fits as many slots as LDS holds): the
     // window starts at the hash's low 24 bits (gk_hash's best mixed) scaled into [0, H)
     uint32_t i = __umulhi((uint32_t)h << 8, t.H);
-    for (uint32_t probe = 0; probe < 32; probe++, i = i + 1 == t.H ? 0u : i + 1) {
-        uint32_t cur = __hip_atomic_load(&t.hdr[i], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
-        if (cur == hd && key_match(k, kk, t.key[i])) return (int)i;   // the common case: one round trip
-        if (cur == 0) {
-            const uint32_t old = atomicCAS(&t.hdr[i], 0u, 1u);
-            if (old == 0) {
-                t.key[i] = kk;
-                __hip_atomic_store(&t.hdr[i], hd, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_WORKGROUP);
-                return (int)i;
+    uint32_t probe = 0;
+    int s = -1;
+    for (uint32_t trip = 0; __any(need); trip++) {
+        if (need) {
+            uint32_t cur = __hip_atomic_load(&t.hdr[i], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
+            if (cur == 0) {
+                const uint32_t old = atomicCAS(&t.hdr[i], 0u, 1u);
+                if (old == 0) {
+                    t.key[i] = kk;
+                    __hip_atomic_store(&t.hdr[i], hd, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_WORKGROUP);
+                    s = (int)i;
+                    need = false;
+                }
+                cur = old;
             }
-            cur = old;
+            if (need && cur != 1) {                     // a published key: compare
+                __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "workgroup");
+                if (cur == hd && key_match(k, kk, t.key[i])) {
+                    s = (int)i;
+                    need = false;
+                } else if (++probe >= 32) {
+                    need = false;                       // window full: s stays -1
+                } else {
+                    i = i + 1 == t.H ? 0u : i + 1;
+                }
+            }
         }
-        for (uint32_t spin = 0; cur == 1; spin++) {
-            if (spin > (1u << 20)) return -1;           // the HBM table takes the record
-            cur = __hip_atomic_load(&t.hdr[i], __ATOMIC_ACQUIRE, __HIP_MEMORY_SCOPE_WORKGROUP);
-        }
-        if (cur == hd) {                                // published meanwhile: re-read the key
-            __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "workgroup");
-            if (key_match(k, kk, t.key[i])) return (int)i;
-        }
+        if (trip > (1u << 20)) break;                   // never hang: pending lanes spill
     }
-    return -1;
+    return s;
 }
 
 // wave-uniform LDS MIN/MAX update (see g_ext_update).  The slot's lock word is a
@@ -527,7 +542,7 @@ __device__ __forceinline__ int l_insert(const LdsTable& t, const GKey& k, uint64
 // over every address space would also wait for the window prefetch in flight.
 __device__ __forceinline__ uint64_t lds_pos(uint32_t code) { return code == 0xFFFFFFFFu ? NOPOS : code; }
 __device__ __forceinline__ void lds_ext_update(bool need, const ExtLds& e, uint32_t s, uint8_t kind,
-                                               const Cell c, uint32_t pos) {
+                                               const Cell c, uint32_t pos, ScanStats* st) {
 #ifdef CQ_AB_EXT_SKIP   // A/B build: no MIN/MAX update at all (results wrong)
     return;
 #endif
@@ -543,7 +558,11 @@ __device__ __forceinline__ void lds_ext_update(bool need, const ExtLds& e, uint3
         if (!(v1 & 1u) && v1 == v2 && !ext_better(kind, c, pos, cur, cp)) need = false;
     }
 #endif
-    while (__any(need)) {
+    // a lane holds the lock only inside the trip that took it, so a trip never
+    // waits on a holder that cannot run; the bound turns a lock word left odd (a
+    // kernel bug) into a reported error (overflow 2: the query fails loudly)
+    // instead of a hang
+    for (uint32_t trips = 0; __any(need); trips++) {
         if (need) {
             const uint32_t v = __hip_atomic_load(lk, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
             if (!(v & 1u) && atomicCAS(lk, v, v + 1u) == v) {
@@ -556,6 +575,10 @@ __device__ __forceinline__ void lds_ext_update(bool need, const ExtLds& e, uint3
                 __hip_atomic_store(lk, v + 2u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
                 need = false;
             }
+        }
+        if (trips > (1u << 20)) {
+            if (need) atomicExch(&st->overflow, 2ULL);
+            break;
         }
     }
 }
@@ -940,16 +963,12 @@ __global__ __launch_bounds__(SCAN_T) void scan_kernel(const uint8_t* __restrict_
                         }
                     }
                 } else {
-                    uint64_t h = 0;
-                    int s = -1;
-                    if (pass) {
-                        h = gk_hash(key);
+                    const uint64_t h = pass ? gk_hash(key) : 0;
 #ifdef CQ_NO_INSERT   // profiling build: direct-mapped slot, results wrong
-                        s = (int)__umulhi((uint32_t)h << 8, H);
+                    const int s = pass ? (int)__umulhi((uint32_t)h << 8, H) : -1;
 #else
-                        s = l_insert(lt, key, h);
+                    const int s = l_insert(pass, lt, key, h);    // the whole wave (uniform loop)
 #endif
-                    }
                     const bool in_lds = pass && s >= 0;
                     const bool spill = pass && s < 0;
                     if (in_lds) {
@@ -972,7 +991,7 @@ __global__ __launch_bounds__(SCAN_T) void scan_kernel(const uint8_t* __restrict_
                             Cell c = av[a];
                             if (c.kind == K_STR) c.bits = c.bits - tile_g + gt0;
                             lds_ext_update(in_lds && c.kind != K_NULL, le[a], in_lds ? (uint32_t)s : 0u,
-                                           P.acc[a].kind, c, (iter << 15) | pos);
+                                           P.acc[a].kind, c, (iter << 15) | pos, stats);
                         }
                     }
                     if (__any(spill)) {

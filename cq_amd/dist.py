@@ -344,7 +344,8 @@ def join_partitioned(ast, lshard, rshard, lheader: bytes, rheader: bytes, device
         t, err = _local(cq_amd.table_from_routed, rb.data_ptr(), rb.numel(), rg.data_ptr(), rg.numel(), header)
         if t is not None:
             _, e2 = _local(cq_amd.table_set_record_total, t, total)
-            err = err or e2
+            _, e3 = _local(cq_amd.table_set_key_stride, t, world)   # whole keys routed by key mod N
+            err = err or e2 or e3
         agree(err, comm)
         routed.append(t)
     blob, err = _local(cq_amd.query_partial, ast, routed + list(rest))

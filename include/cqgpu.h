@@ -202,6 +202,12 @@ cqgpu_table* cqgpu_table_from_routed(const void* dev_bytes, size_t n, const uint
  * mixed-radix keys over it (route.hip chain_key_kernel).  -1 if below the table's
  * own record count.  A chain's later tables are passed whole to query_partial. */
 int cqgpu_table_set_record_total(cqgpu_table* t, uint64_t total);
+/* A routed table's key stride: cqgpu_route_plan sends whole-number keys to rank
+ * (key mod N), so each rank holds one residue class of them; with stride N the
+ * STAR join indexes a dense key range by (key - kmin) / N instead of declining it
+ * as sparse (the reference's perform_join, evaluator_joins.c:63-181, is unaffected:
+ * the stride only sizes the key-indexed arrays).  -1 for stride 0. */
+int cqgpu_table_set_key_stride(cqgpu_table* t, uint32_t stride);
 
 /* ---- output ----------------------------------------------------------------
  * replaces write_csv_file (reference utils.c:220-289, called by main.c:133 for

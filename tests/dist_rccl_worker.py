@@ -14,7 +14,7 @@ sys.path.insert(0, os.path.dirname(os.path.abspath(__file__)))
 
 
 def main():
-    path, out, sqls = sys.argv[1], sys.argv[2], json.loads(sys.argv[3])
+    out, items = sys.argv[1], json.loads(sys.argv[2])     # items: [[sql, path], ...]
     rank, world = int(os.environ["RANK"]), int(os.environ["WORLD_SIZE"])
     local = int(os.environ.get("LOCAL_RANK", "0"))
     torch.cuda.set_device(local)
@@ -24,9 +24,10 @@ def main():
     from cq_amd import abi
     from cq_amd.dist import init_library_comm
     init_library_comm()
-    t = cq_amd.Table.open_range(path, rank, world)
     results = []
-    for sql in sqls:
+    for sql, path in items:
+        print(f"dist worker: {sql.format(p=path)}", file=sys.stderr, flush=True)   # (a failure names its query)
+        t = cq_amd.Table.open_range(path, rank, world)
         with cqtest.Parsed(sql.format(p=path)) as ast:
             got = None
             for _ in range(2):                      # a warm-up step, then the kept one
@@ -41,7 +42,7 @@ def main():
             results.append({"sql": sql, "status": status, "path": p, "error": cq_amd.last_error(),
                             "result": None if got in (None, "none") else
                             {"columns": got["columns"], "rows": [[list(c) for c in r] for r in got["rows"]]}})
-    t.close()
+        t.close()
     cq_amd.comm_destroy()
     if rank == 0:
         with open(out, "w") as fh:

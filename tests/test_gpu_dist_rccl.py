@@ -122,13 +122,17 @@ def test_gm_local_declines(files):
 
 
 # ---------------------------------------------------------------- cqgpu_dist_query over RCCL, one rank
-DIST = [
-    (GM[0], 1),
-    (GM[2], 1),
-    ("SELECT role, MIN(height), MAX(name), COUNT(*) FROM '{p}' WHERE age > 30 GROUP BY role", 2),
-    ("SELECT gender, role, COUNT(*), STDDEV(height) FROM '{p}' GROUP BY gender, role", 2),
-    ("SELECT role, MEDIAN(age) FROM '{p}' GROUP BY role", 3),
-    ("SELECT name, age FROM '{p}' WHERE age > 78 AND height < 1.05", 3),
+DIST = [   # (sql, the merge path it must take, the file)
+    (GM[0], 1, "plain"),
+    (GM[2], 1, "plain"),
+    ("SELECT role, MIN(height), MAX(name), COUNT(*) FROM '{p}' WHERE age > 30 GROUP BY role", 2, "plain"),
+    ("SELECT gender, role, COUNT(*), STDDEV(height) FROM '{p}' GROUP BY gender, role", 2, "plain"),
+    ("SELECT role, MEDIAN(age) FROM '{p}' GROUP BY role", 3, "plain"),
+    ("SELECT name, age FROM '{p}' WHERE age > 78 AND height < 1.05", 3, "plain"),
+    # gather-merge plans the DATA declines: more than GM_MAXG groups on a
+    # rank, texts over GM_TEXT bytes -- every rank falls to the dense merge together
+    ("SELECT k, COUNT(*), SUM(v) FROM '{p}' GROUP BY k", 2, "many"),
+    ("SELECT k, COUNT(*) FROM '{p}' GROUP BY k", 2, "verylong"),
 ]
 
 
@@ -142,16 +146,22 @@ def _cell(c):
     return (c[0], c[1].encode("latin-1")) if c[0] == "S" else tuple(c)
 
 
-def test_dist_query_one_rank_rccl(files, tmp_path):
+def _dist_run(files, tmp_path, items, env=None):
     out = str(tmp_path / "dist.json")
     cmd = [sys.executable, "-m", "torch.distributed.run", "--nnodes=1", "--nproc-per-node=1",
            "--master-addr", "127.0.0.1", "--master-port", str(_port()), os.path.join(ROOT, "tests", "dist_rccl_worker.py"),
-           files["plain"], out, json.dumps([s for s, _ in DIST])]
-    p = subprocess.run(cmd, cwd=ROOT, capture_output=True, text=True, timeout=110)
-    assert p.returncode == 0, p.stderr[-3000:]
-    res = json.load(open(out))
-    for (sql, path), r in zip(DIST, res):
-        q = sql.format(p=files["plain"])
+           out, json.dumps([[s, files[f]] for s, f in items])]
+    e = dict(os.environ)
+    e.update(env or {})
+    p = subprocess.run(cmd, cwd=ROOT, capture_output=True, text=True, timeout=110, env=e)
+    assert p.returncode == 0, p.stderr[:6000] + "\n...\n" + p.stderr[-2000:]
+    return json.load(open(out))
+
+
+def test_dist_query_one_rank_rccl(files, tmp_path):
+    res = _dist_run(files, tmp_path, [(s, f) for s, _, f in DIST])
+    for (sql, path, f), r in zip(DIST, res):
+        q = sql.format(p=files[f])
         assert r["status"] == 0, (q, r["error"])
         assert r["path"] == path, (q, r["path"])
         want, _ = cqtest.oracle_query(q)
@@ -160,3 +170,14 @@ def test_dist_query_one_rank_rccl(files, tmp_path):
         with cqtest.Parsed(q) as ast:
             tol = tolerant_columns(ast)
         compare(got, want, tol, f"dist_query path {path}: {q}")
+
+
+@pytest.mark.parametrize("knob", ["CQGPU_TEST_GM_FAIL_PART", "CQGPU_TEST_GM_FAIL_FINISH"])
+def test_dist_query_gather_merge_failure_reported(files, tmp_path, knob):
+    """a rank-local failure in the gather-merge -- this rank's part, or rank 0's result
+    build after the merge kernels -- is status -1 with the message on every rank after
+    the same collectives (rank 0 now builds its result before it broadcasts
+    the final status), never a hang"""
+    res = _dist_run(files, tmp_path, [(GM[0], "plain")], env={knob: "1"})
+    assert res[0]["status"] == -1, res[0]
+    assert "injected" in res[0]["error"], res[0]["error"]

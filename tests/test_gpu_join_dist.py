@@ -67,6 +67,7 @@ def _run(ast, ldata: bytes, rdata: bytes, nranks: int, rest=()):
             torch.cuda.synchronize()          # torch's copies before the library's stream reads them
             routed[d][side] = cq_amd.table_from_routed(rb.data_ptr(), rb.numel(), rg.data_ptr(), rg.numel(), hdr)
             cq_amd.table_set_record_total(routed[d][side], total)
+            cq_amd.table_set_key_stride(routed[d][side], nranks)
     whole = [[cq_amd.Table.from_bytes(x) for x in rest] for _ in range(nranks)]
     try:
         blobs = []
@@ -182,11 +183,14 @@ def test_repartitioned_join(files, case, nranks):
     compare(got, want, tol, f"{sql} @ {nranks} ranks")
 
 
-@pytest.mark.parametrize("nranks", [1, 2, 3, 8])
+@pytest.mark.parametrize("nranks", [1, 2, 3, 5, 8])
 def test_repartitioned_fused_join(files, nranks):
-    """config 5's shape after the key repartition: every rank joins its routed sides
-    with the STAR fused join (key-indexed build, no pair array) and reports its groups'
-    first pairs by global left id; the merge must equal the oracle's nested loop"""
+    """config 5's shape after the key repartition: whole-number keys are routed by key
+    mod N (route.hip route_dest), so every rank's build keys are one dense residue
+    class and every rank joins its routed sides with the STAR fused join (slots
+    (key - kmin) / N, no pair array), reporting its groups' first pairs by global left
+    id; the merge must equal the oracle's nested loop.  g_stats is reset per
+    cqgpu_query_partial call, so a rank whose STAR declined reports kind 0 here"""
     data, paths = files
     sql = (f"SELECT u.role, COUNT(*), SUM(o.price), AVG(o.price) FROM '{paths['users']}' AS u "
            f"JOIN '{paths['orders']}' AS o ON u.id = o.customer_id GROUP BY u.role")
@@ -200,7 +204,66 @@ def test_repartitioned_fused_join(files, nranks):
         cq_amd.result_free(tp)
         tol = tolerant_columns(ast)
     compare(got, want, tol, f"{sql} @ {nranks} ranks")
-    assert all(k == 4 for k in kinds), kinds
+    assert len(kinds) == nranks and all(k == 4 for k in kinds), kinds
+
+
+def test_partial_stats_reset_per_call(files):
+    """a general-join partial after a STAR partial reports its own kernel kind (0),
+    not the stale 4 of the call before"""
+    data, paths = files
+    star = (f"SELECT u.role, COUNT(*), SUM(o.price) FROM '{paths['users']}' AS u "
+            f"JOIN '{paths['orders']}' AS o ON u.id = o.customer_id GROUP BY u.role")
+    gen = (f"SELECT u.role, COUNT(*), MIN(o.price) FROM '{paths['users']}' AS u "
+           f"JOIN '{paths['orders']}' AS o ON u.id = o.customer_id GROUP BY u.role")
+    with cqtest.Parsed(star) as ast:
+        tp = _run(ast, data["users"], data["orders"], 2)
+        assert tp and LAST_KINDS == [4, 4], LAST_KINDS
+        cq_amd.result_free(tp)
+    with cqtest.Parsed(gen) as ast:
+        tp = _run(ast, data["users"], data["orders"], 2)
+        assert tp, cq_amd.last_error()
+        assert LAST_KINDS == [0, 0], LAST_KINDS
+        cq_amd.result_free(tp)
+
+
+def test_repartitioned_fused_join_1m_8_ranks():
+    """1e6 users x 1e6 orders over 8 simulated ranks (no small-table slack in the
+    STAR range test): every rank must take STAR, and the merged result must equal the
+    exact nested-loop answer computed here with numpy (COUNT exact, SUM/AVG 1e-6
+    relative; groups in the order of their first matched user)"""
+    n = 1_000_000
+    users = datagen.users_bytes(n, seed=21)
+    orders = datagen.orders_bytes(n, n, seed=22)
+    rng = np.random.default_rng(21)
+    rng.integers(10, 81, n)
+    role = rng.integers(0, 1000, n)
+    rng2 = np.random.default_rng(22)
+    cust = rng2.integers(0, n, n)
+    price = rng2.integers(100, 100000, n)
+    cnt = np.bincount(role[cust], minlength=1000)
+    cents = np.bincount(role[cust], weights=price, minlength=1000)
+    matched = np.zeros(n, dtype=bool)
+    matched[cust] = True
+    first = np.full(1000, n, dtype=np.int64)
+    np.minimum.at(first, role[matched], np.nonzero(matched)[0])
+    order = [r for r in np.argsort(first, kind="stable") if cnt[r] > 0]
+    sql = ("SELECT u.role, COUNT(*), SUM(o.price), AVG(o.price) FROM 'users.csv' AS u "
+           "JOIN 'orders.csv' AS o ON u.id = o.customer_id GROUP BY u.role")
+    with cqtest.Parsed(sql) as ast:
+        tp = _run(ast, users, orders, 8)
+        assert tp, cq_amd.last_error()
+        kinds = list(LAST_KINDS)
+        got = abi.table_to_py(tp)
+        cq_amd.result_free(tp)
+    assert kinds == [4] * 8, kinds
+    rows = got["rows"]
+    assert len(rows) == len(order)
+    for row, r in zip(rows, order):
+        assert row[0][1] in (b"role_%03d" % r, "role_%03d" % r), (row, r)
+        assert row[1][1] == cnt[r], (row, cnt[r])
+        want_sum = cents[r] / 100.0
+        assert abs(row[2][1] - want_sum) <= 1e-6 * abs(want_sum), (row, want_sum)
+        assert abs(row[3][1] - want_sum / cnt[r]) <= 1e-6 * abs(want_sum / cnt[r]), row
 
 
 CHAINS = [

@@ -423,3 +423,43 @@ def test_mixed_class_minmax_across_ranges(mixed_classes, nranks):
             got = _merged(ast, mixed_classes, nranks)
             tol = tolerant_columns(ast)
         compare(got, want, tol, f"{nranks} ranks: {q}")
+
+
+def _very_long_file(tmp_path):
+    p = tmp_path / "verylong.csv"
+    p.write_text("k,v\n" + "\n".join("%s,%d" % ("x" * 60 + str(i % 5), i % 7) for i in range(20_000)) + "\n")
+    return str(p)
+
+
+def _many_groups_file(tmp_path):
+    p = tmp_path / "many.csv"
+    p.write_text("k,v\n" + "\n".join("%d,%d" % (i % 9000, i % 7) for i in range(40_000)) + "\n")
+    return str(p)
+
+
+@pytest.mark.parametrize("kind", ["verylong", "many"])
+def test_single_gpu_keys_past_gather_merge(tmp_path, kind):
+    """the data the gather-merge declines (group keys over 48 bytes, more than 4096
+    groups) on one GPU, through cqgpu_query: the oracle's answer"""
+    path = _very_long_file(tmp_path) if kind == "verylong" else _many_groups_file(tmp_path)
+    q = f"SELECT k, COUNT(*), SUM(v) FROM '{path}' GROUP BY k"
+    want, _ = cqtest.oracle_query(q)
+    with cqtest.Parsed(q) as ast:
+        got = cq_amd.evaluate(ast)
+        tol = tolerant_columns(ast)
+    assert got is not None, cq_amd.last_error()
+    compare(got, want, tol, q)
+
+
+@pytest.mark.parametrize("kind", ["verylong", "many"])
+@pytest.mark.parametrize("nranks", [1, 3])
+def test_dense_merge_keys_past_gather_merge(tmp_path, kind, nranks):
+    """the same data through the dense merge (where cqgpu_dist_query sends it when
+    the gather-merge declines)"""
+    path = _very_long_file(tmp_path) if kind == "verylong" else _many_groups_file(tmp_path)
+    q = f"SELECT k, COUNT(*), SUM(v) FROM '{path}' GROUP BY k"
+    want, _ = cqtest.oracle_query(q)
+    with cqtest.Parsed(q) as ast:
+        got = _dense(ast, path, nranks)
+        tol = tolerant_columns(ast)
+    compare(got, want, tol, f"dense {nranks} ranks: {q}")
