@@ -301,6 +301,13 @@ def main():
     ms_per_step = elapsed * 1000.0 / args.steps
     value = total / (elapsed / args.steps)
 
+    cfg5_dist = None
+    if world > 1 and not args.no_config5 and dist is not None:
+        # configs[4] at N = world: the repartitioned join step inside the library, every rank
+        try:
+            cfg5_dist = config5_dist_leg(args, rank, world, dist)
+        except Exception as e:
+            print(f"config 5 (N > 1) leg failed: {e}", file=sys.stderr)
     rc = 0
     if rank == 0:
         # ---- the last step's answer against the expected one (outside the timed region)
@@ -341,6 +348,10 @@ def main():
             except Exception as e:
                 print(f"config 2 leg failed: {e}", file=sys.stderr)
         cfg5 = None
+        if world > 1 and cfg5_dist is not None:
+            cfg5 = cfg5_dist
+            if not cfg5["verified"]:
+                rc = 3
         if world == 1 and not args.no_config5:
             if table.handle:
                 table.close()
@@ -519,6 +530,40 @@ def config5_leg(args, cq_amd, L):
             "verified_against": "every rank's partial merged (cqgpu_merge_partials) vs the exact per-role COUNT / "
                                 "SUM(price) and first-appearance order of the generators' draws (torch, on device)",
             "cpu_baseline": cpu, "setup_s": round(r["gen_s"], 2)}
+
+
+def config5_dist_leg(args, rank, world, dist):
+    """configs[4] at N = world (every rank): `--join-rows` users and orders per rank,
+    one step = cqgpu_dist_join (route, exchange over RCCL, STAR join with key stride N,
+    merge on rank 0); value = all ranks' users + orders rows / step time"""
+    import ctypes as C
+    import bench_join as bj
+    from cq_amd import abi
+    P = abi.Plan()
+    q = P.query([P.ident("u.role"), P.func("COUNT", P.lit("*")), P.func("SUM", P.ident("o.price"))],
+                "users.csv", alias="u", group_by=["u.role"],
+                joins=[("orders.csv", "o", P.cond("=", P.ident("u.id"), P.ident("o.customer_id")), abi.JOIN_INNER)])
+    r = bj.dist_join_leg(args.join_rows, rank, world, max(3, args.steps // 4), 1, args.seed,
+                         torch.device("cuda", torch.cuda.current_device()), C.pointer(q), dist)
+    if rank != 0:
+        return None
+    step_s = r["step_s"]
+    return {"workload": "config5 at N = %d: SELECT u.role, COUNT(*), SUM(o.price) FROM users u JOIN orders o "
+                        "ON u.id = o.customer_id GROUP BY u.role" % world,
+            "users_total": args.join_rows * world, "orders_total": args.join_rows * world, "ranks": world,
+            "value": r["rows_total"] / step_s, "unit": "rows/s (all ranks' users + orders rows)",
+            "ms_per_step": step_s * 1e3,
+            "step": "cqgpu_dist_join: device routing (key mod N), grouped ncclSend/ncclRecv of records + "
+                    "global ids per side, rebuilt sides, STAR join (key stride N), partial blobs merged on rank 0",
+            "kernel_kinds_per_rank": r["kinds"],
+            "roofline": {"bound": "hbm", "achieved": r["bytes_per_rank"] / step_s / 1e9, "peak": HBM_PEAK_GBS,
+                         "unit": "GB/s", "frac": r["bytes_per_rank"] / step_s / 1e9 / HBM_PEAK_GBS, "traffic": None,
+                         "algorithmic_bytes": "each rank's two CSV shards read once (the exchange's xGMI bytes "
+                                              "and the routed copies come on top)"},
+            "joined_pairs": r["joined_pairs"], "verified": r["verified"],
+            "verified_against": "per-role COUNT / SUM(price) and first-appearance order of the generators' draws "
+                                "(reduced over ranks)",
+            "setup_s": round(r["gen_s"], 2)}
 
 
 def config2_leg(args, cq_amd, abi, L, data):

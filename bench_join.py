@@ -151,6 +151,130 @@ def gen_config5_device(n: int, seed: int, device):
     return u.reshape(-1), o.reshape(-1), cnt, cents, first
 
 
+def gen_config5_shard_device(n: int, rank: int, world: int, seed: int, device):
+    """rank's shard of BASELINE config 5's inputs on the device: users 10^10 + rank n + i
+    (i < n) and n orders with customer ids uniform over all world * n users; every
+    user's role is drawn from one generator shared by all ranks (so each rank can
+    price its orders' groups), the rest from per-rank generators.  Returns the two
+    '\n'-terminated record buffers and this rank's per-role (COUNT, SUM(price) cents)
+    and matched-user mask over all users (summed / or-ed across ranks by the caller)."""
+    import torch
+    ga = torch.Generator(device=device)
+    ga.manual_seed(seed)
+    role_all = torch.randint(0, 1000, (world * n,), generator=ga, device=device, dtype=torch.int64)
+    g = torch.Generator(device=device)
+    g.manual_seed(seed * 1000 + 17 + rank)
+    ri = lambda lo, hi: torch.randint(lo, hi, (n,), generator=g, device=device, dtype=torch.int64)  # noqa: E731
+    ids = torch.arange(n, dtype=torch.int64, device=device) + 10**10 + rank * n
+    u = torch.empty((n, 31), dtype=torch.uint8, device=device)
+    u[:, 0:11] = _digits_t(ids, 11)
+    u[:, 11] = 44
+    u[:, 12:18] = ri(65, 81).to(torch.uint8)[:, None]
+    u[:, 18] = 44
+    u[:, 19:21] = _digits_t(ri(10, 81), 2)
+    u[:, 21] = 44
+    u[:, 22:27] = torch.tensor(list(b"role_"), dtype=torch.uint8, device=device)
+    u[:, 27:30] = _digits_t(role_all[rank * n:(rank + 1) * n], 3)
+    u[:, 30] = 10
+    o = torch.empty((n, 33), dtype=torch.uint8, device=device)
+    o[:, 0:11] = _digits_t(ids, 11)
+    o[:, 11] = 44
+    price = ri(100, 100000)
+    o[:, 12:15] = _digits_t(torch.div(price, 100, rounding_mode="floor"), 3)
+    o[:, 15] = 46
+    o[:, 16:18] = _digits_t(torch.remainder(price, 100), 2)
+    o[:, 18] = 44
+    o[:, 19] = (ri(1, 10) + 48).to(torch.uint8)
+    o[:, 20] = 44
+    cust = torch.randint(0, world * n, (n,), generator=g, device=device, dtype=torch.int64)
+    o[:, 21:32] = _digits_t(cust + 10**10, 11)
+    o[:, 32] = 10
+    del ids
+    r = role_all[cust]
+    cnt = torch.bincount(r, minlength=1000).to(torch.float64)
+    cents = torch.bincount(r, weights=price.to(torch.float64), minlength=1000)
+    matched = torch.zeros(world * n, dtype=torch.uint8, device=device)
+    matched[cust] = 1
+    return u.reshape(-1), o.reshape(-1), cnt, cents, matched, role_all
+
+
+def dist_join_leg(n: int, rank: int, world: int, steps: int, warmup: int, seed: int, device, ast, dist):
+    """BASELINE config 5 at N = world: every rank holds n users and n orders (device-
+    generated CSV shards), and one step is the whole repartitioned join inside the
+    library (cqgpu_dist_join over its RCCL communicator: routing by key mod N, one
+    grouped send / recv per side, rebuilt sides, the STAR join with key stride N, the
+    partial blobs merged on rank 0).  Timed between barriers, max over ranks; rank 0
+    verifies per-role COUNT / SUM(price) and the group order against the generators'
+    draws (reduced over ranks)."""
+    import torch
+    import cq_amd
+    from cq_amd import abi
+    from cq_amd.dist import join_partitioned_rccl
+    uh, oh = b"id,name,age,role\n", b"id,price,quantity,customer_id\n"
+    t0 = time.time()
+    ub, ob, cnt, cents, matched, role_all = gen_config5_shard_device(n, rank, world, seed, device)
+    torch.cuda.synchronize(device)
+    gen_s = time.time() - t0
+    gids = torch.arange(n, dtype=torch.int64, device=device)
+    U = cq_amd.table_from_routed(ub.data_ptr(), ub.numel(), gids.data_ptr(), n, uh)
+    O = cq_amd.table_from_routed(ob.data_ptr(), ob.numel(), gids.data_ptr(), n, oh)
+    nbytes = ub.numel() + ob.numel()
+    del ub, ob, gids
+    dist.all_reduce(cnt)
+    dist.all_reduce(cents)
+    dist.all_reduce(matched, op=dist.ReduceOp.MAX)
+    first = None
+    if rank == 0:
+        idx = torch.nonzero(matched).squeeze(1)
+        fr = torch.full((1000,), world * n, dtype=torch.int64, device=device)
+        fr.scatter_reduce_(0, role_all[idx], idx, reduce="amin")
+        first = fr.cpu().numpy()
+        del idx
+    cnt, cents = cnt.cpu().numpy().astype(np.int64), cents.cpu().numpy()
+    del matched, role_all
+    torch.cuda.empty_cache()
+    last = None
+    for _ in range(warmup):
+        tp = join_partitioned_rccl(ast, U, O)
+        if tp:
+            cq_amd.result_free(tp)
+    dist.barrier()
+    torch.cuda.synchronize(device)
+    t1 = time.perf_counter()
+    for _ in range(steps):
+        tp = join_partitioned_rccl(ast, U, O)
+        if tp:
+            if last:
+                cq_amd.result_free(last)
+            last = tp
+    dist.barrier()
+    torch.cuda.synchronize(device)
+    el = time.perf_counter() - t1
+    t = torch.tensor([el], dtype=torch.float64, device=device)
+    dist.all_reduce(t, op=dist.ReduceOp.MAX)
+    el = float(t.item())
+    kind = cq_amd.stats().get("scan_kernel")
+    kinds = [None] * world
+    dist.all_gather_object(kinds, kind)
+    ok = None
+    if rank == 0:
+        res = abi.table_to_py(last)
+        cq_amd.result_free(last)
+        rows = res["rows"]
+        want = [r for r in np.argsort(first, kind="stable") if cnt[r] > 0]
+        ok = len(rows) == len(want) and all(k == 4 for k in kinds)
+        for row, r in zip(rows, want if ok else []):
+            name = row[0][1].decode() if isinstance(row[0][1], bytes) else row[0][1]
+            ws = cents[r] / 100.0
+            if name != "role_%03d" % r or row[1][1] != cnt[r] or abs(row[2][1] - ws) > 1e-6 * ws:
+                ok = False
+                break
+    U.close()
+    O.close()
+    return {"step_s": el / steps, "rows_total": 2 * n * world, "bytes_per_rank": nbytes, "verified": ok,
+            "kinds": kinds, "gen_s": gen_s, "joined_pairs": int(cnt.sum())}
+
+
 def routed_share_leg(n_total: int, nranks: int, steps: int, warmup: int, seed: int, device, ast, check_order=True):
     """BASELINE config 5 as a rank of an `nranks`-GPU node runs it, on one GPU: the whole
     n_total x n_total inputs are generated on the device, routed with the product's

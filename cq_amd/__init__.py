@@ -104,6 +104,8 @@ def lib():
         L.cqgpu_comm_destroy.argtypes = []
         L.cqgpu_dist_query.restype = TP
         L.cqgpu_dist_query.argtypes = [C.POINTER(abi.Node), vp, C.POINTER(C.c_int), C.POINTER(C.c_int)]
+        L.cqgpu_dist_join.restype = TP
+        L.cqgpu_dist_join.argtypes = [C.POINTER(abi.Node), C.POINTER(vp), C.c_int, C.POINTER(C.c_int)]
         L.cqgpu_gm_local.restype = TP
         L.cqgpu_gm_local.argtypes = [C.POINTER(abi.Node), C.POINTER(vp), C.c_int]
         L.cqgpu_last_stats.argtypes = [C.POINTER(Stats)]
@@ -319,6 +321,16 @@ def dist_query_raw(ast, table: "Table"):
     st, path = C.c_int(0), C.c_int(0)
     tp = lib().cqgpu_dist_query(ast, table.handle, C.byref(st), C.byref(path))
     return (tp if tp else None), st.value, path.value
+
+
+def dist_join_raw(ast, tables):
+    """(result pointer or None, status): the repartitioned JOIN step over the
+    library's RCCL communicator (cqgpu_dist_join); status -1 on every rank when any
+    rank failed"""
+    arr, n = _tables_arg(tables)
+    st = C.c_int(0)
+    tp = lib().cqgpu_dist_join(ast, arr, n, C.byref(st))
+    return (tp if tp else None), st.value
 
 
 def gm_local(ast, shards):

@@ -160,8 +160,9 @@ hipError_t cq_launch_gm_merge(const uint8_t* buf, uint64_t B, uint32_t N, uint32
                               uint32_t* slot_of, uint32_t* flag, uint32_t* dense, uint32_t* idx, void* scan_temp,
                               size_t scan_temp_bytes, unsigned int* err, uint8_t* dst, unsigned int* gcount,
                               uint8_t* mail, hipStream_t s);
+int cq_fast_ext_plan(const cq::ScanPlan* P, int grouped);
 hipError_t cq_launch_raw_merge(const cq::GroupTable* gt, const cq::GroupTable* rt, int nacc, cq::ScanStats* stats,
-                               hipStream_t s);
+                               hipStream_t s, uint32_t max_mask = 0);
 uint64_t cq_jx_windows(uint64_t lo, uint64_t hi, uint32_t ws);
 hipError_t cq_jx_extract(const uint8_t* g, uint64_t lo, uint64_t hi, uint32_t ws, uint32_t delim, uint32_t quote,
                          int kcol, int pcol, int build, int pass, unsigned long long* key, unsigned long long* pay,
@@ -179,7 +180,12 @@ hipError_t cq_jx_star_extract(const uint8_t* g, uint64_t lo, uint64_t hi, uint32
                               uint32_t stride, uint16_t* d16, uint32_t* l32, unsigned long long* ttab,
                               unsigned long long* gsum, unsigned long long* counter, unsigned int* flag,
                               unsigned long long* krange, uint32_t* notmono, unsigned long long* wfl,
-                              uint32_t* gminix, int rp, int grid, hipStream_t s);
+                              uint32_t* gminix, int rp, int grid, hipStream_t s, unsigned long long* pent = nullptr,
+                              uint32_t* pcnt = nullptr, uint32_t np = 0, uint32_t pcap = 0, uint32_t psh = 0);
+hipError_t cq_jx_part_probe(const unsigned long long* pent, const uint32_t* pcnt, uint32_t nsrc, uint32_t np,
+                            uint32_t pcap, unsigned long long range, uint16_t* d16, const uint32_t* notmono,
+                            unsigned long long* gsum, uint32_t* gminix, unsigned long long* npairs, int grid,
+                            hipStream_t s);
 hipError_t cq_jx_star_order(const unsigned long long* wfl, unsigned long long nwin, uint32_t* notmono, hipStream_t s);
 hipError_t cq_jx_star_init(void* d16, size_t d16_bytes, void* small, size_t small_bytes, uint32_t ff0, uint32_t ff1,
                            uint32_t ffw, const void* seed, size_t seed_bytes, int grid, hipStream_t s);
@@ -521,6 +527,7 @@ struct cqgpu_table {
     uint64_t base_offset = 0;
     cq_csv_config cfg{',', '"', true};
     std::vector<std::string> names;
+    std::string header_rec;          // the header record's bytes (routed tables rebuilt on a rank reuse it)
     uint64_t data_begin = 0;
     int device = 0;
     uint32_t lean_ws = 0;            // lean_kernel window stride for this file's record lengths
@@ -606,6 +613,7 @@ cqgpu_table* upload(const uint8_t* host, size_t n, cq_csv_config cfg, uint64_t b
         const char* ls = p;
         while (p < e && *p != '\n' && *p != '\r') p++;
         t->names = split_header(ls, p, cfg.delimiter, cfg.quote, cfg.has_header);
+        t->header_rec.assign(ls, (size_t)(p - ls));
         t->data_begin = 0;
     } else {
         const char* d = (const char*)host;
@@ -615,6 +623,7 @@ cqgpu_table* upload(const uint8_t* host, size_t n, cq_csv_config cfg, uint64_t b
         const char* ls = p;
         while (p < e && *p != '\n' && *p != '\r') p++;
         if (p > ls) t->names = split_header(ls, p, cfg.delimiter, cfg.quote, cfg.has_header);
+        if (cfg.has_header) t->header_rec.assign(ls, (size_t)(p - ls));
         t->data_begin = cfg.has_header ? (uint64_t)(p - d) : 0;
     }
     t->lean_ws = cq_lean_pick_ws(host + t->data_begin, n - std::min<uint64_t>(n, t->data_begin));
@@ -1499,7 +1508,9 @@ TableArena make_arena(DevCtx& c, const ScanPlan& P, uint32_t cap, size_t out_cap
     parts.push_back({(void**)&A.gt.used, 256, 0});
     bool sums_only = true;
     for (int a = 0; a < P.nacc; a++) sums_only = sums_only && P.acc[a].kind == ACC_SUM;
-    if (sums_only) {   // lean_kernel plans: the raw-key table
+    // lean_kernel / fast_kernel plans: the raw-key table (with extreme cells for a
+    // fast_kernel MIN / MAX build, cq_fast_ext_plan)
+    if (sums_only || cq_fast_ext_plan(&P, 1)) {
         parts.push_back({(void**)&A.rt.tag, cap * 4ull, 0});
         parts.push_back({(void**)&A.rt.clslen, cap * 4ull, 0});
         parts.push_back({(void**)&A.rt.w0, cap * 8ull, 0});
@@ -1507,8 +1518,14 @@ TableArena make_arena(DevCtx& c, const ScanPlan& P, uint32_t cap, size_t out_cap
         parts.push_back({(void**)&A.rt.cnt, cap * 8ull, 0});
         parts.push_back({(void**)&A.rt.first, cap * 8ull, 0xff});
         for (int a = 0; a < P.nacc; a++) {
-            parts.push_back({(void**)&A.rt.sum[a], cap * 8ull, 0});
-            parts.push_back({(void**)&A.rt.num[a], cap * 8ull, 0});
+            if (P.acc[a].kind == ACC_SUM) {
+                parts.push_back({(void**)&A.rt.sum[a], cap * 8ull, 0});
+                parts.push_back({(void**)&A.rt.num[a], cap * 8ull, 0});
+            } else {
+                parts.push_back({(void**)&A.rt.ext[a], cap * (size_t)sizeof(Cell), 0});
+                parts.push_back({(void**)&A.rt.extpos[a], cap * 8ull, 0xff});
+                parts.push_back({(void**)&A.rt.lock[a], cap * 4ull, 0});
+            }
         }
         parts.push_back({(void**)&A.rt.used, 256, 0});
     }
@@ -3200,6 +3217,20 @@ bool sample_key_range(const cqgpu_table* t, int col, uint64_t S, uint64_t* kmin,
     return true;
 }
 
+// average record bytes of a table's sampled data (records and their terminators)
+double sample_record_bytes(const cqgpu_table* t) {
+    const std::string& s = t->sample;
+    size_t i = 0, nrec = 0, used = 0;
+    while (i < s.size()) {
+        while (i < s.size() && (s[i] == '\n' || s[i] == '\r')) i++;
+        while (i < s.size() && s[i] != '\n' && s[i] != '\r') i++;
+        if (i >= s.size()) break;
+        nrec++;
+        used = i;
+    }
+    return nrec ? (double)used / (double)nrec : 64.0;
+}
+
 // The fused aggregate join: one INNER JOIN on `ident = ident`
 // without WHERE, COUNT / SUM / AVG of one probe-side (right) column, GROUP BY one
 // build-side (left) column or none, every other item a left column.  No record-start
@@ -3390,7 +3421,8 @@ cq_table* run_fast_join(DevCtx& c, cq_node* q, Compiled& C, const cqgpu_table* L
     // sends the query on to the record-array path below.
     if (!getenv("CQ_AMD_NO_STAR_JOIN")) {
         cqgpu_table* Lm = const_cast<cqgpu_table*>(L);
-        for (int round = 0; round < 2; round++) {
+        bool no_part = getenv("CQ_AMD_NO_PART_PROBE") != nullptr;
+        for (int round = 0; round < 3; round++) {
             uint64_t kmin = 0, kmax = 0, est = 0;
             const uint64_t S = L->key_stride ? L->key_stride : 1;
             auto it = Lm->key_range.find(kl);
@@ -3446,9 +3478,39 @@ cq_table* run_fast_join(DevCtx& c, cq_node* q, Compiled& C, const cqgpu_table* L
                                         l32.as<uint32_t>(), ttab, gsum, cnts, sflag, skr, snotmono,
                                         wfl.as<unsigned long long>(), nullptr, rpl, xgrid, c.stream));
             HIPCHECK(cq_jx_star_order(wfl.as<unsigned long long>(), nwb, snotmono, c.stream));
-            HIPCHECK(cq_jx_star_extract(R->g, R->data_begin, R->n, wsr3, d, dq, kr, vcol, 0, kmin, range, (uint32_t)S, d16,
-                                        l32.as<uint32_t>(), ttab, gsum, cnts + 1, sflag, nullptr, snotmono, nullptr,
-                                        gminix, rpr, xgrid, c.stream));
+            // the probe: when d16 (2 bytes per key slot) outgrows one XCD's 4 MiB L2, in two
+            // passes -- every probe record's (slot, payload) appended to its key partition
+            // (2 MiB d16 slices), then each partition looked up by the blocks of one XCD
+            // (fast.hip jx_part_probe_kernel); else one pass with the lookups in place
+            // (test knobs: CQGPU_PART_PROBE_MIN slots above which it partitions, default 2^21;
+            //  CQGPU_PART_PROBE_SHIFT log2 slots per partition, default 20)
+            const char* pm_env = getenv("CQGPU_PART_PROBE_MIN");
+            const char* ps_env = getenv("CQGPU_PART_PROBE_SHIFT");
+            const uint64_t part_min = pm_env ? strtoull(pm_env, nullptr, 10) : (2ull << 20);
+            const uint32_t PSH = ps_env ? (uint32_t)std::min(std::max(atoi(ps_env), 4), 24) : 20u;
+            const uint64_t np64 = (range + (1ull << PSH) - 1) >> PSH;
+            const bool pprobe = !no_part && range > part_min && np64 <= 4096 && xgrid >= 8;
+            DevBuf pent, pcnt;
+            if (pprobe) {
+                const uint64_t rb = R->n > R->data_begin ? R->n - R->data_begin : 0;
+                const uint64_t est_r = (uint64_t)((double)rb / std::max(1.0, sample_record_bytes(R))) + 1;
+                const uint64_t per = est_r / ((uint64_t)xgrid * np64);
+                const uint32_t pcap = (uint32_t)std::min<uint64_t>(per + per / 4 + 256, 1u << 30);
+                DevBuf a((size_t)xgrid * np64 * pcap * 8), b((size_t)xgrid * np64 * 4);
+                std::swap(pent.p, a.p);
+                std::swap(pcnt.p, b.p);
+                HIPCHECK(cq_jx_star_extract(R->g, R->data_begin, R->n, wsr3, d, dq, kr, vcol, 0, kmin, range, (uint32_t)S,
+                                            d16, l32.as<uint32_t>(), ttab, gsum, cnts + 1, sflag, nullptr, snotmono,
+                                            nullptr, gminix, rpr, xgrid, c.stream, pent.as<unsigned long long>(),
+                                            pcnt.as<uint32_t>(), (uint32_t)np64, pcap, PSH));
+                HIPCHECK(cq_jx_part_probe(pent.as<unsigned long long>(), pcnt.as<uint32_t>(), (uint32_t)xgrid,
+                                          (uint32_t)np64, pcap, range, d16, snotmono, gsum, gminix, cnts + 1,
+                                          std::max(8, (c.ncu / 8) * 8), c.stream));
+            } else {
+                HIPCHECK(cq_jx_star_extract(R->g, R->data_begin, R->n, wsr3, d, dq, kr, vcol, 0, kmin, range, (uint32_t)S,
+                                            d16, l32.as<uint32_t>(), ttab, gsum, cnts + 1, sflag, nullptr, snotmono,
+                                            nullptr, gminix, rpr, xgrid, c.stream));
+            }
             HIPCHECK(cq_jx_star_first(d16, l32.as<uint32_t>(), range, snotmono, gfirst, cnts + 2, c.ncu * 4, c.stream));
             PHASE("star launch");
             bool fb = false;
@@ -3509,6 +3571,11 @@ cq_table* run_fast_join(DevCtx& c, cq_node* q, Compiled& C, const cqgpu_table* L
             HIPCHECK(hipMemcpyAsync(&fl, sflag, 4, hipMemcpyDeviceToHost, c.stream));
             HIPCHECK(hipMemcpyAsync(kr2, skr, 16, hipMemcpyDeviceToHost, c.stream));
             HIPCHECK(hipStreamSynchronize(c.stream));
+            // a full partition region (skewed probe keys) or a wide payload: again, unpartitioned
+            if (fl == 128u && !no_part) {
+                no_part = true;
+                continue;
+            }
             // only a range miss is worth a second round (with the range the build saw)
             if (fl != 16u || kr2[0] > kr2[1] || learned) break;
             Lm->key_range[kl] = {kr2[0], kr2[1]};
@@ -6573,11 +6640,12 @@ int dist_dense(DevCtx& c, DistComm& m, cq_node* q, cqgpu_table* t, cq_table** re
 }
 
 // ---- blobs: every rank's cqgpu_query_partial to rank 0, merged there
-void dist_blob(DevCtx& c, DistComm& m, cq_node* q, cqgpu_table* t, cq_table** res) {
+void dist_blob(DevCtx& c, DistComm& m, cq_node* q, cqgpu_table* const* tabs, int ntabs, cq_table** res,
+               bool bad_in = false, const std::string& err_in = std::string()) {
     void* blob = nullptr;
-    const size_t n = cqgpu_query_partial(q, &t, 1, &blob);
+    const size_t n = bad_in ? 0 : cqgpu_query_partial(q, tabs, ntabs, &blob);
     const bool bad = n == 0;
-    std::string err = bad ? (g_err.empty() ? g_inel : g_err) : std::string();
+    std::string err = bad_in ? err_in : (bad ? (g_err.empty() ? g_inel : g_err) : std::string());
     struct Free { void* b; ~Free() { free(b); } } fr{blob};
     const int N = m.world;
     DevBuf pair((size_t)N * 16 + 16), dblob(std::max<size_t>(n, 16));
@@ -6623,6 +6691,101 @@ void dist_blob(DevCtx& c, DistComm& m, cq_node* q, cqgpu_table* t, cq_table** re
         if (*res) { cqgpu_result_free(*res); *res = nullptr; }
         throw PeerFail{m.rank == 0 ? rerr : std::string("rank 0 failed to finish the merge")};
     }
+}
+
+// ---- the repartitioned JOIN step (cqgpu_dist_join): per side the device routing
+// (cqgpu_route_plan: whole keys by key mod N, others by hash), every rank's per-
+// destination byte / record counts in one all-gather (with each rank's failure flag),
+// the records and their global ids in one grouped send / recv per side over the
+// communicator, the received records rebuilt as this rank's side (file order, global
+// ids, key stride N, whole-input record total), then the join partials as blobs to
+// rank 0 (dist_blob).  No host round trip carries data; the host reads only counts.
+void dist_join(DevCtx& c, DistComm& m, cq_node* q, cqgpu_table* const* tables, int ntables, cq_table** res) {
+    const int N = m.world;
+    std::string err;
+    bool bad = false;
+    struct TabFree { void operator()(cqgpu_table* t) const { if (t) cqgpu_table_free(t); } };
+    std::vector<std::unique_ptr<cqgpu_table, TabFree>> routed;
+    for (int side = 0; side < 2; side++) {
+        std::vector<uint64_t> nb(N, 0), nr(N, 0);
+        if (!bad && cqgpu_route_plan(q, tables, ntables, side, N, nb.data(), nr.data()) != 0) {
+            bad = true;
+            err = g_err.empty() ? g_inel : g_err;
+            if (!g_inel.empty()) err = "query outside the GPU executor's subset: " + g_inel;
+        }
+        // all ranks' counts: [nb(N), nr(N), bad] per rank
+        const size_t W = 2 * (size_t)N + 1;
+        std::vector<uint64_t> mine(W, 0), all(W * N, 0);
+        for (int d = 0; d < N; d++) { mine[d] = bad ? 0 : nb[d]; mine[N + d] = bad ? 0 : nr[d]; }
+        mine[2 * N] = bad ? 1 : 0;
+        {
+            DevBuf dc(W * 8 * (N + 1));
+            uint64_t* dp = dc.as<uint64_t>();
+            HIPCHECK(hipMemcpyAsync(dp + W * N, mine.data(), W * 8, hipMemcpyHostToDevice, c.stream));
+            NCCLCHECK(ncclAllGather(dp + W * N, dp, W, ncclUint64, m.comm, c.stream));
+            HIPCHECK(hipMemcpyAsync(all.data(), dp, W * N * 8, hipMemcpyDeviceToHost, c.stream));
+            HIPCHECK(hipStreamSynchronize(c.stream));
+        }
+        for (int r = 0; r < N; r++)
+            if (all[(size_t)r * W + 2 * N]) {
+                if (tables[side]) tables[side]->route.reset();
+                throw PeerFail{bad ? err : std::string("a peer rank failed")};
+            }
+        // global ids: this rank's records follow every lower rank's; the whole input's total
+        uint64_t base = 0, total = 0;
+        std::vector<uint64_t> sb(N + 1, 0), sr(N + 1, 0), rb(N + 1, 0), rr(N + 1, 0);
+        for (int r = 0; r < N; r++) {
+            uint64_t recs = 0;
+            for (int d = 0; d < N; d++) recs += all[(size_t)r * W + N + d];
+            if (r < m.rank) base += recs;
+            total += recs;
+        }
+        for (int d = 0; d < N; d++) {
+            sb[d + 1] = sb[d] + nb[d];
+            sr[d + 1] = sr[d] + nr[d];
+            rb[d + 1] = rb[d] + all[(size_t)d * W + m.rank];          // from source d, in source order
+            rr[d + 1] = rr[d] + all[(size_t)d * W + N + m.rank];
+        }
+        if (total >= (1ull << 32)) throw PeerFail{"dist_join: 2^32 or more records on a join side"};   // (every rank)
+        DevBuf sbytes(std::max<uint64_t>(sb[N], 16)), sgids(std::max<uint64_t>(sr[N], 2) * 8);
+        DevBuf rbytes(std::max<uint64_t>(rb[N], 16)), rgids(std::max<uint64_t>(rr[N], 2) * 8);
+        // a local failure from here on still takes part in every collective (the sizes are
+        // agreed) and is reported by the next agreement: side 1's count gather or dist_blob's
+        if (cqgpu_route_fill(tables[side], base, sbytes.p, sgids.as<uint64_t>()) != 0) {
+            bad = true;
+            err = g_err;
+        }
+        NCCLCHECK(ncclGroupStart());
+        for (int d = 0; d < N; d++) {
+            if (nb[d]) {
+                NCCLCHECK(ncclSend(sbytes.as<uint8_t>() + sb[d], nb[d], ncclUint8, d, m.comm, c.stream));
+                NCCLCHECK(ncclSend(sgids.as<uint64_t>() + sr[d], nr[d], ncclUint64, d, m.comm, c.stream));
+            }
+            if (rb[d + 1] > rb[d]) {
+                NCCLCHECK(ncclRecv(rbytes.as<uint8_t>() + rb[d], rb[d + 1] - rb[d], ncclUint8, d, m.comm, c.stream));
+                NCCLCHECK(ncclRecv(rgids.as<uint64_t>() + rr[d], rr[d + 1] - rr[d], ncclUint64, d, m.comm, c.stream));
+            }
+        }
+        NCCLCHECK(ncclGroupEnd());
+        const std::string& hdr = tables[side]->header_rec;
+        cqgpu_table* t = bad ? nullptr
+                             : cqgpu_table_from_routed(rbytes.p, rb[N], rgids.as<uint64_t>(), rr[N], tables[side]->cfg,
+                                                       hdr.data(), hdr.size());
+        if (!t && !bad) {
+            bad = true;
+            err = g_err;
+        }
+        routed.emplace_back(t);
+        if (t) {
+            t->gid_total = total;
+            t->key_stride = (uint32_t)N;
+        }
+    }
+    std::vector<cqgpu_table*> tabs;
+    tabs.push_back(routed[0].get());
+    tabs.push_back(routed[1].get());
+    for (int i = 2; i < ntables; i++) tabs.push_back(tables[i]);
+    dist_blob(c, m, q, tabs.data(), (int)tabs.size(), res, bad, err);
 }
 
 // the merge the plan takes, decided from the AST and the header alone (no device
@@ -6713,8 +6876,40 @@ cq_table* cqgpu_dist_query(cq_node* q, cqgpu_table* t, int* status, int* path) {
         int dp = dist_path(q, t, D);                     // Ineligible: the same on every rank
         if (dp == DP_GM && dist_gm(c, m, q, t, D, &res) == GM_DECLINE) dp = DP_DENSE;
         if (dp == DP_DENSE && dist_dense(c, m, q, t, &res) != 0) dp = DP_BLOB;
-        if (dp == DP_BLOB) dist_blob(c, m, q, t, &res);
+        if (dp == DP_BLOB) dist_blob(c, m, q, &t, 1, &res);
         if (path) *path = dp;
+        g_stats.total_ms = now_ms() - t0;
+        if (m.rank == 0) g_stats.path = 1;
+        return res;
+    } catch (PeerFail& e) {
+        set_err("cq_amd: %s", e.msg.c_str());
+    } catch (Ineligible& e) {
+        g_inel = e.why;
+        set_err("cq_amd: query outside the GPU executor's subset: %s", e.why.c_str());
+    } catch (HipError& e) {
+        set_err("cq_amd: %s", e.msg.c_str());
+    } catch (std::exception& e) {
+        set_err("cq_amd: %s", e.what());
+    } catch (...) {
+        set_err("cq_amd: %s", "unexpected C++ exception");
+    }
+    if (res) cqgpu_result_free(res);
+    if (status) *status = -1;
+    return nullptr;
+}
+
+cq_table* cqgpu_dist_join(cq_node* q, cqgpu_table* const* tables, int ntables, int* status) {
+    g_err.clear();
+    g_inel.clear();
+    memset(&g_stats, 0, sizeof g_stats);
+    if (status) *status = 0;
+    cq_table* res = nullptr;
+    try {
+        if (ntables < 2 || !tables || !tables[0] || !tables[1]) throw HipError{"dist_join: two join sides needed"};
+        DevCtx& c = ctx();
+        DistComm& m = dist_comm();
+        const double t0 = now_ms();
+        dist_join(c, m, q, tables, ntables, &res);
         g_stats.total_ms = now_ms() - t0;
         if (m.rank == 0) g_stats.path = 1;
         return res;

@@ -82,6 +82,11 @@ struct FastPlan {
     int32_t nacc;
     uint32_t acc1;              // bit a: accumulator a sums SUM argument 1 (else 0)
     const unsigned long long* seed;   // TSLOTS host-placed tags, or null
+    // the one MIN / MAX accumulator of an EXT build (its argument: SUM argument 0);
+    // sum_mask bit a: accumulator a is a SUM / AVG (the flushes skip the extreme)
+    int32_t ext_acc;
+    uint32_t ext_col;           // the argument's column (the flushes re-type the extreme's field)
+    uint32_t sum_mask;
 };
 
 // HBM tables: canonical keys (TAB_GT), raw keys (TAB_RT)
@@ -428,7 +433,34 @@ __device__ __forceinline__ uint8_t* carve(uint8_t*& q, size_t bytes) {
 // non-numeric count; with one SUM argument a double sum for the addends outside the
 // fixed-point path (two SUM arguments: such addends take the HBM table)
 constexpr uint32_t SLOT_BYTES = 32;
-enum SlotOff : uint32_t { SO_CNT = 0, SO_FIRST = 4, SO_FIX0 = 8, SO_FIX1 = 16, SO_DBL = 16, SO_MISS0 = 24, SO_MISS1 = 28 };
+enum SlotOff : uint32_t { SO_CNT = 0, SO_FIRST = 4, SO_FIX0 = 8, SO_FIX1 = 16, SO_DBL = 16, SO_MISS0 = 24, SO_MISS1 = 28,
+                         SO_EXT = 16 };   // (EXT builds: one SUM argument, no double addends -- the word is free)
+
+// MIN / MAX of narrow numerals in one 64-bit LDS atomic: the value as exact 10^-3
+// fixed point (< 10^7 for the <= 4-byte numerals of the fast path) above the
+// record's 32-bit first-row code, so one atomicMin takes the smallest value and,
+// among equal values, the first record (evaluate_aggregate keeps the first cell
+// that compares strictly better, evaluator_aggregates.c:311-326); MAX stores the
+// code complemented under atomicMax.  Initial word: no candidate.
+template <int EXT>
+__device__ __forceinline__ unsigned long long ext_key(uint64_t fix, uint32_t code) {
+    return (fix << 32) | (EXT == 1 ? code : ~code);
+}
+template <int EXT>
+__device__ __forceinline__ unsigned long long ext_none() { return EXT == 1 ? ~0ull : 0ull; }
+// the record's field `col` from global memory (the record passed the fast path: no
+// quote before it, the field exists), typed by the general parser
+__device__ __noinline__ Cell field_cell(const uint8_t* __restrict__ g, uint64_t rec, uint32_t col, uint32_t delim) {
+    const uint8_t* p = g + rec;
+    for (uint32_t c = 0; c < col; p++) {
+        const uint32_t ch = *p;
+        if (ch == delim) c++;
+        else if (ch == '\n' || ch == '\r') return cell_null();
+    }
+    uint32_t len = 0;
+    while (len < 64 && p[len] != delim && p[len] != '\n' && p[len] != '\r') len++;
+    return parse_cell(p, len);
+}
 template <int NS>
 constexpr uint32_t table_bytes(bool grouped) {
     // the tags, and a 32-byte slot record (see SlotOff) per slot
@@ -443,11 +475,12 @@ constexpr uint32_t fixed_bytes() { return (uint32_t)(sizeof(WaveLds) * NWV); }
 // WN: numerals of 5-7 bytes / over 3 decimals are typed here (a side path); without
 // it (the plan's sampled WHERE / SUM fields are all <= 4 bytes) such a record goes
 // whole to slow_kernel, and the kernel keeps only the fixed-point SUM
-template <bool GROUPED, bool WHERE, int NS, bool COMMA, bool CANON, int RP, bool WN>
+template <bool GROUPED, bool WHERE, int NS, bool COMMA, bool CANON, int RP, bool WN, int EXT = 0>
 __global__ __launch_bounds__(LT) void fast_kernel(const uint8_t* __restrict__ g, ScanStats* __restrict__ stats,
                                                   unsigned long long* __restrict__ slow_list,
                                                   unsigned long long slow_cap, const FastPlan fp,
                                                   const GroupTable* __restrict__ tabs) {
+    static_assert(EXT == 0 || (NS == 1 && !WN), "MIN / MAX: one fixed-point argument, no double addends");
     extern __shared__ __align__(16) uint8_t smem[];
     uint8_t* q = smem;
     // LDS table: slot records first (LDS address 0: field offsets fold into the
@@ -470,6 +503,7 @@ __global__ __launch_bounds__(LT) void fast_kernel(const uint8_t* __restrict__ g,
 #pragma unroll
             for (int w = 0; w < 8; w++) r[w] = 0u;
             r[SO_FIRST / 4] = NOFIRST;
+            if (EXT) *(unsigned long long*)(r + SO_EXT / 4) = ext_none<EXT>();
         }
         __syncthreads();
     }
@@ -546,6 +580,8 @@ __global__ __launch_bounds__(LT) void fast_kernel(const uint8_t* __restrict__ g,
     double my_dbl[MAXS] = {0.0, 0.0};
     uint32_t my_num[MAXS] = {0u, 0u};
     uint32_t n_rec = 0, n_pass = 0, n_spill = 0;   // wave totals (uniform)
+    unsigned long long my_ext = ext_none<EXT>();   // ungrouped EXT builds: the lane's extreme key
+    bool saw_num = false;                          // EXT: a numeric candidate (the class bit)
 
     uint32_t prev_next = 0;
     const uint32_t voff = vreg(16u * (uint32_t)lane);
@@ -912,6 +948,12 @@ __global__ __launch_bounds__(LT) void fast_kernel(const uint8_t* __restrict__ g,
                         my_dbl[j] += (on & !sfx[u][j]) ? sdbl[u][j] : 0.0;
                         my_num[j] += on ? 1u : 0u;
                     }
+                    if constexpr (EXT != 0) {
+                        const bool cand = pass[u] & snum[u][0];
+                        const unsigned long long xk = ext_key<EXT>(sfix[u][0], fcw | p[u]);
+                        if (cand) my_ext = EXT == 1 ? (xk < my_ext ? xk : my_ext) : (xk > my_ext ? xk : my_ext);
+                        saw_num |= cand;
+                    }
                 }
             } else {
                 // lookup: the key's two buckets (one 16-byte LDS read each)
@@ -980,10 +1022,18 @@ __global__ __launch_bounds__(LT) void fast_kernel(const uint8_t* __restrict__ g,
                         for (int j = 0; j < NS; j++) {
                             if (snum[u][j] && (FAST_ATOM & 4)) {
                                 if (sfx[u][j]) atomicAdd((unsigned long long*)(r + (j ? SO_FIX1 : SO_FIX0)), (unsigned long long)sfix[u][j]);
-                                else if (NS == 1) atomicAdd((double*)(r + SO_DBL), sdbl[u][j]);
+                                else if (NS == 1 && EXT == 0) atomicAdd((double*)(r + SO_DBL), sdbl[u][j]);
+                            }
+                        }
+                        if constexpr (EXT != 0) {
+                            if (snum[u][0]) {
+                                const unsigned long long xk = ext_key<EXT>(sfix[u][0], fc);
+                                if (EXT == 1) atomicMin((unsigned long long*)(r + SO_EXT), xk);
+                                else atomicMax((unsigned long long*)(r + SO_EXT), xk);
                             }
                         }
                     }
+                    if constexpr (EXT != 0) saw_num |= add & snum[u][0];
 #pragma unroll
                     for (int j = 0; j < NS; j++) {
                         const bool nn = add & !snum[u][j];
@@ -993,7 +1043,19 @@ __global__ __launch_bounds__(LT) void fast_kernel(const uint8_t* __restrict__ g,
                     }
                     const bool spill = pass[u] & (slot[u] < 0);
                     const uint64_t spb = __ballot(spill);
-                    if (spb) {                                       // both buckets full
+                    if (EXT != 0 && spb) {
+                        // both buckets full: the record goes whole to slow_kernel (which keeps
+                        // the extreme in the canonical table); not counted here
+                        unsigned long long base = 0;
+                        if (lane == 0) base = atomicAdd(&stats->slow_records, (unsigned long long)__popcll(spb));
+                        base = __shfl(base, 0, 64);
+                        if (spill) {
+                            const unsigned long long si = base + __popcll(spb & ((1ULL << lane) - 1));
+                            if (si < slow_cap) slow_list[si] = (first_win + i) * wsb + p[u];
+                        }
+                        n_rec -= (uint32_t)__popcll(spb);
+                        n_pass -= (uint32_t)__popcll(spb);
+                    } else if (spb) {                                // both buckets full
                         n_spill += (uint32_t)__popcll(spb);
                         if (spill) {
                             double v0 = 0.0, v1 = 0.0;
@@ -1014,6 +1076,7 @@ __global__ __launch_bounds__(LT) void fast_kernel(const uint8_t* __restrict__ g,
     }
 
     // ---- statistics
+    if (EXT != 0 && __any(saw_num) && lane == 0) atomicOr(&stats->acc_classes[fp.ext_acc], 1u);   // numbers
     if (lane == 0) {
         if (n_rec) atomicAdd(&stats->records, (unsigned long long)n_rec);
         if (n_pass) atomicAdd(&stats->passed, (unsigned long long)n_pass);
@@ -1037,11 +1100,13 @@ __global__ __launch_bounds__(LT) void fast_kernel(const uint8_t* __restrict__ g,
                 nm[j] += __shfl_down(nm[j], o, 64);
             }
         }
+        const GroupTable& gt = tabs[TAB_GT];
+        int gi0 = -1;
         if (lane == 0) {
-            const GroupTable& gt = tabs[TAB_GT];
             GKey k;
             k.cls = GK_ALL; k.len = 0; k.w0 = 0; k.w1 = 0;
             const int gi = g_insert(gt, k, 0x12345678ULL, stats);
+            gi0 = gi;
             if (gi >= 0) {
                 if (c) atomicAdd(&gt.cnt[gi], c);
                 if (f != NOFIRST) {
@@ -1049,6 +1114,7 @@ __global__ __launch_bounds__(LT) void fast_kernel(const uint8_t* __restrict__ g,
                     atomicMin(&gt.first[gi], (unsigned long long)(fw * wsb + (f & 4095)));
                 }
                 for (int a = 0; a < nacc; a++) {
+                    if (EXT != 0 && !((fp.sum_mask >> a) & 1)) continue;
                     const bool j1 = (acc1 >> a) & 1;
                     const double sa = j1 ? sm[MAXS - 1] : sm[0];
                     const unsigned long long na = j1 ? nm[MAXS - 1] : nm[0];
@@ -1059,6 +1125,27 @@ __global__ __launch_bounds__(LT) void fast_kernel(const uint8_t* __restrict__ g,
                 }
             }
         }
+        if constexpr (EXT != 0) {
+            // the wave's extreme (one key order for MIN and MAX), its cell re-typed from
+            // the record, merged under the group's seqlock (wave-uniform call)
+            unsigned long long x = my_ext;
+            for (int o = 32; o > 0; o >>= 1) {
+                const unsigned long long y = __shfl_down(x, o, 64);
+                x = EXT == 1 ? (y < x ? y : x) : (y > x ? y : x);
+            }
+            const int gi = __shfl(gi0, 0, 64);
+            const bool have = lane == 0 && gi >= 0 && x != ext_none<EXT>();
+            Cell cc = cell_null();
+            uint64_t pos = 0;
+            if (have) {
+                const uint32_t code = EXT == 1 ? (uint32_t)x : ~(uint32_t)x;
+                const uint64_t fw = first_win + ((uint64_t)(code >> 16) * gridDim.x + blockIdx.x) * NWV + ((code >> 12) & 15);
+                pos = fw * wsb + (code & 4095);
+                cc = field_cell(g, pos, fp.ext_col, fp.delim);
+            }
+            g_ext_update(have && cc.kind != K_NULL, gt, fp.ext_acc, EXT == 1 ? ACC_MIN : ACC_MAX,
+                         gi >= 0 ? (uint32_t)gi : 0u, cc, pos, stats);
+        }
         return;
     }
 
@@ -1067,15 +1154,32 @@ __global__ __launch_bounds__(LT) void fast_kernel(const uint8_t* __restrict__ g,
     __syncthreads();
     const GroupTable& rt = tabs[TAB_RT];
     const uint32_t rot = (uint32_t)blockIdx.x * (TSLOTS / 64 + 1);
+    static_assert(TSLOTS % LT == 0, "every lane runs every flush trip (the MIN / MAX merge is wave-uniform)");
     for (uint32_t ii = tid; ii < TSLOTS; ii += LT) {
         const uint32_t i = (ii + rot) & (TSLOTS - 1);
         const uint8_t* r = S + i * SLOT_BYTES;
         const uint32_t n = *(const uint32_t*)(r + SO_CNT);
-        if (!n) continue;
-        const uint64_t w0 = T[i];
-        const uint32_t kl = key_len8(w0);
-        const GKey k = raw_key(kl, kl ? w0 : 0ull);
-        const int gi = g_insert(rt, k, gk_hash(k), stats);
+        int gi = -1;
+        if (n) {
+            const uint64_t w0 = T[i];
+            const uint32_t kl = key_len8(w0);
+            const GKey k = raw_key(kl, kl ? w0 : 0ull);
+            gi = g_insert(rt, k, gk_hash(k), stats);
+        }
+        if constexpr (EXT != 0) {
+            const unsigned long long x = *(const unsigned long long*)(r + SO_EXT);
+            const bool have = gi >= 0 && x != ext_none<EXT>();
+            Cell cc = cell_null();
+            uint64_t pos = 0;
+            if (have) {
+                const uint32_t code = EXT == 1 ? (uint32_t)x : ~(uint32_t)x;
+                const uint64_t fw = first_win + ((uint64_t)(code >> 16) * gridDim.x + blockIdx.x) * NWV + ((code >> 12) & 15);
+                pos = fw * wsb + (code & 4095);
+                cc = field_cell(g, pos, fp.ext_col, fp.delim);
+            }
+            g_ext_update(have && cc.kind != K_NULL, rt, fp.ext_acc, EXT == 1 ? ACC_MIN : ACC_MAX,
+                         gi >= 0 ? (uint32_t)gi : 0u, cc, pos, stats);
+        }
         if (gi < 0) continue;
         atomicAdd(&rt.cnt[gi], (unsigned long long)n);
         const uint32_t fc = *(const uint32_t*)(r + SO_FIRST);
@@ -1084,10 +1188,11 @@ __global__ __launch_bounds__(LT) void fast_kernel(const uint8_t* __restrict__ g,
             atomicMin(&rt.first[gi], (unsigned long long)(fw * wsb + (fc & 4095)));
         }
         for (int acc = 0; acc < nacc; acc++) {
+            if (EXT != 0 && !((fp.sum_mask >> acc) & 1)) continue;
             const bool j1 = (acc1 >> acc) & 1;
             const double sa = j1 ? (double)*(const unsigned long long*)(r + SO_FIX1) / 1000.0
                                  : (double)*(const unsigned long long*)(r + SO_FIX0) / 1000.0 +
-                                       (NS == 1 ? *(const double*)(r + SO_DBL) : 0.0);
+                                       (NS == 1 && EXT == 0 ? *(const double*)(r + SO_DBL) : 0.0);
             const uint32_t ms = *(const uint32_t*)(r + (j1 ? SO_MISS1 : SO_MISS0));
             const uint32_t num = n - ms;
             if (num) {
@@ -1144,6 +1249,12 @@ struct JxOut {
                                // (probe: zero -> per group the smallest matched key index, no flags)
     unsigned long long* wfl;   // build: per window its first and last key (order check)
     uint32_t* gminix;          // probe: per group id the smallest matched key index
+    // partitioned STAR probe, pass 1 (PART): no lookup; every matchable probe record
+    // appends (slot, 32-bit payload) to its key partition (slot >> psh) in this block's
+    // region of pent: [block][np][pcap] entries, counts in pcnt[block][np]
+    unsigned long long* pent;
+    uint32_t* pcnt;
+    uint32_t np, pcap, psh;
 };
 // a key's STAR slot (k - kmin) / S when k = kmin (mod S) and the slot is below 2^32,
 // else ~0 (never < range: the host keeps range * S < 2^32).  Exact division by the
@@ -1157,8 +1268,12 @@ __device__ __forceinline__ unsigned long long jx_slot(unsigned long long k, cons
 }
 
 // STAR flags (JxOut.flag): 8 a NULL build key, 16 a key outside [kmin, kmin + range),
-// 32 more GROUP BY tags than JX_G, 64 a repeated build key (placed != occupied)
+// 32 more GROUP BY tags than JX_G, 64 a repeated build key (placed != occupied),
+// 128 a partitioned probe's partition region full or a payload outside 31 bits
+// (the host reruns the probe unpartitioned)
 constexpr uint32_t JX_G = 2048;           // group ids of a STAR join (LDS sums per block)
+constexpr uint32_t JX_PMAX = 4096;        // key partitions of a partitioned STAR probe (LDS counters)
+constexpr uint32_t JX_PNULL = 0x80000000u;   // a partitioned entry's NULL payload
 
 // a GROUP BY raw tag's group id: its slot in the tag table (linear probing; a stale
 // 0 read only leads to the CAS, a set slot never changes)
@@ -1284,13 +1399,20 @@ __device__ __forceinline__ bool jx_key(uint32_t d0, uint32_t d1, uint32_t d2, ui
 #endif
 }
 
-template <bool BUILD, bool COMMA, int NR, bool COUNT, bool STAR = false, int RP = 2>
+template <bool BUILD, bool COMMA, int NR, bool COUNT, bool STAR = false, int RP = 2, bool PART = false>
 __global__ __launch_bounds__(LT) void jx_extract_kernel(const uint8_t* __restrict__ g, const JxPlan jp, const JxOut jo) {
     extern __shared__ __align__(16) uint8_t smem[];
     WaveLds* waves = (WaveLds*)smem;
     // STAR probe: per group id COUNT / fixed-point SUM / SUM count of this block;
-    // STAR build: the block's mirror of the GROUP BY tag table
-    constexpr bool SPROBE = STAR && !BUILD;
+    // STAR build: the block's mirror of the GROUP BY tag table;
+    // partitioned STAR probe (PART): the block's per-partition entry counters
+    static_assert(!PART || (STAR && !BUILD), "PART: the STAR probe's first pass");
+    constexpr bool SPROBE = STAR && !BUILD && !PART;
+    uint32_t* pcl = (uint32_t*)(smem + sizeof(WaveLds) * NWV);
+    if constexpr (PART) {
+        for (uint32_t k = threadIdx.x; k < jo.np; k += LT) pcl[k] = 0u;
+        __syncthreads();
+    }
     constexpr bool SBUILD = STAR && BUILD && NR == 2;
     constexpr uint32_t NG = SPROBE ? JX_G : 1;
     unsigned long long* sfix = (unsigned long long*)(smem + sizeof(WaveLds) * NWV);
@@ -1544,6 +1666,21 @@ __global__ __launch_bounds__(LT) void jx_extract_kernel(const uint8_t* __restric
 #else
                         sflag |= gid == 12345u ? 1u : 0u;
 #endif
+                    } else if (PART) {
+                        // (a NULL key's slot is ~0, >= range: no entry, as it matches nothing)
+                        if (ix < jo.range) {
+                            const uint32_t pr = (uint32_t)ix >> jo.psh;
+                            const unsigned long long pv = pay[u];
+                            const bool pok = pv == JX_NOVAL || pv < (1ull << 31);
+                            const uint32_t at = atomicAdd(&pcl[pr], 1u);
+                            if (at < jo.pcap) {
+                                // (a payload outside 31 bits: an entry pass 2 skips, and the flag)
+                                const uint32_t p32 = pv == JX_NOVAL ? JX_PNULL : (uint32_t)pv;
+                                jo.pent[((size_t)blockIdx.x * jo.np + pr) * jo.pcap + at] =
+                                    pok ? ((unsigned long long)(uint32_t)ix | ((unsigned long long)p32 << 32)) : ~0ull;
+                            }
+                            if (at >= jo.pcap || !pok) sflag |= 128u;
+                        }
                     } else if (k != JX_NULLKEY && ix < jo.range) {
 #if defined(JX_AB_NOLOOK)
 #elif defined(JX_LATE_LOOK)
@@ -1625,6 +1762,12 @@ __global__ __launch_bounds__(LT) void jx_extract_kernel(const uint8_t* __restric
         if (lane == 0 && sflag) atomicOr(jo.flag, sflag);
         if (lane == 0 && nstar) atomicAdd(jo.nbuilt, nstar);   // build: placed; probe: pairs
     }
+    if constexpr (PART) {
+        __syncthreads();
+        for (uint32_t k = threadIdx.x; k < jo.np; k += LT)
+            jo.pcnt[(size_t)blockIdx.x * jo.np + k] = min(pcl[k], jo.pcap);
+        return;
+    }
     if constexpr (SPROBE) {
         __syncthreads();
         for (uint32_t k = threadIdx.x; k < NG; k += LT) {
@@ -1646,6 +1789,68 @@ __global__ __launch_bounds__(LT) void jx_extract_kernel(const uint8_t* __restric
     if (lane == 0 && kmin != ~0ull) {
         atomicMin(&jo.krange[0], kmin);
         atomicMax(&jo.krange[1], kmax);
+    }
+}
+
+// Partitioned STAR probe, pass 2: the entries of key partition p (d16 slots
+// [p << psh, (p + 1) << psh): a 2 MiB slice) are looked up by the blocks of one XCD
+// only -- blocks b and b + 8 share an XCD (MI355X_MICROARCH.md, workgroup dispatch),
+// so block b takes partitions b % 8, b % 8 + 8, ... -- and every block of that XCD
+// works on the same partition at once, so its slice stays in the XCD's 4 MiB L2
+// instead of each lookup fetching a random line from HBM.  The matches aggregate as
+// the unpartitioned probe's do: per group id COUNT / fixed-point SUM / SUM count in
+// LDS, the smallest matched key index (rising build keys) or the d16 match flag.
+__global__ __launch_bounds__(1024) void jx_part_probe_kernel(const unsigned long long* __restrict__ pent,
+                                                             const uint32_t* __restrict__ pcnt, uint32_t nsrc,
+                                                             uint32_t np, uint32_t pcap, uint64_t range,
+                                                             uint16_t* __restrict__ d16,
+                                                             const uint32_t* __restrict__ notmono,
+                                                             unsigned long long* __restrict__ gsum,
+                                                             uint32_t* __restrict__ gminix,
+                                                             unsigned long long* __restrict__ npairs) {
+    __shared__ unsigned long long sfix[JX_G];
+    __shared__ uint32_t scnt[JX_G], snum[JX_G], smix[JX_G];
+    for (uint32_t k = threadIdx.x; k < JX_G; k += blockDim.x) { sfix[k] = 0; scnt[k] = 0; snum[k] = 0; smix[k] = ~0u; }
+    const bool mono = __builtin_amdgcn_readfirstlane(*notmono) == 0u;
+    __syncthreads();
+    const uint32_t x = blockIdx.x & 7u, sub = blockIdx.x >> 3, nsub = gridDim.x >> 3;
+    unsigned long long pairs = 0;
+    for (uint32_t p = x; p < np; p += 8) {
+        for (uint32_t sb = sub; sb < nsrc; sb += nsub) {
+            const uint32_t n = pcnt[(size_t)sb * np + p];
+            const unsigned long long* e = pent + ((size_t)sb * np + p) * pcap;
+            for (uint32_t i = threadIdx.x; i < n; i += blockDim.x) {
+                const unsigned long long v = e[i];
+                const uint32_t ix = (uint32_t)v, p32 = (uint32_t)(v >> 32);
+                if (ix >= range) continue;                       // (a skipped entry: ~0)
+                const uint32_t gv = d16[ix];
+                if (!gv) continue;
+                const uint32_t gi = (gv & 0x7FFFu) - 1u;
+                if (mono) {
+                    if (ix < smix[gi]) atomicMin(&smix[gi], ix);
+                } else if (!(gv & 0x8000u)) {
+                    d16[ix] = (uint16_t)(gv | 0x8000u);          // (every writer: the same value)
+                }
+                atomicAdd(&scnt[gi], 1u);
+                if (p32 != JX_PNULL) {
+                    atomicAdd(&sfix[gi], (unsigned long long)p32);
+                    atomicAdd(&snum[gi], 1u);
+                }
+                pairs++;
+            }
+        }
+    }
+    for (int o = 32; o > 0; o >>= 1) pairs += __shfl_down(pairs, o, 64);
+    if ((threadIdx.x & 63) == 0 && pairs) atomicAdd(npairs, pairs);
+    __syncthreads();
+    for (uint32_t k = threadIdx.x; k < JX_G; k += blockDim.x) {
+        if (!scnt[k]) continue;
+        if (mono) atomicMin(&gminix[k], smix[k]);
+        atomicAdd(&gsum[3 * k], (unsigned long long)scnt[k]);
+        if (snum[k]) {
+            atomicAdd(&gsum[3 * k + 1], sfix[k]);
+            atomicAdd(&gsum[3 * k + 2], (unsigned long long)snum[k]);
+        }
     }
 }
 
@@ -1951,7 +2156,7 @@ bool fcmp_result(uint32_t op, int c) {
 // fast_kernel's plan shape (see the file comment); fills the FastPlan fields that
 // depend on the plan only
 bool fast_shape(const ScanPlan* P, int grouped, FastPlan* fp, int* ns, bool* where, bool* canonical,
-                bool* wide_num = nullptr) {
+                bool* wide_num = nullptr, int* ext_out = nullptr) {
     if (P->nacc > MAX_ACC || P->ngpart > 0) return false;
     const uint32_t d = P->delim;
     if ((d - '0') < 10u || d == '.' || ((d | 32) >= 'a' && (d | 32) <= 'z') || d == '+' || d == '-') return false;
@@ -1963,8 +2168,19 @@ bool fast_shape(const ScanPlan* P, int grouped, FastPlan* fp, int* ns, bool* whe
     fp->nacc = P->nacc;
     int sslot[2] = {-1, -1};
     *ns = 0;
+    // at most one MIN / MAX, over the one numeric argument of the plan (EXT builds)
+    int ext = 0, ext_slot = -1;
+    fp->ext_acc = -1;
     for (int a = 0; a < P->nacc; a++) {
+        if (P->acc[a].kind == ACC_MIN || P->acc[a].kind == ACC_MAX) {
+            if (ext || getenv("CQGPU_NO_FAST_EXT")) return false;
+            ext = P->acc[a].kind == ACC_MIN ? 1 : 2;
+            fp->ext_acc = a;
+            ext_slot = P->acc[a].slot;
+            continue;
+        }
         if (P->acc[a].kind != ACC_SUM) return false;
+        fp->sum_mask |= 1u << a;
         const int slot = P->acc[a].slot;
         int j = 0;
         while (j < *ns && sslot[j] != slot) j++;
@@ -1974,6 +2190,12 @@ bool fast_shape(const ScanPlan* P, int grouped, FastPlan* fp, int* ns, bool* whe
         }
         if (j) fp->acc1 |= 1u << a;
     }
+    if (ext) {
+        if (*ns == 0) sslot[(*ns)++] = ext_slot;
+        if (*ns != 1 || sslot[0] != ext_slot) return false;
+        fp->ext_col = (uint32_t)P->need_col[ext_slot];
+    }
+    if (ext_out) *ext_out = ext;
     int wcol = -1;
     if (P->nprog == 0) {
         *where = false;
@@ -2035,11 +2257,14 @@ bool fast_shape(const ScanPlan* P, int grouped, FastPlan* fp, int* ns, bool* whe
         canon = canon && k == want;
     }
     *canonical = canon;
-    if (wide_num) {       // a WHERE / SUM column whose sampled fields exceed 4 bytes
+    if (wide_num || ext) {   // a WHERE / SUM column whose sampled fields exceed 4 bytes
         bool wn = false;
         for (int k = 0; k < nr; k++)
             if (roles[k] != 3) wn = wn || ((P->fast_wide_cols >> (cols[k] < 63 ? cols[k] : 63)) & 1);
-        *wide_num = wn || getenv("CQGPU_FAST_WN") != nullptr;
+        wn = wn || getenv("CQGPU_FAST_WN") != nullptr;
+        if (wide_num) *wide_num = wn;
+        // MIN / MAX: the narrow-numeral ',' / '"' canonical build only (fixed point, no doubles)
+        if (ext && (wn || !canon || d != ',' || P->quote != '"')) return false;
     }
     return true;
 }
@@ -2074,7 +2299,13 @@ fast_fn_t pick_wc(bool where, int ns, bool comma, bool rp3, bool wn) {
     return (CANON && !wn) ? pick_ns<G, false, true, CANON, false>(ns, rp3) : pick_ns<G, false, true, CANON, true>(ns, rp3);
 }
 template <bool G>
-fast_fn_t pick_fast(bool where, int ns, bool comma, bool canon, bool rp3, bool wn) {
+fast_fn_t pick_fast(bool where, int ns, bool comma, bool canon, bool rp3, bool wn, int ext = 0) {
+    if (ext) {     // (fast_shape: one argument, ',' / '"', canonical roles, narrow numerals)
+        if (where) return ext == 1 ? fast::fast_kernel<G, true, 1, true, true, 2, false, 1>
+                                   : fast::fast_kernel<G, true, 1, true, true, 2, false, 2>;
+        return ext == 1 ? fast::fast_kernel<G, false, 1, true, true, 2, false, 1>
+                        : fast::fast_kernel<G, false, 1, true, true, 2, false, 2>;
+    }
     return canon ? pick_wc<G, true>(where, ns, comma, rp3, wn) : pick_wc<G, false>(where, ns, comma, rp3, wn);
 }
 
@@ -2126,6 +2357,14 @@ int cq_fast_eligible(const cq::ScanPlan* P, int grouped, int want_rows) {
     if (!fast_shape(P, grouped, &fp, &ns, &where, &canon)) return 0;
     return fast_lds(grouped, ns) <= 160 * 1024 ? 1 : 0;
 }
+// 1 when the plan has a MIN / MAX that fast_kernel takes (an EXT build): the
+// executor gives such plans a raw-key table with extreme cells
+int cq_fast_ext_plan(const cq::ScanPlan* P, int grouped) {
+    FastPlan fp;
+    int ns = 0, ext = 0;
+    bool where = false, canon = false;
+    return fast_shape(P, grouped, &fp, &ns, &where, &canon, nullptr, &ext) && ext ? 1 : 0;
+}
 
 // the scan (the caller runs slow_kernel over slow_list, then raw_merge_kernel)
 hipError_t cq_launch_fast(const uint8_t* g, const cq::ScanPlan* P, const cq::GroupTable* gt,
@@ -2135,7 +2374,8 @@ hipError_t cq_launch_fast(const uint8_t* g, const cq::ScanPlan* P, const cq::Gro
     int ns = 0;
     bool where = false, canon = false;
     bool wn = true;
-    if (!fast_shape(P, grouped, &fp, &ns, &where, &canon, &wn)) return hipErrorInvalidValue;
+    int ext = 0;
+    if (!fast_shape(P, grouped, &fp, &ns, &where, &canon, &wn, &ext)) return hipErrorInvalidValue;
     if (((uintptr_t)g & 255) != 0) return hipErrorInvalidValue;
     const uint64_t hi = P->range_end < P->n ? P->range_end : P->n;
     const uint64_t lo = P->data_begin > P->range_begin ? P->data_begin : P->range_begin;
@@ -2144,7 +2384,7 @@ hipError_t cq_launch_fast(const uint8_t* g, const cq::ScanPlan* P, const cq::Gro
     // the sampled stride is 120 records' worth (lean_kernel's choice): below the
     // largest stride the records average under 33 bytes -> the three-record pass,
     // over windows of the largest stride (test knob CQGPU_FAST_RP2: keep two)
-    const bool rp3 = !grouped && fp.ws < (uint32_t)fast::WS && !getenv("CQGPU_FAST_RP2");
+    const bool rp3 = !grouped && !ext && fp.ws < (uint32_t)fast::WS && !getenv("CQGPU_FAST_RP2");
     if (rp3) fp.ws = (uint32_t)fast::WS;
     if (hi > lo) {
         const uint64_t wl = lo / fp.ws, wh = (hi - 1) / fp.ws;
@@ -2171,8 +2411,9 @@ hipError_t cq_launch_fast(const uint8_t* g, const cq::ScanPlan* P, const cq::Gro
     hipError_t e = cq::upload_buffer(tabs_dev[dev & 63], tabs, sizeof tabs, s);
     if (e != hipSuccess) return e;
     const bool comma = P->delim == ',' && P->quote == '"';
-    const fast_fn_t fn = grouped ? pick_fast<true>(where, ns, comma, canon, false, wn)
-                                 : pick_fast<false>(where, ns, comma, canon, rp3, wn);
+    if (ext && grouped && (!rt || !rt->ext[fp.ext_acc] || !rt->lock[fp.ext_acc])) return hipErrorInvalidValue;
+    const fast_fn_t fn = grouped ? pick_fast<true>(where, ns, comma, canon, false, wn, ext)
+                                 : pick_fast<false>(where, ns, comma, canon, rp3, wn, ext);
     const size_t lds = fast_lds(grouped, ns);
     cq::set_max_lds((const void*)fn, (int)lds);
     hipLaunchKernelGGL(fn, dim3(grid), dim3(fast::LT), lds, s, g, stats, slow_list, slow_cap, fp,
@@ -2229,13 +2470,23 @@ hipError_t cq_jx_star_extract(const uint8_t* g, uint64_t lo, uint64_t hi, uint32
                               uint32_t stride, uint16_t* d16, uint32_t* l32, unsigned long long* ttab,
                               unsigned long long* gsum, unsigned long long* counter, unsigned int* flag,
                               unsigned long long* krange, uint32_t* notmono, unsigned long long* wfl,
-                              uint32_t* gminix, int rp, int grid, hipStream_t s) {
+                              uint32_t* gminix, int rp, int grid, hipStream_t s, unsigned long long* pent,
+                              uint32_t* pcnt, uint32_t np, uint32_t pcap, uint32_t psh) {
     using namespace cq::fast;
     JxPlan jp;
     if (!jx_plan(g, lo, hi, ws, delim, quote, kcol, pcol, &jp)) return hipErrorInvalidValue;
     const int nr = pcol >= 0 ? 2 : 1;
     const bool comma = delim == ',' && quote == '"';
     typedef void (*xfn_t)(const uint8_t*, const JxPlan, const JxOut);
+    const bool part = pent != nullptr;
+    if (part && (build || np == 0 || np > JX_PMAX || pcap == 0 || ((unsigned long long)np << psh) < range))
+        return hipErrorInvalidValue;
+    // partitioned probe, pass 1: [comma][roles - 1][three records per pass]
+    static const xfn_t ptab[2][2][2] = {
+        {{jx_extract_kernel<false, false, 1, false, true, 2, true>, jx_extract_kernel<false, false, 1, false, true, 3, true>},
+         {jx_extract_kernel<false, false, 2, false, true, 2, true>, jx_extract_kernel<false, false, 2, false, true, 3, true>}},
+        {{jx_extract_kernel<false, true, 1, false, true, 2, true>, jx_extract_kernel<false, true, 1, false, true, 3, true>},
+         {jx_extract_kernel<false, true, 2, false, true, 2, true>, jx_extract_kernel<false, true, 2, false, true, 3, true>}}};
     // [build][comma][roles - 1][three records per pass: records under ~33 bytes, where
     // two per pass leave a second, mostly idle pass for the lanes holding a third start]
     static const xfn_t tab[2][2][2][2] = {
@@ -2247,9 +2498,15 @@ hipError_t cq_jx_star_extract(const uint8_t* g, uint64_t lo, uint64_t hi, uint32
           {jx_extract_kernel<true, false, 2, false, true>, jx_extract_kernel<true, false, 2, false, true, 3>}},
          {{jx_extract_kernel<true, true, 1, false, true>, jx_extract_kernel<true, true, 1, false, true, 3>},
           {jx_extract_kernel<true, true, 2, false, true>, jx_extract_kernel<true, true, 2, false, true, 3>}}}};
-    const xfn_t fn = tab[build ? 1 : 0][comma ? 1 : 0][nr - 1][rp == 3 ? 1 : 0];
+    const xfn_t fn = part ? ptab[comma ? 1 : 0][nr - 1][rp == 3 ? 1 : 0]
+                          : tab[build ? 1 : 0][comma ? 1 : 0][nr - 1][rp == 3 ? 1 : 0];
     JxOut jo;
     memset(&jo, 0, sizeof jo);
+    jo.pent = pent;
+    jo.pcnt = pcnt;
+    jo.np = np;
+    jo.pcap = pcap;
+    jo.psh = psh;
     jo.flag = flag;
     jo.krange = krange;
     jo.kmin = kmin;
@@ -2271,10 +2528,24 @@ hipError_t cq_jx_star_extract(const uint8_t* g, uint64_t lo, uint64_t hi, uint32
     jo.notmono = notmono;
     jo.wfl = wfl;
     jo.gminix = gminix;
-    const size_t lds = sizeof(WaveLds) * NWV + (build ? (nr == 2 ? (size_t)JX_G * 8 : 0) : (size_t)JX_G * 20);
+    const size_t lds = sizeof(WaveLds) * NWV +
+                       (part ? (size_t)np * 4 : build ? (nr == 2 ? (size_t)JX_G * 8 : 0) : (size_t)JX_G * 20);
     cq::set_max_lds((const void*)fn, (int)lds);
-    if (jp.nwin == 0) return hipSuccess;
+    if (jp.nwin == 0) {
+        if (part) return hipMemsetAsync(pcnt, 0, (size_t)grid * np * 4, s);
+        return hipSuccess;
+    }
     hipLaunchKernelGGL(fn, dim3(grid), dim3(LT), lds, s, g, jp, jo);
+    return hipGetLastError();
+}
+// partitioned STAR probe, pass 2 (jx_part_probe_kernel): `grid` a multiple of 8
+hipError_t cq_jx_part_probe(const unsigned long long* pent, const uint32_t* pcnt, uint32_t nsrc, uint32_t np,
+                            uint32_t pcap, unsigned long long range, uint16_t* d16, const uint32_t* notmono,
+                            unsigned long long* gsum, uint32_t* gminix, unsigned long long* npairs, int grid,
+                            hipStream_t s) {
+    if (grid < 8 || grid % 8) return hipErrorInvalidValue;
+    hipLaunchKernelGGL(cq::fast::jx_part_probe_kernel, dim3(grid), dim3(1024), 0, s, pent, pcnt, nsrc, np, pcap,
+                       (uint64_t)range, d16, notmono, gsum, gminix, npairs);
     return hipGetLastError();
 }
 hipError_t cq_jx_star_order(const unsigned long long* wfl, unsigned long long nwin, uint32_t* notmono, hipStream_t s) {

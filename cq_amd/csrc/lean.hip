@@ -1302,25 +1302,42 @@ __global__ __launch_bounds__(LT) void lean_kernel(const uint8_t* __restrict__ g,
 // Raw keys -> canonical keys: every distinct raw GROUP BY field is typed once by
 // the general parser (infer_type + parse_value, then create_groups' key text,
 // evaluator_aggregates.c:122-141) and its partial state merged into c_gt.
+// A raw key's MIN / MAX cell (fast_kernel's EXT builds) merges like every other
+// extreme: the wave-uniform seqlock update (scanlib.h g_ext_update), so the thread
+// loop has no early exit.  max_mask bit a: accumulator a is a MAX.
 __global__ __launch_bounds__(256) void raw_merge_kernel(ScanStats* __restrict__ stats, const GroupTable gt,
-                                                        const GroupTable rt, int nacc) {
+                                                        const GroupTable rt, int nacc, uint32_t max_mask) {
     __shared__ __align__(16) uint8_t buf[256 * 32];
     const uint32_t i = blockIdx.x * 256 + threadIdx.x;
-    if (i >= rt.cap || rt.tag[i] < 2) return;
-    const GKey k = canonical_key(buf + threadIdx.x * 32, rt.clslen[i] & 0xFFFF, rt.w0[i], rt.w1[i]);
-    const int gi = g_insert(gt, k, gk_hash(k), stats);
-    if (gi < 0) return;
-    atomicAdd(&gt.cnt[gi], rt.cnt[i]);
-    atomicMin(&gt.first[gi], rt.first[i]);
-    rt.cnt[i] = 0;                    // consumed: a chunked rescan merges each chunk's
-    for (int a = 0; a < nacc; a++) {  // raw state once (first offsets merge by MIN)
-        const unsigned long long n = rt.num[a][i];
-        if (n) {
-            atomicAdd(&gt.sum[a][gi], rt.sum[a][i]);
-            atomicAdd(&gt.num[a][gi], n);
-            rt.sum[a][i] = 0;
-            rt.num[a][i] = 0;
+    const bool live = i < rt.cap && rt.tag[i] >= 2;
+    int gi = -1;
+    if (live) {
+        const GKey k = canonical_key(buf + threadIdx.x * 32, rt.clslen[i] & 0xFFFF, rt.w0[i], rt.w1[i]);
+        gi = g_insert(gt, k, gk_hash(k), stats);
+    }
+    if (gi >= 0) {
+        atomicAdd(&gt.cnt[gi], rt.cnt[i]);
+        atomicMin(&gt.first[gi], rt.first[i]);
+        rt.cnt[i] = 0;                    // consumed: a chunked rescan merges each chunk's
+        for (int a = 0; a < nacc; a++) {  // raw state once (first offsets merge by MIN)
+            if (!rt.num[a]) continue;
+            const unsigned long long n = rt.num[a][i];
+            if (n) {
+                atomicAdd(&gt.sum[a][gi], rt.sum[a][i]);
+                atomicAdd(&gt.num[a][gi], n);
+                rt.sum[a][i] = 0;
+                rt.num[a][i] = 0;
+            }
         }
+    }
+    for (int a = 0; a < nacc; a++) {
+        if (!rt.ext[a] || !gt.ext[a]) continue;       // (uniform)
+        const unsigned long long pos = gi >= 0 ? rt.extpos[a][i] : NOPOS;
+        const bool need = gi >= 0 && pos != NOPOS;
+        const Cell c = need ? rt.ext[a][i] : cell_null();
+        g_ext_update(need, gt, a, ((max_mask >> a) & 1) ? ACC_MAX : ACC_MIN, gi >= 0 ? (uint32_t)gi : 0u, c, pos,
+                     stats);
+        if (need) rt.extpos[a][i] = NOPOS;
     }
 }
 
@@ -1595,8 +1612,9 @@ hipError_t cq_launch_lean(const uint8_t* g, const cq::ScanPlan* P, const cq::Gro
 
 // raw-key table -> canonical table (after cq_launch_lean of a grouped plan)
 hipError_t cq_launch_raw_merge(const cq::GroupTable* gt, const cq::GroupTable* rt, int nacc, cq::ScanStats* stats,
-                               hipStream_t s) {
-    hipLaunchKernelGGL(lean::raw_merge_kernel, dim3((rt->cap + 255) / 256), dim3(256), 0, s, stats, *gt, *rt, nacc);
+                               hipStream_t s, uint32_t max_mask) {
+    hipLaunchKernelGGL(lean::raw_merge_kernel, dim3((rt->cap + 255) / 256), dim3(256), 0, s, stats, *gt, *rt, nacc,
+                       max_mask);
     return hipGetLastError();
 }
 

@@ -64,7 +64,6 @@ constexpr int NLCAP = 4096;                  // terminator indices kept per tile
 constexpr int RSMAX = 2048;                  // record slots per pass
 constexpr int KSTR = 1024;                   // LDS bytes for string literals
 constexpr int LDS_BUDGET = 160 * 1024;       // LDS bytes per CU
-constexpr uint64_t NOPOS = ~0ULL;
 
 static_assert(TILE16 % SCAN_T == 0, "tile loads split evenly over the block");
 static_assert(PF == 2, "a lane stages exactly the 32 bytes it classifies");
@@ -377,74 +376,7 @@ __device__ __forceinline__ bool eval_where_vm(const ScanPlan& P, const Cell* kc,
 // Out-of-line entry points for the rare paths, so the hot loop stays small in
 // the instruction cache.  Cells travel by value (a by-reference argument would
 // force the caller's register-resident cells into scratch memory).
-// ------------------------------------------------------------------ MIN/MAX order
-// reference keeps the first cell that compares strictly better (evaluator_aggregates.c:311-326);
-// within one value class that is the lexicographic (value, position) extreme
-__device__ __forceinline__ bool ext_better(uint8_t kind, const Cell& a, uint64_t pa, const Cell& b,
-                                           uint64_t pb) {
-    if (pb == NOPOS) return true;
-    int c = compare(a, b);
-    if (kind == ACC_MIN) return c < 0 || (c == 0 && pa < pb);
-    return c > 0 || (c == 0 && pa < pb);
-}
-__device__ __forceinline__ uint32_t class_bit(const Cell& c) {
-    return c.kind == K_NULL ? 0u : (c.kind == K_STR ? 2u : (c.kind == K_DATE ? 4u : 1u));
-}
-
-
-// MIN/MAX merges take a per-slot lock.  A lock loop written per lane deadlocks
-// on SIMT hardware (the compiler may park the lane that won the lock until every
-// lane of the wave has won it), so every lock loop here is wave-uniform: the loop
-// runs while ANY lane of the wave still needs the lock, and a lane that takes the
-// lock releases it in the same trip.  Callers must reach these with the whole
-// wave (uniform control flow), passing `need` = false for idle lanes.
-__device__ void g_ext_update(bool need, const GroupTable& gt, int a, uint8_t kind, uint32_t i,
-                             const Cell c, uint64_t pos, ScanStats* st) {
-    if (pos == NOPOS) need = false;
-    // the lock word is a sequence number (even free, odd held, +2 per update): a
-    // candidate that loses against a consistent snapshot drops out without the lock
-    // (the extreme only improves), so a hot group serialises only its improvements
-    uint32_t* lk = &gt.lock[a][i];
-    Cell* ec = &gt.ext[a][i];
-    if (need) {
-        const uint32_t v1 = __hip_atomic_load(lk, __ATOMIC_ACQUIRE, __HIP_MEMORY_SCOPE_AGENT);
-        Cell cur;
-        cur.kind = __hip_atomic_load(&ec->kind, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-        cur.len = __hip_atomic_load(&ec->len, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-        cur.bits = __hip_atomic_load(&ec->bits, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-        const uint64_t cp = __hip_atomic_load(&gt.extpos[a][i], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-        __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");
-        const uint32_t v2 = __hip_atomic_load(lk, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-        if (!(v1 & 1u) && v1 == v2 && !ext_better(kind, c, pos, cur, cp)) need = false;
-    }
-    uint32_t trips = 0;
-    while (__any(need)) {
-        if (need) {
-            const uint32_t v = __hip_atomic_load(lk, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-            if (!(v & 1u) && atomicCAS(lk, v, v + 1u) == v) {
-                __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");
-                Cell cur;
-                cur.kind = __hip_atomic_load(&ec->kind, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-                cur.len = __hip_atomic_load(&ec->len, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-                cur.bits = __hip_atomic_load(&ec->bits, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-                uint64_t cp = __hip_atomic_load(&gt.extpos[a][i], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-                if (ext_better(kind, c, pos, cur, cp)) {
-                    __hip_atomic_store(&ec->kind, c.kind, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-                    __hip_atomic_store(&ec->len, c.len, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-                    __hip_atomic_store(&ec->bits, c.bits, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-                    __hip_atomic_store(&gt.extpos[a][i], (unsigned long long)pos, __ATOMIC_RELAXED,
-                                       __HIP_MEMORY_SCOPE_AGENT);
-                }
-                __hip_atomic_store(lk, v + 2u, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_AGENT);
-                need = false;
-            }
-        }
-        if (++trips > (1u << 20)) {                    // never hang: report and give up
-            if (need) atomicExch(&st->overflow, 2ULL);
-            break;
-        }
-    }
-}
+// (ext_better, class_bit and g_ext_update: scanlib.h, shared with fast_kernel)
 
 // Publish candidate `idx` (already written to gt.cand[a][idx]) as the group's
 // extreme if it is better than the current one: a lock-free pointer swing.  Most
@@ -2581,8 +2513,9 @@ hipError_t cq_launch_lean(const uint8_t* g, const cq::ScanPlan* P, const cq::Gro
                           const cq::GroupTable* rt, cq::ScanStats* stats, unsigned long long* row_out,
                           unsigned long long row_cap, int grouped, int grid, hipStream_t s,
                           unsigned long long* slow_list, unsigned long long slow_cap);
+int cq_fast_ext_plan(const cq::ScanPlan* P, int grouped);
 hipError_t cq_launch_raw_merge(const cq::GroupTable* gt, const cq::GroupTable* rt, int nacc, cq::ScanStats* stats,
-                               hipStream_t s);
+                               hipStream_t s, uint32_t max_mask = 0);
 int cq_fast_eligible(const cq::ScanPlan* P, int grouped, int want_rows);
 int cq_fast_waves_per_block();
 hipError_t cq_launch_fast(const uint8_t* g, const cq::ScanPlan* P, const cq::GroupTable* gt,
@@ -2611,10 +2544,16 @@ int cq_set_scan_mode(int mode) {
 int cq_scan_uses_lean(const cq::ScanPlan* P, int with_cells) {
     return !with_cells && lean_enabled() && cq_lean_eligible(P);
 }
+// bit a set: accumulator a is a MAX (raw_merge_kernel's extreme merge)
+static uint32_t max_mask(const cq::ScanPlan* P) {
+    uint32_t m = 0;
+    for (int a = 0; a < P->nacc; a++) m |= (P->acc[a].kind == cq::ACC_MAX ? 1u : 0u) << a;
+    return m;
+}
 // 2 when it runs fast_kernel, 1 lean_kernel, 0 scan_kernel
 int cq_scan_kernel_kind(const cq::ScanPlan* P, int grouped, int want_rows, int with_cells) {
     if (with_cells || !lean_enabled()) return 0;
-    if (scan_mode() == 0 && cq_fast_eligible(P, grouped, want_rows)) return 2;
+    if (scan_mode() == 0 && cq_fast_eligible(P, grouped, want_rows)) return 2;   // (incl. its MIN / MAX builds)
     return cq_lean_eligible(P) ? 1 : 0;
 }
 
@@ -2634,7 +2573,11 @@ hipError_t cq_launch_scan(const uint8_t* g, const cq::ScanPlan* P, const cq::Gro
                           const cq::GroupTable* rt, cq::ScanStats* stats, unsigned long long* row_out,
                           unsigned long long row_cap, int grouped, int grid, hipStream_t s,
                           cq::Cell* cells_out, unsigned long long* slow_list, unsigned long long slow_cap) {
-    if (cq_scan_uses_lean(P, cells_out != nullptr) && (!grouped || rt)) {
+    // fast_kernel's MIN / MAX builds (cq_fast_ext_plan) take the same route as the
+    // lean-eligible plans; any other MIN / MAX plan the general scan_kernel
+    const bool fext = scan_mode() == 0 && !cells_out && lean_enabled() && row_out == nullptr &&
+                      cq_fast_ext_plan(P, grouped) && cq_fast_eligible(P, grouped, 0);
+    if ((cq_scan_uses_lean(P, cells_out != nullptr) || fext) && (!grouped || rt)) {
         // slow_kernel reads this file's plan and table symbols
         hipError_t e0 = cq::upload_symbol((const void*)&HIP_SYMBOL(cq::c_plan), P, sizeof *P, s);
         if (e0 == hipSuccess)
@@ -2660,7 +2603,7 @@ hipError_t cq_launch_scan(const uint8_t* g, const cq::ScanPlan* P, const cq::Gro
                 hipLaunchKernelGGL(cq::slow_kernel<false>, dim3(SLOW_GRID), dim3(256), 0, s, g, stats, row_out, row_cap,
                                    cells_out, slow_list, slow_cap);
             e = hipGetLastError();
-            if (e == hipSuccess && grouped) e = cq_launch_raw_merge(gt, rt, P->nacc, stats, s);
+            if (e == hipSuccess && grouped) e = cq_launch_raw_merge(gt, rt, P->nacc, stats, s, max_mask(P));
             return e;
         }
     }

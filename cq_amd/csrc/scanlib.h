@@ -8,6 +8,8 @@
 
 namespace cq {
 
+constexpr uint64_t NOPOS = ~0ULL;            // no position (no extreme, no first row)
+
 // WHERE shapes the fast kernels are specialised for
 enum : int { W_NONE = 0, W_SIMPLE = 1, W_VM = 2 };
 
@@ -356,5 +358,75 @@ __device__ __forceinline__ unsigned long long wave_slot(bool on, unsigned long l
 __device__ __forceinline__ uint32_t popc_below(uint32_t m, uint32_t b) {
     return (uint32_t)__popc(m & ((1u << b) - 1));
 }
+
+// ------------------------------------------------------------------ MIN/MAX order
+// reference keeps the first cell that compares strictly better (evaluator_aggregates.c:311-326);
+// within one value class that is the lexicographic (value, position) extreme
+__device__ __forceinline__ bool ext_better(uint8_t kind, const Cell& a, uint64_t pa, const Cell& b,
+                                           uint64_t pb) {
+    if (pb == NOPOS) return true;
+    int c = compare(a, b);
+    if (kind == ACC_MIN) return c < 0 || (c == 0 && pa < pb);
+    return c > 0 || (c == 0 && pa < pb);
+}
+__device__ __forceinline__ uint32_t class_bit(const Cell& c) {
+    return c.kind == K_NULL ? 0u : (c.kind == K_STR ? 2u : (c.kind == K_DATE ? 4u : 1u));
+}
+
+
+// MIN/MAX merges take a per-slot lock.  A lock loop written per lane deadlocks
+// on SIMT hardware (the compiler may park the lane that won the lock until every
+// lane of the wave has won it), so every lock loop here is wave-uniform: the loop
+// runs while ANY lane of the wave still needs the lock, and a lane that takes the
+// lock releases it in the same trip.  Callers must reach these with the whole
+// wave (uniform control flow), passing `need` = false for idle lanes.
+__device__ inline void g_ext_update(bool need, const GroupTable& gt, int a, uint8_t kind, uint32_t i,
+                             const Cell c, uint64_t pos, ScanStats* st) {
+    if (pos == NOPOS) need = false;
+    // the lock word is a sequence number (even free, odd held, +2 per update): a
+    // candidate that loses against a consistent snapshot drops out without the lock
+    // (the extreme only improves), so a hot group serialises only its improvements
+    uint32_t* lk = &gt.lock[a][i];
+    Cell* ec = &gt.ext[a][i];
+    if (need) {
+        const uint32_t v1 = __hip_atomic_load(lk, __ATOMIC_ACQUIRE, __HIP_MEMORY_SCOPE_AGENT);
+        Cell cur;
+        cur.kind = __hip_atomic_load(&ec->kind, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        cur.len = __hip_atomic_load(&ec->len, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        cur.bits = __hip_atomic_load(&ec->bits, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        const uint64_t cp = __hip_atomic_load(&gt.extpos[a][i], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");
+        const uint32_t v2 = __hip_atomic_load(lk, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        if (!(v1 & 1u) && v1 == v2 && !ext_better(kind, c, pos, cur, cp)) need = false;
+    }
+    uint32_t trips = 0;
+    while (__any(need)) {
+        if (need) {
+            const uint32_t v = __hip_atomic_load(lk, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+            if (!(v & 1u) && atomicCAS(lk, v, v + 1u) == v) {
+                __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");
+                Cell cur;
+                cur.kind = __hip_atomic_load(&ec->kind, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+                cur.len = __hip_atomic_load(&ec->len, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+                cur.bits = __hip_atomic_load(&ec->bits, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+                uint64_t cp = __hip_atomic_load(&gt.extpos[a][i], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+                if (ext_better(kind, c, pos, cur, cp)) {
+                    __hip_atomic_store(&ec->kind, c.kind, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+                    __hip_atomic_store(&ec->len, c.len, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+                    __hip_atomic_store(&ec->bits, c.bits, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+                    __hip_atomic_store(&gt.extpos[a][i], (unsigned long long)pos, __ATOMIC_RELAXED,
+                                       __HIP_MEMORY_SCOPE_AGENT);
+                }
+                __hip_atomic_store(lk, v + 2u, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_AGENT);
+                need = false;
+            }
+        }
+        if (++trips > (1u << 20)) {                    // never hang: report and give up
+            if (need) atomicExch(&st->overflow, 2ULL);
+            break;
+        }
+    }
+}
+
 
 }  // namespace cq

@@ -302,6 +302,19 @@ def scan_partitioned_rccl(ast, table):
     return tp, cq_amd.DIST_PATHS.get(path, str(path))
 
 
+def join_partitioned_rccl(ast, lshard, rshard, rest=()):
+    """The repartitioned JOIN step with the whole exchange inside the library
+    (cqgpu_dist_join over its own RCCL communicator, init_library_comm): device
+    routing, one grouped send / recv per side, rebuilt sides, local join, partials
+    merged on rank 0.  Returns the result pointer on rank 0 (None elsewhere); raises
+    PeerFailure on EVERY rank when any rank failed.  Every rank must call it."""
+    import cq_amd
+    tp, status = cq_amd.dist_join_raw(ast, [lshard, rshard, *rest])
+    if status != 0:
+        raise PeerFailure(cq_amd.last_error() or "cqgpu_dist_join failed")
+    return tp
+
+
 def join_partitioned(ast, lshard, rshard, lheader: bytes, rheader: bytes, device: torch.device | str,
                      comm_device: torch.device | str | None = None, rest=()):
     """Repartitioned JOIN over this rank's shards of both inputs of the first JOIN.

@@ -165,6 +165,17 @@ int cqgpu_comm_unique_id(void* id_out);
 int cqgpu_comm_init(const void* id, int rank, int world);
 void cqgpu_comm_destroy(void);
 cq_table* cqgpu_dist_query(cq_node* query_ast, cqgpu_table* shard, int* status, int* path);
+/* cqgpu_dist_join: the repartitioned JOIN step (perform_join / process_joins,
+ * evaluator_joins.c:63-181, 237-274, over inputs spread across the ranks) inside the
+ * library.  tables = [this rank's shard of the FROM table, this rank's shard of the
+ * first JOIN's table, a chain's later tables whole].  Both sides are routed by the
+ * first ON key (cqgpu_route_plan's rule: whole number keys by key mod N), the
+ * records and their global ids exchanged in one grouped ncclSend / ncclRecv per
+ * side, rebuilt as this rank's sides (key stride N: a dense build key range stays
+ * on the STAR join), joined locally, and the join partials merged on rank 0
+ * (cqgpu_merge_partials' nested-loop order).  Rank 0 returns the result; *status:
+ * 0, or -1 on EVERY rank when any rank failed (refusals included). */
+cq_table* cqgpu_dist_join(cq_node* query_ast, cqgpu_table* const* tables, int ntables, int* status);
 /* test entry: the gather-merge of `n` shards held by this one process (simulated
  * ranks, no RCCL): every shard's pack, then rank 0's merge kernels; NULL +
  * cqgpu_last_ineligible when the plan or the data leaves the gather-merge */

@@ -26,12 +26,23 @@ def main():
     init_library_comm()
     results = []
     for sql, path in items:
-        print(f"dist worker: {sql.format(p=path)}", file=sys.stderr, flush=True)   # (a failure names its query)
-        t = cq_amd.Table.open_range(path, rank, world)
-        with cqtest.Parsed(sql.format(p=path)) as ast:
+        # path: one file (cqgpu_dist_query over its range shard), or a JOIN's files
+        # [FROM, JOIN, later chain tables] (cqgpu_dist_join: range shards of the first
+        # two, the chain's tables whole); the SQL names them {p}, {q}, {r}, ...
+        paths = path if isinstance(path, list) else [path]
+        text = sql.format(**dict(zip("pqrs", paths)))
+        print(f"dist worker: {text}", file=sys.stderr, flush=True)   # (a failure names its query)
+        tabs = [cq_amd.Table.open_range(x, rank, world) if i < 2 else cq_amd.Table.open(x)
+                for i, x in enumerate(paths)]
+        t = tabs[0]
+        with cqtest.Parsed(text) as ast:
             got = None
             for _ in range(2):                      # a warm-up step, then the kept one
-                tp, status, p = cq_amd.dist_query_raw(ast, t)
+                if len(paths) > 1:
+                    tp, status = cq_amd.dist_join_raw(ast, tabs)
+                    p = 0
+                else:
+                    tp, status, p = cq_amd.dist_query_raw(ast, t)
                 if got is not None or status != 0:
                     break
                 if tp:
@@ -42,7 +53,8 @@ def main():
             results.append({"sql": sql, "status": status, "path": p, "error": cq_amd.last_error(),
                             "result": None if got in (None, "none") else
                             {"columns": got["columns"], "rows": [[list(c) for c in r] for r in got["rows"]]}})
-        t.close()
+        for x in tabs:
+            x.close()
     cq_amd.comm_destroy()
     if rank == 0:
         with open(out, "w") as fh:

@@ -62,6 +62,15 @@ def files(tmp_path_factory):
     out["verylong"] = os.path.join(d, "verylong.csv")
     with open(out["verylong"], "w") as fh:
         fh.write("k,v\n" + "\n".join("%s,%d" % ("x" * 60 + str(i % 5), i % 7) for i in range(20_000)) + "\n")
+    out["users"] = os.path.join(d, "users.csv")
+    with open(out["users"], "wb") as fh:
+        fh.write(datagen.users_bytes(4000, seed=7))
+    out["orders"] = os.path.join(d, "orders.csv")
+    with open(out["orders"], "wb") as fh:
+        fh.write(datagen.orders_bytes(9000, 4500, seed=8))
+    out["roles"] = os.path.join(d, "roles.csv")
+    with open(out["roles"], "w") as fh:
+        fh.write("role,dept\n" + "".join("role_%03d,dept%d\n" % (i, i % 7) for i in range(0, 1000, 3)))
     out["many"] = os.path.join(d, "many.csv")
     with open(out["many"], "w") as fh:
         fh.write("k,v\n" + "\n".join("%d,%d" % (i % 9000, i % 7) for i in range(40_000)) + "\n")
@@ -181,3 +190,43 @@ def test_dist_query_gather_merge_failure_reported(files, tmp_path, knob):
     res = _dist_run(files, tmp_path, [(GM[0], "plain")], env={knob: "1"})
     assert res[0]["status"] == -1, res[0]
     assert "injected" in res[0]["error"], res[0]["error"]
+
+
+JOINS = [   # the repartitioned JOIN step inside the library (cqgpu_dist_join)
+    ("SELECT u.role, COUNT(*), SUM(o.price), AVG(o.price) FROM '{p}' AS u JOIN '{q}' AS o "
+     "ON u.id = o.customer_id GROUP BY u.role", ["users", "orders"]),
+    ("SELECT COUNT(*), SUM(o.price) FROM '{p}' AS u LEFT JOIN '{q}' AS o ON u.id = o.customer_id", ["users", "orders"]),
+    ("SELECT u.name, o.price FROM '{p}' AS u JOIN '{q}' AS o ON u.id = o.customer_id WHERE o.price > 995",
+     ["users", "orders"]),
+    ("SELECT r.dept, COUNT(*), SUM(o.price) FROM '{p}' AS u JOIN '{q}' AS o ON u.id = o.customer_id "
+     "JOIN '{r}' AS r ON u.role = r.role GROUP BY r.dept", ["users", "orders", "roles"]),
+]
+
+
+def test_dist_join_one_rank_rccl(files, tmp_path):
+    """cqgpu_dist_join at world size 1 over RCCL: the routing, the grouped send /
+    recv exchange (to itself), the rebuilt sides (key stride 1), the local join and
+    the partial merge, each query against the oracle over the whole files"""
+    res = _dist_run_paths(files, tmp_path, JOINS)
+    for (sql, keys), r in zip(JOINS, res):
+        q = sql.format(**dict(zip("pqrs", [files[k] for k in keys])))
+        assert r["status"] == 0, (q, r["error"])
+        want, unsup = cqtest.oracle_query(q)
+        assert not unsup
+        got = {"columns": [c.encode("latin-1") for c in r["result"]["columns"]],
+               "rows": [[_cell(c) for c in row] for row in r["result"]["rows"]]}
+        with cqtest.Parsed(q) as ast:
+            tol = tolerant_columns(ast)
+        compare(got, want, tol, f"dist_join: {q}")
+
+
+def _dist_run_paths(files, tmp_path, items, env=None):
+    out = str(tmp_path / "distj.json")
+    cmd = [sys.executable, "-m", "torch.distributed.run", "--nnodes=1", "--nproc-per-node=1",
+           "--master-addr", "127.0.0.1", "--master-port", str(_port()), os.path.join(ROOT, "tests", "dist_rccl_worker.py"),
+           out, json.dumps([[s, [files[k] for k in keys]] for s, keys in items])]
+    e = dict(os.environ)
+    e.update(env or {})
+    p = subprocess.run(cmd, cwd=ROOT, capture_output=True, text=True, timeout=110, env=e)
+    assert p.returncode == 0, p.stderr[:6000] + "\n...\n" + p.stderr[-2000:]
+    return json.load(open(out))

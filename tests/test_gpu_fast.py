@@ -280,3 +280,40 @@ def test_fast_narrow_numerals_late_wide(d, monkeypatch, wn):
             assert st["slow_records"] == 0, st
         else:
             assert st["slow_records"] > 0, st
+
+
+def test_fast_min_max(d):
+    """MIN / MAX of narrow numerals in fast_kernel (EXT builds): (10^-3 fixed-point
+    value, first-row code) in one 64-bit LDS atomic, the extreme's cell re-typed from
+    its record at the flush (evaluate_aggregate keeps the first cell that compares
+    strictly better, evaluator_aggregates.c:311-326): ties between spellings of one
+    value ("1.5" / "1.50" / INTEGER vs DOUBLE) keep the first record's cell; NULLs
+    skipped; groups whose every value is NULL keep NULL"""
+    rng = np.random.default_rng(31)
+    heights = ["1.5", "1.50", "2", "2.0", "0.75", "3", "", "9.99", "0.5"]
+    rows = ["n%d,s,%d,%s,%s,role_%03d" % (i % 7, rng.integers(10, 81), "fm"[i % 2],
+                                           heights[int(rng.integers(0, len(heights)))] if i % 97 else "",
+                                           int(rng.integers(0, 300))) for i in range(150_000)]
+    rows += ["n0,s,40,f,,role_999"] * 5                               # a group of NULLs only
+    p = _write(d / "ext.csv", "name,surname,age,gender,height,role", rows)
+    for q in (f"SELECT role, COUNT(*), SUM(height), AVG(height), MIN(height) FROM '{p}' WHERE age > 30 GROUP BY role",
+              f"SELECT role, MAX(height) FROM '{p}' GROUP BY role",
+              f"SELECT role, MIN(height), COUNT(*) FROM '{p}' WHERE age <= 40 GROUP BY role",
+              f"SELECT MIN(height) FROM '{p}'",
+              f"SELECT COUNT(*), MAX(height), SUM(height) FROM '{p}' WHERE age > 70",
+              f"SELECT gender, MAX(age) FROM '{p}' GROUP BY gender"):
+        check(q)
+
+
+def test_fast_min_max_declined_and_mixed(d):
+    """shapes the EXT builds leave to the general scan: two extremes, an extreme over
+    a second numeric column; and a column that mixes numbers with text (the slow
+    path's STRING cells: value_compare's cross-class "equal" makes the result order-
+    dependent, which the class-split passes reproduce)"""
+    rows = ["%d,%s,%d" % (i % 50, ("x%d" % i) if i % 1009 == 0 else "%d.%d" % (i % 9, i % 10), i % 77)
+            for i in range(80_000)]
+    p = _write(d / "mixed_ext.csv", "g,v,w", rows)
+    check(f"SELECT g, MIN(v), COUNT(*) FROM '{p}' GROUP BY g", fast=False)
+    check(f"SELECT g, MIN(w), MAX(w) FROM '{p}' GROUP BY g", fast=False)
+    check(f"SELECT g, SUM(v), MAX(w) FROM '{p}' GROUP BY g", fast=False)
+    check(f"SELECT g, MAX(w), COUNT(*) FROM '{p}' WHERE w > 5 GROUP BY g")

@@ -154,3 +154,37 @@ def test_star_join_declines(tmp_path):
     assert _run(sqlt.format(u=u, o=o)) == 3
     u, o = _star_tables(tmp_path, 12_000, "shuffled", 14, ntags=5000)
     assert _run(sqlt.format(u=u, o=o)) == 3
+
+
+@pytest.mark.parametrize("order", ["ascending", "shuffled"])
+def test_star_join_partitioned_probe(tmp_path, monkeypatch, order):
+    """the partitioned STAR probe (fast.hip jx_part_probe_kernel: probe records
+    appended per key partition, each partition looked up by one XCD's blocks), forced
+    on small tables with 64-slot partitions; rising build keys (smallest matched key
+    per group) and shuffled ones (d16 match flags, jx_star_first_kernel)"""
+    monkeypatch.setenv("CQGPU_PART_PROBE_MIN", "0")
+    monkeypatch.setenv("CQGPU_PART_PROBE_SHIFT", "6")
+    u, o = _star_tables(tmp_path, 12_000, order, 21)
+    for sql in (f"SELECT u.role, COUNT(*), SUM(o.price), AVG(o.price) FROM '{u}' AS u JOIN '{o}' AS o "
+                "ON u.id = o.customer_id GROUP BY u.role",
+                f"SELECT COUNT(*), SUM(o.quantity) FROM '{u}' AS u JOIN '{o}' AS o ON u.id = o.customer_id",
+                f"SELECT u.name, COUNT(*) FROM '{u}' AS u JOIN '{o}' AS o ON u.id = o.customer_id GROUP BY u.name"):
+        assert _run(sql) == 4, sql
+
+
+def test_star_join_partitioned_probe_falls_back(tmp_path, monkeypatch):
+    """partition regions sized for uniform probe keys: every order of one customer
+    overflows its region, and a payload past 31 bits cannot be an entry -- both rerun
+    the STAR probe unpartitioned (still the oracle's answer, still kind 4)"""
+    monkeypatch.setenv("CQGPU_PART_PROBE_MIN", "0")
+    monkeypatch.setenv("CQGPU_PART_PROBE_SHIFT", "6")
+    n = 12_000
+    rows = [f"{i + 10**10},n{i % 91},{18 + i % 60},r{i % 40:04d}" for i in range(n)]
+    u = _write(tmp_path, "fu.csv", "id,name,age,role", rows)
+    o1 = _write(tmp_path, "fo1.csv", "id,price,customer_id", [f"{j},{j % 997}.25,{10**10 + 77}" for j in range(3000)])
+    o2 = _write(tmp_path, "fo2.csv", "id,price,customer_id",
+                [f"{j},{'9999999' if j == 5 else str(j % 97) + '.5'},{10**10 + (j * 7) % n}" for j in range(3000)])
+    for o in (o1, o2):
+        sql = (f"SELECT u.role, COUNT(*), SUM(o.price) FROM '{u}' AS u JOIN '{o}' AS o "
+               "ON u.id = o.customer_id GROUP BY u.role")
+        assert _run(sql) == 4, sql

@@ -226,11 +226,15 @@ def test_partial_stats_reset_per_call(files):
         cq_amd.result_free(tp)
 
 
-def test_repartitioned_fused_join_1m_8_ranks():
+@pytest.mark.parametrize("partitioned", [False, True])
+def test_repartitioned_fused_join_1m_8_ranks(monkeypatch, partitioned):
     """1e6 users x 1e6 orders over 8 simulated ranks (no small-table slack in the
     STAR range test): every rank must take STAR, and the merged result must equal the
     exact nested-loop answer computed here with numpy (COUNT exact, SUM/AVG 1e-6
     relative; groups in the order of their first matched user)"""
+    if partitioned:      # the partitioned probe on every rank (64 Ki-slot partitions)
+        monkeypatch.setenv("CQGPU_PART_PROBE_MIN", "0")
+        monkeypatch.setenv("CQGPU_PART_PROBE_SHIFT", "16")
     n = 1_000_000
     users = datagen.users_bytes(n, seed=21)
     orders = datagen.orders_bytes(n, n, seed=22)
