@@ -56,6 +56,8 @@ hipError_t cq_launch_finish_pack(const uint8_t* g, uint64_t n, const GroupOut* o
 unsigned int cq_finish_pack_max();
 hipError_t cq_launch_compact(const GroupTable* gt, const ScanPlan* P, GroupOut* out, unsigned int* count,
                              unsigned int cap_out, hipStream_t s, unsigned long long* ofirst);
+hipError_t cq_launch_comp_text(const cq::Cell* cells, uint32_t n, uint32_t cap, uint8_t* out, uint32_t* lens,
+                               hipStream_t s);
 hipError_t cq_launch_gather(const uint8_t* g, const ScanPlan* P, const unsigned long long* recs,
                             uint32_t nrec, Cell* out, hipStream_t s);
 hipError_t cq_launch_copy_strings(const Cell* cells, uint32_t n, const unsigned long long* offs,
@@ -163,6 +165,7 @@ hipError_t cq_launch_gm_merge(const uint8_t* buf, uint64_t B, uint32_t N, uint32
 int cq_fast_ext_plan(const cq::ScanPlan* P, int grouped);
 hipError_t cq_launch_raw_merge(const cq::GroupTable* gt, const cq::GroupTable* rt, int nacc, cq::ScanStats* stats,
                                hipStream_t s, uint32_t max_mask = 0);
+hipError_t cq_launch_join_cross(uint32_t na, uint32_t nb, uint2* pairs, hipStream_t s);
 uint64_t cq_jx_windows(uint64_t lo, uint64_t hi, uint32_t ws);
 hipError_t cq_jx_extract(const uint8_t* g, uint64_t lo, uint64_t hi, uint32_t ws, uint32_t delim, uint32_t quote,
                          int kcol, int pcol, int build, int pass, unsigned long long* key, unsigned long long* pay,
@@ -520,6 +523,19 @@ struct RouteState {
 
 constexpr uint64_t SAMPLE_BYTES = 256u << 10;   // bytes a table keeps for plan-time sampling
 
+// the device byte ranges of the live tables: a group's STRING cells (representative,
+// MIN/MAX and long-key cells) address table bytes, checked before the copy kernel
+// dereferences them (a kernel bug becomes an error, never an out-of-bounds read)
+std::map<uintptr_t, uintptr_t> g_table_ranges;   // begin -> end
+void note_table_bytes(const uint8_t* p, size_t n) { if (p) g_table_ranges[(uintptr_t)p] = (uintptr_t)p + n; }
+void forget_table_bytes(const uint8_t* p) { if (p) g_table_ranges.erase((uintptr_t)p); }
+bool in_some_table(uint64_t a, uint32_t len) {
+    auto it = g_table_ranges.upper_bound((uintptr_t)a);
+    if (it == g_table_ranges.begin()) return false;
+    --it;
+    return a >= it->first && a + len <= it->second;
+}
+
 struct cqgpu_table {
     uint8_t* dbuf = nullptr;
     const uint8_t* g = nullptr;      // device byte 0
@@ -637,6 +653,7 @@ cqgpu_table* upload(const uint8_t* host, size_t n, cq_csv_config cfg, uint64_t b
     }
     size_t total = PAD_BEFORE + n + PAD_AFTER;
     HIPCHECK(hipMalloc(&t->dbuf, total));
+    note_table_bytes(t->dbuf, total);
     HIPCHECK(hipMemsetAsync(t->dbuf, '\n', PAD_BEFORE, c.stream));
     HIPCHECK(hipMemsetAsync(t->dbuf + PAD_BEFORE + n, '\n', PAD_AFTER, c.stream));
     // stream the bytes through pinned staging buffers: groups of P 32 MiB chunks are
@@ -752,8 +769,9 @@ HCell from_value(const cq_value& v) {              // to_value's inverse (result
     return h;
 }
 
-// device cells -> host cells (strings copied back with one kernel)
-std::vector<HCell> fetch_cells(DevCtx& c, const std::vector<Cell>& cells) {
+// device cells -> host cells (strings copied back with one kernel); `table_cells`:
+// every STRING must lie in a live table's bytes
+std::vector<HCell> fetch_cells(DevCtx& c, const std::vector<Cell>& cells, bool table_cells = false) {
     std::vector<HCell> out(cells.size());
     std::vector<unsigned long long> offs(cells.size(), 0);
     unsigned long long total = 0;
@@ -762,6 +780,12 @@ std::vector<HCell> fetch_cells(DevCtx& c, const std::vector<Cell>& cells) {
         out[i].bits = cells[i].bits;
         offs[i] = total;
         if (cells[i].kind == K_STR) total += cells[i].len;
+        if (table_cells && cells[i].kind == K_STR && cells[i].len && !in_some_table(cells[i].bits, cells[i].len)) {
+            char b[160];
+            snprintf(b, sizeof b, "internal: a group's STRING cell %zu of %zu (address 0x%llx, %u bytes) is outside every table",
+                     i, cells.size(), (unsigned long long)cells[i].bits, cells[i].len);
+            throw HipError{b};
+        }
     }
     if (total == 0 && std::none_of(cells.begin(), cells.end(), [](const Cell& x) { return x.kind == K_STR; }))
         return out;
@@ -1624,8 +1648,22 @@ std::vector<HGroup> make_groups(DevCtx& c, const Compiled& C, uint64_t limit, ui
             long_at.push_back(k);
         }
     }
+    if (getenv("CQGPU_DEBUG_GROUPS")) {   // the groups as the device returned them
+        fprintf(stderr, "make_groups: %zu groups, %u cells each\n", outs.size(), ncell);
+        for (size_t i = 0; i < outs.size() && i < 16; i++) {
+            const GroupOut& o = outs[i];
+            fprintf(stderr, "  g%zu cls %u len %u w0 0x%llx w1 0x%llx cnt %llu first %llu\n", i, o.clslen >> 16,
+                    o.clslen & 0xffff, (unsigned long long)o.w0, (unsigned long long)o.w1, (unsigned long long)o.cnt,
+                    (unsigned long long)o.first);
+            for (uint32_t k = 0; k < ncell && (i + 1) * ncell <= fcells.size(); k++)
+                fprintf(stderr, "    cell %u kind %u len %u bits 0x%llx\n", k, fcells[i * ncell + k].kind,
+                        fcells[i * ncell + k].len, (unsigned long long)fcells[i * ncell + k].bits);
+        }
+        for (auto& r : g_table_ranges)
+            fprintf(stderr, "  table bytes [0x%llx, 0x%llx)\n", (unsigned long long)r.first, (unsigned long long)r.second);
+    }
     if (!longs.empty()) {
-        std::vector<HCell> hl = fetch_cells(c, longs);
+        std::vector<HCell> hl = fetch_cells(c, longs, true);
         for (size_t i = 0; i < longs.size(); i++) hcells[long_at[i]] = hl[i];
     }
     PHASE("hcells");
@@ -3056,8 +3094,19 @@ uint32_t key_class_mask(DevCtx& c, const JoinSide& S, int kcol) {
 // RIGHT / FULL append the unmatched right rows (-, r) in row order.  kl / kr:
 // the ON operands' columns of A / B (keyed: both resolved).
 unsigned long long build_pairs(DevCtx& c, JoinSide& A, JoinSide& B, int kl, int kr, bool keyed, bool outer_left,
-                               bool outer_right, DevBuf& pairs) {
+                               bool outer_right, DevBuf& pairs, bool cross = false) {
     unsigned long long np = 0;
+    if (cross && A.n && B.n) {
+        // JOIN without ON: evaluate_join_condition is true for a NULL condition
+        // (evaluator_joins.c:42), so every (l, r) pair matches, in the nested loops'
+        // order, and no row of either side is unmatched
+        np = (unsigned long long)A.n * B.n;
+        if (np >= (1ull << 31)) throw Ineligible{"JOIN without ON: a cross product of 2^31 or more pairs"};
+        DevBuf pb(np * 8);
+        std::swap(pairs.p, pb.p);
+        HIPCHECK(cq_launch_join_cross(A.n, B.n, pairs.as<uint2>(), c.stream));
+        return np;
+    }
     if (keyed && A.n && B.n) {
         const uint32_t ls = (uint32_t)A.cols.size(), rs = (uint32_t)B.cols.size();
         const uint32_t lk = (uint32_t)A.slot(kl), rk = (uint32_t)B.slot(kr);
@@ -3687,7 +3736,7 @@ cq_table* run_join(DevCtx& c, cq_node* q, const cqgpu_table* L, const cqgpu_tabl
     struct Level {
         const cqgpu_table* R;
         std::string ra;
-        bool outer_left, outer_right, keyed;
+        bool outer_left, outer_right, keyed, cross;
         int kl, kr, nleft;
         std::set<int> lneed, rneed;
     };
@@ -3704,13 +3753,14 @@ cq_table* run_join(DevCtx& c, cq_node* q, const cqgpu_table* L, const cqgpu_tabl
         v.R = rights[j];
         if (!v.R) throw Ineligible{"join table failed to load"};
         cq_node* on = jn->u.join.on;
-        if (!on) throw Ineligible{"JOIN without ON (cross product)"};
+        v.cross = on == nullptr;              // JOIN without ON: the cross product (evaluator_joins.c:42)
+        if (v.cross && part && j == 0) throw Ineligible{"JOIN without ON across partials"};
         v.ra = jn->u.join.alias ? jn->u.join.alias : "right";
         cqgpu_table W;                       // the left side's schema at this level
         W.names = wnames;
         // ON operands (anything but `ident = ident` matches no pair)
         v.kl = v.kr = -1;
-        if (on->kind == CQ_N_CONDITION && on->u.bin.op && !strcmp(on->u.bin.op, "=") && on->u.bin.lhs &&
+        if (on && on->kind == CQ_N_CONDITION && on->u.bin.op && !strcmp(on->u.bin.op, "=") && on->u.bin.lhs &&
             on->u.bin.rhs && on->u.bin.lhs->kind == CQ_N_IDENTIFIER && on->u.bin.rhs->kind == CQ_N_IDENTIFIER) {
             v.kl = join_on_index(on->u.bin.lhs->u.text, &W, &W, wa.c_str(), v.R, v.ra.c_str());
             v.kr = join_on_index(on->u.bin.rhs->u.text, v.R, &W, wa.c_str(), v.R, v.ra.c_str());
@@ -3775,7 +3825,7 @@ cq_table* run_join(DevCtx& c, cq_node* q, const cqgpu_table* L, const cqgpu_tabl
         if (Bp->cols.empty()) Bp->cols.push_back(0);
         load_side(c, v.R, *Bp);
         DevBuf pb(8);
-        np = build_pairs(c, *Ap, *Bp, v.kl, v.kr, v.keyed, v.outer_left, v.outer_right, pb);
+        np = build_pairs(c, *Ap, *Bp, v.kl, v.kr, v.keyed, v.outer_left, v.outer_right, pb, v.cross);
         std::swap(pairs.p, pb.p);
         if (part && j == 0 && v.keyed) {     // even when one side is empty on this rank
             part->lmask |= key_class_mask(c, *Ap, v.kl);
@@ -3991,6 +4041,46 @@ cq_table* run_join(DevCtx& c, cq_node* q, const cqgpu_table* L, const cqgpu_tabl
 // columns parsed into cells (record-start kernels + cells_kernel), then the pair
 // aggregation with one "pair" (row, -) per record.  Groups come back in
 // first-appearance order with whole-file byte offsets, like run_aggregate's.
+// Range partials of a composite GROUP BY: each group's key becomes its joined key
+// text (scan.hip comp_text_kernel, from the group's first record), carried as a
+// text key (GK_LONG class) so the dense and blob merges across ranks group by the
+// text byte for byte -- create_groups' own identity (evaluator.c:113-212) -- instead
+// of by the 128-bit part digest each rank computed (exact even for a digest
+// collision between ranks).  Every key of such a plan is composite, so no
+// single-column text key can meet these.
+void comp_key_texts(DevCtx& c, const cqgpu_table* t, const Compiled& C, std::vector<HGroup>& groups) {
+    if (C.P.ngpart < 2 || groups.empty()) return;
+    constexpr uint32_t CAP = 4096;
+    const uint32_t n = (uint32_t)groups.size();
+    std::vector<unsigned long long> recs(n);
+    for (uint32_t i = 0; i < n; i++) {
+        const HGroup& h = groups[i];
+        if (h.first == NOPOS || h.first < t->base_offset || h.first - t->base_offset >= t->n)
+            throw HipError{"composite key text: a group without its first record"};
+        recs[i] = h.first - t->base_offset;
+    }
+    const uint32_t nneed = (uint32_t)std::max(C.P.nneed, 1);
+    DevBuf drecs((size_t)n * 8), dcells((size_t)n * nneed * sizeof(Cell)), dtext((size_t)n * CAP), dlen((size_t)n * 4);
+    HIPCHECK(hipMemcpyAsync(drecs.p, recs.data(), (size_t)n * 8, hipMemcpyHostToDevice, c.stream));
+    HIPCHECK(cq_launch_gather(t->g, &C.P, drecs.as<unsigned long long>(), n, dcells.as<Cell>(), c.stream));
+    HIPCHECK(cq_launch_comp_text(dcells.as<Cell>(), n, CAP, dtext.as<uint8_t>(), dlen.as<uint32_t>(), c.stream));
+    std::vector<uint32_t> lens(n);
+    std::vector<uint8_t> text((size_t)n * CAP);
+    HIPCHECK(hipMemcpyAsync(lens.data(), dlen.p, (size_t)n * 4, hipMemcpyDeviceToHost, c.stream));
+    HIPCHECK(hipMemcpyAsync(text.data(), dtext.p, text.size(), hipMemcpyDeviceToHost, c.stream));
+    HIPCHECK(hipStreamSynchronize(c.stream));
+    for (uint32_t i = 0; i < n; i++) {
+        if (lens[i] == 0xFFFFFFFFu)
+            throw Ineligible{"composite GROUP BY across partials: a key text over 4 KiB or a DOUBLE part of 2^43 or more"};
+        HGroup& h = groups[i];
+        h.kcls = GK_LONG;
+        h.klen = lens[i];
+        h.kbytes.assign((const char*)text.data() + (size_t)i * CAP, lens[i]);
+        h.kw0 = 0;
+        h.kw1 = 0;
+    }
+}
+
 std::vector<HGroup> run_cells_aggregate(DevCtx& c, const cqgpu_table* t, Compiled& C, Literals& Lit,
                                         ScanStats* st_out = nullptr, bool partial = false) {
     parse_literals(c, C.lits, Lit);
@@ -4267,6 +4357,7 @@ uint64_t cache_limit() {
 void cache_drop(size_t i) {
     cqgpu_table* t = g_cache[i].t;
     g_cache.erase(g_cache.begin() + (long)i);
+    forget_table_bytes(t->dbuf);
     if (t->dbuf) (void)hipFree(t->dbuf);
     if (t->gids) (void)hipFree(t->gids);
     delete t;
@@ -4577,9 +4668,11 @@ cqgpu_table* cqgpu_table_from_routed(const void* dev_bytes, size_t n, const uint
         if ((n && !dev_bytes) || (nrec && !dev_gids)) throw HipError{"routed table: null buffer"};
         t = upload(nullptr, 0, cfg, 0, header, header_len);
         // replace the empty upload with the received bytes (records already '\n'-terminated)
+        forget_table_bytes(t->dbuf);
         (void)hipFree(t->dbuf);
         t->dbuf = nullptr;
         HIPCHECK(hipMalloc(&t->dbuf, PAD_BEFORE + n + PAD_AFTER));
+        note_table_bytes(t->dbuf, PAD_BEFORE + n + PAD_AFTER);
         HIPCHECK(hipMemsetAsync(t->dbuf, '\n', PAD_BEFORE, c.stream));
         HIPCHECK(hipMemsetAsync(t->dbuf + PAD_BEFORE + n, '\n', PAD_AFTER, c.stream));
         if (n) HIPCHECK(hipMemcpyAsync(t->dbuf + PAD_BEFORE, dev_bytes, n, hipMemcpyDeviceToDevice, c.stream));
@@ -4633,6 +4726,7 @@ int cqgpu_table_set_record_total(cqgpu_table* t, uint64_t total) {
 
 void cqgpu_table_free(cqgpu_table* t) {
     if (!t) return;
+    forget_table_bytes(t->dbuf);
     if (t->dbuf) (void)hipFree(t->dbuf);
     if (t->gids) (void)hipFree(t->gids);
     delete t;
@@ -5150,6 +5244,7 @@ size_t cqgpu_query_partial(cq_node* q, cqgpu_table* const* tables, int ntables, 
                 groups = run_cells_aggregate(c, t, C, L, &st, true);
             }
         }
+        comp_key_texts(c, t, C, groups);             // (composite keys: their joined texts)
         Blob b;
         b.u32(0x31505143u);                          // "CQP1"
         b.u32((uint32_t)t->names.size());
@@ -5621,6 +5716,7 @@ cqgpu_partial* cqgpu_partial_new(cq_node* q, cqgpu_table* const* tables, int nta
                 groups = run_cells_aggregate(c, t, C, L, &st, true);
             }
         }
+        comp_key_texts(c, t, C, groups);             // (composite keys: their joined texts)
         PHASE("partial scan");
         const uint32_t m = (uint32_t)groups.size();
         p->m = m;

@@ -1245,7 +1245,31 @@ __global__ void gather_kernel(const uint8_t* __restrict__ g,
     parse_record_out(g + recs[i], P, out + (uint64_t)i * P.nneed);
 }
 
-// evaluate_expression (evaluator_expressions.c:23-263) over one record's need
+// ------------------------------------------------------------------ composite key texts
+// One record's parsed need cells (gather_kernel's rows) as a cell view
+struct RowView {
+    const Cell* c;
+};
+__device__ __forceinline__ Cell get_cell(const RowView& v, int a, int = 0) { return v.c[a]; }
+// joined-text sink with a byte cap (n keeps counting past it: the caller sees the overflow)
+struct TextSink {
+    uint8_t* p;
+    uint32_t cap, n;
+    __device__ void byte(uint8_t c) {
+        if (n < cap) p[n] = c;
+        n++;
+    }
+    __device__ void bytes(const uint8_t* q, uint32_t k) { for (uint32_t i = 0; i < k; i++) byte(q[i]); }
+    __device__ void dec(uint64_t v, int mind) {
+        uint8_t t[20];
+        int k = 0;
+        do { t[k++] = (uint8_t)('0' + v % 10); v /= 10; } while (v);
+        while (k < mind) t[k++] = '0';
+        while (k) byte(t[--k]);
+    }
+};
+
+
 // slots: a composite / expression GROUP BY part, prog[b, e)
 template <class CS>
 __device__ Cell eval_expr_vm(const ScanPlan& P, const Cell* kc, const CS& cs, uint32_t b, uint32_t e) {
@@ -1315,6 +1339,27 @@ __device__ GKey plan_group_key(const ScanPlan& P, const Cell* kc, const CS& cs, 
         k.w1 = 0;
     }
     return k;
+}
+
+// A composite GROUP BY group's key as create_groups builds it (evaluator.c:113-212):
+// every part's key text (NULL, %lld, %.6f, %04d-%02d-%02d, the string) joined with
+// '\t', rendered from the group's first record (its need cells, gather_kernel).
+// Range partials carry this text instead of the 128-bit part digest, so the merges
+// across ranks group composite keys byte for byte, as the reference does.
+// lens[i] = ~0: longer than cap or a DOUBLE part of 2^43 or more (not rendered here).
+__global__ void comp_text_kernel(const Cell* __restrict__ cells, uint32_t n, uint32_t cap, uint8_t* __restrict__ out,
+                                 uint32_t* __restrict__ lens) {
+    const ScanPlan& P = c_plan;
+    const uint32_t i = blockIdx.x * blockDim.x + threadIdx.x;
+    if (i >= n) return;
+    const RowView v{cells + (uint64_t)i * P.nneed};
+    TextSink sk{out + (size_t)i * cap, cap, 0};
+    bool ok = true;
+    for (int k = 0; k < MAX_GPART; k++) {
+        if (k >= P.ngpart) break;
+        ok = joined_text_add(sk, plan_group_part(P, P.consts, v, P.nneed, k), k == 0) && ok;
+    }
+    lens[i] = ok && sk.n <= cap ? sk.n : 0xFFFFFFFFu;
 }
 
 // ------------------------------------------------------------------ projection
@@ -1866,6 +1911,13 @@ __global__ void join_fill_kernel(const unsigned int* __restrict__ flags, const u
     if (flags && !flags[i]) return;                           // matched: not appended
     const unsigned long long at = base + (pos ? pos[i] : i);
     pairs[at] = right_side ? make_uint2(JOIN_NONE, i) : make_uint2(i, JOIN_NONE);
+}
+
+// JOIN without ON: every (l, r) pair, l-major (the nested loops' order)
+__global__ void join_cross_kernel(uint32_t na, uint32_t nb, unsigned long long np, uint2* __restrict__ pairs) {
+    for (unsigned long long i = (unsigned long long)blockIdx.x * blockDim.x + threadIdx.x; i < np;
+         i += (unsigned long long)gridDim.x * blockDim.x)
+        pairs[i] = make_uint2((uint32_t)(i / nb), (uint32_t)(i % nb));
 }
 
 // the plan's need slots of one joined row: in registers (plans over <= MAX_NEED
@@ -2669,6 +2721,14 @@ hipError_t cq_launch_gather(const uint8_t* g, const cq::ScanPlan* P, const unsig
     return hipGetLastError();
 }
 
+// (c_plan: the plan cq_launch_gather uploaded for the same cells)
+hipError_t cq_launch_comp_text(const cq::Cell* cells, uint32_t n, uint32_t cap, uint8_t* out, uint32_t* lens,
+                               hipStream_t s) {
+    if (!n) return hipSuccess;
+    hipLaunchKernelGGL(cq::comp_text_kernel, dim3((n + 127) / 128), dim3(128), 0, s, cells, n, cap, out, lens);
+    return hipGetLastError();
+}
+
 hipError_t cq_launch_project(const uint8_t* g, const unsigned long long* recs, uint32_t nrec,
                              const cq::ProjDesc* D, cq::Cell* scratch, cq::Cell* out, hipStream_t s) {
     if (!nrec) return hipSuccess;
@@ -3100,6 +3160,13 @@ hipError_t cq_launch_join_fill(const unsigned int* flags, const unsigned int* po
     if (!n) return hipSuccess;
     hipLaunchKernelGGL(cq::join_fill_kernel, dim3(grid_of(n, 256)), dim3(256), 0, s, flags, pos, n, base, right_side,
                        pairs);
+    return hipGetLastError();
+}
+hipError_t cq_launch_join_cross(uint32_t na, uint32_t nb, uint2* pairs, hipStream_t s) {
+    const unsigned long long np = (unsigned long long)na * nb;
+    if (!np) return hipSuccess;
+    const unsigned grid = (unsigned)std::min<unsigned long long>((np + 255) / 256, 8192);
+    hipLaunchKernelGGL(cq::join_cross_kernel, dim3(grid), dim3(256), 0, s, na, nb, np, pairs);
     return hipGetLastError();
 }
 hipError_t cq_launch_join_agg(const uint2* pairs, unsigned long long np, const cq::JoinMap* M, const cq::Cell* L,

@@ -239,6 +239,14 @@ QUERIES = [
     f"SELECT COUNT(*) FROM {SU} AS u JOIN {SO} AS o ON u.id = o.customer_id",
     f"SELECT u.role, COUNT(*), SUM(o.price) FROM {SU} AS u JOIN {SO} AS o ON u.id = o.customer_id GROUP BY u.role",
     f"SELECT COUNT(*), SUM(o.price), AVG(o.quantity) FROM {SU} AS u JOIN {SO} AS o ON u.id = o.customer_id WHERE u.age > 40",
+    # JOIN without ON (parser_clauses.c:315-318 makes ON optional; evaluate_join_condition
+    # is true for a NULL condition, evaluator_joins.c:42): the cross product
+    f"SELECT COUNT(*) FROM {U} AS u JOIN {O} AS o",
+    f"SELECT u.name, o.price FROM {U} AS u JOIN {O} AS o WHERE o.price > 100",
+    f"SELECT u.role, COUNT(*), SUM(o.price) FROM {U} AS u JOIN {O} AS o GROUP BY u.role",
+    f"SELECT COUNT(*), SUM(o.quantity) FROM {U} AS u LEFT JOIN {O} AS o WHERE u.age > 30",
+    f"SELECT COUNT(*) FROM {U} AS u JOIN {O} AS o ON u.id = o.customer_id JOIN {P} AS p",
+    f"SELECT p.category, COUNT(*) FROM {U} AS u JOIN {O} AS o ON u.id = o.customer_id JOIN {P} AS p GROUP BY p.category",
     # join chains (process_joins, evaluator_joins.c:237-274: level 2 joins "joined")
     f"SELECT COUNT(*) FROM {U} AS u JOIN {O} AS o ON u.id = o.customer_id JOIN {P} AS p ON o.id = p.id",
     f"SELECT p.name, p.category, o.price FROM {U} AS u JOIN {O} AS o ON u.id = o.customer_id JOIN {P} AS p ON o.id = p.id",

