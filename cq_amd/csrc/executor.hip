@@ -26,6 +26,7 @@
 #include <vector>
 
 #include <fcntl.h>
+#include <link.h>
 #include <malloc.h>
 #include <strings.h>
 #include <sys/mman.h>
@@ -327,11 +328,35 @@ struct DevCtx {
 };
 DevCtx g_ctx[64];
 
+// Two HIP runtimes in one process (e.g. /opt/rocm's, pulled in by this library, and
+// the copy a torch wheel ships, loaded afterwards) each own a device state and free
+// the shared one twice at exit: refused at the first device use, with the fix named
+int count_hip_runtime(struct dl_phdr_info* info, size_t, void* data) {
+    const char* n = info->dlpi_name;
+    if (n && strstr(n, "libamdhip64.so")) {
+        char buf[4096];
+        const char* r = realpath(n, buf);
+        ((std::set<std::string>*)data)->insert(r ? r : n);
+    }
+    return 0;
+}
+void check_one_hip_runtime() {
+    std::set<std::string> seen;
+    dl_iterate_phdr(count_hip_runtime, &seen);
+    if (seen.size() > 1) {
+        std::string all;
+        for (auto& s : seen) all += " " + s;
+        throw HipError{"two HIP runtimes are loaded in this process (" + all.substr(1) +
+                       "): load the host framework's HIP (e.g. import torch) before libcqgpu.so"};
+    }
+}
+
 DevCtx& ctx() {
     int dev = 0;
     HIPCHECK(hipGetDevice(&dev));
     DevCtx& c = g_ctx[dev & 63];
     if (c.device != dev) {
+        check_one_hip_runtime();
         c.device = dev;
         HIPCHECK(hipStreamCreateWithFlags(&c.stream, hipStreamNonBlocking));
         HIPCHECK(hipEventCreate(&c.ev0));

@@ -2263,8 +2263,8 @@ bool fast_shape(const ScanPlan* P, int grouped, FastPlan* fp, int* ns, bool* whe
             if (roles[k] != 3) wn = wn || ((P->fast_wide_cols >> (cols[k] < 63 ? cols[k] : 63)) & 1);
         wn = wn || getenv("CQGPU_FAST_WN") != nullptr;
         if (wide_num) *wide_num = wn;
-        // MIN / MAX: the narrow-numeral ',' / '"' canonical build only (fixed point, no doubles)
-        if (ext && (wn || !canon || d != ',' || P->quote != '"')) return false;
+        // MIN / MAX: the narrow-numeral ',' / '"' builds only (fixed point, no doubles)
+        if (ext && (wn || d != ',' || P->quote != '"')) return false;
     }
     return true;
 }
@@ -2300,11 +2300,17 @@ fast_fn_t pick_wc(bool where, int ns, bool comma, bool rp3, bool wn) {
 }
 template <bool G>
 fast_fn_t pick_fast(bool where, int ns, bool comma, bool canon, bool rp3, bool wn, int ext = 0) {
-    if (ext) {     // (fast_shape: one argument, ',' / '"', canonical roles, narrow numerals)
-        if (where) return ext == 1 ? fast::fast_kernel<G, true, 1, true, true, 2, false, 1>
-                                   : fast::fast_kernel<G, true, 1, true, true, 2, false, 2>;
-        return ext == 1 ? fast::fast_kernel<G, false, 1, true, true, 2, false, 1>
-                        : fast::fast_kernel<G, false, 1, true, true, 2, false, 2>;
+    if (ext) {     // (fast_shape: one argument, ',' / '"', narrow numerals)
+        if (canon) {
+            if (where) return ext == 1 ? fast::fast_kernel<G, true, 1, true, true, 2, false, 1>
+                                       : fast::fast_kernel<G, true, 1, true, true, 2, false, 2>;
+            return ext == 1 ? fast::fast_kernel<G, false, 1, true, true, 2, false, 1>
+                            : fast::fast_kernel<G, false, 1, true, true, 2, false, 2>;
+        }
+        if (where) return ext == 1 ? fast::fast_kernel<G, true, 1, true, false, 2, false, 1>
+                                   : fast::fast_kernel<G, true, 1, true, false, 2, false, 2>;
+        return ext == 1 ? fast::fast_kernel<G, false, 1, true, false, 2, false, 1>
+                        : fast::fast_kernel<G, false, 1, true, false, 2, false, 2>;
     }
     return canon ? pick_wc<G, true>(where, ns, comma, rp3, wn) : pick_wc<G, false>(where, ns, comma, rp3, wn);
 }

@@ -2975,7 +2975,10 @@ __global__ void mail_copy_kernel(const uint4* __restrict__ src, const unsigned i
                                  unsigned int cap_out, int nacc, uint32_t ncell, uint32_t sb, uint4* __restrict__ dst) {
     const uint32_t ng = min(*count, cap_out);
     const size_t head = (size_t)ng * (40u + 40u * (uint32_t)nacc + ncell * (uint32_t)sizeof(Cell));
-    const size_t n16 = head / 16;
+    // rounded up: with an odd group count and an even accumulator count the head ends
+    // 8 bytes into a 16-byte unit (the last cell's address word); the extra bytes are
+    // the source's own string section, which the sparse copy below writes identically
+    const size_t n16 = (head + 15) / 16;
     for (size_t i = (size_t)blockIdx.x * blockDim.x + threadIdx.x; i < n16; i += (size_t)gridDim.x * blockDim.x)
         dst[i] = src[i];
     const Cell* cells = (const Cell*)((const uint8_t*)src + (size_t)ng * (40u + 40u * (uint32_t)nacc));
