@@ -165,7 +165,8 @@ hipError_t cq_launch_gm_merge(const uint8_t* buf, uint64_t B, uint32_t N, uint32
                               uint8_t* mail, hipStream_t s);
 int cq_fast_ext_plan(const cq::ScanPlan* P, int grouped);
 hipError_t cq_launch_raw_merge(const cq::GroupTable* gt, const cq::GroupTable* rt, int nacc, cq::ScanStats* stats,
-                               hipStream_t s, uint32_t max_mask = 0);
+                               hipStream_t s, uint32_t max_mask = 0, const uint8_t* g = nullptr,
+                               int pk_acc = -1, uint32_t pk_col = 0, uint32_t delim = ',');
 hipError_t cq_launch_join_cross(uint32_t na, uint32_t nb, uint2* pairs, hipStream_t s);
 uint64_t cq_jx_windows(uint64_t lo, uint64_t hi, uint32_t ws);
 hipError_t cq_jx_extract(const uint8_t* g, uint64_t lo, uint64_t hi, uint32_t ws, uint32_t delim, uint32_t quote,
@@ -1559,7 +1560,7 @@ TableArena make_arena(DevCtx& c, const ScanPlan& P, uint32_t cap, size_t out_cap
     for (int a = 0; a < P.nacc; a++) sums_only = sums_only && P.acc[a].kind == ACC_SUM;
     // lean_kernel / fast_kernel plans: the raw-key table (with extreme cells for a
     // fast_kernel MIN / MAX build, cq_fast_ext_plan)
-    if (sums_only || cq_fast_ext_plan(&P, 1)) {
+    if (sums_only || cq_fast_ext_plan(&P, 1) || cq_fast_ext_plan(&P, 0)) {
         parts.push_back({(void**)&A.rt.tag, cap * 4ull, 0});
         parts.push_back({(void**)&A.rt.clslen, cap * 4ull, 0});
         parts.push_back({(void**)&A.rt.w0, cap * 8ull, 0});

@@ -448,18 +448,16 @@ __device__ __forceinline__ unsigned long long ext_key(uint64_t fix, uint32_t cod
 }
 template <int EXT>
 __device__ __forceinline__ unsigned long long ext_none() { return EXT == 1 ? ~0ull : 0ull; }
-// the record's field `col` from global memory (the record passed the fast path: no
-// quote before it, the field exists), typed by the general parser
-__device__ __noinline__ Cell field_cell(const uint8_t* __restrict__ g, uint64_t rec, uint32_t col, uint32_t delim) {
-    const uint8_t* p = g + rec;
-    for (uint32_t c = 0; c < col; p++) {
-        const uint32_t ch = *p;
-        if (ch == delim) c++;
-        else if (ch == '\n' || ch == '\r') return cell_null();
-    }
-    uint32_t len = 0;
-    while (len < 64 && p[len] != delim && p[len] != '\n' && p[len] != '\r') len++;
-    return parse_cell(p, len);
+// The block flushes carry each extreme as one 64-bit key, merged by a global
+// atomicMin (no lock): the fixed-point value (< 2^24: <= 4-byte numerals, scale 10^3;
+// MAX as 2^24 - 1 - value) above the record's byte offset (< 2^40), so the smallest
+// key is the extreme and, among equal values, its first record.  raw_merge_kernel
+// (grouped) / fast_ext_final_kernel (one group) types the winning field once.
+constexpr uint32_t EXT_POS_BITS = 40;
+constexpr uint64_t EXT_FIX_MAX = (1ull << 24) - 1;
+template <int EXT>
+__device__ __forceinline__ unsigned long long ext_packed(uint64_t fix, uint64_t pos) {
+    return ((EXT == 1 ? fix : EXT_FIX_MAX - fix) << EXT_POS_BITS) | pos;
 }
 template <int NS>
 constexpr uint32_t table_bytes(bool grouped) {
@@ -1126,25 +1124,18 @@ __global__ __launch_bounds__(LT) void fast_kernel(const uint8_t* __restrict__ g,
             }
         }
         if constexpr (EXT != 0) {
-            // the wave's extreme (one key order for MIN and MAX), its cell re-typed from
-            // the record, merged under the group's seqlock (wave-uniform call)
+            // the wave's extreme (one key order for MIN and MAX) as a packed key into the
+            // raw table's word 0 (fast_ext_final_kernel merges it into the group)
             unsigned long long x = my_ext;
             for (int o = 32; o > 0; o >>= 1) {
                 const unsigned long long y = __shfl_down(x, o, 64);
                 x = EXT == 1 ? (y < x ? y : x) : (y > x ? y : x);
             }
-            const int gi = __shfl(gi0, 0, 64);
-            const bool have = lane == 0 && gi >= 0 && x != ext_none<EXT>();
-            Cell cc = cell_null();
-            uint64_t pos = 0;
-            if (have) {
+            if (lane == 0 && x != ext_none<EXT>()) {
                 const uint32_t code = EXT == 1 ? (uint32_t)x : ~(uint32_t)x;
                 const uint64_t fw = first_win + ((uint64_t)(code >> 16) * gridDim.x + blockIdx.x) * NWV + ((code >> 12) & 15);
-                pos = fw * wsb + (code & 4095);
-                cc = field_cell(g, pos, fp.ext_col, fp.delim);
+                atomicMin(&tabs[TAB_RT].extpos[fp.ext_acc][0], ext_packed<EXT>(x >> 32, fw * wsb + (code & 4095)));
             }
-            g_ext_update(have && cc.kind != K_NULL, gt, fp.ext_acc, EXT == 1 ? ACC_MIN : ACC_MAX,
-                         gi >= 0 ? (uint32_t)gi : 0u, cc, pos, stats);
         }
         return;
     }
@@ -1166,19 +1157,13 @@ __global__ __launch_bounds__(LT) void fast_kernel(const uint8_t* __restrict__ g,
             const GKey k = raw_key(kl, kl ? w0 : 0ull);
             gi = g_insert(rt, k, gk_hash(k), stats);
         }
-        if constexpr (EXT != 0) {
+        if constexpr (EXT != 0) {      // the slot's extreme as a packed key (raw_merge_kernel types it)
             const unsigned long long x = *(const unsigned long long*)(r + SO_EXT);
-            const bool have = gi >= 0 && x != ext_none<EXT>();
-            Cell cc = cell_null();
-            uint64_t pos = 0;
-            if (have) {
+            if (gi >= 0 && x != ext_none<EXT>()) {
                 const uint32_t code = EXT == 1 ? (uint32_t)x : ~(uint32_t)x;
                 const uint64_t fw = first_win + ((uint64_t)(code >> 16) * gridDim.x + blockIdx.x) * NWV + ((code >> 12) & 15);
-                pos = fw * wsb + (code & 4095);
-                cc = field_cell(g, pos, fp.ext_col, fp.delim);
+                atomicMin(&rt.extpos[fp.ext_acc][gi], ext_packed<EXT>(x >> 32, fw * wsb + (code & 4095)));
             }
-            g_ext_update(have && cc.kind != K_NULL, rt, fp.ext_acc, EXT == 1 ? ACC_MIN : ACC_MAX,
-                         gi >= 0 ? (uint32_t)gi : 0u, cc, pos, stats);
         }
         if (gi < 0) continue;
         atomicAdd(&rt.cnt[gi], (unsigned long long)n);
@@ -1808,35 +1793,72 @@ __global__ __launch_bounds__(1024) void jx_part_probe_kernel(const unsigned long
                                                              unsigned long long* __restrict__ gsum,
                                                              uint32_t* __restrict__ gminix,
                                                              unsigned long long* __restrict__ npairs) {
+    // per group: fixed-point sum, count, NULL-payload count (the SUM count is count -
+    // NULLs: one LDS atomic fewer per match), smallest matched key index
     __shared__ unsigned long long sfix[JX_G];
-    __shared__ uint32_t scnt[JX_G], snum[JX_G], smix[JX_G];
-    for (uint32_t k = threadIdx.x; k < JX_G; k += blockDim.x) { sfix[k] = 0; scnt[k] = 0; snum[k] = 0; smix[k] = ~0u; }
+    __shared__ uint32_t scnt[JX_G], snul[JX_G], smix[JX_G];
+    for (uint32_t k = threadIdx.x; k < JX_G; k += blockDim.x) { sfix[k] = 0; scnt[k] = 0; snul[k] = 0; smix[k] = ~0u; }
     const bool mono = __builtin_amdgcn_readfirstlane(*notmono) == 0u;
     __syncthreads();
     const uint32_t x = blockIdx.x & 7u, sub = blockIdx.x >> 3, nsub = gridDim.x >> 3;
     unsigned long long pairs = 0;
+    // The block's segments of partition p (sources sub, sub + nsub, ...), up to SEG at a
+    // time, as one flat index space: their counts' prefix in LDS (then uniform
+    // registers), entry j in segment s = #(prefix[k] <= j).  Every lane has U entries
+    // in flight -- their loads, then their d16 lookups, then the LDS updates -- so
+    // neither a segment boundary nor the two dependent loads of an entry idle lanes.
+    constexpr uint32_t U = 8, SEG = 16;
+    __shared__ uint32_t soff[SEG + 1];
     for (uint32_t p = x; p < np; p += 8) {
-        for (uint32_t sb = sub; sb < nsrc; sb += nsub) {
-            const uint32_t n = pcnt[(size_t)sb * np + p];
-            const unsigned long long* e = pent + ((size_t)sb * np + p) * pcap;
-            for (uint32_t i = threadIdx.x; i < n; i += blockDim.x) {
-                const unsigned long long v = e[i];
-                const uint32_t ix = (uint32_t)v, p32 = (uint32_t)(v >> 32);
-                if (ix >= range) continue;                       // (a skipped entry: ~0)
-                const uint32_t gv = d16[ix];
-                if (!gv) continue;
-                const uint32_t gi = (gv & 0x7FFFu) - 1u;
-                if (mono) {
-                    if (ix < smix[gi]) atomicMin(&smix[gi], ix);
-                } else if (!(gv & 0x8000u)) {
-                    d16[ix] = (uint16_t)(gv | 0x8000u);          // (every writer: the same value)
+        for (uint32_t sb0 = sub; sb0 < nsrc; sb0 += SEG * nsub) {
+            __syncthreads();                                   // (the last group's soff reads)
+            if (threadIdx.x < 64) {
+                const uint32_t sb = sb0 + threadIdx.x * nsub;
+                uint32_t c = threadIdx.x < SEG && sb < nsrc ? pcnt[(size_t)sb * np + p] : 0u;
+                for (int o = 1; o < (int)SEG; o <<= 1) {
+                    const uint32_t t = (uint32_t)__shfl_up((int)c, o, 64);
+                    c += threadIdx.x >= (uint32_t)o ? t : 0u;
                 }
-                atomicAdd(&scnt[gi], 1u);
-                if (p32 != JX_PNULL) {
-                    atomicAdd(&sfix[gi], (unsigned long long)p32);
-                    atomicAdd(&snum[gi], 1u);
+                if (threadIdx.x < SEG) soff[threadIdx.x + 1] = c;
+                if (threadIdx.x == 0) soff[0] = 0;
+            }
+            __syncthreads();
+            uint32_t o[SEG + 1];
+#pragma unroll
+            for (uint32_t k = 0; k <= SEG; k++) o[k] = __builtin_amdgcn_readfirstlane(soff[k]);
+            const uint32_t total = o[SEG];
+            for (uint32_t j0 = 0; j0 < total; j0 += U * blockDim.x) {
+                unsigned long long v[U];
+#pragma unroll
+                for (uint32_t u = 0; u < U; u++) {
+                    const uint32_t j = j0 + u * blockDim.x + threadIdx.x;
+                    uint32_t sg = 0;
+#pragma unroll
+                    for (uint32_t k = 1; k < SEG; k++) sg += j >= o[k] ? 1u : 0u;
+                    const size_t at = ((size_t)(sb0 + sg * nsub) * np + p) * pcap + (j - o[sg]);
+                    v[u] = j < total ? __builtin_nontemporal_load(pent + at) : ~0ull;
                 }
-                pairs++;
+                uint32_t gv[U];
+#pragma unroll
+                for (uint32_t u = 0; u < U; u++) {
+                    const uint32_t ix = (uint32_t)v[u];
+                    gv[u] = ix < range ? (uint32_t)d16[ix] : 0u;   // (a skipped entry: ~0)
+                }
+#pragma unroll
+                for (uint32_t u = 0; u < U; u++) {
+                    if (!gv[u]) continue;
+                    const uint32_t ix = (uint32_t)v[u], p32 = (uint32_t)(v[u] >> 32);
+                    const uint32_t gi = (gv[u] & 0x7FFFu) - 1u;
+                    if (mono) {
+                        if (ix < smix[gi]) atomicMin(&smix[gi], ix);
+                    } else if (!(gv[u] & 0x8000u)) {
+                        d16[ix] = (uint16_t)(gv[u] | 0x8000u);     // (every writer: the same value)
+                    }
+                    atomicAdd(&scnt[gi], 1u);
+                    if (p32 != JX_PNULL) atomicAdd(&sfix[gi], (unsigned long long)p32);
+                    else atomicAdd(&snul[gi], 1u);
+                    pairs++;
+                }
             }
         }
     }
@@ -1847,9 +1869,10 @@ __global__ __launch_bounds__(1024) void jx_part_probe_kernel(const unsigned long
         if (!scnt[k]) continue;
         if (mono) atomicMin(&gminix[k], smix[k]);
         atomicAdd(&gsum[3 * k], (unsigned long long)scnt[k]);
-        if (snum[k]) {
+        const uint32_t num = scnt[k] - snul[k];
+        if (num) {
             atomicAdd(&gsum[3 * k + 1], sfix[k]);
-            atomicAdd(&gsum[3 * k + 2], (unsigned long long)snum[k]);
+            atomicAdd(&gsum[3 * k + 2], (unsigned long long)num);
         }
     }
 }
@@ -2264,7 +2287,7 @@ bool fast_shape(const ScanPlan* P, int grouped, FastPlan* fp, int* ns, bool* whe
         wn = wn || getenv("CQGPU_FAST_WN") != nullptr;
         if (wide_num) *wide_num = wn;
         // MIN / MAX: the narrow-numeral ',' / '"' builds only (fixed point, no doubles)
-        if (ext && (wn || d != ',' || P->quote != '"')) return false;
+        if (ext && (wn || d != ',' || P->quote != '"' || P->n >= (1ull << fast::EXT_POS_BITS))) return false;
     }
     return true;
 }
@@ -2417,7 +2440,8 @@ hipError_t cq_launch_fast(const uint8_t* g, const cq::ScanPlan* P, const cq::Gro
     hipError_t e = cq::upload_buffer(tabs_dev[dev & 63], tabs, sizeof tabs, s);
     if (e != hipSuccess) return e;
     const bool comma = P->delim == ',' && P->quote == '"';
-    if (ext && grouped && (!rt || !rt->ext[fp.ext_acc] || !rt->lock[fp.ext_acc])) return hipErrorInvalidValue;
+    // (EXT builds: the packed extreme keys go to the raw table's extpos words)
+    if (ext && (!rt || !rt->extpos[fp.ext_acc] || rt->cap < 1)) return hipErrorInvalidValue;
     const fast_fn_t fn = grouped ? pick_fast<true>(where, ns, comma, canon, false, wn, ext)
                                  : pick_fast<false>(where, ns, comma, canon, rp3, wn, ext);
     const size_t lds = fast_lds(grouped, ns);
@@ -2428,6 +2452,43 @@ hipError_t cq_launch_fast(const uint8_t* g, const cq::ScanPlan* P, const cq::Gro
 }
 
 int cq_fast_waves_per_block() { return fast::NWV; }
+
+// one-group MIN / MAX build: the packed key the waves left in the raw table's word 0,
+// typed from its record and merged into the group (the canonical table's GK_ALL key)
+__global__ void fast_ext_final_kernel(const uint8_t* __restrict__ g, const GroupTable gt, const GroupTable rt, int a,
+                                      uint32_t col, uint32_t delim, uint8_t kind, ScanStats* __restrict__ stats) {
+    const unsigned long long x = rt.extpos[a][0];
+    int gi = -1;
+    Cell cc = cell_null();
+    uint64_t pos = NOPOS;
+    if (threadIdx.x == 0 && x != ~0ull) {
+        GKey k;
+        k.cls = GK_ALL; k.len = 0; k.w0 = 0; k.w1 = 0;
+        gi = g_insert(gt, k, 0x12345678ULL, stats);       // (fast_kernel's one-group key and hash)
+        pos = x & ((1ull << fast::EXT_POS_BITS) - 1);
+        cc = field_cell(g, pos, col, delim);
+    }
+    g_ext_update(gi >= 0 && cc.kind != K_NULL, gt, a, kind, gi >= 0 ? (uint32_t)gi : 0u, cc, pos, stats);
+    if (threadIdx.x == 0) rt.extpos[a][0] = ~0ull;     // consumed (a chunked rescan adds its own)
+}
+// the MIN / MAX accumulator and its column of a fast_kernel EXT build (-1: none)
+int cq_fast_ext_info(const cq::ScanPlan* P, int grouped, uint32_t* col) {
+    FastPlan fp;
+    int ns = 0, ext = 0;
+    bool where = false, canon = false;
+    if (!fast_shape(P, grouped, &fp, &ns, &where, &canon, nullptr, &ext) || !ext) return -1;
+    *col = fp.ext_col;
+    return fp.ext_acc;
+}
+hipError_t cq_fast_ext_final(const uint8_t* g, const cq::ScanPlan* P, const cq::GroupTable* gt, const cq::GroupTable* rt,
+                             cq::ScanStats* stats, hipStream_t s) {
+    uint32_t col = 0;
+    const int a = cq_fast_ext_info(P, 0, &col);
+    if (a < 0 || !rt || !rt->extpos[a]) return hipErrorInvalidValue;
+    hipLaunchKernelGGL(fast_ext_final_kernel, dim3(1), dim3(64), 0, s, g, *gt, *rt, a, col, (uint32_t)P->delim,
+                       (uint8_t)P->acc[a].kind, stats);
+    return hipGetLastError();
+}
 
 // ---- fused aggregate join (executor.hip run_fast_join)
 // windows of the table's bytes [lo, hi) at stride ws

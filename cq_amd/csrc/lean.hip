@@ -1305,8 +1305,13 @@ __global__ __launch_bounds__(LT) void lean_kernel(const uint8_t* __restrict__ g,
 // A raw key's MIN / MAX cell (fast_kernel's EXT builds) merges like every other
 // extreme: the wave-uniform seqlock update (scanlib.h g_ext_update), so the thread
 // loop has no early exit.  max_mask bit a: accumulator a is a MAX.
+// pk_acc >= 0: that accumulator's rt.extpos words hold fast_kernel's packed extreme
+// keys (fast.hip ext_packed: value bits above a 40-bit record offset), typed here from
+// the record's field pk_col -- once per raw key instead of once per block
 __global__ __launch_bounds__(256) void raw_merge_kernel(ScanStats* __restrict__ stats, const GroupTable gt,
-                                                        const GroupTable rt, int nacc, uint32_t max_mask) {
+                                                        const GroupTable rt, int nacc, uint32_t max_mask,
+                                                        const uint8_t* __restrict__ g, int pk_acc, uint32_t pk_col,
+                                                        uint32_t delim) {
     __shared__ __align__(16) uint8_t buf[256 * 32];
     const uint32_t i = blockIdx.x * 256 + threadIdx.x;
     const bool live = i < rt.cap && rt.tag[i] >= 2;
@@ -1332,9 +1337,17 @@ __global__ __launch_bounds__(256) void raw_merge_kernel(ScanStats* __restrict__ 
     }
     for (int a = 0; a < nacc; a++) {
         if (!rt.ext[a] || !gt.ext[a]) continue;       // (uniform)
-        const unsigned long long pos = gi >= 0 ? rt.extpos[a][i] : NOPOS;
-        const bool need = gi >= 0 && pos != NOPOS;
-        const Cell c = need ? rt.ext[a][i] : cell_null();
+        const unsigned long long w = gi >= 0 ? rt.extpos[a][i] : NOPOS;
+        bool need = gi >= 0 && w != NOPOS;
+        unsigned long long pos = w;
+        Cell c = cell_null();
+        if (a == pk_acc) {
+            pos = need ? (w & ((1ull << 40) - 1)) : NOPOS;
+            if (need) c = field_cell(g, pos, pk_col, delim);
+            need = need && c.kind != K_NULL;
+        } else if (need) {
+            c = rt.ext[a][i];
+        }
         g_ext_update(need, gt, a, ((max_mask >> a) & 1) ? ACC_MAX : ACC_MIN, gi >= 0 ? (uint32_t)gi : 0u, c, pos,
                      stats);
         if (need) rt.extpos[a][i] = NOPOS;
@@ -1612,9 +1625,11 @@ hipError_t cq_launch_lean(const uint8_t* g, const cq::ScanPlan* P, const cq::Gro
 
 // raw-key table -> canonical table (after cq_launch_lean of a grouped plan)
 hipError_t cq_launch_raw_merge(const cq::GroupTable* gt, const cq::GroupTable* rt, int nacc, cq::ScanStats* stats,
-                               hipStream_t s, uint32_t max_mask) {
+                               hipStream_t s, uint32_t max_mask, const uint8_t* g, int pk_acc, uint32_t pk_col,
+                               uint32_t delim) {
+    if (pk_acc >= 0 && !g) return hipErrorInvalidValue;
     hipLaunchKernelGGL(lean::raw_merge_kernel, dim3((rt->cap + 255) / 256), dim3(256), 0, s, stats, *gt, *rt, nacc,
-                       max_mask);
+                       max_mask, g, pk_acc, pk_col, delim);
     return hipGetLastError();
 }
 

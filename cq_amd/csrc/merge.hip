@@ -433,7 +433,7 @@ hipError_t cq_excl_sum_u32(void* temp, size_t* temp_bytes, const unsigned int* i
 // on entry (cq_gm_merge_scratch sizes them); err zero
 size_t cq_gm_scan_bytes(uint32_t T) {
     size_t tb = 0;
-    cq_excl_sum_u32(nullptr, &tb, nullptr, nullptr, T, nullptr);
+    (void)cq_excl_sum_u32(nullptr, &tb, nullptr, nullptr, T, nullptr);   // (a size query)
     return tb;
 }
 hipError_t cq_launch_gm_merge(const uint8_t* buf, uint64_t B, uint32_t N, uint32_t maxg, int nacc, uint32_t R,

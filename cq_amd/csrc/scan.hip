@@ -2566,8 +2566,12 @@ hipError_t cq_launch_lean(const uint8_t* g, const cq::ScanPlan* P, const cq::Gro
                           unsigned long long row_cap, int grouped, int grid, hipStream_t s,
                           unsigned long long* slow_list, unsigned long long slow_cap);
 int cq_fast_ext_plan(const cq::ScanPlan* P, int grouped);
+int cq_fast_ext_info(const cq::ScanPlan* P, int grouped, uint32_t* col);
+hipError_t cq_fast_ext_final(const uint8_t* g, const cq::ScanPlan* P, const cq::GroupTable* gt, const cq::GroupTable* rt,
+                             cq::ScanStats* stats, hipStream_t s);
 hipError_t cq_launch_raw_merge(const cq::GroupTable* gt, const cq::GroupTable* rt, int nacc, cq::ScanStats* stats,
-                               hipStream_t s, uint32_t max_mask = 0);
+                               hipStream_t s, uint32_t max_mask = 0, const uint8_t* g = nullptr,
+                               int pk_acc = -1, uint32_t pk_col = 0, uint32_t delim = ',');
 int cq_fast_eligible(const cq::ScanPlan* P, int grouped, int want_rows);
 int cq_fast_waves_per_block();
 hipError_t cq_launch_fast(const uint8_t* g, const cq::ScanPlan* P, const cq::GroupTable* gt,
@@ -2655,7 +2659,11 @@ hipError_t cq_launch_scan(const uint8_t* g, const cq::ScanPlan* P, const cq::Gro
                 hipLaunchKernelGGL(cq::slow_kernel<false>, dim3(SLOW_GRID), dim3(256), 0, s, g, stats, row_out, row_cap,
                                    cells_out, slow_list, slow_cap);
             e = hipGetLastError();
-            if (e == hipSuccess && grouped) e = cq_launch_raw_merge(gt, rt, P->nacc, stats, s, max_mask(P));
+            uint32_t pk_col = 0;
+            const int pk_acc = fext ? cq_fast_ext_info(P, grouped, &pk_col) : -1;
+            if (e == hipSuccess && grouped)
+                e = cq_launch_raw_merge(gt, rt, P->nacc, stats, s, max_mask(P), g, pk_acc, pk_col, P->delim);
+            if (e == hipSuccess && !grouped && pk_acc >= 0) e = cq_fast_ext_final(g, P, gt, rt, stats, s);
             return e;
         }
     }

@@ -374,6 +374,21 @@ __device__ __forceinline__ uint32_t class_bit(const Cell& c) {
 }
 
 
+// the record's field `col` from global memory (the record passed a fast path: no
+// quote before it, the field exists), typed by the general parser
+static __device__ __noinline__ Cell field_cell(const uint8_t* __restrict__ g, uint64_t rec, uint32_t col,
+                                               uint32_t delim) {
+    const uint8_t* p = g + rec;
+    for (uint32_t c = 0; c < col; p++) {
+        const uint32_t ch = *p;
+        if (ch == delim) c++;
+        else if (ch == '\n' || ch == '\r') return cell_null();
+    }
+    uint32_t len = 0;
+    while (len < 64 && p[len] != delim && p[len] != '\n' && p[len] != '\r') len++;
+    return parse_cell(p, len);
+}
+
 // MIN/MAX merges take a per-slot lock.  A lock loop written per lane deadlocks
 // on SIMT hardware (the compiler may park the lane that won the lock until every
 // lane of the wave has won it), so every lock loop here is wave-uniform: the loop

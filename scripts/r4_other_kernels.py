@@ -20,6 +20,7 @@ import cqtest  # noqa: E402
 ap = argparse.ArgumentParser()
 ap.add_argument("--rows", type=int, default=100_000_000)
 ap.add_argument("--steps", type=int, default=10)
+ap.add_argument("--only", default="", help="run the plans whose name holds this text")
 args = ap.parse_args()
 data = datagen.header_of(True) + bench.gen_rows(42, 0, args.rows, True, 8)
 nb = len(data)
@@ -39,6 +40,8 @@ FORCE = {"scan_kernel (config 3 forced)": 1}
 KIND = {0: "scan_kernel", 1: "lean_kernel", 2: "fast_kernel"}
 out = {}
 for name, sql in Q.items():
+    if args.only not in name:
+        continue
     q = sql.format(p=path)
     ms = []
     old = cq_amd.set_scan_kernel(FORCE.get(name, 0))

@@ -284,8 +284,9 @@ def test_fast_narrow_numerals_late_wide(d, monkeypatch, wn):
 
 def test_fast_min_max(d):
     """MIN / MAX of narrow numerals in fast_kernel (EXT builds): (10^-3 fixed-point
-    value, first-row code) in one 64-bit LDS atomic, the extreme's cell re-typed from
-    its record at the flush (evaluate_aggregate keeps the first cell that compares
+    value, first-row code) in one 64-bit LDS atomic; the blocks' extremes merged as
+    (value, record offset) keys by one global atomicMin and the winner's cell typed
+    once from its record by raw_merge_kernel (evaluate_aggregate keeps the first cell that compares
     strictly better, evaluator_aggregates.c:311-326): ties between spellings of one
     value ("1.5" / "1.50" / INTEGER vs DOUBLE) keep the first record's cell; NULLs
     skipped; groups whose every value is NULL keep NULL"""
