@@ -87,6 +87,10 @@ struct FastPlan {
     int32_t ext_acc;
     uint32_t ext_col;           // the argument's column (the flushes re-type the extreme's field)
     uint32_t sum_mask;
+    // WSTR builds: WHERE `column op 'literal'` with a 1-8 byte STRING literal: its bytes
+    // as a big-endian word, zero padded (strcmp order of zero-padded words), cut at a NUL
+    uint32_t wstr_lit;          // 1: the WHERE literal is such a STRING
+    uint64_t wstr;
 };
 
 // HBM tables: canonical keys (TAB_GT), raw keys (TAB_RT)
@@ -473,12 +477,13 @@ constexpr uint32_t fixed_bytes() { return (uint32_t)(sizeof(WaveLds) * NWV); }
 // WN: numerals of 5-7 bytes / over 3 decimals are typed here (a side path); without
 // it (the plan's sampled WHERE / SUM fields are all <= 4 bytes) such a record goes
 // whole to slow_kernel, and the kernel keeps only the fixed-point SUM
-template <bool GROUPED, bool WHERE, int NS, bool COMMA, bool CANON, int RP, bool WN, int EXT = 0>
+template <bool GROUPED, bool WHERE, int NS, bool COMMA, bool CANON, int RP, bool WN, int EXT = 0, bool WSTR = false>
 __global__ __launch_bounds__(LT) void fast_kernel(const uint8_t* __restrict__ g, ScanStats* __restrict__ stats,
                                                   unsigned long long* __restrict__ slow_list,
                                                   unsigned long long slow_cap, const FastPlan fp,
                                                   const GroupTable* __restrict__ tabs) {
     static_assert(EXT == 0 || (NS == 1 && !WN), "MIN / MAX: one fixed-point argument, no double addends");
+    static_assert(!WSTR || (WHERE && !WN && EXT == 0), "STRING-literal WHERE: the narrow-numeral builds");
     extern __shared__ __align__(16) uint8_t smem[];
     uint8_t* q = smem;
     // LDS table: slot records first (LDS address 0: field offsets fold into the
@@ -790,10 +795,11 @@ __global__ __launch_bounds__(LT) void fast_kernel(const uint8_t* __restrict__ g,
             continue;
 #endif
             // ---- field bytes (one batch of LDS reads)
-            uint32_t wd[RP], sd[RP][MAXS], k0[RP], k1[RP];
+            uint32_t wd[RP], wd1[RP], sd[RP][MAXS], k0[RP], k1[RP];
 #pragma unroll
             for (int u = 0; u < RP; u++) {
-                if (WHERE) wd[u] = ld4a(pa[u] + wst[u]);
+                if (WSTR) ld8a(pa[u] + wst[u], wd[u], wd1[u]);
+                else if (WHERE) wd[u] = ld4a(pa[u] + wst[u]);
 #pragma unroll
                 for (int j = 0; j < NS; j++) sd[u][j] = ld4a(pa[u] + sst[u][j]);
                 if (GROUPED) ld8a(pa[u] + gst[u], k0[u], k1[u]);
@@ -804,7 +810,26 @@ __global__ __launch_bounds__(LT) void fast_kernel(const uint8_t* __restrict__ g,
             bool wu[RP];
 #pragma unroll
             for (int u = 0; u < RP; u++) { pass[u] = true; wu[u] = false; }
-            if (WHERE) {
+            if (WSTR) {
+                // a STRING field of 1-8 bytes: no leading digit / sign / dot (never a
+                // numeral or a date, infer_type csv_reader.c:133-240), no byte <= ' '
+                // (trim_whitespace is a no-op); then strcmp against the literal is the
+                // order of the zero-padded big-endian words.  Any other non-empty field
+                // goes whole to slow_kernel (wu).
+#pragma unroll
+                for (int u = 0; u < RP; u++) {
+                    const uint32_t len = wen[u] - wst[u];
+                    const uint32_t m0 = len_mask(len, 0), m1 = len_mask(len, 1);
+                    const uint32_t a0 = wd[u] & m0, a1 = wd1[u] & m1;
+                    const uint32_t c0 = a0 & 0xFFu;
+                    const bool ok = (len - 1u < 8u) & !(is_digit(c0) | (c0 == '-') | (c0 == '+') | (c0 == '.')) &
+                                    ((low_bytes(a0, m0 & 0x80808080u) | low_bytes(a1, m1 & 0x80808080u)) == 0);
+                    const uint64_t x = ((uint64_t)__builtin_bswap32(a0) << 32) | __builtin_bswap32(a1);
+                    const uint64_t ws = fp.wstr;
+                    pass[u] = len == 0 ? pass_null : tt_result(wtt, x < ws ? -1 : (x > ws ? 1 : 0));
+                    wu[u] = !ok & (len != 0) & !fail[u];
+                }
+            } else if (WHERE) {
                 bool wide = false;
 #pragma unroll
                 for (int u = 0; u < RP; u++) {
@@ -2224,12 +2249,22 @@ bool fast_shape(const ScanPlan* P, int grouped, FastPlan* fp, int* ns, bool* whe
         *where = false;
     } else if (P->nprog == 3 && P->prog[0].op == OP_COL && P->prog[1].op == OP_CONST && P->prog[2].op == OP_CMP) {
         const Cell& L = P->consts[P->prog[1].b];
-        if (L.kind != K_INT && L.kind != K_DBL) return false;
+        const bool slit = L.kind == K_STR && L.len >= 1 && L.len <= 8;
+        if (L.kind != K_INT && L.kind != K_DBL && !slit) return false;
         *where = true;
         wcol = P->need_col[P->prog[0].a];
         const uint32_t op = P->prog[2].a;
         fp->wtt = (fcmp_result(op, -1) ? 1u : 0u) | (fcmp_result(op, 0) ? 2u : 0u) | (fcmp_result(op, 1) ? 4u : 0u);
         fp->pass_null = fcmp_result(op, -1) ? 1u : 0u;             // NULL < any non-NULL
+        if (slit) {   // (the literal's bytes: cq_launch_fast; ',' / '"' canonical narrow builds only)
+            fp->wstr_lit = 1;
+            if (ext || d != ',' || P->quote != '"') return false;
+        }
+    } else {
+        return false;
+    }
+    if (*where && !fp->wstr_lit) {   // numeric literal: the thresholds
+        const Cell& L = P->consts[P->prog[1].b];
         double lv;
         if (L.kind == K_INT) lv = (double)(int64_t)L.bits;
         else memcpy(&lv, &L.bits, 8);
@@ -2255,8 +2290,6 @@ bool fast_shape(const ScanPlan* P, int grouped, FastPlan* fp, int* ns, bool* whe
         B = B > 9999 ? 9999 : B;
         if (A > B) { fp->wa = 0xFFFFFFFFu; fp->ww = 0; }     // empty: M - wa = M + 1 > 0
         else { fp->wa = (uint32_t)A; fp->ww = (uint32_t)(B - A); }
-    } else {
-        return false;
     }
     if (grouped && (P->group_slot < 0 || P->lean_k16)) return false;
     // the roles' fields in column order (equal columns share a field; ties keep the
@@ -2280,14 +2313,16 @@ bool fast_shape(const ScanPlan* P, int grouped, FastPlan* fp, int* ns, bool* whe
         canon = canon && k == want;
     }
     *canonical = canon;
-    if (wide_num || ext) {   // a WHERE / SUM column whose sampled fields exceed 4 bytes
+    if (wide_num || ext || fp->wstr_lit) {   // a WHERE / SUM column whose sampled fields exceed 4 bytes
         bool wn = false;
-        for (int k = 0; k < nr; k++)
-            if (roles[k] != 3) wn = wn || ((P->fast_wide_cols >> (cols[k] < 63 ? cols[k] : 63)) & 1);
+        for (int k = 0; k < nr; k++)      // (a STRING-literal WHERE reads up to 8 bytes itself)
+            if (roles[k] != 3 && !(roles[k] == 0 && fp->wstr_lit))
+                wn = wn || ((P->fast_wide_cols >> (cols[k] < 63 ? cols[k] : 63)) & 1);
         wn = wn || getenv("CQGPU_FAST_WN") != nullptr;
         if (wide_num) *wide_num = wn;
         // MIN / MAX: the narrow-numeral ',' / '"' builds only (fixed point, no doubles)
         if (ext && (wn || d != ',' || P->quote != '"' || P->n >= (1ull << fast::EXT_POS_BITS))) return false;
+        if (fp->wstr_lit && (wn || !canon)) return false;   // (the STRING-literal builds: narrow, canonical)
     }
     return true;
 }
@@ -2322,7 +2357,12 @@ fast_fn_t pick_wc(bool where, int ns, bool comma, bool rp3, bool wn) {
     return (CANON && !wn) ? pick_ns<G, false, true, CANON, false>(ns, rp3) : pick_ns<G, false, true, CANON, true>(ns, rp3);
 }
 template <bool G>
-fast_fn_t pick_fast(bool where, int ns, bool comma, bool canon, bool rp3, bool wn, int ext = 0) {
+fast_fn_t pick_fast(bool where, int ns, bool comma, bool canon, bool rp3, bool wn, int ext = 0, bool wstr = false) {
+    if (wstr) {    // (fast_shape: ',' / '"', canonical roles, narrow numerals, no MIN / MAX)
+        if (ns == 0) return fast::fast_kernel<G, true, 0, true, true, 2, false, 0, true>;
+        return ns == 1 ? fast::fast_kernel<G, true, 1, true, true, 2, false, 0, true>
+                       : fast::fast_kernel<G, true, 2, true, true, 2, false, 0, true>;
+    }
     if (ext) {     // (fast_shape: one argument, ',' / '"', narrow numerals)
         if (canon) {
             if (where) return ext == 1 ? fast::fast_kernel<G, true, 1, true, true, 2, false, 1>
@@ -2413,7 +2453,7 @@ hipError_t cq_launch_fast(const uint8_t* g, const cq::ScanPlan* P, const cq::Gro
     // the sampled stride is 120 records' worth (lean_kernel's choice): below the
     // largest stride the records average under 33 bytes -> the three-record pass,
     // over windows of the largest stride (test knob CQGPU_FAST_RP2: keep two)
-    const bool rp3 = !grouped && !ext && fp.ws < (uint32_t)fast::WS && !getenv("CQGPU_FAST_RP2");
+    const bool rp3 = !grouped && !ext && !fp.wstr_lit && fp.ws < (uint32_t)fast::WS && !getenv("CQGPU_FAST_RP2");
     if (rp3) fp.ws = (uint32_t)fast::WS;
     if (hi > lo) {
         const uint64_t wl = lo / fp.ws, wh = (hi - 1) / fp.ws;
@@ -2439,11 +2479,26 @@ hipError_t cq_launch_fast(const uint8_t* g, const cq::ScanPlan* P, const cq::Gro
     else memset(&tabs[1], 0, sizeof tabs[1]);
     hipError_t e = cq::upload_buffer(tabs_dev[dev & 63], tabs, sizeof tabs, s);
     if (e != hipSuccess) return e;
+    if (fp.wstr_lit) {   // the literal's bytes (a STRING cell points at device memory); strcmp stops at a NUL
+        const Cell& L = P->consts[P->prog[1].b];
+        uint8_t b[8] = {0, 0, 0, 0, 0, 0, 0, 0};
+        hipError_t e = hipMemcpyAsync(b, (const void*)(uintptr_t)L.bits, L.len, hipMemcpyDeviceToHost, s);
+        if (e == hipSuccess) e = hipStreamSynchronize(s);
+        if (e != hipSuccess) return e;
+        bool nul = false;
+        uint64_t x = 0;
+        for (int i = 0; i < 8; i++) {
+            nul = nul || b[i] == 0;
+            x = (x << 8) | (nul ? 0u : b[i]);
+        }
+        fp.wstr = x;
+    }
     const bool comma = P->delim == ',' && P->quote == '"';
     // (EXT builds: the packed extreme keys go to the raw table's extpos words)
     if (ext && (!rt || !rt->extpos[fp.ext_acc] || rt->cap < 1)) return hipErrorInvalidValue;
-    const fast_fn_t fn = grouped ? pick_fast<true>(where, ns, comma, canon, false, wn, ext)
-                                 : pick_fast<false>(where, ns, comma, canon, rp3, wn, ext);
+    const bool wstr = fp.wstr_lit != 0;
+    const fast_fn_t fn = grouped ? pick_fast<true>(where, ns, comma, canon, false, wn, ext, wstr)
+                                 : pick_fast<false>(where, ns, comma, canon, rp3, wn, ext, wstr);
     const size_t lds = fast_lds(grouped, ns);
     cq::set_max_lds((const void*)fn, (int)lds);
     hipLaunchKernelGGL(fn, dim3(grid), dim3(fast::LT), lds, s, g, stats, slow_list, slow_cap, fp,

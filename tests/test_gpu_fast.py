@@ -164,8 +164,8 @@ def test_fast_role_orders(d):
 def test_fast_not_for_other_shapes(d):
     rows = ["%d,%d,k%d" % (i % 9, i % 4, i % 3) for i in range(1000)]
     p = _write(d / "other.csv", "a,b,c", rows)
-    # a STRING literal in WHERE and row-returning SELECTs are lean_kernel's shapes
-    st = check(f"SELECT c, COUNT(*) FROM '{p}' WHERE c != 'x' GROUP BY c", fast=False)
+    # a STRING literal over 8 bytes and row-returning SELECTs are lean_kernel's shapes
+    st = check(f"SELECT c, COUNT(*) FROM '{p}' WHERE c != 'x12345678' GROUP BY c", fast=False)
     assert st["scan_kernel"] != 2, st
     st = check(f"SELECT a, b FROM '{p}' WHERE b > 1", fast=False)
     assert st["scan_kernel"] != 2, st
@@ -318,3 +318,26 @@ def test_fast_min_max_declined_and_mixed(d):
     check(f"SELECT g, MIN(w), MAX(w) FROM '{p}' GROUP BY g", fast=False)
     check(f"SELECT g, SUM(v), MAX(w) FROM '{p}' GROUP BY g", fast=False)
     check(f"SELECT g, MAX(w), COUNT(*) FROM '{p}' WHERE w > 5 GROUP BY g")
+
+
+def test_fast_string_literal_where(d):
+    """WHERE `column op 'literal'` (1-8 byte STRING literal) in fast_kernel: a field of
+    1-8 bytes with no leading digit / sign / dot and no byte <= ' ' is a STRING
+    (infer_type, csv_reader.c:133-240) compared by strcmp order (evaluate_expression
+    -> value_compare); numeral- or date-shaped fields, 9+ byte fields and fields with
+    blanks go whole to slow_kernel, which types them exactly (value_compare across
+    classes); empty fields are NULL"""
+    rng = np.random.default_rng(77)
+    words = ["f", "m", "fe", "ff", "e", "g", "role_001", "role_0010", "12", "1990-01-01", "-x", ".5", "f ",
+             "zz", "F", "", "a&b"]
+    rows = ["%s,%d,%s,%d.%d,role_%03d" % ("n%d" % (i % 5), i % 90, words[int(rng.integers(0, len(words)))],
+                                         i % 3, i % 10, int(rng.integers(0, 200))) for i in range(120_000)]
+    p = _write(d / "wstr.csv", "name,age,gender,height,role", rows)
+    for lit, op in (("f", "="), ("m", "!="), ("f", "<"), ("fe", ">"), ("role_001", ">="), ("g", "<="), ("F", "=")):
+        check(f"SELECT role, COUNT(*), SUM(height), AVG(height) FROM '{p}' WHERE gender {op} '{lit}' GROUP BY role")
+    check(f"SELECT COUNT(*), SUM(height) FROM '{p}' WHERE gender = 'f'")
+    check(f"SELECT COUNT(*) FROM '{p}' WHERE gender > 'e'")
+    check(f"SELECT role, COUNT(*) FROM '{p}' WHERE gender = 'f' GROUP BY role")
+    # the literal itself numeral-shaped (a STRING literal all the same) and a 9-byte literal
+    check(f"SELECT role, COUNT(*) FROM '{p}' WHERE gender = '12' GROUP BY role")
+    check(f"SELECT role, COUNT(*) FROM '{p}' WHERE gender = 'role_0010' GROUP BY role", fast=False)
