@@ -1827,48 +1827,58 @@ __global__ __launch_bounds__(1024) void jx_part_probe_kernel(const unsigned long
     __syncthreads();
     const uint32_t x = blockIdx.x & 7u, sub = blockIdx.x >> 3, nsub = gridDim.x >> 3;
     unsigned long long pairs = 0;
-    // The block's segments of partition p (sources sub, sub + nsub, ...), up to SEG at a
-    // time, as one flat index space: their counts' prefix in LDS (then uniform
-    // registers), entry j in segment s = #(prefix[k] <= j).  Every lane has U entries
-    // in flight -- their loads, then their d16 lookups, then the LDS updates -- so
-    // neither a segment boundary nor the two dependent loads of an entry idle lanes.
-    constexpr uint32_t U = 8, SEG = 16;
-    __shared__ uint32_t soff[SEG + 1];
+    // Work items of partition p: chunks of CH entries of the block's segments (sources
+    // sub, sub + nsub, ...), SEG segments at a time; wave w takes items w, w + NW, ...
+    // A chunk is one segment's entries [c * CH, c * CH + CH): every lane loads U of
+    // them (lane-strided: coalesced), then their U d16 lookups, then the LDS updates,
+    // so a lane keeps U independent loads in flight and the item -> (segment, chunk)
+    // map is scalar work once per chunk, not vector work per entry.
+    constexpr uint32_t U = 8, CH = 64 * U, SEG = 16, NW = 1024 / 64;
+    __shared__ uint32_t sitem[SEG + 1], scount[SEG];
+    const uint32_t wv = threadIdx.x >> 6, lane = threadIdx.x & 63;
     for (uint32_t p = x; p < np; p += 8) {
         for (uint32_t sb0 = sub; sb0 < nsrc; sb0 += SEG * nsub) {
-            __syncthreads();                                   // (the last group's soff reads)
+            __syncthreads();                                   // (the last group's reads)
             if (threadIdx.x < 64) {
                 const uint32_t sb = sb0 + threadIdx.x * nsub;
-                uint32_t c = threadIdx.x < SEG && sb < nsrc ? pcnt[(size_t)sb * np + p] : 0u;
+                const uint32_t n = threadIdx.x < SEG && sb < nsrc ? pcnt[(size_t)sb * np + p] : 0u;
+                uint32_t c = (n + CH - 1) / CH;                  // chunks of this segment
                 for (int o = 1; o < (int)SEG; o <<= 1) {
                     const uint32_t t = (uint32_t)__shfl_up((int)c, o, 64);
                     c += threadIdx.x >= (uint32_t)o ? t : 0u;
                 }
-                if (threadIdx.x < SEG) soff[threadIdx.x + 1] = c;
-                if (threadIdx.x == 0) soff[0] = 0;
+                if (threadIdx.x < SEG) { sitem[threadIdx.x + 1] = c; scount[threadIdx.x] = n; }
+                if (threadIdx.x == 0) sitem[0] = 0;
             }
             __syncthreads();
-            uint32_t o[SEG + 1];
-#pragma unroll
-            for (uint32_t k = 0; k <= SEG; k++) o[k] = __builtin_amdgcn_readfirstlane(soff[k]);
-            const uint32_t total = o[SEG];
-            for (uint32_t j0 = 0; j0 < total; j0 += U * blockDim.x) {
+            const uint32_t items = __builtin_amdgcn_readfirstlane(sitem[SEG]);
+            uint32_t sg = 0;
+            for (uint32_t t = wv; t < items; t += NW) {
+                while (sg + 1 < SEG && __builtin_amdgcn_readfirstlane(sitem[sg + 1]) <= t) sg++;   // (t rises)
+                const uint32_t c0 = (t - __builtin_amdgcn_readfirstlane(sitem[sg])) * CH;
+                const uint32_t n = __builtin_amdgcn_readfirstlane(scount[sg]);
+                const unsigned long long* e = pent + ((size_t)(sb0 + sg * nsub) * np + p) * pcap;
                 unsigned long long v[U];
 #pragma unroll
                 for (uint32_t u = 0; u < U; u++) {
-                    const uint32_t j = j0 + u * blockDim.x + threadIdx.x;
-                    uint32_t sg = 0;
-#pragma unroll
-                    for (uint32_t k = 1; k < SEG; k++) sg += j >= o[k] ? 1u : 0u;
-                    const size_t at = ((size_t)(sb0 + sg * nsub) * np + p) * pcap + (j - o[sg]);
-                    v[u] = j < total ? __builtin_nontemporal_load(pent + at) : ~0ull;
+                    const uint32_t i = c0 + u * 64 + lane;
+                    v[u] = i < n ? __builtin_nontemporal_load(e + i) : ~0ull;
                 }
                 uint32_t gv[U];
 #pragma unroll
                 for (uint32_t u = 0; u < U; u++) {
                     const uint32_t ix = (uint32_t)v[u];
+#ifdef PP_NOLOOK                                           // experiment: no d16 lookups (wrong results)
+                    gv[u] = ix < range ? (ix & 1023u) + 1u : 0u;
+#else
                     gv[u] = ix < range ? (uint32_t)d16[ix] : 0u;   // (a skipped entry: ~0)
+#endif
                 }
+#ifdef PP_NOATOM                                           // experiment: no LDS updates (wrong results)
+#pragma unroll
+                for (uint32_t u = 0; u < U; u++) pairs += gv[u] ? 1u : 0u;
+                continue;
+#endif
 #pragma unroll
                 for (uint32_t u = 0; u < U; u++) {
                     if (!gv[u]) continue;
