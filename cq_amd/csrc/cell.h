@@ -697,7 +697,7 @@ CQ_HD bool text_has_tab(const Cell& c) {
 // byte stream into two independent 64-bit lanes.  A list with a tab inside a part
 // never joins to the same text as a list without one (its text has more tabs), so
 // these keys (GK_COMP, len = part count | COMPT_FLAG) never meet the per-part
-// digests.  false: a DOUBLE part of 2^43 or more (its %.6f text is not rendered here).
+// digests.  Every cell renders (true); a DOUBLE through dbl_text, cut at 255 bytes.
 constexpr uint32_t COMPT_FLAG = 0x8000;
 struct TextHash {
     uint64_t a = 0xCBF29CE484222325ULL, b = 0x84222325CBF29CE4ULL;
@@ -734,6 +734,90 @@ struct TextWindow {
         while (n) byte(t[--n]);
     }
 };
+// glibc's "%.6f" of a double, exactly (the binary value rounded half-even to 6
+// decimals): below 2^43 through micro_units; from 2^43 the value m * 2^e has at most
+// 9 fraction bits (integer part below 2^53, fraction f / 2^k rounded in 32-bit
+// arithmetic) or is an integer, rendered from base-10^9 limbs (up to 309 digits);
+// inf / nan as glibc prints them
+template <class H>
+CQ_HD void dbl_text(H& h, uint64_t bits) {
+    const uint32_t ex = (uint32_t)((bits >> 52) & 0x7FF);
+    const uint64_t frac = bits & ((1ULL << 52) - 1);
+    if (bits >> 63) h.byte('-');
+    if (ex == 0x7FF) {
+        if (frac) h.bytes((const uint8_t*)"nan", 3);
+        else h.bytes((const uint8_t*)"inf", 3);
+        return;
+    }
+    const double ax = as_dbl(bits & ~(1ULL << 63));
+    if (ax < 8796093022208.0) {                         // < 2^43
+        const uint64_t u = micro_units(ax);
+        h.dec(u / 1000000ULL, 1);
+        h.byte('.');
+        h.dec(u % 1000000ULL, 6);
+        return;
+    }
+    const uint64_t m = frac | (1ULL << 52);             // (normal: >= 2^43)
+    const int32_t e = (int32_t)ex - 1075;
+    if (e < 0) {                                        // 2^43 <= x < 2^53: k = -e <= 9 fraction bits
+        const uint32_t k = (uint32_t)(-e);
+        uint64_t ip = m >> k;
+        const uint64_t f = m & ((1ULL << k) - 1);
+        const uint64_t n = f * 1000000ULL;               // < 2^29
+        uint64_t q = n >> k;
+        const uint64_t r = n & ((1ULL << k) - 1), half = 1ULL << (k - 1);
+        if (r > half || (r == half && (q & 1))) q++;
+        if (q == 1000000ULL) { ip++; q = 0; }
+        h.dec(ip, 1);
+        h.byte('.');
+        h.dec(q, 6);
+        return;
+    }
+    if (e <= 11) {                                      // m * 2^e < 2^64
+        h.dec(m << e, 1);
+    } else {                                            // base-10^9 limbs, least significant first
+        uint32_t L[36];
+        uint32_t nl = 2;
+        L[0] = (uint32_t)(m % 1000000000ULL);
+        L[1] = (uint32_t)(m / 1000000000ULL);           // (m < 2^53 < 10^18)
+        for (int32_t left = e; left > 0;) {
+            const uint32_t s = left > 29 ? 29u : (uint32_t)left;
+            uint64_t carry = 0;
+            for (uint32_t i = 0; i < nl; i++) {
+                const uint64_t v = ((uint64_t)L[i] << s) + carry;
+                L[i] = (uint32_t)(v % 1000000000ULL);
+                carry = v / 1000000000ULL;
+            }
+            while (carry && nl < 36) { L[nl++] = (uint32_t)(carry % 1000000000ULL); carry /= 1000000000ULL; }
+            left -= (int32_t)s;
+        }
+        while (nl > 1 && L[nl - 1] == 0) nl--;
+        h.dec(L[nl - 1], 1);
+        for (uint32_t i = nl - 1; i-- > 0;) h.dec(L[i], 9);
+    }
+    h.bytes((const uint8_t*)".000000", 7);
+}
+
+// a key part's text as the reference's `char key_part[256]` holds it: snprintf
+// keeps the first 255 bytes (a %.6f of a double above ~1e248 is longer)
+template <class H>
+struct Cap255 {
+    H& h;
+    uint32_t n;
+    CQ_HDM void byte(uint8_t c) {
+        if (n < 255) h.byte(c);
+        n++;
+    }
+    CQ_HDM void bytes(const uint8_t* p, uint32_t k) { for (uint32_t i = 0; i < k; i++) byte(p[i]); }
+    CQ_HDM void dec(uint64_t v, int mind) {
+        uint8_t t[20];
+        int k = 0;
+        do { t[k++] = (uint8_t)('0' + v % 10); v /= 10; } while (v);
+        while (k < mind) t[k++] = '0';
+        while (k) byte(t[--k]);
+    }
+};
+
 template <class H>
 CQ_HD bool joined_text_add(H& h, const Cell& c, bool first) {
     if (!first) h.byte('\t');
@@ -746,13 +830,8 @@ CQ_HD bool joined_text_add(H& h, const Cell& c, bool first) {
             break;
         }
         case K_DBL: {
-            const double x = as_dbl(c.bits), ax = x < 0 ? -x : x;
-            if (!(ax < 8796093022208.0)) return false;
-            const uint64_t u = micro_units(ax);
-            if (c.bits >> 63) h.byte('-');
-            h.dec(u / 1000000ULL, 1);
-            h.byte('.');
-            h.dec(u % 1000000ULL, 6);
+            Cap255<H> cp{h, 0};
+            dbl_text(cp, c.bits);
             break;
         }
         case K_DATE: {

@@ -3053,7 +3053,7 @@ std::vector<HGroup> aggregate_pairs(DevCtx& c, Compiled& C, const JoinMap& MA, c
         break;
     }
     g_stats.passed = st.passed;
-    if (st.key_flags & 2u) throw Ineligible{"composite GROUP BY: a part list with a tab and a DOUBLE of 2^43 or more"};
+    if (st.key_flags & 2u) throw HipError{"internal: a composite key part the joined text could not render"};
     std::vector<int> rep_ord(C.rep_cols.size());
     for (size_t i = 0; i < rep_ord.size(); i++) rep_ord[i] = (int)i;
     std::vector<HGroup> groups =
@@ -4097,7 +4097,7 @@ void comp_key_texts(DevCtx& c, const cqgpu_table* t, const Compiled& C, std::vec
     HIPCHECK(hipStreamSynchronize(c.stream));
     for (uint32_t i = 0; i < n; i++) {
         if (lens[i] == 0xFFFFFFFFu)
-            throw Ineligible{"composite GROUP BY across partials: a key text over 4 KiB or a DOUBLE part of 2^43 or more"};
+            throw Ineligible{"composite GROUP BY across partials: a key text over 4 KiB"};
         HGroup& h = groups[i];
         h.kcls = GK_LONG;
         h.klen = lens[i];

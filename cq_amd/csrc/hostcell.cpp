@@ -39,3 +39,31 @@ extern "C" cq::Cell cq_host_eval(const cq::Insn* code, uint32_t n, const cq::Cel
     }
     return sp > 0 ? st[sp - 1] : cell_null();
 }
+
+// a DOUBLE cell's composite-key part text (cell.h joined_text_add: "%.6f", the first
+// 255 bytes) into out (256 bytes); its length.  Checked on the CPU against Python's
+// correctly rounded formatting (tests/test_key_text.py).
+namespace {
+struct HostSink {
+    char* p;
+    uint32_t n;
+    void byte(uint8_t c) { if (n < 255) p[n] = (char)c; n++; }
+    void bytes(const uint8_t* q, uint32_t k) { for (uint32_t i = 0; i < k; i++) byte(q[i]); }
+    void dec(uint64_t v, int mind) {
+        uint8_t t[20];
+        int k = 0;
+        do { t[k++] = (uint8_t)('0' + v % 10); v /= 10; } while (v);
+        while (k < mind) t[k++] = '0';
+        while (k) byte(t[--k]);
+    }
+};
+}  // namespace
+extern "C" uint32_t cq_host_double_key_text(uint64_t bits, char* out) {
+    HostSink h{out, 0};
+    cq::Cell c;
+    c.kind = cq::K_DBL;
+    c.len = 0;
+    c.bits = bits;
+    cq::joined_text_add(h, c, true);
+    return h.n < 255 ? h.n : 255;
+}

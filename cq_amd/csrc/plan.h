@@ -163,7 +163,7 @@ struct ScanStats {
     unsigned int acc_classes[MAX_ACC];  // OR of value classes seen per accumulator (1 num, 2 str, 4 date)
     unsigned long long slow_records;    // records the fast field walk handed to the general parser
     unsigned long long clk[8];          // profiling builds (CQ_CLOCKS): shader cycles per phase, summed over waves
-    unsigned int key_flags;             // composite GROUP BY: 2 = a tab list with a DOUBLE part >= 2^43 (refused)
+    unsigned int key_flags;             // composite GROUP BY: 2 = a joined text that could not render (never: every cell renders)
 };
 
 // a MIN/MAX candidate published by one block (or wave) for one group

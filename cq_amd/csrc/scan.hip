@@ -1346,7 +1346,7 @@ __device__ GKey plan_group_key(const ScanPlan& P, const Cell* kc, const CS& cs, 
 // '\t', rendered from the group's first record (its need cells, gather_kernel).
 // Range partials carry this text instead of the 128-bit part digest, so the merges
 // across ranks group composite keys byte for byte, as the reference does.
-// lens[i] = ~0: longer than cap or a DOUBLE part of 2^43 or more (not rendered here).
+// lens[i] = ~0: longer than cap.
 __global__ void comp_text_kernel(const Cell* __restrict__ cells, uint32_t n, uint32_t cap, uint8_t* __restrict__ out,
                                  uint32_t* __restrict__ lens) {
     const ScanPlan& P = c_plan;

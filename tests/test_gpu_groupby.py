@@ -227,3 +227,39 @@ def test_joined_text_collision_fails_loudly(tmp_path, monkeypatch):
         tol = tolerant_columns(ast)
     compare(got, want, tol, sql)
     assert len(want["rows"]) == 10        # 'a\tb'+'c' and 'a'+'b\tc' join to one text
+
+
+def test_tab_parts_with_large_doubles(tmp_path):
+    """A composite key whose text part holds a tab next to a DOUBLE part of 2^43 or
+    more: the joined text renders the double's full "%.6f" (the exact binary value,
+    integer digits up to the key_part[256] cut, evaluator.c:113-212), so
+    ("x\\t9007199254740993.000000", ...) style collisions of the reference's texts
+    are reproduced; one GPU and 3 range partials against the oracle"""
+    import random
+    rng = random.Random(11)
+    a_vals = ["x\ty", "x", "p\tq", "p"]
+    d_vals = ["8796093022208.5", "9007199254740993", "123456789012345.125", "1e20", "1.5e300", "-2.5e17",
+              "17592186044416.0078125", "8796093022208.00048828125", "3", "0.5"]
+    rows = ["a,d,c"] + ["%s,%s,%d" % (rng.choice(a_vals), rng.choice(d_vals), rng.randrange(9)) for _ in range(3000)]
+    p = tmp_path / "bigd.csv"
+    p.write_text("\n".join(rows) + "\n")
+    from cq_amd import abi
+    for sql in (f"SELECT a, d, COUNT(*), SUM(c) FROM '{p}' GROUP BY a, d",
+                f"SELECT d, COUNT(*) FROM '{p}' GROUP BY d, a"):
+        want, unsup = cqtest.oracle_query(sql)
+        assert not unsup
+        with cqtest.Parsed(sql) as ast:
+            got = cq_amd.evaluate(ast)
+            tol = tolerant_columns(ast)
+            assert not cq_amd.last_ineligible(), (sql, cq_amd.last_ineligible())
+            compare(got, want, tol, sql)
+            tabs = [cq_amd.Table.open_range(str(p), r, 3) for r in range(3)]
+            blobs = [cq_amd.query_partial(ast, [t]) for t in tabs]
+            for t in tabs:
+                t.close()
+            assert all(blobs), cq_amd.last_error() or cq_amd.last_ineligible()
+            tp = cq_amd.merge_partials(ast, blobs)
+            assert tp, cq_amd.last_error()
+            merged = abi.table_to_py(tp)
+            cq_amd.result_free(tp)
+        compare(merged, want, tol, sql + " (3 partials)")
