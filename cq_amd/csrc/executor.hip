@@ -2992,7 +2992,8 @@ void side_gids(DevCtx& c, const cqgpu_table* t, uint32_t n, DevBuf& own, const u
 // then compaction and the representative cells of each group's first pair
 // (join_finish_kernel): groups in first-pair order, `first` / `extpos` = pair indexes
 std::vector<HGroup> aggregate_pairs(DevCtx& c, Compiled& C, const JoinMap& MA, const JoinMap& MR, const uint2* pairs,
-                                    unsigned long long np, const Cell* Lc, const Cell* Rc, ScanStats& st) {
+                                    unsigned long long np, const Cell* Lc, const Cell* Rc, ScanStats& st,
+                                    bool all_splits = false) {
     const int grouped = C.grouped ? 1 : 0;
     constexpr uint32_t SB = 48;
     const uint32_t ncell = (uint32_t)MR.n + (uint32_t)C.P.nacc + 1;
@@ -3064,10 +3065,13 @@ std::vector<HGroup> aggregate_pairs(DevCtx& c, Compiled& C, const JoinMap& MA, c
     // is the first occurrence of that class's extreme.  One more pass per such
     // accumulator computes, per class, the extreme (with its first position) and the
     // first position of any cell of the class; groups come out in the same order.
+    // all_splits (a join partial): also for one class, since another rank may hold
+    // cells of another class and the merge then needs this rank's first position of
+    // each class, not its extreme's
     for (int a = 0; a < C.P.nacc; a++) {
         if (C.P.acc[a].kind == ACC_SUM || C.P.acc[a].cls) continue;   // (a class-split pass itself)
         const unsigned m = st.acc_classes[a];
-        if (!(m & (m - 1))) continue;
+        if (!m || (!all_splits && !(m & (m - 1)))) continue;
         Compiled C2 = C;
         C2.P.nacc = 6;
         for (int k = 0; k < 3; k++) {
@@ -4006,7 +4010,8 @@ cq_table* run_join(DevCtx& c, cq_node* q, const cqgpu_table* L, const cqgpu_tabl
         const JoinMap MA = join_map(C.need_cols, nl, A, B);
         const JoinMap MR = join_map(C.rep_cols, nl, A, B);
         ScanStats st;
-        groups = aggregate_pairs(c, C, MA, MR, pairs.as<uint2>(), np, A.cells.as<Cell>(), B.cells.as<Cell>(), st);
+        groups = aggregate_pairs(c, C, MA, MR, pairs.as<uint2>(), np, A.cells.as<Cell>(), B.cells.as<Cell>(), st,
+                                 part != nullptr);
         if (!C.vla.empty()) {
             std::vector<JoinMap> VM;
             for (auto& v : C.vla) VM.push_back(join_map(std::vector<int>{v.second}, nl, A, B));
@@ -4021,6 +4026,11 @@ cq_table* run_join(DevCtx& c, cq_node* q, const cqgpu_table* L, const cqgpu_tabl
                 if (h.first != NOPOS) pidx.push_back(h.first);
                 for (int a = 0; a < C.P.nacc; a++)
                     if (h.extpos[a] != NOPOS) pidx.push_back(h.extpos[a]);
+                for (const HGroup::ClassSplit& cs : h.split)     // (per-class MIN/MAX state)
+                    for (int k = 0; k < 3; k++) {
+                        if (cs.extpos[k] != NOPOS) pidx.push_back(cs.extpos[k]);
+                        if (cs.first[k] != NOPOS) pidx.push_back(cs.first[k]);
+                    }
             }
             for (unsigned long long p : pidx)
                 if (p >= np) throw HipError{"join partial: pair position out of range"};
@@ -4046,6 +4056,11 @@ cq_table* run_join(DevCtx& c, cq_node* q, const cqgpu_table* L, const cqgpu_tabl
                     if (h.first != NOPOS) h.first = keys[k++];
                     for (int a = 0; a < C.P.nacc; a++)
                         if (h.extpos[a] != NOPOS) h.extpos[a] = keys[k++];
+                    for (HGroup::ClassSplit& cs : h.split)
+                        for (int j = 0; j < 3; j++) {
+                            if (cs.extpos[j] != NOPOS) cs.extpos[j] = keys[k++];
+                            if (cs.first[j] != NOPOS) cs.first[j] = keys[k++];
+                        }
                 }
             }
         }
@@ -5444,15 +5459,15 @@ cq_table* cqgpu_merge_partials(cq_node* q, const void* const* blobs, const size_
         // per class the extreme and first position (HGroup::split); a partial that saw
         // one class has that class's extreme only, whose position stands in for the
         // class's first -- ranges are disjoint and ordered, so only the order between
-        // partials matters there.  Hash-repartitioned join partials interleave
-        // positions across ranks and are refused.
+        // partials matters there.  Join partials interleave positions across ranks, so
+        // each carries every class's true first position (aggregate_pairs all_splits),
+        // as global (left id, right id) order keys.
         bool mixed[MAX_ACC] = {};
         for (uint32_t a = 0; a < nacc; a++) {
             if (C.P.acc[a].kind == ACC_SUM) continue;
             uint32_t m = 0;
             for (auto& pt : parts) m |= pt.classes[a];
             mixed[a] = (m & (m - 1)) != 0;
-            if (mixed[a] && joined) throw Ineligible{"MIN/MAX over a column mixing numbers, strings and dates"};
         }
         auto split_of = [](HGroup& h, int a) -> HGroup::ClassSplit& {
             for (auto& cs : h.split)

@@ -111,6 +111,13 @@ def files(tmp_path_factory):
     f["sb"] = ("k,w\n" + "".join(f"{'' if i % 53 == 0 else 'key%03d' % (i % 170)},{i * 3}\n"
                                   for i in range(700))).encode()
     f["mixed"] = b"k,z\n1,a\nx,b\n2,c\n,d\n2020-01-02,e\nx,f\n1.0,g\n"
+    # a column mixing numbers, strings and dates (MIN/MAX keep the class of the
+    # group's first non-NULL cell in nested-loop order, evaluator_aggregates.c:311-326)
+    tags = ["12", "abc", "2020-01-01", "", "7.5", "zz", "1999-12-31", "-3", "b"]
+    lines = ["id,tag,role"]
+    for i in range(2200):
+        lines.append(f"{int(rng.integers(0, 1800))},{tags[int(rng.integers(0, len(tags)))]},r{int(rng.integers(0, 9))}")
+    f["mu"] = ("\n".join(lines) + "\n").encode()
     # chain tables: roles of "du" (role_20..22 missing, role_05 twice, a NULL role) and
     # labels of the order quantities
     f["rl"] = ("role,dept,grade\n" + "".join(f"role_{i:02d},dept{i % 4},{i % 3}\n" for i in range(20))
@@ -160,6 +167,13 @@ QUERIES = [
     ("du", "do", "SELECT o.id, u.age FROM '{L}' AS u JOIN '{R}' AS o ON u.id = o.customer_id LIMIT 15 OFFSET 5"),
     ("du", "do", "SELECT DISTINCT u.role FROM '{L}' AS u JOIN '{R}' AS o ON u.id = o.customer_id"),
     ("sa", "sb", "SELECT * FROM '{L}' AS a JOIN '{R}' AS b ON a.k = b.k WHERE b.w < 100"),
+    # MIN/MAX over a column mixing value classes: every rank's per-class first
+    # positions and extremes as global pair keys
+    ("mu", "do", "SELECT u.role, COUNT(*), MIN(u.tag), MAX(u.tag) FROM '{L}' AS u JOIN '{R}' AS o "
+                 "ON u.id = o.customer_id GROUP BY u.role"),
+    ("mu", "do", "SELECT MIN(u.tag), MAX(u.tag), COUNT(*) FROM '{L}' AS u JOIN '{R}' AS o ON u.id = o.customer_id"),
+    ("mu", "do", "SELECT o.quantity, MAX(u.tag) FROM '{L}' AS u LEFT JOIN '{R}' AS o ON u.id = o.customer_id "
+                 "GROUP BY o.quantity"),
     # STDDEV across partials: per-rank (sum, squared deviations, count), merged exactly
     ("du", "do", "SELECT u.role, STDDEV(o.price), COUNT(*) FROM '{L}' AS u JOIN '{R}' AS o "
                  "ON u.id = o.customer_id GROUP BY u.role"),
