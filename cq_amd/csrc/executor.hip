@@ -1734,6 +1734,7 @@ std::vector<HGroup> make_groups(DevCtx& c, const Compiled& C, uint64_t limit, ui
         h.reps.resize(nrep);
         for (size_t i = 0; i < rep_ord.size(); i++) h.reps[rep_ord[i]] = cs[i];
     }
+    PHASE("groups");
     return groups;
 }
 
@@ -2972,6 +2973,17 @@ struct JoinPartial {
     // order, with their global order keys ((global left id << 32) | global right id)
     cq_table* rows = nullptr;
     std::vector<unsigned long long> row_keys;
+    // the joined plan's shape (run_join's compile): accumulators, representative
+    // cells, STDDEV / MEDIAN states -- the blob's header, without a second compile
+    int nacc = -1;
+    uint32_t nrep = 0, nvla = 0;
+    // the fused join's groups serialised straight from the packed result (no HGroup
+    // objects): `ng` records in the blob's group format, `first_at[i]` the byte offset
+    // of group i's first-pair key (patched to its global id by run_fast_join)
+    bool direct = false;
+    uint64_t ng = 0;
+    std::vector<uint8_t> gblob;
+    std::vector<size_t> first_at;
     ~JoinPartial() { if (rows) cqgpu_result_free(rows); }
 };
 
@@ -3450,6 +3462,83 @@ cq_table* run_fast_join(DevCtx& c, cq_node* q, Compiled& C, const cqgpu_table* L
             cq_table* res = nullptr;
             if (!part && grouped && presorted && ng) res = build_direct(C, hbuf.data(), ng, ncell, SB, rep_ord, Lit, ~0ull);
             PHASE("direct");
+            if (part && presorted && C.vla.empty()) {
+                // the partial's groups in the blob's group format, straight from the packed
+                // records (cqgpu_query_partial's "CQJ1" writer, field for field); any STRING
+                // cell longer than the inline bytes takes the HGroup path below
+                const size_t rec = 40 + 40 * (size_t)C.P.nacc;
+                const Cell* cells = (const Cell*)(hbuf.data() + ng * rec);
+                const uint8_t* sbytes = hbuf.data() + ng * rec + (size_t)ng * ncell * sizeof(Cell);
+                bool inline_ok = true;
+                for (size_t k = 0; k < (size_t)ng * ncell; k++)
+                    inline_ok = inline_ok && !(cells[k].kind == K_STR && cells[k].len > SB);
+                if (inline_ok) {
+                    const uint32_t nrep = (uint32_t)C.rep_cols.size();
+                    // sized once for the worst case (every cell a SB-byte string), written
+                    // through a raw cursor, trimmed at the end
+                    const size_t cell_max = 16 + SB;
+                    const size_t per = 4 + 4 + 8 + 8 + 4 + 16 + 8 + 8 + (size_t)C.P.nacc * (24 + cell_max) +
+                                       (size_t)nrep * cell_max + 4 + cell_max;
+                    std::vector<uint8_t>& gb = part->gblob;
+                    gb.resize((size_t)ng * per);
+                    uint8_t* w = gb.data();
+                    auto u32 = [&](uint32_t v) { memcpy(w, &v, 4); w += 4; };
+                    auto u64 = [&](uint64_t v) { memcpy(w, &v, 8); w += 8; };
+                    auto bytes = [&](const void* src, uint32_t n) { u32(n); memcpy(w, src, n); w += n; };
+                    part->first_at.clear();
+                    part->first_at.reserve(ng);
+                    auto cell_out = [&](size_t k) {
+                        const Cell& x = cells[k];
+                        u32(x.kind);
+                        u64(x.bits);
+                        bytes(sbytes + k * SB, x.kind == K_STR ? x.len : 0u);
+                    };
+                    std::vector<int> rep_at(nrep, -1);          // h.reps[rep_ord[i]] = cs[i]
+                    for (size_t i = 0; i < rep_ord.size(); i++) rep_at[rep_ord[i]] = (int)i;
+                    for (unsigned int i = 0; i < ng; i++) {
+                        const uint8_t* r = hbuf.data() + i * rec;
+                        const uint32_t cl = ((const uint32_t*)r)[0];
+                        const uint64_t w0 = ((const uint64_t*)r)[1], w1 = ((const uint64_t*)r)[2];
+                        const uint32_t kcls = cl >> 16, klen = cl & 0xffff;
+                        u32(kcls);
+                        u32(klen);
+                        u64(w0);
+                        u64(w1);
+                        if (kcls == GK_LONG) {
+                            const size_t k = (size_t)i * ncell + FD.ncols + C.P.nacc;
+                            bytes(sbytes + k * SB, cells[k].kind == K_STR ? cells[k].len : 0u);
+                        } else if (kcls == GK_STR) {
+                            uint8_t kb[16];
+                            const uint32_t n = std::min<uint32_t>(klen, 16);
+                            for (uint32_t j = 0; j < n; j++) kb[j] = (uint8_t)((j < 8 ? w0 >> (8 * j) : w1 >> (8 * (j - 8))) & 0xff);
+                            bytes(kb, n);
+                        } else {
+                            u32(0);
+                        }
+                        u64(((const unsigned long long*)r)[3]);          // COUNT
+                        part->first_at.push_back((size_t)(w - gb.data()));
+                        u64(((const unsigned long long*)r)[4]);          // first pair (patched)
+                        const uint64_t* qq = (const uint64_t*)(r + 40);
+                        for (int a = 0; a < C.P.nacc; a++) {
+                            u64(qq[5 * a]);                              // SUM (f64 bits)
+                            u64(qq[5 * a + 1]);                          // numeric count
+                            u64(NOPOS);                                  // (SUM plans: no extreme)
+                            cell_out((size_t)i * ncell + FD.ncols + a);
+                        }
+                        for (uint32_t rr = 0; rr < nrep; rr++) {
+                            if (rep_at[rr] >= 0) cell_out((size_t)i * ncell + rep_at[rr]);
+                            else { u32(K_NULL); u64(0); u32(0); }
+                        }
+                        u32(0);                                          // no class splits
+                    }
+                    gb.resize((size_t)(w - gb.data()));
+                    part->direct = true;
+                    part->ng = ng;
+                    g_stats.groups = ng;
+                    PHASE("serialize");
+                    return JOIN_PART_DONE;
+                }
+            }
             if (!res) {
                 std::vector<GroupOut> outs(ng);
                 std::vector<Cell> fcells((size_t)ng * ncell);
@@ -3611,24 +3700,52 @@ cq_table* run_fast_join(DevCtx& c, cq_node* q, Compiled& C, const cqgpu_table* L
                     Lw->rec_starts = std::move(b);
                 }
                 if (L->gids && L->ngids != Lw->nrec_starts) throw HipError{"routed table: record count differs from its ids"};
+                PHASE("recs");
                 std::vector<unsigned long long> qo;
-                for (const HGroup& h : part->groups)
-                    if (h.first != NOPOS) qo.push_back(h.first >> 32);
+                std::vector<size_t> qat;                 // (direct blob: where each first lives)
+                if (part->direct) {
+                    for (size_t at : part->first_at) {
+                        unsigned long long f;
+                        memcpy(&f, part->gblob.data() + at, 8);
+                        if (f != NOPOS) { qo.push_back(f >> 32); qat.push_back(at); }
+                    }
+                } else {
+                    for (const HGroup& h : part->groups)
+                        if (h.first != NOPOS) qo.push_back(h.first >> 32);
+                }
                 if (!qo.empty()) {
-                    DevBuf dq(qo.size() * 8), dk(qo.size() * 8);
-                    HIPCHECK(hipMemcpyAsync(dq.p, qo.data(), qo.size() * 8, hipMemcpyHostToDevice, c.stream));
-                    HIPCHECK(cq_launch_offset_gid(Lw->rec_starts->as<unsigned long long>(), Lw->nrec_starts,
-                                                  dq.as<unsigned long long>(), (uint32_t)qo.size(), L->gids,
-                                                  dk.as<unsigned long long>(), c.stream));
-                    HIPCHECK(hipMemcpyAsync(qo.data(), dk.p, qo.size() * 8, hipMemcpyDeviceToHost, c.stream));
+                    // (through the pinned staging buffer and the bump scratch: pageable
+                    // copies and fresh device buffers cost more than the lookup itself)
+                    const size_t qb = qo.size() * 8;
+                    Scratch dqk(c, 2 * qb + 64);
+                    unsigned long long* dq = (unsigned long long*)dqk.p;
+                    unsigned long long* dk = dq + qo.size();
+                    unsigned long long* hq = (unsigned long long*)pinned(c, qb);
+                    memcpy(hq, qo.data(), qb);
+                    HIPCHECK(hipMemcpyAsync(dq, hq, qb, hipMemcpyHostToDevice, c.stream));
+                    HIPCHECK(cq_launch_offset_gid(Lw->rec_starts->as<unsigned long long>(), Lw->nrec_starts, dq,
+                                                  (uint32_t)qo.size(), L->gids, dk, c.stream));
+                    HIPCHECK(hipMemcpyAsync(hq, dk, qb, hipMemcpyDeviceToHost, c.stream));
+                    PHASE("gid launch");
                     HIPCHECK(hipStreamSynchronize(c.stream));
-                    size_t k = 0;
-                    for (HGroup& h : part->groups) {
-                        if (h.first == NOPOS) continue;
-                        if (qo[k] >= (1ull << 32)) throw HipError{"fused join partial: left id out of range"};
-                        h.first = qo[k++] << 32;
+                    PHASE("gid sync");
+                    memcpy(qo.data(), hq, qb);
+                    for (unsigned long long g : qo)
+                        if (g >= (1ull << 32)) throw HipError{"fused join partial: left id out of range"};
+                    if (part->direct) {
+                        for (size_t k = 0; k < qo.size(); k++) {
+                            const unsigned long long f = qo[k] << 32;
+                            memcpy(part->gblob.data() + qat[k], &f, 8);
+                        }
+                    } else {
+                        size_t k = 0;
+                        for (HGroup& h : part->groups) {
+                            if (h.first == NOPOS) continue;
+                            h.first = qo[k++] << 32;
+                        }
                     }
                 }
+                PHASE("gids");
                 if (jnames) part->names = *jnames;
                 for (int a = 0; a < MAX_ACC; a++) part->acc_classes[a] = 0;    // SUM only
                 // key classes (bit 1: numbers): every build key is a canonical INTEGER (else the
@@ -3755,8 +3872,9 @@ cq_table* run_join(DevCtx& c, cq_node* q, const cqgpu_table* L, const cqgpu_tabl
     const int nj = q->u.q.join_count;
     if (nj < 1) throw HipError{"run_join without a JOIN"};
     PhaseClock pc;
+    PhaseClock* const outer_phase = g_phase;
     g_phase = &pc;
-    struct Unset { ~Unset() { g_phase = nullptr; } } unset_;
+    struct Unset { PhaseClock* o; ~Unset() { g_phase = o; } } unset_{outer_phase};
     if (nrights < nj) throw Ineligible{"join table not given"};
     // across partials the first level runs on the key-routed sides; a chain's later
     // levels join each rank's joined rows with the whole next table (every joined
@@ -3815,6 +3933,11 @@ cq_table* run_join(DevCtx& c, cq_node* q, const cqgpu_table* L, const cqgpu_tabl
     RowPlan RP;
     if (rows) compile_rows(&J, q, C, RP);
     else compile_aggregate(&J, q, C);
+    if (part && !rows) {
+        part->nacc = C.P.nacc;
+        part->nrep = (uint32_t)C.rep_cols.size();
+        part->nvla = (uint32_t)C.vla.size();
+    }
     if (!rows && nj == 1 && lv[0].keyed && !lv[0].outer_left && !lv[0].outer_right &&
         !(part && getenv("CQ_AMD_NO_PART_FAST_JOIN"))) {
         // (partials: the STAR form only, its groups globalised into *part)
@@ -4270,8 +4393,9 @@ cq_table* query_impl(cq_node* q, cqgpu_table* const* tables, int ntables) {
         return res;
     }
     PhaseClock pc;
+    PhaseClock* const outer_phase = g_phase;
     g_phase = &pc;
-    struct Unset { ~Unset() { g_phase = nullptr; } } unset_;
+    struct Unset { PhaseClock* o; ~Unset() { g_phase = o; } } unset_{outer_phase};
     Compiled C;
     compile_aggregate(t, q, C);
     PHASE("compile");
@@ -5183,8 +5307,12 @@ size_t cqgpu_query_partial(cq_node* q, cqgpu_table* const* tables, int ntables, 
             // repartitioned INNER JOIN: this rank's routed sides (cqgpu_route_* + cqgpu_table_from_routed)
             check_plan_shape(q, t, true);
             if (ntables < 2 || !tables[1]) throw Ineligible{"join table not given"};
+            PhaseClock pc;
+            g_phase = &pc;
+            struct Unset { ~Unset() { g_phase = nullptr; } } unset_;
             JoinPartial jp;
             (void)run_join(c, q, t, tables + 1, ntables - 1, &jp);
+            PHASE("join");
             if (jp.rows) {                           // "CQR1": names, then per row its order key and cells
                 Blob b;
                 b.u32(0x31525143u);
@@ -5204,39 +5332,45 @@ size_t cqgpu_query_partial(cq_node* q, cqgpu_table* const* tables, int ntables, 
                 *blob_out = out;
                 return b.d.size();
             }
-            Compiled C;
-            cqgpu_table J;
-            J.names = jp.names;
-            compile_aggregate(&J, q, C);
+            if (jp.nacc < 0) throw HipError{"join partial: the plan's shape was not recorded"};
+            const int nacc = jp.nacc;
+            const uint32_t nrep = jp.nrep, nvla = jp.nvla;
             Blob b;
+            b.d.reserve(256 + jp.groups.size() * (64 + 48 * (size_t)nacc + 24 * (size_t)nrep));
             b.u32(0x314a5143u);                      // "CQJ1"
             b.u32((uint32_t)jp.names.size());
             for (auto& nm : jp.names) b.str(nm);
-            b.u32((uint32_t)C.P.nacc);
-            for (int a = 0; a < C.P.nacc; a++) b.u32(jp.acc_classes[a]);
-            const uint32_t nrep = (uint32_t)C.rep_cols.size();
+            b.u32((uint32_t)nacc);
+            for (int a = 0; a < nacc; a++) b.u32(jp.acc_classes[a]);
             b.u32(nrep);
-            b.u32((uint32_t)C.vla.size());
+            b.u32(nvla);
             b.u32(jp.lmask);
             b.u32(jp.rmask);
-            b.u64(jp.groups.size());
+            if (jp.direct) {                          // (run_fast_join wrote the groups already)
+                b.u64(jp.ng);
+                b.raw(jp.gblob.data(), jp.gblob.size());
+            } else {
+                b.u64(jp.groups.size());
+            }
             for (const HGroup& h : jp.groups) {
                 b.u32(h.kcls); b.u32(h.klen); b.u64(h.kw0); b.u64(h.kw1); b.str(h.kbytes);
                 b.u64(h.cnt); b.u64(h.first);
-                for (int a = 0; a < C.P.nacc; a++) {
+                for (int a = 0; a < nacc; a++) {
                     b.f64(h.sum[a]); b.u64(h.num[a]); b.u64(h.extpos[a]); b.cell(h.ext[a]);
                 }
                 for (uint32_t r = 0; r < nrep; r++) b.cell(r < h.reps.size() ? h.reps[r] : HCell());
-                for (size_t v = 0; v < C.vla.size(); v++) {
+                for (size_t v = 0; v < nvla; v++) {
                     b.f64(h.vsum[v]); b.f64(h.vm2[v]); b.f64(h.vn[v]);
                     b.mvals(v < h.mvals.size() ? &h.mvals[v] : nullptr);
                 }
                 b.split(h.split);
             }
+            PHASE("serialize");
             void* out = malloc(std::max<size_t>(b.d.size(), 1));
             if (!out) throw HipError{"out of host memory"};
             memcpy(out, b.d.data(), b.d.size());
             *blob_out = out;
+            PHASE("blob");
             return b.d.size();
         }
         check_plan_shape(q, t);
@@ -5721,8 +5855,9 @@ cqgpu_partial* cqgpu_partial_new(cq_node* q, cqgpu_table* const* tables, int nta
     g_err.clear();
     std::unique_ptr<cqgpu_partial> p(new cqgpu_partial);
     PhaseClock pc;
+    PhaseClock* const outer_phase = g_phase;
     g_phase = &pc;
-    struct Unset { ~Unset() { g_phase = nullptr; } } unset_;
+    struct Unset { PhaseClock* o; ~Unset() { g_phase = o; } } unset_{outer_phase};
     try {
         DevCtx& c = ctx();
         bump_reset(c);
@@ -6178,8 +6313,9 @@ cq_table* cqgpu_partial_result(cqgpu_partial* p, cq_node* q) {
     g_inel.clear();
     g_err.clear();
     PhaseClock pc;
+    PhaseClock* const outer_phase = g_phase;
     g_phase = &pc;
-    struct Unset { ~Unset() { g_phase = nullptr; } } unset_;
+    struct Unset { PhaseClock* o; ~Unset() { g_phase = o; } } unset_{outer_phase};
     try {
         if (!p || p->op != COLL_DONE || p->at != p->stages.size()) throw HipError{"partial_result: merge not finished"};
         DevCtx& c = ctx();

@@ -183,12 +183,18 @@ __device__ __forceinline__ void classify32(const v4u a, const v4u b, const CK& k
 #ifndef FAST_OLD_CLS
     if (COMMA) {
         uint32_t us[4], un[4];
+        uint32_t rdp = 0;
 #pragma unroll
         for (int j = 0; j < 8; j++) {
             const uint32_t x = j < 4 ? a[j & 3] : b[j & 3];
             const uint32_t rn = __builtin_amdgcn_perm(k.tn1, k.tn0, x ^ 0x06060606u);
             const uint32_t rd = __builtin_amdgcn_perm(k.td1, k.td0, x ^ 0x2E2E2E2Eu);
-#ifdef FAST_OLD_Q
+#ifndef FAST_NO_Q3
+            // q: the AND of the dwords' rd (a quote is the only byte with bit 7 clear),
+            // two dwords per v_bitop3 (caller: q starts all ones, a quote clears a bit 7)
+            if (j & 1) q = __builtin_amdgcn_bitop3_b32(q, rdp, rd, 0x80);
+            else rdp = rd;
+#elif defined(FAST_OLD_Q)
             q = __builtin_amdgcn_bitop3_b32(rd - 0x01010101u, rd, q, 0xBA);   // (t & ~rd) | q: quotes
 #else
             q = __builtin_amdgcn_bitop3_b32(rd, q, k.m80, 0xCE);                // q | (~rd & 0x80): quotes (rd 0x00)
@@ -303,8 +309,17 @@ struct Num {
     uint32_t M, k;
     bool ok, dot;
 };
+// SWAR constants of the record pass.  A VOP3 instruction cannot take a literal, so
+// LLVM keeps them in SGPRs, and on gfx950 a VALU instruction reading an SGPR issues at
+// half rate; fast_kernel holds them in VGPRs instead (vreg; FAST_NO_VK: literals)
+struct NK {
+    uint32_t k80, k7f, k1e, w4;
+};
+__device__ __forceinline__ NK nk_literals() { return NK{0x80808080u, 0x7F7F7F7Fu, 0x1E1E1E1Eu, 0x010A6400u}; }
+__device__ __forceinline__ uint32_t nzb(uint32_t t, const NK& K) { return (((t & K.k7f) + K.k7f) | t) & K.k80; }
+__device__ __forceinline__ uint32_t ltb(uint32_t x, uint32_t rep_n, const NK& K) { return ~((x | K.k80) - rep_n) & ~x & K.k80; }
 template <bool DOT>
-__device__ __forceinline__ Num num4(uint32_t d, uint32_t len) {
+__device__ __forceinline__ Num num4(uint32_t d, uint32_t len, const NK& K = nk_literals()) {
     Num r;
     // (32 - 8 len) mod 32: LLVM folds it into 24 * len, a full-width v_mul_lo_u32
     uint32_t l8 = len << 3;
@@ -316,7 +331,7 @@ __device__ __forceinline__ Num num4(uint32_t d, uint32_t len) {
     r.dot = false;
     r.k = 0;
     if (DOT) {
-        const uint32_t fd = ~nonzero_bytes(v ^ 0x1E1E1E1Eu) & 0x80808080u & (0xFFFFFFFFu << (sh & 31));   // '.' ^ '0'
+        const uint32_t fd = ~nzb(v ^ K.k1e, K) & K.k80 & (0xFFFFFFFFu << (sh & 31));   // '.' ^ '0'
         const uint32_t low = fd & (0u - fd);
 #ifdef FAST_OLD_NUMK
         const uint32_t below = ((low << 1) - (low != 0 ? 1u : 0u)) & 0x01010100u;
@@ -335,9 +350,9 @@ __device__ __forceinline__ Num num4(uint32_t d, uint32_t len) {
         r.k = (uint32_t)__popc(~t1 & 0x80808080u);
 #endif
     }
-    const bool digits = lt_bytes(v, 0x0A0A0A0Au) == 0x80808080u;
+    const bool digits = ltb(v, 0x0A0A0A0Au, K) == K.k80;
     r.ok = (len - 1u <= 3u) & digits & (!DOT | (len > 1u) | !r.dot);
-    r.M = __builtin_amdgcn_udot4(v, 0x010A6400u, __umul24(v & 0xFFu, 1000u), false);
+    r.M = __builtin_amdgcn_udot4(v, K.w4, __umul24(v & 0xFFu, 1000u), false);
     return r;
 }
 // 1-7 bytes (d0/d1: the field's first 8 bytes, unmasked)
@@ -376,6 +391,7 @@ __device__ __forceinline__ double p10(uint32_t k) {
 
 // 0x80 in every byte < 0x21 (blank, control, NUL) among the f-flagged bytes
 __device__ __forceinline__ uint32_t low_bytes(uint32_t d, uint32_t f) { return lt_bytes(d, 0x21212121u) & f; }
+__device__ __forceinline__ uint32_t low_bytes(uint32_t d, uint32_t f, const NK& K) { return ltb(d, 0x21212121u, K) & f; }
 
 }  // namespace fast
 
@@ -537,6 +553,11 @@ __global__ __launch_bounds__(LT) void fast_kernel(const uint8_t* __restrict__ g,
 #endif
     ck.w0 = vreg(0x08040201u);
     ck.w1 = vreg(0x80402010u);
+#ifndef FAST_NO_VK
+    const NK nk{vreg(0x80808080u), vreg(0x7F7F7F7Fu), vreg(0x1E1E1E1Eu), vreg(0x010A6400u)};
+#else
+    const NK nk = nk_literals();
+#endif
     ck.rd = vreg(fp.delim * 0x01010101u);
     ck.rq = vreg(rep_q);
     const uint64_t first_win = fp.first_win;    // (scalar: the window loads' base)
@@ -649,10 +670,18 @@ __global__ __launch_bounds__(LT) void fast_kernel(const uint8_t* __restrict__ g,
 #pragma unroll
         for (int i = 0; i < 4; i++) la[i] = ((const v4u*)W.bytes)[4 * lane + i];
 #endif
+#ifndef FAST_NO_Q3
+        uint32_t sep0, nl0, sep1, nl1, qf = COMMA ? 0xFFFFFFFFu : 0u;
+#else
         uint32_t sep0, nl0, sep1, nl1, qf = 0;
+#endif
         classify32<COMMA>(la[0], la[1], ck, sep0, nl0, qf);
         classify32<COMMA>(la[2], la[3], ck, sep1, nl1, qf);
+#ifndef FAST_NO_Q3
+        const bool wq = __ballot(((COMMA ? ~qf : qf) & 0x80808080u) != 0) != 0;   // window may hold a quote (uniform)
+#else
         const bool wq = __ballot((qf & 0x80808080u) != 0) != 0;   // window may hold a quote (uniform)
+#endif
         if (wq) {
             W.qt[2 * lane] = quote_bits(la[0], la[1], rep_q);
             W.qt[2 * lane + 1] = quote_bits(la[2], la[3], rep_q);
@@ -823,7 +852,7 @@ __global__ __launch_bounds__(LT) void fast_kernel(const uint8_t* __restrict__ g,
                     const uint32_t a0 = wd[u] & m0, a1 = wd1[u] & m1;
                     const uint32_t c0 = a0 & 0xFFu;
                     const bool ok = (len - 1u < 8u) & !(is_digit(c0) | (c0 == '-') | (c0 == '+') | (c0 == '.')) &
-                                    ((low_bytes(a0, m0 & 0x80808080u) | low_bytes(a1, m1 & 0x80808080u)) == 0);
+                                    ((low_bytes(a0, m0 & nk.k80, nk) | low_bytes(a1, m1 & nk.k80, nk)) == 0);
                     const uint64_t x = ((uint64_t)__builtin_bswap32(a0) << 32) | __builtin_bswap32(a1);
                     const uint64_t ws = fp.wstr;
                     pass[u] = len == 0 ? pass_null : tt_result(wtt, x < ws ? -1 : (x > ws ? 1 : 0));
@@ -834,7 +863,7 @@ __global__ __launch_bounds__(LT) void fast_kernel(const uint8_t* __restrict__ g,
 #pragma unroll
                 for (int u = 0; u < RP; u++) {
                     const uint32_t len = wen[u] - wst[u];
-                    const Num n = num4<false>(wd[u], len);
+                    const Num n = num4<false>(wd[u], len, nk);
                     pass[u] = len == 0 ? pass_null : ((n.M - wa <= ww) != wneg);
                     wu[u] = !n.ok & (len != 0) & !fail[u];
                     wide |= wu[u];
@@ -875,7 +904,7 @@ __global__ __launch_bounds__(LT) void fast_kernel(const uint8_t* __restrict__ g,
 #pragma unroll
                 for (int u = 0; u < RP; u++) {
                     const uint32_t len = sen[u][j] - sst[u][j];
-                    const Num n = num4<true>(sd[u][j], len);
+                    const Num n = num4<true>(sd[u][j], len, nk);
 #ifdef FAST_OLD_NUMK
                     const uint32_t mul = (n.k & 2) ? ((n.k & 1) ? 1u : 10u) : ((n.k & 1) ? 100u : 1000u);
 #else
@@ -927,7 +956,7 @@ __global__ __launch_bounds__(LT) void fast_kernel(const uint8_t* __restrict__ g,
                     const uint32_t klen = gen[u] - gst[u];
                     const uint32_t m0 = len_mask(klen, 0), m1 = len_mask(klen, 1);
                     const uint32_t a0 = k0[u] & m0, a1 = k1[u] & m1;
-                    fail[u] |= (klen > 8u) | ((low_bytes(a0, m0 & 0x80808080u) | low_bytes(a1, m1 & 0x80808080u)) != 0);
+                    fail[u] |= (klen > 8u) | ((low_bytes(a0, m0 & nk.k80, nk) | low_bytes(a1, m1 & nk.k80, nk)) != 0);
                     tag[u] = klen ? ((uint64_t)a0 | ((uint64_t)a1 << 32)) : (1ull << 32);
                     hb[u] = fast_key_hash((uint32_t)tag[u], (uint32_t)(tag[u] >> 32));
                 }
@@ -1488,10 +1517,18 @@ __global__ __launch_bounds__(LT) void jx_extract_kernel(const uint8_t* __restric
         v4u la[4];
 #pragma unroll
         for (int k = 0; k < 4; k++) la[k] = ((const v4u*)W.bytes)[4 * lane + k];
+#ifndef FAST_NO_Q3
+        uint32_t sep0, nl0, sep1, nl1, qf = COMMA ? 0xFFFFFFFFu : 0u;
+#else
         uint32_t sep0, nl0, sep1, nl1, qf = 0;
+#endif
         classify32<COMMA>(la[0], la[1], ck, sep0, nl0, qf);
         classify32<COMMA>(la[2], la[3], ck, sep1, nl1, qf);
+#ifndef FAST_NO_Q3
+        bad = bad || __ballot(((COMMA ? ~qf : qf) & 0x80808080u) != 0) != 0;      // a quote: the general join
+#else
         bad = bad || __ballot((qf & 0x80808080u) != 0) != 0;      // a quote: the general join
+#endif
         const uint64_t nl = (uint64_t)nl0 | ((uint64_t)nl1 << 32);
         const uint32_t prev_top = (uint32_t)__builtin_amdgcn_update_dpp(0, (int)(nl1 >> 31), 0x138, 0xf, 0xf, true);
         const uint32_t pb = prevw >> 24;
