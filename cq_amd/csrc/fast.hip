@@ -1278,6 +1278,7 @@ struct JxOut {
     // kmin + i S.  A table routed by key mod N (route.hip) holds on rank d only keys
     // = d (mod N): dense with stride N.  S = 1: sshift 0, smask 0, sinv 1.
     uint32_t sshift, smask, sinv;
+    uint32_t stride;           // S itself (the build's slot-domain key range back to keys)
     uint16_t* d16;             // build: group id + 1 of key kmin + i S (0: no build record);
                                // probe: | 0x8000 once a probe record met it
     uint32_t* l32;             // build: that record's byte offset
@@ -1509,6 +1510,7 @@ __global__ __launch_bounds__(LT) void jx_extract_kernel(const uint8_t* __restric
     const uint32_t lane_lds = vreg(wlds + (uint32_t)lane * LB);
     bool bad = false;
     unsigned long long kmin = ~0ull, kmax = 0ull;
+    uint32_t smin = ~0u, smax = 0u;          // STAR build: the in-range keys' extreme slots
     uint32_t i = blockIdx.x * NWV + wv;
     if (i < nwin) load_win(g, first_win + i, wsb, wlds, voff, prev_next);
     for (; i < nwin; i += wstep) {
@@ -1567,8 +1569,10 @@ __global__ __launch_bounds__(LT) void jx_extract_kernel(const uint8_t* __restric
         const uint32_t nmine = (uint32_t)__popcll(todo);
         uint32_t at_next = STAR ? 0u : jo.wbase[i] + wave_incl_scan(nmine) - nmine;
         bool issued = false;
-        // STAR build: this lane's first and last key (its records come in file order)
-        unsigned long long lfirst = ~0ull, llast = 0ull;
+        // STAR build: this lane's first and last key (its records come in file order),
+        // as slots: keys map to slots monotonically, and a key outside the range flags
+        // the query for a retry, which discards this round's order anyway
+        uint32_t lfirst = ~0u, llast = 0u;
         bool lany = false, lbad = false;
         while (__any(todo != 0)) {
             uint32_t p[RP], pa[RP], fst[RP][2], fen[RP][2], e[RP];
@@ -1691,13 +1695,20 @@ __global__ __launch_bounds__(LT) void jx_extract_kernel(const uint8_t* __restric
                     const unsigned long long ix = jx_slot(k, jo);
                     if (BUILD) {
                         if (k == JX_NULLKEY) { sflag |= 8u; continue; }
-                        kmin = k < kmin ? k : kmin;
-                        kmax = k > kmax ? k : kmax;
-                        lbad = lbad || (lany && k <= llast);
-                        lfirst = lany ? lfirst : k;
-                        llast = k;
+                        if (ix >= jo.range) {                   // (rare: the retry's range)
+                            kmin = k < kmin ? k : kmin;
+                            kmax = k > kmax ? k : kmax;
+                            sflag |= 16u;
+                            continue;
+                        }
+                        // the in-range keys' extremes and order in 32-bit slots
+                        const uint32_t x32 = (uint32_t)ix;
+                        smin = x32 < smin ? x32 : smin;
+                        smax = x32 > smax ? x32 : smax;
+                        lbad = lbad || (lany && x32 <= llast);
+                        lfirst = lany ? lfirst : x32;
+                        llast = x32;
                         lany = true;
-                        if (ix >= jo.range) { sflag |= 16u; continue; }
                         bool full = false;
                         uint32_t gid = 0;
 #ifndef JX_AB_NOTAG
@@ -1788,10 +1799,10 @@ __global__ __launch_bounds__(LT) void jx_extract_kernel(const uint8_t* __restric
             // order check between windows (an empty window: not checked, not rising)
             const uint64_t am = __ballot(lany);
             const uint64_t above = lane < 63 ? am >> (lane + 1) : 0ull;
-            const unsigned long long nfirst = __shfl(lfirst, above ? (int)(lane + 1 + __builtin_ctzll(above)) : lane, 64);
+            const uint32_t nfirst = (uint32_t)__shfl((int)lfirst, above ? (int)(lane + 1 + __builtin_ctzll(above)) : lane, 64);
             lbad = lbad || (lany && above && llast >= nfirst);
-            const unsigned long long wf = __shfl(lfirst, am ? __builtin_ctzll(am) : 0, 64);
-            const unsigned long long wl = __shfl(llast, am ? 63 - __builtin_clzll(am) : 0, 64);
+            const unsigned long long wf = (uint32_t)__shfl((int)lfirst, am ? __builtin_ctzll(am) : 0, 64);
+            const unsigned long long wl = (uint32_t)__shfl((int)llast, am ? 63 - __builtin_clzll(am) : 0, 64);
             if (lane == 0) {
                 jo.wfl[2 * (uint64_t)i] = am ? wf : ~0ull;
                 jo.wfl[2 * (uint64_t)i + 1] = am ? wl : 0ull;
@@ -1827,6 +1838,14 @@ __global__ __launch_bounds__(LT) void jx_extract_kernel(const uint8_t* __restric
             }
         }
         return;
+    }
+    if constexpr (STAR && BUILD) {            // slots back to keys: kmin + slot * S
+        if (smin != ~0u) {
+            const unsigned long long a = jo.kmin + (unsigned long long)smin * jo.stride;
+            const unsigned long long b = jo.kmin + (unsigned long long)smax * jo.stride;
+            kmin = a < kmin ? a : kmin;
+            kmax = b > kmax ? b : kmax;
+        }
     }
     for (int o = 32; o > 0; o >>= 1) {
         const unsigned long long a = __shfl_down(kmin, o, 64), b = __shfl_down(kmax, o, 64);
@@ -2683,6 +2702,7 @@ hipError_t cq_jx_star_extract(const uint8_t* g, uint64_t lo, uint64_t hi, uint32
     if (stride == 0 || (unsigned long long)stride * range >= (1ull << 32)) return hipErrorInvalidValue;
     jo.sshift = (uint32_t)__builtin_ctz(stride);
     jo.smask = (1u << jo.sshift) - 1u;
+    jo.stride = stride;
     {
         const uint32_t m = stride >> jo.sshift;     // odd: Newton's iteration for m^-1 mod 2^32
         uint32_t inv = m;                           // (correct to 3 bits; each step doubles them)
