@@ -514,7 +514,8 @@ def config5_leg(args, cq_amd, L):
     try:
         with open(os.path.join(ROOT, "profiles", "config5_traffic.json")) as fh:
             tj = json.load(fh)
-        if tj.get("rows_total") == n * N and tj.get("ranks") == N:
+        # (the routed bytes pin the shape: the route's field projection changes them)
+        if tj.get("rows_total") == n * N and tj.get("ranks") == N and tj.get("rank_bytes") == r["bytes"]:
             traffic = tj.get("hbm_bytes_per_step")
     except Exception:
         pass

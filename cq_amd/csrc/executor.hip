@@ -244,6 +244,10 @@ hipError_t cq_sort_dest(void* temp, size_t* temp_bytes, const unsigned int* kin,
 hipError_t cq_launch_iota_u64(uint32_t n, unsigned long long* out, hipStream_t s);
 hipError_t cq_launch_gather_len(const uint32_t* len, const uint32_t* order, uint32_t n, unsigned long long* out,
                                 hipStream_t s);
+hipError_t cq_launch_route_project(const uint8_t* g, const unsigned long long* recs, uint32_t n, uint64_t end,
+                                   uint64_t mask, uint32_t last_keep, uint32_t delim, uint32_t quote,
+                                   const unsigned long long* codes, const uint32_t* cls, uint32_t nranks, uint32_t* len,
+                                   uint32_t* dest, uint8_t* proj, hipStream_t s);
 hipError_t cq_launch_route_copy(const uint8_t* g, const unsigned long long* recs, const uint32_t* order,
                                 const uint32_t* len, const unsigned long long* off, uint32_t n, uint64_t gid_base,
                                 uint8_t* out, unsigned long long* gids, hipStream_t s);
@@ -543,8 +547,11 @@ std::string rtrim(std::string s) {
 // join-key repartition state of a shard between cqgpu_route_plan and cqgpu_route_fill
 struct RouteState {
     DevBuf recs, order, len, off;
+    DevBuf proj;                   // the projected records at their source offsets (keep != ~0)
     uint32_t n = 0;
     uint64_t bytes = 0;
+    uint64_t keep = ~0ull;         // columns sent (route_keep_mask; ~0: whole records)
+    uint32_t last_keep = ~0u;
 };
 
 constexpr uint64_t SAMPLE_BYTES = 256u << 10;   // bytes a table keeps for plan-time sampling
@@ -3670,9 +3677,11 @@ cq_table* run_fast_join(DevCtx& c, cq_node* q, Compiled& C, const cqgpu_table* L
                 // (two records per lane pass here, whatever the record length: the partition
                 // append holds more state per record, and the three-record build measured
                 // 0.92 vs 0.72 ms on config 5's 33-byte orders, same box)
+                const char* prp = getenv("CQGPU_PART_RP");
+                const int rpp = prp ? (atoi(prp) == 3 ? 3 : 2) : 2;
                 HIPCHECK(cq_jx_star_extract(R->g, R->data_begin, R->n, 3968u, d, dq, kr, vcol, 0, kmin, range, (uint32_t)S,
                                             d16, l32.as<uint32_t>(), ttab, gsum, cnts + 1, sflag, nullptr, snotmono,
-                                            nullptr, gminix, 2, xgrid, c.stream, pent.as<unsigned long long>(),
+                                            nullptr, gminix, rpp, xgrid, c.stream, pent.as<unsigned long long>(),
                                             pcnt.as<uint32_t>(), (uint32_t)np64, pcap, PSH));
                 HIPCHECK(cq_jx_part_probe(pent.as<unsigned long long>(), pcnt.as<uint32_t>(), (uint32_t)xgrid,
                                           (uint32_t)np64, pcap, range, d16, snotmono, gsum, gminix, cnts + 1,
@@ -3870,6 +3879,81 @@ cq_table* run_fast_join(DevCtx& c, cq_node* q, Compiled& C, const cqgpu_table* L
 // Every level runs on the device; between levels only the columns later levels,
 // the WHERE, the groups and the SELECT read are gathered into a cell table of the
 // joined rows (NULL cells for an outer join's missing side).
+// The columns of join side `side` (0: FROM, 1: the first JOIN's table) that a
+// repartitioned join reads -- the first level's needs as run_join plans them
+// (ON keys, and every column the WHERE, SELECT, GROUP BY, aggregates, HAVING /
+// ORDER BY and the chain's later levels read) -- as route.hip's keep mask: bit c
+// for column c, bit 63 for every column from 63 on.  ~0 (whole records): a plan
+// this cannot plan (the route or the join itself then reports it), CQGPU_NO_ROUTE_PROJECT.
+uint64_t route_keep_mask(cq_node* q, cqgpu_table* const* tables, int ntables, int side, uint32_t* last_keep) {
+    *last_keep = ~0u;
+    if (getenv("CQGPU_NO_ROUTE_PROJECT")) return ~0ull;
+    try {
+        const int nj = q->u.q.join_count;
+        if (nj < 1 || ntables < nj + 1) return ~0ull;
+        std::vector<std::string> wnames = tables[0]->names;
+        std::string wa = (q->u.q.from && q->u.q.from->u.from.alias) ? q->u.q.from->u.from.alias : "main";
+        std::vector<int> nleft(nj), kl(nj, -1), kr(nj, -1);
+        for (int j = 0; j < nj; j++) {
+            cq_node* jn = q->u.q.joins[j];
+            const cqgpu_table* R = tables[j + 1];
+            if (!jn || jn->kind != CQ_N_JOIN || !R) return ~0ull;
+            const std::string ra = jn->u.join.alias ? jn->u.join.alias : "right";
+            cqgpu_table W;
+            W.names = wnames;
+            cq_node* on = jn->u.join.on;
+            if (on && on->kind == CQ_N_CONDITION && on->u.bin.op && !strcmp(on->u.bin.op, "=") && on->u.bin.lhs &&
+                on->u.bin.rhs && on->u.bin.lhs->kind == CQ_N_IDENTIFIER && on->u.bin.rhs->kind == CQ_N_IDENTIFIER) {
+                kl[j] = join_on_index(on->u.bin.lhs->u.text, &W, &W, wa.c_str(), R, ra.c_str());
+                kr[j] = join_on_index(on->u.bin.rhs->u.text, R, &W, wa.c_str(), R, ra.c_str());
+            }
+            nleft[j] = (int)wnames.size();
+            std::vector<std::string> nn;
+            for (auto& nm : wnames) nn.push_back(wa + "." + nm);
+            for (auto& nm : R->names) nn.push_back(ra + "." + nm);
+            wnames.swap(nn);
+            wa = "joined";
+        }
+        cqgpu_table J;
+        J.cfg = tables[0]->cfg;
+        J.names = wnames;
+        Compiled C;
+        RowPlan RP;
+        if (is_row_query(q)) compile_rows(&J, q, C, RP);
+        else compile_aggregate(&J, q, C);
+        std::set<int> cur(C.need_cols.begin(), C.need_cols.end());
+        cur.insert(C.rep_cols.begin(), C.rep_cols.end());
+        for (auto& v : C.vla) cur.insert(v.second);
+        cur.insert(RP.cols.begin(), RP.cols.end());
+        std::set<int> lneed, rneed;
+        for (int j = nj - 1; j >= 0; j--) {
+            lneed.clear();
+            rneed.clear();
+            for (int f : cur) {
+                if (f < nleft[j]) lneed.insert(f);
+                else rneed.insert(f - nleft[j]);
+            }
+            if (kl[j] >= 0 && kr[j] >= 0) { lneed.insert(kl[j]); rneed.insert(kr[j]); }
+            cur = lneed;
+        }
+        const std::set<int>& need = side == 0 ? lneed : rneed;
+        const int ncols = (int)tables[side]->names.size();
+        if (need.empty() || (int)need.size() >= ncols) return ~0ull;
+        uint64_t m = 0;
+        int last = 0;
+        for (int f : need) {
+            if (f < 0) return ~0ull;
+            m |= 1ull << (f < 63 ? f : 63);
+            last = std::max(last, f);
+        }
+        *last_keep = (m >> 63) ? ~0u : (uint32_t)last;
+        return m;
+    } catch (...) {
+        *last_keep = ~0u;
+        return ~0ull;
+    }
+}
+
 cq_table* run_join(DevCtx& c, cq_node* q, const cqgpu_table* L, const cqgpu_table* const* rights, int nrights,
                    JoinPartial* part = nullptr) {
     const int nj = q->u.q.join_count;
@@ -4734,6 +4818,7 @@ int cqgpu_route_plan(cq_node* q, cqgpu_table* const* tables, int ntables, int si
         std::swap(st->recs.p, S.recs.p);
         const uint32_t n = S.n;
         st->n = n;
+        st->keep = route_keep_mask(q, tables, ntables, side, &st->last_keep);
         std::vector<unsigned long long> per(2 * (size_t)nranks, 0);
         if (n) {
             DevBuf codes((size_t)n * 8), cls((size_t)n * 4), dest((size_t)n * 4), dsorted((size_t)n * 4),
@@ -4741,9 +4826,19 @@ int cqgpu_route_plan(cq_node* q, cqgpu_table* const* tables, int ntables, int si
                 off((size_t)n * 8), dst((2 * (size_t)nranks + 2) * 8);
             HIPCHECK(cq_launch_join_code(S.cells.as<Cell>(), 1, 0, n, codes.as<unsigned long long>(), cls.as<uint32_t>(),
                                          idx.as<uint32_t>(), nullptr, c.stream));
-            HIPCHECK(cq_launch_route_len(t->g, st->recs.as<unsigned long long>(), n, codes.as<unsigned long long>(),
-                                         cls.as<uint32_t>(), (uint32_t)nranks, len.as<uint32_t>(), dest.as<uint32_t>(),
-                                         c.stream));
+            if (st->keep != ~0ull) {
+                DevBuf proj(t->n + 64);
+                HIPCHECK(cq_launch_route_project(t->g, st->recs.as<unsigned long long>(), n, t->n, st->keep,
+                                                 st->last_keep, (uint8_t)t->cfg.delimiter, (uint8_t)t->cfg.quote,
+                                                 codes.as<unsigned long long>(), cls.as<uint32_t>(), (uint32_t)nranks,
+                                                 len.as<uint32_t>(), dest.as<uint32_t>(), proj.as<uint8_t>(),
+                                                 c.stream));
+                std::swap(st->proj.p, proj.p);
+            } else {
+                HIPCHECK(cq_launch_route_len(t->g, st->recs.as<unsigned long long>(), n, codes.as<unsigned long long>(),
+                                             cls.as<uint32_t>(), (uint32_t)nranks, len.as<uint32_t>(),
+                                             dest.as<uint32_t>(), c.stream));
+            }
             int bits = 1;
             while ((1 << bits) < nranks) bits++;
             size_t tb = 0;
@@ -4807,7 +4902,8 @@ int cqgpu_route_fill(cqgpu_table* t, uint64_t gid_base, void* dev_bytes, uint64_
         if (gid_base + st.n >= (1ull << 32)) throw HipError{"route: 2^32 - 1 or more records on a join side"};
         if (st.n) {
             if (!dev_bytes || !dev_gids) throw HipError{"route_fill: null output buffer"};
-            HIPCHECK(cq_launch_route_copy(t->g, st.recs.as<unsigned long long>(), st.order.as<uint32_t>(),
+            HIPCHECK(cq_launch_route_copy(st.keep != ~0ull ? st.proj.as<uint8_t>() : t->g,
+                                          st.recs.as<unsigned long long>(), st.order.as<uint32_t>(),
                                           st.len.as<uint32_t>(), st.off.as<unsigned long long>(), st.n, gid_base,
                                           (uint8_t*)dev_bytes, (unsigned long long*)dev_gids, c.stream));
             HIPCHECK(hipStreamSynchronize(c.stream));
@@ -5777,11 +5873,11 @@ uint64_t text_hash(const uint8_t* b, uint32_t n, uint64_t seed) {
     return h;
 }
 
-int cell_class(const HCell& x) { return x.kind == K_STR ? 1 : x.kind == K_DATE ? 2 : 0; }
+static int cell_class(const HCell& x) { return x.kind == K_STR ? 1 : x.kind == K_DATE ? 2 : 0; }
 
 // per-class state of MIN/MAX accumulator a (HGroup::split, or the one class a
 // single-class partial saw, whose extreme position stands in for its first)
-HGroup::ClassSplit class_split(const HGroup& h, int a) {
+static HGroup::ClassSplit class_split(const HGroup& h, int a) {
     for (const auto& cs : h.split)
         if (cs.acc == a) return cs;
     HGroup::ClassSplit cs;

@@ -11,10 +11,14 @@
 //
 // The send buffer is the records themselves (bytes up to the terminator, one
 // '\n' appended), grouped by destination and in file order within a destination,
-// plus one u64 global record id per record.  Concatenated in source-rank order the
+// plus one u64 global record id per record.  With a keep mask (the columns the plan
+// reads from this side, executor.hip route_keep_mask) every other field is sent
+// empty -- its delimiter stays, so every kept field keeps its column -- and the
+// record ends after its last kept field: an empty or missing field is NULL, and the
+// plan never reads those columns.  Concatenated in source-rank order the
 // received records are a file-ordered subsequence of the whole input, so the local
 // join's (l, r) nested-loop order is the global one restricted to this rank.
-// Work is byte copying: HBM-bound, no LDS, no MFMA.
+// Work is byte copying: HBM-bound, no MFMA (LDS only to stage the projection).
 #include <hip/hip_runtime.h>
 
 #include <stdint.h>
@@ -38,6 +42,60 @@ __device__ __forceinline__ uint32_t route_dest(uint64_t code, uint32_t cls, uint
     if (cls == 1u && v >= 0.0 && v < 9007199254740992.0 && v == __builtin_floor(v))
         return (uint32_t)((uint64_t)v % nranks);
     return (uint32_t)(mix64(code ^ ((uint64_t)cls << 62)) % nranks);
+}
+
+__device__ __forceinline__ bool r_nl(uint32_t c) { return c == '\n' || c == '\r'; }
+__device__ __forceinline__ bool r_blank(uint32_t c) { return c == ' ' || c == '\t'; }
+
+// The record at p with only the fields of `mask` (bit c: column c; columns from 63 on
+// follow bit 63) and the delimiters before the last kept one; returns its length
+// with the closing '\n'; WRITE: into out (out == p allowed: bytes only move
+// forward).  Field ends as parse_line finds them (csv_reader.c:278-338, scan.hip
+// g_field): a quoted field runs to its closing quote (a doubled quote inside), then
+// to the delimiter; a field's raw bytes (blanks, quotes) are copied as they are, so
+// the receiver's parser reads the same values.
+template <bool WRITE>
+__device__ uint32_t project_record(const uint8_t* p, uint64_t mask, uint32_t last_keep, uint32_t delim,
+                                   uint32_t quote, uint8_t* out) {
+    uint32_t i = 0, o = 0;
+    for (uint32_t col = 0;; col++) {
+        const uint32_t s = i;
+        uint32_t c = p[i];
+        while (r_blank(c)) c = p[++i];
+        if (!r_nl(c)) {
+            if (c == quote) {
+                i++;
+                for (;;) {
+                    c = p[i];
+                    if (r_nl(c)) break;
+                    if (c == quote) {
+                        if (p[i + 1] == quote) { i += 2; continue; }
+                        i++;
+                        break;
+                    }
+                    i++;
+                }
+            }
+            c = p[i];
+            while (c != delim && !r_nl(c)) c = p[++i];
+        }
+        const bool keep = (mask >> (col < 63 ? col : 63)) & 1;
+        if (keep) {
+            if (WRITE)
+                for (uint32_t k = s; k < i; k++) out[o + k - s] = p[k];
+            o += i - s;
+        }
+        if (p[i] != delim || col >= last_keep) break;     // the record ends / nothing kept after
+        if (WRITE) out[o] = (uint8_t)delim;
+        o++;
+        i++;
+    }
+    if (o == 0) {                                          // all kept fields empty: a lone delimiter
+        if (WRITE) out[0] = (uint8_t)delim;                // keeps the record a record (an empty
+        o = 1;                                             // line is none), its fields NULL
+    }
+    if (WRITE) out[o] = '\n';
+    return o + 1;
 }
 
 // record length (through the terminator, which becomes '\n') and destination rank
@@ -74,6 +132,58 @@ __global__ void route_len_kernel(const uint8_t* __restrict__ g, const unsigned l
     }
     len[i] = (uint32_t)(pos - st) + 1;
     dest[i] = route_dest(codes[i], cls[i], nranks);
+}
+
+// The projected records (a keep mask: project_record), each written over its own
+// source position in `proj` (a projected record is never longer than the record, so
+// route_copy_kernel then moves them like whole records), their lengths and
+// destination ranks (route_len_kernel's job for whole records).  One wave per 64 consecutive records: their byte span (up to the
+// next record's start; `end` = the byte count, the padding '\n' ends the last) is
+// staged in LDS with 16-byte loads, each lane projects its record in place there
+// (forward: every byte is written at or before the byte it came from) and the wave
+// stores the span back with 16-byte stores (the edge chunks, shared with the
+// neighbouring waves' spans, byte by byte within the span).  A span over RP_CAP
+// bytes (long records) is projected from global memory by each lane directly.
+constexpr uint32_t RP_CAP = 4096;
+__global__ __launch_bounds__(256) void route_project_kernel(const uint8_t* __restrict__ g,
+                                                            const unsigned long long* __restrict__ recs, uint32_t n,
+                                                            uint64_t end, uint64_t mask, uint32_t last_keep,
+                                                            uint32_t delim, uint32_t quote,
+                                                            const unsigned long long* __restrict__ codes,
+                                                            const uint32_t* __restrict__ cls, uint32_t nranks,
+                                                            uint32_t* __restrict__ len, uint32_t* __restrict__ dest,
+                                                            uint8_t* __restrict__ proj) {
+    __shared__ __attribute__((aligned(16))) uint8_t buf[4][RP_CAP];
+    const uint32_t lane = threadIdx.x & 63, w = threadIdx.x >> 6;
+    const uint64_t i0 = ((uint64_t)blockIdx.x * 256 + threadIdx.x) & ~63ull;
+    const uint64_t i = i0 + lane;
+    const bool live = i0 < n;
+    uint64_t a = 0, b = 0;
+    if (live) {
+        a = recs[i0] & ~15ull;
+        b = ((i0 + 64 < n ? recs[i0 + 64] : end + 1) + 15) & ~15ull;
+    }
+    const bool fits = live && b - a <= RP_CAP;
+    uint8_t* L = buf[w];
+    if (fits)
+        for (uint64_t q = a + lane * 16; q < b; q += 64 * 16) *(uint4*)(L + (q - a)) = *(const uint4*)(g + q);
+    __syncthreads();
+    if (i < n) {
+        const uint64_t st = recs[i];
+        const uint32_t m = fits ? project_record<true>(L + (st - a), mask, last_keep, delim, quote, L + (st - a))
+                                : project_record<true>(g + st, mask, last_keep, delim, quote, proj + st);
+        len[i] = m;
+        dest[i] = route_dest(codes[i], cls[i], nranks);
+    }
+    __syncthreads();
+    if (fits) {                                            // only [S, E): the edge chunks are shared
+        const uint64_t S = recs[i0], E = i0 + 64 < n ? recs[i0 + 64] : end + 1;
+        for (uint64_t q = a + lane * 16; q < b; q += 64 * 16) {
+            if (q >= S && q + 16 <= E) *(uint4*)(proj + q) = *(const uint4*)(L + (q - a));
+            else
+                for (uint64_t k = q < S ? S : q; k < q + 16 && k < E; k++) proj[k] = L[k - a];
+        }
+    }
 }
 
 // per-destination record and byte starts from the destination-sorted layout
@@ -318,6 +428,16 @@ hipError_t cq_launch_gather_len(const uint32_t* len, const uint32_t* order, uint
                                 hipStream_t s) {
     if (!n) return hipSuccess;
     gather_len_kernel<<<blocks(n, 256), 256, 0, s>>>(len, order, n, out);
+    return hipGetLastError();
+}
+
+hipError_t cq_launch_route_project(const uint8_t* g, const unsigned long long* recs, uint32_t n, uint64_t end,
+                                   uint64_t mask, uint32_t last_keep, uint32_t delim, uint32_t quote,
+                                   const unsigned long long* codes, const uint32_t* cls, uint32_t nranks, uint32_t* len,
+                                   uint32_t* dest, uint8_t* proj, hipStream_t s) {
+    if (!n) return hipSuccess;
+    route_project_kernel<<<blocks(n, 256), 256, 0, s>>>(g, recs, n, end, mask, last_keep, delim, quote, codes, cls,
+                                                        nranks, len, dest, proj);
     return hipGetLastError();
 }
 

@@ -17,6 +17,7 @@ ap.add_argument("out")
 ap.add_argument("--traffic", default=None)
 ap.add_argument("--rows-total", type=int, default=500_000_000)
 ap.add_argument("--ranks", type=int, default=8)
+ap.add_argument("--rank-bytes", type=int, default=None, help="rank 0's routed bytes (bench config5 rank_bytes)")
 a = ap.parse_args()
 res = collections.defaultdict(lambda: collections.defaultdict(list))
 for f in glob.glob(os.path.join(a.src, "**", "*counter_collection.csv"), recursive=True):
@@ -44,5 +45,5 @@ doc = {"source": a.src, "kernels": out, "hbm_bytes_per_step": step,
 json.dump(doc, open(a.out, "w"), indent=1)
 print(json.dumps({k: round(v.get("hbm_bytes_per_launch", 0) / 1e9, 3) for k, v in out.items()}), "step GB", step / 1e9)
 if a.traffic:
-    json.dump({"rows_total": a.rows_total, "ranks": a.ranks, "hbm_bytes_per_step": step,
-               "source": a.out}, open(a.traffic, "w"), indent=1)
+    json.dump({"rows_total": a.rows_total, "ranks": a.ranks, "rank_bytes": a.rank_bytes,
+               "hbm_bytes_per_step": step, "source": a.out}, open(a.traffic, "w"), indent=1)

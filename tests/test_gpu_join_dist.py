@@ -9,6 +9,8 @@ cqgpu_merge_partials must reproduce the oracle's nested-loop join over the whole
 files (reference evaluator_joins.c:63-181): counts, group set and first-appearance
 order exact, SUM/AVG within 1e-6 relative.
 """
+import re
+
 import numpy as np
 import pytest
 import torch
@@ -389,8 +391,56 @@ def test_mixed_key_classes_refused_empty_side():
         assert "value classes" in cq_amd.last_ineligible(), cq_amd.last_ineligible()
 
 
-def test_route_counts(files):
-    """every record is routed exactly once; bytes = record bytes + one newline each"""
+def _project(rec: bytes, keep, last_keep, delim=b",", quote=b'"'):
+    """the record with only the fields in `keep` and the delimiters up to the last
+    kept one (route.hip project_record); field ends as parse_line finds them
+    (csv_reader.c:278-338): blanks, then a quoted run to its closing quote (doubled
+    quotes inside), then up to the delimiter; raw bytes copied as they are"""
+    d, qt = delim[0], quote[0]
+    out, i, col = bytearray(), 0, 0
+    n = len(rec)
+    at = lambda k: rec[k] if k < n else 10
+    while True:
+        s = i
+        while at(i) in (32, 9):
+            i += 1
+        if at(i) not in (10, 13):
+            if at(i) == qt:
+                i += 1
+                while at(i) not in (10, 13):
+                    if at(i) == qt:
+                        if at(i + 1) == qt:
+                            i += 2
+                            continue
+                        i += 1
+                        break
+                    i += 1
+            while at(i) != d and at(i) not in (10, 13):
+                i += 1
+        if col in keep:
+            out += rec[s:i]
+        if at(i) != d or col >= last_keep:
+            break
+        out.append(d)
+        i += 1
+        col += 1
+    return bytes(out) if out else delim
+
+
+def _routed_records(ast, table, side, nranks, base):
+    nb, nr = cq_amd.route_plan(ast, [table[0], table[1]], side, nranks)
+    sb = torch.empty(max(sum(nb), 1), dtype=torch.uint8, device="cuda")
+    sg = torch.empty(max(sum(nr), 1), dtype=torch.int64, device="cuda")
+    cq_amd.route_fill(table[side], base, sb.data_ptr(), sg.data_ptr())
+    torch.cuda.synchronize()
+    got = bytes(sb.cpu().numpy()[:sum(nb)]).split(b"\n")[:-1]
+    return nb, nr, got, sg.cpu().numpy()[:sum(nr)] - base
+
+
+def test_route_counts(files, monkeypatch):
+    """every record is routed exactly once; bytes = record bytes + one newline each
+    (whole records: projection off)"""
+    monkeypatch.setenv("CQGPU_NO_ROUTE_PROJECT", "1")
     data, _ = files
     body = data["do"].split(b"\n", 1)[1]
     recs = [ln for ln in body.split(b"\n") if ln]
@@ -398,19 +448,74 @@ def test_route_counts(files):
     with cqtest.Parsed(sql) as ast:
         lt = cq_amd.Table.from_bytes(data["du"])
         rt = cq_amd.Table.from_bytes(data["do"])
-        nb, nr = cq_amd.route_plan(ast, [lt, rt], 1, 4)
+        nb, nr, got, gids = _routed_records(ast, (lt, rt), 1, 4, 100)
         assert sum(nr) == len(recs)
         assert sum(nb) == sum(len(r) + 1 for r in recs)
-        sb = torch.empty(sum(nb), dtype=torch.uint8, device="cuda")
-        sg = torch.empty(sum(nr), dtype=torch.int64, device="cuda")
-        cq_amd.route_fill(rt, 100, sb.data_ptr(), sg.data_ptr())
-        torch.cuda.synchronize()
-        got = bytes(sb.cpu().numpy()).split(b"\n")[:-1]
-        gids = sg.cpu().numpy() - 100
         assert sorted(gids.tolist()) == list(range(len(recs)))
         assert [recs[i] for i in gids] == got
         lt.close()
         rt.close()
+
+
+PROJ_LEFT = (b"id,name,age,role,note\n"
+             b"1,ann,30,admin,x\n"
+             b' 2 , "b,o""b" ,41, "ops, east" ,"q\n'      # an unclosed quote runs to the line end
+             b",,,,\n"
+             b"3,c\n"
+             b"  \n"
+             b'4,"d",,  dev  ,"n,1"\n'
+             b"5\r\n"
+             b',"e""",52,"r""1",z,extra,more\n'
+             b"6,f,60,,\n")
+PROJ_RIGHT = b"id,price,quantity,customer_id\n1,2.5,3,1\n2,4.0,1, 2 \n3,,2,\n4,9.5,1,5\n5,1.0,7,6\n"
+
+
+@pytest.mark.parametrize("sql,keep", [
+    ("SELECT u.role, COUNT(*) FROM 'u' AS u JOIN 'o' AS o ON u.id = o.customer_id GROUP BY u.role",
+     ({0, 3}, {3})),
+    ("SELECT COUNT(*) FROM 'u' AS u LEFT JOIN 'o' AS o ON u.id = o.customer_id", ({0}, {3})),
+    ("SELECT u.name, SUM(o.price) FROM 'u' AS u JOIN 'o' AS o ON u.id = o.customer_id "
+     "WHERE u.age > 1 GROUP BY u.name", ({0, 1, 2}, {1, 3})),
+    ("SELECT o.quantity, MAX(u.note) FROM 'u' AS u RIGHT JOIN 'o' AS o ON u.id = o.customer_id "
+     "GROUP BY o.quantity ORDER BY o.quantity", ({0, 4}, {2, 3})),
+])
+def test_route_projection_bytes(sql, keep):
+    """the routed bytes hold each record's needed fields only (route.hip
+    project_record), byte for byte as the field splitter finds them: quoted
+    delimiters, doubled quotes, blanks, short and long rows, CR endings, all-empty
+    records (a lone delimiter: still a record)"""
+    with cqtest.Parsed(sql) as ast:
+        tabs = (cq_amd.Table.from_bytes(PROJ_LEFT), cq_amd.Table.from_bytes(PROJ_RIGHT))
+        try:
+            for side, data in enumerate((PROJ_LEFT, PROJ_RIGHT)):
+                recs = [ln for ln in re.split(rb"\r?\n", data.split(b"\n", 1)[1]) if ln]
+                nb, nr, got, gids = _routed_records(ast, tabs, side, 3, 0)
+                assert sorted(gids.tolist()) == list(range(len(recs))), side
+                want = [_project(recs[i], keep[side], max(keep[side])) for i in gids]
+                assert got == want, (side, got, want)
+                assert sum(nb) == sum(len(r) + 1 for r in want)
+        finally:
+            for t in tabs:
+                t.close()
+
+
+@pytest.mark.parametrize("case", [1, 4, 8, 9, 10, 11, 13, 16, 19, 20])
+def test_route_projection_results(files, case, monkeypatch):
+    """the same partial-merge result with whole records and with projected ones"""
+    data, paths = files
+    lk, rk, tmpl = QUERIES[case]
+    sql = tmpl.replace("{L}", paths[lk]).replace("{R}", paths[rk])
+    with cqtest.Parsed(sql) as ast:
+        res = []
+        for off in (False, True):
+            if off:
+                monkeypatch.setenv("CQGPU_NO_ROUTE_PROJECT", "1")
+            tp = _run(ast, data[lk], data[rk], 3)
+            assert tp, cq_amd.last_error()
+            res.append(abi.table_to_py(tp))
+            cq_amd.result_free(tp)
+        tol = tolerant_columns(ast)
+    compare(res[1], res[0], tol, f"{sql}: projected vs whole records")   # (float sums: summation order)
 
 
 def _dist_worker(rank, world, port, lpath, rpath, sql, q, rest=()):
