@@ -3601,7 +3601,9 @@ cq_table* run_fast_join(DevCtx& c, cq_node* q, Compiled& C, const cqgpu_table* L
             uint64_t kmin = 0, kmax = 0, est = 0;
             const uint64_t S = L->key_stride ? L->key_stride : 1;
             auto it = Lm->key_range.find(kl);
-            const bool learned = it != Lm->key_range.end();
+            // (CQGPU_NO_LEARNED_RANGE: every call as a fresh table's first -- a routed
+            //  table rebuilt per step, as the multi-GPU join does)
+            const bool learned = it != Lm->key_range.end() && !getenv("CQGPU_NO_LEARNED_RANGE");
             if (learned) {
                 kmin = it->second.first;
                 kmax = it->second.second;
@@ -3669,7 +3671,10 @@ cq_table* run_fast_join(DevCtx& c, cq_node* q, Compiled& C, const cqgpu_table* L
             if (pprobe) {
                 const uint64_t rb = R->n > R->data_begin ? R->n - R->data_begin : 0;
                 const uint64_t est_r = (uint64_t)((double)rb / std::max(1.0, sample_record_bytes(R))) + 1;
-                const uint64_t per = est_r / ((uint64_t)xgrid * np64);
+                // (a sampled range is padded past the keys: the probe keys fill the
+                // partitions of about `est` slots, not all np64 of them)
+                const uint64_t np_eff = std::max<uint64_t>(1, std::min<uint64_t>(range, est) >> PSH);
+                const uint64_t per = est_r / ((uint64_t)xgrid * std::min<uint64_t>(np64, np_eff));
                 const uint32_t pcap = (uint32_t)std::min<uint64_t>(per + per / 4 + 256, 1u << 30);
                 DevBuf a((size_t)xgrid * np64 * pcap * 8), b((size_t)xgrid * np64 * 4);
                 std::swap(pent.p, a.p);
