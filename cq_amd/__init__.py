@@ -80,6 +80,13 @@ def lib():
                                        C.POINTER(C.c_uint64), C.POINTER(C.c_uint64)]
         L.cqgpu_route_fill.restype = C.c_int
         L.cqgpu_route_fill.argtypes = [C.c_void_p, C.c_uint64, C.c_void_p, C.c_void_p]
+        L.cqgpu_join_outer_matched.restype = C.c_int
+        L.cqgpu_join_outer_matched.argtypes = [C.POINTER(abi.Node), C.POINTER(C.c_void_p), C.c_int, C.c_int,
+                                               C.POINTER(C.POINTER(C.c_uint8)), C.POINTER(C.c_uint64)]
+        L.cqgpu_join_outer_set.restype = C.c_int
+        L.cqgpu_join_outer_set.argtypes = [C.c_int, C.c_void_p, C.c_uint64, C.c_int]
+        L.cqgpu_join_outer_clear.restype = None
+        L.cqgpu_join_outer_clear.argtypes = []
         L.cqgpu_table_set_record_total.restype = C.c_int
         L.cqgpu_table_set_record_total.argtypes = [C.c_void_p, C.c_uint64]
         L.cqgpu_table_set_key_stride.restype = C.c_int
@@ -224,6 +231,33 @@ def query_partial(ast, tables) -> bytes:
         return C.string_at(blob, size)
     finally:
         C.CDLL(None).free(blob)
+
+
+def join_outer_matched(ast, tables, level: int) -> bytes | None:
+    """This rank's matched flags over a chain's later RIGHT / FULL level's records
+    (cqgpu_join_outer_matched, one byte per record); None when the level needs no
+    global set."""
+    arr, n = _tables_arg(tables)
+    fl = C.POINTER(C.c_uint8)()
+    nrec = C.c_uint64(0)
+    r = lib().cqgpu_join_outer_matched(ast, arr, n, level, C.byref(fl), C.byref(nrec))
+    if r < 0:
+        raise RuntimeError(last_error() or "cqgpu_join_outer_matched failed")
+    if r == 0:
+        return None
+    return C.string_at(fl, nrec.value) if nrec.value else b""
+
+
+def join_outer_set(level: int, matched: bytes, emit: bool) -> None:
+    """The ranks' OR of join_outer_matched for `level` (cqgpu_join_outer_set); emit on
+    exactly one rank."""
+    buf = C.create_string_buffer(bytes(matched), max(len(matched), 1))
+    if lib().cqgpu_join_outer_set(level, buf, len(matched), 1 if emit else 0) != 0:
+        raise RuntimeError(last_error() or "cqgpu_join_outer_set failed")
+
+
+def join_outer_clear() -> None:
+    lib().cqgpu_join_outer_clear()
 
 
 def route_plan(ast, tables, side: int, nranks: int) -> tuple[list[int], list[int]]:

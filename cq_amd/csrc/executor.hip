@@ -102,6 +102,8 @@ hipError_t cq_launch_join_count(const cq::Cell* L, uint32_t ls, uint32_t lk, uin
 hipError_t cq_launch_join_emit(const cq::Cell* L, uint32_t ls, uint32_t lk, uint32_t nL, const cq::JoinRight* J,
                                const uint32_t* lo, const unsigned long long* cnt, const unsigned long long* offs,
                                uint2* pairs, unsigned int* rmatched, hipStream_t s);
+hipError_t cq_launch_outer_global(unsigned int* unm, uint32_t n, const uint8_t* gset, uint32_t emit, uint8_t* matched_out,
+                                  hipStream_t s);
 hipError_t cq_launch_join_fill(const unsigned int* flags, const unsigned int* pos, uint32_t n, unsigned long long base,
                                int right_side, uint2* pairs, hipStream_t s);
 hipError_t cq_launch_join_gather(const uint2* pairs, unsigned long long np, const cq::JoinMap* M, const cq::Cell* L,
@@ -2991,8 +2993,24 @@ struct JoinPartial {
     uint64_t ng = 0;
     std::vector<uint8_t> gblob;
     std::vector<size_t> first_at;
+    // cqgpu_join_outer_matched: run the chain up to this level, keep its right side's
+    // locally matched records (one byte each) and stop
+    int probe_level = -1;
+    std::vector<uint8_t> probe_out;
     ~JoinPartial() { if (rows) cqgpu_result_free(rows); }
 };
+
+// A chain's later RIGHT / FULL level across partials (perform_join's unmatched right
+// rows, evaluator_joins.c:143-171, chained through process_joins :268-270): the
+// level's table is whole on every rank, and its unmatched records are the ones no
+// rank's joined rows matched.  Per level: the OR over the ranks of their matched
+// flags (cqgpu_join_outer_set), and whether this rank's partial carries the
+// unmatched records (exactly one rank does).
+struct OuterSet {
+    std::vector<uint8_t> matched;
+    bool emit = false;
+};
+std::map<int, OuterSet> g_outer_sets;
 
 // global record ids of a join side: the routed ids, or the local row index
 void side_gids(DevCtx& c, const cqgpu_table* t, uint32_t n, DevBuf& own, const unsigned long long** out) {
@@ -3142,9 +3160,14 @@ uint32_t key_class_mask(DevCtx& c, const JoinSide& S, int kcol) {
 // rows ascending; LEFT / FULL put an unmatched left row (l, -) in its place,
 // RIGHT / FULL append the unmatched right rows (-, r) in row order.  kl / kr:
 // the ON operands' columns of A / B (keyed: both resolved).
+// gset (device, one byte per right record; with outer_right): the records some rank
+// matched -- the unmatched rows appended are the others, and only when gemit;
+// matched_out (device, with outer_right): this call's matched flags of the right side
 unsigned long long build_pairs(DevCtx& c, JoinSide& A, JoinSide& B, int kl, int kr, bool keyed, bool outer_left,
-                               bool outer_right, DevBuf& pairs, bool cross = false) {
+                               bool outer_right, DevBuf& pairs, bool cross = false, const uint8_t* gset = nullptr,
+                               bool gemit = true, uint8_t* matched_out = nullptr) {
     unsigned long long np = 0;
+    const bool global_right = outer_right && (gset || matched_out);
     if (cross && A.n && B.n) {
         // JOIN without ON: evaluate_join_condition is true for a NULL condition
         // (evaluator_joins.c:42), so every (l, r) pair matches, in the nested loops'
@@ -3154,6 +3177,7 @@ unsigned long long build_pairs(DevCtx& c, JoinSide& A, JoinSide& B, int kl, int 
         DevBuf pb(np * 8);
         std::swap(pairs.p, pb.p);
         HIPCHECK(cq_launch_join_cross(A.n, B.n, pairs.as<uint2>(), c.stream));
+        if (matched_out) HIPCHECK(hipMemsetAsync(matched_out, 1, B.n, c.stream));
         return np;
     }
     if (keyed && A.n && B.n) {
@@ -3240,6 +3264,8 @@ unsigned long long build_pairs(DevCtx& c, JoinSide& A, JoinSide& B, int kl, int 
                                      cnt.as<unsigned long long>(), offs.as<unsigned long long>(), pairs.as<uint2>(),
                                      outer_right ? unm.as<unsigned int>() : nullptr, c.stream));
         np = nleft;
+        if (global_right)
+            HIPCHECK(cq_launch_outer_global(unm.as<unsigned int>(), B.n, gset, gemit ? 1u : 0u, matched_out, c.stream));
         if (outer_right) {
             size_t tb3 = 0;
             HIPCHECK(cq_excl_sum_u32(nullptr, &tb3, unm.as<unsigned int>(), upos.as<unsigned int>(), B.n, c.stream));
@@ -3254,6 +3280,30 @@ unsigned long long build_pairs(DevCtx& c, JoinSide& A, JoinSide& B, int kl, int 
             np += (unsigned long long)ul[0] + ul[1];
         }
         HIPCHECK(hipStreamSynchronize(c.stream));        // before the scratch buffers of this block are freed
+    }
+    else if (global_right && B.n) {
+        // nothing matches on this rank: the left rows (LEFT / FULL) NULL-padded, then
+        // the right records no rank matched (on the emitting rank)
+        const unsigned long long nl2 = outer_left ? A.n : 0;
+        DevBuf unm((size_t)B.n * 4), upos((size_t)B.n * 4);
+        HIPCHECK(hipMemsetD32Async((hipDeviceptr_t)unm.p, 1u, B.n, c.stream));
+        HIPCHECK(cq_launch_outer_global(unm.as<unsigned int>(), B.n, gset, gemit ? 1u : 0u, matched_out, c.stream));
+        size_t tb3 = 0;
+        HIPCHECK(cq_excl_sum_u32(nullptr, &tb3, unm.as<unsigned int>(), upos.as<unsigned int>(), B.n, c.stream));
+        DevBuf temp3(tb3);
+        HIPCHECK(cq_excl_sum_u32(temp3.p, &tb3, unm.as<unsigned int>(), upos.as<unsigned int>(), B.n, c.stream));
+        unsigned int ul[2] = {0, 0};
+        HIPCHECK(hipMemcpyAsync(&ul[0], upos.as<unsigned int>() + B.n - 1, 4, hipMemcpyDeviceToHost, c.stream));
+        HIPCHECK(hipMemcpyAsync(&ul[1], unm.as<unsigned int>() + B.n - 1, 4, hipMemcpyDeviceToHost, c.stream));
+        HIPCHECK(hipStreamSynchronize(c.stream));
+        const unsigned long long nr2 = (unsigned long long)ul[0] + ul[1];
+        DevBuf pb(std::max<unsigned long long>(nl2 + nr2, 1) * 8);
+        std::swap(pairs.p, pb.p);
+        if (nl2) HIPCHECK(cq_launch_join_fill(nullptr, nullptr, (uint32_t)nl2, 0, 0, pairs.as<uint2>(), c.stream));
+        if (nr2) HIPCHECK(cq_launch_join_fill(unm.as<unsigned int>(), upos.as<unsigned int>(), B.n, nl2, 1,
+                                              pairs.as<uint2>(), c.stream));
+        HIPCHECK(hipStreamSynchronize(c.stream));
+        np = nl2 + nr2;
     }
     else if (outer_left || outer_right) {
         // nothing matches: every row of the outer side(s), NULL-padded
@@ -3971,7 +4021,8 @@ cq_table* run_join(DevCtx& c, cq_node* q, const cqgpu_table* L, const cqgpu_tabl
     // across partials the first level runs on the key-routed sides; a chain's later
     // levels join each rank's joined rows with the whole next table (every joined
     // row lives on one rank, so INNER and LEFT need nothing global; the unmatched
-    // right rows of a later RIGHT / FULL level would)
+    // right rows of a later RIGHT / FULL level are the records no rank matched:
+    // g_outer_sets, cqgpu_join_outer_matched / cqgpu_join_outer_set)
     const bool chain = part && nj > 1;
     struct Level {
         const cqgpu_table* R;
@@ -4007,7 +4058,6 @@ cq_table* run_join(DevCtx& c, cq_node* q, const cqgpu_table* L, const cqgpu_tabl
         }
         v.keyed = v.kl >= 0 && v.kr >= 0;
         if (part && j == 0 && !v.keyed) throw Ineligible{"JOIN without an `ident = ident` ON across partials"};
-        if (part && j > 0 && v.outer_right) throw Ineligible{"RIGHT/FULL JOIN after the first level across partials"};
         if (part && j > 0 && v.R->gids) throw HipError{"join chain across partials: a later level's table must be whole"};
         v.nleft = (int)wnames.size();
         std::vector<std::string> nn;        // copy_columns_with_prefix (evaluator_joins.c:30-37)
@@ -4069,8 +4119,40 @@ cq_table* run_join(DevCtx& c, cq_node* q, const cqgpu_table* L, const cqgpu_tabl
         Bp->cols.assign(v.rneed.begin(), v.rneed.end());
         if (Bp->cols.empty()) Bp->cols.push_back(0);
         load_side(c, v.R, *Bp);
+        // a later RIGHT / FULL level across partials: the ranks' matched records
+        const bool probe_here = part && part->probe_level == j;
+        const OuterSet* os = nullptr;
+        DevBuf gdev, mdev;
+        if (part && j > 0 && v.outer_right && !probe_here) {
+            auto it = g_outer_sets.find(j);
+            if (it == g_outer_sets.end())
+                throw Ineligible{"RIGHT/FULL JOIN after the first level across partials without the ranks' matched "
+                                 "records (cqgpu_join_outer_set)"};
+            if (it->second.matched.size() != Bp->n)
+                throw HipError{"join_outer_set: " + std::to_string(it->second.matched.size()) +
+                               " flags for a level of " + std::to_string(Bp->n) + " records"};
+            os = &it->second;
+            DevBuf g(std::max<size_t>(Bp->n, 1));
+            std::swap(gdev.p, g.p);
+            if (Bp->n)
+                HIPCHECK(hipMemcpyAsync(gdev.p, os->matched.data(), Bp->n, hipMemcpyHostToDevice, c.stream));
+        }
+        if (probe_here) {
+            DevBuf mb(std::max<size_t>(Bp->n, 1));
+            std::swap(mdev.p, mb.p);
+        }
         DevBuf pb(8);
-        np = build_pairs(c, *Ap, *Bp, v.kl, v.kr, v.keyed, v.outer_left, v.outer_right, pb, v.cross);
+        np = build_pairs(c, *Ap, *Bp, v.kl, v.kr, v.keyed, v.outer_left, v.outer_right || probe_here, pb, v.cross,
+                         os ? gdev.as<uint8_t>() : nullptr, os ? os->emit : true,
+                         probe_here ? mdev.as<uint8_t>() : nullptr);
+        if (probe_here) {
+            part->probe_out.assign(Bp->n, 0);
+            if (Bp->n)
+                HIPCHECK(hipMemcpyAsync(part->probe_out.data(), mdev.p, Bp->n, hipMemcpyDeviceToHost, c.stream));
+            HIPCHECK(hipStreamSynchronize(c.stream));
+            return nullptr;
+        }
+        HIPCHECK(hipStreamSynchronize(c.stream));       // (gdev is released at the end of this level)
         std::swap(pairs.p, pb.p);
         if (part && j == 0 && v.keyed) {     // even when one side is empty on this rank
             part->lmask |= key_class_mask(c, *Ap, v.kl);
@@ -5404,6 +5486,58 @@ cq_table* cqgpu_debug_cells(cqgpu_table* t, const int* cols, int ncols, const un
 // add, first offsets and extremes take the (value, offset) minimum, and the
 // representative row is the one of the smallest first offset -- what
 // create_groups / evaluate_aggregate give on the whole file.
+// a chain's later RIGHT / FULL level across partials (include/cqgpu.h)
+int cqgpu_join_outer_matched(cq_node* q, cqgpu_table* const* tables, int ntables, int level, const uint8_t** flags,
+                             uint64_t* n) {
+    g_inel.clear();
+    g_err.clear();
+    memset(&g_stats, 0, sizeof g_stats);
+    static thread_local std::vector<uint8_t> out;
+    if (flags) *flags = nullptr;
+    if (n) *n = 0;
+    try {
+        if (!q || q->kind != CQ_N_QUERY || level < 1 || level >= q->u.q.join_count) return 0;
+        cq_node* jn = q->u.q.joins[level];
+        if (!jn || jn->kind != CQ_N_JOIN) throw Ineligible{"malformed JOIN"};
+        if (jn->u.join.kind != CQ_JOIN_RIGHT && jn->u.join.kind != CQ_JOIN_FULL) return 0;
+        if (ntables < 2 || !tables || !tables[0]) throw HipError{"no table"};
+        DevCtx& c = ctx();
+        bump_reset(c);
+        check_plan_shape(q, tables[0], true);
+        JoinPartial jp;
+        jp.probe_level = level;
+        (void)run_join(c, q, tables[0], tables + 1, ntables - 1, &jp);
+        out.swap(jp.probe_out);
+        if (flags) *flags = out.data();
+        if (n) *n = out.size();
+        return 1;
+    } catch (Ineligible& e) {
+        g_inel = e.why;
+        set_err("cq_amd: query outside the GPU executor's subset: %s", e.why.c_str());
+    } catch (HipError& e) {
+        set_err("cq_amd: %s", e.msg.c_str());
+    } catch (std::exception& e) {
+        set_err("cq_amd: %s", e.what());
+    } catch (...) {
+        set_err("cq_amd: %s", "unexpected C++ exception");
+    }
+    return -1;
+}
+
+int cqgpu_join_outer_set(int level, const uint8_t* matched, uint64_t n, int emit) {
+    g_err.clear();
+    if (level < 1 || (n && !matched)) {
+        set_err("cq_amd: %s", "join_outer_set: bad arguments");
+        return -1;
+    }
+    OuterSet& o = g_outer_sets[level];
+    o.matched.assign(matched, matched + n);
+    o.emit = emit != 0;
+    return 0;
+}
+
+void cqgpu_join_outer_clear(void) { g_outer_sets.clear(); }
+
 size_t cqgpu_query_partial(cq_node* q, cqgpu_table* const* tables, int ntables, void** blob_out) {
     if (blob_out) *blob_out = nullptr;
     g_inel.clear();
@@ -7169,6 +7303,47 @@ void dist_join(DevCtx& c, DistComm& m, cq_node* q, cqgpu_table* const* tables, i
     tabs.push_back(routed[0].get());
     tabs.push_back(routed[1].get());
     for (int i = 2; i < ntables; i++) tabs.push_back(tables[i]);
+    // a chain's later RIGHT / FULL levels: every rank's matched flags over the level's
+    // whole table, OR-ed by a MAX all-reduce over bytes; rank 0's partial carries the
+    // records no rank matched (cqgpu_join_outer_* in include/cqgpu.h)
+    g_outer_sets.clear();
+    struct ClearSets { ~ClearSets() { g_outer_sets.clear(); } } clear_sets_;
+    const int nj = q && q->kind == CQ_N_QUERY ? q->u.q.join_count : 0;
+    for (int j = 1; j < nj && 1 + j < ntables; j++) {
+        cq_node* jn = q->u.q.joins[j];
+        if (!jn || jn->kind != CQ_N_JOIN || (jn->u.join.kind != CQ_JOIN_RIGHT && jn->u.join.kind != CQ_JOIN_FULL))
+            continue;
+        cqgpu_table* T = tables[1 + j];           // whole on every rank: the same record count
+        if (!T) throw PeerFail{"dist_join: a chain table is missing"};
+        if (!T->rec_starts) {
+            std::unique_ptr<DevBuf> b(new DevBuf());
+            T->nrec_starts = all_records(c, T, *b);
+            T->rec_starts = std::move(b);
+        }
+        const uint64_t nrec = T->nrec_starts;
+        std::vector<uint8_t> flags(nrec, 0);
+        if (!bad) {
+            const uint8_t* fl = nullptr;
+            uint64_t n = 0;
+            const int r = cqgpu_join_outer_matched(q, tabs.data(), (int)tabs.size(), j, &fl, &n);
+            if (r < 0 || (r == 1 && n != nrec)) {
+                bad = true;
+                err = r < 0 ? g_err : std::string("join_outer_matched: record count differs");
+            } else if (r == 1 && n) {
+                memcpy(flags.data(), fl, n);
+            }
+        }
+        if (nrec) {
+            DevBuf dm(nrec);
+            HIPCHECK(hipMemcpyAsync(dm.p, flags.data(), nrec, hipMemcpyHostToDevice, c.stream));
+            NCCLCHECK(ncclAllReduce(dm.p, dm.p, nrec, ncclUint8, ncclMax, m.comm, c.stream));
+            HIPCHECK(hipMemcpyAsync(flags.data(), dm.p, nrec, hipMemcpyDeviceToHost, c.stream));
+            HIPCHECK(hipStreamSynchronize(c.stream));
+        }
+        OuterSet& o = g_outer_sets[j];
+        o.matched.swap(flags);
+        o.emit = m.rank == 0;
+    }
     dist_blob(c, m, q, tabs.data(), (int)tabs.size(), res, bad, err);
 }
 

@@ -388,6 +388,19 @@ __global__ void rs_write_kernel(const uint8_t* __restrict__ g, uint64_t lo, uint
     for (uint32_t mm = m; mm; mm &= mm - 1) out[pos++] = p0 + (uint32_t)__builtin_ctz(mm);
 }
 
+// a later RIGHT / FULL level across partials (executor.hip OuterSet): unm[i] = 1 for a
+// right record this rank's rows did not match -> matched_out[i] (this rank's matched
+// flags), and unm[i] = 1 only for the records no rank matched (gset[i] = 0), on the
+// emitting rank
+__global__ void outer_global_kernel(unsigned int* __restrict__ unm, uint32_t n, const uint8_t* __restrict__ gset,
+                                    uint32_t emit, uint8_t* __restrict__ matched_out) {
+    const uint32_t i = blockIdx.x * blockDim.x + threadIdx.x;
+    if (i >= n) return;
+    const unsigned int u = unm[i];
+    if (matched_out) matched_out[i] = u ? 0 : 1;
+    if (gset) unm[i] = emit && !gset[i] ? 1u : 0u;
+}
+
 inline uint32_t blocks(uint64_t n, uint32_t b) { return (uint32_t)((n + b - 1) / b); }
 
 }  // namespace
@@ -431,6 +444,12 @@ hipError_t cq_launch_gather_len(const uint32_t* len, const uint32_t* order, uint
     return hipGetLastError();
 }
 
+hipError_t cq_launch_outer_global(unsigned int* unm, uint32_t n, const uint8_t* gset, uint32_t emit, uint8_t* matched_out,
+                                  hipStream_t s) {
+    if (!n) return hipSuccess;
+    outer_global_kernel<<<blocks(n, 256), 256, 0, s>>>(unm, n, gset, emit, matched_out);
+    return hipGetLastError();
+}
 hipError_t cq_launch_route_project(const uint8_t* g, const unsigned long long* recs, uint32_t n, uint64_t end,
                                    uint64_t mask, uint32_t last_keep, uint32_t delim, uint32_t quote,
                                    const unsigned long long* codes, const uint32_t* cls, uint32_t nranks, uint32_t* len,

@@ -315,6 +315,26 @@ def join_partitioned_rccl(ast, lshard, rshard, rest=()):
     return tp
 
 
+def outer_sets(ast, tables, nlevels: int, comm) -> None:
+    """A chain's later RIGHT / FULL levels (cqgpu_join_outer_* in include/cqgpu.h): per
+    level, every rank's matched flags over the level's whole table, OR-ed by a MAX
+    all-reduce over bytes; rank 0's partial carries the records no rank matched.
+    Every rank must call it, before query_partial."""
+    import cq_amd
+    cq_amd.join_outer_clear()
+    for j in range(1, nlevels + 1):
+        flags, err = _local(cq_amd.join_outer_matched, ast, tables, j)
+        agree(err, comm)
+        if flags is None:                  # (decided by the plan alone: the same on every rank)
+            continue
+        t = torch.frombuffer(bytearray(flags), dtype=torch.uint8).to(comm) if flags else \
+            torch.zeros(0, dtype=torch.uint8, device=comm)
+        if t.numel():
+            dist.all_reduce(t, op=dist.ReduceOp.MAX)
+        _, err = _local(cq_amd.join_outer_set, j, bytes(t.cpu().numpy()), dist.get_rank() == 0)
+        agree(err, comm)
+
+
 def join_partitioned(ast, lshard, rshard, lheader: bytes, rheader: bytes, device: torch.device | str,
                      comm_device: torch.device | str | None = None, rest=()):
     """Repartitioned JOIN over this rank's shards of both inputs of the first JOIN.
@@ -332,7 +352,12 @@ def join_partitioned(ast, lshard, rshard, lheader: bytes, rheader: bytes, device
         # one rank: every record routes to itself in its own order (the stable sort by
         # destination is the identity), so the shards are already the routed tables
         # and their record ids the local row indexes
-        return cq_amd.merge_partials(ast, [cq_amd.query_partial(ast, [lshard, rshard, *rest])])
+        comm = torch.device(comm_device) if comm_device is not None else torch.device(device)
+        outer_sets(ast, [lshard, rshard, *rest], len(rest), comm)
+        try:
+            return cq_amd.merge_partials(ast, [cq_amd.query_partial(ast, [lshard, rshard, *rest])])
+        finally:
+            cq_amd.join_outer_clear()
     comm = torch.device(comm_device) if comm_device is not None else torch.device(device)
     routed = []
     for side, (tab, header) in enumerate(((lshard, lheader), (rshard, rheader))):
@@ -361,7 +386,11 @@ def join_partitioned(ast, lshard, rshard, lheader: bytes, rheader: bytes, device
             err = err or e2 or e3
         agree(err, comm)
         routed.append(t)
-    blob, err = _local(cq_amd.query_partial, ast, routed + list(rest))
+    try:
+        outer_sets(ast, routed + list(rest), len(rest), comm)
+        blob, err = _local(cq_amd.query_partial, ast, routed + list(rest))
+    finally:
+        cq_amd.join_outer_clear()
     agree(err, comm)
     blobs = gather_blobs(blob, comm)
     if rank != 0:

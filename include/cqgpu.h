@@ -92,6 +92,22 @@ void cqgpu_result_free(cq_table* r);
  * blob.  Returns blob size (0 on error); *blob_out is freed with free(). */
 size_t cqgpu_query_partial(cq_node* query_ast, cqgpu_table* const* tables, int ntables,
                            void** blob_out);
+/* A chain's later RIGHT / FULL JOIN across partials (perform_join's unmatched right
+ * rows, evaluator_joins.c:143-171, chained through process_joins :268-270).  The
+ * level's table is whole on every rank; its unmatched records are the ones no rank's
+ * joined rows matched.  For each such level j, in order, before cqgpu_query_partial:
+ *   every rank: cqgpu_join_outer_matched(q, tables, n, j, &flags, &nrec) -- this rank's
+ *     matched flags over the level's records (one byte each, library memory valid
+ *     until the next call), the earlier levels' sets applied; returns 1, or 0 when
+ *     level j needs no set (level 0, INNER / LEFT), -1 on error;
+ *   the ranks OR the flags (an all-reduce MAX over bytes);
+ *   every rank: cqgpu_join_outer_set(j, global_flags, nrec, emit) with emit = 1 on
+ *     exactly one rank: that rank's partial carries the unmatched records.
+ * The sets stay until cqgpu_join_outer_clear. */
+int cqgpu_join_outer_matched(cq_node* query_ast, cqgpu_table* const* tables, int ntables, int level,
+                             const uint8_t** flags, uint64_t* nrec);
+int cqgpu_join_outer_set(int level, const uint8_t* matched, uint64_t nrec, int emit);
+void cqgpu_join_outer_clear(void);
 /* Merge the partial blobs of all ranks (any order) into the final result, with
  * HAVING / ORDER BY / DISTINCT / LIMIT applied as evaluate_query would. */
 cq_table* cqgpu_merge_partials(cq_node* query_ast, const void* const* blobs, const size_t* sizes,

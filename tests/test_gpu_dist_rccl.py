@@ -200,6 +200,12 @@ JOINS = [   # the repartitioned JOIN step inside the library (cqgpu_dist_join)
      ["users", "orders"]),
     ("SELECT r.dept, COUNT(*), SUM(o.price) FROM '{p}' AS u JOIN '{q}' AS o ON u.id = o.customer_id "
      "JOIN '{r}' AS r ON u.role = r.role GROUP BY r.dept", ["users", "orders", "roles"]),
+    # a later RIGHT / FULL level: the matched flags all-reduced (MAX over bytes) inside
+    # the library, rank 0's partial carrying the records no rank matched
+    ("SELECT r.dept, COUNT(*), SUM(o.price) FROM '{p}' AS u JOIN '{q}' AS o ON u.id = o.customer_id "
+     "RIGHT JOIN '{r}' AS r ON u.role = r.role GROUP BY r.dept", ["users", "orders", "roles"]),
+    ("SELECT COUNT(*), MIN(r.role), MAX(u.name) FROM '{p}' AS u JOIN '{q}' AS o ON u.id = o.customer_id "
+     "FULL JOIN '{r}' AS r ON u.role = r.role", ["users", "orders", "roles"]),
 ]
 
 

@@ -42,8 +42,11 @@ def _shards(data: bytes, nranks: int, seed: int):
 LAST_KINDS = []   # per rank, the scan kernel kind of its partial (4: the STAR fused join)
 
 
-def _run(ast, ldata: bytes, rdata: bytes, nranks: int, rest=()):
-    """rest: a chain's later JOIN tables, whole on every rank"""
+def _run(ast, ldata: bytes, rdata: bytes, nranks: int, rest=(), outer=True):
+    """rest: a chain's later JOIN tables, whole on every rank.  outer: run the later
+    RIGHT / FULL levels' protocol (cqgpu_join_outer_*, as cq_amd.dist.outer_sets):
+    per level every rank's matched flags, OR-ed, handed back to every rank with rank
+    0 emitting the records no rank matched"""
     lh, ls = _shards(ldata, nranks, 1)
     rh, rs = _shards(rdata, nranks, 2)
     routed = [[None, None] for _ in range(nranks)]
@@ -71,14 +74,30 @@ def _run(ast, ldata: bytes, rdata: bytes, nranks: int, rest=()):
             cq_amd.table_set_record_total(routed[d][side], total)
             cq_amd.table_set_key_stride(routed[d][side], nranks)
     whole = [[cq_amd.Table.from_bytes(x) for x in rest] for _ in range(nranks)]
+    sets = {}
+
+    def apply(d, upto):                    # rank d's view of the sets of the levels below `upto`
+        cq_amd.join_outer_clear()
+        for jj, g in sets.items():
+            if jj < upto:
+                cq_amd.join_outer_set(jj, g, d == 0)
     try:
+        for j in range(1, len(rest) + 1 if outer else 1):
+            fl = []
+            for d in range(nranks):
+                apply(d, j)
+                fl.append(cq_amd.join_outer_matched(ast, routed[d] + whole[d], j))
+            if fl[0] is not None:
+                sets[j] = np.bitwise_or.reduce([np.frombuffer(f, np.uint8) for f in fl]).tobytes()
         blobs = []
         LAST_KINDS.clear()
         for d in range(nranks):
+            apply(d, len(rest) + 1)
             blobs.append(cq_amd.query_partial(ast, routed[d] + whole[d]))
             LAST_KINDS.append(cq_amd.stats().get("scan_kernel"))
         tp = cq_amd.merge_partials(ast, blobs)
     finally:
+        cq_amd.join_outer_clear()
         for t in ls + rs + [x for pr in routed for x in pr] + [x for w in whole for x in w]:
             t.close()
     return tp
@@ -310,6 +329,21 @@ CHAINS = [
     (["rl", "qt"], "SELECT q.label, q.q FROM '{L}' AS u JOIN '{R}' AS o ON u.id = o.customer_id "
                    "LEFT JOIN '{X}' AS r ON u.role = r.role LEFT JOIN '{Y}' AS q ON r.grade = q.q "
                    "LIMIT 40 OFFSET 500"),
+    # a later RIGHT / FULL level (evaluator_joins.c:143-171 through :268-270): its
+    # unmatched records are the ones no rank matched ("rl": role_20..22 missing, a NULL
+    # role; "qt": q = 9 matches no grade), emitted once, after every left-driven row
+    (["rl"], "SELECT COUNT(*) FROM '{L}' AS u JOIN '{R}' AS o ON u.id = o.customer_id "
+             "RIGHT JOIN '{X}' AS r ON u.role = r.role"),
+    (["rl"], "SELECT r.dept, COUNT(*), SUM(o.price), MIN(r.role) FROM '{L}' AS u JOIN '{R}' AS o "
+             "ON u.id = o.customer_id FULL JOIN '{X}' AS r ON u.role = r.role GROUP BY r.dept"),
+    (["rl"], "SELECT r.role, r.dept, o.id FROM '{L}' AS u LEFT JOIN '{R}' AS o ON u.id = o.customer_id "
+             "RIGHT JOIN '{X}' AS r ON u.role = r.role WHERE o.price > 990 OR r.grade = 7 OR r.grade = 0"),
+    (["rl", "qt"], "SELECT q.label, COUNT(*), MAX(r.dept) FROM '{L}' AS u JOIN '{R}' AS o "
+                   "ON u.id = o.customer_id RIGHT JOIN '{X}' AS r ON u.role = r.role "
+                   "FULL JOIN '{Y}' AS q ON r.grade = q.q GROUP BY q.label"),
+    (["rl", "qt"], "SELECT r.dept, q.label, u.name FROM '{L}' AS u JOIN '{R}' AS o ON u.id = o.customer_id "
+                   "FULL JOIN '{X}' AS r ON u.role = r.role RIGHT JOIN '{Y}' AS q ON r.grade = q.q "
+                   "ORDER BY q.label LIMIT 30 OFFSET 3"),
 ]
 
 
@@ -341,15 +375,31 @@ def test_join_chain_across_partials(files, case, nranks):
     compare(got, want, tol, f"{sql} @ {nranks} ranks")
 
 
-def test_join_chain_right_later_refused(files):
-    """a later level's RIGHT / FULL JOIN needs every rank's matches: refused, not approximated"""
+def test_join_chain_right_later_needs_sets(files):
+    """a later level's RIGHT / FULL JOIN needs every rank's matches: without the
+    ranks' OR-ed flags (cqgpu_join_outer_set) it is refused, not approximated"""
     data, paths = files
     sql = _chain_sql(paths, ["rl"], "SELECT COUNT(*) FROM '{L}' AS u JOIN '{R}' AS o ON u.id = o.customer_id "
                                      "RIGHT JOIN '{X}' AS r ON u.role = r.role")
     with cqtest.Parsed(sql) as ast:
         with pytest.raises(RuntimeError):
-            _run(ast, data["du"], data["do"], 3, [data["rl"]])
-        assert "RIGHT/FULL JOIN after the first level" in cq_amd.last_ineligible()
+            _run(ast, data["du"], data["do"], 3, [data["rl"]], outer=False)
+        assert "without the ranks' matched records" in cq_amd.last_ineligible()
+        # flags of the wrong length are an error, not a wrong answer
+        lt, rt, xt = (cq_amd.Table.from_bytes(data[k]) for k in ("du", "do", "rl"))
+        try:
+            cq_amd.join_outer_set(1, b"\x00" * 3, True)
+            with pytest.raises(RuntimeError, match="flags for a level of"):
+                cq_amd.query_partial(ast, [lt, rt, xt])
+            cq_amd.join_outer_clear()
+            # a level that needs no set: INNER / LEFT, and level 0
+            assert cq_amd.join_outer_matched(ast, [lt, rt, xt], 0) is None
+            fl = cq_amd.join_outer_matched(ast, [lt, rt, xt], 1)
+            assert fl is not None and len(fl) == data["rl"].count(b"\n") - 1
+        finally:
+            cq_amd.join_outer_clear()
+            for t in (lt, rt, xt):
+                t.close()
 
 
 def test_mixed_key_classes_refused(files):
@@ -589,14 +639,18 @@ def test_join_partitioned_processes(files, world):
     compare(got, want, tol, sql + f" @ {world} processes")
 
 
+@pytest.mark.parametrize("case", [0, 10])
 @pytest.mark.parametrize("world", [1, 2])
-def test_join_chain_processes(files, world):
+def test_join_chain_processes(files, world, case):
     """a three-table chain through cq_amd.dist.join_partitioned in separate processes
-    (gloo): routed first level, whole third table, merged on rank 0 vs the oracle"""
+    (gloo): routed first level, whole third table, merged on rank 0 vs the oracle;
+    case 10 a later FULL JOIN (dist.outer_sets: the ranks' matched flags OR-ed by an
+    all-reduce)"""
     import socket
     import torch.multiprocessing as mp
     data, paths = files
-    sql = _chain_sql(paths, ["rl"], CHAINS[0][1])
+    assert CHAINS[case][0] == ["rl"]
+    sql = _chain_sql(paths, ["rl"], CHAINS[case][1])
     want, unsup = cqtest.oracle_query(sql)
     assert not unsup
     s = socket.socket()
