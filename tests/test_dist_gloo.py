@@ -280,3 +280,48 @@ def test_dense_merge_rank_local_failure_raises_everywhere(world, bad):
     for r in range(world):
         assert res[r].startswith("peer-failure"), res
     assert "injected rank-local failure" in res[bad]
+
+
+def _oworker(rank, world, port, q):
+    """dist.outer_sets over gloo with the library's three calls replaced by fakes:
+    level 1 (RIGHT / FULL) flags differ per rank, level 2 needs no set"""
+    import torch.distributed as dist
+    import cq_amd
+    from cq_amd import dist as cd
+    os.environ["MASTER_ADDR"] = "127.0.0.1"
+    os.environ["MASTER_PORT"] = str(port)
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    calls = []
+    try:
+        def matched(ast, tables, level):
+            calls.append(("matched", level))
+            if level == 2:
+                return None
+            return bytes(1 if i % (rank + 2) == 0 else 0 for i in range(23))
+        cq_amd.join_outer_matched = matched
+        cq_amd.join_outer_set = lambda level, flags, emit: calls.append(("set", level, bytes(flags), emit))
+        cq_amd.join_outer_clear = lambda: calls.append(("clear",))
+        cd.outer_sets(None, [], 2, "cpu")
+        q.put((rank, calls))
+    finally:
+        dist.destroy_process_group()
+
+
+@pytest.mark.parametrize("world", [2, 3])
+def test_outer_sets_gloo(world):
+    """a chain's later RIGHT / FULL level (cq_amd.dist.outer_sets): every rank gets the
+    OR of the ranks' matched flags, rank 0 alone emits, a level that needs no set is
+    skipped on every rank"""
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    port = _free_port()
+    procs = [ctx.Process(target=_oworker, args=(r, world, port, q)) for r in range(world)]
+    for p in procs:
+        p.start()
+    res = dict(q.get(timeout=120) for _ in range(world))
+    for p in procs:
+        p.join(timeout=60)
+        assert p.exitcode == 0
+    want = bytes(1 if any(i % (r + 2) == 0 for r in range(world)) else 0 for i in range(23))
+    for rank, calls in res.items():
+        assert calls == [("clear",), ("matched", 1), ("set", 1, want, rank == 0), ("matched", 2)], (rank, calls)
