@@ -102,6 +102,15 @@ hipError_t cq_launch_join_count(const cq::Cell* L, uint32_t ls, uint32_t lk, uin
 hipError_t cq_launch_join_emit(const cq::Cell* L, uint32_t ls, uint32_t lk, uint32_t nL, const cq::JoinRight* J,
                                const uint32_t* lo, const unsigned long long* cnt, const unsigned long long* offs,
                                uint2* pairs, unsigned int* rmatched, hipStream_t s);
+hipError_t cq_launch_route_runs(const uint32_t* dest, const uint32_t* len, uint32_t n, uint32_t nw,
+                                unsigned long long* rcnt, unsigned long long* rbytes, hipStream_t s);
+hipError_t cq_launch_route_run_starts(const unsigned long long* cbase, const unsigned long long* bbase,
+                                     const unsigned long long* rcnt, const unsigned long long* rbytes, uint32_t nw,
+                                     uint32_t nranks, unsigned long long* starts, hipStream_t s);
+hipError_t cq_launch_route_scatter(const uint8_t* g, const unsigned long long* recs, const uint32_t* dest,
+                                   const uint32_t* len, uint32_t n, uint32_t nw, uint64_t end,
+                                   const unsigned long long* cbase, const unsigned long long* bbase, uint64_t gid_base,
+                                   uint8_t* out, unsigned long long* gids, hipStream_t s);
 hipError_t cq_launch_outer_global(unsigned int* unm, uint32_t n, const uint8_t* gset, uint32_t emit, uint8_t* matched_out,
                                   hipStream_t s);
 hipError_t cq_launch_join_fill(const unsigned int* flags, const unsigned int* pos, uint32_t n, unsigned long long base,
@@ -550,6 +559,11 @@ std::string rtrim(std::string s) {
 struct RouteState {
     DevBuf recs, order, len, off;
     DevBuf proj;                   // the projected records at their source offsets (keep != ~0)
+    // nranks <= 64: the destination-run layout (route.hip route_runs_kernel) -- each
+    // record's destination, and every (destination, wave) run's record / byte base
+    DevBuf dest, cbase, bbase;
+    uint32_t nw = 0;
+    bool runs = false;
     uint32_t n = 0;
     uint64_t bytes = 0;
     uint64_t keep = ~0ull;         // columns sent (route_keep_mask; ~0: whole records)
@@ -4908,9 +4922,8 @@ int cqgpu_route_plan(cq_node* q, cqgpu_table* const* tables, int ntables, int si
         st->keep = route_keep_mask(q, tables, ntables, side, &st->last_keep);
         std::vector<unsigned long long> per(2 * (size_t)nranks, 0);
         if (n) {
-            DevBuf codes((size_t)n * 8), cls((size_t)n * 4), dest((size_t)n * 4), dsorted((size_t)n * 4),
-                idx((size_t)n * 4), len((size_t)n * 4), order((size_t)n * 4), lens((size_t)n * 8),
-                off((size_t)n * 8), dst((2 * (size_t)nranks + 2) * 8);
+            DevBuf codes((size_t)n * 8), cls((size_t)n * 4), dest((size_t)n * 4), idx((size_t)n * 4),
+                len((size_t)n * 4), dst((2 * (size_t)nranks + 2) * 8);
             HIPCHECK(cq_launch_join_code(S.cells.as<Cell>(), 1, 0, n, codes.as<unsigned long long>(), cls.as<uint32_t>(),
                                          idx.as<uint32_t>(), nullptr, c.stream));
             if (st->keep != ~0ull) {
@@ -4926,6 +4939,41 @@ int cqgpu_route_plan(cq_node* q, cqgpu_table* const* tables, int ntables, int si
                                              cls.as<uint32_t>(), (uint32_t)nranks, len.as<uint32_t>(),
                                              dest.as<uint32_t>(), c.stream));
             }
+            if (nranks <= 64 && !getenv("CQGPU_ROUTE_SORT")) {
+                // destination runs: per (destination, wave) counts, one exclusive scan each
+                const uint32_t nw = (uint32_t)(((uint64_t)n + 63) / 64);
+                const size_t nrun = (size_t)nranks * nw;
+                DevBuf rc(nrun * 8), rbt(nrun * 8), cb(nrun * 8), bb(nrun * 8);
+                HIPCHECK(hipMemsetAsync(rc.p, 0, nrun * 8, c.stream));
+                HIPCHECK(hipMemsetAsync(rbt.p, 0, nrun * 8, c.stream));
+                HIPCHECK(cq_launch_route_runs(dest.as<uint32_t>(), len.as<uint32_t>(), n, nw,
+                                              rc.as<unsigned long long>(), rbt.as<unsigned long long>(), c.stream));
+                size_t tr = 0;
+                HIPCHECK(cq_excl_sum_u64(nullptr, &tr, rc.as<unsigned long long>(), cb.as<unsigned long long>(), nrun,
+                                         c.stream));
+                DevBuf tmp(tr);
+                HIPCHECK(cq_excl_sum_u64(tmp.p, &tr, rc.as<unsigned long long>(), cb.as<unsigned long long>(), nrun,
+                                         c.stream));
+                HIPCHECK(cq_excl_sum_u64(tmp.p, &tr, rbt.as<unsigned long long>(), bb.as<unsigned long long>(), nrun,
+                                         c.stream));
+                HIPCHECK(cq_launch_route_run_starts(cb.as<unsigned long long>(), bb.as<unsigned long long>(),
+                                                    rc.as<unsigned long long>(), rbt.as<unsigned long long>(), nw,
+                                                    (uint32_t)nranks, dst.as<unsigned long long>(), c.stream));
+                std::vector<unsigned long long> starts(2 * (size_t)nranks + 2);
+                HIPCHECK(hipMemcpyAsync(starts.data(), dst.p, starts.size() * 8, hipMemcpyDeviceToHost, c.stream));
+                HIPCHECK(hipStreamSynchronize(c.stream));
+                for (int r = 0; r < nranks; r++) {
+                    per[nranks + r] = starts[r + 1] - starts[r];
+                    per[r] = starts[nranks + 2 + r] - starts[nranks + 1 + r];
+                }
+                st->runs = true;
+                st->nw = nw;
+                std::swap(st->dest.p, dest.p);
+                std::swap(st->len.p, len.p);
+                std::swap(st->cbase.p, cb.p);
+                std::swap(st->bbase.p, bb.p);
+            } else {
+            DevBuf dsorted((size_t)n * 4), order((size_t)n * 4), lens((size_t)n * 8), off((size_t)n * 8);
             int bits = 1;
             while ((1 << bits) < nranks) bits++;
             size_t tb = 0;
@@ -4955,6 +5003,7 @@ int cqgpu_route_plan(cq_node* q, cqgpu_table* const* tables, int ntables, int si
             std::swap(st->order.p, order.p);
             std::swap(st->len.p, len.p);
             std::swap(st->off.p, off.p);
+            }
         }
         st->bytes = 0;
         for (int r = 0; r < nranks; r++) {
@@ -4989,10 +5038,17 @@ int cqgpu_route_fill(cqgpu_table* t, uint64_t gid_base, void* dev_bytes, uint64_
         if (gid_base + st.n >= (1ull << 32)) throw HipError{"route: 2^32 - 1 or more records on a join side"};
         if (st.n) {
             if (!dev_bytes || !dev_gids) throw HipError{"route_fill: null output buffer"};
-            HIPCHECK(cq_launch_route_copy(st.keep != ~0ull ? st.proj.as<uint8_t>() : t->g,
-                                          st.recs.as<unsigned long long>(), st.order.as<uint32_t>(),
-                                          st.len.as<uint32_t>(), st.off.as<unsigned long long>(), st.n, gid_base,
-                                          (uint8_t*)dev_bytes, (unsigned long long*)dev_gids, c.stream));
+            const uint8_t* src = st.keep != ~0ull ? st.proj.as<uint8_t>() : t->g;
+            if (st.runs)
+                HIPCHECK(cq_launch_route_scatter(src, st.recs.as<unsigned long long>(), st.dest.as<uint32_t>(),
+                                                 st.len.as<uint32_t>(), st.n, st.nw, t->n,
+                                                 st.cbase.as<unsigned long long>(),
+                                                 st.bbase.as<unsigned long long>(), gid_base, (uint8_t*)dev_bytes,
+                                                 (unsigned long long*)dev_gids, c.stream));
+            else
+                HIPCHECK(cq_launch_route_copy(src, st.recs.as<unsigned long long>(), st.order.as<uint32_t>(),
+                                              st.len.as<uint32_t>(), st.off.as<unsigned long long>(), st.n, gid_base,
+                                              (uint8_t*)dev_bytes, (unsigned long long*)dev_gids, c.stream));
             HIPCHECK(hipStreamSynchronize(c.stream));
         }
         t->route.reset();

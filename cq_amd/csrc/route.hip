@@ -242,6 +242,147 @@ __global__ void route_copy_kernel(const uint8_t* __restrict__ g, const unsigned 
     }
 }
 
+// ---- the send buffer by destination runs (nranks <= RUN_MAXN).  The send buffer is
+// the records grouped by destination, file order within one; the 64 consecutive
+// records of a wave contribute one run per destination they hold.  route_runs_kernel
+// writes each (destination d, wave w) run's record and byte count at [d * nw + w]
+// (destination-major: one exclusive scan of each array gives every run's send-buffer
+// record and byte base), route_scatter_kernel puts each record at its run's byte base
+// plus the bytes of the run's records before it, and its global id at the run's
+// record base plus its rank in the run.  Every read is a file-order stream (no gather
+// through a sorted order); the writes are up to nranks contiguous runs per wave.
+constexpr uint32_t RUN_MAXN = 64;
+
+__device__ __forceinline__ unsigned long long wave_incl_u64(unsigned long long x, uint32_t lane) {
+    for (int o = 1; o < 64; o <<= 1) {
+        const unsigned long long y = __shfl_up(x, o, 64);
+        if (lane >= (uint32_t)o) x += y;
+    }
+    return x;
+}
+// the same over 32 bits by DPP row shifts / broadcasts (no LDS crossbar): the runs'
+// byte sums when every record of the wave is under 2^25 bytes (64 of them fit)
+__device__ __forceinline__ uint32_t wave_incl_u32(uint32_t x) {
+    x += (uint32_t)__builtin_amdgcn_update_dpp(0, (int)x, 0x111, 0xf, 0xf, true);   // row_shr:1
+    x += (uint32_t)__builtin_amdgcn_update_dpp(0, (int)x, 0x112, 0xf, 0xf, true);   // row_shr:2
+    x += (uint32_t)__builtin_amdgcn_update_dpp(0, (int)x, 0x114, 0xf, 0xf, true);   // row_shr:4
+    x += (uint32_t)__builtin_amdgcn_update_dpp(0, (int)x, 0x118, 0xf, 0xf, true);   // row_shr:8
+    x += (uint32_t)__builtin_amdgcn_update_dpp(0, (int)x, 0x142, 0xa, 0xf, false);  // row_bcast:15
+    x += (uint32_t)__builtin_amdgcn_update_dpp(0, (int)x, 0x143, 0xc, 0xf, false);  // row_bcast:31
+    return x;
+}
+__device__ __forceinline__ unsigned long long wave_incl_len(uint32_t x, bool wide, uint32_t lane) {
+    return wide ? wave_incl_u64(x, lane) : (unsigned long long)wave_incl_u32(x);
+}
+
+__global__ __launch_bounds__(256) void route_runs_kernel(const uint32_t* __restrict__ dest,
+                                                         const uint32_t* __restrict__ len, uint32_t n, uint32_t nw,
+                                                         unsigned long long* __restrict__ rcnt,
+                                                         unsigned long long* __restrict__ rbytes) {
+    const uint32_t lane = threadIdx.x & 63;
+    const uint64_t i = (uint64_t)blockIdx.x * 256 + threadIdx.x;
+    const uint32_t w = (uint32_t)(i >> 6);
+    if (((uint64_t)w << 6) >= n) return;                 // (a whole wave)
+    const bool valid = i < n;
+    const uint32_t d = valid ? dest[i] : ~0u;
+    const uint32_t m = valid ? len[i] : 0u;
+    const bool wide = __ballot(m >= (1u << 25)) != 0;
+    bool todo = valid;
+    for (;;) {                                           // one trip per destination present
+        const uint64_t pend = __ballot(todo);
+        if (!pend) break;
+        const uint32_t d0 = (uint32_t)__shfl((int)d, (int)__builtin_ctzll(pend), 64);
+        const bool mine = todo && d == d0;
+        const uint64_t mk = __ballot(mine);
+        const unsigned long long b = wave_incl_len(mine ? m : 0u, wide, lane);
+        if (lane == 63) {
+            rcnt[(uint64_t)d0 * nw + w] = (unsigned long long)__popcll(mk);
+            rbytes[(uint64_t)d0 * nw + w] = b;
+        }
+        todo = todo && !mine;
+    }
+}
+
+__global__ __launch_bounds__(256) void route_scatter_kernel(const uint8_t* __restrict__ g,
+                                                            const unsigned long long* __restrict__ recs,
+                                                            const uint32_t* __restrict__ dest,
+                                                            const uint32_t* __restrict__ len, uint32_t n, uint32_t nw,
+                                                            uint64_t end,
+                                                            const unsigned long long* __restrict__ cbase,
+                                                            const unsigned long long* __restrict__ bbase,
+                                                            uint64_t gid_base, uint8_t* __restrict__ out,
+                                                            unsigned long long* __restrict__ gids) {
+    // the wave's source span staged in LDS with 16-byte loads (route_project_kernel's
+    // span: up to the next record's start; the padding '\n' ends the last record), so
+    // the byte copy below reads LDS instead of waiting on HBM per record group
+    __shared__ __attribute__((aligned(16))) uint8_t buf[4][RP_CAP];
+    const uint32_t lane = threadIdx.x & 63;
+    const uint64_t i = (uint64_t)blockIdx.x * 256 + threadIdx.x;
+    const uint32_t w = (uint32_t)(i >> 6);
+    const uint64_t i0 = (uint64_t)w << 6;
+    const bool live = i0 < n;
+    uint64_t a = 0, b = 0;
+    if (live) {
+        a = recs[i0] & ~15ull;
+        b = ((i0 + 64 < n ? recs[i0 + 64] : end + 1) + 15) & ~15ull;
+    }
+    const bool fits = live && b - a <= RP_CAP;
+    uint8_t* L = buf[threadIdx.x >> 6];
+    if (fits)
+        for (uint64_t q = a + lane * 16; q < b; q += 64 * 16) *(uint4*)(L + (q - a)) = *(const uint4*)(g + q);
+    __syncthreads();
+    if (!live) return;
+    const bool valid = i < n;
+    const uint32_t d = valid ? dest[i] : ~0u;
+    const uint32_t m = valid ? len[i] : 0u;
+    const unsigned long long src = valid ? recs[i] : 0ull;
+    unsigned long long dst = 0;
+    bool todo = valid;
+    const uint64_t below = lane ? (~0ull >> (64 - lane)) : 0ull;
+    const bool wide = __ballot(m >= (1u << 25)) != 0;
+    for (;;) {
+        const uint64_t pend = __ballot(todo);
+        if (!pend) break;
+        const uint32_t d0 = (uint32_t)__shfl((int)d, (int)__builtin_ctzll(pend), 64);
+        const bool mine = todo && d == d0;
+        const uint64_t mk = __ballot(mine);
+        const uint32_t x = mine ? m : 0u;
+        const unsigned long long pre = wave_incl_len(x, wide, lane) - x;
+        if (mine) {
+            const uint64_t at = (uint64_t)d0 * nw + w;
+            dst = bbase[at] + pre;
+            gids[cbase[at] + (uint64_t)__popcll(mk & below)] = gid_base + i;
+        }
+        todo = todo && !mine;
+    }
+    // four records at a time, 16 lanes each (lane k of a group moves bytes k, k + 16, ...)
+    const uint32_t grp = lane >> 4, sub = lane & 15;
+    for (uint32_t r = 0; r < 64; r += 4) {
+        const int from = (int)(r + grp);
+        const unsigned long long s = __shfl(src, from, 64);
+        const unsigned long long t = __shfl(dst, from, 64);
+        const uint32_t mm = (uint32_t)__shfl((int)m, from, 64);     // 0 past n
+        if (fits)
+            for (uint32_t k = sub; k < mm; k += 16) out[t + k] = k + 1 == mm ? (uint8_t)'\n' : L[s - a + k];
+        else
+            for (uint32_t k = sub; k < mm; k += 16) out[t + k] = k + 1 == mm ? (uint8_t)'\n' : g[s + k];
+    }
+}
+
+// starts[0..nranks]: each destination's first send-buffer record (starts[nranks] = n);
+// starts[nranks+1 .. 2*nranks+1]: the same in bytes (route_bounds_kernel's layout)
+__global__ void route_run_starts_kernel(const unsigned long long* __restrict__ cbase,
+                                        const unsigned long long* __restrict__ bbase,
+                                        const unsigned long long* __restrict__ rcnt,
+                                        const unsigned long long* __restrict__ rbytes, uint32_t nw, uint32_t nranks,
+                                        unsigned long long* __restrict__ starts) {
+    const uint32_t d = blockIdx.x * blockDim.x + threadIdx.x;
+    if (d > nranks) return;
+    const uint64_t last = (uint64_t)nranks * nw - 1;
+    starts[d] = d < nranks ? cbase[(uint64_t)d * nw] : cbase[last] + rcnt[last];
+    starts[nranks + 1 + d] = d < nranks ? bbase[(uint64_t)d * nw] : bbase[last] + rbytes[last];
+}
+
 // (l, r) pair -> its position key in the reference's output order (perform_join,
 // evaluator_joins.c:63-171): (global left id << 32 | global right id) for matched
 // pairs, (left id << 32) for an unmatched left row (it is its row's only output),
@@ -444,6 +585,29 @@ hipError_t cq_launch_gather_len(const uint32_t* len, const uint32_t* order, uint
     return hipGetLastError();
 }
 
+hipError_t cq_launch_route_runs(const uint32_t* dest, const uint32_t* len, uint32_t n, uint32_t nw,
+                                unsigned long long* rcnt, unsigned long long* rbytes, hipStream_t s) {
+    if (!n) return hipSuccess;
+    route_runs_kernel<<<blocks((uint64_t)nw * 64, 256), 256, 0, s>>>(dest, len, n, nw, rcnt, rbytes);
+    return hipGetLastError();
+}
+hipError_t cq_launch_route_run_starts(const unsigned long long* cbase, const unsigned long long* bbase,
+                                     const unsigned long long* rcnt, const unsigned long long* rbytes, uint32_t nw,
+                                     uint32_t nranks, unsigned long long* starts, hipStream_t s) {
+    if (!nw || !nranks) return hipSuccess;
+    route_run_starts_kernel<<<blocks((uint64_t)nranks + 1, 256), 256, 0, s>>>(cbase, bbase, rcnt, rbytes, nw, nranks,
+                                                                              starts);
+    return hipGetLastError();
+}
+hipError_t cq_launch_route_scatter(const uint8_t* g, const unsigned long long* recs, const uint32_t* dest,
+                                   const uint32_t* len, uint32_t n, uint32_t nw, uint64_t end,
+                                   const unsigned long long* cbase, const unsigned long long* bbase, uint64_t gid_base,
+                                   uint8_t* out, unsigned long long* gids, hipStream_t s) {
+    if (!n) return hipSuccess;
+    route_scatter_kernel<<<blocks((uint64_t)nw * 64, 256), 256, 0, s>>>(g, recs, dest, len, n, nw, end, cbase,
+                                                                        bbase, gid_base, out, gids);
+    return hipGetLastError();
+}
 hipError_t cq_launch_outer_global(unsigned int* unm, uint32_t n, const uint8_t* gset, uint32_t emit, uint8_t* matched_out,
                                   hipStream_t s) {
     if (!n) return hipSuccess;

@@ -507,6 +507,37 @@ def test_route_counts(files, monkeypatch):
         rt.close()
 
 
+@pytest.mark.parametrize("nranks", [1, 3, 8, 64, 70])
+def test_route_runs_equal_sort(files, nranks, monkeypatch):
+    """the destination-run routing (route.hip route_runs / route_scatter, nranks <= 64)
+    writes the same send buffer, ids and per-rank counts as the sorted-order copy
+    (CQGPU_ROUTE_SORT=1; above 64 ranks both take it), projected and whole records"""
+    data, _ = files
+    for sql in ("SELECT u.role, COUNT(*) FROM 'u' AS u JOIN 'o' AS o ON u.id = o.customer_id GROUP BY u.role",
+                "SELECT * FROM 'u' AS u JOIN 'o' AS o ON u.id = o.customer_id"):
+        with cqtest.Parsed(sql) as ast:
+            tabs = (cq_amd.Table.from_bytes(data["du"]), cq_amd.Table.from_bytes(data["do"]))
+            try:
+                for side in (0, 1):
+                    got = []
+                    for sort in (False, True):
+                        if sort:
+                            monkeypatch.setenv("CQGPU_ROUTE_SORT", "1")
+                        else:
+                            monkeypatch.delenv("CQGPU_ROUTE_SORT", raising=False)
+                        nb, nr = cq_amd.route_plan(ast, list(tabs), side, nranks)
+                        sb = torch.empty(max(sum(nb), 1), dtype=torch.uint8, device="cuda")
+                        sg = torch.empty(max(sum(nr), 1), dtype=torch.int64, device="cuda")
+                        cq_amd.route_fill(tabs[side], 7, sb.data_ptr(), sg.data_ptr())
+                        torch.cuda.synchronize()
+                        got.append((nb, nr, bytes(sb.cpu().numpy()[:sum(nb)]), sg.cpu().numpy()[:sum(nr)].tolist()))
+                    assert got[0] == got[1], (sql, side)
+                    assert sorted(got[0][3]) == list(range(7, 7 + sum(got[0][1])))
+            finally:
+                for t in tabs:
+                    t.close()
+
+
 PROJ_LEFT = (b"id,name,age,role,note\n"
              b"1,ann,30,admin,x\n"
              b' 2 , "b,o""b" ,41, "ops, east" ,"q\n'      # an unclosed quote runs to the line end
