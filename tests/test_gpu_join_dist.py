@@ -23,7 +23,7 @@ from test_gpu_parity import compare, tolerant_columns
 pytestmark = pytest.mark.gpu
 
 
-def _shards(data: bytes, nranks: int, seed: int):
+def _shards(data: bytes, nranks: int, seed: int, cfg=None):
     header, body = data.split(b"\n", 1)
     header += b"\n"
     rng = np.random.default_rng(seed)
@@ -33,22 +33,22 @@ def _shards(data: bytes, nranks: int, seed: int):
     for r in range(nranks):
         pc = body[cuts[r]:cuts[r + 1]]
         if r == 0:
-            tabs.append(cq_amd.Table.from_bytes(header + pc))
+            tabs.append(cq_amd.Table.from_bytes(header + pc, cfg=cfg))
         else:
-            tabs.append(cq_amd.Table.from_bytes(pc, base_offset=len(header) + cuts[r], header=header))
+            tabs.append(cq_amd.Table.from_bytes(pc, cfg=cfg, base_offset=len(header) + cuts[r], header=header))
     return header, tabs
 
 
 LAST_KINDS = []   # per rank, the scan kernel kind of its partial (4: the STAR fused join)
 
 
-def _run(ast, ldata: bytes, rdata: bytes, nranks: int, rest=(), outer=True):
+def _run(ast, ldata: bytes, rdata: bytes, nranks: int, rest=(), outer=True, cfg=None):
     """rest: a chain's later JOIN tables, whole on every rank.  outer: run the later
     RIGHT / FULL levels' protocol (cqgpu_join_outer_*, as cq_amd.dist.outer_sets):
     per level every rank's matched flags, OR-ed, handed back to every rank with rank
     0 emitting the records no rank matched"""
-    lh, ls = _shards(ldata, nranks, 1)
-    rh, rs = _shards(rdata, nranks, 2)
+    lh, ls = _shards(ldata, nranks, 1, cfg)
+    rh, rs = _shards(rdata, nranks, 2, cfg)
     routed = [[None, None] for _ in range(nranks)]
     keep = []
     for side, (hdr, sh) in enumerate(((lh, ls), (rh, rs))):
@@ -70,10 +70,11 @@ def _run(ast, ldata: bytes, rdata: bytes, nranks: int, rest=(), outer=True):
             rg = torch.cat([sg[ro[d]:ro[d + 1]] for _, sg, _, ro in sends])
             keep += [rb, rg]
             torch.cuda.synchronize()          # torch's copies before the library's stream reads them
-            routed[d][side] = cq_amd.table_from_routed(rb.data_ptr(), rb.numel(), rg.data_ptr(), rg.numel(), hdr)
+            routed[d][side] = cq_amd.table_from_routed(rb.data_ptr(), rb.numel(), rg.data_ptr(), rg.numel(), hdr,
+                                                       cfg)
             cq_amd.table_set_record_total(routed[d][side], total)
             cq_amd.table_set_key_stride(routed[d][side], nranks)
-    whole = [[cq_amd.Table.from_bytes(x) for x in rest] for _ in range(nranks)]
+    whole = [[cq_amd.Table.from_bytes(x, cfg=cfg) for x in rest] for _ in range(nranks)]
     sets = {}
 
     def apply(d, upto):                    # rank d's view of the sets of the levels below `upto`
@@ -216,6 +217,51 @@ def test_repartitioned_join(files, case, nranks):
         cq_amd.result_free(tp)
         tol = tolerant_columns(ast)
     compare(got, want, tol, f"{sql} @ {nranks} ranks")
+
+
+DIALECT = [   # ';' delimiter, "'" quote: quoted names holding the delimiter, doubled quotes
+    "SELECT u.role, COUNT(*), SUM(o.price), MAX(u.name) FROM '{L}' AS u JOIN '{R}' AS o "
+    "ON u.id = o.customer_id GROUP BY u.role",
+    "SELECT u.name, o.price FROM '{L}' AS u JOIN '{R}' AS o ON u.id = o.customer_id WHERE o.price > 900",
+    "SELECT o.quantity, COUNT(*), MIN(u.name) FROM '{L}' AS u RIGHT JOIN '{R}' AS o "
+    "ON u.id = o.customer_id GROUP BY o.quantity",
+]
+
+
+@pytest.mark.parametrize("nranks", [1, 3])
+@pytest.mark.parametrize("case", range(len(DIALECT)))
+def test_repartitioned_join_dialect(files, tmp_path, case, nranks):
+    """the repartition with another CSV dialect (delimiter ';', quote "'"): the route's
+    field projection and the routed tables keep the dialect's field split
+    (csv_reader.c:278-338) -- quoted names holding ';' and doubled quotes"""
+    data, _ = files
+    cfg = abi.csv_config(";", "'")
+
+    def conv(b: bytes, quote_col: int) -> bytes:
+        out = []
+        for i, ln in enumerate(b.decode().split("\n")):
+            f = ln.split(",")
+            if i > 0 and 0 <= quote_col < len(f) and f[quote_col]:
+                v = f[quote_col]
+                v = v + ";x" if i % 3 == 0 else (v + "''q" if i % 3 == 1 else v)
+                f[quote_col] = "'" + v + "'"
+            out.append(";".join(f))
+        return "\n".join(out).encode()
+    lb, rb = conv(data["du"], 1), conv(data["do"], -1)
+    paths = {}
+    for k, v in (("L", lb), ("R", rb)):
+        paths[k] = str(tmp_path / f"{k}.csv")
+        open(paths[k], "wb").write(v)
+    sql = DIALECT[case].replace("{L}", paths["L"]).replace("{R}", paths["R"])
+    want, unsup = cqtest.oracle_query(sql, cfg)
+    assert not unsup, sql
+    with cqtest.Parsed(sql) as ast:
+        tp = _run(ast, lb, rb, nranks, cfg=cfg)
+        assert tp, cq_amd.last_error()
+        got = abi.table_to_py(tp)
+        cq_amd.result_free(tp)
+        tol = tolerant_columns(ast)
+    compare(got, want, tol, f"{sql} @ {nranks} ranks (dialect ; ')")
 
 
 @pytest.mark.parametrize("nranks", [1, 2, 3, 5, 8])
