@@ -311,6 +311,21 @@ def routed_share_leg(n_total: int, nranks: int, steps: int, warmup: int, seed: i
         sends.append((sb, sg, np.concatenate([[0], np.cumsum(nb)]).astype(np.int64),
                       np.concatenate([[0], np.cumsum(nr)]).astype(np.int64)))
     route_s = time.perf_counter() - t0
+    # rank 0's share of the two input files (algorithmic bytes = file
+    # bytes): its routed rows as whole CSV records -- the route's plan with the field
+    # projection off; the shard it reads holds only the fields the plan needs
+    file_share = 0
+    old = os.environ.get("CQGPU_NO_ROUTE_PROJECT")
+    os.environ["CQGPU_NO_ROUTE_PROJECT"] = "1"
+    try:
+        for side, tab in enumerate((U, O)):
+            nb, _ = cq_amd.route_plan(ast, [U, O], side, nranks)
+            file_share += int(nb[0])
+    finally:
+        if old is None:
+            os.environ.pop("CQGPU_NO_ROUTE_PROJECT", None)
+        else:
+            os.environ["CQGPU_NO_ROUTE_PROJECT"] = old
     U.close()
     O.close()
     rank_rows = [int(sends[0][3][d + 1] - sends[0][3][d]) + int(sends[1][3][d + 1] - sends[1][3][d])
@@ -365,6 +380,7 @@ def routed_share_leg(n_total: int, nranks: int, steps: int, warmup: int, seed: i
             ok = False
             break
     return {"step_s": step_s, "kernel_ms": sum(ms) / len(ms), "rows": rank_rows[0], "bytes": rank_bytes[0],
+            "file_bytes": file_share,
             "rank_rows": rank_rows, "kinds": kinds, "verified": ok, "route_s": route_s, "gen_s": gen_s,
             "joined_pairs": int(cnt.sum())}
 

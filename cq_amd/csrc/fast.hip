@@ -851,8 +851,9 @@ __global__ __launch_bounds__(LT) void fast_kernel(const uint8_t* __restrict__ g,
                     const uint32_t m0 = len_mask(len, 0), m1 = len_mask(len, 1);
                     const uint32_t a0 = wd[u] & m0, a1 = wd1[u] & m1;
                     const uint32_t c0 = a0 & 0xFFu;
-                    const bool ok = (len - 1u < 8u) & !(is_digit(c0) | (c0 == '-') | (c0 == '+') | (c0 == '.')) &
-                                    ((low_bytes(a0, m0 & nk.k80, nk) | low_bytes(a1, m1 & nk.k80, nk)) == 0);
+                    const bool ok = (int)(len - 1u < 8u) &
+                                    (int)!(is_digit(c0) | (c0 == '-') | (c0 == '+') | (c0 == '.')) &
+                                    (int)((low_bytes(a0, m0 & nk.k80, nk) | low_bytes(a1, m1 & nk.k80, nk)) == 0);
                     const uint64_t x = ((uint64_t)__builtin_bswap32(a0) << 32) | __builtin_bswap32(a1);
                     const uint64_t ws = fp.wstr;
                     pass[u] = len == 0 ? pass_null : tt_result(wtt, x < ws ? -1 : (x > ws ? 1 : 0));
@@ -1153,12 +1154,10 @@ __global__ __launch_bounds__(LT) void fast_kernel(const uint8_t* __restrict__ g,
             }
         }
         const GroupTable& gt = tabs[TAB_GT];
-        int gi0 = -1;
         if (lane == 0) {
             GKey k;
             k.cls = GK_ALL; k.len = 0; k.w0 = 0; k.w1 = 0;
             const int gi = g_insert(gt, k, 0x12345678ULL, stats);
-            gi0 = gi;
             if (gi >= 0) {
                 if (c) atomicAdd(&gt.cnt[gi], c);
                 if (f != NOFIRST) {

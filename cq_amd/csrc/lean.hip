@@ -970,8 +970,9 @@ __global__ __launch_bounds__(LT) void lean_kernel(const uint8_t* __restrict__ g,
                         const uint32_t c0 = a0 & 0xFFu;
                         mask8(Rr.wfl, a0, a1);
                         const uint32_t f0 = len_mask(Rr.wfl, 0) & 0x80808080u, f1 = len_mask(Rr.wfl, 1) & 0x80808080u;
-                        const bool ok = (Rr.wfl - 1 < 8u) & !(is_digit(c0) | (c0 == '-') | (c0 == '+') | (c0 == '.')) &
-                                        ((low_bytes(a0, f0) | low_bytes(a1, f1)) == 0);
+                        const bool ok = (int)(Rr.wfl - 1 < 8u) &
+                                        (int)!(is_digit(c0) | (c0 == '-') | (c0 == '+') | (c0 == '.')) &
+                                        (int)((low_bytes(a0, f0) | low_bytes(a1, f1)) == 0);
                         const uint64_t x = bswap64(a0, a1);
                         if (ok) outcome[u] = tt_result(wtt, x < wstr ? -1 : (x > wstr ? 1 : 0));
                         typed |= ok;
