@@ -584,6 +584,43 @@ def test_route_runs_equal_sort(files, nranks, monkeypatch):
                     t.close()
 
 
+def test_route_long_records(monkeypatch):
+    """records whose 64-record wave spans more than the LDS stage (route.hip RP_CAP:
+    the projection and the scatter then read global memory lane by lane) and one record
+    of 2^25 bytes and more (the runs' byte sums take the 64-bit scan): the same bytes
+    through the destination runs and the sorted-order copy, projected and whole, and
+    the projection byte for byte as the field split finds it"""
+    rng = np.random.default_rng(11)
+    lines = [b"id,pad,v"]
+    for i in range(700):
+        pad = b"x" * (int(rng.integers(40, 220)) if i != 333 else (1 << 25) + 77)
+        lines.append(b"%d,%s,%d" % (int(rng.integers(0, 300)), pad, i * 3))
+    data = b"\n".join(lines) + b"\n"
+    small = b"id,w\n" + b"".join(b"%d,%d\n" % (i, i) for i in range(300))
+    recs = lines[1:]
+    for sql, keep in (("SELECT a.v, COUNT(*) FROM 'a' AS a JOIN 'b' AS b ON a.id = b.id GROUP BY a.v", {0, 2}),
+                      ("SELECT * FROM 'a' AS a JOIN 'b' AS b ON a.id = b.id", None)):
+        with cqtest.Parsed(sql) as ast:
+            tabs = (cq_amd.Table.from_bytes(data), cq_amd.Table.from_bytes(small))
+            try:
+                for nranks in (1, 5):
+                    got = []
+                    for sort in (False, True):
+                        if sort:
+                            monkeypatch.setenv("CQGPU_ROUTE_SORT", "1")
+                        else:
+                            monkeypatch.delenv("CQGPU_ROUTE_SORT", raising=False)
+                        nb, nr, out, gids = _routed_records(ast, tabs, 0, nranks, 0)
+                        got.append((nb, nr, out, gids.tolist()))
+                    assert got[0] == got[1], (sql, nranks)
+                    nb, nr, out, gids = got[0]
+                    want = [recs[i] if keep is None else _project(recs[i], keep, max(keep)) for i in gids]
+                    assert out == want, (sql, nranks)
+            finally:
+                for t in tabs:
+                    t.close()
+
+
 PROJ_LEFT = (b"id,name,age,role,note\n"
              b"1,ann,30,admin,x\n"
              b' 2 , "b,o""b" ,41, "ops, east" ,"q\n'      # an unclosed quote runs to the line end
