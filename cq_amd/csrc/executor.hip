@@ -111,6 +111,8 @@ hipError_t cq_launch_route_scatter(const uint8_t* g, const unsigned long long* r
                                    const uint32_t* len, uint32_t n, uint32_t nw, uint64_t end,
                                    const unsigned long long* cbase, const unsigned long long* bbase, uint64_t gid_base,
                                    uint8_t* out, unsigned long long* gids, hipStream_t s);
+hipError_t cq_launch_gid_narrow(const unsigned long long* in, uint64_t n, uint32_t* out, hipStream_t s);
+hipError_t cq_launch_gid_widen(const uint32_t* in, uint64_t n, unsigned long long* out, hipStream_t s);
 hipError_t cq_launch_outer_global(unsigned int* unm, uint32_t n, const uint8_t* gset, uint32_t emit, uint8_t* matched_out,
                                   hipStream_t s);
 hipError_t cq_launch_join_fill(const unsigned int* flags, const unsigned int* pos, uint32_t n, unsigned long long base,
@@ -7329,18 +7331,22 @@ void dist_join(DevCtx& c, DistComm& m, cq_node* q, cqgpu_table* const* tables, i
             bad = true;
             err = g_err;
         }
+        // the ids travel as 32 bits (total < 2^32 above): 4 bytes a record off the exchange
+        DevBuf sg32(std::max<uint64_t>(sr[N], 2) * 4), rg32(std::max<uint64_t>(rr[N], 2) * 4);
+        HIPCHECK(cq_launch_gid_narrow(sgids.as<unsigned long long>(), sr[N], sg32.as<uint32_t>(), c.stream));
         NCCLCHECK(ncclGroupStart());
         for (int d = 0; d < N; d++) {
             if (nb[d]) {
                 NCCLCHECK(ncclSend(sbytes.as<uint8_t>() + sb[d], nb[d], ncclUint8, d, m.comm, c.stream));
-                NCCLCHECK(ncclSend(sgids.as<uint64_t>() + sr[d], nr[d], ncclUint64, d, m.comm, c.stream));
+                NCCLCHECK(ncclSend(sg32.as<uint32_t>() + sr[d], nr[d], ncclUint32, d, m.comm, c.stream));
             }
             if (rb[d + 1] > rb[d]) {
                 NCCLCHECK(ncclRecv(rbytes.as<uint8_t>() + rb[d], rb[d + 1] - rb[d], ncclUint8, d, m.comm, c.stream));
-                NCCLCHECK(ncclRecv(rgids.as<uint64_t>() + rr[d], rr[d + 1] - rr[d], ncclUint64, d, m.comm, c.stream));
+                NCCLCHECK(ncclRecv(rg32.as<uint32_t>() + rr[d], rr[d + 1] - rr[d], ncclUint32, d, m.comm, c.stream));
             }
         }
         NCCLCHECK(ncclGroupEnd());
+        HIPCHECK(cq_launch_gid_widen(rg32.as<uint32_t>(), rr[N], rgids.as<unsigned long long>(), c.stream));
         const std::string& hdr = tables[side]->header_rec;
         cqgpu_table* t = bad ? nullptr
                              : cqgpu_table_from_routed(rbytes.p, rb[N], rgids.as<uint64_t>(), rr[N], tables[side]->cfg,

@@ -242,7 +242,7 @@ __global__ void route_copy_kernel(const uint8_t* __restrict__ g, const unsigned 
     }
 }
 
-// ---- the send buffer by destination runs (nranks <= RUN_MAXN).  The send buffer is
+// ---- the send buffer by destination runs (nranks <= 64: executor.hip route_plan).  The send buffer is
 // the records grouped by destination, file order within one; the 64 consecutive
 // records of a wave contribute one run per destination they hold.  route_runs_kernel
 // writes each (destination d, wave w) run's record and byte count at [d * nw + w]
@@ -251,8 +251,6 @@ __global__ void route_copy_kernel(const uint8_t* __restrict__ g, const unsigned 
 // plus the bytes of the run's records before it, and its global id at the run's
 // record base plus its rank in the run.  Every read is a file-order stream (no gather
 // through a sorted order); the writes are up to nranks contiguous runs per wave.
-constexpr uint32_t RUN_MAXN = 64;
-
 __device__ __forceinline__ unsigned long long wave_incl_u64(unsigned long long x, uint32_t lane) {
     for (int o = 1; o < 64; o <<= 1) {
         const unsigned long long y = __shfl_up(x, o, 64);
@@ -606,6 +604,25 @@ hipError_t cq_launch_route_scatter(const uint8_t* g, const unsigned long long* r
     if (!n) return hipSuccess;
     route_scatter_kernel<<<blocks((uint64_t)nw * 64, 256), 256, 0, s>>>(g, recs, dest, len, n, nw, end, cbase,
                                                                         bbase, gid_base, out, gids);
+    return hipGetLastError();
+}
+// the join exchange's record ids as 32 bits (every id < 2^32, checked by the caller)
+__global__ void gid_narrow_kernel(const unsigned long long* __restrict__ in, uint64_t n, uint32_t* __restrict__ out) {
+    const uint64_t i = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
+    if (i < n) out[i] = (uint32_t)in[i];
+}
+__global__ void gid_widen_kernel(const uint32_t* __restrict__ in, uint64_t n, unsigned long long* __restrict__ out) {
+    const uint64_t i = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
+    if (i < n) out[i] = in[i];
+}
+hipError_t cq_launch_gid_narrow(const unsigned long long* in, uint64_t n, uint32_t* out, hipStream_t s) {
+    if (!n) return hipSuccess;
+    gid_narrow_kernel<<<blocks(n, 256), 256, 0, s>>>(in, n, out);
+    return hipGetLastError();
+}
+hipError_t cq_launch_gid_widen(const uint32_t* in, uint64_t n, unsigned long long* out, hipStream_t s) {
+    if (!n) return hipSuccess;
+    gid_widen_kernel<<<blocks(n, 256), 256, 0, s>>>(in, n, out);
     return hipGetLastError();
 }
 hipError_t cq_launch_outer_global(unsigned int* unm, uint32_t n, const uint8_t* gset, uint32_t emit, uint8_t* matched_out,

@@ -218,7 +218,12 @@ int cqgpu_route_plan(cq_node* query_ast, cqgpu_table* const* tables, int ntables
 /* route_fill: writes the planned send buffer into device memory: records grouped
  * by destination rank (file order within a rank, each '\n'-terminated) into
  * dev_bytes, and their global record ids (gid_base + local record index) into
- * dev_gids.  gid_base = records of this side on lower ranks. */
+ * dev_gids.  gid_base = records of this side on lower ranks.  Each record carries
+ * only the fields the plan reads from this side (ON keys, WHERE, SELECT, GROUP BY,
+ * aggregates, HAVING / ORDER BY, a chain's later levels): every other field is
+ * empty with its delimiter kept, the record ends after its last needed field, and a
+ * record whose needed fields are all empty is a lone delimiter (environment
+ * CQGPU_NO_ROUTE_PROJECT=1: whole records). */
 int cqgpu_route_fill(cqgpu_table* t, uint64_t gid_base, void* dev_bytes, uint64_t* dev_gids);
 /* table over received records (device memory, copied) with their global ids and
  * the side's header record */
