@@ -242,15 +242,19 @@ __global__ void route_copy_kernel(const uint8_t* __restrict__ g, const unsigned 
     }
 }
 
-// ---- the send buffer by destination runs (nranks <= 64: executor.hip route_plan).  The send buffer is
-// the records grouped by destination, file order within one; the 64 consecutive
-// records of a wave contribute one run per destination they hold.  route_runs_kernel
+// ---- the send buffer by destination runs (nranks <= 64, executor.hip route_plan).
+// The send buffer is the records grouped by destination, file order within one; the
+// 64 consecutive records of a wave contribute one run per destination they hold.  route_runs_kernel
 // writes each (destination d, wave w) run's record and byte count at [d * nw + w]
 // (destination-major: one exclusive scan of each array gives every run's send-buffer
 // record and byte base), route_scatter_kernel puts each record at its run's byte base
 // plus the bytes of the run's records before it, and its global id at the run's
 // record base plus its rank in the run.  Every read is a file-order stream (no gather
 // through a sorted order); the writes are up to nranks contiguous runs per wave.
+
+// inclusive wave scans: 64-bit through the LDS crossbar, 32-bit by DPP row shifts /
+// broadcasts (the runs' byte sums when every record of the wave is under 2^25 bytes,
+// so 64 of them fit)
 __device__ __forceinline__ unsigned long long wave_incl_u64(unsigned long long x, uint32_t lane) {
     for (int o = 1; o < 64; o <<= 1) {
         const unsigned long long y = __shfl_up(x, o, 64);
@@ -258,8 +262,6 @@ __device__ __forceinline__ unsigned long long wave_incl_u64(unsigned long long x
     }
     return x;
 }
-// the same over 32 bits by DPP row shifts / broadcasts (no LDS crossbar): the runs'
-// byte sums when every record of the wave is under 2^25 bytes (64 of them fit)
 __device__ __forceinline__ uint32_t wave_incl_u32(uint32_t x) {
     x += (uint32_t)__builtin_amdgcn_update_dpp(0, (int)x, 0x111, 0xf, 0xf, true);   // row_shr:1
     x += (uint32_t)__builtin_amdgcn_update_dpp(0, (int)x, 0x112, 0xf, 0xf, true);   // row_shr:2
