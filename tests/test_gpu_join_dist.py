@@ -145,6 +145,7 @@ def files(tmp_path_factory):
     f["rl"] = ("role,dept,grade\n" + "".join(f"role_{i:02d},dept{i % 4},{i % 3}\n" for i in range(20))
                + "role_05,dept9,7\n,deptx,0\n").encode()
     f["qt"] = b"q,label\n0,lab0\n2,lab2\n1,lab1\n2,lab2b\n9,lab9\n"
+    f["ex"] = b"role,dept,grade\n"          # a later level's table with no records
     paths = {}
     for k, v in f.items():
         p = d / f"{k}.csv"
@@ -390,6 +391,11 @@ CHAINS = [
     (["rl", "qt"], "SELECT r.dept, q.label, u.name FROM '{L}' AS u JOIN '{R}' AS o ON u.id = o.customer_id "
                    "FULL JOIN '{X}' AS r ON u.role = r.role RIGHT JOIN '{Y}' AS q ON r.grade = q.q "
                    "ORDER BY q.label LIMIT 30 OFFSET 3"),
+    # ... whose table has no records: RIGHT keeps nothing, FULL every joined row
+    (["ex"], "SELECT COUNT(*), MIN(r.dept) FROM '{L}' AS u JOIN '{R}' AS o ON u.id = o.customer_id "
+             "RIGHT JOIN '{X}' AS r ON u.role = r.role"),
+    (["ex"], "SELECT r.dept, COUNT(*), SUM(o.price) FROM '{L}' AS u JOIN '{R}' AS o ON u.id = o.customer_id "
+             "FULL JOIN '{X}' AS r ON u.role = r.role GROUP BY r.dept"),
 ]
 
 
