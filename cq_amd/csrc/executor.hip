@@ -111,6 +111,9 @@ hipError_t cq_launch_route_scatter(const uint8_t* g, const unsigned long long* r
                                    const uint32_t* len, uint32_t n, uint32_t nw, uint64_t end,
                                    const unsigned long long* cbase, const unsigned long long* bbase, uint64_t gid_base,
                                    uint8_t* out, unsigned long long* gids, hipStream_t s);
+hipError_t cq_launch_pack_first_gid(uint8_t* pk, const unsigned int* count, uint32_t cap, uint32_t rec,
+                                    const unsigned long long* starts, unsigned long long n,
+                                    const unsigned long long* gids, hipStream_t s);
 hipError_t cq_launch_gid_narrow(const unsigned long long* in, uint64_t n, uint32_t* out, hipStream_t s);
 hipError_t cq_launch_gid_widen(const uint32_t* in, uint64_t n, unsigned long long* out, hipStream_t s);
 hipError_t cq_launch_outer_global(unsigned int* unm, uint32_t n, const uint8_t* gset, uint32_t emit, uint8_t* matched_out,
@@ -3467,6 +3470,13 @@ cq_table* run_fast_join(DevCtx& c, cq_node* q, Compiled& C, const cqgpu_table* L
     // the groups `fill` puts into an arena's table (raw tags when grouped) -> the result:
     // raw_merge / compact / finish / pack, one synchronisation; *fallback when the
     // flags at dflag ask for another path (nothing returned then)
+    // a STAR partial: the packed groups' first pairs mapped to global left ids on the
+    // device before the mailbox copy (route.hip pack_first_gid_kernel); `first_mapped`
+    // says the result holds ids
+    const unsigned long long* map_starts = nullptr;
+    const unsigned long long* map_gids = nullptr;
+    unsigned long long map_n = 0;
+    bool first_mapped = false;
     auto results = [&](const std::function<void(TableArena&)>& fill, const unsigned int* dflag, uint64_t records,
                        int kind, bool* fallback) -> cq_table* {
         *fallback = false;
@@ -3490,9 +3500,15 @@ cq_table* run_fast_join(DevCtx& c, cq_node* q, Compiled& C, const cqgpu_table* L
                                            (unsigned long long*)ofs.p));
                 HIPCHECK(cq_launch_finish_pack(L->g, L->n, A.out, (const unsigned long long*)ofs.p, A.out_count,
                                                cap_out, &FD, pk.p, A.stats, mail, c.stream));
+                if (map_starts) {
+                    HIPCHECK(cq_launch_pack_first_gid(pk.p, A.out_count, cap_out, 40u + 40u * (uint32_t)C.P.nacc,
+                                                      map_starts, map_n, map_gids, c.stream));
+                    first_mapped = true;
+                }
                 HIPCHECK(cq_launch_mail_copy(pk.p, A.out_count, cap_out, C.P.nacc, ncell, SB, mail + MAIL_HDR,
                                              c.stream));
             } else {
+                first_mapped = false;
                 HIPCHECK(cq_launch_compact(&A.gt, &C.P, A.out, A.out_count, cap_out, c.stream, nullptr));
                 HIPCHECK(cq_launch_finish(L->g, L->n, A.out, A.out_count, cap_out, &FD, dcells, dbytes, c.stream));
                 HIPCHECK(cq_launch_pack_result(A.out, A.out_count, cap_out, C.P.nacc, dcells, dbytes, ncell, SB,
@@ -3663,6 +3679,19 @@ cq_table* run_fast_join(DevCtx& c, cq_node* q, Compiled& C, const cqgpu_table* L
     if (!getenv("CQ_AMD_NO_STAR_JOIN")) {
         cqgpu_table* Lm = const_cast<cqgpu_table*>(L);
         bool no_part = getenv("CQ_AMD_NO_PART_PROBE") != nullptr;
+        if (part && !getenv("CQGPU_HOST_FIRST_IDS")) {
+            // the partial's first pairs become global left ids on the device: the left
+            // table's file-order record starts (once per table: it is immutable)
+            if (!Lm->rec_starts) {
+                std::unique_ptr<DevBuf> b(new DevBuf());
+                Lm->nrec_starts = all_records(c, L, *b);
+                Lm->rec_starts = std::move(b);
+            }
+            if (L->gids && L->ngids != Lm->nrec_starts) throw HipError{"routed table: record count differs from its ids"};
+            map_starts = Lm->rec_starts->as<unsigned long long>();
+            map_n = Lm->nrec_starts;
+            map_gids = L->gids;
+        }
         for (int round = 0; round < 3; round++) {
             uint64_t kmin = 0, kmax = 0, est = 0;
             const uint64_t S = L->key_stride ? L->key_stride : 1;
@@ -3786,7 +3815,21 @@ cq_table* run_fast_join(DevCtx& c, cq_node* q, Compiled& C, const cqgpu_table* L
                 PHASE("recs");
                 std::vector<unsigned long long> qo;
                 std::vector<size_t> qat;                 // (direct blob: where each first lives)
-                if (part->direct) {
+                if (first_mapped) {                      // ids already (pack_first_gid_kernel)
+                    auto check = [](unsigned long long f) {
+                        if (f != NOPOS && (f >> 32) == 0xFFFFFFFFull)
+                            throw HipError{"fused join partial: left id out of range"};
+                    };
+                    if (part->direct) {
+                        for (size_t at : part->first_at) {
+                            unsigned long long f;
+                            memcpy(&f, part->gblob.data() + at, 8);
+                            check(f);
+                        }
+                    } else {
+                        for (const HGroup& h : part->groups) check(h.first);
+                    }
+                } else if (part->direct) {
                     for (size_t at : part->first_at) {
                         unsigned long long f;
                         memcpy(&f, part->gblob.data() + at, 8);

@@ -608,6 +608,37 @@ hipError_t cq_launch_route_scatter(const uint8_t* g, const unsigned long long* r
                                                                         bbase, gid_base, out, gids);
     return hipGetLastError();
 }
+// A fused-join partial's packed groups (scan.hip pack layout: group i's record at
+// i * rec, its first pair's (left byte offset << 32) at byte 32), mapped in place
+// before the mailbox copy: each offset to its record's global id (offset_gid_kernel's
+// search over the file-order record starts), so the host reads ids, not offsets
+__global__ void pack_first_gid_kernel(uint8_t* __restrict__ pk, const unsigned int* __restrict__ count,
+                                      uint32_t cap, uint32_t rec, const unsigned long long* __restrict__ starts,
+                                      unsigned long long n, const unsigned long long* __restrict__ gids) {
+    const uint32_t i = blockIdx.x * blockDim.x + threadIdx.x;
+    const uint32_t ng = min(*count, cap);
+    if (i >= ng) return;
+    unsigned long long* f = (unsigned long long*)(pk + (size_t)i * rec + 32);
+    const unsigned long long v = *f;
+    if (v == ~0ull) return;                               // no first pair
+    const unsigned long long o = v >> 32;
+    unsigned long long lo = 0, hi = n;                    // first start > o
+    while (lo < hi) {
+        const unsigned long long mid = (lo + hi) >> 1;
+        if (starts[mid] <= o) lo = mid + 1;
+        else hi = mid;
+    }
+    const unsigned long long idx = lo ? lo - 1 : 0;
+    const unsigned long long gid = n == 0 ? 0xFFFFFFFFull : (gids ? gids[idx] : idx);
+    *f = (gid < 0xFFFFFFFFull ? gid : 0xFFFFFFFFull) << 32;   // (0xFFFFFFFF: out of range, the host refuses)
+}
+hipError_t cq_launch_pack_first_gid(uint8_t* pk, const unsigned int* count, uint32_t cap, uint32_t rec,
+                                    const unsigned long long* starts, unsigned long long n,
+                                    const unsigned long long* gids, hipStream_t s) {
+    if (!cap) return hipSuccess;
+    pack_first_gid_kernel<<<blocks(cap, 256), 256, 0, s>>>(pk, count, cap, rec, starts, n, gids);
+    return hipGetLastError();
+}
 // the join exchange's record ids as 32 bits (every id < 2^32, checked by the caller)
 __global__ void gid_narrow_kernel(const unsigned long long* __restrict__ in, uint64_t n, uint32_t* __restrict__ out) {
     const uint64_t i = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
