@@ -7419,13 +7419,31 @@ void dist_join(DevCtx& c, DistComm& m, cq_node* q, cqgpu_table* const* tables, i
         if (!jn || jn->kind != CQ_N_JOIN || (jn->u.join.kind != CQ_JOIN_RIGHT && jn->u.join.kind != CQ_JOIN_FULL))
             continue;
         cqgpu_table* T = tables[1 + j];           // whole on every rank: the same record count
-        if (!T) throw PeerFail{"dist_join: a chain table is missing"};
-        if (!T->rec_starts) {
-            std::unique_ptr<DevBuf> b(new DevBuf());
-            T->nrec_starts = all_records(c, T, *b);
-            T->rec_starts = std::move(b);
+        uint64_t nrec = 0;
+        if (!T) {
+            bad = true;                           // (still in every collective below)
+            err = "dist_join: a chain table is missing";
+        } else {
+            if (!T->rec_starts) {
+                std::unique_ptr<DevBuf> b(new DevBuf());
+                T->nrec_starts = all_records(c, T, *b);
+                T->rec_starts = std::move(b);
+            }
+            nrec = T->nrec_starts;
         }
-        const uint64_t nrec = T->nrec_starts;
+        {                                         // every rank sizes the flags alike
+            DevBuf dn(8);
+            HIPCHECK(hipMemcpyAsync(dn.p, &nrec, 8, hipMemcpyHostToDevice, c.stream));
+            NCCLCHECK(ncclAllReduce(dn.p, dn.p, 1, ncclUint64, ncclMax, m.comm, c.stream));
+            uint64_t mx = 0;
+            HIPCHECK(hipMemcpyAsync(&mx, dn.p, 8, hipMemcpyDeviceToHost, c.stream));
+            HIPCHECK(hipStreamSynchronize(c.stream));
+            if (mx != nrec && !bad) {
+                bad = true;
+                err = "dist_join: a chain table's record count differs between ranks";
+            }
+            nrec = mx;
+        }
         std::vector<uint8_t> flags(nrec, 0);
         if (!bad) {
             const uint8_t* fl = nullptr;
