@@ -327,6 +327,12 @@ def outer_sets(ast, tables, nlevels: int, comm) -> None:
         agree(err, comm)
         if flags is None:                  # (decided by the plan alone: the same on every rank)
             continue
+        # the level's table is whole on every rank: the same record count, checked
+        # before the byte all-reduce (mismatched sizes would not reduce)
+        n = torch.tensor([len(flags), -len(flags)], dtype=torch.int64, device=comm)
+        dist.all_reduce(n, op=dist.ReduceOp.MAX)
+        if int(n[0]) != -int(n[1]):
+            raise PeerFailure(f"rank {dist.get_rank()}: a chain table's record count differs between ranks")
         t = torch.frombuffer(bytearray(flags), dtype=torch.uint8).to(comm) if flags else \
             torch.zeros(0, dtype=torch.uint8, device=comm)
         if t.numel():

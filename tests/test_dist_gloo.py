@@ -325,3 +325,42 @@ def test_outer_sets_gloo(world):
     want = bytes(1 if any(i % (r + 2) == 0 for r in range(world)) else 0 for i in range(23))
     for rank, calls in res.items():
         assert calls == [("clear",), ("matched", 1), ("set", 1, want, rank == 0), ("matched", 2)], (rank, calls)
+
+
+def _omworker(rank, world, port, q):
+    """dist.outer_sets where rank 1's level table holds fewer records"""
+    import torch.distributed as dist
+    import cq_amd
+    from cq_amd import dist as cd
+    os.environ["MASTER_ADDR"] = "127.0.0.1"
+    os.environ["MASTER_PORT"] = str(port)
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    try:
+        cq_amd.join_outer_matched = lambda ast, tables, level: bytes(23 if rank != 1 else 20)
+        cq_amd.join_outer_set = lambda level, flags, emit: None
+        cq_amd.join_outer_clear = lambda: None
+        try:
+            cd.outer_sets(None, [], 1, "cpu")
+            q.put((rank, "no error"))
+        except cd.PeerFailure as e:
+            q.put((rank, str(e)))
+    finally:
+        dist.destroy_process_group()
+
+
+def test_outer_sets_size_mismatch_gloo():
+    """flags of different lengths (a chain table that differs between ranks) are a
+    PeerFailure on every rank, never a mismatched all-reduce"""
+    world = 2
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    port = _free_port()
+    procs = [ctx.Process(target=_omworker, args=(r, world, port, q)) for r in range(world)]
+    for p in procs:
+        p.start()
+    res = dict(q.get(timeout=120) for _ in range(world))
+    for p in procs:
+        p.join(timeout=60)
+        assert p.exitcode == 0
+    for rank, msg in res.items():
+        assert "record count differs" in msg, (rank, msg)
