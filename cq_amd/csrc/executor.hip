@@ -716,7 +716,9 @@ cqgpu_table* upload(const uint8_t* host, size_t n, cq_csv_config cfg, uint64_t b
     // while the previous group's chunks are in flight to the device
     const size_t CH = 32ull << 20;
     const unsigned hw = std::max(1u, std::thread::hardware_concurrency());
-    const size_t P = std::min<size_t>(8, std::max(1u, hw / 2));
+    const char* up_env = getenv("CQGPU_UPLOAD_THREADS");
+    const size_t P = up_env ? (size_t)std::min(std::max(atoi(up_env), 1), 64)
+                            : std::min<size_t>(8, std::max(1u, hw / 2));
     const size_t nch = (n + CH - 1) / CH;
     uint8_t* st = (uint8_t*)pinned(c, 2 * P * std::min(CH, std::max<size_t>(n, 1)));
     const size_t slot = std::min(CH, std::max<size_t>(n, 1));
