@@ -19,6 +19,11 @@ LIB_PATH = os.environ.get("CQ_AMD_LIB") or os.path.join(HERE, "lib", "libcqgpu.s
 _lib = None
 
 
+# cqgpu_coll_fn (include/cqgpu.h): the test backend's collective callback
+COLL_FN = C.CFUNCTYPE(C.c_int, C.c_void_p, C.c_int, C.c_int, C.c_int, C.c_int, C.c_void_p, C.c_void_p,
+                      C.c_uint64)
+
+
 class Coll(C.Structure):
     """cqgpu_coll: the next collective of the device-side merge (cqgpu.h)"""
     _fields_ = [("op", C.c_int32), ("pad", C.c_int32), ("count", C.c_uint64)]
@@ -109,6 +114,8 @@ def lib():
         L.cqgpu_comm_init.restype = C.c_int
         L.cqgpu_comm_init.argtypes = [vp, C.c_int, C.c_int]
         L.cqgpu_comm_destroy.argtypes = []
+        L.cqgpu_comm_init_host.restype = C.c_int
+        L.cqgpu_comm_init_host.argtypes = [C.c_int, C.c_int, COLL_FN, vp]
         L.cqgpu_dist_query.restype = TP
         L.cqgpu_dist_query.argtypes = [C.POINTER(abi.Node), vp, C.POINTER(C.c_int), C.POINTER(C.c_int)]
         L.cqgpu_dist_join.restype = TP

@@ -6830,8 +6830,141 @@ namespace {
         if (r_ != ncclSuccess) throw HipError{std::string(#x) + ": " + ncclGetErrorString(r_)}; \
     } while (0)
 
-struct DistComm {
+// The collectives the N > 1 step issues, behind one table.  The product backend is
+// RCCL over the library's own communicator (RcclColl).  The test backend (HostColl,
+// cqgpu_comm_init_host) stages every buffer through host memory and hands it to a
+// caller-supplied function -- the tests run the very same dist_gm / dist_dense /
+// dist_blob / dist_join code at world size 2 and 3 over torch.distributed gloo, with
+// several processes sharing one GPU (RCCL refuses two ranks on one device).
+enum CollDt { CD_U8 = 0, CD_U32 = 1, CD_U64 = 2, CD_I64 = 3, CD_F64 = 4 };
+enum CollRed { CR_SUM = 0, CR_MIN = 1, CR_MAX = 2 };
+size_t coll_elem(CollDt t) { return t == CD_U8 ? 1 : (t == CD_U32 ? 4 : 8); }
+
+struct Coll {
+    virtual ~Coll() {}
+    // in place
+    virtual void all_reduce(void* buf, size_t n, CollDt t, CollRed o, hipStream_t s) = 0;
+    // recv = every rank's n elements of send, in rank order (send may lie inside recv)
+    virtual void all_gather(const void* send, void* recv, size_t n, CollDt t, hipStream_t s) = 0;
+    // in place; the result on `root` only
+    virtual void reduce(void* buf, size_t n, CollDt t, CollRed o, int root, hipStream_t s) = 0;
+    // root's send into every rank's recv
+    virtual void broadcast(const void* send, void* recv, size_t n, CollDt t, int root, hipStream_t s) = 0;
+    // point to point between group_start and group_end (all of one group run together)
+    virtual void group_start() = 0;
+    virtual void send(const void* buf, size_t n, CollDt t, int peer, hipStream_t s) = 0;
+    virtual void recv(void* buf, size_t n, CollDt t, int peer, hipStream_t s) = 0;
+    virtual void group_end(hipStream_t s) = 0;
+};
+
+ncclDataType_t nccl_dt(CollDt t) {
+    switch (t) {
+        case CD_U8: return ncclUint8;
+        case CD_U32: return ncclUint32;
+        case CD_U64: return ncclUint64;
+        case CD_I64: return ncclInt64;
+        default: return ncclFloat64;
+    }
+}
+ncclRedOp_t nccl_op(CollRed o) { return o == CR_SUM ? ncclSum : (o == CR_MIN ? ncclMin : ncclMax); }
+
+struct RcclColl : Coll {
     ncclComm_t comm = nullptr;
+    ~RcclColl() override {
+        if (comm) (void)ncclCommDestroy(comm);
+    }
+    void all_reduce(void* buf, size_t n, CollDt t, CollRed o, hipStream_t s) override {
+        NCCLCHECK(ncclAllReduce(buf, buf, n, nccl_dt(t), nccl_op(o), comm, s));
+    }
+    void all_gather(const void* send, void* recv, size_t n, CollDt t, hipStream_t s) override {
+        NCCLCHECK(ncclAllGather(send, recv, n, nccl_dt(t), comm, s));
+    }
+    void reduce(void* buf, size_t n, CollDt t, CollRed o, int root, hipStream_t s) override {
+        NCCLCHECK(ncclReduce(buf, buf, n, nccl_dt(t), nccl_op(o), root, comm, s));
+    }
+    void broadcast(const void* send, void* recv, size_t n, CollDt t, int root, hipStream_t s) override {
+        NCCLCHECK(ncclBroadcast(send, recv, n, nccl_dt(t), root, comm, s));
+    }
+    void group_start() override { NCCLCHECK(ncclGroupStart()); }
+    void send(const void* buf, size_t n, CollDt t, int peer, hipStream_t s) override {
+        NCCLCHECK(ncclSend(buf, n, nccl_dt(t), peer, comm, s));
+    }
+    void recv(void* buf, size_t n, CollDt t, int peer, hipStream_t s) override {
+        NCCLCHECK(ncclRecv(buf, n, nccl_dt(t), peer, comm, s));
+    }
+    void group_end(hipStream_t) override { NCCLCHECK(ncclGroupEnd()); }
+};
+
+// test backend: device buffers staged through host memory, each collective one call of
+// the caller's function (cqgpu.h cqgpu_coll_fn), synchronous on the library's stream
+struct HostColl : Coll {
+    cqgpu_coll_fn fn = nullptr;
+    void* user = nullptr;
+    int world = 1;
+    struct Pending {
+        void* dev;
+        std::vector<uint8_t> host;
+    };
+    std::vector<std::vector<uint8_t>> sends;   // alive until group_end
+    std::vector<Pending> recvs;
+    void call(int op, CollDt t, CollRed o, int peer, const void* sb, void* rb, size_t n) {
+        if (fn(user, op, (int)t, (int)o, peer, sb, rb, (uint64_t)n) != 0)
+            throw HipError{"host collective backend: operation " + std::to_string(op) + " failed"};
+    }
+    std::vector<uint8_t> down(const void* dev, size_t bytes, hipStream_t s) {
+        std::vector<uint8_t> h(std::max<size_t>(bytes, 1));
+        if (bytes) HIPCHECK(hipMemcpyAsync(h.data(), dev, bytes, hipMemcpyDeviceToHost, s));
+        HIPCHECK(hipStreamSynchronize(s));
+        return h;
+    }
+    void up(void* dev, const uint8_t* h, size_t bytes, hipStream_t s) {
+        if (bytes) HIPCHECK(hipMemcpyAsync(dev, h, bytes, hipMemcpyHostToDevice, s));
+        HIPCHECK(hipStreamSynchronize(s));
+    }
+    void all_reduce(void* buf, size_t n, CollDt t, CollRed o, hipStream_t s) override {
+        std::vector<uint8_t> h = down(buf, n * coll_elem(t), s);
+        call(CQGPU_HC_ALLREDUCE, t, o, -1, h.data(), h.data(), n);
+        up(buf, h.data(), n * coll_elem(t), s);
+    }
+    void all_gather(const void* send, void* recv, size_t n, CollDt t, hipStream_t s) override {
+        const size_t b = n * coll_elem(t);
+        std::vector<uint8_t> h = down(send, b, s), r(std::max<size_t>(b * world, 1));
+        call(CQGPU_HC_ALLGATHER, t, CR_SUM, -1, h.data(), r.data(), n);
+        up(recv, r.data(), b * world, s);
+    }
+    void reduce(void* buf, size_t n, CollDt t, CollRed o, int root, hipStream_t s) override {
+        std::vector<uint8_t> h = down(buf, n * coll_elem(t), s);
+        call(CQGPU_HC_REDUCE, t, o, root, h.data(), h.data(), n);
+        up(buf, h.data(), n * coll_elem(t), s);
+    }
+    void broadcast(const void* send, void* recv, size_t n, CollDt t, int root, hipStream_t s) override {
+        std::vector<uint8_t> h = down(send ? send : recv, n * coll_elem(t), s);
+        call(CQGPU_HC_BROADCAST, t, CR_SUM, root, h.data(), h.data(), n);
+        up(recv, h.data(), n * coll_elem(t), s);
+    }
+    void group_start() override {
+        sends.clear();
+        recvs.clear();
+    }
+    void send(const void* buf, size_t n, CollDt t, int peer, hipStream_t s) override {
+        sends.push_back(down(buf, n * coll_elem(t), s));
+        call(CQGPU_HC_SEND, t, CR_SUM, peer, sends.back().data(), nullptr, n);
+    }
+    void recv(void* buf, size_t n, CollDt t, int peer, hipStream_t s) override {
+        recvs.push_back(Pending{buf, std::vector<uint8_t>(std::max<size_t>(n * coll_elem(t), 1))});
+        call(CQGPU_HC_RECV, t, CR_SUM, peer, nullptr, recvs.back().host.data(), n);
+        recvs.back().host.resize(n * coll_elem(t));
+    }
+    void group_end(hipStream_t s) override {
+        call(CQGPU_HC_GROUP_END, CD_U8, CR_SUM, -1, nullptr, nullptr, 0);
+        for (Pending& p : recvs) up(p.dev, p.host.data(), p.host.size(), s);
+        sends.clear();
+        recvs.clear();
+    }
+};
+
+struct DistComm {
+    std::unique_ptr<Coll> be;            // RcclColl, or HostColl in the tests
     int rank = 0, world = 1;
 };
 DistComm g_comm[64];
@@ -6840,7 +6973,7 @@ DistComm& dist_comm() {
     int dev = 0;
     HIPCHECK(hipGetDevice(&dev));
     DistComm& m = g_comm[dev & 63];
-    if (!m.comm) throw HipError{"dist_query: no communicator on this device (cqgpu_comm_init)"};
+    if (!m.be) throw HipError{"dist_query: no communicator on this device (cqgpu_comm_init)"};
     return m;
 }
 
@@ -6904,7 +7037,7 @@ bool agree_any(DevCtx& c, DistComm& m, bool bad) {
     b.hword[0] = bad ? 1u : 0u;
     uint32_t* dw = b.word.as<uint32_t>();
     HIPCHECK(hipMemcpyAsync(dw, b.hword, 4, hipMemcpyHostToDevice, c.stream));
-    NCCLCHECK(ncclAllReduce(dw, dw, 1, ncclUint32, ncclMax, m.comm, c.stream));
+    m.be->all_reduce(dw, 1, CD_U32, CR_MAX, c.stream);
     HIPCHECK(hipMemcpyAsync(b.hword + 1, dw, 4, hipMemcpyDeviceToHost, c.stream));
     HIPCHECK(hipStreamSynchronize(c.stream));
     return b.hword[1] != 0;
@@ -6914,7 +7047,7 @@ bool agree_any(DevCtx& c, DistComm& m, bool bad) {
 uint32_t bcast_status(DevCtx& c, DistComm& m, const uint32_t* dsrc) {
     DistBufs& b = dist_bufs();
     uint32_t* dw = b.word.as<uint32_t>() + 4;
-    NCCLCHECK(ncclBroadcast(m.rank == 0 ? (const void*)dsrc : (const void*)dw, dw, 1, ncclUint32, 0, m.comm, c.stream));
+    m.be->broadcast(m.rank == 0 ? (const void*)dsrc : (const void*)dw, dw, 1, CD_U32, 0, c.stream);
     HIPCHECK(hipMemcpyAsync(b.hword + 2, dw, 4, hipMemcpyDeviceToHost, c.stream));
     HIPCHECK(hipStreamSynchronize(c.stream));
     return b.hword[2];
@@ -7064,13 +7197,13 @@ uint32_t dist_gm(DevCtx& c, DistComm& m, cq_node* q, const cqgpu_table* t, const
         h.status = GM_FAILED;
         HIPCHECK(hipMemcpyAsync(dst, &h, GM_HDR, hipMemcpyHostToDevice, c.stream));
     }
-    NCCLCHECK(ncclGroupStart());
+    m.be->group_start();
     if (m.rank == 0) {
-        for (uint32_t r = 1; r < N; r++) NCCLCHECK(ncclRecv(recv + r * B, B, ncclUint8, (int)r, m.comm, c.stream));
+        for (uint32_t r = 1; r < N; r++) m.be->recv(recv + r * B, B, CD_U8, (int)r, c.stream);
     } else {
-        NCCLCHECK(ncclSend(dst, B, ncclUint8, 0, m.comm, c.stream));
+        m.be->send(dst, B, CD_U8, 0, c.stream);
     }
-    NCCLCHECK(ncclGroupEnd());
+    m.be->group_end(c.stream);
     uint32_t fin = GM_OK;                               // rank 0: the final status
     std::string rerr;
     if (m.rank == 0) {
@@ -7140,7 +7273,7 @@ bool allgather_var(DevCtx& c, DistComm& m, const void* buf, uint64_t n, bool bad
     uint64_t* dp = pair.as<uint64_t>();
     uint64_t mine[2] = {bad ? 0 : n, bad ? 1ull : 0ull};
     HIPCHECK(hipMemcpyAsync(dp + 2 * N, mine, 16, hipMemcpyHostToDevice, c.stream));
-    NCCLCHECK(ncclAllGather(dp + 2 * N, dp, 2, ncclUint64, m.comm, c.stream));
+    m.be->all_gather(dp + 2 * N, dp, 2, CD_U64, c.stream);
     std::vector<uint64_t> all((size_t)2 * N);
     HIPCHECK(hipMemcpyAsync(all.data(), dp, all.size() * 8, hipMemcpyDeviceToHost, c.stream));
     HIPCHECK(hipStreamSynchronize(c.stream));
@@ -7156,7 +7289,7 @@ bool allgather_var(DevCtx& c, DistComm& m, const void* buf, uint64_t n, bool bad
     if (any) return false;
     DevBuf pad(mx), gathered(mx * N);
     if (n) HIPCHECK(hipMemcpyAsync(pad.p, buf, n, hipMemcpyDeviceToDevice, c.stream));
-    NCCLCHECK(ncclAllGather(pad.p, gathered.p, mx, ncclUint8, m.comm, c.stream));
+    m.be->all_gather(pad.p, gathered.p, mx, CD_U8, c.stream);
     DevBuf cat(std::max<uint64_t>(tot, 16));
     uint64_t at = 0;
     for (int r = 0; r < N; r++) {
@@ -7184,7 +7317,7 @@ int dist_dense(DevCtx& c, DistComm& m, cq_node* q, cqgpu_table* t, cq_table** re
         b.hword[1] = inel ? 1u : 0u;
         uint32_t* dw = b.word.as<uint32_t>() + 8;
         HIPCHECK(hipMemcpyAsync(dw, b.hword, 8, hipMemcpyHostToDevice, c.stream));
-        NCCLCHECK(ncclAllReduce(dw, dw, 2, ncclUint32, ncclMax, m.comm, c.stream));
+        m.be->all_reduce(dw, 2, CD_U32, CR_MAX, c.stream);
         HIPCHECK(hipMemcpyAsync(b.hword + 4, dw, 8, hipMemcpyDeviceToHost, c.stream));
         HIPCHECK(hipStreamSynchronize(c.stream));
         if (b.hword[4]) {
@@ -7231,13 +7364,11 @@ int dist_dense(DevCtx& c, DistComm& m, cq_node* q, cqgpu_table* t, cq_table** re
             have_sizes = true;
         } else {
             if (nx.count) {
-                const ncclDataType_t ty = (nx.op == COLL_ALLREDUCE_SUM_F64 || nx.op == COLL_REDUCE_SUM_F64) ? ncclFloat64
-                                                                                                           : ncclInt64;
+                const CollDt ty = (nx.op == COLL_ALLREDUCE_SUM_F64 || nx.op == COLL_REDUCE_SUM_F64) ? CD_F64 : CD_I64;
                 if (nx.op == COLL_ALLREDUCE_MIN_I64 || nx.op == COLL_ALLREDUCE_SUM_F64)
-                    NCCLCHECK(ncclAllReduce(buf.p, buf.p, nx.count, ty, nx.op == COLL_ALLREDUCE_MIN_I64 ? ncclMin : ncclSum,
-                                            m.comm, c.stream));
+                    m.be->all_reduce(buf.p, nx.count, ty, nx.op == COLL_ALLREDUCE_MIN_I64 ? CR_MIN : CR_SUM, c.stream);
                 else
-                    NCCLCHECK(ncclReduce(buf.p, buf.p, nx.count, ty, ncclSum, 0, m.comm, c.stream));
+                    m.be->reduce(buf.p, nx.count, ty, CR_SUM, 0, c.stream);
             }
             std::swap(result.p, buf.p);
         }
@@ -7273,7 +7404,7 @@ void dist_blob(DevCtx& c, DistComm& m, cq_node* q, cqgpu_table* const* tabs, int
     uint64_t* dp = pair.as<uint64_t>();
     uint64_t mine[2] = {bad ? 0 : (uint64_t)n, bad ? 1ull : 0ull};
     HIPCHECK(hipMemcpyAsync(dp + 2 * N, mine, 16, hipMemcpyHostToDevice, c.stream));
-    NCCLCHECK(ncclAllGather(dp + 2 * N, dp, 2, ncclUint64, m.comm, c.stream));
+    m.be->all_gather(dp + 2 * N, dp, 2, CD_U64, c.stream);
     std::vector<uint64_t> all((size_t)2 * N);
     HIPCHECK(hipMemcpyAsync(all.data(), dp, all.size() * 8, hipMemcpyDeviceToHost, c.stream));
     if (n) HIPCHECK(hipMemcpyAsync(dblob.p, blob, n, hipMemcpyHostToDevice, c.stream));
@@ -7283,14 +7414,14 @@ void dist_blob(DevCtx& c, DistComm& m, cq_node* q, cqgpu_table* const* tabs, int
     std::vector<uint64_t> off(N + 1, 0);
     for (int r = 0; r < N; r++) off[r + 1] = off[r] + all[2 * r];
     DevBuf gathered(m.rank == 0 ? std::max<uint64_t>(off[N], 16) : 16);
-    NCCLCHECK(ncclGroupStart());
+    m.be->group_start();
     if (m.rank == 0) {
         for (int r = 1; r < N; r++)
-            if (all[2 * r]) NCCLCHECK(ncclRecv(gathered.as<uint8_t>() + off[r], all[2 * r], ncclUint8, r, m.comm, c.stream));
+            if (all[2 * r]) m.be->recv(gathered.as<uint8_t>() + off[r], all[2 * r], CD_U8, r, c.stream);
     } else {
-        NCCLCHECK(ncclSend(dblob.p, n, ncclUint8, 0, m.comm, c.stream));
+        m.be->send(dblob.p, n, CD_U8, 0, c.stream);
     }
-    NCCLCHECK(ncclGroupEnd());
+    m.be->group_end(c.stream);
     DistBufs& b = dist_bufs();
     std::string rerr;
     if (m.rank == 0) {
@@ -7343,7 +7474,7 @@ void dist_join(DevCtx& c, DistComm& m, cq_node* q, cqgpu_table* const* tables, i
             DevBuf dc(W * 8 * (N + 1));
             uint64_t* dp = dc.as<uint64_t>();
             HIPCHECK(hipMemcpyAsync(dp + W * N, mine.data(), W * 8, hipMemcpyHostToDevice, c.stream));
-            NCCLCHECK(ncclAllGather(dp + W * N, dp, W, ncclUint64, m.comm, c.stream));
+            m.be->all_gather(dp + W * N, dp, W, CD_U64, c.stream);
             HIPCHECK(hipMemcpyAsync(all.data(), dp, W * N * 8, hipMemcpyDeviceToHost, c.stream));
             HIPCHECK(hipStreamSynchronize(c.stream));
         }
@@ -7368,38 +7499,67 @@ void dist_join(DevCtx& c, DistComm& m, cq_node* q, cqgpu_table* const* tables, i
             rr[d + 1] = rr[d] + all[(size_t)d * W + N + m.rank];
         }
         if (total >= (1ull << 32)) throw PeerFail{"dist_join: 2^32 or more records on a join side"};   // (every rank)
-        DevBuf sbytes(std::max<uint64_t>(sb[N], 16)), sgids(std::max<uint64_t>(sr[N], 2) * 8);
-        DevBuf rbytes(std::max<uint64_t>(rb[N], 16)), rgids(std::max<uint64_t>(rr[N], 2) * 8);
-        // a local failure from here on still takes part in every collective (the sizes are
-        // agreed) and is reported by the next agreement: side 1's count gather or dist_blob's
-        if (cqgpu_route_fill(tables[side], base, sbytes.p, sgids.as<uint64_t>()) != 0) {
+        // every buffer sized by the agreed counts, allocated and filled under one try:
+        // a rank that fails here (a receive side sized by key skew can run out of
+        // memory) says so in one agreement BEFORE the grouped send / recv, so no rank
+        // is left waiting in a transfer its peer never posts
+        DevBuf sbytes, sgids, rbytes, rgids, sg32, rg32;
+        try {
+            if (getenv("CQGPU_TEST_DIST_FAIL_ALLOC"))           // test knob: this rank's allocation fails
+                throw HipError{"dist_join: injected exchange allocation failure (CQGPU_TEST_DIST_FAIL_ALLOC)"};
+            DevBuf a(std::max<uint64_t>(sb[N], 16)), b(std::max<uint64_t>(sr[N], 2) * 8);
+            DevBuf e(std::max<uint64_t>(rb[N], 16)), f(std::max<uint64_t>(rr[N], 2) * 8);
+            // the ids travel as 32 bits (total < 2^32 above): 4 bytes a record off the exchange
+            DevBuf g(std::max<uint64_t>(sr[N], 2) * 4), h(std::max<uint64_t>(rr[N], 2) * 4);
+            std::swap(sbytes.p, a.p);
+            std::swap(sgids.p, b.p);
+            std::swap(rbytes.p, e.p);
+            std::swap(rgids.p, f.p);
+            std::swap(sg32.p, g.p);
+            std::swap(rg32.p, h.p);
+            if (cqgpu_route_fill(tables[side], base, sbytes.p, sgids.as<uint64_t>()) != 0) throw HipError{g_err};
+            HIPCHECK(cq_launch_gid_narrow(sgids.as<unsigned long long>(), sr[N], sg32.as<uint32_t>(), c.stream));
+        } catch (HipError& e) {
             bad = true;
-            err = g_err;
+            err = e.msg;
+        } catch (std::exception& e) {
+            bad = true;
+            err = e.what();
         }
-        // the ids travel as 32 bits (total < 2^32 above): 4 bytes a record off the exchange
-        DevBuf sg32(std::max<uint64_t>(sr[N], 2) * 4), rg32(std::max<uint64_t>(rr[N], 2) * 4);
-        HIPCHECK(cq_launch_gid_narrow(sgids.as<unsigned long long>(), sr[N], sg32.as<uint32_t>(), c.stream));
-        NCCLCHECK(ncclGroupStart());
+        (void)hipGetLastError();
+        if (agree_any(c, m, bad)) {
+            if (tables[side]) tables[side]->route.reset();
+            throw PeerFail{bad ? err : std::string("a peer rank failed")};
+        }
+        m.be->group_start();
         for (int d = 0; d < N; d++) {
             if (nb[d]) {
-                NCCLCHECK(ncclSend(sbytes.as<uint8_t>() + sb[d], nb[d], ncclUint8, d, m.comm, c.stream));
-                NCCLCHECK(ncclSend(sg32.as<uint32_t>() + sr[d], nr[d], ncclUint32, d, m.comm, c.stream));
+                m.be->send(sbytes.as<uint8_t>() + sb[d], nb[d], CD_U8, d, c.stream);
+                m.be->send(sg32.as<uint32_t>() + sr[d], nr[d], CD_U32, d, c.stream);
             }
             if (rb[d + 1] > rb[d]) {
-                NCCLCHECK(ncclRecv(rbytes.as<uint8_t>() + rb[d], rb[d + 1] - rb[d], ncclUint8, d, m.comm, c.stream));
-                NCCLCHECK(ncclRecv(rg32.as<uint32_t>() + rr[d], rr[d + 1] - rr[d], ncclUint32, d, m.comm, c.stream));
+                m.be->recv(rbytes.as<uint8_t>() + rb[d], rb[d + 1] - rb[d], CD_U8, d, c.stream);
+                m.be->recv(rg32.as<uint32_t>() + rr[d], rr[d + 1] - rr[d], CD_U32, d, c.stream);
             }
         }
-        NCCLCHECK(ncclGroupEnd());
-        HIPCHECK(cq_launch_gid_widen(rg32.as<uint32_t>(), rr[N], rgids.as<unsigned long long>(), c.stream));
-        const std::string& hdr = tables[side]->header_rec;
-        cqgpu_table* t = bad ? nullptr
-                             : cqgpu_table_from_routed(rbytes.p, rb[N], rgids.as<uint64_t>(), rr[N], tables[side]->cfg,
-                                                       hdr.data(), hdr.size());
-        if (!t && !bad) {
+        m.be->group_end(c.stream);
+        // a local failure from here on is reported by the next agreement (side 1's count
+        // gather, the outer levels' agreement or dist_blob's size gather)
+        cqgpu_table* t = nullptr;
+        try {
+            HIPCHECK(cq_launch_gid_widen(rg32.as<uint32_t>(), rr[N], rgids.as<unsigned long long>(), c.stream));
+            const std::string& hdr = tables[side]->header_rec;
+            t = cqgpu_table_from_routed(rbytes.p, rb[N], rgids.as<uint64_t>(), rr[N], tables[side]->cfg, hdr.data(),
+                                        hdr.size());
+            if (!t) throw HipError{g_err};
+        } catch (HipError& e) {
             bad = true;
-            err = g_err;
+            err = e.msg;
+        } catch (std::exception& e) {
+            bad = true;
+            err = e.what();
         }
+        (void)hipGetLastError();
         routed.emplace_back(t);
         if (t) {
             t->gid_total = total;
@@ -7416,38 +7576,63 @@ void dist_join(DevCtx& c, DistComm& m, cq_node* q, cqgpu_table* const* tables, i
     g_outer_sets.clear();
     struct ClearSets { ~ClearSets() { g_outer_sets.clear(); } } clear_sets_;
     const int nj = q && q->kind == CQ_N_QUERY ? q->u.q.join_count : 0;
-    for (int j = 1; j < nj && 1 + j < ntables; j++) {
+    // every rank runs every level up to the plan's join count -- the plan is the same on
+    // every rank, its table list may not be: a missing table is this rank's failure,
+    // never a skipped collective
+    for (int j = 1; j < nj; j++) {
         cq_node* jn = q->u.q.joins[j];
         if (!jn || jn->kind != CQ_N_JOIN || (jn->u.join.kind != CQ_JOIN_RIGHT && jn->u.join.kind != CQ_JOIN_FULL))
             continue;
-        cqgpu_table* T = tables[1 + j];           // whole on every rank: the same record count
+        cqgpu_table* T = 1 + j < ntables ? tables[1 + j] : nullptr;   // whole on every rank: the same record count
+        if (getenv("CQGPU_TEST_DIST_CHAIN_MISSING")) T = nullptr;     // test knob: this rank lacks the table
         uint64_t nrec = 0;
         if (!T) {
             bad = true;                           // (still in every collective below)
             err = "dist_join: a chain table is missing";
         } else {
-            if (!T->rec_starts) {
-                std::unique_ptr<DevBuf> b(new DevBuf());
-                T->nrec_starts = all_records(c, T, *b);
-                T->rec_starts = std::move(b);
+            try {
+                if (!T->rec_starts) {
+                    std::unique_ptr<DevBuf> b(new DevBuf());
+                    T->nrec_starts = all_records(c, T, *b);
+                    T->rec_starts = std::move(b);
+                }
+                nrec = T->nrec_starts;
+            } catch (HipError& e) {
+                bad = true;
+                err = e.msg;
             }
-            nrec = T->nrec_starts;
+            (void)hipGetLastError();
         }
         {                                         // every rank sizes the flags alike
-            DevBuf dn(8);
-            HIPCHECK(hipMemcpyAsync(dn.p, &nrec, 8, hipMemcpyHostToDevice, c.stream));
-            NCCLCHECK(ncclAllReduce(dn.p, dn.p, 1, ncclUint64, ncclMax, m.comm, c.stream));
-            uint64_t mx = 0;
-            HIPCHECK(hipMemcpyAsync(&mx, dn.p, 8, hipMemcpyDeviceToHost, c.stream));
+            DevBuf dn(16);
+            uint64_t hv[2] = {nrec, ~nrec};       // MAX of n and of ~n: max and min at once
+            HIPCHECK(hipMemcpyAsync(dn.p, hv, 16, hipMemcpyHostToDevice, c.stream));
+            m.be->all_reduce(dn.p, 2, CD_U64, CR_MAX, c.stream);
+            HIPCHECK(hipMemcpyAsync(hv, dn.p, 16, hipMemcpyDeviceToHost, c.stream));
             HIPCHECK(hipStreamSynchronize(c.stream));
-            if (mx != nrec && !bad) {
+            if ((hv[0] != ~hv[1] || hv[0] != nrec) && !bad) {
                 bad = true;
                 err = "dist_join: a chain table's record count differs between ranks";
             }
-            nrec = mx;
+            nrec = hv[0];
         }
-        std::vector<uint8_t> flags(nrec, 0);
-        if (!bad) {
+        std::vector<uint8_t> flags;
+        DevBuf dm;
+        try {
+            flags.assign(nrec, 0);
+            if (nrec) {
+                DevBuf x(nrec);
+                std::swap(dm.p, x.p);
+            }
+        } catch (HipError& e) {
+            bad = true;
+            err = e.msg;
+        } catch (std::exception& e) {
+            bad = true;
+            err = e.what();
+        }
+        if (agree_any(c, m, bad)) throw PeerFail{bad ? err : std::string("a peer rank failed")};
+        {
             const uint8_t* fl = nullptr;
             uint64_t n = 0;
             const int r = cqgpu_join_outer_matched(q, tabs.data(), (int)tabs.size(), j, &fl, &n);
@@ -7459,9 +7644,8 @@ void dist_join(DevCtx& c, DistComm& m, cq_node* q, cqgpu_table* const* tables, i
             }
         }
         if (nrec) {
-            DevBuf dm(nrec);
             HIPCHECK(hipMemcpyAsync(dm.p, flags.data(), nrec, hipMemcpyHostToDevice, c.stream));
-            NCCLCHECK(ncclAllReduce(dm.p, dm.p, nrec, ncclUint8, ncclMax, m.comm, c.stream));
+            m.be->all_reduce(dm.p, nrec, CD_U8, CR_MAX, c.stream);
             HIPCHECK(hipMemcpyAsync(flags.data(), dm.p, nrec, hipMemcpyDeviceToHost, c.stream));
             HIPCHECK(hipStreamSynchronize(c.stream));
         }
@@ -7510,14 +7694,13 @@ int cqgpu_comm_init(const void* id, int rank, int world) {
         int dev = 0;
         HIPCHECK(hipGetDevice(&dev));
         DistComm& m = g_comm[dev & 63];
-        if (m.comm) {
-            (void)ncclCommDestroy(m.comm);
-            m.comm = nullptr;
-        }
+        m.be.reset();
         ncclUniqueId uid;
         memcpy(&uid, id, sizeof uid);
         (void)ctx();                                   // the device context (stream) first
-        NCCLCHECK(ncclCommInitRank(&m.comm, world, uid, rank));
+        std::unique_ptr<RcclColl> r(new RcclColl);
+        NCCLCHECK(ncclCommInitRank(&r->comm, world, uid, rank));
+        m.be = std::move(r);
         m.rank = rank;
         m.world = world;
         return 0;
@@ -7533,12 +7716,37 @@ int cqgpu_comm_init(const void* id, int rank, int world) {
     }
 }
 
+int cqgpu_comm_init_host(int rank, int world, cqgpu_coll_fn fn, void* user) {
+    g_err.clear();
+    try {
+        if (!fn || world < 1 || rank < 0 || rank >= world) throw HipError{"comm_init_host: bad arguments"};
+        int dev = 0;
+        HIPCHECK(hipGetDevice(&dev));
+        DistComm& m = g_comm[dev & 63];
+        m.be.reset();
+        (void)ctx();
+        std::unique_ptr<HostColl> h(new HostColl);
+        h->fn = fn;
+        h->user = user;
+        h->world = world;
+        m.be = std::move(h);
+        m.rank = rank;
+        m.world = world;
+        return 0;
+    } catch (HipError& e) {
+        set_err("cq_amd: %s", e.msg.c_str());
+        return -1;
+    } catch (std::exception& e) {
+        set_err("cq_amd: %s", e.what());
+        return -1;
+    }
+}
+
 void cqgpu_comm_destroy(void) {
     int dev = 0;
     if (hipGetDevice(&dev) != hipSuccess) return;
     DistComm& m = g_comm[dev & 63];
-    if (m.comm) (void)ncclCommDestroy(m.comm);
-    m.comm = nullptr;
+    m.be.reset();
     m.rank = 0;
     m.world = 1;
 }

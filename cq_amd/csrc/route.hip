@@ -45,7 +45,8 @@ __device__ __forceinline__ uint32_t route_dest(uint64_t code, uint32_t cls, uint
 }
 
 __device__ __forceinline__ bool r_nl(uint32_t c) { return c == '\n' || c == '\r'; }
-__device__ __forceinline__ bool r_blank(uint32_t c) { return c == ' ' || c == '\t'; }
+// parse_line's leading isspace skip (csv_reader.c:287) minus the terminators: scanlib.h is_blank
+__device__ __forceinline__ bool r_blank(uint32_t c) { return c == ' ' || c == '\t' || c == 0x0b || c == 0x0c; }
 
 // The record at p with only the fields of `mask` (bit c: column c; columns from 63 on
 // follow bit 63) and the delimiters before the last kept one; returns its length

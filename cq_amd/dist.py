@@ -287,6 +287,77 @@ def init_library_comm(device: torch.device | str | None = None) -> None:
     cq_amd.comm_init(bytes(t.cpu().numpy()), rank, world)
 
 
+_HOST_COMM = {}      # device -> the ctypes callback (kept alive while the library holds it)
+
+_GLOO_DT = {0: torch.uint8, 1: torch.int32, 2: torch.int64, 3: torch.int64, 4: torch.float64}
+_ELEM = {0: 1, 1: 4, 2: 8, 3: 8, 4: 8}
+
+
+def init_host_comm() -> None:
+    """TEST backend of the library's N > 1 step (cqgpu_comm_init_host): the library
+    stages each collective's device buffers through host memory and calls back here,
+    where torch.distributed (gloo) runs it.  The library's own protocol code --
+    cqgpu_dist_query's gather-merge / dense / blob merges and cqgpu_dist_join's
+    exchange, outer sets and status agreements -- then runs unchanged at world size
+    > 1 on a one-GPU box (several ranks sharing the device, which RCCL refuses).
+    u32 / u64 travel as int32 / int64 (their reductions here are MAX over small
+    values and SUM of counts); byte movements are dtype-blind."""
+    import ctypes as C
+    import sys
+    import numpy as np
+    import cq_amd
+    rank, world = dist.get_rank(), dist.get_world_size()
+    pending = []
+    ops = {0: dist.ReduceOp.SUM, 1: dist.ReduceOp.MIN, 2: dist.ReduceOp.MAX}
+
+    def raw(ptr, nbytes):
+        if nbytes == 0:
+            return torch.zeros(0, dtype=torch.uint8)
+        return torch.from_numpy(np.ctypeslib.as_array((C.c_uint8 * nbytes).from_address(ptr)))
+
+    def view(ptr, count, dtype):
+        return raw(ptr, count * _ELEM[dtype]).view(_GLOO_DT[dtype])
+
+    def fn(user, op, dtype, redop, peer, send, recv, count):
+        try:
+            nb = count * _ELEM[dtype]
+            if op == 1:                                   # ALLREDUCE (in place)
+                if count:
+                    dist.all_reduce(view(send, count, dtype), op=ops[redop])
+            elif op == 2:                                 # ALLGATHER
+                if nb:
+                    tmp = [torch.empty(nb, dtype=torch.uint8) for _ in range(world)]
+                    dist.all_gather(tmp, raw(send, nb).clone())
+                    raw(recv, nb * world).copy_(torch.cat(tmp))
+            elif op == 3:                                 # REDUCE to `peer` (in place)
+                if count:
+                    dist.reduce(view(send, count, dtype), dst=peer, op=ops[redop])
+            elif op == 4:                                 # BROADCAST from `peer` (in place)
+                if count:
+                    dist.broadcast(view(send, count, dtype), src=peer)
+            elif op == 5:                                 # SEND (posted until GROUP_END)
+                if nb:
+                    pending.append(dist.isend(raw(send, nb), dst=peer))
+            elif op == 6:                                 # RECV (posted until GROUP_END)
+                if nb:
+                    pending.append(dist.irecv(raw(recv, nb), src=peer))
+            elif op == 7:                                 # GROUP_END
+                for w in pending:
+                    w.wait()
+                pending.clear()
+            else:
+                return 1
+            return 0
+        except Exception as e:                            # (the library fails the step)
+            print(f"cq_amd host collective op {op} on rank {rank}: {e!r}", file=sys.stderr, flush=True)
+            return 1
+
+    cb = cq_amd.COLL_FN(fn)
+    _HOST_COMM[torch.cuda.current_device() if torch.cuda.is_available() else 0] = cb
+    if cq_amd.lib().cqgpu_comm_init_host(rank, world, cb, None) != 0:
+        raise RuntimeError(cq_amd.last_error() or "cqgpu_comm_init_host failed")
+
+
 def scan_partitioned_rccl(ast, table):
     """One range-partitioned query step with the whole merge inside the library
     (cqgpu_dist_query over its own RCCL communicator, init_library_comm): no
@@ -359,8 +430,8 @@ def join_partitioned(ast, lshard, rshard, lheader: bytes, rheader: bytes, device
         # destination is the identity), so the shards are already the routed tables
         # and their record ids the local row indexes
         comm = torch.device(comm_device) if comm_device is not None else torch.device(device)
-        outer_sets(ast, [lshard, rshard, *rest], len(rest), comm)
         try:
+            outer_sets(ast, [lshard, rshard, *rest], len(rest), comm)
             return cq_amd.merge_partials(ast, [cq_amd.query_partial(ast, [lshard, rshard, *rest])])
         finally:
             cq_amd.join_outer_clear()

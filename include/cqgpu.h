@@ -180,6 +180,21 @@ void cqgpu_partial_free(cqgpu_partial* p);
 int cqgpu_comm_unique_id(void* id_out);
 int cqgpu_comm_init(const void* id, int rank, int world);
 void cqgpu_comm_destroy(void);
+/* Test backend of the same step: instead of RCCL, every collective stages its device
+ * buffers through host memory and calls fn(user, op, dtype, redop, peer, send, recv,
+ * count) -- count elements of dtype (0 u8, 1 u32, 2 u64, 3 i64, 4 f64), redop 0 SUM,
+ * 1 MIN, 2 MAX, peer the root / peer rank or -1.  ALLREDUCE / REDUCE / BROADCAST work
+ * in place on `send` (== recv); ALLGATHER fills recv with world * count elements;
+ * SEND / RECV post a transfer whose host buffer stays valid until GROUP_END, which
+ * must complete every posted transfer.  fn returns 0, anything else fails the step.
+ * cq_amd.dist.init_host_comm binds it to torch.distributed gloo, so the library's
+ * own N > 1 protocol (cqgpu_dist_query / cqgpu_dist_join) runs at world size 2 and 3
+ * with the ranks sharing one GPU.  Not for production: RCCL is the product path. */
+enum { CQGPU_HC_ALLREDUCE = 1, CQGPU_HC_ALLGATHER = 2, CQGPU_HC_REDUCE = 3, CQGPU_HC_BROADCAST = 4,
+       CQGPU_HC_SEND = 5, CQGPU_HC_RECV = 6, CQGPU_HC_GROUP_END = 7 };
+typedef int (*cqgpu_coll_fn)(void* user, int op, int dtype, int redop, int peer, const void* send, void* recv,
+                             uint64_t count);
+int cqgpu_comm_init_host(int rank, int world, cqgpu_coll_fn fn, void* user);
 cq_table* cqgpu_dist_query(cq_node* query_ast, cqgpu_table* shard, int* status, int* path);
 /* cqgpu_dist_join: the repartitioned JOIN step (perform_join / process_joins,
  * evaluator_joins.c:63-181, 237-274, over inputs spread across the ranks) inside the

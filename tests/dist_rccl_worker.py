@@ -1,5 +1,7 @@
 """Worker for tests/test_gpu_dist_rccl.py (run under torch.distributed.run): the
-library's own RCCL communicator (cq_amd.dist.init_library_comm), then every query
+library's own RCCL communicator (cq_amd.dist.init_library_comm) -- or, with
+CQ_TEST_HOST_COMM=1, its host-staged test backend over gloo (init_host_comm, ranks
+sharing one GPU) -- then every query
 of argv through cqgpu_dist_query on this rank's range shard; rank 0 writes the
 results (and the merge path each took) as JSON to the output file."""
 import json
@@ -17,13 +19,30 @@ def main():
     out, items = sys.argv[1], json.loads(sys.argv[2])     # items: [[sql, path], ...]
     rank, world = int(os.environ["RANK"]), int(os.environ["WORLD_SIZE"])
     local = int(os.environ.get("LOCAL_RANK", "0"))
-    torch.cuda.set_device(local)
-    dist.init_process_group("nccl", device_id=torch.device("cuda", local))
+    host = os.environ.get("CQ_TEST_HOST_COMM") == "1"
+    if host:
+        # the library's collectives through its host-staged test backend over gloo:
+        # every rank on the one GPU of the box (RCCL would refuse a shared device)
+        torch.cuda.set_device(local % torch.cuda.device_count())
+        dist.init_process_group("gloo")
+    else:
+        torch.cuda.set_device(local)
+        dist.init_process_group("nccl", device_id=torch.device("cuda", local))
     import cqtest
     import cq_amd
     from cq_amd import abi
-    from cq_amd.dist import init_library_comm
-    init_library_comm()
+    from cq_amd.dist import init_host_comm, init_library_comm
+    if host:
+        init_host_comm()
+    else:
+        init_library_comm()
+    # failure injection on one rank only: CQ_TEST_RANK_ENV="<rank>:<NAME>=<value>"
+    spec = os.environ.get("CQ_TEST_RANK_ENV", "")
+    if spec:
+        r, kv = spec.split(":", 1)
+        if int(r) == rank:
+            k, v = kv.split("=", 1)
+            os.environ[k] = v
     results = []
     for sql, path in items:
         # path: one file (cqgpu_dist_query over its range shard), or a JOIN's files
@@ -56,6 +75,8 @@ def main():
         for x in tabs:
             x.close()
     cq_amd.comm_destroy()
+    with open(f"{out}.{rank}", "w") as fh:         # every rank's statuses and errors
+        json.dump([{"status": r["status"], "error": r["error"]} for r in results], fh)
     if rank == 0:
         with open(out, "w") as fh:
             json.dump(results, fh, default=lambda b: b.decode("latin-1") if isinstance(b, bytes) else str(b))

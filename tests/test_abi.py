@@ -141,6 +141,8 @@ def _declared_functions():
         text = open(os.path.join(INC, h)).read()
         text = re.sub(r"/\*.*?\*/", "", text, flags=re.S)
         for m in re.finditer(r"^[A-Za-z_][\w\s\*]*?\b(\w+)\s*\(", text, flags=re.M):
+            if m.group(0).startswith("typedef"):          # a function-pointer type, not a symbol
+                continue
             if m.group(1) not in ("if", "while", "typedef"):
                 names.add(m.group(1))
     return names

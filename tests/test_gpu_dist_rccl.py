@@ -262,3 +262,88 @@ def test_gm_decline_then_dense_same_process(files, kind):
             compare(got, want, set(), f"blobs after gm: {q}")
     finally:
         t.close()
+
+
+# ---------------------------------------------------------------- the same protocol at world size 2 and 3
+# The library's N > 1 code (dist_gm / dist_dense / dist_blob / dist_join: size
+# agreements, per-destination offsets, gid bases, grouped send / recv, outer-set
+# all-reduces, status broadcasts) through its host-staged collective backend
+# (cqgpu_comm_init_host) over gloo, 2 and 3 processes sharing the box's GPU.  Only the
+# transport differs from the RCCL runs: every collective call site is the same code.
+def _host_run(files, tmp_path, items, world, env=None, paths_of=None):
+    out = str(tmp_path / f"host{world}.json")
+    if paths_of is None:
+        payload = [[s, files[f]] for s, f in items]
+    else:
+        payload = [[s, [files[k] for k in keys]] for s, keys in items]
+    cmd = [sys.executable, "-m", "torch.distributed.run", "--nnodes=1", f"--nproc-per-node={world}",
+           "--master-addr", "127.0.0.1", "--master-port", str(_port()), os.path.join(ROOT, "tests", "dist_rccl_worker.py"),
+           out, json.dumps(payload)]
+    e = dict(os.environ)
+    e["CQ_TEST_HOST_COMM"] = "1"
+    e.update(env or {})
+    p = subprocess.run(cmd, cwd=ROOT, capture_output=True, text=True, timeout=110, env=e)
+    assert p.returncode == 0, p.stderr[:6000] + "\n...\n" + p.stderr[-2000:]
+    per_rank = [json.load(open(f"{out}.{r}")) for r in range(world)]
+    return json.load(open(out)), per_rank
+
+
+def _as_got(r):
+    return {"columns": [c.encode("latin-1") for c in r["result"]["columns"]],
+            "rows": [[_cell(c) for c in row] for row in r["result"]["rows"]]}
+
+
+@pytest.mark.parametrize("world", [2, 3])
+def test_dist_query_multi_rank_host_backend(files, tmp_path, world):
+    """cqgpu_dist_query at world size 2 and 3: gather-merge, dense and blob paths (and
+    the gather-merge declines falling to the dense merge together) vs the oracle"""
+    res, per = _host_run(files, tmp_path, [(s, f) for s, _, f in DIST], world)
+    for (sql, path, f), r in zip(DIST, res):
+        q = sql.format(p=files[f])
+        assert r["status"] == 0, (q, r["error"])
+        assert r["path"] == path, (q, r["path"])
+        for pr in per:
+            assert pr[DIST.index((sql, path, f))]["status"] == 0
+        want, _ = cqtest.oracle_query(q)
+        with cqtest.Parsed(q) as ast:
+            tol = tolerant_columns(ast)
+        compare(_as_got(r), want, tol, f"dist_query {world} ranks, path {path}: {q}")
+
+
+@pytest.mark.parametrize("world", [2, 3])
+def test_dist_join_multi_rank_host_backend(files, tmp_path, world):
+    """cqgpu_dist_join at world size 2 and 3: routing, the exchange with per-destination
+    offsets and gid bases, rebuilt sides with key stride N, chains with a later RIGHT /
+    FULL level (the outer-set all-reduces) -- each against the oracle"""
+    res, per = _host_run(files, tmp_path, JOINS, world, paths_of=True)
+    for i, ((sql, keys), r) in enumerate(zip(JOINS, res)):
+        q = sql.format(**dict(zip("pqrs", [files[k] for k in keys])))
+        assert r["status"] == 0, (q, r["error"])
+        assert all(pr[i]["status"] == 0 for pr in per), (q, per)
+        want, unsup = cqtest.oracle_query(q)
+        assert not unsup
+        with cqtest.Parsed(q) as ast:
+            tol = tolerant_columns(ast)
+        compare(_as_got(r), want, tol, f"dist_join {world} ranks: {q}")
+
+
+@pytest.mark.parametrize("knob,kind", [
+    ("CQGPU_TEST_GM_FAIL_PART", "query"),            # one rank's gather-merge part
+    ("CQGPU_TEST_GM_FAIL_FINISH", "query"),          # (read by rank 0 only)
+    ("CQGPU_TEST_DIST_FAIL_ALLOC", "join"),          # one rank's exchange buffers
+    ("CQGPU_TEST_DIST_CHAIN_MISSING", "chain"),      # one rank lacks a chain level's table
+])
+def test_dist_one_rank_failure_reaches_every_rank(files, tmp_path, knob, kind):
+    """a failure on ONE rank of three is status -1 on EVERY rank after the same
+    collectives -- no rank left waiting in a transfer or reduce its peer never posts
+    (exchange allocations and the chain loop inside the agreement)"""
+    fail_rank = 0 if knob == "CQGPU_TEST_GM_FAIL_FINISH" else 1
+    env = {"CQ_TEST_RANK_ENV": f"{fail_rank}:{knob}=1"}
+    if kind == "query":
+        res, per = _host_run(files, tmp_path, [(GM[0], "plain")], 3, env=env)
+    else:
+        item = JOINS[0] if kind == "join" else JOINS[4]
+        res, per = _host_run(files, tmp_path, [item], 3, env=env, paths_of=True)
+    for r, pr in enumerate(per):
+        assert pr[0]["status"] == -1, (r, pr)
+    assert "injected" in per[fail_rank][0]["error"] or "missing" in per[fail_rank][0]["error"], per[fail_rank]

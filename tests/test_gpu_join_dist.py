@@ -40,6 +40,7 @@ def _shards(data: bytes, nranks: int, seed: int, cfg=None):
 
 
 LAST_KINDS = []   # per rank, the scan kernel kind of its partial (4: the STAR fused join)
+LAST_BLOBS = []   # per rank, its partial blob
 
 
 def _run(ast, ldata: bytes, rdata: bytes, nranks: int, rest=(), outer=True, cfg=None):
@@ -96,6 +97,7 @@ def _run(ast, ldata: bytes, rdata: bytes, nranks: int, rest=(), outer=True, cfg=
             apply(d, len(rest) + 1)
             blobs.append(cq_amd.query_partial(ast, routed[d] + whole[d]))
             LAST_KINDS.append(cq_amd.stats().get("scan_kernel"))
+        LAST_BLOBS[:] = blobs
         tp = cq_amd.merge_partials(ast, blobs)
     finally:
         cq_amd.join_outer_clear()
@@ -287,6 +289,27 @@ def test_repartitioned_fused_join(files, nranks):
         tol = tolerant_columns(ast)
     compare(got, want, tol, f"{sql} @ {nranks} ranks")
     assert len(kinds) == nranks and all(k == 4 for k in kinds), kinds
+
+
+@pytest.mark.parametrize("nranks", [1, 3])
+def test_first_ids_device_equals_host(files, nranks, monkeypatch):
+    """the STAR partial's first-pair global ids mapped on the device
+    (route.hip pack_first_gid_kernel, the default) and by the host lookup
+    (CQGPU_HOST_FIRST_IDS=1): the same blobs, byte for byte"""
+    data, paths = files
+    sql = (f"SELECT u.role, COUNT(*), SUM(o.price) FROM '{paths['users']}' AS u "
+           f"JOIN '{paths['orders']}' AS o ON u.id = o.customer_id GROUP BY u.role")
+    got = []
+    with cqtest.Parsed(sql) as ast:
+        for host in (False, True):
+            if host:
+                monkeypatch.setenv("CQGPU_HOST_FIRST_IDS", "1")
+            tp = _run(ast, data["users"], data["orders"], nranks)
+            assert tp, cq_amd.last_error()
+            assert all(k == 4 for k in LAST_KINDS), LAST_KINDS
+            cq_amd.result_free(tp)
+            got.append(list(LAST_BLOBS))
+    assert got[0] == got[1]
 
 
 def test_partial_stats_reset_per_call(files):
@@ -504,7 +527,7 @@ def _project(rec: bytes, keep, last_keep, delim=b",", quote=b'"'):
     at = lambda k: rec[k] if k < n else 10
     while True:
         s = i
-        while at(i) in (32, 9):
+        while at(i) in (32, 9, 11, 12):     # isspace minus the terminators
             i += 1
         if at(i) not in (10, 13):
             if at(i) == qt:
@@ -636,7 +659,9 @@ PROJ_LEFT = (b"id,name,age,role,note\n"
              b'4,"d",,  dev  ,"n,1"\n'
              b"5\r\n"
              b',"e""",52,"r""1",z,extra,more\n'
-             b"6,f,60,,\n")
+             b"6,f,60,,\n"
+             # \v / \f before a quoted field holding the delimiter
+             b'7,\x0b"g,h",61,\x0c"ops,w",\x0b\x0c"n,2"\n')
 PROJ_RIGHT = b"id,price,quantity,customer_id\n1,2.5,3,1\n2,4.0,1, 2 \n3,,2,\n4,9.5,1,5\n5,1.0,7,6\n"
 
 
