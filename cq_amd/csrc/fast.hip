@@ -71,9 +71,9 @@ struct FastPlan {
     uint32_t lo_s, hi_s;        // owned starts: from lo_s in the first window, below hi_s in the last
     uint32_t ws;                // window stride (multiple of 128, <= WS)
     uint32_t delim, quote;
-    uint32_t skip[4];           // field k's column minus field k-1's (field 0: its column); fields = the
+    uint32_t skip[5];           // field k's column minus field k-1's (field 0: its column); fields = the
                                 // roles' columns ascending (equal columns: skip 0)
-    uint32_t rank[4];           // field index of WHERE, SUM 0, SUM 1, GROUP BY
+    uint32_t rank[5];           // field index of WHERE, SUM 0, SUM 1, GROUP BY, WHERE column 1 (WX == 2)
     uint32_t wtt;               // WHERE truth table (bit 0 <, 1 ==, 2 >)
     int32_t wlo, whi;           // INTEGER field M: M < L <=> M < wlo; M > L <=> M > whi
     uint32_t wa, ww, wneg;      // a 1-4 digit INTEGER M passes <=> ((M - wa) <=u ww) != wneg
@@ -91,7 +91,27 @@ struct FastPlan {
     // as a big-endian word, zero padded (strcmp order of zero-padded words), cut at a NUL
     uint32_t wstr_lit;          // 1: the WHERE literal is such a STRING
     uint64_t wstr;
+    // WX builds: a compound WHERE (evaluate_condition's NOT / AND / OR tree over up to 4
+    // leaves `column op literal` or `column [NOT] IN (literals)`, evaluator_conditions.c:
+    // 62-164) over up to 2 columns.  Every leaf is evaluated (as the reference evaluates
+    // both sides of AND / OR), the tree is the 16-entry truth table wx_tt over the leaf
+    // outcomes.  A NUMBER column's fields are typed as exact 10^-3 fixed point V (the SUM
+    // path's num4: <= 4 bytes); a comparison is an interval of V whose bounds the host
+    // found with the reference's own double compare (RN(V / 1000) against the literal's
+    // double); a STRING column's 1-8 byte fields compare as zero-padded big-endian words.
+    uint32_t wx_nleaf;
+    uint32_t wx_tt;
+    uint32_t wx_str;            // bit c: WHERE column c is a STRING column (else a NUMBER one)
+    uint32_t lx_col[4];         // the leaf's WHERE column (0 / 1)
+    uint32_t lx_kind[4];        // LX_*
+    uint32_t lx_a[4], lx_w[4], lx_neg[4];   // LX_NUM: ((V - a) <=u w) != neg; LX_*IN: neg = NOT IN
+    uint32_t lx_null[4];        // the leaf's outcome for a NULL (empty) field
+    uint32_t lx_tt[4];          // LX_STR: truth table over (<, ==, >)
+    uint32_t lx_nin[4];         // LX_*IN: items
+    uint64_t lx_lit[4];         // LX_STR: the literal's word
+    uint64_t lx_in[4][8];       // LX_*IN: V values (numbers) or words (strings)
 };
+enum : uint32_t { LX_NUM = 0, LX_STR = 1, LX_NIN = 2, LX_SIN = 3 };
 
 // HBM tables: canonical keys (TAB_GT), raw keys (TAB_RT)
 enum : int { TAB_GT = 0, TAB_RT = 1 };
@@ -493,13 +513,16 @@ constexpr uint32_t fixed_bytes() { return (uint32_t)(sizeof(WaveLds) * NWV); }
 // WN: numerals of 5-7 bytes / over 3 decimals are typed here (a side path); without
 // it (the plan's sampled WHERE / SUM fields are all <= 4 bytes) such a record goes
 // whole to slow_kernel, and the kernel keeps only the fixed-point SUM
-template <bool GROUPED, bool WHERE, int NS, bool COMMA, bool CANON, int RP, bool WN, int EXT = 0, bool WSTR = false>
+// WX: a compound WHERE over WX (1 or 2) columns (FastPlan wx_*, lx_*)
+template <bool GROUPED, bool WHERE, int NS, bool COMMA, bool CANON, int RP, bool WN, int EXT = 0, bool WSTR = false,
+          int WX = 0>
 __global__ __launch_bounds__(LT) void fast_kernel(const uint8_t* __restrict__ g, ScanStats* __restrict__ stats,
                                                   unsigned long long* __restrict__ slow_list,
                                                   unsigned long long slow_cap, const FastPlan fp,
                                                   const GroupTable* __restrict__ tabs) {
     static_assert(EXT == 0 || (NS == 1 && !WN), "MIN / MAX: one fixed-point argument, no double addends");
     static_assert(!WSTR || (WHERE && !WN && EXT == 0), "STRING-literal WHERE: the narrow-numeral builds");
+    static_assert(WX == 0 || (WHERE && !WN && EXT == 0 && !WSTR && COMMA && RP == 2), "compound WHERE builds");
     extern __shared__ __align__(16) uint8_t smem[];
     uint8_t* q = smem;
     // LDS table: slot records first (LDS address 0: field offsets fold into the
@@ -527,11 +550,12 @@ __global__ __launch_bounds__(LT) void fast_kernel(const uint8_t* __restrict__ g,
         __syncthreads();
     }
 
-    constexpr int NR = (WHERE ? 1 : 0) + NS + (GROUPED ? 1 : 0);   // roles, in column order
-    constexpr int KW = 0, KS0 = WHERE ? 1 : 0, KG = NR - 1;
-    uint32_t skip[4], rk[4];
+    // roles, in column order (CANON: WHERE, WHERE column 1, SUM 0, SUM 1, GROUP BY)
+    constexpr int NR = (WHERE ? 1 : 0) + (WX == 2 ? 1 : 0) + NS + (GROUPED ? 1 : 0);
+    constexpr int KW = 0, KW1 = 1, KS0 = (WHERE ? 1 : 0) + (WX == 2 ? 1 : 0), KG = NR - 1;
+    uint32_t skip[5], rk[5];
 #pragma unroll
-    for (int k = 0; k < 4; k++) {
+    for (int k = 0; k < 5; k++) {
         skip[k] = __builtin_amdgcn_readfirstlane(fp.skip[k]);
         rk[k] = __builtin_amdgcn_readfirstlane(fp.rank[k]);
     }
@@ -718,7 +742,7 @@ __global__ __launch_bounds__(LT) void fast_kernel(const uint8_t* __restrict__ g,
 #endif
         while (__any(todo != 0)) {
             // ---- two records of this lane
-            uint32_t p[RP], pa[RP], fst[RP][4], fen[RP][4], e[RP];   // p: window offset, pa: LDS address
+            uint32_t p[RP], pa[RP], fst[RP][5], fen[RP][5], e[RP];   // p: window offset, pa: LDS address
             uint64_t sv[RP];
             bool valid[RP], fail[RP];
 #pragma unroll
@@ -792,7 +816,7 @@ __global__ __launch_bounds__(LT) void fast_kernel(const uint8_t* __restrict__ g,
             }
 
             // ---- each role's field: compile-time ranks (CANON) or the plan's (uniform selects)
-            uint32_t wst[RP] = {}, wen[RP] = {}, gst[RP] = {}, gen[RP] = {};
+            uint32_t wst[RP] = {}, wen[RP] = {}, gst[RP] = {}, gen[RP] = {}, xst[RP] = {}, xen[RP] = {};
             uint32_t sst[RP][MAXS] = {}, sen[RP][MAXS] = {};
 #pragma unroll
             for (int u = 0; u < RP; u++) {
@@ -807,11 +831,13 @@ __global__ __launch_bounds__(LT) void fast_kernel(const uint8_t* __restrict__ g,
                 };
                 if (CANON) {
                     if (WHERE) { wst[u] = fst[u][KW]; wen[u] = fen[u][KW]; }
+                    if (WX == 2) { xst[u] = fst[u][KW1]; xen[u] = fen[u][KW1]; }
 #pragma unroll
                     for (int j = 0; j < NS; j++) { sst[u][j] = fst[u][KS0 + j]; sen[u][j] = fen[u][KS0 + j]; }
                     if (GROUPED) { gst[u] = fst[u][KG]; gen[u] = fen[u][KG]; }
                 } else {
                     if (WHERE) pick(rk[0], wst[u], wen[u]);
+                    if (WX == 2) pick(rk[4], xst[u], xen[u]);
 #pragma unroll
                     for (int j = 0; j < NS; j++) pick(rk[1 + j], sst[u][j], sen[u][j]);
                     if (GROUPED) pick(rk[3], gst[u], gen[u]);
@@ -824,10 +850,11 @@ __global__ __launch_bounds__(LT) void fast_kernel(const uint8_t* __restrict__ g,
             continue;
 #endif
             // ---- field bytes (one batch of LDS reads)
-            uint32_t wd[RP], wd1[RP], sd[RP][MAXS], k0[RP], k1[RP];
+            uint32_t wd[RP], wd1[RP], sd[RP][MAXS], k0[RP], k1[RP], xd[RP], xd1[RP];
 #pragma unroll
             for (int u = 0; u < RP; u++) {
-                if (WSTR) ld8a(pa[u] + wst[u], wd[u], wd1[u]);
+                if (WX == 2) ld8a(pa[u] + xst[u], xd[u], xd1[u]);
+                if (WSTR || WX) ld8a(pa[u] + wst[u], wd[u], wd1[u]);
                 else if (WHERE) wd[u] = ld4a(pa[u] + wst[u]);
 #pragma unroll
                 for (int j = 0; j < NS; j++) sd[u][j] = ld4a(pa[u] + sst[u][j]);
@@ -839,7 +866,68 @@ __global__ __launch_bounds__(LT) void fast_kernel(const uint8_t* __restrict__ g,
             bool wu[RP];
 #pragma unroll
             for (int u = 0; u < RP; u++) { pass[u] = true; wu[u] = false; }
-            if (WSTR) {
+            if constexpr (WX != 0) {
+                // per WHERE column its typed value (uniform class), then every leaf, then
+                // the tree's truth table (a field this path cannot type: wu, slow_kernel)
+                const uint32_t tt16 = fp.wx_tt, nleaf = fp.wx_nleaf;
+#pragma unroll
+                for (int u = 0; u < RP; u++) {
+                    bool cnull[2], cok[2];
+                    uint32_t cv[2];
+                    uint64_t cx[2];
+#pragma unroll
+                    for (int c = 0; c < WX; c++) {
+                        const uint32_t len = c ? xen[u] - xst[u] : wen[u] - wst[u];
+                        const uint32_t a0r = c ? xd[u] : wd[u], a1r = c ? xd1[u] : wd1[u];
+                        cnull[c] = len == 0;
+                        cv[c] = 0;
+                        cx[c] = 0;
+                        if ((fp.wx_str >> c) & 1) {
+                            const uint32_t m0 = len_mask(len, 0), m1 = len_mask(len, 1);
+                            const uint32_t a0 = a0r & m0, a1 = a1r & m1;
+                            const uint32_t c0 = a0 & 0xFFu;
+                            cok[c] = (int)(len - 1u < 8u) & (int)!(is_digit(c0) | (c0 == '-') | (c0 == '+') | (c0 == '.')) &
+                                     (int)((low_bytes(a0, m0 & nk.k80, nk) | low_bytes(a1, m1 & nk.k80, nk)) == 0);
+                            cx[c] = ((uint64_t)__builtin_bswap32(a0) << 32) | __builtin_bswap32(a1);
+                        } else {
+                            const Num n = num4<true>(a0r, len, nk);
+                            const uint32_t mul = (uint32_t)(0x0001000A006403E8ull >> (n.k << 4)) & 0xFFFFu;
+                            cv[c] = __umul24(n.M, mul);
+                            cok[c] = n.ok;
+                        }
+                        wu[u] |= !cok[c] & !cnull[c] & !fail[u];
+                    }
+                    uint32_t idx = 0;
+#pragma unroll
+                    for (int l = 0; l < 4; l++) {
+                        if ((uint32_t)l < nleaf) {
+                            const uint32_t c = WX == 2 ? fp.lx_col[l] : 0u;
+                            const uint32_t V = c ? cv[WX - 1] : cv[0];
+                            const uint64_t X = c ? cx[WX - 1] : cx[0];
+                            const bool nul = c ? cnull[WX - 1] : cnull[0];
+                            const uint32_t kind = fp.lx_kind[l];
+                            bool b;
+                            if (kind == LX_NUM) {
+                                b = (V - fp.lx_a[l] <= fp.lx_w[l]) != (fp.lx_neg[l] != 0);
+                            } else if (kind == LX_STR) {
+                                const uint64_t lit = fp.lx_lit[l];
+                                b = tt_result(fp.lx_tt[l], X < lit ? -1 : (X > lit ? 1 : 0));
+                            } else {
+                                bool hit = false;
+                                const uint32_t nin = fp.lx_nin[l];
+#pragma unroll
+                                for (uint32_t t = 0; t < 8; t++)
+                                    if (t < nin)
+                                        hit |= kind == LX_NIN ? V == (uint32_t)fp.lx_in[l][t] : X == fp.lx_in[l][t];
+                                b = hit != (fp.lx_neg[l] != 0);
+                            }
+                            b = nul ? fp.lx_null[l] != 0 : b;
+                            idx |= (b ? 1u : 0u) << l;
+                        }
+                    }
+                    pass[u] = (tt16 >> idx) & 1u;
+                }
+            } else if (WSTR) {
                 // a STRING field of 1-8 bytes: no leading digit / sign / dot (never a
                 // numeral or a date, infer_type csv_reader.c:133-240), no byte <= ' '
                 // (trim_whitespace is a no-op); then strcmp against the literal is the
@@ -893,6 +981,21 @@ __global__ __launch_bounds__(LT) void fast_kernel(const uint8_t* __restrict__ g,
                 }
             }
 
+#if defined(FAST_EXP_NOB)      // experiment: the record pass up to the WHERE outcome only
+            {
+                uint32_t x = 0;
+#pragma unroll
+                for (int u = 0; u < RP; u++) {
+                    x ^= (uint32_t)pass[u] ^ (uint32_t)wu[u] ^ (uint32_t)fail[u];
+#pragma unroll
+                    for (int j = 0; j < NS; j++) x ^= sd[u][j];
+                    if (GROUPED) x ^= k0[u] ^ k1[u];
+                }
+                n_rec += (uint32_t)__popcll(__ballot(x & 1));
+            }
+            if (last_pass) FAST_ISSUE();
+            continue;
+#endif
             // ---- SUM addends: fixed point (10^-3) for numerals of <= 4 bytes (<= 3 decimals);
             //      5-7 byte numerals as strtod's double; su: not typed here
             uint64_t sfix[RP][MAXS];
@@ -2266,10 +2369,192 @@ bool fcmp_result(uint32_t op, int c) {
     }
 }
 
+// A compound WHERE for the WX builds: the post-order program (plan.h OP_*) read as a
+// tree of NOT / AND / OR over leaves `column op literal` (either side), `column [NOT]
+// IN (literals)` and constants; <= 4 leaves over <= 2 columns, each column's literals
+// of one class (NUMBER: INTEGER / DOUBLE, negated by a unary minus or not; STRING: 1-8
+// bytes).  The tree becomes a truth table over the leaves' outcomes (every leaf is
+// evaluated, as evaluator_conditions.c:76-86 evaluates both sides).  `s`: the stream
+// to read STRING literal bytes with (launch time), null at plan time.  wslot: the need
+// slots of the WHERE columns.
+namespace {
+// the fixed-point field values V (exact 10^-3, < 10^7: <= 4-byte numerals) whose double
+// RN(V / 1000) -- the strtod value parse_value gives the field -- compares >= (gt:
+// >) the literal's double: the smallest such V (10^7 + 1: none)
+uint32_t wx_first_v(double l, bool gt) {
+    uint32_t lo = 0, hi = 10000001u;              // answer in [lo, hi]
+    while (lo < hi) {
+        const uint32_t m = lo + (hi - lo) / 2;
+        const double v = (double)m / 1000.0;
+        if (gt ? v > l : v >= l) hi = m;
+        else lo = m + 1;
+    }
+    return lo;
+}
+bool wx_word(const Cell& L, hipStream_t s, uint64_t* w) {
+    if (L.kind != K_STR || L.len < 1 || L.len > 8) return false;
+    if (!s) { *w = 0; return true; }
+    uint8_t b[8] = {0, 0, 0, 0, 0, 0, 0, 0};
+    if (hipMemcpyAsync(b, (const void*)(uintptr_t)L.bits, L.len, hipMemcpyDeviceToHost, s) != hipSuccess) return false;
+    if (hipStreamSynchronize(s) != hipSuccess) return false;
+    bool nul = false;
+    uint64_t x = 0;
+    for (int i = 0; i < 8; i++) {                 // strcmp stops at a NUL
+        nul = nul || b[i] == 0;
+        x = (x << 8) | (nul ? 0u : b[i]);
+    }
+    *w = x;
+    return true;
+}
+}  // namespace
+
+bool wx_compile(const ScanPlan* P, FastPlan* fp, int wslot[2], int* nwc, hipStream_t s) {
+    if (getenv("CQGPU_NO_FAST_WX")) return false;
+    struct It { int kind; int v; bool neg; };      // kind 0 column (v slot), 1 literal (v const), 2 tree (v table)
+    It st[16];
+    int sp = 0, nleaf = 0;
+    *nwc = 0;
+    int ccls[2] = {-1, -1};                        // per WHERE column: 0 NUMBER, 1 STRING
+    auto colx = [&](int slot) -> int {
+        for (int c = 0; c < *nwc; c++)
+            if (wslot[c] == slot) return c;
+        if (*nwc == 2) return -1;
+        wslot[*nwc] = slot;
+        return (*nwc)++;
+    };
+    auto leaf_table = [](int j) {
+        uint32_t t = 0;
+        for (uint32_t i = 0; i < 16; i++) t |= ((i >> j) & 1u) << i;
+        return t;
+    };
+    auto number = [&](const It& x, double* v) {
+        const Cell& L = P->consts[x.v];
+        if (L.kind == K_INT) *v = (double)(int64_t)L.bits;
+        else if (L.kind == K_DBL) memcpy(v, &L.bits, 8);
+        else return false;
+        if (x.neg) *v = -*v;
+        return std::isfinite(*v);
+    };
+    for (int pc = 0; pc < P->nprog; pc++) {
+        const Insn& in = P->prog[pc];
+        if (sp >= 14) return false;
+        switch (in.op) {
+            case OP_COL: st[sp++] = It{0, (int)in.a, false}; break;
+            case OP_CONST: st[sp++] = It{1, (int)in.b, false}; break;
+            case OP_NEG:
+                if (sp < 1 || st[sp - 1].kind != 1 || st[sp - 1].neg) return false;
+                {
+                    const Cell& L = P->consts[st[sp - 1].v];
+                    if (L.kind != K_INT && L.kind != K_DBL) return false;
+                    if (L.kind == K_INT && (int64_t)L.bits == INT64_MIN) return false;
+                }
+                st[sp - 1].neg = true;
+                break;
+            case OP_BOOL: st[sp++] = It{2, in.a ? 0xFFFF : 0, false}; break;
+            case OP_NOT:
+                if (sp < 1 || st[sp - 1].kind != 2) return false;
+                st[sp - 1].v = ~st[sp - 1].v & 0xFFFF;
+                break;
+            case OP_AND: case OP_OR: {
+                if (sp < 2 || st[sp - 1].kind != 2 || st[sp - 2].kind != 2) return false;
+                const int r = st[--sp].v;
+                st[sp - 1].v = in.op == OP_AND ? (st[sp - 1].v & r) : (st[sp - 1].v | r);
+                break;
+            }
+            case OP_CMP: {
+                if (sp < 2 || nleaf == 4) return false;
+                It l = st[sp - 2], r = st[sp - 1];
+                sp -= 2;
+                uint32_t op = in.a;
+                if (l.kind == 1 && r.kind == 0) {          // literal op column: mirror the operator
+                    std::swap(l, r);
+                    op = op == CMP_LT ? CMP_GT : op == CMP_GT ? CMP_LT : op == CMP_LE ? CMP_GE : op == CMP_GE ? CMP_LE : op;
+                }
+                if (l.kind != 0 || r.kind != 1) return false;
+                const int c = colx(l.v);
+                if (c < 0) return false;
+                const int j = nleaf++;
+                fp->lx_col[j] = (uint32_t)c;
+                fp->lx_null[j] = fcmp_result(op, -1) ? 1u : 0u;     // NULL < any non-NULL
+                uint64_t w;
+                if (wx_word(P->consts[r.v], s, &w)) {
+                    if (r.neg || ccls[c] == 0) return false;
+                    ccls[c] = 1;
+                    fp->lx_kind[j] = fast::LX_STR;
+                    fp->lx_lit[j] = w;
+                    fp->lx_tt[j] = (fcmp_result(op, -1) ? 1u : 0u) | (fcmp_result(op, 0) ? 2u : 0u) |
+                                   (fcmp_result(op, 1) ? 4u : 0u);
+                } else {
+                    double lv;
+                    if (!number(r, &lv) || ccls[c] == 1) return false;
+                    ccls[c] = 0;
+                    // V < Vlt <=> RN(V/1000) < l;  V < Vle <=> RN(V/1000) <= l
+                    const int64_t vlt = wx_first_v(lv, false), vle = wx_first_v(lv, true);
+                    const bool lt = fcmp_result(op, -1), eq = fcmp_result(op, 0), gt = fcmp_result(op, 1);
+                    int64_t A, B;
+                    fp->lx_kind[j] = fast::LX_NUM;
+                    fp->lx_neg[j] = 0;
+                    if (lt && !eq && gt) { fp->lx_neg[j] = 1; A = vlt; B = vle - 1; }
+                    else if (!lt && !eq && !gt) { A = 1; B = 0; }
+                    else {
+                        A = lt ? 0 : (eq ? vlt : vle);
+                        B = gt ? 10000000 : (eq ? vle - 1 : vlt - 1);
+                    }
+                    if (A > B) { fp->lx_a[j] = 0xFFFFFFFFu; fp->lx_w[j] = 0; }   // empty (V + 1 > 0)
+                    else { fp->lx_a[j] = (uint32_t)A; fp->lx_w[j] = (uint32_t)(B - A); }
+                }
+                st[sp++] = It{2, (int)leaf_table(j), false};
+                break;
+            }
+            case OP_IN: {
+                const int k = in.b;
+                if (k < 1 || k > 8 || sp < k + 1 || nleaf == 4) return false;
+                const It l = st[sp - k - 1];
+                if (l.kind != 0) return false;
+                const int c = colx(l.v);
+                if (c < 0) return false;
+                const int j = nleaf++;
+                fp->lx_col[j] = (uint32_t)c;
+                fp->lx_neg[j] = in.a ? 1u : 0u;
+                fp->lx_null[j] = in.a ? 1u : 0u;           // NULL matches no item: IN false, NOT IN true
+                fp->lx_nin[j] = (uint32_t)k;
+                for (int t = 0; t < k; t++) {
+                    const It x = st[sp - k + t];
+                    if (x.kind != 1) return false;
+                    uint64_t w;
+                    if (!x.neg && wx_word(P->consts[x.v], s, &w)) {
+                        if (ccls[c] == 0) return false;
+                        ccls[c] = 1;
+                        fp->lx_in[j][t] = w;
+                    } else {
+                        double lv;
+                        if (!number(x, &lv) || ccls[c] == 1) return false;
+                        ccls[c] = 0;
+                        const uint32_t vlt = wx_first_v(lv, false), vle = wx_first_v(lv, true);
+                        fp->lx_in[j][t] = vlt < vle ? vlt : 0xFFFFFFFFu;     // the one V equal to it, or none
+                    }
+                }
+                fp->lx_kind[j] = ccls[c] == 1 ? fast::LX_SIN : fast::LX_NIN;
+                sp -= k + 1;
+                st[sp++] = It{2, (int)leaf_table(j), false};
+                break;
+            }
+            default:
+                return false;
+        }
+    }
+    if (sp != 1 || st[0].kind != 2 || nleaf == 0 || *nwc == 0) return false;
+    fp->wx_nleaf = (uint32_t)nleaf;
+    fp->wx_tt = (uint32_t)st[0].v;
+    fp->wx_str = (ccls[0] == 1 ? 1u : 0u) | (ccls[1] == 1 ? 2u : 0u);
+    // leaves beyond nleaf never run; the table ignores their bits (they read as 0)
+    return true;
+}
+
 // fast_kernel's plan shape (see the file comment); fills the FastPlan fields that
 // depend on the plan only
 bool fast_shape(const ScanPlan* P, int grouped, FastPlan* fp, int* ns, bool* where, bool* canonical,
-                bool* wide_num = nullptr, int* ext_out = nullptr) {
+                bool* wide_num = nullptr, int* ext_out = nullptr, int* wx_out = nullptr, hipStream_t wx_s = nullptr) {
     if (P->nacc > MAX_ACC || P->ngpart > 0) return false;
     const uint32_t d = P->delim;
     if ((d - '0') < 10u || d == '.' || ((d | 32) >= 'a' && (d | 32) <= 'z') || d == '+' || d == '-') return false;
@@ -2309,7 +2594,7 @@ bool fast_shape(const ScanPlan* P, int grouped, FastPlan* fp, int* ns, bool* whe
         fp->ext_col = (uint32_t)P->need_col[ext_slot];
     }
     if (ext_out) *ext_out = ext;
-    int wcol = -1;
+    int wcol = -1, wcol1 = -1, wx = 0;
     if (P->nprog == 0) {
         *where = false;
     } else if (P->nprog == 3 && P->prog[0].op == OP_COL && P->prog[1].op == OP_CONST && P->prog[2].op == OP_CMP) {
@@ -2326,9 +2611,14 @@ bool fast_shape(const ScanPlan* P, int grouped, FastPlan* fp, int* ns, bool* whe
             if (ext || d != ',' || P->quote != '"') return false;
         }
     } else {
-        return false;
+        int wslot[2] = {-1, -1};
+        if (ext || d != ',' || P->quote != '"' || !wx_compile(P, fp, wslot, &wx, wx_s)) return false;
+        *where = true;
+        wcol = P->need_col[wslot[0]];
+        wcol1 = wx == 2 ? P->need_col[wslot[1]] : -1;
     }
-    if (*where && !fp->wstr_lit) {   // numeric literal: the thresholds
+    if (wx_out) *wx_out = wx;
+    if (*where && !fp->wstr_lit && !wx) {   // numeric literal: the thresholds
         const Cell& L = P->consts[P->prog[1].b];
         double lv;
         if (L.kind == K_INT) lv = (double)(int64_t)L.bits;
@@ -2359,8 +2649,9 @@ bool fast_shape(const ScanPlan* P, int grouped, FastPlan* fp, int* ns, bool* whe
     if (grouped && (P->group_slot < 0 || P->lean_k16)) return false;
     // the roles' fields in column order (equal columns share a field; ties keep the
     // role order WHERE, SUM 0, SUM 1, GROUP BY)
-    int cols[4], roles[4], nr = 0;
+    int cols[5], roles[5], nr = 0;
     if (*where) { cols[nr] = wcol; roles[nr++] = 0; }
+    if (wx == 2) { cols[nr] = wcol1; roles[nr++] = 4; }
     for (int j = 0; j < *ns; j++) { cols[nr] = P->need_col[sslot[j]]; roles[nr++] = 1 + j; }
     if (grouped) { cols[nr] = P->need_col[P->group_slot]; roles[nr++] = 3; }
     for (int a = 1; a < nr; a++)
@@ -2373,21 +2664,26 @@ bool fast_shape(const ScanPlan* P, int grouped, FastPlan* fp, int* ns, bool* whe
         if (cols[k] < 0) return false;
         fp->skip[k] = (uint32_t)(k ? cols[k] - cols[k - 1] : cols[k]);
         fp->rank[roles[k]] = (uint32_t)k;
-        // compile-time ranks: WHERE 0, SUM j (WHERE ? 1 : 0) + j, GROUP BY the last
-        const int want = roles[k] == 0 ? 0 : (roles[k] == 3 ? nr - 1 : (*where ? 1 : 0) + roles[k] - 1);
+        // compile-time ranks: WHERE 0, WHERE column 1 (WX == 2) 1, SUM j (WHERE ? 1 : 0) +
+        // (WX == 2 ? 1 : 0) + j, GROUP BY the last
+        const int sbase = (*where ? 1 : 0) + (wx == 2 ? 1 : 0);
+        const int want = roles[k] == 0 ? 0 : roles[k] == 4 ? 1 : (roles[k] == 3 ? nr - 1 : sbase + roles[k] - 1);
         canon = canon && k == want;
     }
     *canonical = canon;
-    if (wide_num || ext || fp->wstr_lit) {   // a WHERE / SUM column whose sampled fields exceed 4 bytes
+    if (wide_num || ext || fp->wstr_lit || wx) {   // a WHERE / SUM column whose sampled fields exceed 4 bytes
         bool wn = false;
-        for (int k = 0; k < nr; k++)      // (a STRING-literal WHERE reads up to 8 bytes itself)
-            if (roles[k] != 3 && !(roles[k] == 0 && fp->wstr_lit))
-                wn = wn || ((P->fast_wide_cols >> (cols[k] < 63 ? cols[k] : 63)) & 1);
+        for (int k = 0; k < nr; k++) {    // (a STRING-literal WHERE reads up to 8 bytes itself)
+            if (roles[k] == 3 || (roles[k] == 0 && fp->wstr_lit)) continue;
+            if (wx && (roles[k] == 0 || roles[k] == 4) && ((fp->wx_str >> (roles[k] == 0 ? 0 : 1)) & 1)) continue;
+            wn = wn || ((P->fast_wide_cols >> (cols[k] < 63 ? cols[k] : 63)) & 1);
+        }
         wn = wn || getenv("CQGPU_FAST_WN") != nullptr;
         if (wide_num) *wide_num = wn;
         // MIN / MAX: the narrow-numeral ',' / '"' builds only (fixed point, no doubles)
         if (ext && (wn || d != ',' || P->quote != '"' || P->n >= (1ull << fast::EXT_POS_BITS))) return false;
         if (fp->wstr_lit && (wn || !canon)) return false;   // (the STRING-literal builds: narrow, canonical)
+        if (wx && wn) return false;                         // (the compound builds: narrow numerals)
     }
     return true;
 }
@@ -2421,8 +2717,22 @@ fast_fn_t pick_wc(bool where, int ns, bool comma, bool rp3, bool wn) {
     if (!comma) return pick_ns<G, false, false, CANON, true>(ns, rp3);
     return (CANON && !wn) ? pick_ns<G, false, true, CANON, false>(ns, rp3) : pick_ns<G, false, true, CANON, true>(ns, rp3);
 }
+// the compound-WHERE builds (fast_shape: ',' / '"', narrow numerals, two records a pass)
+template <bool G, int WXN>
+fast_fn_t pick_wx(int ns, bool canon) {
+    if (canon) {
+        if (ns == 0) return fast::fast_kernel<G, true, 0, true, true, 2, false, 0, false, WXN>;
+        return ns == 1 ? fast::fast_kernel<G, true, 1, true, true, 2, false, 0, false, WXN>
+                       : fast::fast_kernel<G, true, 2, true, true, 2, false, 0, false, WXN>;
+    }
+    if (ns == 0) return fast::fast_kernel<G, true, 0, true, false, 2, false, 0, false, WXN>;
+    return ns == 1 ? fast::fast_kernel<G, true, 1, true, false, 2, false, 0, false, WXN>
+                   : fast::fast_kernel<G, true, 2, true, false, 2, false, 0, false, WXN>;
+}
 template <bool G>
-fast_fn_t pick_fast(bool where, int ns, bool comma, bool canon, bool rp3, bool wn, int ext = 0, bool wstr = false) {
+fast_fn_t pick_fast(bool where, int ns, bool comma, bool canon, bool rp3, bool wn, int ext = 0, bool wstr = false,
+                    int wx = 0) {
+    if (wx) return wx == 1 ? pick_wx<G, 1>(ns, canon) : pick_wx<G, 2>(ns, canon);
     if (wstr) {    // (fast_shape: ',' / '"', canonical roles, narrow numerals, no MIN / MAX)
         if (ns == 0) return fast::fast_kernel<G, true, 0, true, true, 2, false, 0, true>;
         return ns == 1 ? fast::fast_kernel<G, true, 1, true, true, 2, false, 0, true>
@@ -2508,8 +2818,8 @@ hipError_t cq_launch_fast(const uint8_t* g, const cq::ScanPlan* P, const cq::Gro
     int ns = 0;
     bool where = false, canon = false;
     bool wn = true;
-    int ext = 0;
-    if (!fast_shape(P, grouped, &fp, &ns, &where, &canon, &wn, &ext)) return hipErrorInvalidValue;
+    int ext = 0, wx = 0;
+    if (!fast_shape(P, grouped, &fp, &ns, &where, &canon, &wn, &ext, &wx, s)) return hipErrorInvalidValue;
     if (((uintptr_t)g & 255) != 0) return hipErrorInvalidValue;
     const uint64_t hi = P->range_end < P->n ? P->range_end : P->n;
     const uint64_t lo = P->data_begin > P->range_begin ? P->data_begin : P->range_begin;
@@ -2518,7 +2828,7 @@ hipError_t cq_launch_fast(const uint8_t* g, const cq::ScanPlan* P, const cq::Gro
     // the sampled stride is 120 records' worth (lean_kernel's choice): below the
     // largest stride the records average under 33 bytes -> the three-record pass,
     // over windows of the largest stride (test knob CQGPU_FAST_RP2: keep two)
-    const bool rp3 = !grouped && !ext && !fp.wstr_lit && fp.ws < (uint32_t)fast::WS && !getenv("CQGPU_FAST_RP2");
+    const bool rp3 = !grouped && !ext && !fp.wstr_lit && !wx && fp.ws < (uint32_t)fast::WS && !getenv("CQGPU_FAST_RP2");
     if (rp3) fp.ws = (uint32_t)fast::WS;
     if (hi > lo) {
         const uint64_t wl = lo / fp.ws, wh = (hi - 1) / fp.ws;
@@ -2562,8 +2872,8 @@ hipError_t cq_launch_fast(const uint8_t* g, const cq::ScanPlan* P, const cq::Gro
     // (EXT builds: the packed extreme keys go to the raw table's extpos words)
     if (ext && (!rt || !rt->extpos[fp.ext_acc] || rt->cap < 1)) return hipErrorInvalidValue;
     const bool wstr = fp.wstr_lit != 0;
-    const fast_fn_t fn = grouped ? pick_fast<true>(where, ns, comma, canon, false, wn, ext, wstr)
-                                 : pick_fast<false>(where, ns, comma, canon, rp3, wn, ext, wstr);
+    const fast_fn_t fn = grouped ? pick_fast<true>(where, ns, comma, canon, false, wn, ext, wstr, wx)
+                                 : pick_fast<false>(where, ns, comma, canon, rp3, wn, ext, wstr, wx);
     const size_t lds = fast_lds(grouped, ns);
     cq::set_max_lds((const void*)fn, (int)lds);
     hipLaunchKernelGGL(fn, dim3(grid), dim3(fast::LT), lds, s, g, stats, slow_list, slow_cap, fp,

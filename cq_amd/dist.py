@@ -307,7 +307,7 @@ def init_host_comm() -> None:
     import numpy as np
     import cq_amd
     rank, world = dist.get_rank(), dist.get_world_size()
-    pending = []
+    pending, own_send, own_recv = [], [], []
     ops = {0: dist.ReduceOp.SUM, 1: dist.ReduceOp.MIN, 2: dist.ReduceOp.MAX}
 
     def raw(ptr, nbytes):
@@ -336,15 +336,25 @@ def init_host_comm() -> None:
                 if count:
                     dist.broadcast(view(send, count, dtype), src=peer)
             elif op == 5:                                 # SEND (posted until GROUP_END)
-                if nb:
+                if nb and peer == rank:                   # (gloo has no self transfer: matched in order below)
+                    own_send.append(raw(send, nb).clone())
+                elif nb:
                     pending.append(dist.isend(raw(send, nb), dst=peer))
             elif op == 6:                                 # RECV (posted until GROUP_END)
-                if nb:
+                if nb and peer == rank:
+                    own_recv.append(raw(recv, nb))
+                elif nb:
                     pending.append(dist.irecv(raw(recv, nb), src=peer))
             elif op == 7:                                 # GROUP_END
                 for w in pending:
                     w.wait()
                 pending.clear()
+                if len(own_send) != len(own_recv):
+                    raise RuntimeError("unmatched transfers to self")
+                for a, b in zip(own_send, own_recv):
+                    b.copy_(a)
+                own_send.clear()
+                own_recv.clear()
             else:
                 return 1
             return 0

@@ -4,7 +4,7 @@
 #  =3: + field loads, typing, keys, hashes; the results of these builds are wrong)
 set -e
 cd "$(dirname "$0")/../cq_amd/csrc"
-F="-O3 -std=c++17 -fPIC --offload-arch=gfx950 -ffp-contract=off -I../../include"
+F="-O3 -std=c++17 -fPIC --offload-arch=gfx950 -ffp-contract=off -I../../include -mllvm -amdgpu-sched-strategy=max-ilp"
 for v in ${VARIANTS:-"f1:-DFAST_PROF=1" "f2:-DFAST_PROF=2" "f3:-DFAST_PROF=3"}; do
   n=${v%%:*}; d=$(echo "${v#*:}" | tr "+" " ")
   ( /opt/rocm/bin/hipcc $F $d -c fast.hip -o /tmp/fast_$n.o && \

@@ -13,4 +13,6 @@ cat $OUT/ingest.txt
 timeout -k 10 100 ./scripts/micro/ingest /tmp/f.bin pread 16 32 >> $OUT/ingest.txt 2>&1
 timeout -k 10 100 ./scripts/micro/ingest /tmp/f.bin pread 8 64 >> $OUT/ingest.txt 2>&1
 tail -6 $OUT/ingest.txt
+timeout -k 10 300 python scripts/variant_bench.py base nob f3 --rounds 2 > $OUT/variants.txt 2>&1
+cat $OUT/variants.txt
 exit $rc

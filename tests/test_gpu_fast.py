@@ -341,3 +341,60 @@ def test_fast_string_literal_where(d):
     # the literal itself numeral-shaped (a STRING literal all the same) and a 9-byte literal
     check(f"SELECT role, COUNT(*) FROM '{p}' WHERE gender = '12' GROUP BY role")
     check(f"SELECT role, COUNT(*) FROM '{p}' WHERE gender = 'role_0010' GROUP BY role", fast=False)
+
+
+def test_fast_compound_where(d):
+    """compound WHEREs on fast_kernel (the WX builds): NOT / AND / OR trees of up to 4
+    leaves over up to 2 columns -- comparisons either way round, BETWEEN (AND of >= and
+    <=, parser_expressions.c:481-523), [NOT] IN lists of up to 8 literals -- evaluated
+    as the parsed tree with every leaf evaluated (evaluator_conditions.c:62-164;
+    right-associative, no precedence).  NUMBER columns: 1-4 byte numerals typed as exact
+    10^-3 fixed point compared with the reference's double semantics (dotted fields,
+    literals such as 1.1 that no double equals exactly, negative literals); STRING
+    columns: 1-8 byte words.  Fields of other shapes (wide numerals, dates, blanks,
+    signs, 9+ bytes) and empty ones (NULL) exercise slow_kernel and the NULL outcomes."""
+    rng = np.random.default_rng(91)
+    words = ["f", "m", "fe", "ff", "e", "g", "role_001", "role_0010", "12", "1990-01-01", "-x", ".5", "f ",
+             "zz", "F", ""]
+    ages = [str(x) for x in range(0, 100)] + ["", "12345", "-3", "1.5", "7.25", " 8", "abc", "30.0", "2024-01-05"]
+    hts = ["1.1", "1.10", "2.25", "1.5", "0.001", "1.", ".5", "2", "", "1.1234", "9999", "1.0"]
+    rows = ["%s,%s,%s,%s,role_%03d" % ("n%d" % (i % 5), ages[int(rng.integers(0, len(ages)))] if i % 13 else str(i % 90),
+                                      words[int(rng.integers(0, len(words)))], hts[int(rng.integers(0, len(hts)))],
+                                      int(rng.integers(0, 40))) for i in range(150_000)]
+    p = _write(d / "wx.csv", "name,age,gender,height,role", rows)
+    G = "SELECT role, COUNT(*), SUM(height), AVG(height) FROM '{p}' WHERE {w} GROUP BY role"
+    for w in ("age BETWEEN 20 AND 40",
+              "age > 30 AND gender = 'f'",
+              "age < 20 OR gender != 'm'",
+              "gender = 'f' AND age > 30 OR age < 10",          # AND(=, OR(>, <)): no precedence
+              "NOT age > 30",
+              "30 < age AND 50 >= age",
+              "age > -5 AND height < 2",
+              "height = 1.1 OR height >= 2.25",
+              "height BETWEEN 1.1 AND 1.5",
+              "age IN (10, 20, 30.0, 45)",
+              "age NOT IN (10, 20, 30, 45) AND gender IN ('f', 'm', 'fe')",
+              "role IN ('role_001', 'role_002', 'role_010', 'role_039')",
+              "gender NOT IN ('f', 'm') OR age = 7",
+              "height IN (1.1, 2.25, 0.001, 2)",
+              "age != 50 AND age != 60 AND age != 70 AND gender > 'e'"):
+        check(G.format(p=p, w=w))
+    # ungrouped, two SUM columns, the WHERE column also summed
+    check(f"SELECT COUNT(*), SUM(height) FROM '{p}' WHERE age BETWEEN 25 AND 35")
+    check(f"SELECT COUNT(*) FROM '{p}' WHERE gender = 'f' OR gender = 'm'")
+    check(f"SELECT role, SUM(age), AVG(height) FROM '{p}' WHERE age > 20 AND height > 1.2 GROUP BY role")
+    check(f"SELECT gender, COUNT(*), SUM(age) FROM '{p}' WHERE age BETWEEN 10 AND 60 GROUP BY gender")
+    # outside the compound builds (5 leaves; a column compared with both classes;
+    # 3 WHERE columns): the general kernels, same answers
+    check(G.format(p=p, w="age = 1 OR age = 2 OR age = 3 OR age = 4 OR age = 5"), fast=False)
+    check(G.format(p=p, w="age > 30 OR age = 'abc'"), fast=False)
+    check(G.format(p=p, w="age > 30 AND gender = 'f' AND height > 1.2"), fast=False)
+
+
+def test_fast_compound_where_declines_wide_numerals(d):
+    """a NUMBER WHERE column whose sampled fields exceed 4 bytes keeps the general
+    kernels (the compound builds type <= 4-byte numerals only)"""
+    rows = ["%d,%d.%03d,g%d" % (i % 100, 1000 + i % 9000, i % 1000, i % 7) for i in range(30_000)]
+    p = _write(d / "wxwide.csv", "a,b,g", rows)
+    st = check(f"SELECT g, COUNT(*) FROM '{p}' WHERE b BETWEEN 2000 AND 3000 AND a > 10 GROUP BY g", fast=False)
+    assert st["scan_kernel"] != 2, st
