@@ -489,16 +489,18 @@ def end_to_end(data, config, L, cq_amd, exp, rows):
 
 
 def config5_leg(args, cq_amd, L):
-    """configs[4] as one rank of the 8-GPU node runs it: users x orders of 500 M rows
-    each (`--join-rows` x `--join-ranks`), generated on the device, routed by the
-    product's key routing (whole keys by key mod N) into 8 shards on this one GPU, each
-    shard rebuilt as its rank receives it; rank 0's cqgpu_query_partial (the STAR fused
-    join over its routed 62.5 M + 62.5 M rows with key stride 8) is the timed step.
-    Every rank's partial runs once and their merge is verified against the exact
-    per-role COUNT / SUM(price) and group order of the generators' draws.  Roofline
-    bytes: the rank's two routed CSV shards, HBM traffic from
-    profiles/config5_traffic.json when it was measured for this shape.  CPU baseline:
-    the reference's nested-loop join at 5 K x 5 K and 20 K x 20 K."""
+    """configs[4] as rank 0 of the 8-GPU node runs its WHOLE step, on one GPU: users x
+    orders of 500 M rows each (`--join-rows` x `--join-ranks`), generated on the
+    device and cut into 8 range shards; the step is everything rank 0 does with the
+    typed exchange (bench_join.typed_rank_step_leg): count its users shard's records,
+    type both shards into 16-byte users / 8-byte orders entries routed by key mod 8,
+    receive region 0 of every rank's entries (a device copy standing in for the xGMI
+    transfer, whose bytes are reported beside it), the STAR join over them, the
+    partial blob and the merge of all 8 partials.  Verified against the exact per-role
+    COUNT / SUM(price) and group order of the generators' draws.  Roofline bytes
+    (SURVEY.md 8d): the rank's share of both files + the entries it writes and the
+    entries it reads.  CPU baseline: the reference's nested-loop join at 5 K x 5 K and
+    20 K x 20 K (row-pairs/s, not comparable)."""
     import ctypes as C
     import bench_join as bj
     from cq_amd import abi
@@ -508,17 +510,9 @@ def config5_leg(args, cq_amd, L):
                 "users.csv", alias="u", group_by=["u.role"],
                 joins=[("orders.csv", "o", P.cond("=", P.ident("u.id"), P.ident("o.customer_id")), abi.JOIN_INNER)])
     ast = C.pointer(q)
-    r = bj.routed_share_leg(n * N, N, args.steps, args.warmup, args.seed, torch.device("cuda"), ast)
+    r = bj.typed_rank_step_leg(n * N, N, args.steps, args.warmup, args.seed, torch.device("cuda"), ast)
     step_s = r["step_s"]
-    traffic = None
-    try:
-        with open(os.path.join(ROOT, "profiles", "config5_traffic.json")) as fh:
-            tj = json.load(fh)
-        # (the routed bytes pin the shape: the route's field projection changes them)
-        if tj.get("rows_total") == n * N and tj.get("ranks") == N and tj.get("rank_bytes") == r["bytes"]:
-            traffic = tj.get("hbm_bytes_per_step")
-    except Exception:
-        pass
+    alg = r["file_bytes"] + r["entry_bytes_written"] + r["entry_bytes_read"]
     cpu = None
     if not args.no_cpu:
         cpu = {}
@@ -527,27 +521,30 @@ def config5_leg(args, cq_amd, L):
                 cpu["%dx%d" % (m, m)] = bj.cpu_baseline(m, args.seed)
             except Exception as e:
                 cpu["%dx%d" % (m, m)] = {"error": str(e)}
-    return {"workload": "config5 (rank 0 of %d after the key repartition): SELECT u.role, COUNT(*), SUM(o.price) "
+    xgmi = 7 * 153e9                     # 7 xGMI links per GPU at ~153 GB/s each (peak)
+    return {"workload": "config5 (rank 0 of %d, its whole step): SELECT u.role, COUNT(*), SUM(o.price) "
                         "FROM users u JOIN orders o ON u.id = o.customer_id GROUP BY u.role" % N,
             "users_total": n * N, "orders_total": n * N, "ranks": N,
-            "rank_rows": r["rows"], "rank_bytes": r["bytes"], "rank_file_bytes": r["file_bytes"],
-            "rows_per_rank": r["rank_rows"],
-            "value": r["rows"] / step_s, "unit": "rows/s (rank 0's routed users + orders rows)",
-            "ms_per_step": step_s * 1e3, "kernel_ms": r["kernel_ms"],
-            "step": "cqgpu_query_partial on rank 0's routed shards (STAR join build + probe + flush, "
-                    "first-pair global ids, partial blob); not included: the all-to-all and the merge",
-            "kernel": {4: "cq::fast::jx_extract_kernel<STAR> build + probe (key stride %d), jx_star_first_kernel, "
-                          "jx_star_flush_kernel (+ raw_merge)" % N}.get(r["kinds"][0], "general join pipeline"),
+            "rank_rows": r["rows"], "rank_file_bytes": r["file_bytes"],
+            "value": r["rows"] / step_s, "unit": "rows/s (rank 0's share of the users + orders rows)",
+            "ms_per_step": step_s * 1e3,
+            "step": "count + typed send of both shards (key mod %d) + receive (device copy of the entries the "
+                    "rank receives) + STAR join over the entries + partial blob + merge of the %d partials" % (N, N),
+            "phases_ms": r["phases_ms"],
             "kernel_kinds_per_rank": r["kinds"],
-            "roofline": {"bound": "hbm", "achieved": r["file_bytes"] / step_s / 1e9, "peak": HBM_PEAK_GBS,
-                         "unit": "GB/s", "frac": r["file_bytes"] / step_s / 1e9 / HBM_PEAK_GBS, "traffic": traffic,
-                         "algorithmic_bytes": "rank 0's share of the users + orders files: its routed rows as whole "
-                                              "CSV records (SURVEY.md 8d: bytes = file bytes)",
-                         "shard_bytes": r["bytes"],
-                         "frac_of_shard": r["bytes"] / step_s / 1e9 / HBM_PEAK_GBS,
-                         "shard": "the routed shard the step reads: each record cut to the fields the plan "
-                                  "needs by the route (bytes read once / step / peak = frac_of_shard)"},
-            "route_whole_inputs_s": r["route_s"],
+            "exchange": {"sent_bytes": r["xgmi_sent_bytes"], "received_bytes": r["xgmi_received_bytes"],
+                         "entries_received": r["recv_entries"],
+                         "entry_bytes": "16 per users record {key/N - qbase, global id, GROUP BY bytes}, 8 per "
+                                        "orders record {key/N - qbase, price in 10^-3}",
+                         "xgmi_bound_ms": max(r["xgmi_sent_bytes"], r["xgmi_received_bytes"]) / xgmi * 1e3,
+                         "note": "not in ms_per_step: one GPU has no peer; xgmi_bound_ms = the larger direction "
+                                 "over 7 links at their 153 GB/s peak"},
+            "roofline": {"bound": "hbm", "achieved": alg / step_s / 1e9, "peak": HBM_PEAK_GBS,
+                         "unit": "GB/s", "frac": alg / step_s / 1e9 / HBM_PEAK_GBS, "traffic": None,
+                         "algorithmic_bytes": alg,
+                         "algorithmic": "rank 0's share of both files (%d B) + the entries its send pass writes "
+                                        "(%d B) + the entries its join reads (%d B) (SURVEY.md 8d)"
+                                        % (r["file_bytes"], r["entry_bytes_written"], r["entry_bytes_read"])},
             "joined_pairs": r["joined_pairs"],
             "verified": r["verified"],
             "verified_against": "every rank's partial merged (cqgpu_merge_partials) vs the exact per-role COUNT / "

@@ -262,7 +262,7 @@ def dist_join_leg(n: int, rank: int, world: int, steps: int, warmup: int, seed: 
         cq_amd.result_free(last)
         rows = res["rows"]
         want = [r for r in np.argsort(first, kind="stable") if cnt[r] > 0]
-        ok = len(rows) == len(want) and all(k == 4 for k in kinds)
+        ok = len(rows) == len(want) and all(k in (4, 5) for k in kinds)     # (5: the typed exchange)
         for row, r in zip(rows, want if ok else []):
             name = row[0][1].decode() if isinstance(row[0][1], bytes) else row[0][1]
             ws = cents[r] / 100.0
@@ -383,6 +383,136 @@ def routed_share_leg(n_total: int, nranks: int, steps: int, warmup: int, seed: i
             "file_bytes": file_share,
             "rank_rows": rank_rows, "kinds": kinds, "verified": ok, "route_s": route_s, "gen_s": gen_s,
             "joined_pairs": int(cnt.sum())}
+
+
+def typed_rank_step_leg(n_total: int, nranks: int, steps: int, warmup: int, seed: int, device, ast):
+    """BASELINE config 5 as rank 0 of an `nranks`-GPU node runs its WHOLE step, on one
+    GPU, with the typed exchange (include/cqgpu.h cqgpu_typed_*): the n_total x n_total
+    inputs are generated on the device and cut into `nranks` range shards (the files'
+    byte ranges every rank holds); ranks 1..N-1's sends and partials are prepared once,
+    untimed.  One timed step is everything rank 0 does:
+      count    its users shard's records per window (the global ids' bases)
+      send     both shards typed into 16-byte users / 8-byte orders entries by key mod N
+      receive  region 0 of every rank's entries gathered into its receive buffers (a
+               device copy standing in for the xGMI transfer, whose bytes are reported)
+      join     the STAR join over the received entries, its partial blob
+      merge    cqgpu_merge_partials of the N blobs (rank 0's role)
+    The merged answer is verified against the generators' exact per-role COUNT /
+    SUM(price) and first-appearance order."""
+    import torch
+    import cq_amd
+    from cq_amd import abi
+    uh, oh = b"id,name,age,role\n", b"id,price,quantity,customer_id\n"
+    t0 = time.time()
+    ub, ob, cnt, cents, first = gen_config5_device(n_total, seed, device)
+    torch.cuda.synchronize(device)
+    gen_s = time.time() - t0
+    if n_total % nranks:
+        raise ValueError("rows not divisible by ranks")
+    n = n_total // nranks
+    U, O = [], []
+    for r in range(nranks):
+        gids = torch.arange(n, dtype=torch.int64, device=device)
+        us, os_ = ub[r * n * 31:(r + 1) * n * 31], ob[r * n * 33:(r + 1) * n * 33]
+        U.append(cq_amd.table_from_routed(us.data_ptr(), us.numel(), gids.data_ptr(), n, uh))
+        O.append(cq_amd.table_from_routed(os_.data_ptr(), os_.numel(), gids.data_ptr(), n, oh))
+    file_bytes = n * 31 + n * 33
+    del ub, ob
+    torch.cuda.empty_cache()
+    pair = lambda r: [U[r], O[r]]  # noqa: E731
+    if not cq_amd.typed_plan(ast, pair(0)):
+        raise RuntimeError("config 5's plan outside the typed exchange: " + cq_amd.last_ineligible())
+    nrec = [cq_amd.typed_count(ast, pair(r)) for r in range(nranks)]
+    gbase = [sum(nrec[:r]) for r in range(nranks)]
+    smin = min(cq_amd.typed_sample_kmin(ast, pair(r)) for r in range(nranks))
+    qbase = smin // nranks
+    cu, co, kmin, kmax, flags = [], [], (1 << 64) - 1, 0, 0
+    for r in range(nranks):
+        c1, kr, f1 = cq_amd.typed_send(ast, pair(r), 0, nranks, qbase, gbase[r])
+        c2, _, f2 = cq_amd.typed_send(ast, pair(r), 1, nranks, qbase, 0)
+        cu.append(c1)
+        co.append(c2)
+        kmin, kmax, flags = min(kmin, kr[0]), max(kmax, kr[1]), flags | f1 | f2
+    if flags:
+        raise RuntimeError(f"typed send flags {flags:#x}")
+    qoff, rng = kmin // nranks - qbase, kmax // nranks - kmin // nranks + 1
+    recv_u = [sum(cu[s][d] for s in range(nranks)) for d in range(nranks)]
+    recv_o = [sum(co[s][d] for s in range(nranks)) for d in range(nranks)]
+    bu = torch.empty(max(recv_u) * 16 + 16, dtype=torch.uint8, device=device)
+    bo = torch.empty(max(recv_o) * 8 + 16, dtype=torch.uint8, device=device)
+    blobs = [None] * nranks
+    kinds = [None] * nranks
+    for d in range(1, nranks):                      # the other ranks' partials (untimed)
+        torch.cuda.synchronize(device)
+        nu = cq_amd.typed_gather(U, d, bu.data_ptr(), recv_u[d])
+        no = cq_amd.typed_gather(O, d, bo.data_ptr(), recv_o[d])
+        blobs[d] = cq_amd.typed_partial(ast, pair(d), bu.data_ptr(), nu, bo.data_ptr(), no, qoff, rng)
+        kinds[d] = cq_amd.stats().get("scan_kernel")
+        if blobs[d] is None:
+            raise RuntimeError(cq_amd.last_ineligible() or cq_amd.last_error())
+    phases = {}
+
+    def step(timed_phases=False):
+        def mark(name):
+            if timed_phases:
+                torch.cuda.synchronize(device)
+                phases[name] = phases.get(name, 0.0) + time.perf_counter() - mark.t
+                mark.t = time.perf_counter()
+        mark.t = time.perf_counter()
+        cq_amd.typed_reset(U[0])
+        cq_amd.typed_reset(O[0])
+        cq_amd.typed_count(ast, pair(0))
+        mark("count")
+        c1, _, f1 = cq_amd.typed_send(ast, pair(0), 0, nranks, qbase, gbase[0])
+        c2, _, f2 = cq_amd.typed_send(ast, pair(0), 1, nranks, qbase, 0)
+        if f1 | f2:
+            raise RuntimeError(f"typed send flags {f1 | f2:#x}")
+        mark("send")
+        nu = cq_amd.typed_gather(U, 0, bu.data_ptr(), recv_u[0])
+        no = cq_amd.typed_gather(O, 0, bo.data_ptr(), recv_o[0])
+        mark("receive")
+        blob = cq_amd.typed_partial(ast, pair(0), bu.data_ptr(), nu, bo.data_ptr(), no, qoff, rng)
+        if blob is None:
+            raise RuntimeError(cq_amd.last_ineligible() or cq_amd.last_error())
+        kinds[0] = cq_amd.stats().get("scan_kernel")
+        mark("join")
+        tp = cq_amd.merge_partials(ast, [blob] + blobs[1:])
+        mark("merge")
+        return tp
+    for _ in range(warmup):
+        cq_amd.result_free(step())
+    torch.cuda.synchronize(device)
+    t1 = time.perf_counter()
+    last = None
+    for _ in range(steps):
+        tp = step()
+        if last:
+            cq_amd.result_free(last)
+        last = tp
+    torch.cuda.synchronize(device)
+    step_s = (time.perf_counter() - t1) / steps
+    cq_amd.result_free(step(timed_phases=True))      # one more step, synchronised per phase
+    res = abi.table_to_py(last)
+    cq_amd.result_free(last)
+    rows = res["rows"]
+    want = [r for r in np.argsort(first, kind="stable") if cnt[r] > 0]
+    ok = len(rows) == len(want) and all(k == 5 for k in kinds)
+    for row, r in zip(rows, want if ok else []):
+        name = row[0][1].decode() if isinstance(row[0][1], bytes) else row[0][1]
+        ws = cents[r] / 100.0
+        if name != "role_%03d" % r or row[1][1] != cnt[r] or abs(row[2][1] - ws) > 1e-6 * ws:
+            ok = False
+            break
+    sent = sum(16 * cu[0][d] + 8 * co[0][d] for d in range(1, nranks))
+    received = sum(16 * cu[s][0] + 8 * co[s][0] for s in range(1, nranks))
+    entry_bytes_written = 16 * sum(cu[0]) + 8 * sum(co[0])
+    entry_bytes_read = 16 * recv_u[0] + 8 * recv_o[0]
+    for t in U + O:
+        t.close()
+    return {"step_s": step_s, "rows": 2 * n, "file_bytes": file_bytes, "entry_bytes_written": entry_bytes_written,
+            "entry_bytes_read": entry_bytes_read, "xgmi_sent_bytes": sent, "xgmi_received_bytes": received,
+            "phases_ms": {k: round(v * 1e3, 4) for k, v in phases.items()}, "kinds": kinds, "verified": ok,
+            "gen_s": gen_s, "joined_pairs": int(cnt.sum()), "recv_entries": [recv_u[0], recv_o[0]]}
 
 
 def cpu_baseline(n: int, seed: int):

@@ -114,6 +114,24 @@ def lib():
         L.cqgpu_comm_init.restype = C.c_int
         L.cqgpu_comm_init.argtypes = [vp, C.c_int, C.c_int]
         L.cqgpu_comm_destroy.argtypes = []
+        L.cqgpu_typed_plan.restype = C.c_int
+        L.cqgpu_typed_plan.argtypes = [C.POINTER(abi.Node), C.POINTER(vp), C.c_int]
+        L.cqgpu_typed_sample_kmin.restype = C.c_uint64
+        L.cqgpu_typed_sample_kmin.argtypes = [C.POINTER(abi.Node), C.POINTER(vp), C.c_int]
+        L.cqgpu_typed_count.restype = C.c_int64
+        L.cqgpu_typed_count.argtypes = [C.POINTER(abi.Node), C.POINTER(vp), C.c_int]
+        L.cqgpu_typed_send.restype = C.c_int
+        L.cqgpu_typed_send.argtypes = [C.POINTER(abi.Node), C.POINTER(vp), C.c_int, C.c_int, C.c_int, C.c_uint64,
+                                       C.c_uint64, C.c_uint64, C.POINTER(C.c_uint64), C.POINTER(C.c_uint64),
+                                       C.POINTER(C.c_uint32)]
+        L.cqgpu_typed_region.restype = vp
+        L.cqgpu_typed_region.argtypes = [vp, C.c_int, C.POINTER(C.c_uint64), C.POINTER(C.c_uint64)]
+        L.cqgpu_typed_reset.argtypes = [vp]
+        L.cqgpu_typed_gather.restype = C.c_int64
+        L.cqgpu_typed_gather.argtypes = [C.POINTER(vp), C.c_int, C.c_int, vp, C.c_uint64]
+        L.cqgpu_typed_partial.restype = C.c_size_t
+        L.cqgpu_typed_partial.argtypes = [C.POINTER(abi.Node), C.POINTER(vp), C.c_int, vp, C.c_uint64, vp, C.c_uint64,
+                                          C.c_uint64, C.c_uint64, C.POINTER(vp)]
         L.cqgpu_comm_init_host.restype = C.c_int
         L.cqgpu_comm_init_host.argtypes = [C.c_int, C.c_int, COLL_FN, vp]
         L.cqgpu_dist_query.restype = TP
@@ -384,3 +402,55 @@ def gm_local(ast, shards):
     lib().cqgpu_result_free(tp)
     return out
 
+
+
+# ---- the typed exchange of the repartitioned JOIN (include/cqgpu.h cqgpu_typed_*)
+def typed_plan(ast, tables) -> bool:
+    return lib().cqgpu_typed_plan(ast, *_tables_arg(tables)) == 1
+
+
+def typed_sample_kmin(ast, tables) -> int:
+    return lib().cqgpu_typed_sample_kmin(ast, *_tables_arg(tables))
+
+
+def typed_count(ast, tables) -> int:
+    n = lib().cqgpu_typed_count(ast, *_tables_arg(tables))
+    if n < 0:
+        raise RuntimeError(last_error() or "cqgpu_typed_count failed")
+    return n
+
+
+def typed_send(ast, tables, side: int, nranks: int, qbase: int, gid_base: int, cap: int = 0):
+    """(counts per destination, (build keys' min, max), flags)"""
+    counts = (C.c_uint64 * nranks)()
+    kr = (C.c_uint64 * 2)()
+    fl = C.c_uint32(0)
+    if lib().cqgpu_typed_send(ast, *_tables_arg(tables), side, nranks, qbase, gid_base, cap, counts, kr,
+                              C.byref(fl)) != 0:
+        raise RuntimeError(last_error() or "cqgpu_typed_send failed")
+    return list(counts), (kr[0], kr[1]), fl.value
+
+
+def typed_reset(table) -> None:
+    lib().cqgpu_typed_reset(table.handle)
+
+
+def typed_gather(senders, dest: int, dev_out: int, cap_entries: int) -> int:
+    arr = (C.c_void_p * len(senders))(*[t.handle.value for t in senders])
+    n = lib().cqgpu_typed_gather(arr, len(senders), dest, dev_out, cap_entries)
+    if n < 0:
+        raise RuntimeError(last_error() or "cqgpu_typed_gather failed")
+    return n
+
+
+def typed_partial(ast, tables, build_ptr: int, nbuild: int, probe_ptr: int, nprobe: int, qoff: int, rng: int):
+    """the blob, or None with last_ineligible() saying why the entries left the STAR join"""
+    out = C.c_void_p()
+    n = lib().cqgpu_typed_partial(ast, *_tables_arg(tables), build_ptr, nbuild, probe_ptr, nprobe, qoff,
+                                  rng, C.byref(out))
+    if n == 0:
+        return None
+    try:
+        return C.string_at(out, n)
+    finally:
+        C.CDLL(None).free(out)

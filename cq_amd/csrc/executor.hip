@@ -66,6 +66,7 @@ hipError_t cq_launch_gather(const uint8_t* g, const ScanPlan* P, const unsigned 
 hipError_t cq_launch_copy_strings(const Cell* cells, uint32_t n, const unsigned long long* offs,
                                   uint8_t* out, hipStream_t s);
 cq::Cell cq_host_parse_cell(const uint8_t* text, uint32_t len);
+cq::GKey cq_host_group_key(cq::Cell c);
 cq::Cell cq_host_eval(const cq::Insn* code, uint32_t n, const cq::Cell* cols, const cq::Cell* consts);
 hipError_t cq_launch_cells(const uint8_t* g, uint64_t tn, const unsigned long long* recs, uint32_t n,
                            const cq::ColsDesc* D, cq::Cell* out, hipStream_t s);
@@ -219,6 +220,16 @@ hipError_t cq_jx_star_flush(int grouped, int value, const unsigned long long* tt
                             const unsigned long long* cnts, const cq::GroupTable* rt, int nacc, cq::ScanStats* stats,
                             unsigned int* flag, hipStream_t s);
 uint32_t cq_jx_star_groups();
+hipError_t cq_jx_route(const uint8_t* g, uint64_t lo, uint64_t hi, uint32_t ws, uint32_t delim, uint32_t quote,
+                       int kcol, int pcol, int build, int rp, const unsigned int* wbase, uint32_t nranks,
+                       unsigned long long qbase, unsigned long long gbase, void* rent, unsigned long long rcap,
+                       unsigned long long* rcount, unsigned int* flag, unsigned long long* krange, int grid,
+                       hipStream_t s);
+hipError_t cq_jx_ent_build(const void* ent, unsigned long long n, uint32_t qoff, unsigned long long range, uint16_t* d16,
+                           uint32_t* l32, unsigned long long* ttab, unsigned long long* nplaced, unsigned int* flag,
+                           int grid, hipStream_t s, int ungrouped);
+hipError_t cq_jx_ent_probe(const void* ent, unsigned long long n, uint32_t qoff, unsigned long long range, uint16_t* d16,
+                           unsigned long long* gsum, unsigned long long* npairs, int grid, hipStream_t s);
 hipError_t cq_jx_probe(int grouped, int value, int direct, const unsigned long long* pkey,
                        const unsigned long long* ppay, const uint32_t* poff, uint32_t n, unsigned long long kmin,
                        const void* table, uint64_t tcap, const unsigned long long* bpay, const uint32_t* boff,
@@ -239,6 +250,7 @@ hipError_t cq_launch_project(const uint8_t* g, const unsigned long long* recs, u
                              const ProjDesc* D, Cell* scratch, Cell* out, hipStream_t s);
 int cq_set_scan_mode(int mode);
 int cq_scan_uses_lean(const cq::ScanPlan* P, int with_cells);
+int cq_fast_eligible(const cq::ScanPlan* P, int grouped, int want_rows);
 int cq_scan_kernel_kind(const cq::ScanPlan* P, int grouped, int want_rows, int with_cells);
 uint32_t cq_fast_seed(const uint8_t* data, uint64_t n, uint32_t delim, uint32_t quote, uint32_t col,
                       unsigned long long* tags);
@@ -577,6 +589,16 @@ struct RouteState {
     uint32_t last_keep = ~0u;
 };
 
+// the typed join exchange's send side of one table (cqgpu_typed_send): nranks regions
+// of `cap` fixed-size entries (16 B build, 8 B probe), counts[d] of them used
+struct TypedSend {
+    DevBuf ent;
+    uint64_t cap = 0, esize = 0;
+    std::vector<uint64_t> counts;
+    uint32_t flags = 0;
+    unsigned long long krange[2] = {~0ull, 0ull};   // the build side's keys' min, max (every non-NULL one)
+};
+
 constexpr uint64_t SAMPLE_BYTES = 256u << 10;   // bytes a table keeps for plan-time sampling
 
 // the device byte ranges of the live tables: a group's STRING cells (representative,
@@ -620,6 +642,12 @@ struct cqgpu_table {
     std::unique_ptr<RouteState> route;    // pending repartition (cqgpu_route_plan)
     std::unique_ptr<DevBuf> rec_starts;   // record start offsets, file order (built on first need; immutable table)
     uint32_t nrec_starts = 0;
+    // the typed join exchange (cqgpu_typed_*): this table's pending entries, and its
+    // record count and per-window record bases of the stride they were counted at
+    std::unique_ptr<TypedSend> tsend;
+    uint64_t typed_nrec = ~0ull;
+    uint32_t typed_ws = 0;
+    std::unique_ptr<DevBuf> typed_wbase;
 };
 
 namespace {
@@ -5369,6 +5397,8 @@ int cqgpu_explain(cq_node* q, const char* header, cq_csv_config cfg, char* out, 
         t.cfg = cfg;
         size_t hl = strlen(header);
         t.names = split_header(header, header + hl, cfg.delimiter, cfg.quote, cfg.has_header);
+        t.wide4_cols = 0;           // (no sample: every field taken as narrow, keys as <= 8 bytes)
+        t.long_cols = 0;
         check_plan_shape(q, &t);
         Compiled C;
         std::string s;
@@ -5401,6 +5431,10 @@ int cqgpu_explain(cq_node* q, const char* header, cq_csv_config cfg, char* out, 
             s += " " + std::to_string(C.P.prog[i].op) + "/" + std::to_string(C.P.prog[i].a) + "/" +
                  std::to_string(C.P.prog[i].b);
         s += "\ngroup_slot: " + std::to_string(C.P.group_slot) + (C.group_missing ? " missing" : "");
+        // (the literals typed on the host, as parse_literals types them for a launch)
+        for (size_t i = 0; i < C.lits.size() && i < (size_t)MAX_CONST; i++)
+            C.P.consts[i] = cq_host_parse_cell((const uint8_t*)C.lits[i].data(), (uint32_t)C.lits[i].size());
+        s += "\nfast: " + std::to_string(cq_fast_eligible(&C.P, C.grouped ? 1 : 0, 0));
         s += "\nacc:";
         for (int a = 0; a < C.P.nacc; a++)
             s += " " + std::to_string(C.P.acc[a].kind) + "@" + std::to_string(C.P.acc[a].slot);
@@ -5666,6 +5700,48 @@ int cqgpu_join_outer_set(int level, const uint8_t* matched, uint64_t n, int emit
 
 void cqgpu_join_outer_clear(void) { g_outer_sets.clear(); }
 
+}  // extern "C"
+
+namespace {
+// a join partial's "CQJ1" blob (cqgpu_query_partial; the typed exchange's partials too)
+void join_blob(const JoinPartial& jp, Blob& b) {
+    if (jp.nacc < 0) throw HipError{"join partial: the plan's shape was not recorded"};
+    const int nacc = jp.nacc;
+    const uint32_t nrep = jp.nrep, nvla = jp.nvla;
+    b.d.reserve(256 + (jp.direct ? jp.gblob.size() : jp.groups.size() * (64 + 48 * (size_t)nacc + 24 * (size_t)nrep)));
+    b.u32(0x314a5143u);                      // "CQJ1"
+    b.u32((uint32_t)jp.names.size());
+    for (auto& nm : jp.names) b.str(nm);
+    b.u32((uint32_t)nacc);
+    for (int a = 0; a < nacc; a++) b.u32(jp.acc_classes[a]);
+    b.u32(nrep);
+    b.u32(nvla);
+    b.u32(jp.lmask);
+    b.u32(jp.rmask);
+    if (jp.direct) {                          // (run_fast_join wrote the groups already)
+        b.u64(jp.ng);
+        b.raw(jp.gblob.data(), jp.gblob.size());
+    } else {
+        b.u64(jp.groups.size());
+    }
+    for (const HGroup& h : jp.groups) {
+        b.u32(h.kcls); b.u32(h.klen); b.u64(h.kw0); b.u64(h.kw1); b.str(h.kbytes);
+        b.u64(h.cnt); b.u64(h.first);
+        for (int a = 0; a < nacc; a++) {
+            b.f64(h.sum[a]); b.u64(h.num[a]); b.u64(h.extpos[a]); b.cell(h.ext[a]);
+        }
+        for (uint32_t r = 0; r < nrep; r++) b.cell(r < h.reps.size() ? h.reps[r] : HCell());
+        for (size_t v = 0; v < nvla; v++) {
+            b.f64(h.vsum[v]); b.f64(h.vm2[v]); b.f64(h.vn[v]);
+            b.mvals(v < h.mvals.size() ? &h.mvals[v] : nullptr);
+        }
+        b.split(h.split);
+    }
+}
+}  // namespace
+
+extern "C" {
+
 size_t cqgpu_query_partial(cq_node* q, cqgpu_table* const* tables, int ntables, void** blob_out) {
     if (blob_out) *blob_out = nullptr;
     g_inel.clear();
@@ -5705,39 +5781,8 @@ size_t cqgpu_query_partial(cq_node* q, cqgpu_table* const* tables, int ntables, 
                 *blob_out = out;
                 return b.d.size();
             }
-            if (jp.nacc < 0) throw HipError{"join partial: the plan's shape was not recorded"};
-            const int nacc = jp.nacc;
-            const uint32_t nrep = jp.nrep, nvla = jp.nvla;
             Blob b;
-            b.d.reserve(256 + jp.groups.size() * (64 + 48 * (size_t)nacc + 24 * (size_t)nrep));
-            b.u32(0x314a5143u);                      // "CQJ1"
-            b.u32((uint32_t)jp.names.size());
-            for (auto& nm : jp.names) b.str(nm);
-            b.u32((uint32_t)nacc);
-            for (int a = 0; a < nacc; a++) b.u32(jp.acc_classes[a]);
-            b.u32(nrep);
-            b.u32(nvla);
-            b.u32(jp.lmask);
-            b.u32(jp.rmask);
-            if (jp.direct) {                          // (run_fast_join wrote the groups already)
-                b.u64(jp.ng);
-                b.raw(jp.gblob.data(), jp.gblob.size());
-            } else {
-                b.u64(jp.groups.size());
-            }
-            for (const HGroup& h : jp.groups) {
-                b.u32(h.kcls); b.u32(h.klen); b.u64(h.kw0); b.u64(h.kw1); b.str(h.kbytes);
-                b.u64(h.cnt); b.u64(h.first);
-                for (int a = 0; a < nacc; a++) {
-                    b.f64(h.sum[a]); b.u64(h.num[a]); b.u64(h.extpos[a]); b.cell(h.ext[a]);
-                }
-                for (uint32_t r = 0; r < nrep; r++) b.cell(r < h.reps.size() ? h.reps[r] : HCell());
-                for (size_t v = 0; v < nvla; v++) {
-                    b.f64(h.vsum[v]); b.f64(h.vm2[v]); b.f64(h.vn[v]);
-                    b.mvals(v < h.mvals.size() ? &h.mvals[v] : nullptr);
-                }
-                b.split(h.split);
-            }
+            join_blob(jp, b);
             PHASE("serialize");
             void* out = malloc(std::max<size_t>(b.d.size(), 1));
             if (!out) throw HipError{"out of host memory"};
@@ -6833,6 +6878,446 @@ void cqgpu_partial_free(cqgpu_partial* p) { delete p; }
 
 }  // extern "C"
 
+// ==================================================================== typed join exchange
+// SURVEY.md section 8e's (key, row id, payload) entries for the repartitioned JOIN: the
+// sender types every record once (fast.hip jx_extract_kernel ROUTE: the ON key as a
+// canonical INTEGER, the build side's GROUP BY bytes or the probe side's SUM argument
+// as 10^-3 fixed point) and writes a fixed-size entry into its destination's region
+// (key mod N) -- 16 bytes {key / N - qbase, global record id, tag} per build record,
+// 8 bytes {key / N - qbase, payload} per probe record -- instead of CSV text; the
+// receiver's STAR join reads the entries (jx_ent_*) instead of re-parsing.  Plans:
+// one INNER JOIN `l.k = r.k` without WHERE, COUNT / SUM / AVG of one right column,
+// GROUP BY one left column (its value the only other item) or no GROUP BY.  Anything
+// the entries cannot carry exactly (a quote, a key that is not a canonical INTEGER or
+// NULL, a GROUP BY value over 8 bytes, a wider numeral, a NULL or repeated build key,
+// more than JX_G groups, a sparse key range) sends every rank back to the CSV-record
+// exchange together.
+namespace {
+
+struct TypedJoin {
+    Compiled C;
+    std::vector<std::string> names;   // the joined schema (alias.col)
+    int kl = -1, kr = -1;             // ON key columns of the left / right table
+    int gcol = -1;                    // GROUP BY column (left table; -1: no GROUP BY)
+    int vcol = -1;                    // SUM / AVG argument (right table; -1: none)
+};
+
+bool typed_join_plan(cq_node* q, const cqgpu_table* L, const cqgpu_table* R, TypedJoin& tj, std::string& why) {
+    why.clear();
+    if (getenv("CQGPU_NO_TYPED_JOIN")) { why = "disabled"; return false; }
+    if (!q || q->kind != CQ_N_QUERY || q->u.q.join_count != 1 || !L || !R) { why = "not one JOIN"; return false; }
+    cq_node* jn = q->u.q.joins[0];
+    if (!jn || jn->kind != CQ_N_JOIN || jn->u.join.kind != CQ_JOIN_INNER) { why = "not an INNER JOIN"; return false; }
+    if (L->cfg.delimiter != ',' || L->cfg.quote != '"' || R->cfg.delimiter != ',' || R->cfg.quote != '"') {
+        why = "CSV dialect";
+        return false;
+    }
+    try {
+        check_plan_shape(q, L, true);
+        cq_node* on = jn->u.join.on;
+        const std::string la = (q->u.q.from && q->u.q.from->u.from.alias) ? q->u.q.from->u.from.alias : "main";
+        const std::string ra = jn->u.join.alias ? jn->u.join.alias : "right";
+        cqgpu_table W;
+        W.names = L->names;
+        if (on && on->kind == CQ_N_CONDITION && on->u.bin.op && !strcmp(on->u.bin.op, "=") && on->u.bin.lhs &&
+            on->u.bin.rhs && on->u.bin.lhs->kind == CQ_N_IDENTIFIER && on->u.bin.rhs->kind == CQ_N_IDENTIFIER) {
+            tj.kl = join_on_index(on->u.bin.lhs->u.text, &W, &W, la.c_str(), R, ra.c_str());
+            tj.kr = join_on_index(on->u.bin.rhs->u.text, R, &W, la.c_str(), R, ra.c_str());
+        }
+        if (tj.kl < 0 || tj.kr < 0) { why = "ON"; return false; }
+        tj.names.clear();
+        for (auto& nm : L->names) tj.names.push_back(la + "." + nm);
+        for (auto& nm : R->names) tj.names.push_back(ra + "." + nm);
+        cqgpu_table J;
+        J.cfg = L->cfg;
+        J.names = tj.names;
+        if (is_row_query(q)) { why = "row-returning"; return false; }
+        compile_aggregate(&J, q, tj.C);
+    } catch (Ineligible& e) {
+        why = e.why;
+        return false;
+    }
+    const Compiled& C = tj.C;
+    const int nl = (int)L->names.size();
+    if (C.group_missing || C.P.nprog != 0 || C.P.ngpart != 0 || !C.vla.empty() || C.wide) { why = "plan"; return false; }
+    if (C.grouped) {
+        if (C.P.group_slot < 0) { why = "GROUP BY"; return false; }
+        tj.gcol = C.need_cols[C.P.group_slot];
+        if (tj.gcol >= nl) { why = "GROUP BY a right column"; return false; }
+    }
+    for (int a = 0; a < C.P.nacc; a++) {
+        if (C.P.acc[a].kind != ACC_SUM) { why = "MIN / MAX"; return false; }
+        const int col = C.need_cols[C.P.acc[a].slot];
+        if (col < nl || (tj.vcol >= 0 && col - nl != tj.vcol)) { why = "aggregate columns"; return false; }
+        tj.vcol = col - nl;
+    }
+    for (int rc : C.rep_cols)
+        if (rc != tj.gcol) { why = "an item other than the GROUP BY column"; return false; }
+    for (const OutCol& o : C.outs)
+        if (o.kind != OUT_COUNT && o.kind != OUT_SUM && o.kind != OUT_AVG && o.kind != OUT_REP && o.kind != OUT_CONST &&
+            o.kind != OUT_NULL) {
+            why = "items";
+            return false;
+        }
+    return true;
+}
+
+// the window stride and records per lane pass of a side (run_fast_join's rule)
+void typed_stride(const cqgpu_table* t, uint32_t* ws, int* rp) {
+    const uint32_t w = t->lean_ws ? t->lean_ws : 3968u;
+    *rp = w < 3968u && !getenv("CQGPU_FAST_RP2") ? 3 : 2;
+    *ws = *rp == 3 ? 3968u : w;
+}
+
+// a first qbase guess: the build side's sampled keys' minimum (sample_key_range pads it
+// down) / N -- a key below it flags the send (16) and the retry takes the exact minimum
+uint64_t typed_sample_kmin(const cqgpu_table* t, int kcol) {
+    uint64_t kmin = 0, kmax = 0, est = 0;
+    if (!sample_key_range(t, kcol, 1, &kmin, &kmax, &est)) return 0;
+    return kmin;
+}
+
+// the build side's records (the count pass: per window its record count, exclusive
+// scan -> each window's first record index); kept on the table (immutable)
+uint64_t typed_count(DevCtx& c, cqgpu_table* t, int kcol, int pcol) {
+    uint32_t ws;
+    int rp;
+    typed_stride(t, &ws, &rp);
+    if (t->typed_nrec != ~0ull && t->typed_ws == ws && t->typed_wbase) return t->typed_nrec;
+    const uint64_t nw = cq_jx_windows(t->data_begin, t->n, ws);
+    if (nw >= (1ull << 31)) throw Ineligible{"typed exchange: too many windows"};
+    DevBuf wc(std::max<uint64_t>(nw, 1) * 4), ctl(64);
+    std::unique_ptr<DevBuf> wb(new DevBuf(std::max<uint64_t>(nw, 1) * 4));
+    HIPCHECK(hipMemsetAsync(ctl.p, 0, 64, c.stream));
+    HIPCHECK(cq_jx_extract(t->g, t->data_begin, t->n, ws, (uint8_t)t->cfg.delimiter, (uint8_t)t->cfg.quote, kcol, pcol,
+                           1, 0, nullptr, nullptr, nullptr, wc.as<unsigned int>(), nullptr, 0, ctl.as<unsigned int>(),
+                           (unsigned long long*)(ctl.as<uint8_t>() + 16), c.ncu, c.stream));
+    uint64_t n = 0;
+    if (nw) {
+        size_t tb = 0;
+        HIPCHECK(cq_excl_sum_u32(nullptr, &tb, wc.as<unsigned int>(), wb->as<unsigned int>(), nw, c.stream));
+        DevBuf tmp(tb + 16);
+        HIPCHECK(cq_excl_sum_u32(tmp.p, &tb, wc.as<unsigned int>(), wb->as<unsigned int>(), nw, c.stream));
+        unsigned int tail[2] = {0, 0};
+        HIPCHECK(hipMemcpyAsync(&tail[0], wb->as<unsigned int>() + nw - 1, 4, hipMemcpyDeviceToHost, c.stream));
+        HIPCHECK(hipMemcpyAsync(&tail[1], wc.as<unsigned int>() + nw - 1, 4, hipMemcpyDeviceToHost, c.stream));
+        HIPCHECK(hipStreamSynchronize(c.stream));
+        n = (uint64_t)tail[0] + tail[1];
+    }
+    t->typed_nrec = n;
+    t->typed_ws = ws;
+    t->typed_wbase = std::move(wb);
+    return n;
+}
+
+// one side's entries into nranks regions (t->tsend); `cap` entries per region (0: an
+// estimate from the record count); flags as cq_jx_route's, plus 256 when a region was
+// too small (counts then hold the entries each region needed)
+void typed_send(DevCtx& c, cqgpu_table* t, bool build, int kcol, int pcol, int nranks, uint64_t qbase,
+                uint64_t gbase, uint64_t cap) {
+    uint32_t ws;
+    int rp;
+    typed_stride(t, &ws, &rp);
+    const unsigned int* wbase = nullptr;
+    uint64_t nrec = 0;
+    if (build) {
+        nrec = typed_count(c, t, kcol, pcol);
+        wbase = t->typed_wbase->as<unsigned int>();
+    } else {
+        const uint64_t nb = t->n > t->data_begin ? t->n - t->data_begin : 0;
+        nrec = (uint64_t)((double)nb / std::max(2.0, sample_record_bytes(t)) * 1.05) + 1;
+    }
+    if (!cap) cap = nrec / (uint64_t)nranks + nrec / (8 * (uint64_t)nranks) + 4096;
+    std::unique_ptr<TypedSend> ts(new TypedSend);
+    ts->esize = build ? 16 : 8;
+    ts->cap = cap;
+    {
+        DevBuf e((size_t)nranks * cap * ts->esize + 16);
+        std::swap(ts->ent.p, e.p);
+    }
+    DevBuf ctl(64 + (size_t)nranks * 8);
+    unsigned int* flag = ctl.as<unsigned int>();
+    unsigned long long* kr = (unsigned long long*)(ctl.as<uint8_t>() + 16);
+    unsigned long long* rc = (unsigned long long*)(ctl.as<uint8_t>() + 64);
+    HIPCHECK(hipMemsetAsync(ctl.p, 0, 64 + (size_t)nranks * 8, c.stream));
+    HIPCHECK(hipMemsetAsync(kr, 0xff, 8, c.stream));
+    HIPCHECK(cq_jx_route(t->g, t->data_begin, t->n, ws, (uint8_t)t->cfg.delimiter, (uint8_t)t->cfg.quote, kcol, pcol,
+                         build ? 1 : 0, rp, wbase, (uint32_t)nranks, qbase, gbase, ts->ent.p, cap, rc, flag, kr, c.ncu,
+                         c.stream));
+    std::vector<uint8_t> h(64 + (size_t)nranks * 8);
+    HIPCHECK(hipMemcpyAsync(h.data(), ctl.p, h.size(), hipMemcpyDeviceToHost, c.stream));
+    HIPCHECK(hipStreamSynchronize(c.stream));
+    memcpy(&ts->flags, h.data(), 4);
+    memcpy(ts->krange, h.data() + 16, 16);
+    ts->counts.assign(nranks, 0);
+    memcpy(ts->counts.data(), h.data() + 64, (size_t)nranks * 8);
+    for (uint64_t x : ts->counts)
+        if (x > cap) ts->flags |= 256u;
+    t->tsend = std::move(ts);
+}
+
+// the receiving rank: STAR over the entries -> this rank's groups in `part`; returns
+// the flags (0: done; 16 / 32 / 64: the entries do not fit the STAR form)
+uint32_t typed_receive(DevCtx& c, const TypedJoin& tj, const void* ub, uint64_t nu, const void* ob, uint64_t no,
+                       uint64_t qoff, uint64_t range, JoinPartial& part) {
+    const uint32_t G = cq_jx_star_groups();
+    const bool grouped = tj.gcol >= 0;
+    if (range >= (1ull << 31) || qoff >= (1ull << 32)) return 16u;
+    const size_t b16 = (range * 2 + 15) & ~(size_t)15;
+    DevBuf d16(b16 + 16), l32(range * 4 + 16);
+    const size_t o_gsum = (size_t)G * 8, o_first = o_gsum + (size_t)G * 24, o_ctl = o_first + (size_t)G * 4;
+    DevBuf small(o_ctl + 64);
+    unsigned long long* ttab = small.as<unsigned long long>();
+    unsigned long long* gsum = (unsigned long long*)(small.as<uint8_t>() + o_gsum);
+    uint32_t* gfirst = (uint32_t*)(small.as<uint8_t>() + o_first);
+    unsigned int* flag = (unsigned int*)(small.as<uint8_t>() + o_ctl);
+    unsigned long long* cnts = (unsigned long long*)(small.as<uint8_t>() + o_ctl + 8);   // placed, pairs, occupied
+    uint32_t* notmono = (uint32_t*)(small.as<uint8_t>() + o_ctl + 32);
+    HIPCHECK(cq_jx_star_init(d16.p, b16, small.p, o_ctl + 64, (uint32_t)o_first, (uint32_t)o_ctl,
+                             (uint32_t)o_ctl + 48, nullptr, 0, c.ncu * 4, c.stream));
+    HIPCHECK(hipMemsetAsync(notmono, 1, 4, c.stream));     // the matched-flag form of the first pairs
+    HIPCHECK(hipEventRecord(c.ev0, c.stream));
+    // (ungrouped: no tag lookup, every build entry in group 0)
+    HIPCHECK(cq_jx_ent_build(ub, nu, (uint32_t)qoff, range, d16.as<uint16_t>(), l32.as<uint32_t>(), ttab, cnts, flag,
+                             c.ncu * 4, c.stream, grouped ? 0 : 1));
+    HIPCHECK(cq_jx_ent_probe(ob, no, (uint32_t)qoff, range, d16.as<uint16_t>(), gsum, cnts + 1, c.ncu * 4, c.stream));
+    HIPCHECK(cq_jx_star_first(d16.as<uint16_t>(), l32.as<uint32_t>(), range, notmono, gfirst, cnts + 2, c.ncu * 4,
+                              c.stream));
+    HIPCHECK(hipEventRecord(c.ev1, c.stream));
+    std::vector<uint8_t> h(o_ctl + 64);
+    uint8_t* hp = (uint8_t*)pinned(c, h.size());
+    HIPCHECK(hipMemcpyAsync(hp, small.p, h.size(), hipMemcpyDeviceToHost, c.stream));
+    HIPCHECK(hipStreamSynchronize(c.stream));
+    memcpy(h.data(), hp, h.size());
+    float ms = 0;
+    HIPCHECK(hipEventElapsedTime(&ms, c.ev0, c.ev1));
+    g_stats.scan_ms = ms;
+    uint32_t fl = 0;
+    memcpy(&fl, h.data() + o_ctl, 4);
+    unsigned long long cn[3];
+    memcpy(cn, h.data() + o_ctl + 8, 24);
+    if (cn[0] != cn[2]) fl |= 64u;                       // a repeated build key
+    if (fl) return fl;
+    g_stats.records = nu + no;
+    g_stats.passed = cn[1];
+    g_stats.scan_kernel = 5;                             // the typed STAR join
+    const unsigned long long* ht = (const unsigned long long*)h.data();
+    const unsigned long long* hs = (const unsigned long long*)(h.data() + o_gsum);
+    const uint32_t* hf = (const uint32_t*)(h.data() + o_first);
+    const int nacc = tj.C.P.nacc;
+    const uint32_t nrep = (uint32_t)tj.C.rep_cols.size();
+    std::vector<HGroup> groups;
+    auto fill = [&](HGroup& x, uint32_t s) {
+        x.cnt = hs[3 * s];
+        x.first = hf[s] == ~0u ? NOPOS : ((unsigned long long)hf[s] << 32);
+        for (int a = 0; a < nacc; a++) {
+            x.sum[a] = hs[3 * s + 2] ? (double)(long long)hs[3 * s + 1] / 1000.0 : 0.0;
+            x.num[a] = hs[3 * s + 2];
+        }
+    };
+    for (uint32_t s = 0; s < G; s++) {
+        if (!hs[3 * s]) continue;
+        HGroup x;
+        fill(x, s);
+        if (grouped) {
+            // the tag's bytes (fast_kernel's tag: zero padded, (1 << 32) for the empty field)
+            const unsigned long long tag = ht[s];
+            uint8_t b[8];
+            uint32_t len = 0;
+            if (tag != (1ull << 32)) {
+                for (uint32_t j = 0; j < 8; j++) {
+                    b[j] = (uint8_t)(tag >> (8 * j));
+                    if (b[j]) len = j + 1;
+                }
+            }
+            const Cell cell = cq_host_parse_cell(b, len);
+            const GKey k = cq_host_group_key(cell);
+            x.kcls = k.cls;
+            x.klen = k.len;
+            x.kw0 = k.w0;
+            x.kw1 = k.w1;
+            if (k.cls == GK_STR) x.kbytes.assign((const char*)b, std::min<uint32_t>(k.len, 8));
+            HCell rep;
+            rep.kind = cell.kind;
+            rep.bits = cell.kind == K_STR ? 0 : cell.bits;
+            if (cell.kind == K_STR) rep.s.assign((const char*)(uintptr_t)cell.bits, cell.len);
+            for (uint32_t r = 0; r < nrep; r++) x.reps.push_back(rep);
+        } else {
+            x.kcls = GK_ALL;
+        }
+        // raw tags of one canonical key (e.g. "1.0" and "1.00") are one group: counts and
+        // sums add, the first pair is the smaller, its row gives the representative cells
+        HGroup* same = nullptr;
+        for (HGroup& y : groups)
+            if (y.kcls == x.kcls && y.klen == x.klen && y.kw0 == x.kw0 && y.kw1 == x.kw1) { same = &y; break; }
+        if (!same) { groups.push_back(std::move(x)); continue; }
+        same->cnt += x.cnt;
+        for (int a = 0; a < nacc; a++) { same->sum[a] += x.sum[a]; same->num[a] += x.num[a]; }
+        if (x.first < same->first) { same->first = x.first; same->reps = x.reps; }
+    }
+    part.groups = std::move(groups);
+    part.names = tj.names;
+    part.nacc = nacc;
+    part.nrep = nrep;
+    part.nvla = 0;
+    for (int a = 0; a < MAX_ACC; a++) part.acc_classes[a] = 0;   // SUM only
+    part.lmask |= nu ? 2u : 0u;                                    // (canonical INTEGER keys: numbers)
+    part.rmask |= no ? 2u : 0u;
+    g_stats.groups = part.groups.size();
+    return 0;
+}
+
+}  // namespace
+
+extern "C" {
+
+int cqgpu_typed_plan(cq_node* q, cqgpu_table* const* tables, int ntables) {
+    g_inel.clear();
+    g_err.clear();
+    if (ntables != 2 || !tables || !tables[0] || !tables[1]) return 0;
+    TypedJoin tj;
+    std::string why;
+    const bool ok = typed_join_plan(q, tables[0], tables[1], tj, why);
+    if (!ok) g_inel = why;
+    return ok ? 1 : 0;
+}
+
+uint64_t cqgpu_typed_sample_kmin(cq_node* q, cqgpu_table* const* tables, int ntables) {
+    TypedJoin tj;
+    std::string why;
+    if (ntables != 2 || !tables || !tables[0] || !tables[1] || !typed_join_plan(q, tables[0], tables[1], tj, why))
+        return ~0ull;
+    return tables[0]->n > tables[0]->data_begin ? typed_sample_kmin(tables[0], tj.kl) : ~0ull;
+}
+
+int64_t cqgpu_typed_count(cq_node* q, cqgpu_table* const* tables, int ntables) {
+    g_err.clear();
+    try {
+        TypedJoin tj;
+        std::string why;
+        if (ntables != 2 || !typed_join_plan(q, tables[0], tables[1], tj, why)) throw Ineligible{"typed exchange: " + why};
+        DevCtx& c = ctx();
+        return (int64_t)typed_count(c, tables[0], tj.kl, tj.gcol);
+    } catch (Ineligible& e) {
+        g_inel = e.why;
+        set_err("cq_amd: %s", e.why.c_str());
+    } catch (HipError& e) {
+        set_err("cq_amd: %s", e.msg.c_str());
+    } catch (std::exception& e) {
+        set_err("cq_amd: %s", e.what());
+    }
+    return -1;
+}
+
+int cqgpu_typed_send(cq_node* q, cqgpu_table* const* tables, int ntables, int side, int nranks, uint64_t qbase,
+                     uint64_t gid_base, uint64_t cap, uint64_t* counts, uint64_t* krange, uint32_t* flags) {
+    g_err.clear();
+    try {
+        TypedJoin tj;
+        std::string why;
+        if (ntables != 2 || (side != 0 && side != 1) || nranks < 1 || nranks > 64 ||
+            !typed_join_plan(q, tables[0], tables[1], tj, why))
+            throw Ineligible{"typed exchange: " + why};
+        DevCtx& c = ctx();
+        cqgpu_table* t = tables[side];
+        typed_send(c, t, side == 0, side == 0 ? tj.kl : tj.kr, side == 0 ? tj.gcol : tj.vcol, nranks, qbase, gid_base,
+                   cap);
+        for (int d = 0; d < nranks; d++) counts[d] = t->tsend->counts[d];
+        if (krange) { krange[0] = t->tsend->krange[0]; krange[1] = t->tsend->krange[1]; }
+        if (flags) *flags = t->tsend->flags;
+        return 0;
+    } catch (Ineligible& e) {
+        g_inel = e.why;
+        set_err("cq_amd: %s", e.why.c_str());
+    } catch (HipError& e) {
+        set_err("cq_amd: %s", e.msg.c_str());
+    } catch (std::exception& e) {
+        set_err("cq_amd: %s", e.what());
+    }
+    return -1;
+}
+
+void cqgpu_typed_reset(cqgpu_table* t) {
+    if (!t) return;
+    t->tsend.reset();
+    t->typed_nrec = ~0ull;
+    t->typed_ws = 0;
+    t->typed_wbase.reset();
+}
+
+const void* cqgpu_typed_region(const cqgpu_table* t, int dest, uint64_t* entries, uint64_t* entry_bytes) {
+    if (!t || !t->tsend || dest < 0 || (size_t)dest >= t->tsend->counts.size()) return nullptr;
+    const TypedSend& ts = *t->tsend;
+    if (entries) *entries = std::min(ts.counts[dest], ts.cap);
+    if (entry_bytes) *entry_bytes = ts.esize;
+    return ts.ent.as<uint8_t>() + (size_t)dest * ts.cap * ts.esize;
+}
+
+int64_t cqgpu_typed_gather(cqgpu_table* const* senders, int nsenders, int dest, void* dev_out, uint64_t cap_entries) {
+    g_err.clear();
+    try {
+        DevCtx& c = ctx();
+        uint64_t at = 0, esize = 0;
+        for (int r = 0; r < nsenders; r++) {
+            uint64_t n = 0, eb = 0;
+            const void* p = cqgpu_typed_region(senders[r], dest, &n, &eb);
+            if (!p) throw HipError{"typed_gather: a sender has no entries"};
+            if (esize && eb != esize) throw HipError{"typed_gather: entries of different sides"};
+            esize = eb;
+            if (at + n > cap_entries) throw HipError{"typed_gather: the output is too small"};
+            if (n) HIPCHECK(hipMemcpyAsync((uint8_t*)dev_out + at * eb, p, n * eb, hipMemcpyDeviceToDevice, c.stream));
+            at += n;
+        }
+        HIPCHECK(hipStreamSynchronize(c.stream));
+        return (int64_t)at;
+    } catch (HipError& e) {
+        set_err("cq_amd: %s", e.msg.c_str());
+    } catch (std::exception& e) {
+        set_err("cq_amd: %s", e.what());
+    }
+    return -1;
+}
+
+size_t cqgpu_typed_partial(cq_node* q, cqgpu_table* const* tables, int ntables, const void* dev_build, uint64_t nbuild,
+                           const void* dev_probe, uint64_t nprobe, uint64_t qoff, uint64_t range, void** blob_out) {
+    if (blob_out) *blob_out = nullptr;
+    g_inel.clear();
+    g_err.clear();
+    memset(&g_stats, 0, sizeof g_stats);
+    try {
+        TypedJoin tj;
+        std::string why;
+        if (ntables != 2 || !typed_join_plan(q, tables[0], tables[1], tj, why)) throw Ineligible{"typed exchange: " + why};
+        DevCtx& c = ctx();
+        bump_reset(c);
+        JoinPartial jp;
+        const uint32_t fl = typed_receive(c, tj, dev_build, nbuild, dev_probe, nprobe, qoff, range, jp);
+        if (fl) {
+            char b[96];
+            snprintf(b, sizeof b, "typed exchange: the entries do not fit the STAR join (flags %#x)", fl);
+            throw Ineligible{b};
+        }
+        Blob b;
+        join_blob(jp, b);
+        void* out = malloc(std::max<size_t>(b.d.size(), 1));
+        if (!out) throw HipError{"out of host memory"};
+        memcpy(out, b.d.data(), b.d.size());
+        *blob_out = out;
+        g_stats.path = 1;
+        return b.d.size();
+    } catch (Ineligible& e) {
+        g_inel = e.why;
+        set_err("cq_amd: %s", e.why.c_str());
+    } catch (HipError& e) {
+        set_err("cq_amd: %s", e.msg.c_str());
+    } catch (std::exception& e) {
+        set_err("cq_amd: %s", e.what());
+    }
+    return 0;
+}
+
+}  // extern "C"
+
 // ==================================================================== N > 1 over RCCL
 // The whole range-partitioned step inside the library (cqgpu.h cqgpu_dist_query):
 // one communicator per device, every collective on the device context's stream,
@@ -7417,12 +7902,20 @@ int dist_dense(DevCtx& c, DistComm& m, cq_node* q, cqgpu_table* t, cq_table** re
 }
 
 // ---- blobs: every rank's cqgpu_query_partial to rank 0, merged there
+// (blob: this rank's partial, malloc'd -- freed here; n == 0: this rank failed with err)
+void dist_blob_send(DevCtx& c, DistComm& m, cq_node* q, void* blob, size_t n, const std::string& err_in,
+                    cq_table** res);
 void dist_blob(DevCtx& c, DistComm& m, cq_node* q, cqgpu_table* const* tabs, int ntabs, cq_table** res,
                bool bad_in = false, const std::string& err_in = std::string()) {
     void* blob = nullptr;
     const size_t n = bad_in ? 0 : cqgpu_query_partial(q, tabs, ntabs, &blob);
+    const std::string err = bad_in ? err_in : (n == 0 ? (g_err.empty() ? g_inel : g_err) : std::string());
+    dist_blob_send(c, m, q, blob, n, err, res);
+}
+void dist_blob_send(DevCtx& c, DistComm& m, cq_node* q, void* blob, size_t n, const std::string& err_in,
+                    cq_table** res) {
     const bool bad = n == 0;
-    std::string err = bad_in ? err_in : (bad ? (g_err.empty() ? g_inel : g_err) : std::string());
+    const std::string err = err_in;
     struct Free { void* b; ~Free() { free(b); } } fr{blob};
     const int N = m.world;
     DevBuf pair((size_t)N * 16 + 16), dblob(std::max<size_t>(n, 16));
@@ -7477,7 +7970,177 @@ void dist_blob(DevCtx& c, DistComm& m, cq_node* q, cqgpu_table* const* tabs, int
 // communicator, the received records rebuilt as this rank's side (file order, global
 // ids, key stride N, whole-input record total), then the join partials as blobs to
 // rank 0 (dist_blob).  No host round trip carries data; the host reads only counts.
+// ---- the typed exchange inside cqgpu_dist_join (see "typed join exchange" above):
+// every rank decides the same at every step -- from the plan, then from flags and
+// counts every rank has gathered -- so the ranks take it, retry it or leave it for the
+// CSV-record exchange together.  Returns true when *res / the status is final.
+bool g_join_typed = false;             // the last cqgpu_dist_join took the typed exchange
+bool dist_join_typed(DevCtx& c, DistComm& m, cq_node* q, cqgpu_table* const* tables, int ntables, cq_table** res) {
+    const int N = m.world;
+    if (ntables != 2 || N > 16) return false;
+    TypedJoin tj;
+    std::string why;
+    if (!typed_join_plan(q, tables[0], tables[1], tj, why)) return false;   // (the plan: the same everywhere)
+    std::string err;
+    bool bad = false;
+    uint64_t nrec = 0;
+    try {
+        nrec = typed_count(c, tables[0], tj.kl, tj.gcol);
+    } catch (HipError& e) { bad = true; err = e.msg; } catch (Ineligible& e) { bad = true; err = e.why; }
+    (void)hipGetLastError();
+    // every rank's record count (the global ids' bases) and failure flag
+    // every rank's record count (the global ids' bases), sampled key minimum, failure flag
+    std::vector<uint64_t> all(3 * (size_t)N, 0);
+    {
+        DevBuf dc(24 * ((size_t)N + 1));
+        uint64_t mine[3] = {nrec, tables[0]->n > tables[0]->data_begin ? typed_sample_kmin(tables[0], tj.kl) : ~0ull,
+                            bad ? 1ull : 0ull};
+        HIPCHECK(hipMemcpyAsync(dc.as<uint8_t>() + 24 * N, mine, 24, hipMemcpyHostToDevice, c.stream));
+        m.be->all_gather(dc.as<uint8_t>() + 24 * N, dc.p, 3, CD_U64, c.stream);
+        HIPCHECK(hipMemcpyAsync(all.data(), dc.p, 24 * (size_t)N, hipMemcpyDeviceToHost, c.stream));
+        HIPCHECK(hipStreamSynchronize(c.stream));
+    }
+    uint64_t gbase = 0, total = 0, smin = ~0ull;
+    for (int r = 0; r < N; r++) {
+        if (all[3 * r + 2]) throw PeerFail{bad ? err : std::string("a peer rank failed")};
+        if (r < m.rank) gbase += all[3 * r];
+        total += all[3 * r];
+        smin = std::min(smin, all[3 * r + 1]);
+    }
+    if (total >= (1ull << 32)) return false;
+    uint64_t qbase = smin == ~0ull ? 0 : smin / (uint64_t)N, cap_u = 0, cap_o = 0;
+    // per rank: counts_u[N], counts_o[N], flags, kmin, kmax, bad
+    const size_t W = 2 * (size_t)N + 4;
+    std::vector<uint64_t> g(W * N, 0);
+    for (int attempt = 0;; attempt++) {
+        std::vector<uint64_t> mine(W, 0);
+        try {
+            if (getenv("CQGPU_TEST_TYPED_FAIL"))                 // test knob: this rank's send fails
+                throw HipError{"dist_join: injected typed-exchange failure (CQGPU_TEST_TYPED_FAIL)"};
+            typed_send(c, tables[0], true, tj.kl, tj.gcol, N, qbase, gbase, cap_u);
+            typed_send(c, tables[1], false, tj.kr, tj.vcol, N, qbase, 0, cap_o);
+            const TypedSend &su = *tables[0]->tsend, &so = *tables[1]->tsend;
+            for (int d = 0; d < N; d++) { mine[d] = su.counts[d]; mine[N + d] = so.counts[d]; }
+            mine[2 * N] = su.flags | so.flags;
+            mine[2 * N + 1] = su.krange[0];
+            mine[2 * N + 2] = su.krange[1];
+        } catch (HipError& e) { bad = true; err = e.msg; } catch (Ineligible& e) { bad = true; err = e.why; }
+        (void)hipGetLastError();
+        mine[2 * N + 3] = bad ? 1 : 0;
+        {
+            DevBuf dc(W * 8 * ((size_t)N + 1));
+            HIPCHECK(hipMemcpyAsync(dc.as<uint8_t>() + W * 8 * N, mine.data(), W * 8, hipMemcpyHostToDevice, c.stream));
+            m.be->all_gather(dc.as<uint8_t>() + W * 8 * N, dc.p, W, CD_U64, c.stream);
+            HIPCHECK(hipMemcpyAsync(g.data(), dc.p, W * 8 * N, hipMemcpyDeviceToHost, c.stream));
+            HIPCHECK(hipStreamSynchronize(c.stream));
+        }
+        uint64_t flags = 0, kmin = ~0ull, kmax = 0, need_u = 0, need_o = 0;
+        for (int r = 0; r < N; r++) {
+            const uint64_t* x = g.data() + W * r;
+            if (x[2 * N + 3]) {
+                tables[0]->tsend.reset();
+                tables[1]->tsend.reset();
+                throw PeerFail{bad ? err : std::string("a peer rank failed")};
+            }
+            flags |= x[2 * N];
+            kmin = std::min(kmin, x[2 * N + 1]);
+            kmax = std::max(kmax, x[2 * N + 2]);
+            for (int d = 0; d < N; d++) { need_u = std::max(need_u, x[d]); need_o = std::max(need_o, x[N + d]); }
+        }
+        if ((flags & (1u | 8u | 512u)) || attempt == 2) {          // not typable: every rank to the CSV exchange
+            tables[0]->tsend.reset();
+            tables[1]->tsend.reset();
+            return false;
+        }
+        if (flags & (16u | 256u)) {
+            if (flags & 16u) qbase = kmin / (uint64_t)N;
+            if (flags & 256u) { cap_u = need_u; cap_o = need_o; }
+            continue;
+        }
+        if (kmin > kmax) kmin = kmax = qbase * (uint64_t)N;            // no build keys anywhere
+        break;
+    }
+    uint64_t kmin = ~0ull, kmax = 0;
+    std::vector<uint64_t> recv_u(N, 0), recv_o(N, 0);
+    for (int r = 0; r < N; r++) {
+        const uint64_t* x = g.data() + W * r;
+        kmin = std::min(kmin, x[2 * N + 1]);
+        kmax = std::max(kmax, x[2 * N + 2]);
+        for (int d = 0; d < N; d++) { recv_u[d] += x[d]; recv_o[d] += x[N + d]; }
+    }
+    if (kmin > kmax) kmin = kmax = qbase * (uint64_t)N;
+    const uint64_t qoff = kmin / (uint64_t)N - qbase, range = kmax / (uint64_t)N - kmin / (uint64_t)N + 1;
+    if (range > 4 * *std::min_element(recv_u.begin(), recv_u.end()) + 1024 || range >= (1ull << 31)) {
+        tables[0]->tsend.reset();
+        tables[1]->tsend.reset();
+        return false;                                             // not a dense key range on every rank
+    }
+    // the entries: region d of every rank to rank d, in one grouped send / recv per side
+    DevBuf ru, ro;
+    try {
+        DevBuf a(std::max<uint64_t>(recv_u[m.rank], 1) * 16), b(std::max<uint64_t>(recv_o[m.rank], 1) * 8);
+        std::swap(ru.p, a.p);
+        std::swap(ro.p, b.p);
+    } catch (HipError& e) { bad = true; err = e.msg; }
+    (void)hipGetLastError();
+    if (agree_any(c, m, bad)) {
+        tables[0]->tsend.reset();
+        tables[1]->tsend.reset();
+        throw PeerFail{bad ? err : std::string("a peer rank failed")};
+    }
+    for (int side = 0; side < 2; side++) {
+        const TypedSend& ts = *tables[side]->tsend;
+        uint8_t* rb = side == 0 ? ru.as<uint8_t>() : ro.as<uint8_t>();
+        m.be->group_start();
+        uint64_t at = 0;
+        for (int d = 0; d < N; d++) {
+            const uint64_t ns = ts.counts[d];
+            if (ns) m.be->send(ts.ent.as<uint8_t>() + (size_t)d * ts.cap * ts.esize, ns * ts.esize, CD_U8, d, c.stream);
+            const uint64_t nr = g[W * d + (size_t)side * N + m.rank];          // from source d
+            if (nr) m.be->recv(rb + at * ts.esize, nr * ts.esize, CD_U8, d, c.stream);
+            at += nr;
+        }
+        m.be->group_end(c.stream);
+    }
+    tables[0]->tsend.reset();
+    tables[1]->tsend.reset();
+    // this rank's STAR join over its entries; a rank whose entries do not fit (a repeated
+    // build key, more than JX_G groups) sends every rank back to the CSV exchange
+    JoinPartial jp;
+    uint32_t fl = 0;
+    try {
+        fl = typed_receive(c, tj, ru.p, recv_u[m.rank], ro.p, recv_o[m.rank], qoff, range, jp);
+    } catch (HipError& e) { bad = true; err = e.msg; }
+    (void)hipGetLastError();
+    {
+        DistBufs& b = dist_bufs();
+        b.hword[0] = bad ? 1u : 0u;
+        b.hword[1] = fl ? 1u : 0u;
+        uint32_t* dw = b.word.as<uint32_t>() + 8;
+        HIPCHECK(hipMemcpyAsync(dw, b.hword, 8, hipMemcpyHostToDevice, c.stream));
+        m.be->all_reduce(dw, 2, CD_U32, CR_MAX, c.stream);
+        HIPCHECK(hipMemcpyAsync(b.hword + 4, dw, 8, hipMemcpyDeviceToHost, c.stream));
+        HIPCHECK(hipStreamSynchronize(c.stream));
+        if (b.hword[4]) throw PeerFail{bad ? err : std::string("a peer rank failed")};
+        if (b.hword[5]) return false;
+    }
+    void* blob = nullptr;
+    size_t n = 0;
+    try {
+        Blob bb;
+        join_blob(jp, bb);
+        blob = malloc(std::max<size_t>(bb.d.size(), 1));
+        if (!blob) throw HipError{"out of host memory"};
+        memcpy(blob, bb.d.data(), bb.d.size());
+        n = bb.d.size();
+    } catch (HipError& e) { err = e.msg; n = 0; }
+    g_join_typed = true;
+    dist_blob_send(c, m, q, blob, n, err, res);
+    return true;
+}
+
 void dist_join(DevCtx& c, DistComm& m, cq_node* q, cqgpu_table* const* tables, int ntables, cq_table** res) {
+    if (!getenv("CQGPU_NO_TYPED_JOIN") && dist_join_typed(c, m, q, tables, ntables, res)) return;
     const int N = m.world;
     std::string err;
     bool bad = false;
@@ -7826,8 +8489,10 @@ cq_table* cqgpu_dist_join(cq_node* q, cqgpu_table* const* tables, int ntables, i
         DevCtx& c = ctx();
         DistComm& m = dist_comm();
         const double t0 = now_ms();
+        g_join_typed = false;
         dist_join(c, m, q, tables, ntables, &res);
         g_stats.total_ms = now_ms() - t0;
+        if (g_join_typed) g_stats.scan_kernel = 5;      // (the typed exchange's STAR join)
         if (m.rank == 0) g_stats.path = 1;
         return res;
     } catch (PeerFail& e) {

@@ -112,6 +112,9 @@ struct FastPlan {
     uint64_t lx_in[4][8];       // LX_*IN: V values (numbers) or words (strings)
 };
 enum : uint32_t { LX_NUM = 0, LX_STR = 1, LX_NIN = 2, LX_SIN = 3 };
+// a leaf's parameters in LDS (WX builds): meta (kind | col << 2 | neg << 3 | null << 4 |
+// tt << 5 | nin << 8), a, w, 0, lit (2 words), in[8] (16 words)
+constexpr uint32_t LX_WORDS = 22;
 
 // HBM tables: canonical keys (TAB_GT), raw keys (TAB_RT)
 enum : int { TAB_GT = 0, TAB_RT = 1 };
@@ -534,6 +537,32 @@ __global__ __launch_bounds__(LT) void fast_kernel(const uint8_t* __restrict__ g,
         T = (unsigned long long*)carve(q, TSLOTS * 8);
     }
     WaveLds* waves = (WaveLds*)carve(q, sizeof(WaveLds) * NWV);
+    // WX builds: the leaves' parameters in LDS, read once per record pass -- as kernel
+    // arguments the compiler keeps them in scalar registers across the loop and spills
+    // (v_writelane / v_readlane) the loop's own state
+    uint32_t* lxl = nullptr;
+    if constexpr (WX != 0) {
+        lxl = (uint32_t*)carve(q, 4 * LX_WORDS * 4);
+        if (threadIdx.x == 0) {
+#pragma unroll
+            for (int l = 0; l < 4; l++) {
+                uint32_t* L = lxl + l * LX_WORDS;
+                L[0] = fp.lx_kind[l] | (fp.lx_col[l] << 2) | (fp.lx_neg[l] << 3) | (fp.lx_null[l] << 4) |
+                       (fp.lx_tt[l] << 5) | (fp.lx_nin[l] << 8);
+                L[1] = fp.lx_a[l];
+                L[2] = fp.lx_w[l];
+                L[3] = 0;
+                L[4] = (uint32_t)fp.lx_lit[l];
+                L[5] = (uint32_t)(fp.lx_lit[l] >> 32);
+#pragma unroll
+                for (int t = 0; t < 8; t++) {
+                    L[6 + 2 * t] = (uint32_t)fp.lx_in[l][t];
+                    L[7 + 2 * t] = (uint32_t)(fp.lx_in[l][t] >> 32);
+                }
+            }
+        }
+        __syncthreads();
+    }
     const int tid = threadIdx.x, lane = tid & 63;
     const int wv = __builtin_amdgcn_readfirstlane(tid >> 6);
     WaveLds& W = waves[wv];
@@ -901,27 +930,30 @@ __global__ __launch_bounds__(LT) void fast_kernel(const uint8_t* __restrict__ g,
 #pragma unroll
                     for (int l = 0; l < 4; l++) {
                         if ((uint32_t)l < nleaf) {
-                            const uint32_t c = WX == 2 ? fp.lx_col[l] : 0u;
+                            const uint32_t* L = lxl + l * LX_WORDS;
+                            const uint32_t meta = __builtin_amdgcn_readfirstlane(L[0]);
+                            const uint32_t c = WX == 2 ? (meta >> 2) & 1u : 0u;
                             const uint32_t V = c ? cv[WX - 1] : cv[0];
                             const uint64_t X = c ? cx[WX - 1] : cx[0];
                             const bool nul = c ? cnull[WX - 1] : cnull[0];
-                            const uint32_t kind = fp.lx_kind[l];
+                            const uint32_t kind = meta & 3u;
+                            const bool neg = (meta >> 3) & 1u;
                             bool b;
                             if (kind == LX_NUM) {
-                                b = (V - fp.lx_a[l] <= fp.lx_w[l]) != (fp.lx_neg[l] != 0);
+                                b = (V - L[1] <= L[2]) != neg;
                             } else if (kind == LX_STR) {
-                                const uint64_t lit = fp.lx_lit[l];
-                                b = tt_result(fp.lx_tt[l], X < lit ? -1 : (X > lit ? 1 : 0));
+                                const uint64_t lit = (uint64_t)L[4] | ((uint64_t)L[5] << 32);
+                                b = tt_result((meta >> 5) & 7u, X < lit ? -1 : (X > lit ? 1 : 0));
                             } else {
                                 bool hit = false;
-                                const uint32_t nin = fp.lx_nin[l];
-#pragma unroll
-                                for (uint32_t t = 0; t < 8; t++)
-                                    if (t < nin)
-                                        hit |= kind == LX_NIN ? V == (uint32_t)fp.lx_in[l][t] : X == fp.lx_in[l][t];
-                                b = hit != (fp.lx_neg[l] != 0);
+                                const uint32_t nin = (meta >> 8) & 15u;
+                                for (uint32_t t = 0; t < nin; t++) {
+                                    const uint64_t v = (uint64_t)L[6 + 2 * t] | ((uint64_t)L[7 + 2 * t] << 32);
+                                    hit |= kind == LX_NIN ? V == (uint32_t)v : X == v;
+                                }
+                                b = hit != neg;
                             }
-                            b = nul ? fp.lx_null[l] != 0 : b;
+                            b = nul ? ((meta >> 4) & 1u) != 0 : b;
                             idx |= (b ? 1u : 0u) << l;
                         }
                     }
@@ -1397,6 +1429,22 @@ struct JxOut {
     unsigned long long* pent;
     uint32_t* pcnt;
     uint32_t np, pcap, psh;
+    // ROUTE (the typed exchange of the multi-GPU join): every
+    // record with a non-NULL key goes to rank key mod rn as one fixed-size entry in that
+    // destination's region of rent (rcap entries each, filled in no particular order):
+    //   BUILD  uint4 {q32, gid, tag lo, tag hi}: q32 = key / rn - qbase, gid = gbase +
+    //          the record's index in this table (file order), tag = the GROUP BY bytes
+    //   PROBE  uint2 {q32, pay}: pay = the SUM argument in 10^-3 units (JX_PNULL: NULL)
+    // Flags: 8 a NULL build key, 16 a build q32 outside [0, 2^32 - 1) (the host retries
+    // with the keys' own minimum), 256 a region full (retried with exact capacities),
+    // 512 a payload outside 31 bits.  A probe key outside the window matches no build
+    // key and is not sent.
+    void* rent;
+    unsigned long long* rcount;   // per destination: entries reserved
+    uint64_t rcap;
+    uint64_t rmagic;              // ceil(2^64 / rn) (rn > 1): key / rn = mulhi(key, rmagic) for keys < 2^58
+    uint64_t qbase, gbase;
+    uint32_t rn;
 };
 // a key's STAR slot (k - kmin) / S when k = kmin (mod S) and the slot is below 2^32,
 // else ~0 (never < range: the host keeps range * S < 2^32).  Exact division by the
@@ -1541,8 +1589,10 @@ __device__ __forceinline__ bool jx_key(uint32_t d0, uint32_t d1, uint32_t d2, ui
 #endif
 }
 
-template <bool BUILD, bool COMMA, int NR, bool COUNT, bool STAR = false, int RP = 2, bool PART = false>
+template <bool BUILD, bool COMMA, int NR, bool COUNT, bool STAR = false, int RP = 2, bool PART = false,
+          bool ROUTE = false>
 __global__ __launch_bounds__(LT) void jx_extract_kernel(const uint8_t* __restrict__ g, const JxPlan jp, const JxOut jo) {
+    static_assert(!ROUTE || (!STAR && !COUNT), "ROUTE: the emit pass of the record form");
     extern __shared__ __align__(16) uint8_t smem[];
     WaveLds* waves = (WaveLds*)smem;
     // STAR probe: per group id COUNT / fixed-point SUM / SUM count of this block;
@@ -1669,7 +1719,7 @@ __global__ __launch_bounds__(LT) void jx_extract_kernel(const uint8_t* __restric
         // record j of this lane in this window lands at wbase[i] + (the lanes below's
         // records) + j: file order
         const uint32_t nmine = (uint32_t)__popcll(todo);
-        uint32_t at_next = STAR ? 0u : jo.wbase[i] + wave_incl_scan(nmine) - nmine;
+        uint32_t at_next = (STAR || (ROUTE && !BUILD)) ? 0u : jo.wbase[i] + wave_incl_scan(nmine) - nmine;
         bool issued = false;
         // STAR build: this lane's first and last key (its records come in file order),
         // as slots: keys map to slots monotonically, and a key outside the range flags
@@ -1873,6 +1923,71 @@ __global__ __launch_bounds__(LT) void jx_extract_kernel(const uint8_t* __restric
                         }
                     }
                 }
+            } else if constexpr (ROUTE) {
+                // destination and q32 of each record, then per destination one wave-wide
+                // reservation in its region (ballots; one atomic per destination present)
+                uint32_t dd[RP], q32[RP], gid[RP];
+                bool take[RP];
+                uint64_t pos[RP];
+#pragma unroll
+                for (int u = 0; u < RP; u++) {
+                    gid[u] = valid[u] ? (uint32_t)(jo.gbase + at_next) : 0u;
+                    at_next += valid[u] ? 1u : 0u;
+                    const unsigned long long k = key[u];
+                    take[u] = valid[u] && !fail[u] && k != JX_NULLKEY;
+                    if (BUILD && valid[u] && !fail[u] && k == JX_NULLKEY) sflag |= 8u;
+                    const unsigned long long q = jo.rn > 1u ? __umul64hi(k, jo.rmagic) : k;
+                    dd[u] = (uint32_t)(k - q * jo.rn);
+                    const unsigned long long qq = q - jo.qbase;
+                    q32[u] = (uint32_t)qq;
+                    if (BUILD && take[u]) {                       // (every build key: a retry's window)
+                        kmin = k < kmin ? k : kmin;
+                        kmax = k > kmax ? k : kmax;
+                    }
+                    if (take[u] && (q < jo.qbase || qq >= 0xFFFFFFFFull)) {
+                        take[u] = false;                          // (probe: matches no build key)
+                        if (BUILD) sflag |= 16u;
+                    }
+                    if (!BUILD && take[u] && pay[u] != JX_NOVAL &&
+                        ((long long)pay[u] < -2147483647ll || (long long)pay[u] > 2147483647ll)) {
+                        sflag |= 512u;
+                        take[u] = false;
+                    }
+                    pos[u] = ~0ull;
+                }
+                const uint32_t nd = __builtin_amdgcn_readfirstlane(jo.rn);
+                const uint64_t lt = lane ? (~0ull >> (64 - lane)) : 0ull;
+                for (uint32_t d = 0; d < nd; d++) {
+                    uint64_t m[RP];
+                    uint32_t tot = 0;
+#pragma unroll
+                    for (int u = 0; u < RP; u++) {
+                        m[u] = __ballot(take[u] && dd[u] == d);
+                        tot += (uint32_t)__popcll(m[u]);
+                    }
+                    if (tot == 0) continue;
+                    unsigned long long base = 0;
+                    if (lane == 0) base = atomicAdd(&jo.rcount[d], (unsigned long long)tot);
+                    base = __shfl(base, 0, 64);
+                    uint32_t pre = 0;
+#pragma unroll
+                    for (int u = 0; u < RP; u++) {
+                        if ((m[u] >> lane) & 1ull) pos[u] = base + pre + (uint32_t)__popcll(m[u] & lt);
+                        pre += (uint32_t)__popcll(m[u]);
+                    }
+                }
+#pragma unroll
+                for (int u = 0; u < RP; u++) {
+                    if (!take[u]) continue;
+                    if (pos[u] >= jo.rcap) { sflag |= 256u; continue; }
+                    const uint64_t at = (uint64_t)dd[u] * jo.rcap + pos[u];
+                    if (BUILD) {
+                        ((uint4*)jo.rent)[at] = make_uint4(q32[u], gid[u], (uint32_t)pay[u], (uint32_t)(pay[u] >> 32));
+                    } else {
+                        const uint32_t p32 = pay[u] == JX_NOVAL ? JX_PNULL : (uint32_t)pay[u];
+                        ((uint2*)jo.rent)[at] = make_uint2(q32[u], p32);
+                    }
+                }
             } else {
 #pragma unroll
                 for (int u = 0; u < RP; u++) {
@@ -1914,7 +2029,7 @@ __global__ __launch_bounds__(LT) void jx_extract_kernel(const uint8_t* __restric
     }
     if (COUNT) return;
     if (__any(bad) && lane == 0) atomicOr(jo.flag, 1u);
-    if constexpr (STAR) {
+    if constexpr (STAR || ROUTE) {
         for (int o = 32; o > 0; o >>= 1) {
             sflag |= (uint32_t)__shfl_down((int)sflag, o, 64);
             nstar += __shfl_down(nstar, o, 64);
@@ -2190,6 +2305,110 @@ __global__ __launch_bounds__(1024) void jx_star_flush_kernel(const unsigned long
     }
 }
 
+
+// ------------------------------------------------------------------ STAR over typed entries
+// The receiving rank of the typed exchange (jx_extract_kernel ROUTE): the same STAR
+// arrays as the CSV form -- d16 (group id + 1, bit 15 once a probe entry matched),
+// l32 (here the build record's GLOBAL id, so a group's first pair needs no offset
+// lookup), the GROUP BY tag table ttab, per group COUNT / fixed-point SUM / SUM count
+// in gsum -- filled from the fixed-size entries instead of re-parsing CSV.  Slot =
+// q32 - qoff (one residue class of a dense key range: key mod N routing).
+// Flags: 16 a q32 outside [qoff, qoff + range), 32 more tags than JX_G.
+__global__ __launch_bounds__(1024) void jx_ent_build_kernel(const uint4* __restrict__ ent, uint64_t n, uint32_t qoff,
+                                                            uint64_t range, uint16_t* __restrict__ d16,
+                                                            uint32_t* __restrict__ l32,
+                                                            unsigned long long* __restrict__ ttab,
+                                                            unsigned long long* __restrict__ nplaced,
+                                                            unsigned int* __restrict__ flag, uint32_t ungrouped) {
+    __shared__ unsigned long long lt[JX_G];       // the block's mirror of the tag table
+    for (uint32_t k = threadIdx.x; k < JX_G; k += blockDim.x) lt[k] = ttab[k];
+    __syncthreads();
+    uint32_t fl = 0;
+    unsigned long long placed = 0;
+    const uint64_t nt = (uint64_t)gridDim.x * blockDim.x;
+    for (uint64_t i = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x; i < n; i += 2 * nt) {
+        uint4 e[2];
+        bool ok[2];
+#pragma unroll
+        for (int u = 0; u < 2; u++) {                // two entries in flight per thread
+            ok[u] = i + u * nt < n;
+            e[u] = ok[u] ? ent[i + u * nt] : make_uint4(0u, 0u, 0u, 0u);
+        }
+#pragma unroll
+        for (int u = 0; u < 2; u++) {
+            if (!ok[u]) continue;
+            const uint64_t slot = (uint64_t)(uint32_t)(e[u].x - qoff);
+            if (e[u].x < qoff || slot >= range) { fl |= 16u; continue; }
+            bool full = false;
+            const unsigned long long tag = (unsigned long long)e[u].z | ((unsigned long long)e[u].w << 32);
+            const uint32_t gid = ungrouped ? 0u : jx_tag_gid_lds(lt, ttab, tag, full);
+            if (full) { fl |= 32u; continue; }
+            d16[slot] = (uint16_t)(gid + 1u);
+            l32[slot] = e[u].y;
+            placed++;
+        }
+    }
+    for (int o = 32; o > 0; o >>= 1) {
+        fl |= (uint32_t)__shfl_down((int)fl, o, 64);
+        placed += __shfl_down(placed, o, 64);
+    }
+    if ((threadIdx.x & 63) == 0) {
+        if (fl) atomicOr(flag, fl);
+        if (placed) atomicAdd(nplaced, placed);
+    }
+}
+
+// probe: every entry's slot looked up in d16 (bit 15 set on a first match, for
+// jx_star_first_kernel), its pair added to the block's per-group LDS sums, then the
+// sums into gsum; npairs: the pairs found
+__global__ __launch_bounds__(1024) void jx_ent_probe_kernel(const uint2* __restrict__ ent, uint64_t n, uint32_t qoff,
+                                                            uint64_t range, uint16_t* __restrict__ d16,
+                                                            unsigned long long* __restrict__ gsum,
+                                                            unsigned long long* __restrict__ npairs) {
+    __shared__ unsigned long long sfix[JX_G];
+    __shared__ uint32_t scnt[JX_G], snum[JX_G];
+    for (uint32_t k = threadIdx.x; k < JX_G; k += blockDim.x) { sfix[k] = 0; scnt[k] = 0; snum[k] = 0; }
+    __syncthreads();
+    unsigned long long pairs = 0;
+    const uint64_t nt = (uint64_t)gridDim.x * blockDim.x;
+    constexpr int U = 4;                              // entries in flight per thread
+    for (uint64_t i = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x; i < n; i += U * nt) {
+        uint2 e[U];
+        uint32_t gv[U];
+        uint64_t slot[U];
+#pragma unroll
+        for (int u = 0; u < U; u++) e[u] = i + u * nt < n ? ent[i + u * nt] : make_uint2(0xFFFFFFFFu, 0u);
+#pragma unroll
+        for (int u = 0; u < U; u++) {
+            slot[u] = (uint64_t)(uint32_t)(e[u].x - qoff);
+            const bool in = e[u].x >= qoff && slot[u] < range;
+            gv[u] = in ? (uint32_t)d16[slot[u]] : 0u;
+        }
+#pragma unroll
+        for (int u = 0; u < U; u++) {
+            if (!gv[u]) continue;
+            const uint32_t gi = (gv[u] & 0x7FFFu) - 1u;
+            if (!(gv[u] & 0x8000u)) d16[slot[u]] = (uint16_t)(gv[u] | 0x8000u);   // (every writer: the same value)
+            atomicAdd(&scnt[gi], 1u);
+            if (e[u].y != JX_PNULL) {
+                atomicAdd(&sfix[gi], (unsigned long long)(long long)(int32_t)e[u].y);
+                atomicAdd(&snum[gi], 1u);
+            }
+            pairs++;
+        }
+    }
+    for (int o = 32; o > 0; o >>= 1) pairs += __shfl_down(pairs, o, 64);
+    if ((threadIdx.x & 63) == 0 && pairs) atomicAdd(npairs, pairs);
+    __syncthreads();
+    for (uint32_t k = threadIdx.x; k < JX_G; k += blockDim.x) {
+        if (!scnt[k]) continue;
+        atomicAdd(&gsum[3 * k], (unsigned long long)scnt[k]);
+        if (snum[k]) {
+            atomicAdd(&gsum[3 * k + 1], sfix[k]);
+            atomicAdd(&gsum[3 * k + 2], (unsigned long long)snum[k]);
+        }
+    }
+}
 
 // ------------------------------------------------------------------ fused join: build, probe + aggregate
 // The build side's keys into an open-addressing table of 16-byte entries (stored key
@@ -2781,10 +3000,10 @@ bool jx_plan(const uint8_t* g, uint64_t lo, uint64_t hi, uint32_t ws, uint32_t d
     return true;
 }
 
-size_t fast_lds(int grouped, int ns) {
+size_t fast_lds(int grouped, int ns, int wx = 0) {
     const size_t t = !grouped ? 0 : (ns == 0 ? fast::table_bytes<0>(true) : (ns == 1 ? fast::table_bytes<1>(true)
                                                                                      : fast::table_bytes<2>(true)));
-    return fast::fixed_bytes() + t + 256;
+    return fast::fixed_bytes() + t + 256 + (wx ? 4 * fast::LX_WORDS * 4 : 0);
 }
 
 }  // namespace
@@ -2798,8 +3017,9 @@ int cq_fast_eligible(const cq::ScanPlan* P, int grouped, int want_rows) {
     FastPlan fp;
     int ns = 0;
     bool where = false, canon = false;
-    if (!fast_shape(P, grouped, &fp, &ns, &where, &canon)) return 0;
-    return fast_lds(grouped, ns) <= 160 * 1024 ? 1 : 0;
+    int wx = 0;
+    if (!fast_shape(P, grouped, &fp, &ns, &where, &canon, nullptr, nullptr, &wx)) return 0;
+    return fast_lds(grouped, ns, wx) <= 160 * 1024 ? 1 : 0;
 }
 // 1 when the plan has a MIN / MAX that fast_kernel takes (an EXT build): the
 // executor gives such plans a raw-key table with extreme cells
@@ -2874,7 +3094,7 @@ hipError_t cq_launch_fast(const uint8_t* g, const cq::ScanPlan* P, const cq::Gro
     const bool wstr = fp.wstr_lit != 0;
     const fast_fn_t fn = grouped ? pick_fast<true>(where, ns, comma, canon, false, wn, ext, wstr, wx)
                                  : pick_fast<false>(where, ns, comma, canon, rp3, wn, ext, wstr, wx);
-    const size_t lds = fast_lds(grouped, ns);
+    const size_t lds = fast_lds(grouped, ns, wx);
     cq::set_max_lds((const void*)fn, (int)lds);
     hipLaunchKernelGGL(fn, dim3(grid), dim3(fast::LT), lds, s, g, stats, slow_list, slow_cap, fp,
                        (const GroupTable*)tabs_dev[dev & 63]);
@@ -3084,6 +3304,66 @@ hipError_t cq_jx_star_flush(int grouped, int value, const unsigned long long* tt
     return hipGetLastError();
 }
 uint32_t cq_jx_star_groups() { return cq::fast::JX_G; }
+
+// the typed exchange's sender pass over one side (jx_extract_kernel ROUTE): build = 1
+// writes 16-byte {q32, gid, tag} entries (needs wbase: the count pass's exclusive
+// scan), build = 0 8-byte {q32, pay} entries; region d of `rent` holds rcap entries,
+// rcount[d] the entries reserved (> rcap: flag 256)
+hipError_t cq_jx_route(const uint8_t* g, uint64_t lo, uint64_t hi, uint32_t ws, uint32_t delim, uint32_t quote,
+                       int kcol, int pcol, int build, int rp, const unsigned int* wbase, uint32_t nranks,
+                       unsigned long long qbase, unsigned long long gbase, void* rent, unsigned long long rcap,
+                       unsigned long long* rcount, unsigned int* flag, unsigned long long* krange, int grid,
+                       hipStream_t s) {
+    using namespace cq::fast;
+    JxPlan jp;
+    if (!jx_plan(g, lo, hi, ws, delim, quote, kcol, pcol, &jp)) return hipErrorInvalidValue;
+    if (nranks < 1 || nranks > 64 || (build && !wbase)) return hipErrorInvalidValue;
+    const int nr = pcol >= 0 ? 2 : 1;
+    if (delim != ',' || quote != '"') return hipErrorInvalidValue;      // (the ',' / '"' builds)
+    typedef void (*xfn_t)(const uint8_t*, const JxPlan, const JxOut);
+    // [build][roles - 1][three records per pass]
+    static const xfn_t tab[2][2][2] = {
+        {{jx_extract_kernel<false, true, 1, false, false, 2, false, true>, jx_extract_kernel<false, true, 1, false, false, 3, false, true>},
+         {jx_extract_kernel<false, true, 2, false, false, 2, false, true>, jx_extract_kernel<false, true, 2, false, false, 3, false, true>}},
+        {{jx_extract_kernel<true, true, 1, false, false, 2, false, true>, jx_extract_kernel<true, true, 1, false, false, 3, false, true>},
+         {jx_extract_kernel<true, true, 2, false, false, 2, false, true>, jx_extract_kernel<true, true, 2, false, false, 3, false, true>}}};
+    const xfn_t fn = tab[build ? 1 : 0][nr - 1][rp == 3 ? 1 : 0];
+    JxOut jo;
+    memset(&jo, 0, sizeof jo);
+    jo.wbase = wbase;
+    jo.flag = flag;
+    jo.krange = krange;
+    jo.rent = rent;
+    jo.rcount = rcount;
+    jo.rcap = rcap;
+    jo.rn = nranks;
+    // ceil(2^64 / n): key / n = mulhi(key, magic) for keys below 2^64 / n (canonical keys < 10^15)
+    jo.rmagic = nranks > 1 ? (unsigned long long)(((unsigned __int128)1 << 64) / nranks) + 1ull : 0ull;
+    if (nranks > 1 && (nranks & (nranks - 1)) == 0) jo.rmagic = 1ull << (64 - __builtin_ctz(nranks));
+    jo.qbase = qbase;
+    jo.gbase = gbase;
+    const size_t lds = sizeof(WaveLds) * NWV;
+    cq::set_max_lds((const void*)fn, (int)lds);
+    if (jp.nwin == 0) return hipSuccess;
+    hipLaunchKernelGGL(fn, dim3(grid), dim3(LT), lds, s, g, jp, jo);
+    return hipGetLastError();
+}
+// the receiving rank's STAR over the entries (jx_ent_build_kernel, jx_ent_probe_kernel)
+hipError_t cq_jx_ent_build(const void* ent, unsigned long long n, uint32_t qoff, unsigned long long range, uint16_t* d16,
+                           uint32_t* l32, unsigned long long* ttab, unsigned long long* nplaced, unsigned int* flag,
+                           int grid, hipStream_t s, int ungrouped) {
+    if (!n) return hipSuccess;
+    hipLaunchKernelGGL(cq::fast::jx_ent_build_kernel, dim3(grid), dim3(1024), 0, s, (const uint4*)ent, (uint64_t)n, qoff,
+                       (uint64_t)range, d16, l32, ttab, nplaced, flag, (uint32_t)(ungrouped != 0));
+    return hipGetLastError();
+}
+hipError_t cq_jx_ent_probe(const void* ent, unsigned long long n, uint32_t qoff, unsigned long long range, uint16_t* d16,
+                           unsigned long long* gsum, unsigned long long* npairs, int grid, hipStream_t s) {
+    if (!n) return hipSuccess;
+    hipLaunchKernelGGL(cq::fast::jx_ent_probe_kernel, dim3(grid), dim3(1024), 0, s, (const uint2*)ent, (uint64_t)n, qoff,
+                       (uint64_t)range, d16, gsum, npairs);
+    return hipGetLastError();
+}
 
 hipError_t cq_jx_build(const unsigned long long* key, uint32_t n, void* table, uint64_t tcap, unsigned int* flag,
                        int grid, hipStream_t s) {

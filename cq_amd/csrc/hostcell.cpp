@@ -5,6 +5,8 @@
 #include "cell.h"
 
 extern "C" cq::Cell cq_host_parse_cell(const uint8_t* text, uint32_t len) { return cq::parse_cell(text, len); }
+// create_groups' canonical key of a cell (the typed join exchange's tags, on the host)
+extern "C" cq::GKey cq_host_group_key(cq::Cell c) { return cq::group_key(c); }
 
 #include "plan.h"
 

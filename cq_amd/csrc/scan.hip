@@ -2633,7 +2633,9 @@ hipError_t cq_launch_scan(const uint8_t* g, const cq::ScanPlan* P, const cq::Gro
     // lean-eligible plans; any other MIN / MAX plan the general scan_kernel
     const bool fext = scan_mode() == 0 && !cells_out && lean_enabled() && row_out == nullptr &&
                       cq_fast_ext_plan(P, grouped) && cq_fast_eligible(P, grouped, 0);
-    if ((cq_scan_uses_lean(P, cells_out != nullptr) || fext) && (!grouped || rt)) {
+    // (plans fast_kernel takes that lean_kernel does not: its compound-WHERE builds)
+    const bool fonly = scan_mode() == 0 && !cells_out && lean_enabled() && cq_fast_eligible(P, grouped, row_out != nullptr);
+    if ((cq_scan_uses_lean(P, cells_out != nullptr) || fext || fonly) && (!grouped || rt)) {
         // slow_kernel reads this file's plan and table symbols
         hipError_t e0 = cq::upload_symbol((const void*)&HIP_SYMBOL(cq::c_plan), P, sizeof *P, s);
         if (e0 == hipSuccess)

@@ -207,6 +207,51 @@ cq_table* cqgpu_dist_query(cq_node* query_ast, cqgpu_table* shard, int* status, 
  * (cqgpu_merge_partials' nested-loop order).  Rank 0 returns the result; *status:
  * 0, or -1 on EVERY rank when any rank failed (refusals included). */
 cq_table* cqgpu_dist_join(cq_node* query_ast, cqgpu_table* const* tables, int ntables, int* status);
+/* ---- the typed exchange of the repartitioned JOIN (SURVEY.md section 8e's
+ * (key, row id, payload) entries; cqgpu_dist_join takes it whenever the plan and the
+ * data allow, falling back to the CSV-record exchange below together on every rank).
+ * Plan: one INNER JOIN `l.k = r.k` without WHERE, COUNT / SUM / AVG of one right
+ * column, GROUP BY one left column (its value the only other item) or none.  Every
+ * record of the FROM table (side 0, the build side) becomes a 16-byte entry
+ * {key / N - qbase, global record id, GROUP BY bytes}, every record of the JOIN table
+ * (side 1) an 8-byte entry {key / N - qbase, SUM argument in 10^-3 units or
+ * 0x80000000 for NULL}, in the region of rank key mod N (perform_join's keys as
+ * canonical INTEGERs, evaluator_joins.c:40-60; a NULL probe key and a probe key
+ * outside the build keys' window match nothing and are not sent).  The receiver
+ * joins the entries with the STAR join (one residue class of a dense key range) and
+ * writes the same "CQJ1" partial cqgpu_query_partial would.
+ *   cqgpu_typed_plan     1 when the plan takes the typed exchange (0: *_ineligible says why)
+ *   cqgpu_typed_sample_kmin  the build side's sampled key minimum (first qbase = min / N)
+ *   cqgpu_typed_count    the FROM table's records (the build side's count pass); the
+ *                        caller sums the lower ranks' counts into gid_base
+ *   cqgpu_typed_send     one side's entries into N regions kept by the table (cap
+ *                        entries each, 0: estimated); counts[N] the entries per
+ *                        region, krange the build side's keys' min and max, flags: 1
+ *                        not typable (quote, key or value shape), 8 a NULL build key,
+ *                        16 a build key / N - qbase outside 32 bits (retry with qbase =
+ *                        kmin / N), 256 a region too small (retry with cap = max count),
+ *                        512 a payload outside 31 bits
+ *   cqgpu_typed_region   region `dest` of a table's entries (device pointer)
+ *   cqgpu_typed_gather   regions `dest` of several tables, concatenated into dev_out (one
+ *                        GPU standing in for the exchange: tests and the benchmark)
+ *   cqgpu_typed_partial  the receiving rank's STAR join over its entries: slot = q32 - qoff,
+ *                        range slots (qoff = kmin / N - qbase, range = kmax / N - kmin / N + 1
+ *                        over the global build keys); the blob as cqgpu_query_partial's,
+ *                        0 + *_ineligible when the entries do not fit the STAR join */
+int cqgpu_typed_plan(cq_node* query_ast, cqgpu_table* const* tables, int ntables);
+int64_t cqgpu_typed_count(cq_node* query_ast, cqgpu_table* const* tables, int ntables);
+/* the build side's sampled key minimum (a first qbase is its minimum over the ranks / N) */
+uint64_t cqgpu_typed_sample_kmin(cq_node* query_ast, cqgpu_table* const* tables, int ntables);
+int cqgpu_typed_send(cq_node* query_ast, cqgpu_table* const* tables, int ntables, int side, int nranks, uint64_t qbase,
+                     uint64_t gid_base, uint64_t cap, uint64_t* counts, uint64_t* krange, uint32_t* flags);
+const void* cqgpu_typed_region(const cqgpu_table* t, int dest, uint64_t* entries, uint64_t* entry_bytes);
+/* drop a table's entries and its cached record count (the next send recounts) */
+void cqgpu_typed_reset(cqgpu_table* t);
+int64_t cqgpu_typed_gather(cqgpu_table* const* senders, int nsenders, int dest, void* dev_out, uint64_t cap_entries);
+size_t cqgpu_typed_partial(cq_node* query_ast, cqgpu_table* const* tables, int ntables, const void* dev_build,
+                           uint64_t nbuild, const void* dev_probe, uint64_t nprobe, uint64_t qoff, uint64_t range,
+                           void** blob_out);
+
 /* test entry: the gather-merge of `n` shards held by this one process (simulated
  * ranks, no RCCL): every shard's pack, then rank 0's merge kernels; NULL +
  * cqgpu_last_ineligible when the plan or the data leaves the gather-merge */

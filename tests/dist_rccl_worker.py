@@ -70,6 +70,7 @@ def main():
                 else:
                     got = "none"
             results.append({"sql": sql, "status": status, "path": p, "error": cq_amd.last_error(),
+                            "kernel": cq_amd.stats().get("scan_kernel"),
                             "result": None if got in (None, "none") else
                             {"columns": got["columns"], "rows": [[list(c) for c in r] for r in got["rows"]]}})
         for x in tabs:

@@ -172,3 +172,37 @@ def test_explain_without_device():
     assert "need: 2 4 5" in text and "group_slot: 2" in text
     q2 = P.query([P.ident("a")], "x.csv", joins=[("y.csv", None, P.cond("=", P.ident("a"), P.ident("b")), 0)])
     assert lib.cqgpu_explain(C.pointer(q2), b"a,b", abi.csv_config(), buf, 4096) != 0
+
+
+@pytest.mark.parametrize("where,fast", [
+    ("age > 30", 1),
+    ("age BETWEEN 20 AND 40", 1),                                    # AND(>=, <=)
+    ("age > 30 AND gender = 'f'", 1),                                # NUMBER and STRING columns
+    ("role IN ('role_001', 'role_002')", 1),
+    ("NOT age > 30", 1),
+    ("30 < age", 1),                                                 # literal on the left
+    ("age > -5", 1),                                                 # unary minus literal
+    ("height IN (1.1, 2.25)", 1),
+    ("age < 20 OR gender != 'm' AND age > 70", 1),
+    ("age = 1 OR age = 2 OR age = 3 OR age = 4 OR age = 5", 0),      # 5 leaves
+    ("age > 30 OR age = 'abc'", 0),                                  # one column, both classes
+    ("age > 30 AND gender = 'f' AND height > 1.2", 0),               # 3 WHERE columns
+    ("age + 1 > 30", 0),                                             # arithmetic
+    ("role IN ('a', 'b', 'c', 'd', 'e', 'f', 'g', 'h', 'i')", 0),    # 9 items
+    ("gender = 'abcdefghi'", 0),                                     # a 9-byte literal
+])
+def test_fast_kernel_where_shapes_on_cpu(where, fast):
+    """which WHEREs fast_kernel's builds take (fast.hip fast_shape / wx_compile), decided
+    on the host from the plan alone: compound trees of <= 4 leaves over <= 2 columns"""
+    import cqtest
+    lib = cq_amd.lib()
+    lib.cqgpu_explain.restype = C.c_int
+    lib.cqgpu_explain.argtypes = [C.POINTER(abi.Node), C.c_char_p, abi.CsvConfig, C.c_char_p, C.c_size_t]
+    buf = C.create_string_buffer(8192)
+    sql = f"SELECT role, COUNT(*), SUM(height), AVG(height) FROM 'x.csv' WHERE {where} GROUP BY role"
+    with cqtest.Parsed(sql) as ast:
+        if lib.cqgpu_explain(ast, b"name,surname,age,gender,height,role", abi.csv_config(), buf, 8192) != 0:
+            assert fast == 0, (where, lib.cqgpu_last_error())    # (outside the GPU subset altogether)
+            return
+    lines = dict(ln.split(": ", 1) for ln in buf.value.decode().split("\n") if ln.startswith("fast: "))
+    assert lines["fast"] == str(fast), (where, buf.value.decode())

@@ -319,6 +319,8 @@ def test_dist_join_multi_rank_host_backend(files, tmp_path, world):
     for i, ((sql, keys), r) in enumerate(zip(JOINS, res)):
         q = sql.format(**dict(zip("pqrs", [files[k] for k in keys])))
         assert r["status"] == 0, (q, r["error"])
+        if i == 0:                                   # config 5's shape: the typed exchange
+            assert r["kernel"] == 5, (q, r)
         assert all(pr[i]["status"] == 0 for pr in per), (q, per)
         want, unsup = cqtest.oracle_query(q)
         assert not unsup
@@ -330,8 +332,9 @@ def test_dist_join_multi_rank_host_backend(files, tmp_path, world):
 @pytest.mark.parametrize("knob,kind", [
     ("CQGPU_TEST_GM_FAIL_PART", "query"),            # one rank's gather-merge part
     ("CQGPU_TEST_GM_FAIL_FINISH", "query"),          # (read by rank 0 only)
-    ("CQGPU_TEST_DIST_FAIL_ALLOC", "join"),          # one rank's exchange buffers
+    ("CQGPU_TEST_DIST_FAIL_ALLOC", "join"),          # one rank's CSV-exchange buffers
     ("CQGPU_TEST_DIST_CHAIN_MISSING", "chain"),      # one rank lacks a chain level's table
+    ("CQGPU_TEST_TYPED_FAIL", "typed"),              # one rank's typed-exchange send
 ])
 def test_dist_one_rank_failure_reaches_every_rank(files, tmp_path, knob, kind):
     """a failure on ONE rank of three is status -1 on EVERY rank after the same
@@ -339,11 +342,28 @@ def test_dist_one_rank_failure_reaches_every_rank(files, tmp_path, knob, kind):
     (exchange allocations and the chain loop inside the agreement)"""
     fail_rank = 0 if knob == "CQGPU_TEST_GM_FAIL_FINISH" else 1
     env = {"CQ_TEST_RANK_ENV": f"{fail_rank}:{knob}=1"}
+    if kind == "join":
+        env["CQGPU_NO_TYPED_JOIN"] = "1"              # (the CSV exchange's allocation)
     if kind == "query":
         res, per = _host_run(files, tmp_path, [(GM[0], "plain")], 3, env=env)
     else:
-        item = JOINS[0] if kind == "join" else JOINS[4]
+        item = JOINS[0] if kind in ("join", "typed") else JOINS[4]
         res, per = _host_run(files, tmp_path, [item], 3, env=env, paths_of=True)
     for r, pr in enumerate(per):
         assert pr[0]["status"] == -1, (r, pr)
     assert "injected" in per[fail_rank][0]["error"] or "missing" in per[fail_rank][0]["error"], per[fail_rank]
+
+
+@pytest.mark.parametrize("world", [2, 3])
+def test_dist_join_multi_rank_csv_exchange(files, tmp_path, world):
+    """the CSV-record exchange (CQGPU_NO_TYPED_JOIN=1: every plan takes it) at world size
+    2 and 3 -- the fallback the typed exchange leaves to -- against the oracle"""
+    res, per = _host_run(files, tmp_path, JOINS[:2], world, env={"CQGPU_NO_TYPED_JOIN": "1"}, paths_of=True)
+    for (sql, keys), r in zip(JOINS[:2], res):
+        q = sql.format(**dict(zip("pqrs", [files[k] for k in keys])))
+        assert r["status"] == 0, (q, r["error"])
+        assert r["kernel"] != 5, (q, r)
+        want, _ = cqtest.oracle_query(q)
+        with cqtest.Parsed(q) as ast:
+            tol = tolerant_columns(ast)
+        compare(_as_got(r), want, tol, f"dist_join (CSV exchange) {world} ranks: {q}")

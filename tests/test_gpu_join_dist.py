@@ -291,6 +291,43 @@ def test_repartitioned_fused_join(files, nranks):
     assert len(kinds) == nranks and all(k == 4 for k in kinds), kinds
 
 
+def _blob_groups(blob: bytes):
+    """a "CQJ1" partial's groups, field by field -- everything but the table addresses
+    STRING cells carry in their bits (meaningless across table instances)"""
+    import struct
+    o = [0]
+
+    def take(fmt):
+        v = struct.unpack_from("<" + fmt, blob, o[0])
+        o[0] += struct.calcsize("<" + fmt)
+        return v[0]
+
+    def text():
+        n = take("I")
+        o[0] += n
+        return blob[o[0] - n:o[0]]
+
+    def cell():
+        k, bits, s = take("I"), take("Q"), text()
+        return (k, s) if k == 3 else (k, bits)
+    assert take("I") == 0x314a5143
+    names = [text() for _ in range(take("I"))]
+    nacc = take("I")
+    classes = [take("I") for _ in range(nacc)]
+    nrep, nvla = take("I"), take("I")
+    masks = (take("I"), take("I"))
+    out = [names, classes, nrep, nvla, masks]
+    for _ in range(take("Q")):
+        g = [take("I"), take("I"), take("Q"), take("Q"), text(), take("Q"), take("Q")]
+        g.append([(take("d"), take("Q"), take("Q"), cell()) for _ in range(nacc)])
+        g.append([cell() for _ in range(nrep)])
+        assert nvla == 0
+        g.append(take("I"))                       # class splits (none for these plans)
+        out.append(g)
+    assert o[0] == len(blob)
+    return out
+
+
 @pytest.mark.parametrize("nranks", [1, 3])
 def test_first_ids_device_equals_host(files, nranks, monkeypatch):
     """the STAR partial's first-pair global ids mapped on the device
@@ -308,7 +345,7 @@ def test_first_ids_device_equals_host(files, nranks, monkeypatch):
             assert tp, cq_amd.last_error()
             assert all(k == 4 for k in LAST_KINDS), LAST_KINDS
             cq_amd.result_free(tp)
-            got.append(list(LAST_BLOBS))
+            got.append([_blob_groups(b) for b in LAST_BLOBS])
     assert got[0] == got[1]
 
 
@@ -817,3 +854,121 @@ def test_join_chain_processes(files, world, case):
     with cqtest.Parsed(sql) as ast:
         tol = tolerant_columns(ast)
     compare(got, want, tol, sql + f" @ {world} processes")
+
+
+# ---------------------------------------------------------------- the typed exchange
+TYPED = [
+    "SELECT u.role, COUNT(*), SUM(o.price), AVG(o.price) FROM '{u}' AS u JOIN '{o}' AS o ON u.id = o.customer_id "
+    "GROUP BY u.role",
+    "SELECT COUNT(*) FROM '{u}' AS u JOIN '{o}' AS o ON u.id = o.customer_id",
+    "SELECT COUNT(*), SUM(o.price) FROM '{u}' AS u JOIN '{o}' AS o ON u.id = o.customer_id",
+    "SELECT u.role, COUNT(*) FROM '{u}' AS u JOIN '{o}' AS o ON u.id = o.customer_id GROUP BY u.role "
+    "ORDER BY COUNT(*) DESC LIMIT 5",
+    "SELECT u.role, 7, AVG(o.price) FROM '{u}' AS u JOIN '{o}' AS o ON o.customer_id = u.id GROUP BY u.role",
+]
+
+
+def _typed(ast, ldata, rdata, nranks, stats=None):
+    from cq_amd.dist import typed_join_local
+    _, ls = _shards(ldata, nranks, 1)
+    _, rs = _shards(rdata, nranks, 2)
+    try:
+        blobs = typed_join_local(ast, ls, rs, stats)
+        if blobs is None:
+            return None, cq_amd.last_ineligible()
+        return cq_amd.merge_partials(ast, blobs), LAST_KINDS
+    finally:
+        for t in ls + rs:
+            t.close()
+
+
+@pytest.mark.parametrize("nranks", [1, 2, 3, 5, 8])
+@pytest.mark.parametrize("qi", range(len(TYPED)))
+def test_typed_exchange_equals_oracle(files, nranks, qi):
+    """SURVEY 8e's typed (key, row id, payload) exchange: every simulated rank's
+    16-byte build / 8-byte probe entries routed by key mod N, each destination's STAR
+    join over its entries, the partials merged -- the oracle's nested loop: COUNT exact,
+    SUM / AVG 1e-6 relative, groups in the order of their first matched user"""
+    data, paths = files
+    sql = TYPED[qi].format(u=paths["users"], o=paths["orders"])
+    want, unsup = cqtest.oracle_query(sql)
+    assert not unsup
+    st = {}
+    with cqtest.Parsed(sql) as ast:
+        tp, why = _typed(ast, data["users"], data["orders"], nranks, st)
+        assert tp, (cq_amd.last_error(), why)
+        got = abi.table_to_py(tp)
+        cq_amd.result_free(tp)
+        tol = tolerant_columns(ast)
+    compare(got, want, tol, f"typed exchange {nranks} ranks: {sql}")
+    assert sum(st["recv_entries_u"]) == 4000 and st["attempts"] == 1, st
+
+
+def test_typed_exchange_large_keys_retry(tmp_path):
+    """keys near 10^14: key / N does not fit 32 bits, the first attempt flags it and the
+    second runs with qbase = the keys' minimum / N; and a probe side with keys outside
+    the build window, NULL keys and NULL / negative prices"""
+    rng = np.random.default_rng(41)
+    n = 3000
+    users = "id,name,role\n" + "".join("%d,n%d,r%02d\n" % (10**14 + 7 * i, i, rng.integers(0, 30)) for i in range(n))
+    rows = []
+    for i in range(9000):
+        k = int(rng.integers(0, n + 200))
+        cid = "" if i % 97 == 0 else str(10**14 + 7 * k if k < n else 10**14 + 7 * k + 3)
+        pr = "" if i % 89 == 0 else ("-%d.%02d" % (rng.integers(0, 50), rng.integers(0, 100)) if i % 31 == 0
+                                     else "%d.%d" % (rng.integers(0, 999), rng.integers(0, 10)))
+        rows.append("%d,%s,%s" % (i, pr, cid))
+    orders = "id,price,customer_id\n" + "\n".join(rows) + "\n"
+    up, op = tmp_path / "u.csv", tmp_path / "o.csv"
+    up.write_text(users)
+    op.write_text(orders)
+    sql = (f"SELECT u.role, COUNT(*), SUM(o.price), AVG(o.price) FROM '{up}' AS u JOIN '{op}' AS o "
+           f"ON u.id = o.customer_id GROUP BY u.role")
+    want, _ = cqtest.oracle_query(sql)
+    for nranks in (1, 3, 8):
+        st = {}
+        with cqtest.Parsed(sql) as ast:
+            tp, why = _typed(ast, users.encode(), orders.encode(), nranks, st)
+            assert tp, (cq_amd.last_error(), why)
+            got = abi.table_to_py(tp)
+            cq_amd.result_free(tp)
+            tol = tolerant_columns(ast)
+        compare(got, want, tol, f"typed, large keys, {nranks} ranks")
+        assert st["attempts"] <= 2 and st["qbase"] > 0, st
+
+
+@pytest.mark.parametrize("case", ["dup", "null", "quote", "sparse", "tags", "canon"])
+def test_typed_exchange_declines_or_merges(tmp_path, case):
+    """data the entries cannot carry exactly leaves the typed exchange (None: the
+    caller takes the CSV exchange) -- a repeated or NULL build key, a quote, a sparse key
+    range; tags of one canonical key ("1.0", "1.00", "1") merge into one group"""
+    users = ["id,name,role"] + ["%d,n%d,%s" % (100 + i, i, "r%d" % (i % 4)) for i in range(400)]
+    orders = ["id,price,customer_id"] + ["%d,%d.5,%d" % (i, i % 50, 100 + (i * 7) % 400) for i in range(1500)]
+    if case == "dup":
+        users.append("150,dup,r1")
+    elif case == "null":
+        users.append(",nul,r2")
+    elif case == "quote":
+        users[5] = '104,"q,x",r0'
+    elif case == "sparse":
+        users.append("100000000,far,r3")
+    elif case == "tags":
+        users = ["id,name,role"] + ["%d,n%d,%s" % (100 + i, i, ["1.0", "1.00", "1", "2.5"][i % 4]) for i in range(400)]
+    elif case == "canon":
+        users = ["id,name,role"] + ["%d,n%d,%s" % (100 + i, i, ["x", "y", "", "z"][i % 4]) for i in range(400)]
+    up, op = tmp_path / "u.csv", tmp_path / "o.csv"
+    up.write_text("\n".join(users) + "\n")
+    op.write_text("\n".join(orders) + "\n")
+    sql = (f"SELECT u.role, COUNT(*), SUM(o.price) FROM '{up}' AS u JOIN '{op}' AS o "
+           f"ON u.id = o.customer_id GROUP BY u.role")
+    with cqtest.Parsed(sql) as ast:
+        tp, why = _typed(ast, up.read_bytes(), op.read_bytes(), 3)
+        if case in ("dup", "null", "quote", "sparse"):
+            assert tp is None, case
+            return
+        assert tp, (cq_amd.last_error(), why)
+        got = abi.table_to_py(tp)
+        cq_amd.result_free(tp)
+        tol = tolerant_columns(ast)
+    want, _ = cqtest.oracle_query(sql)
+    compare(got, want, tol, f"typed {case}")
