@@ -422,19 +422,21 @@ def typed_rank_step_leg(n_total: int, nranks: int, steps: int, warmup: int, seed
     pair = lambda r: [U[r], O[r]]  # noqa: E731
     if not cq_amd.typed_plan(ast, pair(0)):
         raise RuntimeError("config 5's plan outside the typed exchange: " + cq_amd.last_ineligible())
-    nrec = [cq_amd.typed_count(ast, pair(r)) for r in range(nranks)]
-    gbase = [sum(nrec[:r]) for r in range(nranks)]
     smin = min(cq_amd.typed_sample_kmin(ast, pair(r)) for r in range(nranks))
     qbase = smin // nranks
-    cu, co, kmin, kmax, flags = [], [], (1 << 64) - 1, 0, 0
+    cu, co, nrec, kmin, kmax, flags = [], [], [], (1 << 64) - 1, 0, 0
     for r in range(nranks):
-        c1, kr, f1 = cq_amd.typed_send(ast, pair(r), 0, nranks, qbase, gbase[r])
-        c2, _, f2 = cq_amd.typed_send(ast, pair(r), 1, nranks, qbase, 0)
+        nu, c1, kr, f1 = cq_amd.typed_count(ast, pair(r), 0, nranks, qbase)
+        _, c2, _, f2 = cq_amd.typed_count(ast, pair(r), 1, nranks, qbase)
         cu.append(c1)
         co.append(c2)
+        nrec.append(nu)
         kmin, kmax, flags = min(kmin, kr[0]), max(kmax, kr[1]), flags | f1 | f2
+    gbase = [sum(nrec[:r]) for r in range(nranks)]
+    for r in range(nranks):
+        flags |= cq_amd.typed_send(ast, pair(r), 0, gbase[r]) | cq_amd.typed_send(ast, pair(r), 1, 0)
     if flags:
-        raise RuntimeError(f"typed send flags {flags:#x}")
+        raise RuntimeError(f"typed exchange flags {flags:#x}")
     qoff, rng = kmin // nranks - qbase, kmax // nranks - kmin // nranks + 1
     recv_u = [sum(cu[s][d] for s in range(nranks)) for d in range(nranks)]
     recv_o = [sum(co[s][d] for s in range(nranks)) for d in range(nranks)]
@@ -461,12 +463,12 @@ def typed_rank_step_leg(n_total: int, nranks: int, steps: int, warmup: int, seed
         mark.t = time.perf_counter()
         cq_amd.typed_reset(U[0])
         cq_amd.typed_reset(O[0])
-        cq_amd.typed_count(ast, pair(0))
+        cq_amd.typed_count(ast, pair(0), 0, nranks, qbase)
+        cq_amd.typed_count(ast, pair(0), 1, nranks, qbase)
         mark("count")
-        c1, _, f1 = cq_amd.typed_send(ast, pair(0), 0, nranks, qbase, gbase[0])
-        c2, _, f2 = cq_amd.typed_send(ast, pair(0), 1, nranks, qbase, 0)
-        if f1 | f2:
-            raise RuntimeError(f"typed send flags {f1 | f2:#x}")
+        f = cq_amd.typed_send(ast, pair(0), 0, gbase[0]) | cq_amd.typed_send(ast, pair(0), 1, 0)
+        if f:
+            raise RuntimeError(f"typed send flags {f:#x}")
         mark("send")
         nu = cq_amd.typed_gather(U, 0, bu.data_ptr(), recv_u[0])
         no = cq_amd.typed_gather(O, 0, bo.data_ptr(), recv_o[0])

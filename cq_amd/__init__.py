@@ -119,10 +119,10 @@ def lib():
         L.cqgpu_typed_sample_kmin.restype = C.c_uint64
         L.cqgpu_typed_sample_kmin.argtypes = [C.POINTER(abi.Node), C.POINTER(vp), C.c_int]
         L.cqgpu_typed_count.restype = C.c_int64
-        L.cqgpu_typed_count.argtypes = [C.POINTER(abi.Node), C.POINTER(vp), C.c_int]
+        L.cqgpu_typed_count.argtypes = [C.POINTER(abi.Node), C.POINTER(vp), C.c_int, C.c_int, C.c_int, C.c_uint64,
+                                        C.POINTER(C.c_uint64), C.POINTER(C.c_uint64), C.POINTER(C.c_uint32)]
         L.cqgpu_typed_send.restype = C.c_int
-        L.cqgpu_typed_send.argtypes = [C.POINTER(abi.Node), C.POINTER(vp), C.c_int, C.c_int, C.c_int, C.c_uint64,
-                                       C.c_uint64, C.c_uint64, C.POINTER(C.c_uint64), C.POINTER(C.c_uint64),
+        L.cqgpu_typed_send.argtypes = [C.POINTER(abi.Node), C.POINTER(vp), C.c_int, C.c_int, C.c_uint64,
                                        C.POINTER(C.c_uint32)]
         L.cqgpu_typed_region.restype = vp
         L.cqgpu_typed_region.argtypes = [vp, C.c_int, C.POINTER(C.c_uint64), C.POINTER(C.c_uint64)]
@@ -413,22 +413,24 @@ def typed_sample_kmin(ast, tables) -> int:
     return lib().cqgpu_typed_sample_kmin(ast, *_tables_arg(tables))
 
 
-def typed_count(ast, tables) -> int:
-    n = lib().cqgpu_typed_count(ast, *_tables_arg(tables))
-    if n < 0:
-        raise RuntimeError(last_error() or "cqgpu_typed_count failed")
-    return n
-
-
-def typed_send(ast, tables, side: int, nranks: int, qbase: int, gid_base: int, cap: int = 0):
-    """(counts per destination, (build keys' min, max), flags)"""
+def typed_count(ast, tables, side: int, nranks: int, qbase: int):
+    """the count pass: (records (build) / entries (probe), counts per destination,
+    (build keys' min, max), flags)"""
     counts = (C.c_uint64 * nranks)()
     kr = (C.c_uint64 * 2)()
     fl = C.c_uint32(0)
-    if lib().cqgpu_typed_send(ast, *_tables_arg(tables), side, nranks, qbase, gid_base, cap, counts, kr,
-                              C.byref(fl)) != 0:
+    n = lib().cqgpu_typed_count(ast, *_tables_arg(tables), side, nranks, qbase, counts, kr, C.byref(fl))
+    if n < 0:
+        raise RuntimeError(last_error() or "cqgpu_typed_count failed")
+    return n, list(counts), (kr[0], kr[1]), fl.value
+
+
+def typed_send(ast, tables, side: int, gid_base: int) -> int:
+    """the emit pass after typed_count; returns its flags"""
+    fl = C.c_uint32(0)
+    if lib().cqgpu_typed_send(ast, *_tables_arg(tables), side, gid_base, C.byref(fl)) != 0:
         raise RuntimeError(last_error() or "cqgpu_typed_send failed")
-    return list(counts), (kr[0], kr[1]), fl.value
+    return fl.value
 
 
 def typed_reset(table) -> None:

@@ -221,9 +221,9 @@ hipError_t cq_jx_star_flush(int grouped, int value, const unsigned long long* tt
                             unsigned int* flag, hipStream_t s);
 uint32_t cq_jx_star_groups();
 hipError_t cq_jx_route(const uint8_t* g, uint64_t lo, uint64_t hi, uint32_t ws, uint32_t delim, uint32_t quote,
-                       int kcol, int pcol, int build, int rp, const unsigned int* wbase, uint32_t nranks,
-                       unsigned long long qbase, unsigned long long gbase, void* rent, unsigned long long rcap,
-                       unsigned long long* rcount, unsigned int* flag, unsigned long long* krange, int grid,
+                       int kcol, int pcol, int build, int rp, int pass, uint32_t nranks, unsigned long long qbase,
+                       unsigned long long gbase, unsigned int* rcnt, unsigned int* wcount, const unsigned int* roffs,
+                       const unsigned int* wbase, void* rent, unsigned int* flag, unsigned long long* krange, int grid,
                        hipStream_t s);
 hipError_t cq_jx_ent_build(const void* ent, unsigned long long n, uint32_t qoff, unsigned long long range, uint16_t* d16,
                            uint32_t* l32, unsigned long long* ttab, unsigned long long* nplaced, unsigned int* flag,
@@ -589,14 +589,21 @@ struct RouteState {
     uint32_t last_keep = ~0u;
 };
 
-// the typed join exchange's send side of one table (cqgpu_typed_send): nranks regions
-// of `cap` fixed-size entries (16 B build, 8 B probe), counts[d] of them used
+// the typed join exchange's send side of one table (cqgpu_typed_count / _send): the
+// count pass's per (destination, window) entry counts and their scan, then the entries,
+// destination d's in [rstart[d], rstart[d + 1]) (16 B build, 8 B probe)
 struct TypedSend {
-    DevBuf ent;
-    uint64_t cap = 0, esize = 0;
-    std::vector<uint64_t> counts;
+    uint32_t N = 0, ws = 0;
+    int rp = 2;
+    uint64_t qbase = 0, nwin = 0;
+    DevBuf rcnt, roffs, wcount, wbase;
+    std::vector<uint64_t> counts, rstart;
+    uint64_t nrec = 0;                              // (build) the table's records
     uint32_t flags = 0;
     unsigned long long krange[2] = {~0ull, 0ull};   // the build side's keys' min, max (every non-NULL one)
+    DevBuf ent;
+    uint64_t esize = 0;
+    bool emitted = false;
 };
 
 constexpr uint64_t SAMPLE_BYTES = 256u << 10;   // bytes a table keeps for plan-time sampling
@@ -642,12 +649,8 @@ struct cqgpu_table {
     std::unique_ptr<RouteState> route;    // pending repartition (cqgpu_route_plan)
     std::unique_ptr<DevBuf> rec_starts;   // record start offsets, file order (built on first need; immutable table)
     uint32_t nrec_starts = 0;
-    // the typed join exchange (cqgpu_typed_*): this table's pending entries, and its
-    // record count and per-window record bases of the stride they were counted at
+    // the typed join exchange (cqgpu_typed_*): this table's counts and pending entries
     std::unique_ptr<TypedSend> tsend;
-    uint64_t typed_nrec = ~0ull;
-    uint32_t typed_ws = 0;
-    std::unique_ptr<DevBuf> typed_wbase;
 };
 
 namespace {
@@ -5886,6 +5889,10 @@ cq_table* cqgpu_merge_partials(cq_node* q, const void* const* blobs, const size_
     memset(&g_stats, 0, sizeof g_stats);
     g_inel.clear();
     g_err.clear();
+    PhaseClock pc;
+    PhaseClock* const outer_phase = g_phase;
+    g_phase = &pc;
+    struct Unset { PhaseClock* o; ~Unset() { g_phase = o; } } unset_{outer_phase};
     try {
         DevCtx& c = ctx();
         if (nblobs < 1) throw HipError{"no partials"};
@@ -5957,6 +5964,7 @@ cq_table* cqgpu_merge_partials(cq_node* q, const void* const* blobs, const size_
                 throw HipError{"partials from different plans"};
             if (nv > (uint32_t)MAX_ACC) throw HipError{"bad partial blob"};
             const uint64_t ng = r.u64();
+            pt.groups.reserve((size_t)std::min<uint64_t>(ng, (r.n - r.o) / 40 + 1));
             for (uint64_t gi = 0; gi < ng; gi++) {
                 HGroup h;
                 h.kcls = r.u32(); h.klen = r.u32(); h.kw0 = r.u64(); h.kw1 = r.u64(); h.kbytes = r.str();
@@ -5987,6 +5995,7 @@ cq_table* cqgpu_merge_partials(cq_node* q, const void* const* blobs, const size_
                 pt.groups.push_back(std::move(h));
             }
         }
+        PHASE("merge parse");
         // the plan binds columns by name: compile it against the shards' header
         const bool joined = magic0 == 0x314a5143u;
         if (joined) {
@@ -6041,14 +6050,20 @@ cq_table* cqgpu_merge_partials(cq_node* q, const void* const* blobs, const size_
             return (C.P.acc[a].kind == ACC_MIN ? cv < 0 : cv > 0) || (cv == 0 && xp < yp);
         };
         std::vector<HGroup> merged;
+        size_t total_groups = 0;
+        for (auto& pt : parts) total_groups += pt.groups.size();
+        merged.reserve(total_groups);
         std::unordered_map<std::string, size_t> where;
+        where.reserve(total_groups * 2);
+        std::string id;
         for (auto& pt : parts) {
             for (HGroup& h : pt.groups) {
                 // group identity: class + text for text keys, class + payload otherwise
-                std::string id = std::to_string(h.kcls) + ":";
+                // (raw bytes of the words: a fixed-width key, no decimal formatting)
+                id.assign((const char*)&h.kcls, 4);
                 if (h.kcls == GK_STR || h.kcls == GK_LONG) id += h.kbytes;
-                else if (h.kcls == GK_COMP) id += std::to_string(h.kw0) + "/" + std::to_string(h.kw1);
-                else id += std::to_string(h.kw0);
+                else if (h.kcls == GK_COMP) { id.append((const char*)&h.kw0, 8); id.append((const char*)&h.kw1, 8); }
+                else id.append((const char*)&h.kw0, 8);
                 for (uint32_t a = 0; a < nacc; a++)
                     if (mixed[a]) (void)split_of(h, (int)a);
                 auto it = where.find(id);
@@ -6125,13 +6140,30 @@ cq_table* cqgpu_merge_partials(cq_node* q, const void* const* blobs, const size_
                 h.vla_ok[v] = h.vn[v] > 0;
                 h.vla[v] = h.vn[v] > 0 ? sqrt(h.vm2[v] / h.vn[v]) : 0.0;
             }
-        std::stable_sort(merged.begin(), merged.end(),
-                         [](const HGroup& x, const HGroup& y) { return x.first < y.first; });
+        PHASE("merge groups");
+        {                                  // (by index: an HGroup is large to move)
+            std::vector<uint32_t> ord(merged.size());
+            for (size_t i = 0; i < ord.size(); i++) ord[i] = (uint32_t)i;
+            std::stable_sort(ord.begin(), ord.end(),
+                             [&](uint32_t x, uint32_t y) { return merged[x].first < merged[y].first; });
+            bool sorted = true;
+            for (size_t i = 0; i < ord.size() && sorted; i++) sorted = ord[i] == i;
+            if (!sorted) {
+                std::vector<HGroup> out;
+                out.reserve(merged.size());
+                for (uint32_t i : ord) out.push_back(std::move(merged[i]));
+                merged.swap(out);
+            }
+        }
+        PHASE("merge sort");
         Literals L;
         parse_literals(c, C.lits, L);
+        PHASE("merge literals");
         g_stats.groups = merged.size();
         cq_table* res = build_groups(C, merged, L, c);
+        PHASE("merge build");
         post_ops(c, res, q);
+        PHASE("merge post");
         g_stats.path = 1;
         return res;
     } catch (Ineligible& e) {
@@ -6977,89 +7009,114 @@ uint64_t typed_sample_kmin(const cqgpu_table* t, int kcol) {
     return kmin;
 }
 
-// the build side's records (the count pass: per window its record count, exclusive
-// scan -> each window's first record index); kept on the table (immutable)
-uint64_t typed_count(DevCtx& c, cqgpu_table* t, int kcol, int pcol) {
-    uint32_t ws;
-    int rp;
-    typed_stride(t, &ws, &rp);
-    if (t->typed_nrec != ~0ull && t->typed_ws == ws && t->typed_wbase) return t->typed_nrec;
-    const uint64_t nw = cq_jx_windows(t->data_begin, t->n, ws);
-    if (nw >= (1ull << 31)) throw Ineligible{"typed exchange: too many windows"};
-    DevBuf wc(std::max<uint64_t>(nw, 1) * 4), ctl(64);
-    std::unique_ptr<DevBuf> wb(new DevBuf(std::max<uint64_t>(nw, 1) * 4));
-    HIPCHECK(hipMemsetAsync(ctl.p, 0, 64, c.stream));
-    HIPCHECK(cq_jx_extract(t->g, t->data_begin, t->n, ws, (uint8_t)t->cfg.delimiter, (uint8_t)t->cfg.quote, kcol, pcol,
-                           1, 0, nullptr, nullptr, nullptr, wc.as<unsigned int>(), nullptr, 0, ctl.as<unsigned int>(),
-                           (unsigned long long*)(ctl.as<uint8_t>() + 16), c.ncu, c.stream));
-    uint64_t n = 0;
-    if (nw) {
-        size_t tb = 0;
-        HIPCHECK(cq_excl_sum_u32(nullptr, &tb, wc.as<unsigned int>(), wb->as<unsigned int>(), nw, c.stream));
-        DevBuf tmp(tb + 16);
-        HIPCHECK(cq_excl_sum_u32(tmp.p, &tb, wc.as<unsigned int>(), wb->as<unsigned int>(), nw, c.stream));
-        unsigned int tail[2] = {0, 0};
-        HIPCHECK(hipMemcpyAsync(&tail[0], wb->as<unsigned int>() + nw - 1, 4, hipMemcpyDeviceToHost, c.stream));
-        HIPCHECK(hipMemcpyAsync(&tail[1], wc.as<unsigned int>() + nw - 1, 4, hipMemcpyDeviceToHost, c.stream));
-        HIPCHECK(hipStreamSynchronize(c.stream));
-        n = (uint64_t)tail[0] + tail[1];
-    }
-    t->typed_nrec = n;
-    t->typed_ws = ws;
-    t->typed_wbase = std::move(wb);
-    return n;
-}
-
-// one side's entries into nranks regions (t->tsend); `cap` entries per region (0: an
-// estimate from the record count); flags as cq_jx_route's, plus 256 when a region was
-// too small (counts then hold the entries each region needed)
-void typed_send(DevCtx& c, cqgpu_table* t, bool build, int kcol, int pcol, int nranks, uint64_t qbase,
-                uint64_t gbase, uint64_t cap) {
-    uint32_t ws;
-    int rp;
-    typed_stride(t, &ws, &rp);
-    const unsigned int* wbase = nullptr;
-    uint64_t nrec = 0;
-    if (build) {
-        nrec = typed_count(c, t, kcol, pcol);
-        wbase = t->typed_wbase->as<unsigned int>();
-    } else {
-        const uint64_t nb = t->n > t->data_begin ? t->n - t->data_begin : 0;
-        nrec = (uint64_t)((double)nb / std::max(2.0, sample_record_bytes(t)) * 1.05) + 1;
-    }
-    if (!cap) cap = nrec / (uint64_t)nranks + nrec / (8 * (uint64_t)nranks) + 4096;
+// the count pass over one side (jx_extract_kernel ROUTE 1): per (destination, window)
+// the entries, their destination-major exclusive scan (every entry's region position
+// base) and per destination the entries; build: the records per window and their scan
+// (the global ids); flags 1 (a key the entries cannot carry: the CSV exchange), 8, 16
+TypedSend& typed_count_pass(DevCtx& c, cqgpu_table* t, bool build, int kcol, int N, uint64_t qbase) {
     std::unique_ptr<TypedSend> ts(new TypedSend);
-    ts->esize = build ? 16 : 8;
-    ts->cap = cap;
+    typed_stride(t, &ts->ws, &ts->rp);
+    ts->N = (uint32_t)N;
+    ts->qbase = qbase;
+    const uint64_t nw = cq_jx_windows(t->data_begin, t->n, ts->ws);
+    if (nw * (uint64_t)N >= (1ull << 31)) throw Ineligible{"typed exchange: too many windows"};
+    ts->nwin = nw;
+    const uint64_t nn = std::max<uint64_t>(nw * (uint64_t)N, 1);
     {
-        DevBuf e((size_t)nranks * cap * ts->esize + 16);
-        std::swap(ts->ent.p, e.p);
+        DevBuf a(nn * 4), b(nn * 4 + 16);
+        std::swap(ts->rcnt.p, a.p);
+        std::swap(ts->roffs.p, b.p);
+        if (build) {
+            DevBuf x(std::max<uint64_t>(nw, 1) * 4), y(std::max<uint64_t>(nw, 1) * 4 + 16);
+            std::swap(ts->wcount.p, x.p);
+            std::swap(ts->wbase.p, y.p);
+        }
     }
-    DevBuf ctl(64 + (size_t)nranks * 8);
+    DevBuf ctl(64);
     unsigned int* flag = ctl.as<unsigned int>();
     unsigned long long* kr = (unsigned long long*)(ctl.as<uint8_t>() + 16);
-    unsigned long long* rc = (unsigned long long*)(ctl.as<uint8_t>() + 64);
-    HIPCHECK(hipMemsetAsync(ctl.p, 0, 64 + (size_t)nranks * 8, c.stream));
+    HIPCHECK(hipMemsetAsync(ctl.p, 0, 64, c.stream));
     HIPCHECK(hipMemsetAsync(kr, 0xff, 8, c.stream));
-    HIPCHECK(cq_jx_route(t->g, t->data_begin, t->n, ws, (uint8_t)t->cfg.delimiter, (uint8_t)t->cfg.quote, kcol, pcol,
-                         build ? 1 : 0, rp, wbase, (uint32_t)nranks, qbase, gbase, ts->ent.p, cap, rc, flag, kr, c.ncu,
+    if (!nw) HIPCHECK(hipMemsetAsync(ts->rcnt.p, 0, nn * 4, c.stream));
+    HIPCHECK(cq_jx_route(t->g, t->data_begin, t->n, ts->ws, (uint8_t)t->cfg.delimiter, (uint8_t)t->cfg.quote, kcol, -1,
+                         build ? 1 : 0, ts->rp, 1, (uint32_t)N, qbase, 0, ts->rcnt.as<unsigned int>(),
+                         build ? ts->wcount.as<unsigned int>() : nullptr, nullptr, nullptr, nullptr, flag, kr, c.ncu,
                          c.stream));
-    std::vector<uint8_t> h(64 + (size_t)nranks * 8);
-    HIPCHECK(hipMemcpyAsync(h.data(), ctl.p, h.size(), hipMemcpyDeviceToHost, c.stream));
+    size_t tb = 0;
+    HIPCHECK(cq_excl_sum_u32(nullptr, &tb, ts->rcnt.as<unsigned int>(), ts->roffs.as<unsigned int>(), nn, c.stream));
+    if (build && nw) {
+        size_t tb2 = 0;
+        HIPCHECK(cq_excl_sum_u32(nullptr, &tb2, ts->wcount.as<unsigned int>(), ts->wbase.as<unsigned int>(), nw, c.stream));
+        tb = std::max(tb, tb2);
+    }
+    DevBuf tmp(tb + 16);
+    HIPCHECK(cq_excl_sum_u32(tmp.p, &tb, ts->rcnt.as<unsigned int>(), ts->roffs.as<unsigned int>(), nn, c.stream));
+    if (build && nw)
+        HIPCHECK(cq_excl_sum_u32(tmp.p, &tb, ts->wcount.as<unsigned int>(), ts->wbase.as<unsigned int>(), nw, c.stream));
+    // back to the host: every destination's first position (a strided copy), the totals,
+    // the flags and the key range
+    uint8_t* h = (uint8_t*)pinned(c, 64 + 8 * (size_t)N + 32);
+    uint32_t* hstart = (uint32_t*)(h + 64);
+    uint32_t* htail = hstart + N;                    // [0] last roffs, [1] last rcnt, [2] last wbase, [3] last wcount
+    if (nw) {
+        HIPCHECK(hipMemcpy2DAsync(hstart, 4, ts->roffs.p, nw * 4, 4, (size_t)N, hipMemcpyDeviceToHost, c.stream));
+        HIPCHECK(hipMemcpyAsync(htail, ts->roffs.as<unsigned int>() + nn - 1, 4, hipMemcpyDeviceToHost, c.stream));
+        HIPCHECK(hipMemcpyAsync(htail + 1, ts->rcnt.as<unsigned int>() + nn - 1, 4, hipMemcpyDeviceToHost, c.stream));
+        if (build) {
+            HIPCHECK(hipMemcpyAsync(htail + 2, ts->wbase.as<unsigned int>() + nw - 1, 4, hipMemcpyDeviceToHost, c.stream));
+            HIPCHECK(hipMemcpyAsync(htail + 3, ts->wcount.as<unsigned int>() + nw - 1, 4, hipMemcpyDeviceToHost, c.stream));
+        }
+    }
+    HIPCHECK(hipMemcpyAsync(h, ctl.p, 32, hipMemcpyDeviceToHost, c.stream));
     HIPCHECK(hipStreamSynchronize(c.stream));
-    memcpy(&ts->flags, h.data(), 4);
-    memcpy(ts->krange, h.data() + 16, 16);
-    ts->counts.assign(nranks, 0);
-    memcpy(ts->counts.data(), h.data() + 64, (size_t)nranks * 8);
-    for (uint64_t x : ts->counts)
-        if (x > cap) ts->flags |= 256u;
+    memcpy(&ts->flags, h, 4);
+    memcpy(ts->krange, h + 16, 16);
+    ts->rstart.assign((size_t)N + 1, 0);
+    ts->counts.assign(N, 0);
+    if (nw) {
+        for (int d = 0; d < N; d++) ts->rstart[d] = hstart[d];
+        ts->rstart[N] = (uint64_t)htail[0] + htail[1];
+        ts->nrec = build ? (uint64_t)htail[2] + htail[3] : 0;
+    }
+    for (int d = 0; d < N; d++) ts->counts[d] = ts->rstart[d + 1] - ts->rstart[d];
     t->tsend = std::move(ts);
+    return *t->tsend;
+}
+
+// the emit pass (jx_extract_kernel ROUTE 2) after typed_count_pass: every entry at its
+// position; flags 1 (a payload the entries cannot carry), 512
+uint32_t typed_emit_pass(DevCtx& c, cqgpu_table* t, bool build, int kcol, int pcol, uint64_t gbase) {
+    if (!t->tsend) throw HipError{"typed exchange: send without a count"};
+    TypedSend& ts = *t->tsend;
+    ts.esize = build ? 16 : 8;
+    const uint64_t total = ts.rstart[ts.N];
+    {
+        DevBuf e(std::max<uint64_t>(total, 1) * ts.esize + 16);
+        std::swap(ts.ent.p, e.p);
+    }
+    DevBuf ctl(64);
+    unsigned int* flag = ctl.as<unsigned int>();
+    unsigned long long* kr = (unsigned long long*)(ctl.as<uint8_t>() + 16);
+    HIPCHECK(hipMemsetAsync(ctl.p, 0, 64, c.stream));
+    HIPCHECK(cq_jx_route(t->g, t->data_begin, t->n, ts.ws, (uint8_t)t->cfg.delimiter, (uint8_t)t->cfg.quote, kcol, pcol,
+                         build ? 1 : 0, ts.rp, 2, ts.N, ts.qbase, gbase, nullptr, nullptr, ts.roffs.as<unsigned int>(),
+                         build ? ts.wbase.as<unsigned int>() : nullptr, ts.ent.p, flag, kr, c.ncu, c.stream));
+    uint32_t* h = (uint32_t*)pinned(c, 16);
+    HIPCHECK(hipMemcpyAsync(h, flag, 4, hipMemcpyDeviceToHost, c.stream));
+    HIPCHECK(hipStreamSynchronize(c.stream));
+    ts.emitted = true;
+    ts.flags |= h[0];
+    return h[0];
 }
 
 // the receiving rank: STAR over the entries -> this rank's groups in `part`; returns
 // the flags (0: done; 16 / 32 / 64: the entries do not fit the STAR form)
 uint32_t typed_receive(DevCtx& c, const TypedJoin& tj, const void* ub, uint64_t nu, const void* ob, uint64_t no,
                        uint64_t qoff, uint64_t range, JoinPartial& part) {
+    PhaseClock pc;
+    PhaseClock* const outer_phase = g_phase;
+    g_phase = &pc;
+    struct Unset { PhaseClock* o; ~Unset() { g_phase = o; } } unset_{outer_phase};
     const uint32_t G = cq_jx_star_groups();
     const bool grouped = tj.gcol >= 0;
     if (range >= (1ull << 31) || qoff >= (1ull << 32)) return 16u;
@@ -7084,10 +7141,12 @@ uint32_t typed_receive(DevCtx& c, const TypedJoin& tj, const void* ub, uint64_t 
     HIPCHECK(cq_jx_star_first(d16.as<uint16_t>(), l32.as<uint32_t>(), range, notmono, gfirst, cnts + 2, c.ncu * 4,
                               c.stream));
     HIPCHECK(hipEventRecord(c.ev1, c.stream));
+    PHASE("typed launch");
     std::vector<uint8_t> h(o_ctl + 64);
     uint8_t* hp = (uint8_t*)pinned(c, h.size());
     HIPCHECK(hipMemcpyAsync(hp, small.p, h.size(), hipMemcpyDeviceToHost, c.stream));
     HIPCHECK(hipStreamSynchronize(c.stream));
+    PHASE("typed kernels");
     memcpy(h.data(), hp, h.size());
     float ms = 0;
     HIPCHECK(hipEventElapsedTime(&ms, c.ev0, c.ev1));
@@ -7107,6 +7166,8 @@ uint32_t typed_receive(DevCtx& c, const TypedJoin& tj, const void* ub, uint64_t 
     const int nacc = tj.C.P.nacc;
     const uint32_t nrep = (uint32_t)tj.C.rep_cols.size();
     std::vector<HGroup> groups;
+    groups.reserve(G);
+    std::map<std::tuple<uint64_t, uint64_t, uint64_t>, size_t> at;
     auto fill = [&](HGroup& x, uint32_t s) {
         x.cnt = hs[3 * s];
         x.first = hf[s] == ~0u ? NOPOS : ((unsigned long long)hf[s] << 32);
@@ -7147,10 +7208,14 @@ uint32_t typed_receive(DevCtx& c, const TypedJoin& tj, const void* ub, uint64_t 
         }
         // raw tags of one canonical key (e.g. "1.0" and "1.00") are one group: counts and
         // sums add, the first pair is the smaller, its row gives the representative cells
-        HGroup* same = nullptr;
-        for (HGroup& y : groups)
-            if (y.kcls == x.kcls && y.klen == x.klen && y.kw0 == x.kw0 && y.kw1 == x.kw1) { same = &y; break; }
-        if (!same) { groups.push_back(std::move(x)); continue; }
+        const auto kk = std::make_tuple((uint64_t)x.kcls << 32 | x.klen, x.kw0, x.kw1);
+        auto it = at.find(kk);
+        if (it == at.end()) {
+            at.emplace(kk, groups.size());
+            groups.push_back(std::move(x));
+            continue;
+        }
+        HGroup* same = &groups[it->second];
         same->cnt += x.cnt;
         for (int a = 0; a < nacc; a++) { same->sum[a] += x.sum[a]; same->num[a] += x.num[a]; }
         if (x.first < same->first) { same->first = x.first; same->reps = x.reps; }
@@ -7164,6 +7229,7 @@ uint32_t typed_receive(DevCtx& c, const TypedJoin& tj, const void* ub, uint64_t 
     part.lmask |= nu ? 2u : 0u;                                    // (canonical INTEGER keys: numbers)
     part.rmask |= no ? 2u : 0u;
     g_stats.groups = part.groups.size();
+    PHASE("typed groups");
     return 0;
 }
 
@@ -7190,14 +7256,21 @@ uint64_t cqgpu_typed_sample_kmin(cq_node* q, cqgpu_table* const* tables, int nta
     return tables[0]->n > tables[0]->data_begin ? typed_sample_kmin(tables[0], tj.kl) : ~0ull;
 }
 
-int64_t cqgpu_typed_count(cq_node* q, cqgpu_table* const* tables, int ntables) {
+int64_t cqgpu_typed_count(cq_node* q, cqgpu_table* const* tables, int ntables, int side, int nranks, uint64_t qbase,
+                          uint64_t* counts, uint64_t* krange, uint32_t* flags) {
     g_err.clear();
     try {
         TypedJoin tj;
         std::string why;
-        if (ntables != 2 || !typed_join_plan(q, tables[0], tables[1], tj, why)) throw Ineligible{"typed exchange: " + why};
+        if (ntables != 2 || (side != 0 && side != 1) || nranks < 1 || nranks > 64 ||
+            !typed_join_plan(q, tables[0], tables[1], tj, why))
+            throw Ineligible{"typed exchange: " + why};
         DevCtx& c = ctx();
-        return (int64_t)typed_count(c, tables[0], tj.kl, tj.gcol);
+        const TypedSend& ts = typed_count_pass(c, tables[side], side == 0, side == 0 ? tj.kl : tj.kr, nranks, qbase);
+        for (int d = 0; d < nranks; d++) if (counts) counts[d] = ts.counts[d];
+        if (krange) { krange[0] = ts.krange[0]; krange[1] = ts.krange[1]; }
+        if (flags) *flags = ts.flags;
+        return (int64_t)(side == 0 ? ts.nrec : ts.rstart[nranks]);
     } catch (Ineligible& e) {
         g_inel = e.why;
         set_err("cq_amd: %s", e.why.c_str());
@@ -7209,22 +7282,17 @@ int64_t cqgpu_typed_count(cq_node* q, cqgpu_table* const* tables, int ntables) {
     return -1;
 }
 
-int cqgpu_typed_send(cq_node* q, cqgpu_table* const* tables, int ntables, int side, int nranks, uint64_t qbase,
-                     uint64_t gid_base, uint64_t cap, uint64_t* counts, uint64_t* krange, uint32_t* flags) {
+int cqgpu_typed_send(cq_node* q, cqgpu_table* const* tables, int ntables, int side, uint64_t gid_base, uint32_t* flags) {
     g_err.clear();
     try {
         TypedJoin tj;
         std::string why;
-        if (ntables != 2 || (side != 0 && side != 1) || nranks < 1 || nranks > 64 ||
-            !typed_join_plan(q, tables[0], tables[1], tj, why))
+        if (ntables != 2 || (side != 0 && side != 1) || !typed_join_plan(q, tables[0], tables[1], tj, why))
             throw Ineligible{"typed exchange: " + why};
         DevCtx& c = ctx();
-        cqgpu_table* t = tables[side];
-        typed_send(c, t, side == 0, side == 0 ? tj.kl : tj.kr, side == 0 ? tj.gcol : tj.vcol, nranks, qbase, gid_base,
-                   cap);
-        for (int d = 0; d < nranks; d++) counts[d] = t->tsend->counts[d];
-        if (krange) { krange[0] = t->tsend->krange[0]; krange[1] = t->tsend->krange[1]; }
-        if (flags) *flags = t->tsend->flags;
+        const uint32_t f = typed_emit_pass(c, tables[side], side == 0, side == 0 ? tj.kl : tj.kr,
+                                           side == 0 ? tj.gcol : tj.vcol, gid_base);
+        if (flags) *flags = f;
         return 0;
     } catch (Ineligible& e) {
         g_inel = e.why;
@@ -7238,19 +7306,15 @@ int cqgpu_typed_send(cq_node* q, cqgpu_table* const* tables, int ntables, int si
 }
 
 void cqgpu_typed_reset(cqgpu_table* t) {
-    if (!t) return;
-    t->tsend.reset();
-    t->typed_nrec = ~0ull;
-    t->typed_ws = 0;
-    t->typed_wbase.reset();
+    if (t) t->tsend.reset();
 }
 
 const void* cqgpu_typed_region(const cqgpu_table* t, int dest, uint64_t* entries, uint64_t* entry_bytes) {
-    if (!t || !t->tsend || dest < 0 || (size_t)dest >= t->tsend->counts.size()) return nullptr;
+    if (!t || !t->tsend || !t->tsend->emitted || dest < 0 || (uint32_t)dest >= t->tsend->N) return nullptr;
     const TypedSend& ts = *t->tsend;
-    if (entries) *entries = std::min(ts.counts[dest], ts.cap);
+    if (entries) *entries = ts.counts[dest];
     if (entry_bytes) *entry_bytes = ts.esize;
-    return ts.ent.as<uint8_t>() + (size_t)dest * ts.cap * ts.esize;
+    return ts.ent.as<uint8_t>() + ts.rstart[dest] * ts.esize;
 }
 
 int64_t cqgpu_typed_gather(cqgpu_table* const* senders, int nsenders, int dest, void* dev_out, uint64_t cap_entries) {
@@ -7981,113 +8045,99 @@ bool dist_join_typed(DevCtx& c, DistComm& m, cq_node* q, cqgpu_table* const* tab
     TypedJoin tj;
     std::string why;
     if (!typed_join_plan(q, tables[0], tables[1], tj, why)) return false;   // (the plan: the same everywhere)
+    struct Drop {
+        cqgpu_table* const* t;
+        ~Drop() { t[0]->tsend.reset(); t[1]->tsend.reset(); }
+    } drop_{tables};
     std::string err;
     bool bad = false;
-    uint64_t nrec = 0;
-    try {
-        nrec = typed_count(c, tables[0], tj.kl, tj.gcol);
-    } catch (HipError& e) { bad = true; err = e.msg; } catch (Ineligible& e) { bad = true; err = e.why; }
-    (void)hipGetLastError();
-    // every rank's record count (the global ids' bases) and failure flag
-    // every rank's record count (the global ids' bases), sampled key minimum, failure flag
-    std::vector<uint64_t> all(3 * (size_t)N, 0);
-    {
-        DevBuf dc(24 * ((size_t)N + 1));
-        uint64_t mine[3] = {nrec, tables[0]->n > tables[0]->data_begin ? typed_sample_kmin(tables[0], tj.kl) : ~0ull,
-                            bad ? 1ull : 0ull};
-        HIPCHECK(hipMemcpyAsync(dc.as<uint8_t>() + 24 * N, mine, 24, hipMemcpyHostToDevice, c.stream));
-        m.be->all_gather(dc.as<uint8_t>() + 24 * N, dc.p, 3, CD_U64, c.stream);
-        HIPCHECK(hipMemcpyAsync(all.data(), dc.p, 24 * (size_t)N, hipMemcpyDeviceToHost, c.stream));
+    auto gather_words = [&](const std::vector<uint64_t>& mine, std::vector<uint64_t>& all) {
+        const size_t W = mine.size();
+        all.assign(W * (size_t)N, 0);
+        DevBuf dc(W * 8 * ((size_t)N + 1));
+        HIPCHECK(hipMemcpyAsync(dc.as<uint8_t>() + W * 8 * N, mine.data(), W * 8, hipMemcpyHostToDevice, c.stream));
+        m.be->all_gather(dc.as<uint8_t>() + W * 8 * N, dc.p, W, CD_U64, c.stream);
+        HIPCHECK(hipMemcpyAsync(all.data(), dc.p, W * 8 * N, hipMemcpyDeviceToHost, c.stream));
         HIPCHECK(hipStreamSynchronize(c.stream));
-    }
-    uint64_t gbase = 0, total = 0, smin = ~0ull;
-    for (int r = 0; r < N; r++) {
-        if (all[3 * r + 2]) throw PeerFail{bad ? err : std::string("a peer rank failed")};
-        if (r < m.rank) gbase += all[3 * r];
-        total += all[3 * r];
-        smin = std::min(smin, all[3 * r + 1]);
-    }
-    if (total >= (1ull << 32)) return false;
-    uint64_t qbase = smin == ~0ull ? 0 : smin / (uint64_t)N, cap_u = 0, cap_o = 0;
-    // per rank: counts_u[N], counts_o[N], flags, kmin, kmax, bad
-    const size_t W = 2 * (size_t)N + 4;
-    std::vector<uint64_t> g(W * N, 0);
+    };
+    // the first qbase: the ranks' sampled build keys' minimum / N
+    std::vector<uint64_t> g;
+    gather_words({tables[0]->n > tables[0]->data_begin ? typed_sample_kmin(tables[0], tj.kl) : ~0ull}, g);
+    uint64_t smin = ~0ull;
+    for (int r = 0; r < N; r++) smin = std::min(smin, g[r]);
+    uint64_t qbase = smin == ~0ull ? 0 : smin / (uint64_t)N;
+    // count passes: per rank [counts_u[N], counts_o[N], flags, kmin, kmax, records, bad]
+    const size_t W = 2 * (size_t)N + 5;
     for (int attempt = 0;; attempt++) {
         std::vector<uint64_t> mine(W, 0);
         try {
             if (getenv("CQGPU_TEST_TYPED_FAIL"))                 // test knob: this rank's send fails
                 throw HipError{"dist_join: injected typed-exchange failure (CQGPU_TEST_TYPED_FAIL)"};
-            typed_send(c, tables[0], true, tj.kl, tj.gcol, N, qbase, gbase, cap_u);
-            typed_send(c, tables[1], false, tj.kr, tj.vcol, N, qbase, 0, cap_o);
-            const TypedSend &su = *tables[0]->tsend, &so = *tables[1]->tsend;
+            const TypedSend& su = typed_count_pass(c, tables[0], true, tj.kl, N, qbase);
+            const TypedSend& so = typed_count_pass(c, tables[1], false, tj.kr, N, qbase);
             for (int d = 0; d < N; d++) { mine[d] = su.counts[d]; mine[N + d] = so.counts[d]; }
             mine[2 * N] = su.flags | so.flags;
             mine[2 * N + 1] = su.krange[0];
             mine[2 * N + 2] = su.krange[1];
+            mine[2 * N + 3] = su.nrec;
         } catch (HipError& e) { bad = true; err = e.msg; } catch (Ineligible& e) { bad = true; err = e.why; }
         (void)hipGetLastError();
-        mine[2 * N + 3] = bad ? 1 : 0;
-        {
-            DevBuf dc(W * 8 * ((size_t)N + 1));
-            HIPCHECK(hipMemcpyAsync(dc.as<uint8_t>() + W * 8 * N, mine.data(), W * 8, hipMemcpyHostToDevice, c.stream));
-            m.be->all_gather(dc.as<uint8_t>() + W * 8 * N, dc.p, W, CD_U64, c.stream);
-            HIPCHECK(hipMemcpyAsync(g.data(), dc.p, W * 8 * N, hipMemcpyDeviceToHost, c.stream));
-            HIPCHECK(hipStreamSynchronize(c.stream));
-        }
-        uint64_t flags = 0, kmin = ~0ull, kmax = 0, need_u = 0, need_o = 0;
+        mine[2 * N + 4] = bad ? 1 : 0;
+        gather_words(mine, g);
+        uint64_t flags = 0, kmin = ~0ull;
         for (int r = 0; r < N; r++) {
             const uint64_t* x = g.data() + W * r;
-            if (x[2 * N + 3]) {
-                tables[0]->tsend.reset();
-                tables[1]->tsend.reset();
-                throw PeerFail{bad ? err : std::string("a peer rank failed")};
-            }
+            if (x[2 * N + 4]) throw PeerFail{bad ? err : std::string("a peer rank failed")};
             flags |= x[2 * N];
             kmin = std::min(kmin, x[2 * N + 1]);
-            kmax = std::max(kmax, x[2 * N + 2]);
-            for (int d = 0; d < N; d++) { need_u = std::max(need_u, x[d]); need_o = std::max(need_o, x[N + d]); }
         }
-        if ((flags & (1u | 8u | 512u)) || attempt == 2) {          // not typable: every rank to the CSV exchange
-            tables[0]->tsend.reset();
-            tables[1]->tsend.reset();
-            return false;
-        }
-        if (flags & (16u | 256u)) {
-            if (flags & 16u) qbase = kmin / (uint64_t)N;
-            if (flags & 256u) { cap_u = need_u; cap_o = need_o; }
+        if ((flags & (1u | 8u)) || ((flags & 16u) && attempt >= 1)) return false;   // every rank to the CSV exchange
+        if (flags & 16u) {                                        // again with the build keys' own minimum
+            qbase = kmin / (uint64_t)N;
             continue;
         }
-        if (kmin > kmax) kmin = kmax = qbase * (uint64_t)N;            // no build keys anywhere
         break;
     }
-    uint64_t kmin = ~0ull, kmax = 0;
+    uint64_t kmin = ~0ull, kmax = 0, gbase = 0, total = 0;
     std::vector<uint64_t> recv_u(N, 0), recv_o(N, 0);
     for (int r = 0; r < N; r++) {
         const uint64_t* x = g.data() + W * r;
         kmin = std::min(kmin, x[2 * N + 1]);
         kmax = std::max(kmax, x[2 * N + 2]);
+        if (r < m.rank) gbase += x[2 * N + 3];
+        total += x[2 * N + 3];
         for (int d = 0; d < N; d++) { recv_u[d] += x[d]; recv_o[d] += x[N + d]; }
     }
-    if (kmin > kmax) kmin = kmax = qbase * (uint64_t)N;
+    if (total >= (1ull << 32)) return false;
+    if (kmin > kmax) kmin = kmax = qbase * (uint64_t)N;            // no build keys anywhere
     const uint64_t qoff = kmin / (uint64_t)N - qbase, range = kmax / (uint64_t)N - kmin / (uint64_t)N + 1;
-    if (range > 4 * *std::min_element(recv_u.begin(), recv_u.end()) + 1024 || range >= (1ull << 31)) {
-        tables[0]->tsend.reset();
-        tables[1]->tsend.reset();
+    if (range > 4 * *std::min_element(recv_u.begin(), recv_u.end()) + 1024 || range >= (1ull << 31))
         return false;                                             // not a dense key range on every rank
-    }
-    // the entries: region d of every rank to rank d, in one grouped send / recv per side
+    // emit passes, then one agreement on their flags (a GROUP BY value or a payload the
+    // entries cannot carry: every rank to the CSV exchange) and on failures
+    uint32_t ef = 0;
     DevBuf ru, ro;
     try {
+        ef |= typed_emit_pass(c, tables[0], true, tj.kl, tj.gcol, gbase);
+        ef |= typed_emit_pass(c, tables[1], false, tj.kr, tj.vcol, 0);
         DevBuf a(std::max<uint64_t>(recv_u[m.rank], 1) * 16), b(std::max<uint64_t>(recv_o[m.rank], 1) * 8);
         std::swap(ru.p, a.p);
         std::swap(ro.p, b.p);
     } catch (HipError& e) { bad = true; err = e.msg; }
     (void)hipGetLastError();
-    if (agree_any(c, m, bad)) {
-        tables[0]->tsend.reset();
-        tables[1]->tsend.reset();
-        throw PeerFail{bad ? err : std::string("a peer rank failed")};
+    {
+        DistBufs& b = dist_bufs();
+        b.hword[0] = bad ? 1u : 0u;
+        b.hword[1] = ef ? 1u : 0u;
+        uint32_t* dw = b.word.as<uint32_t>() + 8;
+        HIPCHECK(hipMemcpyAsync(dw, b.hword, 8, hipMemcpyHostToDevice, c.stream));
+        m.be->all_reduce(dw, 2, CD_U32, CR_MAX, c.stream);
+        HIPCHECK(hipMemcpyAsync(b.hword + 4, dw, 8, hipMemcpyDeviceToHost, c.stream));
+        HIPCHECK(hipStreamSynchronize(c.stream));
+        if (b.hword[4]) throw PeerFail{bad ? err : std::string("a peer rank failed")};
+        if (b.hword[5]) return false;
     }
+    // the entries: region d of every rank to rank d, in one grouped send / recv per side
     for (int side = 0; side < 2; side++) {
         const TypedSend& ts = *tables[side]->tsend;
         uint8_t* rb = side == 0 ? ru.as<uint8_t>() : ro.as<uint8_t>();
@@ -8095,7 +8145,7 @@ bool dist_join_typed(DevCtx& c, DistComm& m, cq_node* q, cqgpu_table* const* tab
         uint64_t at = 0;
         for (int d = 0; d < N; d++) {
             const uint64_t ns = ts.counts[d];
-            if (ns) m.be->send(ts.ent.as<uint8_t>() + (size_t)d * ts.cap * ts.esize, ns * ts.esize, CD_U8, d, c.stream);
+            if (ns) m.be->send(ts.ent.as<uint8_t>() + ts.rstart[d] * ts.esize, ns * ts.esize, CD_U8, d, c.stream);
             const uint64_t nr = g[W * d + (size_t)side * N + m.rank];          // from source d
             if (nr) m.be->recv(rb + at * ts.esize, nr * ts.esize, CD_U8, d, c.stream);
             at += nr;

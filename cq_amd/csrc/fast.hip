@@ -1430,18 +1430,21 @@ struct JxOut {
     uint32_t* pcnt;
     uint32_t np, pcap, psh;
     // ROUTE (the typed exchange of the multi-GPU join): every
-    // record with a non-NULL key goes to rank key mod rn as one fixed-size entry in that
-    // destination's region of rent (rcap entries each, filled in no particular order):
+    // record with a non-NULL key goes to rank key mod rn as one fixed-size entry:
     //   BUILD  uint4 {q32, gid, tag lo, tag hi}: q32 = key / rn - qbase, gid = gbase +
     //          the record's index in this table (file order), tag = the GROUP BY bytes
     //   PROBE  uint2 {q32, pay}: pay = the SUM argument in 10^-3 units (JX_PNULL: NULL)
+    // Two passes, no atomics: ROUTE 1 counts per window i and destination d the entries
+    // (rcnt[d * nwin + i]; BUILD: the window's records into wcount as well); the host
+    // scans rcnt destination-major (roffs), so destination d's entries fill
+    // [roffs[d * nwin], roffs[(d + 1) * nwin]) of rent with no hole; ROUTE 2 writes
+    // each entry at roffs[d * nwin + i] + its rank among the window's entries for d.
     // Flags: 8 a NULL build key, 16 a build q32 outside [0, 2^32 - 1) (the host retries
-    // with the keys' own minimum), 256 a region full (retried with exact capacities),
-    // 512 a payload outside 31 bits.  A probe key outside the window matches no build
-    // key and is not sent.
+    // with the keys' own minimum), 512 a payload outside 31 bits.  A probe key outside
+    // the window matches no build key and is not sent.
     void* rent;
-    unsigned long long* rcount;   // per destination: entries reserved
-    uint64_t rcap;
+    unsigned int* rcnt;           // ROUTE 1
+    const unsigned int* roffs;    // ROUTE 2
     uint64_t rmagic;              // ceil(2^64 / rn) (rn > 1): key / rn = mulhi(key, rmagic) for keys < 2^58
     uint64_t qbase, gbase;
     uint32_t rn;
@@ -1590,9 +1593,9 @@ __device__ __forceinline__ bool jx_key(uint32_t d0, uint32_t d1, uint32_t d2, ui
 }
 
 template <bool BUILD, bool COMMA, int NR, bool COUNT, bool STAR = false, int RP = 2, bool PART = false,
-          bool ROUTE = false>
+          int ROUTE = 0>
 __global__ __launch_bounds__(LT) void jx_extract_kernel(const uint8_t* __restrict__ g, const JxPlan jp, const JxOut jo) {
-    static_assert(!ROUTE || (!STAR && !COUNT), "ROUTE: the emit pass of the record form");
+    static_assert(ROUTE == 0 || (!STAR && !COUNT), "ROUTE: the record form's passes");
     extern __shared__ __align__(16) uint8_t smem[];
     WaveLds* waves = (WaveLds*)smem;
     // STAR probe: per group id COUNT / fixed-point SUM / SUM count of this block;
@@ -1719,7 +1722,16 @@ __global__ __launch_bounds__(LT) void jx_extract_kernel(const uint8_t* __restric
         // record j of this lane in this window lands at wbase[i] + (the lanes below's
         // records) + j: file order
         const uint32_t nmine = (uint32_t)__popcll(todo);
-        uint32_t at_next = (STAR || (ROUTE && !BUILD)) ? 0u : jo.wbase[i] + wave_incl_scan(nmine) - nmine;
+        uint32_t at_next = (STAR || ROUTE == 1 || (ROUTE == 2 && !BUILD)) ? 0u
+                                                                         : jo.wbase[i] + wave_incl_scan(nmine) - nmine;
+        // ROUTE: lane d (< rn) holds destination d's entries of this window so far, and
+        // (emit) its first position
+        uint32_t rrun = 0, rbase = 0;
+        if constexpr (ROUTE == 2) rbase = (uint32_t)lane < jo.rn ? jo.roffs[(uint64_t)lane * nwin + i] : 0u;
+        if constexpr (ROUTE == 1 && BUILD) {
+            const uint32_t tot = __builtin_amdgcn_readlane(wave_incl_scan(nmine), 63);
+            if (lane == 0) jo.wcount[i] = tot;
+        }
         bool issued = false;
         // STAR build: this lane's first and last key (its records come in file order),
         // as slots: keys map to slots monotonically, and a key outside the range flags
@@ -1923,40 +1935,40 @@ __global__ __launch_bounds__(LT) void jx_extract_kernel(const uint8_t* __restric
                         }
                     }
                 }
-            } else if constexpr (ROUTE) {
-                // destination and q32 of each record, then per destination one wave-wide
-                // reservation in its region (ballots; one atomic per destination present)
+            } else if constexpr (ROUTE != 0) {
+                // destination and q32 of each record, then per destination its entries'
+                // ranks in the window (ballots; the count pass and the emit pass decide
+                // `take` alike -- a record either pass fails flags the whole exchange)
                 uint32_t dd[RP], q32[RP], gid[RP];
                 bool take[RP];
-                uint64_t pos[RP];
 #pragma unroll
                 for (int u = 0; u < RP; u++) {
                     gid[u] = valid[u] ? (uint32_t)(jo.gbase + at_next) : 0u;
                     at_next += valid[u] ? 1u : 0u;
                     const unsigned long long k = key[u];
                     take[u] = valid[u] && !fail[u] && k != JX_NULLKEY;
-                    if (BUILD && valid[u] && !fail[u] && k == JX_NULLKEY) sflag |= 8u;
+                    if (ROUTE == 1 && BUILD && valid[u] && !fail[u] && k == JX_NULLKEY) sflag |= 8u;
                     const unsigned long long q = jo.rn > 1u ? __umul64hi(k, jo.rmagic) : k;
                     dd[u] = (uint32_t)(k - q * jo.rn);
                     const unsigned long long qq = q - jo.qbase;
                     q32[u] = (uint32_t)qq;
-                    if (BUILD && take[u]) {                       // (every build key: a retry's window)
+                    if (ROUTE == 1 && BUILD && take[u]) {          // (every build key: a retry's window)
                         kmin = k < kmin ? k : kmin;
                         kmax = k > kmax ? k : kmax;
                     }
                     if (take[u] && (q < jo.qbase || qq >= 0xFFFFFFFFull)) {
                         take[u] = false;                          // (probe: matches no build key)
-                        if (BUILD) sflag |= 16u;
+                        if (ROUTE == 1 && BUILD) sflag |= 16u;
                     }
-                    if (!BUILD && take[u] && pay[u] != JX_NOVAL &&
-                        ((long long)pay[u] < -2147483647ll || (long long)pay[u] > 2147483647ll)) {
-                        sflag |= 512u;
-                        take[u] = false;
-                    }
-                    pos[u] = ~0ull;
+                    if (ROUTE == 2 && !BUILD && take[u] && pay[u] != JX_NOVAL &&
+                        ((long long)pay[u] < -2147483647ll || (long long)pay[u] > 2147483647ll))
+                        sflag |= 512u;                            // (still written: the flag drops the exchange)
                 }
                 const uint32_t nd = __builtin_amdgcn_readfirstlane(jo.rn);
                 const uint64_t lt = lane ? (~0ull >> (64 - lane)) : 0ull;
+                uint32_t pos[RP];
+#pragma unroll
+                for (int u = 0; u < RP; u++) pos[u] = 0;
                 for (uint32_t d = 0; d < nd; d++) {
                     uint64_t m[RP];
                     uint32_t tot = 0;
@@ -1966,26 +1978,26 @@ __global__ __launch_bounds__(LT) void jx_extract_kernel(const uint8_t* __restric
                         tot += (uint32_t)__popcll(m[u]);
                     }
                     if (tot == 0) continue;
-                    unsigned long long base = 0;
-                    if (lane == 0) base = atomicAdd(&jo.rcount[d], (unsigned long long)tot);
-                    base = __shfl(base, 0, 64);
-                    uint32_t pre = 0;
+                    if constexpr (ROUTE == 2) {
+                        uint32_t pre = __builtin_amdgcn_readlane(rbase, d) + __builtin_amdgcn_readlane(rrun, d);
+#pragma unroll
+                        for (int u = 0; u < RP; u++) {
+                            if ((m[u] >> lane) & 1ull) pos[u] = pre + (uint32_t)__popcll(m[u] & lt);
+                            pre += (uint32_t)__popcll(m[u]);
+                        }
+                    }
+                    rrun += (uint32_t)lane == d ? tot : 0u;
+                }
+                if constexpr (ROUTE == 2) {
 #pragma unroll
                     for (int u = 0; u < RP; u++) {
-                        if ((m[u] >> lane) & 1ull) pos[u] = base + pre + (uint32_t)__popcll(m[u] & lt);
-                        pre += (uint32_t)__popcll(m[u]);
-                    }
-                }
-#pragma unroll
-                for (int u = 0; u < RP; u++) {
-                    if (!take[u]) continue;
-                    if (pos[u] >= jo.rcap) { sflag |= 256u; continue; }
-                    const uint64_t at = (uint64_t)dd[u] * jo.rcap + pos[u];
-                    if (BUILD) {
-                        ((uint4*)jo.rent)[at] = make_uint4(q32[u], gid[u], (uint32_t)pay[u], (uint32_t)(pay[u] >> 32));
-                    } else {
-                        const uint32_t p32 = pay[u] == JX_NOVAL ? JX_PNULL : (uint32_t)pay[u];
-                        ((uint2*)jo.rent)[at] = make_uint2(q32[u], p32);
+                        if (!take[u]) continue;
+                        if (BUILD) {
+                            ((uint4*)jo.rent)[pos[u]] = make_uint4(q32[u], gid[u], (uint32_t)pay[u], (uint32_t)(pay[u] >> 32));
+                        } else {
+                            const uint32_t p32 = pay[u] == JX_NOVAL ? JX_PNULL : (uint32_t)pay[u];
+                            ((uint2*)jo.rent)[pos[u]] = make_uint2(q32[u], p32);
+                        }
                     }
                 }
             } else {
@@ -2010,6 +2022,9 @@ __global__ __launch_bounds__(LT) void jx_extract_kernel(const uint8_t* __restric
             uint32_t ni = i + wstep;
             asm volatile("" : "+s"(ni));
             load_win(g, first_win + ni, wsb, wlds, voff, prev_next);
+        }
+        if constexpr (ROUTE == 1) {
+            if ((uint32_t)lane < jo.rn) jo.rcnt[(uint64_t)lane * nwin + i] = rrun;
         }
         if constexpr (STAR && BUILD) {
             // keys rising across the lanes too; the window's first and last for the
@@ -2381,6 +2396,9 @@ __global__ __launch_bounds__(1024) void jx_ent_probe_kernel(const uint2* __restr
 #pragma unroll
         for (int u = 0; u < U; u++) {
             slot[u] = (uint64_t)(uint32_t)(e[u].x - qoff);
+#if PROBE_EXP == 2
+            slot[u] = (i + u * nt) % range;
+#endif
             const bool in = e[u].x >= qoff && slot[u] < range;
             gv[u] = in ? (uint32_t)d16[slot[u]] : 0u;
         }
@@ -2388,7 +2406,9 @@ __global__ __launch_bounds__(1024) void jx_ent_probe_kernel(const uint2* __restr
         for (int u = 0; u < U; u++) {
             if (!gv[u]) continue;
             const uint32_t gi = (gv[u] & 0x7FFFu) - 1u;
+#if !defined(PROBE_EXP) || PROBE_EXP == 0
             if (!(gv[u] & 0x8000u)) d16[slot[u]] = (uint16_t)(gv[u] | 0x8000u);   // (every writer: the same value)
+#endif
             atomicAdd(&scnt[gi], 1u);
             if (e[u].y != JX_PNULL) {
                 atomicAdd(&sfix[gi], (unsigned long long)(long long)(int32_t)e[u].y);
@@ -3305,37 +3325,45 @@ hipError_t cq_jx_star_flush(int grouped, int value, const unsigned long long* tt
 }
 uint32_t cq_jx_star_groups() { return cq::fast::JX_G; }
 
-// the typed exchange's sender pass over one side (jx_extract_kernel ROUTE): build = 1
-// writes 16-byte {q32, gid, tag} entries (needs wbase: the count pass's exclusive
-// scan), build = 0 8-byte {q32, pay} entries; region d of `rent` holds rcap entries,
-// rcount[d] the entries reserved (> rcap: flag 256)
+// the typed exchange's sender passes over one side (jx_extract_kernel ROUTE):
+//   pass 1  per window i and destination d the entries into rcnt[d * nwin + i] (build:
+//           the window's records into wcount); pcol is ignored (the key field only)
+//   pass 2  the entries at roffs[d * nwin + i] + their rank (roffs: rcnt's exclusive
+//           scan, destination-major); build: 16-byte {q32, gid, tag} (wbase: wcount's
+//           exclusive scan), probe 8-byte {q32, pay}
 hipError_t cq_jx_route(const uint8_t* g, uint64_t lo, uint64_t hi, uint32_t ws, uint32_t delim, uint32_t quote,
-                       int kcol, int pcol, int build, int rp, const unsigned int* wbase, uint32_t nranks,
-                       unsigned long long qbase, unsigned long long gbase, void* rent, unsigned long long rcap,
-                       unsigned long long* rcount, unsigned int* flag, unsigned long long* krange, int grid,
+                       int kcol, int pcol, int build, int rp, int pass, uint32_t nranks, unsigned long long qbase,
+                       unsigned long long gbase, unsigned int* rcnt, unsigned int* wcount, const unsigned int* roffs,
+                       const unsigned int* wbase, void* rent, unsigned int* flag, unsigned long long* krange, int grid,
                        hipStream_t s) {
     using namespace cq::fast;
     JxPlan jp;
+    if (pass == 1) pcol = -1;
     if (!jx_plan(g, lo, hi, ws, delim, quote, kcol, pcol, &jp)) return hipErrorInvalidValue;
-    if (nranks < 1 || nranks > 64 || (build && !wbase)) return hipErrorInvalidValue;
+    if (nranks < 1 || nranks > 64) return hipErrorInvalidValue;
+    if (pass == 1 ? (!rcnt || (build && !wcount)) : (!roffs || !rent || (build && !wbase))) return hipErrorInvalidValue;
     const int nr = pcol >= 0 ? 2 : 1;
     if (delim != ',' || quote != '"') return hipErrorInvalidValue;      // (the ',' / '"' builds)
     typedef void (*xfn_t)(const uint8_t*, const JxPlan, const JxOut);
-    // [build][roles - 1][three records per pass]
-    static const xfn_t tab[2][2][2] = {
-        {{jx_extract_kernel<false, true, 1, false, false, 2, false, true>, jx_extract_kernel<false, true, 1, false, false, 3, false, true>},
-         {jx_extract_kernel<false, true, 2, false, false, 2, false, true>, jx_extract_kernel<false, true, 2, false, false, 3, false, true>}},
-        {{jx_extract_kernel<true, true, 1, false, false, 2, false, true>, jx_extract_kernel<true, true, 1, false, false, 3, false, true>},
-         {jx_extract_kernel<true, true, 2, false, false, 2, false, true>, jx_extract_kernel<true, true, 2, false, false, 3, false, true>}}};
-    const xfn_t fn = tab[build ? 1 : 0][nr - 1][rp == 3 ? 1 : 0];
+    // count: [build][three records per pass]; emit: [build][roles - 1][three records per pass]
+    static const xfn_t ctab[2][2] = {
+        {jx_extract_kernel<false, true, 1, false, false, 2, false, 1>, jx_extract_kernel<false, true, 1, false, false, 3, false, 1>},
+        {jx_extract_kernel<true, true, 1, false, false, 2, false, 1>, jx_extract_kernel<true, true, 1, false, false, 3, false, 1>}};
+    static const xfn_t etab[2][2][2] = {
+        {{jx_extract_kernel<false, true, 1, false, false, 2, false, 2>, jx_extract_kernel<false, true, 1, false, false, 3, false, 2>},
+         {jx_extract_kernel<false, true, 2, false, false, 2, false, 2>, jx_extract_kernel<false, true, 2, false, false, 3, false, 2>}},
+        {{jx_extract_kernel<true, true, 1, false, false, 2, false, 2>, jx_extract_kernel<true, true, 1, false, false, 3, false, 2>},
+         {jx_extract_kernel<true, true, 2, false, false, 2, false, 2>, jx_extract_kernel<true, true, 2, false, false, 3, false, 2>}}};
+    const xfn_t fn = pass == 1 ? ctab[build ? 1 : 0][rp == 3 ? 1 : 0] : etab[build ? 1 : 0][nr - 1][rp == 3 ? 1 : 0];
     JxOut jo;
     memset(&jo, 0, sizeof jo);
     jo.wbase = wbase;
+    jo.wcount = wcount;
     jo.flag = flag;
     jo.krange = krange;
     jo.rent = rent;
-    jo.rcount = rcount;
-    jo.rcap = rcap;
+    jo.rcnt = rcnt;
+    jo.roffs = roffs;
     jo.rn = nranks;
     // ceil(2^64 / n): key / n = mulhi(key, magic) for keys below 2^64 / n (canonical keys < 10^15)
     jo.rmagic = nranks > 1 ? (unsigned long long)(((unsigned __int128)1 << 64) / nranks) + 1ull : 0ull;

@@ -487,42 +487,36 @@ def join_partitioned(ast, lshard, rshard, lheader: bytes, rheader: bytes, device
 
 def typed_join_local(ast, lshards, rshards, stats: dict | None = None):
     """The typed exchange (include/cqgpu.h cqgpu_typed_*) over N simulated ranks held
-    by this one process on one GPU: every rank's entries into N regions, the regions
+    by this one process on one GPU, in cqgpu_dist_join's order: every rank's count
+    passes, the global ids' bases and qbase, every rank's emit passes, the regions
     gathered per destination (a device copy standing in for the xGMI transfer), every
     destination's STAR partial.  Returns the N blobs for cq_amd.merge_partials, or None
     when the plan or the data leave the typed exchange (the caller takes the CSV
-    exchange).  stats (optional) receives the entry counts and bytes per rank."""
+    exchange).  stats (optional) receives the entry counts per rank."""
     import cq_amd
     n = len(lshards)
-    if not cq_amd.typed_plan(ast, [lshards[0], rshards[0]]):
+    pair = lambda r: [lshards[r], rshards[r]]  # noqa: E731
+    if not cq_amd.typed_plan(ast, pair(0)):
         return None
-    nrec = [cq_amd.typed_count(ast, [lshards[r], rshards[r]]) for r in range(n)]
-    gbase = [sum(nrec[:r]) for r in range(n)]
-    if sum(nrec) >= 1 << 32:
-        return None
-    smin = min(cq_amd.typed_sample_kmin(ast, [lshards[r], rshards[r]]) for r in range(n))
-    qbase, cap_u, cap_o = (0 if smin == (1 << 64) - 1 else smin // n), 0, 0
-    for attempt in range(3):
-        flags, kmin, kmax, need_u, need_o = 0, (1 << 64) - 1, 0, 0, 0
-        cu, co = [], []
+    smin = min(cq_amd.typed_sample_kmin(ast, pair(r)) for r in range(n))
+    qbase = 0 if smin == (1 << 64) - 1 else smin // n
+    for attempt in range(2):
+        flags, kmin, kmax, cu, co, nrec = 0, (1 << 64) - 1, 0, [], [], []
         for r in range(n):
-            c1, kr, f1 = cq_amd.typed_send(ast, [lshards[r], rshards[r]], 0, n, qbase, gbase[r], cap_u)
-            c2, _, f2 = cq_amd.typed_send(ast, [lshards[r], rshards[r]], 1, n, qbase, 0, cap_o)
+            nu, c1, kr, f1 = cq_amd.typed_count(ast, pair(r), 0, n, qbase)
+            _, c2, _, f2 = cq_amd.typed_count(ast, pair(r), 1, n, qbase)
             flags |= f1 | f2
             kmin, kmax = min(kmin, kr[0]), max(kmax, kr[1])
-            need_u, need_o = max(need_u, max(c1)), max(need_o, max(c2))
             cu.append(c1)
             co.append(c2)
-        if flags & (1 | 8 | 512):
+            nrec.append(nu)
+        if flags & (1 | 8) or (flags & 16 and attempt == 1):
             return None
-        if flags & (16 | 256):
-            if flags & 16:
-                qbase = kmin // n
-            if flags & 256:
-                cap_u, cap_o = need_u, need_o
+        if flags & 16:
+            qbase = kmin // n
             continue
         break
-    else:
+    if sum(nrec) >= 1 << 32:
         return None
     if kmin > kmax:                                # no build keys at all
         kmin = kmax = qbase * n
@@ -532,6 +526,12 @@ def typed_join_local(ast, lshards, rshards, stats: dict | None = None):
     recv_o = [sum(co[s][d] for s in range(n)) for d in range(n)]
     if rng > 4 * min(recv_u) + 1024:               # not a dense key range on every rank
         return None
+    ef = 0
+    for r in range(n):
+        ef |= cq_amd.typed_send(ast, pair(r), 0, sum(nrec[:r]))
+        ef |= cq_amd.typed_send(ast, pair(r), 1, 0)
+    if ef:
+        return None
     blobs = []
     for d in range(n):
         bu = torch.empty(max(recv_u[d], 1) * 16, dtype=torch.uint8, device="cuda")
@@ -539,7 +539,7 @@ def typed_join_local(ast, lshards, rshards, stats: dict | None = None):
         torch.cuda.synchronize()
         nu = cq_amd.typed_gather(lshards, d, bu.data_ptr(), recv_u[d])
         no = cq_amd.typed_gather(rshards, d, bo.data_ptr(), recv_o[d])
-        blob = cq_amd.typed_partial(ast, [lshards[d], rshards[d]], bu.data_ptr(), nu, bo.data_ptr(), no, qoff, rng)
+        blob = cq_amd.typed_partial(ast, pair(d), bu.data_ptr(), nu, bo.data_ptr(), no, qoff, rng)
         if blob is None:
             return None
         blobs.append(blob)

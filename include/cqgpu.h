@@ -222,16 +222,17 @@ cq_table* cqgpu_dist_join(cq_node* query_ast, cqgpu_table* const* tables, int nt
  * writes the same "CQJ1" partial cqgpu_query_partial would.
  *   cqgpu_typed_plan     1 when the plan takes the typed exchange (0: *_ineligible says why)
  *   cqgpu_typed_sample_kmin  the build side's sampled key minimum (first qbase = min / N)
- *   cqgpu_typed_count    the FROM table's records (the build side's count pass); the
- *                        caller sums the lower ranks' counts into gid_base
- *   cqgpu_typed_send     one side's entries into N regions kept by the table (cap
- *                        entries each, 0: estimated); counts[N] the entries per
- *                        region, krange the build side's keys' min and max, flags: 1
- *                        not typable (quote, key or value shape), 8 a NULL build key,
- *                        16 a build key / N - qbase outside 32 bits (retry with qbase =
- *                        kmin / N), 256 a region too small (retry with cap = max count),
- *                        512 a payload outside 31 bits
+ *   cqgpu_typed_count    the count pass over side `side` (kept by the table): counts[N]
+ *                        the entries per destination, krange the build side's keys'
+ *                        min and max, flags 1 not typable (quote, key shape), 8 a NULL
+ *                        build key, 16 a build key / N - qbase outside 32 bits (retry
+ *                        with qbase = kmin / N); returns the side's records (build; the
+ *                        caller sums the lower ranks' into gid_base) or entries (probe)
+ *   cqgpu_typed_send     the emit pass after the count: the entries, destination d's
+ *                        contiguous (no atomics, no holes); flags 1 (a GROUP BY value or
+ *                        numeral the entries cannot carry), 512 (a payload over 31 bits)
  *   cqgpu_typed_region   region `dest` of a table's entries (device pointer)
+ *   cqgpu_typed_reset    drop a table's counts and entries
  *   cqgpu_typed_gather   regions `dest` of several tables, concatenated into dev_out (one
  *                        GPU standing in for the exchange: tests and the benchmark)
  *   cqgpu_typed_partial  the receiving rank's STAR join over its entries: slot = q32 - qoff,
@@ -239,13 +240,12 @@ cq_table* cqgpu_dist_join(cq_node* query_ast, cqgpu_table* const* tables, int nt
  *                        over the global build keys); the blob as cqgpu_query_partial's,
  *                        0 + *_ineligible when the entries do not fit the STAR join */
 int cqgpu_typed_plan(cq_node* query_ast, cqgpu_table* const* tables, int ntables);
-int64_t cqgpu_typed_count(cq_node* query_ast, cqgpu_table* const* tables, int ntables);
-/* the build side's sampled key minimum (a first qbase is its minimum over the ranks / N) */
 uint64_t cqgpu_typed_sample_kmin(cq_node* query_ast, cqgpu_table* const* tables, int ntables);
-int cqgpu_typed_send(cq_node* query_ast, cqgpu_table* const* tables, int ntables, int side, int nranks, uint64_t qbase,
-                     uint64_t gid_base, uint64_t cap, uint64_t* counts, uint64_t* krange, uint32_t* flags);
+int64_t cqgpu_typed_count(cq_node* query_ast, cqgpu_table* const* tables, int ntables, int side, int nranks,
+                          uint64_t qbase, uint64_t* counts, uint64_t* krange, uint32_t* flags);
+int cqgpu_typed_send(cq_node* query_ast, cqgpu_table* const* tables, int ntables, int side, uint64_t gid_base,
+                     uint32_t* flags);
 const void* cqgpu_typed_region(const cqgpu_table* t, int dest, uint64_t* entries, uint64_t* entry_bytes);
-/* drop a table's entries and its cached record count (the next send recounts) */
 void cqgpu_typed_reset(cqgpu_table* t);
 int64_t cqgpu_typed_gather(cqgpu_table* const* senders, int nsenders, int dest, void* dev_out, uint64_t cap_entries);
 size_t cqgpu_typed_partial(cq_node* query_ast, cqgpu_table* const* tables, int ntables, const void* dev_build,

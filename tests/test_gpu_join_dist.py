@@ -864,7 +864,7 @@ TYPED = [
     "SELECT COUNT(*), SUM(o.price) FROM '{u}' AS u JOIN '{o}' AS o ON u.id = o.customer_id",
     "SELECT u.role, COUNT(*) FROM '{u}' AS u JOIN '{o}' AS o ON u.id = o.customer_id GROUP BY u.role "
     "ORDER BY COUNT(*) DESC LIMIT 5",
-    "SELECT u.role, 7, AVG(o.price) FROM '{u}' AS u JOIN '{o}' AS o ON o.customer_id = u.id GROUP BY u.role",
+    "SELECT u.role, 7, AVG(o.price) FROM '{u}' AS u JOIN '{o}' AS o ON u.id = o.customer_id GROUP BY u.role",
 ]
 
 
@@ -910,11 +910,11 @@ def test_typed_exchange_large_keys_retry(tmp_path):
     the build window, NULL keys and NULL / negative prices"""
     rng = np.random.default_rng(41)
     n = 3000
-    users = "id,name,role\n" + "".join("%d,n%d,r%02d\n" % (10**14 + 7 * i, i, rng.integers(0, 30)) for i in range(n))
+    users = "id,name,role\n" + "".join("%d,n%d,r%02d\n" % (10**14 + i, i, rng.integers(0, 30)) for i in range(n))
     rows = []
     for i in range(9000):
-        k = int(rng.integers(0, n + 200))
-        cid = "" if i % 97 == 0 else str(10**14 + 7 * k if k < n else 10**14 + 7 * k + 3)
+        k = int(rng.integers(0, n + 200))                 # (k >= n: a key no user has)
+        cid = "" if i % 97 == 0 else str(10**14 + k if k < n else 10**14 + 5 * k)
         pr = "" if i % 89 == 0 else ("-%d.%02d" % (rng.integers(0, 50), rng.integers(0, 100)) if i % 31 == 0
                                      else "%d.%d" % (rng.integers(0, 999), rng.integers(0, 10)))
         rows.append("%d,%s,%s" % (i, pr, cid))
