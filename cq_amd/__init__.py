@@ -83,6 +83,14 @@ def lib():
         L.cqgpu_route_plan.restype = C.c_int
         L.cqgpu_route_plan.argtypes = [C.POINTER(abi.Node), C.POINTER(C.c_void_p), C.c_int, C.c_int, C.c_int,
                                        C.POINTER(C.c_uint64), C.POINTER(C.c_uint64)]
+        L.cqgpu_route_plan2.restype = C.c_int64
+        L.cqgpu_route_plan2.argtypes = [C.POINTER(abi.Node), C.POINTER(C.c_void_p), C.c_int, C.c_int, C.c_int,
+                                        C.c_int, C.c_uint32, C.POINTER(C.c_uint64), C.POINTER(C.c_uint64),
+                                        C.POINTER(C.c_uint64)]
+        L.cqgpu_route_major.restype = C.c_uint32
+        L.cqgpu_route_major.argtypes = [C.POINTER(C.c_uint64), C.POINTER(C.c_uint64)]
+        L.cqgpu_table_set_replicated.restype = C.c_int
+        L.cqgpu_table_set_replicated.argtypes = [C.c_void_p, C.c_uint32, C.c_int]
         L.cqgpu_route_fill.restype = C.c_int
         L.cqgpu_route_fill.argtypes = [C.c_void_p, C.c_uint64, C.c_void_p, C.c_void_p]
         L.cqgpu_join_outer_matched.restype = C.c_int
@@ -307,6 +315,34 @@ def table_from_routed(dev_bytes_ptr: int, nbytes: int, dev_gids_ptr: int, nrec: 
     """A join side rebuilt from received records (device memory) and their global ids."""
     return Table(lib().cqgpu_table_from_routed(dev_bytes_ptr, nbytes, dev_gids_ptr, nrec,
                                                cfg or abi.csv_config(), header, len(header)))
+
+
+def route_plan2(ast, tables, side: int, nranks: int, rank: int, mode: int = 0):
+    """cqgpu_route_plan2: the routing of tables[side] for `rank` in routing mode `mode`
+    (0 key routing; 1-3 the majority key class of cqgpu_route_major, other non-NULL
+    classes to every rank; a JOIN without ON: side 0 stays, side 1 to every rank).
+    Returns (bytes per destination, records per destination, this side's record
+    count on this rank, its ON keys per value class [NULL, number, string, date])."""
+    arr, n = _tables_arg(tables)
+    nb = (C.c_uint64 * nranks)()
+    nr = (C.c_uint64 * nranks)()
+    cc = (C.c_uint64 * 4)()
+    own = lib().cqgpu_route_plan2(ast, arr, n, side, nranks, rank, mode, nb, nr, cc)
+    if own < 0:
+        raise RuntimeError(last_error() or "cqgpu_route_plan2 failed")
+    return list(nb), list(nr), int(own), list(cc)
+
+
+def route_major(lcounts, rcounts) -> int:
+    """cqgpu_route_major over the ranks' summed class counts of both sides."""
+    return int(lib().cqgpu_route_major((C.c_uint64 * 4)(*lcounts), (C.c_uint64 * 4)(*rcounts)))
+
+
+def table_set_replicated(table: "Table", mode: int, owner: bool) -> None:
+    """cqgpu_table_set_replicated: a routed side's replication mode (0-3, 4 whole on
+    every rank) and whether this rank owns what every rank finds."""
+    if lib().cqgpu_table_set_replicated(table.handle, mode, 1 if owner else 0) != 0:
+        raise RuntimeError(last_error() or "cqgpu_table_set_replicated failed")
 
 
 def table_set_key_stride(table: "Table", stride: int) -> None:

@@ -105,13 +105,18 @@ hipError_t cq_launch_join_count(const cq::Cell* L, uint32_t ls, uint32_t lk, uin
 hipError_t cq_launch_join_emit(const cq::Cell* L, uint32_t ls, uint32_t lk, uint32_t nL, const cq::JoinRight* J,
                                const uint32_t* lo, const unsigned long long* cnt, const unsigned long long* offs,
                                uint2* pairs, unsigned int* rmatched, hipStream_t s);
-hipError_t cq_launch_route_runs(const uint32_t* dest, const uint32_t* len, uint32_t n, uint32_t nw,
+hipError_t cq_launch_route_runs(const uint32_t* dest, const uint32_t* len, uint32_t n, uint32_t nw, uint32_t nranks,
                                 unsigned long long* rcnt, unsigned long long* rbytes, hipStream_t s);
+hipError_t cq_launch_route_dest_mode(const uint32_t* cls, uint32_t n, uint32_t nranks, uint32_t rep, uint32_t fixed,
+                                    uint32_t* dest, hipStream_t s);
+hipError_t cq_launch_pair_rep_flags(const uint2* pairs, unsigned long long np, const cq::Cell* L, uint32_t ls,
+                                    uint32_t lk, const cq::Cell* R, uint32_t rs, uint32_t rk, uint32_t major,
+                                    unsigned int* flags, hipStream_t s);
 hipError_t cq_launch_route_run_starts(const unsigned long long* cbase, const unsigned long long* bbase,
                                      const unsigned long long* rcnt, const unsigned long long* rbytes, uint32_t nw,
                                      uint32_t nranks, unsigned long long* starts, hipStream_t s);
 hipError_t cq_launch_route_scatter(const uint8_t* g, const unsigned long long* recs, const uint32_t* dest,
-                                   const uint32_t* len, uint32_t n, uint32_t nw, uint64_t end,
+                                   const uint32_t* len, uint32_t n, uint32_t nw, uint32_t nranks, uint64_t end,
                                    const unsigned long long* cbase, const unsigned long long* bbase, uint64_t gid_base,
                                    uint8_t* out, unsigned long long* gids, hipStream_t s);
 hipError_t cq_launch_pack_first_gid(uint8_t* pk, const unsigned int* count, uint32_t cap, uint32_t rec,
@@ -581,7 +586,7 @@ struct RouteState {
     // nranks <= 64: the destination-run layout (route.hip route_runs_kernel) -- each
     // record's destination, and every (destination, wave) run's record / byte base
     DevBuf dest, cbase, bbase;
-    uint32_t nw = 0;
+    uint32_t nw = 0, nranks = 0;
     bool runs = false;
     uint32_t n = 0;
     uint64_t bytes = 0;
@@ -647,6 +652,13 @@ struct cqgpu_table {
     uint64_t ngids = 0;
     uint64_t gid_total = 0;               // routed tables: records of the whole input (every rank's share)
     std::unique_ptr<RouteState> route;    // pending repartition (cqgpu_route_plan)
+    // a routed side's replication (cqgpu_table_set_replicated): rep_major 1-3: every
+    // non-NULL key of another value class went to every rank; bcast: every record of
+    // this side is on every rank (a JOIN without ON); rep_owner: this rank keeps what
+    // every rank finds (pairs of two replicated records, a cross join's unmatched rows)
+    uint32_t rep_major = 0;
+    bool bcast = false;
+    bool rep_owner = true;
     std::unique_ptr<DevBuf> rec_starts;   // record start offsets, file order (built on first need; immutable table)
     uint32_t nrec_starts = 0;
     // the typed join exchange (cqgpu_typed_*): this table's counts and pending entries
@@ -1735,6 +1747,7 @@ std::vector<HGroup> make_groups(DevCtx& c, const Compiled& C, uint64_t limit, ui
     if (!C.grouped && outs.empty()) {
         GroupOut z;
         memset(&z, 0, sizeof z);
+        z.clslen = (uint32_t)GK_ALL << 16;   // the kernels' key of the one group (partials merge by it)
         z.first = NOPOS;
         for (int a = 0; a < MAX_ACC; a++) z.extpos[a] = NOPOS;
         outs.push_back(z);
@@ -3048,6 +3061,10 @@ JoinMap join_map(const std::vector<int>& jcols, int nl, const JoinSide& A, const
     return M;
 }
 
+// JoinPartial::lmask bit: the partial's sides were routed with the minority key
+// classes replicated (cqgpu_route_plan2), so cross-class pairs need no refusal
+constexpr uint32_t REP_ROUTED = 0x10u;
+
 // per-rank state of a repartitioned join (cqgpu_query_partial over routed tables)
 struct JoinPartial {
     std::vector<std::string> names;   // joined schema (alias.col)
@@ -4161,7 +4178,9 @@ cq_table* run_join(DevCtx& c, cq_node* q, const cqgpu_table* L, const cqgpu_tabl
         if (!v.R) throw Ineligible{"join table failed to load"};
         cq_node* on = jn->u.join.on;
         v.cross = on == nullptr;              // JOIN without ON: the cross product (evaluator_joins.c:42)
-        if (v.cross && part && j == 0) throw Ineligible{"JOIN without ON across partials"};
+        // across partials the first level's JOIN table must be on every rank
+        // (cqgpu_route_plan2's cross routing, marked by cqgpu_table_set_replicated)
+        if (v.cross && part && j == 0 && !v.R->bcast) throw Ineligible{"JOIN without ON across partials"};
         v.ra = jn->u.join.alias ? jn->u.join.alias : "right";
         cqgpu_table W;                       // the left side's schema at this level
         W.names = wnames;
@@ -4173,7 +4192,16 @@ cq_table* run_join(DevCtx& c, cq_node* q, const cqgpu_table* L, const cqgpu_tabl
             v.kr = join_on_index(on->u.bin.rhs->u.text, v.R, &W, wa.c_str(), v.R, v.ra.c_str());
         }
         v.keyed = v.kl >= 0 && v.kr >= 0;
-        if (part && j == 0 && !v.keyed) throw Ineligible{"JOIN without an `ident = ident` ON across partials"};
+        if (part && j == 0 && !v.keyed && !v.cross) throw Ineligible{"JOIN without an `ident = ident` ON across partials"};
+        if (part && j == 0 && (L->rep_major || v.R->rep_major)) {
+            // keys of several value classes, the minority classes replicated to every
+            // rank (cqgpu_route_plan2): INNER pairs are exact once the pairs of two
+            // replicated records are kept on one rank; an outer join's unmatched rows
+            // would need every rank's matches
+            if (L->rep_major != v.R->rep_major || !v.keyed) throw HipError{"join sides routed in different modes"};
+            if (v.outer_left || v.outer_right)
+                throw Ineligible{"an outer JOIN over keys of different value classes across partials"};
+        }
         if (part && j > 0 && v.R->gids) throw HipError{"join chain across partials: a later level's table must be whole"};
         v.nleft = (int)wnames.size();
         std::vector<std::string> nn;        // copy_columns_with_prefix (evaluator_joins.c:30-37)
@@ -4196,7 +4224,7 @@ cq_table* run_join(DevCtx& c, cq_node* q, const cqgpu_table* L, const cqgpu_tabl
         part->nrep = (uint32_t)C.rep_cols.size();
         part->nvla = (uint32_t)C.vla.size();
     }
-    if (!rows && nj == 1 && lv[0].keyed && !lv[0].outer_left && !lv[0].outer_right &&
+    if (!rows && nj == 1 && lv[0].keyed && !lv[0].outer_left && !lv[0].outer_right && !L->rep_major &&
         !(part && getenv("CQ_AMD_NO_PART_FAST_JOIN"))) {
         // (partials: the STAR form only, its groups globalised into *part)
         cq_table* fj = run_fast_join(c, q, C, L, lv[0].R, lv[0].kl, lv[0].kr, lv[0].nleft, part, &J.names);
@@ -4258,9 +4286,32 @@ cq_table* run_join(DevCtx& c, cq_node* q, const cqgpu_table* L, const cqgpu_tabl
             std::swap(mdev.p, mb.p);
         }
         DevBuf pb(8);
-        np = build_pairs(c, *Ap, *Bp, v.kl, v.kr, v.keyed, v.outer_left, v.outer_right || probe_here, pb, v.cross,
-                         os ? gdev.as<uint8_t>() : nullptr, os ? os->emit : true,
+        // a cross join's first level across partials: the JOIN table is whole on every
+        // rank, so its unmatched rows (RIGHT / FULL) exist only when the FROM table is
+        // empty on every rank, and one rank emits them
+        const bool right_rows = !(part && j == 0 && v.cross) || (L->gid_total == 0 && v.R->rep_owner);
+        np = build_pairs(c, *Ap, *Bp, v.kl, v.kr, v.keyed, v.outer_left, (v.outer_right && right_rows) || probe_here,
+                         pb, v.cross, os ? gdev.as<uint8_t>() : nullptr, os ? os->emit : true,
                          probe_here ? mdev.as<uint8_t>() : nullptr);
+        if (part && j == 0 && v.keyed && L->rep_major && !L->rep_owner && np) {
+            // pairs of two replicated records: every rank found them, the owner keeps them
+            DevBuf fl(np * 4), pos(np * 4), kept(np * 8);
+            HIPCHECK(cq_launch_pair_rep_flags(pb.as<uint2>(), np, Ap->cells.as<Cell>(), (uint32_t)Ap->cols.size(),
+                                              (uint32_t)Ap->slot(v.kl), Bp->cells.as<Cell>(), (uint32_t)Bp->cols.size(),
+                                              (uint32_t)Bp->slot(v.kr), L->rep_major, fl.as<unsigned int>(), c.stream));
+            size_t tb = 0;
+            HIPCHECK(cq_excl_sum_u32(nullptr, &tb, fl.as<unsigned int>(), pos.as<unsigned int>(), np, c.stream));
+            DevBuf temp(tb);
+            HIPCHECK(cq_excl_sum_u32(temp.p, &tb, fl.as<unsigned int>(), pos.as<unsigned int>(), np, c.stream));
+            HIPCHECK(cq_launch_key_flagged(pb.as<unsigned long long>(), np, fl.as<unsigned int>(), pos.as<unsigned int>(),
+                                           kept.as<unsigned long long>(), c.stream));
+            unsigned int last[2] = {0, 0};
+            HIPCHECK(hipMemcpyAsync(&last[0], pos.as<unsigned int>() + np - 1, 4, hipMemcpyDeviceToHost, c.stream));
+            HIPCHECK(hipMemcpyAsync(&last[1], fl.as<unsigned int>() + np - 1, 4, hipMemcpyDeviceToHost, c.stream));
+            HIPCHECK(hipStreamSynchronize(c.stream));
+            np = (unsigned long long)last[0] + last[1];
+            std::swap(pb.p, kept.p);
+        }
         if (probe_here) {
             part->probe_out.assign(Bp->n, 0);
             if (Bp->n)
@@ -4273,6 +4324,7 @@ cq_table* run_join(DevCtx& c, cq_node* q, const cqgpu_table* L, const cqgpu_tabl
         if (part && j == 0 && v.keyed) {     // even when one side is empty on this rank
             part->lmask |= key_class_mask(c, *Ap, v.kl);
             part->rmask |= key_class_mask(c, *Bp, v.kr);
+            if (L->rep_major) part->lmask |= REP_ROUTED;   // the cross-class pairs are exact (replicated)
         }
         if (chain) {                         // route.hip chain_key_kernel
             DevBuf nk((size_t)std::max<unsigned long long>(np, 1) * 8);
@@ -4988,114 +5040,102 @@ cqgpu_table* cqgpu_table_open_range(const char* path, cq_csv_config cfg, int ran
 uint64_t cqgpu_table_base_offset(const cqgpu_table* t) { return t ? t->base_offset : 0; }
 
 // ---- join-key repartition (multi-GPU JOIN) -----------------------------------
-int cqgpu_route_plan(cq_node* q, cqgpu_table* const* tables, int ntables, int side, int nranks,
-                     uint64_t* bytes_per_rank, uint64_t* recs_per_rank) {
-    g_inel.clear();
-    g_err.clear();
-    try {
-        DevCtx& c = ctx();
-        bump_reset(c);
-        if (ntables < 2 || !tables[0] || !tables[1] || (side != 0 && side != 1)) throw HipError{"route: bad tables"};
-        if (nranks < 1 || nranks > 4096) throw HipError{"route: bad rank count"};
-        // the first JOIN's ON keys route both its sides; a chain's later tables stay whole
-        if (!q || q->kind != CQ_N_QUERY || q->u.q.join_count < 1 || !q->u.q.joins[0]) throw Ineligible{"no JOIN"};
-        check_plan_shape(q, tables[0], true);
-        cq_node* jn = q->u.q.joins[0];
-        cq_node* on = jn->u.join.on;
-        const cqgpu_table* L = tables[0];
-        const cqgpu_table* R = tables[1];
-        const char* la = (q->u.q.from && q->u.q.from->u.from.alias) ? q->u.q.from->u.from.alias : "main";
-        const char* ra = jn->u.join.alias ? jn->u.join.alias : "right";
-        int k = -1;
-        if (on && on->kind == CQ_N_CONDITION && on->u.bin.op && !strcmp(on->u.bin.op, "=") && on->u.bin.lhs &&
-            on->u.bin.rhs && on->u.bin.lhs->kind == CQ_N_IDENTIFIER && on->u.bin.rhs->kind == CQ_N_IDENTIFIER) {
-            // same operand binding as run_join (evaluator_joins.c:49-52)
-            k = side == 0 ? join_on_index(on->u.bin.lhs->u.text, L, L, la, R, ra)
-                          : join_on_index(on->u.bin.rhs->u.text, R, L, la, R, ra);
+namespace {
+// cqgpu_route_plan / cqgpu_route_plan2: rank < 0 = the caller's rank unknown (a JOIN
+// without ON is refused); mode 0 = key routing, 1-3 = non-NULL keys of other classes
+// to every rank; class_counts (optional): this side's keys per class (NULL, number,
+// string, date)
+void route_plan_impl(cq_node* q, cqgpu_table* const* tables, int ntables, int side, int nranks, int rank,
+                     uint32_t mode, uint64_t* bytes_per_rank, uint64_t* recs_per_rank, uint64_t* class_counts) {
+    DevCtx& c = ctx();
+    bump_reset(c);
+    if (ntables < 2 || !tables[0] || !tables[1] || (side != 0 && side != 1)) throw HipError{"route: bad tables"};
+    if (nranks < 1 || nranks > 4096) throw HipError{"route: bad rank count"};
+    if (rank >= nranks || mode > 3) throw HipError{"route: bad rank or mode"};
+    // the first JOIN's ON keys route both its sides; a chain's later tables stay whole
+    if (!q || q->kind != CQ_N_QUERY || q->u.q.join_count < 1 || !q->u.q.joins[0]) throw Ineligible{"no JOIN"};
+    check_plan_shape(q, tables[0], true);
+    cq_node* jn = q->u.q.joins[0];
+    cq_node* on = jn->u.join.on;
+    const cqgpu_table* L = tables[0];
+    const cqgpu_table* R = tables[1];
+    const char* la = (q->u.q.from && q->u.q.from->u.from.alias) ? q->u.q.from->u.from.alias : "main";
+    const char* ra = jn->u.join.alias ? jn->u.join.alias : "right";
+    int k = -1;
+    if (on && on->kind == CQ_N_CONDITION && on->u.bin.op && !strcmp(on->u.bin.op, "=") && on->u.bin.lhs &&
+        on->u.bin.rhs && on->u.bin.lhs->kind == CQ_N_IDENTIFIER && on->u.bin.rhs->kind == CQ_N_IDENTIFIER) {
+        // same operand binding as run_join (evaluator_joins.c:49-52)
+        k = side == 0 ? join_on_index(on->u.bin.lhs->u.text, L, L, la, R, ra)
+                      : join_on_index(on->u.bin.rhs->u.text, R, L, la, R, ra);
+    }
+    // a JOIN without ON (evaluator_joins.c:41: every pair matches): the FROM side
+    // stays on its rank, the JOIN side goes to every rank
+    const bool cross = on == nullptr && rank >= 0;
+    if (k < 0 && !cross) throw Ineligible{"JOIN without an `ident = ident` ON across partials"};
+    const bool special = cross || mode != 0;
+    if (special && (nranks > 64 || getenv("CQGPU_ROUTE_SORT")))
+        throw Ineligible{"replicated join routing over more than 64 ranks"};
+    cqgpu_table* t = tables[side];
+    auto st = std::make_unique<RouteState>();
+    JoinSide S;
+    S.cols.push_back(k >= 0 ? k : 0);
+    load_side(c, t, S);
+    std::swap(st->recs.p, S.recs.p);
+    const uint32_t n = S.n;
+    st->n = n;
+    st->keep = route_keep_mask(q, tables, ntables, side, &st->last_keep);
+    std::vector<unsigned long long> per(2 * (size_t)nranks, 0);
+    if (n) {
+        DevBuf codes((size_t)n * 8), cls((size_t)n * 4), dest((size_t)n * 4), idx((size_t)n * 4),
+            len((size_t)n * 4), dst((2 * (size_t)nranks + 2) * 8), pcls(64);
+        HIPCHECK(hipMemsetAsync(pcls.p, 0, 16, c.stream));
+        HIPCHECK(cq_launch_join_code(S.cells.as<Cell>(), 1, 0, n, codes.as<unsigned long long>(), cls.as<uint32_t>(),
+                                     idx.as<uint32_t>(), class_counts && !cross ? pcls.as<unsigned int>() : nullptr,
+                                     c.stream));
+        if (class_counts && !cross) {
+            unsigned int pc4[4] = {0, 0, 0, 0};
+            HIPCHECK(hipMemcpyAsync(pc4, pcls.p, 16, hipMemcpyDeviceToHost, c.stream));
+            HIPCHECK(hipStreamSynchronize(c.stream));
+            for (int j = 0; j < 4; j++) class_counts[j] = pc4[j];
         }
-        if (k < 0) throw Ineligible{"JOIN without an `ident = ident` ON across partials"};
-        cqgpu_table* t = tables[side];
-        auto st = std::make_unique<RouteState>();
-        JoinSide S;
-        S.cols.push_back(k);
-        load_side(c, t, S);
-        std::swap(st->recs.p, S.recs.p);
-        const uint32_t n = S.n;
-        st->n = n;
-        st->keep = route_keep_mask(q, tables, ntables, side, &st->last_keep);
-        std::vector<unsigned long long> per(2 * (size_t)nranks, 0);
-        if (n) {
-            DevBuf codes((size_t)n * 8), cls((size_t)n * 4), dest((size_t)n * 4), idx((size_t)n * 4),
-                len((size_t)n * 4), dst((2 * (size_t)nranks + 2) * 8);
-            HIPCHECK(cq_launch_join_code(S.cells.as<Cell>(), 1, 0, n, codes.as<unsigned long long>(), cls.as<uint32_t>(),
-                                         idx.as<uint32_t>(), nullptr, c.stream));
-            if (st->keep != ~0ull) {
-                DevBuf proj(t->n + 64);
-                HIPCHECK(cq_launch_route_project(t->g, st->recs.as<unsigned long long>(), n, t->n, st->keep,
-                                                 st->last_keep, (uint8_t)t->cfg.delimiter, (uint8_t)t->cfg.quote,
-                                                 codes.as<unsigned long long>(), cls.as<uint32_t>(), (uint32_t)nranks,
-                                                 len.as<uint32_t>(), dest.as<uint32_t>(), proj.as<uint8_t>(),
-                                                 c.stream));
-                std::swap(st->proj.p, proj.p);
-            } else {
-                HIPCHECK(cq_launch_route_len(t->g, st->recs.as<unsigned long long>(), n, codes.as<unsigned long long>(),
-                                             cls.as<uint32_t>(), (uint32_t)nranks, len.as<uint32_t>(),
-                                             dest.as<uint32_t>(), c.stream));
-            }
-            if (nranks <= 64 && !getenv("CQGPU_ROUTE_SORT")) {
-                // destination runs: per (destination, wave) counts, one exclusive scan each
-                const uint32_t nw = (uint32_t)(((uint64_t)n + 63) / 64);
-                const size_t nrun = (size_t)nranks * nw;
-                DevBuf rc(nrun * 8), rbt(nrun * 8), cb(nrun * 8), bb(nrun * 8);
-                HIPCHECK(hipMemsetAsync(rc.p, 0, nrun * 8, c.stream));
-                HIPCHECK(hipMemsetAsync(rbt.p, 0, nrun * 8, c.stream));
-                HIPCHECK(cq_launch_route_runs(dest.as<uint32_t>(), len.as<uint32_t>(), n, nw,
-                                              rc.as<unsigned long long>(), rbt.as<unsigned long long>(), c.stream));
-                size_t tr = 0;
-                HIPCHECK(cq_excl_sum_u64(nullptr, &tr, rc.as<unsigned long long>(), cb.as<unsigned long long>(), nrun,
-                                         c.stream));
-                DevBuf tmp(tr);
-                HIPCHECK(cq_excl_sum_u64(tmp.p, &tr, rc.as<unsigned long long>(), cb.as<unsigned long long>(), nrun,
-                                         c.stream));
-                HIPCHECK(cq_excl_sum_u64(tmp.p, &tr, rbt.as<unsigned long long>(), bb.as<unsigned long long>(), nrun,
-                                         c.stream));
-                HIPCHECK(cq_launch_route_run_starts(cb.as<unsigned long long>(), bb.as<unsigned long long>(),
-                                                    rc.as<unsigned long long>(), rbt.as<unsigned long long>(), nw,
-                                                    (uint32_t)nranks, dst.as<unsigned long long>(), c.stream));
-                std::vector<unsigned long long> starts(2 * (size_t)nranks + 2);
-                HIPCHECK(hipMemcpyAsync(starts.data(), dst.p, starts.size() * 8, hipMemcpyDeviceToHost, c.stream));
-                HIPCHECK(hipStreamSynchronize(c.stream));
-                for (int r = 0; r < nranks; r++) {
-                    per[nranks + r] = starts[r + 1] - starts[r];
-                    per[r] = starts[nranks + 2 + r] - starts[nranks + 1 + r];
-                }
-                st->runs = true;
-                st->nw = nw;
-                std::swap(st->dest.p, dest.p);
-                std::swap(st->len.p, len.p);
-                std::swap(st->cbase.p, cb.p);
-                std::swap(st->bbase.p, bb.p);
-            } else {
-            DevBuf dsorted((size_t)n * 4), order((size_t)n * 4), lens((size_t)n * 8), off((size_t)n * 8);
-            int bits = 1;
-            while ((1 << bits) < nranks) bits++;
-            size_t tb = 0;
-            HIPCHECK(cq_sort_dest(nullptr, &tb, dest.as<unsigned int>(), dsorted.as<unsigned int>(), idx.as<unsigned int>(),
-                                  order.as<unsigned int>(), n, bits, c.stream));
-            DevBuf temp(tb);
-            HIPCHECK(cq_sort_dest(temp.p, &tb, dest.as<unsigned int>(), dsorted.as<unsigned int>(), idx.as<unsigned int>(),
-                                  order.as<unsigned int>(), n, bits, c.stream));
-            HIPCHECK(cq_launch_gather_len(len.as<uint32_t>(), order.as<uint32_t>(), n, lens.as<unsigned long long>(),
-                                          c.stream));
-            size_t tb2 = 0;
-            HIPCHECK(cq_excl_sum_u64(nullptr, &tb2, lens.as<unsigned long long>(), off.as<unsigned long long>(), n,
+        if (st->keep != ~0ull) {
+            DevBuf proj(t->n + 64);
+            HIPCHECK(cq_launch_route_project(t->g, st->recs.as<unsigned long long>(), n, t->n, st->keep,
+                                             st->last_keep, (uint8_t)t->cfg.delimiter, (uint8_t)t->cfg.quote,
+                                             codes.as<unsigned long long>(), cls.as<uint32_t>(), (uint32_t)nranks,
+                                             len.as<uint32_t>(), dest.as<uint32_t>(), proj.as<uint8_t>(),
+                                             c.stream));
+            std::swap(st->proj.p, proj.p);
+        } else {
+            HIPCHECK(cq_launch_route_len(t->g, st->recs.as<unsigned long long>(), n, codes.as<unsigned long long>(),
+                                         cls.as<uint32_t>(), (uint32_t)nranks, len.as<uint32_t>(),
+                                         dest.as<uint32_t>(), c.stream));
+        }
+        if (special)
+            HIPCHECK(cq_launch_route_dest_mode(cls.as<uint32_t>(), n, (uint32_t)nranks, cross ? 0u : mode,
+                                               cross ? (side == 0 ? (uint32_t)rank : (uint32_t)nranks) : ~0u,
+                                               dest.as<uint32_t>(), c.stream));
+        if (nranks <= 64 && !getenv("CQGPU_ROUTE_SORT")) {
+            // destination runs: per (destination, wave) counts, one exclusive scan each
+            // (dest == nranks: the record's copy in every destination's run)
+            const uint32_t nw = (uint32_t)(((uint64_t)n + 63) / 64);
+            const size_t nrun = (size_t)nranks * nw;
+            DevBuf rc(nrun * 8), rbt(nrun * 8), cb(nrun * 8), bb(nrun * 8);
+            HIPCHECK(hipMemsetAsync(rc.p, 0, nrun * 8, c.stream));
+            HIPCHECK(hipMemsetAsync(rbt.p, 0, nrun * 8, c.stream));
+            HIPCHECK(cq_launch_route_runs(dest.as<uint32_t>(), len.as<uint32_t>(), n, nw, (uint32_t)nranks,
+                                          rc.as<unsigned long long>(), rbt.as<unsigned long long>(), c.stream));
+            size_t tr = 0;
+            HIPCHECK(cq_excl_sum_u64(nullptr, &tr, rc.as<unsigned long long>(), cb.as<unsigned long long>(), nrun,
                                      c.stream));
-            DevBuf temp2(tb2);
-            HIPCHECK(cq_excl_sum_u64(temp2.p, &tb2, lens.as<unsigned long long>(), off.as<unsigned long long>(), n,
+            DevBuf tmp(tr);
+            HIPCHECK(cq_excl_sum_u64(tmp.p, &tr, rc.as<unsigned long long>(), cb.as<unsigned long long>(), nrun,
                                      c.stream));
-            HIPCHECK(cq_launch_route_bounds(dsorted.as<uint32_t>(), off.as<unsigned long long>(),
-                                            lens.as<unsigned long long>(), n, (uint32_t)nranks,
-                                            dst.as<unsigned long long>(), c.stream));
+            HIPCHECK(cq_excl_sum_u64(tmp.p, &tr, rbt.as<unsigned long long>(), bb.as<unsigned long long>(), nrun,
+                                     c.stream));
+            HIPCHECK(cq_launch_route_run_starts(cb.as<unsigned long long>(), bb.as<unsigned long long>(),
+                                                rc.as<unsigned long long>(), rbt.as<unsigned long long>(), nw,
+                                                (uint32_t)nranks, dst.as<unsigned long long>(), c.stream));
             std::vector<unsigned long long> starts(2 * (size_t)nranks + 2);
             HIPCHECK(hipMemcpyAsync(starts.data(), dst.p, starts.size() * 8, hipMemcpyDeviceToHost, c.stream));
             HIPCHECK(hipStreamSynchronize(c.stream));
@@ -5103,19 +5143,71 @@ int cqgpu_route_plan(cq_node* q, cqgpu_table* const* tables, int ntables, int si
                 per[nranks + r] = starts[r + 1] - starts[r];
                 per[r] = starts[nranks + 2 + r] - starts[nranks + 1 + r];
             }
-            std::swap(st->order.p, order.p);
+            st->runs = true;
+            st->nw = nw;
+            st->nranks = (uint32_t)nranks;
+            std::swap(st->dest.p, dest.p);
             std::swap(st->len.p, len.p);
-            std::swap(st->off.p, off.p);
-            }
-        }
-        st->bytes = 0;
+            std::swap(st->cbase.p, cb.p);
+            std::swap(st->bbase.p, bb.p);
+        } else {
+        DevBuf dsorted((size_t)n * 4), order((size_t)n * 4), lens((size_t)n * 8), off((size_t)n * 8);
+        int bits = 1;
+        while ((1 << bits) < nranks) bits++;
+        size_t tb = 0;
+        HIPCHECK(cq_sort_dest(nullptr, &tb, dest.as<unsigned int>(), dsorted.as<unsigned int>(), idx.as<unsigned int>(),
+                              order.as<unsigned int>(), n, bits, c.stream));
+        DevBuf temp(tb);
+        HIPCHECK(cq_sort_dest(temp.p, &tb, dest.as<unsigned int>(), dsorted.as<unsigned int>(), idx.as<unsigned int>(),
+                              order.as<unsigned int>(), n, bits, c.stream));
+        HIPCHECK(cq_launch_gather_len(len.as<uint32_t>(), order.as<uint32_t>(), n, lens.as<unsigned long long>(),
+                                      c.stream));
+        size_t tb2 = 0;
+        HIPCHECK(cq_excl_sum_u64(nullptr, &tb2, lens.as<unsigned long long>(), off.as<unsigned long long>(), n,
+                                 c.stream));
+        DevBuf temp2(tb2);
+        HIPCHECK(cq_excl_sum_u64(temp2.p, &tb2, lens.as<unsigned long long>(), off.as<unsigned long long>(), n,
+                                 c.stream));
+        HIPCHECK(cq_launch_route_bounds(dsorted.as<uint32_t>(), off.as<unsigned long long>(),
+                                        lens.as<unsigned long long>(), n, (uint32_t)nranks,
+                                        dst.as<unsigned long long>(), c.stream));
+        std::vector<unsigned long long> starts(2 * (size_t)nranks + 2);
+        HIPCHECK(hipMemcpyAsync(starts.data(), dst.p, starts.size() * 8, hipMemcpyDeviceToHost, c.stream));
+        HIPCHECK(hipStreamSynchronize(c.stream));
         for (int r = 0; r < nranks; r++) {
-            st->bytes += per[r];
-            if (bytes_per_rank) bytes_per_rank[r] = per[r];
-            if (recs_per_rank) recs_per_rank[r] = per[nranks + r];
+            per[nranks + r] = starts[r + 1] - starts[r];
+            per[r] = starts[nranks + 2 + r] - starts[nranks + 1 + r];
         }
-        t->route = std::move(st);
-        return 0;
+        std::swap(st->order.p, order.p);
+        std::swap(st->len.p, len.p);
+        std::swap(st->off.p, off.p);
+        }
+    }
+    st->bytes = 0;
+    for (int r = 0; r < nranks; r++) {
+        st->bytes += per[r];
+        if (bytes_per_rank) bytes_per_rank[r] = per[r];
+        if (recs_per_rank) recs_per_rank[r] = per[nranks + r];
+    }
+    if (class_counts && (!n || cross))
+        for (int j = 0; j < 4; j++) class_counts[j] = 0;
+    t->route = std::move(st);
+}
+}  // namespace
+
+int cqgpu_route_plan(cq_node* q, cqgpu_table* const* tables, int ntables, int side, int nranks,
+                     uint64_t* bytes_per_rank, uint64_t* recs_per_rank) {
+    return cqgpu_route_plan2(q, tables, ntables, side, nranks, -1, 0, bytes_per_rank, recs_per_rank, nullptr) < 0 ? -1
+                                                                                                               : 0;
+}
+
+int64_t cqgpu_route_plan2(cq_node* q, cqgpu_table* const* tables, int ntables, int side, int nranks, int rank,
+                          uint32_t mode, uint64_t* bytes_per_rank, uint64_t* recs_per_rank, uint64_t* class_counts) {
+    g_inel.clear();
+    g_err.clear();
+    try {
+        route_plan_impl(q, tables, ntables, side, nranks, rank, mode, bytes_per_rank, recs_per_rank, class_counts);
+        return (int64_t)tables[side]->route->n;
     } catch (Ineligible& e) {
         g_inel = e.why;
         set_err("cq_amd: query outside the GPU executor's subset: %s", e.why.c_str());
@@ -5144,7 +5236,7 @@ int cqgpu_route_fill(cqgpu_table* t, uint64_t gid_base, void* dev_bytes, uint64_
             const uint8_t* src = st.keep != ~0ull ? st.proj.as<uint8_t>() : t->g;
             if (st.runs)
                 HIPCHECK(cq_launch_route_scatter(src, st.recs.as<unsigned long long>(), st.dest.as<uint32_t>(),
-                                                 st.len.as<uint32_t>(), st.n, st.nw, t->n,
+                                                 st.len.as<uint32_t>(), st.n, st.nw, st.nranks, t->n,
                                                  st.cbase.as<unsigned long long>(),
                                                  st.bbase.as<unsigned long long>(), gid_base, (uint8_t*)dev_bytes,
                                                  (unsigned long long*)dev_gids, c.stream));
@@ -5229,6 +5321,31 @@ int cqgpu_table_set_key_stride(cqgpu_table* t, uint32_t stride) {
     t->key_stride = stride;
     t->key_range.clear();                   // learned ranges assumed the old stride
     return 0;
+}
+
+int cqgpu_table_set_replicated(cqgpu_table* t, uint32_t mode, int owner) {
+    g_err.clear();
+    if (!t || mode > 4) {
+        set_err("cq_amd: %s", "table_set_replicated: mode 0-4");
+        return -1;
+    }
+    t->rep_major = mode <= 3 ? mode : 0u;
+    t->bcast = mode == 4;
+    t->rep_owner = owner != 0;
+    return 0;
+}
+
+uint32_t cqgpu_route_major(const uint64_t* lcounts, const uint64_t* rcounts) {
+    // value_compare (csv_reader.c:126-129): non-NULL keys of different classes are
+    // "equal", so such a pair exists iff the sides hold some classes x != y
+    bool mixed = false;
+    for (int x = 1; x < 4; x++)
+        for (int y = 1; y < 4; y++) mixed = mixed || (x != y && lcounts[x] && rcounts[y]);
+    if (!mixed) return 0;
+    uint32_t best = 1;                     // the class most records hold routes by key
+    for (uint32_t k = 2; k < 4; k++)
+        if (lcounts[k] + rcounts[k] > lcounts[best] + rcounts[best]) best = k;
+    return best;
 }
 
 int cqgpu_table_set_record_total(cqgpu_table* t, uint64_t total) {
@@ -5903,6 +6020,7 @@ cq_table* cqgpu_merge_partials(cq_node* q, const void* const* blobs, const size_
         };
         std::vector<Part> parts(nblobs);
         uint32_t nacc = 0, nrep = 0, nvla = 0, magic0 = 0, lmask = 0, rmask = 0;
+        uint32_t rep_all = REP_ROUTED;    // every partial's sides routed with replication
         if (sizes[0] >= 4 && *(const uint32_t*)blobs[0] == 0x31525143u) {
             // "CQR1": a row-returning join's rows from every rank, merged in the
             // reference's nested-loop order by their global (left id, right id) keys
@@ -5916,7 +6034,9 @@ cq_table* cqgpu_merge_partials(cq_node* q, const void* const* blobs, const size_
                 for (auto& x : nm) x = r.str();
                 if (bi == 0) names = nm;
                 else if (nm != names) throw HipError{"partials from different plans"};
-                lmask |= r.u32();
+                const uint32_t lm = r.u32();
+                lmask |= lm;
+                rep_all &= lm;
                 rmask |= r.u32();
                 const uint64_t nr = r.u64();
                 for (uint64_t i = 0; i < nr; i++) {
@@ -5929,7 +6049,7 @@ cq_table* cqgpu_merge_partials(cq_node* q, const void* const* blobs, const size_
             }
             for (int x = 1; x < 4; x++)           // value_compare's cross-class "equal" (csv_reader.c:128)
                 for (int y = 1; y < 4; y++)
-                    if (x != y && (lmask >> x & 1) && (rmask >> y & 1))
+                    if (x != y && (lmask >> x & 1) && (rmask >> y & 1) && !rep_all)
                         throw Ineligible{"join keys of different value classes across partials"};
             if (all.size() > (size_t)INT32_MAX) throw Ineligible{"more than 2^31-1 result rows"};
             std::stable_sort(all.begin(), all.end(), [](const Row& a, const Row& b) { return a.key < b.key; });
@@ -5958,7 +6078,12 @@ cq_table* cqgpu_merge_partials(cq_node* q, const void* const* blobs, const size_
             for (uint32_t a = 0; a < na; a++) pt.classes.push_back(r.u32());
             const uint32_t nr = r.u32();
             const uint32_t nv = r.u32();
-            if (magic == 0x314a5143u) { lmask |= r.u32(); rmask |= r.u32(); }
+            if (magic == 0x314a5143u) {
+                const uint32_t lm = r.u32();
+                lmask |= lm;
+                rep_all &= lm;
+                rmask |= r.u32();
+            }
             if (bi == 0) { nacc = na; nrep = nr; nvla = nv; }
             else if (pt.names != parts[0].names || na != nacc || nr != nrep || nv != nvla)
                 throw HipError{"partials from different plans"};
@@ -6000,10 +6125,11 @@ cq_table* cqgpu_merge_partials(cq_node* q, const void* const* blobs, const size_
         const bool joined = magic0 == 0x314a5143u;
         if (joined) {
             // value_compare calls keys of different non-NULL classes equal (csv_reader.c:128):
-            // such pairs span ranks after a hash repartition, so the plan is refused
+            // such pairs span ranks after a plain hash repartition, so the plan is refused
+            // unless every partial's sides were routed with replication (cqgpu_route_plan2)
             for (int x = 1; x < 4; x++)
                 for (int y = 1; y < 4; y++)
-                    if (x != y && (lmask >> x & 1) && (rmask >> y & 1))
+                    if (x != y && (lmask >> x & 1) && (rmask >> y & 1) && !rep_all)
                         throw Ineligible{"join keys of different value classes across partials"};
         }
         cqgpu_table meta;
@@ -7183,7 +7309,7 @@ uint32_t typed_receive(DevCtx& c, const TypedJoin& tj, const void* ub, uint64_t 
         if (grouped) {
             // the tag's bytes (fast_kernel's tag: zero padded, (1 << 32) for the empty field)
             const unsigned long long tag = ht[s];
-            uint8_t b[8];
+            uint8_t b[8] = {0, 0, 0, 0, 0, 0, 0, 0};
             uint32_t len = 0;
             if (tag != (1ull << 32)) {
                 for (uint32_t j = 0; j < 8; j++) {
@@ -7197,7 +7323,11 @@ uint32_t typed_receive(DevCtx& c, const TypedJoin& tj, const void* ub, uint64_t 
             x.klen = k.len;
             x.kw0 = k.w0;
             x.kw1 = k.w1;
-            if (k.cls == GK_STR) x.kbytes.assign((const char*)b, std::min<uint32_t>(k.len, 8));
+            if (k.cls == GK_STR) {                      // the key's text (a NULL key's is "NULL")
+                char kt[16];
+                for (uint32_t j = 0; j < 16; j++) kt[j] = (char)((j < 8 ? k.w0 >> (8 * j) : k.w1 >> (8 * (j - 8))) & 0xFF);
+                x.kbytes.assign(kt, std::min<uint32_t>(k.len, 16));
+            }
             HCell rep;
             rep.kind = cell.kind;
             rep.bits = cell.kind == K_STR ? 0 : cell.bits;
@@ -8196,18 +8326,71 @@ void dist_join(DevCtx& c, DistComm& m, cq_node* q, cqgpu_table* const* tables, i
     bool bad = false;
     struct TabFree { void operator()(cqgpu_table* t) const { if (t) cqgpu_table_free(t); } };
     std::vector<std::unique_ptr<cqgpu_table, TabFree>> routed;
+    auto plan_failed = [&]() {
+        bad = true;
+        err = g_err.empty() ? g_inel : g_err;
+        if (!g_inel.empty()) err = "query outside the GPU executor's subset: " + g_inel;
+    };
+    // the routing mode, agreed before either side moves (cqgpu_route_plan2): a JOIN
+    // without ON keeps side 0 and sends side 1 to every rank; keys of several value
+    // classes (value_compare's cross-class "equal", csv_reader.c:126-129) route the
+    // majority class by key and replicate the others.  Both sides' mode-0 plans give
+    // the class counts; they are kept when the mode stays 0.
+    cq_node* j0 = q && q->kind == CQ_N_QUERY && q->u.q.join_count > 0 ? q->u.q.joins[0] : nullptr;
+    const bool cross = j0 && j0->kind == CQ_N_JOIN && j0->u.join.on == nullptr;
+    uint32_t mode = 0;
+    std::unique_ptr<RouteState> pre[2];
+    std::vector<uint64_t> pre_nb[2], pre_nr[2];
+    if (!cross) {
+        uint64_t cc[2][4] = {{0, 0, 0, 0}, {0, 0, 0, 0}};
+        for (int side = 0; side < 2 && !bad; side++) {
+            pre_nb[side].assign(N, 0);
+            pre_nr[side].assign(N, 0);
+            if (cqgpu_route_plan2(q, tables, ntables, side, N, m.rank, 0, pre_nb[side].data(), pre_nr[side].data(),
+                                  cc[side]) < 0)
+                plan_failed();
+            else
+                pre[side] = std::move(tables[side]->route);    // (tables[0] may be tables[1]: a self-join)
+        }
+        std::vector<uint64_t> mine(9, 0), all(9 * (size_t)N, 0);
+        for (int k = 0; k < 4; k++) { mine[k] = cc[0][k]; mine[4 + k] = cc[1][k]; }
+        mine[8] = bad ? 1 : 0;
+        {
+            DevBuf dc(9 * 8 * (N + 1));
+            uint64_t* dp = dc.as<uint64_t>();
+            HIPCHECK(hipMemcpyAsync(dp + 9 * N, mine.data(), 9 * 8, hipMemcpyHostToDevice, c.stream));
+            m.be->all_gather(dp + 9 * N, dp, 9, CD_U64, c.stream);
+            HIPCHECK(hipMemcpyAsync(all.data(), dp, 9 * N * 8, hipMemcpyDeviceToHost, c.stream));
+            HIPCHECK(hipStreamSynchronize(c.stream));
+        }
+        uint64_t lc[4] = {0, 0, 0, 0}, rc[4] = {0, 0, 0, 0};
+        for (int r = 0; r < N; r++) {
+            if (all[(size_t)r * 9 + 8]) throw PeerFail{bad ? err : std::string("a peer rank failed")};
+            for (int k = 0; k < 4; k++) { lc[k] += all[(size_t)r * 9 + k]; rc[k] += all[(size_t)r * 9 + 4 + k]; }
+        }
+        mode = cqgpu_route_major(lc, rc);
+        if (mode) pre[0].reset(), pre[1].reset();     // re-planned with the mode below
+    }
     for (int side = 0; side < 2; side++) {
         std::vector<uint64_t> nb(N, 0), nr(N, 0);
-        if (!bad && cqgpu_route_plan(q, tables, ntables, side, N, nb.data(), nr.data()) != 0) {
-            bad = true;
-            err = g_err.empty() ? g_inel : g_err;
-            if (!g_inel.empty()) err = "query outside the GPU executor's subset: " + g_inel;
+        uint64_t nown = 0;                         // this rank's records of the side (global id span)
+        if (!bad && pre[side]) {
+            nb = pre_nb[side];
+            nr = pre_nr[side];
+            nown = pre[side]->n;
+            tables[side]->route = std::move(pre[side]);
+        } else if (!bad) {
+            const int64_t n = cqgpu_route_plan2(q, tables, ntables, side, N, m.rank, mode, nb.data(), nr.data(),
+                                                nullptr);
+            if (n < 0) plan_failed();
+            else nown = (uint64_t)n;
         }
-        // all ranks' counts: [nb(N), nr(N), bad] per rank
-        const size_t W = 2 * (size_t)N + 1;
+        // all ranks' counts: [nb(N), nr(N), bad, own records] per rank
+        const size_t W = 2 * (size_t)N + 2;
         std::vector<uint64_t> mine(W, 0), all(W * N, 0);
         for (int d = 0; d < N; d++) { mine[d] = bad ? 0 : nb[d]; mine[N + d] = bad ? 0 : nr[d]; }
         mine[2 * N] = bad ? 1 : 0;
+        mine[2 * N + 1] = bad ? 0 : nown;
         {
             DevBuf dc(W * 8 * (N + 1));
             uint64_t* dp = dc.as<uint64_t>();
@@ -8225,8 +8408,7 @@ void dist_join(DevCtx& c, DistComm& m, cq_node* q, cqgpu_table* const* tables, i
         uint64_t base = 0, total = 0;
         std::vector<uint64_t> sb(N + 1, 0), sr(N + 1, 0), rb(N + 1, 0), rr(N + 1, 0);
         for (int r = 0; r < N; r++) {
-            uint64_t recs = 0;
-            for (int d = 0; d < N; d++) recs += all[(size_t)r * W + N + d];
+            const uint64_t recs = all[(size_t)r * W + 2 * N + 1];
             if (r < m.rank) base += recs;
             total += recs;
         }
@@ -8302,6 +8484,9 @@ void dist_join(DevCtx& c, DistComm& m, cq_node* q, cqgpu_table* const* tables, i
         if (t) {
             t->gid_total = total;
             t->key_stride = (uint32_t)N;
+            t->rep_major = cross ? 0u : mode;
+            t->bcast = cross && side == 1;
+            t->rep_owner = m.rank == 0;
         }
     }
     std::vector<cqgpu_table*> tabs;

@@ -276,9 +276,12 @@ __device__ __forceinline__ unsigned long long wave_incl_len(uint32_t x, bool wid
     return wide ? wave_incl_u64(x, lane) : (unsigned long long)wave_incl_u32(x);
 }
 
+// dest == nranks (BCAST): the record goes to every rank (a replicated join record,
+// cqgpu_route_plan2) -- it is counted in every destination's run of its wave, so each
+// destination's region stays in file order
 __global__ __launch_bounds__(256) void route_runs_kernel(const uint32_t* __restrict__ dest,
                                                          const uint32_t* __restrict__ len, uint32_t n, uint32_t nw,
-                                                         unsigned long long* __restrict__ rcnt,
+                                                         uint32_t nranks, unsigned long long* __restrict__ rcnt,
                                                          unsigned long long* __restrict__ rbytes) {
     const uint32_t lane = threadIdx.x & 63;
     const uint64_t i = (uint64_t)blockIdx.x * 256 + threadIdx.x;
@@ -288,6 +291,18 @@ __global__ __launch_bounds__(256) void route_runs_kernel(const uint32_t* __restr
     const uint32_t d = valid ? dest[i] : ~0u;
     const uint32_t m = valid ? len[i] : 0u;
     const bool wide = __ballot(m >= (1u << 25)) != 0;
+    if (__ballot(d == nranks) != 0) {                    // broadcast records: every destination in turn
+        for (uint32_t d0 = 0; d0 < nranks; d0++) {
+            const bool mine = valid && (d == d0 || d == nranks);
+            const uint64_t mk = __ballot(mine);
+            const unsigned long long b = wave_incl_len(mine ? m : 0u, wide, lane);
+            if (lane == 63) {
+                rcnt[(uint64_t)d0 * nw + w] = (unsigned long long)__popcll(mk);
+                rbytes[(uint64_t)d0 * nw + w] = b;
+            }
+        }
+        return;
+    }
     bool todo = valid;
     for (;;) {                                           // one trip per destination present
         const uint64_t pend = __ballot(todo);
@@ -308,7 +323,7 @@ __global__ __launch_bounds__(256) void route_scatter_kernel(const uint8_t* __res
                                                             const unsigned long long* __restrict__ recs,
                                                             const uint32_t* __restrict__ dest,
                                                             const uint32_t* __restrict__ len, uint32_t n, uint32_t nw,
-                                                            uint64_t end,
+                                                            uint32_t nranks, uint64_t end,
                                                             const unsigned long long* __restrict__ cbase,
                                                             const unsigned long long* __restrict__ bbase,
                                                             uint64_t gid_base, uint8_t* __restrict__ out,
@@ -337,10 +352,40 @@ __global__ __launch_bounds__(256) void route_scatter_kernel(const uint8_t* __res
     const uint32_t d = valid ? dest[i] : ~0u;
     const uint32_t m = valid ? len[i] : 0u;
     const unsigned long long src = valid ? recs[i] : 0ull;
-    unsigned long long dst = 0;
-    bool todo = valid;
     const uint64_t below = lane ? (~0ull >> (64 - lane)) : 0ull;
     const bool wide = __ballot(m >= (1u << 25)) != 0;
+    const uint32_t grp = lane >> 4, sub = lane & 15;
+    // four records at a time, 16 lanes each (lane k of a group moves bytes k, k + 16, ...)
+    auto copy = [&](unsigned long long dst, uint32_t mlen) {
+        for (uint32_t r = 0; r < 64; r += 4) {
+            const int from = (int)(r + grp);
+            const unsigned long long s = __shfl(src, from, 64);
+            const unsigned long long t = __shfl(dst, from, 64);
+            const uint32_t mm = (uint32_t)__shfl((int)mlen, from, 64);     // 0 past n / not sent
+            if (fits)
+                for (uint32_t k = sub; k < mm; k += 16) out[t + k] = k + 1 == mm ? (uint8_t)'\n' : L[s - a + k];
+            else
+                for (uint32_t k = sub; k < mm; k += 16) out[t + k] = k + 1 == mm ? (uint8_t)'\n' : g[s + k];
+        }
+    };
+    if (__ballot(d == nranks) != 0) {                    // broadcast records: one copy per destination
+        for (uint32_t d0 = 0; d0 < nranks; d0++) {
+            const bool mine = valid && (d == d0 || d == nranks);
+            const uint64_t mk = __ballot(mine);
+            const uint32_t x = mine ? m : 0u;
+            const unsigned long long pre = wave_incl_len(x, wide, lane) - x;
+            unsigned long long dst = 0;
+            if (mine) {
+                const uint64_t at = (uint64_t)d0 * nw + w;
+                dst = bbase[at] + pre;
+                gids[cbase[at] + (uint64_t)__popcll(mk & below)] = gid_base + i;
+            }
+            copy(dst, x);
+        }
+        return;
+    }
+    unsigned long long dst = 0;
+    bool todo = valid;
     for (;;) {
         const uint64_t pend = __ballot(todo);
         if (!pend) break;
@@ -356,18 +401,7 @@ __global__ __launch_bounds__(256) void route_scatter_kernel(const uint8_t* __res
         }
         todo = todo && !mine;
     }
-    // four records at a time, 16 lanes each (lane k of a group moves bytes k, k + 16, ...)
-    const uint32_t grp = lane >> 4, sub = lane & 15;
-    for (uint32_t r = 0; r < 64; r += 4) {
-        const int from = (int)(r + grp);
-        const unsigned long long s = __shfl(src, from, 64);
-        const unsigned long long t = __shfl(dst, from, 64);
-        const uint32_t mm = (uint32_t)__shfl((int)m, from, 64);     // 0 past n
-        if (fits)
-            for (uint32_t k = sub; k < mm; k += 16) out[t + k] = k + 1 == mm ? (uint8_t)'\n' : L[s - a + k];
-        else
-            for (uint32_t k = sub; k < mm; k += 16) out[t + k] = k + 1 == mm ? (uint8_t)'\n' : g[s + k];
-    }
+    copy(dst, m);
 }
 
 // starts[0..nranks]: each destination's first send-buffer record (starts[nranks] = n);
@@ -543,6 +577,19 @@ __global__ void outer_global_kernel(unsigned int* __restrict__ unm, uint32_t n, 
     if (gset) unm[i] = emit && !gset[i] ? 1u : 0u;
 }
 
+// cqgpu_route_plan2's destinations beyond the key routing: fixed != ~0 sends every
+// record there (a JOIN without ON: the FROM side to its own rank, the JOIN side to
+// every rank = nranks); rep (1-3) sends each non-NULL key of another value class to
+// every rank (value_compare calls keys of different classes "equal",
+// csv_reader.c:126-129, so such a record may match on any rank)
+__global__ void route_dest_mode_kernel(const uint32_t* __restrict__ cls, uint32_t n, uint32_t nranks, uint32_t rep,
+                                       uint32_t fixed, uint32_t* __restrict__ dest) {
+    const uint32_t i = blockIdx.x * blockDim.x + threadIdx.x;
+    if (i >= n) return;
+    if (fixed != ~0u) dest[i] = fixed;
+    else if (rep && cls[i] && cls[i] != rep) dest[i] = nranks;
+}
+
 inline uint32_t blocks(uint64_t n, uint32_t b) { return (uint32_t)((n + b - 1) / b); }
 
 }  // namespace
@@ -586,10 +633,16 @@ hipError_t cq_launch_gather_len(const uint32_t* len, const uint32_t* order, uint
     return hipGetLastError();
 }
 
-hipError_t cq_launch_route_runs(const uint32_t* dest, const uint32_t* len, uint32_t n, uint32_t nw,
+hipError_t cq_launch_route_dest_mode(const uint32_t* cls, uint32_t n, uint32_t nranks, uint32_t rep, uint32_t fixed,
+                                    uint32_t* dest, hipStream_t s) {
+    if (!n) return hipSuccess;
+    route_dest_mode_kernel<<<blocks(n, 256), 256, 0, s>>>(cls, n, nranks, rep, fixed, dest);
+    return hipGetLastError();
+}
+hipError_t cq_launch_route_runs(const uint32_t* dest, const uint32_t* len, uint32_t n, uint32_t nw, uint32_t nranks,
                                 unsigned long long* rcnt, unsigned long long* rbytes, hipStream_t s) {
     if (!n) return hipSuccess;
-    route_runs_kernel<<<blocks((uint64_t)nw * 64, 256), 256, 0, s>>>(dest, len, n, nw, rcnt, rbytes);
+    route_runs_kernel<<<blocks((uint64_t)nw * 64, 256), 256, 0, s>>>(dest, len, n, nw, nranks, rcnt, rbytes);
     return hipGetLastError();
 }
 hipError_t cq_launch_route_run_starts(const unsigned long long* cbase, const unsigned long long* bbase,
@@ -601,12 +654,12 @@ hipError_t cq_launch_route_run_starts(const unsigned long long* cbase, const uns
     return hipGetLastError();
 }
 hipError_t cq_launch_route_scatter(const uint8_t* g, const unsigned long long* recs, const uint32_t* dest,
-                                   const uint32_t* len, uint32_t n, uint32_t nw, uint64_t end,
+                                   const uint32_t* len, uint32_t n, uint32_t nw, uint32_t nranks, uint64_t end,
                                    const unsigned long long* cbase, const unsigned long long* bbase, uint64_t gid_base,
                                    uint8_t* out, unsigned long long* gids, hipStream_t s) {
     if (!n) return hipSuccess;
-    route_scatter_kernel<<<blocks((uint64_t)nw * 64, 256), 256, 0, s>>>(g, recs, dest, len, n, nw, end, cbase,
-                                                                        bbase, gid_base, out, gids);
+    route_scatter_kernel<<<blocks((uint64_t)nw * 64, 256), 256, 0, s>>>(g, recs, dest, len, n, nw, nranks, end,
+                                                                        cbase, bbase, gid_base, out, gids);
     return hipGetLastError();
 }
 // A fused-join partial's packed groups (scan.hip pack layout: group i's record at

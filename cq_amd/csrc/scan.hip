@@ -1920,6 +1920,22 @@ __global__ void join_cross_kernel(uint32_t na, uint32_t nb, unsigned long long n
         pairs[i] = make_uint2((uint32_t)(i / nb), (uint32_t)(i % nb));
 }
 
+// A repartitioned join whose keys mix value classes (cqgpu_route_plan2's replication):
+// every non-NULL key of a class other than `major` was sent to every rank, so a pair
+// of two such records is found on every rank; flags[i] = 0 for those pairs (the
+// rank that owns them keeps them: not called there), 1 for every other pair.  An
+// unmatched side (JOIN_NONE) never occurs: outer joins are refused in this mode.
+__global__ void pair_rep_flags_kernel(const uint2* __restrict__ pairs, unsigned long long np,
+                                      const Cell* __restrict__ L, uint32_t ls, uint32_t lk,
+                                      const Cell* __restrict__ R, uint32_t rs, uint32_t rk, uint32_t major,
+                                      unsigned int* __restrict__ flags) {
+    const unsigned long long i = (unsigned long long)blockIdx.x * blockDim.x + threadIdx.x;
+    if (i >= np) return;
+    const uint2 p = pairs[i];
+    const uint32_t a = key_class(L[(uint64_t)p.x * ls + lk]), b = key_class(R[(uint64_t)p.y * rs + rk]);
+    flags[i] = (a != 0u && a != major && b != 0u && b != major) ? 0u : 1u;
+}
+
 // the plan's need slots of one joined row: in registers (plans over <= MAX_NEED
 // columns), or a view of the cell tables (wide plans)
 __device__ __forceinline__ void join_cells(const JoinMap& M, const Cell* L, const Cell* R, uint2 pr,
@@ -3173,6 +3189,14 @@ hipError_t cq_launch_join_fill(const unsigned int* flags, const unsigned int* po
     if (!n) return hipSuccess;
     hipLaunchKernelGGL(cq::join_fill_kernel, dim3(grid_of(n, 256)), dim3(256), 0, s, flags, pos, n, base, right_side,
                        pairs);
+    return hipGetLastError();
+}
+hipError_t cq_launch_pair_rep_flags(const uint2* pairs, unsigned long long np, const cq::Cell* L, uint32_t ls,
+                                    uint32_t lk, const cq::Cell* R, uint32_t rs, uint32_t rk, uint32_t major,
+                                    unsigned int* flags, hipStream_t s) {
+    if (!np) return hipSuccess;
+    hipLaunchKernelGGL(cq::pair_rep_flags_kernel, dim3((unsigned)((np + 255) / 256)), dim3(256), 0, s, pairs, np, L, ls,
+                       lk, R, rs, rk, major, flags);
     return hipGetLastError();
 }
 hipError_t cq_launch_join_cross(uint32_t na, uint32_t nb, uint2* pairs, hipStream_t s) {

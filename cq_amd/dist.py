@@ -422,6 +422,12 @@ def outer_sets(ast, tables, nlevels: int, comm) -> None:
         agree(err, comm)
 
 
+def first_join_cross(ast) -> bool:
+    """the plan's first JOIN has no ON (a cross join: side 1 goes to every rank)"""
+    q = ast.contents.u.q
+    return q.join_count > 0 and not q.joins[0].contents.u.join.on
+
+
 def join_partitioned(ast, lshard, rshard, lheader: bytes, rheader: bytes, device: torch.device | str,
                      comm_device: torch.device | str | None = None, rest=()):
     """Repartitioned JOIN over this rank's shards of both inputs of the first JOIN.
@@ -446,12 +452,25 @@ def join_partitioned(ast, lshard, rshard, lheader: bytes, rheader: bytes, device
         finally:
             cq_amd.join_outer_clear()
     comm = torch.device(comm_device) if comm_device is not None else torch.device(device)
+    cross = first_join_cross(ast)
+    mode = 0
+    if not cross:
+        # the routing mode (cqgpu_route_plan2): keys of several value classes route the
+        # majority class by key and replicate the others -- agreed from every rank's
+        # class counts of both sides before anything moves
+        counts, err = _local(lambda: [cq_amd.route_plan2(ast, [lshard, rshard], s, world, rank)[3]
+                                      for s in (0, 1)])
+        agree(err, comm)
+        t = torch.tensor(counts[0] + counts[1], dtype=torch.int64, device=comm)
+        dist.all_reduce(t)
+        tot = [int(x) for x in t.cpu()]
+        mode = cq_amd.route_major(tot[:4], tot[4:])
     routed = []
     for side, (tab, header) in enumerate(((lshard, lheader), (rshard, rheader))):
-        plan, err = _local(cq_amd.route_plan, ast, [lshard, rshard], side, world)
+        plan, err = _local(cq_amd.route_plan2, ast, [lshard, rshard], side, world, rank, mode)
         agree(err, comm)
-        nbytes, nrecs = plan
-        base, total = base_and_total(sum(nrecs), comm)
+        nbytes, nrecs, nown, _ = plan
+        base, total = base_and_total(nown, comm)
 
         def fill():
             b = torch.empty(max(sum(nbytes), 1), dtype=torch.uint8, device=device)
@@ -470,7 +489,8 @@ def join_partitioned(ast, lshard, rshard, lheader: bytes, rheader: bytes, device
         if t is not None:
             _, e2 = _local(cq_amd.table_set_record_total, t, total)
             _, e3 = _local(cq_amd.table_set_key_stride, t, world)   # whole keys routed by key mod N
-            err = err or e2 or e3
+            _, e4 = _local(cq_amd.table_set_replicated, t, (4 if side == 1 else 0) if cross else mode, rank == 0)
+            err = err or e2 or e3 or e4
         agree(err, comm)
         routed.append(t)
     try:

@@ -275,6 +275,33 @@ cq_table* cqgpu_gm_local(cq_node* query_ast, cqgpu_table* const* shards, int n);
  * cqgpu_last_error() / cqgpu_last_ineligible() set. */
 int cqgpu_route_plan(cq_node* query_ast, cqgpu_table* const* tables, int ntables, int side, int nranks,
                      uint64_t* bytes_per_rank, uint64_t* recs_per_rank);
+/* route_plan2: route_plan for the caller's `rank` with a routing mode, which lifts
+ * two refusals of route_plan:
+ *  - keys of different value classes (value_compare calls any two non-NULL keys of
+ *    different classes equal, csv_reader.c:126-129, used by the join at
+ *    evaluator_joins.c:53-55): mode = cqgpu_route_major(every rank's class counts of
+ *    both sides); keys of class `mode` and NULL keys route by key as before, every
+ *    other record goes to EVERY rank (in each destination's region, file order kept);
+ *  - a JOIN without ON (every pair matches, evaluator_joins.c:41): side 0's records
+ *    stay on `rank`, side 1's go to every rank (mode ignored).
+ * class_counts (optional, 4 entries): this side's ON keys per value class (NULL,
+ * number, string, date) -- mode 0's plan returns them for the agreement.  The
+ * receiver marks both rebuilt sides with cqgpu_table_set_replicated.  N <= 64.
+ * Returns this side's record count on this rank (the span of its global ids: a
+ * replicated record counts once, though it is in every destination's count), or -1. */
+int64_t cqgpu_route_plan2(cq_node* query_ast, cqgpu_table* const* tables, int ntables, int side, int nranks,
+                          int rank, uint32_t mode, uint64_t* bytes_per_rank, uint64_t* recs_per_rank,
+                          uint64_t* class_counts);
+/* the routing mode for every rank's summed class counts of the two sides: 0 when no
+ * pair of keys of different non-NULL classes can occur, else the class (1-3) most
+ * keys hold (it routes by key; the others are replicated) */
+uint32_t cqgpu_route_major(const uint64_t* left_class_counts, const uint64_t* right_class_counts);
+/* a routed side's replication, for cqgpu_query_partial: mode 0 none, 1-3 the
+ * route_plan2 mode (a pair of two replicated records is found on every rank and kept
+ * only where owner != 0; outer joins are refused in this mode), 4 every record of
+ * this side is on every rank (a JOIN without ON's side 1; owner != 0: this rank
+ * emits a RIGHT / FULL join's unmatched rows).  Exactly one rank passes owner = 1. */
+int cqgpu_table_set_replicated(cqgpu_table* t, uint32_t mode, int owner);
 /* route_fill: writes the planned send buffer into device memory: records grouped
  * by destination rank (file order within a rank, each '\n'-terminated) into
  * dev_bytes, and their global record ids (gid_base + local record index) into

@@ -71,6 +71,24 @@ def files(tmp_path_factory):
     out["roles"] = os.path.join(d, "roles.csv")
     with open(out["roles"], "w") as fh:
         fh.write("role,dept\n" + "".join("role_%03d,dept%d\n" % (i, i % 7) for i in range(0, 1000, 3)))
+    # join keys mixing value classes (numbers, strings, dates, NULL) on both sides, and a
+    # small table for JOINs without ON
+    def mk_key(r):
+        k = int(r.integers(0, 10))
+        if k < 5:
+            return str(int(r.integers(0, 40))) if k else f"{int(r.integers(0, 40))}.0"
+        if k < 8:
+            return "s%02d" % int(r.integers(0, 25))
+        return "" if k == 8 else "2021-03-%02d" % int(r.integers(1, 9))
+    out["mk"] = os.path.join(d, "mk.csv")
+    with open(out["mk"], "w") as fh:
+        fh.write("k,v,g\n" + "".join(f"{mk_key(rng)},{i},{i % 3}\n" for i in range(300)))
+    out["mk2"] = os.path.join(d, "mk2.csv")
+    with open(out["mk2"], "w") as fh:
+        fh.write("k,w\n" + "".join(f"{mk_key(rng)},{i}\n" for i in range(150)))
+    out["qt"] = os.path.join(d, "qt.csv")
+    with open(out["qt"], "w") as fh:
+        fh.write("q,label\n0,lab0\n2,lab2\n1,lab1\n2,lab2b\n9,lab9\n")
     out["many"] = os.path.join(d, "many.csv")
     with open(out["many"], "w") as fh:
         fh.write("k,v\n" + "\n".join("%d,%d" % (i % 9000, i % 7) for i in range(40_000)) + "\n")
@@ -207,6 +225,39 @@ JOINS = [   # the repartitioned JOIN step inside the library (cqgpu_dist_join)
     ("SELECT COUNT(*), MIN(r.role), MAX(u.name) FROM '{p}' AS u JOIN '{q}' AS o ON u.id = o.customer_id "
      "FULL JOIN '{r}' AS r ON u.role = r.role", ["users", "orders", "roles"]),
 ]
+
+
+JOINS_X = [   # mixed key classes (the minority classes replicated) and JOINs without ON
+    ("SELECT a.g, COUNT(*), SUM(b.w), MAX(b.k) FROM '{p}' AS a JOIN '{q}' AS b ON a.k = b.k GROUP BY a.g",
+     ["mk", "mk2"]),
+    ("SELECT a.v, b.w FROM '{p}' AS a JOIN '{q}' AS b ON a.k = b.k WHERE b.w < 40", ["mk", "mk2"]),
+    ("SELECT u.role, COUNT(*), MAX(b.label) FROM '{p}' AS u JOIN '{q}' AS b GROUP BY u.role", ["users", "qt"]),
+    ("SELECT COUNT(*), SUM(u.age) FROM '{p}' AS u RIGHT JOIN '{q}' AS b", ["users", "qt"]),
+    ("SELECT b.label, COUNT(*) FROM '{p}' AS u JOIN '{q}' AS b JOIN '{r}' AS c ON b.q = c.q GROUP BY b.label",
+     ["mk2", "qt", "qt"]),
+]
+
+
+@pytest.mark.parametrize("world", [1, 2, 3])
+def test_dist_join_mixed_and_cross(files, tmp_path, world):
+    """cqgpu_dist_join's agreed routing mode (cqgpu_route_plan2): keys of several value
+    classes and JOINs without ON at world size 1 over RCCL and 2 / 3 over the host
+    backend, against the oracle"""
+    if world == 1:
+        res = _dist_run_paths(files, tmp_path, JOINS_X)
+        per = None
+    else:
+        res, per = _host_run(files, tmp_path, JOINS_X, world, paths_of=True)
+    for i, ((sql, keys), r) in enumerate(zip(JOINS_X, res)):
+        q = sql.format(**dict(zip("pqrs", [files[k] for k in keys])))
+        assert r["status"] == 0, (q, r["error"])
+        if per:
+            assert all(pr[i]["status"] == 0 for pr in per), (q, per)
+        want, unsup = cqtest.oracle_query(q)
+        assert not unsup
+        with cqtest.Parsed(q) as ast:
+            tol = tolerant_columns(ast)
+        compare(_as_got(r), want, tol, f"dist_join {world} ranks: {q}")
 
 
 def test_dist_join_one_rank_rccl(files, tmp_path):

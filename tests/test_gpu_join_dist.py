@@ -18,6 +18,7 @@ import torch
 import cqtest
 import cq_amd
 from cq_amd import abi, datagen
+from cq_amd.dist import first_join_cross
 from test_gpu_parity import compare, tolerant_columns
 
 pytestmark = pytest.mark.gpu
@@ -28,7 +29,7 @@ def _shards(data: bytes, nranks: int, seed: int, cfg=None):
     header += b"\n"
     rng = np.random.default_rng(seed)
     fr = sorted(rng.uniform(0.05, 0.95, nranks - 1)) if nranks > 1 else []
-    cuts = [0] + [body.index(b"\n", int(len(body) * f)) + 1 for f in fr] + [len(body)]
+    cuts = [0] + [body.index(b"\n", int(len(body) * f)) + 1 if body else 0 for f in fr] + [len(body)]
     tabs = []
     for r in range(nranks):
         pc = body[cuts[r]:cuts[r + 1]]
@@ -40,6 +41,7 @@ def _shards(data: bytes, nranks: int, seed: int, cfg=None):
 
 
 LAST_KINDS = []   # per rank, the scan kernel kind of its partial (4: the STAR fused join)
+LAST_MODE = [0]   # the routing mode of the last _run (cqgpu_route_major)
 LAST_BLOBS = []   # per rank, its partial blob
 
 
@@ -52,16 +54,27 @@ def _run(ast, ldata: bytes, rdata: bytes, nranks: int, rest=(), outer=True, cfg=
     rh, rs = _shards(rdata, nranks, 2, cfg)
     routed = [[None, None] for _ in range(nranks)]
     keep = []
+    # the routing mode every rank agrees on (cq_amd.dist.join_partitioned's sequence):
+    # a JOIN without ON sends side 1 everywhere; mixed key classes replicate the minority
+    cross = first_join_cross(ast)
+    mode = 0
+    if not cross:
+        tot = np.zeros(8, dtype=np.int64)
+        for r in range(nranks):
+            for side in (0, 1):
+                tot[4 * side: 4 * side + 4] += cq_amd.route_plan2(ast, [ls[r], rs[r]], side, nranks, r)[3]
+        mode = cq_amd.route_major([int(x) for x in tot[:4]], [int(x) for x in tot[4:]])
+    LAST_MODE[:] = [mode]
     for side, (hdr, sh) in enumerate(((lh, ls), (rh, rs))):
-        plans = [cq_amd.route_plan(ast, [ls[r], rs[r]], side, nranks) for r in range(nranks)]
-        total = sum(sum(nr) for _, nr in plans)
+        plans = [cq_amd.route_plan2(ast, [ls[r], rs[r]], side, nranks, r, mode) for r in range(nranks)]
+        total = sum(p[2] for p in plans)
         sends, base = [], 0
         for r in range(nranks):
-            nb, nr = plans[r]
+            nb, nr, nown, _ = plans[r]
             sb = torch.empty(max(sum(nb), 1), dtype=torch.uint8, device="cuda")
             sg = torch.empty(max(sum(nr), 1), dtype=torch.int64, device="cuda")
             cq_amd.route_fill(sh[r], base, sb.data_ptr(), sg.data_ptr())
-            base += sum(nr)
+            base += nown
             bo = np.concatenate([[0], np.cumsum(nb)]).astype(int)
             ro = np.concatenate([[0], np.cumsum(nr)]).astype(int)
             sends.append((sb, sg, bo, ro))
@@ -75,6 +88,7 @@ def _run(ast, ldata: bytes, rdata: bytes, nranks: int, rest=(), outer=True, cfg=
                                                        cfg)
             cq_amd.table_set_record_total(routed[d][side], total)
             cq_amd.table_set_key_stride(routed[d][side], nranks)
+            cq_amd.table_set_replicated(routed[d][side], (4 if side == 1 else 0) if cross else mode, d == 0)
     whole = [[cq_amd.Table.from_bytes(x, cfg=cfg) for x in rest] for _ in range(nranks)]
     sets = {}
 
@@ -135,6 +149,17 @@ def files(tmp_path_factory):
     f["sb"] = ("k,w\n" + "".join(f"{'' if i % 53 == 0 else 'key%03d' % (i % 170)},{i * 3}\n"
                                   for i in range(700))).encode()
     f["mixed"] = b"k,z\n1,a\nx,b\n2,c\n,d\n2020-01-02,e\nx,f\n1.0,g\n"
+    # larger mixed-class key columns: numbers (INTEGER and DOUBLE spellings), strings,
+    # dates and NULLs on both sides
+    def mk_key(r):
+        k = int(r.integers(0, 10))
+        if k < 5:
+            return str(int(r.integers(0, 40))) if k else f"{int(r.integers(0, 40))}.0"
+        if k < 8:
+            return "s%02d" % int(r.integers(0, 25))
+        return "" if k == 8 else "2021-03-%02d" % int(r.integers(1, 9))
+    f["mk"] = ("k,v,g\n" + "".join(f"{mk_key(rng)},{i},{i % 3}\n" for i in range(300))).encode()
+    f["mk2"] = ("k,w\n" + "".join(f"{mk_key(rng)},{i}\n" for i in range(150))).encode()
     # a column mixing numbers, strings and dates (MIN/MAX keep the class of the
     # group's first non-NULL cell in nested-loop order, evaluator_aggregates.c:311-326)
     tags = ["12", "abc", "2020-01-01", "", "7.5", "zz", "1999-12-31", "-3", "b"]
@@ -514,43 +539,108 @@ def test_join_chain_right_later_needs_sets(files):
                 t.close()
 
 
-def test_mixed_key_classes_refused(files):
-    """value_compare's cross-class "equal" pairs cannot be hash-routed: the merge refuses"""
+MIXED = [   # keys of several value classes: value_compare calls any two non-NULL keys of
+    # different classes equal (csv_reader.c:126-129, the join's compare at
+    # evaluator_joins.c:53-55) -- the majority class routes by key, the others go to
+    # every rank, and a pair of two replicated records is kept by rank 0 only
+    ("mixed", "sa", "SELECT COUNT(*) FROM '{L}' AS a JOIN '{R}' AS b ON a.k = b.k"),
+    ("mk", "mk2", "SELECT COUNT(*), SUM(b.w), MIN(a.v) FROM '{L}' AS a JOIN '{R}' AS b ON a.k = b.k"),
+    ("mk", "mk2", "SELECT a.g, COUNT(*), SUM(b.w), MAX(b.k) FROM '{L}' AS a JOIN '{R}' AS b ON a.k = b.k "
+                  "GROUP BY a.g"),
+    ("mk", "mk2", "SELECT a.v, b.w, a.k, b.k FROM '{L}' AS a JOIN '{R}' AS b ON a.k = b.k WHERE b.w < 60"),
+    ("mk", "sa", "SELECT a.g, COUNT(*) FROM '{L}' AS a JOIN '{R}' AS b ON a.k = b.k GROUP BY a.g"),
+    ("mixed", "mixed", "SELECT a.z, b.z FROM '{L}' AS a JOIN '{R}' AS b ON a.k = b.k"),
+    ("mk", "mk2", "SELECT b.w, COUNT(*) FROM '{L}' AS a JOIN '{R}' AS b ON a.k = b.k JOIN '{C}' AS c "
+                  "ON a.g = c.q GROUP BY b.w ORDER BY b.w LIMIT 12"),
+]
+
+
+@pytest.mark.parametrize("nranks", [1, 2, 3, 5])
+@pytest.mark.parametrize("case", range(len(MIXED)))
+def test_mixed_key_classes_across_partials(files, case, nranks):
+    """mixed key classes across partials (cqgpu_route_plan2's replication) vs the oracle"""
     data, paths = files
-    sql = f"SELECT COUNT(*) FROM '{paths['mixed']}' AS a JOIN '{paths['sa']}' AS b ON a.k = b.k"
+    lk, rk, tmpl = MIXED[case]
+    sql = tmpl.replace("{L}", paths[lk]).replace("{R}", paths[rk]).replace("{C}", paths["qt"])
+    want, unsup = cqtest.oracle_query(sql)
+    assert not unsup, sql
     with cqtest.Parsed(sql) as ast:
-        tp = _run(ast, data["mixed"], data["sa"], 2)
-        assert not tp
-        assert "value classes" in cq_amd.last_ineligible()
+        rest = (data["qt"],) if "{C}" in tmpl else ()
+        tp = _run(ast, data[lk], data[rk], nranks, rest=rest)
+        assert tp, (cq_amd.last_error(), cq_amd.last_ineligible())
+        assert LAST_MODE[0] != 0, "the data mixes key classes: a replicated routing"
+        got = abi.table_to_py(tp)
+        cq_amd.result_free(tp)
+        tol = tolerant_columns(ast)
+    compare(got, want, tol, f"{sql} @ {nranks} ranks")
 
 
-def test_mixed_key_classes_refused_empty_side():
+def test_mixed_key_classes_empty_side():
     """ADVICE r1 layout: 5 ranks, a right side of three INTEGER keys, a left side of
-    the same INTEGER keys plus many STRING keys.  The routing sends the STRING rows
-    to ranks that receive no right rows; those ranks must still record their left
-    key classes, so the merge sees STRING (left) against INTEGER (right) and refuses
-    (value_compare's cross-class "equal" pairs cannot be hash-routed)"""
+    the same INTEGER keys plus many STRING keys: the STRING rows (the majority) route
+    by key, to ranks that receive no right rows, the INTEGER rows of the right side
+    go to every rank -- every cross-class pair exactly once, vs the oracle"""
     left = b"k,v\n" + b"".join(b"%s,%d\n" % ((b"%d" % (i % 3 + 1)) if i % 4 == 0 else (b"s%02d" % (i % 40)), i)
                                  for i in range(400))
     right = b"k,w\n1,10\n2,20\n3,30\n"
-    sql = "SELECT COUNT(*) FROM 'l' AS a JOIN 'r' AS b ON a.k = b.k"
+    want = {"count": 0}
+    for i in range(400):
+        want["count"] += 1 if i % 4 == 0 else 3      # an INTEGER key matches its own; a STRING key all three
+    sql = "SELECT COUNT(*), SUM(b.w) FROM 'l' AS a JOIN 'r' AS b ON a.k = b.k"
     with cqtest.Parsed(sql) as ast:
-        lh, ls = _shards(left, 5, 1)
-        rh, rs = _shards(right, 5, 2)
-        recv = []
-        for side, sh in ((0, ls), (1, rs)):
-            per = np.zeros(5, dtype=int)
-            for r in range(5):
-                _, nr = cq_amd.route_plan(ast, [ls[r], rs[r]], side, 5)
-                per += np.array(nr)
-            recv.append(per)
-        for t in ls + rs:
-            t.close()
-        # the layout the advice describes: some rank gets left rows (only STRING keys) and no right rows
-        assert any(recv[0][d] > 0 and recv[1][d] == 0 for d in range(5)), recv
-        tp = _run(ast, left, right, 5)
-        assert not tp
-        assert "value classes" in cq_amd.last_ineligible(), cq_amd.last_ineligible()
+        for n in (1, 2, 5):
+            tp = _run(ast, left, right, n)
+            assert tp, (cq_amd.last_error(), cq_amd.last_ineligible())
+            got = abi.table_to_py(tp)
+            cq_amd.result_free(tp)
+            s = sum(((i % 3 + 1) * 10) if i % 4 == 0 else 60 for i in range(400))
+            assert got["rows"][0][0][1] == want["count"], (n, got)
+            assert abs(got["rows"][0][1][1] - s) < 1e-6 * s, (n, got)
+            assert LAST_MODE[0] == 2, LAST_MODE      # strings are the majority class
+
+
+@pytest.mark.parametrize("kind", ["LEFT", "RIGHT", "FULL"])
+def test_mixed_key_classes_outer_refused(files, kind):
+    """an outer JOIN over mixed key classes across partials: its unmatched rows would
+    need every rank's matches -- refused on every rank, never approximated"""
+    data, paths = files
+    sql = f"SELECT COUNT(*) FROM '{paths['mixed']}' AS a {kind} JOIN '{paths['sa']}' AS b ON a.k = b.k"
+    with cqtest.Parsed(sql) as ast:
+        with pytest.raises(RuntimeError, match="outer JOIN over keys of different value classes"):
+            _run(ast, data["mixed"], data["sa"], 2)
+
+
+CROSS = [   # JOIN without ON (evaluator_joins.c:41: every pair matches): side 0 stays on its
+    # rank, side 1 goes to every rank; order keys (left id, right id) as ever
+    ("sa", "qt", "SELECT COUNT(*), SUM(b.q), MIN(a.k) FROM '{L}' AS a JOIN '{R}' AS b"),
+    ("du", "qt", "SELECT u.role, COUNT(*), MAX(b.label) FROM '{L}' AS u JOIN '{R}' AS b GROUP BY u.role"),
+    ("sa", "qt", "SELECT a.k, b.label FROM '{L}' AS a JOIN '{R}' AS b WHERE a.v < 40"),
+    ("sa", "ex", "SELECT a.k, b.dept FROM '{L}' AS a LEFT JOIN '{R}' AS b WHERE a.v < 30"),
+    ("sa", "qt", "SELECT COUNT(*), SUM(a.v) FROM '{L}' AS a RIGHT JOIN '{R}' AS b"),
+    ("ex", "qt", "SELECT b.q, b.label, a.role FROM '{L}' AS a RIGHT JOIN '{R}' AS b"),
+    ("ex", "qt", "SELECT COUNT(*), MAX(b.label) FROM '{L}' AS a FULL JOIN '{R}' AS b"),
+    ("sa", "qt", "SELECT b.label, COUNT(*) FROM '{L}' AS a JOIN '{R}' AS b JOIN '{C}' AS c ON b.q = c.q "
+                 "GROUP BY b.label"),
+]
+
+
+@pytest.mark.parametrize("nranks", [1, 2, 3])
+@pytest.mark.parametrize("case", range(len(CROSS)))
+def test_cross_join_across_partials(files, case, nranks):
+    """a JOIN without ON across partials (side 1 on every rank) vs the oracle"""
+    data, paths = files
+    lk, rk, tmpl = CROSS[case]
+    sql = tmpl.replace("{L}", paths[lk]).replace("{R}", paths[rk]).replace("{C}", paths["qt"])
+    want, unsup = cqtest.oracle_query(sql)
+    assert not unsup, sql
+    with cqtest.Parsed(sql) as ast:
+        rest = (data["qt"],) if "{C}" in tmpl else ()
+        tp = _run(ast, data[lk], data[rk], nranks, rest=rest)
+        assert tp, (cq_amd.last_error(), cq_amd.last_ineligible())
+        got = abi.table_to_py(tp)
+        cq_amd.result_free(tp)
+        tol = tolerant_columns(ast)
+    compare(got, want, tol, f"{sql} @ {nranks} ranks")
 
 
 def _project(rec: bytes, keep, last_keep, delim=b",", quote=b'"'):
