@@ -5,8 +5,8 @@ cd "$GRAFT_REPO_ROOT"
 export TMPDIR=/tmp
 OUT=gpurun_out/r6h
 mkdir -p $OUT
-timeout -k 10 500 python -u -m pytest tests/test_gpu_join_dist.py tests/test_gpu_dist_rccl.py -m gpu -x -q --timeout 200 \
-   --timeout-method thread -k "mixed or cross or repartitioned_join or chain or host_backend or one_rank" > $OUT/pt_x.log 2>&1
+timeout -k 10 500 python -u -m pytest tests/test_gpu_join_dist.py -m gpu -x -q --timeout 200 \
+   --timeout-method thread -k "typed" > $OUT/pt_x.log 2>&1
 rc=$?; echo "targeted rc=$rc"; tail -25 $OUT/pt_x.log
 [ $rc -eq 0 ] || exit $rc
 timeout -k 10 700 python -u -m pytest tests -m gpu -x -q --timeout 200 --timeout-method thread > $OUT/pt.log 2>&1
