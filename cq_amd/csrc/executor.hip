@@ -233,6 +233,9 @@ hipError_t cq_jx_route(const uint8_t* g, uint64_t lo, uint64_t hi, uint32_t ws, 
 hipError_t cq_jx_ent_build(const void* ent, unsigned long long n, uint32_t qoff, unsigned long long range, uint16_t* d16,
                            uint32_t* l32, unsigned long long* ttab, unsigned long long* nplaced, unsigned int* flag,
                            int grid, hipStream_t s, int ungrouped);
+hipError_t cq_jx_ent_part(const void* ent, unsigned long long n, uint32_t qoff, unsigned long long range, uint32_t np,
+                          uint32_t pcap, uint32_t psh, unsigned long long* pent, uint32_t* pcnt, unsigned int* flag,
+                          int grid, hipStream_t s);
 hipError_t cq_jx_ent_probe(const void* ent, unsigned long long n, uint32_t qoff, unsigned long long range, uint16_t* d16,
                            unsigned long long* gsum, unsigned long long* npairs, int grid, hipStream_t s);
 hipError_t cq_jx_probe(int grouped, int value, int direct, const unsigned long long* pkey,
@@ -363,7 +366,6 @@ struct DevCtx {
     // the start of every query, so the query path makes no hipMalloc / hipFree
     uint8_t* bump = nullptr;
     size_t bump_size = 0, bump_used = 0;
-    hipEvent_t up_ev[2] = {nullptr, nullptr};   // table upload: staging-buffer reuse
     uint64_t query_gen = 1;            // bumped at every query (literal cache lifetimes)
 };
 DevCtx g_ctx[64];
@@ -760,57 +762,81 @@ cqgpu_table* upload(const uint8_t* host, size_t n, cq_csv_config cfg, uint64_t b
     note_table_bytes(t->dbuf, total);
     HIPCHECK(hipMemsetAsync(t->dbuf, '\n', PAD_BEFORE, c.stream));
     HIPCHECK(hipMemsetAsync(t->dbuf + PAD_BEFORE + n, '\n', PAD_AFTER, c.stream));
-    // stream the bytes through pinned staging buffers: groups of P 32 MiB chunks are
-    // copied from the (page-cached, mmapped) source by P host threads at once --
-    // one thread's memcpy runs at ~10 GB/s, far below the host-to-device link --
-    // while the previous group's chunks are in flight to the device
-    const size_t CH = 32ull << 20;
+    // stream the bytes through a ring of S pinned slots: P host threads claim chunks in
+    // order and fill them (pread from the file, or memcpy out of the mapping) -- one
+    // thread's copy runs at ~10 GB/s, far below the host-to-device link -- while this
+    // thread issues each filled chunk's DMA in order and records its slot's event; a
+    // thread reuses a slot once the DMA of the chunk before it in that slot is done.
+    // Continuous: the link never waits for a whole group, only the first chunk's fill
+    // and the last chunk's DMA are exposed (CQGPU_UPLOAD_THREADS, CQGPU_UPLOAD_CHUNK_MB)
     const unsigned hw = std::max(1u, std::thread::hardware_concurrency());
     const char* up_env = getenv("CQGPU_UPLOAD_THREADS");
+    const char* ch_env = getenv("CQGPU_UPLOAD_CHUNK_MB");
     const size_t P = up_env ? (size_t)std::min(std::max(atoi(up_env), 1), 64)
                             : std::min<size_t>(8, std::max(1u, hw / 2));
+    const size_t CH = (ch_env ? (size_t)std::min(std::max(atoi(ch_env), 1), 256) : 32) << 20;
     const size_t nch = (n + CH - 1) / CH;
-    uint8_t* st = (uint8_t*)pinned(c, 2 * P * std::min(CH, std::max<size_t>(n, 1)));
+    const size_t S = std::max<size_t>(2 * P, 4);
     const size_t slot = std::min(CH, std::max<size_t>(n, 1));
-    if (!c.up_ev[0]) {
-        HIPCHECK(hipEventCreateWithFlags(&c.up_ev[0], hipEventDisableTiming));
-        HIPCHECK(hipEventCreateWithFlags(&c.up_ev[1], hipEventDisableTiming));
-    }
-    for (size_t g0 = 0, grp = 0; g0 < nch; g0 += P, grp++) {
-        uint8_t* base = st + (grp & 1) * P * slot;
-        if (grp >= 2) HIPCHECK(hipEventSynchronize(c.up_ev[grp & 1]));   // group grp-2's copies left these buffers
-        const size_t gn = std::min(P, nch - g0);
-        std::atomic<int> rerr{0};
-        auto part = [&](size_t k) {
-            const size_t off = (g0 + k) * CH, len = std::min(CH, n - off);
+    uint8_t* st = (uint8_t*)pinned(c, S * slot);
+    std::vector<hipEvent_t> ev(S, nullptr);
+    for (auto& e : ev) HIPCHECK(hipEventCreateWithFlags(&e, hipEventDisableTiming));
+    struct EvFree {
+        std::vector<hipEvent_t>& v;
+        ~EvFree() { for (auto e : v) if (e) (void)hipEventDestroy(e); }
+    } ev_free_{ev};
+    std::atomic<size_t> next{0}, issued{0};
+    std::atomic<int> rerr{0};
+    std::unique_ptr<std::atomic<uint8_t>[]> filled(new std::atomic<uint8_t>[nch ? nch : 1]);
+    for (size_t k = 0; k < nch; k++) filled[k].store(0, std::memory_order_relaxed);
+    auto worker = [&]() {
+        for (;;) {
+            const size_t k = next.fetch_add(1);
+            if (k >= nch || rerr.load()) return;
+            if (k >= S) {                      // the slot's previous chunk: issued, then copied
+                while (issued.load(std::memory_order_acquire) <= k - S) {
+                    if (rerr.load()) return;
+                    std::this_thread::yield();
+                }
+                if (hipEventSynchronize(ev[k % S]) != hipSuccess) { rerr.store(EIO); return; }
+            }
+            uint8_t* dst = st + (k % S) * slot;
+            const size_t off = k * CH, len = std::min(CH, n - off);
             if (fd < 0) {
-                memcpy(base + k * slot, host + off, len);
-                return;
+                memcpy(dst, host + off, len);
+            } else {
+                size_t got = 0;
+                while (got < len) {
+                    const ssize_t r = pread(fd, dst + got, len - got, (off_t)(fd_off + off + got));
+                    if (r < 0 && errno == EINTR) continue;
+                    if (r <= 0) { rerr.store(r < 0 ? errno : EIO); return; }
+                    got += (size_t)r;
+                }
             }
-            size_t got = 0;
-            while (got < len) {
-                const ssize_t r = pread(fd, base + k * slot + got, len - got, (off_t)(fd_off + off + got));
-                if (r < 0 && errno == EINTR) continue;
-                if (r <= 0) { rerr.store(r < 0 ? errno : EIO); return; }
-                got += (size_t)r;
-            }
-        };
-        std::vector<std::thread> th;
-        for (size_t k = 1; k < gn; k++) th.emplace_back(part, k);
-        part(0);
-        for (auto& x : th) x.join();
-        if (rerr.load()) {
-            (void)hipStreamSynchronize(c.stream);
-            (void)hipFree(t->dbuf);
-            delete t;
-            throw HipError{std::string("upload: pread: ") + strerror(rerr.load())};
+            filled[k].store(1, std::memory_order_release);
         }
-        for (size_t k = 0; k < gn; k++) {
-            const size_t off = (g0 + k) * CH;
-            HIPCHECK(hipMemcpyAsync(t->dbuf + PAD_BEFORE + off, base + k * slot, std::min(CH, n - off),
-                                    hipMemcpyHostToDevice, c.stream));
-        }
-        HIPCHECK(hipEventRecord(c.up_ev[grp & 1], c.stream));
+    };
+    std::vector<std::thread> th;
+    for (size_t k = 0; k < std::min(P, nch); k++) th.emplace_back(worker);
+    hipError_t herr = hipSuccess;
+    for (size_t k = 0; k < nch && herr == hipSuccess; k++) {
+        while (!filled[k].load(std::memory_order_acquire) && !rerr.load()) std::this_thread::yield();
+        if (rerr.load()) break;
+        const size_t off = k * CH;
+        herr = hipMemcpyAsync(t->dbuf + PAD_BEFORE + off, st + (k % S) * slot, std::min(CH, n - off),
+                              hipMemcpyHostToDevice, c.stream);
+        if (herr == hipSuccess) herr = hipEventRecord(ev[k % S], c.stream);
+        issued.store(k + 1, std::memory_order_release);
+    }
+    if (herr != hipSuccess && !rerr.load()) rerr.store(EIO);
+    for (auto& x : th) x.join();
+    if (rerr.load()) {
+        (void)hipStreamSynchronize(c.stream);
+        forget_table_bytes(t->dbuf);
+        (void)hipFree(t->dbuf);
+        delete t;
+        throw HipError{herr != hipSuccess ? std::string("upload: ") + hipGetErrorString(herr)
+                                          : std::string("upload: pread: ") + strerror(rerr.load())};
     }
     HIPCHECK(hipStreamSynchronize(c.stream));
     t->g = t->dbuf + PAD_BEFORE;
@@ -6016,7 +6042,6 @@ cq_table* cqgpu_merge_partials(cq_node* q, const void* const* blobs, const size_
         struct Part {
             std::vector<std::string> names;
             std::vector<uint32_t> classes;
-            std::vector<HGroup> groups;
         };
         std::vector<Part> parts(nblobs);
         uint32_t nacc = 0, nrep = 0, nvla = 0, magic0 = 0, lmask = 0, rmask = 0;
@@ -6065,6 +6090,10 @@ cq_table* cqgpu_merge_partials(cq_node* q, const void* const* blobs, const size_
             g_stats.path = 1;
             return res;
         }
+        // headers first (the plan, the accumulators' classes); every blob's groups are
+        // then parsed straight into the merge, one scratch group at a time
+        std::vector<size_t> gat(nblobs, 0);
+        std::vector<uint64_t> gcount(nblobs, 0);
         for (int bi = 0; bi < nblobs; bi++) {
             Reader r{(const uint8_t*)blobs[bi], sizes[bi], 0};
             const uint32_t magic = r.u32();
@@ -6087,38 +6116,9 @@ cq_table* cqgpu_merge_partials(cq_node* q, const void* const* blobs, const size_
             if (bi == 0) { nacc = na; nrep = nr; nvla = nv; }
             else if (pt.names != parts[0].names || na != nacc || nr != nrep || nv != nvla)
                 throw HipError{"partials from different plans"};
-            if (nv > (uint32_t)MAX_ACC) throw HipError{"bad partial blob"};
-            const uint64_t ng = r.u64();
-            pt.groups.reserve((size_t)std::min<uint64_t>(ng, (r.n - r.o) / 40 + 1));
-            for (uint64_t gi = 0; gi < ng; gi++) {
-                HGroup h;
-                h.kcls = r.u32(); h.klen = r.u32(); h.kw0 = r.u64(); h.kw1 = r.u64(); h.kbytes = r.str();
-                h.cnt = r.u64(); h.first = r.u64();
-                for (uint32_t a = 0; a < nacc; a++) {
-                    h.sum[a] = r.f64(); h.num[a] = r.u64(); h.extpos[a] = r.u64(); h.ext[a] = r.cell();
-                }
-                for (uint32_t k = 0; k < nrep; k++) h.reps.push_back(r.cell());
-                for (uint32_t v = 0; v < nvla; v++) {
-                    h.vsum[v] = r.f64(); h.vm2[v] = r.f64(); h.vn[v] = r.f64();
-                    const uint64_t nv = r.u64();
-                    if (nv > (r.n - r.o) / 8) throw HipError{"truncated partial blob"};
-                    if (nv) {
-                        if (h.mvals.size() <= v) h.mvals.resize(v + 1);
-                        h.mvals[v].resize(nv);
-                        for (auto& x : h.mvals[v]) x = r.u64();
-                    }
-                }
-                const uint32_t ns = r.u32();
-                if (ns > nacc) throw HipError{"bad partial blob"};
-                for (uint32_t j = 0; j < ns; j++) {
-                    HGroup::ClassSplit cs;
-                    cs.acc = (int)r.u32();
-                    if (cs.acc < 0 || cs.acc >= (int)nacc) throw HipError{"bad partial blob"};
-                    for (int k = 0; k < 3; k++) { cs.ext[k] = r.cell(); cs.extpos[k] = r.u64(); cs.first[k] = r.u64(); }
-                    h.split.push_back(cs);
-                }
-                pt.groups.push_back(std::move(h));
-            }
+            if (nv > (uint32_t)MAX_ACC || na > (uint32_t)MAX_ACC) throw HipError{"bad partial blob"};
+            gcount[bi] = r.u64();
+            gat[bi] = r.o;
         }
         PHASE("merge parse");
         // the plan binds columns by name: compile it against the shards' header
@@ -6176,29 +6176,78 @@ cq_table* cqgpu_merge_partials(cq_node* q, const void* const* blobs, const size_
             return (C.P.acc[a].kind == ACC_MIN ? cv < 0 : cv > 0) || (cv == 0 && xp < yp);
         };
         std::vector<HGroup> merged;
-        size_t total_groups = 0;
-        for (auto& pt : parts) total_groups += pt.groups.size();
-        merged.reserve(total_groups);
-        std::unordered_map<std::string, size_t> where;
-        where.reserve(total_groups * 2);
-        std::string id;
-        for (auto& pt : parts) {
-            for (HGroup& h : pt.groups) {
-                // group identity: class + text for text keys, class + payload otherwise
-                // (raw bytes of the words: a fixed-width key, no decimal formatting)
-                id.assign((const char*)&h.kcls, 4);
-                if (h.kcls == GK_STR || h.kcls == GK_LONG) id += h.kbytes;
-                else if (h.kcls == GK_COMP) { id.append((const char*)&h.kw0, 8); id.append((const char*)&h.kw1, 8); }
-                else id.append((const char*)&h.kw0, 8);
+        uint64_t total_groups = 0;
+        for (int bi = 0; bi < nblobs; bi++) total_groups += gcount[bi];
+        merged.reserve((size_t)std::min<uint64_t>(total_groups, 1u << 22));
+        // group identity: class + text for text keys, both words for composite digests,
+        // the first word otherwise (raw bytes of a fixed-width key, no decimal formatting);
+        // an open-addressing table of merged indexes over the identity's hash
+        auto text_key = [](const HGroup& h) { return h.kcls == GK_STR || h.kcls == GK_LONG; };
+        auto key_hash = [&](const HGroup& h) {
+            uint64_t x = (uint64_t)h.kcls * 0x9E3779B97F4A7C15ull;
+            if (text_key(h)) {
+                uint64_t f = 1469598103934665603ull;     // FNV-1a of the text
+                for (unsigned char ch : h.kbytes) f = (f ^ ch) * 1099511628211ull;
+                x ^= f;
+            } else {
+                x ^= h.kw0 + 0x632BE59BD9B4E019ull;
+                if (h.kcls == GK_COMP) x ^= h.kw1 * 0xC2B2AE3D27D4EB4Full;
+            }
+            x ^= x >> 31; x *= 0xBF58476D1CE4E5B9ull; x ^= x >> 29;
+            return x;
+        };
+        auto same_key = [&](const HGroup& a, const HGroup& b) {
+            if (a.kcls != b.kcls) return false;
+            if (text_key(a)) return a.kbytes == b.kbytes;
+            return a.kw0 == b.kw0 && (a.kcls != GK_COMP || a.kw1 == b.kw1);
+        };
+        uint64_t cap = 64;
+        while (cap < 2 * std::min<uint64_t>(total_groups, 1ull << 30) + 2) cap <<= 1;
+        std::vector<uint32_t> slot_of((size_t)cap, 0u);          // merged index + 1
+        HGroup h;                                                // the scratch group
+        for (int bi = 0; bi < nblobs; bi++) {
+            Reader r{(const uint8_t*)blobs[bi], sizes[bi], gat[bi]};
+            for (uint64_t gi = 0; gi < gcount[bi]; gi++) {
+                h.kcls = r.u32(); h.klen = r.u32(); h.kw0 = r.u64(); h.kw1 = r.u64(); h.kbytes = r.str();
+                h.cnt = r.u64(); h.first = r.u64();
+                for (uint32_t a = 0; a < nacc; a++) {
+                    h.sum[a] = r.f64(); h.num[a] = r.u64(); h.extpos[a] = r.u64(); h.ext[a] = r.cell();
+                }
+                h.reps.clear();
+                for (uint32_t k = 0; k < nrep; k++) h.reps.push_back(r.cell());
+                for (auto& mv : h.mvals) mv.clear();
+                for (uint32_t v = 0; v < nvla; v++) {
+                    h.vsum[v] = r.f64(); h.vm2[v] = r.f64(); h.vn[v] = r.f64();
+                    const uint64_t nv = r.u64();
+                    if (nv > (r.n - r.o) / 8) throw HipError{"truncated partial blob"};
+                    if (nv) {
+                        if (h.mvals.size() <= v) h.mvals.resize(v + 1);
+                        h.mvals[v].resize(nv);
+                        for (auto& x : h.mvals[v]) x = r.u64();
+                    }
+                }
+                h.split.clear();
+                const uint32_t ns = r.u32();
+                if (ns > nacc) throw HipError{"bad partial blob"};
+                for (uint32_t j = 0; j < ns; j++) {
+                    HGroup::ClassSplit cs;
+                    cs.acc = (int)r.u32();
+                    if (cs.acc < 0 || cs.acc >= (int)nacc) throw HipError{"bad partial blob"};
+                    for (int k = 0; k < 3; k++) { cs.ext[k] = r.cell(); cs.extpos[k] = r.u64(); cs.first[k] = r.u64(); }
+                    h.split.push_back(cs);
+                }
                 for (uint32_t a = 0; a < nacc; a++)
                     if (mixed[a]) (void)split_of(h, (int)a);
-                auto it = where.find(id);
-                if (it == where.end()) {
-                    where.emplace(id, merged.size());
+                uint64_t at = key_hash(h) & (cap - 1);
+                while (slot_of[at] && !same_key(merged[slot_of[at] - 1], h)) at = (at + 1) & (cap - 1);
+                if (!slot_of[at]) {
+                    if (merged.size() >= (size_t)UINT32_MAX - 1) throw Ineligible{"too many groups to merge"};
+                    slot_of[at] = (uint32_t)merged.size() + 1;
                     merged.push_back(std::move(h));
+                    h = HGroup();
                     continue;
                 }
-                HGroup& m = merged[it->second];
+                HGroup& m = merged[slot_of[at] - 1];
                 m.cnt += h.cnt;
                 if (h.first < m.first) { m.first = h.first; m.reps = h.reps; }
                 for (uint32_t a = 0; a < nacc; a++) {
@@ -7238,7 +7287,7 @@ uint32_t typed_emit_pass(DevCtx& c, cqgpu_table* t, bool build, int kcol, int pc
 // the receiving rank: STAR over the entries -> this rank's groups in `part`; returns
 // the flags (0: done; 16 / 32 / 64: the entries do not fit the STAR form)
 uint32_t typed_receive(DevCtx& c, const TypedJoin& tj, const void* ub, uint64_t nu, const void* ob, uint64_t no,
-                       uint64_t qoff, uint64_t range, JoinPartial& part) {
+                       uint64_t qoff, uint64_t range, JoinPartial& part, bool allow_part = true) {
     PhaseClock pc;
     PhaseClock* const outer_phase = g_phase;
     g_phase = &pc;
@@ -7263,7 +7312,35 @@ uint32_t typed_receive(DevCtx& c, const TypedJoin& tj, const void* ub, uint64_t 
     // (ungrouped: no tag lookup, every build entry in group 0)
     HIPCHECK(cq_jx_ent_build(ub, nu, (uint32_t)qoff, range, d16.as<uint16_t>(), l32.as<uint32_t>(), ttab, cnts, flag,
                              c.ncu * 4, c.stream, grouped ? 0 : 1));
-    HIPCHECK(cq_jx_ent_probe(ob, no, (uint32_t)qoff, range, d16.as<uint16_t>(), gsum, cnts + 1, c.ncu * 4, c.stream));
+    // the probe: when d16 outgrows an XCD's L2, in two passes -- the entries into 2 MiB
+    // key partitions (jx_ent_part_kernel), then each partition looked up by one XCD's
+    // blocks (jx_part_probe_kernel, the CSV STAR's pass 2); a full segment (skewed keys)
+    // reruns the whole receive unpartitioned.  CQGPU_TYPED_NO_PART=1: one pass; test
+    // knobs as the CSV STAR's: CQGPU_PART_PROBE_MIN (slots above which it partitions,
+    // default 2^21; also the probe entries' floor, 2^20 by default), CQGPU_PART_PROBE_SHIFT
+    const char* pm_env = getenv("CQGPU_PART_PROBE_MIN");
+    const char* ps_env = getenv("CQGPU_PART_PROBE_SHIFT");
+    const uint64_t part_min = pm_env ? strtoull(pm_env, nullptr, 10) : (2ull << 20);
+    const uint32_t PSH = ps_env ? (uint32_t)std::min(std::max(atoi(ps_env), 4), 24) : 20u;
+    const uint64_t np64 = (range + (1ull << PSH) - 1) >> PSH;
+    const uint32_t pgrid = (uint32_t)c.ncu;
+    const bool pprobe = allow_part && !getenv("CQGPU_TYPED_NO_PART") && range > part_min && np64 <= 4096 &&
+                        no >= std::min<uint64_t>(part_min / 2, 1ull << 20) && pgrid >= 8;
+    DevBuf pent, pcnt;
+    if (pprobe) {
+        const uint64_t per = no / ((uint64_t)pgrid * np64) + 1;
+        const uint32_t pcap = (uint32_t)std::min<uint64_t>(per + per / 4 + 256, 1u << 30);
+        DevBuf a((size_t)pgrid * np64 * pcap * 8), b((size_t)pgrid * np64 * 4);
+        std::swap(pent.p, a.p);
+        std::swap(pcnt.p, b.p);
+        HIPCHECK(cq_jx_ent_part(ob, no, (uint32_t)qoff, range, (uint32_t)np64, pcap, PSH, pent.as<unsigned long long>(),
+                                pcnt.as<uint32_t>(), flag, (int)pgrid, c.stream));
+        HIPCHECK(cq_jx_part_probe(pent.as<unsigned long long>(), pcnt.as<uint32_t>(), pgrid, (uint32_t)np64, pcap, range,
+                                  d16.as<uint16_t>(), notmono, gsum, gfirst, cnts + 1, std::max(8, (c.ncu / 8) * 8),
+                                  c.stream));
+    } else {
+        HIPCHECK(cq_jx_ent_probe(ob, no, (uint32_t)qoff, range, d16.as<uint16_t>(), gsum, cnts + 1, c.ncu * 4, c.stream));
+    }
     HIPCHECK(cq_jx_star_first(d16.as<uint16_t>(), l32.as<uint32_t>(), range, notmono, gfirst, cnts + 2, c.ncu * 4,
                               c.stream));
     HIPCHECK(hipEventRecord(c.ev1, c.stream));
@@ -7279,6 +7356,10 @@ uint32_t typed_receive(DevCtx& c, const TypedJoin& tj, const void* ub, uint64_t 
     g_stats.scan_ms = ms;
     uint32_t fl = 0;
     memcpy(&fl, h.data() + o_ctl, 4);
+    if (fl & 128u) {                                     // a partition segment overflowed
+        HIPCHECK(hipStreamSynchronize(c.stream));         // (the partition buffers go out of scope)
+        return typed_receive(c, tj, ub, nu, ob, no, qoff, range, part, false);
+    }
     unsigned long long cn[3];
     memcpy(cn, h.data() + o_ctl + 8, 24);
     if (cn[0] != cn[2]) fl |= 64u;                       // a repeated build key

@@ -2178,7 +2178,8 @@ __global__ __launch_bounds__(1024) void jx_part_probe_kernel(const unsigned long
                         d16[ix] = (uint16_t)(gv[u] | 0x8000u);     // (every writer: the same value)
                     }
                     atomicAdd(&scnt[gi], 1u);
-                    if (p32 != JX_PNULL) atomicAdd(&sfix[gi], (unsigned long long)p32);
+                    // (signed: a typed entry's payload may be negative; the CSV pass 1's are < 2^31)
+                    if (p32 != JX_PNULL) atomicAdd(&sfix[gi], (unsigned long long)(long long)(int32_t)p32);
                     else atomicAdd(&snul[gi], 1u);
                     pairs++;
                 }
@@ -2371,6 +2372,47 @@ __global__ __launch_bounds__(1024) void jx_ent_build_kernel(const uint4* __restr
         if (fl) atomicOr(flag, fl);
         if (placed) atomicAdd(nplaced, placed);
     }
+}
+
+// partitioned probe over typed entries, pass 1: every probe entry whose slot (q32 -
+// qoff) is inside the build range, as {slot, payload} into its key partition's segment
+// (slot >> psh) of this block -- the layout jx_part_probe_kernel (pass 2: each XCD's
+// blocks look one 2 MiB d16 slice up at a time, in its L2) reads.  An entry past its
+// segment's capacity sets flag 128 (the caller reruns unpartitioned).  Entries are
+// read in block-contiguous runs, so a block's segments fill in entry order.
+__global__ __launch_bounds__(1024) void jx_ent_part_kernel(const uint2* __restrict__ ent, uint64_t n, uint32_t qoff,
+                                                           uint64_t range, uint32_t np, uint32_t pcap, uint32_t psh,
+                                                           unsigned long long* __restrict__ pent,
+                                                           uint32_t* __restrict__ pcnt, unsigned int* __restrict__ flag) {
+    extern __shared__ uint32_t pcl[];                // per partition: this block's entries so far
+    for (uint32_t k = threadIdx.x; k < np; k += blockDim.x) pcl[k] = 0;
+    __syncthreads();
+    const uint64_t per = (n + gridDim.x - 1) / gridDim.x;
+    const uint64_t lo = (uint64_t)blockIdx.x * per, hi = min(n, lo + per);
+    unsigned long long* seg = pent + (size_t)blockIdx.x * np * pcap;
+    bool over = false;
+    constexpr int U = 4;                             // entries in flight per thread
+    for (uint64_t i = lo + threadIdx.x; i < hi; i += U * blockDim.x) {
+        uint2 e[U];
+#pragma unroll
+        for (int u = 0; u < U; u++) {
+            const unsigned long long v =
+                i + u * blockDim.x < hi ? __builtin_nontemporal_load((const unsigned long long*)ent + i + u * blockDim.x) : 0ull;
+            e[u] = make_uint2((uint32_t)v, (uint32_t)(v >> 32));
+        }
+#pragma unroll
+        for (int u = 0; u < U; u++) {
+            const uint32_t slot = e[u].x - qoff;
+            if (i + u * blockDim.x >= hi || e[u].x < qoff || (uint64_t)slot >= range) continue;
+            const uint32_t pr = slot >> psh;
+            const uint32_t at = atomicAdd(&pcl[pr], 1u);
+            if (at < pcap) seg[(size_t)pr * pcap + at] = (unsigned long long)slot | ((unsigned long long)e[u].y << 32);
+            else over = true;
+        }
+    }
+    if (__any(over) && (threadIdx.x & 63) == 0) atomicOr(flag, 128u);
+    __syncthreads();
+    for (uint32_t k = threadIdx.x; k < np; k += blockDim.x) pcnt[(size_t)blockIdx.x * np + k] = min(pcl[k], pcap);
 }
 
 // probe: every entry's slot looked up in d16 (bit 15 set on a first match, for
@@ -3383,6 +3425,16 @@ hipError_t cq_jx_ent_build(const void* ent, unsigned long long n, uint32_t qoff,
     if (!n) return hipSuccess;
     hipLaunchKernelGGL(cq::fast::jx_ent_build_kernel, dim3(grid), dim3(1024), 0, s, (const uint4*)ent, (uint64_t)n, qoff,
                        (uint64_t)range, d16, l32, ttab, nplaced, flag, (uint32_t)(ungrouped != 0));
+    return hipGetLastError();
+}
+hipError_t cq_jx_ent_part(const void* ent, unsigned long long n, uint32_t qoff, unsigned long long range, uint32_t np,
+                          uint32_t pcap, uint32_t psh, unsigned long long* pent, uint32_t* pcnt, unsigned int* flag,
+                          int grid, hipStream_t s) {
+    if (np == 0 || np > cq::fast::JX_PMAX || ((unsigned long long)np << psh) < range) return hipErrorInvalidValue;
+    const size_t lds = (size_t)np * 4;
+    cq::set_max_lds((const void*)cq::fast::jx_ent_part_kernel, (int)lds);
+    hipLaunchKernelGGL(cq::fast::jx_ent_part_kernel, dim3(grid), dim3(1024), lds, s, (const uint2*)ent, (uint64_t)n, qoff,
+                       (uint64_t)range, np, pcap, psh, pent, pcnt, flag);
     return hipGetLastError();
 }
 hipError_t cq_jx_ent_probe(const void* ent, unsigned long long n, uint32_t qoff, unsigned long long range, uint16_t* d16,

@@ -994,6 +994,52 @@ def test_typed_exchange_equals_oracle(files, nranks, qi):
     assert sum(st["recv_entries_u"]) == 4000 and st["attempts"] == 1, st
 
 
+@pytest.mark.parametrize("nranks", [1, 3, 8])
+@pytest.mark.parametrize("qi", range(len(TYPED)))
+def test_typed_exchange_partitioned_probe(files, nranks, qi, monkeypatch):
+    """the receiver's two-pass probe (jx_ent_part_kernel: entries into key partitions of
+    16 slots, then jx_part_probe_kernel per XCD) forced at test size -- the oracle's
+    answer, as the one-pass probe gives it"""
+    monkeypatch.setenv("CQGPU_PART_PROBE_MIN", "0")
+    monkeypatch.setenv("CQGPU_PART_PROBE_SHIFT", "4")
+    data, paths = files
+    sql = TYPED[qi].format(u=paths["users"], o=paths["orders"])
+    want, unsup = cqtest.oracle_query(sql)
+    assert not unsup
+    with cqtest.Parsed(sql) as ast:
+        tp, why = _typed(ast, data["users"], data["orders"], nranks, {})
+        assert tp, (cq_amd.last_error(), why)
+        got = abi.table_to_py(tp)
+        cq_amd.result_free(tp)
+        tol = tolerant_columns(ast)
+    compare(got, want, tol, f"typed exchange, partitioned probe, {nranks} ranks: {sql}")
+
+
+def test_typed_exchange_partition_overflow(tmp_path, monkeypatch):
+    """skewed probe keys (90 % of 120 K orders on one user) overflow a partition
+    segment: the receive reruns unpartitioned and still gives the oracle's answer"""
+    monkeypatch.setenv("CQGPU_PART_PROBE_MIN", "0")
+    monkeypatch.setenv("CQGPU_PART_PROBE_SHIFT", "4")
+    rng = np.random.default_rng(9)
+    users = "id,name,role\n" + "".join("%d,n%d,r%d\n" % (i, i, i % 7) for i in range(1000))
+    orders = "id,price,customer_id\n" + "".join(
+        "%d,%d.%d,%d\n" % (i, rng.integers(0, 99), rng.integers(0, 9), 5 if i % 10 else rng.integers(0, 1000))
+        for i in range(120_000))
+    up, op = tmp_path / "u.csv", tmp_path / "o.csv"
+    up.write_text(users)
+    op.write_text(orders)
+    sql = (f"SELECT u.role, COUNT(*), SUM(o.price) FROM '{up}' AS u JOIN '{op}' AS o "
+           f"ON u.id = o.customer_id GROUP BY u.role")
+    want, _ = cqtest.oracle_query(sql)
+    with cqtest.Parsed(sql) as ast:
+        tp, why = _typed(ast, users.encode(), orders.encode(), 1, {})
+        assert tp, (cq_amd.last_error(), why)
+        got = abi.table_to_py(tp)
+        cq_amd.result_free(tp)
+        tol = tolerant_columns(ast)
+    compare(got, want, tol, "typed exchange, partition overflow")
+
+
 def test_typed_exchange_large_keys_retry(tmp_path):
     """keys near 10^14: key / N does not fit 32 bits, the first attempt flags it and the
     second runs with qbase = the keys' minimum / N; and a probe side with keys outside
