@@ -163,7 +163,7 @@ def cpu_baseline(rows, seed, config=3):
            "seconds": secs, "host_cores": os.cpu_count()}
     host_full = os.path.join(ROOT, "profiles", "r5_ref_full_bench_host.json")
     if config == 3 and os.path.exists(host_full):
-        # the full 1e8-row file on a GPU box's own host (scripts/r5_ref_full.py): same
+        # the full 1e8-row file on a GPU box's own host (scripts/archive/r5_ref_full.py): same
         # kind of box as this run, measured separately because it takes ~2.5 minutes
         try:
             with open(host_full) as fh:

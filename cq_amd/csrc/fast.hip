@@ -2342,16 +2342,22 @@ __global__ __launch_bounds__(1024) void jx_ent_build_kernel(const uint4* __restr
     uint32_t fl = 0;
     unsigned long long placed = 0;
     const uint64_t nt = (uint64_t)gridDim.x * blockDim.x;
-    for (uint64_t i = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x; i < n; i += 2 * nt) {
-        uint4 e[2];
-        bool ok[2];
+    // (latency-bound at two entries in flight per thread: SQ_WAIT_ANY / SQ_WAVE_CYCLES 0.72,
+    // profiles/r6_pmc.json; JXB_U entries in flight, streamed past the caches)
+#ifndef JXB_U
+#define JXB_U 4
+#endif
+    for (uint64_t i = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x; i < n; i += JXB_U * nt) {
+        uint4 e[JXB_U];
+        bool ok[JXB_U];
 #pragma unroll
-        for (int u = 0; u < 2; u++) {                // two entries in flight per thread
+        for (int u = 0; u < JXB_U; u++) {
             ok[u] = i + u * nt < n;
-            e[u] = ok[u] ? ent[i + u * nt] : make_uint4(0u, 0u, 0u, 0u);
+            const v4u x = ok[u] ? __builtin_nontemporal_load((const v4u*)(ent + i + u * nt)) : v4u{0u, 0u, 0u, 0u};
+            e[u] = make_uint4(x.x, x.y, x.z, x.w);
         }
 #pragma unroll
-        for (int u = 0; u < 2; u++) {
+        for (int u = 0; u < JXB_U; u++) {
             if (!ok[u]) continue;
             const uint64_t slot = (uint64_t)(uint32_t)(e[u].x - qoff);
             if (e[u].x < qoff || slot >= range) { fl |= 16u; continue; }

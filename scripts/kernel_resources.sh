@@ -17,7 +17,7 @@ for ln in open(sys.argv[1]):
     for key, tag in (("VGPRs:", "V"), ("AGPRs:", "A"), ("ScratchSize [bytes/lane]:", "scr"), ("SGPRs Spill:", "sS"),
                      ("VGPRs Spill:", "vS"), ("Occupancy [waves/SIMD]:", "occ"), ("SGPRs:", "S"), ("LDS Size [bytes/block]:", "lds")):
         if cur and (" " + key) in ln:
-            out[cur][tag] = ln.rsplit(key, 1)[1].strip()
+            out[cur][tag] = ln.rsplit(key, 1)[1].split("[")[0].strip()
 import subprocess
 names = list(out)
 dem = subprocess.run(["c++filt"], input="\n".join(names), capture_output=True, text=True).stdout.split("\n")

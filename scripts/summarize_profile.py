@@ -39,9 +39,15 @@ def main():
     if stats:
         shutil.copy(stats[0], a.prefix + "_kernel_stats.csv")
     # counters per kernel class: config 3's and config 2's fast_kernel, config 5's jx kernels
-    classes = {"config3": "fast_kernel<true", "config2": "fast_kernel<false", "config5_probe": "jx_probe_kernel",
-               "config5_extract_build": "jx_extract_kernel<true", "config5_extract_probe": "jx_extract_kernel<false",
-               "config5_build": "jx_build"}
+    classes = {"config3": "fast_kernel<true", "config2": "fast_kernel<false",
+               # config 5's rank step (the typed exchange): the sender's count / emit window
+               # walks, the receiver's STAR build, partition pass, partitioned probe, first pairs
+               "config5_count_build": "jx_extract_kernel<true, true, 1, false, false, 3, false, 1>",
+               "config5_count_probe": "jx_extract_kernel<false, true, 1, false, false, 3, false, 1>",
+               "config5_emit_build": "jx_extract_kernel<true, true, 2, false, false, 3, false, 2>",
+               "config5_emit_probe": "jx_extract_kernel<false, true, 2, false, false, 3, false, 2>",
+               "config5_ent_build": "jx_ent_build_kernel", "config5_ent_part": "jx_ent_part_kernel",
+               "config5_part_probe": "jx_part_probe_kernel", "config5_star_first": "jx_star_first_kernel"}
     out = {}
     for name, pat in classes.items():
         counters = {}
