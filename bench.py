@@ -522,6 +522,12 @@ def config5_leg(args, cq_amd, L):
             except Exception as e:
                 cpu["%dx%d" % (m, m)] = {"error": str(e)}
     xgmi = 7 * 153e9                     # 7 xGMI links per GPU at ~153 GB/s each (peak)
+    traffic = None                       # HBM bytes per step from the last PMC passes (profiles/)
+    try:
+        with open(os.path.join(ROOT, "profiles", "config5_traffic.json")) as fh:
+            traffic = json.load(fh).get("hbm_bytes_per_step")
+    except (OSError, ValueError):
+        pass
     return {"workload": "config5 (rank 0 of %d, its whole step): SELECT u.role, COUNT(*), SUM(o.price) "
                         "FROM users u JOIN orders o ON u.id = o.customer_id GROUP BY u.role" % N,
             "users_total": n * N, "orders_total": n * N, "ranks": N,
@@ -540,7 +546,9 @@ def config5_leg(args, cq_amd, L):
                          "note": "not in ms_per_step: one GPU has no peer; xgmi_bound_ms = the larger direction "
                                  "over 7 links at their 153 GB/s peak"},
             "roofline": {"bound": "hbm", "achieved": alg / step_s / 1e9, "peak": HBM_PEAK_GBS,
-                         "unit": "GB/s", "frac": alg / step_s / 1e9 / HBM_PEAK_GBS, "traffic": None,
+                         "unit": "GB/s", "frac": alg / step_s / 1e9 / HBM_PEAK_GBS, "traffic": traffic,
+                         "traffic_source": "profiles/config5_traffic.json (rocprofv3 FETCH_SIZE x 2 + WRITE_SIZE "
+                                           "summed over the step's kernels)",
                          "algorithmic_bytes": alg,
                          "algorithmic": "rank 0's share of both files (%d B) + the entries its send pass writes "
                                         "(%d B) + the entries its join reads (%d B) (SURVEY.md 8d)"
