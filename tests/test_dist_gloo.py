@@ -364,3 +364,83 @@ def test_outer_sets_size_mismatch_gloo():
         assert p.exitcode == 0
     for rank, msg in res.items():
         assert "record count differs" in msg, (rank, msg)
+
+
+def _jworker(rank, world, port, q, kind):
+    """cq_amd.dist.join_partitioned's sequence with the library's device calls faked:
+    the routing mode agreed from every rank's class counts, global-id bases from each
+    rank's own record count, both rebuilt sides marked replicated alike"""
+    import ctypes as C
+    import torch
+    import torch.distributed as dist
+    import cq_amd
+    from cq_amd import abi
+    from cq_amd import dist as cd
+    os.environ["MASTER_ADDR"] = "127.0.0.1"
+    os.environ["MASTER_PORT"] = str(port)
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    try:
+        torch.cuda.synchronize = lambda *a, **k: None
+        calls = []
+        # ON keys per value class (NULL, number, string, date) on this rank, per side
+        counts = {0: [1, 5 + rank, 0, 0], 1: [0, 3, 2 if kind == "mixed" and rank == 1 else 0, 0]}
+
+        def plan2(ast, tables, side, n, r, mode=0):
+            assert r == rank
+            calls.append(("plan", side, mode))
+            nown = 10 + 3 * rank + side
+            nr = [nown // n + (1 if d < nown % n else 0) for d in range(n)]
+            return [4 * x for x in nr], nr, nown, counts[side]
+        cq_amd.route_plan2 = plan2
+        cq_amd.route_fill = lambda tab, base, b, g: calls.append(("fill", base))
+        cq_amd.table_from_routed = lambda *a: object()
+        cq_amd.table_set_record_total = lambda t, total: calls.append(("total", total))
+        cq_amd.table_set_key_stride = lambda t, s: None
+        cq_amd.table_set_replicated = lambda t, mode, owner: calls.append(("rep", mode, owner))
+        cq_amd.query_partial = lambda ast, tabs: b"blob%d" % rank
+        cq_amd.merge_partials = lambda ast, blobs: list(blobs)
+        cq_amd.join_outer_clear = lambda: None
+        P = abi.Plan()
+        on = None if kind == "cross" else P.cond("=", P.ident("a.k"), P.ident("b.k"))
+        qn = P.query([P.func("COUNT", P.lit("*"))], "l.csv", alias="a", joins=[("r.csv", "b", on, abi.JOIN_INNER)])
+        res = cd.join_partitioned(C.pointer(qn), "L", "R", b"k\n", b"k\n", "cpu", "cpu")
+        q.put((rank, calls, res))
+    finally:
+        dist.destroy_process_group()
+
+
+@pytest.mark.parametrize("kind", ["plain", "mixed", "cross"])
+@pytest.mark.parametrize("world", [2, 3])
+def test_join_partitioned_routing_mode_gloo(world, kind):
+    """every rank takes the same routing mode (cqgpu_route_major over the summed class
+    counts: numbers vs a rank's STRING keys -> replicate, majority class 1), bases its
+    global ids on the lower ranks' own record counts and marks its rebuilt sides alike,
+    rank 0 the owner; a JOIN without ON skips the class agreement and marks side 1 whole"""
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    port = _free_port()
+    procs = [ctx.Process(target=_jworker, args=(r, world, port, q, kind)) for r in range(world)]
+    for p in procs:
+        p.start()
+    res = {r: (c, m) for r, c, m in (q.get(timeout=120) for _ in range(world))}
+    for p in procs:
+        p.join(timeout=60)
+        assert p.exitcode == 0
+    mode = {"plain": 0, "mixed": 1, "cross": 0}[kind]
+    for rank, (calls, merged) in res.items():
+        plans = [c for c in calls if c[0] == "plan"]
+        want_plans = ([] if kind == "cross" else [("plan", 0, 0), ("plan", 1, 0)]) + [("plan", 0, mode),
+                                                                                     ("plan", 1, mode)]
+        assert plans == want_plans, (rank, plans)
+        for side in (0, 1):
+            own = [10 + 3 * r + side for r in range(world)]
+            fills = [c for c in calls if c[0] == "fill"]
+            assert fills[side] == ("fill", sum(own[:rank])), (rank, fills)
+            totals = [c for c in calls if c[0] == "total"]
+            assert totals[side] == ("total", sum(own)), (rank, totals)
+        reps = [c for c in calls if c[0] == "rep"]
+        want = [("rep", 0, rank == 0), ("rep", 4, rank == 0)] if kind == "cross" else \
+               [("rep", mode, rank == 0), ("rep", mode, rank == 0)]
+        assert reps == want, (rank, reps)
+        if rank == 0:
+            assert merged == [b"blob%d" % r for r in range(world)]
