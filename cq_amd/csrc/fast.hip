@@ -899,85 +899,151 @@ __global__ __launch_bounds__(LT) void fast_kernel(const uint8_t* __restrict__ g,
                 // per WHERE column its typed value (uniform class), then every leaf, then
                 // the tree's truth table (a field this path cannot type: wu, slow_kernel)
                 const uint32_t tt16 = fp.wx_tt, nleaf = fp.wx_nleaf;
-                bool cnull[RP][2];
-                uint32_t cv[RP][2];
-                uint64_t cx[RP][2];
+                if constexpr (WX == 1) {
+                    // one WHERE column (BETWEEN, IN, OR / AND over one column): leaf-major
+                    bool cnull[RP][2];
+                    uint32_t cv[RP][2];
+                    uint64_t cx[RP][2];
 #pragma unroll
-                for (int u = 0; u < RP; u++) {
-                    bool cok[2];
+                    for (int u = 0; u < RP; u++) {
+                        bool cok[2];
 #pragma unroll
-                    for (int c = 0; c < WX; c++) {
-                        const uint32_t len = c ? xen[u] - xst[u] : wen[u] - wst[u];
-                        const uint32_t a0r = c ? xd[u] : wd[u], a1r = c ? xd1[u] : wd1[u];
-                        cnull[u][c] = len == 0;
-                        cv[u][c] = 0;
-                        cx[u][c] = 0;
-                        if ((fp.wx_str >> c) & 1) {
-                            const uint32_t m0 = len_mask(len, 0), m1 = len_mask(len, 1);
-                            const uint32_t a0 = a0r & m0, a1 = a1r & m1;
-                            const uint32_t c0 = a0 & 0xFFu;
-                            cok[c] = (int)(len - 1u < 8u) & (int)!(is_digit(c0) | (c0 == '-') | (c0 == '+') | (c0 == '.')) &
-                                     (int)((low_bytes(a0, m0 & nk.k80, nk) | low_bytes(a1, m1 & nk.k80, nk)) == 0);
-                            cx[u][c] = ((uint64_t)__builtin_bswap32(a0) << 32) | __builtin_bswap32(a1);
-                        } else {
-                            const Num n = num4<true>(a0r, len, nk);
-                            const uint32_t mul = (uint32_t)(0x0001000A006403E8ull >> (n.k << 4)) & 0xFFFFu;
-                            cv[u][c] = __umul24(n.M, mul);
-                            cok[c] = n.ok;
+                        for (int c = 0; c < WX; c++) {
+                            const uint32_t len = c ? xen[u] - xst[u] : wen[u] - wst[u];
+                            const uint32_t a0r = c ? xd[u] : wd[u], a1r = c ? xd1[u] : wd1[u];
+                            cnull[u][c] = len == 0;
+                            cv[u][c] = 0;
+                            cx[u][c] = 0;
+                            if ((fp.wx_str >> c) & 1) {
+                                const uint32_t m0 = len_mask(len, 0), m1 = len_mask(len, 1);
+                                const uint32_t a0 = a0r & m0, a1 = a1r & m1;
+                                const uint32_t c0 = a0 & 0xFFu;
+                                cok[c] = (int)(len - 1u < 8u) & (int)!(is_digit(c0) | (c0 == '-') | (c0 == '+') | (c0 == '.')) &
+                                         (int)((low_bytes(a0, m0 & nk.k80, nk) | low_bytes(a1, m1 & nk.k80, nk)) == 0);
+                                cx[u][c] = ((uint64_t)__builtin_bswap32(a0) << 32) | __builtin_bswap32(a1);
+                            } else {
+                                const Num n = num4<true>(a0r, len, nk);
+                                const uint32_t mul = (uint32_t)(0x0001000A006403E8ull >> (n.k << 4)) & 0xFFFFu;
+                                cv[u][c] = __umul24(n.M, mul);
+                                cok[c] = n.ok;
+                            }
+                            wu[u] |= !cok[c] & !cnull[u][c] & !fail[u];
                         }
-                        wu[u] |= !cok[c] & !cnull[u][c] & !fail[u];
-                    }
                 }
-                // leaf by leaf, both records at once: a leaf's parameters (and an IN
-                // list's items) are read from LDS once per pass, not once per record
-                uint32_t idx[RP];
+                    // leaf by leaf, both records at once: a leaf's parameters (and an IN
+                    // list's items) are read from LDS once per pass, not once per record
+                    uint32_t idx[RP];
 #pragma unroll
-                for (int u = 0; u < RP; u++) idx[u] = 0;
+                    for (int u = 0; u < RP; u++) idx[u] = 0;
 #pragma unroll
-                for (int l = 0; l < 4; l++) {
-                    if ((uint32_t)l < nleaf) {
-                        const uint32_t* L = lxl + l * LX_WORDS;
-                        const uint32_t meta = __builtin_amdgcn_readfirstlane(L[0]);
-                        const uint32_t c = WX == 2 ? (meta >> 2) & 1u : 0u;
-                        const uint32_t kind = meta & 3u;
-                        const bool neg = (meta >> 3) & 1u, nulv = (meta >> 4) & 1u;
-                        bool b[RP];
-                        if (kind == LX_NUM) {
-                            const uint32_t la = L[1], lw = L[2];
+                    for (int l = 0; l < 4; l++) {
+                        if ((uint32_t)l < nleaf) {
+                            const uint32_t* L = lxl + l * LX_WORDS;
+                            const uint32_t meta = __builtin_amdgcn_readfirstlane(L[0]);
+                            const uint32_t c = WX == 2 ? (meta >> 2) & 1u : 0u;
+                            const uint32_t kind = meta & 3u;
+                            const bool neg = (meta >> 3) & 1u, nulv = (meta >> 4) & 1u;
+                            bool b[RP];
+                            if (kind == LX_NUM) {
+                                const uint32_t la = L[1], lw = L[2];
 #pragma unroll
-                            for (int u = 0; u < RP; u++) b[u] = ((c ? cv[u][WX - 1] : cv[u][0]) - la <= lw) != neg;
-                        } else if (kind == LX_STR) {
-                            const uint64_t lit = (uint64_t)L[4] | ((uint64_t)L[5] << 32);
-                            const uint32_t tt = (meta >> 5) & 7u;
+                                for (int u = 0; u < RP; u++) b[u] = ((c ? cv[u][WX - 1] : cv[u][0]) - la <= lw) != neg;
+                            } else if (kind == LX_STR) {
+                                const uint64_t lit = (uint64_t)L[4] | ((uint64_t)L[5] << 32);
+                                const uint32_t tt = (meta >> 5) & 7u;
+#pragma unroll
+                                for (int u = 0; u < RP; u++) {
+                                    const uint64_t X = c ? cx[u][WX - 1] : cx[u][0];
+                                    b[u] = tt_result(tt, X < lit ? -1 : (X > lit ? 1 : 0));
+                                }
+                            } else {
+                                bool hit[RP];
+#pragma unroll
+                                for (int u = 0; u < RP; u++) hit[u] = false;
+                                const uint32_t nin = (meta >> 8) & 15u;
+                                for (uint32_t t = 0; t < nin; t++) {
+                                    const uint64_t v = (uint64_t)L[6 + 2 * t] | ((uint64_t)L[7 + 2 * t] << 32);
+#pragma unroll
+                                    for (int u = 0; u < RP; u++)
+                                        hit[u] |= kind == LX_NIN ? (c ? cv[u][WX - 1] : cv[u][0]) == (uint32_t)v
+                                                                 : (c ? cx[u][WX - 1] : cx[u][0]) == v;
+                                }
+#pragma unroll
+                                for (int u = 0; u < RP; u++) b[u] = hit[u] != neg;
+                            }
 #pragma unroll
                             for (int u = 0; u < RP; u++) {
-                                const uint64_t X = c ? cx[u][WX - 1] : cx[u][0];
-                                b[u] = tt_result(tt, X < lit ? -1 : (X > lit ? 1 : 0));
+                                const bool nul = c ? cnull[u][WX - 1] : cnull[u][0];
+                                idx[u] |= ((nul ? nulv : b[u]) ? 1u : 0u) << l;
                             }
-                        } else {
-                            bool hit[RP];
-#pragma unroll
-                            for (int u = 0; u < RP; u++) hit[u] = false;
-                            const uint32_t nin = (meta >> 8) & 15u;
-                            for (uint32_t t = 0; t < nin; t++) {
-                                const uint64_t v = (uint64_t)L[6 + 2 * t] | ((uint64_t)L[7 + 2 * t] << 32);
-#pragma unroll
-                                for (int u = 0; u < RP; u++)
-                                    hit[u] |= kind == LX_NIN ? (c ? cv[u][WX - 1] : cv[u][0]) == (uint32_t)v
-                                                             : (c ? cx[u][WX - 1] : cx[u][0]) == v;
-                            }
-#pragma unroll
-                            for (int u = 0; u < RP; u++) b[u] = hit[u] != neg;
                         }
-#pragma unroll
-                        for (int u = 0; u < RP; u++) {
-                            const bool nul = c ? cnull[u][WX - 1] : cnull[u][0];
-                            idx[u] |= ((nul ? nulv : b[u]) ? 1u : 0u) << l;
-                        }
-                    }
                 }
 #pragma unroll
-                for (int u = 0; u < RP; u++) pass[u] = (tt16 >> idx[u]) & 1u;
+                    for (int u = 0; u < RP; u++) pass[u] = (tt16 >> idx[u]) & 1u;
+                } else {
+                    // two WHERE columns: record-major (the leaf-major form's live [RP][2] typed
+                    // values pushed this build into scratch: 64 bytes / lane, 3 % slower)
+#pragma unroll
+                    for (int u = 0; u < RP; u++) {
+                        bool cnull[2], cok[2];
+                        uint32_t cv[2];
+                        uint64_t cx[2];
+#pragma unroll
+                        for (int c = 0; c < WX; c++) {
+                            const uint32_t len = c ? xen[u] - xst[u] : wen[u] - wst[u];
+                            const uint32_t a0r = c ? xd[u] : wd[u], a1r = c ? xd1[u] : wd1[u];
+                            cnull[c] = len == 0;
+                            cv[c] = 0;
+                            cx[c] = 0;
+                            if ((fp.wx_str >> c) & 1) {
+                                const uint32_t m0 = len_mask(len, 0), m1 = len_mask(len, 1);
+                                const uint32_t a0 = a0r & m0, a1 = a1r & m1;
+                                const uint32_t c0 = a0 & 0xFFu;
+                                cok[c] = (int)(len - 1u < 8u) & (int)!(is_digit(c0) | (c0 == '-') | (c0 == '+') | (c0 == '.')) &
+                                         (int)((low_bytes(a0, m0 & nk.k80, nk) | low_bytes(a1, m1 & nk.k80, nk)) == 0);
+                                cx[c] = ((uint64_t)__builtin_bswap32(a0) << 32) | __builtin_bswap32(a1);
+                            } else {
+                                const Num n = num4<true>(a0r, len, nk);
+                                const uint32_t mul = (uint32_t)(0x0001000A006403E8ull >> (n.k << 4)) & 0xFFFFu;
+                                cv[c] = __umul24(n.M, mul);
+                                cok[c] = n.ok;
+                            }
+                            wu[u] |= !cok[c] & !cnull[c] & !fail[u];
+                        }
+                        uint32_t idx = 0;
+#pragma unroll
+                        for (int l = 0; l < 4; l++) {
+                            if ((uint32_t)l < nleaf) {
+                                const uint32_t* L = lxl + l * LX_WORDS;
+                                const uint32_t meta = __builtin_amdgcn_readfirstlane(L[0]);
+                                const uint32_t c = WX == 2 ? (meta >> 2) & 1u : 0u;
+                                const uint32_t V = c ? cv[WX - 1] : cv[0];
+                                const uint64_t X = c ? cx[WX - 1] : cx[0];
+                                const bool nul = c ? cnull[WX - 1] : cnull[0];
+                                const uint32_t kind = meta & 3u;
+                                const bool neg = (meta >> 3) & 1u;
+                                bool b;
+                                if (kind == LX_NUM) {
+                                    b = (V - L[1] <= L[2]) != neg;
+                                } else if (kind == LX_STR) {
+                                    const uint64_t lit = (uint64_t)L[4] | ((uint64_t)L[5] << 32);
+                                    b = tt_result((meta >> 5) & 7u, X < lit ? -1 : (X > lit ? 1 : 0));
+                                } else {
+                                    bool hit = false;
+                                    const uint32_t nin = (meta >> 8) & 15u;
+                                    for (uint32_t t = 0; t < nin; t++) {
+                                        const uint64_t v = (uint64_t)L[6 + 2 * t] | ((uint64_t)L[7 + 2 * t] << 32);
+                                        hit |= kind == LX_NIN ? V == (uint32_t)v : X == v;
+                                    }
+                                    b = hit != neg;
+                                }
+                                b = nul ? ((meta >> 4) & 1u) != 0 : b;
+                                idx |= (b ? 1u : 0u) << l;
+                            }
+                        }
+                        pass[u] = (tt16 >> idx) & 1u;
+                }
+                }
             } else if (WSTR) {
                 // a STRING field of 1-8 bytes: no leading digit / sign / dot (never a
                 // numeral or a date, infer_type csv_reader.c:133-240), no byte <= ' '
