@@ -232,12 +232,15 @@ hipError_t cq_jx_route(const uint8_t* g, uint64_t lo, uint64_t hi, uint32_t ws, 
                        hipStream_t s);
 hipError_t cq_jx_ent_build(const void* ent, unsigned long long n, uint32_t qoff, unsigned long long range, uint16_t* d16,
                            uint32_t* l32, unsigned long long* ttab, unsigned long long* nplaced, unsigned int* flag,
-                           int grid, hipStream_t s, int ungrouped);
+                           int grid, hipStream_t s, int ungrouped, uint32_t* notmono);
+hipError_t cq_jx_ent_first(const uint32_t* gminix, const uint32_t* l32, const uint32_t* notmono, uint32_t* gfirst,
+                           hipStream_t s);
 hipError_t cq_jx_ent_part(const void* ent, unsigned long long n, uint32_t qoff, unsigned long long range, uint32_t np,
                           uint32_t pcap, uint32_t psh, unsigned long long* pent, uint32_t* pcnt, unsigned int* flag,
                           int grid, hipStream_t s);
 hipError_t cq_jx_ent_probe(const void* ent, unsigned long long n, uint32_t qoff, unsigned long long range, uint16_t* d16,
-                           unsigned long long* gsum, unsigned long long* npairs, int grid, hipStream_t s);
+                           unsigned long long* gsum, unsigned long long* npairs, int grid, hipStream_t s,
+                           const uint32_t* notmono, uint32_t* gminix);
 hipError_t cq_jx_probe(int grouped, int value, int direct, const unsigned long long* pkey,
                        const unsigned long long* ppay, const uint32_t* poff, uint32_t n, unsigned long long kmin,
                        const void* table, uint64_t tcap, const unsigned long long* bpay, const uint32_t* boff,
@@ -7297,21 +7300,29 @@ uint32_t typed_receive(DevCtx& c, const TypedJoin& tj, const void* ub, uint64_t 
     if (range >= (1ull << 31) || qoff >= (1ull << 32)) return 16u;
     const size_t b16 = (range * 2 + 15) & ~(size_t)15;
     DevBuf d16(b16 + 16), l32(range * 4 + 16);
-    const size_t o_gsum = (size_t)G * 8, o_first = o_gsum + (size_t)G * 24, o_ctl = o_first + (size_t)G * 4;
+    // small: tags, per group sums, first ids, smallest matched slots (both ~0 at the
+    // start), flags and counts
+    const size_t o_gsum = (size_t)G * 8, o_first = o_gsum + (size_t)G * 24, o_minix = o_first + (size_t)G * 4,
+                 o_ctl = o_minix + (size_t)G * 4;
     DevBuf small(o_ctl + 64);
     unsigned long long* ttab = small.as<unsigned long long>();
     unsigned long long* gsum = (unsigned long long*)(small.as<uint8_t>() + o_gsum);
     uint32_t* gfirst = (uint32_t*)(small.as<uint8_t>() + o_first);
+    uint32_t* gminix = (uint32_t*)(small.as<uint8_t>() + o_minix);
     unsigned int* flag = (unsigned int*)(small.as<uint8_t>() + o_ctl);
     unsigned long long* cnts = (unsigned long long*)(small.as<uint8_t>() + o_ctl + 8);   // placed, pairs, occupied
     uint32_t* notmono = (uint32_t*)(small.as<uint8_t>() + o_ctl + 32);
     HIPCHECK(cq_jx_star_init(d16.p, b16, small.p, o_ctl + 64, (uint32_t)o_first, (uint32_t)o_ctl,
                              (uint32_t)o_ctl + 48, nullptr, 0, c.ncu * 4, c.stream));
-    HIPCHECK(hipMemsetAsync(notmono, 1, 4, c.stream));     // the matched-flag form of the first pairs
+    // notmono (zeroed by star_init): the build sets it unless the slots rise along the
+    // entries (global-id order); rising, the probe keeps each group's smallest matched
+    // slot (no d16 match flags, no jx_star_first scan); CQGPU_TYPED_FLAGS=1 forces the
+    // matched-flag form
+    if (getenv("CQGPU_TYPED_FLAGS")) HIPCHECK(hipMemsetAsync(notmono, 1, 4, c.stream));
     HIPCHECK(hipEventRecord(c.ev0, c.stream));
     // (ungrouped: no tag lookup, every build entry in group 0)
     HIPCHECK(cq_jx_ent_build(ub, nu, (uint32_t)qoff, range, d16.as<uint16_t>(), l32.as<uint32_t>(), ttab, cnts, flag,
-                             c.ncu * 4, c.stream, grouped ? 0 : 1));
+                             c.ncu * 4, c.stream, grouped ? 0 : 1, notmono));
     // the probe: when d16 outgrows an XCD's L2, in two passes -- the entries into 2 MiB
     // key partitions (jx_ent_part_kernel), then each partition looked up by one XCD's
     // blocks (jx_part_probe_kernel, the CSV STAR's pass 2); a full segment (skewed keys)
@@ -7336,11 +7347,13 @@ uint32_t typed_receive(DevCtx& c, const TypedJoin& tj, const void* ub, uint64_t 
         HIPCHECK(cq_jx_ent_part(ob, no, (uint32_t)qoff, range, (uint32_t)np64, pcap, PSH, pent.as<unsigned long long>(),
                                 pcnt.as<uint32_t>(), flag, (int)pgrid, c.stream));
         HIPCHECK(cq_jx_part_probe(pent.as<unsigned long long>(), pcnt.as<uint32_t>(), pgrid, (uint32_t)np64, pcap, range,
-                                  d16.as<uint16_t>(), notmono, gsum, gfirst, cnts + 1, std::max(8, (c.ncu / 8) * 8),
+                                  d16.as<uint16_t>(), notmono, gsum, gminix, cnts + 1, std::max(8, (c.ncu / 8) * 8),
                                   c.stream));
     } else {
-        HIPCHECK(cq_jx_ent_probe(ob, no, (uint32_t)qoff, range, d16.as<uint16_t>(), gsum, cnts + 1, c.ncu * 4, c.stream));
+        HIPCHECK(cq_jx_ent_probe(ob, no, (uint32_t)qoff, range, d16.as<uint16_t>(), gsum, cnts + 1, c.ncu * 4, c.stream,
+                                 notmono, gminix));
     }
+    HIPCHECK(cq_jx_ent_first(gminix, l32.as<uint32_t>(), notmono, gfirst, c.stream));   // (rising keys only)
     HIPCHECK(cq_jx_star_first(d16.as<uint16_t>(), l32.as<uint32_t>(), range, notmono, gfirst, cnts + 2, c.ncu * 4,
                               c.stream));
     HIPCHECK(hipEventRecord(c.ev1, c.stream));
@@ -7362,7 +7375,9 @@ uint32_t typed_receive(DevCtx& c, const TypedJoin& tj, const void* ub, uint64_t 
     }
     unsigned long long cn[3];
     memcpy(cn, h.data() + o_ctl + 8, 24);
-    if (cn[0] != cn[2]) fl |= 64u;                       // a repeated build key
+    uint32_t nm = 0;
+    memcpy(&nm, h.data() + o_ctl + 32, 4);
+    if (nm && cn[0] != cn[2]) fl |= 64u;                 // a repeated build key (rising keys are distinct)
     if (fl) return fl;
     g_stats.records = nu + no;
     g_stats.passed = cn[1];

@@ -2064,11 +2064,17 @@ __global__ __launch_bounds__(LT) void jx_extract_kernel(const uint8_t* __restric
                     }
                     if (tot == 0) continue;
                     if constexpr (ROUTE == 2) {
-                        uint32_t pre = __builtin_amdgcn_readlane(rbase, d) + __builtin_amdgcn_readlane(rrun, d);
+                        // file order within the window's run for d: the lanes below's records,
+                        // then this lane's earlier ones (entries in global-id order: the
+                        // receiver's STAR sees its build keys rise when the ids do)
+                        const uint32_t pre = __builtin_amdgcn_readlane(rbase, d) + __builtin_amdgcn_readlane(rrun, d);
+                        uint32_t below = 0;
+#pragma unroll
+                        for (int u = 0; u < RP; u++) below += (uint32_t)__popcll(m[u] & lt);
+                        uint32_t mine = 0;
 #pragma unroll
                         for (int u = 0; u < RP; u++) {
-                            if ((m[u] >> lane) & 1ull) pos[u] = pre + (uint32_t)__popcll(m[u] & lt);
-                            pre += (uint32_t)__popcll(m[u]);
+                            if ((m[u] >> lane) & 1ull) pos[u] = pre + below + mine++;
                         }
                     }
                     rrun += (uint32_t)lane == d ? tot : 0u;
@@ -2420,12 +2426,14 @@ __global__ __launch_bounds__(1024) void jx_ent_build_kernel(const uint4* __restr
                                                             uint32_t* __restrict__ l32,
                                                             unsigned long long* __restrict__ ttab,
                                                             unsigned long long* __restrict__ nplaced,
-                                                            unsigned int* __restrict__ flag, uint32_t ungrouped) {
+                                                            unsigned int* __restrict__ flag, uint32_t ungrouped,
+                                                            uint32_t* __restrict__ notmono) {
     __shared__ unsigned long long lt[JX_G];       // the block's mirror of the tag table
     for (uint32_t k = threadIdx.x; k < JX_G; k += blockDim.x) lt[k] = ttab[k];
     __syncthreads();
     uint32_t fl = 0;
     unsigned long long placed = 0;
+    bool fall = false;
     const uint64_t nt = (uint64_t)gridDim.x * blockDim.x;
     // (latency-bound at two entries in flight per thread: SQ_WAIT_ANY / SQ_WAVE_CYCLES 0.72,
     // profiles/r6_pmc.json; JXB_U entries in flight, streamed past the caches)
@@ -2434,12 +2442,15 @@ __global__ __launch_bounds__(1024) void jx_ent_build_kernel(const uint4* __restr
 #endif
     for (uint64_t i = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x; i < n; i += JXB_U * nt) {
         uint4 e[JXB_U];
+        uint32_t nq[JXB_U];
         bool ok[JXB_U];
 #pragma unroll
         for (int u = 0; u < JXB_U; u++) {
             ok[u] = i + u * nt < n;
             const v4u x = ok[u] ? __builtin_nontemporal_load((const v4u*)(ent + i + u * nt)) : v4u{0u, 0u, 0u, 0u};
             e[u] = make_uint4(x.x, x.y, x.z, x.w);
+            // the next entry's q32 (lanes 0-62: the line the next lane loads)
+            nq[u] = i + u * nt + 1 < n ? ((const uint32_t*)(ent + i + u * nt + 1))[0] : ~0u;
         }
 #pragma unroll
         for (int u = 0; u < JXB_U; u++) {
@@ -2453,8 +2464,13 @@ __global__ __launch_bounds__(1024) void jx_ent_build_kernel(const uint4* __restr
             d16[slot] = (uint16_t)(gid + 1u);
             l32[slot] = e[u].y;
             placed++;
+            // the entries come in global-id order (sources in rank order, each in file
+            // order): slots rising along them mean a group's smallest matched slot is its
+            // smallest matched id -- the probe then needs no match flags in d16
+            if (nq[u] <= e[u].x) fall = true;
         }
     }
+    if (__any(fall) && (threadIdx.x & 63) == 0) atomicOr(notmono, 1u);
     for (int o = 32; o > 0; o >>= 1) {
         fl |= (uint32_t)__shfl_down((int)fl, o, 64);
         placed += __shfl_down(placed, o, 64);
@@ -2463,6 +2479,13 @@ __global__ __launch_bounds__(1024) void jx_ent_build_kernel(const uint4* __restr
         if (fl) atomicOr(flag, fl);
         if (placed) atomicAdd(nplaced, placed);
     }
+}
+
+// the rising-keys form's first pairs: each group's smallest matched slot -> its id
+__global__ void jx_ent_first_kernel(const uint32_t* __restrict__ gminix, const uint32_t* __restrict__ l32,
+                                    const uint32_t* __restrict__ notmono, uint32_t* __restrict__ gfirst) {
+    if (*notmono) return;
+    for (uint32_t k = threadIdx.x; k < JX_G; k += blockDim.x) gfirst[k] = gminix[k] != ~0u ? l32[gminix[k]] : ~0u;
 }
 
 // partitioned probe over typed entries, pass 1: every probe entry whose slot (q32 -
@@ -2512,10 +2535,15 @@ __global__ __launch_bounds__(1024) void jx_ent_part_kernel(const uint2* __restri
 __global__ __launch_bounds__(1024) void jx_ent_probe_kernel(const uint2* __restrict__ ent, uint64_t n, uint32_t qoff,
                                                             uint64_t range, uint16_t* __restrict__ d16,
                                                             unsigned long long* __restrict__ gsum,
-                                                            unsigned long long* __restrict__ npairs) {
+                                                            unsigned long long* __restrict__ npairs,
+                                                            const uint32_t* __restrict__ notmono,
+                                                            uint32_t* __restrict__ gminix) {
     __shared__ unsigned long long sfix[JX_G];
-    __shared__ uint32_t scnt[JX_G], snum[JX_G];
-    for (uint32_t k = threadIdx.x; k < JX_G; k += blockDim.x) { sfix[k] = 0; scnt[k] = 0; snum[k] = 0; }
+    __shared__ uint32_t scnt[JX_G], snum[JX_G], smix[JX_G];
+    for (uint32_t k = threadIdx.x; k < JX_G; k += blockDim.x) { sfix[k] = 0; scnt[k] = 0; snum[k] = 0; smix[k] = ~0u; }
+    // rising build keys (jx_ent_build_kernel): the smallest matched slot per group in
+    // LDS instead of the d16 match flags
+    const bool mono = __builtin_amdgcn_readfirstlane(*notmono) == 0u;
     __syncthreads();
     unsigned long long pairs = 0;
     const uint64_t nt = (uint64_t)gridDim.x * blockDim.x;
@@ -2540,7 +2568,11 @@ __global__ __launch_bounds__(1024) void jx_ent_probe_kernel(const uint2* __restr
             if (!gv[u]) continue;
             const uint32_t gi = (gv[u] & 0x7FFFu) - 1u;
 #if !defined(PROBE_EXP) || PROBE_EXP == 0
-            if (!(gv[u] & 0x8000u)) d16[slot[u]] = (uint16_t)(gv[u] | 0x8000u);   // (every writer: the same value)
+            if (mono) {
+                if ((uint32_t)slot[u] < smix[gi]) atomicMin(&smix[gi], (uint32_t)slot[u]);
+            } else if (!(gv[u] & 0x8000u)) {
+                d16[slot[u]] = (uint16_t)(gv[u] | 0x8000u);   // (every writer: the same value)
+            }
 #endif
             atomicAdd(&scnt[gi], 1u);
             if (e[u].y != JX_PNULL) {
@@ -2555,6 +2587,7 @@ __global__ __launch_bounds__(1024) void jx_ent_probe_kernel(const uint2* __restr
     __syncthreads();
     for (uint32_t k = threadIdx.x; k < JX_G; k += blockDim.x) {
         if (!scnt[k]) continue;
+        if (mono) atomicMin(&gminix[k], smix[k]);
         atomicAdd(&gsum[3 * k], (unsigned long long)scnt[k]);
         if (snum[k]) {
             atomicAdd(&gsum[3 * k + 1], sfix[k]);
@@ -3512,10 +3545,15 @@ hipError_t cq_jx_route(const uint8_t* g, uint64_t lo, uint64_t hi, uint32_t ws, 
 // the receiving rank's STAR over the entries (jx_ent_build_kernel, jx_ent_probe_kernel)
 hipError_t cq_jx_ent_build(const void* ent, unsigned long long n, uint32_t qoff, unsigned long long range, uint16_t* d16,
                            uint32_t* l32, unsigned long long* ttab, unsigned long long* nplaced, unsigned int* flag,
-                           int grid, hipStream_t s, int ungrouped) {
+                           int grid, hipStream_t s, int ungrouped, uint32_t* notmono) {
     if (!n) return hipSuccess;
     hipLaunchKernelGGL(cq::fast::jx_ent_build_kernel, dim3(grid), dim3(1024), 0, s, (const uint4*)ent, (uint64_t)n, qoff,
-                       (uint64_t)range, d16, l32, ttab, nplaced, flag, (uint32_t)(ungrouped != 0));
+                       (uint64_t)range, d16, l32, ttab, nplaced, flag, (uint32_t)(ungrouped != 0), notmono);
+    return hipGetLastError();
+}
+hipError_t cq_jx_ent_first(const uint32_t* gminix, const uint32_t* l32, const uint32_t* notmono, uint32_t* gfirst,
+                           hipStream_t s) {
+    hipLaunchKernelGGL(cq::fast::jx_ent_first_kernel, dim3(1), dim3(1024), 0, s, gminix, l32, notmono, gfirst);
     return hipGetLastError();
 }
 hipError_t cq_jx_ent_part(const void* ent, unsigned long long n, uint32_t qoff, unsigned long long range, uint32_t np,
@@ -3529,10 +3567,11 @@ hipError_t cq_jx_ent_part(const void* ent, unsigned long long n, uint32_t qoff, 
     return hipGetLastError();
 }
 hipError_t cq_jx_ent_probe(const void* ent, unsigned long long n, uint32_t qoff, unsigned long long range, uint16_t* d16,
-                           unsigned long long* gsum, unsigned long long* npairs, int grid, hipStream_t s) {
+                           unsigned long long* gsum, unsigned long long* npairs, int grid, hipStream_t s,
+                           const uint32_t* notmono, uint32_t* gminix) {
     if (!n) return hipSuccess;
     hipLaunchKernelGGL(cq::fast::jx_ent_probe_kernel, dim3(grid), dim3(1024), 0, s, (const uint2*)ent, (uint64_t)n, qoff,
-                       (uint64_t)range, d16, gsum, npairs);
+                       (uint64_t)range, d16, gsum, npairs, notmono, gminix);
     return hipGetLastError();
 }
 

@@ -1015,6 +1015,39 @@ def test_typed_exchange_partitioned_probe(files, nranks, qi, monkeypatch):
     compare(got, want, tol, f"typed exchange, partitioned probe, {nranks} ranks: {sql}")
 
 
+@pytest.mark.parametrize("order", ["rising", "shuffled"])
+@pytest.mark.parametrize("flags", [False, True])
+def test_typed_exchange_first_pair_forms(tmp_path, monkeypatch, order, flags):
+    """a group's first pair: with the build keys rising along the entries (global-id
+    order) the probe keeps each group's smallest matched slot; shuffled keys -- or
+    CQGPU_TYPED_FLAGS=1 -- take the d16 match flags and the first-pair scan.  Both give
+    the oracle's groups in first-appearance order, at 1 and 3 ranks"""
+    if flags:
+        monkeypatch.setenv("CQGPU_TYPED_FLAGS", "1")
+    rng = np.random.default_rng(17)
+    ids = np.arange(3000) + 500
+    if order == "shuffled":
+        rng.shuffle(ids)
+    users = "id,name,role\n" + "".join("%d,n%d,r%02d\n" % (k, i, rng.integers(0, 40)) for i, k in enumerate(ids))
+    orders = "id,price,customer_id\n" + "".join(
+        "%d,%d.%d,%d\n" % (i, rng.integers(0, 999), rng.integers(0, 9), 500 + rng.integers(0, 3200))
+        for i in range(12000))
+    up, op = tmp_path / "u.csv", tmp_path / "o.csv"
+    up.write_text(users)
+    op.write_text(orders)
+    sql = (f"SELECT u.role, COUNT(*), SUM(o.price) FROM '{up}' AS u JOIN '{op}' AS o "
+           f"ON u.id = o.customer_id GROUP BY u.role")
+    want, _ = cqtest.oracle_query(sql)
+    for nranks in (1, 3):
+        with cqtest.Parsed(sql) as ast:
+            tp, why = _typed(ast, users.encode(), orders.encode(), nranks, {})
+            assert tp, (cq_amd.last_error(), why)
+            got = abi.table_to_py(tp)
+            cq_amd.result_free(tp)
+            tol = tolerant_columns(ast)
+        compare(got, want, tol, f"typed exchange, {order} keys, flags {flags}, {nranks} ranks")
+
+
 def test_typed_exchange_partition_overflow(tmp_path, monkeypatch):
     """skewed probe keys (90 % of 120 K orders on one user) overflow a partition
     segment: the receive reruns unpartitioned and still gives the oracle's answer"""
