@@ -2215,15 +2215,17 @@ void free_row(cq_row& row) {
 }
 
 // build_aggregated_result rows (evaluator_aggregates.c:596-693)
+// order (optional): row g is groups[(*order)[g]] (a merge's first-pair order without
+// moving the groups)
 cq_table* build_groups(const Compiled& C, const std::vector<HGroup>& groups, const Literals& L,
-                       DevCtx& c) {
+                       DevCtx& c, const std::vector<uint32_t>* order = nullptr) {
     cq_table* r = new_result(C.names);
     r->nrows = r->row_capacity = (int)groups.size();
     r->rows = (cq_row*)malloc(sizeof(cq_row) * std::max<size_t>(groups.size(), 1));
     std::vector<HCell> litcells;
     if (!L.cells.empty()) litcells = L.host;
     for (size_t g = 0; g < groups.size(); g++) {
-        const HGroup& h = groups[g];
+        const HGroup& h = groups[order ? (*order)[g] : g];
         cq_row& row = r->rows[g];
         row.ncols = r->ncols;
         row.values = (cq_value*)calloc(std::max(r->ncols, 1), sizeof(cq_value));
@@ -6319,26 +6321,20 @@ cq_table* cqgpu_merge_partials(cq_node* q, const void* const* blobs, const size_
                 h.vla[v] = h.vn[v] > 0 ? sqrt(h.vm2[v] / h.vn[v]) : 0.0;
             }
         PHASE("merge groups");
-        {                                  // (by index: an HGroup is large to move)
-            std::vector<uint32_t> ord(merged.size());
-            for (size_t i = 0; i < ord.size(); i++) ord[i] = (uint32_t)i;
-            std::stable_sort(ord.begin(), ord.end(),
-                             [&](uint32_t x, uint32_t y) { return merged[x].first < merged[y].first; });
-            bool sorted = true;
-            for (size_t i = 0; i < ord.size() && sorted; i++) sorted = ord[i] == i;
-            if (!sorted) {
-                std::vector<HGroup> out;
-                out.reserve(merged.size());
-                for (uint32_t i : ord) out.push_back(std::move(merged[i]));
-                merged.swap(out);
-            }
+        // first-pair order, by index (an HGroup is large to move; the rows are built in it)
+        std::vector<uint32_t> ord(merged.size());
+        {
+            std::vector<std::pair<unsigned long long, uint32_t>> fk(merged.size());
+            for (size_t i = 0; i < fk.size(); i++) fk[i] = {merged[i].first, (uint32_t)i};
+            std::sort(fk.begin(), fk.end());             // (ties by index: a stable order)
+            for (size_t i = 0; i < fk.size(); i++) ord[i] = fk[i].second;
         }
         PHASE("merge sort");
         Literals L;
         parse_literals(c, C.lits, L);
         PHASE("merge literals");
         g_stats.groups = merged.size();
-        cq_table* res = build_groups(C, merged, L, c);
+        cq_table* res = build_groups(C, merged, L, c, &ord);
         PHASE("merge build");
         post_ops(c, res, q);
         PHASE("merge post");
@@ -7389,7 +7385,15 @@ uint32_t typed_receive(DevCtx& c, const TypedJoin& tj, const void* ub, uint64_t 
     const uint32_t nrep = (uint32_t)tj.C.rep_cols.size();
     std::vector<HGroup> groups;
     groups.reserve(G);
-    std::map<std::tuple<uint64_t, uint64_t, uint64_t>, size_t> at;
+    struct KeyHash {
+        size_t operator()(const std::tuple<uint64_t, uint64_t, uint64_t>& k) const {
+            uint64_t x = std::get<0>(k) * 0x9E3779B97F4A7C15ull ^ std::get<1>(k) ^ (std::get<2>(k) * 0xC2B2AE3D27D4EB4Full);
+            x ^= x >> 29;
+            return (size_t)(x * 0xBF58476D1CE4E5B9ull);
+        }
+    };
+    std::unordered_map<std::tuple<uint64_t, uint64_t, uint64_t>, size_t, KeyHash> at;
+    at.reserve(2 * (size_t)G);
     auto fill = [&](HGroup& x, uint32_t s) {
         x.cnt = hs[3 * s];
         x.first = hf[s] == ~0u ? NOPOS : ((unsigned long long)hf[s] << 32);

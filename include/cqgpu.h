@@ -266,8 +266,9 @@ cq_table* cqgpu_gm_local(cq_node* query_ast, cqgpu_table* const* shards, int n);
  * (concatenated in source-rank order) and runs cqgpu_query_partial on the pair;
  * cqgpu_merge_partials gives the whole-input result -- groups in first-appearance
  * order of the (l, r) nested loop, as perform_join + create_groups would.
- * Inputs whose keys mix value classes (which value_compare calls "equal") are
- * refused by the merge.
+ * Keys of several value classes (which value_compare calls "equal" across classes)
+ * and a JOIN without ON take cqgpu_route_plan2's replicated routing below; with plain
+ * cqgpu_route_plan such inputs are refused by the merge.
  *
  * route_plan: computes the routing of tables[side] (tables = {FROM shard, JOIN
  * shard}, needed to bind the ON operands) and writes per destination rank the
