@@ -2054,6 +2054,40 @@ __global__ __launch_bounds__(LT) void jx_extract_kernel(const uint8_t* __restric
                 uint32_t pos[RP];
 #pragma unroll
                 for (int u = 0; u < RP; u++) pos[u] = 0;
+                if (nd <= 8u) {
+                    // one packed histogram per lane (8-bit fields, destinations 0-3 / 4-7 in
+                    // two words; at most 64 * RP <= 192 per field) and two wave scans of it,
+                    // instead of a ballot and popcount per destination and record: the
+                    // scans' totals are each destination's entries this pass (lane d's
+                    // running count); emit: the exclusive scans are the entries of the lanes
+                    // below per destination -- a record's file-order rank in its run is that
+                    // plus this lane's earlier records of the same destination
+                    uint32_t h0 = 0, h1 = 0;
+#pragma unroll
+                    for (int u = 0; u < RP; u++) {
+                        const uint32_t one = take[u] ? 1u << (8u * (dd[u] & 3u)) : 0u;
+                        h0 += dd[u] < 4u ? one : 0u;
+                        h1 += dd[u] < 4u ? 0u : one;
+                    }
+                    const uint32_t s0 = wave_incl_scan(h0), s1 = wave_incl_scan(h1);
+                    const uint32_t t0 = __builtin_amdgcn_readlane(s0, 63), t1 = __builtin_amdgcn_readlane(s1, 63);
+                    if constexpr (ROUTE == 2) {
+                        const uint32_t e0 = s0 - h0, e1 = s1 - h1;        // exclusive: the lanes below
+                        const int base = (int)(rbase + rrun);               // lane d: destination d's next
+#pragma unroll
+                        for (int u = 0; u < RP; u++) {
+                            const uint32_t d = dd[u] & 7u;
+                            uint32_t mine = 0;
+#pragma unroll
+                            for (int v = 0; v < u; v++) mine += (take[v] && dd[v] == dd[u]) ? 1u : 0u;
+                            const uint32_t below = ((d < 4u ? e0 : e1) >> (8u * (d & 3u))) & 0xFFu;
+                            const uint32_t b = (uint32_t)__shfl(base, (int)d, 64);
+                            pos[u] = b + below + mine;
+                        }
+                    }
+                    const uint32_t tw = lane < 4 ? t0 : t1;
+                    rrun += (uint32_t)lane < nd ? (tw >> (8u * ((uint32_t)lane & 3u))) & 0xFFu : 0u;
+                } else
                 for (uint32_t d = 0; d < nd; d++) {
                     uint64_t m[RP];
                     uint32_t tot = 0;
