@@ -107,6 +107,9 @@ hipError_t cq_launch_join_emit(const cq::Cell* L, uint32_t ls, uint32_t lk, uint
                                uint2* pairs, unsigned int* rmatched, hipStream_t s);
 hipError_t cq_launch_route_runs(const uint32_t* dest, const uint32_t* len, uint32_t n, uint32_t nw, uint32_t nranks,
                                 unsigned long long* rcnt, unsigned long long* rbytes, hipStream_t s);
+hipError_t cq_launch_typed_summary(const unsigned int* roffs, const unsigned int* rcnt, const unsigned int* wbase,
+                                   const unsigned int* wcount, uint64_t nw, uint32_t nranks, const uint32_t* ctl,
+                                   uint32_t* out, hipStream_t s);
 hipError_t cq_launch_route_dest_mode(const uint32_t* cls, uint32_t n, uint32_t nranks, uint32_t rep, uint32_t fixed,
                                     uint32_t* dest, hipStream_t s);
 hipError_t cq_launch_pair_rep_flags(const uint2* pairs, unsigned long long np, const cq::Cell* L, uint32_t ls,
@@ -7227,22 +7230,18 @@ TypedSend& typed_count_pass(DevCtx& c, cqgpu_table* t, bool build, int kcol, int
     HIPCHECK(cq_excl_sum_u32(tmp.p, &tb, ts->rcnt.as<unsigned int>(), ts->roffs.as<unsigned int>(), nn, c.stream));
     if (build && nw)
         HIPCHECK(cq_excl_sum_u32(tmp.p, &tb, ts->wcount.as<unsigned int>(), ts->wbase.as<unsigned int>(), nw, c.stream));
-    // back to the host: every destination's first position (a strided copy), the totals,
-    // the flags and the key range
-    uint8_t* h = (uint8_t*)pinned(c, 64 + 8 * (size_t)N + 32);
-    uint32_t* hstart = (uint32_t*)(h + 64);
-    uint32_t* htail = hstart + N;                    // [0] last roffs, [1] last rcnt, [2] last wbase, [3] last wcount
-    if (nw) {
-        HIPCHECK(hipMemcpy2DAsync(hstart, 4, ts->roffs.p, nw * 4, 4, (size_t)N, hipMemcpyDeviceToHost, c.stream));
-        HIPCHECK(hipMemcpyAsync(htail, ts->roffs.as<unsigned int>() + nn - 1, 4, hipMemcpyDeviceToHost, c.stream));
-        HIPCHECK(hipMemcpyAsync(htail + 1, ts->rcnt.as<unsigned int>() + nn - 1, 4, hipMemcpyDeviceToHost, c.stream));
-        if (build) {
-            HIPCHECK(hipMemcpyAsync(htail + 2, ts->wbase.as<unsigned int>() + nw - 1, 4, hipMemcpyDeviceToHost, c.stream));
-            HIPCHECK(hipMemcpyAsync(htail + 3, ts->wcount.as<unsigned int>() + nw - 1, 4, hipMemcpyDeviceToHost, c.stream));
-        }
-    }
-    HIPCHECK(hipMemcpyAsync(h, ctl.p, 32, hipMemcpyDeviceToHost, c.stream));
+    // back to the host in one copy (typed_summary_kernel): the flags and key range, every
+    // destination's first position, the totals
+    DevBuf dsum(4 * (12 + (size_t)N));
+    HIPCHECK(cq_launch_typed_summary(ts->roffs.as<unsigned int>(), ts->rcnt.as<unsigned int>(),
+                                     build && nw ? ts->wbase.as<unsigned int>() : nullptr,
+                                     build && nw ? ts->wcount.as<unsigned int>() : nullptr, nw, (uint32_t)N,
+                                     (const uint32_t*)ctl.p, dsum.as<uint32_t>(), c.stream));
+    uint8_t* h = (uint8_t*)pinned(c, 4 * (12 + (size_t)N));
+    HIPCHECK(hipMemcpyAsync(h, dsum.p, 4 * (12 + (size_t)N), hipMemcpyDeviceToHost, c.stream));
     HIPCHECK(hipStreamSynchronize(c.stream));
+    uint32_t* hstart = (uint32_t*)(h + 32);
+    uint32_t* htail = hstart + N;                    // [0] last roffs, [1] last rcnt, [2] last wbase, [3] last wcount
     memcpy(&ts->flags, h, 4);
     memcpy(ts->krange, h + 16, 16);
     ts->rstart.assign((size_t)N + 1, 0);

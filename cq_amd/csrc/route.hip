@@ -639,6 +639,32 @@ hipError_t cq_launch_route_dest_mode(const uint32_t* cls, uint32_t n, uint32_t n
     route_dest_mode_kernel<<<blocks(n, 256), 256, 0, s>>>(cls, n, nranks, rep, fixed, dest);
     return hipGetLastError();
 }
+// the typed exchange's count pass, back to the host in one copy: every destination's
+// first region position (roffs[d * nw]), the last window's scan and count (the totals),
+// the build side's last window base and records, and the 32-byte control block
+// (flags, key range)
+__global__ void typed_summary_kernel(const unsigned int* __restrict__ roffs, const unsigned int* __restrict__ rcnt,
+                                     const unsigned int* __restrict__ wbase, const unsigned int* __restrict__ wcount,
+                                     uint64_t nw, uint32_t nranks, const uint32_t* __restrict__ ctl,
+                                     uint32_t* __restrict__ out) {
+    const uint32_t t = threadIdx.x;
+    const uint64_t nn = nw * nranks;
+    if (t < 8) out[t] = ctl[t];
+    if (t < nranks) out[8 + t] = nw ? roffs[(uint64_t)t * nw] : 0u;
+    if (t == 0) {
+        out[8 + nranks] = nw ? roffs[nn - 1] : 0u;
+        out[9 + nranks] = nw ? rcnt[nn - 1] : 0u;
+        out[10 + nranks] = nw && wbase ? wbase[nw - 1] : 0u;
+        out[11 + nranks] = nw && wcount ? wcount[nw - 1] : 0u;
+    }
+}
+hipError_t cq_launch_typed_summary(const unsigned int* roffs, const unsigned int* rcnt, const unsigned int* wbase,
+                                   const unsigned int* wcount, uint64_t nw, uint32_t nranks, const uint32_t* ctl,
+                                   uint32_t* out, hipStream_t s) {
+    if (nranks > 64) return hipErrorInvalidValue;
+    typed_summary_kernel<<<1, 64, 0, s>>>(roffs, rcnt, wbase, wcount, nw, nranks, ctl, out);
+    return hipGetLastError();
+}
 hipError_t cq_launch_route_runs(const uint32_t* dest, const uint32_t* len, uint32_t n, uint32_t nw, uint32_t nranks,
                                 unsigned long long* rcnt, unsigned long long* rbytes, hipStream_t s) {
     if (!n) return hipSuccess;
