@@ -228,11 +228,12 @@ hipError_t cq_jx_star_flush(int grouped, int value, const unsigned long long* tt
                             const unsigned long long* cnts, const cq::GroupTable* rt, int nacc, cq::ScanStats* stats,
                             unsigned int* flag, hipStream_t s);
 uint32_t cq_jx_star_groups();
+uint32_t cq_jx_rchunk();
 hipError_t cq_jx_route(const uint8_t* g, uint64_t lo, uint64_t hi, uint32_t ws, uint32_t delim, uint32_t quote,
                        int kcol, int pcol, int build, int rp, int pass, uint32_t nranks, unsigned long long qbase,
                        unsigned long long gbase, unsigned int* rcnt, unsigned int* wcount, const unsigned int* roffs,
-                       const unsigned int* wbase, void* rent, unsigned int* flag, unsigned long long* krange, int grid,
-                       hipStream_t s);
+                       const unsigned int* wbase, void* rent, uint32_t cap, unsigned int* flag,
+                       unsigned long long* krange, int grid, hipStream_t s);
 hipError_t cq_jx_ent_build(const void* ent, unsigned long long n, uint32_t qoff, unsigned long long range, uint16_t* d16,
                            uint32_t* l32, unsigned long long* ttab, unsigned long long* nplaced, unsigned int* flag,
                            int grid, hipStream_t s, int ungrouped, uint32_t* notmono);
@@ -617,6 +618,8 @@ struct TypedSend {
     DevBuf ent;
     uint64_t esize = 0;
     bool emitted = false;
+    bool one_pass = false;                          // (probe) entries written by the count (ROUTE 3)
+    uint32_t eflags = 0;                            // one pass: the emit pass's flags (512)
 };
 
 constexpr uint64_t SAMPLE_BYTES = 256u << 10;   // bytes a table keeps for plan-time sampling
@@ -671,6 +674,7 @@ struct cqgpu_table {
     uint32_t nrec_starts = 0;
     // the typed join exchange (cqgpu_typed_*): this table's counts and pending entries
     std::unique_ptr<TypedSend> tsend;
+    uint64_t est_records = 0;        // the sample's record count scaled to the table (0: not yet)
 };
 
 namespace {
@@ -7189,8 +7193,11 @@ uint64_t typed_sample_kmin(const cqgpu_table* t, int kcol) {
 // the count pass over one side (jx_extract_kernel ROUTE 1): per (destination, window)
 // the entries, their destination-major exclusive scan (every entry's region position
 // base) and per destination the entries; build: the records per window and their scan
-// (the global ids); flags 1 (a key the entries cannot carry: the CSV exchange), 8, 16
-TypedSend& typed_count_pass(DevCtx& c, cqgpu_table* t, bool build, int kcol, int N, uint64_t qbase) {
+// (the global ids); flags 1 (a key the entries cannot carry: the CSV exchange), 8, 16.
+// The probe side (pcol: its SUM column or -1) at N <= 8 takes one pass instead
+// (typed_one_pass); CQGPU_TYPED_TWO_PASS=1 keeps the count + emit passes.
+bool typed_one_pass(DevCtx& c, cqgpu_table* t, int kcol, int pcol, TypedSend& ts);
+TypedSend& typed_count_pass(DevCtx& c, cqgpu_table* t, bool build, int kcol, int N, uint64_t qbase, int pcol = -1) {
     std::unique_ptr<TypedSend> ts(new TypedSend);
     typed_stride(t, &ts->ws, &ts->rp);
     ts->N = (uint32_t)N;
@@ -7198,6 +7205,10 @@ TypedSend& typed_count_pass(DevCtx& c, cqgpu_table* t, bool build, int kcol, int
     const uint64_t nw = cq_jx_windows(t->data_begin, t->n, ts->ws);
     if (nw * (uint64_t)N >= (1ull << 31)) throw Ineligible{"typed exchange: too many windows"};
     ts->nwin = nw;
+    if (!build && N <= 8 && nw && !getenv("CQGPU_TYPED_TWO_PASS") && typed_one_pass(c, t, kcol, pcol, *ts)) {
+        t->tsend = std::move(ts);
+        return *t->tsend;
+    }
     const uint64_t nn = std::max<uint64_t>(nw * (uint64_t)N, 1);
     {
         DevBuf a(nn * 4), b(nn * 4 + 16);
@@ -7217,8 +7228,8 @@ TypedSend& typed_count_pass(DevCtx& c, cqgpu_table* t, bool build, int kcol, int
     if (!nw) HIPCHECK(hipMemsetAsync(ts->rcnt.p, 0, nn * 4, c.stream));
     HIPCHECK(cq_jx_route(t->g, t->data_begin, t->n, ts->ws, (uint8_t)t->cfg.delimiter, (uint8_t)t->cfg.quote, kcol, -1,
                          build ? 1 : 0, ts->rp, 1, (uint32_t)N, qbase, 0, ts->rcnt.as<unsigned int>(),
-                         build ? ts->wcount.as<unsigned int>() : nullptr, nullptr, nullptr, nullptr, flag, kr, c.ncu,
-                         c.stream));
+                         build ? ts->wcount.as<unsigned int>() : nullptr, nullptr, nullptr, nullptr, 0u, flag, kr,
+                         c.ncu, c.stream));
     size_t tb = 0;
     HIPCHECK(cq_excl_sum_u32(nullptr, &tb, ts->rcnt.as<unsigned int>(), ts->roffs.as<unsigned int>(), nn, c.stream));
     if (build && nw) {
@@ -7256,11 +7267,77 @@ TypedSend& typed_count_pass(DevCtx& c, cqgpu_table* t, bool build, int kcol, int
     return *t->tsend;
 }
 
+// the probe side's single pass (jx_extract_kernel ROUTE 3): entries written while they
+// are counted, destination d's region [d cap, (d + 1) cap) filled in chunks from its
+// cursor with holes at the waves' chunk tails (the receivers skip them); the region
+// capacity is twice the sampled share plus a chunk per wave with a window.  False (nothing kept):
+// no sample, or a region overflowed (skewed keys) -- the caller runs the two passes.
+bool typed_one_pass(DevCtx& c, cqgpu_table* t, int kcol, int pcol, TypedSend& ts) {
+    if (!t->est_records) {                            // (once per table: the sample is fixed)
+        uint64_t skmin = 0, skmax = 0, est = 0;
+        if (!sample_key_range(t, kcol, 1, &skmin, &skmax, &est)) return false;
+        t->est_records = est;
+    }
+    const uint64_t est = t->est_records;
+    const uint32_t N = ts.N;
+    const char* ce = getenv("CQGPU_TEST_ONE_PASS_CAP");     // test knob: the region capacity
+    const uint64_t cap64 = ce ? strtoull(ce, nullptr, 10)
+                              : 2 * est / N + std::min<uint64_t>(ts.nwin, (uint64_t)c.ncu * 16) * cq_jx_rchunk() + 4096;
+    if (cap64 == 0 || cap64 >= (1ull << 31)) return false;
+    const uint32_t cap = (uint32_t)cap64;
+    {
+        DevBuf e((size_t)N * cap * 8 + 16);
+        std::swap(ts.ent.p, e.p);
+    }
+    const size_t hb = 64 + (size_t)N * 256;           // flags, key range, then the cursors (stride 256 B)
+    DevBuf ctl(hb);
+    unsigned int* flag = ctl.as<unsigned int>();
+    unsigned long long* kr = (unsigned long long*)(ctl.as<uint8_t>() + 16);
+    unsigned int* cur = (unsigned int*)(ctl.as<uint8_t>() + 64);
+    HIPCHECK(hipMemsetAsync(ctl.p, 0, hb, c.stream));
+    HIPCHECK(cq_jx_route(t->g, t->data_begin, t->n, ts.ws, (uint8_t)t->cfg.delimiter, (uint8_t)t->cfg.quote, kcol, pcol,
+                         0, ts.rp, 3, N, ts.qbase, 0, cur, nullptr, nullptr, nullptr, ts.ent.p, cap, flag, kr, c.ncu,
+                         c.stream));
+    uint8_t* h = (uint8_t*)pinned(c, hb);
+    HIPCHECK(hipMemcpyAsync(h, ctl.p, hb, hipMemcpyDeviceToHost, c.stream));
+    HIPCHECK(hipStreamSynchronize(c.stream));
+    uint32_t fl = 0;
+    memcpy(&fl, h, 4);
+    bool over = (fl & 1024u) != 0;
+    ts.rstart.assign((size_t)N + 1, 0);
+    ts.counts.assign(N, 0);
+    for (uint32_t d = 0; d < N; d++) {
+        uint32_t n = 0;
+        memcpy(&n, h + 64 + 256 * (size_t)d, 4);
+        over = over || n > cap;
+        ts.rstart[d] = (uint64_t)d * cap;
+        ts.counts[d] = n;
+    }
+    ts.rstart[N] = (uint64_t)N * cap;
+    if (over) {
+        DevBuf drop;
+        std::swap(ts.ent.p, drop.p);
+        ts.rstart.clear();
+        ts.counts.clear();
+        return false;
+    }
+    ts.flags = fl & ~512u;
+    ts.eflags = fl & 512u;
+    ts.esize = 8;
+    ts.one_pass = true;
+    return true;
+}
+
 // the emit pass (jx_extract_kernel ROUTE 2) after typed_count_pass: every entry at its
 // position; flags 1 (a payload the entries cannot carry), 512
 uint32_t typed_emit_pass(DevCtx& c, cqgpu_table* t, bool build, int kcol, int pcol, uint64_t gbase) {
     if (!t->tsend) throw HipError{"typed exchange: send without a count"};
     TypedSend& ts = *t->tsend;
+    if (ts.one_pass) {                                    // (written by the count pass)
+        ts.emitted = true;
+        ts.flags |= ts.eflags;
+        return ts.eflags;
+    }
     ts.esize = build ? 16 : 8;
     const uint64_t total = ts.rstart[ts.N];
     {
@@ -7273,7 +7350,7 @@ uint32_t typed_emit_pass(DevCtx& c, cqgpu_table* t, bool build, int kcol, int pc
     HIPCHECK(hipMemsetAsync(ctl.p, 0, 64, c.stream));
     HIPCHECK(cq_jx_route(t->g, t->data_begin, t->n, ts.ws, (uint8_t)t->cfg.delimiter, (uint8_t)t->cfg.quote, kcol, pcol,
                          build ? 1 : 0, ts.rp, 2, ts.N, ts.qbase, gbase, nullptr, nullptr, ts.roffs.as<unsigned int>(),
-                         build ? ts.wbase.as<unsigned int>() : nullptr, ts.ent.p, flag, kr, c.ncu, c.stream));
+                         build ? ts.wbase.as<unsigned int>() : nullptr, ts.ent.p, 0u, flag, kr, c.ncu, c.stream));
     uint32_t* h = (uint32_t*)pinned(c, 16);
     HIPCHECK(hipMemcpyAsync(h, flag, 4, hipMemcpyDeviceToHost, c.stream));
     HIPCHECK(hipStreamSynchronize(c.stream));
@@ -7495,11 +7572,14 @@ int64_t cqgpu_typed_count(cq_node* q, cqgpu_table* const* tables, int ntables, i
             !typed_join_plan(q, tables[0], tables[1], tj, why))
             throw Ineligible{"typed exchange: " + why};
         DevCtx& c = ctx();
-        const TypedSend& ts = typed_count_pass(c, tables[side], side == 0, side == 0 ? tj.kl : tj.kr, nranks, qbase);
+        const TypedSend& ts = typed_count_pass(c, tables[side], side == 0, side == 0 ? tj.kl : tj.kr, nranks, qbase,
+                                               side == 0 ? -1 : tj.vcol);
         for (int d = 0; d < nranks; d++) if (counts) counts[d] = ts.counts[d];
         if (krange) { krange[0] = ts.krange[0]; krange[1] = ts.krange[1]; }
         if (flags) *flags = ts.flags;
-        return (int64_t)(side == 0 ? ts.nrec : ts.rstart[nranks]);
+        uint64_t sent = 0;
+        for (int d = 0; d < nranks; d++) sent += ts.counts[d];
+        return (int64_t)(side == 0 ? ts.nrec : sent);
     } catch (Ineligible& e) {
         g_inel = e.why;
         set_err("cq_amd: %s", e.why.c_str());
@@ -8303,7 +8383,7 @@ bool dist_join_typed(DevCtx& c, DistComm& m, cq_node* q, cqgpu_table* const* tab
             if (getenv("CQGPU_TEST_TYPED_FAIL"))                 // test knob: this rank's send fails
                 throw HipError{"dist_join: injected typed-exchange failure (CQGPU_TEST_TYPED_FAIL)"};
             const TypedSend& su = typed_count_pass(c, tables[0], true, tj.kl, N, qbase);
-            const TypedSend& so = typed_count_pass(c, tables[1], false, tj.kr, N, qbase);
+            const TypedSend& so = typed_count_pass(c, tables[1], false, tj.kr, N, qbase, tj.vcol);
             for (int d = 0; d < N; d++) { mine[d] = su.counts[d]; mine[N + d] = so.counts[d]; }
             mine[2 * N] = su.flags | so.flags;
             mine[2 * N + 1] = su.krange[0];

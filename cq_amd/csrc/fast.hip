@@ -1527,8 +1527,17 @@ struct JxOut {
     // Flags: 8 a NULL build key, 16 a build q32 outside [0, 2^32 - 1) (the host retries
     // with the keys' own minimum), 512 a payload outside 31 bits.  A probe key outside
     // the window matches no build key and is not sent.
+    // ROUTE 3 (probe side, rn <= 8): one pass, no count.  Destination d's entries fill
+    // region [d * cap, (d + 1) * cap) of rent in chunks of JX_RCHUNK entries, which a
+    // wave's lane d reserves from the cursor rcnt[64 d] when its current chunk cannot hold
+    // the pass's entries for d (the pass's first ones close the old chunk, the rest open
+    // the new one); at the end each wave's unused chunk tails become holes {~0, JX_PNULL}
+    // (q32 ~0 is never below qoff + range: the receivers skip them).  The probe's order
+    // inside a region is free: its entries only add to sums and counts, and the first
+    // pair of a group is its build record's.  A cursor past cap sets 1024 (the host
+    // reruns the two passes).
     void* rent;
-    unsigned int* rcnt;           // ROUTE 1
+    unsigned int* rcnt;           // ROUTE 1; ROUTE 3: the destinations' cursors (stride 64)
     const unsigned int* roffs;    // ROUTE 2
     uint64_t rmagic;              // ceil(2^64 / rn) (rn > 1): key / rn = mulhi(key, rmagic) for keys < 2^58
     uint64_t qbase, gbase;
@@ -1552,6 +1561,7 @@ __device__ __forceinline__ unsigned long long jx_slot(unsigned long long k, cons
 constexpr uint32_t JX_G = 2048;           // group ids of a STAR join (LDS sums per block)
 constexpr uint32_t JX_PMAX = 4096;        // key partitions of a partitioned STAR probe (LDS counters)
 constexpr uint32_t JX_PNULL = 0x80000000u;   // a partitioned entry's NULL payload
+constexpr uint32_t JX_RCHUNK = 192;          // ROUTE 3 chunk (>= one pass's entries for one destination)
 
 // a GROUP BY raw tag's group id: its slot in the tag table (linear probing; a stale
 // 0 read only leads to the CAS, a set slot never changes)
@@ -1681,6 +1691,7 @@ template <bool BUILD, bool COMMA, int NR, bool COUNT, bool STAR = false, int RP 
           int ROUTE = 0>
 __global__ __launch_bounds__(LT) void jx_extract_kernel(const uint8_t* __restrict__ g, const JxPlan jp, const JxOut jo) {
     static_assert(ROUTE == 0 || (!STAR && !COUNT), "ROUTE: the record form's passes");
+    static_assert(ROUTE != 3 || !BUILD, "ROUTE 3: the probe side");
     extern __shared__ __align__(16) uint8_t smem[];
     WaveLds* waves = (WaveLds*)smem;
     // STAR probe: per group id COUNT / fixed-point SUM / SUM count of this block;
@@ -1751,6 +1762,7 @@ __global__ __launch_bounds__(LT) void jx_extract_kernel(const uint8_t* __restric
     bool bad = false;
     unsigned long long kmin = ~0ull, kmax = 0ull;
     uint32_t smin = ~0u, smax = 0u;          // STAR build: the in-range keys' extreme slots
+    uint32_t ccur = 0, cend = 0;             // ROUTE 3: lane d's chunk for destination d (next, end)
     uint32_t i = blockIdx.x * NWV + wv;
     if (i < nwin) load_win(g, first_win + i, wsb, wlds, voff, prev_next);
     for (; i < nwin; i += wstep) {
@@ -1807,7 +1819,7 @@ __global__ __launch_bounds__(LT) void jx_extract_kernel(const uint8_t* __restric
         // record j of this lane in this window lands at wbase[i] + (the lanes below's
         // records) + j: file order
         const uint32_t nmine = (uint32_t)__popcll(todo);
-        uint32_t at_next = (STAR || ROUTE == 1 || (ROUTE == 2 && !BUILD)) ? 0u
+        uint32_t at_next = (STAR || ROUTE == 1 || ROUTE == 3 || (ROUTE == 2 && !BUILD)) ? 0u
                                                                          : jo.wbase[i] + wave_incl_scan(nmine) - nmine;
         // ROUTE: lane d (< rn) holds destination d's entries of this window so far, and
         // (emit) its first position
@@ -2045,7 +2057,7 @@ __global__ __launch_bounds__(LT) void jx_extract_kernel(const uint8_t* __restric
                         take[u] = false;                          // (probe: matches no build key)
                         if (ROUTE == 1 && BUILD) sflag |= 16u;
                     }
-                    if (ROUTE == 2 && !BUILD && take[u] && pay[u] != JX_NOVAL &&
+                    if (ROUTE >= 2 && !BUILD && take[u] && pay[u] != JX_NOVAL &&
                         ((long long)pay[u] < -2147483647ll || (long long)pay[u] > 2147483647ll))
                         sflag |= 512u;                            // (still written: the flag drops the exchange)
                 }
@@ -2086,7 +2098,35 @@ __global__ __launch_bounds__(LT) void jx_extract_kernel(const uint8_t* __restric
                         }
                     }
                     const uint32_t tw = lane < 4 ? t0 : t1;
-                    rrun += (uint32_t)lane < nd ? (tw >> (8u * ((uint32_t)lane & 3u))) & 0xFFu : 0u;
+                    const uint32_t td = (uint32_t)lane < nd ? (tw >> (8u * ((uint32_t)lane & 3u))) & 0xFFu : 0u;
+                    rrun += td;
+                    if constexpr (ROUTE == 3) {
+                        // lane d: a new chunk when the current one cannot take this pass's
+                        // entries for d; an entry of rank r among them lands at cur + r in the
+                        // old chunk while r < room, else at the new chunk's r - room
+                        const uint32_t room = cend - ccur;
+                        uint32_t nb = 0;
+                        if (td > room) nb = atomicAdd(&jo.rcnt[(uint32_t)lane * 64u], JX_RCHUNK);
+                        const uint32_t e0 = s0 - h0, e1 = s1 - h1;
+#pragma unroll
+                        for (int u = 0; u < RP; u++) {
+                            const uint32_t d = dd[u] & 7u;
+                            uint32_t mine = 0;
+#pragma unroll
+                            for (int v = 0; v < u; v++) mine += (take[v] && dd[v] == dd[u]) ? 1u : 0u;
+                            const uint32_t r = (((d < 4u ? e0 : e1) >> (8u * (d & 3u))) & 0xFFu) + mine;
+                            const uint32_t cd = (uint32_t)__shfl((int)ccur, (int)d, 64);
+                            const uint32_t rd = (uint32_t)__shfl((int)room, (int)d, 64);
+                            const uint32_t bd = (uint32_t)__shfl((int)nb, (int)d, 64);
+                            pos[u] = r < rd ? cd + r : bd + (r - rd);
+                        }
+                        if (td > room) {
+                            ccur = nb + (td - room);
+                            cend = nb + JX_RCHUNK;
+                        } else {
+                            ccur += td;
+                        }
+                    }
                 } else
                 for (uint32_t d = 0; d < nd; d++) {
                     uint64_t m[RP];
@@ -2112,6 +2152,15 @@ __global__ __launch_bounds__(LT) void jx_extract_kernel(const uint8_t* __restric
                         }
                     }
                     rrun += (uint32_t)lane == d ? tot : 0u;
+                }
+                if constexpr (ROUTE == 3) {
+#pragma unroll
+                    for (int u = 0; u < RP; u++) {
+                        if (!take[u]) continue;
+                        if (pos[u] >= jo.cap) { sflag |= 1024u; continue; }     // (the region is full)
+                        const uint32_t p32 = pay[u] == JX_NOVAL ? JX_PNULL : (uint32_t)pay[u];
+                        ((uint2*)jo.rent)[(uint64_t)(dd[u] & 7u) * jo.cap + pos[u]] = make_uint2(q32[u], p32);
+                    }
                 }
                 if constexpr (ROUTE == 2) {
 #pragma unroll
@@ -2168,6 +2217,14 @@ __global__ __launch_bounds__(LT) void jx_extract_kernel(const uint8_t* __restric
         }
     }
     if (COUNT) return;
+    if constexpr (ROUTE == 3) {                   // this wave's chunk tails: holes
+        const uint32_t nd = __builtin_amdgcn_readfirstlane(jo.rn);
+        for (uint32_t d = 0; d < nd; d++) {
+            const uint32_t a = __builtin_amdgcn_readlane(ccur, d), b = __builtin_amdgcn_readlane(cend, d);
+            for (uint32_t q = a + (uint32_t)lane; q < b && q < jo.cap; q += 64u)
+                ((uint2*)jo.rent)[(uint64_t)d * jo.cap + q] = make_uint2(~0u, JX_PNULL);
+        }
+    }
     if (__any(bad) && lane == 0) atomicOr(jo.flag, 1u);
     if constexpr (STAR || ROUTE) {
         for (int o = 32; o > 0; o >>= 1) {
@@ -3524,6 +3581,7 @@ hipError_t cq_jx_star_flush(int grouped, int value, const unsigned long long* tt
     return hipGetLastError();
 }
 uint32_t cq_jx_star_groups() { return cq::fast::JX_G; }
+uint32_t cq_jx_rchunk() { return cq::fast::JX_RCHUNK; }
 
 // the typed exchange's sender passes over one side (jx_extract_kernel ROUTE):
 //   pass 1  per window i and destination d the entries into rcnt[d * nwin + i] (build:
@@ -3531,17 +3589,21 @@ uint32_t cq_jx_star_groups() { return cq::fast::JX_G; }
 //   pass 2  the entries at roffs[d * nwin + i] + their rank (roffs: rcnt's exclusive
 //           scan, destination-major); build: 16-byte {q32, gid, tag} (wbase: wcount's
 //           exclusive scan), probe 8-byte {q32, pay}
+//   pass 3  (probe, nranks <= 8) the entries in one pass: destination d's in chunks of
+//           [d * cap, (d + 1) * cap) of rent, reserved from the cursors rcnt[64 d] (zeroed)
 hipError_t cq_jx_route(const uint8_t* g, uint64_t lo, uint64_t hi, uint32_t ws, uint32_t delim, uint32_t quote,
                        int kcol, int pcol, int build, int rp, int pass, uint32_t nranks, unsigned long long qbase,
                        unsigned long long gbase, unsigned int* rcnt, unsigned int* wcount, const unsigned int* roffs,
-                       const unsigned int* wbase, void* rent, unsigned int* flag, unsigned long long* krange, int grid,
-                       hipStream_t s) {
+                       const unsigned int* wbase, void* rent, uint32_t cap, unsigned int* flag,
+                       unsigned long long* krange, int grid, hipStream_t s) {
     using namespace cq::fast;
     JxPlan jp;
     if (pass == 1) pcol = -1;
     if (!jx_plan(g, lo, hi, ws, delim, quote, kcol, pcol, &jp)) return hipErrorInvalidValue;
     if (nranks < 1 || nranks > 64) return hipErrorInvalidValue;
-    if (pass == 1 ? (!rcnt || (build && !wcount)) : (!roffs || !rent || (build && !wbase))) return hipErrorInvalidValue;
+    if (pass == 3 ? (build || nranks > 8 || !rcnt || !rent || !cap)
+                  : pass == 1 ? (!rcnt || (build && !wcount)) : (!roffs || !rent || (build && !wbase)))
+        return hipErrorInvalidValue;
     const int nr = pcol >= 0 ? 2 : 1;
     if (delim != ',' || quote != '"') return hipErrorInvalidValue;      // (the ',' / '"' builds)
     typedef void (*xfn_t)(const uint8_t*, const JxPlan, const JxOut);
@@ -3554,7 +3616,12 @@ hipError_t cq_jx_route(const uint8_t* g, uint64_t lo, uint64_t hi, uint32_t ws, 
          {jx_extract_kernel<false, true, 2, false, false, 2, false, 2>, jx_extract_kernel<false, true, 2, false, false, 3, false, 2>}},
         {{jx_extract_kernel<true, true, 1, false, false, 2, false, 2>, jx_extract_kernel<true, true, 1, false, false, 3, false, 2>},
          {jx_extract_kernel<true, true, 2, false, false, 2, false, 2>, jx_extract_kernel<true, true, 2, false, false, 3, false, 2>}}};
-    const xfn_t fn = pass == 1 ? ctab[build ? 1 : 0][rp == 3 ? 1 : 0] : etab[build ? 1 : 0][nr - 1][rp == 3 ? 1 : 0];
+    static const xfn_t otab[2][2] = {
+        {jx_extract_kernel<false, true, 1, false, false, 2, false, 3>, jx_extract_kernel<false, true, 1, false, false, 3, false, 3>},
+        {jx_extract_kernel<false, true, 2, false, false, 2, false, 3>, jx_extract_kernel<false, true, 2, false, false, 3, false, 3>}};
+    const xfn_t fn = pass == 1   ? ctab[build ? 1 : 0][rp == 3 ? 1 : 0]
+                     : pass == 3 ? otab[nr - 1][rp == 3 ? 1 : 0]
+                                 : etab[build ? 1 : 0][nr - 1][rp == 3 ? 1 : 0];
     JxOut jo;
     memset(&jo, 0, sizeof jo);
     jo.wbase = wbase;
@@ -3565,6 +3632,7 @@ hipError_t cq_jx_route(const uint8_t* g, uint64_t lo, uint64_t hi, uint32_t ws, 
     jo.rcnt = rcnt;
     jo.roffs = roffs;
     jo.rn = nranks;
+    jo.cap = cap;
     // ceil(2^64 / n): key / n = mulhi(key, magic) for keys below 2^64 / n (canonical keys < 10^15)
     jo.rmagic = nranks > 1 ? (unsigned long long)(((unsigned __int128)1 << 64) / nranks) + 1ull : 0ull;
     if (nranks > 1 && (nranks & (nranks - 1)) == 0) jo.rmagic = 1ull << (64 - __builtin_ctz(nranks));

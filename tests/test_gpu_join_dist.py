@@ -1015,6 +1015,40 @@ def test_typed_exchange_partitioned_probe(files, nranks, qi, monkeypatch):
     compare(got, want, tol, f"typed exchange, partitioned probe, {nranks} ranks: {sql}")
 
 
+@pytest.mark.parametrize("mode", ["one_pass", "two_pass", "overflow"])
+@pytest.mark.parametrize("nranks", [2, 3, 8])
+def test_typed_exchange_probe_pass_forms(files, nranks, mode, monkeypatch):
+    """the probe side's entries: one pass by default (jx_extract_kernel ROUTE 3: chunks
+    from per-destination cursors, holes at the waves' chunk tails, which the receivers
+    skip); the count + emit passes under CQGPU_TYPED_TWO_PASS=1 and when a region
+    overflows its capacity (CQGPU_TEST_ONE_PASS_CAP) -- the oracle's answer every way,
+    the two-pass entries exactly the probe records with a key in range"""
+    data, paths = files
+    sql = TYPED[0].format(u=paths["users"], o=paths["orders"])
+    want, unsup = cqtest.oracle_query(sql)
+    assert not unsup
+    if mode == "two_pass":
+        monkeypatch.setenv("CQGPU_TYPED_TWO_PASS", "1")
+    elif mode == "overflow":
+        monkeypatch.setenv("CQGPU_TEST_ONE_PASS_CAP", "5")
+    with cqtest.Parsed(sql) as ast:
+        st = {}
+        tp, why = _typed(ast, data["users"], data["orders"], nranks, st)
+        assert tp, (cq_amd.last_error(), why)
+        got = abi.table_to_py(tp)
+        cq_amd.result_free(tp)
+        tol = tolerant_columns(ast)
+        monkeypatch.setenv("CQGPU_TYPED_TWO_PASS", "1")
+        exact = {}
+        tp2, _ = _typed(ast, data["users"], data["orders"], nranks, exact)
+        cq_amd.result_free(tp2)
+    compare(got, want, tol, f"typed exchange ({mode}) {nranks} ranks: {sql}")
+    if mode == "one_pass":          # chunk tails: holes beside the same entries
+        assert sum(st["sent_entries_o"]) > sum(exact["sent_entries_o"]), (st, exact)
+    else:
+        assert st["sent_entries_o"] == exact["sent_entries_o"], (st, exact)
+
+
 @pytest.mark.parametrize("order", ["rising", "shuffled"])
 @pytest.mark.parametrize("flags", [False, True])
 def test_typed_exchange_first_pair_forms(tmp_path, monkeypatch, order, flags):
