@@ -541,7 +541,8 @@ def config5_leg(args, cq_amd, L):
             "exchange": {"sent_bytes": r["xgmi_sent_bytes"], "received_bytes": r["xgmi_received_bytes"],
                          "entries_received": r["recv_entries"],
                          "entry_bytes": "16 per users record {key/N - qbase, global id, GROUP BY bytes}, 8 per "
-                                        "orders record {key/N - qbase, price in 10^-3}",
+                                        "orders record {key/N - qbase, price in 10^-3}; the orders counts include "
+                                        "the one-pass send's holes (chunk tails, skipped by the receiver)",
                          "xgmi_bound_ms": max(r["xgmi_sent_bytes"], r["xgmi_received_bytes"]) / xgmi * 1e3,
                          "note": "not in ms_per_step: one GPU has no peer; xgmi_bound_ms = the larger direction "
                                  "over 7 links at their 153 GB/s peak"},

@@ -6256,7 +6256,12 @@ cq_table* cqgpu_merge_partials(cq_node* q, const void* const* blobs, const size_
                     if (merged.size() >= (size_t)UINT32_MAX - 1) throw Ineligible{"too many groups to merge"};
                     slot_of[at] = (uint32_t)merged.size() + 1;
                     merged.push_back(std::move(h));
-                    h = HGroup();
+                    // (no fresh HGroup: every field the next group uses is parsed over, the
+                    // moved-from containers are cleared -- a default HGroup is ~1 KiB to build)
+                    h.kbytes.clear();
+                    h.reps.clear();
+                    h.mvals.clear();
+                    h.split.clear();
                     continue;
                 }
                 HGroup& m = merged[slot_of[at] - 1];

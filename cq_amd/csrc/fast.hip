@@ -2540,7 +2540,9 @@ __global__ __launch_bounds__(1024) void jx_ent_build_kernel(const uint4* __restr
             ok[u] = i + u * nt < n;
             const v4u x = ok[u] ? __builtin_nontemporal_load((const v4u*)(ent + i + u * nt)) : v4u{0u, 0u, 0u, 0u};
             e[u] = make_uint4(x.x, x.y, x.z, x.w);
-            // the next entry's q32 (lanes 0-62: the line the next lane loads)
+            // the next entry's q32 (lanes 0-62: the line the next lane loads; measured
+            // against a ds_bpermute of the next lane's entry, which competed with the tag
+            // lookups' LDS: 0.69 -> 0.75 ms)
             nq[u] = i + u * nt + 1 < n ? ((const uint32_t*)(ent + i + u * nt + 1))[0] : ~0u;
         }
 #pragma unroll
